@@ -1,0 +1,117 @@
+"""ctypes / numpy mirror of include/mte.h (the C-ABI of libmte.so).
+
+Plain layout definitions only; no behaviour.  Field order and sizes must match
+include/mte.h exactly (checked by tests/test_abi.py).
+"""
+import ctypes as C
+
+import numpy as np
+
+MTE_ABI_VERSION = 1
+MTE_MAX_KEYS = 8
+MTE_MAX_CLIENTS = 32
+
+MTE_OK = 0
+MTE_E_INVALID_ARG = -1
+MTE_E_NO_DEVICE = -2
+MTE_E_HIP = -3
+MTE_E_CAPACITY = -4
+MTE_E_SEQ_ORDER = -5
+MTE_E_MSN_ORDER = -6
+MTE_E_MSN_GT_SEQ = -7
+MTE_E_INSERT_FAILED = -8
+MTE_E_UNSUPPORTED = -9
+MTE_E_STATE = -10
+MTE_E_OOM = -11
+MTE_E_CLIENT_RANGE = -12
+
+ERROR_NAMES = {
+    MTE_E_INVALID_ARG: "invalid argument",
+    MTE_E_NO_DEVICE: "no HIP device",
+    MTE_E_HIP: "HIP runtime error",
+    MTE_E_CAPACITY: "segment capacity exceeded",
+    MTE_E_SEQ_ORDER: "0x030: Incoming remote op sequence# <= local collabWindow's currentSequence#",
+    MTE_E_MSN_ORDER: "0x031: Incoming remote op minSequence# < local collabWindow's minSequence#",
+    MTE_E_MSN_GT_SEQ: "0x039: Incoming op sequence# < minSequence#",
+    MTE_E_INSERT_FAILED: "MergeTree insert failed",
+    MTE_E_UNSUPPORTED: "unsupported op shape",
+    MTE_E_STATE: "call out of order",
+    MTE_E_OOM: "out of memory",
+    MTE_E_CLIENT_RANGE: "too many clients in one document",
+}
+
+OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP = 0, 1, 2, 3
+F_MARKER, F_MSG_END, F_REWRITE = 0x1, 0x2, 0x4
+NO_PROPS = 0xFFFFFFFF
+DOC_NEW_LENGTH_CALC = 0x1
+
+# 32-byte mte_op record.
+OP_DTYPE = np.dtype([
+    ("seq", "<i4"), ("ref_seq", "<i4"), ("min_seq", "<i4"),
+    ("type", "u1"), ("client", "u1"), ("flags", "<u2"),
+    ("pos1", "<i4"), ("pos2", "<i4"), ("a", "<u4"), ("b", "<u4"),
+])
+assert OP_DTYPE.itemsize == 32
+
+PROP_DTYPE = np.dtype([("key", "<u4"), ("value", "<u4")])
+PROPSET_DTYPE = np.dtype([("first", "<u4"), ("count", "<u4")])
+DOC_INIT_DTYPE = np.dtype([
+    ("text_off", "<u4"), ("text_len", "<u4"), ("flags", "<u4"), ("propset", "<u4"),
+    ("min_seq", "<i4"), ("cur_seq", "<i4"),
+])
+assert DOC_INIT_DTYPE.itemsize == 24
+
+
+class MteConfig(C.Structure):
+    _fields_ = [("device", C.c_int32), ("n_keys", C.c_uint32),
+                ("seg_capacity", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class MteBatch(C.Structure):
+    _fields_ = [("n_docs", C.c_uint32), ("op_offsets", C.c_void_p), ("ops", C.c_void_p),
+                ("n_ops", C.c_uint64), ("text", C.c_void_p), ("text_units", C.c_uint64),
+                ("propsets", C.c_void_p), ("n_propsets", C.c_uint32),
+                ("props", C.c_void_p), ("n_props", C.c_uint32)]
+
+
+class MteStats(C.Structure):
+    _fields_ = [("ops_applied", C.c_uint64), ("segs_scanned", C.c_uint64),
+                ("segs_written", C.c_uint64), ("prop_writes", C.c_uint64),
+                ("units_inserted", C.c_uint64), ("max_segs", C.c_uint64),
+                ("kernel_ms", C.c_double), ("algo_bytes", C.c_double)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+class MteDocView(C.Structure):
+    _fields_ = [("status", C.c_int32), ("cur_seq", C.c_int32), ("min_seq", C.c_int32),
+                ("length", C.c_uint32),
+                ("text", C.c_void_p), ("text_cap", C.c_uint32), ("n_text", C.c_uint32),
+                ("seg_len", C.c_void_p), ("seg_kind", C.c_void_p), ("seg_props", C.c_void_p),
+                ("seg_cap", C.c_uint32), ("n_segs", C.c_uint32)]
+
+
+# Every symbol include/mte.h declares (tests check libmte.so exports them all).
+EXPORTED_SYMBOLS = [
+    "mte_abi_version", "mte_strerror", "mte_create", "mte_destroy", "mte_last_error",
+    "mte_load_docs", "mte_submit", "mte_run", "mte_sync", "mte_reset", "mte_digest",
+    "mte_digest_device", "mte_read_doc", "mte_doc_status", "mte_stats_get",
+]
+
+
+def ptr(a):
+    """Address of a numpy array's data (None for empty / None)."""
+    if a is None or a.size == 0:
+        return None
+    return a.ctypes.data
+
+
+class MergeTreeError(RuntimeError):
+    """A replay error, carrying the engine status code (and, where one exists,
+    the hex assert code of the reference)."""
+
+    def __init__(self, code, detail=""):
+        self.code = code
+        msg = ERROR_NAMES.get(code, f"error {code}")
+        super().__init__(f"{msg} ({code}){': ' + detail if detail else ''}")

@@ -1,0 +1,164 @@
+"""Python binding of libmte.so (the HIP engine) through its C-ABI.
+
+`DeviceEngine` is a thin ctypes layer over include/mte.h: documents are loaded
+once, batches of op records are uploaded to HBM and replayed by the gfx950
+kernels.  There is no CPU fallback: if libmte.so (or a HIP device) is missing
+this module raises.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _native
+from .abi import (DOC_INIT_DTYPE, EXPORTED_SYMBOLS, OP_DTYPE, PROP_DTYPE, PROPSET_DTYPE,
+                  MergeTreeError, MteBatch, MteConfig, MteDocView, MteStats, ptr)
+from .packing import units_to_str
+
+
+def _arr(a, dtype):
+    if a is None:
+        return np.zeros(0, dtype)
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+def make_batch_struct(n_docs, batch):
+    """-> (MteBatch, keepalive list)."""
+    offs = _arr(batch["op_offsets"], np.uint64)
+    ops = _arr(batch["ops"], OP_DTYPE)
+    text = _arr(batch.get("text"), np.uint16)
+    ps = _arr(batch.get("propsets"), PROPSET_DTYPE)
+    pe = _arr(batch.get("props"), PROP_DTYPE)
+    if len(offs) != n_docs + 1:
+        raise ValueError("op_offsets must have n_docs+1 entries")
+    b = MteBatch(n_docs, ptr(offs), ptr(ops), len(ops), ptr(text), len(text),
+                 ptr(ps), len(ps), ptr(pe), len(pe))
+    return b, [offs, ops, text, ps, pe]
+
+
+class EngineBase:
+    """Operations shared by the device engine and the CPU oracle binding."""
+
+    n_keys = 0
+    n_docs = 0
+
+    def _check(self, rc, what=""):
+        if rc != 0:
+            raise MergeTreeError(rc, f"{what}: {self._last_error()}")
+
+    def _last_error(self):
+        return ""
+
+    def read_doc(self, doc):
+        """-> dict(status, cur_seq, min_seq, length, text, segs=[(len, kind, props)])."""
+        v = MteDocView()
+        self._check(self._read_doc(doc, C.byref(v)), "read_doc")
+        text = np.zeros(max(v.n_text, 1), np.uint16)
+        nseg = max(v.n_segs, 1)
+        seg_len = np.zeros(nseg, np.uint32)
+        seg_kind = np.zeros(nseg, np.uint32)
+        seg_props = np.zeros(nseg * max(self.n_keys, 1), np.uint32)
+        v.text, v.text_cap = ptr(text), len(text)
+        v.seg_len, v.seg_kind, v.seg_props, v.seg_cap = ptr(seg_len), ptr(seg_kind), ptr(seg_props), nseg
+        self._check(self._read_doc(doc, C.byref(v)), "read_doc")
+        props = seg_props[: v.n_segs * self.n_keys].reshape(v.n_segs, self.n_keys) if self.n_keys else \
+            np.zeros((v.n_segs, 0), np.uint32)
+        segs = [(int(seg_len[i]), int(seg_kind[i]), tuple(int(x) for x in props[i]))
+                for i in range(v.n_segs)]
+        return {"status": v.status, "cur_seq": v.cur_seq, "min_seq": v.min_seq,
+                "length": v.length, "text": units_to_str(text[: v.n_text]), "segs": segs}
+
+    def digest(self):
+        out = np.zeros(self.n_docs * 4, np.uint64)
+        self._check(self._digest(ptr(out), self.n_docs), "digest")
+        return out.reshape(self.n_docs, 4)
+
+    def statuses(self):
+        out = np.zeros(self.n_docs, np.int32)
+        self._check(self._doc_status(ptr(out), self.n_docs), "doc_status")
+        return out
+
+    def stats(self):
+        s = MteStats()
+        self._check(self._stats(C.byref(s)), "stats")
+        return s.as_dict()
+
+
+class DeviceEngine(EngineBase):
+    """One mte_ctx on one HIP device (one per process / GPU)."""
+
+    def __init__(self, n_keys=0, device=0, seg_capacity=0):
+        self.lib = _native.load_mte()
+        self.n_keys = n_keys
+        ctx = C.c_void_p()
+        cfg = MteConfig(device, n_keys, seg_capacity, 0)
+        rc = self.lib.mte_create(C.byref(cfg), C.byref(ctx))
+        if rc != 0:
+            raise MergeTreeError(rc, "mte_create: " + self.lib.mte_strerror(rc).decode())
+        self.ctx = ctx
+        self._keep = []
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.mte_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _last_error(self):
+        return self.lib.mte_last_error(self.ctx).decode()
+
+    def load_docs(self, inits, text=None, propsets=None, props=None):
+        inits = _arr(inits, DOC_INIT_DTYPE)
+        text = _arr(text, np.uint16)
+        ps = _arr(propsets, PROPSET_DTYPE)
+        pe = _arr(props, PROP_DTYPE)
+        self.n_docs = len(inits)
+        self._check(self.lib.mte_load_docs(self.ctx, len(inits), ptr(inits), ptr(text), len(text),
+                                           ptr(ps), len(ps), ptr(pe), len(pe)), "load_docs")
+
+    def submit(self, batch):
+        b, keep = make_batch_struct(self.n_docs, batch)
+        self._check(self.lib.mte_submit(self.ctx, C.byref(b)), "submit")
+        self._keep = keep  # inputs are copied by mte_submit; kept only for debugging
+
+    def run(self):
+        self._check(self.lib.mte_run(self.ctx), "run")
+
+    def sync(self):
+        """Raises on a HIP error.  Per-doc replay errors are left in statuses()."""
+        rc = self.lib.mte_sync(self.ctx)
+        if rc not in (0,) and rc > -4:
+            self._check(rc, "sync")
+        return rc
+
+    def apply_batch(self, batch):
+        self.submit(batch)
+        self.run()
+        return self.sync()
+
+    def reset(self):
+        self._check(self.lib.mte_reset(self.ctx), "reset")
+
+    def digest_device(self, device_ptr):
+        self._check(self.lib.mte_digest_device(self.ctx, C.c_void_p(device_ptr), self.n_docs),
+                    "digest_device")
+
+    def _read_doc(self, doc, vptr):
+        return self.lib.mte_read_doc(self.ctx, doc, vptr)
+
+    def _digest(self, p, n):
+        return self.lib.mte_digest(self.ctx, p, n)
+
+    def _doc_status(self, p, n):
+        return self.lib.mte_doc_status(self.ctx, p, n)
+
+    def _stats(self, sp):
+        return self.lib.mte_stats_get(self.ctx, sp)
+
+
+def exported_symbols():
+    return list(EXPORTED_SYMBOLS)

@@ -1,0 +1,231 @@
+"""Host half of Client.applyMsg: turn ISequencedDocumentMessage objects into
+32-byte op records for the device engine.
+
+Reference behaviour mirrored here (packages/dds/merge-tree/src):
+  * short client ids in first-seen order, the observer's own id first
+    (Client.getOrAddShortClientId / startOrUpdateCollaboration,
+    client.ts:683-698, 1163-1183); every message registers its sender
+    (client.ts:920), "op" or not;
+  * only type "op" messages carry a merge-tree op; all messages advance
+    currentSeq / minSeq (client.ts:922-934) -> non-op messages become NOOP
+    records;
+  * GROUP ops apply their members in order with the same sequenced message
+    (client.ts:876-884) -> one record per member, MSG_END on the last;
+  * insert specs: string -> text, {text, props} -> text with props,
+    {marker:{refType}, props} -> marker (test/testClient.ts:32-44,
+    textSegment.ts:40-48, mergeTreeNodes.ts:602-609); an insert without seg
+    is a no-op (client.ts:481-487);
+  * annotate props: null deletes, anything else sets; combiningOp "rewrite"
+    is supported, other combining ops are rejected.
+Property keys are interned to plane indices and values to ids of their
+canonical JSON (sorted keys), so id equality == matchProperties
+(properties.ts:66-100).
+"""
+import json
+
+import numpy as np
+
+from .abi import (F_MARKER, F_MSG_END, F_REWRITE, MTE_E_CLIENT_RANGE, MTE_E_INVALID_ARG,
+                  MTE_E_UNSUPPORTED, MTE_MAX_CLIENTS, NO_PROPS, OP_ANNOTATE, OP_DTYPE,
+                  OP_INSERT, OP_NOOP, OP_REMOVE, PROP_DTYPE, PROPSET_DTYPE, MergeTreeError)
+
+INSERT, REMOVE, ANNOTATE, GROUP = 0, 1, 2, 3  # MergeTreeDeltaType, ops.ts:43-48
+I32_MIN, I32_MAX = -(1 << 31), (1 << 31) - 1
+
+
+def canonical_json(v) -> str:
+    return json.dumps(v, sort_keys=True, separators=(",", ":"), ensure_ascii=False)
+
+
+def utf16_units(s: str) -> np.ndarray:
+    """JS strings are UTF-16 code-unit arrays (textSegment.ts:52-55)."""
+    return np.frombuffer(s.encode("utf-16-le"), dtype="<u2").copy()
+
+
+def units_to_str(u) -> str:
+    return np.asarray(u, dtype="<u2").tobytes().decode("utf-16-le", errors="surrogatepass")
+
+
+class Interner:
+    """Key -> plane index, canonical JSON value -> id (0 is reserved for null)."""
+
+    def __init__(self, n_keys: int):
+        self.n_keys = n_keys
+        self.keys = {}
+        self.key_names = []
+        self.values = {}
+        self.value_json = [None]
+
+    def key(self, name: str) -> int:
+        k = self.keys.get(name)
+        if k is None:
+            if len(self.key_names) >= self.n_keys:
+                raise MergeTreeError(MTE_E_UNSUPPORTED,
+                                     f"more than n_keys={self.n_keys} property keys ({name!r})")
+            k = len(self.key_names)
+            self.keys[name] = k
+            self.key_names.append(name)
+        return k
+
+    def value(self, v) -> int:
+        if v is None:
+            return 0
+        cj = canonical_json(v)
+        i = self.values.get(cj)
+        if i is None:
+            i = len(self.value_json)
+            self.values[cj] = i
+            self.value_json.append(cj)
+        return i
+
+    def decode_props(self, planes) -> dict:
+        out = {}
+        for k, vid in enumerate(planes):
+            if vid:
+                out[self.key_names[k]] = json.loads(self.value_json[vid])
+        return out
+
+
+class PropTable:
+    """Property sets of one batch (mte_propset / mte_prop arrays)."""
+
+    def __init__(self, interner: Interner):
+        self.interner = interner
+        self.sets = []
+        self.entries = []
+
+    def add(self, props: dict) -> int:
+        if props is None:
+            return NO_PROPS
+        if not isinstance(props, dict):
+            raise MergeTreeError(MTE_E_INVALID_ARG, "props must be an object")
+        first = len(self.entries)
+        for name, v in props.items():
+            self.entries.append((self.interner.key(name), self.interner.value(v)))
+        self.sets.append((first, len(self.entries) - first))
+        return len(self.sets) - 1
+
+    def arrays(self):
+        ps = np.array(self.sets, dtype=PROPSET_DTYPE) if self.sets else np.zeros(0, PROPSET_DTYPE)
+        pe = np.array(self.entries, dtype=PROP_DTYPE) if self.entries else np.zeros(0, PROP_DTYPE)
+        return ps, pe
+
+
+class DocClients:
+    """Per-document long -> short client id map (client.ts:683-698)."""
+
+    def __init__(self, observer_id: str):
+        self.observer = observer_id
+        self.ids = {observer_id: 0}
+
+    def short(self, long_id) -> int:
+        i = self.ids.get(long_id)
+        if i is None:
+            i = len(self.ids)
+            self.ids[long_id] = i
+        return i
+
+
+def _check_i32(v, what):
+    if not isinstance(v, int) or isinstance(v, bool) or v < I32_MIN or v > I32_MAX:
+        raise MergeTreeError(MTE_E_INVALID_ARG, f"{what}={v!r} is not an int32")
+    return v
+
+
+class BatchBuilder:
+    """Collects messages for n_docs documents and emits one mte_batch."""
+
+    def __init__(self, n_docs: int, interner: Interner):
+        self.n_docs = n_docs
+        self.interner = interner
+        self.props = PropTable(interner)
+        self.ops = [[] for _ in range(n_docs)]
+        self.text = []
+        self.text_units = 0
+
+    def _text(self, s: str):
+        u = utf16_units(s)
+        off = self.text_units
+        self.text.append(u)
+        self.text_units += len(u)
+        return off, len(u)
+
+    def add_message(self, doc: int, clients: DocClients, msg: dict):
+        """Client.applyMsg(msg, local=false) for one document (client.ts:918-935)."""
+        sender = msg.get("clientId")
+        short = clients.short(sender)
+        if short >= MTE_MAX_CLIENTS:
+            raise MergeTreeError(MTE_E_CLIENT_RANGE, f"client {sender!r}")
+        seq = _check_i32(msg["sequenceNumber"], "sequenceNumber")
+        ref = _check_i32(msg.get("referenceSequenceNumber", 0), "referenceSequenceNumber")
+        msn = _check_i32(msg["minimumSequenceNumber"], "minimumSequenceNumber")
+        recs = []
+        if msg.get("type", "op") == "op":
+            if sender == clients.observer:
+                raise MergeTreeError(MTE_E_UNSUPPORTED, "ack of a local op (observer replay only)")
+            self._op_records(msg.get("contents"), recs)
+        if not recs:
+            recs.append((OP_NOOP, 0, 0, 0, 0, NO_PROPS))
+        out = self.ops[doc]
+        last = len(recs) - 1
+        for i, (t, flags, p1, p2, a, b) in enumerate(recs):
+            if i == last:
+                flags |= F_MSG_END
+            out.append((seq, ref, msn, t, short, flags, p1, p2, a, b))
+
+    def _op_records(self, op, recs):
+        if not isinstance(op, dict):
+            raise MergeTreeError(MTE_E_INVALID_ARG, "op contents must be an object")
+        t = op.get("type")
+        if t == GROUP:
+            for member in op.get("ops", []):
+                self._op_records(member, recs)
+            return
+        if "pos1" not in op and op.get("relativePos1") is not None:
+            raise MergeTreeError(MTE_E_UNSUPPORTED, "relativePos1")
+        if t in (REMOVE, ANNOTATE) and "pos2" not in op:
+            raise MergeTreeError(MTE_E_UNSUPPORTED, "range op without pos2")
+        if t == INSERT:
+            seg = op.get("seg")
+            if seg is None:  # applyInsertOp returns false: no segment
+                recs.append((OP_NOOP, 0, 0, 0, 0, NO_PROPS))
+                return
+            pos = _check_i32(op.get("pos1", 0), "pos1")
+            if isinstance(seg, str):
+                off, n = self._text(seg)
+                recs.append((OP_INSERT, 0, pos, n, off, NO_PROPS))
+            elif isinstance(seg, dict) and "text" in seg:
+                off, n = self._text(seg["text"])
+                recs.append((OP_INSERT, 0, pos, n, off, self.props.add(seg.get("props"))))
+            elif isinstance(seg, dict) and "marker" in seg:
+                ref_type = _check_i32(seg["marker"].get("refType", 0), "refType")
+                recs.append((OP_INSERT, F_MARKER, pos, ref_type, 0, self.props.add(seg.get("props"))))
+            else:
+                raise MergeTreeError(MTE_E_INVALID_ARG, f"Unrecognized IJSONSegment type: {seg!r}")
+        elif t == REMOVE:
+            recs.append((OP_REMOVE, 0, _check_i32(op["pos1"], "pos1"), _check_i32(op["pos2"], "pos2"),
+                         0, NO_PROPS))
+        elif t == ANNOTATE:
+            comb = op.get("combiningOp")
+            flags = 0
+            if comb is not None:
+                if comb.get("name") != "rewrite":
+                    raise MergeTreeError(MTE_E_UNSUPPORTED, f"combiningOp {comb.get('name')!r}")
+                flags = F_REWRITE
+            ps = self.props.add(op.get("props", {}))
+            recs.append((OP_ANNOTATE, flags, _check_i32(op["pos1"], "pos1"),
+                         _check_i32(op["pos2"], "pos2"), ps, NO_PROPS))
+        else:
+            raise MergeTreeError(MTE_E_INVALID_ARG, f"unknown op type {t!r}")
+
+    def build(self):
+        """-> dict of numpy arrays forming one mte_batch."""
+        counts = np.array([len(o) for o in self.ops], dtype=np.uint64)
+        offsets = np.zeros(self.n_docs + 1, dtype=np.uint64)
+        np.cumsum(counts, out=offsets[1:])
+        flat = [r for o in self.ops for r in o]
+        ops = np.array(flat, dtype=OP_DTYPE) if flat else np.zeros(0, OP_DTYPE)
+        text = np.concatenate(self.text) if self.text else np.zeros(0, dtype="<u2")
+        ps, pe = self.props.arrays()
+        return {"op_offsets": offsets, "ops": ops, "text": text.astype("<u2"),
+                "propsets": ps, "props": pe}

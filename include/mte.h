@@ -1,0 +1,209 @@
+/*
+ * mte.h — C-ABI of the MI355X batched sequence-merge engine (libmte.so).
+ *
+ * The engine replays *sequenced* merge-tree messages for many independent
+ * documents at once, as an observer client would (every message is remote).
+ * It replaces, for that path, the following reference interfaces
+ * (paths relative to /root/reference/packages/dds/merge-tree/src/):
+ *
+ *   Client.applyMsg(msg, local=false)        client.ts:918-935
+ *     -> Client.applyRemoteOp                client.ts:862-889
+ *        -> applyInsertOp / applyRemoveRangeOp / applyAnnotateRangeOp
+ *                                            client.ts:470-505 / 405-428 / 435-463
+ *        -> MergeTree.insertSegments         mergeTree.ts:1394-1422
+ *        -> MergeTree.markRangeRemoved       mergeTree.ts:1908-2000
+ *        -> MergeTree.annotateRange          mergeTree.ts:1864-1906
+ *     -> Client.updateSeqNumbers / setMinSeq client.ts:937-945, mergeTree.ts:1077-1093
+ *   Read-out: TestClient.getText             test/testClient.ts:148-150
+ *             Client.getLength               client.ts:1161
+ *             Client.getPropertiesAtPosition client.ts:1133-1141
+ *
+ * Conventions: every function returns an int status (0 = MTE_OK, < 0 = error,
+ * never an exception or longjmp across the ABI).  Input buffers are copied
+ * before the call returns, so the caller may free them.  Outputs go to caller
+ * buffers (query-size-then-fill where sizes are data dependent).  One mte_ctx
+ * drives one HIP device; a ctx is not thread-safe, different ctxs are
+ * independent (one per process / GPU).  No torch or HIP types appear here.
+ */
+#ifndef MTE_H_
+#define MTE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTE_ABI_VERSION 1
+
+/* Property key planes held per segment (host interns key strings to 0..n_keys-1). */
+#define MTE_MAX_KEYS 8
+/* Distinct short client ids per document (removedClientIds is a bitmask). */
+#define MTE_MAX_CLIENTS 32
+
+/* ---- status codes ---------------------------------------------------------
+ * Where the reference raises an assert with a hex code, the equivalent code is
+ * noted (common-utils assert(cond, 0xNNN)).                                  */
+#define MTE_OK 0
+#define MTE_E_INVALID_ARG (-1)
+#define MTE_E_NO_DEVICE (-2)   /* no HIP device / HIP runtime error at create   */
+#define MTE_E_HIP (-3)         /* HIP runtime error (see mte_last_error)        */
+#define MTE_E_CAPACITY (-4)    /* doc exceeded its segment capacity             */
+#define MTE_E_SEQ_ORDER (-5)   /* seq <= currentSeq          (0x030, 0x038)     */
+#define MTE_E_MSN_ORDER (-6)   /* msn < window minSeq        (0x031, 0x04f)     */
+#define MTE_E_MSN_GT_SEQ (-7)  /* msn > seq                  (0x039, 0x04e)     */
+#define MTE_E_INSERT_FAILED (-8) /* "MergeTree insert failed" mergeTree.ts:1666-1672 */
+#define MTE_E_UNSUPPORTED (-9) /* op shape outside the engine (combiningOp other
+                                  than rewrite, relativePos, local/ack ops)     */
+#define MTE_E_STATE (-10)      /* call out of order (e.g. run before submit)    */
+#define MTE_E_OOM (-11)        /* device or host allocation failed              */
+#define MTE_E_CLIENT_RANGE (-12) /* short client id >= MTE_MAX_CLIENTS          */
+
+/* ---- op records ----------------------------------------------------------- */
+/* MergeTreeDeltaType, ops.ts:43-48.  NOOP = a sequenced message that is not an
+ * "op" (or an insert without seg): it still advances currentSeq / minSeq
+ * (client.ts:922, 934).  GROUP ops (ops.ts:121-124) are flattened by the host
+ * into consecutive records with the same seq; only the last carries MSG_END.  */
+#define MTE_OP_INSERT 0
+#define MTE_OP_REMOVE 1
+#define MTE_OP_ANNOTATE 2
+#define MTE_OP_NOOP 3
+
+#define MTE_F_MARKER 0x0001u  /* insert spec {marker:{refType}} (mergeTreeNodes.ts:602-609) */
+#define MTE_F_MSG_END 0x0002u /* last record of its message: window update follows      */
+#define MTE_F_REWRITE 0x0004u /* annotate combiningOp {name:"rewrite"} (segmentPropertiesManager.ts:105-119) */
+
+#define MTE_NO_PROPS 0xFFFFFFFFu
+
+/* 32-byte op record (ISequencedDocumentMessage + IMergeTreeDeltaOp, packed).   */
+typedef struct mte_op {
+  int32_t seq;     /* sequenceNumber                                          */
+  int32_t ref_seq; /* referenceSequenceNumber                                 */
+  int32_t min_seq; /* minimumSequenceNumber                                   */
+  uint8_t type;    /* MTE_OP_*                                                */
+  uint8_t client;  /* short client id in first-seen order (client.ts:683-698) */
+  uint16_t flags;  /* MTE_F_*                                                 */
+  int32_t pos1;    /* insert pos / range start                                */
+  int32_t pos2;    /* range end; insert text: UTF-16 unit count; marker: refType */
+  uint32_t a;      /* insert text: unit offset in the batch text; annotate: propset */
+  uint32_t b;      /* insert: propset of seg.props, or MTE_NO_PROPS            */
+} mte_op;
+
+/* A property set: entries[first .. first+count).  value 0 = JSON null (delete
+ * the key, segmentPropertiesManager.ts:142-147); other values are host-interned
+ * ids of canonical JSON values (equality == matchProperties, properties.ts:66). */
+typedef struct mte_prop {
+  uint32_t key;
+  uint32_t value;
+} mte_prop;
+typedef struct mte_propset {
+  uint32_t first;
+  uint32_t count;
+} mte_propset;
+
+/* ---- context / documents -------------------------------------------------- */
+typedef struct mte_ctx mte_ctx;
+
+typedef struct mte_config {
+  int32_t device;        /* HIP device ordinal                                  */
+  uint32_t n_keys;       /* property planes per segment, 0..MTE_MAX_KEYS        */
+  uint32_t seg_capacity; /* segments per doc kept in HBM (0 = default 4096)     */
+  uint32_t flags;        /* reserved, 0                                         */
+} mte_config;
+
+/* IMergeTreeOptions.mergeTreeUseNewLengthCalculations, mergeTree.ts:386-399. */
+#define MTE_DOC_NEW_LENGTH_CALC 0x1u
+
+/* Initial document: one text segment inserted before collaboration starts, as
+ * the reference replay harness does (client.replay.spec.ts:22-23): seq 0
+ * (UniversalSequenceNumber) and clientId -1 (LocalClientId), constants.ts:11,14. */
+typedef struct mte_doc_init {
+  uint32_t text_off; /* units offset into the load text buffer                */
+  uint32_t text_len; /* 0 = empty document                                    */
+  uint32_t flags;    /* MTE_DOC_*                                             */
+  uint32_t propset;  /* props of the initial segment, or MTE_NO_PROPS          */
+  int32_t min_seq;   /* collab window at load (startOrUpdateCollaboration)    */
+  int32_t cur_seq;
+} mte_doc_init;
+
+/* One batch of sequenced ops for all documents of the ctx. */
+typedef struct mte_batch {
+  uint32_t n_docs;            /* must equal the loaded doc count               */
+  const uint64_t* op_offsets; /* n_docs+1: doc d owns ops[op_offsets[d]..[d+1]) */
+  const mte_op* ops;          /* per doc in sequence order                     */
+  uint64_t n_ops;
+  const uint16_t* text; /* UTF-16 payload of inserts (mte_op.a/.pos2)        */
+  uint64_t text_units;
+  const mte_propset* propsets;
+  uint32_t n_propsets;
+  const mte_prop* props;
+  uint32_t n_props;
+} mte_batch;
+
+typedef struct mte_stats {
+  uint64_t ops_applied;     /* records applied (NOOPs included)               */
+  uint64_t segs_scanned;    /* sum over ops of live segments before the op    */
+  uint64_t segs_written;    /* split halves + inserted + marked segments      */
+  uint64_t prop_writes;     /* (segment, key) property writes                 */
+  uint64_t units_inserted;  /* UTF-16 units inserted                          */
+  uint64_t max_segs;        /* max segments held by any doc                   */
+  double kernel_ms;         /* device time of the last mte_run (HIP events)   */
+  double algo_bytes;        /* sum of B_op of the last run   */
+} mte_stats;
+
+/* Per-doc read-out (query-size-then-fill).  On input the *_cap fields give the
+ * capacity of the caller arrays (0 / NULL = query only); on output the n_*
+ * fields give the sizes.  Segments are the visible (non-removed) segments in
+ * document order; text is the getText() string (markers contribute no units,
+ * MergeTreeTextHelper.ts:49-74).                                              */
+typedef struct mte_doc_view {
+  int32_t status;  /* 0 or the MTE_E_* that stopped this doc                 */
+  int32_t cur_seq; /* collabWindow.currentSeq                               */
+  int32_t min_seq; /* collabWindow.minSeq                                   */
+  uint32_t length; /* getLength(): visible units incl. markers              */
+  uint16_t* text;
+  uint32_t text_cap;
+  uint32_t n_text;
+  uint32_t* seg_len;   /* per visible segment: length                       */
+  uint32_t* seg_kind;  /* 0 = text, 1 + refType = marker                    */
+  uint32_t* seg_props; /* n_keys values per segment (0 = absent)            */
+  uint32_t seg_cap;
+  uint32_t n_segs;
+} mte_doc_view;
+
+int mte_abi_version(void);
+const char* mte_strerror(int code);
+
+int mte_create(const mte_config* cfg, mte_ctx** out);
+int mte_destroy(mte_ctx* ctx);
+const char* mte_last_error(const mte_ctx* ctx);
+
+/* Load (or reload) all documents; resets every doc to its initial state. */
+int mte_load_docs(mte_ctx* ctx, uint32_t n_docs, const mte_doc_init* docs,
+                  const uint16_t* text, uint64_t text_units,
+                  const mte_propset* propsets, uint32_t n_propsets,
+                  const mte_prop* props, uint32_t n_props);
+
+/* Upload one batch (host -> HBM, async on the ctx stream). */
+int mte_submit(mte_ctx* ctx, const mte_batch* batch);
+/* Enqueue the replay of the submitted batch; returns without waiting. */
+int mte_run(mte_ctx* ctx);
+/* Wait for the ctx stream; returns the first per-doc error, if any. */
+int mte_sync(mte_ctx* ctx);
+/* Restore every doc to its loaded state (device side); the batch stays. */
+int mte_reset(mte_ctx* ctx);
+
+/* Canonical per-doc digest, 4 x uint64 per doc (see DESIGN.md "Digest"). */
+int mte_digest(mte_ctx* ctx, uint64_t* out, uint32_t n_docs);
+/* Same digest written to a caller-owned device buffer (for RCCL gathers). */
+int mte_digest_device(mte_ctx* ctx, void* device_out, uint32_t n_docs);
+
+int mte_read_doc(mte_ctx* ctx, uint32_t doc, mte_doc_view* view);
+int mte_doc_status(mte_ctx* ctx, int32_t* out, uint32_t n_docs);
+int mte_stats_get(mte_ctx* ctx, mte_stats* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTE_H_ */

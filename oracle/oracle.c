@@ -1,0 +1,587 @@
+/*
+ * oracle.c — CPU restatement of merge-tree observer replay (TEST INFRASTRUCTURE).
+ *
+ * This file restates, for a client that only receives sequenced remote ops,
+ * the semantics of the reference TypeScript merge-tree
+ * (/root/reference/packages/dds/merge-tree/src, cited below as file:line).
+ * It is a *flat* restatement: a document is an ordered array of segments and
+ * every perspective length is recomputed by a linear scan, instead of the
+ * reference's B+tree with PartialSequenceLengths.  SURVEY.md Appendix A and
+ * DESIGN.md ("Flat restatement") argue the equivalence; the golden fixtures
+ * pin it.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it.
+ */
+#include "oracle.h"
+
+#include <limits.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define NONE_SEQ INT32_MAX /* "removedSeq undefined" */
+
+typedef struct {
+  int32_t len;   /* cachedLength (text: UTF-16 units, marker: 1)          */
+  int32_t seq;   /* insert seq (UniversalSequenceNumber 0 for load text)  */
+  int32_t rseq;  /* removedSeq or NONE_SEQ                                */
+  uint32_t rmask;/* removedClientIds as a set (mergeTreeNodes.ts:134-150) */
+  int32_t cli;   /* clientId (-1 = LocalClientId, constants.ts:14)        */
+  uint32_t kind; /* 0 text, 1 + refType for a marker                      */
+  uint32_t toff; /* text offset into the ctx text arena                   */
+  uint32_t props[MTE_MAX_KEYS];
+} oseg;
+
+typedef struct {
+  oseg* s;
+  uint32_t n, cap;
+  int32_t min_seq, cur_seq;
+  uint32_t flags;
+  int32_t status;
+  /* stats */
+  uint64_t ops, scanned, written, pwrites, units, max_segs;
+  /* scratch */
+  int32_t* L;
+  int64_t* P;
+  uint32_t scratch_cap;
+  /* loaded state, for reload */
+  mte_doc_init init;
+  uint32_t init_props[MTE_MAX_KEYS];
+} odoc;
+
+struct orc_ctx {
+  uint32_t n_keys;
+  uint32_t n_docs;
+  odoc* docs;
+  uint16_t* arena;
+  uint64_t arena_n, arena_cap;
+};
+
+/* ------------------------------------------------------------------------ */
+
+static int arena_append(orc_ctx* c, const uint16_t* t, uint64_t n, uint64_t* base) {
+  if (c->arena_n + n > c->arena_cap) {
+    uint64_t nc = c->arena_cap ? c->arena_cap : 1024;
+    while (nc < c->arena_n + n) nc *= 2;
+    uint16_t* a = (uint16_t*)realloc(c->arena, nc * sizeof(uint16_t));
+    if (!a) return MTE_E_OOM;
+    c->arena = a;
+    c->arena_cap = nc;
+  }
+  *base = c->arena_n;
+  if (n) memcpy(c->arena + c->arena_n, t, n * sizeof(uint16_t));
+  c->arena_n += n;
+  return MTE_OK;
+}
+
+static int doc_reserve(odoc* d, uint32_t need) {
+  if (need <= d->cap) return MTE_OK;
+  uint32_t nc = d->cap ? d->cap : 64;
+  while (nc < need) nc *= 2;
+  oseg* s = (oseg*)realloc(d->s, (size_t)nc * sizeof(oseg));
+  if (!s) return MTE_E_OOM;
+  d->s = s;
+  d->cap = nc;
+  return MTE_OK;
+}
+
+static int doc_scratch(odoc* d) {
+  if (d->n <= d->scratch_cap) return MTE_OK;
+  uint32_t nc = d->cap;
+  int32_t* L = (int32_t*)realloc(d->L, (size_t)nc * sizeof(int32_t));
+  if (!L) return MTE_E_OOM;
+  d->L = L;
+  int64_t* P = (int64_t*)realloc(d->P, (size_t)nc * sizeof(int64_t));
+  if (!P) return MTE_E_OOM;
+  d->P = P;
+  d->scratch_cap = nc;
+  return MTE_OK;
+}
+
+/* Insert `cnt` empty slots at index `at` (shifting the tail right). */
+static int doc_open(odoc* d, uint32_t at, uint32_t cnt) {
+  int rc = doc_reserve(d, d->n + cnt);
+  if (rc) return rc;
+  memmove(d->s + at + cnt, d->s + at, (size_t)(d->n - at) * sizeof(oseg));
+  d->n += cnt;
+  return MTE_OK;
+}
+
+/*
+ * Perspective length of a leaf for (refSeq r, clientId c), with m = the
+ * window minSeq before this message.  Returns -1 for "undefined".
+ *   new calc:  mergeTree.ts:1003-1026
+ *   legacy:    mergeTree.ts:1028-1054
+ * The observer never sends, so the local branch (mergeTree.ts:985-995,
+ * localNetLength 553-594) is never taken for op application.
+ */
+static inline int32_t leaf_len(const oseg* s, int32_t r, int c, int32_t m, int newcalc) {
+  const int removed = s->rseq != NONE_SEQ;
+  const int by_c = (int)((s->rmask >> c) & 1u);
+  if (newcalc) {
+    if (removed) {
+      if (s->rseq <= m) return -1;
+      if (s->rseq <= r || by_c) return 0;
+    }
+    return (s->seq <= r || s->cli == c) ? s->len : 0;
+  }
+  if (removed && s->rseq <= r) return -1;
+  if (s->cli == c || s->seq <= r) return (removed && by_c) ? 0 : s->len;
+  return removed ? -1 : 0;
+}
+
+/* L[i] and exclusive prefix P[i] (undefined leaves contribute 0).  Returns the
+ * total perspective length.  This is the flat restatement of nodeLength on
+ * blocks (partialLengths.ts:667-702 == sum of leaf lengths, test/testUtils.ts
+ * :173-248). */
+static int64_t doc_lengths(odoc* d, int32_t r, int c, int32_t m, int newcalc) {
+  int64_t p = 0;
+  for (uint32_t i = 0; i < d->n; i++) {
+    int32_t l = leaf_len(&d->s[i], r, c, m, newcalc);
+    d->L[i] = l;
+    d->P[i] = p;
+    if (l > 0) p += l;
+  }
+  return p;
+}
+
+/*
+ * ensureIntervalBoundary(pos) (mergeTree.ts:1698-1702): the insertingWalk with
+ * TreeMaintenanceSequenceNumber enters the first leaf with pos < len (breakTie
+ * is false for it, 1705-1721) and splitLeafSegment splits it when the offset is
+ * > 0 (1681-1696).  The tail inherits seq/clientId/removal/props
+ * (mergeTreeNodes.ts:505-534, textSegment.ts:105-113); markers never split
+ * (mergeTreeNodes.ts:644-646).  L/P are kept consistent.  Returns the index of
+ * the new tail segment or -1.
+ */
+static int64_t doc_split_at(odoc* d, int64_t pos, uint64_t* written) {
+  for (uint32_t i = 0; i < d->n; i++) {
+    int32_t l = d->L[i];
+    if (l <= 0) continue;
+    if (pos < d->P[i]) return -1;
+    if (pos < d->P[i] + l) {
+      int64_t off = pos - d->P[i];
+      if (off == 0 || d->s[i].kind != 0) return -1;
+      if (doc_open(d, i + 1, 1)) return -2;
+      /* keep scratch arrays in step */
+      if (doc_scratch(d)) return -2;
+      memmove(d->L + i + 2, d->L + i + 1, (size_t)(d->n - i - 2) * sizeof(int32_t));
+      memmove(d->P + i + 2, d->P + i + 1, (size_t)(d->n - i - 2) * sizeof(int64_t));
+      oseg* head = &d->s[i];
+      oseg* tail = &d->s[i + 1];
+      *tail = *head;
+      tail->len = head->len - (int32_t)off;
+      tail->toff = head->toff + (uint32_t)off;
+      head->len = (int32_t)off;
+      d->L[i] = (int32_t)off;
+      d->L[i + 1] = tail->len;
+      d->P[i + 1] = d->P[i] + off;
+      *written += 2;
+      return (int64_t)i + 1;
+    }
+  }
+  return -1;
+}
+
+/* PropertiesManager.addProperties for a remote observer (collaborating, no
+ * pending local keys, so shouldModifyKey is true for every key):
+ * segmentPropertiesManager.ts:63-151.  rewrite first clears the keys not in
+ * newProps (105-119); then null deletes, anything else sets (121-148).  The
+ * falsy-value test of the rewrite loop cancels against the set loop, so the net
+ * effect is "clear all, then apply". */
+static uint64_t apply_props(uint32_t* props, uint32_t n_keys, const mte_propset* ps,
+                            const mte_prop* pe, int rewrite) {
+  uint64_t w = 0;
+  if (rewrite) {
+    for (uint32_t k = 0; k < n_keys; k++) props[k] = 0;
+  }
+  for (uint32_t j = 0; j < ps->count; j++) {
+    const mte_prop* p = &pe[ps->first + j];
+    if (p->key < n_keys) {
+      props[p->key] = p->value; /* value 0 == null == delete */
+      w++;
+    }
+  }
+  return w;
+}
+
+typedef struct {
+  const mte_batch* b;
+  uint64_t text_base;
+  uint32_t n_keys;
+  const uint16_t* arena;
+} apply_env;
+
+/* Client.completeAndLogOp asserts (client.ts:525-528). */
+static int check_op_window(const odoc* d, const mte_op* op) {
+  if (!(d->cur_seq < op->seq)) return MTE_E_SEQ_ORDER;
+  if (!(d->min_seq <= op->min_seq)) return MTE_E_MSN_ORDER;
+  return MTE_OK;
+}
+
+/* Canonical zamboni: drop tombstones with removedSeq <= minSeq.  The reference
+ * unlinks the same segments lazily (scourNode, mergeTree.ts:681-747); the
+ * difference is not observable (such leaves are "undefined" for every later
+ * op in both length modes, and never visible). */
+static void doc_compact(odoc* d) {
+  uint32_t w = 0;
+  for (uint32_t i = 0; i < d->n; i++) {
+    if (d->s[i].rseq != NONE_SEQ && d->s[i].rseq <= d->min_seq) continue;
+    if (w != i) d->s[w] = d->s[i];
+    w++;
+  }
+  d->n = w;
+}
+
+/* One op record.  Client.applyMsg -> applyRemoteOp (client.ts:918-935,
+ * 862-889) -> updateSeqNumbers (937-945). */
+static int doc_apply(odoc* d, const mte_op* op, const apply_env* env) {
+  const int newcalc = (d->flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
+  const int32_t r = op->ref_seq, s = op->seq, m = d->min_seq;
+  const int c = op->client;
+  int rc;
+  if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
+  d->ops++;
+  if (d->n > d->max_segs) d->max_segs = d->n;
+  if (op->type != MTE_OP_NOOP) d->scanned += d->n;
+
+  if (op->type == MTE_OP_INSERT) {
+    /* applyInsertOp (client.ts:470-505) -> insertSegments (mergeTree.ts:1394-1422) */
+    if ((rc = doc_scratch(d))) return rc;
+    int64_t total = doc_lengths(d, r, c, m, newcalc);
+    int64_t pos = op->pos1;
+    int64_t tail = doc_split_at(d, pos, &d->written); /* ensureIntervalBoundary */
+    if (tail == -2) return MTE_E_OOM;
+    const int is_marker = (op->flags & MTE_F_MARKER) != 0;
+    int32_t len = is_marker ? 1 : op->pos2;
+    if (len > 0) { /* blockInsert skips zero-length segments, mergeTree.ts:1645 */
+      /* insertingWalk + breakTie (mergeTree.ts:1723-1825, 1705-1721): the new
+       * segment goes before the first defined leaf whose prefix equals pos
+       * (a zero-length leaf at pos ties in favour of the newer seq), else at
+       * the end; undefined leaves are skipped.  pos > length fails
+       * (mergeTree.ts:1666-1672). */
+      uint32_t at = d->n;
+      if (tail >= 0) {
+        at = (uint32_t)tail;
+      } else {
+        for (uint32_t i = 0; i < d->n; i++) {
+          if (d->L[i] >= 0 && d->P[i] >= pos) { at = i; break; }
+        }
+        if (at == d->n && pos > total) return MTE_E_INSERT_FAILED;
+      }
+      if ((rc = doc_open(d, at, 1))) return rc;
+      oseg* ns = &d->s[at];
+      memset(ns, 0, sizeof(*ns));
+      ns->len = len;
+      ns->seq = s;
+      ns->cli = c;
+      ns->rseq = NONE_SEQ;
+      ns->rmask = 0;
+      if (is_marker) {
+        ns->kind = 1u + (uint32_t)op->pos2;
+        ns->toff = 0;
+      } else {
+        ns->kind = 0;
+        ns->toff = (uint32_t)(env->text_base + op->a);
+        d->units += (uint64_t)len;
+      }
+      if (op->b != MTE_NO_PROPS)
+        d->pwrites += apply_props(ns->props, env->n_keys, &env->b->propsets[op->b], env->b->props, 0);
+      d->written += 1;
+    }
+    if ((rc = check_op_window(d, op))) return rc;
+  } else if (op->type == MTE_OP_REMOVE || op->type == MTE_OP_ANNOTATE) {
+    /* markRangeRemoved (mergeTree.ts:1908-2000) / annotateRange (1864-1906):
+     * two ensureIntervalBoundary, then nodeMap (2274-2330) visits the leaves
+     * with len > 0 overlapping [start, end). */
+    if ((rc = doc_scratch(d))) return rc;
+    int64_t start = op->pos1, end = op->pos2;
+    doc_lengths(d, r, c, m, newcalc);
+    if (doc_split_at(d, start, &d->written) == -2) return MTE_E_OOM;
+    if (doc_split_at(d, end, &d->written) == -2) return MTE_E_OOM;
+    if (end != start) {
+      for (uint32_t i = 0; i < d->n; i++) {
+        int32_t l = d->L[i];
+        if (l <= 0) continue;
+        if (d->P[i] >= end) break;
+        if (d->P[i] + l <= start) continue;
+        oseg* g = &d->s[i];
+        if (op->type == MTE_OP_REMOVE) {
+          /* markRemoved closure (mergeTree.ts:1924-1962): keep the earlier
+           * removedSeq and add the client to removedClientIds (1939-1942). */
+          if (g->rseq == NONE_SEQ) {
+            g->rseq = s;
+            g->rmask = 1u << c;
+          } else {
+            g->rmask |= 1u << c;
+          }
+        } else {
+          d->pwrites += apply_props(g->props, env->n_keys, &env->b->propsets[op->a], env->b->props,
+                                    (op->flags & MTE_F_REWRITE) != 0);
+        }
+        d->written += 1;
+      }
+    }
+    if ((rc = check_op_window(d, op))) return rc;
+  } else if (op->type != MTE_OP_NOOP) {
+    return MTE_E_INVALID_ARG;
+  }
+
+  if (op->flags & MTE_F_MSG_END) {
+    /* updateSeqNumbers (client.ts:937-945) -> setMinSeq (mergeTree.ts:1077-1093) */
+    if (!(d->cur_seq <= s)) return MTE_E_SEQ_ORDER;          /* 0x038 */
+    d->cur_seq = s;
+    if (!(op->min_seq <= s)) return MTE_E_MSN_GT_SEQ;        /* 0x039 / 0x04e */
+    if (!(d->min_seq <= op->min_seq)) return MTE_E_MSN_ORDER; /* 0x04f */
+    if (op->min_seq > d->min_seq) {
+      d->min_seq = op->min_seq;
+      doc_compact(d);
+    }
+  }
+  return MTE_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+
+int orc_create(uint32_t n_keys, orc_ctx** out) {
+  if (!out || n_keys > MTE_MAX_KEYS) return MTE_E_INVALID_ARG;
+  orc_ctx* c = (orc_ctx*)calloc(1, sizeof(orc_ctx));
+  if (!c) return MTE_E_OOM;
+  c->n_keys = n_keys;
+  *out = c;
+  return MTE_OK;
+}
+
+static void free_docs(orc_ctx* c) {
+  for (uint32_t i = 0; i < c->n_docs; i++) {
+    free(c->docs[i].s);
+    free(c->docs[i].L);
+    free(c->docs[i].P);
+  }
+  free(c->docs);
+  c->docs = NULL;
+  c->n_docs = 0;
+}
+
+int orc_destroy(orc_ctx* c) {
+  if (!c) return MTE_E_INVALID_ARG;
+  free_docs(c);
+  free(c->arena);
+  free(c);
+  return MTE_OK;
+}
+
+int orc_load_docs(orc_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const uint16_t* text,
+                  uint64_t text_units, const mte_propset* propsets, uint32_t n_propsets,
+                  const mte_prop* props, uint32_t n_props) {
+  (void)n_props;
+  if (!c || (n_docs && !docs)) return MTE_E_INVALID_ARG;
+  free_docs(c);
+  c->arena_n = 0;
+  uint64_t base = 0;
+  int rc = arena_append(c, text, text_units, &base);
+  if (rc) return rc;
+  c->docs = (odoc*)calloc(n_docs ? n_docs : 1, sizeof(odoc));
+  if (!c->docs) return MTE_E_OOM;
+  c->n_docs = n_docs;
+  for (uint32_t i = 0; i < n_docs; i++) {
+    odoc* d = &c->docs[i];
+    const mte_doc_init* in = &docs[i];
+    if ((uint64_t)in->text_off + in->text_len > text_units) return MTE_E_INVALID_ARG;
+    d->init = *in;
+    d->flags = in->flags;
+    d->min_seq = in->min_seq;
+    d->cur_seq = in->cur_seq;
+    if (in->text_len > 0) {
+      if ((rc = doc_reserve(d, 64))) return rc;
+      oseg* g = &d->s[0];
+      memset(g, 0, sizeof(*g));
+      g->len = (int32_t)in->text_len;
+      g->seq = 0;   /* UniversalSequenceNumber */
+      g->cli = -1;  /* LocalClientId */
+      g->rseq = NONE_SEQ;
+      g->toff = (uint32_t)(base + in->text_off);
+      if (in->propset != MTE_NO_PROPS) {
+        if (in->propset >= n_propsets) return MTE_E_INVALID_ARG;
+        apply_props(g->props, c->n_keys, &propsets[in->propset], props, 0);
+      }
+      d->n = 1;
+    }
+  }
+  return MTE_OK;
+}
+
+typedef struct {
+  orc_ctx* c;
+  const mte_batch* b;
+  uint64_t base;
+  uint32_t d0, d1, stride;
+} worker_arg;
+
+static void* worker(void* p) {
+  worker_arg* w = (worker_arg*)p;
+  apply_env env = {w->b, w->base, w->c->n_keys, w->c->arena};
+  for (uint32_t di = w->d0; di < w->d1; di += w->stride) {
+    odoc* d = &w->c->docs[di];
+    if (d->status) continue;
+    for (uint64_t k = w->b->op_offsets[di]; k < w->b->op_offsets[di + 1]; k++) {
+      int rc = doc_apply(d, &w->b->ops[k], &env);
+      if (rc) {
+        d->status = rc;
+        break;
+      }
+    }
+  }
+  return NULL;
+}
+
+int orc_apply_batch(orc_ctx* c, const mte_batch* b, int n_threads) {
+  if (!c || !b || b->n_docs != c->n_docs || !b->op_offsets) return MTE_E_INVALID_ARG;
+  if (b->op_offsets[b->n_docs] != b->n_ops) return MTE_E_INVALID_ARG;
+  for (uint64_t k = 0; k < b->n_ops; k++) {
+    const mte_op* op = &b->ops[k];
+    if (op->type == MTE_OP_INSERT && !(op->flags & MTE_F_MARKER) && op->pos2 > 0 &&
+        (uint64_t)op->a + (uint64_t)op->pos2 > b->text_units)
+      return MTE_E_INVALID_ARG;
+    if (op->type == MTE_OP_INSERT && op->b != MTE_NO_PROPS && op->b >= b->n_propsets)
+      return MTE_E_INVALID_ARG;
+    if (op->type == MTE_OP_ANNOTATE && op->a >= b->n_propsets) return MTE_E_INVALID_ARG;
+  }
+  uint64_t base = 0;
+  int rc = arena_append(c, b->text, b->text_units, &base);
+  if (rc) return rc;
+  if (n_threads < 1) n_threads = 1;
+  if ((uint32_t)n_threads > c->n_docs) n_threads = c->n_docs ? (int)c->n_docs : 1;
+  worker_arg* args = (worker_arg*)calloc((size_t)n_threads, sizeof(worker_arg));
+  pthread_t* th = (pthread_t*)calloc((size_t)n_threads, sizeof(pthread_t));
+  if (!args || !th) {
+    free(args);
+    free(th);
+    return MTE_E_OOM;
+  }
+  for (int t = 0; t < n_threads; t++) {
+    args[t] = (worker_arg){c, b, base, (uint32_t)t, c->n_docs, (uint32_t)n_threads};
+  }
+  if (n_threads == 1) {
+    worker(&args[0]);
+  } else {
+    for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, worker, &args[t]);
+    for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+  }
+  free(args);
+  free(th);
+  return MTE_OK;
+}
+
+int orc_read_doc(orc_ctx* c, uint32_t doc, mte_doc_view* v) {
+  if (!c || !v || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  odoc* d = &c->docs[doc];
+  v->status = d->status;
+  v->cur_seq = d->cur_seq;
+  v->min_seq = d->min_seq;
+  uint32_t length = 0, nt = 0, ns = 0;
+  for (uint32_t i = 0; i < d->n; i++) {
+    const oseg* g = &d->s[i];
+    if (g->rseq != NONE_SEQ) continue; /* gatherText: removed -> not visible */
+    if (ns < v->seg_cap) {
+      if (v->seg_len) v->seg_len[ns] = (uint32_t)g->len;
+      if (v->seg_kind) v->seg_kind[ns] = g->kind;
+      if (v->seg_props)
+        for (uint32_t k = 0; k < c->n_keys; k++) v->seg_props[(size_t)ns * c->n_keys + k] = g->props[k];
+    }
+    ns++;
+    length += (uint32_t)g->len;
+    if (g->kind == 0) {
+      for (int32_t u = 0; u < g->len; u++) {
+        if (nt < v->text_cap && v->text) v->text[nt] = c->arena[g->toff + (uint32_t)u];
+        nt++;
+      }
+    }
+  }
+  v->length = length;
+  v->n_text = nt;
+  v->n_segs = ns;
+  return MTE_OK;
+}
+
+/* ---- canonical digest (DESIGN.md "Digest") ------------------------------- */
+#define M61 ((1ull << 61) - 1)
+static const uint64_t DIG_B1 = 0x1d8e4e27c47d124full % ((1ull << 61) - 1);
+static const uint64_t DIG_B2 = 0x0a0761d6478bd642ull % ((1ull << 61) - 1);
+
+static inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+static inline uint64_t mulmod61(uint64_t a, uint64_t b) {
+  unsigned __int128 p = (unsigned __int128)a * b;
+  uint64_t lo = (uint64_t)(p & M61), hi = (uint64_t)(p >> 61);
+  uint64_t r = lo + hi;
+  if (r >= M61) r -= M61;
+  return r;
+}
+static inline uint64_t addmod61(uint64_t a, uint64_t b) {
+  uint64_t r = a + b;
+  if (r >= M61) r -= M61;
+  return r;
+}
+
+int orc_digest(orc_ctx* c, uint64_t* out, uint32_t n_docs) {
+  if (!c || !out || n_docs != c->n_docs) return MTE_E_INVALID_ARG;
+  for (uint32_t di = 0; di < n_docs; di++) {
+    odoc* d = &c->docs[di];
+    uint64_t n = 0, h1 = 0, h2 = 0, sum = 0;
+    for (uint32_t i = 0; i < d->n; i++) {
+      const oseg* g = &d->s[i];
+      if (g->rseq != NONE_SEQ) continue;
+      uint64_t ph = 0;
+      for (uint32_t k = 0; k < c->n_keys; k++)
+        if (g->props[k]) ph += mix64(((uint64_t)(k + 1) << 32) | g->props[k]);
+      for (int32_t u = 0; u < g->len; u++) {
+        uint64_t rec = g->kind == 0 ? (uint64_t)c->arena[g->toff + (uint32_t)u]
+                                    : ((1ull << 32) | (uint64_t)(g->kind - 1));
+        uint64_t x = mix64(rec * 0x9E3779B97F4A7C15ull + ph) % M61;
+        h1 = addmod61(mulmod61(h1, DIG_B1), x);
+        h2 = addmod61(mulmod61(h2, DIG_B2), x);
+        sum += x;
+        n++;
+      }
+    }
+    out[4 * (size_t)di + 0] = n;
+    out[4 * (size_t)di + 1] = h1;
+    out[4 * (size_t)di + 2] = h2;
+    out[4 * (size_t)di + 3] = sum;
+  }
+  return MTE_OK;
+}
+
+int orc_doc_status(orc_ctx* c, int32_t* out, uint32_t n_docs) {
+  if (!c || !out || n_docs != c->n_docs) return MTE_E_INVALID_ARG;
+  for (uint32_t i = 0; i < n_docs; i++) out[i] = c->docs[i].status;
+  return MTE_OK;
+}
+
+int orc_stats_get(orc_ctx* c, mte_stats* o) {
+  if (!c || !o) return MTE_E_INVALID_ARG;
+  memset(o, 0, sizeof(*o));
+  for (uint32_t i = 0; i < c->n_docs; i++) {
+    odoc* d = &c->docs[i];
+    o->ops_applied += d->ops;
+    o->segs_scanned += d->scanned;
+    o->segs_written += d->written;
+    o->prop_writes += d->pwrites;
+    o->units_inserted += d->units;
+    if (d->max_segs > o->max_segs) o->max_segs = d->max_segs;
+  }
+  o->algo_bytes = 32.0 * (double)o->ops_applied + 20.0 * (double)o->segs_scanned +
+                  20.0 * (double)o->segs_written + 4.0 * (double)o->prop_writes +
+                  2.0 * (double)o->units_inserted;
+  return MTE_OK;
+}
+
+int orc_doc_nsegs(orc_ctx* c, uint32_t doc, uint32_t* out) {
+  if (!c || !out || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  *out = c->docs[doc].n;
+  return MTE_OK;
+}

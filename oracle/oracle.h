@@ -1,0 +1,47 @@
+/*
+ * oracle.h — CPU restatement of the reference merge-tree observer replay.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker
+ * (or as the timed CPU baseline).  The product path (libmte.so) never links,
+ * loads or calls it.
+ *
+ * Pinning: the restatement is checked against all 1,920 round checkpoints of
+ * the 30 golden replay fixtures of the reference
+ * (packages/dds/merge-tree/src/test/results/ JSON files, replayed as in
+ * test/client.replay.spec.ts:16-60) and against known-answer scenarios
+ * transcribed from test/client.applyMsg.spec.ts, mergeTree.markRangeRemoved
+ * .spec.ts and mergeTree.annotate.spec.ts (tests/test_oracle_*.py).
+ *
+ * It takes the same op records / batches as include/mte.h.
+ */
+#ifndef MTE_ORACLE_H_
+#define MTE_ORACLE_H_
+
+#include "../include/mte.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_ctx orc_ctx;
+
+int orc_create(uint32_t n_keys, orc_ctx** out);
+int orc_destroy(orc_ctx* c);
+int orc_load_docs(orc_ctx* c, uint32_t n_docs, const mte_doc_init* docs,
+                  const uint16_t* text, uint64_t text_units,
+                  const mte_propset* propsets, uint32_t n_propsets,
+                  const mte_prop* props, uint32_t n_props);
+/* Apply a batch immediately, docs spread over n_threads pthreads. */
+int orc_apply_batch(orc_ctx* c, const mte_batch* b, int n_threads);
+int orc_read_doc(orc_ctx* c, uint32_t doc, mte_doc_view* v);
+int orc_digest(orc_ctx* c, uint64_t* out, uint32_t n_docs);
+int orc_doc_status(orc_ctx* c, int32_t* out, uint32_t n_docs);
+int orc_stats_get(orc_ctx* c, mte_stats* out);
+/* Segments currently held by a doc (canonical model: tombstones included). */
+int orc_doc_nsegs(orc_ctx* c, uint32_t doc, uint32_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
