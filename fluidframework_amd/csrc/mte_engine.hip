@@ -1,0 +1,1024 @@
+// mte_engine.hip — C-ABI (include/mte.h) + gfx950 kernels of the batched
+// sequence-merge engine.  See DESIGN.md for the data layout and the mapping
+// to the reference (packages/dds/merge-tree/src).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <type_traits>
+#include <string>
+#include <vector>
+
+#include "mte_kernels.h"
+
+using namespace mte;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// replay
+// ---------------------------------------------------------------------------
+
+struct OpView {  // wave-uniform copy of one record
+  int32_t seq, ref_seq, min_seq;
+  uint32_t type, client, flags;
+  int32_t pos1, pos2;
+  uint32_t a, b;
+};
+
+__device__ __forceinline__ OpView load_op(const mte_op* __restrict__ ops, uint64_t k) {
+  const mte_op o = ops[k];
+  OpView v;
+  v.seq = o.seq;
+  v.ref_seq = o.ref_seq;
+  v.min_seq = o.min_seq;
+  v.type = o.type;
+  v.client = o.client;
+  v.flags = o.flags;
+  v.pos1 = o.pos1;
+  v.pos2 = o.pos2;
+  v.a = o.a;
+  v.b = o.b;
+  return v;
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t apply_propset_seg(Seg<K>& s, const ReplayArgs& a, uint32_t psi) {
+  const mte_propset ps = a.ps[psi];
+  uint32_t w = 0;
+  for (uint32_t t = 0; t < ps.count; t++) {
+    const mte_prop p = a.pe[ps.first + t];
+    if (p.key < a.n_keys) {
+#pragma unroll
+      for (int k = 0; k < K; k++)
+        if ((uint32_t)k == p.key) s.pr[k] = p.value;
+      w++;
+    }
+  }
+  return w;
+}
+
+// Returns 0 = batch range done, 1 = re-pick E, or a negative MTE_E_*.
+template <int E, int K>
+__device__ int run_ops(const ReplayArgs& a, int doc, DocHdr& h, uint64_t& k, uint64_t k1, int emin,
+                       uint32_t* lds, unsigned long long (&st)[kNumStats]) {
+  const int l = lane_id();
+  const int base = l * E;
+  const uint64_t dbase = (uint64_t)doc * a.cap;
+  const bool newcalc = (h.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
+  int n = h.nseg;
+
+  Regs<E, K> R;
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    const int i = base + j;
+    if (i < n) {
+      R.len[j] = a.soa.len[dbase + i];
+      R.seq[j] = a.soa.seq[dbase + i];
+      R.rseq[j] = a.soa.rseq[dbase + i];
+      R.rmask[j] = a.soa.rmask[dbase + i];
+      R.meta[j] = a.soa.meta[dbase + i];
+      R.toff[j] = a.soa.toff[dbase + i];
+#pragma unroll
+      for (int kk = 0; kk < K; kk++) R.pr[kk][j] = a.soa.props[kk * a.soa.plane_stride + dbase + i];
+    } else {
+      R.len[j] = 0;
+      R.seq[j] = 0;
+      R.rseq[j] = 0;
+      R.rmask[j] = 0;
+      R.meta[j] = 0;
+      R.toff[j] = 0;
+#pragma unroll
+      for (int kk = 0; kk < K; kk++) R.pr[kk][j] = 0;
+    }
+  }
+
+  int reason = 0;
+  const int lim = kWave * E < (int)a.cap ? kWave * E : (int)a.cap;
+  for (; k < k1; k++) {
+    if (n + 2 > lim) {
+      reason = 1;
+      break;
+    }
+    const OpView op = load_op(a.ops, k);
+    st[kStOps]++;
+    if ((unsigned long long)n > st[kStMaxSegs]) st[kStMaxSegs] = (unsigned long long)n;
+    const int c = (int)op.client;
+    if (c >= MTE_MAX_CLIENTS) {
+      reason = MTE_E_CLIENT_RANGE;
+      break;
+    }
+    const int32_t r = op.ref_seq, s = op.seq, m = h.min_seq;
+
+    if (op.type == MTE_OP_INSERT) {
+      // Client.applyInsertOp -> MergeTree.insertSegments (client.ts:470-505,
+      // mergeTree.ts:1394-1422)
+      st[kStScanned] += (unsigned long long)n;
+      int32_t L[E], P[E];
+      leaf_lengths<E, K>(R, n, r, c, m, newcalc, L);
+      const int32_t total = prefix<E>(L, P);
+      const int32_t pos = op.pos1;
+      int32_t off = 0;
+      const int xs = find_split<E>(L, P, pos, &off);  // ensureIntervalBoundary
+      const bool marker = (op.flags & MTE_F_MARKER) != 0;
+      const int32_t nlen = marker ? 1 : op.pos2;
+      int g = -1;
+      if (xs < 0 && nlen > 0) {
+        g = find_slot<E>(L, P, pos);
+        if (g < 0) {
+          if (pos > total) {
+            reason = MTE_E_INSERT_FAILED;  // mergeTree.ts:1666-1672
+            break;
+          }
+          g = n;
+        }
+      }
+      Seg<K> ns;
+      if (nlen > 0) {
+        ns.len = nlen;
+        ns.seq = s;
+        ns.rseq = kNone;
+        ns.rmask = 0;
+        ns.meta = (uint32_t)(c + 1) | ((marker ? 1u + (uint32_t)op.pos2 : 0u) << 8);
+        ns.toff = marker ? 0u : a.text_base + op.a;
+#pragma unroll
+        for (int kk = 0; kk < K; kk++) ns.pr[kk] = 0;
+        if (op.b != MTE_NO_PROPS) st[kStPwrites] += apply_propset_seg<K>(ns, a, op.b);
+        if (!marker) st[kStUnits] += (unsigned long long)nlen;
+      }
+      if (xs >= 0) {
+        Seg<K> tail = get_seg<E, K>(R, xs);
+        tail.len -= off;
+        tail.toff += (uint32_t)off;
+        if (nlen > 0) {
+          shift_all<E, K>(R, xs + 1, xs + 2);
+          put_seg<E, K>(R, xs + 1, ns);
+          put_seg<E, K>(R, xs + 2, tail);
+          n += 2;
+          st[kStWritten] += 3;
+        } else {
+          shift_all<E, K>(R, xs + 1, INT32_MAX);
+          put_seg<E, K>(R, xs + 1, tail);
+          n += 1;
+          st[kStWritten] += 2;
+        }
+        put<E>(R.len, xs, off);  // head keeps [0, off)
+      } else if (nlen > 0) {
+        shift_all<E, K>(R, g, INT32_MAX);
+        put_seg<E, K>(R, g, ns);
+        n += 1;
+        st[kStWritten] += 1;
+      }
+    } else if (op.type == MTE_OP_REMOVE || op.type == MTE_OP_ANNOTATE) {
+      // markRangeRemoved (mergeTree.ts:1908-2000) / annotateRange (1864-1906)
+      st[kStScanned] += (unsigned long long)n;
+      const int32_t start = op.pos1, end = op.pos2;
+      int32_t L[E], P[E];
+      leaf_lengths<E, K>(R, n, r, c, m, newcalc, L);
+      prefix<E>(L, P);
+      int32_t oa = 0, ob = 0;
+      const int xa = find_split<E>(L, P, start, &oa);
+      const int xb = find_split<E>(L, P, end, &ob);
+      // order the (at most two) split events by (index, offset)
+      int x1 = xa, x2 = xb;
+      int32_t o1 = oa, o2 = ob;
+      if (x1 < 0 || (x2 >= 0 && (x2 < x1 || (x2 == x1 && ob < oa)))) {
+        x1 = xb;
+        x2 = xa;
+        o1 = ob;
+        o2 = oa;
+      }
+      if (x2 >= 0 && x1 == x2 && o1 == o2) x2 = -1;  // same boundary twice
+      if (x1 < 0) {
+        x1 = x2;
+        o1 = o2;
+        x2 = -1;
+      }
+      if (x1 >= 0 && x2 < 0) {
+        Seg<K> t = get_seg<E, K>(R, x1);
+        t.len -= o1;
+        t.toff += (uint32_t)o1;
+        shift_all<E, K>(R, x1 + 1, INT32_MAX);
+        put_seg<E, K>(R, x1 + 1, t);
+        put<E>(R.len, x1, o1);
+        n += 1;
+        st[kStWritten] += 2;
+      } else if (x1 >= 0) {
+        Seg<K> t1 = get_seg<E, K>(R, x1);
+        Seg<K> t2 = (x2 == x1) ? t1 : get_seg<E, K>(R, x2);
+        const int32_t len1 = t1.len, len2 = t2.len;
+        shift_all<E, K>(R, x1 + 1, x2 + 2);
+        put<E>(R.len, x1, o1);
+        if (x2 == x1) {  // three pieces of one segment
+          t1.len = o2 - o1;
+          t1.toff += (uint32_t)o1;
+          t2.len = len1 - o2;
+          t2.toff += (uint32_t)o2;
+        } else {
+          t1.len = len1 - o1;
+          t1.toff += (uint32_t)o1;
+          put<E>(R.len, x2 + 1, o2);  // head of the second split segment
+          t2.len = len2 - o2;
+          t2.toff += (uint32_t)o2;
+        }
+        put_seg<E, K>(R, x1 + 1, t1);
+        put_seg<E, K>(R, x2 + 2, t2);
+        n += 2;
+        st[kStWritten] += 4;
+      }
+      if (end != start) {
+        // nodeMap (mergeTree.ts:2274-2330): leaves with len > 0 overlapping [start, end)
+        leaf_lengths<E, K>(R, n, r, c, m, newcalc, L);
+        prefix<E>(L, P);
+        bool in[E];
+        unsigned cnt = 0;
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+          in[j] = L[j] > 0 && P[j] < end && P[j] + L[j] > start;
+          cnt += (unsigned)__popcll(__ballot(in[j]));
+        }
+        st[kStWritten] += cnt;
+        if (op.type == MTE_OP_REMOVE) {
+          // markRemoved (mergeTree.ts:1924-1962): keep the earliest removedSeq,
+          // add the client to removedClientIds
+          const uint32_t bit = 1u << c;
+#pragma unroll
+          for (int j = 0; j < E; j++) {
+            if (in[j]) {
+              R.rseq[j] = (R.rseq[j] == kNone) ? s : R.rseq[j];
+              R.rmask[j] |= bit;
+            }
+          }
+        } else {
+          // PropertiesManager.addProperties (segmentPropertiesManager.ts:63-151)
+          if (op.flags & MTE_F_REWRITE) {
+#pragma unroll
+            for (int kk = 0; kk < K; kk++)
+#pragma unroll
+              for (int j = 0; j < E; j++) R.pr[kk][j] = in[j] ? 0u : R.pr[kk][j];
+          }
+          const mte_propset ps = a.ps[op.a];
+          unsigned nw = 0;
+          for (uint32_t t = 0; t < ps.count; t++) {
+            const mte_prop p = a.pe[ps.first + t];
+            if (p.key >= a.n_keys) continue;
+            nw++;
+#pragma unroll
+            for (int kk = 0; kk < K; kk++) {
+              if ((uint32_t)kk == p.key) {
+#pragma unroll
+                for (int j = 0; j < E; j++) R.pr[kk][j] = in[j] ? p.value : R.pr[kk][j];
+              }
+            }
+          }
+          st[kStPwrites] += (unsigned long long)cnt * nw;
+        }
+      }
+    } else if (op.type != MTE_OP_NOOP) {
+      reason = MTE_E_INVALID_ARG;
+      break;
+    }
+
+    if (op.type != MTE_OP_NOOP) {  // Client.completeAndLogOp (client.ts:525-528)
+      if (!(h.cur_seq < s)) { reason = MTE_E_SEQ_ORDER; k++; break; }
+      if (!(h.min_seq <= op.min_seq)) { reason = MTE_E_MSN_ORDER; k++; break; }
+    }
+    if (op.flags & MTE_F_MSG_END) {
+      // updateSeqNumbers (client.ts:937-945) -> setMinSeq (mergeTree.ts:1077-1093)
+      if (!(h.cur_seq <= s)) { reason = MTE_E_SEQ_ORDER; k++; break; }
+      h.cur_seq = s;
+      if (!(op.min_seq <= s)) { reason = MTE_E_MSN_GT_SEQ; k++; break; }
+      if (!(h.min_seq <= op.min_seq)) { reason = MTE_E_MSN_ORDER; k++; break; }
+      if (op.min_seq > h.min_seq) {
+        h.min_seq = op.min_seq;
+        // zamboni: drop tombstones with removedSeq <= minSeq (stream compaction through LDS)
+        bool keep[E];
+        int32_t cntl = 0;
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+          keep[j] = (base + j < n) && !(R.rseq[j] != kNone && R.rseq[j] <= h.min_seq);
+          cntl += keep[j] ? 1 : 0;
+        }
+        const int32_t incl = wave_incl_scan(cntl);
+        const int n_new = rdlane(incl, kWave - 1);
+        if (n_new != n) {
+          int32_t dst[E];
+          int32_t d0 = incl - cntl;
+#pragma unroll
+          for (int j = 0; j < E; j++) {
+            dst[j] = d0;
+            d0 += keep[j] ? 1 : 0;
+          }
+          auto compact = [&](auto& F) {
+#pragma unroll
+            for (int j = 0; j < E; j++)
+              if (keep[j]) lds[dst[j]] = (uint32_t)F[j];
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+            for (int j = 0; j < E; j++) F[j] = (std::remove_reference_t<decltype(F[0])>)lds[base + j];
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          };
+          compact(R.len);
+          compact(R.seq);
+          compact(R.rseq);
+          compact(R.rmask);
+          compact(R.meta);
+          compact(R.toff);
+#pragma unroll
+          for (int kk = 0; kk < K; kk++) compact(R.pr[kk]);
+          n = n_new;
+          if (E > emin && n + 8 <= 16 * E) {
+            k++;
+            reason = 1;
+            break;
+          }
+        }
+      }
+    }
+  }
+
+  // write back (also on error / escalation)
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    const int i = base + j;
+    if (i < n) {
+      a.soa.len[dbase + i] = R.len[j];
+      a.soa.seq[dbase + i] = R.seq[j];
+      a.soa.rseq[dbase + i] = R.rseq[j];
+      a.soa.rmask[dbase + i] = R.rmask[j];
+      a.soa.meta[dbase + i] = R.meta[j];
+      a.soa.toff[dbase + i] = R.toff[j];
+#pragma unroll
+      for (int kk = 0; kk < K; kk++) a.soa.props[kk * a.soa.plane_stride + dbase + i] = R.pr[kk][j];
+    }
+  }
+  h.nseg = n;
+  return reason;
+}
+
+template <int EMIN, int EMAX, int K, bool LAST>
+__global__ __launch_bounds__(256) void replay_kernel(ReplayArgs a, int pass) {
+  __shared__ uint32_t lds_all[kDocsPerBlock][kWave * EMAX];
+  const int w = threadIdx.x / kWave;
+  const int doc = blockIdx.x * kDocsPerBlock + w;
+  if (doc >= (int)a.n_docs) return;
+  uint32_t* lds = lds_all[w];
+  DocHdr h = a.hdr[doc];
+  if (h.status != 0) return;
+  if (pass > 0 && !(h.flags & kHdrNeedsEsc)) return;
+  h.flags &= ~kHdrNeedsEsc;
+  const uint64_t kb = a.op_off[doc];
+  uint64_t k = kb + h.resume;
+  const uint64_t k1 = a.op_off[doc + 1];
+  unsigned long long st[kNumStats] = {0, 0, 0, 0, 0, 0};
+  while (k < k1) {
+    const int n = h.nseg;
+    int E = 0;
+    if (EMIN <= 1 && EMAX >= 1 && n + 2 <= kWave * 1) E = 1;
+    else if (EMIN <= 2 && EMAX >= 2 && n + 2 <= kWave * 2) E = 2;
+    else if (EMIN <= 4 && EMAX >= 4 && n + 2 <= kWave * 4) E = 4;
+    else if (EMIN <= 8 && EMAX >= 8 && n + 2 <= kWave * 8) E = 8;
+    else if (EMIN <= 16 && EMAX >= 16 && n + 2 <= kWave * 16) E = 16;
+    if (E == 0 || n + 2 > (int)a.cap) {
+      if (LAST || n + 2 > (int)a.cap) h.status = MTE_E_CAPACITY;
+      else h.flags |= kHdrNeedsEsc;
+      break;
+    }
+    int rc = 0;
+    if constexpr (EMIN <= 1 && EMAX >= 1) if (E == 1) rc = run_ops<1, K>(a, doc, h, k, k1, EMIN, lds, st);
+    if constexpr (EMIN <= 2 && EMAX >= 2) if (E == 2) rc = run_ops<2, K>(a, doc, h, k, k1, EMIN, lds, st);
+    if constexpr (EMIN <= 4 && EMAX >= 4) if (E == 4) rc = run_ops<4, K>(a, doc, h, k, k1, EMIN, lds, st);
+    if constexpr (EMIN <= 8 && EMAX >= 8) if (E == 8) rc = run_ops<8, K>(a, doc, h, k, k1, EMIN, lds, st);
+    if constexpr (EMIN <= 16 && EMAX >= 16) if (E == 16) rc = run_ops<16, K>(a, doc, h, k, k1, EMIN, lds, st);
+    if (rc < 0) {
+      h.status = rc;
+      break;
+    }
+  }
+  h.resume = (uint32_t)(k - kb);
+  if (lane_id() == 0) {
+    a.hdr[doc] = h;
+    unsigned long long* sd = a.stats + (size_t)doc * kNumStats;
+#pragma unroll
+    for (int t = 0; t < kNumStats; t++) {
+      if (t == kStMaxSegs) sd[t] = sd[t] > st[t] ? sd[t] : st[t];
+      else sd[t] += st[t];
+    }
+  }
+}
+
+// reset resume/escalation flags and stats at the start of a batch
+__global__ void begin_batch_kernel(DocHdr* hdr, unsigned long long* stats, uint32_t n_docs) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n_docs) return;
+  hdr[d].resume = 0;
+  hdr[d].flags &= ~kHdrNeedsEsc;
+#pragma unroll
+  for (int t = 0; t < kNumStats; t++) stats[(size_t)d * kNumStats + t] = 0;
+}
+
+// (re)initialise docs from their load description: one seq-0 LocalClientId
+// text segment (client.replay.spec.ts:22-23)
+__global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_doc_init* inits,
+                             const uint32_t* init_props, uint32_t n_keys, uint32_t n_docs) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n_docs) return;
+  const mte_doc_init in = inits[d];
+  DocHdr h;
+  h.nseg = in.text_len > 0 ? 1 : 0;
+  h.min_seq = in.min_seq;
+  h.cur_seq = in.cur_seq;
+  h.status = 0;
+  h.flags = in.flags & MTE_DOC_NEW_LENGTH_CALC;
+  h.resume = 0;
+  h.pad0 = h.pad1 = 0;
+  hdr[d] = h;
+  const uint64_t i = (uint64_t)d * cap;
+  soa.len[i] = (int32_t)in.text_len;
+  soa.seq[i] = 0;
+  soa.rseq[i] = kNone;
+  soa.rmask[i] = 0;
+  soa.meta[i] = 0;  // clientId -1, text
+  soa.toff[i] = in.text_off;
+  for (uint32_t k = 0; k < n_keys; k++) soa.props[k * soa.plane_stride + i] = init_props[(size_t)d * MTE_MAX_KEYS + k];
+}
+
+// ---------------------------------------------------------------------------
+// digest (DESIGN.md "Digest"): H = sum_p x_p * B^(n-1-p) mod 2^61-1
+// ---------------------------------------------------------------------------
+constexpr uint64_t kM61 = (1ull << 61) - 1;
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t fold61(uint64_t x) {
+  uint64_t r = (x & kM61) + (x >> 61);
+  return r >= kM61 ? r - kM61 : r;
+}
+__device__ __forceinline__ uint64_t mulmod61(uint64_t a, uint64_t b) {
+  const uint64_t lo = a * b;
+  const uint64_t hi = __umul64hi(a, b);
+  uint64_t r = (lo & kM61) + ((hi << 3) | (lo >> 61));
+  r = (r & kM61) + (r >> 61);
+  return r >= kM61 ? r - kM61 : r;
+}
+__device__ __forceinline__ uint64_t addmod61(uint64_t a, uint64_t b) {
+  uint64_t r = a + b;
+  return r >= kM61 ? r - kM61 : r;
+}
+__device__ __forceinline__ uint64_t powmod61(const uint64_t* tab, uint32_t e) {
+  uint64_t r = 1;
+  for (int i = 0; e; i++, e >>= 1)
+    if (e & 1u) r = mulmod61(r, tab[i]);
+  return r;
+}
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, kWave);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, kWave);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+struct DigestArgs {
+  const DocHdr* hdr;
+  SegSoA soa;
+  uint32_t cap;
+  uint32_t n_keys;
+  uint32_t n_docs;
+  const uint16_t* arena;
+  const uint64_t* pow1;  // B1^(2^i), i < 32
+  const uint64_t* pow2;
+  uint64_t* out;
+};
+
+__global__ __launch_bounds__(256) void digest_kernel(DigestArgs a) {
+  const int w = threadIdx.x / kWave;
+  const int l = lane_id();
+  const int doc = blockIdx.x * kDocsPerBlock + w;
+  if (doc >= (int)a.n_docs) return;
+  const int n = a.hdr[doc].nseg;
+  const uint64_t db = (uint64_t)doc * a.cap;
+  int32_t tot = 0;
+  for (int c0 = 0; c0 < n; c0 += kWave) {
+    const int i = c0 + l;
+    const int32_t L = (i < n && a.soa.rseq[db + i] == kNone) ? a.soa.len[db + i] : 0;
+    tot += rdlane(wave_incl_scan(L), kWave - 1);
+  }
+  uint64_t h1 = 0, h2 = 0, xs = 0;
+  int32_t carry = 0;
+  for (int c0 = 0; c0 < n; c0 += kWave) {
+    const int i = c0 + l;
+    const bool vis = i < n && a.soa.rseq[db + i] == kNone;
+    const int32_t L = vis ? a.soa.len[db + i] : 0;
+    const int32_t incl = wave_incl_scan(L);
+    const int32_t P = carry + incl - L;
+    uint64_t c1 = 0, c2 = 0, xl = 0;
+    if (L > 0) {
+      uint64_t ph = 0;
+      for (uint32_t k = 0; k < a.n_keys; k++) {
+        const uint32_t v = a.soa.props[k * a.soa.plane_stride + db + i];
+        if (v) ph += mix64(((uint64_t)(k + 1) << 32) | v);
+      }
+      const uint32_t kind = a.soa.meta[db + i] >> 8;
+      const uint32_t toff = a.soa.toff[db + i];
+      uint64_t s1 = 0, s2 = 0;
+      for (int32_t u = 0; u < L; u++) {
+        const uint64_t rec = kind == 0 ? (uint64_t)a.arena[toff + (uint32_t)u] : ((1ull << 32) | (uint64_t)(kind - 1));
+        const uint64_t x = fold61(mix64(rec * 0x9E3779B97F4A7C15ull + ph));
+        s1 = addmod61(mulmod61(s1, a.pow1[0]), x);
+        s2 = addmod61(mulmod61(s2, a.pow2[0]), x);
+        xl += x;
+      }
+      const uint32_t e = (uint32_t)(tot - P - L);
+      c1 = mulmod61(s1, powmod61(a.pow1, e));
+      c2 = mulmod61(s2, powmod61(a.pow2, e));
+    }
+#pragma unroll
+    for (int m = 1; m < kWave; m <<= 1) {
+      c1 = addmod61(c1, shfl_xor64(c1, m));
+      c2 = addmod61(c2, shfl_xor64(c2, m));
+      xl += shfl_xor64(xl, m);
+    }
+    h1 = addmod61(h1, c1);
+    h2 = addmod61(h2, c2);
+    xs += xl;
+    carry += rdlane(incl, kWave - 1);
+  }
+  if (l == 0) {
+    a.out[4 * (size_t)doc + 0] = (uint64_t)tot;
+    a.out[4 * (size_t)doc + 1] = h1;
+    a.out[4 * (size_t)doc + 2] = h2;
+    a.out[4 * (size_t)doc + 3] = xs;
+  }
+}
+
+// host helpers for the digest constants (must match oracle/oracle.c)
+uint64_t h_mulmod61(uint64_t a, uint64_t b) {
+  unsigned __int128 p = (unsigned __int128)a * b;
+  uint64_t r = (uint64_t)(p & kM61) + (uint64_t)(p >> 61);
+  return r >= kM61 ? r - kM61 : r;
+}
+const uint64_t kDigB1 = 0x1d8e4e27c47d124full % kM61;
+const uint64_t kDigB2 = 0x0a0761d6478bd642ull % kM61;
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+
+struct mte_ctx {
+  int device = 0;
+  uint32_t n_keys = 0, kt = 0;  // kt: template planes (0/4/8)
+  uint32_t cap = 1024;
+  uint32_t n_docs = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool ran = false, submitted = false;
+  std::string err;
+
+  DocHdr* hdr = nullptr;
+  SegSoA soa{};
+  unsigned long long* stats = nullptr;
+  mte_doc_init* d_inits = nullptr;
+  uint32_t* d_init_props = nullptr;
+  uint64_t* d_pow = nullptr;  // pow1[32], pow2[32]
+  uint64_t* d_digest = nullptr;
+
+  // text arena
+  uint16_t* arena = nullptr;
+  uint64_t arena_n = 0, arena_cap = 0;
+  std::vector<uint16_t> h_arena;
+
+  // batch
+  mte_op* d_ops = nullptr;
+  uint64_t ops_cap = 0, n_ops = 0;
+  uint64_t* d_off = nullptr;
+  uint64_t off_cap = 0;
+  mte_propset* d_ps = nullptr;
+  uint64_t ps_cap = 0;
+  mte_prop* d_pe = nullptr;
+  uint64_t pe_cap = 0;
+  uint32_t batch_text_base = 0;
+};
+
+namespace {
+
+int set_err(mte_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                  \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return set_err(ctx, MTE_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                     __LINE__);                                                            \
+  } while (0)
+
+template <typename T>
+int grow(mte_ctx* c, T** p, uint64_t* cap, uint64_t need, bool keep = false, uint64_t keep_n = 0) {
+  if (need <= *cap && *p) return MTE_OK;
+  uint64_t nc = *cap ? *cap : 256;
+  while (nc < need) nc *= 2;
+  T* q = nullptr;
+  HIPCHK(c, hipMalloc((void**)&q, nc * sizeof(T)));
+  if (keep && *p && keep_n) HIPCHK(c, hipMemcpyAsync(q, *p, keep_n * sizeof(T), hipMemcpyDeviceToDevice, c->stream));
+  if (*p) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipFree(*p));
+  }
+  *p = q;
+  *cap = nc;
+  return MTE_OK;
+}
+
+void free_docs(mte_ctx* c) {
+  void* ps[] = {c->hdr, c->soa.len, c->soa.seq, c->soa.rseq, c->soa.rmask, c->soa.meta, c->soa.toff,
+                c->soa.props, c->stats, c->d_inits, c->d_init_props, c->d_digest};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+  c->hdr = nullptr;
+  c->soa = SegSoA{};
+  c->stats = nullptr;
+  c->d_inits = nullptr;
+  c->d_init_props = nullptr;
+  c->d_digest = nullptr;
+  c->n_docs = 0;
+}
+
+int launch_reset(mte_ctx* c) {
+  if (!c->n_docs) return MTE_OK;
+  const uint32_t blocks = (c->n_docs + 255) / 256;
+  hipLaunchKernelGGL(reset_kernel, dim3(blocks), dim3(256), 0, c->stream, c->hdr, c->soa, c->cap,
+                     c->d_inits, c->d_init_props, c->n_keys, c->n_docs);
+  HIPCHK(c, hipGetLastError());
+  c->ran = false;
+  return MTE_OK;
+}
+
+template <int K>
+int launch_replay(mte_ctx* c, const ReplayArgs& a) {
+  const uint32_t blocks = (c->n_docs + kDocsPerBlock - 1) / kDocsPerBlock;
+  hipLaunchKernelGGL((replay_kernel<1, 4, K, false>), dim3(blocks), dim3(256), 0, c->stream, a, 0);
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL((replay_kernel<8, 16, K, true>), dim3(blocks), dim3(256), 0, c->stream, a, 1);
+  HIPCHK(c, hipGetLastError());
+  return MTE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mte_abi_version(void) { return MTE_ABI_VERSION; }
+
+const char* mte_strerror(int code) {
+  switch (code) {
+    case MTE_OK: return "ok";
+    case MTE_E_INVALID_ARG: return "invalid argument";
+    case MTE_E_NO_DEVICE: return "no HIP device";
+    case MTE_E_HIP: return "HIP runtime error";
+    case MTE_E_CAPACITY: return "segment capacity exceeded";
+    case MTE_E_SEQ_ORDER: return "0x030: remote op sequence number <= currentSeq";
+    case MTE_E_MSN_ORDER: return "0x031: remote op minSequenceNumber < minSeq";
+    case MTE_E_MSN_GT_SEQ: return "0x039: sequence number < minSequenceNumber";
+    case MTE_E_INSERT_FAILED: return "MergeTree insert failed";
+    case MTE_E_UNSUPPORTED: return "unsupported op";
+    case MTE_E_STATE: return "call out of order";
+    case MTE_E_OOM: return "out of memory";
+    case MTE_E_CLIENT_RANGE: return "client id out of range";
+    default: return "unknown error";
+  }
+}
+
+const char* mte_last_error(const mte_ctx* c) { return c ? c->err.c_str() : "null ctx"; }
+
+int mte_create(const mte_config* cfg, mte_ctx** out) {
+  if (!cfg || !out || cfg->n_keys > MTE_MAX_KEYS) return MTE_E_INVALID_ARG;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MTE_E_NO_DEVICE;
+  if (cfg->device < 0 || cfg->device >= ndev) return MTE_E_NO_DEVICE;
+  mte_ctx* c = new (std::nothrow) mte_ctx();
+  if (!c) return MTE_E_OOM;
+  c->device = cfg->device;
+  c->n_keys = cfg->n_keys;
+  c->kt = cfg->n_keys == 0 ? 0 : (cfg->n_keys <= 4 ? 4 : 8);
+  c->cap = cfg->seg_capacity ? cfg->seg_capacity : 1024;
+  if (c->cap < 64) c->cap = 64;
+  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    delete c;
+    return MTE_E_NO_DEVICE;
+  }
+  uint64_t pw[64];
+  pw[0] = kDigB1;
+  pw[32] = kDigB2;
+  for (int i = 1; i < 32; i++) {
+    pw[i] = h_mulmod61(pw[i - 1], pw[i - 1]);
+    pw[32 + i] = h_mulmod61(pw[32 + i - 1], pw[32 + i - 1]);
+  }
+  if (hipMalloc((void**)&c->d_pow, sizeof(pw)) != hipSuccess ||
+      hipMemcpy(c->d_pow, pw, sizeof(pw), hipMemcpyHostToDevice) != hipSuccess) {
+    delete c;
+    return MTE_E_OOM;
+  }
+  *out = c;
+  return MTE_OK;
+}
+
+int mte_destroy(mte_ctx* c) {
+  if (!c) return MTE_E_INVALID_ARG;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  free_docs(c);
+  void* ps[] = {c->arena, c->d_ops, c->d_off, c->d_ps, c->d_pe, c->d_pow};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return MTE_OK;
+}
+
+int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const uint16_t* text,
+                  uint64_t text_units, const mte_propset* propsets, uint32_t n_propsets,
+                  const mte_prop* props, uint32_t n_props) {
+  if (!c || (n_docs && !docs) || (text_units && !text)) return MTE_E_INVALID_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::vector<uint32_t> iprops((size_t)n_docs * MTE_MAX_KEYS, 0u);
+  for (uint32_t d = 0; d < n_docs; d++) {
+    const mte_doc_init& in = docs[d];
+    if ((uint64_t)in.text_off + in.text_len > text_units || in.text_len > 0x7fffffffu)
+      return set_err(c, MTE_E_INVALID_ARG, "doc %u: initial text out of range", d);
+    if (in.propset != MTE_NO_PROPS) {
+      if (in.propset >= n_propsets || !propsets) return set_err(c, MTE_E_INVALID_ARG, "doc %u: bad propset", d);
+      const mte_propset ps = propsets[in.propset];
+      if ((uint64_t)ps.first + ps.count > n_props) return set_err(c, MTE_E_INVALID_ARG, "doc %u: bad propset", d);
+      for (uint32_t t = 0; t < ps.count; t++) {
+        const mte_prop p = props[ps.first + t];
+        if (p.key < c->n_keys) iprops[(size_t)d * MTE_MAX_KEYS + p.key] = p.value;
+      }
+    }
+  }
+  free_docs(c);
+  c->n_docs = n_docs;
+  c->submitted = false;
+  c->n_ops = 0;
+  const uint64_t nslots = (uint64_t)(n_docs ? n_docs : 1) * c->cap;
+  c->soa.plane_stride = nslots;
+  HIPCHK(c, hipMalloc((void**)&c->hdr, sizeof(DocHdr) * (n_docs ? n_docs : 1)));
+  HIPCHK(c, hipMalloc((void**)&c->soa.len, nslots * 4));
+  HIPCHK(c, hipMalloc((void**)&c->soa.seq, nslots * 4));
+  HIPCHK(c, hipMalloc((void**)&c->soa.rseq, nslots * 4));
+  HIPCHK(c, hipMalloc((void**)&c->soa.rmask, nslots * 4));
+  HIPCHK(c, hipMalloc((void**)&c->soa.meta, nslots * 4));
+  HIPCHK(c, hipMalloc((void**)&c->soa.toff, nslots * 4));
+  // kt (>= n_keys) planes, so the register-resident kernels never index past the array
+  HIPCHK(c, hipMalloc((void**)&c->soa.props, nslots * 4 * (c->kt ? c->kt : 1)));
+  HIPCHK(c, hipMemsetAsync(c->soa.props, 0, nslots * 4 * (c->kt ? c->kt : 1), c->stream));
+  HIPCHK(c, hipMalloc((void**)&c->stats, sizeof(unsigned long long) * kNumStats * (n_docs ? n_docs : 1)));
+  HIPCHK(c, hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * kNumStats * (n_docs ? n_docs : 1), c->stream));
+  HIPCHK(c, hipMalloc((void**)&c->d_inits, sizeof(mte_doc_init) * (n_docs ? n_docs : 1)));
+  HIPCHK(c, hipMalloc((void**)&c->d_init_props, sizeof(uint32_t) * iprops.size() + 4));
+  HIPCHK(c, hipMalloc((void**)&c->d_digest, sizeof(uint64_t) * 4 * (n_docs ? n_docs : 1)));
+  if (n_docs) {
+    HIPCHK(c, hipMemcpyAsync(c->d_inits, docs, sizeof(mte_doc_init) * n_docs, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_init_props, iprops.data(), sizeof(uint32_t) * iprops.size(),
+                             hipMemcpyHostToDevice, c->stream));
+  }
+  // text arena restarts with the load text
+  c->arena_n = 0;
+  c->h_arena.assign(text, text + text_units);
+  int rc = grow(c, &c->arena, &c->arena_cap, text_units + 1);
+  if (rc) return rc;
+  if (text_units)
+    HIPCHK(c, hipMemcpyAsync(c->arena, text, text_units * 2, hipMemcpyHostToDevice, c->stream));
+  c->arena_n = text_units;
+  rc = launch_reset(c);
+  if (rc) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MTE_OK;
+}
+
+int mte_submit(mte_ctx* c, const mte_batch* b) {
+  if (!c || !b || b->n_docs != c->n_docs || !b->op_offsets) return MTE_E_INVALID_ARG;
+  if (b->op_offsets[0] != 0 || b->op_offsets[b->n_docs] != b->n_ops) return set_err(c, MTE_E_INVALID_ARG, "op_offsets");
+  for (uint32_t d = 0; d < b->n_docs; d++)
+    if (b->op_offsets[d + 1] < b->op_offsets[d]) return set_err(c, MTE_E_INVALID_ARG, "op_offsets not sorted");
+  for (uint32_t i = 0; i < b->n_propsets; i++)
+    if ((uint64_t)b->propsets[i].first + b->propsets[i].count > b->n_props)
+      return set_err(c, MTE_E_INVALID_ARG, "propset %u out of range", i);
+  // host-side validation of every record, so no kernel can index out of bounds
+  for (uint64_t k = 0; k < b->n_ops; k++) {
+    const mte_op& o = b->ops[k];
+    if (o.type > MTE_OP_NOOP) return set_err(c, MTE_E_INVALID_ARG, "op %llu: type %u", (unsigned long long)k, o.type);
+    if (o.type == MTE_OP_INSERT) {
+      if (!(o.flags & MTE_F_MARKER) && o.pos2 > 0 && (uint64_t)o.a + (uint64_t)o.pos2 > b->text_units)
+        return set_err(c, MTE_E_INVALID_ARG, "op %llu: text out of range", (unsigned long long)k);
+      if ((o.flags & MTE_F_MARKER) && (o.pos2 < 0 || o.pos2 >= (1 << 23)))
+        return set_err(c, MTE_E_INVALID_ARG, "op %llu: refType out of range", (unsigned long long)k);
+      if (!(o.flags & MTE_F_MARKER) && o.pos2 < 0)
+        return set_err(c, MTE_E_INVALID_ARG, "op %llu: negative text length", (unsigned long long)k);
+      if (o.b != MTE_NO_PROPS && o.b >= b->n_propsets)
+        return set_err(c, MTE_E_INVALID_ARG, "op %llu: propset out of range", (unsigned long long)k);
+    } else if (o.type == MTE_OP_ANNOTATE && o.a >= b->n_propsets) {
+      return set_err(c, MTE_E_INVALID_ARG, "op %llu: propset out of range", (unsigned long long)k);
+    }
+  }
+  if (c->arena_n + b->text_units >= (1ull << 32)) return set_err(c, MTE_E_OOM, "text arena exceeds 2^32 units");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  // append batch text to the arena
+  if ((rc = grow(c, &c->arena, &c->arena_cap, c->arena_n + b->text_units + 1, true, c->arena_n))) return rc;
+  if (b->text_units)
+    HIPCHK(c, hipMemcpyAsync(c->arena + c->arena_n, b->text, b->text_units * 2, hipMemcpyHostToDevice, c->stream));
+  c->h_arena.insert(c->h_arena.end(), b->text, b->text + b->text_units);
+  c->batch_text_base = (uint32_t)c->arena_n;
+  c->arena_n += b->text_units;
+  if ((rc = grow(c, &c->d_ops, &c->ops_cap, b->n_ops + 1))) return rc;
+  if ((rc = grow(c, &c->d_off, &c->off_cap, (uint64_t)b->n_docs + 1))) return rc;
+  if ((rc = grow(c, &c->d_ps, &c->ps_cap, (uint64_t)b->n_propsets + 1))) return rc;
+  if ((rc = grow(c, &c->d_pe, &c->pe_cap, (uint64_t)b->n_props + 1))) return rc;
+  if (b->n_ops) HIPCHK(c, hipMemcpyAsync(c->d_ops, b->ops, b->n_ops * sizeof(mte_op), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_off, b->op_offsets, ((uint64_t)b->n_docs + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  if (b->n_propsets)
+    HIPCHK(c, hipMemcpyAsync(c->d_ps, b->propsets, b->n_propsets * sizeof(mte_propset), hipMemcpyHostToDevice, c->stream));
+  if (b->n_props)
+    HIPCHK(c, hipMemcpyAsync(c->d_pe, b->props, b->n_props * sizeof(mte_prop), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // host buffers may be freed after return
+  c->n_ops = b->n_ops;
+  c->submitted = true;
+  return MTE_OK;
+}
+
+int mte_run(mte_ctx* c) {
+  if (!c) return MTE_E_INVALID_ARG;
+  if (!c->submitted) return set_err(c, MTE_E_STATE, "mte_run before mte_submit");
+  if (!c->n_docs) return MTE_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipLaunchKernelGGL(begin_batch_kernel, dim3((c->n_docs + 255) / 256), dim3(256), 0, c->stream, c->hdr, c->stats,
+                     c->n_docs);
+  HIPCHK(c, hipGetLastError());
+  ReplayArgs a;
+  a.hdr = c->hdr;
+  a.soa = c->soa;
+  a.cap = c->cap;
+  a.n_docs = c->n_docs;
+  a.ops = c->d_ops;
+  a.op_off = c->d_off;
+  a.ps = c->d_ps;
+  a.pe = c->d_pe;
+  a.n_keys = c->n_keys;
+  a.text_base = c->batch_text_base;
+  a.stats = c->stats;
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  int rc = c->kt == 0 ? launch_replay<0>(c, a) : (c->kt == 4 ? launch_replay<4>(c, a) : launch_replay<8>(c, a));
+  if (rc) return rc;
+  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  c->ran = true;
+  return MTE_OK;
+}
+
+int mte_sync(mte_ctx* c) {
+  if (!c) return MTE_E_INVALID_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MTE_OK;
+}
+
+int mte_reset(mte_ctx* c) {
+  if (!c) return MTE_E_INVALID_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  return launch_reset(c);
+}
+
+int mte_digest_device(mte_ctx* c, void* out, uint32_t n_docs) {
+  if (!c || !out || n_docs != c->n_docs) return MTE_E_INVALID_ARG;
+  if (!n_docs) return MTE_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  DigestArgs a;
+  a.hdr = c->hdr;
+  a.soa = c->soa;
+  a.cap = c->cap;
+  a.n_keys = c->n_keys;
+  a.n_docs = c->n_docs;
+  a.arena = c->arena;
+  a.pow1 = c->d_pow;
+  a.pow2 = c->d_pow + 32;
+  a.out = (uint64_t*)out;
+  hipLaunchKernelGGL(digest_kernel, dim3((n_docs + kDocsPerBlock - 1) / kDocsPerBlock), dim3(256), 0, c->stream, a);
+  HIPCHK(c, hipGetLastError());
+  return MTE_OK;
+}
+
+int mte_digest(mte_ctx* c, uint64_t* out, uint32_t n_docs) {
+  if (!c || !out || n_docs != c->n_docs) return MTE_E_INVALID_ARG;
+  if (!n_docs) return MTE_OK;
+  int rc = mte_digest_device(c, c->d_digest, n_docs);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(out, c->d_digest, sizeof(uint64_t) * 4 * n_docs, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MTE_OK;
+}
+
+int mte_doc_status(mte_ctx* c, int32_t* out, uint32_t n_docs) {
+  if (!c || !out || n_docs != c->n_docs) return MTE_E_INVALID_ARG;
+  if (!n_docs) return MTE_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<DocHdr> h(n_docs);
+  HIPCHK(c, hipMemcpyAsync(h.data(), c->hdr, sizeof(DocHdr) * n_docs, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (uint32_t i = 0; i < n_docs; i++) out[i] = h[i].status;
+  return MTE_OK;
+}
+
+int mte_read_doc(mte_ctx* c, uint32_t doc, mte_doc_view* v) {
+  if (!c || !v || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  DocHdr h;
+  HIPCHK(c, hipMemcpyAsync(&h, c->hdr + doc, sizeof(DocHdr), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint32_t n = (uint32_t)std::max(h.nseg, 0);
+  const uint64_t db = (uint64_t)doc * c->cap;
+  std::vector<int32_t> len(n + 1), rseq(n + 1);
+  std::vector<uint32_t> meta(n + 1), toff(n + 1), props((size_t)(n + 1) * (c->n_keys ? c->n_keys : 1));
+  if (n) {
+    HIPCHK(c, hipMemcpyAsync(len.data(), c->soa.len + db, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(rseq.data(), c->soa.rseq + db, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(meta.data(), c->soa.meta + db, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(toff.data(), c->soa.toff + db, n * 4, hipMemcpyDeviceToHost, c->stream));
+    for (uint32_t k = 0; k < c->n_keys; k++)
+      HIPCHK(c, hipMemcpyAsync(props.data() + (size_t)k * n, c->soa.props + k * c->soa.plane_stride + db, n * 4,
+                               hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  v->status = h.status;
+  v->cur_seq = h.cur_seq;
+  v->min_seq = h.min_seq;
+  uint32_t length = 0, nt = 0, ns = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (rseq[i] != kNone) continue;  // gatherText: only segments not removed
+    const uint32_t kind = meta[i] >> 8;
+    if (ns < v->seg_cap) {
+      if (v->seg_len) v->seg_len[ns] = (uint32_t)len[i];
+      if (v->seg_kind) v->seg_kind[ns] = kind;
+      if (v->seg_props)
+        for (uint32_t k = 0; k < c->n_keys; k++) v->seg_props[(size_t)ns * c->n_keys + k] = props[(size_t)k * n + i];
+    }
+    ns++;
+    length += (uint32_t)len[i];
+    if (kind == 0) {
+      for (int32_t u = 0; u < len[i]; u++) {
+        if (nt < v->text_cap && v->text) v->text[nt] = c->h_arena[toff[i] + (uint32_t)u];
+        nt++;
+      }
+    }
+  }
+  v->length = length;
+  v->n_text = nt;
+  v->n_segs = ns;
+  return MTE_OK;
+}
+
+int mte_stats_get(mte_ctx* c, mte_stats* o) {
+  if (!c || !o) return MTE_E_INVALID_ARG;
+  std::memset(o, 0, sizeof(*o));
+  if (!c->n_docs) return MTE_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<unsigned long long> s((size_t)c->n_docs * kNumStats);
+  HIPCHK(c, hipMemcpyAsync(s.data(), c->stats, s.size() * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (uint32_t d = 0; d < c->n_docs; d++) {
+    const unsigned long long* x = &s[(size_t)d * kNumStats];
+    o->ops_applied += x[kStOps];
+    o->segs_scanned += x[kStScanned];
+    o->segs_written += x[kStWritten];
+    o->prop_writes += x[kStPwrites];
+    o->units_inserted += x[kStUnits];
+    if (x[kStMaxSegs] > o->max_segs) o->max_segs = x[kStMaxSegs];
+  }
+  if (c->ran) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) o->kernel_ms = ms;
+  }
+  o->algo_bytes = 32.0 * (double)o->ops_applied + 20.0 * (double)o->segs_scanned + 20.0 * (double)o->segs_written +
+                  4.0 * (double)o->prop_writes + 2.0 * (double)o->units_inserted;
+  return MTE_OK;
+}
+
+}  // extern "C"

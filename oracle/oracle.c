@@ -47,7 +47,7 @@ typedef struct {
   /* loaded state, for reload */
   mte_doc_init init;
   uint32_t init_props[MTE_MAX_KEYS];
-} odoc;
+} __attribute__((aligned(128))) odoc; /* one cache-line pair per doc: no false sharing between threads */
 
 struct orc_ctx {
   uint32_t n_keys;
@@ -381,7 +381,8 @@ int orc_load_docs(orc_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
   uint64_t base = 0;
   int rc = arena_append(c, text, text_units, &base);
   if (rc) return rc;
-  c->docs = (odoc*)calloc(n_docs ? n_docs : 1, sizeof(odoc));
+  c->docs = (odoc*)aligned_alloc(128, (size_t)(n_docs ? n_docs : 1) * sizeof(odoc));
+  if (c->docs) memset(c->docs, 0, (size_t)(n_docs ? n_docs : 1) * sizeof(odoc));
   if (!c->docs) return MTE_E_OOM;
   c->n_docs = n_docs;
   for (uint32_t i = 0; i < n_docs; i++) {
@@ -450,6 +451,11 @@ int orc_apply_batch(orc_ctx* c, const mte_batch* b, int n_threads) {
   uint64_t base = 0;
   int rc = arena_append(c, b->text, b->text_units, &base);
   if (rc) return rc;
+  /* stats describe the last batch, like mte_stats_get */
+  for (uint32_t i = 0; i < c->n_docs; i++) {
+    odoc* d = &c->docs[i];
+    d->ops = d->scanned = d->written = d->pwrites = d->units = d->max_segs = 0;
+  }
   if (n_threads < 1) n_threads = 1;
   if ((uint32_t)n_threads > c->n_docs) n_threads = c->n_docs ? (int)c->n_docs : 1;
   worker_arg* args = (worker_arg*)calloc((size_t)n_threads, sizeof(worker_arg));

@@ -1,0 +1,136 @@
+"""Parity of the HIP engine (through the C-ABI) with the CPU restatement and the
+reference's golden fixtures.  Bit-exact: texts, visible segments, property
+planes, digests, per-doc status and the op statistics must all be equal."""
+import numpy as np
+import pytest
+
+from fixtures_util import replay_fixtures
+from scenarios import SCENARIOS, expected_of, run_scenario
+
+from fluidframework_amd import gen
+from fluidframework_amd.abi import MTE_E_CAPACITY
+from fluidframework_amd.engine import DeviceEngine
+from oracle import OracleEngine
+
+pytestmark = pytest.mark.gpu
+
+STAT_KEYS = ["ops_applied", "segs_scanned", "segs_written", "prop_writes", "units_inserted", "max_segs"]
+
+
+def replay_both(stream, threads=8):
+    n_keys = stream["n_keys"]
+    o = OracleEngine(n_keys, threads=threads)
+    o.load_docs(stream["inits"], stream["init_text"])
+    o.apply_batch(stream["batch"])
+    d = DeviceEngine(n_keys)
+    d.load_docs(stream["inits"], stream["init_text"])
+    d.apply_batch(stream["batch"])
+    return o, d
+
+
+def assert_same(o, d, sample_docs=16):
+    np.testing.assert_array_equal(d.statuses(), o.statuses())
+    np.testing.assert_array_equal(d.digest(), o.digest())
+    so, sd = o.stats(), d.stats()
+    for k in STAT_KEYS:
+        assert sd[k] == so[k], k
+    n = o.n_docs
+    for doc in sorted(set(np.linspace(0, n - 1, min(n, sample_docs)).astype(int).tolist())):
+        assert d.read_doc(doc) == o.read_doc(doc)
+
+
+def test_gpu_replays_reference_fixtures():
+    passed, failures, eng = replay_fixtures(lambda k: DeviceEngine(k))
+    assert failures == []
+    assert passed == 30 * 64 * 2
+    _, _, oeng = replay_fixtures(lambda k: OracleEngine(k), check=False)
+    np.testing.assert_array_equal(eng.digest(), oeng.digest())
+
+
+@pytest.mark.parametrize("name", sorted(SCENARIOS))
+def test_gpu_scenarios(name):
+    st_o, text_o, rd_o, _ = run_scenario(OracleEngine(8), name)
+    st_d, text_d, rd_d, _ = run_scenario(DeviceEngine(8), name)
+    assert st_d == st_o
+    assert rd_d == rd_o
+    exp = expected_of(name)
+    if exp is not None and not exp.startswith("ERR:"):
+        assert text_d == exp
+
+
+@pytest.mark.parametrize("cfg,n_docs,ops", [(2, 300, 1000), (3, 64, 4000), (4, 2000, 500)])
+def test_gpu_matches_oracle_generated(cfg, n_docs, ops):
+    s = gen.generate(cfg, n_docs=n_docs, ops_per_doc=ops, doc_base=7)
+    o, d = replay_both(s)
+    assert (o.statuses() == 0).all()
+    assert_same(o, d)
+
+
+def test_gpu_length_modes_and_keys():
+    for mode in (1, 2):
+        for n_keys in (0, 4, 8):
+            s = gen.generate(3, n_docs=40, ops_per_doc=1500, length_mode=mode)
+            if n_keys != 4:
+                s["n_keys"] = n_keys
+            o, d = replay_both(s)
+            assert_same(o, d, sample_docs=4)
+
+
+def test_gpu_multi_batch_equals_single_batch():
+    s = gen.generate(3, n_docs=50, ops_per_doc=3000)
+    one = DeviceEngine(s["n_keys"])
+    one.load_docs(s["inits"], s["init_text"])
+    one.apply_batch(s["batch"])
+    many = DeviceEngine(s["n_keys"])
+    many.load_docs(s["inits"], s["init_text"])
+    b = s["batch"]
+    offs = b["op_offsets"].astype(np.int64)
+    for lo_frac, hi_frac in [(0, 0.3), (0.3, 0.31), (0.31, 1.0)]:
+        parts, new_offs = [], [0]
+        for doc in range(50):
+            n = offs[doc + 1] - offs[doc]
+            lo, hi = offs[doc] + int(n * lo_frac), offs[doc] + int(n * hi_frac)
+            parts.append(b["ops"][lo:hi])
+            new_offs.append(new_offs[-1] + hi - lo)
+        sub = dict(b)
+        sub["ops"] = np.concatenate(parts)
+        sub["op_offsets"] = np.array(new_offs, np.uint64)
+        # text offsets of each batch are relative to that batch's text: resubmit
+        # the whole text each time and the engine rebases them
+        many.apply_batch(sub)
+    np.testing.assert_array_equal(many.digest(), one.digest())
+
+
+def test_gpu_reset_rerun_is_deterministic():
+    s = gen.generate(2, n_docs=100, ops_per_doc=1000)
+    d = DeviceEngine(s["n_keys"])
+    d.load_docs(s["inits"], s["init_text"])
+    d.apply_batch(s["batch"])
+    first = d.digest().copy()
+    for _ in range(2):
+        d.reset()
+        d.run()
+        d.sync()
+        np.testing.assert_array_equal(d.digest(), first)
+
+
+def test_gpu_large_docs_escalate_register_tiers():
+    # insert-only streams grow to hundreds of segments per doc: exercises the
+    # E = 1 -> 2 -> 4 -> 8 -> 16 register tiers and the second pass
+    s = gen.generate(2, n_docs=24, ops_per_doc=420, mix=gen.MIX_INSERT, min_length=0)
+    o, d = replay_both(s)
+    assert o.stats()["max_segs"] > 512
+    assert_same(o, d, sample_docs=24)
+
+
+def test_gpu_capacity_error_is_reported():
+    s = gen.generate(2, n_docs=4, ops_per_doc=800, mix=gen.MIX_INSERT, min_length=0)
+    d = DeviceEngine(s["n_keys"])
+    d.load_docs(s["inits"], s["init_text"])
+    d.apply_batch(s["batch"])
+    o = OracleEngine(s["n_keys"])
+    o.load_docs(s["inits"], s["init_text"])
+    o.apply_batch(s["batch"])
+    assert o.stats()["max_segs"] > 1022
+    st = d.statuses()
+    assert (st == MTE_E_CAPACITY).all()
