@@ -13,404 +13,11 @@
 #include <vector>
 
 #include "mte_kernels.h"
+#include "mte_replay.h"
 
 using namespace mte;
 
 namespace {
-
-// ---------------------------------------------------------------------------
-// replay
-// ---------------------------------------------------------------------------
-
-struct OpView {  // wave-uniform copy of one record
-  int32_t seq, ref_seq, min_seq;
-  uint32_t type, client, flags;
-  int32_t pos1, pos2;
-  uint32_t a, b;
-};
-
-__device__ __forceinline__ OpView load_op(const mte_op* __restrict__ ops, uint64_t k) {
-  const mte_op o = ops[k];
-  OpView v;
-  v.seq = o.seq;
-  v.ref_seq = o.ref_seq;
-  v.min_seq = o.min_seq;
-  v.type = o.type;
-  v.client = o.client;
-  v.flags = o.flags;
-  v.pos1 = o.pos1;
-  v.pos2 = o.pos2;
-  v.a = o.a;
-  v.b = o.b;
-  return v;
-}
-
-template <int K>
-__device__ __forceinline__ uint32_t apply_propset_seg(Seg<K>& s, const ReplayArgs& a, uint32_t psi) {
-  const mte_propset ps = a.ps[psi];
-  uint32_t w = 0;
-  for (uint32_t t = 0; t < ps.count; t++) {
-    const mte_prop p = a.pe[ps.first + t];
-    if (p.key < a.n_keys) {
-#pragma unroll
-      for (int k = 0; k < K; k++)
-        if ((uint32_t)k == p.key) s.pr[k] = p.value;
-      w++;
-    }
-  }
-  return w;
-}
-
-// Returns 0 = batch range done, 1 = re-pick E, or a negative MTE_E_*.
-template <int E, int K>
-__device__ int run_ops(const ReplayArgs& a, int doc, DocHdr& h, uint64_t& k, uint64_t k1, int emin,
-                       uint32_t* lds, unsigned long long (&st)[kNumStats]) {
-  const int l = lane_id();
-  const int base = l * E;
-  const uint64_t dbase = (uint64_t)doc * a.cap;
-  const bool newcalc = (h.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
-  int n = h.nseg;
-
-  Regs<E, K> R;
-#pragma unroll
-  for (int j = 0; j < E; j++) {
-    const int i = base + j;
-    if (i < n) {
-      R.len[j] = a.soa.len[dbase + i];
-      R.seq[j] = a.soa.seq[dbase + i];
-      R.rseq[j] = a.soa.rseq[dbase + i];
-      R.rmask[j] = a.soa.rmask[dbase + i];
-      R.meta[j] = a.soa.meta[dbase + i];
-      R.toff[j] = a.soa.toff[dbase + i];
-#pragma unroll
-      for (int kk = 0; kk < K; kk++) R.pr[kk][j] = a.soa.props[kk * a.soa.plane_stride + dbase + i];
-    } else {
-      R.len[j] = 0;
-      R.seq[j] = 0;
-      R.rseq[j] = 0;
-      R.rmask[j] = 0;
-      R.meta[j] = 0;
-      R.toff[j] = 0;
-#pragma unroll
-      for (int kk = 0; kk < K; kk++) R.pr[kk][j] = 0;
-    }
-  }
-
-  int reason = 0;
-  const int lim = kWave * E < (int)a.cap ? kWave * E : (int)a.cap;
-  for (; k < k1; k++) {
-    if (n + 2 > lim) {
-      reason = 1;
-      break;
-    }
-    const OpView op = load_op(a.ops, k);
-    st[kStOps]++;
-    if ((unsigned long long)n > st[kStMaxSegs]) st[kStMaxSegs] = (unsigned long long)n;
-    const int c = (int)op.client;
-    if (c >= MTE_MAX_CLIENTS) {
-      reason = MTE_E_CLIENT_RANGE;
-      break;
-    }
-    const int32_t r = op.ref_seq, s = op.seq, m = h.min_seq;
-
-    if (op.type == MTE_OP_INSERT) {
-      // Client.applyInsertOp -> MergeTree.insertSegments (client.ts:470-505,
-      // mergeTree.ts:1394-1422)
-      st[kStScanned] += (unsigned long long)n;
-      int32_t L[E], P[E];
-      leaf_lengths<E, K>(R, n, r, c, m, newcalc, L);
-      const int32_t total = prefix<E>(L, P);
-      const int32_t pos = op.pos1;
-      int32_t off = 0;
-      const int xs = find_split<E>(L, P, pos, &off);  // ensureIntervalBoundary
-      const bool marker = (op.flags & MTE_F_MARKER) != 0;
-      const int32_t nlen = marker ? 1 : op.pos2;
-      int g = -1;
-      if (xs < 0 && nlen > 0) {
-        g = find_slot<E>(L, P, pos);
-        if (g < 0) {
-          if (pos > total) {
-            reason = MTE_E_INSERT_FAILED;  // mergeTree.ts:1666-1672
-            break;
-          }
-          g = n;
-        }
-      }
-      Seg<K> ns;
-      if (nlen > 0) {
-        ns.len = nlen;
-        ns.seq = s;
-        ns.rseq = kNone;
-        ns.rmask = 0;
-        ns.meta = (uint32_t)(c + 1) | ((marker ? 1u + (uint32_t)op.pos2 : 0u) << 8);
-        ns.toff = marker ? 0u : a.text_base + op.a;
-#pragma unroll
-        for (int kk = 0; kk < K; kk++) ns.pr[kk] = 0;
-        if (op.b != MTE_NO_PROPS) st[kStPwrites] += apply_propset_seg<K>(ns, a, op.b);
-        if (!marker) st[kStUnits] += (unsigned long long)nlen;
-      }
-      if (xs >= 0) {
-        Seg<K> tail = get_seg<E, K>(R, xs);
-        tail.len -= off;
-        tail.toff += (uint32_t)off;
-        if (nlen > 0) {
-          shift_all<E, K>(R, xs + 1, xs + 2);
-          put_seg<E, K>(R, xs + 1, ns);
-          put_seg<E, K>(R, xs + 2, tail);
-          n += 2;
-          st[kStWritten] += 3;
-        } else {
-          shift_all<E, K>(R, xs + 1, INT32_MAX);
-          put_seg<E, K>(R, xs + 1, tail);
-          n += 1;
-          st[kStWritten] += 2;
-        }
-        put<E>(R.len, xs, off);  // head keeps [0, off)
-      } else if (nlen > 0) {
-        shift_all<E, K>(R, g, INT32_MAX);
-        put_seg<E, K>(R, g, ns);
-        n += 1;
-        st[kStWritten] += 1;
-      }
-    } else if (op.type == MTE_OP_REMOVE || op.type == MTE_OP_ANNOTATE) {
-      // markRangeRemoved (mergeTree.ts:1908-2000) / annotateRange (1864-1906)
-      st[kStScanned] += (unsigned long long)n;
-      const int32_t start = op.pos1, end = op.pos2;
-      int32_t L[E], P[E];
-      leaf_lengths<E, K>(R, n, r, c, m, newcalc, L);
-      prefix<E>(L, P);
-      int32_t oa = 0, ob = 0;
-      const int xa = find_split<E>(L, P, start, &oa);
-      const int xb = find_split<E>(L, P, end, &ob);
-      // order the (at most two) split events by (index, offset)
-      int x1 = xa, x2 = xb;
-      int32_t o1 = oa, o2 = ob;
-      if (x1 < 0 || (x2 >= 0 && (x2 < x1 || (x2 == x1 && ob < oa)))) {
-        x1 = xb;
-        x2 = xa;
-        o1 = ob;
-        o2 = oa;
-      }
-      if (x2 >= 0 && x1 == x2 && o1 == o2) x2 = -1;  // same boundary twice
-      if (x1 < 0) {
-        x1 = x2;
-        o1 = o2;
-        x2 = -1;
-      }
-      if (x1 >= 0 && x2 < 0) {
-        Seg<K> t = get_seg<E, K>(R, x1);
-        t.len -= o1;
-        t.toff += (uint32_t)o1;
-        shift_all<E, K>(R, x1 + 1, INT32_MAX);
-        put_seg<E, K>(R, x1 + 1, t);
-        put<E>(R.len, x1, o1);
-        n += 1;
-        st[kStWritten] += 2;
-      } else if (x1 >= 0) {
-        Seg<K> t1 = get_seg<E, K>(R, x1);
-        Seg<K> t2 = (x2 == x1) ? t1 : get_seg<E, K>(R, x2);
-        const int32_t len1 = t1.len, len2 = t2.len;
-        shift_all<E, K>(R, x1 + 1, x2 + 2);
-        put<E>(R.len, x1, o1);
-        if (x2 == x1) {  // three pieces of one segment
-          t1.len = o2 - o1;
-          t1.toff += (uint32_t)o1;
-          t2.len = len1 - o2;
-          t2.toff += (uint32_t)o2;
-        } else {
-          t1.len = len1 - o1;
-          t1.toff += (uint32_t)o1;
-          put<E>(R.len, x2 + 1, o2);  // head of the second split segment
-          t2.len = len2 - o2;
-          t2.toff += (uint32_t)o2;
-        }
-        put_seg<E, K>(R, x1 + 1, t1);
-        put_seg<E, K>(R, x2 + 2, t2);
-        n += 2;
-        st[kStWritten] += 4;
-      }
-      if (end != start) {
-        // nodeMap (mergeTree.ts:2274-2330): leaves with len > 0 overlapping [start, end)
-        leaf_lengths<E, K>(R, n, r, c, m, newcalc, L);
-        prefix<E>(L, P);
-        bool in[E];
-        unsigned cnt = 0;
-#pragma unroll
-        for (int j = 0; j < E; j++) {
-          in[j] = L[j] > 0 && P[j] < end && P[j] + L[j] > start;
-          cnt += (unsigned)__popcll(__ballot(in[j]));
-        }
-        st[kStWritten] += cnt;
-        if (op.type == MTE_OP_REMOVE) {
-          // markRemoved (mergeTree.ts:1924-1962): keep the earliest removedSeq,
-          // add the client to removedClientIds
-          const uint32_t bit = 1u << c;
-#pragma unroll
-          for (int j = 0; j < E; j++) {
-            if (in[j]) {
-              R.rseq[j] = (R.rseq[j] == kNone) ? s : R.rseq[j];
-              R.rmask[j] |= bit;
-            }
-          }
-        } else {
-          // PropertiesManager.addProperties (segmentPropertiesManager.ts:63-151)
-          if (op.flags & MTE_F_REWRITE) {
-#pragma unroll
-            for (int kk = 0; kk < K; kk++)
-#pragma unroll
-              for (int j = 0; j < E; j++) R.pr[kk][j] = in[j] ? 0u : R.pr[kk][j];
-          }
-          const mte_propset ps = a.ps[op.a];
-          unsigned nw = 0;
-          for (uint32_t t = 0; t < ps.count; t++) {
-            const mte_prop p = a.pe[ps.first + t];
-            if (p.key >= a.n_keys) continue;
-            nw++;
-#pragma unroll
-            for (int kk = 0; kk < K; kk++) {
-              if ((uint32_t)kk == p.key) {
-#pragma unroll
-                for (int j = 0; j < E; j++) R.pr[kk][j] = in[j] ? p.value : R.pr[kk][j];
-              }
-            }
-          }
-          st[kStPwrites] += (unsigned long long)cnt * nw;
-        }
-      }
-    } else if (op.type != MTE_OP_NOOP) {
-      reason = MTE_E_INVALID_ARG;
-      break;
-    }
-
-    if (op.type != MTE_OP_NOOP) {  // Client.completeAndLogOp (client.ts:525-528)
-      if (!(h.cur_seq < s)) { reason = MTE_E_SEQ_ORDER; k++; break; }
-      if (!(h.min_seq <= op.min_seq)) { reason = MTE_E_MSN_ORDER; k++; break; }
-    }
-    if (op.flags & MTE_F_MSG_END) {
-      // updateSeqNumbers (client.ts:937-945) -> setMinSeq (mergeTree.ts:1077-1093)
-      if (!(h.cur_seq <= s)) { reason = MTE_E_SEQ_ORDER; k++; break; }
-      h.cur_seq = s;
-      if (!(op.min_seq <= s)) { reason = MTE_E_MSN_GT_SEQ; k++; break; }
-      if (!(h.min_seq <= op.min_seq)) { reason = MTE_E_MSN_ORDER; k++; break; }
-      if (op.min_seq > h.min_seq) {
-        h.min_seq = op.min_seq;
-        // zamboni: drop tombstones with removedSeq <= minSeq (stream compaction through LDS)
-        bool keep[E];
-        int32_t cntl = 0;
-#pragma unroll
-        for (int j = 0; j < E; j++) {
-          keep[j] = (base + j < n) && !(R.rseq[j] != kNone && R.rseq[j] <= h.min_seq);
-          cntl += keep[j] ? 1 : 0;
-        }
-        const int32_t incl = wave_incl_scan(cntl);
-        const int n_new = rdlane(incl, kWave - 1);
-        if (n_new != n) {
-          int32_t dst[E];
-          int32_t d0 = incl - cntl;
-#pragma unroll
-          for (int j = 0; j < E; j++) {
-            dst[j] = d0;
-            d0 += keep[j] ? 1 : 0;
-          }
-          auto compact = [&](auto& F) {
-#pragma unroll
-            for (int j = 0; j < E; j++)
-              if (keep[j]) lds[dst[j]] = (uint32_t)F[j];
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll
-            for (int j = 0; j < E; j++) F[j] = (std::remove_reference_t<decltype(F[0])>)lds[base + j];
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-          };
-          compact(R.len);
-          compact(R.seq);
-          compact(R.rseq);
-          compact(R.rmask);
-          compact(R.meta);
-          compact(R.toff);
-#pragma unroll
-          for (int kk = 0; kk < K; kk++) compact(R.pr[kk]);
-          n = n_new;
-          if (E > emin && n + 8 <= 16 * E) {
-            k++;
-            reason = 1;
-            break;
-          }
-        }
-      }
-    }
-  }
-
-  // write back (also on error / escalation)
-#pragma unroll
-  for (int j = 0; j < E; j++) {
-    const int i = base + j;
-    if (i < n) {
-      a.soa.len[dbase + i] = R.len[j];
-      a.soa.seq[dbase + i] = R.seq[j];
-      a.soa.rseq[dbase + i] = R.rseq[j];
-      a.soa.rmask[dbase + i] = R.rmask[j];
-      a.soa.meta[dbase + i] = R.meta[j];
-      a.soa.toff[dbase + i] = R.toff[j];
-#pragma unroll
-      for (int kk = 0; kk < K; kk++) a.soa.props[kk * a.soa.plane_stride + dbase + i] = R.pr[kk][j];
-    }
-  }
-  h.nseg = n;
-  return reason;
-}
-
-template <int EMIN, int EMAX, int K, bool LAST>
-__global__ __launch_bounds__(256) void replay_kernel(ReplayArgs a, int pass) {
-  __shared__ uint32_t lds_all[kDocsPerBlock][kWave * EMAX];
-  const int w = threadIdx.x / kWave;
-  const int doc = blockIdx.x * kDocsPerBlock + w;
-  if (doc >= (int)a.n_docs) return;
-  uint32_t* lds = lds_all[w];
-  DocHdr h = a.hdr[doc];
-  if (h.status != 0) return;
-  if (pass > 0 && !(h.flags & kHdrNeedsEsc)) return;
-  h.flags &= ~kHdrNeedsEsc;
-  const uint64_t kb = a.op_off[doc];
-  uint64_t k = kb + h.resume;
-  const uint64_t k1 = a.op_off[doc + 1];
-  unsigned long long st[kNumStats] = {0, 0, 0, 0, 0, 0};
-  while (k < k1) {
-    const int n = h.nseg;
-    int E = 0;
-    if (EMIN <= 1 && EMAX >= 1 && n + 2 <= kWave * 1) E = 1;
-    else if (EMIN <= 2 && EMAX >= 2 && n + 2 <= kWave * 2) E = 2;
-    else if (EMIN <= 4 && EMAX >= 4 && n + 2 <= kWave * 4) E = 4;
-    else if (EMIN <= 8 && EMAX >= 8 && n + 2 <= kWave * 8) E = 8;
-    else if (EMIN <= 16 && EMAX >= 16 && n + 2 <= kWave * 16) E = 16;
-    if (E == 0 || n + 2 > (int)a.cap) {
-      if (LAST || n + 2 > (int)a.cap) h.status = MTE_E_CAPACITY;
-      else h.flags |= kHdrNeedsEsc;
-      break;
-    }
-    int rc = 0;
-    if constexpr (EMIN <= 1 && EMAX >= 1) if (E == 1) rc = run_ops<1, K>(a, doc, h, k, k1, EMIN, lds, st);
-    if constexpr (EMIN <= 2 && EMAX >= 2) if (E == 2) rc = run_ops<2, K>(a, doc, h, k, k1, EMIN, lds, st);
-    if constexpr (EMIN <= 4 && EMAX >= 4) if (E == 4) rc = run_ops<4, K>(a, doc, h, k, k1, EMIN, lds, st);
-    if constexpr (EMIN <= 8 && EMAX >= 8) if (E == 8) rc = run_ops<8, K>(a, doc, h, k, k1, EMIN, lds, st);
-    if constexpr (EMIN <= 16 && EMAX >= 16) if (E == 16) rc = run_ops<16, K>(a, doc, h, k, k1, EMIN, lds, st);
-    if (rc < 0) {
-      h.status = rc;
-      break;
-    }
-  }
-  h.resume = (uint32_t)(k - kb);
-  if (lane_id() == 0) {
-    a.hdr[doc] = h;
-    unsigned long long* sd = a.stats + (size_t)doc * kNumStats;
-#pragma unroll
-    for (int t = 0; t < kNumStats; t++) {
-      if (t == kStMaxSegs) sd[t] = sd[t] > st[t] ? sd[t] : st[t];
-      else sd[t] += st[t];
-    }
-  }
-}
 
 // reset resume/escalation flags and stats at the start of a batch
 __global__ void begin_batch_kernel(DocHdr* hdr, unsigned long long* stats, uint32_t n_docs) {
@@ -672,8 +279,10 @@ int launch_reset(mte_ctx* c) {
 template <int K>
 int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   const uint32_t blocks = (c->n_docs + kDocsPerBlock - 1) / kDocsPerBlock;
+  // pass 1: register tiers E = 1, 2, 4 (docs up to 254 segments)
   hipLaunchKernelGGL((replay_kernel<1, 4, K, false>), dim3(blocks), dim3(256), 0, c->stream, a, 0);
   HIPCHK(c, hipGetLastError());
+  // pass 2: docs that outgrew pass 1 resume with E = 8, 16 (up to 1022 segments)
   hipLaunchKernelGGL((replay_kernel<8, 16, K, true>), dim3(blocks), dim3(256), 0, c->stream, a, 1);
   HIPCHK(c, hipGetLastError());
   return MTE_OK;
