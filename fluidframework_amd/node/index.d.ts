@@ -1,0 +1,111 @@
+// Type declarations of the MI355X batched sequence-merge engine's host layer
+// (index.js).  The surface mirrors @fluidframework/merge-tree's Client /
+// MergeTree for the remote-op path (packages/dds/merge-tree/src/client.ts,
+// mergeTree.ts); see index.js for the reference file:line of each member.
+
+export type PropertySet = { [key: string]: any };
+
+export interface ICombiningOp {
+  name: string;
+  defaultValue?: any;
+}
+
+/** IJSONSegment as carried by insert ops (ops.ts, textSegment.ts:40-48, mergeTreeNodes.ts:602-609). */
+export type IJSONSegment =
+  | string
+  | { text: string; props?: PropertySet }
+  | { marker: { refType?: number }; props?: PropertySet };
+
+export interface IMergeTreeOp {
+  type: 0 | 1 | 2 | 3;
+  pos1?: number;
+  pos2?: number;
+  seg?: IJSONSegment;
+  props?: PropertySet;
+  combiningOp?: ICombiningOp;
+  ops?: IMergeTreeOp[];
+}
+
+/** The fields of ISequencedDocumentMessage the path reads (protocol.ts:212). */
+export interface ISequencedDocumentMessage {
+  clientId: string | null;
+  sequenceNumber: number;
+  referenceSequenceNumber: number;
+  minimumSequenceNumber: number;
+  type: string;
+  contents: IMergeTreeOp | any;
+}
+
+export interface EngineOptions {
+  device?: number;
+  nKeys?: number;
+  segCapacity?: number;
+}
+
+export interface ClientOptions {
+  observerId?: string;
+  newLengthCalc?: boolean;
+  props?: PropertySet;
+  minSeq?: number;
+  currentSeq?: number;
+}
+
+export class MergeTreeError extends Error {
+  code: number;
+  assertCode?: number;
+}
+
+export interface EngineStats {
+  opsApplied: number;
+  segsScanned: number;
+  segsWritten: number;
+  propWrites: number;
+  unitsInserted: number;
+  maxSegs: number;
+  kernelMs: number;
+  algoBytes: number;
+}
+
+export class MergeTreeEngine {
+  constructor(options?: EngineOptions);
+  readonly nKeys: number;
+  createClient(initialText?: string, options?: ClientOptions): BatchClient;
+  start(): void;
+  flush(): void;
+  digests(): BigUint64Array;
+  statuses(): Int32Array;
+  stats(): EngineStats;
+  close(): void;
+}
+
+export interface BatchMergeTree {
+  insertSegments(pos: number, segments: Array<IJSONSegment | { toJSONObject(): IJSONSegment }>,
+    refSeq: number, clientId: number, seq: number): void;
+  markRangeRemoved(start: number, end: number, refSeq: number, clientId: number, seq: number): void;
+  annotateRange(start: number, end: number, props: PropertySet, combiningOp: ICombiningOp | undefined,
+    refSeq: number, clientId: number, seq: number): void;
+}
+
+export interface VisibleSegment {
+  kind: "text" | "marker";
+  text?: string;
+  refType?: number;
+  length: number;
+  props?: PropertySet;
+}
+
+export class BatchClient {
+  readonly mergeTree: BatchMergeTree;
+  readonly longClientId: string;
+  applyMsg(msg: ISequencedDocumentMessage, local?: boolean): void;
+  getOrAddShortClientId(longId: string): number;
+  getClientId(): number;
+  getLongClientId(shortId: number): string | undefined;
+  flush(): void;
+  getText(): string;
+  getLength(): number;
+  getCurrentSeq(): number;
+  getCollabWindow(): { clientId: number; currentSeq: number; minSeq: number; collaborating: boolean };
+  getPropertiesAtPosition(pos: number): PropertySet | undefined;
+  getSegments(): VisibleSegment[];
+}

@@ -1,0 +1,260 @@
+"use strict";
+/*
+ * index.js — drop-in host layer of the MI355X batched sequence-merge engine.
+ *
+ * `MergeTreeEngine` owns one engine context (one HIP device, many documents).
+ * `BatchClient` is one document seen by an observer client and keeps the
+ * surface of @fluidframework/merge-tree's Client for the remote-op path:
+ *
+ *   applyMsg(msg, local=false)           Client.applyMsg          client.ts:918-935
+ *   getText()                            TestClient.getText       test/testClient.ts:148-150
+ *   getLength()                          Client.getLength         client.ts:1161
+ *   getPropertiesAtPosition(pos)         Client.getPropertiesAtPosition client.ts:1133-1141
+ *   getCurrentSeq() / getCollabWindow()  Client.getCurrentSeq / CollaborationWindow
+ *   getOrAddShortClientId(longId)        client.ts:683-698
+ *   mergeTree.insertSegments(pos, segments, refSeq, clientId, seq)  mergeTree.ts:1394-1422
+ *   mergeTree.markRangeRemoved(start, end, refSeq, clientId, seq)   mergeTree.ts:1908-2000
+ *   mergeTree.annotateRange(start, end, props, combiningOp, refSeq, clientId, seq)
+ *                                                                   mergeTree.ts:1864-1906
+ *
+ * Messages are queued per document; the first read-out (or flush()) packs the
+ * queued messages of every document of the engine into one batch, uploads it
+ * (N-API -> C-ABI mte_submit) and replays it on the GPU (mte_run + mte_sync).
+ * There is no CPU fallback: without libmte.so / a HIP device the constructor
+ * throws.  Delta / maintenance callbacks are not emitted (DESIGN.md
+ * "Boundary"), local ops and combining ops other than "rewrite" throw.
+ */
+const path = require("path");
+const packing = require("./packing");
+
+const { BatchBuilder, DocClients, Interner, MergeTreeError, packDocInits } = packing;
+
+let addon = null;
+function loadAddon() {
+  if (addon === null) {
+    // built in-tree by `make -C fluidframework_amd/node` (DESIGN.md "Build")
+    addon = require(path.join(__dirname, "..", "_lib", "mte_napi.node"));
+  }
+  return addon;
+}
+
+// MTE_E_* -> the reference assert code with the same meaning (client.ts:525-528,
+// 940-943; mergeTree.ts:1078-1084, 1666-1672)
+const ASSERT_CODES = { "-5": 0x030, "-6": 0x031, "-7": 0x039 };
+
+function docError(code, doc) {
+  const a = loadAddon();
+  const e = new MergeTreeError(code, "document " + doc + ": " + a.strerror(code));
+  if (ASSERT_CODES[String(code)] !== undefined) e.assertCode = ASSERT_CODES[String(code)];
+  return e;
+}
+
+function segmentSpec(seg) {
+  // ISegment objects expose toJSONObject() (textSegment.ts:57-63, mergeTreeNodes.ts:611-621)
+  if (seg && typeof seg.toJSONObject === "function") return seg.toJSONObject();
+  return seg;
+}
+
+class MergeTreeEngine {
+  /**
+   * @param {{device?: number, nKeys?: number, segCapacity?: number}} [options]
+   */
+  constructor(options) {
+    const o = options || {};
+    this.nKeys = o.nKeys === undefined ? 8 : o.nKeys;
+    this.addon = loadAddon();
+    this.ctx = this.addon.create(o.device || 0, this.nKeys, o.segCapacity || 0);
+    this.interner = new Interner(this.nKeys);
+    this.docs = [];
+    this.clients = [];
+    this.started = false;
+    this.pending = null;
+    this.views = [];
+  }
+
+  /** A new document (before the first flush).  initialText becomes one seq-0
+   *  segment of LocalClientId, as the replay harness loads it
+   *  (client.replay.spec.ts:22-23). */
+  createClient(initialText, options) {
+    if (this.started) throw new MergeTreeError(-10, "createClient after the engine started");
+    const o = options || {};
+    const doc = this.docs.length;
+    this.docs.push({ text: initialText || "", newLengthCalc: !!o.newLengthCalc, props: o.props,
+      minSeq: o.minSeq || 0, currentSeq: o.currentSeq || 0 });
+    const c = new BatchClient(this, doc, o.observerId === undefined ? "A" : o.observerId);
+    this.clients.push(c);
+    return c;
+  }
+
+  start() {
+    if (this.started) return;
+    const p = packDocInits(this.docs, this.interner);
+    this.addon.loadDocs(this.ctx, p.inits, p.text, p.propsets, p.props);
+    this.started = true;
+    this.pending = new BatchBuilder(this.docs.length, this.interner);
+    this.views = new Array(this.docs.length).fill(null);
+  }
+
+  _batch() {
+    this.start();
+    return this.pending;
+  }
+
+  /** Replay every queued message of every document on the GPU. */
+  flush() {
+    this.start();
+    if (this.pending.count === 0) return;
+    const b = this.pending.build();
+    this.pending = new BatchBuilder(this.docs.length, this.interner);
+    this.views.fill(null);
+    this.addon.submit(this.ctx, b.offsets, b.ops, b.text, b.propsets, b.props);
+    this.addon.run(this.ctx);
+    this.addon.sync(this.ctx);
+  }
+
+  _view(doc) {
+    this.flush();
+    let v = this.views[doc];
+    if (v === null) {
+      v = this.addon.readDoc(this.ctx, doc, this.nKeys);
+      this.views[doc] = v;
+    }
+    if (v.status !== 0) throw docError(v.status, doc);
+    return v;
+  }
+
+  /** Per-doc canonical digests (4 x u64 each, DESIGN.md "Digest"). */
+  digests() {
+    this.flush();
+    const out = new BigUint64Array(this.docs.length * 4);
+    this.addon.digest(this.ctx, out);
+    return out;
+  }
+
+  statuses() {
+    this.flush();
+    const out = new Int32Array(this.docs.length);
+    this.addon.docStatus(this.ctx, out);
+    return out;
+  }
+
+  stats() {
+    return this.addon.stats(this.ctx);
+  }
+
+  close() {
+    if (this.ctx) {
+      this.addon.destroy(this.ctx);
+      this.ctx = null;
+    }
+  }
+}
+
+class BatchClient {
+  constructor(engine, doc, observerId) {
+    this.engine = engine;
+    this.doc = doc;
+    this.longClientId = observerId;
+    this.clients = new DocClients(observerId);
+    this.lastMinSeq = 0;
+    const self = this;
+    // MergeTree-level entry points (clientId = short id, as in the reference)
+    this.mergeTree = {
+      insertSegments(pos, segments, refSeq, clientId, seq) {
+        let p = pos;
+        for (const s of segments) { // mergeTree.ts:1394-1422: insertPos += len per segment
+          const spec = segmentSpec(s);
+          self.engine._batch().addRaw(self.doc, seq, refSeq, self.lastMinSeq, clientId,
+            { type: 0, pos1: p, seg: spec });
+          p += typeof spec === "string" ? spec.length : ("marker" in spec ? 1 : spec.text.length);
+        }
+      },
+      markRangeRemoved(start, end, refSeq, clientId, seq) {
+        self.engine._batch().addRaw(self.doc, seq, refSeq, self.lastMinSeq, clientId,
+          { type: 1, pos1: start, pos2: end });
+      },
+      annotateRange(start, end, props, combiningOp, refSeq, clientId, seq) {
+        const op = { type: 2, pos1: start, pos2: end, props };
+        if (combiningOp) op.combiningOp = combiningOp;
+        self.engine._batch().addRaw(self.doc, seq, refSeq, self.lastMinSeq, clientId, op);
+      },
+    };
+  }
+
+  /** Client.applyMsg (client.ts:918-935); remote messages only. */
+  applyMsg(msg, local) {
+    if (local) throw new MergeTreeError(-9, "local ops are not supported by the batch engine");
+    this.engine._batch().addMessage(this.doc, this.clients, msg);
+    if (msg.minimumSequenceNumber > this.lastMinSeq) this.lastMinSeq = msg.minimumSequenceNumber;
+  }
+
+  getOrAddShortClientId(longId) {
+    return this.clients.short(longId);
+  }
+
+  getClientId() {
+    return 0;
+  }
+
+  getLongClientId(shortId) {
+    for (const [k, v] of this.clients.ids) if (v === shortId) return k;
+    return undefined;
+  }
+
+  flush() {
+    this.engine.flush();
+  }
+
+  getText() {
+    return this.engine._view(this.doc).text;
+  }
+
+  getLength() {
+    return this.engine._view(this.doc).length;
+  }
+
+  getCurrentSeq() {
+    return this.engine._view(this.doc).curSeq;
+  }
+
+  getCollabWindow() {
+    const v = this.engine._view(this.doc);
+    return { clientId: 0, currentSeq: v.curSeq, minSeq: v.minSeq, collaborating: true };
+  }
+
+  /** Properties of the visible segment containing pos (undefined when it has none). */
+  getPropertiesAtPosition(pos) {
+    const v = this.engine._view(this.doc);
+    const nk = this.engine.nKeys;
+    let p = 0;
+    for (let i = 0; i < v.segLen.length; i++) {
+      const len = v.segLen[i];
+      if (pos >= p && pos < p + len) {
+        return this.engine.interner.decode(nk ? v.segProps.subarray(i * nk, (i + 1) * nk) : []);
+      }
+      p += len;
+    }
+    return undefined;
+  }
+
+  /** Visible segments in order: {kind: "text"|"marker", text?, refType?, length, props?} */
+  getSegments() {
+    const v = this.engine._view(this.doc);
+    const nk = this.engine.nKeys;
+    const out = [];
+    let t = 0;
+    for (let i = 0; i < v.segLen.length; i++) {
+      const kind = v.segKind[i];
+      const props = this.engine.interner.decode(nk ? v.segProps.subarray(i * nk, (i + 1) * nk) : []);
+      if (kind === 0) {
+        out.push({ kind: "text", text: v.text.substr(t, v.segLen[i]), length: v.segLen[i], props });
+        t += v.segLen[i];
+      } else {
+        out.push({ kind: "marker", refType: kind - 1, length: 1, props });
+      }
+    }
+    return out;
+  }
+}
+
+module.exports = { MergeTreeEngine, BatchClient, MergeTreeError, loadAddon, packing };

@@ -1,0 +1,324 @@
+"use strict";
+/*
+ * packing.js — host half of Client.applyMsg for the device engine: turns
+ * ISequencedDocumentMessage objects into 32-byte op records (include/mte.h
+ * mte_op) plus a UTF-16 text arena and property tables.
+ *
+ * Reference behaviour mirrored (packages/dds/merge-tree/src):
+ *  - short client ids in first-seen order, the observer's own id first
+ *    (Client.getOrAddShortClientId / startOrUpdateCollaboration,
+ *    client.ts:683-698, 1163-1183); every message registers its sender
+ *    (client.ts:920), "op" or not;
+ *  - only type "op" messages carry a merge-tree op, every message advances
+ *    currentSeq / minSeq (client.ts:922-934): non-op messages become NOOP
+ *    records;
+ *  - GROUP ops apply their members in order under one sequenced message
+ *    (client.ts:876-884): one record per member, MSG_END on the last;
+ *  - insert specs: string -> text, {text, props}, {marker:{refType}, props}
+ *    (test/testClient.ts:32-44, textSegment.ts:40-48, mergeTreeNodes.ts:602-609);
+ *    an insert without seg is a no-op (client.ts:481-487);
+ *  - annotate: null deletes a key, anything else sets it; combiningOp
+ *    "rewrite" is supported, other combining ops are rejected.
+ * Property keys are interned to plane indices and values to ids of their
+ * canonical JSON (sorted keys), so id equality == matchProperties
+ * (properties.ts:66-100).
+ *
+ * Written in the Node-12-compatible subset of JavaScript (no ?. / ??), see
+ * DESIGN.md "Host language".  Mirrors fluidframework_amd/packing.py record
+ * for record (tests/test_node_host.py checks the bytes are identical).
+ */
+
+const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 3;
+const F_MARKER = 0x1, F_MSG_END = 0x2, F_REWRITE = 0x4;
+const NO_PROPS = 0xffffffff;
+const MAX_CLIENTS = 32;
+const OP_BYTES = 32;
+const DOC_INIT_BYTES = 24;
+const DOC_NEW_LENGTH_CALC = 0x1;
+
+// MergeTreeDeltaType, ops.ts:43-48
+const INSERT = 0, REMOVE = 1, ANNOTATE = 2, GROUP = 3;
+
+const E_INVALID_ARG = -1, E_UNSUPPORTED = -9, E_CLIENT_RANGE = -12;
+
+class MergeTreeError extends Error {
+  constructor(code, message) {
+    super(message);
+    this.code = code;
+  }
+}
+
+function canonicalJson(v) {
+  if (v === null || typeof v !== "object") return JSON.stringify(v);
+  if (Array.isArray(v)) return "[" + v.map(canonicalJson).join(",") + "]";
+  const keys = Object.keys(v).sort();
+  return "{" + keys.map((k) => JSON.stringify(k) + ":" + canonicalJson(v[k])).join(",") + "}";
+}
+
+function checkI32(v, what) {
+  if (typeof v !== "number" || !Number.isInteger(v) || v < -2147483648 || v > 2147483647) {
+    throw new MergeTreeError(E_INVALID_ARG, what + "=" + String(v) + " is not an int32");
+  }
+  return v;
+}
+
+/** Key -> plane index, canonical JSON value -> id (0 is reserved for null). */
+class Interner {
+  constructor(nKeys) {
+    this.nKeys = nKeys;
+    this.keys = new Map();
+    this.keyNames = [];
+    this.values = new Map();
+    this.valueJson = [null];
+  }
+  key(name) {
+    let k = this.keys.get(name);
+    if (k === undefined) {
+      if (this.keyNames.length >= this.nKeys) {
+        throw new MergeTreeError(E_UNSUPPORTED, "more than nKeys=" + this.nKeys + " property keys (" + name + ")");
+      }
+      k = this.keyNames.length;
+      this.keys.set(name, k);
+      this.keyNames.push(name);
+    }
+    return k;
+  }
+  value(v) {
+    if (v === null || v === undefined) return 0;
+    const cj = canonicalJson(v);
+    let i = this.values.get(cj);
+    if (i === undefined) {
+      i = this.valueJson.length;
+      this.values.set(cj, i);
+      this.valueJson.push(cj);
+    }
+    return i;
+  }
+  /** plane values of one segment -> PropertySet (undefined when empty) */
+  decode(planes) {
+    let out;
+    for (let k = 0; k < planes.length; k++) {
+      if (planes[k]) {
+        if (out === undefined) out = {};
+        out[this.keyNames[k]] = JSON.parse(this.valueJson[planes[k]]);
+      }
+    }
+    return out;
+  }
+}
+
+/** Per-document long -> short client id map (client.ts:683-698). */
+class DocClients {
+  constructor(observerId) {
+    this.observer = observerId;
+    this.ids = new Map([[observerId, 0]]);
+  }
+  short(longId) {
+    let i = this.ids.get(longId);
+    if (i === undefined) {
+      i = this.ids.size;
+      this.ids.set(longId, i);
+    }
+    return i;
+  }
+}
+
+/** Property sets of one batch (mte_propset / mte_prop arrays). */
+class PropTable {
+  constructor(interner) {
+    this.interner = interner;
+    this.sets = [];
+    this.entries = [];
+  }
+  add(props) {
+    if (props === undefined || props === null) return NO_PROPS;
+    if (typeof props !== "object" || Array.isArray(props)) {
+      throw new MergeTreeError(E_INVALID_ARG, "props must be an object");
+    }
+    const first = this.entries.length / 2;
+    for (const name of Object.keys(props)) {
+      this.entries.push(this.interner.key(name), this.interner.value(props[name]));
+    }
+    this.sets.push(first, this.entries.length / 2 - first);
+    return this.sets.length / 2 - 1;
+  }
+}
+
+function utf16(s) {
+  const u = new Uint16Array(s.length);
+  for (let i = 0; i < s.length; i++) u[i] = s.charCodeAt(i); // JS strings are UTF-16 (textSegment.ts:52-55)
+  return u;
+}
+
+/** Collects messages for nDocs documents and emits one mte_batch. */
+class BatchBuilder {
+  constructor(nDocs, interner) {
+    this.nDocs = nDocs;
+    this.interner = interner;
+    this.props = new PropTable(interner);
+    this.docOps = [];
+    for (let d = 0; d < nDocs; d++) this.docOps.push([]);
+    this.text = [];
+    this.textUnits = 0;
+    this.count = 0;
+  }
+
+  _text(s) {
+    if (typeof s !== "string") throw new MergeTreeError(E_INVALID_ARG, "text must be a string");
+    const off = this.textUnits;
+    this.text.push(s);
+    this.textUnits += s.length;
+    return [off, s.length];
+  }
+
+  /** Client.applyMsg(msg, local=false) for one document (client.ts:918-935). */
+  addMessage(doc, clients, msg) {
+    const sender = msg.clientId;
+    const short = clients.short(sender);
+    if (short >= MAX_CLIENTS) throw new MergeTreeError(E_CLIENT_RANGE, "client " + String(sender));
+    const seq = checkI32(msg.sequenceNumber, "sequenceNumber");
+    const ref = checkI32(msg.referenceSequenceNumber === undefined ? 0 : msg.referenceSequenceNumber,
+      "referenceSequenceNumber");
+    const msn = checkI32(msg.minimumSequenceNumber, "minimumSequenceNumber");
+    const recs = [];
+    if ((msg.type === undefined ? "op" : msg.type) === "op") {
+      if (sender === clients.observer) {
+        throw new MergeTreeError(E_UNSUPPORTED, "ack of a local op (observer replay only)");
+      }
+      this._opRecords(msg.contents, recs);
+    }
+    if (recs.length === 0) recs.push([OP_NOOP, 0, 0, 0, 0, NO_PROPS]);
+    recs[recs.length - 1][1] |= F_MSG_END;
+    for (const r of recs) this.docOps[doc].push([seq, ref, msn, r[0], short, r[1], r[2], r[3], r[4], r[5]]);
+    this.count += recs.length;
+  }
+
+  /** One MergeTree-level call (insertSegments / markRangeRemoved / annotateRange):
+   *  a record that does not close a message (no window update). */
+  addRaw(doc, seq, ref, msn, client, op) {
+    if (client < 0 || client >= MAX_CLIENTS) throw new MergeTreeError(E_CLIENT_RANGE, "client " + client);
+    const recs = [];
+    this._opRecords(op, recs);
+    for (const r of recs) {
+      this.docOps[doc].push([checkI32(seq, "seq"), checkI32(ref, "refSeq"), msn, r[0], client, r[1], r[2], r[3],
+        r[4], r[5]]);
+    }
+    this.count += recs.length;
+  }
+
+  _opRecords(op, recs) {
+    if (op === null || typeof op !== "object") throw new MergeTreeError(E_INVALID_ARG, "op contents must be an object");
+    const t = op.type;
+    if (t === GROUP) {
+      for (const member of op.ops || []) this._opRecords(member, recs);
+      return;
+    }
+    if (!("pos1" in op) && op.relativePos1 !== undefined && op.relativePos1 !== null) {
+      throw new MergeTreeError(E_UNSUPPORTED, "relativePos1");
+    }
+    if ((t === REMOVE || t === ANNOTATE) && !("pos2" in op)) {
+      throw new MergeTreeError(E_UNSUPPORTED, "range op without pos2");
+    }
+    if (t === INSERT) {
+      const seg = op.seg;
+      if (seg === undefined || seg === null) { // applyInsertOp returns false: no segment
+        recs.push([OP_NOOP, 0, 0, 0, 0, NO_PROPS]);
+        return;
+      }
+      const pos = checkI32(op.pos1 === undefined ? 0 : op.pos1, "pos1");
+      if (typeof seg === "string") {
+        const tx = this._text(seg);
+        recs.push([OP_INSERT, 0, pos, tx[1], tx[0], NO_PROPS]);
+      } else if (typeof seg === "object" && "text" in seg) {
+        const tx = this._text(seg.text);
+        recs.push([OP_INSERT, 0, pos, tx[1], tx[0], this.props.add(seg.props)]);
+      } else if (typeof seg === "object" && "marker" in seg) {
+        const rt = checkI32(seg.marker.refType === undefined ? 0 : seg.marker.refType, "refType");
+        recs.push([OP_INSERT, F_MARKER, pos, rt, 0, this.props.add(seg.props)]);
+      } else {
+        throw new MergeTreeError(E_INVALID_ARG, "Unrecognized IJSONSegment type: " + JSON.stringify(seg));
+      }
+    } else if (t === REMOVE) {
+      recs.push([OP_REMOVE, 0, checkI32(op.pos1, "pos1"), checkI32(op.pos2, "pos2"), 0, NO_PROPS]);
+    } else if (t === ANNOTATE) {
+      let flags = 0;
+      const comb = op.combiningOp;
+      if (comb !== undefined && comb !== null) {
+        if (comb.name !== "rewrite") throw new MergeTreeError(E_UNSUPPORTED, "combiningOp " + String(comb.name));
+        flags = F_REWRITE;
+      }
+      const ps = this.props.add(op.props === undefined ? {} : op.props);
+      recs.push([OP_ANNOTATE, flags, checkI32(op.pos1, "pos1"), checkI32(op.pos2, "pos2"), ps, NO_PROPS]);
+    } else {
+      throw new MergeTreeError(E_INVALID_ARG, "unknown op type " + String(t));
+    }
+  }
+
+  /** -> {offsets: BigUint64Array, ops: Uint8Array, text: Uint16Array, propsets, props: Uint32Array} */
+  build() {
+    const offsets = new BigUint64Array(this.nDocs + 1);
+    const ops = Buffer.alloc(this.count * OP_BYTES);
+    let k = 0;
+    for (let d = 0; d < this.nDocs; d++) {
+      for (const r of this.docOps[d]) {
+        const o = k * OP_BYTES;
+        ops.writeInt32LE(r[0], o);
+        ops.writeInt32LE(r[1], o + 4);
+        ops.writeInt32LE(r[2], o + 8);
+        ops.writeUInt8(r[3], o + 12);
+        ops.writeUInt8(r[4], o + 13);
+        ops.writeUInt16LE(r[5], o + 14);
+        ops.writeInt32LE(r[6], o + 16);
+        ops.writeInt32LE(r[7], o + 20);
+        ops.writeUInt32LE(r[8] >>> 0, o + 24);
+        ops.writeUInt32LE(r[9] >>> 0, o + 28);
+        k++;
+      }
+      offsets[d + 1] = BigInt(k);
+    }
+    const text = new Uint16Array(this.textUnits);
+    let t = 0;
+    for (const s of this.text) {
+      for (let i = 0; i < s.length; i++) text[t++] = s.charCodeAt(i);
+    }
+    return {
+      offsets,
+      ops: new Uint8Array(ops.buffer, ops.byteOffset, ops.length),
+      text,
+      propsets: Uint32Array.from(this.props.sets),
+      props: Uint32Array.from(this.props.entries),
+    };
+  }
+}
+
+/** mte_doc_init records + load text for documents created before start(). */
+function packDocInits(docs, interner) {
+  const buf = Buffer.alloc(docs.length * DOC_INIT_BYTES);
+  const props = new PropTable(interner);
+  let off = 0;
+  const parts = [];
+  docs.forEach((d, i) => {
+    const o = i * DOC_INIT_BYTES;
+    buf.writeUInt32LE(off, o);
+    buf.writeUInt32LE(d.text.length, o + 4);
+    buf.writeUInt32LE(d.newLengthCalc ? DOC_NEW_LENGTH_CALC : 0, o + 8);
+    buf.writeUInt32LE(props.add(d.props) >>> 0, o + 12);
+    buf.writeInt32LE(d.minSeq || 0, o + 16);
+    buf.writeInt32LE(d.currentSeq || 0, o + 20);
+    parts.push(d.text);
+    off += d.text.length;
+  });
+  const text = utf16(parts.join(""));
+  return {
+    inits: new Uint8Array(buf.buffer, buf.byteOffset, buf.length),
+    text,
+    propsets: Uint32Array.from(props.sets),
+    props: Uint32Array.from(props.entries),
+  };
+}
+
+module.exports = {
+  OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, F_MARKER, F_MSG_END, F_REWRITE, NO_PROPS, MAX_CLIENTS,
+  INSERT, REMOVE, ANNOTATE, GROUP,
+  MergeTreeError, Interner, DocClients, PropTable, BatchBuilder, canonicalJson, packDocInits, utf16,
+};

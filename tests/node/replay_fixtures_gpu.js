@@ -1,0 +1,33 @@
+"use strict";
+// GPU test: the Node host layer (BatchClient over the N-API addon) replays
+// the reference's golden fixtures as client "A" (client.replay.spec.ts:16-60)
+// and checks initialText / resultText of every round.  Prints one JSON line.
+const { MergeTreeEngine } = require("../../fluidframework_amd/node");
+const { loadFixtures, asMsg } = require("./fixtures");
+
+const fx = loadFixtures();
+const eng = new MergeTreeEngine({ nKeys: 8 });
+const clients = fx.map((f) => eng.createClient(f.rounds[0].initialText));
+let passed = 0;
+const failures = [];
+const nRounds = Math.max.apply(null, fx.map((f) => f.rounds.length));
+for (let r = 0; r < nRounds; r++) {
+  fx.forEach((f, d) => {
+    if (r >= f.rounds.length) return;
+    const got = clients[d].getText();
+    if (got === f.rounds[r].initialText) passed++; else failures.push([f.name, r, "initial"]);
+    for (const m of f.rounds[r].msgs) clients[d].applyMsg(asMsg(m));
+  });
+  fx.forEach((f, d) => {
+    if (r >= f.rounds.length) return;
+    const got = clients[d].getText();
+    if (got === f.rounds[r].resultText && clients[d].getLength() === got.length) passed++;
+    else failures.push([f.name, r, "result"]);
+  });
+}
+const dig = eng.digests();
+const hex = [];
+for (let i = 0; i < dig.length; i++) hex.push(dig[i].toString(16));
+process.stdout.write(JSON.stringify({ passed, failures: failures.slice(0, 5), nFailures: failures.length,
+  digests: hex, stats: eng.stats() }) + "\n");
+eng.close();

@@ -1,0 +1,82 @@
+"""The Node host layer (fluidframework_amd/node): N-API addon over the C-ABI
+and the JS BatchClient that mirrors merge-tree's Client surface.
+
+CPU: the addon loads and exports its functions; the JS packer turns every
+golden-fixture message into exactly the bytes the Python packer produces.
+GPU: the JS BatchClient replays the golden fixtures through the addon and
+gets every reference checkpoint text, with digests equal to the oracle's."""
+import base64
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from fixtures_util import as_msg, load_fixtures
+from fluidframework_amd.packing import BatchBuilder, DocClients, Interner
+from oracle import OracleEngine
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NODE = shutil.which("node")
+ADDON = os.path.join(ROOT, "fluidframework_amd", "_lib", "mte_napi.node")
+pytestmark = pytest.mark.skipif(NODE is None, reason="node not installed")
+
+EXPORTS = ["abiVersion", "strerror", "create", "destroy", "lastError", "loadDocs", "submit", "run",
+           "sync", "reset", "digest", "docStatus", "readDoc", "stats"]
+
+
+def node(*args, timeout=300):
+    r = subprocess.run([NODE, *args], cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return r.stdout
+
+
+def test_addon_loads_and_exports():
+    assert os.path.exists(ADDON), "build the addon: make -C fluidframework_amd/node"
+    out = node("-e", "const m=require(process.argv[1]);"
+                     "console.log(JSON.stringify({keys:Object.keys(m),abi:m.abiVersion(),"
+                     "e:m.strerror(-5)}))", ADDON)
+    j = json.loads(out)
+    assert sorted(j["keys"]) == sorted(EXPORTS)
+    assert j["abi"] == 1
+    assert j["e"].startswith("0x030")
+
+
+def test_engine_without_device_throws_or_works():
+    out = node("-e", "const m=require('./fluidframework_amd/node');"
+                     "try{const e=new m.MergeTreeEngine();e.close();console.log('ok')}"
+                     "catch(err){console.log('err',err.code)}")
+    assert out.strip() in ("ok", "err -2")
+
+
+def test_js_packing_matches_python_packing_on_fixtures():
+    lines = node("tests/node/pack_fixtures.js").splitlines()
+    fx = load_fixtures()
+    interner = Interner(8)
+    clients = [DocClients("A") for _ in fx]
+    assert len(lines) == max(len(f["rounds"]) for f in fx)
+    for r, line in enumerate(lines):
+        j = json.loads(line)
+        bb = BatchBuilder(len(fx), interner)
+        for d, f in enumerate(fx):
+            if r < len(f["rounds"]):
+                for m in f["rounds"][r]["msgs"]:
+                    bb.add_message(d, clients[d], as_msg(m))
+        b = bb.build()
+        for key, arr in (("offsets", b["op_offsets"]), ("ops", b["ops"]), ("text", b["text"]),
+                         ("propsets", b["propsets"]), ("props", b["props"])):
+            assert base64.b64decode(j[key]) == np.ascontiguousarray(arr).tobytes(), (r, key)
+
+
+@pytest.mark.gpu
+def test_node_batch_client_replays_fixtures_on_gpu():
+    j = json.loads(node("tests/node/replay_fixtures_gpu.js", timeout=600))
+    assert j["nFailures"] == 0, j["failures"]
+    assert j["passed"] == 30 * 64 * 2
+    # same final state as the CPU restatement fed by the Python packer
+    from fixtures_util import replay_fixtures
+    _, _, o = replay_fixtures(lambda k: OracleEngine(k), check=False)
+    want = [format(int(x), "x") for x in o.digest().reshape(-1)]
+    assert j["digests"] == want
