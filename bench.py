@@ -68,6 +68,7 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl")
 
+    from fluidframework_amd import dist as fdist
     from fluidframework_amd import gen
     from fluidframework_amd.engine import DeviceEngine
 
@@ -78,7 +79,7 @@ def main():
 
     t0 = time.time()
     stream = gen.generate(args.config, n_docs=n_docs, ops_per_doc=ops_per_doc,
-                          doc_base=rank * n_docs, n_threads=threads)
+                          doc_base=fdist.shard_doc_base(rank, n_docs), n_threads=threads)
     gen_s = time.time() - t0
     n_ops_rank = int(stream["batch"]["op_offsets"][-1])
 
@@ -118,23 +119,13 @@ def main():
     elapsed = t_elapsed
     total_ops = n_ops_rank * world
     digest = eng.digest()
-    digest_fold = int(np.bitwise_xor.reduce(digest[:, 1] ^ digest[:, 2]))
+    fold = fdist.digest_fold(digest)
     if dist is not None:
-        import torch
-        t = torch.tensor([t_elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        n = torch.tensor([n_ops_rank], dtype=torch.int64, device=f"cuda:{local_rank}")
-        dist.all_reduce(n, op=dist.ReduceOp.SUM)
-        total_ops = int(n.item())
-        # the verification collective: gather every rank's per-doc digests (RCCL)
-        dd = torch.empty((n_docs, 4), dtype=torch.int64, device=f"cuda:{local_rank}")
-        eng.digest_device(dd.data_ptr())
-        eng.sync()
-        gathered = [torch.empty_like(dd) for _ in range(world)]
-        dist.all_gather(gathered, dd)
-        allg = torch.cat(gathered).cpu().numpy().view(np.uint64)
-        digest_fold = int(np.bitwise_xor.reduce(allg[:, 1] ^ allg[:, 2]))
+        dev = f"cuda:{local_rank}"
+        elapsed = fdist.max_over_ranks(dist, t_elapsed, device=dev)
+        total_ops = fdist.sum_over_ranks(dist, n_ops_rank, device=dev)
+        # the verification collective: every rank's per-doc digests over RCCL
+        fold = fdist.digest_fold(fdist.gather_digests(dist, engine=eng, device=dev))
 
     ms_per_step = elapsed * 1000.0 / args.steps
     value = total_ops / (elapsed / args.steps)
@@ -185,7 +176,7 @@ def main():
             "algo_bytes_per_op": algo_bytes / max(1, stats["ops_applied"]),
         },
         "cpu_baseline": cpu,
-        "digest_fold": f"{digest_fold:016x}",
+        "digest_fold": f"{fold:016x}",
         "parity_sample": parity,
         "gen_s": round(gen_s, 2),
     }
