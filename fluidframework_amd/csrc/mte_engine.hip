@@ -55,6 +55,62 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
   for (uint32_t k = 0; k < n_keys; k++) soa.props[k * soa.plane_stride + i] = init_props[(size_t)d * MTE_MAX_KEYS + k];
 }
 
+// Compile the batch's op records into the 64-byte device records the replay
+// kernels stage through LDS (mte_kernels.h): insert text offsets rebased onto
+// the ctx arena, the new segment's meta word, and the first two property
+// entries of the op's propset inlined.  Runs once per mte_submit, one thread
+// per record; 2 chunks of NOOP padding follow the last record.
+__global__ void compile_kernel(const mte_op* __restrict__ ops, uint64_t n_ops, const mte_propset* __restrict__ ps,
+                               const mte_prop* __restrict__ pe, uint32_t n_keys, uint32_t text_base,
+                               uint4* __restrict__ recs) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_ops + 2 * kChunk) return;
+  uint32_t w[16] = {0, 0, 0, MTE_OP_NOOP, 0, 0, 0, 0, kNoKey | (kNoKey << 8), 0, 0, MTE_NO_PROPS, 0, 0, 0, 0};
+  if (i < n_ops) {
+    const mte_op o = ops[i];
+    w[0] = (uint32_t)o.seq;
+    w[1] = (uint32_t)o.ref_seq;
+    w[2] = (uint32_t)o.min_seq;
+    w[3] = (uint32_t)o.type | ((uint32_t)o.client << 8) | ((uint32_t)o.flags << 16);
+    w[4] = (uint32_t)o.pos1;
+    w[5] = (uint32_t)o.pos2;
+    uint32_t psi = MTE_NO_PROPS;
+    if (o.type == MTE_OP_INSERT) {
+      const bool marker = (o.flags & MTE_F_MARKER) != 0;
+      w[5] = marker ? 1u : (uint32_t)o.pos2;
+      w[6] = marker ? 0u : text_base + o.a;
+      w[7] = ((uint32_t)o.client + 1u) | ((marker ? 1u + (uint32_t)o.pos2 : 0u) << 8);
+      psi = o.b;
+    } else if (o.type == MTE_OP_ANNOTATE) {
+      psi = o.a;
+    }
+    w[11] = psi;
+    if (psi != MTE_NO_PROPS) {
+      const mte_propset s = ps[psi];
+      uint32_t k0 = kNoKey, k1 = kNoKey, nw = 0;
+      for (uint32_t t = 0; t < s.count; t++) {
+        const mte_prop p = pe[s.first + t];
+        const bool ok = p.key < n_keys;
+        nw += ok ? 1u : 0u;
+        if (t == 0) {
+          k0 = ok ? p.key : kNoKey;
+          w[9] = p.value;
+        } else if (t == 1) {
+          k1 = ok ? p.key : kNoKey;
+          w[10] = p.value;
+        }
+      }
+      w[8] = k0 | (k1 << 8) | ((s.count > 2 ? 1u : 0u) << 16);
+      w[12] = nw;
+    }
+  }
+  uint4* r = recs + 4 * i;
+  r[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  r[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  r[2] = make_uint4(w[8], w[9], w[10], w[11]);
+  r[3] = make_uint4(w[12], w[13], w[14], w[15]);
+}
+
 // ---------------------------------------------------------------------------
 // digest (DESIGN.md "Digest"): H = sum_p x_p * B^(n-1-p) mod 2^61-1
 // ---------------------------------------------------------------------------
@@ -206,6 +262,10 @@ struct mte_ctx {
   // batch
   mte_op* d_ops = nullptr;
   uint64_t ops_cap = 0, n_ops = 0;
+  uint4* d_recs = nullptr;  // compiled records, 4 x uint4 each
+  uint64_t recs_cap = 0;
+  uint32_t* d_pairs = nullptr;  // pass-1 doc pairs
+  uint32_t n_pairs = 0;
   uint64_t* d_off = nullptr;
   uint64_t off_cap = 0;
   mte_propset* d_ps = nullptr;
@@ -253,8 +313,7 @@ int grow(mte_ctx* c, T** p, uint64_t* cap, uint64_t need, bool keep = false, uin
 }
 
 void free_docs(mte_ctx* c) {
-  void* ps[] = {c->hdr, c->soa.len, c->soa.seq, c->soa.rseq, c->soa.rmask, c->soa.meta, c->soa.toff,
-                c->soa.props, c->stats, c->d_inits, c->d_init_props, c->d_digest};
+  void* ps[] = {c->hdr, c->soa.len, c->stats, c->d_inits, c->d_init_props, c->d_digest, c->d_pairs};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   c->hdr = nullptr;
@@ -263,6 +322,8 @@ void free_docs(mte_ctx* c) {
   c->d_inits = nullptr;
   c->d_init_props = nullptr;
   c->d_digest = nullptr;
+  c->d_pairs = nullptr;
+  c->n_pairs = 0;
   c->n_docs = 0;
 }
 
@@ -278,12 +339,13 @@ int launch_reset(mte_ctx* c) {
 
 template <int K>
 int launch_replay(mte_ctx* c, const ReplayArgs& a) {
-  const uint32_t blocks = (c->n_docs + kDocsPerBlock - 1) / kDocsPerBlock;
-  // pass 1: register tiers E = 1, 2, 4 (docs up to 254 segments)
-  hipLaunchKernelGGL((replay_kernel<1, 4, K, false>), dim3(blocks), dim3(256), 0, c->stream, a, 0);
+  // pass 1: two documents per wavefront (docs up to 126 segments)
+  const uint32_t b1 = (c->n_pairs + kPairsPerBlock - 1) / kPairsPerBlock;
+  hipLaunchKernelGGL((pair_kernel<K>), dim3(b1), dim3(256), 0, c->stream, a);
   HIPCHK(c, hipGetLastError());
-  // pass 2: docs that outgrew pass 1 resume with E = 8, 16 (up to 1022 segments)
-  hipLaunchKernelGGL((replay_kernel<8, 16, K, true>), dim3(blocks), dim3(256), 0, c->stream, a, 1);
+  // pass 2: docs that outgrew pass 1 continue one per wavefront (up to 1022 segments)
+  const uint32_t b2 = (c->n_docs + kDocsPerBlock - 1) / kDocsPerBlock;
+  hipLaunchKernelGGL((big_kernel<K>), dim3(b2), dim3(256), 0, c->stream, a);
   HIPCHK(c, hipGetLastError());
   return MTE_OK;
 }
@@ -353,7 +415,7 @@ int mte_destroy(mte_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   free_docs(c);
-  void* ps[] = {c->arena, c->d_ops, c->d_off, c->d_ps, c->d_pe, c->d_pow};
+  void* ps[] = {c->arena, c->d_ops, c->d_recs, c->d_off, c->d_ps, c->d_pe, c->d_pow};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -391,20 +453,34 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
   const uint64_t nslots = (uint64_t)(n_docs ? n_docs : 1) * c->cap;
   c->soa.plane_stride = nslots;
   HIPCHK(c, hipMalloc((void**)&c->hdr, sizeof(DocHdr) * (n_docs ? n_docs : 1)));
-  HIPCHK(c, hipMalloc((void**)&c->soa.len, nslots * 4));
-  HIPCHK(c, hipMalloc((void**)&c->soa.seq, nslots * 4));
-  HIPCHK(c, hipMalloc((void**)&c->soa.rseq, nslots * 4));
-  HIPCHK(c, hipMalloc((void**)&c->soa.rmask, nslots * 4));
-  HIPCHK(c, hipMalloc((void**)&c->soa.meta, nslots * 4));
-  HIPCHK(c, hipMalloc((void**)&c->soa.toff, nslots * 4));
-  // kt (>= n_keys) planes, so the register-resident kernels never index past the array
-  HIPCHK(c, hipMalloc((void**)&c->soa.props, nslots * 4 * (c->kt ? c->kt : 1)));
+  // one allocation, planes at stride nslots: len seq rseq rmask meta toff props[kt]
+  // (kt >= n_keys planes, so the register-resident kernels never index past it)
+  {
+    const uint64_t planes = kFieldPlanes + (c->kt ? c->kt : 1);
+    uint32_t* base = nullptr;
+    HIPCHK(c, hipMalloc((void**)&base, nslots * 4 * planes));
+    c->soa.len = (int32_t*)base;
+    c->soa.seq = (int32_t*)(base + 1 * nslots);
+    c->soa.rseq = (int32_t*)(base + 2 * nslots);
+    c->soa.rmask = base + 3 * nslots;
+    c->soa.meta = base + 4 * nslots;
+    c->soa.toff = base + 5 * nslots;
+    c->soa.props = base + kFieldPlanes * nslots;
+  }
   HIPCHK(c, hipMemsetAsync(c->soa.props, 0, nslots * 4 * (c->kt ? c->kt : 1), c->stream));
   HIPCHK(c, hipMalloc((void**)&c->stats, sizeof(unsigned long long) * kNumStats * (n_docs ? n_docs : 1)));
   HIPCHK(c, hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * kNumStats * (n_docs ? n_docs : 1), c->stream));
   HIPCHK(c, hipMalloc((void**)&c->d_inits, sizeof(mte_doc_init) * (n_docs ? n_docs : 1)));
   HIPCHK(c, hipMalloc((void**)&c->d_init_props, sizeof(uint32_t) * iprops.size() + 4));
   HIPCHK(c, hipMalloc((void**)&c->d_digest, sizeof(uint64_t) * 4 * (n_docs ? n_docs : 1)));
+  {
+    // pass-1 pairs: docs (2p, 2p+1); an odd last doc runs alone
+    c->n_pairs = (n_docs + 1) / 2;
+    std::vector<uint32_t> pairs((size_t)c->n_pairs * 2 + 2, 0xffffffffu);
+    for (uint32_t d = 0; d < n_docs; d++) pairs[d] = d;
+    HIPCHK(c, hipMalloc((void**)&c->d_pairs, pairs.size() * 4));
+    HIPCHK(c, hipMemcpy(c->d_pairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice));
+  }
   if (n_docs) {
     HIPCHK(c, hipMemcpyAsync(c->d_inits, docs, sizeof(mte_doc_init) * n_docs, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_init_props, iprops.data(), sizeof(uint32_t) * iprops.size(),
@@ -469,6 +545,14 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
     HIPCHK(c, hipMemcpyAsync(c->d_ps, b->propsets, b->n_propsets * sizeof(mte_propset), hipMemcpyHostToDevice, c->stream));
   if (b->n_props)
     HIPCHK(c, hipMemcpyAsync(c->d_pe, b->props, b->n_props * sizeof(mte_prop), hipMemcpyHostToDevice, c->stream));
+  // compile the records (one pass over the batch, HBM-bound)
+  if ((rc = grow(c, &c->d_recs, &c->recs_cap, 4 * (b->n_ops + 2 * kChunk)))) return rc;
+  {
+    const uint64_t nthr = b->n_ops + 2 * kChunk;
+    hipLaunchKernelGGL(compile_kernel, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, c->stream, c->d_ops,
+                       b->n_ops, c->d_ps, c->d_pe, c->n_keys, c->batch_text_base, c->d_recs);
+    HIPCHK(c, hipGetLastError());
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));  // host buffers may be freed after return
   c->n_ops = b->n_ops;
   c->submitted = true;
@@ -485,16 +569,18 @@ int mte_run(mte_ctx* c) {
   HIPCHK(c, hipGetLastError());
   ReplayArgs a;
   a.hdr = c->hdr;
-  a.soa = c->soa;
+  a.planes = (uint32_t*)c->soa.len;
+  a.stride = c->soa.plane_stride;
   a.cap = c->cap;
   a.n_docs = c->n_docs;
-  a.ops = c->d_ops;
+  a.recs = c->d_recs;
   a.op_off = c->d_off;
   a.ps = c->d_ps;
   a.pe = c->d_pe;
   a.n_keys = c->n_keys;
-  a.text_base = c->batch_text_base;
   a.stats = c->stats;
+  a.pair_docs = c->d_pairs;
+  a.n_pairs = c->n_pairs;
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   int rc = c->kt == 0 ? launch_replay<0>(c, a) : (c->kt == 4 ? launch_replay<4>(c, a) : launch_replay<8>(c, a));
   if (rc) return rc;

@@ -1,407 +1,636 @@
-// mte_replay.h — the replay kernel: one wavefront per document, segments in
-// VGPRs (see mte_kernels.h for the layout and primitives).
+// mte_replay.h — the replay kernels.
+//
+//   pair_kernel  — pass 1: two documents per wavefront, E in {1, 2} (<= 126
+//                  segments each).  The wave alternates between its two
+//                  documents op by op, so all documents of a 10k-doc batch
+//                  are resident on the chip at once (one wave per doc would
+//                  need 10k resident waves; the chip holds 8 per SIMD).
+//   big_kernel   — pass 2: one document per wavefront, E in {4, 8, 16}
+//                  (<= 1022 segments), for documents pass 1 escalated.
+//
+// Both run the same per-op step (doc_step) on a register-resident document.
+// Op records (64 B compiled records, mte_kernels.h) are staged through LDS in
+// 1 KiB chunks of 16, double-buffered: the next chunk's global load is issued
+// when a chunk starts and written to LDS half-way through it, so the per-op
+// read is three LDS broadcast reads.
 #pragma once
 
 #include <type_traits>
 
 #include "mte_kernels.h"
 
+// Build-time knobs (tools/variants.sh builds A/B variants; defaults are the product build)
+#ifndef MTE_PAIR_WAVES
+#define MTE_PAIR_WAVES 5
+#endif
+#ifndef MTE_BURST
+#define MTE_BURST 128
+#endif
+#ifndef MTE_PASS1_EMAX
+#define MTE_PASS1_EMAX 4
+#endif
+
 namespace mte {
 
+constexpr uint32_t kBurst = MTE_BURST;  // ops per burst in pass 1
+
+// per-document replay state (wave-uniform except the in-flight chunk `sv`);
+// op cursors are 32-bit, relative to the document's first record of the batch
+struct DocRun {
+  int doc;
+  int n;
+  int32_t min_seq, cur_seq;
+  int32_t status;
+  uint32_t flags;
+  bool running;
+  const uint4* recp;  // the doc's first compiled record (4 x uint4 each)
+  uint32_t k, k1;     // current op, end
+  uint32_t cbase;     // first record of the current LDS chunk
+  int par;            // LDS buffer holding the current chunk
+  uint4* stage;       // LDS: 2 chunks x 16 records x 4 uint4
+  uint4 sv;           // next chunk (in flight), one uint4 per lane
+  uint32_t st[kNumStats];
+};
+
+__device__ __forceinline__ void fence_wave() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// start staging at record D.k: chunk 0 synchronously, chunk 1 in flight
+__device__ __forceinline__ void stage_begin(DocRun& D, const ReplayArgs& a) {
+  const int l = lane_id();
+  D.cbase = D.k;
+  D.par = 0;
+  D.stage[l] = D.recp[4 * D.cbase + (uint32_t)l];
+  D.sv = D.recp[4 * (D.cbase + kChunk) + (uint32_t)l];
+  fence_wave();
+}
+
 // ISegment.addProperties for a remote op (segmentPropertiesManager.ts:63-151):
-// each key of the set is written (value 0 = null = delete).  The first two
-// entries come prefetched with the op; longer sets are read here.
-template <typename F>
-__device__ __forceinline__ uint32_t for_each_prop(const OpView& op, uint32_t psi, const ReplayArgs& a, F&& f) {
-  uint32_t w = 0;
-  if (op.pcnt > 0 && op.pk0 < a.n_keys) { f(op.pk0, op.pv0); w++; }
-  if (op.pcnt > 1 && op.pk1 < a.n_keys) { f(op.pk1, op.pv1); w++; }
-  if (op.pcnt > 2) {
+// entries in order, value 0 (null) deletes.  The first two entries come with
+// the compiled record; longer sets are read here.  Applied to the slots with
+// sel[j] set (E slots per lane, K planes); no lambdas, so the register arrays
+// never need an address.
+template <int E, int K>
+__device__ __forceinline__ void set_plane(uint32_t (&pr)[K > 0 ? K : 1][E], const bool (&sel)[E], uint32_t key,
+                                          uint32_t val) {
+  // branch-free over planes: a `kk == key` branch gets folded into pr[key],
+  // a dynamic index that would push the whole register file to scratch
+#pragma unroll
+  for (int kk = 0; kk < K; kk++) {
+    const bool hit = (uint32_t)kk == key;
+#pragma unroll
+    for (int jj = 0; jj < E; jj++) pr[kk][jj] = (hit && sel[jj]) ? val : pr[kk][jj];
+  }
+}
+
+template <int E, int K>
+__device__ __forceinline__ void apply_props(uint32_t (&pr)[K > 0 ? K : 1][E], const bool (&sel)[E], uint32_t pk,
+                                            uint32_t v0, uint32_t v1, uint32_t psi, const ReplayArgs& a) {
+  const uint32_t k0 = pk & 0xffu, k1 = (pk >> 8) & 0xffu;
+  if (k0 != kNoKey) set_plane<E, K>(pr, sel, k0, v0);
+  if (k1 != kNoKey) set_plane<E, K>(pr, sel, k1, v1);
+  if (pk >> 16) {
     const mte_propset ps = a.ps[psi];
     for (uint32_t t = 2; t < ps.count; t++) {
       const mte_prop p = a.pe[ps.first + t];
-      if (p.key < a.n_keys) { f(p.key, p.value); w++; }
+      if (p.key < a.n_keys) set_plane<E, K>(pr, sel, uni(p.key), uni(p.value));
     }
   }
-  return w;
 }
 
-// Returns 0 = batch range done, 1 = re-pick E, or a negative MTE_E_*.
+// one plane of the zamboni stream compaction: scatter kept slots to their
+// compacted index in LDS, gather back lane-major
+template <int E, typename T>
+__device__ __forceinline__ void compact_plane(T (&F)[E], const bool (&keep)[E], const int32_t (&dst)[E],
+                                              uint32_t* zlds) {
+  const int base = lane_id() * E;
+#pragma unroll
+  for (int jj = 0; jj < E; jj++)
+    if (keep[jj]) zlds[dst[jj]] = (uint32_t)F[jj];
+  fence_wave();
+#pragma unroll
+  for (int jj = 0; jj < E; jj++) F[jj] = (T)zlds[base + jj];
+  fence_wave();
+}
+
+// Shift every plane (and, for range ops, the L / P planes).  A scheduling
+// barrier between planes keeps the compiler from interleaving all planes'
+// old and new values (which doubles the live register state).
+template <int E, int K, bool LP>
+__device__ __forceinline__ void shift_all(Regs<E, K>& R, int32_t (&L)[E], int32_t (&P)[E], int t1, int t2) {
+  pull_shift<E>(R.len, t1, t2);
+  __builtin_amdgcn_sched_barrier(0);
+  pull_shift<E>(R.seq, t1, t2);
+  __builtin_amdgcn_sched_barrier(0);
+  pull_shift<E>(R.rseq, t1, t2);
+  __builtin_amdgcn_sched_barrier(0);
+  pull_shift<E>(R.rmask, t1, t2);
+  __builtin_amdgcn_sched_barrier(0);
+  pull_shift<E>(R.meta, t1, t2);
+  __builtin_amdgcn_sched_barrier(0);
+  pull_shift<E>(R.toff, t1, t2);
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    __builtin_amdgcn_sched_barrier(0);
+    pull_shift<E>(R.pr[k], t1, t2);
+  }
+  if constexpr (LP) {
+    __builtin_amdgcn_sched_barrier(0);
+    pull_shift<E>(L, t1, t2);
+    __builtin_amdgcn_sched_barrier(0);
+    pull_shift<E>(P, t1, t2);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 template <int E, int K>
-__device__ int run_ops(const ReplayArgs& a, int doc, DocHdr& h, uint64_t& k, uint64_t k1, int emin,
-                       uint32_t* lds, uint32_t (&st)[kNumStats]) {
-  const int l = lane_id();
-  const int base = l * E;
-  const uint64_t dbase = (uint64_t)doc * a.cap;
-  const bool newcalc = (h.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
-  int n = h.nseg;
-
-  // uniform per-field base pointers (SGPR) + 32-bit lane offsets: saddr addressing
-  int32_t* __restrict__ p_len = a.soa.len + dbase;
-  int32_t* __restrict__ p_seq = a.soa.seq + dbase;
-  int32_t* __restrict__ p_rseq = a.soa.rseq + dbase;
-  uint32_t* __restrict__ p_rmask = a.soa.rmask + dbase;
-  uint32_t* __restrict__ p_meta = a.soa.meta + dbase;
-  uint32_t* __restrict__ p_toff = a.soa.toff + dbase;
-  uint32_t* __restrict__ p_props = a.soa.props + dbase;
-  const uint64_t pstride = a.soa.plane_stride;
-
-  Regs<E, K> R;
+__device__ __forceinline__ void load_regs(Regs<E, K>& R, const DocRun& D, const ReplayArgs& a) {
+  const uint32_t* pl = a.planes + (uint64_t)D.doc * a.cap;
+  const uint64_t st = a.stride;
+  const int base = lane_id() * E;
 #pragma unroll
   for (int j = 0; j < E; j++) {
-    const uint32_t i = (uint32_t)(base + j);
-    const bool v = (int)i < n;
-    R.len[j] = v ? p_len[i] : 0;
-    R.seq[j] = v ? p_seq[i] : 0;
-    R.rseq[j] = v ? p_rseq[i] : 0;
-    R.rmask[j] = v ? p_rmask[i] : 0u;
-    R.meta[j] = v ? p_meta[i] : 0u;
-    R.toff[j] = v ? p_toff[i] : 0u;
+    const int i = base + j;
+    const bool v = i < D.n;
+    const uint32_t x = (uint32_t)(v ? i : 0);
+    R.len[j] = v ? (int32_t)pl[x] : 0;
+    R.seq[j] = v ? (int32_t)pl[st + x] : 0;
+    R.rseq[j] = v ? (int32_t)pl[2 * st + x] : kPad;
+    R.rmask[j] = v ? pl[3 * st + x] : 0u;
+    R.meta[j] = v ? pl[4 * st + x] : 0u;
+    R.toff[j] = v ? pl[5 * st + x] : 0u;
 #pragma unroll
-    for (int kk = 0; kk < K; kk++) R.pr[kk][j] = v ? p_props[kk * pstride + i] : 0u;
+    for (int k = 0; k < K; k++) R.pr[k][j] = v ? pl[(kFieldPlanes + k) * st + x] : 0u;
   }
+}
 
+template <int E, int K>
+__device__ __forceinline__ void store_regs(const Regs<E, K>& R, const DocRun& D, const ReplayArgs& a) {
+  uint32_t* pl = a.planes + (uint64_t)D.doc * a.cap;
+  const uint64_t st = a.stride;
+  const int base = lane_id() * E;
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    const int i = base + j;
+    if (i < D.n) {
+      const uint32_t x = (uint32_t)i;
+      pl[x] = (uint32_t)R.len[j];
+      pl[st + x] = (uint32_t)R.seq[j];
+      pl[2 * st + x] = (uint32_t)R.rseq[j];
+      pl[3 * st + x] = R.rmask[j];
+      pl[4 * st + x] = R.meta[j];
+      pl[5 * st + x] = R.toff[j];
+#pragma unroll
+      for (int k = 0; k < K; k++) pl[(kFieldPlanes + k) * st + x] = R.pr[k][j];
+    }
+  }
+}
+
+// A split of one leaf, applied after the shift: the head keeps [0, o) at
+// slot h, the tail [o, len) lands at slot tl with its text offset advanced.
+struct SplitPatch {
+  int h, tl;      // -1: none
+  int32_t o, len; // offset, length of the leaf before the split
+  uint32_t toff;  // text offset of the leaf before the split
+  int32_t pos;    // document position of the tail (P of the tail slot)
+};
+
+// One op record of one document: Client.applyMsg -> applyRemoteOp ->
+// insertSegments / markRangeRemoved / annotateRange -> updateSeqNumbers
+// (client.ts:918-945).  Returns 0 (applied), 1 (re-pick the register tier
+// before this op, or after a compaction that shrank the doc), or a negative
+// MTE_E_* (the doc stops).
+//
+// Structure: a scalar decision phase (visibility lengths, prefix scan and the
+// split / insert-slot lookups, then wave-uniform shift thresholds and split
+// patches) followed by ONE vector apply phase shared by all op types, so the
+// register state flows through a single path (no per-branch copies).
+template <int E, int K>
+__device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, const ReplayArgs& a, uint32_t* zlds, int emin) {
+  const int l = lane_id();
+  const int base = l * E;
   const int lim = kWave * E < (int)a.cap ? kWave * E : (int)a.cap;
-  // op chunks, double-buffered without register copies: chunk q (records
-  // [kq, kq + 64)) lives in buf[q & 1]; entering chunk q issues the load of
-  // chunk q+1 into the other buffer and the propset gather of chunk q.
-  OpChunk bufA, bufB;
-  uint64_t cbase = k;
-  int par = 0;
-  chunk_load_ops(bufA, a.ops, cbase, k1);
-  chunk_load_ops(bufB, a.ops, cbase + kWave, k1);
-  chunk_load_props(bufA, a.ps, a.pe);
+  if (D.n + 2 > lim || D.st[kStOps] >= (1u << 20)) return 1;
 
-  int reason = 0;
-  for (; k < k1; k++) {
-    // re-pick E when the doc no longer fits; also return every 2^20 ops so the
-    // 32-bit stat counters never wrap
-    if (n + 2 > lim || st[kStOps] >= (1u << 20)) {
-      reason = 1;
-      break;
-    }
-    int j = (int)(k - cbase);
-    if (j == kWave) {
-      cbase += kWave;
-      j = 0;
-      par ^= 1;
-      if (par) {
-        chunk_load_ops(bufA, a.ops, cbase + kWave, k1);
-        chunk_load_props(bufB, a.ps, a.pe);
-      } else {
-        chunk_load_ops(bufB, a.ops, cbase + kWave, k1);
-        chunk_load_props(bufA, a.ps, a.pe);
-      }
-    }
-    const OpView op = par ? chunk_op(bufB, j) : chunk_op(bufA, j);
-    st[kStOps]++;
-    st[kStMaxSegs] = (uint32_t)n > st[kStMaxSegs] ? (uint32_t)n : st[kStMaxSegs];
-    const int c = (int)op.client;
-    if (c >= MTE_MAX_CLIENTS) {
-      reason = MTE_E_CLIENT_RANGE;
-      break;
-    }
-    const int32_t r = op.ref_seq, s = op.seq, m = h.min_seq;
+  // ---- op record from the LDS stage --------------------------------------
+  int j = (int)(D.k - D.cbase);
+  if (j == kChunk) {
+    D.cbase += kChunk;
+    D.par ^= 1;
+    j = 0;
+    D.sv = D.recp[4 * (D.cbase + kChunk) + (uint32_t)l];  // chunk after next, in flight
+  }
+  if (j == kChunk / 2) {
+    D.stage[(D.par ^ 1) * 4 * kChunk + l] = D.sv;  // next chunk -> the other buffer
+    fence_wave();
+  }
+  const uint4* rec = D.stage + D.par * 4 * kChunk + 4 * j;
+  const uint4 q0 = rec[0], q1 = rec[1];
+  const uint32_t w3 = uni(q0.w);
+  const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
+  if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
+  D.st[kStOps]++;
+  D.st[kStMaxSegs] = (uint32_t)D.n > D.st[kStMaxSegs] ? (uint32_t)D.n : D.st[kStMaxSegs];
+  const int32_t s = uni((int32_t)q0.x);
+  const int32_t msn = uni((int32_t)q0.z);
+  int n = D.n;
 
-    if (op.type == MTE_OP_INSERT) {
+  if (type == MTE_OP_INSERT || type == MTE_OP_REMOVE || type == MTE_OP_ANNOTATE) {
+    const bool ins = type == MTE_OP_INSERT;
+    D.st[kStScanned] += (uint32_t)n;
+    const int32_t r = uni((int32_t)q0.y);
+    const int32_t pos1 = uni((int32_t)q1.x), pos2 = uni((int32_t)q1.y);
+    int32_t L[E], P[E];
+    leaf_lengths<E, K>(R, r, c + 1, (int)c, D.min_seq, (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0, L);
+    const int32_t total = prefix<E>(L, P);
+
+    // ---- scalar decisions ------------------------------------------------
+    int t1 = INT32_MAX, t2 = INT32_MAX;  // shift thresholds (pull_shift)
+    SplitPatch pa{-1, -1, 0, 0, 0u, 0}, pb{-1, -1, 0, 0, 0u, 0};
+    int g = -1;  // slot of the new segment
+    if (ins) {
       // Client.applyInsertOp -> MergeTree.insertSegments (client.ts:470-505,
-      // mergeTree.ts:1394-1422)
-      st[kStScanned] += (uint32_t)n;
-      int32_t L[E], P[E];
-      leaf_lengths<E, K>(R, n, r, c, m, newcalc, L);
-      const int32_t total = prefix<E>(L, P);
-      const int32_t pos = op.pos1;
+      // mergeTree.ts:1394-1422): ensureIntervalBoundary, then insertingWalk
+      const int32_t nlen = pos2;
       int32_t off = 0;
-      const int xs = find_split<E>(L, P, pos, &off);  // ensureIntervalBoundary
-      const bool marker = (op.flags & MTE_F_MARKER) != 0;
-      const int32_t nlen = marker ? 1 : op.pos2;
-      int g = -1;
-      if (xs < 0 && nlen > 0) {
-        g = find_slot<E>(L, P, pos);
-        if (g < 0) {
-          if (pos > total) {
-            reason = MTE_E_INSERT_FAILED;  // mergeTree.ts:1666-1672
-            break;
-          }
-          g = n;
-        }
-      }
+      const int xs = find_split<E>(L, P, pos1, &off);
       if (xs >= 0) {
-        // split: head keeps [0, off), the shift copies it into the tail slot
-        const int32_t xlen = bcast<E>(R.len, xs);
-        const uint32_t xtoff = bcast<E>(R.toff, xs);
-        if (nlen > 0) {
-          shift_all<E, K>(R, xs, xs + 1);  // slot xs+1: new segment, xs+2: tail
+        pa.h = xs;
+        pa.o = off;
+        pa.len = bcast<E>(R.len, xs);
+        pa.toff = bcast<E>(R.toff, xs);
+        t1 = xs;
+        if (nlen > 0) {  // [head][new][tail]
+          t2 = xs + 1;
           g = xs + 1;
-          st[kStWritten] += 3;
+          pa.tl = xs + 2;
+          D.st[kStWritten] += 3;
         } else {
-          shift_all<E, K>(R, xs, INT32_MAX);
-          st[kStWritten] += 2;
+          pa.tl = xs + 1;
+          D.st[kStWritten] += 2;
         }
-        const int tail = nlen > 0 ? xs + 2 : xs + 1;
-        put<E>(R.len, xs, off);
-        put<E>(R.len, tail, xlen - off);
-        put<E>(R.toff, tail, xtoff + (uint32_t)off);
         n += 1;
       } else if (nlen > 0) {
-        shift_all<E, K>(R, g - 1, INT32_MAX);
-        st[kStWritten] += 1;
+        g = find_slot<E>(L, P, pos1);
+        if (g < 0) {
+          if (pos1 > total) return MTE_E_INSERT_FAILED;  // mergeTree.ts:1666-1672
+          g = n;
+        }
+        t1 = g - 1;
+        D.st[kStWritten] += 1;
       }
-      if (nlen > 0) {
-        uint32_t pr[K > 0 ? K : 1];
-#pragma unroll
-        for (int kk = 0; kk < (K > 0 ? K : 1); kk++) pr[kk] = 0;
-        if (op.b != MTE_NO_PROPS)
-          st[kStPwrites] += for_each_prop(op, op.b, a, [&](uint32_t key, uint32_t val) {
-#pragma unroll
-            for (int kk = 0; kk < K; kk++) pr[kk] = ((uint32_t)kk == key) ? val : pr[kk];
-          });
-        if (!marker) st[kStUnits] += (uint32_t)nlen;
-        const uint32_t meta = (uint32_t)(c + 1) | ((marker ? 1u + (uint32_t)op.pos2 : 0u) << 8);
-        put_new<E, K>(R, g, nlen, s, meta, marker ? 0u : a.text_base + op.a, pr);
-        n += 1;
-      }
-    } else if (op.type == MTE_OP_REMOVE || op.type == MTE_OP_ANNOTATE) {
-      // markRangeRemoved (mergeTree.ts:1908-2000) / annotateRange (1864-1906)
-      st[kStScanned] += (uint32_t)n;
-      const int32_t start = op.pos1, end = op.pos2;
-      int32_t L[E], P[E];
-      leaf_lengths<E, K>(R, n, r, c, m, newcalc, L);
-      prefix<E>(L, P);
-      int32_t oa = 0, ob = 0;
-      const int xa = find_split<E>(L, P, start, &oa);
-      const int xb = find_split<E>(L, P, end, &ob);
-      // order the (at most two) split events by (index, offset)
-      int x1 = xa, x2 = xb;
-      int32_t o1 = oa, o2 = ob;
-      if (x1 < 0 || (x2 >= 0 && (x2 < x1 || (x2 == x1 && ob < oa)))) {
-        x1 = xb;
-        x2 = xa;
-        o1 = ob;
-        o2 = oa;
-      }
-      if (x2 >= 0 && x1 == x2 && o1 == o2) x2 = -1;  // same boundary twice
+      if (nlen > 0) n += 1;
+    } else {
+      // markRangeRemoved (mergeTree.ts:1908-2000) / annotateRange
+      // (1864-1906): the two ensureIntervalBoundary calls, ordered by position
+      const int32_t b1 = pos1 < pos2 ? pos1 : pos2, b2 = pos1 < pos2 ? pos2 : pos1;
+      int32_t o1 = 0, o2 = 0;
+      int x1 = find_split<E>(L, P, b1, &o1);
+      int x2 = b2 != b1 ? find_split<E>(L, P, b2, &o2) : -1;
+      int32_t bb1 = b1;
       if (x1 < 0) {
         x1 = x2;
         o1 = o2;
+        bb1 = b2;
         x2 = -1;
       }
-      if (x1 >= 0 && x2 < 0) {
-        const int32_t xlen = bcast<E>(R.len, x1);
-        const uint32_t xtoff = bcast<E>(R.toff, x1);
-        shift_all<E, K>(R, x1, INT32_MAX);  // slot x1+1 = copy of x1
-        put<E>(R.len, x1, o1);
-        put<E>(R.len, x1 + 1, xlen - o1);
-        put<E>(R.toff, x1 + 1, xtoff + (uint32_t)o1);
+      if (x1 >= 0) {
+        pa.h = x1;
+        pa.tl = x1 + 1;
+        pa.o = o1;
+        pa.len = bcast<E>(R.len, x1);
+        pa.toff = bcast<E>(R.toff, x1);
+        pa.pos = bb1;
+        t1 = x1;
         n += 1;
-        st[kStWritten] += 2;
-      } else if (x1 >= 0) {
-        const int32_t len1 = bcast<E>(R.len, x1);
-        const uint32_t toff1 = bcast<E>(R.toff, x1);
-        const int32_t len2 = bcast<E>(R.len, x2);
-        const uint32_t toff2 = bcast<E>(R.toff, x2);
-        if (x2 == x1) {  // three pieces of one segment: [0,o1) [o1,o2) [o2,len)
-          shift_all<E, K>(R, x1, x1 + 1);
-          put<E>(R.len, x1, o1);
-          put<E>(R.len, x1 + 1, o2 - o1);
-          put<E>(R.toff, x1 + 1, toff1 + (uint32_t)o1);
-          put<E>(R.len, x1 + 2, len1 - o2);
-          put<E>(R.toff, x1 + 2, toff1 + (uint32_t)o2);
-        } else {  // x1 < x2: tails at x1+1 and x2+2, second head at x2+1
-          shift_all<E, K>(R, x1, x2 + 1);
-          put<E>(R.len, x1, o1);
-          put<E>(R.len, x1 + 1, len1 - o1);
-          put<E>(R.toff, x1 + 1, toff1 + (uint32_t)o1);
-          put<E>(R.len, x2 + 1, o2);
-          put<E>(R.len, x2 + 2, len2 - o2);
-          put<E>(R.toff, x2 + 2, toff2 + (uint32_t)o2);
-        }
-        n += 2;
-        st[kStWritten] += 4;
-      }
-      if (end != start) {
-        // nodeMap (mergeTree.ts:2274-2330): leaves with len > 0 overlapping [start, end)
-        leaf_lengths<E, K>(R, n, r, c, m, newcalc, L);
-        prefix<E>(L, P);
-        bool in[E];
-        unsigned cnt = 0;
-#pragma unroll
-        for (int j2 = 0; j2 < E; j2++) {
-          in[j2] = L[j2] > 0 && P[j2] < end && P[j2] + L[j2] > start;
-          cnt += (unsigned)__popcll(__ballot(in[j2]));
-        }
-        st[kStWritten] += cnt;
-        if (op.type == MTE_OP_REMOVE) {
-          // markRemoved (mergeTree.ts:1924-1962): keep the earliest removedSeq,
-          // add the client to removedClientIds
-          const uint32_t bit = 1u << c;
-#pragma unroll
-          for (int j2 = 0; j2 < E; j2++) {
-            R.rseq[j2] = (in[j2] && R.rseq[j2] == kNone) ? s : R.rseq[j2];
-            R.rmask[j2] = in[j2] ? (R.rmask[j2] | bit) : R.rmask[j2];
-          }
-        } else if (cnt > 0) {
-          // PropertiesManager.addProperties (segmentPropertiesManager.ts:63-151)
-          if (op.flags & MTE_F_REWRITE) {
-#pragma unroll
-            for (int kk = 0; kk < K; kk++)
-#pragma unroll
-              for (int j2 = 0; j2 < E; j2++) R.pr[kk][j2] = in[j2] ? 0u : R.pr[kk][j2];
-          }
-          const uint32_t nw = for_each_prop(op, op.a, a, [&](uint32_t key, uint32_t val) {
-#pragma unroll
-            for (int kk = 0; kk < K; kk++) {
-              if ((uint32_t)kk == key) {
-#pragma unroll
-                for (int j2 = 0; j2 < E; j2++) R.pr[kk][j2] = in[j2] ? val : R.pr[kk][j2];
-              }
-            }
-          });
-          st[kStPwrites] += cnt * nw;
+        D.st[kStWritten] += 2;
+        if (x2 >= 0) {
+          // after the first split the second leaf sits at x2 + 1; when both
+          // boundaries fall in one leaf it is the first split's tail
+          const bool same = x2 == x1;
+          pb.h = x2 + 1;
+          pb.tl = x2 + 2;
+          pb.o = same ? o2 - o1 : o2;
+          pb.len = same ? pa.len - o1 : bcast<E>(R.len, x2);
+          pb.toff = same ? pa.toff + (uint32_t)o1 : bcast<E>(R.toff, x2);
+          pb.pos = b2;
+          t2 = x2 + 1;
+          n += 1;
+          D.st[kStWritten] += 2;
         }
       }
-    } else if (op.type != MTE_OP_NOOP) {
-      reason = MTE_E_INVALID_ARG;
-      break;
     }
 
-    if (op.type != MTE_OP_NOOP) {  // Client.completeAndLogOp (client.ts:525-528)
-      if (!(h.cur_seq < s)) { reason = MTE_E_SEQ_ORDER; k++; break; }
-      if (!(h.min_seq <= op.min_seq)) { reason = MTE_E_MSN_ORDER; k++; break; }
+    // ---- vector apply ----------------------------------------------------
+    if (t1 != INT32_MAX) {
+      if (ins) shift_all<E, K, false>(R, L, P, t1, t2);
+      else shift_all<E, K, true>(R, L, P, t1, t2);
     }
-    if (op.flags & MTE_F_MSG_END) {
-      // updateSeqNumbers (client.ts:937-945) -> setMinSeq (mergeTree.ts:1077-1093)
-      if (!(h.cur_seq <= s)) { reason = MTE_E_SEQ_ORDER; k++; break; }
-      h.cur_seq = s;
-      if (!(op.min_seq <= s)) { reason = MTE_E_MSN_GT_SEQ; k++; break; }
-      if (!(h.min_seq <= op.min_seq)) { reason = MTE_E_MSN_ORDER; k++; break; }
-      if (op.min_seq > h.min_seq) {
-        h.min_seq = op.min_seq;
-        // zamboni: drop tombstones with removedSeq <= minSeq (stream compaction through LDS)
-        bool keep[E];
-        int32_t cntl = 0;
 #pragma unroll
-        for (int j2 = 0; j2 < E; j2++) {
-          keep[j2] = (base + j2 < n) && !(R.rseq[j2] != kNone && R.rseq[j2] <= h.min_seq);
-          cntl += keep[j2] ? 1 : 0;
-        }
-        const int32_t incl = wave_incl_scan(cntl);
-        const int n_new = rdlane(incl, kWave - 1);
-        if (n_new != n) {
-          int32_t dst[E];
-          int32_t d0 = incl - cntl;
+    for (int pi = 0; pi < 2; pi++) {
+      const SplitPatch& p = pi == 0 ? pa : pb;
+      if (p.h >= 0) {
 #pragma unroll
-          for (int j2 = 0; j2 < E; j2++) {
-            dst[j2] = d0;
-            d0 += keep[j2] ? 1 : 0;
-          }
-          auto compact = [&](auto& F) {
-#pragma unroll
-            for (int j2 = 0; j2 < E; j2++)
-              if (keep[j2]) lds[dst[j2]] = (uint32_t)F[j2];
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll
-            for (int j2 = 0; j2 < E; j2++) F[j2] = (std::remove_reference_t<decltype(F[0])>)lds[base + j2];
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-          };
-          compact(R.len);
-          compact(R.seq);
-          compact(R.rseq);
-          compact(R.rmask);
-          compact(R.meta);
-          compact(R.toff);
-#pragma unroll
-          for (int kk = 0; kk < K; kk++) compact(R.pr[kk]);
-          n = n_new;
-          // drop to a smaller register tier once the doc fits in half of it
-          if (E > emin && n + 2 + 16 <= 32 * E) {
-            k++;
-            reason = 1;
-            break;
+        for (int jj = 0; jj < E; jj++) {
+          const bool hd = base + jj == p.h, tl = base + jj == p.tl;
+          R.len[jj] = hd ? p.o : (tl ? p.len - p.o : R.len[jj]);
+          R.toff[jj] = tl ? p.toff + (uint32_t)p.o : R.toff[jj];
+          if (!ins) {
+            L[jj] = hd ? p.o : (tl ? p.len - p.o : L[jj]);
+            P[jj] = tl ? p.pos : P[jj];
           }
         }
+      }
+    }
+    if (g >= 0) {
+      // the new segment (mergeTree.ts:1599-1611, textSegment.ts:40-48,
+      // mergeTreeNodes.ts:602-609)
+      const uint4 q2 = rec[2];
+      const uint32_t meta = uni(q1.w), toff = uni(q1.z), psi = uni(q2.w);
+      uint32_t pr[K > 0 ? K : 1][1];
+      const bool one[1] = {true};
+#pragma unroll
+      for (int kk = 0; kk < (K > 0 ? K : 1); kk++) pr[kk][0] = 0;
+      if (psi != MTE_NO_PROPS) {
+        apply_props<1, K>(pr, one, uni(q2.x), uni(q2.y), uni(q2.z), psi, a);
+        D.st[kStPwrites] += uni(rec[3].x);
+      }
+      if ((meta >> 8) == 0) D.st[kStUnits] += (uint32_t)pos2;
+#pragma unroll
+      for (int jj = 0; jj < E; jj++) {
+        const bool at = base + jj == g;
+        R.len[jj] = at ? pos2 : R.len[jj];
+        R.seq[jj] = at ? s : R.seq[jj];
+        R.rseq[jj] = at ? kNone : R.rseq[jj];
+        R.rmask[jj] = at ? 0u : R.rmask[jj];
+        R.meta[jj] = at ? meta : R.meta[jj];
+        R.toff[jj] = at ? toff : R.toff[jj];
+#pragma unroll
+        for (int kk = 0; kk < K; kk++) R.pr[kk][jj] = at ? pr[kk][0] : R.pr[kk][jj];
+      }
+    }
+    if (!ins && pos2 != pos1) {
+      // nodeMap (mergeTree.ts:2274-2330): after the splits no visible leaf
+      // straddles start or end, so a leaf is in range iff start <= P < end
+      bool in[E];
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int jj = 0; jj < E; jj++) {
+        in[jj] = L[jj] > 0 && P[jj] >= pos1 && P[jj] < pos2;
+        cnt += (uint32_t)__popcll(__ballot(in[jj]));
+      }
+      D.st[kStWritten] += cnt;
+      if (type == MTE_OP_REMOVE) {
+        // markRemoved (mergeTree.ts:1924-1962): keep the earliest removedSeq,
+        // add the client to removedClientIds
+        const uint32_t bit = 1u << c;
+#pragma unroll
+        for (int jj = 0; jj < E; jj++) {
+          R.rseq[jj] = (in[jj] && R.rseq[jj] == kNone) ? s : R.rseq[jj];
+          R.rmask[jj] = in[jj] ? (R.rmask[jj] | bit) : R.rmask[jj];
+        }
+      } else if (cnt > 0) {
+        // PropertiesManager.addProperties (segmentPropertiesManager.ts:63-151)
+        const uint4 q2 = rec[2];
+        if (flags & MTE_F_REWRITE) {
+#pragma unroll
+          for (int kk = 0; kk < K; kk++)
+#pragma unroll
+            for (int jj = 0; jj < E; jj++) R.pr[kk][jj] = in[jj] ? 0u : R.pr[kk][jj];
+        }
+        apply_props<E, K>(R.pr, in, uni(q2.x), uni(q2.y), uni(q2.z), uni(q2.w), a);
+        D.st[kStPwrites] += cnt * uni(rec[3].x);
+      }
+    }
+  } else if (type != MTE_OP_NOOP) {
+    return MTE_E_INVALID_ARG;
+  }
+  D.n = n;
+  D.k++;
+
+  if (type != MTE_OP_NOOP) {  // Client.completeAndLogOp (client.ts:525-528)
+    if (!(D.cur_seq < s)) return MTE_E_SEQ_ORDER;
+    if (!(D.min_seq <= msn)) return MTE_E_MSN_ORDER;
+  }
+  if (flags & MTE_F_MSG_END) {
+    // updateSeqNumbers (client.ts:937-945) -> setMinSeq (mergeTree.ts:1077-1093)
+    if (!(D.cur_seq <= s)) return MTE_E_SEQ_ORDER;
+    D.cur_seq = s;
+    if (!(msn <= s)) return MTE_E_MSN_GT_SEQ;
+    if (!(D.min_seq <= msn)) return MTE_E_MSN_ORDER;
+    if (msn > D.min_seq) {
+      D.min_seq = msn;
+      // zamboni: drop tombstones with removedSeq <= minSeq (padding included)
+      // by a stream compaction staged through LDS
+      bool keep[E];
+      int32_t cntl = 0;
+#pragma unroll
+      for (int jj = 0; jj < E; jj++) {
+        keep[jj] = R.rseq[jj] > msn;
+        cntl += keep[jj] ? 1 : 0;
+      }
+      const int32_t incl = wave_incl_scan(cntl);
+      const int n_new = rdlane(incl, kWave - 1);
+      if (n_new != n) {
+        int32_t dst[E];
+        int32_t d0 = incl - cntl;
+#pragma unroll
+        for (int jj = 0; jj < E; jj++) {
+          dst[jj] = d0;
+          d0 += keep[jj] ? 1 : 0;
+        }
+        compact_plane<E>(R.len, keep, dst, zlds);
+        compact_plane<E>(R.seq, keep, dst, zlds);
+        compact_plane<E>(R.rseq, keep, dst, zlds);
+        compact_plane<E>(R.rmask, keep, dst, zlds);
+        compact_plane<E>(R.meta, keep, dst, zlds);
+        compact_plane<E>(R.toff, keep, dst, zlds);
+#pragma unroll
+        for (int kk = 0; kk < K; kk++) compact_plane<E>(R.pr[kk], keep, dst, zlds);
+#pragma unroll
+        for (int jj = 0; jj < E; jj++) {
+          const bool pad = base + jj >= n_new;
+          R.rseq[jj] = pad ? kPad : R.rseq[jj];
+          R.len[jj] = pad ? 0 : R.len[jj];
+        }
+        D.n = n_new;
+        // drop to a smaller register tier once the doc fits in half of it
+        if (E > emin && n_new + 2 + 16 <= 32 * E) return 1;
       }
     }
   }
-
-  // write back (also on error / escalation)
-#pragma unroll
-  for (int j = 0; j < E; j++) {
-    const uint32_t i = (uint32_t)(base + j);
-    if ((int)i < n) {
-      p_len[i] = R.len[j];
-      p_seq[i] = R.seq[j];
-      p_rseq[i] = R.rseq[j];
-      p_rmask[i] = R.rmask[j];
-      p_meta[i] = R.meta[j];
-      p_toff[i] = R.toff[j];
-#pragma unroll
-      for (int kk = 0; kk < K; kk++) p_props[kk * pstride + i] = R.pr[kk][j];
-    }
-  }
-  h.nseg = n;
-  return reason;
+  return 0;
 }
 
-template <int EMIN, int EMAX, int K, bool LAST>
-__global__ __launch_bounds__(256) void replay_kernel(ReplayArgs a, int pass) {
-  __shared__ uint32_t lds_all[kDocsPerBlock][kWave * EMAX];
-  // wave index: uniform by construction; readfirstlane tells the compiler, so
-  // every doc-derived value (header, pointers, op cursor) lives in SGPRs
+__device__ __forceinline__ void run_init(DocRun& D, const ReplayArgs& a, int doc, bool escalated_only, uint4* stage) {
+  D.doc = doc;
+  D.running = false;
+  D.stage = stage;
+#pragma unroll
+  for (int t = 0; t < kNumStats; t++) D.st[t] = 0;
+  D.n = 0;
+  D.status = 0;
+  D.k = D.k1 = 0;
+  if (doc < 0) return;
+  const DocHdr h = a.hdr[doc];
+  const uint64_t kb = a.op_off[doc];
+  D.n = h.nseg;
+  D.min_seq = h.min_seq;
+  D.cur_seq = h.cur_seq;
+  D.status = h.status;
+  D.flags = h.flags;
+  D.recp = a.recs + 4 * kb;
+  D.k = h.resume;
+  D.k1 = (uint32_t)(a.op_off[doc + 1] - kb);
+  if (h.status != 0) return;
+  if (escalated_only && !(h.flags & kHdrNeedsEsc)) return;
+  D.flags &= ~kHdrNeedsEsc;
+  D.running = D.k < D.k1;
+  if (D.running) stage_begin(D, a);
+}
+
+// add the 32-bit per-doc counters into the doc's 64-bit stats in HBM
+__device__ __forceinline__ void run_flush_stats(DocRun& D, const ReplayArgs& a) {
+  if (D.doc >= 0 && lane_id() == 0) {
+    unsigned long long* sd = a.stats + (size_t)D.doc * kNumStats;
+#pragma unroll
+    for (int t = 0; t < kNumStats; t++) {
+      if (t == kStMaxSegs) sd[t] = sd[t] > D.st[t] ? sd[t] : D.st[t];
+      else sd[t] += D.st[t];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < kNumStats; t++) D.st[t] = 0;
+}
+
+__device__ __forceinline__ void run_finish(DocRun& D, const ReplayArgs& a) {
+  if (D.doc < 0) return;
+  if (lane_id() == 0) {
+    DocHdr h;
+    h.nseg = D.n;
+    h.min_seq = D.min_seq;
+    h.cur_seq = D.cur_seq;
+    h.status = D.status;
+    h.flags = D.flags;
+    h.resume = D.k;
+    h.pad0 = h.pad1 = 0;
+    a.hdr[D.doc] = h;
+  }
+}
+
+// handle a doc_step result: 0 keep going, otherwise the doc leaves the loop
+__device__ __forceinline__ bool step_done(DocRun& D, int rc) {
+  if (rc < 0) {
+    D.status = rc;
+    D.running = false;
+    return true;
+  }
+  if (D.k >= D.k1) D.running = false;
+  return rc != 0 || !D.running;
+}
+
+// One burst of up to `limit` ops of one document at register tier E: load
+// its segments into VGPRs, replay, write them back.  Returns early when the
+// document needs another tier or stops.
+template <int E, int K>
+__device__ __forceinline__ void burst_run(DocRun& D, const ReplayArgs& a, uint32_t* zlds, int emin, uint32_t limit) {
+  Regs<E, K> R;
+  load_regs<E, K>(R, D, a);
+  const uint32_t kend = D.k1 - D.k > limit ? D.k + limit : D.k1;
+  while (D.running) {
+    const int rc = doc_step<E, K>(R, D, a, zlds, emin);
+    if (step_done(D, rc) || D.k >= kend) break;
+  }
+  store_regs<E, K>(R, D, a);
+  run_flush_stats(D, a);
+}
+
+// tier for the next burst in pass 1 (E <= 4, 254 segments); larger documents
+// continue in pass 2
+__device__ __forceinline__ int pick_pass1_tier(DocRun& D, uint32_t cap) {
+  if (D.n + 2 > (int)cap) {
+    D.status = MTE_E_CAPACITY;
+    D.running = false;
+    return 0;
+  }
+  if (D.n + 2 <= kWave) return 1;
+  if (D.n + 2 <= 2 * kWave) return 2;
+  if (MTE_PASS1_EMAX >= 4 && D.n + 2 <= 4 * kWave) return 4;
+  D.flags |= kHdrNeedsEsc;  // continue in the big-doc pass
+  D.running = false;
+  return 0;
+}
+
+template <int K>
+__device__ __forceinline__ void pass1_burst(DocRun& D, const ReplayArgs& a, uint32_t* zlds) {
+  const int e = pick_pass1_tier(D, a.cap);
+  if (e == 1) burst_run<1, K>(D, a, zlds, 1, kBurst);
+  else if (e == 2) burst_run<2, K>(D, a, zlds, 1, kBurst);
+  else if constexpr (MTE_PASS1_EMAX >= 4) {
+    if (e == 4) burst_run<4, K>(D, a, zlds, 1, kBurst);
+  }
+}
+
+// pass 1: two documents per wavefront, replayed in alternating bursts, so a
+// 10k-document batch is resident on the chip at once with the register
+// budget of one document (E <= 4)
+template <int K>
+__global__ __launch_bounds__(256, MTE_PAIR_WAVES) void pair_kernel(ReplayArgs a) {
+  __shared__ uint4 stage_all[kPairsPerBlock][2][2 * 4 * kChunk];
+  __shared__ uint32_t zlds_all[kPairsPerBlock][kWave * 4];
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+  const int pair = (int)blockIdx.x * kPairsPerBlock + w;
+  if (pair >= (int)a.n_pairs) return;
+  const int da = (int)a.pair_docs[2 * pair], db = (int)a.pair_docs[2 * pair + 1];
+  DocRun A, B;
+  run_init(A, a, da, false, stage_all[w][0]);
+  run_init(B, a, db == da ? -1 : db, false, stage_all[w][1]);
+  uint32_t* zlds = zlds_all[w];
+  while (A.running || B.running) {
+    if (A.running) pass1_burst<K>(A, a, zlds);
+    if (B.running) pass1_burst<K>(B, a, zlds);
+  }
+  run_finish(A, a);
+  run_finish(B, a);
+}
+
+template <int E, int K>
+__device__ __forceinline__ void single_run(DocRun& D, const ReplayArgs& a, uint32_t* zlds) {
+  Regs<E, K> R;
+  load_regs<E, K>(R, D, a);
+  while (D.running) {
+    const int rc = doc_step<E, K>(R, D, a, zlds, 4);
+    if (step_done(D, rc)) break;
+  }
+  store_regs<E, K>(R, D, a);
+  run_flush_stats(D, a);
+}
+
+// pass 2: one document per wavefront, for the documents pass 1 escalated
+template <int K>
+__global__ __launch_bounds__(256) void big_kernel(ReplayArgs a) {
+  __shared__ uint4 stage_all[kDocsPerBlock][2 * 4 * kChunk];
+  __shared__ uint32_t zlds_all[kDocsPerBlock][kWave * 16];
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
   const int doc = (int)blockIdx.x * kDocsPerBlock + w;
   if (doc >= (int)a.n_docs) return;
-  uint32_t* lds = lds_all[w];
-  DocHdr h = a.hdr[doc];
-  if (h.status != 0) return;
-  if (pass > 0 && !(h.flags & kHdrNeedsEsc)) return;
-  h.flags &= ~kHdrNeedsEsc;
-  const uint64_t kb = a.op_off[doc];
-  uint64_t k = kb + h.resume;
-  const uint64_t k1 = a.op_off[doc + 1];
-  unsigned long long st[kNumStats] = {0, 0, 0, 0, 0, 0};
-  while (k < k1) {
-    const int n = h.nseg;
-    int E = 0;
-    if (EMIN <= 1 && EMAX >= 1 && n + 2 <= kWave * 1) E = 1;
-    else if (EMIN <= 2 && EMAX >= 2 && n + 2 <= kWave * 2) E = 2;
-    else if (EMIN <= 4 && EMAX >= 4 && n + 2 <= kWave * 4) E = 4;
-    else if (EMIN <= 8 && EMAX >= 8 && n + 2 <= kWave * 8) E = 8;
-    else if (EMIN <= 16 && EMAX >= 16 && n + 2 <= kWave * 16) E = 16;
-    if (E == 0 || n + 2 > (int)a.cap) {
-      if (LAST || n + 2 > (int)a.cap) h.status = MTE_E_CAPACITY;
-      else h.flags |= kHdrNeedsEsc;
+  DocRun D;
+  run_init(D, a, doc, true, stage_all[w]);
+  if (!D.running && !(a.hdr[doc].flags & kHdrNeedsEsc)) return;  // untouched doc: leave the header alone
+  uint32_t* zlds = zlds_all[w];
+  while (D.running) {
+    const int n = D.n;
+    if (n + 2 > (int)a.cap || n + 2 > 16 * kWave) {
+      D.status = MTE_E_CAPACITY;
       break;
     }
-    int rc = 0;
-    uint32_t s32[kNumStats] = {0, 0, 0, 0, 0, 0};
-    if constexpr (EMIN <= 1 && EMAX >= 1) if (E == 1) rc = run_ops<1, K>(a, doc, h, k, k1, EMIN, lds, s32);
-    if constexpr (EMIN <= 2 && EMAX >= 2) if (E == 2) rc = run_ops<2, K>(a, doc, h, k, k1, EMIN, lds, s32);
-    if constexpr (EMIN <= 4 && EMAX >= 4) if (E == 4) rc = run_ops<4, K>(a, doc, h, k, k1, EMIN, lds, s32);
-    if constexpr (EMIN <= 8 && EMAX >= 8) if (E == 8) rc = run_ops<8, K>(a, doc, h, k, k1, EMIN, lds, s32);
-    if constexpr (EMIN <= 16 && EMAX >= 16) if (E == 16) rc = run_ops<16, K>(a, doc, h, k, k1, EMIN, lds, s32);
-#pragma unroll
-    for (int t = 0; t < kNumStats; t++) {
-      if (t == kStMaxSegs) st[t] = st[t] > s32[t] ? st[t] : s32[t];
-      else st[t] += s32[t];
-    }
-    if (rc < 0) {
-      h.status = rc;
-      break;
-    }
+    if (n + 2 <= 4 * kWave) single_run<4, K>(D, a, zlds);
+    else if (n + 2 <= 8 * kWave) single_run<8, K>(D, a, zlds);
+    else single_run<16, K>(D, a, zlds);
   }
-  h.resume = (uint32_t)(k - kb);
-  if (lane_id() == 0) {
-    a.hdr[doc] = h;
-    unsigned long long* sd = a.stats + (size_t)doc * kNumStats;
-#pragma unroll
-    for (int t = 0; t < kNumStats; t++) {
-      if (t == kStMaxSegs) sd[t] = sd[t] > st[t] ? sd[t] : st[t];
-      else sd[t] += st[t];
-    }
-  }
+  run_finish(D, a);
 }
 
 }  // namespace mte

@@ -38,7 +38,7 @@ def main():
     which = sys.argv[1:] or ["all"]
     base3 = gen.generate(3, n_docs=10000, ops_per_doc=2000)
     if "all" in which or "scale" in which:
-        for nd in (256, 1024, 2048, 4096, 10000):
+        for nd in (256, 4096, 10000):
             run(f"cfg3 docs={nd}", gen.slice_docs(base3, 0, nd))
     if "all" in which or "noop" in which:
         s = gen.slice_docs(base3, 0, 10000)
