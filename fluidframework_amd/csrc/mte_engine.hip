@@ -59,12 +59,12 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
 // kernels stage through LDS (mte_kernels.h): insert text offsets rebased onto
 // the ctx arena, the new segment's meta word, and the first two property
 // entries of the op's propset inlined.  Runs once per mte_submit, one thread
-// per record; 2 chunks of NOOP padding follow the last record.
+// per record; kRecPad NOOP records follow the last one.
 __global__ void compile_kernel(const mte_op* __restrict__ ops, uint64_t n_ops, const mte_propset* __restrict__ ps,
                                const mte_prop* __restrict__ pe, uint32_t n_keys, uint32_t text_base,
                                uint4* __restrict__ recs) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_ops + 2 * kChunk) return;
+  if (i >= n_ops + kRecPad) return;
   uint32_t w[16] = {0, 0, 0, MTE_OP_NOOP, 0, 0, 0, 0, kNoKey | (kNoKey << 8), 0, 0, MTE_NO_PROPS, 0, 0, 0, 0};
   if (i < n_ops) {
     const mte_op o = ops[i];
@@ -81,6 +81,7 @@ __global__ void compile_kernel(const mte_op* __restrict__ ops, uint64_t n_ops, c
       w[6] = marker ? 0u : text_base + o.a;
       w[7] = ((uint32_t)o.client + 1u) | ((marker ? 1u + (uint32_t)o.pos2 : 0u) << 8);
       psi = o.b;
+      if (psi != MTE_NO_PROPS) w[3] |= kFlagHasProps << 16;
     } else if (o.type == MTE_OP_ANNOTATE) {
       psi = o.a;
     }
@@ -546,9 +547,9 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
   if (b->n_props)
     HIPCHK(c, hipMemcpyAsync(c->d_pe, b->props, b->n_props * sizeof(mte_prop), hipMemcpyHostToDevice, c->stream));
   // compile the records (one pass over the batch, HBM-bound)
-  if ((rc = grow(c, &c->d_recs, &c->recs_cap, 4 * (b->n_ops + 2 * kChunk)))) return rc;
+  if ((rc = grow(c, &c->d_recs, &c->recs_cap, 4 * (b->n_ops + kRecPad)))) return rc;
   {
-    const uint64_t nthr = b->n_ops + 2 * kChunk;
+    const uint64_t nthr = b->n_ops + kRecPad;
     hipLaunchKernelGGL(compile_kernel, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, c->stream, c->d_ops,
                        b->n_ops, c->d_ps, c->d_pe, c->n_keys, c->batch_text_base, c->d_recs);
     HIPCHK(c, hipGetLastError());

@@ -60,8 +60,10 @@ struct SegSoA {
 // w7 insert: meta of the new segment | w8 k0 | k1 << 8 | (count > 2) << 16 (key 0xff = none)
 // w9 v0 | w10 v1 | w11 propset index (MTE_NO_PROPS) | w12 keys < n_keys in the set | w13-15 0
 constexpr int kRecWords = 16;
-constexpr int kChunk = 16;  // records per LDS staging chunk (1 KiB: one dwordx4 per lane)
 constexpr uint32_t kNoKey = 0xffu;
+constexpr uint32_t kRecPad = 128;  // NOOP records after the last one (prefetch reads run ahead)
+// internal op flag (high bit of mte_op.flags, set by compile_kernel): insert with props
+constexpr uint32_t kFlagHasProps = 0x8000u;
 
 struct ReplayArgs {
   DocHdr* hdr;

@@ -9,10 +9,10 @@
 //                  (<= 1022 segments), for documents pass 1 escalated.
 //
 // Both run the same per-op step (doc_step) on a register-resident document.
-// Op records (64 B compiled records, mte_kernels.h) are staged through LDS in
-// 1 KiB chunks of 16, double-buffered: the next chunk's global load is issued
-// when a chunk starts and written to LDS half-way through it, so the per-op
-// read is three LDS broadcast reads.
+// Op records (64 B compiled records, mte_kernels.h) are read with scalar
+// loads straight into SGPRs (the op index is wave-uniform): the next op's
+// first 32 bytes are in flight while the current op runs, and every 64 ops a
+// vector load touches the next 64 records so the scalar loads hit L2.
 #pragma once
 
 #include <type_traits>
@@ -34,8 +34,8 @@ namespace mte {
 
 constexpr uint32_t kBurst = MTE_BURST;  // ops per burst in pass 1
 
-// per-document replay state (wave-uniform except the in-flight chunk `sv`);
-// op cursors are 32-bit, relative to the document's first record of the batch
+// per-document replay state (wave-uniform); op cursors are 32-bit, relative
+// to the document's first record of the batch
 struct DocRun {
   int doc;
   int n;
@@ -45,11 +45,6 @@ struct DocRun {
   bool running;
   const uint4* recp;  // the doc's first compiled record (4 x uint4 each)
   uint32_t k, k1;     // current op, end
-  uint32_t cbase;     // first record of the current LDS chunk
-  int par;            // LDS buffer holding the current chunk
-  uint4* stage;       // LDS: 2 chunks x 16 records x 4 uint4
-  uint4 sv;           // next chunk (in flight), one uint4 per lane
-  uint32_t st[kNumStats];
 };
 
 __device__ __forceinline__ void fence_wave() {
@@ -57,14 +52,25 @@ __device__ __forceinline__ void fence_wave() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// start staging at record D.k: chunk 0 synchronously, chunk 1 in flight
-__device__ __forceinline__ void stage_begin(DocRun& D, const ReplayArgs& a) {
-  const int l = lane_id();
-  D.cbase = D.k;
-  D.par = 0;
-  D.stage[l] = D.recp[4 * D.cbase + (uint32_t)l];
-  D.sv = D.recp[4 * (D.cbase + kChunk) + (uint32_t)l];
-  fence_wave();
+// ---- scalar op fetch -------------------------------------------------------
+// Records are read through the constant address space: the op index is
+// wave-uniform, so the compiler emits s_load straight into SGPRs (no vector
+// load, no readfirstlane) and tracks the lgkmcnt wait itself.  The records
+// are never written while a replay kernel runs.
+typedef int32_t s8v __attribute__((ext_vector_type(8)));
+typedef const __attribute__((address_space(4))) s8v* cs8p;
+
+__device__ __forceinline__ s8v sload8(const uint4* p) { return *(cs8p)(const void*)p; }
+__device__ __forceinline__ s8v sload8_props(const uint4* p) { return *(cs8p)(const void*)(p + 2); }  // words 8..15
+__device__ __forceinline__ void swait(s8v&) {}
+
+// L2 prefetch: lane l touches record `from + l` (one 64-B line each).  The
+// loaded word is folded into `sink` one prefetch later (64 ops on), so the
+// wait for it never stalls.
+__device__ __forceinline__ void touch_records(const DocRun& D, uint32_t from, uint32_t& pending, uint32_t& sink) {
+  sink ^= pending;
+  const uint32_t r = from + (uint32_t)lane_id();
+  pending = r < D.k1 + 64 ? reinterpret_cast<const uint32_t*>(D.recp + 4 * r)[0] : 0u;
 }
 
 // ISegment.addProperties for a remote op (segmentPropertiesManager.ts:63-151):
@@ -208,40 +214,31 @@ struct SplitPatch {
 // patches) followed by ONE vector apply phase shared by all op types, so the
 // register state flows through a single path (no per-branch copies).
 template <int E, int K>
-__device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, const ReplayArgs& a, uint32_t* zlds, int emin) {
+__device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)[kNumStats], s8v& cur,
+                                        const ReplayArgs& a, uint32_t* zlds, int emin) {
   const int l = lane_id();
   const int base = l * E;
   const int lim = kWave * E < (int)a.cap ? kWave * E : (int)a.cap;
-  if (D.n + 2 > lim || D.st[kStOps] >= (1u << 20)) return 1;
+  if (D.n + 2 > lim || st[kStOps] >= (1u << 20)) return 1;
 
-  // ---- op record from the LDS stage --------------------------------------
-  int j = (int)(D.k - D.cbase);
-  if (j == kChunk) {
-    D.cbase += kChunk;
-    D.par ^= 1;
-    j = 0;
-    D.sv = D.recp[4 * (D.cbase + kChunk) + (uint32_t)l];  // chunk after next, in flight
-  }
-  if (j == kChunk / 2) {
-    D.stage[(D.par ^ 1) * 4 * kChunk + l] = D.sv;  // next chunk -> the other buffer
-    fence_wave();
-  }
-  const uint4* rec = D.stage + D.par * 4 * kChunk + 4 * j;
-  const uint4 q0 = rec[0], q1 = rec[1];
-  const uint32_t w3 = uni(q0.w);
+  // ---- op record: words 0..7 were prefetched into `cur` -------------------
+  const s8v op = cur;
+  const uint4* rec = D.recp + 4 * D.k;
+  if (D.k + 1 < D.k1) cur = sload8(rec + 4);  // next op, in flight during this one
+  const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
-  D.st[kStOps]++;
-  D.st[kStMaxSegs] = (uint32_t)D.n > D.st[kStMaxSegs] ? (uint32_t)D.n : D.st[kStMaxSegs];
-  const int32_t s = uni((int32_t)q0.x);
-  const int32_t msn = uni((int32_t)q0.z);
+  st[kStOps]++;
+  st[kStMaxSegs] = (uint32_t)D.n > st[kStMaxSegs] ? (uint32_t)D.n : st[kStMaxSegs];
+  const int32_t s = op[0];
+  const int32_t msn = op[2];
   int n = D.n;
 
   if (type == MTE_OP_INSERT || type == MTE_OP_REMOVE || type == MTE_OP_ANNOTATE) {
     const bool ins = type == MTE_OP_INSERT;
-    D.st[kStScanned] += (uint32_t)n;
-    const int32_t r = uni((int32_t)q0.y);
-    const int32_t pos1 = uni((int32_t)q1.x), pos2 = uni((int32_t)q1.y);
+    st[kStScanned] += (uint32_t)n;
+    const int32_t r = op[1];
+    const int32_t pos1 = op[4], pos2 = op[5];
     int32_t L[E], P[E];
     leaf_lengths<E, K>(R, r, c + 1, (int)c, D.min_seq, (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0, L);
     const int32_t total = prefix<E>(L, P);
@@ -266,10 +263,10 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, const ReplayAr
           t2 = xs + 1;
           g = xs + 1;
           pa.tl = xs + 2;
-          D.st[kStWritten] += 3;
+          st[kStWritten] += 3;
         } else {
           pa.tl = xs + 1;
-          D.st[kStWritten] += 2;
+          st[kStWritten] += 2;
         }
         n += 1;
       } else if (nlen > 0) {
@@ -279,7 +276,7 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, const ReplayAr
           g = n;
         }
         t1 = g - 1;
-        D.st[kStWritten] += 1;
+        st[kStWritten] += 1;
       }
       if (nlen > 0) n += 1;
     } else {
@@ -305,7 +302,7 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, const ReplayAr
         pa.pos = bb1;
         t1 = x1;
         n += 1;
-        D.st[kStWritten] += 2;
+        st[kStWritten] += 2;
         if (x2 >= 0) {
           // after the first split the second leaf sits at x2 + 1; when both
           // boundaries fall in one leaf it is the first split's tail
@@ -318,7 +315,7 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, const ReplayAr
           pb.pos = b2;
           t2 = x2 + 1;
           n += 1;
-          D.st[kStWritten] += 2;
+          st[kStWritten] += 2;
         }
       }
     }
@@ -347,17 +344,17 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, const ReplayAr
     if (g >= 0) {
       // the new segment (mergeTree.ts:1599-1611, textSegment.ts:40-48,
       // mergeTreeNodes.ts:602-609)
-      const uint4 q2 = rec[2];
-      const uint32_t meta = uni(q1.w), toff = uni(q1.z), psi = uni(q2.w);
+      const uint32_t meta = (uint32_t)op[7], toff = (uint32_t)op[6];
       uint32_t pr[K > 0 ? K : 1][1];
       const bool one[1] = {true};
 #pragma unroll
       for (int kk = 0; kk < (K > 0 ? K : 1); kk++) pr[kk][0] = 0;
-      if (psi != MTE_NO_PROPS) {
-        apply_props<1, K>(pr, one, uni(q2.x), uni(q2.y), uni(q2.z), psi, a);
-        D.st[kStPwrites] += uni(rec[3].x);
+      if (K > 0 && (flags & kFlagHasProps)) {
+        const s8v q2 = sload8_props(rec);  // same 64-B line as `op`: a scalar-cache hit
+        apply_props<1, K>(pr, one, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], (uint32_t)q2[3], a);
+        st[kStPwrites] += (uint32_t)q2[4];
       }
-      if ((meta >> 8) == 0) D.st[kStUnits] += (uint32_t)pos2;
+      if ((meta >> 8) == 0) st[kStUnits] += (uint32_t)pos2;
 #pragma unroll
       for (int jj = 0; jj < E; jj++) {
         const bool at = base + jj == g;
@@ -381,7 +378,7 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, const ReplayAr
         in[jj] = L[jj] > 0 && P[jj] >= pos1 && P[jj] < pos2;
         cnt += (uint32_t)__popcll(__ballot(in[jj]));
       }
-      D.st[kStWritten] += cnt;
+      st[kStWritten] += cnt;
       if (type == MTE_OP_REMOVE) {
         // markRemoved (mergeTree.ts:1924-1962): keep the earliest removedSeq,
         // add the client to removedClientIds
@@ -393,15 +390,15 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, const ReplayAr
         }
       } else if (cnt > 0) {
         // PropertiesManager.addProperties (segmentPropertiesManager.ts:63-151)
-        const uint4 q2 = rec[2];
+        const s8v q2 = sload8_props(rec);
         if (flags & MTE_F_REWRITE) {
 #pragma unroll
           for (int kk = 0; kk < K; kk++)
 #pragma unroll
             for (int jj = 0; jj < E; jj++) R.pr[kk][jj] = in[jj] ? 0u : R.pr[kk][jj];
         }
-        apply_props<E, K>(R.pr, in, uni(q2.x), uni(q2.y), uni(q2.z), uni(q2.w), a);
-        D.st[kStPwrites] += cnt * uni(rec[3].x);
+        apply_props<E, K>(R.pr, in, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], (uint32_t)q2[3], a);
+        st[kStPwrites] += cnt * (uint32_t)q2[4];
       }
     }
   } else if (type != MTE_OP_NOOP) {
@@ -464,12 +461,9 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, const ReplayAr
   return 0;
 }
 
-__device__ __forceinline__ void run_init(DocRun& D, const ReplayArgs& a, int doc, bool escalated_only, uint4* stage) {
+__device__ __forceinline__ void run_init(DocRun& D, const ReplayArgs& a, int doc, bool escalated_only) {
   D.doc = doc;
   D.running = false;
-  D.stage = stage;
-#pragma unroll
-  for (int t = 0; t < kNumStats; t++) D.st[t] = 0;
   D.n = 0;
   D.status = 0;
   D.k = D.k1 = 0;
@@ -488,21 +482,20 @@ __device__ __forceinline__ void run_init(DocRun& D, const ReplayArgs& a, int doc
   if (escalated_only && !(h.flags & kHdrNeedsEsc)) return;
   D.flags &= ~kHdrNeedsEsc;
   D.running = D.k < D.k1;
-  if (D.running) stage_begin(D, a);
 }
 
 // add the 32-bit per-doc counters into the doc's 64-bit stats in HBM
-__device__ __forceinline__ void run_flush_stats(DocRun& D, const ReplayArgs& a) {
+__device__ __forceinline__ void run_flush_stats(const DocRun& D, uint32_t (&st)[kNumStats], const ReplayArgs& a) {
   if (D.doc >= 0 && lane_id() == 0) {
     unsigned long long* sd = a.stats + (size_t)D.doc * kNumStats;
 #pragma unroll
     for (int t = 0; t < kNumStats; t++) {
-      if (t == kStMaxSegs) sd[t] = sd[t] > D.st[t] ? sd[t] : D.st[t];
-      else sd[t] += D.st[t];
+      if (t == kStMaxSegs) sd[t] = sd[t] > st[t] ? sd[t] : st[t];
+      else sd[t] += st[t];
     }
   }
 #pragma unroll
-  for (int t = 0; t < kNumStats; t++) D.st[t] = 0;
+  for (int t = 0; t < kNumStats; t++) st[t] = 0;
 }
 
 __device__ __forceinline__ void run_finish(DocRun& D, const ReplayArgs& a) {
@@ -537,14 +530,22 @@ __device__ __forceinline__ bool step_done(DocRun& D, int rc) {
 template <int E, int K>
 __device__ __forceinline__ void burst_run(DocRun& D, const ReplayArgs& a, uint32_t* zlds, int emin, uint32_t limit) {
   Regs<E, K> R;
+  uint32_t st[kNumStats] = {0, 0, 0, 0, 0, 0};
   load_regs<E, K>(R, D, a);
   const uint32_t kend = D.k1 - D.k > limit ? D.k + limit : D.k1;
+  s8v cur = sload8(D.recp + 4 * D.k);
+  uint32_t pending = 0, sink = 0;
+  touch_records(D, D.k + 16, pending, sink);
   while (D.running) {
-    const int rc = doc_step<E, K>(R, D, a, zlds, emin);
+    if ((D.k & 63u) == 0) touch_records(D, D.k + 64, pending, sink);
+    const int rc = doc_step<E, K>(R, D, st, cur, a, zlds, emin);
     if (step_done(D, rc) || D.k >= kend) break;
   }
+  swait(cur);  // no scalar load may be left in flight
   store_regs<E, K>(R, D, a);
-  run_flush_stats(D, a);
+  run_flush_stats(D, st, a);
+  sink ^= pending;
+  if (sink == 0x9e3779b9u && D.doc < 0) a.stats[0] = sink;  // keeps the prefetch loads alive
 }
 
 // tier for the next burst in pass 1 (E <= 4, 254 segments); larger documents
@@ -573,51 +574,84 @@ __device__ __forceinline__ void pass1_burst(DocRun& D, const ReplayArgs& a, uint
   }
 }
 
+// DocRun <-> a DocHdr image in LDS (pass 1 keeps both documents of a pair
+// there between bursts, so only the running document's state occupies SGPRs)
+__device__ __forceinline__ bool run_from_lds(DocRun& D, const DocHdr* hl, int doc, const ReplayArgs& a) {
+  const uint4 h0 = reinterpret_cast<const uint4*>(hl)[0], h1 = reinterpret_cast<const uint4*>(hl)[1];
+  D.doc = doc;
+  D.n = uni((int32_t)h0.x);
+  D.min_seq = uni((int32_t)h0.y);
+  D.cur_seq = uni((int32_t)h0.z);
+  D.status = uni((int32_t)h0.w);
+  D.flags = uni(h1.x);
+  D.k = uni(h1.y);
+  const uint64_t kb = a.op_off[doc];
+  D.recp = a.recs + 4 * kb;
+  D.k1 = (uint32_t)(a.op_off[doc + 1] - kb);
+  D.running = D.status == 0 && D.k < D.k1 && !(D.flags & kHdrNeedsEsc);
+  return D.running;
+}
+
+__device__ __forceinline__ void run_to_lds(const DocRun& D, DocHdr* hl) {
+  if (lane_id() == 0) {
+    uint4* p = reinterpret_cast<uint4*>(hl);
+    p[0] = make_uint4((uint32_t)D.n, (uint32_t)D.min_seq, (uint32_t)D.cur_seq, (uint32_t)D.status);
+    p[1] = make_uint4(D.flags, D.k, 0u, 0u);
+  }
+  fence_wave();
+}
+
 // pass 1: two documents per wavefront, replayed in alternating bursts, so a
 // 10k-document batch is resident on the chip at once with the register
 // budget of one document (E <= 4)
 template <int K>
 __global__ __launch_bounds__(256, MTE_PAIR_WAVES) void pair_kernel(ReplayArgs a) {
-  __shared__ uint4 stage_all[kPairsPerBlock][2][2 * 4 * kChunk];
   __shared__ uint32_t zlds_all[kPairsPerBlock][kWave * 4];
+  __shared__ DocHdr hl_all[kPairsPerBlock][2];
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
   const int pair = (int)blockIdx.x * kPairsPerBlock + w;
   if (pair >= (int)a.n_pairs) return;
-  const int da = (int)a.pair_docs[2 * pair], db = (int)a.pair_docs[2 * pair + 1];
-  DocRun A, B;
-  run_init(A, a, da, false, stage_all[w][0]);
-  run_init(B, a, db == da ? -1 : db, false, stage_all[w][1]);
+  int docs[2] = {(int)a.pair_docs[2 * pair], (int)a.pair_docs[2 * pair + 1]};
+  if (docs[1] == docs[0]) docs[1] = -1;
+  DocHdr* hl = hl_all[w];
   uint32_t* zlds = zlds_all[w];
-  while (A.running || B.running) {
-    if (A.running) pass1_burst<K>(A, a, zlds);
-    if (B.running) pass1_burst<K>(B, a, zlds);
+  uint32_t live = 0;  // bit t: document t still has ops to run in this pass
+#pragma unroll
+  for (int t = 0; t < 2; t++) {
+    if (docs[t] >= 0) {
+      DocHdr h = a.hdr[docs[t]];
+      h.flags &= ~kHdrNeedsEsc;
+      if (lane_id() == 0) hl[t] = h;
+      live |= 1u << t;
+    }
   }
-  run_finish(A, a);
-  run_finish(B, a);
-}
-
-template <int E, int K>
-__device__ __forceinline__ void single_run(DocRun& D, const ReplayArgs& a, uint32_t* zlds) {
-  Regs<E, K> R;
-  load_regs<E, K>(R, D, a);
-  while (D.running) {
-    const int rc = doc_step<E, K>(R, D, a, zlds, 4);
-    if (step_done(D, rc)) break;
+  fence_wave();
+  // one burst per iteration, alternating between the two documents; a single
+  // copy of the burst code serves both (the document is a runtime index)
+  for (int t = 0; live; t ^= 1) {
+    if (!(live & (1u << t))) continue;
+    const int doc = t ? docs[1] : docs[0];
+    DocRun D;
+    if (run_from_lds(D, &hl[t], doc, a)) pass1_burst<K>(D, a, zlds);
+    run_to_lds(D, &hl[t]);
+    if (!D.running) live &= ~(1u << t);
   }
-  store_regs<E, K>(R, D, a);
-  run_flush_stats(D, a);
+  if (lane_id() == 0) {
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+      if (docs[t] >= 0) a.hdr[docs[t]] = hl[t];  // resume = the op cursor
+  }
 }
 
 // pass 2: one document per wavefront, for the documents pass 1 escalated
 template <int K>
 __global__ __launch_bounds__(256) void big_kernel(ReplayArgs a) {
-  __shared__ uint4 stage_all[kDocsPerBlock][2 * 4 * kChunk];
   __shared__ uint32_t zlds_all[kDocsPerBlock][kWave * 16];
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
   const int doc = (int)blockIdx.x * kDocsPerBlock + w;
   if (doc >= (int)a.n_docs) return;
   DocRun D;
-  run_init(D, a, doc, true, stage_all[w]);
+  run_init(D, a, doc, true);
   if (!D.running && !(a.hdr[doc].flags & kHdrNeedsEsc)) return;  // untouched doc: leave the header alone
   uint32_t* zlds = zlds_all[w];
   while (D.running) {
@@ -626,9 +660,9 @@ __global__ __launch_bounds__(256) void big_kernel(ReplayArgs a) {
       D.status = MTE_E_CAPACITY;
       break;
     }
-    if (n + 2 <= 4 * kWave) single_run<4, K>(D, a, zlds);
-    else if (n + 2 <= 8 * kWave) single_run<8, K>(D, a, zlds);
-    else single_run<16, K>(D, a, zlds);
+    if (n + 2 <= 4 * kWave) burst_run<4, K>(D, a, zlds, 4, 0xffffffffu);
+    else if (n + 2 <= 8 * kWave) burst_run<8, K>(D, a, zlds, 4, 0xffffffffu);
+    else burst_run<16, K>(D, a, zlds, 4, 0xffffffffu);
   }
   run_finish(D, a);
 }
