@@ -14,6 +14,7 @@
 
 #include "mte_kernels.h"
 #include "mte_replay.h"
+#include "mte_stream.h"
 
 using namespace mte;
 
@@ -347,6 +348,9 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   // pass 2: docs that outgrew pass 1 continue one per wavefront (up to 1022 segments)
   const uint32_t b2 = (c->n_docs + kDocsPerBlock - 1) / kDocsPerBlock;
   hipLaunchKernelGGL((big_kernel<K>), dim3(b2), dim3(256), 0, c->stream, a);
+  HIPCHK(c, hipGetLastError());
+  // pass 3: larger docs (up to the ctx capacity), HBM-resident, streamed per op
+  hipLaunchKernelGGL((stream_kernel<K>), dim3(b2), dim3(256), 0, c->stream, a);
   HIPCHK(c, hipGetLastError());
   return MTE_OK;
 }

@@ -7,6 +7,7 @@
 //                  need 10k resident waves; the chip holds 8 per SIMD).
 //   big_kernel   — pass 2: one document per wavefront, E in {4, 8, 16}
 //                  (<= 1022 segments), for documents pass 1 escalated.
+//   stream_kernel — pass 3 (mte_stream.h): larger documents, HBM-resident.
 //
 // Both run the same per-op step (doc_step) on a register-resident document.
 // Op records (64 B compiled records, mte_kernels.h) are read with scalar
@@ -656,8 +657,12 @@ __global__ __launch_bounds__(256) void big_kernel(ReplayArgs a) {
   uint32_t* zlds = zlds_all[w];
   while (D.running) {
     const int n = D.n;
-    if (n + 2 > (int)a.cap || n + 2 > 16 * kWave) {
+    if (n + 2 > (int)a.cap) {
       D.status = MTE_E_CAPACITY;
+      break;
+    }
+    if (n + 2 > 16 * kWave) {  // beyond the register tiers: continue in pass 3 (mte_stream.h)
+      D.flags |= kHdrNeedsEsc;
       break;
     }
     if (n + 2 <= 4 * kWave) burst_run<4, K>(D, a, zlds, 4, 0xffffffffu);

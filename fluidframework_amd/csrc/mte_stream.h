@@ -1,0 +1,387 @@
+// mte_stream.h — pass 3: documents beyond the register tiers (> 1,022
+// segments), replayed one wavefront per document with the segment planes
+// left in HBM and streamed per op in tiles of 256 slots (4 per lane,
+// lane-major, coalesced).
+//
+// Per op, the same algorithm as doc_step (mte_replay.h), restated over tiles:
+//   A  scan tiles front to back: perspective lengths, running prefix, the
+//      split / insert-slot lookups (stops once every target is found and the
+//      prefix has passed the op's positions);
+//   B  the split + insert shift as a back-to-front tiled move of every plane
+//      (new[i] = old[i - d(i)], d(i) = (i > t1) + (i > t2)), then the split
+//      patches and the new segment (single-lane stores);
+//   C  for remove / annotate, a second front-to-back scan on the new layout
+//      that marks the leaves with start <= P < end;
+// and, when minSeq advances, a tiled stream compaction (zamboni).
+// Loads bypass L1 (agent-scope relaxed atomics = sc1) and every phase ends
+// with s_waitcnt vmcnt(0), so each phase reads what the previous one wrote.
+// This path is bandwidth- and latency-bound by design (O(n) bytes per op); it
+// exists so that no document size is refused below the ctx capacity.
+#pragma once
+
+#include "mte_replay.h"
+
+namespace mte {
+
+constexpr int kTileE = 4;
+constexpr int kTile = kWave * kTileE;  // slots per tile
+
+__device__ __forceinline__ uint32_t ld_l2(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Every slot index this path computes is checked against the doc's capacity
+// before it touches memory; a violation (an engine bug) stops the document
+// with MTE_E_STATE instead of faulting the device.
+#define MTE_SLOT_OK(i, cap) ((unsigned)(i) < (unsigned)(cap))
+
+// hot planes (len seq rseq rmask meta toff) of tile [tb, tb + kTile); slots >= n are padding
+template <int K>
+__device__ __forceinline__ void tile_load_hot(Regs<kTileE, K>& R, const uint32_t* pl, uint64_t st, int tb, int n) {
+  const int base = tb + lane_id() * kTileE;
+#pragma unroll
+  for (int j = 0; j < kTileE; j++) {
+    const int i = base + j;
+    const bool v = i < n;
+    const uint32_t x = (uint32_t)(v ? i : 0);
+    R.len[j] = v ? (int32_t)ld_l2(pl + x) : 0;
+    R.seq[j] = v ? (int32_t)ld_l2(pl + st + x) : 0;
+    R.rseq[j] = v ? (int32_t)ld_l2(pl + 2 * st + x) : kPad;
+    R.rmask[j] = v ? ld_l2(pl + 3 * st + x) : 0u;
+    R.meta[j] = v ? ld_l2(pl + 4 * st + x) : 0u;
+    R.toff[j] = v ? ld_l2(pl + 5 * st + x) : 0u;
+  }
+}
+
+// One op of one HBM-resident document (see the file comment).  Returns 0 or
+// a negative MTE_E_*.
+template <int K>
+__device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const ReplayArgs& a, uint32_t* zlds) {
+  constexpr int E = kTileE;
+  const int l = lane_id();
+  uint32_t* pl = a.planes + (uint64_t)D.doc * a.cap;
+  const uint64_t sd = a.stride;
+  const int nplanes = kFieldPlanes + K;
+
+  const s8v op = cur;
+  const uint4* rec = D.recp + 4 * D.k;
+  if (D.k + 1 < D.k1) cur = sload8(rec + 4);
+  const uint32_t w3 = (uint32_t)op[3];
+  const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
+  if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
+  if (type > MTE_OP_NOOP) return MTE_E_INVALID_ARG;
+  st[kStOps]++;
+  st[kStMaxSegs] = (uint32_t)D.n > st[kStMaxSegs] ? (uint32_t)D.n : st[kStMaxSegs];
+  const int32_t s = op[0], r = op[1], msn = op[2];
+  const int32_t pos1 = op[4], pos2 = op[5];
+  const bool ins = type == MTE_OP_INSERT;
+  const bool rng = type == MTE_OP_REMOVE || type == MTE_OP_ANNOTATE;
+  const bool newcalc = (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
+  int n = D.n;
+
+  if (ins || rng) {
+    st[kStScanned] += (uint32_t)n;
+    // ---- A: scan -----------------------------------------------------------
+    const int32_t b1 = ins ? pos1 : (pos1 < pos2 ? pos1 : pos2);
+    const int32_t b2 = ins ? pos1 : (pos1 < pos2 ? pos2 : pos1);
+    int xa = -1, xb = -1, gs = -1;  // split at b1, split at b2 (range only), first defined leaf with P >= pos
+    int32_t oa = 0, ob = 0, lena = 0, lenb = 0;
+    uint32_t toffa = 0, toffb = 0;
+    int32_t carry = 0;
+    bool complete = true;  // the scan reached the end of the document
+    for (int tb = 0; tb < n; tb += kTile) {
+      Regs<E, K> R;
+      tile_load_hot<K>(R, pl, sd, tb, n);
+      int32_t L[E], P[E];
+      leaf_lengths<E, K>(R, r, c + 1, (int)c, D.min_seq, newcalc, L);
+      const int32_t tot = prefix<E>(L, P);
+#pragma unroll
+      for (int j = 0; j < E; j++) P[j] += carry;
+      if (xa < 0) {
+        int32_t o = 0;
+        const int x = find_split<E>(L, P, b1, &o);
+        if (x >= 0) {
+          xa = tb + x;
+          oa = o;
+          lena = bcast<E>(R.len, x);
+          toffa = bcast<E>(R.toff, x);
+        }
+      }
+      if (rng && b2 != b1 && xb < 0) {
+        int32_t o = 0;
+        const int x = find_split<E>(L, P, b2, &o);
+        if (x >= 0) {
+          xb = tb + x;
+          ob = o;
+          lenb = bcast<E>(R.len, x);
+          toffb = bcast<E>(R.toff, x);
+        }
+      }
+      if (ins && gs < 0) {
+        const int x = find_slot<E>(L, P, pos1);
+        if (x >= 0) gs = tb + x;
+      }
+      carry += tot;
+      // every later leaf has P >= carry > both positions: nothing more to find
+      if (carry > b2 && (!ins || gs >= 0 || xa >= 0) && tb + kTile < n) {
+        complete = false;
+        break;
+      }
+    }
+    // ---- decisions (as doc_step) --------------------------------------------
+    int t1 = INT32_MAX, t2 = INT32_MAX, g = -1;
+    SplitPatch pa{-1, -1, 0, 0, 0u, 0}, pb{-1, -1, 0, 0, 0u, 0};
+    if (ins) {
+      const int32_t nlen = pos2;
+      if (xa >= 0) {
+        pa = SplitPatch{xa, nlen > 0 ? xa + 2 : xa + 1, oa, lena, toffa, pos1};
+        t1 = xa;
+        if (nlen > 0) {
+          t2 = xa + 1;
+          g = xa + 1;
+        }
+        st[kStWritten] += nlen > 0 ? 3 : 2;
+        n += 1;
+      } else if (nlen > 0) {
+        g = gs;
+        if (g < 0) {
+          if (complete && pos1 > carry) return MTE_E_INSERT_FAILED;  // mergeTree.ts:1666-1672
+          g = n;
+        }
+        t1 = g - 1;
+        st[kStWritten] += 1;
+      }
+      if (nlen > 0) n += 1;
+    } else {
+      int x1 = xa, x2 = xb;
+      int32_t o1 = oa, o2 = ob, l1 = lena, l2 = lenb, bb1 = b1;
+      uint32_t f1 = toffa, f2 = toffb;
+      if (x1 < 0) {
+        x1 = x2;
+        o1 = o2;
+        l1 = l2;
+        f1 = f2;
+        bb1 = b2;
+        x2 = -1;
+      }
+      if (x1 >= 0) {
+        pa = SplitPatch{x1, x1 + 1, o1, l1, f1, bb1};
+        t1 = x1;
+        n += 1;
+        st[kStWritten] += 2;
+        if (x2 >= 0) {
+          const bool same = x2 == x1;
+          pb = SplitPatch{x2 + 1, x2 + 2, same ? o2 - o1 : o2, same ? l1 - o1 : l2, same ? f1 + (uint32_t)o1 : f2, b2};
+          t2 = x2 + 1;
+          n += 1;
+          st[kStWritten] += 2;
+        }
+      }
+    }
+    if (n + 2 > (int)a.cap) return MTE_E_CAPACITY;
+    // ---- B: shift back to front, then patches and the new segment --------------
+    if (t1 != INT32_MAX) {
+      const int lo = t1 + 1;
+      for (int tb = ((n - 1) / kTile) * kTile; tb + kTile > lo; tb -= kTile) {
+        const int base = tb + l * E;
+        for (int p = 0; p < nplanes; p++) {
+          uint32_t* q = pl + (uint64_t)p * sd;
+          uint32_t v[E];
+#pragma unroll
+          for (int j = 0; j < E; j++) {
+            const int i = base + j;
+            const int src = i - ((i > t1 ? 1 : 0) + (i > t2 ? 1 : 0));
+            // src is -1 only for the new segment's slot 0 (t1 == -1), which the
+            // new-segment stores below overwrite: never read before the doc
+            v[j] = (i < n && i >= lo && MTE_SLOT_OK(src, a.cap)) ? ld_l2(q + src) : 0u;
+          }
+#pragma unroll
+          for (int j = 0; j < E; j++) {
+            const int i = base + j;
+            if (i < n && i >= lo && MTE_SLOT_OK(i, a.cap)) q[i] = v[j];
+          }
+        }
+        vm_drain();
+      }
+    }
+    if ((pa.h >= 0 && !(MTE_SLOT_OK(pa.h, a.cap) && MTE_SLOT_OK(pa.tl, a.cap))) ||
+        (pb.h >= 0 && !(MTE_SLOT_OK(pb.h, a.cap) && MTE_SLOT_OK(pb.tl, a.cap))) || (g >= 0 && !MTE_SLOT_OK(g, a.cap)))
+      return MTE_E_STATE;
+    if (l == 0) {
+#pragma unroll
+      for (int pi = 0; pi < 2; pi++) {
+        const SplitPatch& p = pi == 0 ? pa : pb;
+        if (p.h >= 0) {
+          pl[p.h] = (uint32_t)p.o;
+          pl[p.tl] = (uint32_t)(p.len - p.o);
+          pl[5 * sd + p.tl] = p.toff + (uint32_t)p.o;
+        }
+      }
+      if (g >= 0) {
+        pl[g] = (uint32_t)pos2;
+        pl[sd + g] = (uint32_t)s;
+        pl[2 * sd + g] = (uint32_t)kNone;
+        pl[3 * sd + g] = 0u;
+        pl[4 * sd + g] = (uint32_t)op[7];
+        pl[5 * sd + g] = (uint32_t)op[6];
+      }
+    }
+    if (g >= 0) {
+      uint32_t pr[K > 0 ? K : 1][1];
+      const bool one[1] = {true};
+#pragma unroll
+      for (int kk = 0; kk < (K > 0 ? K : 1); kk++) pr[kk][0] = 0;
+      if (K > 0 && (flags & kFlagHasProps)) {
+        const s8v q2 = sload8_props(rec);
+        apply_props<1, K>(pr, one, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], (uint32_t)q2[3], a);
+        st[kStPwrites] += (uint32_t)q2[4];
+      }
+      if (l == 0) {
+#pragma unroll
+        for (int kk = 0; kk < K; kk++) pl[(kFieldPlanes + kk) * sd + g] = pr[kk][0];
+      }
+      if (((uint32_t)op[7] >> 8) == 0) st[kStUnits] += (uint32_t)pos2;
+    }
+    vm_drain();
+    // ---- C: mark [start, end) on the new layout ---------------------------------
+    if (rng && pos2 > pos1) {
+      s8v q2 = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (type == MTE_OP_ANNOTATE) q2 = sload8_props(rec);
+      const bool rem = type == MTE_OP_REMOVE;
+      int32_t cy = 0;
+      uint32_t cnt_all = 0;
+      for (int tb = 0; tb < n && cy < pos2; tb += kTile) {
+        Regs<E, K> R;
+        tile_load_hot<K>(R, pl, sd, tb, n);
+        int32_t L[E], P[E];
+        leaf_lengths<E, K>(R, r, c + 1, (int)c, D.min_seq, newcalc, L);
+        const int32_t tot = prefix<E>(L, P);
+        bool in[E];
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+          P[j] += cy;
+          in[j] = L[j] > 0 && P[j] >= pos1 && P[j] < pos2;
+          cnt += (uint32_t)__popcll(__ballot(in[j]));
+        }
+        cy += tot;
+        if (cnt == 0) continue;
+        cnt_all += cnt;
+        const int base = tb + l * E;
+        if (rem) {
+          // markRemoved (mergeTree.ts:1924-1962)
+#pragma unroll
+          for (int j = 0; j < E; j++) {
+            if (in[j]) {
+              pl[2 * sd + base + j] = (uint32_t)(R.rseq[j] == kNone ? s : R.rseq[j]);
+              pl[3 * sd + base + j] = R.rmask[j] | (1u << c);
+            }
+          }
+        } else if (K > 0) {
+          // PropertiesManager.addProperties (segmentPropertiesManager.ts:63-151)
+          uint32_t pr[K > 0 ? K : 1][E];
+#pragma unroll
+          for (int kk = 0; kk < K; kk++)
+#pragma unroll
+            for (int j = 0; j < E; j++) {
+              const int i = base + j;
+              pr[kk][j] = i < n ? ld_l2(pl + (kFieldPlanes + kk) * sd + i) : 0u;
+              if (flags & MTE_F_REWRITE) pr[kk][j] = in[j] ? 0u : pr[kk][j];
+            }
+          apply_props<E, K>(pr, in, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], (uint32_t)q2[3], a);
+#pragma unroll
+          for (int kk = 0; kk < K; kk++)
+#pragma unroll
+            for (int j = 0; j < E; j++)
+              if (in[j]) pl[(kFieldPlanes + kk) * sd + base + j] = pr[kk][j];
+        }
+      }
+      st[kStWritten] += cnt_all;
+      if (type == MTE_OP_ANNOTATE) st[kStPwrites] += cnt_all * (uint32_t)q2[4];
+      vm_drain();
+    }
+  }
+  D.n = n;
+  D.k++;
+
+  if (type != MTE_OP_NOOP) {  // Client.completeAndLogOp (client.ts:525-528)
+    if (!(D.cur_seq < s)) return MTE_E_SEQ_ORDER;
+    if (!(D.min_seq <= msn)) return MTE_E_MSN_ORDER;
+  }
+  if (flags & MTE_F_MSG_END) {
+    // updateSeqNumbers (client.ts:937-945) -> setMinSeq (mergeTree.ts:1077-1093)
+    if (!(D.cur_seq <= s)) return MTE_E_SEQ_ORDER;
+    D.cur_seq = s;
+    if (!(msn <= s)) return MTE_E_MSN_GT_SEQ;
+    if (!(D.min_seq <= msn)) return MTE_E_MSN_ORDER;
+    if (msn > D.min_seq) {
+      D.min_seq = msn;
+      // zamboni as a tiled stream compaction, front to back (dst <= src)
+      int32_t w = 0;
+      for (int tb = 0; tb < n; tb += kTile) {
+        const int base = tb + l * E;
+        bool keep[E];
+        int32_t cntl = 0;
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+          const int i = base + j;
+          keep[j] = i < n && (int32_t)ld_l2(pl + 2 * sd + i) > msn;
+          cntl += keep[j] ? 1 : 0;
+        }
+        const int32_t incl = wave_incl_scan(cntl);
+        const int32_t tot = rdlane(incl, kWave - 1);
+        if (tot != kTile || w != tb) {
+          int32_t dst = w + incl - cntl;
+          for (int p = 0; p < nplanes; p++) {
+            uint32_t* q = pl + (uint64_t)p * sd;
+            uint32_t v[E];
+#pragma unroll
+            for (int j = 0; j < E; j++) v[j] = keep[j] ? ld_l2(q + base + j) : 0u;
+            int32_t d0 = dst;
+#pragma unroll
+            for (int j = 0; j < E; j++) {
+              if (keep[j] && MTE_SLOT_OK(d0, a.cap)) q[d0] = v[j];
+              d0 += keep[j] ? 1 : 0;
+            }
+          }
+          vm_drain();
+        }
+        w += tot;
+      }
+      D.n = w;
+    }
+  }
+  return 0;
+}
+
+// pass 3: documents pass 2 escalated (more than 1,022 segments)
+template <int K>
+__global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
+  __shared__ uint32_t zlds_all[kDocsPerBlock][kWave];
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+  const int doc = (int)blockIdx.x * kDocsPerBlock + w;
+  if (doc >= (int)a.n_docs) return;
+  if (!(a.hdr[doc].flags & kHdrNeedsEsc)) return;  // untouched doc: leave the header alone
+  DocRun D;
+  run_init(D, a, doc, true);
+  uint32_t st[kNumStats] = {0, 0, 0, 0, 0, 0};
+  if (D.running) {
+    s8v cur = sload8(D.recp + 4 * D.k);
+    while (D.running) {
+      const int rc = stream_step<K>(D, st, cur, a, zlds_all[w]);
+      if (rc < 0) {
+        D.status = rc;
+        D.running = false;
+      } else if (D.k >= D.k1) {
+        D.running = false;
+      } else if (st[kStOps] >= (1u << 20)) {
+        run_flush_stats(D, st, a);
+      }
+    }
+    run_flush_stats(D, st, a);
+  }
+  run_finish(D, a);
+}
+
+}  // namespace mte

@@ -134,3 +134,52 @@ def test_gpu_capacity_error_is_reported():
     assert o.stats()["max_segs"] > 1022
     st = d.statuses()
     assert (st == MTE_E_CAPACITY).all()
+
+
+def replay_both_cap(stream, cap, threads=8):
+    n_keys = stream["n_keys"]
+    o = OracleEngine(n_keys, threads=threads)
+    o.load_docs(stream["inits"], stream["init_text"])
+    o.apply_batch(stream["batch"])
+    d = DeviceEngine(n_keys, seg_capacity=cap)
+    d.load_docs(stream["inits"], stream["init_text"])
+    d.apply_batch(stream["batch"])
+    return o, d
+
+
+def test_gpu_stream_pass_insert_heavy_large_docs():
+    # insert-only docs grow past the register tiers (1,022 segments): pass 3
+    s = gen.generate(2, n_docs=12, ops_per_doc=2600, mix=gen.MIX_INSERT, min_length=0)
+    o, d = replay_both_cap(s, 8192)
+    assert o.stats()["max_segs"] > 2000
+    assert (o.statuses() == 0).all()
+    assert_same(o, d, sample_docs=12)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_gpu_stream_pass_long_docs_all_ops(mode):
+    # config-5 shaped (scaled down): a long initial text split by insert /
+    # remove / annotate ops in deep rounds (1,024 concurrent ops), both
+    # length-calc modes
+    s = gen.generate(3, n_docs=6, ops_per_doc=4000, init_len=20000, round_ops=1024, min_length=16,
+                     length_mode=mode)
+    o, d = replay_both_cap(s, 16384)
+    assert o.stats()["max_segs"] > 1100
+    assert (o.statuses() == 0).all()
+    assert_same(o, d, sample_docs=6)
+
+
+def test_gpu_stream_pass_annotate_heavy():
+    s = gen.generate(3, n_docs=6, ops_per_doc=3000, init_len=6000, round_ops=512, min_length=16,
+                     length_mode=1, mix=gen.MIX_INSERT | gen.MIX_ANNOTATE)
+    o, d = replay_both_cap(s, 16384)
+    assert o.stats()["max_segs"] > 4000
+    assert (o.statuses() == 0).all()
+    assert_same(o, d, sample_docs=6)
+
+
+def test_gpu_stream_pass_capacity_error():
+    s = gen.generate(2, n_docs=3, ops_per_doc=1400, mix=gen.MIX_INSERT, min_length=0)
+    o, d = replay_both_cap(s, 1536)
+    assert o.stats()["max_segs"] > 1534
+    assert (d.statuses() == MTE_E_CAPACITY).all()
