@@ -96,7 +96,7 @@ class MteDocView(C.Structure):
 EXPORTED_SYMBOLS = [
     "mte_abi_version", "mte_strerror", "mte_create", "mte_destroy", "mte_last_error",
     "mte_load_docs", "mte_submit", "mte_run", "mte_sync", "mte_reset", "mte_digest",
-    "mte_digest_device", "mte_read_doc", "mte_doc_status", "mte_stats_get",
+    "mte_digest_device", "mte_read_doc", "mte_doc_status", "mte_stats_get", "mte_set_stats",
 ]
 
 

@@ -246,6 +246,7 @@ struct mte_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool ran = false, submitted = false;
+  bool stats_on = true;
   std::string err;
 
   DocHdr* hdr = nullptr;
@@ -339,18 +340,18 @@ int launch_reset(mte_ctx* c) {
   return MTE_OK;
 }
 
-template <int K>
+template <int K, bool S>
 int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   // pass 1: two documents per wavefront (docs up to 126 segments)
   const uint32_t b1 = (c->n_pairs + kPairsPerBlock - 1) / kPairsPerBlock;
-  hipLaunchKernelGGL((pair_kernel<K>), dim3(b1), dim3(256), 0, c->stream, a);
+  hipLaunchKernelGGL((pair_kernel<K, S>), dim3(b1), dim3(256), 0, c->stream, a);
   HIPCHK(c, hipGetLastError());
   // pass 2: docs that outgrew pass 1 continue one per wavefront (up to 1022 segments)
   const uint32_t b2 = (c->n_docs + kDocsPerBlock - 1) / kDocsPerBlock;
-  hipLaunchKernelGGL((big_kernel<K>), dim3(b2), dim3(256), 0, c->stream, a);
+  hipLaunchKernelGGL((big_kernel<K, S>), dim3(b2), dim3(256), 0, c->stream, a);
   HIPCHK(c, hipGetLastError());
   // pass 3: larger docs (up to the ctx capacity), HBM-resident, streamed per op
-  hipLaunchKernelGGL((stream_kernel<K>), dim3(b2), dim3(256), 0, c->stream, a);
+  hipLaunchKernelGGL((stream_kernel<K, S>), dim3(b2), dim3(256), 0, c->stream, a);
   HIPCHK(c, hipGetLastError());
   return MTE_OK;
 }
@@ -587,7 +588,12 @@ int mte_run(mte_ctx* c) {
   a.pair_docs = c->d_pairs;
   a.n_pairs = c->n_pairs;
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-  int rc = c->kt == 0 ? launch_replay<0>(c, a) : (c->kt == 4 ? launch_replay<4>(c, a) : launch_replay<8>(c, a));
+  int rc;
+  if (c->stats_on)
+    rc = c->kt == 0 ? launch_replay<0, true>(c, a) : (c->kt == 4 ? launch_replay<4, true>(c, a) : launch_replay<8, true>(c, a));
+  else
+    rc = c->kt == 0 ? launch_replay<0, false>(c, a)
+                    : (c->kt == 4 ? launch_replay<4, false>(c, a) : launch_replay<8, false>(c, a));
   if (rc) return rc;
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
   c->ran = true;
@@ -692,6 +698,12 @@ int mte_read_doc(mte_ctx* c, uint32_t doc, mte_doc_view* v) {
   v->length = length;
   v->n_text = nt;
   v->n_segs = ns;
+  return MTE_OK;
+}
+
+int mte_set_stats(mte_ctx* c, int enable) {
+  if (!c) return MTE_E_INVALID_ARG;
+  c->stats_on = enable != 0;
   return MTE_OK;
 }
 

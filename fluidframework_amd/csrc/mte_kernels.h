@@ -106,8 +106,11 @@ __device__ __forceinline__ int32_t wave_incl_scan(int32_t v) {
   return v;
 }
 
-// value of lane l-1 (lane 0 gets 0)
-__device__ __forceinline__ int32_t lane_prev(int32_t v) { return dpp<kWaveShr1>(v); }
+// value of lane l-1 (lane 0 gets 0: bound_ctrl, so no zero-initialised
+// destination is needed and the move is a single v_mov_b32_dpp)
+__device__ __forceinline__ int32_t lane_prev(int32_t v) {
+  return __builtin_amdgcn_mov_dpp(v, kWaveShr1, 0xf, 0xf, true);
+}
 
 __device__ __forceinline__ int32_t rdlane(int32_t v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int lane) {

@@ -122,34 +122,68 @@ __device__ __forceinline__ void compact_plane(T (&F)[E], const bool (&keep)[E], 
   fence_wave();
 }
 
-// Shift every plane (and, for range ops, the L / P planes).  A scheduling
-// barrier between planes keeps the compiler from interleaving all planes'
-// old and new values (which doubles the live register state).
+template <int E, int NF, typename T>
+__device__ __forceinline__ void shift_grab(uint32_t (&last)[NF], uint32_t (&last2)[NF], int f, const T (&F)[E]) {
+  last[f] = (uint32_t)F[E - 1];
+  last2[f] = (uint32_t)F[E >= 2 ? E - 2 : 0];
+}
+
+template <int E, int NF, typename T>
+__device__ __forceinline__ void shift_apply(T (&F)[E], const uint32_t (&p1)[NF], const uint32_t (&p2)[NF], int f,
+                                            const bool (&g1)[E], const bool (&g2)[E]) {
+#pragma unroll
+  for (int j = E - 1; j >= 0; j--) {
+    const T m1 = (j >= 1) ? F[j >= 1 ? j - 1 : 0] : (T)p1[f];
+    const T m2 = (j >= 2) ? F[j >= 2 ? j - 2 : 0] : ((j == 1) ? (T)p1[f] : (T)p2[f]);
+    F[j] = g2[j] ? m2 : (g1[j] ? m1 : F[j]);
+  }
+}
+
+// Shift every plane (and, for range ops, the L / P planes): new[i] =
+// old[i - d(i)] with d(i) = (i > t1) + (i > t2), as pull_shift does for one
+// plane.  The cross-lane moves of all planes are issued first and the selects
+// after, so no DPP read waits on the VALU write just before it (a chained
+// move per plane costs two hazard nops each).
 template <int E, int K, bool LP>
 __device__ __forceinline__ void shift_all(Regs<E, K>& R, int32_t (&L)[E], int32_t (&P)[E], int t1, int t2) {
-  pull_shift<E>(R.len, t1, t2);
-  __builtin_amdgcn_sched_barrier(0);
-  pull_shift<E>(R.seq, t1, t2);
-  __builtin_amdgcn_sched_barrier(0);
-  pull_shift<E>(R.rseq, t1, t2);
-  __builtin_amdgcn_sched_barrier(0);
-  pull_shift<E>(R.rmask, t1, t2);
-  __builtin_amdgcn_sched_barrier(0);
-  pull_shift<E>(R.meta, t1, t2);
-  __builtin_amdgcn_sched_barrier(0);
-  pull_shift<E>(R.toff, t1, t2);
+  constexpr int NF = kFieldPlanes + K + (LP ? 2 : 0);
+  uint32_t last[NF], last2[NF];
+  shift_grab<E, NF>(last, last2, 0, R.len);
+  shift_grab<E, NF>(last, last2, 1, R.seq);
+  shift_grab<E, NF>(last, last2, 2, R.rseq);
+  shift_grab<E, NF>(last, last2, 3, R.rmask);
+  shift_grab<E, NF>(last, last2, 4, R.meta);
+  shift_grab<E, NF>(last, last2, 5, R.toff);
 #pragma unroll
-  for (int k = 0; k < K; k++) {
-    __builtin_amdgcn_sched_barrier(0);
-    pull_shift<E>(R.pr[k], t1, t2);
-  }
+  for (int k = 0; k < K; k++) shift_grab<E, NF>(last, last2, kFieldPlanes + k, R.pr[k]);
   if constexpr (LP) {
-    __builtin_amdgcn_sched_barrier(0);
-    pull_shift<E>(L, t1, t2);
-    __builtin_amdgcn_sched_barrier(0);
-    pull_shift<E>(P, t1, t2);
+    shift_grab<E, NF>(last, last2, NF - 2, L);
+    shift_grab<E, NF>(last, last2, NF - 1, P);
   }
-  __builtin_amdgcn_sched_barrier(0);
+  uint32_t p1[NF], p2[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) p1[f] = (uint32_t)lane_prev((int32_t)last[f]);  // old[base - 1]
+#pragma unroll
+  for (int f = 0; f < NF; f++) p2[f] = (uint32_t)lane_prev((int32_t)(E >= 2 ? last2[f] : p1[f]));  // old[base - 2]
+  const int base = lane_id() * E;
+  bool g1[E], g2[E];
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    g1[j] = base + j > t1;
+    g2[j] = base + j > t2;
+  }
+  shift_apply<E, NF>(R.len, p1, p2, 0, g1, g2);
+  shift_apply<E, NF>(R.seq, p1, p2, 1, g1, g2);
+  shift_apply<E, NF>(R.rseq, p1, p2, 2, g1, g2);
+  shift_apply<E, NF>(R.rmask, p1, p2, 3, g1, g2);
+  shift_apply<E, NF>(R.meta, p1, p2, 4, g1, g2);
+  shift_apply<E, NF>(R.toff, p1, p2, 5, g1, g2);
+#pragma unroll
+  for (int k = 0; k < K; k++) shift_apply<E, NF>(R.pr[k], p1, p2, kFieldPlanes + k, g1, g2);
+  if constexpr (LP) {
+    shift_apply<E, NF>(L, p1, p2, NF - 2, g1, g2);
+    shift_apply<E, NF>(P, p1, p2, NF - 1, g1, g2);
+  }
 }
 
 template <int E, int K>
@@ -204,6 +238,14 @@ struct SplitPatch {
   int32_t pos;    // document position of the tail (P of the tail slot)
 };
 
+// Statistics (mte_stats: the Client.measureOps-style accounting and the
+// algorithmic byte count) are a compile-time option of the replay kernels:
+// S = false drops every counter update from the per-op path.
+#define MTE_STAT(...) \
+  if constexpr (S) {    \
+    __VA_ARGS__         \
+  }
+
 // One op record of one document: Client.applyMsg -> applyRemoteOp ->
 // insertSegments / markRangeRemoved / annotateRange -> updateSeqNumbers
 // (client.ts:918-945).  Returns 0 (applied), 1 (re-pick the register tier
@@ -214,13 +256,16 @@ struct SplitPatch {
 // split / insert-slot lookups, then wave-uniform shift thresholds and split
 // patches) followed by ONE vector apply phase shared by all op types, so the
 // register state flows through a single path (no per-branch copies).
-template <int E, int K>
+template <int E, int K, bool S>
 __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)[kNumStats], s8v& cur,
                                         const ReplayArgs& a, uint32_t* zlds, int emin) {
   const int l = lane_id();
   const int base = l * E;
   const int lim = kWave * E < (int)a.cap ? kWave * E : (int)a.cap;
-  if (D.n + 2 > lim || st[kStOps] >= (1u << 20)) return 1;
+  if (D.n + 2 > lim) return 1;
+  if constexpr (S) {
+    if (st[kStOps] >= (1u << 20)) return 1;
+  }
 
   // ---- op record: words 0..7 were prefetched into `cur` -------------------
   const s8v op = cur;
@@ -229,15 +274,15 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
-  st[kStOps]++;
-  st[kStMaxSegs] = (uint32_t)D.n > st[kStMaxSegs] ? (uint32_t)D.n : st[kStMaxSegs];
+  MTE_STAT(st[kStOps]++;)
+  MTE_STAT(st[kStMaxSegs] = (uint32_t)D.n > st[kStMaxSegs] ? (uint32_t)D.n : st[kStMaxSegs];)
   const int32_t s = op[0];
   const int32_t msn = op[2];
   int n = D.n;
 
   if (type == MTE_OP_INSERT || type == MTE_OP_REMOVE || type == MTE_OP_ANNOTATE) {
     const bool ins = type == MTE_OP_INSERT;
-    st[kStScanned] += (uint32_t)n;
+    MTE_STAT(st[kStScanned] += (uint32_t)n;)
     const int32_t r = op[1];
     const int32_t pos1 = op[4], pos2 = op[5];
     int32_t L[E], P[E];
@@ -264,10 +309,10 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
           t2 = xs + 1;
           g = xs + 1;
           pa.tl = xs + 2;
-          st[kStWritten] += 3;
+          MTE_STAT(st[kStWritten] += 3;)
         } else {
           pa.tl = xs + 1;
-          st[kStWritten] += 2;
+          MTE_STAT(st[kStWritten] += 2;)
         }
         n += 1;
       } else if (nlen > 0) {
@@ -277,7 +322,7 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
           g = n;
         }
         t1 = g - 1;
-        st[kStWritten] += 1;
+        MTE_STAT(st[kStWritten] += 1;)
       }
       if (nlen > 0) n += 1;
     } else {
@@ -303,7 +348,7 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
         pa.pos = bb1;
         t1 = x1;
         n += 1;
-        st[kStWritten] += 2;
+        MTE_STAT(st[kStWritten] += 2;)
         if (x2 >= 0) {
           // after the first split the second leaf sits at x2 + 1; when both
           // boundaries fall in one leaf it is the first split's tail
@@ -316,7 +361,7 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
           pb.pos = b2;
           t2 = x2 + 1;
           n += 1;
-          st[kStWritten] += 2;
+          MTE_STAT(st[kStWritten] += 2;)
         }
       }
     }
@@ -353,9 +398,9 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
       if (K > 0 && (flags & kFlagHasProps)) {
         const s8v q2 = sload8_props(rec);  // same 64-B line as `op`: a scalar-cache hit
         apply_props<1, K>(pr, one, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], (uint32_t)q2[3], a);
-        st[kStPwrites] += (uint32_t)q2[4];
+        MTE_STAT(st[kStPwrites] += (uint32_t)q2[4];)
       }
-      if ((meta >> 8) == 0) st[kStUnits] += (uint32_t)pos2;
+      MTE_STAT(if ((meta >> 8) == 0) st[kStUnits] += (uint32_t)pos2;)
 #pragma unroll
       for (int jj = 0; jj < E; jj++) {
         const bool at = base + jj == g;
@@ -379,7 +424,7 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
         in[jj] = L[jj] > 0 && P[jj] >= pos1 && P[jj] < pos2;
         cnt += (uint32_t)__popcll(__ballot(in[jj]));
       }
-      st[kStWritten] += cnt;
+      MTE_STAT(st[kStWritten] += cnt;)
       if (type == MTE_OP_REMOVE) {
         // markRemoved (mergeTree.ts:1924-1962): keep the earliest removedSeq,
         // add the client to removedClientIds
@@ -399,7 +444,7 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
             for (int jj = 0; jj < E; jj++) R.pr[kk][jj] = in[jj] ? 0u : R.pr[kk][jj];
         }
         apply_props<E, K>(R.pr, in, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], (uint32_t)q2[3], a);
-        st[kStPwrites] += cnt * (uint32_t)q2[4];
+        MTE_STAT(st[kStPwrites] += cnt * (uint32_t)q2[4];)
       }
     }
   } else if (type != MTE_OP_NOOP) {
@@ -528,7 +573,7 @@ __device__ __forceinline__ bool step_done(DocRun& D, int rc) {
 // One burst of up to `limit` ops of one document at register tier E: load
 // its segments into VGPRs, replay, write them back.  Returns early when the
 // document needs another tier or stops.
-template <int E, int K>
+template <int E, int K, bool S>
 __device__ __forceinline__ void burst_run(DocRun& D, const ReplayArgs& a, uint32_t* zlds, int emin, uint32_t limit) {
   Regs<E, K> R;
   uint32_t st[kNumStats] = {0, 0, 0, 0, 0, 0};
@@ -539,12 +584,12 @@ __device__ __forceinline__ void burst_run(DocRun& D, const ReplayArgs& a, uint32
   touch_records(D, D.k + 16, pending, sink);
   while (D.running) {
     if ((D.k & 63u) == 0) touch_records(D, D.k + 64, pending, sink);
-    const int rc = doc_step<E, K>(R, D, st, cur, a, zlds, emin);
+    const int rc = doc_step<E, K, S>(R, D, st, cur, a, zlds, emin);
     if (step_done(D, rc) || D.k >= kend) break;
   }
   swait(cur);  // no scalar load may be left in flight
   store_regs<E, K>(R, D, a);
-  run_flush_stats(D, st, a);
+  if constexpr (S) run_flush_stats(D, st, a);
   sink ^= pending;
   if (sink == 0x9e3779b9u && D.doc < 0) a.stats[0] = sink;  // keeps the prefetch loads alive
 }
@@ -565,13 +610,13 @@ __device__ __forceinline__ int pick_pass1_tier(DocRun& D, uint32_t cap) {
   return 0;
 }
 
-template <int K>
+template <int K, bool S>
 __device__ __forceinline__ void pass1_burst(DocRun& D, const ReplayArgs& a, uint32_t* zlds) {
   const int e = pick_pass1_tier(D, a.cap);
-  if (e == 1) burst_run<1, K>(D, a, zlds, 1, kBurst);
-  else if (e == 2) burst_run<2, K>(D, a, zlds, 1, kBurst);
+  if (e == 1) burst_run<1, K, S>(D, a, zlds, 1, kBurst);
+  else if (e == 2) burst_run<2, K, S>(D, a, zlds, 1, kBurst);
   else if constexpr (MTE_PASS1_EMAX >= 4) {
-    if (e == 4) burst_run<4, K>(D, a, zlds, 1, kBurst);
+    if (e == 4) burst_run<4, K, S>(D, a, zlds, 1, kBurst);
   }
 }
 
@@ -605,7 +650,7 @@ __device__ __forceinline__ void run_to_lds(const DocRun& D, DocHdr* hl) {
 // pass 1: two documents per wavefront, replayed in alternating bursts, so a
 // 10k-document batch is resident on the chip at once with the register
 // budget of one document (E <= 4)
-template <int K>
+template <int K, bool S>
 __global__ __launch_bounds__(256, MTE_PAIR_WAVES) void pair_kernel(ReplayArgs a) {
   __shared__ uint32_t zlds_all[kPairsPerBlock][kWave * 4];
   __shared__ DocHdr hl_all[kPairsPerBlock][2];
@@ -633,7 +678,7 @@ __global__ __launch_bounds__(256, MTE_PAIR_WAVES) void pair_kernel(ReplayArgs a)
     if (!(live & (1u << t))) continue;
     const int doc = t ? docs[1] : docs[0];
     DocRun D;
-    if (run_from_lds(D, &hl[t], doc, a)) pass1_burst<K>(D, a, zlds);
+    if (run_from_lds(D, &hl[t], doc, a)) pass1_burst<K, S>(D, a, zlds);
     run_to_lds(D, &hl[t]);
     if (!D.running) live &= ~(1u << t);
   }
@@ -645,7 +690,7 @@ __global__ __launch_bounds__(256, MTE_PAIR_WAVES) void pair_kernel(ReplayArgs a)
 }
 
 // pass 2: one document per wavefront, for the documents pass 1 escalated
-template <int K>
+template <int K, bool S>
 __global__ __launch_bounds__(256) void big_kernel(ReplayArgs a) {
   __shared__ uint32_t zlds_all[kDocsPerBlock][kWave * 16];
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
@@ -665,9 +710,9 @@ __global__ __launch_bounds__(256) void big_kernel(ReplayArgs a) {
       D.flags |= kHdrNeedsEsc;
       break;
     }
-    if (n + 2 <= 4 * kWave) burst_run<4, K>(D, a, zlds, 4, 0xffffffffu);
-    else if (n + 2 <= 8 * kWave) burst_run<8, K>(D, a, zlds, 4, 0xffffffffu);
-    else burst_run<16, K>(D, a, zlds, 4, 0xffffffffu);
+    if (n + 2 <= 4 * kWave) burst_run<4, K, S>(D, a, zlds, 4, 1u << 19);
+    else if (n + 2 <= 8 * kWave) burst_run<8, K, S>(D, a, zlds, 4, 1u << 19);
+    else burst_run<16, K, S>(D, a, zlds, 4, 1u << 19);
   }
   run_finish(D, a);
 }

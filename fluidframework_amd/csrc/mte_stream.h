@@ -56,7 +56,7 @@ __device__ __forceinline__ void tile_load_hot(Regs<kTileE, K>& R, const uint32_t
 
 // One op of one HBM-resident document (see the file comment).  Returns 0 or
 // a negative MTE_E_*.
-template <int K>
+template <int K, bool S>
 __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const ReplayArgs& a, uint32_t* zlds) {
   constexpr int E = kTileE;
   const int l = lane_id();
@@ -71,8 +71,8 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
   if (type > MTE_OP_NOOP) return MTE_E_INVALID_ARG;
-  st[kStOps]++;
-  st[kStMaxSegs] = (uint32_t)D.n > st[kStMaxSegs] ? (uint32_t)D.n : st[kStMaxSegs];
+  MTE_STAT(st[kStOps]++;)
+  MTE_STAT(st[kStMaxSegs] = (uint32_t)D.n > st[kStMaxSegs] ? (uint32_t)D.n : st[kStMaxSegs];)
   const int32_t s = op[0], r = op[1], msn = op[2];
   const int32_t pos1 = op[4], pos2 = op[5];
   const bool ins = type == MTE_OP_INSERT;
@@ -81,7 +81,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   int n = D.n;
 
   if (ins || rng) {
-    st[kStScanned] += (uint32_t)n;
+    MTE_STAT(st[kStScanned] += (uint32_t)n;)
     // ---- A: scan -----------------------------------------------------------
     const int32_t b1 = ins ? pos1 : (pos1 < pos2 ? pos1 : pos2);
     const int32_t b2 = ins ? pos1 : (pos1 < pos2 ? pos2 : pos1);
@@ -141,7 +141,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
           t2 = xa + 1;
           g = xa + 1;
         }
-        st[kStWritten] += nlen > 0 ? 3 : 2;
+        MTE_STAT(st[kStWritten] += nlen > 0 ? 3 : 2;)
         n += 1;
       } else if (nlen > 0) {
         g = gs;
@@ -150,7 +150,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
           g = n;
         }
         t1 = g - 1;
-        st[kStWritten] += 1;
+        MTE_STAT(st[kStWritten] += 1;)
       }
       if (nlen > 0) n += 1;
     } else {
@@ -169,13 +169,13 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
         pa = SplitPatch{x1, x1 + 1, o1, l1, f1, bb1};
         t1 = x1;
         n += 1;
-        st[kStWritten] += 2;
+        MTE_STAT(st[kStWritten] += 2;)
         if (x2 >= 0) {
           const bool same = x2 == x1;
           pb = SplitPatch{x2 + 1, x2 + 2, same ? o2 - o1 : o2, same ? l1 - o1 : l2, same ? f1 + (uint32_t)o1 : f2, b2};
           t2 = x2 + 1;
           n += 1;
-          st[kStWritten] += 2;
+          MTE_STAT(st[kStWritten] += 2;)
         }
       }
     }
@@ -235,7 +235,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
       if (K > 0 && (flags & kFlagHasProps)) {
         const s8v q2 = sload8_props(rec);
         apply_props<1, K>(pr, one, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], (uint32_t)q2[3], a);
-        st[kStPwrites] += (uint32_t)q2[4];
+        MTE_STAT(st[kStPwrites] += (uint32_t)q2[4];)
       }
       if (l == 0) {
 #pragma unroll
@@ -297,7 +297,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
               if (in[j]) pl[(kFieldPlanes + kk) * sd + base + j] = pr[kk][j];
         }
       }
-      st[kStWritten] += cnt_all;
+      MTE_STAT(st[kStWritten] += cnt_all;)
       if (type == MTE_OP_ANNOTATE) st[kStPwrites] += cnt_all * (uint32_t)q2[4];
       vm_drain();
     }
@@ -356,7 +356,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
 }
 
 // pass 3: documents pass 2 escalated (more than 1,022 segments)
-template <int K>
+template <int K, bool S>
 __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
   __shared__ uint32_t zlds_all[kDocsPerBlock][kWave];
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
@@ -369,17 +369,17 @@ __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
   if (D.running) {
     s8v cur = sload8(D.recp + 4 * D.k);
     while (D.running) {
-      const int rc = stream_step<K>(D, st, cur, a, zlds_all[w]);
+      const int rc = stream_step<K, S>(D, st, cur, a, zlds_all[w]);
       if (rc < 0) {
         D.status = rc;
         D.running = false;
       } else if (D.k >= D.k1) {
         D.running = false;
-      } else if (st[kStOps] >= (1u << 20)) {
+      } else if (S && st[kStOps] >= (1u << 20)) {
         run_flush_stats(D, st, a);
       }
     }
-    run_flush_stats(D, st, a);
+    if constexpr (S) run_flush_stats(D, st, a);
   }
   run_finish(D, a);
 }

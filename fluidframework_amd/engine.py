@@ -143,6 +143,10 @@ class DeviceEngine(EngineBase):
     def reset(self):
         self._check(self.lib.mte_reset(self.ctx), "reset")
 
+    def set_stats(self, enable):
+        """Statistics accounting on (default) / off (mte_set_stats)."""
+        self._check(self.lib.mte_set_stats(self.ctx, 1 if enable else 0), "set_stats")
+
     def digest_device(self, device_ptr):
         self._check(self.lib.mte_digest_device(self.ctx, C.c_void_p(device_ptr), self.n_docs),
                     "digest_device")

@@ -202,6 +202,11 @@ int mte_digest_device(mte_ctx* ctx, void* device_out, uint32_t n_docs);
 int mte_read_doc(mte_ctx* ctx, uint32_t doc, mte_doc_view* view);
 int mte_doc_status(mte_ctx* ctx, int32_t* out, uint32_t n_docs);
 int mte_stats_get(mte_ctx* ctx, mte_stats* out);
+/* Statistics accounting (the counters of mte_stats, like the reference's
+ * opt-in Client.measureOps, client.ts:71-78) is on by default; with enable = 0
+ * the replay kernels are built without the per-op counter updates and
+ * mte_stats_get reports zero counts (kernel_ms stays valid). */
+int mte_set_stats(mte_ctx* ctx, int enable);
 
 #ifdef __cplusplus
 }

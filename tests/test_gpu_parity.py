@@ -183,3 +183,19 @@ def test_gpu_stream_pass_capacity_error():
     o, d = replay_both_cap(s, 1536)
     assert o.stats()["max_segs"] > 1534
     assert (d.statuses() == MTE_E_CAPACITY).all()
+
+
+@pytest.mark.gpu
+def test_gpu_stats_off_same_result():
+    s = gen.generate(3, n_docs=80, ops_per_doc=2000)
+    on = DeviceEngine(s["n_keys"])
+    on.load_docs(s["inits"], s["init_text"])
+    on.apply_batch(s["batch"])
+    off = DeviceEngine(s["n_keys"])
+    off.set_stats(False)
+    off.load_docs(s["inits"], s["init_text"])
+    off.apply_batch(s["batch"])
+    np.testing.assert_array_equal(off.digest(), on.digest())
+    np.testing.assert_array_equal(off.statuses(), on.statuses())
+    assert on.stats()["ops_applied"] == int(s["batch"]["op_offsets"][-1])
+    assert off.stats()["ops_applied"] == 0
