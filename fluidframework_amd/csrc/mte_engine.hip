@@ -56,61 +56,30 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
   for (uint32_t k = 0; k < n_keys; k++) soa.props[k * soa.plane_stride + i] = init_props[(size_t)d * MTE_MAX_KEYS + k];
 }
 
-// Compile the batch's op records into the 64-byte device records the replay
-// kernels stage through LDS (mte_kernels.h): insert text offsets rebased onto
-// the ctx arena, the new segment's meta word, and the first two property
-// entries of the op's propset inlined.  Runs once per mte_submit, one thread
-// per record; kRecPad NOOP records follow the last one.
-__global__ void compile_kernel(const mte_op* __restrict__ ops, uint64_t n_ops, const mte_propset* __restrict__ ps,
-                               const mte_prop* __restrict__ pe, uint32_t n_keys, uint32_t text_base,
-                               uint4* __restrict__ recs) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_ops + kRecPad) return;
-  uint32_t w[16] = {0, 0, 0, MTE_OP_NOOP, 0, 0, 0, 0, kNoKey | (kNoKey << 8), 0, 0, MTE_NO_PROPS, 0, 0, 0, 0};
-  if (i < n_ops) {
-    const mte_op o = ops[i];
-    w[0] = (uint32_t)o.seq;
-    w[1] = (uint32_t)o.ref_seq;
-    w[2] = (uint32_t)o.min_seq;
-    w[3] = (uint32_t)o.type | ((uint32_t)o.client << 8) | ((uint32_t)o.flags << 16);
-    w[4] = (uint32_t)o.pos1;
-    w[5] = (uint32_t)o.pos2;
-    uint32_t psi = MTE_NO_PROPS;
-    if (o.type == MTE_OP_INSERT) {
-      const bool marker = (o.flags & MTE_F_MARKER) != 0;
-      w[5] = marker ? 1u : (uint32_t)o.pos2;
-      w[6] = marker ? 0u : text_base + o.a;
-      w[7] = ((uint32_t)o.client + 1u) | ((marker ? 1u + (uint32_t)o.pos2 : 0u) << 8);
-      psi = o.b;
-      if (psi != MTE_NO_PROPS) w[3] |= kFlagHasProps << 16;
-    } else if (o.type == MTE_OP_ANNOTATE) {
-      psi = o.a;
-    }
-    w[11] = psi;
-    if (psi != MTE_NO_PROPS) {
-      const mte_propset s = ps[psi];
-      uint32_t k0 = kNoKey, k1 = kNoKey, nw = 0;
-      for (uint32_t t = 0; t < s.count; t++) {
-        const mte_prop p = pe[s.first + t];
-        const bool ok = p.key < n_keys;
-        nw += ok ? 1u : 0u;
-        if (t == 0) {
-          k0 = ok ? p.key : kNoKey;
-          w[9] = p.value;
-        } else if (t == 1) {
-          k1 = ok ? p.key : kNoKey;
-          w[10] = p.value;
-        }
-      }
-      w[8] = k0 | (k1 << 8) | ((s.count > 2 ? 1u : 0u) << 16);
-      w[12] = nw;
+// Compile the batch's property sets into the 32-byte records the replay
+// kernels fetch with one scalar load (mte_kernels.h): the first two entries
+// inlined, the count of keys < n_keys.  One thread per set; runs at the start
+// of every mte_run (inside the timed region).
+__global__ void props_kernel(const mte_propset* __restrict__ ps, uint32_t n_ps, const mte_prop* __restrict__ pe,
+                             uint32_t n_keys, uint4* __restrict__ cps) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_ps) return;
+  const mte_propset s = ps[i];
+  uint32_t k0 = kNoKey, k1 = kNoKey, v0 = 0, v1 = 0, nw = 0;
+  for (uint32_t t = 0; t < s.count; t++) {
+    const mte_prop p = pe[s.first + t];
+    const bool ok = p.key < n_keys;
+    nw += ok ? 1u : 0u;
+    if (t == 0) {
+      k0 = ok ? p.key : kNoKey;
+      v0 = p.value;
+    } else if (t == 1) {
+      k1 = ok ? p.key : kNoKey;
+      v1 = p.value;
     }
   }
-  uint4* r = recs + 4 * i;
-  r[0] = make_uint4(w[0], w[1], w[2], w[3]);
-  r[1] = make_uint4(w[4], w[5], w[6], w[7]);
-  r[2] = make_uint4(w[8], w[9], w[10], w[11]);
-  r[3] = make_uint4(w[12], w[13], w[14], w[15]);
+  cps[2 * i] = make_uint4(k0 | (k1 << 8) | ((s.count > 2 ? 1u : 0u) << 16), v0, v1, nw);
+  cps[2 * i + 1] = make_uint4(0, 0, 0, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -265,8 +234,8 @@ struct mte_ctx {
   // batch
   mte_op* d_ops = nullptr;
   uint64_t ops_cap = 0, n_ops = 0;
-  uint4* d_recs = nullptr;  // compiled records, 4 x uint4 each
-  uint64_t recs_cap = 0;
+  uint4* d_cps = nullptr;  // compiled propsets, 2 x uint4 each (props_kernel)
+  uint64_t cps_cap = 0, n_propsets = 0;
   uint32_t* d_pairs = nullptr;  // pass-1 doc pairs
   uint32_t n_pairs = 0;
   uint64_t* d_off = nullptr;
@@ -421,7 +390,7 @@ int mte_destroy(mte_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   free_docs(c);
-  void* ps[] = {c->arena, c->d_ops, c->d_recs, c->d_off, c->d_ps, c->d_pe, c->d_pow};
+  void* ps[] = {c->arena, c->d_ops, c->d_cps, c->d_off, c->d_ps, c->d_pe, c->d_pow};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -541,7 +510,10 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
   c->h_arena.insert(c->h_arena.end(), b->text, b->text + b->text_units);
   c->batch_text_base = (uint32_t)c->arena_n;
   c->arena_n += b->text_units;
-  if ((rc = grow(c, &c->d_ops, &c->ops_cap, b->n_ops + 1))) return rc;
+  // the replay kernels read the records in place; kRecPad zeroed records
+  // follow the last one for the L2 prefetch that runs ahead
+  if ((rc = grow(c, &c->d_ops, &c->ops_cap, b->n_ops + kRecPad))) return rc;
+  HIPCHK(c, hipMemsetAsync(c->d_ops + b->n_ops, 0, kRecPad * sizeof(mte_op), c->stream));
   if ((rc = grow(c, &c->d_off, &c->off_cap, (uint64_t)b->n_docs + 1))) return rc;
   if ((rc = grow(c, &c->d_ps, &c->ps_cap, (uint64_t)b->n_propsets + 1))) return rc;
   if ((rc = grow(c, &c->d_pe, &c->pe_cap, (uint64_t)b->n_props + 1))) return rc;
@@ -551,16 +523,10 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
     HIPCHK(c, hipMemcpyAsync(c->d_ps, b->propsets, b->n_propsets * sizeof(mte_propset), hipMemcpyHostToDevice, c->stream));
   if (b->n_props)
     HIPCHK(c, hipMemcpyAsync(c->d_pe, b->props, b->n_props * sizeof(mte_prop), hipMemcpyHostToDevice, c->stream));
-  // compile the records (one pass over the batch, HBM-bound)
-  if ((rc = grow(c, &c->d_recs, &c->recs_cap, 4 * (b->n_ops + kRecPad)))) return rc;
-  {
-    const uint64_t nthr = b->n_ops + kRecPad;
-    hipLaunchKernelGGL(compile_kernel, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, c->stream, c->d_ops,
-                       b->n_ops, c->d_ps, c->d_pe, c->n_keys, c->batch_text_base, c->d_recs);
-    HIPCHK(c, hipGetLastError());
-  }
+  if ((rc = grow(c, &c->d_cps, &c->cps_cap, 2 * ((uint64_t)b->n_propsets + 1)))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));  // host buffers may be freed after return
   c->n_ops = b->n_ops;
+  c->n_propsets = b->n_propsets;
   c->submitted = true;
   return MTE_OK;
 }
@@ -570,6 +536,7 @@ int mte_run(mte_ctx* c) {
   if (!c->submitted) return set_err(c, MTE_E_STATE, "mte_run before mte_submit");
   if (!c->n_docs) return MTE_OK;
   HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));  // kernel_ms covers every kernel of the run
   hipLaunchKernelGGL(begin_batch_kernel, dim3((c->n_docs + 255) / 256), dim3(256), 0, c->stream, c->hdr, c->stats,
                      c->n_docs);
   HIPCHK(c, hipGetLastError());
@@ -579,15 +546,21 @@ int mte_run(mte_ctx* c) {
   a.stride = c->soa.plane_stride;
   a.cap = c->cap;
   a.n_docs = c->n_docs;
-  a.recs = c->d_recs;
+  a.recs = reinterpret_cast<const uint4*>(c->d_ops);
+  a.cps = c->d_cps;
   a.op_off = c->d_off;
   a.ps = c->d_ps;
   a.pe = c->d_pe;
   a.n_keys = c->n_keys;
+  a.text_base = c->batch_text_base;
   a.stats = c->stats;
   a.pair_docs = c->d_pairs;
   a.n_pairs = c->n_pairs;
-  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  if (c->n_propsets) {
+    hipLaunchKernelGGL(props_kernel, dim3((uint32_t)((c->n_propsets + 255) / 256)), dim3(256), 0, c->stream, c->d_ps,
+                       (uint32_t)c->n_propsets, c->d_pe, c->n_keys, c->d_cps);
+    HIPCHK(c, hipGetLastError());
+  }
   int rc;
   if (c->stats_on)
     rc = c->kt == 0 ? launch_replay<0, true>(c, a) : (c->kt == 4 ? launch_replay<4, true>(c, a) : launch_replay<8, true>(c, a));

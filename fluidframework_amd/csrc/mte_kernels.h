@@ -54,16 +54,14 @@ struct SegSoA {
   uint64_t plane_stride;
 };
 
-// ---- compiled op record (64 B), built from mte_op + propsets at mte_submit ----
-// w0 seq | w1 ref_seq | w2 min_seq | w3 type | client << 8 | flags << 16
-// w4 pos1 | w5 pos2 (insert: segment length, markers 1) | w6 insert: arena offset of the text
-// w7 insert: meta of the new segment | w8 k0 | k1 << 8 | (count > 2) << 16 (key 0xff = none)
-// w9 v0 | w10 v1 | w11 propset index (MTE_NO_PROPS) | w12 keys < n_keys in the set | w13-15 0
-constexpr int kRecWords = 16;
+// ---- op records --------------------------------------------------------------
+// The replay kernels read the submitted mte_op records (32 B = one s_load_dwordx8)
+// in place: w0 seq | w1 ref_seq | w2 min_seq | w3 type | client << 8 | flags << 16
+// | w4 pos1 | w5 pos2 | w6 a | w7 b (include/mte.h).  Property sets are compiled
+// per run into 32-B records (props_kernel): w0 k0 | k1 << 8 | (count > 2) << 16
+// (key 0xff = none) | w1 v0 | w2 v1 | w3 keys < n_keys in the set | w4-7 0.
 constexpr uint32_t kNoKey = 0xffu;
-constexpr uint32_t kRecPad = 128;  // NOOP records after the last one (prefetch reads run ahead)
-// internal op flag (high bit of mte_op.flags, set by compile_kernel): insert with props
-constexpr uint32_t kFlagHasProps = 0x8000u;
+constexpr uint32_t kRecPad = 512;  // zeroed records after the last op (L2 prefetch runs ahead)
 
 struct ReplayArgs {
   DocHdr* hdr;
@@ -71,11 +69,13 @@ struct ReplayArgs {
   uint64_t stride;
   uint32_t cap;
   uint32_t n_docs;
-  const uint4* recs;       // compiled records, 4 x uint4 each (+ 2 chunks of padding)
+  const uint4* recs;       // the batch's mte_op records, 2 x uint4 each (+ kRecPad)
+  const uint4* cps;        // compiled propsets, 2 x uint4 each
   const uint64_t* op_off;  // n_docs + 1
   const mte_propset* ps;
   const mte_prop* pe;
   uint32_t n_keys;
+  uint32_t text_base;      // arena offset of the batch's text (mte_op.a of inserts)
   unsigned long long* stats;  // n_docs * kNumStats
   const uint32_t* pair_docs;  // pair kernel: doc index per pair half (2 per pair)
   uint32_t n_pairs;

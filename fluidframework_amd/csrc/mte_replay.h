@@ -44,7 +44,7 @@ struct DocRun {
   int32_t status;
   uint32_t flags;
   bool running;
-  const uint4* recp;  // the doc's first compiled record (4 x uint4 each)
+  const uint4* recp;  // the doc's first op record (2 x uint4 each)
   uint32_t k, k1;     // current op, end
 };
 
@@ -62,21 +62,23 @@ typedef int32_t s8v __attribute__((ext_vector_type(8)));
 typedef const __attribute__((address_space(4))) s8v* cs8p;
 
 __device__ __forceinline__ s8v sload8(const uint4* p) { return *(cs8p)(const void*)p; }
-__device__ __forceinline__ s8v sload8_props(const uint4* p) { return *(cs8p)(const void*)(p + 2); }  // words 8..15
+// compiled propset `psi` (mte_kernels.h)
+__device__ __forceinline__ s8v sload_props(const ReplayArgs& a, uint32_t psi) { return sload8(a.cps + 2 * psi); }
 __device__ __forceinline__ void swait(s8v&) {}
 
-// L2 prefetch: lane l touches record `from + l` (one 64-B line each).  The
-// loaded word is folded into `sink` one prefetch later (64 ops on), so the
-// wait for it never stalls.
+// L2 prefetch: lane l touches record `from + 4 l` (one 128-B line per lane,
+// 256 records).  The loaded word is folded into `sink` one prefetch later, so
+// the wait for it never stalls.
+constexpr uint32_t kTouchSpan = 4 * kWave;
 __device__ __forceinline__ void touch_records(const DocRun& D, uint32_t from, uint32_t& pending, uint32_t& sink) {
   sink ^= pending;
-  const uint32_t r = from + (uint32_t)lane_id();
-  pending = r < D.k1 + 64 ? reinterpret_cast<const uint32_t*>(D.recp + 4 * r)[0] : 0u;
+  const uint32_t r = from + 4u * (uint32_t)lane_id();
+  pending = r < D.k1 + kRecPad ? reinterpret_cast<const uint32_t*>(D.recp + 2 * r)[0] : 0u;
 }
 
 // ISegment.addProperties for a remote op (segmentPropertiesManager.ts:63-151):
 // entries in order, value 0 (null) deletes.  The first two entries come with
-// the compiled record; longer sets are read here.  Applied to the slots with
+// the compiled propset record; longer sets are read here.  Applied to the slots with
 // sel[j] set (E slots per lane, K planes); no lambdas, so the register arrays
 // never need an address.
 template <int E, int K>
@@ -269,8 +271,8 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
 
   // ---- op record: words 0..7 were prefetched into `cur` -------------------
   const s8v op = cur;
-  const uint4* rec = D.recp + 4 * D.k;
-  if (D.k + 1 < D.k1) cur = sload8(rec + 4);  // next op, in flight during this one
+  const uint4* rec = D.recp + 2 * D.k;
+  if (D.k + 1 < D.k1) cur = sload8(rec + 2);  // next op, in flight during this one
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
@@ -296,7 +298,7 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
     if (ins) {
       // Client.applyInsertOp -> MergeTree.insertSegments (client.ts:470-505,
       // mergeTree.ts:1394-1422): ensureIntervalBoundary, then insertingWalk
-      const int32_t nlen = pos2;
+      const int32_t nlen = (flags & MTE_F_MARKER) ? 1 : pos2;  // markers have length 1
       int32_t off = 0;
       const int xs = find_split<E>(L, P, pos1, &off);
       if (xs >= 0) {
@@ -390,21 +392,25 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
     if (g >= 0) {
       // the new segment (mergeTree.ts:1599-1611, textSegment.ts:40-48,
       // mergeTreeNodes.ts:602-609)
-      const uint32_t meta = (uint32_t)op[7], toff = (uint32_t)op[6];
+      const bool marker = (flags & MTE_F_MARKER) != 0;
+      const uint32_t meta = (c + 1u) | (marker ? (1u + (uint32_t)pos2) << 8 : 0u);
+      const uint32_t toff = marker ? 0u : a.text_base + (uint32_t)op[6];
+      const uint32_t psi = (uint32_t)op[7];
       uint32_t pr[K > 0 ? K : 1][1];
       const bool one[1] = {true};
 #pragma unroll
       for (int kk = 0; kk < (K > 0 ? K : 1); kk++) pr[kk][0] = 0;
-      if (K > 0 && (flags & kFlagHasProps)) {
-        const s8v q2 = sload8_props(rec);  // same 64-B line as `op`: a scalar-cache hit
-        apply_props<1, K>(pr, one, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], (uint32_t)q2[3], a);
-        MTE_STAT(st[kStPwrites] += (uint32_t)q2[4];)
+      if (K > 0 && psi != MTE_NO_PROPS) {
+        const s8v q2 = sload_props(a, psi);
+        apply_props<1, K>(pr, one, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], psi, a);
+        MTE_STAT(st[kStPwrites] += (uint32_t)q2[3];)
       }
-      MTE_STAT(if ((meta >> 8) == 0) st[kStUnits] += (uint32_t)pos2;)
+      MTE_STAT(if (!marker) st[kStUnits] += (uint32_t)pos2;)
+      const int32_t nlen = marker ? 1 : pos2;
 #pragma unroll
       for (int jj = 0; jj < E; jj++) {
         const bool at = base + jj == g;
-        R.len[jj] = at ? pos2 : R.len[jj];
+        R.len[jj] = at ? nlen : R.len[jj];
         R.seq[jj] = at ? s : R.seq[jj];
         R.rseq[jj] = at ? kNone : R.rseq[jj];
         R.rmask[jj] = at ? 0u : R.rmask[jj];
@@ -436,15 +442,16 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
         }
       } else if (cnt > 0) {
         // PropertiesManager.addProperties (segmentPropertiesManager.ts:63-151)
-        const s8v q2 = sload8_props(rec);
+        const uint32_t psi = (uint32_t)op[6];
+        const s8v q2 = sload_props(a, psi);
         if (flags & MTE_F_REWRITE) {
 #pragma unroll
           for (int kk = 0; kk < K; kk++)
 #pragma unroll
             for (int jj = 0; jj < E; jj++) R.pr[kk][jj] = in[jj] ? 0u : R.pr[kk][jj];
         }
-        apply_props<E, K>(R.pr, in, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], (uint32_t)q2[3], a);
-        MTE_STAT(st[kStPwrites] += cnt * (uint32_t)q2[4];)
+        apply_props<E, K>(R.pr, in, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], psi, a);
+        MTE_STAT(st[kStPwrites] += cnt * (uint32_t)q2[3];)
       }
     }
   } else if (type != MTE_OP_NOOP) {
@@ -521,7 +528,7 @@ __device__ __forceinline__ void run_init(DocRun& D, const ReplayArgs& a, int doc
   D.cur_seq = h.cur_seq;
   D.status = h.status;
   D.flags = h.flags;
-  D.recp = a.recs + 4 * kb;
+  D.recp = a.recs + 2 * kb;
   D.k = h.resume;
   D.k1 = (uint32_t)(a.op_off[doc + 1] - kb);
   if (h.status != 0) return;
@@ -579,11 +586,11 @@ __device__ __forceinline__ void burst_run(DocRun& D, const ReplayArgs& a, uint32
   uint32_t st[kNumStats] = {0, 0, 0, 0, 0, 0};
   load_regs<E, K>(R, D, a);
   const uint32_t kend = D.k1 - D.k > limit ? D.k + limit : D.k1;
-  s8v cur = sload8(D.recp + 4 * D.k);
+  s8v cur = sload8(D.recp + 2 * D.k);
   uint32_t pending = 0, sink = 0;
   touch_records(D, D.k + 16, pending, sink);
   while (D.running) {
-    if ((D.k & 63u) == 0) touch_records(D, D.k + 64, pending, sink);
+    if ((D.k & (kTouchSpan / 2 - 1)) == 0) touch_records(D, D.k + kTouchSpan / 2, pending, sink);
     const int rc = doc_step<E, K, S>(R, D, st, cur, a, zlds, emin);
     if (step_done(D, rc) || D.k >= kend) break;
   }
@@ -632,7 +639,7 @@ __device__ __forceinline__ bool run_from_lds(DocRun& D, const DocHdr* hl, int do
   D.flags = uni(h1.x);
   D.k = uni(h1.y);
   const uint64_t kb = a.op_off[doc];
-  D.recp = a.recs + 4 * kb;
+  D.recp = a.recs + 2 * kb;
   D.k1 = (uint32_t)(a.op_off[doc + 1] - kb);
   D.running = D.status == 0 && D.k < D.k1 && !(D.flags & kHdrNeedsEsc);
   return D.running;

@@ -65,8 +65,8 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   const int nplanes = kFieldPlanes + K;
 
   const s8v op = cur;
-  const uint4* rec = D.recp + 4 * D.k;
-  if (D.k + 1 < D.k1) cur = sload8(rec + 4);
+  const uint4* rec = D.recp + 2 * D.k;
+  if (D.k + 1 < D.k1) cur = sload8(rec + 2);
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
@@ -76,6 +76,8 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   const int32_t s = op[0], r = op[1], msn = op[2];
   const int32_t pos1 = op[4], pos2 = op[5];
   const bool ins = type == MTE_OP_INSERT;
+  const bool marker = ins && (flags & MTE_F_MARKER) != 0;
+  const int32_t nlen = marker ? 1 : pos2;  // insert: length of the new segment
   const bool rng = type == MTE_OP_REMOVE || type == MTE_OP_ANNOTATE;
   const bool newcalc = (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
   int n = D.n;
@@ -133,7 +135,6 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
     int t1 = INT32_MAX, t2 = INT32_MAX, g = -1;
     SplitPatch pa{-1, -1, 0, 0, 0u, 0}, pb{-1, -1, 0, 0, 0u, 0};
     if (ins) {
-      const int32_t nlen = pos2;
       if (xa >= 0) {
         pa = SplitPatch{xa, nlen > 0 ? xa + 2 : xa + 1, oa, lena, toffa, pos1};
         t1 = xa;
@@ -219,12 +220,12 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
         }
       }
       if (g >= 0) {
-        pl[g] = (uint32_t)pos2;
+        pl[g] = (uint32_t)nlen;
         pl[sd + g] = (uint32_t)s;
         pl[2 * sd + g] = (uint32_t)kNone;
         pl[3 * sd + g] = 0u;
-        pl[4 * sd + g] = (uint32_t)op[7];
-        pl[5 * sd + g] = (uint32_t)op[6];
+        pl[4 * sd + g] = (c + 1u) | (marker ? (1u + (uint32_t)pos2) << 8 : 0u);
+        pl[5 * sd + g] = marker ? 0u : a.text_base + (uint32_t)op[6];
       }
     }
     if (g >= 0) {
@@ -232,22 +233,23 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
       const bool one[1] = {true};
 #pragma unroll
       for (int kk = 0; kk < (K > 0 ? K : 1); kk++) pr[kk][0] = 0;
-      if (K > 0 && (flags & kFlagHasProps)) {
-        const s8v q2 = sload8_props(rec);
-        apply_props<1, K>(pr, one, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], (uint32_t)q2[3], a);
-        MTE_STAT(st[kStPwrites] += (uint32_t)q2[4];)
+      const uint32_t psi = (uint32_t)op[7];
+      if (K > 0 && psi != MTE_NO_PROPS) {
+        const s8v q2 = sload_props(a, psi);
+        apply_props<1, K>(pr, one, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], psi, a);
+        MTE_STAT(st[kStPwrites] += (uint32_t)q2[3];)
       }
       if (l == 0) {
 #pragma unroll
         for (int kk = 0; kk < K; kk++) pl[(kFieldPlanes + kk) * sd + g] = pr[kk][0];
       }
-      if (((uint32_t)op[7] >> 8) == 0) st[kStUnits] += (uint32_t)pos2;
+      MTE_STAT(if (!marker) st[kStUnits] += (uint32_t)pos2;)
     }
     vm_drain();
     // ---- C: mark [start, end) on the new layout ---------------------------------
     if (rng && pos2 > pos1) {
       s8v q2 = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (type == MTE_OP_ANNOTATE) q2 = sload8_props(rec);
+      if (type == MTE_OP_ANNOTATE) q2 = sload_props(a, (uint32_t)op[6]);
       const bool rem = type == MTE_OP_REMOVE;
       int32_t cy = 0;
       uint32_t cnt_all = 0;
@@ -289,7 +291,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
               pr[kk][j] = i < n ? ld_l2(pl + (kFieldPlanes + kk) * sd + i) : 0u;
               if (flags & MTE_F_REWRITE) pr[kk][j] = in[j] ? 0u : pr[kk][j];
             }
-          apply_props<E, K>(pr, in, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], (uint32_t)q2[3], a);
+          apply_props<E, K>(pr, in, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], (uint32_t)op[6], a);
 #pragma unroll
           for (int kk = 0; kk < K; kk++)
 #pragma unroll
@@ -298,7 +300,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
         }
       }
       MTE_STAT(st[kStWritten] += cnt_all;)
-      if (type == MTE_OP_ANNOTATE) st[kStPwrites] += cnt_all * (uint32_t)q2[4];
+      if (type == MTE_OP_ANNOTATE) st[kStPwrites] += cnt_all * (uint32_t)q2[3];
       vm_drain();
     }
   }
@@ -367,7 +369,7 @@ __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
   run_init(D, a, doc, true);
   uint32_t st[kNumStats] = {0, 0, 0, 0, 0, 0};
   if (D.running) {
-    s8v cur = sload8(D.recp + 4 * D.k);
+    s8v cur = sload8(D.recp + 2 * D.k);
     while (D.running) {
       const int rc = stream_step<K, S>(D, st, cur, a, zlds_all[w]);
       if (rc < 0) {
