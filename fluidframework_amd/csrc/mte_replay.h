@@ -146,8 +146,33 @@ __device__ __forceinline__ void shift_apply(T (&F)[E], const uint32_t (&p1)[NF],
 // plane.  The cross-lane moves of all planes are issued first and the selects
 // after, so no DPP read waits on the VALU write just before it (a chained
 // move per plane costs two hazard nops each).
+template <int E, typename T>
+__device__ __forceinline__ void shift_perm(T (&F)[E], int addr) {
+  F[0] = (T)__builtin_amdgcn_ds_bpermute(addr, (int32_t)F[0]);
+}
+
 template <int E, int K, bool LP>
 __device__ __forceinline__ void shift_all(Regs<E, K>& R, int32_t (&L)[E], int32_t (&P)[E], int t1, int t2) {
+  if constexpr (E == 1) {
+    // one slot per lane: lane l pulls lane l - d(l) through the LDS crossbar
+    // (ds_bpermute: one LDS-pipe instruction per plane instead of two DPP
+    // moves and two selects on the VALU)
+    const int l = lane_id();
+    const int addr = (l - (l > t1 ? 1 : 0) - (l > t2 ? 1 : 0)) << 2;
+    shift_perm<E>(R.len, addr);
+    shift_perm<E>(R.seq, addr);
+    shift_perm<E>(R.rseq, addr);
+    shift_perm<E>(R.rmask, addr);
+    shift_perm<E>(R.meta, addr);
+    shift_perm<E>(R.toff, addr);
+#pragma unroll
+    for (int k = 0; k < K; k++) shift_perm<E>(R.pr[k], addr);
+    if constexpr (LP) {
+      shift_perm<E>(L, addr);
+      shift_perm<E>(P, addr);
+    }
+    return;
+  }
   constexpr int NF = kFieldPlanes + K + (LP ? 2 : 0);
   uint32_t last[NF], last2[NF];
   shift_grab<E, NF>(last, last2, 0, R.len);
@@ -248,6 +273,23 @@ struct SplitPatch {
     __VA_ARGS__         \
   }
 
+// The collab-window error of an applied op, checked in the reference's order:
+// completeAndLogOp (client.ts:525-528), then updateSeqNumbers (937-945) ->
+// setMinSeq (mergeTree.ts:1078-1084), which sets currentSeq before its asserts.
+__device__ __forceinline__ int window_error(DocRun& D, bool live, bool end, int32_t s, int32_t msn) {
+  if (live) {
+    if (!(D.cur_seq < s)) return MTE_E_SEQ_ORDER;
+    if (!(D.min_seq <= msn)) return MTE_E_MSN_ORDER;
+  }
+  if (end) {
+    if (!(D.cur_seq <= s)) return MTE_E_SEQ_ORDER;
+    D.cur_seq = s;
+    if (!(msn <= s)) return MTE_E_MSN_GT_SEQ;
+    if (!(D.min_seq <= msn)) return MTE_E_MSN_ORDER;
+  }
+  return MTE_E_STATE;  // unreachable: the caller saw a violation
+}
+
 // One op record of one document: Client.applyMsg -> applyRemoteOp ->
 // insertSegments / markRangeRemoved / annotateRange -> updateSeqNumbers
 // (client.ts:918-945).  Returns 0 (applied), 1 (re-pick the register tier
@@ -272,7 +314,9 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
   // ---- op record: words 0..7 were prefetched into `cur` -------------------
   const s8v op = cur;
   const uint4* rec = D.recp + 2 * D.k;
-  if (D.k + 1 < D.k1) cur = sload8(rec + 2);  // next op, in flight during this one
+  // next op, in flight during this one; past a doc's last op this reads the
+  // next doc's first record or the zeroed kRecPad tail (never used)
+  cur = sload8(rec + 2);
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
@@ -460,16 +504,15 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
   D.n = n;
   D.k++;
 
-  if (type != MTE_OP_NOOP) {  // Client.completeAndLogOp (client.ts:525-528)
-    if (!(D.cur_seq < s)) return MTE_E_SEQ_ORDER;
-    if (!(D.min_seq <= msn)) return MTE_E_MSN_ORDER;
-  }
-  if (flags & MTE_F_MSG_END) {
-    // updateSeqNumbers (client.ts:937-945) -> setMinSeq (mergeTree.ts:1077-1093)
-    if (!(D.cur_seq <= s)) return MTE_E_SEQ_ORDER;
+  // Client.completeAndLogOp (client.ts:525-528) and updateSeqNumbers
+  // (client.ts:937-945) -> setMinSeq (mergeTree.ts:1077-1093): one combined
+  // test on the fast path, the exact code (in the reference's order) after
+  const bool live = type != MTE_OP_NOOP, end = (flags & MTE_F_MSG_END) != 0;
+  const bool bad = (live & (s <= D.cur_seq)) | (end & (s < D.cur_seq)) | ((live | end) & (msn < D.min_seq)) |
+                   (end & (msn > s));
+  if (bad) return window_error(D, live, end, s, msn);
+  if (end) {
     D.cur_seq = s;
-    if (!(msn <= s)) return MTE_E_MSN_GT_SEQ;
-    if (!(D.min_seq <= msn)) return MTE_E_MSN_ORDER;
     if (msn > D.min_seq) {
       D.min_seq = msn;
       // zamboni: drop tombstones with removedSeq <= minSeq (padding included)
@@ -588,12 +631,25 @@ __device__ __forceinline__ void burst_run(DocRun& D, const ReplayArgs& a, uint32
   const uint32_t kend = D.k1 - D.k > limit ? D.k + limit : D.k1;
   s8v cur = sload8(D.recp + 2 * D.k);
   uint32_t pending = 0, sink = 0;
-  touch_records(D, D.k + 16, pending, sink);
-  while (D.running) {
-    if ((D.k & (kTouchSpan / 2 - 1)) == 0) touch_records(D, D.k + kTouchSpan / 2, pending, sink);
+  // L2 prefetch of the records: short bursts (pass 1) touch the span after
+  // this burst once, at its start (the first burst its own span too); long
+  // runs touch ahead every kTouchSpan / 2 ops
+  const bool per_burst = limit <= kTouchSpan / 2;
+  if (per_burst) touch_records(D, D.k == 0 ? 0u : D.k + limit, pending, sink);
+  else touch_records(D, D.k + 16, pending, sink);
+  for (;;) {
+    if (!per_burst && (D.k & (kTouchSpan / 2 - 1)) == 0) touch_records(D, D.k + kTouchSpan / 2, pending, sink);
     const int rc = doc_step<E, K, S>(R, D, st, cur, a, zlds, emin);
-    if (step_done(D, rc) || D.k >= kend) break;
+    if (rc != 0) {
+      if (rc < 0) {
+        D.status = rc;
+        D.running = false;
+      }
+      break;
+    }
+    if (D.k >= kend) break;
   }
+  if (D.k >= D.k1) D.running = false;
   swait(cur);  // no scalar load may be left in flight
   store_regs<E, K>(R, D, a);
   if constexpr (S) run_flush_stats(D, st, a);
