@@ -315,8 +315,13 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
   const s8v op = cur;
   const uint4* rec = D.recp + 2 * D.k;
   // next op, in flight during this one; past a doc's last op this reads the
-  // next doc's first record or the zeroed kRecPad tail (never used)
-  cur = sload8(rec + 2);
+  // next doc's first record or the zeroed kRecPad tail (never used).  Scalar
+  // loads complete out of order, so a wait for `op` is an lgkmcnt(0) that
+  // would also wait for this prefetch: the empty asm takes `op` as an input
+  // and hands the prefetch its address, so the wait lands before the issue.
+  uint64_t next = reinterpret_cast<uint64_t>(rec + 2);
+  asm volatile("" : "+s"(next) : "s"(op));
+  cur = sload8(reinterpret_cast<const uint4*>(next));
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
@@ -557,6 +562,12 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
   return 0;
 }
 
+}  // namespace mte
+
+#include "mte_step1.h"
+
+namespace mte {
+
 __device__ __forceinline__ void run_init(DocRun& D, const ReplayArgs& a, int doc, bool escalated_only) {
   D.doc = doc;
   D.running = false;
@@ -639,7 +650,9 @@ __device__ __forceinline__ void burst_run(DocRun& D, const ReplayArgs& a, uint32
   else touch_records(D, D.k + 16, pending, sink);
   for (;;) {
     if (!per_burst && (D.k & (kTouchSpan / 2 - 1)) == 0) touch_records(D, D.k + kTouchSpan / 2, pending, sink);
-    const int rc = doc_step<E, K, S>(R, D, st, cur, a, zlds, emin);
+    int rc;
+    if constexpr (E == 1) rc = doc_step1<K, S>(R, D, st, cur, a, zlds);
+    else rc = doc_step<E, K, S>(R, D, st, cur, a, zlds, emin);
     if (rc != 0) {
       if (rc < 0) {
         D.status = rc;
