@@ -651,7 +651,7 @@ __device__ __forceinline__ void burst_run(DocRun& D, const ReplayArgs& a, uint32
   for (;;) {
     if (!per_burst && (D.k & (kTouchSpan / 2 - 1)) == 0) touch_records(D, D.k + kTouchSpan / 2, pending, sink);
     int rc;
-    if constexpr (E == 1) rc = doc_step1<K, S>(R, D, st, cur, a, zlds);
+    if constexpr (E <= 4) rc = doc_step_v<E, K, S>(R, D, st, cur, a, zlds, emin);
     else rc = doc_step<E, K, S>(R, D, st, cur, a, zlds, emin);
     if (rc != 0) {
       if (rc < 0) {

@@ -1,15 +1,16 @@
-// mte_step1.h — the per-op step of the one-slot-per-lane tier (E == 1,
-// documents of <= 62 segments: most of the ops of a conflict-farm batch).
+// mte_step1.h — the per-op step of the pass-1 register tiers (E <= 4 slots
+// per lane, documents of <= 254 segments: nearly every op of a conflict-farm
+// batch).
 //
 // Same semantics as doc_step (mte_replay.h, which cites the reference for
-// every rule), but the split / insert decisions stay per lane instead of
-// going through scalar lookups: a lane learns "my slot is after the split
-// leaf" from the popcount of the candidate ballot below it (v_mbcnt), "I am
-// the slot right after it" from its neighbour's flag (DPP), and every
-// half of a split leaf is rebuilt from the values the lane pulled in the
-// shift.  The scalar unit — one per CU, shared by four SIMDs — then only
-// decodes the op, branches on the op type and on "is there a split", and
-// keeps the collab window; the rest is VALU work on each SIMD.
+// every rule), but the split / insert decisions stay per slot instead of
+// going through scalar lookups: a slot learns "I am after the split leaf"
+// from the popcount of the candidate ballot in the lanes below (v_mbcnt) plus
+// its own lane's earlier slots, "I am right after it" from its neighbour's
+// flag, and every piece of a split leaf is rebuilt from the values the slot
+// pulled in the shift.  The scalar unit — one per CU, shared by four SIMDs —
+// then only decodes the op, branches on the op type and on "is there a
+// split", and keeps the collab window; the rest is VALU work on each SIMD.
 #pragma once
 
 #include "mte_kernels.h"
@@ -21,29 +22,98 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// A[j] = some flagged slot lies before slot j (in this lane or a lower one)
+template <int E>
+__device__ __forceinline__ void after_flag(const bool (&F)[E], bool (&A)[E]) {
+  bool any = false;
+#pragma unroll
+  for (int j = 0; j < E; j++) any = any || F[j];
+  bool run = lanes_below(__ballot(any)) != 0;
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    A[j] = run;
+    run = run || F[j];
+  }
+}
+
+// F1[j] / F2[j] = the flag of the slot 1 / 2 positions before slot j
+template <int E>
+__device__ __forceinline__ void prev_flags(const bool (&F)[E], bool (&F1)[E], bool (&F2)[E]) {
+  const bool p1 = lane_prev(F[E - 1] ? 1 : 0) != 0;
+  bool p2;
+  if constexpr (E >= 2) p2 = lane_prev(F[E >= 2 ? E - 2 : 0] ? 1 : 0) != 0;
+  else p2 = lane_prev(p1 ? 1 : 0) != 0;
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    F1[j] = j >= 1 ? F[j >= 1 ? j - 1 : 0] : p1;
+    F2[j] = j >= 2 ? F[j >= 2 ? j - 2 : 0] : (j == 1 ? p1 : p2);
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ T perm1(T v, int addr) {
   return (T)__builtin_amdgcn_ds_bpermute(addr, (int32_t)v);
 }
 
-// new[l] = old[l - d(l)] for every plane; addr = (l - d(l)) * 4
-template <int K>
-__device__ __forceinline__ void shift1(Regs<1, K>& R, int addr) {
-  R.len[0] = perm1(R.len[0], addr);
-  R.seq[0] = perm1(R.seq[0], addr);
-  R.rseq[0] = perm1(R.rseq[0], addr);
-  R.rmask[0] = perm1(R.rmask[0], addr);
-  R.meta[0] = perm1(R.meta[0], addr);
-  R.toff[0] = perm1(R.toff[0], addr);
-#pragma unroll
-  for (int k = 0; k < K; k++) R.pr[k][0] = perm1(R.pr[k][0], addr);
+template <int E, typename T>
+__device__ __forceinline__ void perm_plane(T (&F)[E], int addr) {
+  F[0] = perm1(F[0], addr);
 }
 
-// the inserted segment at the lanes with `at` (mergeTree.ts:1599-1611,
+// new[i] = old[i - d(i)], d = g1 + g2 (g2 implies g1), for every plane and
+// the NX extra per-slot values X.  E == 1: one ds_bpermute per plane.  E > 1:
+// the two cross-lane moves of every plane first (DPP), then the selects.
+template <int E, int K, int NX>
+__device__ __forceinline__ void shift_v(Regs<E, K>& R, int32_t (&X)[NX > 0 ? NX : 1][E], const bool (&g1)[E],
+                                        const bool (&g2)[E]) {
+  if constexpr (E == 1) {
+    const int addr = (lane_id() - (g1[0] ? 1 : 0) - (g2[0] ? 1 : 0)) << 2;
+    perm_plane<E>(R.len, addr);
+    perm_plane<E>(R.seq, addr);
+    perm_plane<E>(R.rseq, addr);
+    perm_plane<E>(R.rmask, addr);
+    perm_plane<E>(R.meta, addr);
+    perm_plane<E>(R.toff, addr);
+#pragma unroll
+    for (int k = 0; k < K; k++) perm_plane<E>(R.pr[k], addr);
+#pragma unroll
+    for (int x = 0; x < NX; x++) perm_plane<E>(X[x], addr);
+  } else {
+    constexpr int NF = kFieldPlanes + K + NX;
+    uint32_t last[NF], last2[NF];
+    shift_grab<E, NF>(last, last2, 0, R.len);
+    shift_grab<E, NF>(last, last2, 1, R.seq);
+    shift_grab<E, NF>(last, last2, 2, R.rseq);
+    shift_grab<E, NF>(last, last2, 3, R.rmask);
+    shift_grab<E, NF>(last, last2, 4, R.meta);
+    shift_grab<E, NF>(last, last2, 5, R.toff);
+#pragma unroll
+    for (int k = 0; k < K; k++) shift_grab<E, NF>(last, last2, kFieldPlanes + k, R.pr[k]);
+#pragma unroll
+    for (int x = 0; x < NX; x++) shift_grab<E, NF>(last, last2, kFieldPlanes + K + x, X[x]);
+    uint32_t p1[NF], p2[NF];
+#pragma unroll
+    for (int f = 0; f < NF; f++) p1[f] = (uint32_t)lane_prev((int32_t)last[f]);
+#pragma unroll
+    for (int f = 0; f < NF; f++) p2[f] = (uint32_t)lane_prev((int32_t)last2[f]);
+    shift_apply<E, NF>(R.len, p1, p2, 0, g1, g2);
+    shift_apply<E, NF>(R.seq, p1, p2, 1, g1, g2);
+    shift_apply<E, NF>(R.rseq, p1, p2, 2, g1, g2);
+    shift_apply<E, NF>(R.rmask, p1, p2, 3, g1, g2);
+    shift_apply<E, NF>(R.meta, p1, p2, 4, g1, g2);
+    shift_apply<E, NF>(R.toff, p1, p2, 5, g1, g2);
+#pragma unroll
+    for (int k = 0; k < K; k++) shift_apply<E, NF>(R.pr[k], p1, p2, kFieldPlanes + k, g1, g2);
+#pragma unroll
+    for (int x = 0; x < NX; x++) shift_apply<E, NF>(X[x], p1, p2, kFieldPlanes + K + x, g1, g2);
+  }
+}
+
+// the inserted segment at the slots with `at` (mergeTree.ts:1599-1611,
 // textSegment.ts:40-48, mergeTreeNodes.ts:602-609)
-template <int K, bool S>
-__device__ __forceinline__ void put_new1(Regs<1, K>& R, bool at, const s8v& op, uint32_t c, uint32_t flags,
-                                         const ReplayArgs& a, uint32_t (&st)[kNumStats]) {
+template <int E, int K, bool S>
+__device__ __forceinline__ void put_new_v(Regs<E, K>& R, const bool (&at)[E], const s8v& op, uint32_t c,
+                                          uint32_t flags, const ReplayArgs& a, uint32_t (&st)[kNumStats]) {
   const int32_t s = op[0], pos2 = op[5];
   const bool marker = (flags & MTE_F_MARKER) != 0;
   const int32_t nlen = marker ? 1 : pos2;
@@ -60,21 +130,25 @@ __device__ __forceinline__ void put_new1(Regs<1, K>& R, bool at, const s8v& op, 
     MTE_STAT(st[kStPwrites] += (uint32_t)q2[3];)
   }
   MTE_STAT(if (!marker) st[kStUnits] += (uint32_t)pos2;)
-  R.len[0] = at ? nlen : R.len[0];
-  R.seq[0] = at ? s : R.seq[0];
-  R.rseq[0] = at ? kNone : R.rseq[0];
-  R.rmask[0] = at ? 0u : R.rmask[0];
-  R.meta[0] = at ? meta : R.meta[0];
-  R.toff[0] = at ? toff : R.toff[0];
 #pragma unroll
-  for (int kk = 0; kk < K; kk++) R.pr[kk][0] = at ? pr[kk][0] : R.pr[kk][0];
+  for (int j = 0; j < E; j++) {
+    R.len[j] = at[j] ? nlen : R.len[j];
+    R.seq[j] = at[j] ? s : R.seq[j];
+    R.rseq[j] = at[j] ? kNone : R.rseq[j];
+    R.rmask[j] = at[j] ? 0u : R.rmask[j];
+    R.meta[j] = at[j] ? meta : R.meta[j];
+    R.toff[j] = at[j] ? toff : R.toff[j];
+#pragma unroll
+    for (int kk = 0; kk < K; kk++) R.pr[kk][j] = at[j] ? pr[kk][0] : R.pr[kk][j];
+  }
 }
 
-template <int K, bool S>
-__device__ __forceinline__ int doc_step1(Regs<1, K>& R, DocRun& D, uint32_t (&st)[kNumStats], s8v& cur,
-                                         const ReplayArgs& a, uint32_t* zlds) {
+template <int E, int K, bool S>
+__device__ __forceinline__ int doc_step_v(Regs<E, K>& R, DocRun& D, uint32_t (&st)[kNumStats], s8v& cur,
+                                          const ReplayArgs& a, uint32_t* zlds, int emin) {
   const int l = lane_id();
-  const int lim = kWave < (int)a.cap ? kWave : (int)a.cap;
+  const int base = l * E;
+  const int lim = kWave * E < (int)a.cap ? kWave * E : (int)a.cap;
   if (D.n + 2 > lim) return 1;
   if constexpr (S) {
     if (st[kStOps] >= (1u << 20)) return 1;
@@ -98,113 +172,164 @@ __device__ __forceinline__ int doc_step1(Regs<1, K>& R, DocRun& D, uint32_t (&st
   if (type <= MTE_OP_ANNOTATE) {
     const int32_t r = op[1], pos1 = op[4], pos2 = op[5];
     MTE_STAT(st[kStScanned] += (uint32_t)n;)
-    int32_t L[1], P[1];
-    leaf_lengths<1, K>(R, r, c + 1, (int)c, D.min_seq, (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0, L);
-    const int32_t total = prefix<1>(L, P);
+    int32_t L[E], P[E];
+    leaf_lengths<E, K>(R, r, c + 1, (int)c, D.min_seq, (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0, L);
+    const int32_t total = prefix<E>(L, P);
     // split candidate at b: the visible leaf with P < b < P + L
-    const uint32_t slim = L[0] > 1 ? (uint32_t)(L[0] - 1) : 0u;
+    uint32_t slim[E];
+#pragma unroll
+    for (int j = 0; j < E; j++) slim[j] = L[j] > 1 ? (uint32_t)(L[j] - 1) : 0u;
 
     if (type == MTE_OP_INSERT) {
       // applyInsertOp -> insertSegments (client.ts:470-505, mergeTree.ts:1394-1422)
       const bool marker = (flags & MTE_F_MARKER) != 0;
       const int32_t nlen = marker ? 1 : pos2;
-      const int32_t q = pos1 - P[0];  // split offset, at the split leaf
-      const bool sp = ((uint32_t)q - 1u) < slim;
-      const uint64_t msp = __ballot(sp);
-      bool at = false;
-      if (msp) {
+      int32_t X[1][E];  // split offset, meaningful at the split leaf
+      bool sp[E], any = false;
+#pragma unroll
+      for (int j = 0; j < E; j++) {
+        X[0][j] = pos1 - P[j];
+        sp[j] = ((uint32_t)X[0][j] - 1u) < slim[j];
+        any = any || sp[j];
+      }
+      bool at[E];
+#pragma unroll
+      for (int j = 0; j < E; j++) at[j] = false;
+      if (__ballot(any)) {
         // ensureIntervalBoundary: [head][new][tail], the tail a copy of the leaf
-        const bool after = lanes_below(msp) != 0;        // slot > split leaf
-        const bool nb = lane_prev(sp ? 1 : 0) != 0;       // slot == split leaf + 1
-        const int d = after ? ((nlen > 0 && !nb) ? 2 : 1) : 0;
-        const int addr = (l - d) << 2;
-        shift1<K>(R, addr);
-        const int32_t qp = perm1(q, addr);
-        const bool tail = nlen > 0 ? (lane_prev(nb ? 1 : 0) != 0) : nb;
-        R.len[0] = sp ? q : (tail ? R.len[0] - qp : R.len[0]);
-        R.toff[0] = tail ? R.toff[0] + (uint32_t)qp : R.toff[0];
-        at = nlen > 0 && nb;
+        bool A[E], nb[E], nb2[E], g2[E];
+        after_flag<E>(sp, A);
+        prev_flags<E>(sp, nb, nb2);
+#pragma unroll
+        for (int j = 0; j < E; j++) g2[j] = nlen > 0 && A[j] && !nb[j];
+        bool own[E];
+#pragma unroll
+        for (int j = 0; j < E; j++) own[j] = sp[j];
+        shift_v<E, K, 1>(R, X, A, g2);
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+          const bool tail = nlen > 0 ? nb2[j] : nb[j];
+          R.len[j] = own[j] ? X[0][j] : (tail ? R.len[j] - X[0][j] : R.len[j]);
+          R.toff[j] = tail ? R.toff[j] + (uint32_t)X[0][j] : R.toff[j];
+          at[j] = nlen > 0 && nb[j];
+        }
         n += nlen > 0 ? 2 : 1;
         MTE_STAT(st[kStWritten] += nlen > 0 ? 3u : 2u;)
       } else if (nlen > 0) {
         // insertingWalk: before the first defined leaf with P >= pos
-        const bool cand = L[0] >= 0 && P[0] >= pos1;
-        const uint64_t mg = __ballot(cand);
-        if (mg) {
-          const bool pre = lanes_below(mg) != 0;
-          at = cand && !pre;
-          const int addr = (l - ((pre || cand) ? 1 : 0)) << 2;
-          shift1<K>(R, addr);
+        bool cand[E], anyc = false;
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+          cand[j] = L[j] >= 0 && P[j] >= pos1;
+          anyc = anyc || cand[j];
+        }
+        if (__ballot(anyc)) {
+          bool A[E], g1[E], g2[E];
+          after_flag<E>(cand, A);
+#pragma unroll
+          for (int j = 0; j < E; j++) {
+            at[j] = cand[j] && !A[j];
+            g1[j] = A[j] || cand[j];
+            g2[j] = false;
+          }
+          int32_t none[1][E];
+          shift_v<E, K, 0>(R, none, g1, g2);
         } else {
           if (pos1 > total) return MTE_E_INSERT_FAILED;  // mergeTree.ts:1666-1672
-          at = l == n;                                   // append: the slot is padding
+#pragma unroll
+          for (int j = 0; j < E; j++) at[j] = base + j == n;  // append: the slot is padding
         }
         n += 1;
         MTE_STAT(st[kStWritten] += 1;)
       }
-      if (nlen > 0) put_new1<K, S>(R, at, op, c, flags, a, st);
+      if (nlen > 0) put_new_v<E, K, S>(R, at, op, c, flags, a, st);
     } else {
       // markRangeRemoved / annotateRange: ensureIntervalBoundary at both ends
       // (ordered by position), then mark start <= P < end
       const int32_t b1 = pos1 < pos2 ? pos1 : pos2, b2 = pos1 < pos2 ? pos2 : pos1;
-      bool s1 = ((uint32_t)(b1 - P[0]) - 1u) < slim;
-      bool s2 = b2 != b1 && ((uint32_t)(b2 - P[0]) - 1u) < slim;
-      uint64_t m1 = __ballot(s1), m2 = __ballot(s2);
+      bool s1[E], s2[E], any1 = false, any2 = false;
+#pragma unroll
+      for (int j = 0; j < E; j++) {
+        s1[j] = ((uint32_t)(b1 - P[j]) - 1u) < slim[j];
+        s2[j] = b2 != b1 && ((uint32_t)(b2 - P[j]) - 1u) < slim[j];
+        any1 = any1 || s1[j];
+        any2 = any2 || s2[j];
+      }
+      uint64_t m1 = __ballot(any1), m2 = __ballot(any2);
       int32_t bA = b1;
       if (!m1) {  // only the end splits: it acts as the first split
-        s1 = s2;
-        s2 = false;
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+          s1[j] = s2[j];
+          s2[j] = false;
+        }
         m1 = m2;
         m2 = 0;
         bA = b2;
       }
       if (m1) {
-        const bool A = lanes_below(m1) != 0;              // slot > first split leaf
-        const bool nbB = lane_prev(s2 ? 1 : 0) != 0;       // slot == second split leaf + 1
-        const bool B = m2 != 0 && lanes_below(m2) != 0 && !nbB;
-        const int d = (A ? 1 : 0) + (B ? 1 : 0);
-        const int addr = (l - d) << 2;
-        shift1<K>(R, addr);
-        L[0] = perm1(L[0], addr);
-        P[0] = perm1(P[0], addr);
-        const int fs = perm1((s1 ? 1 : 0) | (s2 ? 2 : 0), addr);
-        // which piece of its source leaf this slot now holds
-        const bool h1 = (fs & 1) != 0, h2 = (fs & 2) != 0;
-        const int32_t oA = bA - P[0], oB = b2 - P[0];
-        const int kp = h1 ? d : d - 1;
-        const int32_t cutA = h1 ? oA : oB;
-        const int32_t st0 = (h1 || h2) ? (kp == 0 ? 0 : (kp == 1 ? cutA : oB)) : 0;
-        const int32_t en = (h1 || h2) ? (kp == 0 ? cutA : ((kp == 1 && h1 && h2) ? oB : R.len[0])) : R.len[0];
-        const int32_t nl = en - st0;
-        L[0] = (h1 || h2) ? nl : L[0];
-        P[0] += st0;
-        R.len[0] = nl;
-        R.toff[0] += (uint32_t)st0;
+        bool A[E], AB[E], nbB[E], nbB2[E], B[E];
+        after_flag<E>(s1, A);
+        after_flag<E>(s2, AB);
+        prev_flags<E>(s2, nbB, nbB2);
+        int32_t X[3][E];  // L, P and the split flags travel with the slot
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+          B[j] = m2 != 0 && AB[j] && !nbB[j];
+          X[0][j] = L[j];
+          X[1][j] = P[j];
+          X[2][j] = (s1[j] ? 1 : 0) | (s2[j] ? 2 : 0);
+        }
+        shift_v<E, K, 3>(R, X, A, B);
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+          // which piece of its source leaf slot j now holds
+          const int d = (A[j] ? 1 : 0) + (B[j] ? 1 : 0);
+          const bool h1 = (X[2][j] & 1) != 0, h2 = (X[2][j] & 2) != 0;
+          const int32_t oA = bA - X[1][j], oB = b2 - X[1][j];
+          const int kp = h1 ? d : d - 1;
+          const int32_t cutA = h1 ? oA : oB;
+          const int32_t st0 = (h1 || h2) ? (kp == 0 ? 0 : (kp == 1 ? cutA : oB)) : 0;
+          const int32_t en = (h1 || h2) ? (kp == 0 ? cutA : ((kp == 1 && h1 && h2) ? oB : R.len[j])) : R.len[j];
+          const int32_t nl = en - st0;
+          L[j] = (h1 || h2) ? nl : X[0][j];
+          P[j] = X[1][j] + st0;
+          R.len[j] = nl;
+          R.toff[j] += (uint32_t)st0;
+        }
         n += m2 ? 2 : 1;
         MTE_STAT(st[kStWritten] += m2 ? 4u : 2u;)
       }
       if (pos2 != pos1) {
         // nodeMap (mergeTree.ts:2274-2330): no visible leaf straddles a boundary
-        const bool in = L[0] > 0 && P[0] >= pos1 && P[0] < pos2;
-        MTE_STAT(st[kStWritten] += (uint32_t)__popcll(__ballot(in));)
+        bool in[E];
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+          in[j] = L[j] > 0 && P[j] >= pos1 && P[j] < pos2;
+          cnt += (uint32_t)__popcll(__ballot(in[j]));
+        }
+        MTE_STAT(st[kStWritten] += cnt;)
         if (type == MTE_OP_REMOVE) {
           // markRemoved (mergeTree.ts:1924-1962)
-          R.rseq[0] = (in && R.rseq[0] == kNone) ? s : R.rseq[0];
-          R.rmask[0] = in ? (R.rmask[0] | (1u << c)) : R.rmask[0];
-        } else {
-          // PropertiesManager.addProperties (segmentPropertiesManager.ts:63-151)
-          const uint64_t min = __ballot(in);
-          if (min) {
-            const uint32_t psi = (uint32_t)op[6];
-            const s8v q2 = sload_props(a, psi);
-            const bool sel[1] = {in};
-            if (flags & MTE_F_REWRITE) {
+          const uint32_t bit = 1u << c;
 #pragma unroll
-              for (int kk = 0; kk < K; kk++) R.pr[kk][0] = in ? 0u : R.pr[kk][0];
-            }
-            apply_props<1, K>(R.pr, sel, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], psi, a);
-            MTE_STAT(st[kStPwrites] += (uint32_t)__popcll(min) * (uint32_t)q2[3];)
+          for (int j = 0; j < E; j++) {
+            R.rseq[j] = (in[j] && R.rseq[j] == kNone) ? s : R.rseq[j];
+            R.rmask[j] = in[j] ? (R.rmask[j] | bit) : R.rmask[j];
           }
+        } else if (cnt > 0) {
+          // PropertiesManager.addProperties (segmentPropertiesManager.ts:63-151)
+          const uint32_t psi = (uint32_t)op[6];
+          const s8v q2 = sload_props(a, psi);
+          if (flags & MTE_F_REWRITE) {
+#pragma unroll
+            for (int kk = 0; kk < K; kk++)
+#pragma unroll
+              for (int j = 0; j < E; j++) R.pr[kk][j] = in[j] ? 0u : R.pr[kk][j];
+          }
+          apply_props<E, K>(R.pr, in, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], psi, a);
+          MTE_STAT(st[kStPwrites] += cnt * (uint32_t)q2[3];)
         }
       }
     }
@@ -223,29 +348,68 @@ __device__ __forceinline__ int doc_step1(Regs<1, K>& R, DocRun& D, uint32_t (&st
     D.cur_seq = s;
     if (msn > D.min_seq) {
       D.min_seq = msn;
-      // zamboni: each kept slot pushes its fields to its compacted lane
-      // (ds_permute); the lanes past the new count become padding
-      const bool keep = R.rseq[0] > msn;
-      const uint64_t mk = __ballot(keep);
-      const int n_new = __popcll(mk);
-      if (n_new != n) {
-        const int addr = (keep ? (int)lanes_below(mk) : kWave - 1) << 2;
-        R.len[0] = __builtin_amdgcn_ds_permute(addr, R.len[0]);
-        R.seq[0] = __builtin_amdgcn_ds_permute(addr, R.seq[0]);
-        R.rseq[0] = __builtin_amdgcn_ds_permute(addr, R.rseq[0]);
-        R.rmask[0] = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int32_t)R.rmask[0]);
-        R.meta[0] = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int32_t)R.meta[0]);
-        R.toff[0] = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int32_t)R.toff[0]);
+      // zamboni: drop tombstones with removedSeq <= minSeq (padding included)
+      if constexpr (E == 1) {
+        // each kept slot pushes its fields to its compacted lane (ds_permute)
+        const bool keep = R.rseq[0] > msn;
+        const uint64_t mk = __ballot(keep);
+        const int n_new = __popcll(mk);
+        if (n_new != n) {
+          const int addr = (keep ? (int)lanes_below(mk) : kWave - 1) << 2;
+          R.len[0] = __builtin_amdgcn_ds_permute(addr, R.len[0]);
+          R.seq[0] = __builtin_amdgcn_ds_permute(addr, R.seq[0]);
+          R.rseq[0] = __builtin_amdgcn_ds_permute(addr, R.rseq[0]);
+          R.rmask[0] = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int32_t)R.rmask[0]);
+          R.meta[0] = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int32_t)R.meta[0]);
+          R.toff[0] = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int32_t)R.toff[0]);
 #pragma unroll
-        for (int kk = 0; kk < K; kk++) R.pr[kk][0] = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int32_t)R.pr[kk][0]);
-        const bool pad = l >= n_new;
-        R.rseq[0] = pad ? kPad : R.rseq[0];
-        R.len[0] = pad ? 0 : R.len[0];
-        D.n = n_new;
+          for (int kk = 0; kk < K; kk++)
+            R.pr[kk][0] = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int32_t)R.pr[kk][0]);
+          const bool pad = l >= n_new;
+          R.rseq[0] = pad ? kPad : R.rseq[0];
+          R.len[0] = pad ? 0 : R.len[0];
+          D.n = n_new;
+        }
+      } else {
+        // stream compaction staged through LDS
+        bool keep[E];
+        int32_t cntl = 0;
+#pragma unroll
+        for (int jj = 0; jj < E; jj++) {
+          keep[jj] = R.rseq[jj] > msn;
+          cntl += keep[jj] ? 1 : 0;
+        }
+        const int32_t incl = wave_incl_scan(cntl);
+        const int n_new = rdlane(incl, kWave - 1);
+        if (n_new != n) {
+          int32_t dst[E];
+          int32_t d0 = incl - cntl;
+#pragma unroll
+          for (int jj = 0; jj < E; jj++) {
+            dst[jj] = d0;
+            d0 += keep[jj] ? 1 : 0;
+          }
+          compact_plane<E>(R.len, keep, dst, zlds);
+          compact_plane<E>(R.seq, keep, dst, zlds);
+          compact_plane<E>(R.rseq, keep, dst, zlds);
+          compact_plane<E>(R.rmask, keep, dst, zlds);
+          compact_plane<E>(R.meta, keep, dst, zlds);
+          compact_plane<E>(R.toff, keep, dst, zlds);
+#pragma unroll
+          for (int kk = 0; kk < K; kk++) compact_plane<E>(R.pr[kk], keep, dst, zlds);
+#pragma unroll
+          for (int jj = 0; jj < E; jj++) {
+            const bool pad = base + jj >= n_new;
+            R.rseq[jj] = pad ? kPad : R.rseq[jj];
+            R.len[jj] = pad ? 0 : R.len[jj];
+          }
+          D.n = n_new;
+          // drop to a smaller register tier once the doc fits in half of it
+          if (E > emin && n_new + 2 + 16 <= 32 * E) return 1;
+        }
       }
     }
   }
-  (void)zlds;
   return 0;
 }
 
