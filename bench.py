@@ -27,6 +27,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "sequenced ops merged/sec (node) at 10k docs×10k ops; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md "Chip-level parameters"
+# PMC-measured HBM bytes of one replay launch (tools/pmc_traffic.py over two
+# rocprofv3 --pmc passes); reported only for the libmte.so it was measured on
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "pmc_traffic_config{cfg}.json")
 
 WORKLOADS = {
     3: "config3: 10k docs x 10k ops/doc, insert/remove/annotate 1:1:1, 1/16 markers, 8 clients, R=64, "
@@ -44,6 +47,23 @@ def host_threads():
         return max(1, min(16, len(os.sched_getaffinity(0))))
     except Exception:
         return max(1, min(16, os.cpu_count() or 1))
+
+
+def pmc_traffic(config, n_docs, ops_per_doc):
+    """(bytes per launch, source) from the committed PMC summary, or (None, why)."""
+    import hashlib
+    path = TRAFFIC_JSON.format(cfg=config)
+    if not os.path.exists(path):
+        return None, "no PMC summary for this config"
+    preset_ok = (n_docs, ops_per_doc) == (None, None)
+    if not preset_ok:
+        return None, "non-default workload size"
+    rec = json.load(open(path))
+    lib = os.path.join(ROOT, "fluidframework_amd", "_lib", "libmte.so")
+    sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+    if rec.get("libmte_sha256") != sha:
+        return None, "PMC summary was taken on a different libmte.so build"
+    return rec["traffic_bytes_per_launch"], os.path.relpath(path, ROOT) + " (" + rec["correction"] + ")"
 
 
 def main():
@@ -144,6 +164,19 @@ def main():
     algo_bytes = stats["algo_bytes"]
     achieved_gbs = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9 if avg_kernel_ms else None
 
+    traffic, traffic_src = pmc_traffic(args.config, args.docs, args.ops)
+
+    # end-to-end: host op records -> HBM (mte_submit, PCIe),
+    # replay, per-doc digests back to the host; one untimed-by-the-contract pass
+    eng.sync()
+    t0 = time.perf_counter()
+    eng.submit(stream["batch"])
+    step()
+    e2e_digest = eng.digest()
+    e2e_s = time.perf_counter() - t0
+    if not np.array_equal(e2e_digest, digest):
+        raise SystemExit(f"rank {rank}: end-to-end pass disagrees with the timed runs")
+
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -180,13 +213,17 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": (achieved_gbs / HBM_PEAK_GBS) if achieved_gbs else None,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "traffic_frac_of_algo": (traffic / algo_bytes) if traffic else None,
             "kernel": "pair_kernel + big_kernel + stream_kernel (replay passes 1-3), HIP events on the engine stream",
             "counters_in_timed_runs": bool(args.stats),
             "kernel_ms": avg_kernel_ms,
             "algo_bytes_per_launch": algo_bytes,
             "algo_bytes_per_op": algo_bytes / max(1, stats["ops_applied"]),
         },
+        "end_to_end": {"ops_per_s": n_ops_rank / e2e_s, "ms": e2e_s * 1e3,
+                       "includes": "mte_submit (host->HBM op upload) + reset + replay + digest read-back, rank 0"},
         "cpu_baseline": cpu,
         "digest_fold": f"{fold:016x}",
         "parity_sample": parity,

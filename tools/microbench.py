@@ -47,6 +47,19 @@ def main():
         ops["type"] = OP_NOOP
         s["batch"]["ops"] = ops
         run("cfg3 all NOOP", s)
+    if "all" in which or "lat" in which:
+        # one wave per CU (512 docs = 256 pairs): per-op latency by op mix
+        for name, kw in (("full", {}),
+                         ("ins+rem", {"mix": gen.MIX_INSERT | gen.MIX_REMOVE, "marker_every": 0}),
+                         ("ins+ann", {"mix": gen.MIX_INSERT | gen.MIX_ANNOTATE, "marker_every": 0})):
+            s = gen.generate(3, n_docs=512, ops_per_doc=2000, **kw)
+            run(f"lat512 {name}", s)
+            if name == "full":
+                s["batch"] = dict(s["batch"])
+                ops = s["batch"]["ops"].copy()
+                ops["type"] = OP_NOOP
+                s["batch"]["ops"] = ops
+                run("lat512 NOOP", s)
     if "all" in which or "types" in which:
         s2 = gen.generate(2, n_docs=10000, ops_per_doc=2000)
         run("cfg2 (ins/rem, K=0)", s2)

@@ -7,7 +7,7 @@ import sys
 
 n_ops = float(sys.argv[1]) if len(sys.argv) > 1 else 1.0
 acc = collections.defaultdict(lambda: collections.defaultdict(float))
-for f in sorted(glob.glob("gpurun_out/pmc*/run_counter_collection.csv")):
+for f in sorted(glob.glob(sys.argv[2] if len(sys.argv) > 2 else "gpurun_out/pmc*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0][:40]
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
