@@ -36,6 +36,9 @@ WORKLOADS = {
        "legacy/new length calc 50/50",
     2: "config2: 1k docs x 1k ops/doc, insert/remove 1:1, 8 clients, R=32",
     4: "config4: 100k docs x 500 ops/doc, insert/remove/annotate, R=8",
+    5: "config5: 64 docs x 2^20 preloaded one-unit segments (mte_load_segments), 262,144 ops/doc in 4 rounds "
+       "of 65,536 concurrent ops (deep collab window, zamboni per round), insert/remove/annotate 1:1:1, "
+       "ranges <= 16 units, 1/16 markers, 8 clients",
 }
 
 
@@ -105,8 +108,9 @@ def main():
     gen_s = time.time() - t0
     n_ops_rank = int(stream["batch"]["op_offsets"][-1])
 
-    eng = DeviceEngine(stream["n_keys"], device=local_rank)
-    eng.load_docs(stream["inits"], stream["init_text"])
+    cap = gen.seg_capacity(args.config, stream["params"])
+    eng = DeviceEngine(stream["n_keys"], device=local_rank, seg_capacity=cap)
+    gen.load_stream(eng, stream)
     eng.submit(stream["batch"])
 
     def step():
@@ -185,7 +189,10 @@ def main():
     cpu = None
     parity = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu, parity = cpu_baseline(stream, digest, args.cpu_seconds)
+        if stream.get("segs") is not None:
+            cpu, parity = cpu_baseline_prefix(stream, cap, args.cpu_seconds, threads)
+        else:
+            cpu, parity = cpu_baseline(stream, digest, args.cpu_seconds)
 
     out = {
         "metric": METRIC,
@@ -216,7 +223,10 @@ def main():
             "traffic": traffic,
             "traffic_source": traffic_src,
             "traffic_frac_of_algo": (traffic / algo_bytes) if traffic else None,
-            "kernel": "pair_kernel + big_kernel + stream_kernel (replay passes 1-3), HIP events on the engine stream",
+            "kernel": ("pair_kernel + big_kernel + " + ("chunk_kernel" if cap >= 8192 else "stream_kernel") +
+                       " (replay passes 1-3), HIP events on the engine stream"),
+            "algo_bytes_note": ("S_live of chunk-pass ops replaced by the chunk slots + summary entries they "
+                                "scanned (SURVEY.md 8(d))" if cap >= 8192 else "SURVEY.md 8(d) B_op"),
             "counters_in_timed_runs": bool(args.stats),
             "kernel_ms": avg_kernel_ms,
             "algo_bytes_per_launch": algo_bytes,
@@ -263,6 +273,39 @@ def cpu_baseline(stream, gpu_digest, target_s):
              "sample": f"first {m} of {n_docs} docs (all their ops, {ops} ops), {dt:.1f} s, "
                        f"oracle/oracle.c flat restatement, {threads} pthreads"},
             {"docs": m, "digest_equal": parity})
+
+
+def cpu_baseline_prefix(stream, cap, target_s, threads):
+    """Long documents (config 5): the flat restatement costs O(S) per op, so the
+    sample is the first k ops of `threads` docs (k sized for ~target_s); its
+    digests are checked against a GPU replay of the same prefix."""
+    from fluidframework_amd import gen
+    from fluidframework_amd.engine import DeviceEngine
+    from oracle import OracleEngine
+
+    n_docs = len(stream["inits"])
+    m = min(n_docs, threads)
+    k = 64
+    while True:
+        sub = gen.prefix_ops(stream, m, k)
+        o = OracleEngine(stream["n_keys"], threads=threads)
+        gen.load_stream(o, sub)
+        t0 = time.perf_counter()
+        o.apply_batch(sub["batch"])
+        dt = time.perf_counter() - t0
+        if dt >= target_s / 4 or k >= int(np.diff(stream["batch"]["op_offsets"].astype(np.int64)).min()):
+            break
+        k = int(k * min(16.0, max(2.0, target_s / max(dt, 1e-3))))
+    ops = int(sub["batch"]["op_offsets"][-1])
+    d = DeviceEngine(stream["n_keys"], seg_capacity=cap)
+    gen.load_stream(d, sub)
+    d.apply_batch(sub["batch"])
+    parity = bool(np.array_equal(o.digest(), d.digest()) and (o.statuses() == 0).all()
+                  and (d.statuses() == 0).all())
+    return ({"value": ops / dt, "unit": "ops/s", "cores": threads, "kind": "port",
+             "sample": f"first {k} ops of the first {m} of {n_docs} docs ({ops} ops at ~2^20 segments/doc), "
+                       f"{dt:.1f} s, oracle/oracle.c flat restatement, {threads} pthreads"},
+            {"docs": m, "ops_per_doc": k, "digest_equal": parity, "checked_against": "GPU replay of the same prefix"})
 
 
 if __name__ == "__main__":

@@ -37,6 +37,7 @@ def load_mte():
         "mte_destroy": ([vp], C.c_int),
         "mte_last_error": ([vp], C.c_char_p),
         "mte_load_docs": ([vp, u32, vp, vp, u64, vp, u32, vp, u32], C.c_int),
+        "mte_load_segments": ([vp, vp, vp, u64], C.c_int),
         "mte_submit": ([vp, vp], C.c_int),
         "mte_run": ([vp], C.c_int),
         "mte_sync": ([vp], C.c_int),

@@ -61,6 +61,13 @@ DOC_INIT_DTYPE = np.dtype([
 ])
 assert DOC_INIT_DTYPE.itemsize == 24
 
+# mte_seg: a segment with merge info (mte_load_segments, snapshot body).
+NOT_REMOVED = 0x7FFFFFFF
+SEG_DTYPE = np.dtype([
+    ("text_off", "<u4"), ("len", "<u4"), ("seq", "<i4"), ("removed_seq", "<i4"),
+    ("removers", "<u4"), ("client", "<i4"), ("kind", "<u4"), ("propset", "<u4")])
+assert SEG_DTYPE.itemsize == 32
+
 
 class MteConfig(C.Structure):
     _fields_ = [("device", C.c_int32), ("n_keys", C.c_uint32),
@@ -78,7 +85,8 @@ class MteStats(C.Structure):
     _fields_ = [("ops_applied", C.c_uint64), ("segs_scanned", C.c_uint64),
                 ("segs_written", C.c_uint64), ("prop_writes", C.c_uint64),
                 ("units_inserted", C.c_uint64), ("max_segs", C.c_uint64),
-                ("kernel_ms", C.c_double), ("algo_bytes", C.c_double)]
+                ("kernel_ms", C.c_double), ("algo_bytes", C.c_double),
+                ("chunk_scanned", C.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -95,7 +103,7 @@ class MteDocView(C.Structure):
 # Every symbol include/mte.h declares (tests check libmte.so exports them all).
 EXPORTED_SYMBOLS = [
     "mte_abi_version", "mte_strerror", "mte_create", "mte_destroy", "mte_last_error",
-    "mte_load_docs", "mte_submit", "mte_run", "mte_sync", "mte_reset", "mte_digest",
+    "mte_load_docs", "mte_load_segments", "mte_submit", "mte_run", "mte_sync", "mte_reset", "mte_digest",
     "mte_digest_device", "mte_read_doc", "mte_doc_status", "mte_stats_get", "mte_set_stats",
 ]
 

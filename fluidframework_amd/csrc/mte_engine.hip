@@ -15,6 +15,7 @@
 #include "mte_kernels.h"
 #include "mte_replay.h"
 #include "mte_stream.h"
+#include "mte_chunk.h"
 
 using namespace mte;
 
@@ -33,12 +34,14 @@ __global__ void begin_batch_kernel(DocHdr* hdr, unsigned long long* stats, uint3
 // (re)initialise docs from their load description: one seq-0 LocalClientId
 // text segment (client.replay.spec.ts:22-23)
 __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_doc_init* inits,
-                             const uint32_t* init_props, uint32_t n_keys, uint32_t n_docs) {
+                             const uint32_t* init_props, uint32_t n_keys, uint32_t n_docs,
+                             const uint64_t* img_off) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= n_docs) return;
   const mte_doc_init in = inits[d];
+  const uint32_t n_img = img_off ? (uint32_t)(img_off[d + 1] - img_off[d]) : 0u;
   DocHdr h;
-  h.nseg = in.text_len > 0 ? 1 : 0;
+  h.nseg = n_img ? (int32_t)n_img : (in.text_len > 0 ? 1 : 0);
   h.min_seq = in.min_seq;
   h.cur_seq = in.cur_seq;
   h.status = 0;
@@ -46,6 +49,7 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
   h.resume = 0;
   h.pad0 = h.pad1 = 0;
   hdr[d] = h;
+  if (n_img) return;  // image_kernel writes the segments
   const uint64_t i = (uint64_t)d * cap;
   soa.len[i] = (int32_t)in.text_len;
   soa.seq[i] = 0;
@@ -54,6 +58,18 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
   soa.meta[i] = 0;  // clientId -1, text
   soa.toff[i] = in.text_off;
   for (uint32_t k = 0; k < n_keys; k++) soa.props[k * soa.plane_stride + i] = init_props[(size_t)d * MTE_MAX_KEYS + k];
+}
+
+// the mte_load_segments image -> the flat planes (one thread per segment)
+__global__ void image_kernel(SegSoA soa, uint32_t cap, uint32_t n_planes, const uint32_t* img, uint64_t img_stride,
+                             const uint32_t* img_doc, const uint64_t* img_off, uint64_t n_img) {
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_img;
+       g += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t d = img_doc[g];
+    const uint64_t x = (uint64_t)d * cap + (g - img_off[d]);
+    uint32_t* pl = reinterpret_cast<uint32_t*>(soa.len);
+    for (uint32_t p = 0; p < n_planes; p++) pl[p * soa.plane_stride + x] = img[p * img_stride + g];
+  }
 }
 
 // Compile the batch's property sets into the 32-byte records the replay
@@ -224,12 +240,24 @@ struct mte_ctx {
   mte_doc_init* d_inits = nullptr;
   uint32_t* d_init_props = nullptr;
   uint64_t* d_pow = nullptr;  // pow1[32], pow2[32]
+
+  // mte_load_segments image (SoA, 6 + kt planes at stride n_img)
+  uint32_t* d_img = nullptr;
+  uint32_t* d_img_doc = nullptr;
+  uint64_t* d_img_off = nullptr;
+  uint64_t n_img = 0;
+
+  // chunked big-document pass (seg_capacity >= kChunkMinCap, mte_chunk.h)
+  bool chunked = false;
+  ChunkArgs ch{};
   uint64_t* d_digest = nullptr;
 
   // text arena
   uint16_t* arena = nullptr;
   uint64_t arena_n = 0, arena_cap = 0;
   std::vector<uint16_t> h_arena;
+  std::vector<mte_propset> h_load_ps;  // mte_load_docs propsets (for mte_load_segments)
+  std::vector<mte_prop> h_load_pe;
 
   // batch
   mte_op* d_ops = nullptr;
@@ -284,7 +312,23 @@ int grow(mte_ctx* c, T** p, uint64_t* cap, uint64_t need, bool keep = false, uin
   return MTE_OK;
 }
 
+void free_image(mte_ctx* c) {
+  void* ps[] = {c->d_img, c->d_img_doc, c->d_img_off};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+  c->d_img = nullptr;
+  c->d_img_doc = nullptr;
+  c->d_img_off = nullptr;
+  c->n_img = 0;
+}
+
 void free_docs(mte_ctx* c) {
+  free_image(c);
+  void* cs[] = {c->ch.arena, c->ch.cnt, c->ch.kc, c->ch.sum};
+  for (void* p : cs)
+    if (p) (void)hipFree(p);
+  c->ch = ChunkArgs{};
+  c->chunked = false;
   void* ps[] = {c->hdr, c->soa.len, c->stats, c->d_inits, c->d_init_props, c->d_digest, c->d_pairs};
   for (void* p : ps)
     if (p) (void)hipFree(p);
@@ -303,8 +347,15 @@ int launch_reset(mte_ctx* c) {
   if (!c->n_docs) return MTE_OK;
   const uint32_t blocks = (c->n_docs + 255) / 256;
   hipLaunchKernelGGL(reset_kernel, dim3(blocks), dim3(256), 0, c->stream, c->hdr, c->soa, c->cap,
-                     c->d_inits, c->d_init_props, c->n_keys, c->n_docs);
+                     c->d_inits, c->d_init_props, c->n_keys, c->n_docs, (const uint64_t*)c->d_img_off);
   HIPCHK(c, hipGetLastError());
+  if (c->n_img) {
+    const uint64_t nb = std::min<uint64_t>((c->n_img + 255) / 256, 65536);
+    hipLaunchKernelGGL(image_kernel, dim3((uint32_t)nb), dim3(256), 0, c->stream, c->soa, c->cap,
+                       (uint32_t)(kFieldPlanes + c->kt), c->d_img, c->n_img, c->d_img_doc,
+                       (const uint64_t*)c->d_img_off, c->n_img);
+    HIPCHK(c, hipGetLastError());
+  }
   c->ran = false;
   return MTE_OK;
 }
@@ -319,8 +370,14 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   const uint32_t b2 = (c->n_docs + kDocsPerBlock - 1) / kDocsPerBlock;
   hipLaunchKernelGGL((big_kernel<K, S>), dim3(b2), dim3(256), 0, c->stream, a);
   HIPCHK(c, hipGetLastError());
-  // pass 3: larger docs (up to the ctx capacity), HBM-resident, streamed per op
-  hipLaunchKernelGGL((stream_kernel<K, S>), dim3(b2), dim3(256), 0, c->stream, a);
+  // pass 3: larger docs (up to the ctx capacity): the chunked pass in big-doc
+  // contexts, otherwise HBM-resident and streamed per op
+  if (c->chunked) {
+    const size_t lds = sizeof(uint32_t) * MTE_MAX_CLIENTS * c->ch.ng_cap + sizeof(ChCtl);
+    hipLaunchKernelGGL((chunk_kernel<K, S>), dim3(c->n_docs), dim3(kChWaves * kWave), lds, c->stream, a, c->ch);
+  } else {
+    hipLaunchKernelGGL((stream_kernel<K, S>), dim3(b2), dim3(256), 0, c->stream, a);
+  }
   HIPCHK(c, hipGetLastError());
   return MTE_OK;
 }
@@ -443,6 +500,24 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     c->soa.props = base + kFieldPlanes * nslots;
   }
   HIPCHK(c, hipMemsetAsync(c->soa.props, 0, nslots * 4 * (c->kt ? c->kt : 1), c->stream));
+  if (c->cap >= kChunkMinCap && n_docs) {
+    // chunk arena: every doc can be re-laid out at kChFill segments per chunk
+    const uint32_t nch_cap = c->cap / kChFill + 2;
+    const uint32_t ng_cap = (nch_cap + kChGroup - 1) / kChGroup;
+    if (ng_cap <= kChMaxGroups) {
+      ChunkArgs& ch = c->ch;
+      ch.nch_cap = nch_cap;
+      ch.ng_cap = ng_cap;
+      const uint64_t nch_all = (uint64_t)n_docs * nch_cap;
+      ch.astride = nch_all * kChSlots;
+      const uint64_t planes = kFieldPlanes + (c->kt ? c->kt : 1);
+      HIPCHK(c, hipMalloc((void**)&ch.arena, ch.astride * 4 * planes));
+      HIPCHK(c, hipMalloc((void**)&ch.cnt, nch_all * 4));
+      HIPCHK(c, hipMalloc((void**)&ch.kc, nch_all * 4));
+      HIPCHK(c, hipMalloc((void**)&ch.sum, nch_all * 4 * MTE_MAX_CLIENTS));
+      c->chunked = true;
+    }
+  }
   HIPCHK(c, hipMalloc((void**)&c->stats, sizeof(unsigned long long) * kNumStats * (n_docs ? n_docs : 1)));
   HIPCHK(c, hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * kNumStats * (n_docs ? n_docs : 1), c->stream));
   HIPCHK(c, hipMalloc((void**)&c->d_inits, sizeof(mte_doc_init) * (n_docs ? n_docs : 1)));
@@ -461,6 +536,10 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     HIPCHK(c, hipMemcpyAsync(c->d_init_props, iprops.data(), sizeof(uint32_t) * iprops.size(),
                              hipMemcpyHostToDevice, c->stream));
   }
+  c->h_load_ps.assign(propsets, propsets + (propsets ? n_propsets : 0));
+  c->h_load_pe.assign(props, props + (props ? n_props : 0));
+  for (const mte_propset& ps : c->h_load_ps)
+    if ((uint64_t)ps.first + ps.count > c->h_load_pe.size()) return set_err(c, MTE_E_INVALID_ARG, "bad load propset");
   // text arena restarts with the load text
   c->arena_n = 0;
   c->h_arena.assign(text, text + text_units);
@@ -470,6 +549,63 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     HIPCHK(c, hipMemcpyAsync(c->arena, text, text_units * 2, hipMemcpyHostToDevice, c->stream));
   c->arena_n = text_units;
   rc = launch_reset(c);
+  if (rc) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MTE_OK;
+}
+
+int mte_load_segments(mte_ctx* c, const uint64_t* seg_offsets, const mte_seg* segs, uint64_t n_segs) {
+  if (!c || !seg_offsets || (n_segs && !segs)) return MTE_E_INVALID_ARG;
+  if (!c->n_docs) return MTE_OK;
+  if (seg_offsets[0] != 0 || seg_offsets[c->n_docs] != n_segs)
+    return set_err(c, MTE_E_INVALID_ARG, "seg_offsets must run from 0 to n_segs");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint32_t np = kFieldPlanes + c->kt;
+  std::vector<uint32_t> img((size_t)np * (n_segs ? n_segs : 1), 0u), doc((size_t)(n_segs ? n_segs : 1), 0u);
+  // propsets of the load: the load propsets/props were consumed by
+  // mte_load_docs; the per-doc initial props are kept, so segment propsets
+  // arrive here through the host copy (set by mte_load_docs)
+  for (uint32_t d = 0; d < c->n_docs; d++) {
+    const uint64_t b = seg_offsets[d], e = seg_offsets[d + 1];
+    if (e < b || e - b > c->cap) return set_err(c, MTE_E_CAPACITY, "doc %u: %llu segments > capacity %u", d,
+                                                (unsigned long long)(e - b), c->cap);
+    for (uint64_t g = b; g < e; g++) {
+      const mte_seg& sg = segs[g];
+      const bool marker = sg.kind != 0;
+      if ((marker && sg.len != 1) || (!marker && (sg.len == 0 || sg.len > 0x7fffffffu)) ||
+          (!marker && (uint64_t)sg.text_off + sg.len > c->h_arena.size()) || sg.client < -1 ||
+          sg.client >= MTE_MAX_CLIENTS || sg.kind > 0xfffffeu || sg.seq < 0 ||
+          (sg.removed_seq != MTE_NOT_REMOVED && sg.removers == 0))
+        return set_err(c, MTE_E_INVALID_ARG, "doc %u segment %llu: bad segment", d, (unsigned long long)(g - b));
+      img[0 * n_segs + g] = sg.len;
+      img[1 * n_segs + g] = (uint32_t)sg.seq;
+      img[2 * n_segs + g] = (uint32_t)(sg.removed_seq == MTE_NOT_REMOVED ? kNone : sg.removed_seq);
+      img[3 * n_segs + g] = sg.removed_seq == MTE_NOT_REMOVED ? 0u : sg.removers;
+      img[4 * n_segs + g] = (uint32_t)(sg.client + 1) | (sg.kind << 8);
+      img[5 * n_segs + g] = marker ? 0u : sg.text_off;
+      if (sg.propset != MTE_NO_PROPS) {
+        if (sg.propset >= c->h_load_ps.size())
+          return set_err(c, MTE_E_INVALID_ARG, "doc %u segment %llu: bad propset", d, (unsigned long long)(g - b));
+        const mte_propset ps = c->h_load_ps[sg.propset];
+        for (uint32_t t = 0; t < ps.count; t++) {
+          const mte_prop p = c->h_load_pe[ps.first + t];
+          if (p.key < c->n_keys) img[(uint64_t)(kFieldPlanes + p.key) * n_segs + g] = p.value;
+        }
+      }
+      doc[g] = d;
+    }
+  }
+  free_image(c);
+  if (!n_segs) return launch_reset(c);
+  HIPCHK(c, hipMalloc((void**)&c->d_img, img.size() * 4));
+  HIPCHK(c, hipMalloc((void**)&c->d_img_doc, doc.size() * 4));
+  HIPCHK(c, hipMalloc((void**)&c->d_img_off, ((size_t)c->n_docs + 1) * 8));
+  HIPCHK(c, hipMemcpy(c->d_img, img.data(), img.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_img_doc, doc.data(), doc.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_img_off, seg_offsets, ((size_t)c->n_docs + 1) * 8, hipMemcpyHostToDevice));
+  c->n_img = n_segs;
+  int rc = launch_reset(c);
   if (rc) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return MTE_OK;
@@ -686,6 +822,7 @@ int mte_stats_get(mte_ctx* c, mte_stats* o) {
   if (!c->n_docs) return MTE_OK;
   HIPCHK(c, hipSetDevice(c->device));
   std::vector<unsigned long long> s((size_t)c->n_docs * kNumStats);
+  unsigned long long chunk_canon = 0;
   HIPCHK(c, hipMemcpyAsync(s.data(), c->stats, s.size() * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   for (uint32_t d = 0; d < c->n_docs; d++) {
@@ -696,12 +833,17 @@ int mte_stats_get(mte_ctx* c, mte_stats* o) {
     o->prop_writes += x[kStPwrites];
     o->units_inserted += x[kStUnits];
     if (x[kStMaxSegs] > o->max_segs) o->max_segs = x[kStMaxSegs];
+    chunk_canon += x[kStChunkCanon];
+    o->chunk_scanned += x[kStChunkScan];
   }
   if (c->ran) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) o->kernel_ms = ms;
   }
-  o->algo_bytes = 32.0 * (double)o->ops_applied + 20.0 * (double)o->segs_scanned + 20.0 * (double)o->segs_written +
+  // ops of the chunked pass count the slots and summary
+  // entries they scanned instead of the document's S_live
+  const double scanned = (double)(o->segs_scanned - chunk_canon) + (double)o->chunk_scanned;
+  o->algo_bytes = 32.0 * (double)o->ops_applied + 20.0 * scanned + 20.0 * (double)o->segs_written +
                   4.0 * (double)o->prop_writes + 2.0 * (double)o->units_inserted;
   return MTE_OK;
 }

@@ -133,7 +133,126 @@ uint32_t pair_set(uint32_t k1, uint32_t k2, uint32_t v1, uint32_t v2) {
   return 27 + pi * 81 + v1 * 9 + v2;
 }
 
+// annotate props: 1-2 keys of {client, bold, color}, values of <= 8 per key,
+// 10% null -> one of the fixed propsets
+uint32_t annotate_set(MT& rng) {
+  const uint32_t nk = (uint32_t)rng.uniform(1, 2);
+  auto pick_val = [&]() -> uint32_t { return rng.uniform(0, 9) == 0 ? 8u : (uint32_t)rng.uniform(0, 7); };
+  if (nk == 1) {
+    const uint32_t k1 = (uint32_t)rng.uniform(0, 2);
+    return single_set(k1, pick_val());
+  }
+  uint32_t k1 = (uint32_t)rng.uniform(0, 2), k2 = (uint32_t)rng.uniform(0, 1);
+  if (k2 >= k1) k2++;
+  if (k2 < k1) std::swap(k1, k2);
+  const uint32_t v1 = pick_val(), v2 = pick_val();
+  return pair_set(k1, k2, v1, v2);
+}
+
+// an insert of 1-3 units of the author's name, or (1 in marker_every) a
+// marker {marker:{refType:1}, props:{markerId:"m<seq>"}}; returns its length
+int32_t gen_insert(const mteg_config& cfg, MT& rng, uint32_t author, int32_t s, mte_op& op, DocOut& out) {
+  const bool marker = cfg.marker_every && rng.uniform(0, cfg.marker_every - 1) == 0;
+  if (marker) {
+    op.flags |= MTE_F_MARKER;
+    op.pos2 = 1;                         // refType
+    op.b = (uint32_t)out.psets.size();   // per-doc index, fixed up at fill
+    out.psets.push_back({(uint32_t)out.props.size(), 1});
+    out.props.push_back({MTEG_KEY_MARKER_ID, 64u + (uint32_t)s});
+    return 1;
+  }
+  const int32_t n = (int32_t)rng.uniform(1, 3);
+  op.pos2 = n;
+  op.a = (uint32_t)out.text.size();  // per-doc offset, fixed up at fill
+  for (int32_t i = 0; i < n; i++) out.text.push_back((uint16_t)('B' + author));
+  return n;
+}
+
+// Long documents (config 5: a preloaded body of init_segs one-unit segments,
+// loaded through mte_load_segments).  The per-unit model of gen_doc would cost
+// O(document) per op, so each author's perspective length is kept instead:
+// within a round (refSeq = round start for every op) an author sees the base
+// text plus its own ops only, so L(r, c) = L0 + inserted_c - removed_c
+// exactly.  The next round's L0 is bounded below by L0 + all inserted - all
+// removed (a unit removed by two authors counts twice), and positions are
+// drawn against that bound, so every op is valid; the stream departs from the
+// farm rule (mergeTreeOperationRunner.ts:164-176) only in drawing from
+// [0, bound] instead of [0, L].  Ranges are short (1..max_range units).
+void gen_doc_long(const mteg_config& cfg, uint32_t d, DocOut& out) {
+  MT rng;
+  const uint32_t key[4] = {0xDEADBEEFu, 0xFEEDBEDu, cfg.config_id, cfg.doc_base + d};
+  rng.init_by_array(key, 4);
+  const uint32_t C = cfg.clients < 1 ? 1 : (cfg.clients > 31 ? 31 : cfg.clients);
+  if (cfg.length_mode == 0) out.flags = (rng.next() & 1u) ? MTE_DOC_NEW_LENGTH_CALC : 0u;
+  else if (cfg.length_mode == 2) out.flags = MTE_DOC_NEW_LENGTH_CALC;
+  out.init_text.resize(cfg.init_segs);
+  for (uint32_t i = 0; i < cfg.init_segs; i++) out.init_text[i] = (uint16_t)('a' + (i % 26));
+  int short_of[32];
+  for (int i = 0; i < 32; i++) short_of[i] = -1;
+  int next_short = 1;
+  std::vector<uint32_t> mix;
+  if (cfg.mix & MTEG_MIX_INSERT) mix.push_back(MTE_OP_INSERT);
+  if (cfg.mix & MTEG_MIX_REMOVE) mix.push_back(MTE_OP_REMOVE);
+  if (cfg.mix & MTEG_MIX_ANNOTATE) mix.push_back(MTE_OP_ANNOTATE);
+  if (mix.empty()) mix.push_back(MTE_OP_INSERT);
+  out.ops.reserve(cfg.ops_per_doc);
+  const uint32_t R = cfg.round_ops ? cfg.round_ops : 1;
+  const int64_t max_range = cfg.max_range ? cfg.max_range : INT32_MAX;
+  int64_t L0 = cfg.init_segs;
+  int32_t seq = 0;
+  uint32_t done = 0;
+  while (done < cfg.ops_per_doc) {
+    const int32_t round_start = seq;
+    int64_t ins[32] = {0}, rem[32] = {0}, all_ins = 0, all_rem = 0;
+    for (uint32_t k = 0; k < R && done < cfg.ops_per_doc; k++, done++) {
+      const uint32_t author = (uint32_t)rng.uniform(0, C - 1);
+      if (short_of[author] < 0) short_of[author] = next_short++;
+      const int c = short_of[author];
+      const int32_t r = round_start;
+      const int32_t s = ++seq;
+      const int64_t L = L0 + ins[c] - rem[c];
+      const uint32_t type = (L <= 0 || L < (int64_t)cfg.min_length)
+                                ? MTE_OP_INSERT
+                                : mix[(size_t)rng.uniform(0, (int64_t)mix.size() - 1)];
+      mte_op op;
+      std::memset(&op, 0, sizeof(op));
+      op.seq = s;
+      op.ref_seq = r;
+      op.min_seq = r;
+      op.type = (uint8_t)type;
+      op.client = (uint8_t)c;
+      op.flags = MTE_F_MSG_END;
+      op.b = MTE_NO_PROPS;
+      if (type == MTE_OP_INSERT) {
+        op.pos1 = (int32_t)rng.uniform(0, L > 0 ? L : 0);
+        const int32_t n = gen_insert(cfg, rng, author, s, op, out);
+        ins[c] += n;
+        all_ins += n;
+      } else {
+        const int64_t start = rng.uniform(0, L - 1);
+        const int64_t span = L - start < max_range ? L - start : max_range;
+        const int64_t end = start + rng.uniform(1, span);
+        op.pos1 = (int32_t)start;
+        op.pos2 = (int32_t)end;
+        if (type == MTE_OP_REMOVE) {
+          rem[c] += end - start;
+          all_rem += end - start;
+        } else {
+          op.a = annotate_set(rng);
+        }
+      }
+      out.ops.push_back(op);
+    }
+    L0 = L0 + all_ins - all_rem;
+    if (L0 < 0) L0 = 0;
+  }
+}
+
 void gen_doc(const mteg_config& cfg, uint32_t d, DocOut& out) {
+  if (cfg.init_segs) {
+    gen_doc_long(cfg, d, out);
+    return;
+  }
   MT rng;
   const uint32_t key[4] = {0xDEADBEEFu, 0xFEEDBEDu, cfg.config_id, cfg.doc_base + d};
   rng.init_by_array(key, 4);
@@ -236,20 +355,7 @@ void gen_doc(const mteg_config& cfg, uint32_t d, DocOut& out) {
             if (++seen >= end) break;
           }
         } else {
-          const uint32_t nk = (uint32_t)rng.uniform(1, 2);
-          auto pick_val = [&]() -> uint32_t {
-            return rng.uniform(0, 9) == 0 ? 8u : (uint32_t)rng.uniform(0, 7);
-          };
-          if (nk == 1) {
-            const uint32_t k1 = (uint32_t)rng.uniform(0, 2);
-            op.a = single_set(k1, pick_val());
-          } else {
-            uint32_t k1 = (uint32_t)rng.uniform(0, 2), k2 = (uint32_t)rng.uniform(0, 1);
-            if (k2 >= k1) k2++;
-            if (k2 < k1) std::swap(k1, k2);
-            const uint32_t v1 = pick_val(), v2 = pick_val();
-            op.a = pair_set(k1, k2, v1, v2);
-          }
+          op.a = annotate_set(rng);
         }
       }
       out.ops.push_back(op);

@@ -46,6 +46,9 @@ typedef struct mteg_config {
   uint32_t length_mode;  /* 0: per doc 50/50, 1: all legacy, 2: all new */
   uint32_t init_len;     /* initial text units per doc                  */
   uint32_t n_threads;
+  uint32_t init_segs;    /* > 0: preload this many one-unit segments per doc
+                            (mte_load_segments) and use the long-doc generator */
+  uint32_t max_range;    /* remove / annotate span cap (0 = farm rule)     */
 } mteg_config;
 
 typedef struct mteg_stream mteg_stream;

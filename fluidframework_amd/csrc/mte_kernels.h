@@ -37,7 +37,19 @@ struct DocHdr {
 };
 constexpr uint32_t kHdrNeedsEsc = 0x80000000u;
 
-enum StatIdx { kStOps = 0, kStScanned, kStWritten, kStPwrites, kStUnits, kStMaxSegs, kNumStats };
+// kStChunkCanon / kStChunkScan (chunk pass only): the canonical S_live of its
+// ops, and the chunk slots + summary entries those ops actually scanned
+enum StatIdx {
+  kStOps = 0,
+  kStScanned,
+  kStWritten,
+  kStPwrites,
+  kStUnits,
+  kStMaxSegs,
+  kStChunkCanon,
+  kStChunkScan,
+  kNumStats
+};
 
 // segment state, structure of arrays, doc-major: field[doc * cap + i].  All
 // planes live in one allocation at a common stride (plane_stride elements):

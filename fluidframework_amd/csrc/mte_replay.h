@@ -640,7 +640,7 @@ __device__ __forceinline__ bool step_done(DocRun& D, int rc) {
 template <int E, int K, bool S>
 __device__ __forceinline__ void burst_run(DocRun& D, const ReplayArgs& a, uint32_t* zlds, int emin, uint32_t limit) {
   Regs<E, K> R;
-  uint32_t st[kNumStats] = {0, 0, 0, 0, 0, 0};
+  uint32_t st[kNumStats] = {};
   load_regs<E, K>(R, D, a);
   const uint32_t kend = D.k1 - D.k > limit ? D.k + limit : D.k1;
   s8v cur = sload8(D.recp + 2 * D.k);

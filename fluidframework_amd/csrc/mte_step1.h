@@ -143,6 +143,201 @@ __device__ __forceinline__ void put_new_v(Regs<E, K>& R, const bool (&at)[E], co
   }
 }
 
+// chunk pass (mte_chunk.h): the insert slot lies in a later chunk
+constexpr int kNextChunk = 2;
+
+// The segment part of one insert / remove / annotate on a register-resident
+// run of segments — a whole document (doc_step_v) or one chunk of a big one
+// (mte_chunk.h, CH = true).  Returns 0, MTE_E_INSERT_FAILED or (CH, insert
+// only, unless `last`) kNextChunk with the registers untouched.  With CH the
+// op's positions are taken relative to `off`, the chunk's first position in
+// the op's perspective; *tot is the chunk's length in that perspective before
+// the op and *dlen its change (+ inserted units, - units the remover saw).
+template <int E, int K, bool S, bool CH>
+__device__ __forceinline__ int seg_op_v(Regs<E, K>& R, int& n, const s8v& op, uint32_t type, uint32_t c,
+                                        uint32_t flags, int32_t m, bool newcalc, int32_t off, bool last,
+                                        int32_t& tot, int32_t& dlen, const ReplayArgs& a,
+                                        uint32_t (&st)[kNumStats]) {
+  const int base = lane_id() * E;
+  const int32_t s = op[0], r = op[1];
+  const int32_t pos1 = op[4] - (CH ? off : 0);
+  const int32_t pos2 = (CH && type != MTE_OP_INSERT) ? op[5] - off : op[5];
+  int32_t L[E], P[E];
+  leaf_lengths<E, K>(R, r, c + 1, (int)c, m, newcalc, L);
+  const int32_t total = prefix<E>(L, P);
+  if constexpr (CH) {
+    tot = total;
+    dlen = 0;
+  }
+  // split candidate at b: the visible leaf with P < b < P + L
+  uint32_t slim[E];
+#pragma unroll
+  for (int j = 0; j < E; j++) slim[j] = L[j] > 1 ? (uint32_t)(L[j] - 1) : 0u;
+
+  if (type == MTE_OP_INSERT) {
+    // applyInsertOp -> insertSegments (client.ts:470-505, mergeTree.ts:1394-1422)
+    const bool marker = (flags & MTE_F_MARKER) != 0;
+    const int32_t nlen = marker ? 1 : pos2;
+    int32_t X[1][E];  // split offset, meaningful at the split leaf
+    bool sp[E], any = false;
+#pragma unroll
+    for (int j = 0; j < E; j++) {
+      X[0][j] = pos1 - P[j];
+      sp[j] = ((uint32_t)X[0][j] - 1u) < slim[j];
+      any = any || sp[j];
+    }
+    bool at[E];
+#pragma unroll
+    for (int j = 0; j < E; j++) at[j] = false;
+    if (__ballot(any)) {
+      // ensureIntervalBoundary: [head][new][tail], the tail a copy of the leaf
+      bool A[E], nb[E], nb2[E], g2[E];
+      after_flag<E>(sp, A);
+      prev_flags<E>(sp, nb, nb2);
+#pragma unroll
+      for (int j = 0; j < E; j++) g2[j] = nlen > 0 && A[j] && !nb[j];
+      bool own[E];
+#pragma unroll
+      for (int j = 0; j < E; j++) own[j] = sp[j];
+      shift_v<E, K, 1>(R, X, A, g2);
+#pragma unroll
+      for (int j = 0; j < E; j++) {
+        const bool tail = nlen > 0 ? nb2[j] : nb[j];
+        R.len[j] = own[j] ? X[0][j] : (tail ? R.len[j] - X[0][j] : R.len[j]);
+        R.toff[j] = tail ? R.toff[j] + (uint32_t)X[0][j] : R.toff[j];
+        at[j] = nlen > 0 && nb[j];
+      }
+      n += nlen > 0 ? 2 : 1;
+      MTE_STAT(st[kStWritten] += nlen > 0 ? 3u : 2u;)
+    } else if (nlen > 0) {
+      // insertingWalk: before the first defined leaf with P >= pos
+      bool cand[E], anyc = false;
+#pragma unroll
+      for (int j = 0; j < E; j++) {
+        cand[j] = L[j] >= 0 && P[j] >= pos1;
+        anyc = anyc || cand[j];
+      }
+      if (__ballot(anyc)) {
+        bool A[E], g1[E], g2[E];
+        after_flag<E>(cand, A);
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+          at[j] = cand[j] && !A[j];
+          g1[j] = A[j] || cand[j];
+          g2[j] = false;
+        }
+        int32_t none[1][E];
+        shift_v<E, K, 0>(R, none, g1, g2);
+      } else {
+        if (CH && !last) return kNextChunk;  // the slot is in a later chunk
+        if (pos1 > total) return MTE_E_INSERT_FAILED;  // mergeTree.ts:1666-1672
+#pragma unroll
+        for (int j = 0; j < E; j++) at[j] = base + j == n;  // append: the slot is padding
+      }
+      n += 1;
+      MTE_STAT(st[kStWritten] += 1;)
+    }
+    if (nlen > 0) put_new_v<E, K, S>(R, at, op, c, flags, a, st);
+    if constexpr (CH) dlen = nlen > 0 ? nlen : 0;
+  } else {
+    // markRangeRemoved / annotateRange: ensureIntervalBoundary at both ends
+    // (ordered by position), then mark start <= P < end
+    const int32_t b1 = pos1 < pos2 ? pos1 : pos2, b2 = pos1 < pos2 ? pos2 : pos1;
+    bool s1[E], s2[E], any1 = false, any2 = false;
+#pragma unroll
+    for (int j = 0; j < E; j++) {
+      s1[j] = ((uint32_t)(b1 - P[j]) - 1u) < slim[j];
+      s2[j] = b2 != b1 && ((uint32_t)(b2 - P[j]) - 1u) < slim[j];
+      any1 = any1 || s1[j];
+      any2 = any2 || s2[j];
+    }
+    uint64_t m1 = __ballot(any1), m2 = __ballot(any2);
+    int32_t bA = b1;
+    if (!m1) {  // only the end splits: it acts as the first split
+#pragma unroll
+      for (int j = 0; j < E; j++) {
+        s1[j] = s2[j];
+        s2[j] = false;
+      }
+      m1 = m2;
+      m2 = 0;
+      bA = b2;
+    }
+    if (m1) {
+      bool A[E], AB[E], nbB[E], nbB2[E], B[E];
+      after_flag<E>(s1, A);
+      after_flag<E>(s2, AB);
+      prev_flags<E>(s2, nbB, nbB2);
+      int32_t X[3][E];  // L, P and the split flags travel with the slot
+#pragma unroll
+      for (int j = 0; j < E; j++) {
+        B[j] = m2 != 0 && AB[j] && !nbB[j];
+        X[0][j] = L[j];
+        X[1][j] = P[j];
+        X[2][j] = (s1[j] ? 1 : 0) | (s2[j] ? 2 : 0);
+      }
+      shift_v<E, K, 3>(R, X, A, B);
+#pragma unroll
+      for (int j = 0; j < E; j++) {
+        // which piece of its source leaf slot j now holds
+        const int d = (A[j] ? 1 : 0) + (B[j] ? 1 : 0);
+        const bool h1 = (X[2][j] & 1) != 0, h2 = (X[2][j] & 2) != 0;
+        const int32_t oA = bA - X[1][j], oB = b2 - X[1][j];
+        const int kp = h1 ? d : d - 1;
+        const int32_t cutA = h1 ? oA : oB;
+        const int32_t st0 = (h1 || h2) ? (kp == 0 ? 0 : (kp == 1 ? cutA : oB)) : 0;
+        const int32_t en = (h1 || h2) ? (kp == 0 ? cutA : ((kp == 1 && h1 && h2) ? oB : R.len[j])) : R.len[j];
+        const int32_t nl = en - st0;
+        L[j] = (h1 || h2) ? nl : X[0][j];
+        P[j] = X[1][j] + st0;
+        R.len[j] = nl;
+        R.toff[j] += (uint32_t)st0;
+      }
+      n += m2 ? 2 : 1;
+      MTE_STAT(st[kStWritten] += m2 ? 4u : 2u;)
+    }
+    if (pos2 != pos1) {
+      // nodeMap (mergeTree.ts:2274-2330): no visible leaf straddles a boundary
+      bool in[E];
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int j = 0; j < E; j++) {
+        in[j] = L[j] > 0 && P[j] >= pos1 && P[j] < pos2;
+        cnt += (uint32_t)__popcll(__ballot(in[j]));
+      }
+      MTE_STAT(st[kStWritten] += cnt;)
+      if (type == MTE_OP_REMOVE) {
+        // markRemoved (mergeTree.ts:1924-1962)
+        const uint32_t bit = 1u << c;
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+          R.rseq[j] = (in[j] && R.rseq[j] == kNone) ? s : R.rseq[j];
+          R.rmask[j] = in[j] ? (R.rmask[j] | bit) : R.rmask[j];
+        }
+        if constexpr (CH) {  // the remover's own view loses the marked units
+          int32_t rl = 0;
+#pragma unroll
+          for (int j = 0; j < E; j++) rl += in[j] ? L[j] : 0;
+          dlen = -rdlane(wave_incl_scan(rl), kWave - 1);
+        }
+      } else if (cnt > 0) {
+        // PropertiesManager.addProperties (segmentPropertiesManager.ts:63-151)
+        const uint32_t psi = (uint32_t)op[6];
+        const s8v q2 = sload_props(a, psi);
+        if (flags & MTE_F_REWRITE) {
+#pragma unroll
+          for (int kk = 0; kk < K; kk++)
+#pragma unroll
+            for (int j = 0; j < E; j++) R.pr[kk][j] = in[j] ? 0u : R.pr[kk][j];
+        }
+        apply_props<E, K>(R.pr, in, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], psi, a);
+        MTE_STAT(st[kStPwrites] += cnt * (uint32_t)q2[3];)
+      }
+    }
+  }
+  return 0;
+}
+
 template <int E, int K, bool S>
 __device__ __forceinline__ int doc_step_v(Regs<E, K>& R, DocRun& D, uint32_t (&st)[kNumStats], s8v& cur,
                                           const ReplayArgs& a, uint32_t* zlds, int emin) {
@@ -170,169 +365,11 @@ __device__ __forceinline__ int doc_step_v(Regs<E, K>& R, DocRun& D, uint32_t (&s
   int n = D.n;
 
   if (type <= MTE_OP_ANNOTATE) {
-    const int32_t r = op[1], pos1 = op[4], pos2 = op[5];
     MTE_STAT(st[kStScanned] += (uint32_t)n;)
-    int32_t L[E], P[E];
-    leaf_lengths<E, K>(R, r, c + 1, (int)c, D.min_seq, (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0, L);
-    const int32_t total = prefix<E>(L, P);
-    // split candidate at b: the visible leaf with P < b < P + L
-    uint32_t slim[E];
-#pragma unroll
-    for (int j = 0; j < E; j++) slim[j] = L[j] > 1 ? (uint32_t)(L[j] - 1) : 0u;
-
-    if (type == MTE_OP_INSERT) {
-      // applyInsertOp -> insertSegments (client.ts:470-505, mergeTree.ts:1394-1422)
-      const bool marker = (flags & MTE_F_MARKER) != 0;
-      const int32_t nlen = marker ? 1 : pos2;
-      int32_t X[1][E];  // split offset, meaningful at the split leaf
-      bool sp[E], any = false;
-#pragma unroll
-      for (int j = 0; j < E; j++) {
-        X[0][j] = pos1 - P[j];
-        sp[j] = ((uint32_t)X[0][j] - 1u) < slim[j];
-        any = any || sp[j];
-      }
-      bool at[E];
-#pragma unroll
-      for (int j = 0; j < E; j++) at[j] = false;
-      if (__ballot(any)) {
-        // ensureIntervalBoundary: [head][new][tail], the tail a copy of the leaf
-        bool A[E], nb[E], nb2[E], g2[E];
-        after_flag<E>(sp, A);
-        prev_flags<E>(sp, nb, nb2);
-#pragma unroll
-        for (int j = 0; j < E; j++) g2[j] = nlen > 0 && A[j] && !nb[j];
-        bool own[E];
-#pragma unroll
-        for (int j = 0; j < E; j++) own[j] = sp[j];
-        shift_v<E, K, 1>(R, X, A, g2);
-#pragma unroll
-        for (int j = 0; j < E; j++) {
-          const bool tail = nlen > 0 ? nb2[j] : nb[j];
-          R.len[j] = own[j] ? X[0][j] : (tail ? R.len[j] - X[0][j] : R.len[j]);
-          R.toff[j] = tail ? R.toff[j] + (uint32_t)X[0][j] : R.toff[j];
-          at[j] = nlen > 0 && nb[j];
-        }
-        n += nlen > 0 ? 2 : 1;
-        MTE_STAT(st[kStWritten] += nlen > 0 ? 3u : 2u;)
-      } else if (nlen > 0) {
-        // insertingWalk: before the first defined leaf with P >= pos
-        bool cand[E], anyc = false;
-#pragma unroll
-        for (int j = 0; j < E; j++) {
-          cand[j] = L[j] >= 0 && P[j] >= pos1;
-          anyc = anyc || cand[j];
-        }
-        if (__ballot(anyc)) {
-          bool A[E], g1[E], g2[E];
-          after_flag<E>(cand, A);
-#pragma unroll
-          for (int j = 0; j < E; j++) {
-            at[j] = cand[j] && !A[j];
-            g1[j] = A[j] || cand[j];
-            g2[j] = false;
-          }
-          int32_t none[1][E];
-          shift_v<E, K, 0>(R, none, g1, g2);
-        } else {
-          if (pos1 > total) return MTE_E_INSERT_FAILED;  // mergeTree.ts:1666-1672
-#pragma unroll
-          for (int j = 0; j < E; j++) at[j] = base + j == n;  // append: the slot is padding
-        }
-        n += 1;
-        MTE_STAT(st[kStWritten] += 1;)
-      }
-      if (nlen > 0) put_new_v<E, K, S>(R, at, op, c, flags, a, st);
-    } else {
-      // markRangeRemoved / annotateRange: ensureIntervalBoundary at both ends
-      // (ordered by position), then mark start <= P < end
-      const int32_t b1 = pos1 < pos2 ? pos1 : pos2, b2 = pos1 < pos2 ? pos2 : pos1;
-      bool s1[E], s2[E], any1 = false, any2 = false;
-#pragma unroll
-      for (int j = 0; j < E; j++) {
-        s1[j] = ((uint32_t)(b1 - P[j]) - 1u) < slim[j];
-        s2[j] = b2 != b1 && ((uint32_t)(b2 - P[j]) - 1u) < slim[j];
-        any1 = any1 || s1[j];
-        any2 = any2 || s2[j];
-      }
-      uint64_t m1 = __ballot(any1), m2 = __ballot(any2);
-      int32_t bA = b1;
-      if (!m1) {  // only the end splits: it acts as the first split
-#pragma unroll
-        for (int j = 0; j < E; j++) {
-          s1[j] = s2[j];
-          s2[j] = false;
-        }
-        m1 = m2;
-        m2 = 0;
-        bA = b2;
-      }
-      if (m1) {
-        bool A[E], AB[E], nbB[E], nbB2[E], B[E];
-        after_flag<E>(s1, A);
-        after_flag<E>(s2, AB);
-        prev_flags<E>(s2, nbB, nbB2);
-        int32_t X[3][E];  // L, P and the split flags travel with the slot
-#pragma unroll
-        for (int j = 0; j < E; j++) {
-          B[j] = m2 != 0 && AB[j] && !nbB[j];
-          X[0][j] = L[j];
-          X[1][j] = P[j];
-          X[2][j] = (s1[j] ? 1 : 0) | (s2[j] ? 2 : 0);
-        }
-        shift_v<E, K, 3>(R, X, A, B);
-#pragma unroll
-        for (int j = 0; j < E; j++) {
-          // which piece of its source leaf slot j now holds
-          const int d = (A[j] ? 1 : 0) + (B[j] ? 1 : 0);
-          const bool h1 = (X[2][j] & 1) != 0, h2 = (X[2][j] & 2) != 0;
-          const int32_t oA = bA - X[1][j], oB = b2 - X[1][j];
-          const int kp = h1 ? d : d - 1;
-          const int32_t cutA = h1 ? oA : oB;
-          const int32_t st0 = (h1 || h2) ? (kp == 0 ? 0 : (kp == 1 ? cutA : oB)) : 0;
-          const int32_t en = (h1 || h2) ? (kp == 0 ? cutA : ((kp == 1 && h1 && h2) ? oB : R.len[j])) : R.len[j];
-          const int32_t nl = en - st0;
-          L[j] = (h1 || h2) ? nl : X[0][j];
-          P[j] = X[1][j] + st0;
-          R.len[j] = nl;
-          R.toff[j] += (uint32_t)st0;
-        }
-        n += m2 ? 2 : 1;
-        MTE_STAT(st[kStWritten] += m2 ? 4u : 2u;)
-      }
-      if (pos2 != pos1) {
-        // nodeMap (mergeTree.ts:2274-2330): no visible leaf straddles a boundary
-        bool in[E];
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int j = 0; j < E; j++) {
-          in[j] = L[j] > 0 && P[j] >= pos1 && P[j] < pos2;
-          cnt += (uint32_t)__popcll(__ballot(in[j]));
-        }
-        MTE_STAT(st[kStWritten] += cnt;)
-        if (type == MTE_OP_REMOVE) {
-          // markRemoved (mergeTree.ts:1924-1962)
-          const uint32_t bit = 1u << c;
-#pragma unroll
-          for (int j = 0; j < E; j++) {
-            R.rseq[j] = (in[j] && R.rseq[j] == kNone) ? s : R.rseq[j];
-            R.rmask[j] = in[j] ? (R.rmask[j] | bit) : R.rmask[j];
-          }
-        } else if (cnt > 0) {
-          // PropertiesManager.addProperties (segmentPropertiesManager.ts:63-151)
-          const uint32_t psi = (uint32_t)op[6];
-          const s8v q2 = sload_props(a, psi);
-          if (flags & MTE_F_REWRITE) {
-#pragma unroll
-            for (int kk = 0; kk < K; kk++)
-#pragma unroll
-              for (int j = 0; j < E; j++) R.pr[kk][j] = in[j] ? 0u : R.pr[kk][j];
-          }
-          apply_props<E, K>(R.pr, in, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], psi, a);
-          MTE_STAT(st[kStPwrites] += cnt * (uint32_t)q2[3];)
-        }
-      }
-    }
+    int32_t tot, dlen;
+    const int rc = seg_op_v<E, K, S, false>(R, n, op, type, c, flags, D.min_seq,
+                                            (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0, 0, true, tot, dlen, a, st);
+    if (rc) return rc;
   } else if (type != MTE_OP_NOOP) {
     return MTE_E_INVALID_ARG;
   }

@@ -367,7 +367,7 @@ __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
   if (!(a.hdr[doc].flags & kHdrNeedsEsc)) return;  // untouched doc: leave the header alone
   DocRun D;
   run_init(D, a, doc, true);
-  uint32_t st[kNumStats] = {0, 0, 0, 0, 0, 0};
+  uint32_t st[kNumStats] = {};
   if (D.running) {
     s8v cur = sload8(D.recp + 2 * D.k);
     while (D.running) {

@@ -10,7 +10,7 @@ import ctypes as C
 import numpy as np
 
 from . import _native
-from .abi import (DOC_INIT_DTYPE, EXPORTED_SYMBOLS, OP_DTYPE, PROP_DTYPE, PROPSET_DTYPE,
+from .abi import (DOC_INIT_DTYPE, EXPORTED_SYMBOLS, OP_DTYPE, PROP_DTYPE, PROPSET_DTYPE, SEG_DTYPE,
                   MergeTreeError, MteBatch, MteConfig, MteDocView, MteStats, ptr)
 from .packing import units_to_str
 
@@ -119,6 +119,12 @@ class DeviceEngine(EngineBase):
         self.n_docs = len(inits)
         self._check(self.lib.mte_load_docs(self.ctx, len(inits), ptr(inits), ptr(text), len(text),
                                            ptr(ps), len(ps), ptr(pe), len(pe)), "load_docs")
+
+    def load_segments(self, seg_offsets, segs):
+        """Replace docs' loaded content with segment lists (mte_load_segments)."""
+        offs = _arr(seg_offsets, np.uint64)
+        segs = _arr(segs, SEG_DTYPE)
+        self._check(self.lib.mte_load_segments(self.ctx, ptr(offs), ptr(segs), len(segs)), "load_segments")
 
     def submit(self, batch):
         b, keep = make_batch_struct(self.n_docs, batch)

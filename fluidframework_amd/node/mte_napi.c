@@ -356,6 +356,7 @@ static napi_value js_stats(napi_env env, napi_callback_info info) {
   set_f64(env, o, "maxSegs", (double)s.max_segs);
   set_f64(env, o, "kernelMs", s.kernel_ms);
   set_f64(env, o, "algoBytes", s.algo_bytes);
+  set_f64(env, o, "chunkScanned", (double)s.chunk_scanned);
   return o;
 }
 

@@ -108,7 +108,8 @@ typedef struct mte_ctx mte_ctx;
 typedef struct mte_config {
   int32_t device;        /* HIP device ordinal                                  */
   uint32_t n_keys;       /* property planes per segment, 0..MTE_MAX_KEYS        */
-  uint32_t seg_capacity; /* segments per doc kept in HBM (0 = default 4096)     */
+  uint32_t seg_capacity; /* segments per doc kept in HBM (0 = default 1024;
+                            >= 8192 adds the chunked big-document pass)       */
   uint32_t flags;        /* reserved, 0                                         */
 } mte_config;
 
@@ -126,6 +127,24 @@ typedef struct mte_doc_init {
   int32_t min_seq;   /* collab window at load (startOrUpdateCollaboration)    */
   int32_t cur_seq;
 } mte_doc_init;
+
+/* A segment with its merge info, as a summary holds it and SnapshotLoader
+ * restores it (IJSONSegmentWithMergeInfo, snapshotChunks.ts:48-78;
+ * snapshotLoader.ts:85-125): seq / client default to UniversalSequenceNumber /
+ * NonCollabClient there; here they are explicit.  client -1 stands for both
+ * LocalClientId and NonCollabClient (constants.ts:14-15): neither equals a
+ * remote short id, which is all the replay asks of it.                      */
+#define MTE_NOT_REMOVED 0x7fffffff
+typedef struct mte_seg {
+  uint32_t text_off;   /* text: unit offset into the mte_load_docs text       */
+  uint32_t len;        /* text: units (> 0); marker: 1                        */
+  int32_t seq;         /* insert seq (0 = UniversalSequenceNumber)            */
+  int32_t removed_seq; /* MTE_NOT_REMOVED or the removal seq                  */
+  uint32_t removers;   /* removedClientIds as a short-id bitmask             */
+  int32_t client;      /* short client id, or -1                              */
+  uint32_t kind;       /* 0 = text, 1 + refType = marker                      */
+  uint32_t propset;    /* index into the mte_load_docs propsets, or MTE_NO_PROPS */
+} mte_seg;
 
 /* One batch of sequenced ops for all documents of the ctx. */
 typedef struct mte_batch {
@@ -150,6 +169,8 @@ typedef struct mte_stats {
   uint64_t max_segs;        /* max segments held by any doc                   */
   double kernel_ms;         /* device time of the last mte_run (HIP events)   */
   double algo_bytes;        /* sum of B_op of the last run   */
+  uint64_t chunk_scanned;   /* chunked pass: chunk slots + summary entries its
+                               ops scanned (replaces their S_live in algo_bytes) */
 } mte_stats;
 
 /* Per-doc read-out (query-size-then-fill).  On input the *_cap fields give the
@@ -184,6 +205,14 @@ int mte_load_docs(mte_ctx* ctx, uint32_t n_docs, const mte_doc_init* docs,
                   const uint16_t* text, uint64_t text_units,
                   const mte_propset* propsets, uint32_t n_propsets,
                   const mte_prop* props, uint32_t n_props);
+
+/* Replace the loaded content of documents with segment lists (a summary's
+ * body, SnapshotLoader.loadBody snapshotLoader.ts:85-130): doc d takes
+ * segs[seg_offsets[d] .. seg_offsets[d+1]); a doc with an empty range keeps its
+ * mte_load_docs text.  Call after mte_load_docs; mte_reset restores this state.
+ * Text offsets and propsets refer to the buffers given to mte_load_docs.     */
+int mte_load_segments(mte_ctx* ctx, const uint64_t* seg_offsets, const mte_seg* segs,
+                      uint64_t n_segs);
 
 /* Upload one batch (host -> HBM, async on the ctx stream). */
 int mte_submit(mte_ctx* ctx, const mte_batch* batch);

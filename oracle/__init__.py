@@ -10,7 +10,7 @@ import subprocess
 
 import numpy as np
 
-from fluidframework_amd.abi import DOC_INIT_DTYPE, PROP_DTYPE, PROPSET_DTYPE, ptr
+from fluidframework_amd.abi import DOC_INIT_DTYPE, PROP_DTYPE, PROPSET_DTYPE, SEG_DTYPE, ptr
 from fluidframework_amd.engine import EngineBase, _arr, make_batch_struct
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -33,6 +33,7 @@ def load():
     for name, args in {
         "orc_create": [u32, vp], "orc_destroy": [vp],
         "orc_load_docs": [vp, u32, vp, vp, u64, vp, u32, vp, u32],
+        "orc_load_segments": [vp, vp, vp, u64],
         "orc_apply_batch": [vp, vp, C.c_int], "orc_read_doc": [vp, u32, vp],
         "orc_digest": [vp, vp, u32], "orc_doc_status": [vp, vp, u32],
         "orc_stats_get": [vp, vp], "orc_doc_nsegs": [vp, u32, vp],
@@ -74,6 +75,11 @@ class OracleEngine(EngineBase):
         self.n_docs = len(inits)
         self._check(self.lib.orc_load_docs(self.ctx, len(inits), ptr(inits), ptr(text), len(text),
                                            ptr(ps), len(ps), ptr(pe), len(pe)), "load_docs")
+
+    def load_segments(self, seg_offsets, segs):
+        offs = _arr(seg_offsets, np.uint64)
+        segs = _arr(segs, SEG_DTYPE)
+        self._check(self.lib.orc_load_segments(self.ctx, ptr(offs), ptr(segs), len(segs)), "load_segments")
 
     def apply_batch(self, batch):
         b, keep = make_batch_struct(self.n_docs, batch)

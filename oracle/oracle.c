@@ -53,6 +53,11 @@ struct orc_ctx {
   uint32_t n_keys;
   uint32_t n_docs;
   odoc* docs;
+  uint64_t load_units;     /* text units given to orc_load_docs */
+  mte_propset* load_ps;    /* propsets given to orc_load_docs (for orc_load_segments) */
+  uint32_t n_load_ps;
+  mte_prop* load_pe;
+  uint32_t n_load_pe;
   uint16_t* arena;
   uint64_t arena_n, arena_cap;
 };
@@ -361,6 +366,11 @@ static void free_docs(orc_ctx* c) {
   free(c->docs);
   c->docs = NULL;
   c->n_docs = 0;
+  free(c->load_ps);
+  free(c->load_pe);
+  c->load_ps = NULL;
+  c->load_pe = NULL;
+  c->n_load_ps = c->n_load_pe = 0;
 }
 
 int orc_destroy(orc_ctx* c) {
@@ -385,6 +395,19 @@ int orc_load_docs(orc_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
   if (c->docs) memset(c->docs, 0, (size_t)(n_docs ? n_docs : 1) * sizeof(odoc));
   if (!c->docs) return MTE_E_OOM;
   c->n_docs = n_docs;
+  c->load_units = text_units;
+  if (n_propsets) {
+    c->load_ps = (mte_propset*)malloc((size_t)n_propsets * sizeof(mte_propset));
+    if (!c->load_ps) return MTE_E_OOM;
+    memcpy(c->load_ps, propsets, (size_t)n_propsets * sizeof(mte_propset));
+    c->n_load_ps = n_propsets;
+  }
+  if (n_props) {
+    c->load_pe = (mte_prop*)malloc((size_t)n_props * sizeof(mte_prop));
+    if (!c->load_pe) return MTE_E_OOM;
+    memcpy(c->load_pe, props, (size_t)n_props * sizeof(mte_prop));
+    c->n_load_pe = n_props;
+  }
   for (uint32_t i = 0; i < n_docs; i++) {
     odoc* d = &c->docs[i];
     const mte_doc_init* in = &docs[i];
@@ -408,6 +431,45 @@ int orc_load_docs(orc_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
       }
       d->n = 1;
     }
+  }
+  return MTE_OK;
+}
+
+/* Snapshot body -> segments with their merge info (SnapshotLoader.loadBody,
+ * snapshotLoader.ts:85-125; IJSONSegmentWithMergeInfo, snapshotChunks.ts:48-78):
+ * seq, clientId, removedSeq and removedClientIds are taken as given. */
+int orc_load_segments(orc_ctx* c, const uint64_t* seg_offsets, const mte_seg* segs, uint64_t n_segs) {
+  if (!c || !seg_offsets || (n_segs && !segs)) return MTE_E_INVALID_ARG;
+  if (seg_offsets[0] != 0 || seg_offsets[c->n_docs] != n_segs) return MTE_E_INVALID_ARG;
+  for (uint32_t i = 0; i < c->n_docs; i++) {
+    const uint64_t b = seg_offsets[i], e = seg_offsets[i + 1];
+    if (e < b) return MTE_E_INVALID_ARG;
+    if (e == b) continue;
+    odoc* d = &c->docs[i];
+    int rc = doc_reserve(d, (uint32_t)(e - b) + 64);
+    if (rc) return rc;
+    for (uint64_t k = b; k < e; k++) {
+      const mte_seg* sg = &segs[k];
+      const int marker = sg->kind != 0;
+      if ((marker && sg->len != 1) || (!marker && (sg->len == 0 || (uint64_t)sg->text_off + sg->len > c->load_units)) ||
+          sg->client < -1 || sg->client >= MTE_MAX_CLIENTS || sg->seq < 0 ||
+          (sg->removed_seq != MTE_NOT_REMOVED && sg->removers == 0))
+        return MTE_E_INVALID_ARG;
+      oseg* g = &d->s[k - b];
+      memset(g, 0, sizeof(*g));
+      g->len = (int32_t)sg->len;
+      g->seq = sg->seq;
+      g->cli = sg->client;
+      g->rseq = sg->removed_seq == MTE_NOT_REMOVED ? NONE_SEQ : sg->removed_seq;
+      g->rmask = sg->removed_seq == MTE_NOT_REMOVED ? 0u : sg->removers;
+      g->kind = sg->kind;
+      g->toff = marker ? 0u : sg->text_off;
+      if (sg->propset != MTE_NO_PROPS) {
+        if (sg->propset >= c->n_load_ps) return MTE_E_INVALID_ARG;
+        apply_props(g->props, c->n_keys, &c->load_ps[sg->propset], c->load_pe, 0);
+      }
+    }
+    d->n = (uint32_t)(e - b);
   }
   return MTE_OK;
 }

@@ -32,6 +32,8 @@ int orc_load_docs(orc_ctx* c, uint32_t n_docs, const mte_doc_init* docs,
                   const uint16_t* text, uint64_t text_units,
                   const mte_propset* propsets, uint32_t n_propsets,
                   const mte_prop* props, uint32_t n_props);
+/* Replace docs' loaded content with segment lists (as mte_load_segments). */
+int orc_load_segments(orc_ctx* c, const uint64_t* seg_offsets, const mte_seg* segs, uint64_t n_segs);
 /* Apply a batch immediately, docs spread over n_threads pthreads. */
 int orc_apply_batch(orc_ctx* c, const mte_batch* b, int n_threads);
 int orc_read_doc(orc_ctx* c, uint32_t doc, mte_doc_view* v);

@@ -1,0 +1,165 @@
+"""GPU parity of the chunked big-document pass (mte_chunk.h, contexts with
+seg_capacity >= 8192) and of snapshot-body loading (mte_load_segments), against
+the CPU restatement: digests, statuses, op statistics and read-outs bit-exact.
+
+Config 5 (64 docs x 2^20 preloaded segments, 4 rounds of 65,536 concurrent
+ops) is exercised here at scaled sizes the flat oracle replays in seconds; the
+full size runs in bench.py --config 5 with a prefix parity sample."""
+import numpy as np
+import pytest
+
+from fluidframework_amd import gen
+from fluidframework_amd.abi import MTE_E_CAPACITY, NOT_REMOVED, OP_DTYPE, SEG_DTYPE
+from fluidframework_amd.engine import DeviceEngine
+from oracle import OracleEngine
+from test_gpu_parity import assert_same
+
+pytestmark = pytest.mark.gpu
+
+
+def both(stream, cap, threads=8):
+    o = OracleEngine(stream["n_keys"], threads=threads)
+    gen.load_stream(o, stream)
+    o.apply_batch(stream["batch"])
+    d = DeviceEngine(stream["n_keys"], seg_capacity=cap)
+    gen.load_stream(d, stream)
+    d.apply_batch(stream["batch"])
+    return o, d
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_gpu_chunk_config5_shaped(mode):
+    # 8 docs x 20,000 preloaded segments, 4 rounds of 2,000 concurrent ops
+    s = gen.generate(5, n_docs=8, ops_per_doc=8000, init_segs=20000, round_ops=2000, length_mode=mode)
+    cap = gen.seg_capacity(5, s["params"])
+    assert cap >= 8192
+    o, d = both(s, cap)
+    assert (o.statuses() == 0).all()
+    assert o.stats()["max_segs"] > 20000
+    assert_same(o, d, sample_docs=8)
+
+
+def test_gpu_chunk_farm_rule_ranges():
+    # long ranges (farm rule: end uniform in [start+1, L]) cross many chunks
+    s = gen.generate(5, n_docs=6, ops_per_doc=3000, init_segs=6000, round_ops=300, max_range=0)
+    o, d = both(s, 16384)
+    assert (o.statuses() == 0).all()
+    assert_same(o, d, sample_docs=6)
+
+
+def test_gpu_chunk_segment_body_equals_one_segment():
+    s = gen.generate(5, n_docs=4, ops_per_doc=4000, init_segs=5000, round_ops=1000)
+    d1 = DeviceEngine(s["n_keys"], seg_capacity=16384)
+    gen.load_stream(d1, s)
+    d1.apply_batch(s["batch"])
+    d2 = DeviceEngine(s["n_keys"], seg_capacity=16384)
+    d2.load_docs(s["inits"], s["init_text"])
+    d2.apply_batch(s["batch"])
+    np.testing.assert_array_equal(d1.statuses(), 0)
+    np.testing.assert_array_equal(d1.digest(), d2.digest())
+
+
+def test_gpu_chunk_reset_and_multi_batch():
+    s = gen.generate(5, n_docs=4, ops_per_doc=4000, init_segs=4000, round_ops=1000)
+    d = DeviceEngine(s["n_keys"], seg_capacity=16384)
+    gen.load_stream(d, s)
+    d.apply_batch(s["batch"])
+    one = d.digest()
+    d.reset()  # back to the loaded segment body
+    d.run()
+    d.sync()
+    np.testing.assert_array_equal(d.digest(), one)
+    # the same ops as 4 batches (one per round)
+    d.reset()
+    d.sync()
+    b = s["batch"]
+    offs = b["op_offsets"].astype(np.int64)
+    for k in range(4):
+        lo = offs[:-1] + k * 1000
+        parts = [b["ops"][int(x):int(x) + 1000] for x in lo]
+        sub = dict(b)
+        sub["ops"] = np.concatenate(parts)
+        sub["op_offsets"] = np.arange(len(offs), dtype=np.uint64) * 1000
+        d.apply_batch(sub)
+    np.testing.assert_array_equal(d.digest(), one)
+
+
+def test_gpu_chunk_insert_hotspot_relayouts():
+    # every insert lands in one chunk: overflow -> re-layout every ~126 ops
+    n0, n_ops = 3000, 2500
+    inits = np.zeros(1, gen.DOC_INIT_DTYPE)
+    inits["text_len"] = n0
+    inits["propset"] = 0xFFFFFFFF
+    text = np.full(n0, ord("a"), np.uint16)
+    offs_s, segs = gen.preload_segments(inits, n0)
+    ops = np.zeros(n_ops, OP_DTYPE)
+    ops["seq"] = np.arange(1, n_ops + 1)
+    ops["ref_seq"] = ops["seq"] - 1  # each op sees all earlier ones
+    ops["min_seq"] = 0
+    ops["type"] = 0
+    ops["client"] = 1 + (np.arange(n_ops) % 3)
+    ops["flags"] = 2  # MSG_END
+    ops["pos1"] = 1500
+    ops["pos2"] = 1
+    ops["a"] = np.arange(n_ops) % 26
+    ops["b"] = 0xFFFFFFFF
+    batch = {"op_offsets": np.array([0, n_ops], np.uint64), "ops": ops,
+             "text": np.arange(ord("A"), ord("A") + 26, dtype=np.uint16)}
+    o = OracleEngine(0)
+    o.load_docs(inits, text)
+    o.load_segments(offs_s, segs)
+    o.apply_batch(batch)
+    d = DeviceEngine(0, seg_capacity=8192)
+    d.load_docs(inits, text)
+    d.load_segments(offs_s, segs)
+    d.apply_batch(batch)
+    assert_same(o, d, sample_docs=1)
+
+
+def test_gpu_chunk_capacity_error():
+    s = gen.generate(5, n_docs=2, ops_per_doc=3000, init_segs=7000, round_ops=3000, mix=gen.MIX_INSERT)
+    d = DeviceEngine(s["n_keys"], seg_capacity=8192)
+    gen.load_stream(d, s)
+    d.apply_batch(s["batch"])
+    assert (d.statuses() == MTE_E_CAPACITY).all()
+
+
+def test_gpu_segment_body_with_merge_info():
+    text = np.frombuffer(("hello world" + "x" * 1500).encode("utf-16-le"), np.uint16)
+    inits = np.zeros(1, gen.DOC_INIT_DTYPE)
+    inits["text_len"] = len(text)
+    inits["propset"] = 0xFFFFFFFF
+    inits["min_seq"] = 5
+    inits["cur_seq"] = 10
+    ps = np.array([(0, 1)], gen.PROPSET_DTYPE)
+    pe = np.array([(1, 7)], gen.PROP_DTYPE)
+    rows = [(0, 5, 0, NOT_REMOVED, 0, -1, 0, 0), (5, 1, 8, 9, 1 << 2, 1, 0, 0xFFFFFFFF),
+            (0, 1, 7, NOT_REMOVED, 0, 3, 2, 0xFFFFFFFF), (6, 5, 6, NOT_REMOVED, 0, 1, 0, 0xFFFFFFFF)]
+    rows += [(11 + i, 1, 0, NOT_REMOVED, 0, -1, 0, 0xFFFFFFFF) for i in range(1500)]
+    segs = np.array(rows, SEG_DTYPE)
+    offs = np.array([0, len(segs)], np.uint64)
+    # a few remote ops on top: remove across the tombstone, annotate, insert
+    ops = np.zeros(3, OP_DTYPE)
+    ops["seq"] = [11, 12, 13]
+    ops["ref_seq"] = [10, 11, 12]
+    ops["min_seq"] = [5, 6, 6]
+    ops["type"] = [1, 2, 0]        # remove [3, 8) across the tombstone, annotate [0, 4), insert "AB" at 2
+    ops["client"] = [2, 3, 1]
+    ops["flags"] = 2               # MSG_END
+    ops["pos1"] = [3, 0, 2]
+    ops["pos2"] = [8, 4, 2]
+    ops["a"] = [0, 0, 0]
+    ops["b"] = [0, 0, 0xFFFFFFFF]
+    batch = {"op_offsets": np.array([0, 3], np.uint64), "ops": ops,
+             "text": np.array([65, 66], np.uint16), "propsets": ps, "props": pe}
+    res = []
+    for eng in (OracleEngine(4), DeviceEngine(4, seg_capacity=8192)):
+        eng.load_docs(inits, text, ps, pe)
+        eng.load_segments(offs, segs)
+        before = eng.read_doc(0)
+        eng.apply_batch(batch)
+        res.append((before, eng.read_doc(0), eng.digest()))
+    assert res[0][0] == res[1][0]
+    assert res[0][0]["text"].startswith("helloworld")
+    assert res[0][1] == res[1][1]
+    np.testing.assert_array_equal(res[0][2], res[1][2])
