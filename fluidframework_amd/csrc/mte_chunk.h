@@ -75,24 +75,32 @@ __device__ __forceinline__ uint64_t ch_slot(const ChunkArgs& ch, int doc, int i)
   return ((uint64_t)doc * ch.nch_cap + (uint32_t)i) * kChSlots;
 }
 
+// A chunk's planes into registers: one 16-byte load per plane and lane (every
+// slot of a chunk is allocated, so slots >= n are read and replaced by
+// padding).  Plain loads: the chunk data is written by this workgroup only,
+// and the CU's L1 is shared by its waves (workgroup-scope coherence).
+__device__ __forceinline__ uint4 ld4(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
 template <int K>
 __device__ __forceinline__ void ch_load(Regs<kChE, K>& R, const ChunkArgs& ch, uint64_t x0, int n) {
-  const uint32_t* pl = ch.arena;
+  const uint32_t* pl = ch.arena + x0 + (uint32_t)lane_id() * kChE;
   const uint64_t st = ch.astride;
+  uint4 q[kFieldPlanes + K];
+#pragma unroll
+  for (int p = 0; p < kFieldPlanes + K; p++) q[p] = ld4(pl + p * st);
   const int base = lane_id() * kChE;
 #pragma unroll
   for (int j = 0; j < kChE; j++) {
-    const int i = base + j;
-    const bool v = i < n;
-    const uint64_t x = x0 + (uint32_t)(v ? i : 0);
-    R.len[j] = v ? (int32_t)ld_ag(pl + x) : 0;
-    R.seq[j] = v ? (int32_t)ld_ag(pl + st + x) : 0;
-    R.rseq[j] = v ? (int32_t)ld_ag(pl + 2 * st + x) : kPad;
-    R.rmask[j] = v ? ld_ag(pl + 3 * st + x) : 0u;
-    R.meta[j] = v ? ld_ag(pl + 4 * st + x) : 0u;
-    R.toff[j] = v ? ld_ag(pl + 5 * st + x) : 0u;
+    const bool v = base + j < n;
+    auto el = [&](int p) -> uint32_t { return j == 0 ? q[p].x : (j == 1 ? q[p].y : (j == 2 ? q[p].z : q[p].w)); };
+    R.len[j] = v ? (int32_t)el(0) : 0;
+    R.seq[j] = v ? (int32_t)el(1) : 0;
+    R.rseq[j] = v ? (int32_t)el(2) : kPad;
+    R.rmask[j] = v ? el(3) : 0u;
+    R.meta[j] = v ? el(4) : 0u;
+    R.toff[j] = v ? el(5) : 0u;
 #pragma unroll
-    for (int k = 0; k < K; k++) R.pr[k][j] = v ? ld_ag(pl + (kFieldPlanes + k) * st + x) : 0u;
+    for (int k = 0; k < K; k++) R.pr[k][j] = v ? el(kFieldPlanes + k) : 0u;
   }
 }
 
@@ -121,8 +129,9 @@ __device__ __forceinline__ void ch_store(const Regs<kChE, K>& R, const ChunkArgs
 // First chunk whose inclusive prefix (column c) is > x (strict) or >= x.
 // Returns the chunk (nch if none) and its exclusive prefix in *excl; *total =
 // the doc's length in the column's perspective.
-__device__ __forceinline__ int ch_find(const uint32_t* G, uint32_t ng, const int32_t* sumc, int nch, int32_t x,
-                                       bool strict, int32_t* excl, int32_t* total) {
+__device__ __forceinline__ int ch_find(const uint32_t* G, uint32_t ng, const int32_t* sumc, const uint32_t* cnt,
+                                       int nch, int32_t x, bool strict, int32_t* excl, int32_t* total,
+                                       int32_t* csum, int* ccnt) {
   const int l = lane_id();
   const uint32_t gpl = (ng + kWave - 1) / kWave;  // groups per lane (<= 8)
   int32_t s = 0;
@@ -137,6 +146,8 @@ __device__ __forceinline__ int ch_find(const uint32_t* G, uint32_t ng, const int
   const uint64_t hm = __ballot(hit);
   if (!hm) {
     *excl = *total;
+    *csum = 0;
+    *ccnt = 0;
     return nch;
   }
   const int ls = __ffsll((long long)hm) - 1;
@@ -147,13 +158,16 @@ __device__ __forceinline__ int ch_find(const uint32_t* G, uint32_t ng, const int
     if (strict ? run + v > x : run + v >= x) break;
     run += v;
   }
-  // the 64 chunks of group g
+  // the 64 chunks of group g (their segment counts come along)
   const int i = (int)g * kChGroup + l;
   const int32_t v = i < nch ? ld_ag(sumc + i) : 0;
+  const int32_t nc = i < nch ? (int32_t)ld_ag(cnt + i) : 0;
   const int32_t ci = wave_incl_scan(v) + run;
   const uint64_t cm = __ballot(strict ? ci > x : ci >= x);
   const int lc = cm ? __ffsll((long long)cm) - 1 : kWave - 1;  // (cm != 0 by construction)
   *excl = rdlane(ci - v, lc);
+  *csum = rdlane(v, lc);
+  *ccnt = rdlane(nc, lc);
   return (int)g * kChGroup + lc;
 }
 
@@ -303,11 +317,17 @@ __device__ int ch_ops(DocRun& D, const ReplayArgs& a, const ChunkArgs& ch, uint3
   const uint32_t ng = (uint32_t)((nch + kChGroup - 1) / kChGroup);
   uint32_t* cnt = ch.cnt + (uint64_t)doc * ch.nch_cap;
   const bool newcalc = (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
+  s8v cur = sload8(D.recp + 2 * D.k);
   while (D.k < D.k1) {
     if constexpr (S) {
       if (st[kStOps] >= 256) run_flush_stats(D, st, a);
     }
-    const s8v op = sload8(D.recp + 2 * D.k);
+    // this op's record was prefetched; the next one is in flight meanwhile
+    // (past the last op it reads the next doc's record or the zeroed tail)
+    const s8v op = cur;
+    uint64_t next = reinterpret_cast<uint64_t>(D.recp + 2 * (D.k + 1));
+    asm volatile("" : "+s"(next) : "s"(op));
+    cur = sload8(reinterpret_cast<const uint4*>(next));
     const uint32_t w3 = (uint32_t)op[3];
     const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
     const int32_t s = op[0], r = op[1], msn = op[2];
@@ -337,36 +357,45 @@ __device__ int ch_ops(DocRun& D, const ReplayArgs& a, const ChunkArgs& ch, uint3
     if (type != MTE_OP_NOOP) {
       const int32_t pos1 = op[4], pos2 = op[5];
       int i0, i1;
-      int32_t ex = 0, total = 0, ex2 = 0;
+      int32_t ex = 0, total = 0, ex2 = 0, cs0 = 0, cs1 = 0;
+      int cn0 = 0, cn1 = 0;
       if (type == MTE_OP_INSERT) {
-        i0 = ch_find(Gc, ng, sumc, nch, pos1, false, &ex, &total);
+        i0 = ch_find(Gc, ng, sumc, cnt, nch, pos1, false, &ex, &total, &cs0, &cn0);
         scan += ng + kChGroup;
         if (pos1 > total) {  // no slot anywhere (mergeTree.ts:1666-1672)
           D.status = MTE_E_INSERT_FAILED;
           return kReqDone;
         }
-        if (i0 >= nch) i0 = nch - 1;
+        if (i0 >= nch) {
+          i0 = nch - 1;
+          cn0 = (int)ld_ag(cnt + i0);
+        }
         i1 = nch - 1;  // an insert may move on to later chunks (kNextChunk)
       } else {
         const int32_t b1 = pos1 < pos2 ? pos1 : pos2, b2 = pos1 < pos2 ? pos2 : pos1;
-        i0 = ch_find(Gc, ng, sumc, nch, b1, true, &ex, &total);
+        i0 = ch_find(Gc, ng, sumc, cnt, nch, b1, true, &ex, &total, &cs0, &cn0);
         scan += ng + kChGroup;
         if (i0 >= nch) {
           i1 = -1;  // the range starts past the end: nothing to split or mark
         } else if (b1 == b2) {
           i1 = ex < b1 ? i0 : -1;  // a split strictly inside a leaf, or nothing
+        } else if (ex + cs0 >= b2) {
+          i1 = i0;  // the range ends in its first chunk
+          cn1 = cn0;
         } else {
           int32_t t2;
-          i1 = ch_find(Gc, ng, sumc, nch, b2, false, &ex2, &t2);
+          i1 = ch_find(Gc, ng, sumc, cnt, nch, b2, false, &ex2, &t2, &cs1, &cn1);
           scan += ng + kChGroup;
-          if (i1 >= nch) i1 = nch - 1;
+          if (i1 >= nch) {
+            i1 = nch - 1;
+            cn1 = (int)ld_ag(cnt + i1);
+          }
         }
         // only the two boundary chunks can grow (one split each)
-        if (i1 >= i0 && ((int)ld_ag(cnt + i0) + 2 > kChSlots - 2 || (int)ld_ag(cnt + i1) + 2 > kChSlots - 2))
-          return kReqRelayout;
+        if (i1 >= i0 && (cn0 + 2 > kChSlots - 2 || cn1 + 2 > kChSlots - 2)) return kReqRelayout;
       }
       for (int i = i0; i <= i1; i++) {
-        int ni = (int)ld_ag(cnt + i);
+        int ni = i == i0 ? cn0 : (int)ld_ag(cnt + i);
         // an insert touches one chunk and nothing is applied before this
         // check; a range op checked its two boundary chunks above (the chunks
         // between them cannot split)
