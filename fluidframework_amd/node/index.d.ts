@@ -42,12 +42,24 @@ export interface EngineOptions {
   segCapacity?: number;
 }
 
+/** IJSONSegmentWithMergeInfo (snapshotChunks.ts:48-78): one segment of a summary body. */
+export interface SegmentWithMergeInfo {
+  json: string | { text: string; props?: PropertySet } | { marker: { refType: number }; props?: PropertySet };
+  client?: string;
+  seq?: number;
+  removedSeq?: number;
+  removedClient?: string;
+  removedClientIds?: string[];
+}
+
 export interface ClientOptions {
   observerId?: string;
   newLengthCalc?: boolean;
   props?: PropertySet;
   minSeq?: number;
   currentSeq?: number;
+  /** Load a summary body instead of initialText (SnapshotLoader.loadBody). */
+  segments?: SegmentWithMergeInfo[];
 }
 
 export class MergeTreeError extends Error {
@@ -58,6 +70,7 @@ export class MergeTreeError extends Error {
 export interface EngineStats {
   opsApplied: number;
   segsScanned: number;
+  chunkScanned?: number;
   segsWritten: number;
   propWrites: number;
   unitsInserted: number;

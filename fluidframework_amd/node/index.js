@@ -27,7 +27,7 @@
 const path = require("path");
 const packing = require("./packing");
 
-const { BatchBuilder, DocClients, Interner, MergeTreeError, packDocInits } = packing;
+const { BatchBuilder, DocClients, Interner, MergeTreeError, packDocInits, packSegments, utf16 } = packing;
 
 let addon = null;
 function loadAddon() {
@@ -74,13 +74,15 @@ class MergeTreeEngine {
 
   /** A new document (before the first flush).  initialText becomes one seq-0
    *  segment of LocalClientId, as the replay harness loads it
-   *  (client.replay.spec.ts:22-23). */
+   *  (client.replay.spec.ts:22-23); options.segments instead loads a summary
+   *  body — IJSONSegmentWithMergeInfo specs with seq / client / removedSeq /
+   *  removedClientIds — as SnapshotLoader.loadBody does (snapshotLoader.ts:85-125). */
   createClient(initialText, options) {
     if (this.started) throw new MergeTreeError(-10, "createClient after the engine started");
     const o = options || {};
     const doc = this.docs.length;
     this.docs.push({ text: initialText || "", newLengthCalc: !!o.newLengthCalc, props: o.props,
-      minSeq: o.minSeq || 0, currentSeq: o.currentSeq || 0 });
+      minSeq: o.minSeq || 0, currentSeq: o.currentSeq || 0, segments: o.segments });
     const c = new BatchClient(this, doc, o.observerId === undefined ? "A" : o.observerId);
     this.clients.push(c);
     return c;
@@ -89,7 +91,21 @@ class MergeTreeEngine {
   start() {
     if (this.started) return;
     const p = packDocInits(this.docs, this.interner);
+    let body = null;
+    if (this.docs.some((d) => d.segments)) {
+      // summary bodies (options.segments): their text follows the load text
+      const ps = Array.from(p.propsets), pe = Array.from(p.props);
+      body = packSegments(this.docs, (i) => this.clients[i].clients,
+        { interner: this.interner, propsetsArr: ps, propsArr: pe, textUnits: p.text.length });
+      const t = new Uint16Array(p.text.length + body.extraText.length);
+      t.set(p.text);
+      t.set(utf16(body.extraText), p.text.length);
+      p.text = t;
+      p.propsets = Uint32Array.from(ps);
+      p.props = Uint32Array.from(pe);
+    }
     this.addon.loadDocs(this.ctx, p.inits, p.text, p.propsets, p.props);
+    if (body) this.addon.loadSegments(this.ctx, body.offsets, body.segs);
     this.started = true;
     this.pending = new BatchBuilder(this.docs.length, this.interner);
     this.views = new Array(this.docs.length).fill(null);

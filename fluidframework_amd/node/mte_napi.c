@@ -197,6 +197,24 @@ static napi_value js_load_docs(napi_env env, napi_callback_info info) {
   return NULL;
 }
 
+/* loadSegments(ctx, offsets BigUint64Array(n+1), segs Uint8Array(32*k)) -> mte_load_segments */
+static napi_value js_load_segments(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  if (!get_args(env, info, 3, argv)) return NULL;
+  mte_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  void *offs, *segs;
+  size_t no, ns;
+  if (!get_bytes(env, argv[1], &offs, &no) || !get_bytes(env, argv[2], &segs, &ns)) return NULL;
+  if (no % 8 || ns % sizeof(mte_seg)) {
+    throw_rc(env, MTE_E_INVALID_ARG, ctx, "loadSegments: buffer sizes");
+    return NULL;
+  }
+  int rc = mte_load_segments(ctx, (const uint64_t*)offs, (const mte_seg*)segs, ns / sizeof(mte_seg));
+  throw_rc(env, rc, ctx, "mte_load_segments");
+  return NULL;
+}
+
 /* submit(ctx, offsets BigUint64Array(n+1), ops Uint8Array(32*k), text Uint16Array,
  *        propsets Uint32Array, props Uint32Array) */
 static napi_value js_submit(napi_env env, napi_callback_info info) {
@@ -368,6 +386,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"destroy", NULL, js_destroy, NULL, NULL, NULL, napi_enumerable, NULL},
       {"lastError", NULL, js_last_error, NULL, NULL, NULL, napi_enumerable, NULL},
       {"loadDocs", NULL, js_load_docs, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"loadSegments", NULL, js_load_segments, NULL, NULL, NULL, napi_enumerable, NULL},
       {"submit", NULL, js_submit, NULL, NULL, NULL, napi_enumerable, NULL},
       {"run", NULL, js_run, NULL, NULL, NULL, napi_enumerable, NULL},
       {"sync", NULL, js_sync, NULL, NULL, NULL, napi_enumerable, NULL},

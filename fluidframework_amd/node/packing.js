@@ -317,8 +317,59 @@ function packDocInits(docs, interner) {
   };
 }
 
+/**
+ * A summary body per document -> mte_seg records (include/mte.h) appended to
+ * the load text of packDocInits.  Each spec is an IJSONSegmentWithMergeInfo
+ * (snapshotChunks.ts:48-78): {json: "text" | {text, props} | {marker:{refType},
+ * props}, client?, seq?, removedSeq?, removedClientIds?}; client ids are
+ * registered in the document's DocClients in order, as SnapshotLoader.loadBody
+ * does (snapshotLoader.ts:90-118); a missing client / seq means NonCollabClient
+ * / UniversalSequenceNumber.
+ */
+function packSegments(docs, clientsOf, inits) {
+  const SEG_BYTES = 32;
+  let n = 0;
+  docs.forEach((d) => { n += d.segments ? d.segments.length : 0; });
+  const buf = Buffer.alloc(n * SEG_BYTES);
+  const offsets = new BigUint64Array(docs.length + 1);
+  const props = new PropTable(inits.interner);
+  props.sets = inits.propsetsArr;
+  props.entries = inits.propsArr;
+  const extra = [];
+  let textOff = inits.textUnits;
+  let k = 0;
+  docs.forEach((d, i) => {
+    offsets[i] = BigInt(k);
+    for (const sp of d.segments || []) {
+      const j = sp.json;
+      let text = null, kind = 0, segProps;
+      if (typeof j === "string") text = j;
+      else if (j && typeof j.text === "string") { text = j.text; segProps = j.props; }
+      else if (j && j.marker) { kind = 1 + (j.marker.refType >>> 0); segProps = j.props; }
+      else throw new MergeTreeError(E_INVALID_ARG, "segment spec");
+      const o = k * SEG_BYTES;
+      buf.writeUInt32LE(text === null ? 0 : textOff, o);
+      buf.writeUInt32LE(text === null ? 1 : text.length, o + 4);
+      buf.writeInt32LE(sp.seq === undefined ? 0 : sp.seq, o + 8);
+      const removed = sp.removedSeq !== undefined;
+      buf.writeInt32LE(removed ? sp.removedSeq : 0x7fffffff, o + 12);
+      let mask = 0;
+      const rc = sp.removedClientIds || (sp.removedClient !== undefined ? [sp.removedClient] : []);
+      for (const id of rc) mask |= 1 << clientsOf(i).short(id);
+      buf.writeUInt32LE(mask >>> 0, o + 16);
+      buf.writeInt32LE(sp.client === undefined ? -1 : clientsOf(i).short(sp.client), o + 20);
+      buf.writeUInt32LE(kind, o + 24);
+      buf.writeUInt32LE(props.add(segProps) >>> 0, o + 28);
+      if (text !== null) { extra.push(text); textOff += text.length; }
+      k++;
+    }
+  });
+  offsets[docs.length] = BigInt(k);
+  return { offsets, segs: new Uint8Array(buf.buffer, buf.byteOffset, buf.length), extraText: extra.join("") };
+}
+
 module.exports = {
   OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, F_MARKER, F_MSG_END, F_REWRITE, NO_PROPS, MAX_CLIENTS,
   INSERT, REMOVE, ANNOTATE, GROUP,
-  MergeTreeError, Interner, DocClients, PropTable, BatchBuilder, canonicalJson, packDocInits, utf16,
+  MergeTreeError, Interner, DocClients, PropTable, BatchBuilder, canonicalJson, packDocInits, packSegments, utf16,
 };

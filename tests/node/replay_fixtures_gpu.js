@@ -7,7 +7,18 @@ const { loadFixtures, asMsg } = require("./fixtures");
 
 const fx = loadFixtures();
 const eng = new MergeTreeEngine({ nKeys: 8 });
-const clients = fx.map((f) => eng.createClient(f.rounds[0].initialText));
+// argv "body": each initial text arrives as a summary body of 3-unit
+// segments (SnapshotLoader.loadBody path, mte_load_segments) instead of one
+// segment; segmentation is unobservable, so every checkpoint must still hold
+const asBody = process.argv[2] === "body";
+function body(t) {
+  const segs = [];
+  for (let i = 0; i < t.length; i += 3) segs.push({ json: t.slice(i, i + 3) });
+  return segs;
+}
+const clients = fx.map((f) => (asBody
+  ? eng.createClient("", { segments: body(f.rounds[0].initialText) })
+  : eng.createClient(f.rounds[0].initialText)));
 let passed = 0;
 const failures = [];
 const nRounds = Math.max.apply(null, fx.map((f) => f.rounds.length));

@@ -23,7 +23,7 @@ NODE = shutil.which("node")
 ADDON = os.path.join(ROOT, "fluidframework_amd", "_lib", "mte_napi.node")
 pytestmark = pytest.mark.skipif(NODE is None, reason="node not installed")
 
-EXPORTS = ["abiVersion", "strerror", "create", "destroy", "lastError", "loadDocs", "submit", "run",
+EXPORTS = ["abiVersion", "strerror", "create", "destroy", "lastError", "loadDocs", "loadSegments", "submit", "run",
            "sync", "reset", "digest", "docStatus", "readDoc", "stats"]
 
 
@@ -80,3 +80,12 @@ def test_node_batch_client_replays_fixtures_on_gpu():
     _, _, o = replay_fixtures(lambda k: OracleEngine(k), check=False)
     want = [format(int(x), "x") for x in o.digest().reshape(-1)]
     assert j["digests"] == want
+
+
+@pytest.mark.gpu
+def test_node_summary_body_load_replays_fixtures_on_gpu():
+    # initial texts loaded as summary bodies (3-unit segments) through
+    # BatchClient options.segments -> loadSegments -> mte_load_segments
+    j = json.loads(node("tests/node/replay_fixtures_gpu.js", "body", timeout=600))
+    assert j["nFailures"] == 0, j["failures"]
+    assert j["passed"] == 30 * 64 * 2
