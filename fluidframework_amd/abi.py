@@ -92,6 +92,11 @@ class MteStats(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class MteSegList(C.Structure):
+    _fields_ = [("segs", C.c_void_p), ("props", C.c_void_p), ("seg_cap", C.c_uint64), ("n_segs", C.c_uint64),
+                ("text", C.c_void_p), ("text_cap", C.c_uint64), ("n_text", C.c_uint64)]
+
+
 class MteDocView(C.Structure):
     _fields_ = [("status", C.c_int32), ("cur_seq", C.c_int32), ("min_seq", C.c_int32),
                 ("length", C.c_uint32),
@@ -104,7 +109,7 @@ class MteDocView(C.Structure):
 EXPORTED_SYMBOLS = [
     "mte_abi_version", "mte_strerror", "mte_create", "mte_destroy", "mte_last_error",
     "mte_load_docs", "mte_load_segments", "mte_submit", "mte_run", "mte_sync", "mte_reset", "mte_digest",
-    "mte_digest_device", "mte_read_doc", "mte_doc_status", "mte_stats_get", "mte_set_stats",
+    "mte_digest_device", "mte_read_doc", "mte_read_segments", "mte_doc_status", "mte_stats_get", "mte_set_stats",
 ]
 
 

@@ -810,6 +810,50 @@ int mte_read_doc(mte_ctx* c, uint32_t doc, mte_doc_view* v) {
   return MTE_OK;
 }
 
+int mte_read_segments(mte_ctx* c, uint32_t doc, mte_seg_list* v) {
+  if (!c || !v || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  DocHdr h;
+  HIPCHK(c, hipMemcpyAsync(&h, c->hdr + doc, sizeof(DocHdr), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint32_t n = (uint32_t)std::max(h.nseg, 0);
+  const uint64_t db = (uint64_t)doc * c->cap;
+  const uint32_t np = kFieldPlanes + c->n_keys;
+  std::vector<uint32_t> pl((size_t)np * (n + 1));
+  for (uint32_t p = 0; p < np && n; p++)
+    HIPCHK(c, hipMemcpyAsync(pl.data() + (size_t)p * n, reinterpret_cast<const uint32_t*>(c->soa.len) +
+                                                             p * c->soa.plane_stride + db,
+                             n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  uint64_t nt = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const int32_t len = (int32_t)pl[i], rseq = (int32_t)pl[2 * (size_t)n + i];
+    const uint32_t meta = pl[4 * (size_t)n + i], kind = meta >> 8;
+    if (i < v->seg_cap && v->segs) {
+      mte_seg& s = v->segs[i];
+      s.text_off = kind == 0 ? (uint32_t)nt : 0u;
+      s.len = (uint32_t)len;
+      s.seq = (int32_t)pl[(size_t)n + i];
+      s.removed_seq = rseq == kNone ? MTE_NOT_REMOVED : rseq;
+      s.removers = rseq == kNone ? 0u : pl[3 * (size_t)n + i];
+      s.client = (int32_t)(meta & 0xffu) - 1;
+      s.kind = kind;
+      s.propset = MTE_NO_PROPS;
+      if (v->props)
+        for (uint32_t k = 0; k < c->n_keys; k++)
+          v->props[(size_t)i * c->n_keys + k] = pl[(size_t)(kFieldPlanes + k) * n + i];
+    }
+    if (kind == 0) {
+      const uint32_t toff = pl[5 * (size_t)n + i];
+      for (int32_t u = 0; u < len; u++, nt++)
+        if (nt < v->text_cap && v->text) v->text[nt] = c->h_arena[toff + (uint32_t)u];
+    }
+  }
+  v->n_segs = n;
+  v->n_text = nt;
+  return MTE_OK;
+}
+
 int mte_set_stats(mte_ctx* c, int enable) {
   if (!c) return MTE_E_INVALID_ARG;
   c->stats_on = enable != 0;

@@ -11,7 +11,7 @@ import numpy as np
 
 from . import _native
 from .abi import (DOC_INIT_DTYPE, EXPORTED_SYMBOLS, OP_DTYPE, PROP_DTYPE, PROPSET_DTYPE, SEG_DTYPE,
-                  MergeTreeError, MteBatch, MteConfig, MteDocView, MteStats, ptr)
+                  MergeTreeError, MteBatch, MteConfig, MteDocView, MteSegList, MteStats, ptr)
 from .packing import units_to_str
 
 
@@ -66,6 +66,19 @@ class EngineBase:
                 for i in range(v.n_segs)]
         return {"status": v.status, "cur_seq": v.cur_seq, "min_seq": v.min_seq,
                 "length": v.length, "text": units_to_str(text[: v.n_text]), "segs": segs}
+
+    def read_segments(self, doc):
+        """-> (segs SEG_DTYPE[n] with text_off into text, props uint32[n, n_keys], text uint16[])."""
+        v = MteSegList()
+        self._check(self._read_segments(doc, C.byref(v)), "read_segments")
+        segs = np.zeros(max(v.n_segs, 1), SEG_DTYPE)
+        props = np.zeros(max(v.n_segs, 1) * max(self.n_keys, 1), np.uint32)
+        text = np.zeros(max(v.n_text, 1), np.uint16)
+        v.segs, v.props, v.seg_cap = ptr(segs), ptr(props), len(segs)
+        v.text, v.text_cap = ptr(text), len(text)
+        self._check(self._read_segments(doc, C.byref(v)), "read_segments")
+        n = v.n_segs
+        return segs[:n], props[: n * self.n_keys].reshape(n, self.n_keys), text[: v.n_text]
 
     def digest(self):
         out = np.zeros(self.n_docs * 4, np.uint64)
@@ -162,6 +175,9 @@ class DeviceEngine(EngineBase):
 
     def _digest(self, p, n):
         return self.lib.mte_digest(self.ctx, p, n)
+
+    def _read_segments(self, doc, lp):
+        return self.lib.mte_read_segments(self.ctx, doc, lp)
 
     def _doc_status(self, p, n):
         return self.lib.mte_doc_status(self.ctx, p, n)

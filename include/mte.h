@@ -229,6 +229,22 @@ int mte_digest(mte_ctx* ctx, uint64_t* out, uint32_t n_docs);
 int mte_digest_device(mte_ctx* ctx, void* device_out, uint32_t n_docs);
 
 int mte_read_doc(mte_ctx* ctx, uint32_t doc, mte_doc_view* view);
+
+/* Every segment a document holds — removed ones above minSeq included — with
+ * its merge info, in document order: the input of a summary writer
+ * (SnapshotV1.extractSegment, snapshotV1.ts:189-265).  Query-size-then-fill
+ * like mte_doc_view.  segs[i].text_off indexes `text`, segs[i].propset is
+ * MTE_NO_PROPS and the values are in props[i * n_keys ..].                   */
+typedef struct mte_seg_list {
+  mte_seg* segs;
+  uint32_t* props;
+  uint64_t seg_cap;
+  uint64_t n_segs;
+  uint16_t* text;
+  uint64_t text_cap;
+  uint64_t n_text;
+} mte_seg_list;
+int mte_read_segments(mte_ctx* ctx, uint32_t doc, mte_seg_list* list);
 int mte_doc_status(mte_ctx* ctx, int32_t* out, uint32_t n_docs);
 int mte_stats_get(mte_ctx* ctx, mte_stats* out);
 /* Statistics accounting (the counters of mte_stats, like the reference's

@@ -34,6 +34,7 @@ def load():
         "orc_create": [u32, vp], "orc_destroy": [vp],
         "orc_load_docs": [vp, u32, vp, vp, u64, vp, u32, vp, u32],
         "orc_load_segments": [vp, vp, vp, u64],
+        "orc_read_segments": [vp, u32, vp],
         "orc_apply_batch": [vp, vp, C.c_int], "orc_read_doc": [vp, u32, vp],
         "orc_digest": [vp, vp, u32], "orc_doc_status": [vp, vp, u32],
         "orc_stats_get": [vp, vp], "orc_doc_nsegs": [vp, u32, vp],
@@ -75,6 +76,9 @@ class OracleEngine(EngineBase):
         self.n_docs = len(inits)
         self._check(self.lib.orc_load_docs(self.ctx, len(inits), ptr(inits), ptr(text), len(text),
                                            ptr(ps), len(ps), ptr(pe), len(pe)), "load_docs")
+
+    def _read_segments(self, doc, lp):
+        return self.lib.orc_read_segments(self.ctx, doc, lp)
 
     def load_segments(self, seg_offsets, segs):
         offs = _arr(seg_offsets, np.uint64)

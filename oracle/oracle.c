@@ -572,6 +572,34 @@ int orc_read_doc(orc_ctx* c, uint32_t doc, mte_doc_view* v) {
   return MTE_OK;
 }
 
+int orc_read_segments(orc_ctx* c, uint32_t doc, mte_seg_list* v) {
+  if (!c || !v || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  odoc* d = &c->docs[doc];
+  uint64_t nt = 0;
+  for (uint32_t i = 0; i < d->n; i++) {
+    const oseg* g = &d->s[i];
+    if (i < v->seg_cap && v->segs) {
+      mte_seg* s = &v->segs[i];
+      s->text_off = g->kind == 0 ? (uint32_t)nt : 0u;
+      s->len = (uint32_t)g->len;
+      s->seq = g->seq;
+      s->removed_seq = g->rseq == NONE_SEQ ? MTE_NOT_REMOVED : g->rseq;
+      s->removers = g->rseq == NONE_SEQ ? 0u : g->rmask;
+      s->client = g->cli;
+      s->kind = g->kind;
+      s->propset = MTE_NO_PROPS;
+      if (v->props)
+        for (uint32_t k = 0; k < c->n_keys; k++) v->props[(size_t)i * c->n_keys + k] = g->props[k];
+    }
+    if (g->kind == 0)
+      for (int32_t u = 0; u < g->len; u++, nt++)
+        if (nt < v->text_cap && v->text) v->text[nt] = c->arena[g->toff + (uint32_t)u];
+  }
+  v->n_segs = d->n;
+  v->n_text = nt;
+  return MTE_OK;
+}
+
 /* ---- canonical digest (DESIGN.md "Digest") ------------------------------- */
 #define M61 ((1ull << 61) - 1)
 static const uint64_t DIG_B1 = 0x1d8e4e27c47d124full % ((1ull << 61) - 1);

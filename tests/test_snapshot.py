@@ -1,0 +1,84 @@
+"""Summary round trip: replay half of a batch, write
+every document's body (snapshotV1.ts:189-265 rules, fluidframework_amd/
+snapshot.py), load the bodies into a fresh engine (snapshotLoader.ts:85-125,
+mte_load_segments) and replay the rest: the digests must equal the
+uninterrupted replay's.  CPU on the restatement, GPU on the engine."""
+import numpy as np
+import pytest
+
+from fluidframework_amd import gen, snapshot
+from fluidframework_amd.engine import DeviceEngine
+from oracle import OracleEngine
+
+
+def split_batch(stream, k):
+    """(first k ops of every doc, the rest)."""
+    b = stream["batch"]
+    o = b["op_offsets"].astype(np.int64)
+    first = gen.prefix_ops(stream, len(o) - 1, k)["batch"]
+    rest_ops = np.concatenate([b["ops"][o[i] + min(k, o[i + 1] - o[i]):o[i + 1]] for i in range(len(o) - 1)])
+    cnt = np.array([max(0, (o[i + 1] - o[i]) - k) for i in range(len(o) - 1)])
+    offs = np.zeros(len(o), np.uint64)
+    offs[1:] = np.cumsum(cnt)
+    return first, dict(b, ops=rest_ops, op_offsets=offs)
+
+
+def round_trip(make, stream, k):
+    full = make(stream["n_keys"])
+    gen.load_stream(full, stream)
+    full.apply_batch(stream["batch"])
+    first, rest = split_batch(stream, k)
+    a = make(stream["n_keys"])
+    gen.load_stream(a, stream)
+    a.apply_batch(first)
+    n = len(stream["inits"])
+    views = [a.read_doc(d) for d in range(n)]
+    bodies = [snapshot.write_body(a, d, views[d]["min_seq"]) for d in range(n)]
+    windows = [(v["min_seq"], v["cur_seq"]) for v in views]
+    inits, text, ps, pe, offs, segs = snapshot.load_bodies(bodies, windows, stream["inits"]["flags"],
+                                                          stream["n_keys"])
+    b = make(stream["n_keys"])
+    b.load_docs(inits, text, ps, pe)
+    b.load_segments(offs, segs)
+    for d in range(n):  # the loaded summary reads out as the summarized doc
+        assert b.read_doc(d)["text"] == views[d]["text"]
+    b.apply_batch(rest)
+    assert (full.statuses() == 0).all() and (b.statuses() == 0).all()
+    np.testing.assert_array_equal(b.digest(), full.digest())
+    return bodies
+
+
+def test_summary_round_trip_oracle():
+    s = gen.generate(3, n_docs=24, ops_per_doc=1500)  # R = 64: cut at a round boundary and inside one
+    for k in (640, 700):
+        bodies = round_trip(lambda nk: OracleEngine(nk), s, k)
+        assert any("removedSeq" in sp for body in bodies for sp in body)  # tombstones above the MSN kept
+        assert any("seq" not in sp for body in bodies for sp in body)     # below-MSN text coalesced
+
+
+def test_summary_writer_coalesces_and_elides():
+    s = gen.generate(2, n_docs=4, ops_per_doc=600)
+    o = OracleEngine(s["n_keys"])
+    gen.load_stream(o, s)
+    o.apply_batch(s["batch"])
+    for d in range(4):
+        v = o.read_doc(d)
+        body = snapshot.write_body(o, d, v["cur_seq"])  # everything at or below the MSN
+        assert all("seq" not in sp and "removedSeq" not in sp for sp in body)
+        units = [u for sp in body for u in (sp["json"] if isinstance(sp["json"], list) else
+                                            sp["json"].get("text", []))]
+        assert "".join(map(chr, units)) == v["text"]
+
+
+@pytest.mark.gpu
+def test_gpu_summary_round_trip():
+    s = gen.generate(3, n_docs=64, ops_per_doc=1500)
+    bodies_d = round_trip(lambda nk: DeviceEngine(nk), s, 700)
+    bodies_o = round_trip(lambda nk: OracleEngine(nk), s, 700)
+    assert bodies_d == bodies_o  # the GPU's summary is the restatement's
+
+
+@pytest.mark.gpu
+def test_gpu_summary_round_trip_long_docs():
+    s = gen.generate(5, n_docs=4, ops_per_doc=4000, init_segs=6000, round_ops=1000)
+    round_trip(lambda nk: DeviceEngine(nk, seg_capacity=16384), s, 2000)
