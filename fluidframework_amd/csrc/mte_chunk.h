@@ -175,7 +175,7 @@ __device__ __forceinline__ int ch_find(const uint32_t* G, uint32_t ng, const int
 
 // block-wide exclusive scan of kc[0, nch) in place; returns the total
 __device__ __forceinline__ int32_t ch_block_scan(uint32_t* kc, int nch, ChCtl* ctl) {
-  const int t = (int)threadIdx.x, w = t / kWave;
+  const int t = (int)threadIdx.x, w = __builtin_amdgcn_readfirstlane(t / kWave);
   const int per = (nch + kChWaves * kWave - 1) / (kChWaves * kWave);
   const int i0 = t * per;
   int32_t s = 0;
@@ -204,7 +204,7 @@ __device__ __forceinline__ int32_t ch_block_scan(uint32_t* kc, int nch, ChCtl* c
 // chunks -> flat planes, dropping tombstones with rseq <= m; returns the new n
 template <int K>
 __device__ int32_t ch_gather(const ReplayArgs& a, const ChunkArgs& ch, int doc, ChCtl* ctl, int nch, int32_t m) {
-  const int w = (int)threadIdx.x / kWave, l = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
   uint32_t* cnt = ch.cnt + (uint64_t)doc * ch.nch_cap;
   uint32_t* kc = ch.kc + (uint64_t)doc * ch.nch_cap;
   for (int i = w; i < nch; i += kChWaves) {
@@ -252,7 +252,7 @@ __device__ int32_t ch_gather(const ReplayArgs& a, const ChunkArgs& ch, int doc, 
 // flat planes -> chunks of kChFill segments; returns the chunk count
 template <int K>
 __device__ int ch_scatter(const ReplayArgs& a, const ChunkArgs& ch, int doc, int n) {
-  const int w = (int)threadIdx.x / kWave, l = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
   uint32_t* cnt = ch.cnt + (uint64_t)doc * ch.nch_cap;
   int nch = (n + kChFill - 1) / kChFill;
   if (nch < 1) nch = 1;
@@ -280,7 +280,7 @@ __device__ int ch_scatter(const ReplayArgs& a, const ChunkArgs& ch, int doc, int
 template <int K>
 __device__ void ch_rebuild(const ChunkArgs& ch, int doc, uint32_t* Gc, int nch, int c, int32_t r, int32_t m,
                            bool newcalc) {
-  const int w = (int)threadIdx.x / kWave, l = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
   const uint32_t* cnt = ch.cnt + (uint64_t)doc * ch.nch_cap;
   int32_t* sumc = ch.sum + ((uint64_t)doc * MTE_MAX_CLIENTS + (uint32_t)c) * ch.nch_cap;
   for (int i = w; i < nch; i += kChWaves) {
@@ -325,7 +325,7 @@ __device__ int ch_ops(DocRun& D, const ReplayArgs& a, const ChunkArgs& ch, uint3
     // this op's record was prefetched; the next one is in flight meanwhile
     // (past the last op it reads the next doc's record or the zeroed tail)
     const s8v op = cur;
-    uint64_t next = reinterpret_cast<uint64_t>(D.recp + 2 * (D.k + 1));
+    uint64_t next = uni64(reinterpret_cast<uint64_t>(D.recp + 2 * (D.k + 1)));
     asm volatile("" : "+s"(next) : "s"(op));
     cur = sload8(reinterpret_cast<const uint4*>(next));
     const uint32_t w3 = (uint32_t)op[3];
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(512) void chunk_kernel(ReplayArgs a, ChunkArgs ch) 
   if (!(a.hdr[doc].flags & kHdrNeedsEsc)) return;  // untouched doc: leave the header alone
   uint32_t* G = ch_lds;  // [MTE_MAX_CLIENTS][ng_cap]
   ChCtl* ctl = reinterpret_cast<ChCtl*>(ch_lds + (size_t)MTE_MAX_CLIENTS * ch.ng_cap);
-  const int w = (int)threadIdx.x / kWave;
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
   DocRun D;
   uint32_t st[kNumStats] = {};
   if (w == 0) {
