@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <type_traits>
@@ -247,6 +248,11 @@ struct mte_ctx {
   uint64_t* d_img_off = nullptr;
   uint64_t n_img = 0;
 
+  // diagnostics: MTE_WAVE_CLOCK=<file> dumps pass-1 start / end times per
+  // pair (s_memrealtime, 100 MHz) at every mte_sync
+  unsigned long long* d_wclock = nullptr;
+  const char* wclock_path = nullptr;
+
   // chunked big-document pass (seg_capacity >= kChunkMinCap, mte_chunk.h)
   bool chunked = false;
   ChunkArgs ch{};
@@ -329,6 +335,8 @@ void free_docs(mte_ctx* c) {
     if (p) (void)hipFree(p);
   c->ch = ChunkArgs{};
   c->chunked = false;
+  if (c->d_wclock) (void)hipFree(c->d_wclock);
+  c->d_wclock = nullptr;
   void* ps[] = {c->hdr, c->soa.len, c->stats, c->d_inits, c->d_init_props, c->d_digest, c->d_pairs};
   for (void* p : ps)
     if (p) (void)hipFree(p);
@@ -364,7 +372,7 @@ template <int K, bool S>
 int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   // pass 1: two documents per wavefront (docs up to 126 segments)
   const uint32_t b1 = (c->n_pairs + kPairsPerBlock - 1) / kPairsPerBlock;
-  hipLaunchKernelGGL((pair_kernel<K, S>), dim3(b1), dim3(256), 0, c->stream, a);
+  hipLaunchKernelGGL((pair_kernel<K, S, kPairsPerBlock>), dim3(b1), dim3(kPairsPerBlock * kWave), 0, c->stream, a);
   HIPCHK(c, hipGetLastError());
   // pass 2: docs that outgrew pass 1 continue one per wavefront (up to 1022 segments)
   const uint32_t b2 = (c->n_docs + kDocsPerBlock - 1) / kDocsPerBlock;
@@ -420,6 +428,7 @@ int mte_create(const mte_config* cfg, mte_ctx** out) {
   c->n_keys = cfg->n_keys;
   c->kt = cfg->n_keys == 0 ? 0 : (cfg->n_keys <= 4 ? 4 : 8);
   c->cap = cfg->seg_capacity ? cfg->seg_capacity : 1024;
+  c->wclock_path = std::getenv("MTE_WAVE_CLOCK");
   if (c->cap < 64) c->cap = 64;
   if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
@@ -692,6 +701,11 @@ int mte_run(mte_ctx* c) {
   a.stats = c->stats;
   a.pair_docs = c->d_pairs;
   a.n_pairs = c->n_pairs;
+  a.wclock = nullptr;
+  if (c->wclock_path) {
+    if (!c->d_wclock) HIPCHK(c, hipMalloc((void**)&c->d_wclock, 16ull * (c->n_pairs + 1)));
+    a.wclock = c->d_wclock;
+  }
   if (c->n_propsets) {
     hipLaunchKernelGGL(props_kernel, dim3((uint32_t)((c->n_propsets + 255) / 256)), dim3(256), 0, c->stream, c->d_ps,
                        (uint32_t)c->n_propsets, c->d_pe, c->n_keys, c->d_cps);
@@ -713,6 +727,14 @@ int mte_sync(mte_ctx* c) {
   if (!c) return MTE_E_INVALID_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->wclock_path && c->d_wclock) {
+    std::vector<unsigned long long> w(2ull * c->n_pairs);
+    HIPCHK(c, hipMemcpy(w.data(), c->d_wclock, w.size() * 8, hipMemcpyDeviceToHost));
+    if (FILE* f = std::fopen(c->wclock_path, "wb")) {
+      std::fwrite(w.data(), 8, w.size(), f);
+      std::fclose(f);
+    }
+  }
   return MTE_OK;
 }
 

@@ -91,6 +91,7 @@ struct ReplayArgs {
   unsigned long long* stats;  // n_docs * kNumStats
   const uint32_t* pair_docs;  // pair kernel: doc index per pair half (2 per pair)
   uint32_t n_pairs;
+  unsigned long long* wclock;  // diagnostics (MTE_WAVE_CLOCK): pass-1 start / end time per pair, or null
 };
 
 // ---- wavefront primitives --------------------------------------------------

@@ -30,6 +30,9 @@
 #ifndef MTE_PASS1_EMAX
 #define MTE_PASS1_EMAX 4
 #endif
+#ifndef MTE_FAIR_PRIO  // 1: pass-1 waves raise their issue priority with the work they have left
+#define MTE_FAIR_PRIO 1
+#endif
 #ifndef MTE_OUTLINE  // 1: pass-1 tiers as out-of-line functions (measured: same time, 1.7x the HBM traffic)
 #define MTE_OUTLINE 0
 #endif
@@ -811,16 +814,41 @@ __device__ __forceinline__ void run_to_lds(const DocRun& D, DocHdr* hl) {
   fence_wave();
 }
 
+// Fair issue between the waves sharing a SIMD.  The SIMD arbiter favours the
+// oldest wave, so with equal work per wave the youngest starves, then runs
+// alone (latency-bound) at the end: measured on config 3 the pass-1 waves
+// ended in five steps by dispatch order, 14.9 ms to 26.3 ms (tools/
+// wave_clock.py).  Setting the priority from the work left (4 levels) keeps
+// the waves of a SIMD abreast, so they finish together.
+__device__ __forceinline__ void fair_prio(uint32_t left, uint32_t total) {
+  if constexpr (MTE_FAIR_PRIO == 1) {
+    const uint32_t q = (uint32_t)(((uint64_t)left * 4u) / (total ? total : 1u));
+    if (q >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (q == 2) __builtin_amdgcn_s_setprio(2);
+    else if (q == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+  } else if constexpr (MTE_FAIR_PRIO == 2) {
+    // geometric bands (> 1/4, > 3/32, > 1/32 of the work left): the last band,
+    // where the waves fall back to age order, is short
+    const uint64_t l32 = (uint64_t)left * 32u, t = total ? total : 1u;
+    if (l32 > 8 * t) __builtin_amdgcn_s_setprio(3);
+    else if (l32 > 3 * t) __builtin_amdgcn_s_setprio(2);
+    else if (l32 > t) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+  }
+}
+
 // pass 1: two documents per wavefront, replayed in alternating bursts, so a
 // 10k-document batch is resident on the chip at once with the register
 // budget of one document (E <= 4)
-template <int K, bool S>
-__global__ __launch_bounds__(256, MTE_PAIR_WAVES) void pair_kernel(ReplayArgs a) {
-  __shared__ uint32_t zlds_all[kPairsPerBlock][kWave * 4];
-  __shared__ DocHdr hl_all[kPairsPerBlock][2];
-  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
-  const int pair = (int)blockIdx.x * kPairsPerBlock + w;
+template <int K, bool S, int WPB>
+__global__ __launch_bounds__(WPB * kWave, MTE_PAIR_WAVES * 4 / WPB) void pair_kernel(ReplayArgs a) {
+  __shared__ uint32_t zlds_all[WPB][kWave * 4];
+  __shared__ DocHdr hl_all[WPB][2];
+  const int w = WPB == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+  const int pair = (int)blockIdx.x * WPB + w;
   if (pair >= (int)a.n_pairs) return;
+  if (a.wclock && lane_id() == 0) a.wclock[2 * pair] = __builtin_amdgcn_s_memrealtime();
   int docs[2] = {(int)a.pair_docs[2 * pair], (int)a.pair_docs[2 * pair + 1]};
   if (docs[1] == docs[0]) docs[1] = -1;
   DocHdr* hl = hl_all[w];
@@ -836,20 +864,32 @@ __global__ __launch_bounds__(256, MTE_PAIR_WAVES) void pair_kernel(ReplayArgs a)
     }
   }
   fence_wave();
+  // ops of the pair in this pass, and those left (for fair_prio)
+  uint32_t total = 0;
+#pragma unroll
+  for (int t = 0; t < 2; t++)
+    if (docs[t] >= 0) total += (uint32_t)(a.op_off[docs[t] + 1] - a.op_off[docs[t]]) - hl[t].resume;
+  total = uni(total);
+  uint32_t left = total;
+  fair_prio(left, total);
   // one burst per iteration, alternating between the two documents; a single
   // copy of the burst code serves both (the document is a runtime index)
   for (int t = 0; live; t ^= 1) {
     if (!(live & (1u << t))) continue;
     const int doc = t ? docs[1] : docs[0];
     DocRun D;
+    const uint32_t k0 = hl[t].resume;
     if (run_from_lds(D, &hl[t], doc, a)) pass1_burst<K, S>(D, a, zlds);
     run_to_lds(D, &hl[t]);
     if (!D.running) live &= ~(1u << t);
+    left -= uni(hl[t].resume - k0);
+    fair_prio(left, total);
   }
   if (lane_id() == 0) {
 #pragma unroll
     for (int t = 0; t < 2; t++)
       if (docs[t] >= 0) a.hdr[docs[t]] = hl[t];  // resume = the op cursor
+    if (a.wclock) a.wclock[2 * pair + 1] = __builtin_amdgcn_s_memrealtime();
   }
 }
 

@@ -6,10 +6,11 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 tail -2 gpurun_out/gpu_tests.log
 timeout -k 10 200 python3 -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke.log 2>&1 || { echo SMOKEFAIL; tail -20 gpurun_out/smoke.log; exit 1; }
 cat gpurun_out/smoke.log
-timeout -k 10 400 python3 -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo BENCHFAIL; tail -20 gpurun_out/bench.err; exit 1; }
-cat gpurun_out/bench.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1 || { echo PROFFAIL; tail -20 gpurun_out/prof.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/pmc_fetch.log 2>&1 || { echo PMCFAIL; tail -20 gpurun_out/pmc_fetch.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/pmc_write.log 2>&1 || { echo PMCFAIL; tail -20 gpurun_out/pmc_write.log; exit 1; }
 python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_traffic_config3.json
+cp gpurun_out/pmc_traffic_config3.json profiles/r01/pmc_traffic_config3.json
+timeout -k 10 400 python3 -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo BENCHFAIL; tail -20 gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.json
 echo ALLOK
