@@ -20,7 +20,8 @@
 
 #include "mte_kernels.h"
 
-// Build-time knobs (tools/variants.sh builds A/B variants; defaults are the product build)
+// Build-time knobs (tools/variants.sh builds A/B variants; defaults are the product build).
+// MTE_FAIR_PRIO: 0 = hardware age order, 1 = 4 linear bands (product), 2 = geometric bands.
 #ifndef MTE_PAIR_WAVES
 #define MTE_PAIR_WAVES 5
 #endif
