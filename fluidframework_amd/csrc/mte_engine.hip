@@ -10,7 +10,9 @@
 #include <cstring>
 #include <new>
 #include <type_traits>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mte_kernels.h"
@@ -248,6 +250,12 @@ struct mte_ctx {
   uint64_t* d_img_off = nullptr;
   uint64_t n_img = 0;
 
+  // pinned staging for op-record uploads (mte_submit), allocated on first use
+  static constexpr int kStages = 3;
+  static constexpr size_t kStageBytes = 64ull << 20;
+  void* stage[kStages] = {nullptr, nullptr, nullptr};
+  hipEvent_t stage_ev[kStages] = {nullptr, nullptr, nullptr};
+
   // diagnostics: MTE_WAVE_CLOCK=<file> dumps pass-1 start / end times per
   // pair (s_memrealtime, 100 MHz) at every mte_sync
   unsigned long long* d_wclock = nullptr;
@@ -390,6 +398,78 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   return MTE_OK;
 }
 
+// Validation of one op record (the kernels index with these fields, so a bad
+// record must never reach them).  Returns nullptr or the reason.
+const char* bad_op(const mte_op& o, const mte_batch* b) {
+  if (o.type > MTE_OP_NOOP) return "type";
+  if (o.type == MTE_OP_INSERT) {
+    if (!(o.flags & MTE_F_MARKER) && o.pos2 > 0 && (uint64_t)o.a + (uint64_t)o.pos2 > b->text_units)
+      return "text out of range";
+    if ((o.flags & MTE_F_MARKER) && (o.pos2 < 0 || o.pos2 >= (1 << 23))) return "refType out of range";
+    if (!(o.flags & MTE_F_MARKER) && o.pos2 < 0) return "negative text length";
+    if (o.b != MTE_NO_PROPS && o.b >= b->n_propsets) return "propset out of range";
+  } else if (o.type == MTE_OP_ANNOTATE && o.a >= b->n_propsets) {
+    return "propset out of range";
+  }
+  return nullptr;
+}
+
+unsigned host_workers() {
+  const unsigned hw = std::thread::hardware_concurrency();
+  return hw == 0 ? 1u : (hw > 16 ? 16u : hw);
+}
+
+// Host op records -> HBM: validated and copied in one pass by host_workers()
+// threads into pinned staging buffers, each buffer's DMA overlapping the
+// filling of the next (pageable hipMemcpy runs at a fraction of PCIe speed).
+// Returns MTE_OK or MTE_E_INVALID_ARG with *bad = the first bad record.
+int upload_ops(mte_ctx* c, const mte_batch* b, uint64_t* bad, const char** why) {
+  for (int i = 0; i < mte_ctx::kStages; i++) {
+    if (!c->stage[i]) HIPCHK(c, hipHostMalloc(&c->stage[i], mte_ctx::kStageBytes, hipHostMallocDefault));
+    if (!c->stage_ev[i]) HIPCHK(c, hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
+  }
+  const uint64_t per_stage = mte_ctx::kStageBytes / sizeof(mte_op);
+  const unsigned nw = host_workers();
+  std::atomic<uint64_t> first_bad{UINT64_MAX};
+  std::vector<const char*> reasons(nw, nullptr);
+  for (uint64_t k0 = 0, it = 0; k0 < b->n_ops; k0 += per_stage, it++) {
+    const int si = (int)(it % mte_ctx::kStages);
+    const uint64_t n = std::min(per_stage, b->n_ops - k0);
+    HIPCHK(c, hipEventSynchronize(c->stage_ev[si]));  // its previous DMA has drained
+    mte_op* dst = static_cast<mte_op*>(c->stage[si]);
+    std::vector<std::thread> th;
+    for (unsigned w = 0; w < nw; w++) {
+      th.emplace_back([&, w]() {
+        const uint64_t a = n * w / nw, e = n * (w + 1) / nw;
+        for (uint64_t k = a; k < e; k++) {
+          const mte_op& o = b->ops[k0 + k];
+          if (const char* r = bad_op(o, b)) {
+            uint64_t cur = first_bad.load();
+            while (k0 + k < cur && !first_bad.compare_exchange_weak(cur, k0 + k)) {
+            }
+            if (first_bad.load() == k0 + k) reasons[w] = r;
+            return;
+          }
+        }
+        std::memcpy(dst + a, b->ops + k0 + a, (e - a) * sizeof(mte_op));
+      });
+    }
+    for (auto& t : th) t.join();
+    if (first_bad.load() != UINT64_MAX) break;
+    HIPCHK(c, hipMemcpyAsync(c->d_ops + k0, dst, n * sizeof(mte_op), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipEventRecord(c->stage_ev[si], c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (first_bad.load() != UINT64_MAX) {
+    *bad = first_bad.load();
+    *why = "bad record";
+    for (const char* r : reasons)
+      if (r) *why = r;
+    return MTE_E_INVALID_ARG;
+  }
+  return MTE_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -459,6 +539,10 @@ int mte_destroy(mte_ctx* c) {
   void* ps[] = {c->arena, c->d_ops, c->d_cps, c->d_off, c->d_ps, c->d_pe, c->d_pow};
   for (void* p : ps)
     if (p) (void)hipFree(p);
+  for (int i = 0; i < mte_ctx::kStages; i++) {
+    if (c->stage[i]) (void)hipHostFree(c->stage[i]);
+    if (c->stage_ev[i]) (void)hipEventDestroy(c->stage_ev[i]);
+  }
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -628,33 +712,9 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
   for (uint32_t i = 0; i < b->n_propsets; i++)
     if ((uint64_t)b->propsets[i].first + b->propsets[i].count > b->n_props)
       return set_err(c, MTE_E_INVALID_ARG, "propset %u out of range", i);
-  // host-side validation of every record, so no kernel can index out of bounds
-  for (uint64_t k = 0; k < b->n_ops; k++) {
-    const mte_op& o = b->ops[k];
-    if (o.type > MTE_OP_NOOP) return set_err(c, MTE_E_INVALID_ARG, "op %llu: type %u", (unsigned long long)k, o.type);
-    if (o.type == MTE_OP_INSERT) {
-      if (!(o.flags & MTE_F_MARKER) && o.pos2 > 0 && (uint64_t)o.a + (uint64_t)o.pos2 > b->text_units)
-        return set_err(c, MTE_E_INVALID_ARG, "op %llu: text out of range", (unsigned long long)k);
-      if ((o.flags & MTE_F_MARKER) && (o.pos2 < 0 || o.pos2 >= (1 << 23)))
-        return set_err(c, MTE_E_INVALID_ARG, "op %llu: refType out of range", (unsigned long long)k);
-      if (!(o.flags & MTE_F_MARKER) && o.pos2 < 0)
-        return set_err(c, MTE_E_INVALID_ARG, "op %llu: negative text length", (unsigned long long)k);
-      if (o.b != MTE_NO_PROPS && o.b >= b->n_propsets)
-        return set_err(c, MTE_E_INVALID_ARG, "op %llu: propset out of range", (unsigned long long)k);
-    } else if (o.type == MTE_OP_ANNOTATE && o.a >= b->n_propsets) {
-      return set_err(c, MTE_E_INVALID_ARG, "op %llu: propset out of range", (unsigned long long)k);
-    }
-  }
   if (c->arena_n + b->text_units >= (1ull << 32)) return set_err(c, MTE_E_OOM, "text arena exceeds 2^32 units");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
-  // append batch text to the arena
-  if ((rc = grow(c, &c->arena, &c->arena_cap, c->arena_n + b->text_units + 1, true, c->arena_n))) return rc;
-  if (b->text_units)
-    HIPCHK(c, hipMemcpyAsync(c->arena + c->arena_n, b->text, b->text_units * 2, hipMemcpyHostToDevice, c->stream));
-  c->h_arena.insert(c->h_arena.end(), b->text, b->text + b->text_units);
-  c->batch_text_base = (uint32_t)c->arena_n;
-  c->arena_n += b->text_units;
   // the replay kernels read the records in place; kRecPad zeroed records
   // follow the last one for the L2 prefetch that runs ahead
   if ((rc = grow(c, &c->d_ops, &c->ops_cap, b->n_ops + kRecPad))) return rc;
@@ -662,7 +722,21 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
   if ((rc = grow(c, &c->d_off, &c->off_cap, (uint64_t)b->n_docs + 1))) return rc;
   if ((rc = grow(c, &c->d_ps, &c->ps_cap, (uint64_t)b->n_propsets + 1))) return rc;
   if ((rc = grow(c, &c->d_pe, &c->pe_cap, (uint64_t)b->n_props + 1))) return rc;
-  if (b->n_ops) HIPCHK(c, hipMemcpyAsync(c->d_ops, b->ops, b->n_ops * sizeof(mte_op), hipMemcpyHostToDevice, c->stream));
+  if (b->n_ops) {
+    // every record is validated on the way (no kernel may index out of bounds)
+    uint64_t bad = 0;
+    const char* why = "";
+    c->submitted = false;
+    if ((rc = upload_ops(c, b, &bad, &why)))
+      return rc == MTE_E_INVALID_ARG ? set_err(c, rc, "op %llu: %s", (unsigned long long)bad, why) : rc;
+  }
+  // append batch text to the arena
+  if ((rc = grow(c, &c->arena, &c->arena_cap, c->arena_n + b->text_units + 1, true, c->arena_n))) return rc;
+  if (b->text_units)
+    HIPCHK(c, hipMemcpyAsync(c->arena + c->arena_n, b->text, b->text_units * 2, hipMemcpyHostToDevice, c->stream));
+  c->h_arena.insert(c->h_arena.end(), b->text, b->text + b->text_units);
+  c->batch_text_base = (uint32_t)c->arena_n;
+  c->arena_n += b->text_units;
   HIPCHK(c, hipMemcpyAsync(c->d_off, b->op_offsets, ((uint64_t)b->n_docs + 1) * 8, hipMemcpyHostToDevice, c->stream));
   if (b->n_propsets)
     HIPCHK(c, hipMemcpyAsync(c->d_ps, b->propsets, b->n_propsets * sizeof(mte_propset), hipMemcpyHostToDevice, c->stream));

@@ -214,7 +214,9 @@ int mte_load_docs(mte_ctx* ctx, uint32_t n_docs, const mte_doc_init* docs,
 int mte_load_segments(mte_ctx* ctx, const uint64_t* seg_offsets, const mte_seg* segs,
                       uint64_t n_segs);
 
-/* Upload one batch (host -> HBM, async on the ctx stream). */
+/* Upload one batch (host -> HBM on the ctx stream; returns once the inputs are
+ * copied).  Every record is validated on the way; on an error the previously
+ * submitted batch is discarded (mte_run then returns MTE_E_STATE).           */
 int mte_submit(mte_ctx* ctx, const mte_batch* batch);
 /* Enqueue the replay of the submitted batch; returns without waiting. */
 int mte_run(mte_ctx* ctx);

@@ -199,3 +199,24 @@ def test_gpu_stats_off_same_result():
     np.testing.assert_array_equal(off.statuses(), on.statuses())
     assert on.stats()["ops_applied"] == int(s["batch"]["op_offsets"][-1])
     assert off.stats()["ops_applied"] == 0
+
+
+@pytest.mark.gpu
+def test_gpu_submit_rejects_bad_record():
+    from fluidframework_amd.abi import MergeTreeError
+    s = gen.generate(3, n_docs=40, ops_per_doc=3000)
+    d = DeviceEngine(s["n_keys"])
+    d.load_docs(s["inits"], s["init_text"])
+    b = dict(s["batch"])
+    ops = b["ops"].copy()
+    ops["type"][77777] = 9  # one bad record deep inside the upload
+    with pytest.raises(MergeTreeError) as e:
+        d.submit(dict(b, ops=ops))
+    assert "op 77777" in str(e.value)
+    with pytest.raises(MergeTreeError):
+        d.run()  # the failed submit discarded the batch
+    d.apply_batch(s["batch"])  # a good batch still replays exactly
+    o = OracleEngine(s["n_keys"], threads=8)
+    o.load_docs(s["inits"], s["init_text"])
+    o.apply_batch(s["batch"])
+    np.testing.assert_array_equal(d.digest(), o.digest())
