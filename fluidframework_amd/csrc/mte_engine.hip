@@ -25,8 +25,10 @@ using namespace mte;
 namespace {
 
 // reset resume/escalation flags and stats at the start of a batch
-__global__ void begin_batch_kernel(DocHdr* hdr, unsigned long long* stats, uint32_t n_docs) {
+__global__ void begin_batch_kernel(DocHdr* hdr, unsigned long long* stats, uint32_t n_docs,
+                                   unsigned long long* gdone) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d == 0) *gdone = 0;
   if (d >= n_docs) return;
   hdr[d].resume = 0;
   hdr[d].flags &= ~kHdrNeedsEsc;
@@ -259,6 +261,7 @@ struct mte_ctx {
   // diagnostics: MTE_WAVE_CLOCK=<file> dumps pass-1 start / end times per
   // pair (s_memrealtime, 100 MHz) at every mte_sync
   unsigned long long* d_wclock = nullptr;
+  unsigned long long* d_gdone = nullptr;  // pass-1 global progress (fair priority)
   const char* wclock_path = nullptr;
 
   // chunked big-document pass (seg_capacity >= kChunkMinCap, mte_chunk.h)
@@ -536,7 +539,7 @@ int mte_destroy(mte_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   free_docs(c);
-  void* ps[] = {c->arena, c->d_ops, c->d_cps, c->d_off, c->d_ps, c->d_pe, c->d_pow};
+  void* ps[] = {c->arena, c->d_ops, c->d_cps, c->d_off, c->d_ps, c->d_pe, c->d_pow, c->d_gdone};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int i = 0; i < mte_ctx::kStages; i++) {
@@ -756,8 +759,9 @@ int mte_run(mte_ctx* c) {
   if (!c->n_docs) return MTE_OK;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));  // kernel_ms covers every kernel of the run
+  if (!c->d_gdone) HIPCHK(c, hipMalloc((void**)&c->d_gdone, 64));
   hipLaunchKernelGGL(begin_batch_kernel, dim3((c->n_docs + 255) / 256), dim3(256), 0, c->stream, c->hdr, c->stats,
-                     c->n_docs);
+                     c->n_docs, c->d_gdone);
   HIPCHK(c, hipGetLastError());
   ReplayArgs a;
   a.hdr = c->hdr;
@@ -776,6 +780,8 @@ int mte_run(mte_ctx* c) {
   a.pair_docs = c->d_pairs;
   a.n_pairs = c->n_pairs;
   a.wclock = nullptr;
+  a.gdone = c->d_gdone;
+  a.n_ops = c->n_ops;
   if (c->wclock_path) {
     if (!c->d_wclock) HIPCHK(c, hipMalloc((void**)&c->d_wclock, 16ull * (c->n_pairs + 1)));
     a.wclock = c->d_wclock;

@@ -92,6 +92,8 @@ struct ReplayArgs {
   const uint32_t* pair_docs;  // pair kernel: doc index per pair half (2 per pair)
   uint32_t n_pairs;
   unsigned long long* wclock;  // diagnostics (MTE_WAVE_CLOCK): pass-1 start / end time per pair, or null
+  unsigned long long* gdone;   // pass 1: ops applied so far by all waves (fair priority), zeroed per run
+  unsigned long long n_ops;    // ops of the batch
 };
 
 // ---- wavefront primitives --------------------------------------------------

@@ -121,4 +121,6 @@ export class BatchClient {
   getCollabWindow(): { clientId: number; currentSeq: number; minSeq: number; collaborating: boolean };
   getPropertiesAtPosition(pos: number): PropertySet | undefined;
   getSegments(): VisibleSegment[];
+  /** Summary body (SnapshotV1.extractSegment rules) + the collab window to load it with. */
+  summarize(): { segments: SegmentWithMergeInfo[]; minSeq: number; currentSeq: number };
 }

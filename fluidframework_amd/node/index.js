@@ -29,6 +29,13 @@ const packing = require("./packing");
 
 const { BatchBuilder, DocClients, Interner, MergeTreeError, packDocInits, packSegments, utf16 } = packing;
 
+// UTF-16 code units -> JS string (chunked: apply() on a huge array overflows the stack)
+function unitsToString(u) {
+  let out = "";
+  for (let i = 0; i < u.length; i += 8192) out += String.fromCharCode.apply(null, u.subarray(i, i + 8192));
+  return out;
+}
+
 let addon = null;
 function loadAddon() {
   if (addon === null) {
@@ -270,6 +277,64 @@ class BatchClient {
       }
     }
     return out;
+  }
+
+  /**
+   * Summary body of this document: SnapshotV1.extractSegment
+   * (snapshotV1.ts:189-265) over the segments the engine holds
+   * (mte_read_segments).  Segments removed at or below minSeq are elided;
+   * segments inserted at or below minSeq and not removed lose their merge
+   * info and coalesce (TextSegment.canAppend textSegment.ts:72-77 +
+   * matchProperties); the rest keep seq / client / removedSeq /
+   * removedClientIds.  Load it with createClient("", {segments, minSeq,
+   * currentSeq}).  Returns {segments, minSeq, currentSeq}.
+   */
+  summarize() {
+    const eng = this.engine;
+    const v = eng._view(this.doc);
+    const minSeq = v.minSeq;
+    const nk = eng.nKeys;
+    const r = eng.addon.readSegments(eng.ctx, this.doc, nk);
+    const dv = new DataView(r.segs.buffer, r.segs.byteOffset, r.segs.byteLength);
+    const n = r.segs.byteLength / 32;
+    const out = [];
+    let prev = null;
+    const json = (sg) => {
+      if (sg.kind === 0) return sg.props ? { text: sg.text, props: sg.props } : sg.text;
+      return sg.props ? { marker: { refType: sg.kind - 1 }, props: sg.props } : { marker: { refType: sg.kind - 1 } };
+    };
+    const same = (a, b) => packing.canonicalJson(a || {}) === packing.canonicalJson(b || {});
+    const canAppend = (a, b) => a.kind === 0 && b.kind === 0 && !a.text.endsWith("\n") &&
+      (a.text.length <= 256 || b.text.length <= 256);
+    for (let i = 0; i < n; i++) {
+      const o = i * 32;
+      const textOff = dv.getUint32(o, true), len = dv.getUint32(o + 4, true), seq = dv.getInt32(o + 8, true);
+      const rseq = dv.getInt32(o + 12, true), removers = dv.getUint32(o + 16, true);
+      const client = dv.getInt32(o + 20, true), kind = dv.getUint32(o + 24, true);
+      const removed = rseq !== 0x7fffffff;
+      if (removed && rseq <= minSeq) continue;
+      const sg = { kind, props: eng.interner.decode(nk ? r.props.subarray(i * nk, (i + 1) * nk) : []),
+        text: kind === 0 ? unitsToString(r.text.subarray(textOff, textOff + len)) : null };
+      if (seq <= minSeq && !removed) {
+        if (prev === null) prev = sg;
+        else if (canAppend(prev, sg) && same(prev.props, sg.props)) prev = { kind: 0, props: prev.props, text: prev.text + sg.text };
+        else { out.push({ json: json(prev) }); prev = sg; }
+        continue;
+      }
+      if (prev !== null) { out.push({ json: json(prev) }); prev = null; }
+      const raw = { json: json(sg) };
+      if (seq > minSeq) { raw.seq = seq; raw.client = this.getLongClientId(client); }
+      if (removed) {
+        const ids = [];
+        for (let c = 0; c < 32; c++) if ((removers >>> c) & 1) ids.push(this.getLongClientId(c));
+        raw.removedSeq = rseq;
+        raw.removedClient = ids[0];
+        raw.removedClientIds = ids;
+      }
+      out.push(raw);
+    }
+    if (prev !== null) out.push({ json: json(prev) });
+    return { segments: out, minSeq, currentSeq: v.curSeq };
   }
 }
 

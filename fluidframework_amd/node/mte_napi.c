@@ -309,6 +309,41 @@ static napi_value u32_array(napi_env env, const uint32_t* src, size_t n) {
 }
 
 /* readDoc(ctx, doc, nKeys) -> {status, curSeq, minSeq, length, text, segLen, segKind, segProps} */
+/* readSegments(ctx, doc, nKeys) -> {segs Uint8Array(32*n) (mte_seg, text_off into text),
+   props Uint32Array(n*nKeys), text Uint16Array} (mte_read_segments) */
+static napi_value js_read_segments(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  if (!get_args(env, info, 3, argv)) return NULL;
+  mte_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  uint32_t doc = 0, nk = 0;
+  NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+  NAPI_CALL(env, napi_get_value_uint32(env, argv[2], &nk));
+  mte_seg_list v;
+  memset(&v, 0, sizeof v);
+  if (throw_rc(env, mte_read_segments(ctx, doc, &v), ctx, "mte_read_segments")) return NULL;  // sizes
+  napi_value o = NULL, ab_s, ab_p, ab_t, ts, tp, tt;
+  void *ps, *pp, *pt;
+  const size_t ns = (size_t)v.n_segs, nt = (size_t)v.n_text, npv = ns * nk;
+  NAPI_CALL(env, napi_create_arraybuffer(env, ns * sizeof(mte_seg), &ps, &ab_s));
+  NAPI_CALL(env, napi_create_arraybuffer(env, npv * 4, &pp, &ab_p));
+  NAPI_CALL(env, napi_create_arraybuffer(env, nt * 2, &pt, &ab_t));
+  v.segs = (mte_seg*)ps;
+  v.props = nk ? (uint32_t*)pp : NULL;
+  v.seg_cap = ns;
+  v.text = (uint16_t*)pt;
+  v.text_cap = nt;
+  if (throw_rc(env, mte_read_segments(ctx, doc, &v), ctx, "mte_read_segments")) return NULL;
+  NAPI_CALL(env, napi_create_typedarray(env, napi_uint8_array, ns * sizeof(mte_seg), ab_s, 0, &ts));
+  NAPI_CALL(env, napi_create_typedarray(env, napi_uint32_array, npv, ab_p, 0, &tp));
+  NAPI_CALL(env, napi_create_typedarray(env, napi_uint16_array, nt, ab_t, 0, &tt));
+  NAPI_CALL(env, napi_create_object(env, &o));
+  napi_set_named_property(env, o, "segs", ts);
+  napi_set_named_property(env, o, "props", tp);
+  napi_set_named_property(env, o, "text", tt);
+  return o;
+}
+
 static napi_value js_read_doc(napi_env env, napi_callback_info info) {
   napi_value argv[3];
   if (!get_args(env, info, 3, argv)) return NULL;
@@ -394,6 +429,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"digest", NULL, js_digest, NULL, NULL, NULL, napi_enumerable, NULL},
       {"docStatus", NULL, js_doc_status, NULL, NULL, NULL, napi_enumerable, NULL},
       {"readDoc", NULL, js_read_doc, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"readSegments", NULL, js_read_segments, NULL, NULL, NULL, napi_enumerable, NULL},
       {"stats", NULL, js_stats, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   if (napi_define_properties(env, exports, sizeof d / sizeof d[0], d) != napi_ok) return NULL;
