@@ -620,10 +620,16 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
   HIPCHK(c, hipMalloc((void**)&c->d_init_props, sizeof(uint32_t) * iprops.size() + 4));
   HIPCHK(c, hipMalloc((void**)&c->d_digest, sizeof(uint64_t) * 4 * (n_docs ? n_docs : 1)));
   {
-    // pass-1 pairs: docs (2p, 2p+1); an odd last doc runs alone
-    c->n_pairs = (n_docs + 1) / 2;
+    // pass-1 pairs: docs (2p, 2p+1), an odd last doc alone.  A batch that fits
+    // the chip at one document per wave (<= CUs x 4 SIMDs x MTE_PAIR_WAVES,
+    // e.g. config 2's 1k docs) runs one per wave instead: pairing it would
+    // leave SIMDs idle and serialise two documents per wave.
+    int n_cu = 0;
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) n_cu = 0;
+    const bool solo = n_cu > 0 && (uint64_t)n_docs <= (uint64_t)n_cu * 4 * MTE_PAIR_WAVES;
+    c->n_pairs = solo ? n_docs : (n_docs + 1) / 2;
     std::vector<uint32_t> pairs((size_t)c->n_pairs * 2 + 2, 0xffffffffu);
-    for (uint32_t d = 0; d < n_docs; d++) pairs[d] = d;
+    for (uint32_t d = 0; d < n_docs; d++) pairs[solo ? 2 * (size_t)d : d] = d;
     HIPCHK(c, hipMalloc((void**)&c->d_pairs, pairs.size() * 4));
     HIPCHK(c, hipMemcpy(c->d_pairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice));
   }

@@ -220,3 +220,13 @@ def test_gpu_submit_rejects_bad_record():
     o.load_docs(s["inits"], s["init_text"])
     o.apply_batch(s["batch"])
     np.testing.assert_array_equal(d.digest(), o.digest())
+
+
+@pytest.mark.gpu
+def test_gpu_paired_pass1_matches_oracle():
+    # > CUs x 4 x 5 docs: pass 1 runs two documents per wave (alternating
+    # bursts); smaller batches run one per wave
+    s = gen.generate(3, n_docs=6000, ops_per_doc=300)
+    o, d = replay_both(s, threads=16)
+    assert (o.statuses() == 0).all()
+    assert_same(o, d, sample_docs=24)
