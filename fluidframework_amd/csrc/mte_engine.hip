@@ -262,6 +262,7 @@ struct mte_ctx {
   // pair (s_memrealtime, 100 MHz) at every mte_sync
   unsigned long long* d_wclock = nullptr;
   unsigned long long* d_gdone = nullptr;  // pass-1 global progress (fair priority)
+  double last_ms = 0, last_ops = 0;       // previous run (pass-1 schedule estimate, MTE_FAIR_PRIO 4)
   const char* wclock_path = nullptr;
 
   // chunked big-document pass (seg_capacity >= kChunkMinCap, mte_chunk.h)
@@ -788,6 +789,9 @@ int mte_run(mte_ctx* c) {
   a.wclock = nullptr;
   a.gdone = c->d_gdone;
   a.n_ops = c->n_ops;
+  // s_memrealtime runs at 100 MHz: ticks = ms x 1e5, scaled to this batch's ops
+  a.eta = (c->last_ms > 0 && c->last_ops > 0) ? (unsigned long long)(c->last_ms * 1e5 * (double)c->n_ops / c->last_ops)
+                                              : 0ull;
   if (c->wclock_path) {
     if (!c->d_wclock) HIPCHK(c, hipMalloc((void**)&c->d_wclock, 16ull * (c->n_pairs + 1)));
     a.wclock = c->d_wclock;
@@ -813,6 +817,13 @@ int mte_sync(mte_ctx* c) {
   if (!c) return MTE_E_INVALID_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->ran) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess && ms > 0.f) {
+      c->last_ms = ms;
+      c->last_ops = (double)c->n_ops;
+    }
+  }
   if (c->wclock_path && c->d_wclock) {
     std::vector<unsigned long long> w(2ull * c->n_pairs);
     HIPCHK(c, hipMemcpy(w.data(), c->d_wclock, w.size() * 8, hipMemcpyDeviceToHost));

@@ -94,6 +94,7 @@ struct ReplayArgs {
   unsigned long long* wclock;  // diagnostics (MTE_WAVE_CLOCK): pass-1 start / end time per pair, or null
   unsigned long long* gdone;   // pass 1: ops applied so far by all waves (fair priority), zeroed per run
   unsigned long long n_ops;    // ops of the batch
+  unsigned long long eta;      // expected pass-1 duration in s_memrealtime ticks (0 = unknown)
 };
 
 // ---- wavefront primitives --------------------------------------------------

@@ -21,9 +21,10 @@
 #include "mte_kernels.h"
 
 // Build-time knobs (tools/variants.sh builds A/B variants; defaults are the product build).
-// MTE_FAIR_PRIO: 0 = hardware age order, 1 = 4 linear bands (product), 2 = geometric bands,
+// MTE_FAIR_PRIO: 0 = hardware age order, 1 = 4 linear bands of work left, 2 = geometric bands,
 // 3 = bands around the global progress (one returning atomic per burst; measured 33.9 ms vs
-// 23.9 ms on config 3: the single contended counter costs more than the balance gains).
+// 23.9 ms on config 3: the single contended counter costs more than the balance gains),
+// 4 = bands around the previous run's schedule (product: 22.6 ms; band 1 on the first run).
 #ifndef MTE_PAIR_WAVES
 #define MTE_PAIR_WAVES 5
 #endif
@@ -33,8 +34,8 @@
 #ifndef MTE_PASS1_EMAX
 #define MTE_PASS1_EMAX 4
 #endif
-#ifndef MTE_FAIR_PRIO  // 1: pass-1 waves raise their issue priority with the work they have left
-#define MTE_FAIR_PRIO 1
+#ifndef MTE_FAIR_PRIO  // pass-1 issue priority policy (below)
+#define MTE_FAIR_PRIO 4
 #endif
 #ifndef MTE_OUTLINE  // 1: pass-1 tiers as out-of-line functions (measured: same time, 1.7x the HBM traffic)
 #define MTE_OUTLINE 0
@@ -830,8 +831,8 @@ __device__ __forceinline__ void fair_prio(uint32_t left, uint32_t total) {
     else if (q == 2) __builtin_amdgcn_s_setprio(2);
     else if (q == 1) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
-  } else if constexpr (MTE_FAIR_PRIO == 3) {
-    // (pair_kernel computes the level itself, against the global progress)
+  } else if constexpr (MTE_FAIR_PRIO >= 3) {
+    // (pair_kernel computes the level itself)
   } else if constexpr (MTE_FAIR_PRIO == 2) {
     // geometric bands (> 1/4, > 3/32, > 1/32 of the work left): the last band,
     // where the waves fall back to age order, is short
@@ -876,7 +877,9 @@ __global__ __launch_bounds__(WPB * kWave, MTE_PAIR_WAVES * 4 / WPB) void pair_ke
     if (docs[t] >= 0) total += (uint32_t)(a.op_off[docs[t] + 1] - a.op_off[docs[t]]) - hl[t].resume;
   total = uni(total);
   uint32_t left = total;
-  fair_prio(left, total);
+  [[maybe_unused]] const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  if constexpr (MTE_FAIR_PRIO == 4) __builtin_amdgcn_s_setprio(2);
+  else fair_prio(left, total);
   // one burst per iteration, alternating between the two documents; a single
   // copy of the burst code serves both (the document is a runtime index)
   for (int t = 0; live; t ^= 1) {
@@ -902,6 +905,21 @@ __global__ __launch_bounds__(WPB * kWave, MTE_PAIR_WAVES * 4 / WPB) void pair_ke
       else if (mine < all) __builtin_amdgcn_s_setprio(2);
       else if (mine < all + band) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
+    } else if constexpr (MTE_FAIR_PRIO == 4) {
+      // against the schedule of the previous run (a.eta ticks for the whole
+      // pass): behind it -> higher priority; without an estimate, by work left
+      if (a.eta) {
+        const unsigned long long el = __builtin_amdgcn_s_memrealtime() - t_start;
+        const unsigned long long mine = (unsigned long long)(total - left) * a.eta;  // done/total vs el/eta
+        const unsigned long long sched = el * total;
+        const unsigned long long band = (unsigned long long)total * a.eta / 32;
+        if (mine + band < sched) __builtin_amdgcn_s_setprio(3);
+        else if (mine < sched) __builtin_amdgcn_s_setprio(2);
+        else if (mine < sched + band) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      } else {
+        fair_prio(left, total);
+      }
     } else {
       fair_prio(left, total);
     }
