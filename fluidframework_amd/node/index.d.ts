@@ -60,6 +60,27 @@ export interface ClientOptions {
   currentSeq?: number;
   /** Load a summary body instead of initialText (SnapshotLoader.loadBody). */
   segments?: SegmentWithMergeInfo[];
+  /** Load a legacy summary (SnapshotLegacy blobs) and queue its catch-up ops. */
+  legacy?: LegacySummary;
+}
+
+/** MergeTreeChunkLegacy (snapshotChunks.ts:22-34) as SnapshotLegacy.emit writes it. */
+export interface LegacyChunk {
+  chunkStartSegmentIndex: number;
+  chunkSegmentCount: number;
+  chunkLengthChars: number;
+  totalLengthChars: number;
+  totalSegmentCount: number;
+  chunkSequenceNumber: number;
+  segmentTexts: any[];
+  headerMetadata?: { orderedChunkMetadata: { id: string }[]; sequenceNumber: number;
+    minSequenceNumber?: number; totalLength: number; totalSegmentCount: number };
+}
+
+export interface LegacySummary {
+  header: LegacyChunk;
+  body?: LegacyChunk;
+  catchupOps?: ISequencedDocumentMessage[];
 }
 
 export class MergeTreeError extends Error {
@@ -123,4 +144,6 @@ export class BatchClient {
   getSegments(): VisibleSegment[];
   /** Summary body (SnapshotV1.extractSegment rules) + the collab window to load it with. */
   summarize(): { segments: SegmentWithMergeInfo[]; minSeq: number; currentSeq: number };
+  /** SnapshotLegacy.extractSync + emit (snapshotlegacy.ts:105-211). */
+  summarizeLegacy(catchUpMsgs?: ISequencedDocumentMessage[], chunkSize?: number): LegacySummary;
 }

@@ -83,15 +83,28 @@ class MergeTreeEngine {
    *  segment of LocalClientId, as the replay harness loads it
    *  (client.replay.spec.ts:22-23); options.segments instead loads a summary
    *  body — IJSONSegmentWithMergeInfo specs with seq / client / removedSeq /
-   *  removedClientIds — as SnapshotLoader.loadBody does (snapshotLoader.ts:85-125). */
+   *  removedClientIds — as SnapshotLoader.loadBody does (snapshotLoader.ts:85-125);
+   *  options.legacy loads a legacy summary (BatchClient.summarizeLegacy) and
+   *  queues its catch-up ops. */
   createClient(initialText, options) {
     if (this.started) throw new MergeTreeError(-10, "createClient after the engine started");
-    const o = options || {};
+    let o = options || {};
+    if (o.legacy) o = Object.assign({}, o, loadLegacy(o.legacy));
     const doc = this.docs.length;
     this.docs.push({ text: initialText || "", newLengthCalc: !!o.newLengthCalc, props: o.props,
       minSeq: o.minSeq || 0, currentSeq: o.currentSeq || 0, segments: o.segments });
     const c = new BatchClient(this, doc, o.observerId === undefined ? "A" : o.observerId);
     this.clients.push(c);
+    if (o.legacy && o.legacy.catchupOps) {
+      // SharedSegmentSequence.loadCore (sequence.ts:588-609): catch-up ops above the window
+      for (const m of o.legacy.catchupOps) {
+        if (m.minimumSequenceNumber < o.minSeq || m.referenceSequenceNumber < o.minSeq ||
+            m.sequenceNumber <= o.minSeq || m.sequenceNumber <= o.currentSeq) {
+          throw new MergeTreeError(-1, "Invalid catchup operations in snapshot: seq " + m.sequenceNumber);
+        }
+      }
+      this.docs[doc].catchup = o.legacy.catchupOps; // queued at start(), after the load
+    }
     return c;
   }
 
@@ -116,6 +129,7 @@ class MergeTreeEngine {
     this.started = true;
     this.pending = new BatchBuilder(this.docs.length, this.interner);
     this.views = new Array(this.docs.length).fill(null);
+    this.docs.forEach((d, i) => { if (d.catchup) for (const m of d.catchup) this.clients[i].applyMsg(m); });
   }
 
   _batch() {
@@ -290,52 +304,146 @@ class BatchClient {
    * currentSeq}).  Returns {segments, minSeq, currentSeq}.
    */
   summarize() {
-    const eng = this.engine;
-    const v = eng._view(this.doc);
+    const v = this.engine._view(this.doc);
     const minSeq = v.minSeq;
-    const nk = eng.nKeys;
-    const r = eng.addon.readSegments(eng.ctx, this.doc, nk);
-    const dv = new DataView(r.segs.buffer, r.segs.byteOffset, r.segs.byteLength);
-    const n = r.segs.byteLength / 32;
     const out = [];
     let prev = null;
-    const json = (sg) => {
-      if (sg.kind === 0) return sg.props ? { text: sg.text, props: sg.props } : sg.text;
-      return sg.props ? { marker: { refType: sg.kind - 1 }, props: sg.props } : { marker: { refType: sg.kind - 1 } };
-    };
-    const same = (a, b) => packing.canonicalJson(a || {}) === packing.canonicalJson(b || {});
-    const canAppend = (a, b) => a.kind === 0 && b.kind === 0 && !a.text.endsWith("\n") &&
-      (a.text.length <= 256 || b.text.length <= 256);
-    for (let i = 0; i < n; i++) {
-      const o = i * 32;
-      const textOff = dv.getUint32(o, true), len = dv.getUint32(o + 4, true), seq = dv.getInt32(o + 8, true);
-      const rseq = dv.getInt32(o + 12, true), removers = dv.getUint32(o + 16, true);
-      const client = dv.getInt32(o + 20, true), kind = dv.getUint32(o + 24, true);
-      const removed = rseq !== 0x7fffffff;
-      if (removed && rseq <= minSeq) continue;
-      const sg = { kind, props: eng.interner.decode(nk ? r.props.subarray(i * nk, (i + 1) * nk) : []),
-        text: kind === 0 ? unitsToString(r.text.subarray(textOff, textOff + len)) : null };
-      if (seq <= minSeq && !removed) {
+    for (const sg of this._heldSegments()) {
+      const removed = sg.rseq !== 0x7fffffff;
+      if (removed && sg.rseq <= minSeq) continue;
+      if (sg.seq <= minSeq && !removed) {
         if (prev === null) prev = sg;
-        else if (canAppend(prev, sg) && same(prev.props, sg.props)) prev = { kind: 0, props: prev.props, text: prev.text + sg.text };
-        else { out.push({ json: json(prev) }); prev = sg; }
+        else if (canAppend(prev, sg) && sameProps(prev.props, sg.props)) prev = { kind: 0, props: prev.props, text: prev.text + sg.text };
+        else { out.push({ json: segJson(prev) }); prev = sg; }
         continue;
       }
-      if (prev !== null) { out.push({ json: json(prev) }); prev = null; }
-      const raw = { json: json(sg) };
-      if (seq > minSeq) { raw.seq = seq; raw.client = this.getLongClientId(client); }
+      if (prev !== null) { out.push({ json: segJson(prev) }); prev = null; }
+      const raw = { json: segJson(sg) };
+      if (sg.seq > minSeq) { raw.seq = sg.seq; raw.client = this.getLongClientId(sg.client); }
       if (removed) {
         const ids = [];
-        for (let c = 0; c < 32; c++) if ((removers >>> c) & 1) ids.push(this.getLongClientId(c));
-        raw.removedSeq = rseq;
+        for (let c = 0; c < 32; c++) if ((sg.removers >>> c) & 1) ids.push(this.getLongClientId(c));
+        raw.removedSeq = sg.rseq;
         raw.removedClient = ids[0];
         raw.removedClientIds = ids;
       }
       out.push(raw);
     }
-    if (prev !== null) out.push({ json: json(prev) });
+    if (prev !== null) out.push({ json: segJson(prev) });
     return { segments: out, minSeq, currentSeq: v.curSeq };
+  }
+
+  /**
+   * Legacy summary (the default when newMergeTreeSnapshotFormat !== true):
+   * SnapshotLegacy.extractSync + emit (snapshotlegacy.ts:105-211).  The
+   * document as it reads at minSeq for NonCollabClient — segments inserted at
+   * or below minSeq and not removed at or below it, coalesced, no merge info —
+   * split into a "header" chunk of ~chunkSize units (with headerMetadata,
+   * snapshotChunks.ts:168-186) and a "body" chunk, plus "catchupOps": the
+   * given messages above minSeq with their minimumSequenceNumber set to minSeq
+   * (SharedSegmentSequence.summarizeMergeTree, sequence.ts:676-686).  Load it
+   * with createClient("", {legacy: blobs}).
+   */
+  summarizeLegacy(catchUpMsgs, chunkSize) {
+    const size = chunkSize === undefined ? SIZE_OF_FIRST_CHUNK : chunkSize;
+    const minSeq = this.engine._view(this.doc).minSeq;
+    const specs = [];
+    let prev = null;
+    for (const sg of this._heldSegments()) {
+      if (sg.seq > minSeq || sg.rseq <= minSeq) continue;
+      if (prev !== null && canAppend(prev, sg) && sameProps(prev.props, sg.props)) {
+        prev = { kind: 0, props: prev.props, text: prev.text + sg.text };
+      } else {
+        if (prev !== null) specs.push(segJson(prev));
+        prev = sg;
+      }
+    }
+    if (prev !== null) specs.push(segJson(prev));
+    const total = specs.reduce((a, sp) => a + specLength(sp), 0);
+    const header = legacyChunk(specs, size, 0, total, minSeq);
+    const ids = [{ id: "header" }];
+    if (header.chunkLengthChars < total) ids.push({ id: "body" });
+    header.headerMetadata = { orderedChunkMetadata: ids, sequenceNumber: minSeq, totalLength: total,
+      totalSegmentCount: specs.length };
+    const blobs = { header };
+    if (header.chunkSegmentCount < specs.length) {
+      blobs.body = legacyChunk(specs, total, header.chunkSegmentCount, total, minSeq);
+    }
+    const catchup = (catchUpMsgs || []).filter((m) => m.sequenceNumber > minSeq)
+      .map((m) => Object.assign({}, m, { minimumSequenceNumber: minSeq }));
+    if (catchup.length > 0) blobs.catchupOps = catchup;
+    return blobs;
+  }
+
+  /** Segments the engine holds for this document (mte_read_segments), decoded. */
+  _heldSegments() {
+    const eng = this.engine;
+    eng._view(this.doc);
+    const nk = eng.nKeys;
+    const r = eng.addon.readSegments(eng.ctx, this.doc, nk);
+    const dv = new DataView(r.segs.buffer, r.segs.byteOffset, r.segs.byteLength);
+    const n = r.segs.byteLength / 32;
+    const out = [];
+    for (let i = 0; i < n; i++) {
+      const o = i * 32;
+      const textOff = dv.getUint32(o, true), len = dv.getUint32(o + 4, true);
+      const kind = dv.getUint32(o + 24, true);
+      out.push({ kind, seq: dv.getInt32(o + 8, true), rseq: dv.getInt32(o + 12, true),
+        removers: dv.getUint32(o + 16, true), client: dv.getInt32(o + 20, true),
+        props: eng.interner.decode(nk ? r.props.subarray(i * nk, (i + 1) * nk) : []),
+        text: kind === 0 ? unitsToString(r.text.subarray(textOff, textOff + len)) : null });
+    }
+    return out;
   }
 }
 
-module.exports = { MergeTreeEngine, BatchClient, MergeTreeError, loadAddon, packing };
+const SIZE_OF_FIRST_CHUNK = 10000; // SnapshotLegacy.sizeOfFirstChunk, snapshotlegacy.ts:52
+
+function segJson(sg) {
+  if (sg.kind === 0) return sg.props ? { text: sg.text, props: sg.props } : sg.text;
+  return sg.props ? { marker: { refType: sg.kind - 1 }, props: sg.props } : { marker: { refType: sg.kind - 1 } };
+}
+
+function sameProps(a, b) { // matchProperties (properties.ts:33-42): empty == undefined
+  return packing.canonicalJson(a || {}) === packing.canonicalJson(b || {});
+}
+
+function canAppend(a, b) { // TextSegment.canAppend (textSegment.ts:72-77)
+  return a.kind === 0 && b.kind === 0 && !a.text.endsWith("\n") && (a.text.length <= 256 || b.text.length <= 256);
+}
+
+function specLength(sp) {
+  return typeof sp === "string" ? sp.length : ("marker" in sp ? 1 : sp.text.length);
+}
+
+function legacyChunk(specs, approxLength, start, totalLength, seq) { // getSeqLengthSegs, snapshotlegacy.ts:66-99
+  let n = 0, length = 0;
+  while (length < approxLength && start + n < specs.length) { length += specLength(specs[start + n]); n++; }
+  return { chunkStartSegmentIndex: start, chunkSegmentCount: n, chunkLengthChars: length,
+    totalLengthChars: totalLength, totalSegmentCount: specs.length, chunkSequenceNumber: seq,
+    segmentTexts: specs.slice(start, start + n) };
+}
+
+/** SnapshotLoader.loadHeader / loadBody (snapshotLoader.ts:130-246) over legacy
+ *  blobs -> {segments, minSeq, currentSeq}; throws the loader's asserts. */
+function loadLegacy(blobs) {
+  const h = blobs.header;
+  const md = h.headerMetadata;
+  if (h.chunkLengthChars > md.totalLength) throw new MergeTreeError(-1, "0x061: Mismatch in totalLength");
+  if (h.chunkSegmentCount > md.totalSegmentCount) throw new MergeTreeError(-1, "0x062: Mismatch in totalSegmentCount");
+  const specs = h.segmentTexts.slice();
+  if (h.chunkSegmentCount < md.totalSegmentCount) {
+    let length = h.chunkLengthChars;
+    for (const c of md.orderedChunkMetadata.slice(1)) {
+      length += blobs[c.id].chunkLengthChars;
+      specs.push(...blobs[c.id].segmentTexts);
+    }
+    if (length !== md.totalLength) throw new MergeTreeError(-1, "0x063: Mismatch in totalLength");
+    if (specs.length !== md.totalSegmentCount) throw new MergeTreeError(-1, "0x064: Mismatch in totalSegmentCount");
+  }
+  const seq = md.sequenceNumber;
+  return { segments: specs.map((json) => ({ json })),
+    minSeq: md.minSequenceNumber !== undefined ? md.minSequenceNumber : seq, currentSeq: seq };
+}
+
+module.exports = { MergeTreeEngine, BatchClient, MergeTreeError, loadAddon, loadLegacy, packing };

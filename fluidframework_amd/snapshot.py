@@ -124,3 +124,119 @@ def load_bodies(bodies, windows, flags, n_keys):
         offs.append(len(rows))
     return (inits, np.array(units, np.uint16), np.array(psets, PROPSET_DTYPE), np.array(pents, PROP_DTYPE),
             np.array(offs, np.uint64), np.array(rows, SEG_DTYPE) if rows else np.zeros(0, SEG_DTYPE))
+
+
+# --- legacy format (the default when newMergeTreeSnapshotFormat !== true) ---------------------
+
+SIZE_OF_FIRST_CHUNK = 10000  # SnapshotLegacy.sizeOfFirstChunk, snapshotlegacy.ts:52
+
+
+class SnapshotLoadError(ValueError):
+    """The loader's asserts (snapshotLoader.ts:170-211, 0x061-0x064) and the catch-up
+    window check (sequence.ts:592-606)."""
+
+
+def _seg_length(spec):
+    return len(spec) if isinstance(spec, list) else len(spec["text"]) if "text" in spec else 1
+
+
+def extract_legacy(engine, doc, min_seq):
+    """SnapshotLegacy.extractSync (snapshotlegacy.ts:153-211): the document as it reads at
+    minSeq for NonCollabClient — segments inserted at or below minSeq and not removed at or
+    below it, coalesced by canAppend + matchProperties, with no merge info.  Properties are
+    the segments' current ones (the reference keeps no per-seq property history either; the
+    catch-up ops re-apply every later annotate in order, so the loaded replay converges)."""
+    segs, props, text = engine.read_segments(doc)
+    out = []
+    prev = None
+    for i in range(len(segs)):
+        s = segs[i]
+        if int(s["seq"]) > min_seq or int(s["removed_seq"]) <= min_seq:
+            continue  # NOT_REMOVED is INT32_MAX, above every minSeq
+        cur = {"kind": int(s["kind"]), "props": tuple(int(x) for x in props[i]),
+               "text": text[int(s["text_off"]): int(s["text_off"]) + int(s["len"])].tolist()
+               if int(s["kind"]) == 0 else None}
+        if prev is not None and _can_append(prev, cur) and prev["props"] == cur["props"]:
+            prev = {"kind": 0, "props": prev["props"], "text": prev["text"] + cur["text"]}
+        else:
+            if prev is not None:
+                out.append(_json(prev))
+            prev = cur
+    if prev is not None:
+        out.append(_json(prev))
+    return out
+
+
+def _legacy_chunk(specs, approx_length, start, total_length, seq):
+    # SnapshotLegacy.getSeqLengthSegs (snapshotlegacy.ts:66-99)
+    n = 0
+    length = 0
+    while length < approx_length and start + n < len(specs):
+        length += _seg_length(specs[start + n])
+        n += 1
+    return {"chunkStartSegmentIndex": start, "chunkSegmentCount": n,
+            "chunkLengthChars": length, "totalLengthChars": total_length,
+            "totalSegmentCount": len(specs), "chunkSequenceNumber": seq,
+            "segmentTexts": specs[start:start + n]}
+
+
+def write_legacy(engine, doc, min_seq, catchup=None, chunk_size=SIZE_OF_FIRST_CHUNK):
+    """SnapshotLegacy.emit (snapshotlegacy.ts:105-151) -> {blob name: chunk}.  "header"
+    holds the first ~chunk_size units with headerMetadata (buildHeaderMetadataForLegacyChunk,
+    snapshotChunks.ts:168-186; minSequenceNumber is absent, so the loader takes
+    sequenceNumber = minSeq for both ends of the window), "body" the rest when any, and
+    "catchupOps" the caller's messages above minSeq when given."""
+    specs = extract_legacy(engine, doc, min_seq)
+    total = sum(_seg_length(s) for s in specs)
+    c1 = _legacy_chunk(specs, chunk_size, 0, total, min_seq)
+    ids = [{"id": "header"}] + ([{"id": "body"}] if c1["chunkLengthChars"] < total else [])
+    c1["headerMetadata"] = {"orderedChunkMetadata": ids, "sequenceNumber": min_seq,
+                            "totalLength": total, "totalSegmentCount": len(specs)}
+    blobs = {"header": c1}
+    if c1["chunkSegmentCount"] < len(specs):
+        blobs["body"] = _legacy_chunk(specs, total, c1["chunkSegmentCount"], total, min_seq)
+    assert sum(c["chunkLengthChars"] for c in blobs.values()) == total  # 0x05d
+    assert sum(c["chunkSegmentCount"] for c in blobs.values()) == len(specs)  # 0x05e
+    if catchup is not None and len(catchup) > 0:
+        blobs["catchupOps"] = catchup
+    return blobs
+
+
+def legacy_window(blobs):
+    """SnapshotLoader.loadHeader (snapshotLoader.ts:130-166): (minSeq, currentSeq)."""
+    md = blobs["header"]["headerMetadata"]
+    return (md.get("minSequenceNumber", md["sequenceNumber"]), md["sequenceNumber"])
+
+
+def legacy_body(blobs):
+    """Header + body chunks -> the body list load_bodies takes (plain specs: seq 0, no
+    client), after the loader's consistency asserts (snapshotLoader.ts:168-211)."""
+    h = blobs["header"]
+    md = h["headerMetadata"]
+    if h["chunkLengthChars"] > md["totalLength"]:
+        raise SnapshotLoadError("0x061: Mismatch in totalLength")
+    if h["chunkSegmentCount"] > md["totalSegmentCount"]:
+        raise SnapshotLoadError("0x062: Mismatch in totalSegmentCount")
+    specs = list(h["segmentTexts"])
+    if h["chunkSegmentCount"] < md["totalSegmentCount"]:
+        length = h["chunkLengthChars"]
+        for meta in md["orderedChunkMetadata"][1:]:
+            c = blobs[meta["id"]]
+            length += c["chunkLengthChars"]
+            specs.extend(c["segmentTexts"])
+        if length != md["totalLength"]:
+            raise SnapshotLoadError("0x063: Mismatch in totalLength")
+        if len(specs) != md["totalSegmentCount"]:
+            raise SnapshotLoadError("0x064: Mismatch in totalSegmentCount")
+    return [{"json": s} for s in specs]
+
+
+def check_catchup(ops, window):
+    """SharedSegmentSequence.loadCore's catch-up check (sequence.ts:590-607) over op
+    records: every catch-up message lies above the loaded window."""
+    min_seq, cur_seq = window
+    bad = (ops["min_seq"] < min_seq) | (ops["ref_seq"] < min_seq) | (ops["seq"] <= max(min_seq, cur_seq))
+    if bad.any():
+        o = ops[int(np.argmax(bad))]
+        raise SnapshotLoadError("Invalid catchup operations in snapshot: seq %d minSeq %d refSeq %d, "
+                                "window (%d, %d)" % (o["seq"], o["min_seq"], o["ref_seq"], min_seq, cur_seq))

@@ -99,3 +99,17 @@ def test_node_summary_round_trip_on_gpu():
     assert j["nFailures"] == 0, j["failures"]
     assert j["passed"] == 30 * 32 * 2
     assert j["segmentsWithMergeInfo"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", ["", "64"])
+def test_node_legacy_summary_round_trip_on_gpu(chunk):
+    # legacy summary (header / body chunks at minSeq + catch-up ops) after 32
+    # rounds, loaded into a second engine (options.legacy), replay the rest
+    args = ("tests/node/legacy_roundtrip_gpu.js",) + ((chunk,) if chunk else ())
+    j = json.loads(node(*args, timeout=600))
+    assert j["nFailures"] == 0, j["failures"]
+    assert j["passed"] == 30 * 32 * 2
+    assert j["catchup"] > 0
+    if chunk:
+        assert j["withBody"] > 0
