@@ -79,6 +79,45 @@ SCENARIOS = {
         "abcd", False,
         [msg("B", 1, 0, 0, rem(1, 3)), msg("B", 2, 1, 0, ins(1, "yz")),
          msg("C", 3, 0, 0, ins(2, "X"))], None),
+    # mergeTree.annotate.spec.ts:17-51 setup: "hello world!" (Universal seq,
+    # LocalClientId) + a remote Tile marker at 3; then a remote annotate of
+    # [1, 5).  :54-71 "not collaborating / remote"
+    "annotate remote (not collaborating)": (
+        "hello world!", False,
+        [msg("remote", 1, 0, 0, ins(3, {"marker": {"refType": 1}})),
+         msg("remote", 2, 1, 0, ann(1, 5, {"propertySource": "remote"}))], "hello world!"),
+    # :491-514 "remote first / remote only"
+    "annotate remote first, remote only": (
+        "hello world!", False,
+        [msg("remote", 1, 0, 0, ins(3, {"marker": {"refType": 1}})),
+         msg("remote", 2, 1, 0, ann(1, 5, {"propertySource": "remote", "remoteProperty": 1}))], None),
+    # :516-524 "split remote": both halves of a split keep the properties (the
+    # split comes from a later remote insert inside the annotated segment)
+    "annotate remote first, split remote": (
+        "hello world!", False,
+        [msg("remote", 1, 0, 0, ins(3, {"marker": {"refType": 1}})),
+         msg("remote", 2, 1, 0, ann(1, 5, {"propertySource": "remote", "remoteProperty": 1})),
+         msg("other", 3, 2, 0, ins(2, "X"))], None),
+    # partialLength.spec.ts:18-45 setup ("hello world!" at seq 0); the spec
+    # asserts the lengths (17 / 0 / 16 / 112 / 2), the texts follow from them
+    # :80-108 "includes length of remote insert"
+    "partial lengths: remote insert": (
+        "hello world!", False, [msg("remote", 1, 0, 0, ins(0, "more "))], "more hello world!"),
+    # :139-167 "includes result of remote delete"
+    "partial lengths: remote delete": ("hello world!", False, [msg("remote", 1, 0, 0, rem(0, 12))], ""),
+    # :170-210 "includes lengths from multiple permutations in single tree"
+    "partial lengths: aggregation": (
+        "hello world!", False,
+        [msg("local", 1, 0, 0, ins(0, "1")), msg("remote", 2, 1, 0, ins(0, "2")),
+         msg("local", 3, 2, 0, ins(0, "3")), msg("remote", 4, 3, 0, ins(0, "4"))], "4321hello world!"),
+    # :212-232 "is correct for different heights"
+    "partial lengths: different heights": (
+        "hello world!", False, [msg("local", i + 1, i, 0, ins(0, "a")) for i in range(100)],
+        "a" * 100 + "hello world!"),
+    # :235-257 "concurrent remote changes are visible to local"
+    "partial lengths: concurrent overlapping remote deletes": (
+        "hello world!", False,
+        [msg("remote", 1, 0, 0, rem(0, 10)), msg("remote2", 2, 0, 0, rem(0, 10))], "d!"),
     # edge cases -------------------------------------------------------------
     "insert into empty doc": ("", False, [msg("B", 1, 0, 0, ins(0, "xy"))], "xy"),
     "zero-length insert splits only": ("abc", False, [msg("B", 1, 0, 0, ins(1, ""))], "abc"),
@@ -135,6 +174,26 @@ SCENARIOS = {
         "abc", False, [msg("B", 1, 0, 1, ins(0, "X")), msg("C", 2, 1, 0, ins(0, "Y"))], "ERR:-6"),
     "msn above seq fails": ("abc", False, [msg("B", 1, 0, 2, ins(0, "X"))], "ERR:-7"),
 }
+
+
+# name -> [(position, properties getPropertiesAtPosition must return)]
+PROPS_AT = {
+    "annotate remote (not collaborating)": [(1, {"propertySource": "remote"})],   # annotate.spec.ts:68-70
+    "annotate remote first, remote only": [(1, {"propertySource": "remote", "remoteProperty": 1})],  # :508-514
+    "annotate remote first, split remote": [                                       # :516-524
+        (1, {"propertySource": "remote", "remoteProperty": 1}), (2, {}),
+        (3, {"propertySource": "remote", "remoteProperty": 1})],
+}
+
+
+def props_at(rd, interner, pos):
+    """Client.getPropertiesAtPosition (client.ts:1133-1141) over a read_doc view."""
+    p = 0
+    for ln, _, planes in rd["segs"]:
+        if p <= pos < p + ln:
+            return interner.decode_props(planes)
+        p += ln
+    return None
 
 
 def run_scenario(engine, name, n_keys=8):

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 from fixtures_util import replay_fixtures
-from scenarios import SCENARIOS, expected_of, run_scenario
+from scenarios import PROPS_AT, SCENARIOS, expected_of, props_at, run_scenario
 
 from fluidframework_amd import gen
 from fluidframework_amd.abi import MTE_E_CAPACITY
@@ -50,8 +50,10 @@ def test_gpu_replays_reference_fixtures():
 @pytest.mark.parametrize("name", sorted(SCENARIOS))
 def test_gpu_scenarios(name):
     st_o, text_o, rd_o, _ = run_scenario(OracleEngine(8), name)
-    st_d, text_d, rd_d, _ = run_scenario(DeviceEngine(8), name)
+    st_d, text_d, rd_d, interner = run_scenario(DeviceEngine(8), name)
     assert st_d == st_o
+    for pos, want in PROPS_AT.get(name, []):
+        assert props_at(rd_d, interner, pos) == want, pos
     assert rd_d == rd_o
     exp = expected_of(name)
     if exp is not None and not exp.startswith("ERR:"):

@@ -1,14 +1,16 @@
 """Known-answer and edge-case scenarios on the CPU restatement."""
 import pytest
 
-from scenarios import SCENARIOS, expected_of, run_scenario
+from scenarios import PROPS_AT, SCENARIOS, expected_of, props_at, run_scenario
 
 from oracle import OracleEngine
 
 
 @pytest.mark.parametrize("name", sorted(SCENARIOS))
 def test_scenario_oracle(oracle_lib, name):
-    st, text, rd, _ = run_scenario(OracleEngine(8), name)
+    st, text, rd, interner = run_scenario(OracleEngine(8), name)
+    for pos, want in PROPS_AT.get(name, []):
+        assert props_at(rd, interner, pos) == want, pos
     exp = expected_of(name)
     if exp is None:
         assert st == 0
