@@ -91,9 +91,38 @@ __device__ __forceinline__ void touch_records(const DocRun& D, uint32_t from, ui
 // the compiled propset record; longer sets are read here.  Applied to the slots with
 // sel[j] set (E slots per lane, K planes); no lambdas, so the register arrays
 // never need an address.
+#ifndef MTE_SET_PLANE_SWITCH
+#define MTE_SET_PLANE_SWITCH 1
+#endif
+
+template <int E>
+__device__ __forceinline__ void set_one_plane(uint32_t (&p)[E], const bool (&sel)[E], uint32_t val) {
+#pragma unroll
+  for (int jj = 0; jj < E; jj++) {
+    uint32_t x = sel[jj] ? val : p[jj];
+    asm volatile("" : "+v"(x));  // keeps each case's selects distinct, so no case merging into p[key]
+    p[jj] = x;
+  }
+}
+
 template <int E, int K>
 __device__ __forceinline__ void set_plane(uint32_t (&pr)[K > 0 ? K : 1][E], const bool (&sel)[E], uint32_t key,
                                           uint32_t val) {
+#if MTE_SET_PLANE_SWITCH
+  // `key` is wave-uniform: one scalar branch picks the plane, so only that
+  // plane's E selects issue (the branch-free form costs K x E selects)
+  switch (key) {
+    case 0: if constexpr (K > 0) set_one_plane<E>(pr[K > 0 ? 0 : 0], sel, val); break;
+    case 1: if constexpr (K > 1) set_one_plane<E>(pr[K > 1 ? 1 : 0], sel, val); break;
+    case 2: if constexpr (K > 2) set_one_plane<E>(pr[K > 2 ? 2 : 0], sel, val); break;
+    case 3: if constexpr (K > 3) set_one_plane<E>(pr[K > 3 ? 3 : 0], sel, val); break;
+    case 4: if constexpr (K > 4) set_one_plane<E>(pr[K > 4 ? 4 : 0], sel, val); break;
+    case 5: if constexpr (K > 5) set_one_plane<E>(pr[K > 5 ? 5 : 0], sel, val); break;
+    case 6: if constexpr (K > 6) set_one_plane<E>(pr[K > 6 ? 6 : 0], sel, val); break;
+    case 7: if constexpr (K > 7) set_one_plane<E>(pr[K > 7 ? 7 : 0], sel, val); break;
+    default: break;
+  }
+#else
   // branch-free over planes: a `kk == key` branch gets folded into pr[key],
   // a dynamic index that would push the whole register file to scratch
 #pragma unroll
@@ -102,6 +131,7 @@ __device__ __forceinline__ void set_plane(uint32_t (&pr)[K > 0 ? K : 1][E], cons
 #pragma unroll
     for (int jj = 0; jj < E; jj++) pr[kk][jj] = (hit && sel[jj]) ? val : pr[kk][jj];
   }
+#endif
 }
 
 template <int E, int K>
