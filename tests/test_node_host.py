@@ -113,3 +113,27 @@ def test_node_legacy_summary_round_trip_on_gpu(chunk):
     assert j["catchup"] > 0
     if chunk:
         assert j["withBody"] > 0
+
+
+def test_node_legacy_loader_checks():
+    # loadLegacy (snapshotLoader.ts:130-246 asserts) is host-only: no GPU needed
+    script = r"""
+const { loadLegacy } = require("./fluidframework_amd/node");
+const chunk = (specs, start, n, len, total, count) => ({ chunkStartSegmentIndex: start, chunkSegmentCount: n,
+  chunkLengthChars: len, totalLengthChars: total, totalSegmentCount: count, chunkSequenceNumber: 7,
+  segmentTexts: specs });
+const header = chunk(["ab", { marker: { refType: 1 } }], 0, 2, 3, 6, 3);
+header.headerMetadata = { orderedChunkMetadata: [{ id: "header" }, { id: "body" }], sequenceNumber: 7,
+  totalLength: 6, totalSegmentCount: 3 };
+const ok = loadLegacy({ header, body: chunk([{ text: "cde", props: { k: 1 } }], 2, 1, 3, 6, 3) });
+const errs = [];
+try { loadLegacy({ header, body: chunk(["cd"], 2, 1, 2, 6, 3) }); } catch (e) { errs.push(e.message); }
+header.chunkSegmentCount = 4;
+try { loadLegacy({ header }); } catch (e) { errs.push(e.message); }
+process.stdout.write(JSON.stringify({ ok, errs }));
+"""
+    j = json.loads(node("-e", script))
+    assert (j["ok"]["minSeq"], j["ok"]["currentSeq"]) == (7, 7)
+    assert [s["json"] for s in j["ok"]["segments"]] == ["ab", {"marker": {"refType": 1}},
+                                                        {"text": "cde", "props": {"k": 1}}]
+    assert "0x063" in j["errs"][0] and "0x062" in j["errs"][1]
