@@ -192,7 +192,7 @@ class BatchClient {
     this.engine = engine;
     this.doc = doc;
     this.longClientId = observerId;
-    this.clients = new DocClients(observerId);
+    this.clients = new DocClients(observerId, engine.docs[doc].minSeq);
     this.lastMinSeq = 0;
     const self = this;
     // MergeTree-level entry points (clientId = short id, as in the reference)

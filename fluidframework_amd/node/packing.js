@@ -108,18 +108,48 @@ class Interner {
 }
 
 /** Per-document long -> short client id map (client.ts:683-698). */
+/** Per-document long -> short client id map (client.ts:683-698) over the
+ *  engine's MAX_CLIENTS slots.  A slot is recycled for a new client once the
+ *  window's minSeq has passed every seq its client used: its segments are then
+ *  visible to every perspective and its tombstones compacted
+ *  (mergeTree.ts:1003-1054, 1077-1093), so the slot number decides no
+ *  visibility rule any more (same rule as fluidframework_amd/packing.py). */
+const NEVER = 0x7fffffff;
 class DocClients {
-  constructor(observerId) {
+  constructor(observerId, minSeq) {
     this.observer = observerId;
     this.ids = new Map([[observerId, 0]]);
+    this.last = new Map([[0, NEVER]]); // slot -> highest seq its client used
+    this.minSeq = minSeq || 0;          // the window's minSeq before the next message
   }
-  short(longId) {
+  short(longId, seq) {
     let i = this.ids.get(longId);
     if (i === undefined) {
-      i = this.ids.size;
+      i = this._freeSlot();
+      if (i >= MAX_CLIENTS) return i; // the caller throws E_CLIENT_RANGE
       this.ids.set(longId, i);
+      this.last.set(i, seq === undefined ? NEVER : seq);
+    } else if (seq !== undefined && this.last.get(i) !== NEVER) {
+      this.last.set(i, Math.max(this.last.get(i), seq));
     }
     return i;
+  }
+  _freeSlot() {
+    const used = new Set(this.ids.values());
+    for (let s = 1; s < MAX_CLIENTS; s++) if (!used.has(s)) return s;
+    let best = -1, bestSeq = NEVER;
+    for (const v of used) {
+      if (v !== 0 && (best < 0 || this.last.get(v) < bestSeq || (this.last.get(v) === bestSeq && v < best))) {
+        best = v;
+        bestSeq = this.last.get(v);
+      }
+    }
+    if (best < 0 || bestSeq > this.minSeq) return MAX_CLIENTS;
+    for (const [k, v] of this.ids) if (v === best) { this.ids.delete(k); break; }
+    return best;
+  }
+  advance(msn) {
+    if (msn > this.minSeq) this.minSeq = msn;
   }
 }
 
@@ -174,12 +204,15 @@ class BatchBuilder {
   /** Client.applyMsg(msg, local=false) for one document (client.ts:918-935). */
   addMessage(doc, clients, msg) {
     const sender = msg.clientId;
-    const short = clients.short(sender);
-    if (short >= MAX_CLIENTS) throw new MergeTreeError(E_CLIENT_RANGE, "client " + String(sender));
     const seq = checkI32(msg.sequenceNumber, "sequenceNumber");
     const ref = checkI32(msg.referenceSequenceNumber === undefined ? 0 : msg.referenceSequenceNumber,
       "referenceSequenceNumber");
     const msn = checkI32(msg.minimumSequenceNumber, "minimumSequenceNumber");
+    const short = clients.short(sender, seq);
+    if (short >= MAX_CLIENTS) {
+      throw new MergeTreeError(E_CLIENT_RANGE, "client " + String(sender) + ": more than " + MAX_CLIENTS +
+        " clients inside the collab window");
+    }
     const recs = [];
     if ((msg.type === undefined ? "op" : msg.type) === "op") {
       if (sender === clients.observer) {
@@ -191,6 +224,7 @@ class BatchBuilder {
     recs[recs.length - 1][1] |= F_MSG_END;
     for (const r of recs) this.docOps[doc].push([seq, ref, msn, r[0], short, r[1], r[2], r[3], r[4], r[5]]);
     this.count += recs.length;
+    clients.advance(msn);
   }
 
   /** One MergeTree-level call (insertSegments / markRangeRemoved / annotateRange):

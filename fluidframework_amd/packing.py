@@ -112,18 +112,52 @@ class PropTable:
 
 
 class DocClients:
-    """Per-document long -> short client id map (client.ts:683-698)."""
+    """Per-document long -> short client id map (client.ts:683-698).
 
-    def __init__(self, observer_id: str):
+    The reference numbers clients forever; the engine's short ids are MTE_MAX_CLIENTS
+    slots (the removers bitmask is 32 bits).  A slot is recycled for a new client once the
+    collab window's minSeq has passed every seq its client used: from then on each of its
+    segments has seq <= minSeq <= refSeq (visible to every perspective whoever inserted
+    it, mergeTree.ts:1003-1054) and each segment it removed has removedSeq <= minSeq and
+    was compacted at that window advance (mergeTree.ts:1077-1093), so the slot number
+    decides no visibility rule any more.  Only clients active inside the window need
+    distinct slots."""
+
+    NEVER = I32_MAX  # slot held for good (observer, ids registered without a seq)
+
+    def __init__(self, observer_id: str, min_seq: int = 0):
         self.observer = observer_id
         self.ids = {observer_id: 0}
+        self.last = {0: self.NEVER}  # slot -> highest seq its client used
+        self.min_seq = min_seq       # the window's minSeq before the next message
 
-    def short(self, long_id) -> int:
+    def short(self, long_id, seq=None) -> int:
         i = self.ids.get(long_id)
         if i is None:
-            i = len(self.ids)
+            i = self._free_slot()
+            if i >= MTE_MAX_CLIENTS:
+                return i  # the caller raises MTE_E_CLIENT_RANGE
             self.ids[long_id] = i
+            self.last[i] = self.NEVER if seq is None else seq
+        elif seq is not None and self.last[i] != self.NEVER:
+            self.last[i] = max(self.last[i], seq)
         return i
+
+    def _free_slot(self) -> int:
+        used = set(self.ids.values())
+        for slot in range(1, MTE_MAX_CLIENTS):
+            if slot not in used:
+                return slot
+        seq, slot = min((self.last[v], v) for v in used if v != 0)
+        if seq > self.min_seq:
+            return MTE_MAX_CLIENTS
+        del self.ids[next(k for k, v in self.ids.items() if v == slot)]
+        return slot
+
+    def advance(self, msn: int):
+        """After a message: the window's minSeq becomes max(minSeq, msn) (client.ts:937-945)."""
+        if msn > self.min_seq:
+            self.min_seq = msn
 
 
 def _check_i32(v, what):
@@ -153,12 +187,13 @@ class BatchBuilder:
     def add_message(self, doc: int, clients: DocClients, msg: dict):
         """Client.applyMsg(msg, local=false) for one document (client.ts:918-935)."""
         sender = msg.get("clientId")
-        short = clients.short(sender)
-        if short >= MTE_MAX_CLIENTS:
-            raise MergeTreeError(MTE_E_CLIENT_RANGE, f"client {sender!r}")
         seq = _check_i32(msg["sequenceNumber"], "sequenceNumber")
         ref = _check_i32(msg.get("referenceSequenceNumber", 0), "referenceSequenceNumber")
         msn = _check_i32(msg["minimumSequenceNumber"], "minimumSequenceNumber")
+        short = clients.short(sender, seq)
+        if short >= MTE_MAX_CLIENTS:
+            raise MergeTreeError(MTE_E_CLIENT_RANGE, f"client {sender!r}: more than {MTE_MAX_CLIENTS} "
+                                 "clients inside the collab window")
         recs = []
         if msg.get("type", "op") == "op":
             if sender == clients.observer:
@@ -172,6 +207,7 @@ class BatchBuilder:
             if i == last:
                 flags |= F_MSG_END
             out.append((seq, ref, msn, t, short, flags, p1, p2, a, b))
+        clients.advance(msn)
 
     def _op_records(self, op, recs):
         if not isinstance(op, dict):

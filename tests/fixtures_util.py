@@ -47,8 +47,14 @@ def doc_inits(texts, flags=0):
     return inits, text
 
 
-def replay_fixtures(engine_factory, files=None, check=True, rounds=None):
+def replay_fixtures(engine_factory, files=None, check=True, rounds=None, fresh_clients=False):
     """Replay fixtures (all docs side by side, one batch per round).
+
+    fresh_clients: every round's senders get new long ids ("B" -> "B#r").  Every
+    op of a fixture round has refSeq == msn == the round's start, so a client's
+    identity only matters inside its round and the reference's texts are the
+    same; 8 x 64 = 512 distinct clients per document exercise the engine's
+    client-slot recycling (DocClients).
 
     Returns (checkpoints_passed, failures)."""
     fx = load_fixtures()
@@ -75,7 +81,10 @@ def replay_fixtures(engine_factory, files=None, check=True, rounds=None):
                     else:
                         passed += 1
                 for m in f["rounds"][r]["msgs"]:
-                    bb.add_message(d, clients[d], as_msg(m))
+                    msg = as_msg(m)
+                    if fresh_clients:
+                        msg["clientId"] = f"{msg['clientId']}#{r}"
+                    bb.add_message(d, clients[d], msg)
         eng.apply_batch(bb.build())
         st = eng.statuses()
         for d, f in enumerate(fx):

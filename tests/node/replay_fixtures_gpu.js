@@ -11,6 +11,9 @@ const eng = new MergeTreeEngine({ nKeys: 8 });
 // segments (SnapshotLoader.loadBody path, mte_load_segments) instead of one
 // segment; segmentation is unobservable, so every checkpoint must still hold
 const asBody = process.argv[2] === "body";
+// argv "fresh": every round's senders get new long ids ("B" -> "B#r"), 512 per
+// document through the 31 client slots (DocClients recycling)
+const fresh = process.argv[2] === "fresh";
 function body(t) {
   const segs = [];
   for (let i = 0; i < t.length; i += 3) segs.push({ json: t.slice(i, i + 3) });
@@ -27,7 +30,11 @@ for (let r = 0; r < nRounds; r++) {
     if (r >= f.rounds.length) return;
     const got = clients[d].getText();
     if (got === f.rounds[r].initialText) passed++; else failures.push([f.name, r, "initial"]);
-    for (const m of f.rounds[r].msgs) clients[d].applyMsg(asMsg(m));
+    for (const m of f.rounds[r].msgs) {
+      const msg = asMsg(m);
+      if (fresh) msg.clientId = msg.clientId + "#" + r;
+      clients[d].applyMsg(msg);
+    }
   });
   fx.forEach((f, d) => {
     if (r >= f.rounds.length) return;

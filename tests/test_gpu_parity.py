@@ -232,3 +232,12 @@ def test_gpu_paired_pass1_matches_oracle():
     o, d = replay_both(s, threads=16)
     assert (o.statuses() == 0).all()
     assert_same(o, d, sample_docs=24)
+
+
+def test_gpu_fixtures_with_fresh_clients_every_round():
+    # 512 distinct senders per document through 31 client slots (DocClients)
+    passed, failures, eng = replay_fixtures(lambda k: DeviceEngine(k), fresh_clients=True)
+    assert failures == []
+    assert passed == 30 * 64 * 2
+    _, _, oeng = replay_fixtures(lambda k: OracleEngine(k), check=False, fresh_clients=True)
+    np.testing.assert_array_equal(eng.digest(), oeng.digest())

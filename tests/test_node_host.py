@@ -51,8 +51,10 @@ def test_engine_without_device_throws_or_works():
     assert out.strip() in ("ok", "err -2")
 
 
-def test_js_packing_matches_python_packing_on_fixtures():
-    lines = node("tests/node/pack_fixtures.js").splitlines()
+@pytest.mark.parametrize("fresh", [False, True])
+def test_js_packing_matches_python_packing_on_fixtures(fresh):
+    # fresh: senders renamed per round, so both DocClients recycle slots alike
+    lines = node("tests/node/pack_fixtures.js", *(("fresh",) if fresh else ())).splitlines()
     fx = load_fixtures()
     interner = Interner(8)
     clients = [DocClients("A") for _ in fx]
@@ -63,7 +65,10 @@ def test_js_packing_matches_python_packing_on_fixtures():
         for d, f in enumerate(fx):
             if r < len(f["rounds"]):
                 for m in f["rounds"][r]["msgs"]:
-                    bb.add_message(d, clients[d], as_msg(m))
+                    msg = as_msg(m)
+                    if fresh:
+                        msg["clientId"] = f"{msg['clientId']}#{r}"
+                    bb.add_message(d, clients[d], msg)
         b = bb.build()
         for key, arr in (("offsets", b["op_offsets"]), ("ops", b["ops"]), ("text", b["text"]),
                          ("propsets", b["propsets"]), ("props", b["props"])):
@@ -137,3 +142,11 @@ process.stdout.write(JSON.stringify({ ok, errs }));
     assert [s["json"] for s in j["ok"]["segments"]] == ["ab", {"marker": {"refType": 1}},
                                                         {"text": "cde", "props": {"k": 1}}]
     assert "0x063" in j["errs"][0] and "0x062" in j["errs"][1]
+
+
+@pytest.mark.gpu
+def test_node_fixtures_with_fresh_clients_on_gpu():
+    # 512 distinct senders per document through the JS DocClients slots
+    j = json.loads(node("tests/node/replay_fixtures_gpu.js", "fresh", timeout=600))
+    assert j["nFailures"] == 0, j["failures"]
+    assert j["passed"] == 30 * 64 * 2

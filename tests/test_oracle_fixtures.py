@@ -28,3 +28,25 @@ def test_oracle_fixture_stats(oracle_lib):
     assert failures == []
     st = eng.stats()
     assert st["ops_applied"] == len(load_fixtures()[0]["rounds"][0]["msgs"])
+
+
+def test_oracle_replays_fixtures_with_fresh_clients_every_round(oracle_lib):
+    # 512 distinct senders per document through 31 client slots: the golden
+    # texts still hold (DocClients recycles a slot once minSeq passed its client)
+    passed, failures, eng = replay_fixtures(lambda k: OracleEngine(k), fresh_clients=True)
+    assert failures == []
+    assert passed == 30 * 64 * 2
+
+
+def test_client_slots_recycle_only_behind_the_window():
+    from fluidframework_amd.abi import MTE_MAX_CLIENTS
+    from fluidframework_amd.packing import DocClients
+    c = DocClients("A")
+    for i in range(1, MTE_MAX_CLIENTS):
+        assert c.short(f"c{i}", seq=i) == i
+    assert c.short("late", seq=40) == MTE_MAX_CLIENTS  # minSeq 0: every slot still in the window
+    c.advance(3)
+    assert c.short("late", seq=40) == 1                # c1 (last seq 1) is behind minSeq 3
+    assert "c1" not in c.ids and c.short("c2", seq=41) == 2
+    assert c.short("later", seq=42) == 3               # c3 (last seq 3 <= 3)
+    assert c.short("again", seq=43) == MTE_MAX_CLIENTS  # c4 .. c31 used seqs above minSeq
