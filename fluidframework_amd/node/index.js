@@ -225,8 +225,13 @@ class BatchClient {
     if (msg.minimumSequenceNumber > this.lastMinSeq) this.lastMinSeq = msg.minimumSequenceNumber;
   }
 
+  /** Client.getOrAddShortClientId (client.ts:683-698).  A short id handed out
+   *  here (no seq attached) keeps its slot for good; ids the engine assigns to
+   *  message senders are recycled behind the window (DocClients). */
   getOrAddShortClientId(longId) {
-    return this.clients.short(longId);
+    const i = this.clients.short(longId);
+    if (i >= packing.MAX_CLIENTS) throw new MergeTreeError(-12, "client " + String(longId) + ": no free client slot");
+    return i;
   }
 
   getClientId() {
