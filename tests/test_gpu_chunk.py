@@ -163,3 +163,35 @@ def test_gpu_segment_body_with_merge_info():
     assert res[0][0]["text"].startswith("helloworld")
     assert res[0][1] == res[1][1]
     np.testing.assert_array_equal(res[0][2], res[1][2])
+
+
+def test_gpu_config5_full_size_batching_invariance():
+    # BASELINE config 5 at full size (64 docs x 2^20 preloaded segments x
+    # 262,144 ops): too large for the flat oracle, so a size-independent
+    # property — the same ops in one batch or as 4 batches (one per round, the
+    # chunk pass re-entered each time) end in identical digests, all statuses
+    # clean — plus the oracle on a prefix of 8 docs x 512 ops
+    s = gen.generate(5)
+    cap = gen.seg_capacity(5, s["params"])
+    d = DeviceEngine(s["n_keys"], seg_capacity=cap)
+    gen.load_stream(d, s)
+    d.apply_batch(s["batch"])
+    assert (d.statuses() == 0).all()
+    one = d.digest()
+    d.reset()
+    d.sync()
+    b = s["batch"]
+    offs = b["op_offsets"].astype(np.int64)
+    per = int(offs[1] - offs[0]) // 4
+    assert (np.diff(offs) == 4 * per).all()
+    for k in range(4):
+        sub = dict(b)
+        sub["ops"] = np.concatenate([b["ops"][int(x) + k * per:int(x) + (k + 1) * per] for x in offs[:-1]])
+        sub["op_offsets"] = np.arange(len(offs), dtype=np.uint64) * per
+        d.apply_batch(sub)
+    assert (d.statuses() == 0).all()
+    np.testing.assert_array_equal(d.digest(), one)
+    d.close()
+    p = gen.prefix_ops(s, 8, 512)
+    o, dd = both(p, cap)
+    assert_same(o, dd)
