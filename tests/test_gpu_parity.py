@@ -241,3 +241,14 @@ def test_gpu_fixtures_with_fresh_clients_every_round():
     assert passed == 30 * 64 * 2
     _, _, oeng = replay_fixtures(lambda k: OracleEngine(k), check=False, fresh_clients=True)
     np.testing.assert_array_equal(eng.digest(), oeng.digest())
+
+
+@pytest.mark.parametrize("cfg", [3, 4])
+def test_gpu_matches_oracle_at_full_bench_size(cfg):
+    # BASELINE configs 3 (10k docs x 10k ops, the headline) and 4 (100k docs x
+    # 500 ops) at full size: every document's digest, status, op statistics and
+    # a sample of read-outs bit-exact against the restatement
+    s = gen.generate(cfg)
+    o, d = replay_both_cap(s, gen.seg_capacity(cfg, s["params"]), threads=16)
+    assert (o.statuses() == 0).all()
+    assert_same(o, d)
