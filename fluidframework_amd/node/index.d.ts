@@ -136,7 +136,8 @@ export class BatchClient {
   getClientId(): number;
   getLongClientId(shortId: number): string | undefined;
   flush(): void;
-  getText(): string;
+  /** TestClient.getText(start?, end?): markers count one position, contribute no text. */
+  getText(start?: number, end?: number): string;
   getLength(): number;
   getCurrentSeq(): number;
   getCollabWindow(): { clientId: number; currentSeq: number; minSeq: number; collaborating: boolean };

@@ -247,8 +247,26 @@ class BatchClient {
     this.engine.flush();
   }
 
-  getText() {
-    return this.engine._view(this.doc).text;
+  /** TestClient.getText(start?, end?) (test/testClient.ts:148) =
+   *  MergeTreeTextHelper.getText with placeholder "" (MergeTreeTextHelper.ts:20-74):
+   *  text units of the visible text segments overlapping [start, end); markers
+   *  occupy one position and contribute nothing. */
+  getText(start, end) {
+    const v = this.engine._view(this.doc);
+    if (start === undefined && end === undefined) return v.text;
+    const s0 = start === undefined ? 0 : start;
+    const e0 = end === undefined ? v.length : end;
+    let out = "";
+    let p = 0, t = 0;
+    for (let i = 0; i < v.segLen.length && p < e0; i++) {
+      const len = v.segLen[i];
+      if (v.segKind[i] === 0) {
+        if (p + len > s0) out += v.text.substring(t + Math.max(s0 - p, 0), t + Math.min(e0 - p, len));
+        t += len;
+      }
+      p += len;
+    }
+    return out;
   }
 
   getLength() {

@@ -39,8 +39,11 @@ for (let r = 0; r < nRounds; r++) {
   fx.forEach((f, d) => {
     if (r >= f.rounds.length) return;
     const got = clients[d].getText();
-    if (got === f.rounds[r].resultText && clients[d].getLength() === got.length) passed++;
-    else failures.push([f.name, r, "result"]);
+    const want = f.rounds[r].resultText;
+    const a = want.length >> 2, b = a + (want.length >> 1); // a ranged read-out (getText(start, end))
+    if (got === want && clients[d].getLength() === got.length && clients[d].getText(a, b) === want.slice(a, b)) {
+      passed++;
+    } else failures.push([f.name, r, "result"]);
   });
 }
 const dig = eng.digests();

@@ -150,3 +150,19 @@ def test_node_fixtures_with_fresh_clients_on_gpu():
     j = json.loads(node("tests/node/replay_fixtures_gpu.js", "fresh", timeout=600))
     assert j["nFailures"] == 0, j["failures"]
     assert j["passed"] == 30 * 64 * 2
+
+
+@pytest.mark.gpu
+def test_node_ranged_get_text_with_marker_on_gpu():
+    # getText(start, end) (testClient.ts:148, MergeTreeTextHelper.ts:20-74):
+    # a marker takes one position and contributes no text
+    script = r"""
+const { MergeTreeEngine } = require("./fluidframework_amd/node");
+const eng = new MergeTreeEngine({ nKeys: 8 });
+const c = eng.createClient("hello world");
+c.applyMsg({ clientId: "B", sequenceNumber: 1, referenceSequenceNumber: 0, minimumSequenceNumber: 0,
+  type: "op", contents: { type: 0, pos1: 3, seg: { marker: { refType: 1 }, props: { markerId: "m" } } } });
+process.stdout.write(JSON.stringify([c.getText(), c.getLength(), c.getText(2, 6), c.getText(3, 4), c.getText(4)]));
+eng.close();
+"""
+    assert json.loads(node("-e", script)) == ["hello world", 12, "llo", "", "lo world"]
