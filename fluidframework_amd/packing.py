@@ -120,8 +120,9 @@ class DocClients:
     segments has seq <= minSeq <= refSeq (visible to every perspective whoever inserted
     it, mergeTree.ts:1003-1054) and each segment it removed has removedSeq <= minSeq and
     was compacted at that window advance (mergeTree.ts:1077-1093), so the slot number
-    decides no visibility rule any more.  Only clients active inside the window need
-    distinct slots."""
+    decides no visibility rule any more (every later op has refSeq >= minSeq: the
+    sequencer's MSN is the minimum of the clients' refSeqs).  Only clients active
+    inside the window need distinct slots."""
 
     NEVER = I32_MAX  # slot held for good (observer, ids registered without a seq)
 
