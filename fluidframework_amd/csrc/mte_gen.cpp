@@ -94,6 +94,16 @@ inline bool visible(const Unit& u, int32_t r, int c) {
   return true;
 }
 
+// the unit's leaf has a defined perspective length (mergeTree.ts:1003-1054):
+// new calc -> every unit still held (tombstones at or below minSeq are gone
+// from the model); legacy -> not a tombstone the perspective saw removed, and
+// not a removed unit it never saw inserted
+inline bool defined(const Unit& u, int32_t r, int c, bool newcalc) {
+  if (newcalc || u.rseq == kNone) return true;
+  if (u.rseq <= r) return false;
+  return u.seq <= r || u.cli == c;
+}
+
 struct DocOut {
   std::vector<mte_op> ops;
   std::vector<uint16_t> text;
@@ -278,13 +288,14 @@ void gen_doc(const mteg_config& cfg, uint32_t d, DocOut& out) {
   if (mix.empty()) mix.push_back(MTE_OP_INSERT);
 
   out.ops.reserve(cfg.ops_per_doc);
-  const uint32_t R = cfg.round_ops ? cfg.round_ops : 1;
+  const uint32_t R = cfg.max_lag ? 1u : (cfg.round_ops ? cfg.round_ops : 1);
   int32_t seq = 0;
   int32_t min_seq = 0;
+  int32_t cref[32] = {0};  // max_lag: each author's refSeq (its last seen seq)
   uint32_t done = 0;
   while (done < cfg.ops_per_doc) {
-    const int32_t round_start = seq;  // refSeq == msn for the whole round
-    if (round_start > min_seq) {
+    const int32_t round_start = seq;  // rounds: refSeq == msn for the whole round
+    if (!cfg.max_lag && round_start > min_seq) {
       min_seq = round_start;
       // zamboni in the model: drop units removed at or below minSeq
       size_t w = 0;
@@ -296,7 +307,17 @@ void gen_doc(const mteg_config& cfg, uint32_t d, DocOut& out) {
       const uint32_t author = (uint32_t)rng.uniform(0, C - 1);
       if (short_of[author] < 0) short_of[author] = next_short++;
       const int c = short_of[author];
-      const int32_t r = round_start;
+      int32_t r = round_start, msn = round_start;
+      if (cfg.max_lag) {
+        // the author catches up to a seq at most max_lag behind; the
+        // sequencer's msn is the lowest refSeq of all authors
+        const int32_t lo = seq - (int32_t)cfg.max_lag;
+        const int32_t want = (int32_t)rng.uniform(lo > 0 ? lo : 0, seq);
+        if (want > cref[author]) cref[author] = want;
+        r = cref[author];
+        msn = cref[0];
+        for (uint32_t a = 1; a < C; a++) msn = cref[a] < msn ? cref[a] : msn;
+      }
       const int32_t s = ++seq;
       int64_t L = 0;
       for (const Unit& u : units) L += visible(u, r, c) ? 1 : 0;
@@ -307,7 +328,7 @@ void gen_doc(const mteg_config& cfg, uint32_t d, DocOut& out) {
       std::memset(&op, 0, sizeof(op));
       op.seq = s;
       op.ref_seq = r;
-      op.min_seq = r;
+      op.min_seq = msn;
       op.type = (uint8_t)type;
       op.client = (uint8_t)c;
       op.flags = MTE_F_MSG_END;
@@ -329,14 +350,16 @@ void gen_doc(const mteg_config& cfg, uint32_t d, DocOut& out) {
           op.a = (uint32_t)out.text.size();  // per-doc offset, fixed up at fill
           for (int32_t i = 0; i < n; i++) out.text.push_back((uint16_t)('B' + author));
         }
-        // model: place before the pos-th unit visible to c
+        // model: the engine's placement: before the first
+        // defined unit with P >= pos.  Lengths alone would not need the exact
+        // place, but with lagging refSeqs a later range op of another
+        // perspective removes units by position, so the order must match.
+        const bool newcalc = (out.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
         size_t at = units.size();
         int64_t seen = 0;
         for (size_t i = 0; i < units.size(); i++) {
-          if (visible(units[i], r, c)) {
-            if (seen == pos) { at = i; break; }
-            seen++;
-          }
+          if (seen >= pos && defined(units[i], r, c, newcalc)) { at = i; break; }
+          if (visible(units[i], r, c)) seen++;
         }
         units.insert(units.begin() + (ptrdiff_t)at, (size_t)n, Unit{s, kNone, 0u, c});
       } else {
@@ -359,6 +382,13 @@ void gen_doc(const mteg_config& cfg, uint32_t d, DocOut& out) {
         }
       }
       out.ops.push_back(op);
+      if (cfg.max_lag && msn > min_seq) {
+        min_seq = msn;  // the window moves after the message (client.ts:934)
+        size_t w = 0;
+        for (size_t i = 0; i < units.size(); i++)
+          if (!(units[i].rseq != kNone && units[i].rseq <= min_seq)) units[w++] = units[i];
+        units.resize(w);
+      }
     }
   }
 }

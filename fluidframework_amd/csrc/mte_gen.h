@@ -5,7 +5,8 @@
  *
  * Stream model, following the reference conflict farm
  * (test/mergeTreeOperationRunner.ts:149-199, test/client.conflictFarm.spec.ts):
- * rounds of R ops whose refSeq == msn == the round's start seq; the author of
+ * rounds of R ops whose refSeq == msn == the round's start seq (or, with
+ * max_lag, per-client lagging refSeqs and msn = their minimum); the author of
  * each op is uniform among C clients; positions are drawn from the author's
  * perspective length; below minLength the op is an insert of the author's
  * name repeated 1-3 times.  PRNG: MT19937 init_by_array([0xDEADBEEF,
@@ -49,6 +50,12 @@ typedef struct mteg_config {
   uint32_t init_segs;    /* > 0: preload this many one-unit segments per doc
                             (mte_load_segments) and use the long-doc generator */
   uint32_t max_range;    /* remove / annotate span cap (0 = farm rule)     */
+  uint32_t max_lag;      /* 0: rounds (refSeq == msn == round start).  > 0:
+                            every client keeps its own refSeq, which moves up
+                            to a seq in [seq - max_lag, seq - 1] when it sends;
+                            msn = the minimum over the clients (the sequencer
+                            rule, deli clientSeqManager.ts:130-137), so ops
+                            see each other's concurrent edits partially */
 } mteg_config;
 
 typedef struct mteg_stream mteg_stream;

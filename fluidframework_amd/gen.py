@@ -19,7 +19,8 @@ KEY_NAMES = ["client", "bold", "color", "markerId"]
 class GenConfig(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in (
         "config_id", "n_docs", "ops_per_doc", "doc_base", "clients", "min_length", "round_ops",
-        "mix", "marker_every", "length_mode", "init_len", "n_threads", "init_segs", "max_range")]
+        "mix", "marker_every", "length_mode", "init_len", "n_threads", "init_segs", "max_range",
+        "max_lag")]
 
 
 class GenSizes(C.Structure):
@@ -73,7 +74,7 @@ def generate(config_id=2, n_docs=None, ops_per_doc=None, doc_base=0, n_threads=N
     cfg = GenConfig(config_id, p["n_docs"], p["ops_per_doc"], doc_base, p["clients"],
                     p["min_length"], p["round_ops"], p["mix"], p["marker_every"],
                     p["length_mode"], p.get("init_len", 0), n_threads or default_threads(),
-                    p.get("init_segs", 0), p.get("max_range", 0))
+                    p.get("init_segs", 0), p.get("max_range", 0), p.get("max_lag", 0))
     h = C.c_void_p()
     rc = lib.mteg_generate(C.byref(cfg), C.byref(h))
     if rc:

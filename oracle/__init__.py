@@ -1,4 +1,5 @@
-"""Python binding of the CPU restatement (oracle/oracle.c).
+"""Python binding of the CPU restatements (oracle/oracle.c flat, oracle/tree.c
+tree-exact).
 
 TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
 cpu_baseline leg of bench.py, always as the checker / the timed CPU baseline,
@@ -30,37 +31,62 @@ def load():
         build()
     lib = C.CDLL(LIB)
     vp, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
-    for name, args in {
-        "orc_create": [u32, vp], "orc_destroy": [vp],
-        "orc_load_docs": [vp, u32, vp, vp, u64, vp, u32, vp, u32],
-        "orc_load_segments": [vp, vp, vp, u64],
-        "orc_read_segments": [vp, u32, vp],
-        "orc_apply_batch": [vp, vp, C.c_int], "orc_read_doc": [vp, u32, vp],
-        "orc_digest": [vp, vp, u32], "orc_doc_status": [vp, vp, u32],
-        "orc_stats_get": [vp, vp], "orc_doc_nsegs": [vp, u32, vp],
-    }.items():
-        f = getattr(lib, name)
-        f.argtypes = args
-        f.restype = C.c_int
+    for pre in ("orc", "ort"):
+        for name, args in {
+            "create": [u32, vp], "destroy": [vp],
+            "load_docs": [vp, u32, vp, vp, u64, vp, u32, vp, u32],
+            "load_segments": [vp, vp, vp, u64],
+            "read_segments": [vp, u32, vp],
+            "apply_batch": [vp, vp, C.c_int], "read_doc": [vp, u32, vp],
+            "digest": [vp, vp, u32], "doc_status": [vp, vp, u32],
+            "stats_get": [vp, vp], "doc_nsegs": [vp, u32, vp],
+        }.items():
+            f = getattr(lib, f"{pre}_{name}")
+            f.argtypes = args
+            f.restype = C.c_int
+    lib.ort_doc_shape.argtypes = [vp, u32, C.c_char_p, u32]
+    lib.ort_doc_shape.restype = C.c_int
     _lib = lib
     return lib
 
 
-class OracleEngine(EngineBase):
-    """Same surface as fluidframework_amd.engine.DeviceEngine, on the CPU."""
+class _Fn:
+    """lib.<prefix>_<name> lookups for one restatement."""
 
-    def __init__(self, n_keys=0, threads=1):
+    def __init__(self, lib, pre):
+        self.lib, self.pre = lib, pre
+
+    def __getattr__(self, name):
+        return getattr(self.lib, f"{self.pre}_{name}")
+
+
+class OracleEngine(EngineBase):
+    """Same surface as fluidframework_amd.engine.DeviceEngine, on the CPU.
+
+    tree=False: the flat restatement (oracle.c).  tree=True: the tree-exact one
+    (tree.c), which keeps the reference's B+tree, its lazy zamboni and therefore
+    its insert placement next to tombstones in legacy length-calc documents."""
+
+    def __init__(self, n_keys=0, threads=1, tree=False):
         self.lib = load()
+        self.f = _Fn(self.lib, "ort" if tree else "orc")
+        self.tree = tree
         self.n_keys = n_keys
         self.threads = threads
         h = C.c_void_p()
-        self._check(self.lib.orc_create(n_keys, C.byref(h)), "orc_create")
+        self._check(self.f.create(n_keys, C.byref(h)), "create")
         self.ctx = h
 
     def close(self):
         if getattr(self, "ctx", None):
-            self.lib.orc_destroy(self.ctx)
+            self.f.destroy(self.ctx)
             self.ctx = None
+
+    def shape(self, doc):
+        """(tree shape string, LRU heap size) of one document (tree=True only)."""
+        buf = C.create_string_buffer(1 << 16)
+        hn = self.lib.ort_doc_shape(self.ctx, doc, buf, len(buf))
+        return buf.value.decode(), hn
 
     def __del__(self):
         try:
@@ -74,36 +100,36 @@ class OracleEngine(EngineBase):
         ps = _arr(propsets, PROPSET_DTYPE)
         pe = _arr(props, PROP_DTYPE)
         self.n_docs = len(inits)
-        self._check(self.lib.orc_load_docs(self.ctx, len(inits), ptr(inits), ptr(text), len(text),
+        self._check(self.f.load_docs(self.ctx, len(inits), ptr(inits), ptr(text), len(text),
                                            ptr(ps), len(ps), ptr(pe), len(pe)), "load_docs")
 
     def _read_segments(self, doc, lp):
-        return self.lib.orc_read_segments(self.ctx, doc, lp)
+        return self.f.read_segments(self.ctx, doc, lp)
 
     def load_segments(self, seg_offsets, segs):
         offs = _arr(seg_offsets, np.uint64)
         segs = _arr(segs, SEG_DTYPE)
-        self._check(self.lib.orc_load_segments(self.ctx, ptr(offs), ptr(segs), len(segs)), "load_segments")
+        self._check(self.f.load_segments(self.ctx, ptr(offs), ptr(segs), len(segs)), "load_segments")
 
     def apply_batch(self, batch):
         b, keep = make_batch_struct(self.n_docs, batch)
-        self._check(self.lib.orc_apply_batch(self.ctx, C.byref(b), self.threads), "apply_batch")
+        self._check(self.f.apply_batch(self.ctx, C.byref(b), self.threads), "apply_batch")
         del keep
         return 0
 
     def nsegs(self, doc):
         n = C.c_uint32()
-        self._check(self.lib.orc_doc_nsegs(self.ctx, doc, C.byref(n)), "nsegs")
+        self._check(self.f.doc_nsegs(self.ctx, doc, C.byref(n)), "nsegs")
         return n.value
 
     def _read_doc(self, doc, vptr):
-        return self.lib.orc_read_doc(self.ctx, doc, vptr)
+        return self.f.read_doc(self.ctx, doc, vptr)
 
     def _digest(self, p, n):
-        return self.lib.orc_digest(self.ctx, p, n)
+        return self.f.digest(self.ctx, p, n)
 
     def _doc_status(self, p, n):
-        return self.lib.orc_doc_status(self.ctx, p, n)
+        return self.f.doc_status(self.ctx, p, n)
 
     def _stats(self, sp):
-        return self.lib.orc_stats_get(self.ctx, sp)
+        return self.f.stats_get(self.ctx, sp)

@@ -13,13 +13,14 @@
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it.
  */
 #include "oracle.h"
+#include "orc_common.h"
 
 #include <limits.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
-#define NONE_SEQ INT32_MAX /* "removedSeq undefined" */
+#define NONE_SEQ ORC_NONE_SEQ
 
 typedef struct {
   int32_t len;   /* cachedLength (text: UTF-16 units, marker: 1)          */
@@ -188,28 +189,6 @@ static int64_t doc_split_at(odoc* d, int64_t pos, uint64_t* written) {
   return -1;
 }
 
-/* PropertiesManager.addProperties for a remote observer (collaborating, no
- * pending local keys, so shouldModifyKey is true for every key):
- * segmentPropertiesManager.ts:63-151.  rewrite first clears the keys not in
- * newProps (105-119); then null deletes, anything else sets (121-148).  The
- * falsy-value test of the rewrite loop cancels against the set loop, so the net
- * effect is "clear all, then apply". */
-static uint64_t apply_props(uint32_t* props, uint32_t n_keys, const mte_propset* ps,
-                            const mte_prop* pe, int rewrite) {
-  uint64_t w = 0;
-  if (rewrite) {
-    for (uint32_t k = 0; k < n_keys; k++) props[k] = 0;
-  }
-  for (uint32_t j = 0; j < ps->count; j++) {
-    const mte_prop* p = &pe[ps->first + j];
-    if (p->key < n_keys) {
-      props[p->key] = p->value; /* value 0 == null == delete */
-      w++;
-    }
-  }
-  return w;
-}
-
 typedef struct {
   const mte_batch* b;
   uint64_t text_base;
@@ -291,7 +270,7 @@ static int doc_apply(odoc* d, const mte_op* op, const apply_env* env) {
         d->units += (uint64_t)len;
       }
       if (op->b != MTE_NO_PROPS)
-        d->pwrites += apply_props(ns->props, env->n_keys, &env->b->propsets[op->b], env->b->props, 0);
+        d->pwrites += orc_apply_props(ns->props, env->n_keys, &env->b->propsets[op->b], env->b->props, 0);
       d->written += 1;
     }
     if ((rc = check_op_window(d, op))) return rc;
@@ -321,7 +300,7 @@ static int doc_apply(odoc* d, const mte_op* op, const apply_env* env) {
             g->rmask |= 1u << c;
           }
         } else {
-          d->pwrites += apply_props(g->props, env->n_keys, &env->b->propsets[op->a], env->b->props,
+          d->pwrites += orc_apply_props(g->props, env->n_keys, &env->b->propsets[op->a], env->b->props,
                                     (op->flags & MTE_F_REWRITE) != 0);
         }
         d->written += 1;
@@ -427,7 +406,7 @@ int orc_load_docs(orc_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
       g->toff = (uint32_t)(base + in->text_off);
       if (in->propset != MTE_NO_PROPS) {
         if (in->propset >= n_propsets) return MTE_E_INVALID_ARG;
-        apply_props(g->props, c->n_keys, &propsets[in->propset], props, 0);
+        orc_apply_props(g->props, c->n_keys, &propsets[in->propset], props, 0);
       }
       d->n = 1;
     }
@@ -466,7 +445,7 @@ int orc_load_segments(orc_ctx* c, const uint64_t* seg_offsets, const mte_seg* se
       g->toff = marker ? 0u : sg->text_off;
       if (sg->propset != MTE_NO_PROPS) {
         if (sg->propset >= c->n_load_ps) return MTE_E_INVALID_ARG;
-        apply_props(g->props, c->n_keys, &c->load_ps[sg->propset], c->load_pe, 0);
+        orc_apply_props(g->props, c->n_keys, &c->load_ps[sg->propset], c->load_pe, 0);
       }
     }
     d->n = (uint32_t)(e - b);
@@ -600,50 +579,18 @@ int orc_read_segments(orc_ctx* c, uint32_t doc, mte_seg_list* v) {
   return MTE_OK;
 }
 
-/* ---- canonical digest (DESIGN.md "Digest") ------------------------------- */
-#define M61 ((1ull << 61) - 1)
-static const uint64_t DIG_B1 = 0x1d8e4e27c47d124full % ((1ull << 61) - 1);
-static const uint64_t DIG_B2 = 0x0a0761d6478bd642ull % ((1ull << 61) - 1);
-
-static inline uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-  return z ^ (z >> 31);
-}
-static inline uint64_t mulmod61(uint64_t a, uint64_t b) {
-  unsigned __int128 p = (unsigned __int128)a * b;
-  uint64_t lo = (uint64_t)(p & M61), hi = (uint64_t)(p >> 61);
-  uint64_t r = lo + hi;
-  if (r >= M61) r -= M61;
-  return r;
-}
-static inline uint64_t addmod61(uint64_t a, uint64_t b) {
-  uint64_t r = a + b;
-  if (r >= M61) r -= M61;
-  return r;
-}
-
+/* ---- canonical digest (DESIGN.md "Digest", orc_common.h) ------------------ */
 int orc_digest(orc_ctx* c, uint64_t* out, uint32_t n_docs) {
   if (!c || !out || n_docs != c->n_docs) return MTE_E_INVALID_ARG;
   for (uint32_t di = 0; di < n_docs; di++) {
     odoc* d = &c->docs[di];
-    uint64_t n = 0, h1 = 0, h2 = 0, sum = 0;
+    orc_digest_acc acc = {0, 0, 0, 0};
     for (uint32_t i = 0; i < d->n; i++) {
       const oseg* g = &d->s[i];
       if (g->rseq != NONE_SEQ) continue;
-      uint64_t ph = 0;
-      for (uint32_t k = 0; k < c->n_keys; k++)
-        if (g->props[k]) ph += mix64(((uint64_t)(k + 1) << 32) | g->props[k]);
-      for (int32_t u = 0; u < g->len; u++) {
-        uint64_t rec = g->kind == 0 ? (uint64_t)c->arena[g->toff + (uint32_t)u]
-                                    : ((1ull << 32) | (uint64_t)(g->kind - 1));
-        uint64_t x = mix64(rec * 0x9E3779B97F4A7C15ull + ph) % M61;
-        h1 = addmod61(mulmod61(h1, DIG_B1), x);
-        h2 = addmod61(mulmod61(h2, DIG_B2), x);
-        sum += x;
-        n++;
-      }
+      orc_digest_seg(&acc, g->kind, g->kind == 0 ? c->arena + g->toff : NULL, g->len, g->props, c->n_keys);
     }
+    const uint64_t n = acc.n, h1 = acc.h1, h2 = acc.h2, sum = acc.sum;
     out[4 * (size_t)di + 0] = n;
     out[4 * (size_t)di + 1] = h1;
     out[4 * (size_t)di + 2] = h2;
