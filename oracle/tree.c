@@ -76,6 +76,7 @@ typedef struct {
   int64_t* P;
   uint32_t flat_cap;
   uint64_t ops;
+  uint64_t n_push, n_pop, n_scour, n_split, n_pack, n_merge;  /* structure counters (tests, tuning) */
   mte_doc_init init;
 } __attribute__((aligned(128))) tdoc;
 
@@ -227,6 +228,7 @@ typedef struct {
   int32_t seq;   /* TreeMaintenanceSequenceNumber (-2) or the op's seq */
   tnode* cand;   /* the new segment (insert) */
   int oom;
+  uint64_t* counter; /* block splits */
 } walk_ctx;
 
 /* breakTie (mergeTree.ts:1705-1721), called only when pos == len */
@@ -282,6 +284,7 @@ static tnode* inserting_walk(tnode* block, int64_t pos, const persp* v, walk_ctx
   block->cc++;
   if (block->cc < MAX_NODES) return NULL;
   tnode* sp = split_block(block);
+  if (w->counter) (*w->counter)++;
   if (!sp) w->oom = 1;
   return sp;
 }
@@ -300,7 +303,7 @@ static int update_root(tdoc* d, tnode* split) {
 
 /* ensureIntervalBoundary (mergeTree.ts:1698-1702) */
 static int ensure_boundary(tdoc* d, int64_t pos, const persp* v) {
-  walk_ctx w = {WALK_SPLIT, -2, NULL, 0};
+  walk_ctx w = {WALK_SPLIT, -2, NULL, 0, &d->n_split};
   tnode* sp = inserting_walk(d->root, pos, v, &w);
   if (w.oom) return MTE_E_OOM;
   return update_root(d, sp);
@@ -318,6 +321,7 @@ static int heap_add(tdoc* d, tnode* seg, int32_t max_seq) {
     d->hcap = nc;
   }
   lru_ent* L = d->heap;
+  d->n_push++;
   L[++d->hn] = (lru_ent){max_seq, seg};
   seg->hrefs++;
   for (uint32_t k = d->hn; k > 1 && L[k >> 1].max_seq - L[k].max_seq > 0; k >>= 1) {
@@ -418,6 +422,7 @@ static int scour_node(tdoc* d, tnode* node, nodevec* hold, uint32_t n_keys) {
         memcpy(t + prev->len, x->text, (size_t)x->len * sizeof(uint16_t));
         prev->text = t;
         prev->len += x->len;
+        d->n_merge++;
         unlink_leaf(x);
       } else {
         if ((rc = nv_push(hold, x))) return rc;
@@ -434,6 +439,7 @@ static int scour_node(tdoc* d, tnode* node, nodevec* hold, uint32_t n_keys) {
 /* packParent (mergeTree.ts:750-798) */
 static int pack_parent(tdoc* d, tnode* parent, uint32_t n_keys) {
   nodevec hold = {NULL, 0, 0};
+  d->n_pack++;
   int rc = MTE_OK;
   for (int i = 0; i < parent->cc; i++) {
     tnode* cb = parent->ch[i];
@@ -476,6 +482,7 @@ static int zamboni(tdoc* d, uint32_t n_keys) {
   for (int i = 0; i < ZAMBONI_MAX; i++) {
     if (d->hn == 0 || d->heap[1].max_seq > d->min_seq) break;
     lru_ent e = heap_get(d);
+    d->n_pop++;
     tnode* seg = e.seg; /* its entry still counts in hrefs: a scour below cannot free it */
     if (seg->parent && seg->parent->scour != 0) {
       tnode* block = seg->parent;
@@ -485,6 +492,7 @@ static int zamboni(tdoc* d, uint32_t n_keys) {
         return rc;
       }
       block->scour = 0;
+      d->n_scour++;
       if (hold.n < block->cc) {
         for (int j = 0; j < hold.n; j++) assign_child(block, hold.v[j], j);
         for (int j = hold.n; j < MAX_NODES; j++) block->ch[j] = NULL;
@@ -596,7 +604,7 @@ static int doc_apply(tdoc* d, const mte_op* op, const apply_env* env) {
         ns->po = 1;
         orc_apply_props(ns->props, env->n_keys, &env->b->propsets[op->b], env->b->props, 0);
       }
-      walk_ctx w = {WALK_INSERT, s, ns, 0};
+      walk_ctx w = {WALK_INSERT, s, ns, 0, &d->n_split};
       tnode* sp = inserting_walk(d->root, op->pos1, &v, &w);
       if (w.oom) return MTE_E_OOM;
       if (!ns->parent) { /* "MergeTree insert failed" (1666-1672) */
@@ -888,7 +896,10 @@ int ort_apply_batch(ort_ctx* c, const mte_batch* b, int n_threads) {
     if (op->type == MTE_OP_INSERT && op->b != MTE_NO_PROPS && op->b >= b->n_propsets) return MTE_E_INVALID_ARG;
     if (op->type == MTE_OP_ANNOTATE && op->a >= b->n_propsets) return MTE_E_INVALID_ARG;
   }
-  for (uint32_t i = 0; i < c->n_docs; i++) c->docs[i].ops = 0;
+  for (uint32_t i = 0; i < c->n_docs; i++) {
+    tdoc* d = &c->docs[i];
+    d->ops = d->n_push = d->n_pop = d->n_scour = d->n_split = d->n_pack = d->n_merge = 0;
+  }
   if (n_threads < 1) n_threads = 1;
   if ((uint32_t)n_threads > c->n_docs) n_threads = c->n_docs ? (int)c->n_docs : 1;
   worker_arg* args = (worker_arg*)calloc((size_t)n_threads, sizeof(worker_arg));
@@ -1005,7 +1016,19 @@ int ort_doc_status(ort_ctx* c, int32_t* out, uint32_t n_docs) {
 int ort_stats_get(ort_ctx* c, mte_stats* o) {
   if (!c || !o) return MTE_E_INVALID_ARG;
   memset(o, 0, sizeof(*o));
-  for (uint32_t i = 0; i < c->n_docs; i++) o->ops_applied += c->docs[i].ops;
+  /* structure counters of the last batch, in the spare fields: segs_scanned =
+   * LRU pushes, segs_written = pops, prop_writes = block scours, units_inserted
+   * = block splits, max_segs = packParent calls, chunk_scanned = append-merges */
+  for (uint32_t i = 0; i < c->n_docs; i++) {
+    const tdoc* d = &c->docs[i];
+    o->ops_applied += d->ops;
+    o->segs_scanned += d->n_push;
+    o->segs_written += d->n_pop;
+    o->prop_writes += d->n_scour;
+    o->units_inserted += d->n_split;
+    o->max_segs += d->n_pack;
+    o->chunk_scanned += d->n_merge;
+  }
   return MTE_OK;
 }
 
