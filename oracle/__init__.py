@@ -44,8 +44,20 @@ def load():
             f = getattr(lib, f"{pre}_{name}")
             f.argtypes = args
             f.restype = C.c_int
-    lib.ort_doc_shape.argtypes = [vp, u32, C.c_char_p, u32]
-    lib.ort_doc_shape.restype = C.c_int
+    for name, args in {
+        "oti_create": [u32, vp], "oti_destroy": [vp],
+        "oti_load_docs": [vp, u32, vp, vp, u64, vp, u32, vp, u32],
+        "oti_load_segments": [vp, vp, vp, u64], "oti_apply_batch": [vp, vp, C.c_int],
+        "oti_read_doc": [vp, u32, vp], "oti_digest": [vp, vp, u32], "oti_doc_status": [vp, vp, u32],
+        "oti_doc_nsegs": [vp, u32, vp],
+    }.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = C.c_int
+    for pre in ("ort", "oti"):
+        f = getattr(lib, f"{pre}_doc_shape")
+        f.argtypes = [vp, u32, C.c_char_p, u32]
+        f.restype = C.c_int
     _lib = lib
     return lib
 
@@ -65,11 +77,13 @@ class OracleEngine(EngineBase):
 
     tree=False: the flat restatement (oracle.c).  tree=True: the tree-exact one
     (tree.c), which keeps the reference's B+tree, its lazy zamboni and therefore
-    its insert placement next to tombstones in legacy length-calc documents."""
+    its insert placement next to tombstones in legacy length-calc documents.
+    tree="items": the same tree on a flat item array (titems.c), the spec of
+    the GPU tree pass."""
 
     def __init__(self, n_keys=0, threads=1, tree=False):
         self.lib = load()
-        self.f = _Fn(self.lib, "ort" if tree else "orc")
+        self.f = _Fn(self.lib, "oti" if tree == "items" else ("ort" if tree else "orc"))
         self.tree = tree
         self.n_keys = n_keys
         self.threads = threads
@@ -85,7 +99,7 @@ class OracleEngine(EngineBase):
     def shape(self, doc):
         """(tree shape string, LRU heap size) of one document (tree=True only)."""
         buf = C.create_string_buffer(1 << 16)
-        hn = self.lib.ort_doc_shape(self.ctx, doc, buf, len(buf))
+        hn = self.f.doc_shape(self.ctx, doc, buf, len(buf))
         return buf.value.decode(), hn
 
     def __del__(self):
@@ -132,4 +146,6 @@ class OracleEngine(EngineBase):
         return self.f.doc_status(self.ctx, p, n)
 
     def _stats(self, sp):
+        if self.tree == "items":
+            return 0
         return self.f.stats_get(self.ctx, sp)
