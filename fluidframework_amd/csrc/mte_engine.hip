@@ -19,6 +19,7 @@
 #include "mte_replay.h"
 #include "mte_stream.h"
 #include "mte_chunk.h"
+#include "mte_tree.h"
 
 using namespace mte;
 
@@ -31,49 +32,66 @@ __global__ void begin_batch_kernel(DocHdr* hdr, unsigned long long* stats, uint3
   if (d == 0) *gdone = 0;
   if (d >= n_docs) return;
   hdr[d].resume = 0;
-  hdr[d].flags &= ~kHdrNeedsEsc;
+  hdr[d].flags &= ~(kHdrNeedsEsc | kHdrTreeEsc);
 #pragma unroll
   for (int t = 0; t < kNumStats; t++) stats[(size_t)d * kNumStats + t] = 0;
 }
 
 // (re)initialise docs from their load description: one seq-0 LocalClientId
 // text segment (client.replay.spec.ts:22-23)
+// Legacy length-calc documents also carry the reference's B+tree (mte_tree.h):
+// the load text is one leaf in the root leaf block (MergeTree starts with an
+// empty root, mergeTree.ts:495-498; the replay harness's insertTextLocal adds
+// one leaf), an empty document one placeholder; a loaded body has
+// reloadFromSegments' blocks of 7 (image_kernel writes the tree words).
 __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_doc_init* inits,
                              const uint32_t* init_props, uint32_t n_keys, uint32_t n_docs,
-                             const uint64_t* img_off) {
+                             const uint64_t* img_off, uint32_t* tree) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= n_docs) return;
   const mte_doc_init in = inits[d];
   const uint32_t n_img = img_off ? (uint32_t)(img_off[d + 1] - img_off[d]) : 0u;
+  const bool legacy = !(in.flags & MTE_DOC_NEW_LENGTH_CALC) && tree != nullptr;
   DocHdr h;
-  h.nseg = n_img ? (int32_t)n_img : (in.text_len > 0 ? 1 : 0);
+  h.nseg = n_img ? (int32_t)n_img : (in.text_len > 0 || legacy ? 1 : 0);
   h.min_seq = in.min_seq;
   h.cur_seq = in.cur_seq;
   h.status = 0;
   h.flags = in.flags & MTE_DOC_NEW_LENGTH_CALC;
   h.resume = 0;
   h.pad0 = h.pad1 = 0;
+  if (legacy) {
+    int depth = 1;
+    for (uint64_t w = 7; n_img && w < n_img; w *= 7) depth++;
+    h.pad0 = n_img ? n_img + 1 : 2;  // next segment id
+    h.pad1 = (uint32_t)depth;         // depth | heap size << 8
+  }
   hdr[d] = h;
   if (n_img) return;  // image_kernel writes the segments
   const uint64_t i = (uint64_t)d * cap;
   soa.len[i] = (int32_t)in.text_len;
   soa.seq[i] = 0;
-  soa.rseq[i] = kNone;
+  soa.rseq[i] = (legacy && in.text_len == 0) ? kPad : kNone;
   soa.rmask[i] = 0;
   soa.meta[i] = 0;  // clientId -1, text
   soa.toff[i] = in.text_off;
+  uint32_t po = 0;
   for (uint32_t k = 0; k < n_keys; k++) soa.props[k * soa.plane_stride + i] = init_props[(size_t)d * MTE_MAX_KEYS + k];
+  if (in.propset != MTE_NO_PROPS) po = kTPo;
+  if (legacy) tree[i] = in.text_len > 0 ? (1u | po | (1u << 8)) : (1u | kTEmpty);
 }
 
 // the mte_load_segments image -> the flat planes (one thread per segment)
+// (the image's last plane is the tree word, for the tree pass)
 __global__ void image_kernel(SegSoA soa, uint32_t cap, uint32_t n_planes, const uint32_t* img, uint64_t img_stride,
-                             const uint32_t* img_doc, const uint64_t* img_off, uint64_t n_img) {
+                             const uint32_t* img_doc, const uint64_t* img_off, uint64_t n_img, uint32_t* tree) {
   for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_img;
        g += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t d = img_doc[g];
     const uint64_t x = (uint64_t)d * cap + (g - img_off[d]);
     uint32_t* pl = reinterpret_cast<uint32_t*>(soa.len);
     for (uint32_t p = 0; p < n_planes; p++) pl[p * soa.plane_stride + x] = img[p * img_stride + g];
+    if (tree) tree[x] = img[n_planes * img_stride + g];
   }
 }
 
@@ -282,8 +300,14 @@ struct mte_ctx {
   uint64_t ops_cap = 0, n_ops = 0;
   uint4* d_cps = nullptr;  // compiled propsets, 2 x uint4 each (props_kernel)
   uint64_t cps_cap = 0, n_propsets = 0;
-  uint32_t* d_pairs = nullptr;  // pass-1 doc pairs
+  uint32_t* d_pairs = nullptr;  // pass-1 doc pairs (new length calc documents)
   uint32_t n_pairs = 0;
+  // tree pass (legacy length calc documents, mte_tree.h)
+  uint32_t* d_tree = nullptr;       // tree word per slot
+  uint2* d_heap = nullptr;          // LRU heap per document
+  uint32_t* d_tree_docs = nullptr;  // the legacy documents
+  uint32_t n_tree = 0;
+  std::vector<uint8_t> h_legacy;    // per doc
   uint64_t* d_off = nullptr;
   uint64_t off_cap = 0;
   mte_propset* d_ps = nullptr;
@@ -349,9 +373,14 @@ void free_docs(mte_ctx* c) {
   c->chunked = false;
   if (c->d_wclock) (void)hipFree(c->d_wclock);
   c->d_wclock = nullptr;
-  void* ps[] = {c->hdr, c->soa.len, c->stats, c->d_inits, c->d_init_props, c->d_digest, c->d_pairs};
+  void* ps[] = {c->hdr, c->soa.len, c->stats, c->d_inits, c->d_init_props, c->d_digest, c->d_pairs,
+                c->d_tree, c->d_heap, c->d_tree_docs};
   for (void* p : ps)
     if (p) (void)hipFree(p);
+  c->d_tree = nullptr;
+  c->d_heap = nullptr;
+  c->d_tree_docs = nullptr;
+  c->n_tree = 0;
   c->hdr = nullptr;
   c->soa = SegSoA{};
   c->stats = nullptr;
@@ -367,13 +396,13 @@ int launch_reset(mte_ctx* c) {
   if (!c->n_docs) return MTE_OK;
   const uint32_t blocks = (c->n_docs + 255) / 256;
   hipLaunchKernelGGL(reset_kernel, dim3(blocks), dim3(256), 0, c->stream, c->hdr, c->soa, c->cap,
-                     c->d_inits, c->d_init_props, c->n_keys, c->n_docs, (const uint64_t*)c->d_img_off);
+                     c->d_inits, c->d_init_props, c->n_keys, c->n_docs, (const uint64_t*)c->d_img_off, c->d_tree);
   HIPCHK(c, hipGetLastError());
   if (c->n_img) {
     const uint64_t nb = std::min<uint64_t>((c->n_img + 255) / 256, 65536);
     hipLaunchKernelGGL(image_kernel, dim3((uint32_t)nb), dim3(256), 0, c->stream, c->soa, c->cap,
                        (uint32_t)(kFieldPlanes + c->kt), c->d_img, c->n_img, c->d_img_doc,
-                       (const uint64_t*)c->d_img_off, c->n_img);
+                       (const uint64_t*)c->d_img_off, c->n_img, c->d_tree);
     HIPCHK(c, hipGetLastError());
   }
   c->ran = false;
@@ -382,9 +411,19 @@ int launch_reset(mte_ctx* c) {
 
 template <int K, bool S>
 int launch_replay(mte_ctx* c, const ReplayArgs& a) {
+  // the tree pass: legacy length calc documents (mte_tree.h), up to 252
+  // items at E <= 4, then up to 1,020 at E = 8 / 16
+  if (c->n_tree) {
+    TreeArgs t{c->d_tree, c->d_heap, c->d_tree_docs, c->n_tree, c->arena};
+    const uint32_t bt = (c->n_tree + kDocsPerBlock - 1) / kDocsPerBlock;
+    hipLaunchKernelGGL((tree_kernel<K, S, false>), dim3(bt), dim3(kDocsPerBlock * kWave), 0, c->stream, a, t);
+    HIPCHK(c, hipGetLastError());
+    hipLaunchKernelGGL((tree_kernel<K, S, true>), dim3(bt), dim3(kDocsPerBlock * kWave), 0, c->stream, a, t);
+    HIPCHK(c, hipGetLastError());
+  }
   // pass 1: two documents per wavefront (docs up to 126 segments)
   const uint32_t b1 = (c->n_pairs + kPairsPerBlock - 1) / kPairsPerBlock;
-  hipLaunchKernelGGL((pair_kernel<K, S, kPairsPerBlock>), dim3(b1), dim3(kPairsPerBlock * kWave), 0, c->stream, a);
+  if (b1) hipLaunchKernelGGL((pair_kernel<K, S, kPairsPerBlock>), dim3(b1), dim3(kPairsPerBlock * kWave), 0, c->stream, a);
   HIPCHK(c, hipGetLastError());
   // pass 2: docs that outgrew pass 1 continue one per wavefront (up to 1022 segments)
   const uint32_t b2 = (c->n_docs + kDocsPerBlock - 1) / kDocsPerBlock;
@@ -625,14 +664,34 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     // the chip at one document per wave (<= CUs x 4 SIMDs x MTE_PAIR_WAVES,
     // e.g. config 2's 1k docs) runs one per wave instead: pairing it would
     // leave SIMDs idle and serialise two documents per wave.
+    // Legacy length-calc documents go to the tree pass instead (mte_tree.h).
+    std::vector<uint32_t> flat_docs, tree_docs;
+    c->h_legacy.assign(n_docs, 0);
+    for (uint32_t d = 0; d < n_docs; d++) {
+      if (docs[d].flags & MTE_DOC_NEW_LENGTH_CALC) {
+        flat_docs.push_back(d);
+      } else {
+        tree_docs.push_back(d);
+        c->h_legacy[d] = 1;
+      }
+    }
+    const uint32_t nf = (uint32_t)flat_docs.size();
     int n_cu = 0;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) n_cu = 0;
-    const bool solo = n_cu > 0 && (uint64_t)n_docs <= (uint64_t)n_cu * 4 * MTE_PAIR_WAVES;
-    c->n_pairs = solo ? n_docs : (n_docs + 1) / 2;
+    const bool solo = n_cu > 0 && (uint64_t)nf <= (uint64_t)n_cu * 4 * MTE_PAIR_WAVES;
+    c->n_pairs = solo ? nf : (nf + 1) / 2;
     std::vector<uint32_t> pairs((size_t)c->n_pairs * 2 + 2, 0xffffffffu);
-    for (uint32_t d = 0; d < n_docs; d++) pairs[solo ? 2 * (size_t)d : d] = d;
+    for (uint32_t i = 0; i < nf; i++) pairs[solo ? 2 * (size_t)i : i] = flat_docs[i];
     HIPCHK(c, hipMalloc((void**)&c->d_pairs, pairs.size() * 4));
     HIPCHK(c, hipMemcpy(c->d_pairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice));
+    c->n_tree = (uint32_t)tree_docs.size();
+    if (c->n_tree) {
+      HIPCHK(c, hipMalloc((void**)&c->d_tree, nslots * 4));
+      HIPCHK(c, hipMemsetAsync(c->d_tree, 0, nslots * 4, c->stream));
+      HIPCHK(c, hipMalloc((void**)&c->d_heap, sizeof(uint2) * (kTreeHeapCap + 1) * (size_t)n_docs));
+      HIPCHK(c, hipMalloc((void**)&c->d_tree_docs, tree_docs.size() * 4));
+      HIPCHK(c, hipMemcpy(c->d_tree_docs, tree_docs.data(), tree_docs.size() * 4, hipMemcpyHostToDevice));
+    }
   }
   if (n_docs) {
     HIPCHK(c, hipMemcpyAsync(c->d_inits, docs, sizeof(mte_doc_init) * n_docs, hipMemcpyHostToDevice, c->stream));
@@ -665,7 +724,9 @@ int mte_load_segments(mte_ctx* c, const uint64_t* seg_offsets, const mte_seg* se
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   const uint32_t np = kFieldPlanes + c->kt;
-  std::vector<uint32_t> img((size_t)np * (n_segs ? n_segs : 1), 0u), doc((size_t)(n_segs ? n_segs : 1), 0u);
+  // planes + the tree word (reloadFromSegments' blocks of 7 per level,
+  // mergeTree.ts:607-652), used by the tree pass
+  std::vector<uint32_t> img((size_t)(np + 1) * (n_segs ? n_segs : 1), 0u), doc((size_t)(n_segs ? n_segs : 1), 0u);
   // propsets of the load: the load propsets/props were consumed by
   // mte_load_docs; the per-doc initial props are kept, so segment propsets
   // arrive here through the host copy (set by mte_load_docs)
@@ -687,6 +748,18 @@ int mte_load_segments(mte_ctx* c, const uint64_t* seg_offsets, const mte_seg* se
       img[3 * n_segs + g] = sg.removed_seq == MTE_NOT_REMOVED ? 0u : sg.removers;
       img[4 * n_segs + g] = (uint32_t)(sg.client + 1) | (sg.kind << 8);
       img[5 * n_segs + g] = marker ? 0u : sg.text_off;
+      {
+        const uint64_t nd = e - b, k = g - b;
+        int depth = 1;
+        for (uint64_t w = 7; w < nd; w *= 7) depth++;
+        uint32_t h = 0;
+        if (k == 0) h = (uint32_t)depth;
+        else {
+          uint64_t w = 7;
+          for (int lv = 1; lv < depth && k % w == 0; lv++, w *= 7) h = (uint32_t)lv;
+        }
+        img[(size_t)np * n_segs + g] = h | (sg.propset != MTE_NO_PROPS ? kTPo : 0u) | ((uint32_t)(k + 1) << 8);
+      }
       if (sg.propset != MTE_NO_PROPS) {
         if (sg.propset >= c->h_load_ps.size())
           return set_err(c, MTE_E_INVALID_ARG, "doc %u segment %llu: bad propset", d, (unsigned long long)(g - b));
@@ -891,6 +964,9 @@ int mte_read_doc(mte_ctx* c, uint32_t doc, mte_doc_view* v) {
   const uint64_t db = (uint64_t)doc * c->cap;
   std::vector<int32_t> len(n + 1), rseq(n + 1);
   std::vector<uint32_t> meta(n + 1), toff(n + 1), props((size_t)(n + 1) * (c->n_keys ? c->n_keys : 1));
+  std::vector<uint32_t> tw(n + 1, 0u);  // tree words (legacy documents)
+  if (n && c->d_tree && c->h_legacy[doc])
+    HIPCHK(c, hipMemcpyAsync(tw.data(), c->d_tree + db, n * 4, hipMemcpyDeviceToHost, c->stream));
   if (n) {
     HIPCHK(c, hipMemcpyAsync(len.data(), c->soa.len + db, n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(rseq.data(), c->soa.rseq + db, n * 4, hipMemcpyDeviceToHost, c->stream));
@@ -908,13 +984,17 @@ int mte_read_doc(mte_ctx* c, uint32_t doc, mte_doc_view* v) {
   for (uint32_t i = 0; i < n; i++) {
     if (rseq[i] != kNone) continue;  // gatherText: only segments not removed
     const uint32_t kind = meta[i] >> 8;
-    if (ns < v->seg_cap) {
-      if (v->seg_len) v->seg_len[ns] = (uint32_t)len[i];
-      if (v->seg_kind) v->seg_kind[ns] = kind;
-      if (v->seg_props)
-        for (uint32_t k = 0; k < c->n_keys; k++) v->seg_props[(size_t)ns * c->n_keys + k] = props[(size_t)k * n + i];
+    if ((tw[i] & kTCont) && ns > 0) {  // a merged leaf reads as one segment
+      if (ns - 1 < v->seg_cap && v->seg_len) v->seg_len[ns - 1] += (uint32_t)len[i];
+    } else {
+      if (ns < v->seg_cap) {
+        if (v->seg_len) v->seg_len[ns] = (uint32_t)len[i];
+        if (v->seg_kind) v->seg_kind[ns] = kind;
+        if (v->seg_props)
+          for (uint32_t k = 0; k < c->n_keys; k++) v->seg_props[(size_t)ns * c->n_keys + k] = props[(size_t)k * n + i];
+      }
+      ns++;
     }
-    ns++;
     length += (uint32_t)len[i];
     if (kind == 0) {
       for (int32_t u = 0; u < len[i]; u++) {
@@ -939,17 +1019,30 @@ int mte_read_segments(mte_ctx* c, uint32_t doc, mte_seg_list* v) {
   const uint64_t db = (uint64_t)doc * c->cap;
   const uint32_t np = kFieldPlanes + c->n_keys;
   std::vector<uint32_t> pl((size_t)np * (n + 1));
+  std::vector<uint32_t> tw(n + 1, 0u);
+  if (n && c->d_tree && c->h_legacy[doc])
+    HIPCHK(c, hipMemcpyAsync(tw.data(), c->d_tree + db, n * 4, hipMemcpyDeviceToHost, c->stream));
   for (uint32_t p = 0; p < np && n; p++)
     HIPCHK(c, hipMemcpyAsync(pl.data() + (size_t)p * n, reinterpret_cast<const uint32_t*>(c->soa.len) +
                                                              p * c->soa.plane_stride + db,
                              n * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   uint64_t nt = 0;
+  uint64_t m = 0;  // segments out (a tree pass placeholder is none, a merged leaf one)
   for (uint32_t i = 0; i < n; i++) {
     const int32_t len = (int32_t)pl[i], rseq = (int32_t)pl[2 * (size_t)n + i];
     const uint32_t meta = pl[4 * (size_t)n + i], kind = meta >> 8;
-    if (i < v->seg_cap && v->segs) {
-      mte_seg& s = v->segs[i];
+    if (tw[i] & kTEmpty) continue;
+    if ((tw[i] & kTCont) && m > 0) {
+      if (m - 1 < v->seg_cap && v->segs) v->segs[m - 1].len += (uint32_t)len;
+      const uint32_t toff = pl[5 * (size_t)n + i];
+      for (int32_t u = 0; u < len; u++, nt++)
+        if (nt < v->text_cap && v->text) v->text[nt] = c->h_arena[toff + (uint32_t)u];
+      continue;
+    }
+    const uint64_t io = m++;
+    if (io < v->seg_cap && v->segs) {
+      mte_seg& s = v->segs[io];
       s.text_off = kind == 0 ? (uint32_t)nt : 0u;
       s.len = (uint32_t)len;
       s.seq = (int32_t)pl[(size_t)n + i];
@@ -960,7 +1053,7 @@ int mte_read_segments(mte_ctx* c, uint32_t doc, mte_seg_list* v) {
       s.propset = MTE_NO_PROPS;
       if (v->props)
         for (uint32_t k = 0; k < c->n_keys; k++)
-          v->props[(size_t)i * c->n_keys + k] = pl[(size_t)(kFieldPlanes + k) * n + i];
+          v->props[(size_t)io * c->n_keys + k] = pl[(size_t)(kFieldPlanes + k) * n + i];
     }
     if (kind == 0) {
       const uint32_t toff = pl[5 * (size_t)n + i];
@@ -968,7 +1061,7 @@ int mte_read_segments(mte_ctx* c, uint32_t doc, mte_seg_list* v) {
         if (nt < v->text_cap && v->text) v->text[nt] = c->h_arena[toff + (uint32_t)u];
     }
   }
-  v->n_segs = n;
+  v->n_segs = m;
   v->n_text = nt;
   return MTE_OK;
 }

@@ -1,0 +1,922 @@
+// mte_tree.h — the tree pass: legacy length-calc documents replayed with the
+// reference's B+tree shape.
+//
+// With the legacy length calculation an insert next to tombstones lands where
+// the reference's insertingWalk puts it: at the end of the first leaf block
+// whose perspective length reaches the position (mergeTree.ts:1743,
+// 1788-1797), which depends on the block edges of its B+tree, and those on
+// every split (1800-1840) and on the lazy LRU zamboni (665-675, 681-838).  This
+// pass carries that tree beside the segments.  Its executable spec is
+// oracle/titems.c (checked against the linked-block tree.c and the reference
+// itself); each function below names the titems.c function it restates.
+//
+// Layout: one wavefront per document, the segments register-resident
+// lane-major as in the flat passes (segment i = slot i % E of lane i / E), plus
+// one more plane, the tree word
+//   bits 0-2  h: block levels this item starts (0 inside a leaf block)
+//   bit  3    cont: continues the previous item's leaf (an append-merge)
+//   bits 4-5  ns: needsScour of the leaf block it starts (0 undefined, 1 false, 2 true)
+//   bit  6    po: segment.properties exists
+//   bit  7    empty: placeholder of an empty leaf block (len 0, undefined to all)
+//   bits 8-31 id: the name the LRU heap entries use
+// and the LRU heap (collections/heap.ts) in LDS, 8 B per entry.  Between
+// launches the tree word lives in TreeArgs::tree, the heap in TreeArgs::heap,
+// depth / next id / heap size in DocHdr pad0 / pad1.
+#pragma once
+
+#include "mte_replay.h"
+
+namespace mte {
+
+constexpr int kTreeHeapCap = 255;  // entries per document (+ the unused index 0)
+constexpr uint32_t kHdrTreeEsc = 0x40000000u;  // tree pass: continue in the E = 8 / 16 kernel
+constexpr uint32_t kTH = 0x7u, kTCont = 0x8u, kTNsShift = 4, kTNs = 0x30u, kTPo = 0x40u, kTEmpty = 0x80u;
+constexpr uint32_t kNsUndef = 0, kNsFalse = 1, kNsTrue = 2;
+constexpr int kMaxNodes = 8;       // MaxNodesInBlock, mergeTreeNodes.ts:373
+constexpr int32_t kTextGranularity = 256;  // textSegment.ts:19
+constexpr uint32_t kIdLimit = 1u << 24;
+
+struct TreeArgs {
+  uint32_t* tree;        // tree word of slot x of doc d: tree[d * cap + x]
+  uint2* heap;           // doc d: heap[d * (kTreeHeapCap + 1) + k], k = 1 .. size
+  const uint32_t* docs;  // the legacy documents
+  uint32_t n_docs;
+  const uint16_t* arena; // text (an append-merge looks at the last unit of a leaf)
+};
+
+__device__ __forceinline__ uint32_t t_h(uint32_t t) { return t & kTH; }
+__device__ __forceinline__ uint32_t t_ns(uint32_t t) { return (t & kTNs) >> kTNsShift; }
+__device__ __forceinline__ uint32_t t_id(uint32_t t) { return t >> 8; }
+
+// ---- wave-wide index helpers (E slots per lane, index = lane * E + j) --------
+
+// first index >= lo with pred, or -1
+template <int E>
+__device__ __forceinline__ int first_where(const bool (&p)[E], int lo) {
+  const int base = lane_id() * E;
+  int best = INT32_MAX;
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    const uint64_t m = __ballot(p[j] && base + j >= lo);
+    if (m) {
+      const int c = (__ffsll((long long)m) - 1) * E + j;
+      best = c < best ? c : best;
+    }
+  }
+  return best == INT32_MAX ? -1 : best;
+}
+
+// last index <= hi with pred, or -1
+template <int E>
+__device__ __forceinline__ int last_where(const bool (&p)[E], int hi) {
+  const int base = lane_id() * E;
+  int best = -1;
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    const uint64_t m = __ballot(p[j] && base + j <= hi);
+    if (m) {
+      const int c = (63 - __clzll((long long)m)) * E + j;
+      best = c > best ? c : best;
+    }
+  }
+  return best;
+}
+
+template <int E>
+__device__ __forceinline__ int count_where(const bool (&p)[E], int lo, int hi) {
+  const int base = lane_id() * E;
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < E; j++) c += __popcll(__ballot(p[j] && base + j >= lo && base + j <= hi));
+  return c;
+}
+
+// index of the r-th (0-based) index in [lo, hi] with pred, or -1
+template <int E>
+__device__ __forceinline__ int nth_where(const bool (&p)[E], int lo, int hi, int r) {
+  const int base = lane_id() * E;
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < E; j++) cnt += (p[j] && base + j >= lo && base + j <= hi) ? 1 : 0;
+  const int incl = wave_incl_scan(cnt);
+  const int excl = incl - cnt;
+  const bool mine = excl <= r && r < incl;
+  int at = -1, k = excl;
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    const bool q = p[j] && base + j >= lo && base + j <= hi;
+    if (q && k == r && at < 0) at = base + j;
+    k += q ? 1 : 0;
+  }
+  const uint64_t m = __ballot(mine);
+  if (!m) return -1;
+  return rdlane(at, __ffsll((long long)m) - 1);
+}
+
+// sum of v over [lo, hi)
+template <int E>
+__device__ __forceinline__ int32_t sum_range(const int32_t (&v)[E], int lo, int hi) {
+  const int base = lane_id() * E;
+  int32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < E; j++) s += (base + j >= lo && base + j < hi) ? v[j] : 0;
+  return rdlane(wave_incl_scan(s), kWave - 1);
+}
+
+// ---- per-document tree state ----------------------------------------------------
+
+struct TreeRun {
+  int depth;
+  uint32_t next_id;
+  uint32_t hn;   // LRU heap entries
+  uint2* hp;     // LDS heap of this wave, hp[1 .. hn]
+  const uint16_t* arena;
+};
+
+template <int E, int K>
+struct TReg {
+  Regs<E, K> R;
+  uint32_t T[E];
+};
+
+// open slot g (new[i] = old[i - 1] for i >= g), every plane
+template <int E, int K>
+__device__ __forceinline__ void open_slot(TReg<E, K>& X, int g) {
+  pull_shift<E>(X.R.len, g - 1, INT32_MAX);
+  pull_shift<E>(X.R.seq, g - 1, INT32_MAX);
+  pull_shift<E>(X.R.rseq, g - 1, INT32_MAX);
+  pull_shift<E>(X.R.rmask, g - 1, INT32_MAX);
+  pull_shift<E>(X.R.meta, g - 1, INT32_MAX);
+  pull_shift<E>(X.R.toff, g - 1, INT32_MAX);
+#pragma unroll
+  for (int k = 0; k < K; k++) pull_shift<E>(X.R.pr[k], g - 1, INT32_MAX);
+  pull_shift<E>(X.T, g - 1, INT32_MAX);
+}
+
+// drop the slots without `keep` (stream compaction through LDS)
+template <int E, int K>
+__device__ __forceinline__ int compact_slots(TReg<E, K>& X, const bool (&keep)[E], int n, uint32_t* zlds) {
+  const int base = lane_id() * E;
+  int32_t cnt = 0;
+#pragma unroll
+  for (int j = 0; j < E; j++) cnt += (keep[j] && base + j < n) ? 1 : 0;
+  const int32_t incl = wave_incl_scan(cnt);
+  const int n_new = rdlane(incl, kWave - 1);
+  if (n_new == n) return n;
+  bool kp[E];
+  int32_t dst[E];
+  int32_t d0 = incl - cnt;
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    kp[j] = keep[j] && base + j < n;
+    dst[j] = d0;
+    d0 += kp[j] ? 1 : 0;
+  }
+  compact_plane<E>(X.R.len, kp, dst, zlds);
+  compact_plane<E>(X.R.seq, kp, dst, zlds);
+  compact_plane<E>(X.R.rseq, kp, dst, zlds);
+  compact_plane<E>(X.R.rmask, kp, dst, zlds);
+  compact_plane<E>(X.R.meta, kp, dst, zlds);
+  compact_plane<E>(X.R.toff, kp, dst, zlds);
+#pragma unroll
+  for (int k = 0; k < K; k++) compact_plane<E>(X.R.pr[k], kp, dst, zlds);
+  compact_plane<E>(X.T, kp, dst, zlds);
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    const bool pad = base + j >= n_new;
+    X.R.rseq[j] = pad ? kPad : X.R.rseq[j];
+    X.R.len[j] = pad ? 0 : X.R.len[j];
+    X.T[j] = pad ? 0u : X.T[j];
+  }
+  return n_new;
+}
+
+// block spans: the last index <= i that starts a level-k block, and the last
+// index of that block
+template <int E>
+__device__ __forceinline__ int span_start(const uint32_t (&T)[E], int i, int k) {
+  bool p[E];
+#pragma unroll
+  for (int j = 0; j < E; j++) p[j] = (int)t_h(T[j]) >= k;
+  const int s = last_where<E>(p, i);
+  return s < 0 ? 0 : s;
+}
+template <int E>
+__device__ __forceinline__ int span_end(const uint32_t (&T)[E], int s, int k, int n) {
+  bool p[E];
+#pragma unroll
+  for (int j = 0; j < E; j++) p[j] = (int)t_h(T[j]) >= k;
+  const int e = first_where<E>(p, s + 1);
+  return (e < 0 || e >= n) ? n - 1 : e - 1;
+}
+
+// children of a level-k block: logical leaves (k = 1) or level-(k-1) starts
+template <int E>
+__device__ __forceinline__ void child_pred(const uint32_t (&T)[E], int k, bool (&p)[E]) {
+#pragma unroll
+  for (int j = 0; j < E; j++)
+    p[j] = k == 1 ? (T[j] & (kTCont | kTEmpty)) == 0 : (int)t_h(T[j]) >= k - 1;
+}
+
+template <int E>
+__device__ __forceinline__ void set_h(uint32_t (&T)[E], int i, uint32_t h, bool clear_ns) {
+  const int base = lane_id() * E;
+#pragma unroll
+  for (int j = 0; j < E; j++)
+    if (base + j == i) T[j] = (T[j] & ~(kTH | (clear_ns ? kTNs : 0u))) | h;
+}
+
+template <int E>
+__device__ __forceinline__ void set_ns(uint32_t (&T)[E], int i, uint32_t ns) {
+  const int base = lane_id() * E;
+#pragma unroll
+  for (int j = 0; j < E; j++)
+    if (base + j == i) T[j] = (T[j] & ~kTNs) | (ns << kTNsShift);
+}
+
+// split_cascade (titems.c): a leaf block gained a child at item i
+template <int E>
+__device__ __forceinline__ void split_cascade(uint32_t (&T)[E], int i, int n, TreeRun& tr) {
+  for (int k = 1;; k++) {
+    const int s = span_start<E>(T, i, k), e = span_end<E>(T, s, k, n);
+    bool p[E];
+    child_pred<E>(T, k, p);
+    if (count_where<E>(p, s, e) < kMaxNodes) return;
+    const int z = nth_where<E>(p, s, e, kMaxNodes / 2);
+    set_h<E>(T, z, (uint32_t)k, k == 1);
+    if (k == tr.depth) {  // the root split: a new root above both halves
+      tr.depth++;
+      set_h<E>(T, 0, (uint32_t)tr.depth, false);
+      return;
+    }
+  }
+}
+
+// ---- LRU heap (collections/heap.ts), uniform code over the LDS array ------------
+
+__device__ __forceinline__ void hp_put(uint2* hp, uint32_t k, uint2 v) {
+  if (lane_id() == 0) hp[k] = v;
+  fence_wave();
+}
+__device__ __forceinline__ uint2 hp_get(const uint2* hp, uint32_t k) {
+  const uint2 v = hp[k];
+  return make_uint2(uni(v.x), uni(v.y));
+}
+
+__device__ __forceinline__ int heap_add(TreeRun& tr, int32_t key, uint32_t id) {
+  if (tr.hn >= (uint32_t)kTreeHeapCap) return MTE_E_CAPACITY;
+  uint32_t k = ++tr.hn;
+  hp_put(tr.hp, k, make_uint2((uint32_t)key, id));
+  while (k > 1) {
+    const uint2 par = hp_get(tr.hp, k >> 1);
+    if (!((int32_t)par.x - key > 0)) break;
+    hp_put(tr.hp, k, par);
+    hp_put(tr.hp, k >> 1, make_uint2((uint32_t)key, id));
+    k >>= 1;
+  }
+  return 0;
+}
+
+__device__ __forceinline__ uint2 heap_pop(TreeRun& tr) {
+  const uint2 x = hp_get(tr.hp, 1);
+  const uint2 last = hp_get(tr.hp, tr.hn);
+  hp_put(tr.hp, 1, last);
+  tr.hn--;
+  uint32_t k = 1;
+  while ((k << 1) <= tr.hn) {
+    uint32_t j = k << 1;
+    const uint2 cj = hp_get(tr.hp, j);
+    uint2 c = cj;
+    if (j < tr.hn) {
+      const uint2 cj1 = hp_get(tr.hp, j + 1);
+      if ((int32_t)cj.x - (int32_t)cj1.x > 0) {
+        j++;
+        c = cj1;
+      }
+    }
+    const uint2 cur = hp_get(tr.hp, k);
+    if ((int32_t)cur.x - (int32_t)c.x <= 0) break;
+    hp_put(tr.hp, k, c);
+    hp_put(tr.hp, j, cur);
+    k = j;
+  }
+  return x;
+}
+
+// add_lru (titems.c): addToLRUSet for the leaf headed at item i
+template <int E>
+__device__ __forceinline__ int add_lru(uint32_t (&T)[E], int i, int32_t seq, int32_t cur_seq, TreeRun& tr) {
+  const int bs = span_start<E>(T, i, 1);
+  const uint32_t tb = bcast<E>(T, bs);
+  if (t_ns(tb) != kNsTrue && seq > cur_seq) {
+    set_ns<E>(T, bs, kNsTrue);
+    return heap_add(tr, seq, t_id(bcast<E>(T, i)));
+  }
+  return 0;
+}
+
+// ---- scour / pack (titems.c scour, drop_keep_starts, pack_parent) ----------------
+
+// scourNode over the leaf block [s, e]: sets drop[] on unlinked items and the
+// cont bit on appended leaves; returns the logical leaves held
+template <int E, int K>
+__device__ __forceinline__ int scour(TReg<E, K>& X, int s, int e, int32_t min_seq, bool (&drop)[E], const TreeRun& tr, int n_keys) {
+  const int base = lane_id() * E;
+  bool head[E];
+#pragma unroll
+  for (int j = 0; j < E; j++) head[j] = (X.T[j] & (kTCont | kTEmpty)) == 0;
+  int held = 0;
+  int prev = -1, prev_last = -1;  // head and last item of the leaf appends go to
+  int32_t prev_len = 0;
+  for (int i = first_where<E>(head, s); i >= 0 && i <= e;) {
+    int xe = first_where<E>(head, i + 1);
+    {
+      // a leaf's texts end at the next head or placeholder, or the block end
+      bool stop[E];
+#pragma unroll
+      for (int j = 0; j < E; j++) stop[j] = (X.T[j] & kTCont) == 0;
+      const int st = first_where<E>(stop, i + 1);
+      xe = st < 0 || st > e + 1 ? e + 1 : st;
+    }
+    const int32_t xl = sum_range<E>(X.R.len, i, xe);
+    const int32_t rseq = bcast<E>(X.R.rseq, i), seq = bcast<E>(X.R.seq, i);
+    if (rseq != kNone) {
+      if (rseq > min_seq) {
+        held++;
+      } else {
+#pragma unroll
+        for (int j = 0; j < E; j++) drop[j] = drop[j] || (base + j >= i && base + j < xe);
+      }
+      prev = -1;
+    } else if (seq <= min_seq) {
+      bool app = false;
+      if (prev >= 0) {
+        const uint32_t pm = bcast<E>(X.R.meta, prev), xm = bcast<E>(X.R.meta, i);
+        const uint32_t pt = bcast<E>(X.T, prev), xt = bcast<E>(X.T, i);
+        bool match = ((pt ^ xt) & kTPo) == 0;
+#pragma unroll
+        for (int k = 0; k < K; k++)
+          if (k < n_keys) match = match && bcast<E>(X.R.pr[k], prev) == bcast<E>(X.R.pr[k], i);
+        const bool text = (pm >> 8) == 0 && (xm >> 8) == 0;
+        bool nl = false;
+        if (text) {
+          const int32_t ll = bcast<E>(X.R.len, prev_last);
+          const uint32_t lo = bcast<E>(X.R.toff, prev_last);
+          nl = ll > 0 && tr.arena[lo + (uint32_t)ll - 1] == (uint16_t)'\n';
+        }
+        app = text && !nl && (prev_len <= kTextGranularity || xl <= kTextGranularity) && match && xl > 0;
+      }
+      if (app) {
+        // TextSegment.append: the leaf becomes texts of the previous one
+#pragma unroll
+        for (int j = 0; j < E; j++)
+          if (base + j == i) X.T[j] = (X.T[j] & 0xffu & ~kTNs) | kTCont;
+        prev_len += xl;
+        prev_last = xe - 1;
+      } else {
+        held++;
+        if (xl > 0) {
+          prev = i;
+          prev_len = xl;
+          prev_last = xe - 1;
+        } else {
+          prev = -1;
+        }
+      }
+    } else {
+      held++;
+      prev = -1;
+    }
+    i = xe <= e ? first_where<E>(head, xe) : -1;
+  }
+  return held;
+}
+
+// titems.c drop_keep_starts over one leaf block [bs, be], then the compaction
+template <int E, int K>
+__device__ __forceinline__ int drop_block(TReg<E, K>& X, int bs, int be, bool (&drop)[E], int n, uint32_t* zlds) {
+  const int base = lane_id() * E;
+  const int j0 = [&] {
+    bool keep[E];
+#pragma unroll
+    for (int j = 0; j < E; j++) keep[j] = !drop[j];
+    return first_where<E>(keep, bs);
+  }();
+  const uint32_t tbs = bcast<E>(X.T, bs);
+  if (j0 < 0 || j0 > be) {
+    // the block lost every leaf: keep a placeholder
+#pragma unroll
+    for (int j = 0; j < E; j++)
+      if (base + j == bs) {
+        drop[j] = false;
+        X.R.len[j] = 0;
+        X.R.rseq[j] = kPad;
+        X.R.rmask[j] = 0;
+        X.R.meta[j] = 0;
+        X.T[j] = (tbs & (kTH | kTNs)) | kTEmpty;
+      }
+  } else if (j0 != bs) {
+#pragma unroll
+    for (int j = 0; j < E; j++)
+      if (base + j == j0) X.T[j] = (X.T[j] & ~(kTH | kTNs)) | (tbs & (kTH | kTNs));
+  }
+  bool keep[E];
+#pragma unroll
+  for (int j = 0; j < E; j++) keep[j] = !drop[j];
+  return compact_slots<E, K>(X, keep, n, zlds);
+}
+
+// group starts of re-packed children: rank r starts a group of the
+// base + 1 / base split (packParent, mergeTree.ts:764-786)
+__device__ __forceinline__ bool group_start(int r, int base, int rem) {
+  const int big = rem * (base + 1);
+  if (r < big) return r % (base + 1) == 0;
+  return (r - big) % base == 0;
+}
+
+// packParent of the level-p block starting at s (titems.c pack_parent)
+template <int E, int K>
+__device__ __forceinline__ int pack_parent(TReg<E, K>& X, int s, int p, int n, int32_t min_seq, TreeRun& tr, uint32_t* zlds,
+                           int n_keys, int& status) {
+  const int base = lane_id() * E;
+  for (;;) {
+    int e = span_end<E>(X.T, s, p, n);
+    const uint32_t top = t_h(bcast<E>(X.T, s));
+    if (p == 2) {
+      bool drop[E];
+#pragma unroll
+      for (int j = 0; j < E; j++) drop[j] = false;
+      for (int b = s; b <= e;) {
+        const int be = span_end<E>(X.T, b, 1, n);
+        scour<E, K>(X, b, be, min_seq, drop, tr, n_keys);
+        b = be + 1;
+      }
+      // held leaves (placeholders go too), re-packed
+      bool keep[E];
+#pragma unroll
+      for (int j = 0; j < E; j++) {
+        const int i = base + j;
+        keep[j] = !(i >= s && i <= e && (drop[j] || (X.T[j] & kTEmpty)));
+        if (i >= s && i <= e) X.T[j] &= ~kTH;
+      }
+      const int n0 = n;
+      n = compact_slots<E, K>(X, keep, n, zlds);
+      e -= n0 - n;
+      if (e < s) {
+        // no leaf left: one empty leaf block
+        if (n + 2 > E * kWave) {
+          status = MTE_E_CAPACITY;
+          return n;
+        }
+        open_slot<E, K>(X, s);
+#pragma unroll
+        for (int j = 0; j < E; j++)
+          if (base + j == s) {
+            X.R.len[j] = 0;
+            X.R.rseq[j] = kPad;
+            X.R.rmask[j] = 0;
+            X.R.meta[j] = 0;
+            X.T[j] = top | kTEmpty;
+          }
+        n++;
+      } else {
+        bool hd[E];
+#pragma unroll
+        for (int j = 0; j < E; j++) hd[j] = (X.T[j] & kTCont) == 0;
+        const int total = count_where<E>(hd, s, e);
+        int cc = total / (kMaxNodes / 2) < kMaxNodes - 1 ? total / (kMaxNodes / 2) : kMaxNodes - 1;
+        if (cc < 1) cc = 1;
+        const int gb = total / cc, rem = total % cc;
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < E; j++) cnt += (hd[j] && base + j >= s && base + j <= e) ? 1 : 0;
+        const int incl = wave_incl_scan(cnt);
+        int r = incl - cnt;
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+          const int i = base + j;
+          if (hd[j] && i >= s && i <= e) {
+            if (group_start(r, gb, rem)) X.T[j] = (X.T[j] & ~(kTH | kTNs)) | (r == 0 ? top : 1u);
+            r++;
+          }
+        }
+      }
+    } else {
+      // level p >= 3: the level-(p-2) blocks regrouped under new level-(p-1) blocks
+      bool ch[E];
+#pragma unroll
+      for (int j = 0; j < E; j++) ch[j] = (int)t_h(X.T[j]) >= p - 2;
+      const int total = count_where<E>(ch, s, e);
+      int cc = total / (kMaxNodes / 2) < kMaxNodes - 1 ? total / (kMaxNodes / 2) : kMaxNodes - 1;
+      if (cc < 1) cc = 1;
+      const int gb = total / cc, rem = total % cc;
+      int cnt = 0;
+#pragma unroll
+      for (int j = 0; j < E; j++) cnt += (ch[j] && base + j >= s && base + j <= e) ? 1 : 0;
+      const int incl = wave_incl_scan(cnt);
+      int r = incl - cnt;
+#pragma unroll
+      for (int j = 0; j < E; j++) {
+        const int i = base + j;
+        if (ch[j] && i >= s && i <= e) {
+          const uint32_t h = group_start(r, gb, rem) ? (r == 0 ? top : (uint32_t)(p - 1)) : (uint32_t)(p - 2);
+          X.T[j] = (X.T[j] & ~kTH) | h;
+          r++;
+        }
+      }
+    }
+    // the parent's own children: an underflow re-packs its parent too
+    if (p >= tr.depth) return n;
+    bool ch[E];
+    child_pred<E>(X.T, p, ch);
+    const int cc = count_where<E>(ch, s, span_end<E>(X.T, s, p, n));
+    if (cc >= kMaxNodes / 2) return n;
+    s = span_start<E>(X.T, s, p + 1);
+    p++;
+  }
+}
+
+// zamboniSegments (titems.c zamboni): at most two scours
+template <int E, int K>
+__device__ __forceinline__ int zamboni(TReg<E, K>& X, int n, int32_t min_seq, TreeRun& tr, uint32_t* zlds, int n_keys,
+                       int& status) {
+  for (int z = 0; z < 2; z++) {
+    if (tr.hn == 0) break;
+    const uint2 top = hp_get(tr.hp, 1);
+    if ((int32_t)top.x > min_seq) break;
+    const uint2 ent = heap_pop(tr);
+    bool hit[E];
+    const int base = lane_id() * E;
+#pragma unroll
+    for (int j = 0; j < E; j++) hit[j] = base + j < n && t_id(X.T[j]) == ent.y && (X.T[j] & (kTCont | kTEmpty)) == 0;
+    const int i = first_where<E>(hit, 0);
+    if (i < 0) continue;  // unlinked
+    const int bs = span_start<E>(X.T, i, 1), be = span_end<E>(X.T, bs, 1, n);
+    if (t_ns(bcast<E>(X.T, bs)) == kNsFalse) continue;
+    bool ch[E];
+    child_pred<E>(X.T, 1, ch);
+    const int before = count_where<E>(ch, bs, be);
+    bool drop[E];
+#pragma unroll
+    for (int j = 0; j < E; j++) drop[j] = false;
+    const int held = scour<E, K>(X, bs, be, min_seq, drop, tr, n_keys);
+    set_ns<E>(X.T, bs, kNsFalse);
+    if (held < before) {
+      n = drop_block<E, K>(X, bs, be, drop, n, zlds);
+      if (held < kMaxNodes / 2 && tr.depth >= 2)
+        n = pack_parent<E, K>(X, span_start<E>(X.T, bs, 2), 2, n, min_seq, tr, zlds, n_keys, status);
+      if (status) return n;
+    }
+  }
+  return n;
+}
+
+// ensureIntervalBoundary (titems.c boundary); returns the new item count
+template <int E, int K, bool S>
+__device__ __forceinline__ int tree_boundary(TReg<E, K>& X, const int32_t (&L)[E], const int32_t (&P)[E], int32_t pos, int n,
+                             TreeRun& tr, uint32_t (&st)[kNumStats], bool& changed) {
+  int32_t off = 0;
+  const int xs = find_split<E>(L, P, pos, &off);
+  const int base = lane_id() * E;
+  if (xs >= 0) {
+    const int32_t len = bcast<E>(X.R.len, xs);
+    open_slot<E, K>(X, xs + 1);
+    const uint32_t id = tr.next_id++;
+#pragma unroll
+    for (int j = 0; j < E; j++) {
+      const int i = base + j;
+      if (i == xs) X.R.len[j] = off;
+      if (i == xs + 1) {
+        X.R.len[j] = len - off;
+        X.R.toff[j] += (uint32_t)off;
+        X.T[j] = (X.T[j] & kTPo) | (id << 8);
+      }
+    }
+    n++;
+    MTE_STAT(st[kStWritten] += 2;)
+    split_cascade<E>(X.T, xs + 1, n, tr);
+    changed = true;
+    return n;
+  }
+  // between two texts of one merged leaf
+  bool c[E];
+#pragma unroll
+  for (int j = 0; j < E; j++) c[j] = (X.T[j] & kTCont) && L[j] > 0 && P[j] == pos;
+  const int ic = first_where<E>(c, 0);
+  if (ic >= 0) {
+    const uint32_t id = tr.next_id++;
+#pragma unroll
+    for (int j = 0; j < E; j++)
+      if (base + j == ic) X.T[j] = (X.T[j] & (kTPo)) | (id << 8);
+    MTE_STAT(st[kStWritten] += 1;)
+    split_cascade<E>(X.T, ic, n, tr);
+    changed = true;
+  }
+  return n;
+}
+
+// One op record of a legacy document (titems.c doc_apply).  Returns 0, 1 (the
+// document needs the next register tier) or a negative MTE_E_*.
+template <int E, int K, bool S>
+__device__ __forceinline__ int tree_step(TReg<E, K>& X, DocRun& D, TreeRun& tr, uint32_t (&st)[kNumStats], s8v& cur,
+                         const ReplayArgs& a, uint32_t* zlds) {
+  const int base = lane_id() * E;
+  const int lim = kWave * E < (int)a.cap ? kWave * E : (int)a.cap;
+  if (D.n + 4 > lim) return 1;
+  if (tr.next_id + 4 >= kIdLimit) return MTE_E_CAPACITY;
+  const s8v op = cur;
+  const uint4* rec = D.recp + 2 * D.k;
+  // (the flat passes order this prefetch behind `op` with an empty asm on
+  // SGPR operands; the tree pass's scalar state is too large for that)
+  cur = sload8(rec + 2);
+  const uint32_t w3 = (uint32_t)op[3];
+  const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
+  if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
+  MTE_STAT(st[kStOps]++;)
+  MTE_STAT(st[kStMaxSegs] = (uint32_t)D.n > st[kStMaxSegs] ? (uint32_t)D.n : st[kStMaxSegs];)
+  const int32_t s = op[0], r = op[1], msn = op[2];
+  const int32_t pos1 = op[4], pos2 = op[5];
+  int n = D.n;
+  int status = 0;
+  const bool newcalc = (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
+
+  if (type == MTE_OP_INSERT || type == MTE_OP_REMOVE || type == MTE_OP_ANNOTATE) {
+    MTE_STAT(st[kStScanned] += (uint32_t)n;)
+    int32_t L[E], P[E];
+    leaf_lengths<E, K>(X.R, r, c + 1, (int)c, D.min_seq, newcalc, L);
+    int32_t total = prefix<E>(L, P);
+    bool changed = false;
+    n = tree_boundary<E, K, S>(X, L, P, pos1, n, tr, st, changed);
+    if (type != MTE_OP_INSERT) {
+      if (changed) {
+        leaf_lengths<E, K>(X.R, r, c + 1, (int)c, D.min_seq, newcalc, L);
+        total = prefix<E>(L, P);
+        changed = false;
+      }
+      n = tree_boundary<E, K, S>(X, L, P, pos2, n, tr, st, changed);
+    }
+    if (changed) {
+      leaf_lengths<E, K>(X.R, r, c + 1, (int)c, D.min_seq, newcalc, L);
+      total = prefix<E>(L, P);
+    }
+    if (type == MTE_OP_INSERT) {
+      const bool marker = (flags & MTE_F_MARKER) != 0;
+      const int32_t nlen = marker ? 1 : pos2;
+      if (nlen > 0) {
+        // the leaf block insertingWalk enters: the first whose end reaches pos
+        bool q[E];
+#pragma unroll
+        for (int j = 0; j < E; j++) q[j] = base + j < n && P[j] + (L[j] > 0 ? L[j] : 0) >= pos1;
+        const int ks = first_where<E>(q, 0);
+        if (ks < 0 || pos1 > total) return MTE_E_INSERT_FAILED;  // mergeTree.ts:1666-1672
+        const int bs = span_start<E>(X.T, ks, 1), be = span_end<E>(X.T, bs, 1, n);
+        const uint32_t tbs = bcast<E>(X.T, bs);
+        int slot;
+        bool replace = false;
+        if (tbs & kTEmpty) {
+          slot = bs;
+          replace = true;
+        } else {
+          bool f[E];
+#pragma unroll
+          for (int j = 0; j < E; j++) f[j] = L[j] >= 0 && P[j] >= pos1 && !(X.T[j] & kTEmpty);
+          slot = first_where<E>(f, ks);
+          if (slot < 0 || slot > be) slot = be + 1;
+        }
+        // the new segment (mergeTree.ts:1599-1611, textSegment.ts:40-48, mergeTreeNodes.ts:602-609)
+        const uint32_t meta = (c + 1u) | (marker ? (1u + (uint32_t)pos2) << 8 : 0u);
+        const uint32_t toff = marker ? 0u : a.text_base + (uint32_t)op[6];
+        const uint32_t psi = (uint32_t)op[7];
+        uint32_t pr[K > 0 ? K : 1][1];
+        const bool one[1] = {true};
+#pragma unroll
+        for (int kk = 0; kk < (K > 0 ? K : 1); kk++) pr[kk][0] = 0;
+        if (K > 0 && psi != MTE_NO_PROPS) {
+          const s8v q2 = sload_props(a, psi);
+          apply_props<1, K>(pr, one, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], psi, a);
+          MTE_STAT(st[kStPwrites] += (uint32_t)q2[3];)
+        }
+        MTE_STAT(if (!marker) st[kStUnits] += (uint32_t)pos2;)
+        MTE_STAT(st[kStWritten] += 1;)
+        const uint32_t id = tr.next_id++;
+        uint32_t tw = (id << 8) | (psi != MTE_NO_PROPS ? kTPo : 0u);
+        if (replace) {
+          tw |= tbs & (kTH | kTNs);
+        } else {
+          open_slot<E, K>(X, slot);
+          n++;
+          if (slot == bs) {  // the new leaf becomes the block's first child
+            tw |= tbs & (kTH | kTNs);
+#pragma unroll
+            for (int j = 0; j < E; j++)
+              if (base + j == slot + 1) X.T[j] &= ~(kTH | kTNs);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+          if (base + j != slot) continue;
+          X.R.len[j] = nlen;
+          X.R.seq[j] = s;
+          X.R.rseq[j] = kNone;
+          X.R.rmask[j] = 0;
+          X.R.meta[j] = meta;
+          X.R.toff[j] = toff;
+#pragma unroll
+          for (int kk = 0; kk < K; kk++) X.R.pr[kk][j] = pr[kk][0];
+          X.T[j] = tw;
+        }
+        if (!replace) split_cascade<E>(X.T, slot, n, tr);
+        const int rc = add_lru<E>(X.T, slot, s, D.cur_seq, tr);
+        if (rc) return rc;
+      }
+    } else if (pos2 != pos1) {
+      // nodeMap over [start, end) (mergeTree.ts:2274-2330)
+      bool in[E];
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int j = 0; j < E; j++) {
+        in[j] = L[j] > 0 && P[j] >= pos1 && P[j] < pos2;
+        cnt += (uint32_t)__popcll(__ballot(in[j]));
+      }
+      MTE_STAT(st[kStWritten] += cnt;)
+      if (type == MTE_OP_REMOVE) {
+        const uint32_t bit = 1u << c;
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+          X.R.rseq[j] = (in[j] && X.R.rseq[j] == kNone) ? s : X.R.rseq[j];
+          X.R.rmask[j] = in[j] ? (X.R.rmask[j] | bit) : X.R.rmask[j];
+        }
+      } else if (cnt > 0) {
+        const uint32_t psi = (uint32_t)op[6];
+        const s8v q2 = sload_props(a, psi);
+        if (flags & MTE_F_REWRITE) {
+#pragma unroll
+          for (int kk = 0; kk < K; kk++)
+#pragma unroll
+            for (int j = 0; j < E; j++) X.R.pr[kk][j] = in[j] ? 0u : X.R.pr[kk][j];
+        }
+        apply_props<E, K>(X.R.pr, in, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], psi, a);
+#pragma unroll
+        for (int j = 0; j < E; j++) X.T[j] |= in[j] ? kTPo : 0u;
+        MTE_STAT(st[kStPwrites] += cnt * (uint32_t)q2[3];)
+      }
+      // addToLRUSet for every touched leaf: the first one of each leaf block
+      bool th[E];
+#pragma unroll
+      for (int j = 0; j < E; j++) th[j] = in[j] && (X.T[j] & kTCont) == 0;
+      for (int i = first_where<E>(th, 0); i >= 0;) {
+        const int rc = add_lru<E>(X.T, i, s, D.cur_seq, tr);
+        if (rc) return rc;
+        const int be = span_end<E>(X.T, span_start<E>(X.T, i, 1), 1, n);
+        i = first_where<E>(th, be + 1);
+      }
+    }
+    n = zamboni<E, K>(X, n, D.min_seq, tr, zlds, a.n_keys, status);
+    if (status) return status;
+  } else if (type != MTE_OP_NOOP) {
+    return MTE_E_INVALID_ARG;
+  }
+  D.n = n;
+  D.k++;
+  const bool live = type != MTE_OP_NOOP, end = (flags & MTE_F_MSG_END) != 0;
+  const bool bad = (live & (s <= D.cur_seq)) | (end & (s < D.cur_seq)) | ((live | end) & (msn < D.min_seq)) |
+                   (end & (msn > s));
+  if (bad) return window_error(D, live, end, s, msn);
+  if (end) {
+    D.cur_seq = s;
+    if (msn > D.min_seq) {
+      D.min_seq = msn;
+      D.n = zamboni<E, K>(X, D.n, D.min_seq, tr, zlds, a.n_keys, status);
+      if (status) return status;
+    }
+  }
+  return 0;
+}
+
+template <int E, int K>
+__device__ __forceinline__ void tree_load(TReg<E, K>& X, const DocRun& D, const ReplayArgs& a, const TreeArgs& t) {
+  load_regs<E, K>(X.R, D, a);
+  const uint32_t* tp = t.tree + (uint64_t)D.doc * a.cap;
+  const int base = lane_id() * E;
+#pragma unroll
+  for (int j = 0; j < E; j++) X.T[j] = base + j < D.n ? tp[base + j] : 0u;
+}
+
+template <int E, int K>
+__device__ __forceinline__ void tree_store(const TReg<E, K>& X, const DocRun& D, const ReplayArgs& a,
+                                           const TreeArgs& t) {
+  store_regs<E, K>(X.R, D, a);
+  uint32_t* tp = t.tree + (uint64_t)D.doc * a.cap;
+  const int base = lane_id() * E;
+#pragma unroll
+  for (int j = 0; j < E; j++)
+    if (base + j < D.n) tp[base + j] = X.T[j];
+}
+
+// one run of a legacy document at tier E: until it ends, stops or needs
+// another tier
+template <int E, int K, bool S>
+__device__ __forceinline__ void tree_burst(DocRun& D, TreeRun& tr, const ReplayArgs& a, const TreeArgs& t, uint32_t* zlds,
+                           int emin) {
+  TReg<E, K> X;
+  uint32_t st[kNumStats] = {};
+  tree_load<E, K>(X, D, a, t);
+  s8v cur = sload8(D.recp + 2 * D.k);
+  for (;;) {
+    const int rc = tree_step<E, K, S>(X, D, tr, st, cur, a, zlds);
+    if (rc < 0) {
+      D.status = rc;
+      D.running = false;
+      break;
+    }
+    if (rc > 0) break;  // needs the next tier
+    if (D.k >= D.k1) {
+      D.running = false;
+      break;
+    }
+    if (E > emin && D.n + 4 + 16 <= 32 * E) break;  // fits the tier below
+    if constexpr (S) {
+      if (st[kStOps] >= (1u << 20)) {
+        run_flush_stats(D, st, a);
+      }
+    }
+  }
+  swait(cur);
+  tree_store<E, K>(X, D, a, t);
+  if constexpr (S) run_flush_stats(D, st, a);
+}
+
+// The tree pass.  BIG = false: tiers E = 1, 2, 4 (documents up to 252 items);
+// a document that outgrows them is flagged kHdrTreeEsc and continues in the
+// BIG = true launch (E = 8, 16; up to 1,020 items).
+template <int K, bool S, bool BIG>
+__global__ __launch_bounds__(256) void tree_kernel(ReplayArgs a, TreeArgs t) {
+  constexpr int EMAX = BIG ? 16 : 4;
+  __shared__ uint32_t zlds_all[kDocsPerBlock][kWave * EMAX];
+  __shared__ uint2 heap_all[kDocsPerBlock][kTreeHeapCap + 1];
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+  const int idx = (int)blockIdx.x * kDocsPerBlock + w;
+  if (idx >= (int)t.n_docs) return;
+  const int doc = uni((int)t.docs[idx]);
+  const uint4 h0 = reinterpret_cast<const uint4*>(a.hdr + doc)[0], h1 = reinterpret_cast<const uint4*>(a.hdr + doc)[1];
+  const uint32_t hflags = uni(h1.x);
+  if (BIG && !(hflags & kHdrTreeEsc)) return;
+  DocRun D;
+  D.doc = doc;
+  D.n = uni((int32_t)h0.x);
+  D.min_seq = uni((int32_t)h0.y);
+  D.cur_seq = uni((int32_t)h0.z);
+  D.status = uni((int32_t)h0.w);
+  D.flags = hflags & ~kHdrTreeEsc;
+  D.k = uni(h1.y);
+  const uint64_t kb = uni64(a.op_off[doc]);
+  D.recp = a.recs + 2 * kb;
+  D.k1 = (uint32_t)(uni64(a.op_off[doc + 1]) - kb);
+  D.running = D.status == 0 && D.k < D.k1;
+  if (!D.running) return;
+  TreeRun tr;
+  tr.depth = (int)uni(h1.w & 0xffu);
+  tr.hn = uni(h1.w >> 8);
+  tr.next_id = uni(h1.z);
+  tr.hp = heap_all[w];
+  tr.arena = t.arena;
+  const uint2* hg = t.heap + (uint64_t)doc * (kTreeHeapCap + 1);
+  for (uint32_t k = (uint32_t)lane_id(); k <= tr.hn; k += kWave) tr.hp[k] = hg[k];
+  fence_wave();
+  uint32_t* zlds = zlds_all[w];
+  while (D.running) {
+    const int n = D.n;
+    if (n + 4 > (int)a.cap || n + 4 > 16 * kWave) {
+      D.status = MTE_E_CAPACITY;
+      break;
+    }
+    if (!BIG) {
+      if (n + 4 <= kWave) tree_burst<1, K, S>(D, tr, a, t, zlds, 1);
+      else if (n + 4 <= 2 * kWave) tree_burst<2, K, S>(D, tr, a, t, zlds, 1);
+      else if (n + 4 <= 4 * kWave) tree_burst<4, K, S>(D, tr, a, t, zlds, 1);
+      else {
+        D.flags |= kHdrTreeEsc;
+        break;
+      }
+    } else {
+      if (n + 4 <= 8 * kWave) tree_burst<8, K, S>(D, tr, a, t, zlds, 8);
+      else tree_burst<16, K, S>(D, tr, a, t, zlds, 8);
+    }
+  }
+  uint2* hw = t.heap + (uint64_t)doc * (kTreeHeapCap + 1);
+  for (uint32_t k = (uint32_t)lane_id(); k <= tr.hn; k += kWave) hw[k] = tr.hp[k];
+  if (lane_id() == 0) {
+    DocHdr o;
+    o.nseg = D.n;
+    o.min_seq = D.min_seq;
+    o.cur_seq = D.cur_seq;
+    o.status = D.status;
+    o.flags = D.flags;
+    o.resume = D.k;
+    o.pad0 = tr.next_id;
+    o.pad1 = (uint32_t)tr.depth | (tr.hn << 8);
+    a.hdr[doc] = o;
+  }
+}
+
+}  // namespace mte

@@ -39,8 +39,10 @@ PRESETS = {
             mix=MIX_INSERT | MIX_REMOVE | MIX_ANNOTATE, marker_every=16, length_mode=0),
     4: dict(n_docs=100000, ops_per_doc=500, clients=8, min_length=8, round_ops=8,
             mix=MIX_INSERT | MIX_REMOVE | MIX_ANNOTATE, marker_every=16, length_mode=0),
+    # config 5 runs the new length calculation: its documents are far beyond
+    # the tree pass that legacy documents need (<= 1,020 items)
     5: dict(n_docs=64, ops_per_doc=262144, clients=8, min_length=16, round_ops=65536,
-            mix=MIX_INSERT | MIX_REMOVE | MIX_ANNOTATE, marker_every=16, length_mode=0,
+            mix=MIX_INSERT | MIX_REMOVE | MIX_ANNOTATE, marker_every=16, length_mode=2,
             init_segs=1 << 20, max_range=16),
 }
 

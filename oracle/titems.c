@@ -65,11 +65,14 @@ typedef struct {
   int32_t* L;
   int64_t* P;
   uint32_t scap;
+  /* the GPU tree pass's statistics (mte_stats), counted the same way */
+  uint64_t ops, scanned, written, pwrites, units, max_segs;
   mte_doc_init init;
 } __attribute__((aligned(128))) idoc;
 
 struct oti_ctx {
   uint32_t n_keys, n_docs;
+  uint32_t limit; /* items + 4 of headroom a document may reach (the GPU tree pass: min(1024, cap)) */
   idoc* docs;
   uint16_t* arena;
   uint64_t arena_n, arena_cap, load_units;
@@ -84,6 +87,7 @@ typedef struct {
   uint64_t text_base;
   uint32_t n_keys;
   const uint16_t* arena;
+  uint32_t limit;
 } env_t;
 
 /* ---- storage --------------------------------------------------------------- */
@@ -448,6 +452,7 @@ static int boundary(idoc* d, int64_t pos) {
     if (l <= 0) continue;
     if (pos < d->P[i]) return MTE_OK;
     if (pos == d->P[i] && d->it[i].cont) { /* between two texts of one merged leaf */
+      d->written += 1;
       d->it[i].cont = 0;
       d->it[i].id = new_id(d);
       split_cascade(d, i);
@@ -467,6 +472,7 @@ static int boundary(idoc* d, int64_t pos) {
       tl->h = 0;
       tl->cont = 0;
       tl->id = new_id(d);
+      d->written += 2;
       hd->len = off;
       d->L[i] = off;
       d->L[i + 1] = tl->len;
@@ -491,7 +497,11 @@ static int doc_apply(idoc* d, const mte_op* op, const env_t* env) {
   const int32_t r = op->ref_seq, s = op->seq, m = d->min_seq;
   const int c = op->client;
   int rc;
+  if (d->n + 4 > env->limit) return MTE_E_CAPACITY;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
+  d->ops++;
+  if (d->n > d->max_segs) d->max_segs = d->n;
+  if (op->type != MTE_OP_NOOP) d->scanned += d->n;
   if (op->type == MTE_OP_INSERT) {
     if ((rc = reserve(d, d->n + 3))) return rc;
     lengths(d, r, c, m, newcalc);
@@ -530,14 +540,16 @@ static int doc_apply(idoc* d, const mte_op* op, const env_t* env) {
       nw.cli = c;
       nw.rseq = NONE_SEQ;
       nw.id = new_id(d);
+      d->written += 1;
       if (is_marker) {
         nw.kind = 1u + (uint32_t)op->pos2;
       } else {
         nw.toff = (uint32_t)(env->text_base + op->a);
+        d->units += (uint64_t)len;
       }
       if (op->b != MTE_NO_PROPS) {
         nw.po = 1;
-        orc_apply_props(nw.props, env->n_keys, &env->b->propsets[op->b], env->b->props, 0);
+        d->pwrites += orc_apply_props(nw.props, env->n_keys, &env->b->propsets[op->b], env->b->props, 0);
       }
       if (replace) {
         nw.h = d->it[slot].h;
@@ -572,6 +584,7 @@ static int doc_apply(idoc* d, const mte_op* op, const env_t* env) {
         if (d->P[i] >= end) break;
         if (d->P[i] + l <= start) continue;
         item* g = &d->it[i];
+        d->written += 1;
         if (op->type == MTE_OP_REMOVE) {
           if (g->rseq == NONE_SEQ) {
             g->rseq = s;
@@ -581,8 +594,8 @@ static int doc_apply(idoc* d, const mte_op* op, const env_t* env) {
           }
         } else {
           g->po = 1;
-          orc_apply_props(g->props, env->n_keys, &env->b->propsets[op->a], env->b->props,
-                          (op->flags & MTE_F_REWRITE) != 0);
+          d->pwrites += orc_apply_props(g->props, env->n_keys, &env->b->propsets[op->a], env->b->props,
+                                        (op->flags & MTE_F_REWRITE) != 0);
         }
         if (!g->cont && (rc = add_lru(d, i, s))) return rc;
       }
@@ -627,6 +640,7 @@ int oti_create(uint32_t n_keys, oti_ctx** out) {
   oti_ctx* c = (oti_ctx*)calloc(1, sizeof(oti_ctx));
   if (!c) return MTE_E_OOM;
   c->n_keys = n_keys;
+  c->limit = 1024;
   *out = c;
   return MTE_OK;
 }
@@ -771,7 +785,7 @@ typedef struct {
 
 static void* worker(void* p) {
   worker_arg* w = (worker_arg*)p;
-  env_t env = {w->b, w->base, w->c->n_keys, w->c->arena};
+  env_t env = {w->b, w->base, w->c->n_keys, w->c->arena, w->c->limit};
   for (uint32_t di = w->d0; di < w->d1; di += w->stride) {
     idoc* d = &w->c->docs[di];
     if (d->status) continue;
@@ -792,6 +806,10 @@ int oti_apply_batch(oti_ctx* c, const mte_batch* b, int n_threads) {
   uint64_t base = 0;
   int rc = arena_append(c, b->text, b->text_units, &base);
   if (rc) return rc;
+  for (uint32_t i = 0; i < c->n_docs; i++) {
+    idoc* d = &c->docs[i];
+    d->ops = d->scanned = d->written = d->pwrites = d->units = d->max_segs = 0;
+  }
   if (n_threads < 1) n_threads = 1;
   if ((uint32_t)n_threads > c->n_docs) n_threads = c->n_docs ? (int)c->n_docs : 1;
   worker_arg* args = (worker_arg*)calloc((size_t)n_threads, sizeof(worker_arg));
@@ -910,4 +928,64 @@ int oti_doc_shape(oti_ctx* c, uint32_t doc, char* buf, uint32_t cap) {
   buf[k] = 0;
 #undef PUT
   return (int)d->hn;
+}
+
+int oti_stats_get(oti_ctx* c, mte_stats* o) {
+  if (!c || !o) return MTE_E_INVALID_ARG;
+  memset(o, 0, sizeof(*o));
+  for (uint32_t i = 0; i < c->n_docs; i++) {
+    const idoc* d = &c->docs[i];
+    o->ops_applied += d->ops;
+    o->segs_scanned += d->scanned;
+    o->segs_written += d->written;
+    o->prop_writes += d->pwrites;
+    o->units_inserted += d->units;
+    if (d->max_segs > o->max_segs) o->max_segs = d->max_segs;
+  }
+  o->algo_bytes = 32.0 * (double)o->ops_applied + 20.0 * (double)o->segs_scanned +
+                  20.0 * (double)o->segs_written + 4.0 * (double)o->prop_writes +
+                  2.0 * (double)o->units_inserted;
+  return MTE_OK;
+}
+
+/* every item a document holds, placeholders skipped and merged leaves joined
+ * (as mte_read_segments) */
+int oti_read_segments(oti_ctx* c, uint32_t doc, mte_seg_list* v) {
+  if (!c || !v || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  const idoc* d = &c->docs[doc];
+  uint64_t nt = 0, m = 0;
+  for (uint32_t i = 0; i < d->n; i++) {
+    const item* g = &d->it[i];
+    if (g->empty) continue;
+    if (g->cont && m > 0) {
+      if (m - 1 < v->seg_cap && v->segs) v->segs[m - 1].len += (uint32_t)g->len;
+    } else {
+      const uint64_t io = m++;
+      if (io < v->seg_cap && v->segs) {
+        mte_seg* s = &v->segs[io];
+        s->text_off = g->kind == 0 ? (uint32_t)nt : 0u;
+        s->len = (uint32_t)g->len;
+        s->seq = g->seq;
+        s->removed_seq = g->rseq == NONE_SEQ ? MTE_NOT_REMOVED : g->rseq;
+        s->removers = g->rseq == NONE_SEQ ? 0u : g->rmask;
+        s->client = g->cli;
+        s->kind = g->kind;
+        s->propset = MTE_NO_PROPS;
+        if (v->props)
+          for (uint32_t k = 0; k < c->n_keys; k++) v->props[(size_t)io * c->n_keys + k] = g->props[k];
+      }
+    }
+    if (g->kind == 0)
+      for (int32_t u = 0; u < g->len; u++, nt++)
+        if (nt < v->text_cap && v->text) v->text[nt] = c->arena[g->toff + (uint32_t)u];
+  }
+  v->n_segs = m;
+  v->n_text = nt;
+  return MTE_OK;
+}
+
+int oti_set_limit(oti_ctx* c, uint32_t limit) {
+  if (!c || limit < 8) return MTE_E_INVALID_ARG;
+  c->limit = limit;
+  return MTE_OK;
 }

@@ -26,6 +26,10 @@ int oti_digest(oti_ctx* c, uint64_t* out, uint32_t n_docs);
 int oti_doc_status(oti_ctx* c, int32_t* out, uint32_t n_docs);
 int oti_doc_nsegs(oti_ctx* c, uint32_t doc, uint32_t* out);
 int oti_doc_shape(oti_ctx* c, uint32_t doc, char* buf, uint32_t cap);
+int oti_stats_get(oti_ctx* c, mte_stats* out);
+/* a document stops with MTE_E_CAPACITY once items + 4 > limit (default 1024) */
+int oti_set_limit(oti_ctx* c, uint32_t limit);
+int oti_read_segments(oti_ctx* c, uint32_t doc, mte_seg_list* v);
 
 #ifdef __cplusplus
 }

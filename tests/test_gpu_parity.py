@@ -10,7 +10,7 @@ from scenarios import PROPS_AT, SCENARIOS, expected_of, props_at, run_scenario
 from fluidframework_amd import gen
 from fluidframework_amd.abi import MTE_E_CAPACITY
 from fluidframework_amd.engine import DeviceEngine
-from oracle import OracleEngine
+from oracle import OracleEngine, SpecOracle
 
 pytestmark = pytest.mark.gpu
 
@@ -18,8 +18,10 @@ STAT_KEYS = ["ops_applied", "segs_scanned", "segs_written", "prop_writes", "unit
 
 
 def replay_both(stream, threads=8):
+    """The engine and its specification (SpecOracle: the flat restatement for
+    new length-calc documents, the tree for legacy ones) on one stream."""
     n_keys = stream["n_keys"]
-    o = OracleEngine(n_keys, threads=threads)
+    o = SpecOracle(n_keys, threads=threads)
     o.load_docs(stream["inits"], stream["init_text"])
     o.apply_batch(stream["batch"])
     d = DeviceEngine(n_keys)
@@ -49,7 +51,7 @@ def test_gpu_replays_reference_fixtures():
 
 @pytest.mark.parametrize("name", sorted(SCENARIOS))
 def test_gpu_scenarios(name):
-    st_o, text_o, rd_o, _ = run_scenario(OracleEngine(8), name)
+    st_o, text_o, rd_o, _ = run_scenario(SpecOracle(8), name)
     st_d, text_d, rd_d, interner = run_scenario(DeviceEngine(8), name)
     assert st_d == st_o
     for pos, want in PROPS_AT.get(name, []):
@@ -140,7 +142,7 @@ def test_gpu_capacity_error_is_reported():
 
 def replay_both_cap(stream, cap, threads=8):
     n_keys = stream["n_keys"]
-    o = OracleEngine(n_keys, threads=threads)
+    o = SpecOracle(n_keys, threads=threads, cap=cap)
     o.load_docs(stream["inits"], stream["init_text"])
     o.apply_batch(stream["batch"])
     d = DeviceEngine(n_keys, seg_capacity=cap)
@@ -151,29 +153,38 @@ def replay_both_cap(stream, cap, threads=8):
 
 def test_gpu_stream_pass_insert_heavy_large_docs():
     # insert-only docs grow past the register tiers (1,022 segments): pass 3
-    s = gen.generate(2, n_docs=12, ops_per_doc=2600, mix=gen.MIX_INSERT, min_length=0)
+    # (new length calc; legacy documents live in the tree pass, <= 1,020 items)
+    s = gen.generate(2, n_docs=12, ops_per_doc=2600, mix=gen.MIX_INSERT, min_length=0, length_mode=2)
     o, d = replay_both_cap(s, 8192)
     assert o.stats()["max_segs"] > 2000
     assert (o.statuses() == 0).all()
     assert_same(o, d, sample_docs=12)
 
 
-@pytest.mark.parametrize("mode", [1, 2])
-def test_gpu_stream_pass_long_docs_all_ops(mode):
+def test_gpu_stream_pass_long_docs_all_ops():
     # config-5 shaped (scaled down): a long initial text split by insert /
-    # remove / annotate ops in deep rounds (1,024 concurrent ops), both
-    # length-calc modes
+    # remove / annotate ops in deep rounds (1,024 concurrent ops)
     s = gen.generate(3, n_docs=6, ops_per_doc=4000, init_len=20000, round_ops=1024, min_length=16,
-                     length_mode=mode)
+                     length_mode=2)
     o, d = replay_both_cap(s, 16384)
     assert o.stats()["max_segs"] > 1100
     assert (o.statuses() == 0).all()
     assert_same(o, d, sample_docs=6)
 
 
+def test_gpu_tree_pass_capacity_for_long_legacy_docs():
+    # the same legacy documents outgrow the tree pass (1,020 items) and stop
+    # with MTE_E_CAPACITY, as the specification does, never diverging
+    s = gen.generate(3, n_docs=6, ops_per_doc=4000, init_len=20000, round_ops=1024, min_length=16,
+                     length_mode=1)
+    o, d = replay_both_cap(s, 16384)
+    assert (o.statuses() == MTE_E_CAPACITY).all()
+    assert_same(o, d, sample_docs=6)
+
+
 def test_gpu_stream_pass_annotate_heavy():
     s = gen.generate(3, n_docs=6, ops_per_doc=3000, init_len=6000, round_ops=512, min_length=16,
-                     length_mode=1, mix=gen.MIX_INSERT | gen.MIX_ANNOTATE)
+                     length_mode=2, mix=gen.MIX_INSERT | gen.MIX_ANNOTATE)
     o, d = replay_both_cap(s, 16384)
     assert o.stats()["max_segs"] > 4000
     assert (o.statuses() == 0).all()
@@ -218,7 +229,7 @@ def test_gpu_submit_rejects_bad_record():
     with pytest.raises(MergeTreeError):
         d.run()  # the failed submit discarded the batch
     d.apply_batch(s["batch"])  # a good batch still replays exactly
-    o = OracleEngine(s["n_keys"], threads=8)
+    o = SpecOracle(s["n_keys"], threads=8)
     o.load_docs(s["inits"], s["init_text"])
     o.apply_batch(s["batch"])
     np.testing.assert_array_equal(d.digest(), o.digest())

@@ -1,0 +1,85 @@
+"""The tree pass (mte_tree.h) on the GPU: legacy length-calc documents whose
+ops see each other with lagging refSeqs, where insert placement next to
+tombstones follows the reference's B+tree block edges.  Checked against the
+specification (SpecOracle: titems.c for these documents, which equals tree.c
+and the reference itself, tests/test_tree_items.py, tests/test_ref_golden.py):
+statuses, digests, op statistics, read-outs and segment lists."""
+import numpy as np
+import pytest
+
+from fluidframework_amd import gen
+from fluidframework_amd.engine import DeviceEngine
+from oracle import OracleEngine, SpecOracle
+from test_gpu_parity import assert_same, replay_both
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("cfg,nd,nops,kw", [
+    (3, 200, 2000, dict(length_mode=1, max_lag=8)),
+    (3, 200, 2000, dict(length_mode=1, max_lag=32)),
+    (3, 100, 4000, dict(length_mode=1, max_lag=128)),
+    (2, 400, 1000, dict(length_mode=0, max_lag=64)),
+    (4, 3000, 500, dict(length_mode=1, max_lag=16)),
+])
+def test_gpu_tree_pass_lagging_refseqs(cfg, nd, nops, kw):
+    s = gen.generate(cfg, n_docs=nd, ops_per_doc=nops, **kw)
+    o, d = replay_both(s)
+    assert_same(o, d, sample_docs=24)
+    # the flat rule would have diverged on many of these documents
+    f = OracleEngine(s["n_keys"], threads=8)
+    gen.load_stream(f, s)
+    f.apply_batch(s["batch"])
+    assert ((f.digest() != o.digest()).any(axis=1) | (f.statuses() != o.statuses())).sum() > 0
+
+
+def test_gpu_tree_pass_segment_lists():
+    s = gen.generate(3, n_docs=40, ops_per_doc=3000, length_mode=1, max_lag=32)
+    o, d = replay_both(s)
+    for doc in range(40):
+        a, b = o.read_segments(doc), d.read_segments(doc)
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
+        np.testing.assert_array_equal(a[2], b[2])
+
+
+def test_gpu_tree_pass_multi_batch_and_reset():
+    # the tree word, the LRU heap and the depth / id counters persist across
+    # batches and are restored by mte_reset
+    s = gen.generate(3, n_docs=64, ops_per_doc=3000, length_mode=1, max_lag=32)
+    one = DeviceEngine(s["n_keys"])
+    gen.load_stream(one, s)
+    one.apply_batch(s["batch"])
+    many = DeviceEngine(s["n_keys"])
+    gen.load_stream(many, s)
+    b = s["batch"]
+    offs = b["op_offsets"].astype(np.int64)
+    for lo_frac, hi_frac in [(0, 0.25), (0.25, 0.26), (0.26, 1.0)]:
+        parts, new_offs = [], [0]
+        for doc in range(64):
+            n = offs[doc + 1] - offs[doc]
+            lo, hi = offs[doc] + int(n * lo_frac), offs[doc] + int(n * hi_frac)
+            parts.append(b["ops"][lo:hi])
+            new_offs.append(new_offs[-1] + hi - lo)
+        many.apply_batch(dict(b, ops=np.concatenate(parts), op_offsets=np.array(new_offs, np.uint64)))
+    np.testing.assert_array_equal(many.statuses(), one.statuses())
+    np.testing.assert_array_equal(many.digest(), one.digest())
+    first = one.digest().copy()
+    one.reset()
+    one.run()
+    one.sync()
+    np.testing.assert_array_equal(one.digest(), first)
+
+
+def test_gpu_tree_pass_loaded_body():
+    # a summary body of 400 one-unit segments (reloadFromSegments' blocks of 7,
+    # three levels), then lagging legacy ops
+    s = gen.generate(3, n_docs=40, ops_per_doc=1500, length_mode=1, max_lag=16, init_len=400)
+    s["segs"] = gen.preload_segments(s["inits"], 400)
+    o = SpecOracle(s["n_keys"], threads=8)
+    gen.load_stream(o, s)
+    o.apply_batch(s["batch"])
+    d = DeviceEngine(s["n_keys"])
+    gen.load_stream(d, s)
+    d.apply_batch(s["batch"])
+    assert_same(o, d, sample_docs=8)
