@@ -83,3 +83,14 @@ def test_gpu_tree_pass_loaded_body():
     gen.load_stream(d, s)
     d.apply_batch(s["batch"])
     assert_same(o, d, sample_docs=8)
+
+
+import ref_golden  # noqa: E402
+
+GOLDEN = ref_golden.load()
+
+
+@pytest.mark.parametrize("rec", GOLDEN, ids=[r["name"] for r in GOLDEN])
+def test_gpu_equals_reference_golden(rec):
+    # the reference merge-tree's own digests and errors (tests/golden/ref_vectors.json.gz)
+    assert ref_golden.check(lambda k: DeviceEngine(k), rec) == []
