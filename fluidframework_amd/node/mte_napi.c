@@ -54,6 +54,7 @@ static int throw_rc(napi_env env, int rc, mte_ctx* ctx, const char* what) {
 
 typedef struct {
   mte_ctx* ctx;
+  uint32_t n_keys; /* the context's property planes: the read-outs size their buffers by it */
 } ctx_box;
 
 static void ctx_finalize(napi_env env, void* data, void* hint) {
@@ -74,13 +75,26 @@ static int get_args(napi_env env, napi_callback_info info, size_t want, napi_val
   return 1;
 }
 
-static mte_ctx* get_ctx(napi_env env, napi_value v) {
+static ctx_box* get_box(napi_env env, napi_value v) {
   ctx_box* b = NULL;
   if (napi_get_value_external(env, v, (void**)&b) != napi_ok || !b || !b->ctx) {
     napi_throw_type_error(env, NULL, "expected a live engine context");
     return NULL;
   }
-  return b->ctx;
+  return b;
+}
+
+static mte_ctx* get_ctx(napi_env env, napi_value v) {
+  ctx_box* b = get_box(env, v);
+  return b ? b->ctx : NULL;
+}
+
+/* The read-outs write the context's n_keys values per segment: a caller's nKeys
+   that differs would size the property buffers wrongly (MTE_E_INVALID_ARG). */
+static int check_nkeys(napi_env env, const ctx_box* b, uint32_t nk) {
+  if (nk == b->n_keys) return 1;
+  throw_rc(env, MTE_E_INVALID_ARG, b->ctx, "nKeys differs from the context's n_keys");
+  return 0;
 }
 
 /* Raw bytes of any TypedArray (or null/undefined -> NULL, 0). */
@@ -149,6 +163,7 @@ static napi_value js_create(napi_env env, napi_callback_info info) {
     return NULL;
   }
   b->ctx = ctx;
+  b->n_keys = nk;
   NAPI_CALL(env, napi_create_external(env, b, ctx_finalize, NULL, &r));
   return r;
 }
@@ -314,11 +329,13 @@ static napi_value u32_array(napi_env env, const uint32_t* src, size_t n) {
 static napi_value js_read_segments(napi_env env, napi_callback_info info) {
   napi_value argv[3];
   if (!get_args(env, info, 3, argv)) return NULL;
-  mte_ctx* ctx = get_ctx(env, argv[0]);
-  if (!ctx) return NULL;
+  ctx_box* box = get_box(env, argv[0]);
+  if (!box) return NULL;
+  mte_ctx* ctx = box->ctx;
   uint32_t doc = 0, nk = 0;
   NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
   NAPI_CALL(env, napi_get_value_uint32(env, argv[2], &nk));
+  if (!check_nkeys(env, box, nk)) return NULL;
   mte_seg_list v;
   memset(&v, 0, sizeof v);
   if (throw_rc(env, mte_read_segments(ctx, doc, &v), ctx, "mte_read_segments")) return NULL;  // sizes
@@ -347,11 +364,13 @@ static napi_value js_read_segments(napi_env env, napi_callback_info info) {
 static napi_value js_read_doc(napi_env env, napi_callback_info info) {
   napi_value argv[3];
   if (!get_args(env, info, 3, argv)) return NULL;
-  mte_ctx* ctx = get_ctx(env, argv[0]);
-  if (!ctx) return NULL;
+  ctx_box* box = get_box(env, argv[0]);
+  if (!box) return NULL;
+  mte_ctx* ctx = box->ctx;
   uint32_t doc = 0, nk = 0;
   NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
   NAPI_CALL(env, napi_get_value_uint32(env, argv[2], &nk));
+  if (!check_nkeys(env, box, nk)) return NULL;
   mte_doc_view v;
   memset(&v, 0, sizeof v);
   if (throw_rc(env, mte_read_doc(ctx, doc, &v), ctx, "mte_read_doc")) return NULL;  // sizes

@@ -208,10 +208,9 @@ class BatchBuilder {
     const ref = checkI32(msg.referenceSequenceNumber === undefined ? 0 : msg.referenceSequenceNumber,
       "referenceSequenceNumber");
     const msn = checkI32(msg.minimumSequenceNumber, "minimumSequenceNumber");
-    const short = clients.short(sender, seq);
-    if (short >= MAX_CLIENTS) {
-      throw new MergeTreeError(E_CLIENT_RANGE, "client " + String(sender) + ": more than " + MAX_CLIENTS +
-        " clients inside the collab window");
+    // a recycled slot is only sound while every op sees past minSeq (DocClients)
+    if (ref < clients.minSeq) {
+      throw new MergeTreeError(E_INVALID_ARG, "referenceSequenceNumber " + ref + " < minSeq " + clients.minSeq);
     }
     const recs = [];
     if ((msg.type === undefined ? "op" : msg.type) === "op") {
@@ -220,6 +219,8 @@ class BatchBuilder {
       }
       this._opRecords(msg.contents, recs);
     }
+    // the slot is taken only once the message has validated
+    const short = slotOf(clients, sender, seq);
     if (recs.length === 0) recs.push([OP_NOOP, 0, 0, 0, 0, NO_PROPS]);
     recs[recs.length - 1][1] |= F_MSG_END;
     for (const r of recs) this.docOps[doc].push([seq, ref, msn, r[0], short, r[1], r[2], r[3], r[4], r[5]]);
@@ -360,6 +361,15 @@ function packDocInits(docs, interner) {
  * does (snapshotLoader.ts:90-118); a missing client / seq means NonCollabClient
  * / UniversalSequenceNumber.
  */
+function slotOf(clients, longId, seq) {
+  const s = clients.short(longId, seq);
+  if (s >= MAX_CLIENTS) {
+    throw new MergeTreeError(E_CLIENT_RANGE, "client " + String(longId) + ": more than " + MAX_CLIENTS +
+      " clients inside the collab window");
+  }
+  return s;
+}
+
 function packSegments(docs, clientsOf, inits) {
   const SEG_BYTES = 32;
   let n = 0;
@@ -387,11 +397,13 @@ function packSegments(docs, clientsOf, inits) {
       buf.writeInt32LE(sp.seq === undefined ? 0 : sp.seq, o + 8);
       const removed = sp.removedSeq !== undefined;
       buf.writeInt32LE(removed ? sp.removedSeq : 0x7fffffff, o + 12);
+      // loaded clients are tied to the seq they inserted / removed at, so their
+      // slots recycle once minSeq passes it like those of live senders
       let mask = 0;
       const rc = sp.removedClientIds || (sp.removedClient !== undefined ? [sp.removedClient] : []);
-      for (const id of rc) mask |= 1 << clientsOf(i).short(id);
+      for (const id of rc) mask |= 1 << slotOf(clientsOf(i), id, removed ? sp.removedSeq : undefined);
       buf.writeUInt32LE(mask >>> 0, o + 16);
-      buf.writeInt32LE(sp.client === undefined ? -1 : clientsOf(i).short(sp.client), o + 20);
+      buf.writeInt32LE(sp.client === undefined ? -1 : slotOf(clientsOf(i), sp.client, sp.seq), o + 20);
       buf.writeUInt32LE(kind, o + 24);
       buf.writeUInt32LE(props.add(segProps) >>> 0, o + 28);
       if (text !== null) { extra.push(text); textOff += text.length; }

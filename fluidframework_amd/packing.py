@@ -191,15 +191,19 @@ class BatchBuilder:
         seq = _check_i32(msg["sequenceNumber"], "sequenceNumber")
         ref = _check_i32(msg.get("referenceSequenceNumber", 0), "referenceSequenceNumber")
         msn = _check_i32(msg["minimumSequenceNumber"], "minimumSequenceNumber")
-        short = clients.short(sender, seq)
-        if short >= MTE_MAX_CLIENTS:
-            raise MergeTreeError(MTE_E_CLIENT_RANGE, f"client {sender!r}: more than {MTE_MAX_CLIENTS} "
-                                 "clients inside the collab window")
+        # a recycled slot is only sound while every op sees past minSeq (DocClients)
+        if ref < clients.min_seq:
+            raise MergeTreeError(MTE_E_INVALID_ARG, f"referenceSequenceNumber {ref} < minSeq {clients.min_seq}")
         recs = []
         if msg.get("type", "op") == "op":
             if sender == clients.observer:
                 raise MergeTreeError(MTE_E_UNSUPPORTED, "ack of a local op (observer replay only)")
             self._op_records(msg.get("contents"), recs)
+        # the slot is taken only once the message has validated
+        short = clients.short(sender, seq)
+        if short >= MTE_MAX_CLIENTS:
+            raise MergeTreeError(MTE_E_CLIENT_RANGE, f"client {sender!r}: more than {MTE_MAX_CLIENTS} "
+                                 "clients inside the collab window")
         if not recs:
             recs.append((OP_NOOP, 0, 0, 0, 0, NO_PROPS))
         out = self.ops[doc]

@@ -94,6 +94,7 @@ def test_gpu_chunk_insert_hotspot_relayouts():
     inits = np.zeros(1, gen.DOC_INIT_DTYPE)
     inits["text_len"] = n0
     inits["propset"] = 0xFFFFFFFF
+    inits["flags"] = 1  # new length calc: 3,000 loaded segments are the chunk pass's
     text = np.full(n0, ord("a"), np.uint16)
     offs_s, segs = gen.preload_segments(inits, n0)
     ops = np.zeros(n_ops, OP_DTYPE)

@@ -166,3 +166,52 @@ process.stdout.write(JSON.stringify([c.getText(), c.getLength(), c.getText(2, 6)
 eng.close();
 """
     assert json.loads(node("-e", script)) == ["hello world", 12, "llo", "", "lo world"]
+
+
+def test_node_loaded_body_clients_recycle_and_are_range_checked():
+    # summary-body clients are tied to their seqs: once minSeq passes them their
+    # slots recycle for new senders; a body naming more clients than slots
+    # inside the window is E_CLIENT_RANGE (never a wrapped 1 << 32 mask)
+    script = r"""
+const P = require("./fluidframework_amd/node/packing.js");
+const it = new P.Interner(2);
+const body = [];
+for (let i = 1; i <= 31; i++) body.push({ json: "x", client: "c" + i, seq: i });
+body.push({ json: "y", client: "c1", seq: 1, removedSeq: 5, removedClientIds: ["c2", "c3"] });
+const docs = [{ text: "", minSeq: 0, currentSeq: 40, segments: body }];
+const clients = new P.DocClients("A", 0);
+const inits = { interner: it, propsetsArr: [], propsArr: [], textUnits: 0 };
+const out = P.packSegments(docs, () => clients, inits);
+const seg = Buffer.from(out.segs.buffer, out.segs.byteOffset, out.segs.length);
+const res = { n: out.segs.length / 32, mask: seg.readUInt32LE(31 * 32 + 16), errs: [] };
+const bb = new P.BatchBuilder(1, it);
+const ins = { type: 0, pos1: 0, seg: "z" };
+try { bb.addMessage(0, clients, { clientId: "new0", sequenceNumber: 41, referenceSequenceNumber: 40,
+  minimumSequenceNumber: 10, contents: ins }); } catch (e) { res.errs.push(e.code); }
+bb.addMessage(0, clients, { clientId: "c31", sequenceNumber: 41, referenceSequenceNumber: 40,
+  minimumSequenceNumber: 10, contents: ins });
+bb.addMessage(0, clients, { clientId: "new1", sequenceNumber: 42, referenceSequenceNumber: 40,
+  minimumSequenceNumber: 10, contents: ins });
+res.new1 = clients.ids.get("new1");
+try { bb.addMessage(0, clients, { clientId: "c31", sequenceNumber: 43, referenceSequenceNumber: 9,
+  minimumSequenceNumber: 10, contents: ins }); } catch (e) { res.errs.push(e.code); }
+const many = [];
+for (let i = 1; i <= 40; i++) many.push({ json: "x", client: "d" + i, seq: 100 + i });
+const fresh = new P.DocClients("A", 0);
+try { P.packSegments([{ text: "", segments: many }], () => fresh, inits); }
+catch (e) { res.errs.push(e.code); }
+process.stdout.write(JSON.stringify(res));
+"""
+    j = json.loads(node("-e", script))
+    assert j["n"] == 32 and j["mask"] == (1 << 2) | (1 << 3)
+    assert j["new1"] == 1          # c1's slot: its last seq (5) is behind minSeq 10
+    assert j["errs"] == [-12, -1, -12]  # window still at 0 / refSeq < minSeq / 40 in-window body clients
+
+
+@pytest.mark.gpu
+def test_node_read_outs_reject_wrong_nkeys_on_gpu():
+    # readDoc / readSegments size their property buffers by the context's n_keys
+    out = node("-e", "const m=require(process.argv[1]);const c=m.create(0,2,1024);const r=[];"
+                     "for(const f of ['readDoc','readSegments'])try{m[f](c,0,5)}catch(e){r.push(e.code)}"
+                     "m.destroy(c);console.log(JSON.stringify(r))", ADDON)
+    assert json.loads(out) == [-1, -1]

@@ -50,3 +50,26 @@ def test_client_slots_recycle_only_behind_the_window():
     assert "c1" not in c.ids and c.short("c2", seq=41) == 2
     assert c.short("later", seq=42) == 3               # c3 (last seq 3 <= 3)
     assert c.short("again", seq=43) == MTE_MAX_CLIENTS  # c4 .. c31 used seqs above minSeq
+
+
+def test_packer_rejects_ref_below_min_seq_and_takes_no_slot_on_error():
+    import pytest
+    from fluidframework_amd.abi import MTE_E_INVALID_ARG, MTE_E_UNSUPPORTED
+    from fluidframework_amd.packing import BatchBuilder, DocClients, Interner, MergeTreeError
+    c = DocClients("A")
+    bb = BatchBuilder(1, Interner(2))
+    ins = {"type": 0, "pos1": 0, "seg": "x"}
+    bb.add_message(0, c, dict(clientId="b", sequenceNumber=1, referenceSequenceNumber=0,
+                              minimumSequenceNumber=1, contents=ins))
+    # a refSeq behind the window's minSeq would let a recycled slot see its
+    # previous owner's segments as its own: rejected
+    with pytest.raises(MergeTreeError) as e:
+        bb.add_message(0, c, dict(clientId="c", sequenceNumber=2, referenceSequenceNumber=0,
+                                  minimumSequenceNumber=1, contents=ins))
+    assert e.value.code == MTE_E_INVALID_ARG
+    # a message that fails validation leaves DocClients untouched
+    with pytest.raises(MergeTreeError) as e:
+        bb.add_message(0, c, dict(clientId="d", sequenceNumber=2, referenceSequenceNumber=1,
+                                  minimumSequenceNumber=1, contents={"type": 0, "relativePos1": {"id": "m"}}))
+    assert e.value.code == MTE_E_UNSUPPORTED
+    assert set(c.ids) == {"A", "b"}

@@ -8,7 +8,7 @@ import pytest
 
 from fluidframework_amd import gen, snapshot
 from fluidframework_amd.engine import DeviceEngine
-from oracle import OracleEngine
+from oracle import OracleEngine, SpecOracle
 
 
 def split_batch(stream, k):
@@ -48,10 +48,12 @@ def round_trip(make, stream, k):
     return bodies
 
 
-def test_summary_round_trip_oracle():
+@pytest.mark.parametrize("spec", [False, True])
+def test_summary_round_trip_oracle(spec):
     s = gen.generate(3, n_docs=24, ops_per_doc=1500)  # R = 64: cut at a round boundary and inside one
+    make = (lambda nk: SpecOracle(nk, threads=8)) if spec else (lambda nk: OracleEngine(nk))
     for k in (640, 700):
-        bodies = round_trip(lambda nk: OracleEngine(nk), s, k)
+        bodies = round_trip(make, s, k)
         assert any("removedSeq" in sp for body in bodies for sp in body)  # tombstones above the MSN kept
         assert any("seq" not in sp for body in bodies for sp in body)     # below-MSN text coalesced
 
@@ -74,7 +76,9 @@ def test_summary_writer_coalesces_and_elides():
 def test_gpu_summary_round_trip():
     s = gen.generate(3, n_docs=64, ops_per_doc=1500)
     bodies_d = round_trip(lambda nk: DeviceEngine(nk), s, 700)
-    bodies_o = round_trip(lambda nk: OracleEngine(nk), s, 700)
+    # the engine's specification (legacy docs: the tree, whose append-merges
+    # coarsen segments that a later remove turns into one tombstone)
+    bodies_o = round_trip(lambda nk: SpecOracle(nk, threads=8), s, 700)
     assert bodies_d == bodies_o  # the GPU's summary is the restatement's
 
 
@@ -156,6 +160,6 @@ def test_legacy_loader_checks():
 def test_gpu_legacy_summary_round_trip():
     s = gen.generate(3, n_docs=64, ops_per_doc=1500)
     blobs_d = legacy_round_trip(lambda nk: DeviceEngine(nk), s, 700, chunk_size=64)
-    blobs_o = legacy_round_trip(lambda nk: OracleEngine(nk), s, 700, chunk_size=64)
+    blobs_o = legacy_round_trip(lambda nk: SpecOracle(nk, threads=8), s, 700, chunk_size=64)
     assert [{k: v for k, v in b.items() if k != "catchupOps"} for b in blobs_d] == \
         [{k: v for k, v in b.items() if k != "catchupOps"} for b in blobs_o]
