@@ -20,6 +20,7 @@
 #include "mte_stream.h"
 #include "mte_chunk.h"
 #include "mte_tree.h"
+#include "mte_passes.h"
 
 using namespace mte;
 
@@ -415,29 +416,22 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   // items at E <= 4, then up to 1,020 at E = 8 / 16
   if (c->n_tree) {
     TreeArgs t{c->d_tree, c->d_heap, c->d_tree_docs, c->n_tree, c->arena};
-    const uint32_t bt = (c->n_tree + kDocsPerBlock - 1) / kDocsPerBlock;
-    hipLaunchKernelGGL((tree_kernel<K, S, false>), dim3(bt), dim3(kDocsPerBlock * kWave), 0, c->stream, a, t);
-    HIPCHK(c, hipGetLastError());
-    hipLaunchKernelGGL((tree_kernel<K, S, true>), dim3(bt), dim3(kDocsPerBlock * kWave), 0, c->stream, a, t);
-    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, (launch_tree<K, S>(a, t, (c->n_tree + kDocsPerBlock - 1) / kDocsPerBlock, c->stream)));
   }
   // pass 1: two documents per wavefront (docs up to 126 segments)
   const uint32_t b1 = (c->n_pairs + kPairsPerBlock - 1) / kPairsPerBlock;
-  if (b1) hipLaunchKernelGGL((pair_kernel<K, S, kPairsPerBlock>), dim3(b1), dim3(kPairsPerBlock * kWave), 0, c->stream, a);
-  HIPCHK(c, hipGetLastError());
+  if (b1) HIPCHK(c, (launch_pair<K, S>(a, b1, c->stream)));
   // pass 2: docs that outgrew pass 1 continue one per wavefront (up to 1022 segments)
   const uint32_t b2 = (c->n_docs + kDocsPerBlock - 1) / kDocsPerBlock;
-  hipLaunchKernelGGL((big_kernel<K, S>), dim3(b2), dim3(256), 0, c->stream, a);
-  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, (launch_big<K, S>(a, b2, c->stream)));
   // pass 3: larger docs (up to the ctx capacity): the chunked pass in big-doc
   // contexts, otherwise HBM-resident and streamed per op
   if (c->chunked) {
     const size_t lds = sizeof(uint32_t) * MTE_MAX_CLIENTS * c->ch.ng_cap + sizeof(ChCtl);
-    hipLaunchKernelGGL((chunk_kernel<K, S>), dim3(c->n_docs), dim3(kChWaves * kWave), lds, c->stream, a, c->ch);
+    HIPCHK(c, (launch_chunk<K, S>(a, c->ch, c->n_docs, lds, c->stream)));
   } else {
-    hipLaunchKernelGGL((stream_kernel<K, S>), dim3(b2), dim3(256), 0, c->stream, a);
+    HIPCHK(c, (launch_stream<K, S>(a, b2, c->stream)));
   }
-  HIPCHK(c, hipGetLastError());
   return MTE_OK;
 }
 

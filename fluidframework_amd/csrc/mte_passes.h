@@ -1,0 +1,31 @@
+// mte_passes.h — host launchers of the replay passes.  Each pass lives in its
+// own translation unit (mte_pass_tree.hip, mte_pass_flat.hip,
+// mte_pass_chunk.hip) so the passes compile in parallel and one can be rebuilt
+// alone; mte_engine.hip drives them (launch_replay).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "mte_kernels.h"
+
+namespace mte {
+
+struct ReplayArgs;
+struct TreeArgs;
+struct ChunkArgs;
+
+// the tree pass over the legacy documents (mte_tree.h): E <= 4, then E = 8 / 16
+template <int K, bool S>
+hipError_t launch_tree(const ReplayArgs& a, const TreeArgs& t, uint32_t blocks, hipStream_t s);
+// pass 1 (two documents per wavefront) and pass 2 (one per wavefront)
+template <int K, bool S>
+hipError_t launch_pair(const ReplayArgs& a, uint32_t blocks, hipStream_t s);
+template <int K, bool S>
+hipError_t launch_big(const ReplayArgs& a, uint32_t blocks, hipStream_t s);
+// pass 3: HBM-streamed (mte_stream.h) or chunked (mte_chunk.h)
+template <int K, bool S>
+hipError_t launch_stream(const ReplayArgs& a, uint32_t blocks, hipStream_t s);
+template <int K, bool S>
+hipError_t launch_chunk(const ReplayArgs& a, const ChunkArgs& ch, uint32_t n_docs, size_t lds, hipStream_t s);
+
+}  // namespace mte
