@@ -12,6 +12,17 @@ document holds (mte_read_segments), for an observer (no unacked segments):
 load_bodies() turns bodies back into mte_seg records for mte_load_segments
 (SnapshotLoader.loadBody, snapshotLoader.ts:85-125).
 
+Blob layouts over those bodies:
+  - V1 (newMergeTreeSnapshotFormat: true): write_v1() is SnapshotV1.emit
+    (snapshotV1.ts:76-165): MergeTreeChunkV1 "header" + "body_N" chunks of
+    ~chunkSize units; summary_body() reads V1 and legacy chunks back
+    (toLatestVersion, snapshotChunks.ts:142-186; loadHeader / loadBody with
+    the 0x061-0x064 asserts, snapshotLoader.ts:126-220);
+  - legacy (the default): write_legacy() / legacy_body(), below.
+to_json() / from_json() convert between the interned form and the JSON the
+reference writes (pinned against packages/dds/sequence/src/test/snapshots,
+tests/test_snapshot_fixtures.py).
+
 Bodies are in the engine's interned form: "client" / removed ids are short
 client ids, property keys are key indices and values interned value ids (the
 host's Interner maps both ways); text is UTF-16 code units (a list of ints).
@@ -19,9 +30,12 @@ removedClientIds lists the removers in ascending short id after the first
 remover when the caller supplies it (seq -> client of the removing op); only
 the set is observable in remote replay.
 """
+import json
+
 import numpy as np
 
 from .abi import DOC_INIT_DTYPE, NOT_REMOVED, PROP_DTYPE, PROPSET_DTYPE, SEG_DTYPE
+from .packing import units_to_str, utf16_units
 
 TEXT_SEGMENT_GRANULARITY = 256  # textSegment.ts (TextSegmentGranularity)
 NEWLINE = 0x0A
@@ -124,6 +138,155 @@ def load_bodies(bodies, windows, flags, n_keys):
         offs.append(len(rows))
     return (inits, np.array(units, np.uint16), np.array(psets, PROPSET_DTYPE), np.array(pents, PROP_DTYPE),
             np.array(offs, np.uint64), np.array(rows, SEG_DTYPE) if rows else np.zeros(0, SEG_DTYPE))
+
+
+# --- V1 format (newMergeTreeSnapshotFormat: true) ----------------------------------------------
+
+CHUNK_SIZE_V1 = 10000  # SnapshotV1.chunkSize, snapshotV1.ts:43
+
+
+def _has_merge_info(spec):
+    # hasMergeInfo, snapshotChunks.ts:80-82
+    return isinstance(spec, dict) and "json" in spec
+
+
+def _v1_chunk(specs, lengths, approx_length, start):
+    # SnapshotV1.getSeqLengthSegs (snapshotV1.ts:76-110); no attribution
+    n = length = 0
+    while length < approx_length and start + n < len(specs):
+        length += lengths[start + n]
+        n += 1
+    return {"version": "1", "segmentCount": n, "length": length, "segments": specs[start:start + n],
+            "startIndex": start}
+
+
+def write_v1(engine, doc, min_seq, cur_seq, chunk_size=CHUNK_SIZE_V1, first_remover=None):
+    """SnapshotV1.extractSync + emit (snapshotV1.ts:117-165, 185-268) -> {blob name: chunk}:
+    "header" carries headerMetadata {minSequenceNumber, sequenceNumber, orderedChunkMetadata,
+    totalLength, totalSegmentCount}; "body_0", "body_1", ... the rest, ~chunk_size units each.
+    Segments below the MSN are plain specs, the others IJSONSegmentWithMergeInfo."""
+    body = write_body(engine, doc, min_seq, first_remover)
+    specs = [sp if len(sp) > 1 else sp["json"] for sp in body]
+    lengths = [_seg_length(sp["json"]) for sp in body]
+    md = {"minSequenceNumber": min_seq, "sequenceNumber": cur_seq, "orderedChunkMetadata": [],
+          "totalLength": 0, "totalSegmentCount": 0}
+    chunks = []
+    while True:  # do { ... } while (totalSegmentCount < segments.length)
+        c = _v1_chunk(specs, lengths, chunk_size, md["totalSegmentCount"])
+        chunks.append(c)
+        md["totalSegmentCount"] += c["segmentCount"]
+        md["totalLength"] += c["length"]
+        if md["totalSegmentCount"] >= len(specs):
+            break
+    head = chunks.pop(0)
+    md["orderedChunkMetadata"] = [{"id": "header"}] + [{"id": f"body_{i}"} for i in range(len(chunks))]
+    head["headerMetadata"] = md
+    blobs = {"header": head}
+    blobs.update({f"body_{i}": c for i, c in enumerate(chunks)})
+    return blobs
+
+
+def to_latest(path, chunk):
+    """toLatestVersion (snapshotChunks.ts:142-186): a legacy chunk read as MergeTreeChunkV1."""
+    v = chunk.get("version")
+    if v == "1":
+        return chunk
+    if v is not None:
+        raise SnapshotLoadError(f"Unsupported chunk path: {path} version: {v}")
+    md = None
+    if path == "header":
+        md = chunk.get("headerMetadata")
+        if md is None:  # buildHeaderMetadataForLegacyChunk
+            ids = [{"id": "header"}] + ([{"id": "body"}] if chunk["chunkLengthChars"] < chunk["totalLengthChars"]
+                                        else [])
+            md = {"orderedChunkMetadata": ids, "minSequenceNumber": chunk.get("chunkMinSequenceNumber"),
+                  "sequenceNumber": chunk["chunkSequenceNumber"], "totalLength": chunk["totalLengthChars"],
+                  "totalSegmentCount": chunk["totalSegmentCount"]}
+    return {"version": "1", "length": chunk["chunkLengthChars"], "segmentCount": chunk["chunkSegmentCount"],
+            "headerMetadata": md, "segments": chunk["segmentTexts"], "startIndex": chunk["chunkStartSegmentIndex"]}
+
+
+def summary_window(blobs):
+    """loadHeader (snapshotLoader.ts:126-166): (minSeq, currentSeq) of either format."""
+    md = to_latest("header", blobs["header"])["headerMetadata"]
+    if md is None:
+        raise SnapshotLoadError("header metadata not available")
+    ms = md.get("minSequenceNumber")
+    return (md["sequenceNumber"] if ms is None else ms, md["sequenceNumber"])
+
+
+def summary_body(blobs):
+    """loadHeader + loadBody (snapshotLoader.ts:126-220) over either format -> (body,
+    n_header): the segments in order as load_bodies takes them (plain specs become
+    {"json": spec}: NonCollabClient at UniversalSequenceNumber) and how many came from
+    the header chunk (the reference reloads those as a tree, reloadFromSegments, and
+    appends the rest with insertSegments)."""
+    h = to_latest("header", blobs["header"])
+    md = h["headerMetadata"]
+    if md is None:
+        raise SnapshotLoadError("header metadata not available")
+    wrap = lambda specs: [sp if _has_merge_info(sp) else {"json": sp} for sp in specs]  # noqa: E731
+    body = wrap(h["segments"])
+    if h["length"] > md["totalLength"]:
+        raise SnapshotLoadError("0x061: Mismatch in totalLength")
+    if h["segmentCount"] > md["totalSegmentCount"]:
+        raise SnapshotLoadError("0x062: Mismatch in totalSegmentCount")
+    n_header = len(body)
+    if h["segmentCount"] == md["totalSegmentCount"]:
+        return body, n_header
+    length = h["length"]
+    for meta in md["orderedChunkMetadata"][1:]:
+        c = to_latest(meta["id"], blobs[meta["id"]])
+        length += c["length"]
+        body.extend(wrap(c["segments"]))
+    if length != md["totalLength"]:
+        raise SnapshotLoadError("0x063: Mismatch in totalLength")
+    if len(body) != md["totalSegmentCount"]:
+        raise SnapshotLoadError("0x064: Mismatch in totalSegmentCount")
+    return body, n_header
+
+
+def to_json(spec, interner, client_name=str):
+    """Interned spec (plain or with merge info) -> the JSON the reference writes."""
+    if _has_merge_info(spec):
+        out = {"json": to_json(spec["json"], interner)}
+        for k in ("client", "removedClient"):
+            if k in spec:
+                out[k] = client_name(spec[k])
+        if "seq" in spec:
+            out["seq"] = spec["seq"]
+        if "removedSeq" in spec:
+            out["removedSeq"] = spec["removedSeq"]
+        if "removedClientIds" in spec:
+            out["removedClientIds"] = [client_name(c) for c in spec["removedClientIds"]]
+        return out
+    if isinstance(spec, list):
+        return units_to_str(spec)
+    props = {interner.key_names[k]: json.loads(interner.value_json[v]) for k, v in spec.get("props", {}).items()}
+    base = {"text": units_to_str(spec["text"])} if "text" in spec else {"marker": spec["marker"]}
+    if props:
+        base["props"] = props
+    return base
+
+
+def from_json(spec, interner, client_id=int):
+    """Reference JSON spec -> interned form (text as UTF-16 units, props by key index)."""
+    if _has_merge_info(spec):
+        out = dict(spec)
+        out["json"] = from_json(spec["json"], interner)
+        for k in ("client", "removedClient"):
+            if k in spec:
+                out[k] = client_id(spec[k])
+        if "removedClientIds" in spec:
+            out["removedClientIds"] = [client_id(c) for c in spec["removedClientIds"]]
+        return out
+    if isinstance(spec, str):
+        return utf16_units(spec).tolist()
+    props = {interner.key(k): interner.value(v) for k, v in (spec.get("props") or {}).items() if v is not None}
+    base = {"text": utf16_units(spec["text"]).tolist()} if "text" in spec else {"marker": dict(spec["marker"])}
+    if props:
+        base["props"] = props
+    return base
 
 
 # --- legacy format (the default when newMergeTreeSnapshotFormat !== true) ---------------------
