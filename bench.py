@@ -6,13 +6,21 @@ documents' initial state: mte_reset + mte_run (device-resident inputs: ops,
 text and property tables are uploaded to HBM before the timed region).
 
 N GPUs: one process per GPU (torch.distributed.run), documents sharded with no
-data-path collective ("weak": every rank replays its own 10k-doc shard; doc
-seeds are global doc indices).  After the timed region the per-doc digests are
-all-gathered over RCCL for verification (the only collective).
+data-path collective.  Default "strong": the config's documents (BASELINE: 10k
+per node) split over the ranks (doc seeds are global doc indices); at N > 1 a
+"weak" side line replays the config's documents on every rank.  After the
+timed region the per-doc digests are all-gathered over RCCL for verification
+(the only collective).
+
+Legacy length-calc documents of the round-model workloads are declared
+round-synchronous (MTE_DOC_ROUND_SYNC: flat passes, declaration checked per
+batch); the "tree_placement" side line replays the same job with them on the
+tree pass (the reference's B+tree placement) and must give the same digests.
 
 Rank 0 prints one JSON line.  At N=1 it also times the CPU restatement
 (oracle/, kind "port") on a bounded sample of the same workload and checks the
-sampled docs' digests against the GPU's.
+sampled docs' digests against the GPU's; the reference merge-tree's own CPU
+rate (measured in the build container, tools/ref_baseline.py) is attached.
 """
 import argparse
 import json
@@ -69,14 +77,83 @@ def pmc_traffic(config, n_docs, ops_per_doc):
     return rec["traffic_bytes_per_launch"], os.path.relpath(path, ROOT) + " (" + rec["correction"] + ")"
 
 
+REF_BASELINE_JSON = os.path.join(ROOT, "profiles", "r02", "ref_cpu_baseline.json")
+
+
+def reference_cpu_baseline(config):
+    """The reference merge-tree itself timed on CPU (tools/ref_baseline.py, run in
+    the build container: the reference does not travel to the GPU box), or None."""
+    if not os.path.exists(REF_BASELINE_JSON):
+        return None
+    rec = json.load(open(REF_BASELINE_JSON)).get(f"config{config}")
+    return rec
+
+
+def run_engine(stream, cap, device, steps, warmup, stats_on, barrier=lambda: None):
+    """Load + submit a stream, one accounting run (mte_stats), warmup, then
+    `steps` timed steps (reset + run) bracketed by barrier + sync.  Returns a
+    dict with the engine, elapsed seconds, kernel ms per step, stats, digest."""
+    from fluidframework_amd import gen
+    from fluidframework_amd.engine import DeviceEngine
+
+    eng = DeviceEngine(stream["n_keys"], device=device, seg_capacity=cap)
+    gen.load_stream(eng, stream)
+    eng.submit(stream["batch"])
+
+    def step():
+        eng.reset()
+        eng.run()
+
+    # one accounting run (mte_stats: ops, segments scanned / written, property
+    # writes, units -> the algorithmic bytes of SURVEY.md 8(d)); the timed runs
+    # then go without the per-op counters (opt-in like the reference's measureOps)
+    step()
+    eng.sync()
+    first_ms = eng.stats()["kernel_ms"]
+    if (eng.statuses() != 0).any():
+        raise SystemExit(f"replay errors {np.unique(eng.statuses())}")
+    stats = eng.stats()
+    stats_digest = eng.digest()
+    eng.set_stats(stats_on)
+    for _ in range(warmup):
+        step()
+    eng.sync()
+    barrier()
+    eng.sync()
+    kernel_ms = []
+    t_start = time.perf_counter()
+    for _ in range(steps):
+        step()
+        # the library brackets its replay kernels with HIP events on its own
+        # stream; read them after the step (waits only for that step)
+        eng.sync()
+        kernel_ms.append(eng.stats()["kernel_ms"])
+    eng.sync()
+    t_elapsed = time.perf_counter() - t_start
+    barrier()
+    digest = eng.digest()
+    if (eng.statuses() != 0).any() or not np.array_equal(digest, stats_digest):
+        raise SystemExit("timed runs disagree with the accounting run")
+    return {"eng": eng, "elapsed": t_elapsed, "kernel_ms": kernel_ms, "stats": stats, "digest": digest,
+            "first_ms": first_ms}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=3)
-    ap.add_argument("--docs", type=int, default=None, help="docs per GPU (default: the config's)")
+    ap.add_argument("--docs", type=int, default=None, help="docs in the whole job (default: the config's)")
     ap.add_argument("--ops", type=int, default=None, help="ops per doc (default: the config's)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong: the config's documents split over the ranks (BASELINE: 10k docs per node); "
+                         "weak: every rank replays that many documents")
+    ap.add_argument("--placement", choices=["round_sync", "tree"], default="round_sync",
+                    help="legacy-calc documents: declared round-synchronous (MTE_DOC_ROUND_SYNC, flat passes, "
+                         "checked per batch) or on the tree pass")
+    ap.add_argument("--no-tree-leg", action="store_true", help="skip the tree-placement side measurement")
+    ap.add_argument("--no-weak-leg", action="store_true", help="skip the weak-scaling side measurement (N > 1)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stats", action="store_true",
@@ -95,76 +172,50 @@ def main():
 
     from fluidframework_amd import dist as fdist
     from fluidframework_amd import gen
-    from fluidframework_amd.engine import DeviceEngine
 
     preset = gen.PRESETS[args.config]
-    n_docs = args.docs or preset["n_docs"]
+    docs_job = args.docs or preset["n_docs"]
     ops_per_doc = args.ops or preset["ops_per_doc"]
     threads = max(1, host_threads() // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", world))))
 
-    t0 = time.time()
-    stream = gen.generate(args.config, n_docs=n_docs, ops_per_doc=ops_per_doc,
-                          doc_base=fdist.shard_doc_base(rank, n_docs), n_threads=threads)
-    gen_s = time.time() - t0
-    n_ops_rank = int(stream["batch"]["op_offsets"][-1])
+    def shard(scaling):
+        """(first global doc, docs) of this rank."""
+        if scaling == "weak":
+            return fdist.shard_doc_base(rank, docs_job), docs_job
+        per = (docs_job + world - 1) // world
+        b = min(docs_job, rank * per)
+        return b, max(0, min(docs_job, b + per) - b)
 
-    cap = gen.seg_capacity(args.config, stream["params"])
-    eng = DeviceEngine(stream["n_keys"], device=local_rank, seg_capacity=cap)
-    gen.load_stream(eng, stream)
-    eng.submit(stream["batch"])
-
-    def step():
-        eng.reset()
-        eng.run()
-
-    # one accounting run (mte_stats: ops, segments scanned / written, property
-    # writes, units -> the algorithmic bytes of SURVEY.md 8(d)); the timed runs
-    # then go without the per-op counters (opt-in like the reference's measureOps)
-    step()
-    eng.sync()
-    if (eng.statuses() != 0).any():
-        raise SystemExit(f"rank {rank}: replay errors {np.unique(eng.statuses())}")
-    stats = eng.stats()
-    stats_digest = eng.digest()
-    eng.set_stats(args.stats)
-    for _ in range(args.warmup):
-        step()
-    eng.sync()
+    def make_stream(scaling, placement):
+        base, n = shard(scaling)
+        kw = {"round_sync": True} if placement == "round_sync" and not preset.get("max_lag") else {}
+        return gen.generate(args.config, n_docs=n, ops_per_doc=ops_per_doc, doc_base=base, n_threads=threads,
+                            **kw)
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    barrier()
-    eng.sync()
-    kernel_ms = []
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        # the library brackets its replay kernels with HIP events on its own
-        # stream; read them after the step (waits only for that step)
-        eng.sync()
-        kernel_ms.append(eng.stats()["kernel_ms"])
-    eng.sync()
-    t_elapsed = time.perf_counter() - t_start
-    barrier()
-
-    elapsed = t_elapsed
+    dev = f"cuda:{local_rank}"
+    t0 = time.time()
+    stream = make_stream(args.scaling, args.placement)
+    gen_s = time.time() - t0
+    n_ops_rank = int(stream["batch"]["op_offsets"][-1])
+    cap = gen.seg_capacity(args.config, stream["params"])
+    r = run_engine(stream, cap, local_rank, args.steps, args.warmup, args.stats, barrier)
+    eng, stats, digest = r["eng"], r["stats"], r["digest"]
+    elapsed = r["elapsed"]
     total_ops = n_ops_rank * world
-    digest = eng.digest()
-    if (eng.statuses() != 0).any() or not np.array_equal(digest, stats_digest):
-        raise SystemExit(f"rank {rank}: timed runs disagree with the accounting run")
     fold = fdist.digest_fold(digest)
     if dist is not None:
-        dev = f"cuda:{local_rank}"
-        elapsed = fdist.max_over_ranks(dist, t_elapsed, device=dev)
+        elapsed = fdist.max_over_ranks(dist, r["elapsed"], device=dev)
         total_ops = fdist.sum_over_ranks(dist, n_ops_rank, device=dev)
         # the verification collective: every rank's per-doc digests over RCCL
         fold = fdist.digest_fold(fdist.gather_digests(dist, engine=eng, device=dev))
 
     ms_per_step = elapsed * 1000.0 / args.steps
     value = total_ops / (elapsed / args.steps)
-    avg_kernel_ms = float(np.mean(kernel_ms)) if kernel_ms else None
+    avg_kernel_ms = float(np.mean(r["kernel_ms"])) if r["kernel_ms"] else None
     algo_bytes = stats["algo_bytes"]
     achieved_gbs = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9 if avg_kernel_ms else None
 
@@ -175,11 +226,39 @@ def main():
     eng.sync()
     t0 = time.perf_counter()
     eng.submit(stream["batch"])
-    step()
+    eng.reset()
+    eng.run()
     e2e_digest = eng.digest()
     e2e_s = time.perf_counter() - t0
     if not np.array_equal(e2e_digest, digest):
         raise SystemExit(f"rank {rank}: end-to-end pass disagrees with the timed runs")
+    del eng, r
+
+    # side measurement: the same job with every legacy-calc document on the
+    # tree pass (no round-synchronous declaration), digest-checked
+    tree_leg = None
+    if args.placement == "round_sync" and not args.no_tree_leg and world == 1:
+        ts = make_stream(args.scaling, "tree")
+        rt = run_engine(ts, cap, local_rank, max(1, args.steps // 2), 1, False)
+        if not np.array_equal(rt["digest"], digest):
+            raise SystemExit("tree placement disagrees with the round-synchronous replay")
+        tms = rt["elapsed"] * 1000.0 / max(1, args.steps // 2)
+        tree_leg = {"ms_per_step": tms, "ops_per_s": n_ops_rank / (tms * 1e-3),
+                    "kernel_ms": float(np.mean(rt["kernel_ms"])), "first_run_kernel_ms": rt["first_ms"],
+                    "digest_equal": True,
+                    "note": "legacy-calc documents on the tree pass (reference B+tree placement, mte_tree.h)"}
+        del rt, ts
+
+    # side measurement at N > 1: weak scaling (every rank the config's docs)
+    weak_leg = None
+    if world > 1 and args.scaling == "strong" and not args.no_weak_leg:
+        ws = make_stream("weak", args.placement)
+        rw = run_engine(ws, cap, local_rank, args.steps, 1, False, barrier)
+        w_el = fdist.max_over_ranks(dist, rw["elapsed"], device=dev)
+        w_ops = fdist.sum_over_ranks(dist, int(ws["batch"]["op_offsets"][-1]), device=dev)
+        weak_leg = {"value": w_ops / (w_el / args.steps), "ms_per_step": w_el * 1000.0 / args.steps,
+                    "docs_per_gpu": int(len(ws["inits"])), "scaling": "weak"}
+        del rw, ws
 
     if rank != 0:
         if dist is not None:
@@ -193,6 +272,7 @@ def main():
             cpu, parity = cpu_baseline_prefix(stream, cap, args.cpu_seconds, threads)
         else:
             cpu, parity = cpu_baseline(stream, digest, args.cpu_seconds)
+    ref_cpu = reference_cpu_baseline(args.config)
 
     out = {
         "metric": METRIC,
@@ -203,15 +283,19 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (seeded MT19937 conflict-farm streams, fluidframework_amd/gen.py)",
         "config": {
             "workload": WORKLOADS.get(args.config, f"config{args.config}"),
-            "docs_per_gpu": n_docs,
+            "docs_total": docs_job if args.scaling == "strong" else docs_job * world,
+            "docs_per_gpu": int(len(stream["inits"])),
             "ops_per_doc": ops_per_doc,
             "ops_per_gpu": n_ops_rank,
+            "placement": ("legacy-calc docs declared round-synchronous (MTE_DOC_ROUND_SYNC): flat passes, "
+                          "declaration checked per batch" if args.placement == "round_sync" else
+                          "legacy-calc docs on the tree pass (reference B+tree placement)"),
             "parallelism": f"doc-sharded x{world} (no data-path collective)",
         },
         "roofline": {
@@ -223,8 +307,8 @@ def main():
             "traffic": traffic,
             "traffic_source": traffic_src,
             "traffic_frac_of_algo": (traffic / algo_bytes) if traffic else None,
-            "kernel": ("pair_kernel + big_kernel + " + ("chunk_kernel" if cap >= 8192 else "stream_kernel") +
-                       " (replay passes 1-3), HIP events on the engine stream"),
+            "kernel": ("tree + pair + big + " + ("chunk" if cap >= 8192 else "stream") +
+                       " replay passes, HIP events on the engine stream"),
             "algo_bytes_note": ("S_live of chunk-pass ops replaced by the chunk slots + summary entries they "
                                 "scanned (SURVEY.md 8(d))" if cap >= 8192 else "SURVEY.md 8(d) B_op"),
             "counters_in_timed_runs": bool(args.stats),
@@ -234,7 +318,10 @@ def main():
         },
         "end_to_end": {"ops_per_s": n_ops_rank / e2e_s, "ms": e2e_s * 1e3,
                        "includes": "mte_submit (host->HBM op upload) + reset + replay + digest read-back, rank 0"},
+        "tree_placement": tree_leg,
+        "weak_scaling": weak_leg,
         "cpu_baseline": cpu,
+        "cpu_baseline_reference": ref_cpu,
         "digest_fold": f"{fold:016x}",
         "parity_sample": parity,
         "gen_s": round(gen_s, 2),

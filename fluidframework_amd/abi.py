@@ -44,6 +44,7 @@ OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP = 0, 1, 2, 3
 F_MARKER, F_MSG_END, F_REWRITE = 0x1, 0x2, 0x4
 NO_PROPS = 0xFFFFFFFF
 DOC_NEW_LENGTH_CALC = 0x1
+DOC_ROUND_SYNC = 0x2
 
 # 32-byte mte_op record.
 OP_DTYPE = np.dtype([

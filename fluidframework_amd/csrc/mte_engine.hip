@@ -38,6 +38,64 @@ __global__ void begin_batch_kernel(DocHdr* hdr, unsigned long long* stats, uint3
   for (int t = 0; t < kNumStats; t++) stats[(size_t)d * kNumStats + t] = 0;
 }
 
+// MTE_DOC_ROUND_SYNC check (include/mte.h; oracle.c round_sync_ok): one wave
+// per declared legacy document, 64 records per step.  A live record violates
+// the declaration when its refSeq is below the highest refSeq so far, or above
+// it but below the highest live seq so far; both maxima are exclusive wave
+// max-scans continued from the header (pad0 = highest refSeq, pad1 = highest
+// live seq, the load's currentSeq to start with).  A violation stops the
+// document before any op of the batch.
+__device__ __forceinline__ int32_t dpp_max(int32_t v, int32_t x) { return v > x ? v : x; }
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ int32_t dppm(int32_t v) {
+  return __builtin_amdgcn_update_dpp(INT32_MIN, v, CTRL, ROWMASK, 0xf, false);
+}
+__device__ __forceinline__ int32_t wave_incl_max(int32_t v) {
+  v = dpp_max(v, dppm<kRowShr1>(v));
+  v = dpp_max(v, dppm<kRowShr2>(v));
+  v = dpp_max(v, dppm<kRowShr4>(v));
+  v = dpp_max(v, dppm<kRowShr8>(v));
+  v = dpp_max(v, dppm<kRowBcast15, 0xa>(v));
+  v = dpp_max(v, dppm<kRowBcast31, 0xc>(v));
+  return v;
+}
+
+__global__ __launch_bounds__(256) void round_sync_kernel(DocHdr* hdr, const uint4* recs, const uint64_t* op_off,
+                                                         const uint32_t* docs, uint32_t n) {
+  const uint32_t w = blockIdx.x * 4 + threadIdx.x / kWave;
+  if (w >= n) return;
+  const int doc = (int)uni(docs[w]);
+  const int l = lane_id();
+  if (uni(hdr[doc].status) != 0) return;
+  int32_t ref = (int32_t)uni(hdr[doc].pad0), seq = (int32_t)uni(hdr[doc].pad1);
+  const uint64_t k0 = op_off[doc], k1 = op_off[doc + 1];
+  bool bad = false;
+  for (uint64_t k = k0; k < k1 && !bad; k += kWave) {
+    const bool in = k + (uint64_t)l < k1;
+    const uint4 w0 = in ? recs[2 * (k + (uint64_t)l)] : make_uint4(0u, 0u, 0u, (uint32_t)MTE_OP_NOOP);
+    const bool live = in && (w0.w & 0xffu) != MTE_OP_NOOP;
+    const int32_t r = (int32_t)w0.y, sq = (int32_t)w0.x;
+    // maxima over the live records before this one (exclusive scans)
+    const int32_t rin = wave_incl_max(live ? r : INT32_MIN), sin = wave_incl_max(live ? sq : INT32_MIN);
+    int32_t rb = (int32_t)__builtin_amdgcn_mov_dpp(rin, kWaveShr1, 0xf, 0xf, false);
+    int32_t sb = (int32_t)__builtin_amdgcn_mov_dpp(sin, kWaveShr1, 0xf, 0xf, false);
+    rb = l == 0 ? INT32_MIN : rb;
+    sb = l == 0 ? INT32_MIN : sb;
+    rb = dpp_max(rb, ref);
+    sb = dpp_max(sb, seq);
+    bad = __ballot(live && (r < rb || (r > rb && r < sb))) != 0;
+    ref = dpp_max(ref, (int32_t)rdlane(rin, kWave - 1));
+    seq = dpp_max(seq, (int32_t)rdlane(sin, kWave - 1));
+  }
+  if (l == 0) {
+    if (bad) hdr[doc].status = MTE_E_UNSUPPORTED;
+    else {
+      hdr[doc].pad0 = (uint32_t)ref;
+      hdr[doc].pad1 = (uint32_t)seq;
+    }
+  }
+}
+
 // (re)initialise docs from their load description: one seq-0 LocalClientId
 // text segment (client.replay.spec.ts:22-23)
 // Legacy length-calc documents also carry the reference's B+tree (mte_tree.h):
@@ -45,6 +103,9 @@ __global__ void begin_batch_kernel(DocHdr* hdr, unsigned long long* stats, uint3
 // empty root, mergeTree.ts:495-498; the replay harness's insertTextLocal adds
 // one leaf), an empty document one placeholder; a loaded body has
 // reloadFromSegments' blocks of 7 (image_kernel writes the tree words).
+// device copy of mte_doc_init::flags: the load text holds a '\n' (engine-internal)
+constexpr uint32_t kInitNl = 0x80000000u;
+
 __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_doc_init* inits,
                              const uint32_t* init_props, uint32_t n_keys, uint32_t n_docs,
                              const uint64_t* img_off, uint32_t* tree) {
@@ -52,13 +113,14 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
   if (d >= n_docs) return;
   const mte_doc_init in = inits[d];
   const uint32_t n_img = img_off ? (uint32_t)(img_off[d + 1] - img_off[d]) : 0u;
-  const bool legacy = !(in.flags & MTE_DOC_NEW_LENGTH_CALC) && tree != nullptr;
+  const bool flat_legacy = (in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC)) == MTE_DOC_ROUND_SYNC;
+  const bool legacy = !(in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC)) && tree != nullptr;
   DocHdr h;
   h.nseg = n_img ? (int32_t)n_img : (in.text_len > 0 || legacy ? 1 : 0);
   h.min_seq = in.min_seq;
   h.cur_seq = in.cur_seq;
   h.status = 0;
-  h.flags = in.flags & MTE_DOC_NEW_LENGTH_CALC;
+  h.flags = in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC);
   h.resume = 0;
   h.pad0 = h.pad1 = 0;
   if (legacy) {
@@ -66,6 +128,10 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
     for (uint64_t w = 7; n_img && w < n_img; w *= 7) depth++;
     h.pad0 = n_img ? n_img + 1 : 2;  // next segment id
     h.pad1 = (uint32_t)depth;         // depth | heap size << 8
+  }
+  if (flat_legacy) {
+    h.pad0 = (uint32_t)INT32_MIN;  // round-sync check: no refSeq yet
+    h.pad1 = (uint32_t)in.cur_seq;  // every later increase must reach it
   }
   hdr[d] = h;
   if (n_img) return;  // image_kernel writes the segments
@@ -79,7 +145,7 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
   uint32_t po = 0;
   for (uint32_t k = 0; k < n_keys; k++) soa.props[k * soa.plane_stride + i] = init_props[(size_t)d * MTE_MAX_KEYS + k];
   if (in.propset != MTE_NO_PROPS) po = kTPo;
-  if (legacy) tree[i] = in.text_len > 0 ? (1u | po | (1u << 8)) : (1u | kTEmpty);
+  if (legacy) tree[i] = in.text_len > 0 ? (1u | po | (1u << 8) | ((in.flags & kInitNl) ? kTNl : 0u)) : (1u | kTEmpty);
 }
 
 // the mte_load_segments image -> the flat planes (one thread per segment)
@@ -254,6 +320,10 @@ struct mte_ctx {
   uint32_t n_docs = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // the tree pass runs on its own stream beside the flat passes (disjoint
+  // documents), forked after the batch set-up and joined before the read-outs
+  hipStream_t tree_stream = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool ran = false, submitted = false;
   bool stats_on = true;
   std::string err;
@@ -309,6 +379,8 @@ struct mte_ctx {
   uint32_t* d_tree_docs = nullptr;  // the legacy documents
   uint32_t n_tree = 0;
   std::vector<uint8_t> h_legacy;    // per doc
+  uint32_t* d_rs_docs = nullptr;    // legacy documents declared MTE_DOC_ROUND_SYNC (flat)
+  uint32_t n_rs = 0;
   uint64_t* d_off = nullptr;
   uint64_t off_cap = 0;
   mte_propset* d_ps = nullptr;
@@ -375,9 +447,11 @@ void free_docs(mte_ctx* c) {
   if (c->d_wclock) (void)hipFree(c->d_wclock);
   c->d_wclock = nullptr;
   void* ps[] = {c->hdr, c->soa.len, c->stats, c->d_inits, c->d_init_props, c->d_digest, c->d_pairs,
-                c->d_tree, c->d_heap, c->d_tree_docs};
+                c->d_tree, c->d_heap, c->d_tree_docs, c->d_rs_docs};
   for (void* p : ps)
     if (p) (void)hipFree(p);
+  c->d_rs_docs = nullptr;
+  c->n_rs = 0;
   c->d_tree = nullptr;
   c->d_heap = nullptr;
   c->d_tree_docs = nullptr;
@@ -415,8 +489,18 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   // the tree pass: legacy length calc documents (mte_tree.h), up to 252
   // items at E <= 4, then up to 1,020 at E = 8 / 16
   if (c->n_tree) {
+    if (!c->tree_stream) {
+      HIPCHK(c, hipStreamCreateWithFlags(&c->tree_stream, hipStreamNonBlocking));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    }
+    // the flat passes only touch documents pass 1 owns or escalates (never a
+    // tree document), so the two streams share no document state
+    HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->tree_stream, c->ev_fork, 0));
     TreeArgs t{c->d_tree, c->d_heap, c->d_tree_docs, c->n_tree, c->arena};
-    HIPCHK(c, (launch_tree<K, S>(a, t, (c->n_tree + kDocsPerBlock - 1) / kDocsPerBlock, c->stream)));
+    HIPCHK(c, (launch_tree<K, S>(a, t, (c->n_tree + kDocsPerBlock - 1) / kDocsPerBlock, c->tree_stream)));
+    HIPCHK(c, hipEventRecord(c->ev_join, c->tree_stream));
   }
   // pass 1: two documents per wavefront (docs up to 126 segments)
   const uint32_t b1 = (c->n_pairs + kPairsPerBlock - 1) / kPairsPerBlock;
@@ -432,6 +516,7 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   } else {
     HIPCHK(c, (launch_stream<K, S>(a, b2, c->stream)));
   }
+  if (c->n_tree) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
   return MTE_OK;
 }
 
@@ -489,6 +574,20 @@ int upload_ops(mte_ctx* c, const mte_batch* b, uint64_t* bad, const char** why) 
           }
         }
         std::memcpy(dst + a, b->ops + k0 + a, (e - a) * sizeof(mte_op));
+        // kRecNl: the insert's text holds a '\n' (the tree pass's append-merge
+        // looks at a leaf's last unit only then, mte_tree.h)
+        for (uint64_t k = a; k < e; k++) {
+          mte_op& o = dst[k];
+          o.flags = (uint16_t)(o.flags & ~kRecNl);
+          if (o.type == MTE_OP_INSERT && !(o.flags & MTE_F_MARKER) && o.pos2 > 0) {
+            const uint16_t* t = b->text + o.a;
+            for (int32_t u = 0; u < o.pos2; u++)
+              if (t[u] == 0x0A) {
+                o.flags = (uint16_t)(o.flags | kRecNl);
+                break;
+              }
+          }
+        }
       });
     }
     for (auto& t : th) t.join();
@@ -580,6 +679,9 @@ int mte_destroy(mte_ctx* c) {
     if (c->stage[i]) (void)hipHostFree(c->stage[i]);
     if (c->stage_ev[i]) (void)hipEventDestroy(c->stage_ev[i]);
   }
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->tree_stream) (void)hipStreamDestroy(c->tree_stream);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -659,11 +761,16 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     // e.g. config 2's 1k docs) runs one per wave instead: pairing it would
     // leave SIMDs idle and serialise two documents per wave.
     // Legacy length-calc documents go to the tree pass instead (mte_tree.h).
-    std::vector<uint32_t> flat_docs, tree_docs;
+    // Round-synchronous legacy documents (MTE_DOC_ROUND_SYNC) stay flat, behind
+    // the per-batch check of round_sync_kernel.
+    std::vector<uint32_t> flat_docs, tree_docs, rs_docs;
     c->h_legacy.assign(n_docs, 0);
     for (uint32_t d = 0; d < n_docs; d++) {
       if (docs[d].flags & MTE_DOC_NEW_LENGTH_CALC) {
         flat_docs.push_back(d);
+      } else if (docs[d].flags & MTE_DOC_ROUND_SYNC) {
+        flat_docs.push_back(d);
+        rs_docs.push_back(d);
       } else {
         tree_docs.push_back(d);
         c->h_legacy[d] = 1;
@@ -678,6 +785,11 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     for (uint32_t i = 0; i < nf; i++) pairs[solo ? 2 * (size_t)i : i] = flat_docs[i];
     HIPCHK(c, hipMalloc((void**)&c->d_pairs, pairs.size() * 4));
     HIPCHK(c, hipMemcpy(c->d_pairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice));
+    c->n_rs = (uint32_t)rs_docs.size();
+    if (c->n_rs) {
+      HIPCHK(c, hipMalloc((void**)&c->d_rs_docs, rs_docs.size() * 4));
+      HIPCHK(c, hipMemcpy(c->d_rs_docs, rs_docs.data(), rs_docs.size() * 4, hipMemcpyHostToDevice));
+    }
     c->n_tree = (uint32_t)tree_docs.size();
     if (c->n_tree) {
       HIPCHK(c, hipMalloc((void**)&c->d_tree, nslots * 4));
@@ -688,7 +800,16 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     }
   }
   if (n_docs) {
-    HIPCHK(c, hipMemcpyAsync(c->d_inits, docs, sizeof(mte_doc_init) * n_docs, hipMemcpyHostToDevice, c->stream));
+    std::vector<mte_doc_init> dinit(docs, docs + n_docs);
+    for (mte_doc_init& di : dinit) {
+      di.flags &= ~kInitNl;
+      for (uint32_t u = 0; u < di.text_len; u++)
+        if (text[di.text_off + u] == 0x0A) {
+          di.flags |= kInitNl;
+          break;
+        }
+    }
+    HIPCHK(c, hipMemcpy(c->d_inits, dinit.data(), sizeof(mte_doc_init) * n_docs, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpyAsync(c->d_init_props, iprops.data(), sizeof(uint32_t) * iprops.size(),
                              hipMemcpyHostToDevice, c->stream));
   }
@@ -752,7 +873,10 @@ int mte_load_segments(mte_ctx* c, const uint64_t* seg_offsets, const mte_seg* se
           uint64_t w = 7;
           for (int lv = 1; lv < depth && k % w == 0; lv++, w *= 7) h = (uint32_t)lv;
         }
-        img[(size_t)np * n_segs + g] = h | (sg.propset != MTE_NO_PROPS ? kTPo : 0u) | ((uint32_t)(k + 1) << 8);
+        bool nl = false;
+        for (uint32_t u = 0; !marker && u < sg.len && !nl; u++) nl = c->h_arena[sg.text_off + u] == 0x0A;
+        img[(size_t)np * n_segs + g] = h | (sg.propset != MTE_NO_PROPS ? kTPo : 0u) | ((uint32_t)(k + 1) << 8) |
+                                       (nl ? kTNl : 0u);
       }
       if (sg.propset != MTE_NO_PROPS) {
         if (sg.propset >= c->h_load_ps.size())
@@ -862,6 +986,11 @@ int mte_run(mte_ctx* c) {
   if (c->wclock_path) {
     if (!c->d_wclock) HIPCHK(c, hipMalloc((void**)&c->d_wclock, 16ull * (c->n_pairs + 1)));
     a.wclock = c->d_wclock;
+  }
+  if (c->n_rs) {
+    hipLaunchKernelGGL(round_sync_kernel, dim3((c->n_rs + 3) / 4), dim3(256), 0, c->stream, c->hdr, a.recs, c->d_off,
+                       c->d_rs_docs, c->n_rs);
+    HIPCHK(c, hipGetLastError());
   }
   if (c->n_propsets) {
     hipLaunchKernelGGL(props_kernel, dim3((uint32_t)((c->n_propsets + 255) / 256)), dim3(256), 0, c->stream, c->d_ps,

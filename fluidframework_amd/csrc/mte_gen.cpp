@@ -159,6 +159,15 @@ uint32_t annotate_set(MT& rng) {
   return pair_set(k1, k2, v1, v2);
 }
 
+// n units of the author's name; with newline_every, 1 in N texts has one unit
+// (any of them) replaced by '\n' (TextSegment.canAppend refuses to append to a
+// text ending in one, textSegment.ts:72-77).  No draw is made without the option.
+void push_text(const mteg_config& cfg, MT& rng, uint32_t author, int32_t n, DocOut& out) {
+  int32_t nl = -1;
+  if (cfg.newline_every && rng.uniform(0, cfg.newline_every - 1) == 0) nl = (int32_t)rng.uniform(0, (uint32_t)n - 1);
+  for (int32_t i = 0; i < n; i++) out.text.push_back(i == nl ? (uint16_t)'\n' : (uint16_t)('B' + author));
+}
+
 // an insert of 1-3 units of the author's name, or (1 in marker_every) a
 // marker {marker:{refType:1}, props:{markerId:"m<seq>"}}; returns its length
 int32_t gen_insert(const mteg_config& cfg, MT& rng, uint32_t author, int32_t s, mte_op& op, DocOut& out) {
@@ -174,7 +183,7 @@ int32_t gen_insert(const mteg_config& cfg, MT& rng, uint32_t author, int32_t s, 
   const int32_t n = (int32_t)rng.uniform(1, 3);
   op.pos2 = n;
   op.a = (uint32_t)out.text.size();  // per-doc offset, fixed up at fill
-  for (int32_t i = 0; i < n; i++) out.text.push_back((uint16_t)('B' + author));
+  push_text(cfg, rng, author, n, out);
   return n;
 }
 
@@ -348,7 +357,7 @@ void gen_doc(const mteg_config& cfg, uint32_t d, DocOut& out) {
           n = (int32_t)rng.uniform(1, 3);
           op.pos2 = n;
           op.a = (uint32_t)out.text.size();  // per-doc offset, fixed up at fill
-          for (int32_t i = 0; i < n; i++) out.text.push_back((uint16_t)('B' + author));
+          push_text(cfg, rng, author, n, out);
         }
         // model: the engine's placement: before the first
         // defined unit with P >= pos.  Lengths alone would not need the exact

@@ -56,6 +56,7 @@ typedef struct mteg_config {
                             msn = the minimum over the clients (the sequencer
                             rule, deli clientSeqManager.ts:130-137), so ops
                             see each other's concurrent edits partially */
+  uint32_t newline_every; /* 1 in N inserted texts holds a '\n' (0 = none) */
 } mteg_config;
 
 typedef struct mteg_stream mteg_stream;

@@ -6,10 +6,12 @@ namespace mte {
 
 template <int K, bool S>
 hipError_t launch_tree(const ReplayArgs& a, const TreeArgs& t, uint32_t blocks, hipStream_t s) {
-  hipLaunchKernelGGL((tree_kernel<K, S, false>), dim3(blocks), dim3(kDocsPerBlock * kWave), 0, s, a, t);
-  const hipError_t e = hipGetLastError();
+  hipLaunchKernelGGL((tree_kernel<K, S, 0>), dim3(blocks), dim3(kDocsPerBlock * kWave), 0, s, a, t);
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((tree_kernel<K, S, true>), dim3(blocks), dim3(kDocsPerBlock * kWave), 0, s, a, t);
+  hipLaunchKernelGGL((tree_kernel<K, S, 1>), dim3(blocks), dim3(kDocsPerBlock * kWave), 0, s, a, t);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL((tree_kernel<K, S, 2>), dim3(blocks), dim3(kDocsPerBlock * kWave), 0, s, a, t);
   return hipGetLastError();
 }
 

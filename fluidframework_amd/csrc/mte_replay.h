@@ -655,7 +655,8 @@ __device__ __forceinline__ void run_finish(DocRun& D, const ReplayArgs& a) {
     h.status = D.status;
     h.flags = D.flags;
     h.resume = D.k;
-    h.pad0 = h.pad1 = 0;
+    h.pad0 = a.hdr[D.doc].pad0;  // MTE_DOC_ROUND_SYNC check state (round_sync_kernel)
+    h.pad1 = a.hdr[D.doc].pad1;
     a.hdr[D.doc] = h;
   }
 }
@@ -843,7 +844,7 @@ __device__ __forceinline__ void run_to_lds(const DocRun& D, DocHdr* hl) {
   if (lane_id() == 0) {
     uint4* p = reinterpret_cast<uint4*>(hl);
     p[0] = make_uint4((uint32_t)D.n, (uint32_t)D.min_seq, (uint32_t)D.cur_seq, (uint32_t)D.status);
-    p[1] = make_uint4(D.flags, D.k, 0u, 0u);
+    reinterpret_cast<uint2*>(hl)[2] = make_uint2(D.flags, D.k);  // pad0 / pad1 kept
   }
   fence_wave();
 }

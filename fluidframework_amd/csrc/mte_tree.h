@@ -18,8 +18,13 @@
 //   bits 4-5  ns: needsScour of the leaf block it starts (0 undefined, 1 false, 2 true)
 //   bit  6    po: segment.properties exists
 //   bit  7    empty: placeholder of an empty leaf block (len 0, undefined to all)
-//   bits 8-31 id: the name the LRU heap entries use
-// and the LRU heap (collections/heap.ts) in LDS, 8 B per entry.  Between
+//   bits 8-30 id: the name the LRU heap entries use
+//   bit  31   nl: the text may hold a '\n' (its insert's text did; mte_submit
+//             marks those records kRecNl), so an append-merge must look at its
+//             last unit in the arena; without it no load is needed
+// and the LRU heap (collections/heap.ts) in LDS, 8 B per entry.  The op
+// records are prefetched with vector loads: a scalar prefetch would share the
+// LDS accesses' wait counter and stall every heap access on it.  Between
 // launches the tree word lives in TreeArgs::tree, the heap in TreeArgs::heap,
 // depth / next id / heap size in DocHdr pad0 / pad1.
 #pragma once
@@ -31,10 +36,12 @@ namespace mte {
 constexpr int kTreeHeapCap = 255;  // entries per document (+ the unused index 0)
 constexpr uint32_t kHdrTreeEsc = 0x40000000u;  // tree pass: continue in the E = 8 / 16 kernel
 constexpr uint32_t kTH = 0x7u, kTCont = 0x8u, kTNsShift = 4, kTNs = 0x30u, kTPo = 0x40u, kTEmpty = 0x80u;
+constexpr uint32_t kTNl = 0x80000000u;
+constexpr uint16_t kRecNl = 0x8000u;  // op record flag (engine-internal): the insert's text holds a '\n'
 constexpr uint32_t kNsUndef = 0, kNsFalse = 1, kNsTrue = 2;
 constexpr int kMaxNodes = 8;       // MaxNodesInBlock, mergeTreeNodes.ts:373
 constexpr int32_t kTextGranularity = 256;  // textSegment.ts:19
-constexpr uint32_t kIdLimit = 1u << 24;
+constexpr uint32_t kIdLimit = 1u << 23;
 
 struct TreeArgs {
   uint32_t* tree;        // tree word of slot x of doc d: tree[d * cap + x]
@@ -46,7 +53,7 @@ struct TreeArgs {
 
 __device__ __forceinline__ uint32_t t_h(uint32_t t) { return t & kTH; }
 __device__ __forceinline__ uint32_t t_ns(uint32_t t) { return (t & kTNs) >> kTNsShift; }
-__device__ __forceinline__ uint32_t t_id(uint32_t t) { return t >> 8; }
+__device__ __forceinline__ uint32_t t_id(uint32_t t) { return (t >> 8) & (kIdLimit - 1u); }
 
 // ---- wave-wide index helpers (E slots per lane, index = lane * E + j) --------
 
@@ -359,7 +366,7 @@ __device__ __forceinline__ int scour(TReg<E, K>& X, int s, int e, int32_t min_se
           if (k < n_keys) match = match && bcast<E>(X.R.pr[k], prev) == bcast<E>(X.R.pr[k], i);
         const bool text = (pm >> 8) == 0 && (xm >> 8) == 0;
         bool nl = false;
-        if (text) {
+        if (text && (bcast<E>(X.T, prev_last) & kTNl)) {
           const int32_t ll = bcast<E>(X.R.len, prev_last);
           const uint32_t lo = bcast<E>(X.R.toff, prev_last);
           nl = ll > 0 && tr.arena[lo + (uint32_t)ll - 1] == (uint16_t)'\n';
@@ -370,7 +377,7 @@ __device__ __forceinline__ int scour(TReg<E, K>& X, int s, int e, int32_t min_se
         // TextSegment.append: the leaf becomes texts of the previous one
 #pragma unroll
         for (int j = 0; j < E; j++)
-          if (base + j == i) X.T[j] = (X.T[j] & 0xffu & ~kTNs) | kTCont;
+          if (base + j == i) X.T[j] = (X.T[j] & ((0xffu & ~kTNs) | kTNl)) | kTCont;
         prev_len += xl;
         prev_last = xe - 1;
       } else {
@@ -589,7 +596,7 @@ __device__ __forceinline__ int tree_boundary(TReg<E, K>& X, const int32_t (&L)[E
       if (i == xs + 1) {
         X.R.len[j] = len - off;
         X.R.toff[j] += (uint32_t)off;
-        X.T[j] = (X.T[j] & kTPo) | (id << 8);
+        X.T[j] = (X.T[j] & (kTPo | kTNl)) | (id << 8);
       }
     }
     n++;
@@ -607,7 +614,7 @@ __device__ __forceinline__ int tree_boundary(TReg<E, K>& X, const int32_t (&L)[E
     const uint32_t id = tr.next_id++;
 #pragma unroll
     for (int j = 0; j < E; j++)
-      if (base + j == ic) X.T[j] = (X.T[j] & (kTPo)) | (id << 8);
+      if (base + j == ic) X.T[j] = (X.T[j] & (kTPo | kTNl)) | (id << 8);
     MTE_STAT(st[kStWritten] += 1;)
     split_cascade<E>(X.T, ic, n, tr);
     changed = true;
@@ -615,20 +622,25 @@ __device__ __forceinline__ int tree_boundary(TReg<E, K>& X, const int32_t (&L)[E
   return n;
 }
 
+// op record k through vector loads: dword i in lane i < 8 (vmcnt, not lgkmcnt)
+__device__ __forceinline__ uint32_t vload_rec(const uint4* rec) {
+  const int l = lane_id();
+  return l < 8 ? reinterpret_cast<const uint32_t*>(rec)[l] : 0u;
+}
+
 // One op record of a legacy document (titems.c doc_apply).  Returns 0, 1 (the
 // document needs the next register tier) or a negative MTE_E_*.
 template <int E, int K, bool S>
-__device__ __forceinline__ int tree_step(TReg<E, K>& X, DocRun& D, TreeRun& tr, uint32_t (&st)[kNumStats], s8v& cur,
-                         const ReplayArgs& a, uint32_t* zlds) {
+__device__ __forceinline__ int tree_step(TReg<E, K>& X, DocRun& D, TreeRun& tr, uint32_t (&st)[kNumStats],
+                                         uint32_t& cur, const ReplayArgs& a, uint32_t* zlds) {
   const int base = lane_id() * E;
   const int lim = kWave * E < (int)a.cap ? kWave * E : (int)a.cap;
   if (D.n + 4 > lim) return 1;
   if (tr.next_id + 4 >= kIdLimit) return MTE_E_CAPACITY;
-  const s8v op = cur;
-  const uint4* rec = D.recp + 2 * D.k;
-  // (the flat passes order this prefetch behind `op` with an empty asm on
-  // SGPR operands; the tree pass's scalar state is too large for that)
-  cur = sload8(rec + 2);
+  s8v op;
+#pragma unroll
+  for (int i = 0; i < 8; i++) op[i] = (int32_t)rdlane(cur, i);
+  cur = vload_rec(D.recp + 2 * (D.k + 1));  // the next record (zeroed pad after the last)
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
@@ -699,7 +711,7 @@ __device__ __forceinline__ int tree_step(TReg<E, K>& X, DocRun& D, TreeRun& tr, 
         MTE_STAT(if (!marker) st[kStUnits] += (uint32_t)pos2;)
         MTE_STAT(st[kStWritten] += 1;)
         const uint32_t id = tr.next_id++;
-        uint32_t tw = (id << 8) | (psi != MTE_NO_PROPS ? kTPo : 0u);
+        uint32_t tw = (id << 8) | (psi != MTE_NO_PROPS ? kTPo : 0u) | ((flags & kRecNl) ? kTNl : 0u);
         if (replace) {
           tw |= tbs & (kTH | kTNs);
         } else {
@@ -821,7 +833,7 @@ __device__ __forceinline__ void tree_burst(DocRun& D, TreeRun& tr, const ReplayA
   TReg<E, K> X;
   uint32_t st[kNumStats] = {};
   tree_load<E, K>(X, D, a, t);
-  s8v cur = sload8(D.recp + 2 * D.k);
+  uint32_t cur = vload_rec(D.recp + 2 * D.k);
   for (;;) {
     const int rc = tree_step<E, K, S>(X, D, tr, st, cur, a, zlds);
     if (rc < 0) {
@@ -841,17 +853,18 @@ __device__ __forceinline__ void tree_burst(DocRun& D, TreeRun& tr, const ReplayA
       }
     }
   }
-  swait(cur);
   tree_store<E, K>(X, D, a, t);
   if constexpr (S) run_flush_stats(D, st, a);
 }
 
-// The tree pass.  BIG = false: tiers E = 1, 2, 4 (documents up to 252 items);
-// a document that outgrows them is flagged kHdrTreeEsc and continues in the
-// BIG = true launch (E = 8, 16; up to 1,020 items).
-template <int K, bool S, bool BIG>
+// The tree pass, three launches.  A kernel's register allocation is that of
+// its largest tier, so the tiers are split by size: TIER 0 runs E = 1, 2
+// (documents up to 124 items, ~130 VGPRs: 3 waves per SIMD); a document that
+// outgrows it is flagged kHdrTreeEsc and continues in TIER 1 (E = 1, 2, 4, up
+// to 252 items), then TIER 2 (E = 8, 16, up to 1,020 items).
+template <int K, bool S, int TIER>
 __global__ __launch_bounds__(256) void tree_kernel(ReplayArgs a, TreeArgs t) {
-  constexpr int EMAX = BIG ? 16 : 4;
+  constexpr int EMAX = TIER == 2 ? 16 : TIER == 1 ? 4 : 2;
   __shared__ uint32_t zlds_all[kDocsPerBlock][kWave * EMAX];
   __shared__ uint2 heap_all[kDocsPerBlock][kTreeHeapCap + 1];
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
@@ -860,7 +873,7 @@ __global__ __launch_bounds__(256) void tree_kernel(ReplayArgs a, TreeArgs t) {
   const int doc = uni((int)t.docs[idx]);
   const uint4 h0 = reinterpret_cast<const uint4*>(a.hdr + doc)[0], h1 = reinterpret_cast<const uint4*>(a.hdr + doc)[1];
   const uint32_t hflags = uni(h1.x);
-  if (BIG && !(hflags & kHdrTreeEsc)) return;
+  if (TIER > 0 && !(hflags & kHdrTreeEsc)) return;
   DocRun D;
   D.doc = doc;
   D.n = uni((int32_t)h0.x);
@@ -890,7 +903,14 @@ __global__ __launch_bounds__(256) void tree_kernel(ReplayArgs a, TreeArgs t) {
       D.status = MTE_E_CAPACITY;
       break;
     }
-    if (!BIG) {
+    if constexpr (TIER == 0) {
+      if (n + 4 <= kWave) tree_burst<1, K, S>(D, tr, a, t, zlds, 1);
+      else if (n + 4 <= 2 * kWave) tree_burst<2, K, S>(D, tr, a, t, zlds, 1);
+      else {
+        D.flags |= kHdrTreeEsc;
+        break;
+      }
+    } else if constexpr (TIER == 1) {
       if (n + 4 <= kWave) tree_burst<1, K, S>(D, tr, a, t, zlds, 1);
       else if (n + 4 <= 2 * kWave) tree_burst<2, K, S>(D, tr, a, t, zlds, 1);
       else if (n + 4 <= 4 * kWave) tree_burst<4, K, S>(D, tr, a, t, zlds, 1);

@@ -9,7 +9,7 @@ import os
 import numpy as np
 
 from . import _native
-from .abi import DOC_INIT_DTYPE, NOT_REMOVED, OP_DTYPE, PROP_DTYPE, PROPSET_DTYPE, SEG_DTYPE, MergeTreeError  # noqa: F401
+from .abi import DOC_INIT_DTYPE, DOC_ROUND_SYNC, NOT_REMOVED, OP_DTYPE, PROP_DTYPE, PROPSET_DTYPE, SEG_DTYPE, MergeTreeError  # noqa: F401
 
 MIX_INSERT, MIX_REMOVE, MIX_ANNOTATE = 1, 2, 4
 N_KEYS = 4  # client, bold, color, markerId
@@ -20,7 +20,7 @@ class GenConfig(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in (
         "config_id", "n_docs", "ops_per_doc", "doc_base", "clients", "min_length", "round_ops",
         "mix", "marker_every", "length_mode", "init_len", "n_threads", "init_segs", "max_range",
-        "max_lag")]
+        "max_lag", "newline_every")]
 
 
 class GenSizes(C.Structure):
@@ -76,7 +76,8 @@ def generate(config_id=2, n_docs=None, ops_per_doc=None, doc_base=0, n_threads=N
     cfg = GenConfig(config_id, p["n_docs"], p["ops_per_doc"], doc_base, p["clients"],
                     p["min_length"], p["round_ops"], p["mix"], p["marker_every"],
                     p["length_mode"], p.get("init_len", 0), n_threads or default_threads(),
-                    p.get("init_segs", 0), p.get("max_range", 0), p.get("max_lag", 0))
+                    p.get("init_segs", 0), p.get("max_range", 0), p.get("max_lag", 0),
+                    p.get("newline_every", 0))
     h = C.c_void_p()
     rc = lib.mteg_generate(C.byref(cfg), C.byref(h))
     if rc:
@@ -98,6 +99,12 @@ def generate(config_id=2, n_docs=None, ops_per_doc=None, doc_base=0, n_threads=N
             raise MergeTreeError(rc, "mteg_fill")
     finally:
         lib.mteg_free(h)
+    if p.get("round_sync"):
+        # the stream is round-synchronous (max_lag 0): declare it, so legacy
+        # documents may replay on the flat passes (MTE_DOC_ROUND_SYNC)
+        if p.get("max_lag", 0):
+            raise ValueError("round_sync needs max_lag == 0")
+        inits["flags"] |= DOC_ROUND_SYNC
     segs = None
     if p.get("init_segs", 0):
         segs = preload_segments(inits, p["init_segs"])

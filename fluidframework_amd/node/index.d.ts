@@ -62,6 +62,25 @@ export interface ClientOptions {
   segments?: SegmentWithMergeInfo[];
   /** Load a legacy summary (SnapshotLegacy blobs) and queue its catch-up ops. */
   legacy?: LegacySummary;
+  /** Load the blobs of either summary format (summarizeV1 / summarizeLegacy). */
+  summary?: LegacySummary | V1Summary;
+}
+
+/** MergeTreeChunkV1 (snapshotChunks.ts:47-55) as SnapshotV1.emit writes it. */
+export interface V1Chunk {
+  version: "1";
+  segmentCount: number;
+  length: number;
+  segments: any[];
+  startIndex: number;
+  headerMetadata?: { minSequenceNumber: number; sequenceNumber: number; orderedChunkMetadata: { id: string }[];
+    totalLength: number; totalSegmentCount: number };
+}
+
+/** "header" plus "body_0", "body_1", ... */
+export interface V1Summary {
+  header: V1Chunk;
+  [bodyId: string]: V1Chunk;
 }
 
 /** MergeTreeChunkLegacy (snapshotChunks.ts:22-34) as SnapshotLegacy.emit writes it. */
@@ -145,6 +164,8 @@ export class BatchClient {
   getSegments(): VisibleSegment[];
   /** Summary body (SnapshotV1.extractSegment rules) + the collab window to load it with. */
   summarize(): { segments: SegmentWithMergeInfo[]; minSeq: number; currentSeq: number };
+  /** SnapshotV1.extractSync + emit (snapshotV1.ts:117-268): header + body_N chunks. */
+  summarizeV1(chunkSize?: number): V1Summary;
   /** SnapshotLegacy.extractSync + emit (snapshotlegacy.ts:105-211). */
   summarizeLegacy(catchUpMsgs?: ISequencedDocumentMessage[], chunkSize?: number): LegacySummary;
 }

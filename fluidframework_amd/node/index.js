@@ -85,10 +85,12 @@ class MergeTreeEngine {
    *  body — IJSONSegmentWithMergeInfo specs with seq / client / removedSeq /
    *  removedClientIds — as SnapshotLoader.loadBody does (snapshotLoader.ts:85-125);
    *  options.legacy loads a legacy summary (BatchClient.summarizeLegacy) and
-   *  queues its catch-up ops. */
+   *  queues its catch-up ops; options.summary loads the blobs of either format
+   *  (summarizeV1 / summarizeLegacy). */
   createClient(initialText, options) {
     if (this.started) throw new MergeTreeError(-10, "createClient after the engine started");
     let o = options || {};
+    if (o.summary) o = Object.assign({}, o, { legacy: o.summary });
     if (o.legacy) o = Object.assign({}, o, loadLegacy(o.legacy));
     const doc = this.docs.length;
     this.docs.push({ text: initialText || "", newLengthCalc: !!o.newLengthCalc, props: o.props,
@@ -357,6 +359,38 @@ class BatchClient {
   }
 
   /**
+   * V1 summary (newMergeTreeSnapshotFormat: true): SnapshotV1.emit
+   * (snapshotV1.ts:117-165) over summarize()'s segments: a "header"
+   * MergeTreeChunkV1 {version, segmentCount, length, segments, startIndex,
+   * headerMetadata} and "body_0", "body_1", ... of ~chunkSize units each.
+   * Segments below the MSN are plain specs, the others IJSONSegmentWithMergeInfo.
+   * Load it with createClient("", {summary: blobs}).
+   */
+  summarizeV1(chunkSize) {
+    const size = chunkSize === undefined ? SNAPSHOT_V1_CHUNK_SIZE : chunkSize;
+    const s = this.summarize();
+    const specs = s.segments.map((sp) => (Object.keys(sp).length === 1 ? sp.json : sp));
+    const lengths = s.segments.map((sp) => specLength(sp.json));
+    const md = { minSequenceNumber: s.minSeq, sequenceNumber: s.currentSeq, orderedChunkMetadata: [],
+      totalLength: 0, totalSegmentCount: 0 };
+    const chunks = [];
+    do { // getSeqLengthSegs (snapshotV1.ts:76-110)
+      const start = md.totalSegmentCount;
+      let n = 0, length = 0;
+      while (length < size && start + n < specs.length) { length += lengths[start + n]; n++; }
+      chunks.push({ version: "1", segmentCount: n, length, segments: specs.slice(start, start + n), startIndex: start });
+      md.totalSegmentCount += n;
+      md.totalLength += length;
+    } while (md.totalSegmentCount < specs.length);
+    const header = chunks.shift();
+    md.orderedChunkMetadata = [{ id: "header" }].concat(chunks.map((_, i) => ({ id: "body_" + i })));
+    header.headerMetadata = md;
+    const blobs = { header };
+    chunks.forEach((c, i) => { blobs["body_" + i] = c; });
+    return blobs;
+  }
+
+  /**
    * Legacy summary (the default when newMergeTreeSnapshotFormat !== true):
    * SnapshotLegacy.extractSync + emit (snapshotlegacy.ts:105-211).  The
    * document as it reads at minSeq for NonCollabClient — segments inserted at
@@ -421,6 +455,7 @@ class BatchClient {
 }
 
 const SIZE_OF_FIRST_CHUNK = 10000; // SnapshotLegacy.sizeOfFirstChunk, snapshotlegacy.ts:52
+const SNAPSHOT_V1_CHUNK_SIZE = 10000; // SnapshotV1.chunkSize, snapshotV1.ts:43
 
 function segJson(sg) {
   if (sg.kind === 0) return sg.props ? { text: sg.text, props: sg.props } : sg.text;
@@ -447,26 +482,49 @@ function legacyChunk(specs, approxLength, start, totalLength, seq) { // getSeqLe
     segmentTexts: specs.slice(start, start + n) };
 }
 
-/** SnapshotLoader.loadHeader / loadBody (snapshotLoader.ts:130-246) over legacy
- *  blobs -> {segments, minSeq, currentSeq}; throws the loader's asserts. */
+/** toLatestVersion (snapshotChunks.ts:142-186): a legacy chunk read as MergeTreeChunkV1. */
+function toLatest(path, c) {
+  if (c.version === "1") return c;
+  if (c.version !== undefined) throw new MergeTreeError(-1, "Unsupported chunk path: " + path + " version: " + c.version);
+  let md;
+  if (path === "header") {
+    md = c.headerMetadata;
+    if (md === undefined) {
+      const ids = [{ id: "header" }];
+      if (c.chunkLengthChars < c.totalLengthChars) ids.push({ id: "body" });
+      md = { orderedChunkMetadata: ids, minSequenceNumber: c.chunkMinSequenceNumber,
+        sequenceNumber: c.chunkSequenceNumber, totalLength: c.totalLengthChars, totalSegmentCount: c.totalSegmentCount };
+    }
+  }
+  return { version: "1", length: c.chunkLengthChars, segmentCount: c.chunkSegmentCount, headerMetadata: md,
+    segments: c.segmentTexts, startIndex: c.chunkStartSegmentIndex };
+}
+
+/** SnapshotLoader.loadHeader / loadBody (snapshotLoader.ts:126-246) over the
+ *  blobs of either format -> {segments, minSeq, currentSeq}; throws the
+ *  loader's asserts.  Plain specs become {json} (NonCollabClient at
+ *  UniversalSequenceNumber); specs with merge info keep it (hasMergeInfo,
+ *  snapshotChunks.ts:80-82). */
 function loadLegacy(blobs) {
-  const h = blobs.header;
+  const h = toLatest("header", blobs.header);
   const md = h.headerMetadata;
-  if (h.chunkLengthChars > md.totalLength) throw new MergeTreeError(-1, "0x061: Mismatch in totalLength");
-  if (h.chunkSegmentCount > md.totalSegmentCount) throw new MergeTreeError(-1, "0x062: Mismatch in totalSegmentCount");
-  const specs = h.segmentTexts.slice();
-  if (h.chunkSegmentCount < md.totalSegmentCount) {
-    let length = h.chunkLengthChars;
-    for (const c of md.orderedChunkMetadata.slice(1)) {
-      length += blobs[c.id].chunkLengthChars;
-      specs.push(...blobs[c.id].segmentTexts);
+  if (md === undefined) throw new MergeTreeError(-1, "header metadata not available");
+  const wrap = (sp) => (sp && typeof sp === "object" && "json" in sp ? sp : { json: sp });
+  if (h.length > md.totalLength) throw new MergeTreeError(-1, "0x061: Mismatch in totalLength");
+  if (h.segmentCount > md.totalSegmentCount) throw new MergeTreeError(-1, "0x062: Mismatch in totalSegmentCount");
+  const specs = h.segments.map(wrap);
+  if (h.segmentCount < md.totalSegmentCount) {
+    let length = h.length;
+    for (const m of md.orderedChunkMetadata.slice(1)) {
+      const c = toLatest(m.id, blobs[m.id]);
+      length += c.length;
+      specs.push(...c.segments.map(wrap));
     }
     if (length !== md.totalLength) throw new MergeTreeError(-1, "0x063: Mismatch in totalLength");
     if (specs.length !== md.totalSegmentCount) throw new MergeTreeError(-1, "0x064: Mismatch in totalSegmentCount");
   }
   const seq = md.sequenceNumber;
-  return { segments: specs.map((json) => ({ json })),
-    minSeq: md.minSequenceNumber !== undefined ? md.minSequenceNumber : seq, currentSeq: seq };
+  return { segments: specs, minSeq: md.minSequenceNumber !== undefined ? md.minSequenceNumber : seq, currentSeq: seq };
 }
 
 module.exports = { MergeTreeEngine, BatchClient, MergeTreeError, loadAddon, loadLegacy, packing };

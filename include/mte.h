@@ -115,6 +115,16 @@ typedef struct mte_config {
 
 /* IMergeTreeOptions.mergeTreeUseNewLengthCalculations, mergeTree.ts:386-399. */
 #define MTE_DOC_NEW_LENGTH_CALC 0x1u
+/* Round-synchronous stream (the conflict-farm model, test/
+ * mergeTreeOperationRunner.ts:149-199): the host declares that the refSeqs of
+ * the document's ops never decrease and that each increase reaches the seq of
+ * every earlier op.  With the legacy length calculation, insert placement then
+ * never depends on the reference's B+tree block edges, so such a
+ * document replays on the flat passes instead of the tree pass.  The engine
+ * checks the declaration per batch: a batch that breaks it stops the document
+ * with MTE_E_UNSUPPORTED before any of the batch's ops (its state stays that of
+ * the previous batch).  Ignored with MTE_DOC_NEW_LENGTH_CALC (always flat). */
+#define MTE_DOC_ROUND_SYNC 0x2u
 
 /* Initial document: one text segment inserted before collaboration starts, as
  * the reference replay harness does (client.replay.spec.ts:22-23): seq 0

@@ -166,9 +166,10 @@ def select_docs(batch, idx):
 
 class SpecOracle:
     """The engine's specification, document by document: the flat restatement
-    (oracle.c) for new length-calc documents and the tree (titems.c, equal to
-    tree.c and to the reference) for legacy ones — what libmte.so computes,
-    statistics and segment read-outs included."""
+    (oracle.c) for new length-calc documents and round-synchronous legacy ones
+    (MTE_DOC_ROUND_SYNC, checked per batch) and the tree (titems.c, equal to
+    tree.c and to the reference) for the other legacy ones — what libmte.so
+    computes, statistics and segment read-outs included."""
 
     def __init__(self, n_keys=0, threads=1, cap=0):
         self.n_keys = n_keys
@@ -182,8 +183,8 @@ class SpecOracle:
 
     def load_docs(self, inits, text=None, propsets=None, props=None):
         inits = _arr(inits, DOC_INIT_DTYPE)
-        new = (inits["flags"] & 1) != 0
-        self.sub = [np.where(new)[0], np.where(~new)[0]]  # flat, tree
+        flat = (inits["flags"] & 3) != 0  # MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC
+        self.sub = [np.where(flat)[0], np.where(~flat)[0]]  # flat, tree
         self.where = np.zeros((len(inits), 2), np.int64)
         for e, idx in enumerate(self.sub):
             self.where[idx, 0] = e

@@ -39,6 +39,7 @@ typedef struct {
   int32_t min_seq, cur_seq;
   uint32_t flags;
   int32_t status;
+  int32_t rs_ref, rs_seq; /* MTE_DOC_ROUND_SYNC: highest refSeq, highest live seq so far */
   /* stats */
   uint64_t ops, scanned, written, pwrites, units, max_segs;
   /* scratch */
@@ -395,6 +396,8 @@ int orc_load_docs(orc_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     d->flags = in->flags;
     d->min_seq = in->min_seq;
     d->cur_seq = in->cur_seq;
+    d->rs_ref = INT32_MIN;
+    d->rs_seq = in->cur_seq;
     if (in->text_len > 0) {
       if ((rc = doc_reserve(d, 64))) return rc;
       oseg* g = &d->s[0];
@@ -460,12 +463,38 @@ typedef struct {
   uint32_t d0, d1, stride;
 } worker_arg;
 
+/* MTE_DOC_ROUND_SYNC (include/mte.h) on a legacy-calc document: the batch's
+ * live ops keep refSeq non-decreasing and each increase reaches every earlier
+ * live op's seq (the load's currentSeq included).  Checked before the batch
+ * applies; a violation stops the document with MTE_E_UNSUPPORTED. */
+static int round_sync_ok(odoc* d, const mte_op* ops, uint64_t k0, uint64_t k1) {
+  int32_t ref = d->rs_ref, seq = d->rs_seq;
+  for (uint64_t k = k0; k < k1; k++) {
+    const mte_op* o = &ops[k];
+    if (o->type == MTE_OP_NOOP) continue;
+    if (o->ref_seq < ref) return 0;
+    if (o->ref_seq > ref) {
+      if (o->ref_seq < seq) return 0;
+      ref = o->ref_seq;
+    }
+    if (o->seq > seq) seq = o->seq;
+  }
+  d->rs_ref = ref;
+  d->rs_seq = seq;
+  return 1;
+}
+
 static void* worker(void* p) {
   worker_arg* w = (worker_arg*)p;
   apply_env env = {w->b, w->base, w->c->n_keys, w->c->arena};
   for (uint32_t di = w->d0; di < w->d1; di += w->stride) {
     odoc* d = &w->c->docs[di];
     if (d->status) continue;
+    if ((d->flags & (MTE_DOC_ROUND_SYNC | MTE_DOC_NEW_LENGTH_CALC)) == MTE_DOC_ROUND_SYNC &&
+        !round_sync_ok(d, w->b->ops, w->b->op_offsets[di], w->b->op_offsets[di + 1])) {
+      d->status = MTE_E_UNSUPPORTED;
+      continue;
+    }
     for (uint64_t k = w->b->op_offsets[di]; k < w->b->op_offsets[di + 1]; k++) {
       int rc = doc_apply(d, &w->b->ops[k], &env);
       if (rc) {

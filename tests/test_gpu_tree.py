@@ -94,3 +94,36 @@ GOLDEN = ref_golden.load()
 def test_gpu_equals_reference_golden(rec):
     # the reference merge-tree's own digests and errors (tests/golden/ref_vectors.json.gz)
     assert ref_golden.check(lambda k: DeviceEngine(k), rec) == []
+
+
+@pytest.mark.parametrize("cfg,nd,nops,kw", [(3, 400, 3000, dict(length_mode=0)),
+                                           (3, 100, 4000, dict(length_mode=1, newline_every=3))])
+def test_gpu_round_sync_legacy_docs_replay_flat(cfg, nd, nops, kw):
+    # MTE_DOC_ROUND_SYNC legacy documents: the flat passes, equal to the spec
+    # (flat) and to the tree oracle's digests
+    from oracle import OracleEngine
+    s = gen.generate(cfg, n_docs=nd, ops_per_doc=nops, round_sync=True, **kw)
+    d = DeviceEngine(s["n_keys"])
+    o = SpecOracle(s["n_keys"], threads=8)
+    t = OracleEngine(s["n_keys"], threads=8, tree="items")
+    for e in (d, o, t):
+        gen.load_stream(e, s)
+        e.apply_batch(s["batch"])
+    np.testing.assert_array_equal(d.statuses(), o.statuses())
+    assert (d.statuses() == 0).all()
+    np.testing.assert_array_equal(d.digest(), o.digest())
+    np.testing.assert_array_equal(d.digest(), t.digest())
+    for doc in (0, nd // 2, nd - 1):
+        assert d.read_doc(doc) == o.read_doc(doc)
+
+
+def test_gpu_round_sync_violation_stops_before_the_batch():
+    from fluidframework_amd.abi import DOC_ROUND_SYNC, MTE_E_UNSUPPORTED
+    s = gen.generate(3, n_docs=64, ops_per_doc=600, length_mode=1, max_lag=8)
+    s["inits"]["flags"] |= DOC_ROUND_SYNC
+    d = DeviceEngine(s["n_keys"])
+    gen.load_stream(d, s)
+    fresh = d.digest().copy()
+    d.apply_batch(s["batch"])
+    assert (d.statuses() == MTE_E_UNSUPPORTED).all()
+    np.testing.assert_array_equal(d.digest(), fresh)

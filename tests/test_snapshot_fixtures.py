@@ -126,3 +126,32 @@ def test_gpu_writer_reproduces_reference_blobs(version, name):
     want = FIXTURES[f"{version}/{name}"]
     for bid, c in blobs.items():
         assert digest(c) == want[bid]["sha256"], bid
+
+
+@pytest.mark.gpu
+def test_node_host_writer_reproduces_reference_blobs():
+    # the Node host's summarizeV1 / summarizeLegacy over the same loaded strings,
+    # and its loader reading them back (tests/node/snapshot_fixtures_gpu.js)
+    import shutil
+    import subprocess
+    node = shutil.which("node")
+    if node is None:
+        pytest.skip("node not installed")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cases = []
+    for version, name in [("v1", "withMarkers"), ("v1", "withAnnotations"), ("legacy", "withMarkers"),
+                          ("legacy", "headerAndBody")]:
+        it = ss.interner()
+        seg = ss.build(name)
+        cases.append({"name": f"{version}/{name}", "version": version,
+                      "segments": [{"json": snapshot.to_json(sp["json"], it)} for sp in ss.body(seg, it)],
+                      "text": ss.expected_view(seg)[0]})
+    r = subprocess.run([node, "tests/node/snapshot_fixtures_gpu.js"], cwd=root, input=json.dumps(cases),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for c, got in zip(cases, json.loads(r.stdout)):
+        want = FIXTURES[c["name"]]
+        assert sorted(got["blobs"]) == sorted(want)
+        for bid, chunk in got["blobs"].items():
+            assert digest(chunk) == want[bid]["sha256"], (c["name"], bid)
+        assert got["text"] == c["text"]
