@@ -5,7 +5,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_DIR = os.path.join(_HERE, "_lib")
+# MTE_LIB_DIR: another in-tree build of the same libraries (the profiling
+# build of tools/tree_prof.py --prof); the product default is _lib/
+LIB_DIR = os.environ.get("MTE_LIB_DIR") or os.path.join(_HERE, "_lib")
 _cache = {}
 
 

@@ -43,6 +43,19 @@ constexpr int kMaxNodes = 8;       // MaxNodesInBlock, mergeTreeNodes.ts:373
 constexpr int32_t kTextGranularity = 256;  // textSegment.ts:19
 constexpr uint32_t kIdLimit = 1u << 23;
 
+// MTE_TREE_PROF (a profiling build only, `make prof`): with statistics on, the
+// tree pass's counters become phase clocks (s_memrealtime ticks, 100 MHz):
+// segs_scanned = lengths + boundaries, segs_written = insert / range marks +
+// LRU, prop_writes = the op's zamboni, units_inserted = the whole op,
+// max_segs = the largest per-doc zamboni time at msn advances.
+#ifdef MTE_TREE_PROF
+#define TSTAT(...)
+#define TPROF(...) MTE_STAT(__VA_ARGS__)
+#else
+#define TSTAT(...) MTE_STAT(__VA_ARGS__)
+#define TPROF(...)
+#endif
+
 struct TreeArgs {
   uint32_t* tree;        // tree word of slot x of doc d: tree[d * cap + x]
   uint2* heap;           // doc d: heap[d * (kTreeHeapCap + 1) + k], k = 1 .. size
@@ -600,7 +613,7 @@ __device__ __forceinline__ int tree_boundary(TReg<E, K>& X, const int32_t (&L)[E
       }
     }
     n++;
-    MTE_STAT(st[kStWritten] += 2;)
+    TSTAT(st[kStWritten] += 2;)
     split_cascade<E>(X.T, xs + 1, n, tr);
     changed = true;
     return n;
@@ -615,7 +628,7 @@ __device__ __forceinline__ int tree_boundary(TReg<E, K>& X, const int32_t (&L)[E
 #pragma unroll
     for (int j = 0; j < E; j++)
       if (base + j == ic) X.T[j] = (X.T[j] & (kTPo | kTNl)) | (id << 8);
-    MTE_STAT(st[kStWritten] += 1;)
+    TSTAT(st[kStWritten] += 1;)
     split_cascade<E>(X.T, ic, n, tr);
     changed = true;
   }
@@ -644,16 +657,18 @@ __device__ __forceinline__ int tree_step(TReg<E, K>& X, DocRun& D, TreeRun& tr, 
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
-  MTE_STAT(st[kStOps]++;)
-  MTE_STAT(st[kStMaxSegs] = (uint32_t)D.n > st[kStMaxSegs] ? (uint32_t)D.n : st[kStMaxSegs];)
+  TSTAT(st[kStOps]++;)
+  TSTAT(st[kStMaxSegs] = (uint32_t)D.n > st[kStMaxSegs] ? (uint32_t)D.n : st[kStMaxSegs];)
   const int32_t s = op[0], r = op[1], msn = op[2];
   const int32_t pos1 = op[4], pos2 = op[5];
   int n = D.n;
   int status = 0;
   const bool newcalc = (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
+  uint64_t tq0 = 0, tq1 = 0, tq2 = 0, tq3 = 0;
+  TPROF(tq0 = wall_clock64(); tq1 = tq2 = tq3 = tq0;)
 
   if (type == MTE_OP_INSERT || type == MTE_OP_REMOVE || type == MTE_OP_ANNOTATE) {
-    MTE_STAT(st[kStScanned] += (uint32_t)n;)
+    TSTAT(st[kStScanned] += (uint32_t)n;)
     int32_t L[E], P[E];
     leaf_lengths<E, K>(X.R, r, c + 1, (int)c, D.min_seq, newcalc, L);
     int32_t total = prefix<E>(L, P);
@@ -671,6 +686,7 @@ __device__ __forceinline__ int tree_step(TReg<E, K>& X, DocRun& D, TreeRun& tr, 
       leaf_lengths<E, K>(X.R, r, c + 1, (int)c, D.min_seq, newcalc, L);
       total = prefix<E>(L, P);
     }
+    TPROF(tq1 = wall_clock64();)
     if (type == MTE_OP_INSERT) {
       const bool marker = (flags & MTE_F_MARKER) != 0;
       const int32_t nlen = marker ? 1 : pos2;
@@ -706,10 +722,10 @@ __device__ __forceinline__ int tree_step(TReg<E, K>& X, DocRun& D, TreeRun& tr, 
         if (K > 0 && psi != MTE_NO_PROPS) {
           const s8v q2 = sload_props(a, psi);
           apply_props<1, K>(pr, one, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], psi, a);
-          MTE_STAT(st[kStPwrites] += (uint32_t)q2[3];)
+          TSTAT(st[kStPwrites] += (uint32_t)q2[3];)
         }
-        MTE_STAT(if (!marker) st[kStUnits] += (uint32_t)pos2;)
-        MTE_STAT(st[kStWritten] += 1;)
+        TSTAT(if (!marker) st[kStUnits] += (uint32_t)pos2;)
+        TSTAT(st[kStWritten] += 1;)
         const uint32_t id = tr.next_id++;
         uint32_t tw = (id << 8) | (psi != MTE_NO_PROPS ? kTPo : 0u) | ((flags & kRecNl) ? kTNl : 0u);
         if (replace) {
@@ -750,7 +766,7 @@ __device__ __forceinline__ int tree_step(TReg<E, K>& X, DocRun& D, TreeRun& tr, 
         in[j] = L[j] > 0 && P[j] >= pos1 && P[j] < pos2;
         cnt += (uint32_t)__popcll(__ballot(in[j]));
       }
-      MTE_STAT(st[kStWritten] += cnt;)
+      TSTAT(st[kStWritten] += cnt;)
       if (type == MTE_OP_REMOVE) {
         const uint32_t bit = 1u << c;
 #pragma unroll
@@ -770,7 +786,7 @@ __device__ __forceinline__ int tree_step(TReg<E, K>& X, DocRun& D, TreeRun& tr, 
         apply_props<E, K>(X.R.pr, in, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], psi, a);
 #pragma unroll
         for (int j = 0; j < E; j++) X.T[j] |= in[j] ? kTPo : 0u;
-        MTE_STAT(st[kStPwrites] += cnt * (uint32_t)q2[3];)
+        TSTAT(st[kStPwrites] += cnt * (uint32_t)q2[3];)
       }
       // addToLRUSet for every touched leaf: the first one of each leaf block
       bool th[E];
@@ -783,7 +799,9 @@ __device__ __forceinline__ int tree_step(TReg<E, K>& X, DocRun& D, TreeRun& tr, 
         i = first_where<E>(th, be + 1);
       }
     }
+    TPROF(tq2 = wall_clock64();)
     n = zamboni<E, K>(X, n, D.min_seq, tr, zlds, a.n_keys, status);
+    TPROF(tq3 = wall_clock64();)
     if (status) return status;
   } else if (type != MTE_OP_NOOP) {
     return MTE_E_INVALID_ARG;
@@ -798,10 +816,15 @@ __device__ __forceinline__ int tree_step(TReg<E, K>& X, DocRun& D, TreeRun& tr, 
     D.cur_seq = s;
     if (msn > D.min_seq) {
       D.min_seq = msn;
+      uint64_t tz = 0;
+      TPROF(tz = wall_clock64();)
       D.n = zamboni<E, K>(X, D.n, D.min_seq, tr, zlds, a.n_keys, status);
+      TPROF(st[kStMaxSegs] += (uint32_t)(wall_clock64() - tz);)
       if (status) return status;
     }
   }
+  TPROF(st[kStScanned] += (uint32_t)(tq1 - tq0); st[kStWritten] += (uint32_t)(tq2 - tq1);
+        st[kStPwrites] += (uint32_t)(tq3 - tq2); st[kStUnits] += (uint32_t)(wall_clock64() - tq0);)
   return 0;
 }
 
