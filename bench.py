@@ -89,6 +89,60 @@ def reference_cpu_baseline(config):
     return rec
 
 
+class NodeComm:
+    """Barrier, scalar reductions and the digest gather of an N-GPU job: RCCL
+    through libmte.so's mte_comm_* on a context of its own (fluidframework_amd/
+    comm.py bootstraps the unique id), or torch.distributed if that cannot start."""
+
+    def __init__(self, rank, world, local_rank):
+        from fluidframework_amd import comm as fcomm
+        from fluidframework_amd.engine import DeviceEngine
+        self.rank, self.world = rank, world
+        self.dist = None
+        try:
+            self.eng = DeviceEngine(0, device=local_rank)
+            fcomm.join(self.eng, rank, world)
+            self.kind = "rccl via libmte.so mte_comm_* (no torch)"
+        except Exception as e:  # pragma: no cover - hardware dependent
+            import torch
+            import torch.distributed as dist
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl")
+            self.dist, self.dev = dist, f"cuda:{local_rank}"
+            self.kind = f"torch.distributed nccl (mte_comm failed: {e})"
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+        else:
+            self.eng.comm_barrier()
+
+    def max(self, v):
+        from fluidframework_amd import dist as fdist
+        if self.dist is not None:
+            return fdist.max_over_ranks(self.dist, v, device=self.dev)
+        return self.eng.comm_allreduce(float(v), "max")
+
+    def sum(self, v):
+        from fluidframework_amd import dist as fdist
+        if self.dist is not None:
+            return fdist.sum_over_ranks(self.dist, v, device=self.dev)
+        return self.eng.comm_allreduce(float(v), "sum")
+
+    def gather_digests(self, eng, docs_per_rank):
+        from fluidframework_amd import dist as fdist
+        if self.dist is not None:
+            return fdist.gather_digests(self.dist, engine=eng, device=self.dev)
+        eng.comm_share(self.eng)
+        return eng.comm_gather_digests(self.world, docs_per_rank).reshape(-1, 4)
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+        else:
+            self.eng.comm_destroy()
+
+
 def run_engine(stream, cap, device, steps, warmup, stats_on, barrier=lambda: None):
     """Load + submit a stream, one accounting run (mte_stats), warmup, then
     `steps` timed steps (reset + run) bracketed by barrier + sync.  Returns a
@@ -163,15 +217,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
 
     from fluidframework_amd import dist as fdist
     from fluidframework_amd import gen
+    from fluidframework_amd.engine import DeviceEngine
+
+    # node level: RCCL through libmte.so (mte_comm_*), one communicator per
+    # process on a context of its own; torch.distributed only if that fails
+    node = None
+    if world > 1:
+        node = NodeComm(rank, world, local_rank)
 
     preset = gen.PRESETS[args.config]
     docs_job = args.docs or preset["n_docs"]
@@ -193,10 +248,9 @@ def main():
                             **kw)
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        if node is not None:
+            node.barrier()
 
-    dev = f"cuda:{local_rank}"
     t0 = time.time()
     stream = make_stream(args.scaling, args.placement)
     gen_s = time.time() - t0
@@ -207,11 +261,12 @@ def main():
     elapsed = r["elapsed"]
     total_ops = n_ops_rank * world
     fold = fdist.digest_fold(digest)
-    if dist is not None:
-        elapsed = fdist.max_over_ranks(dist, r["elapsed"], device=dev)
-        total_ops = fdist.sum_over_ranks(dist, n_ops_rank, device=dev)
+    if node is not None:
+        elapsed = node.max(r["elapsed"])
+        total_ops = int(node.sum(n_ops_rank))
         # the verification collective: every rank's per-doc digests over RCCL
-        fold = fdist.digest_fold(fdist.gather_digests(dist, engine=eng, device=dev))
+        per = docs_job if args.scaling == "weak" else (docs_job + world - 1) // world
+        fold = fdist.digest_fold(node.gather_digests(eng, per))
 
     ms_per_step = elapsed * 1000.0 / args.steps
     value = total_ops / (elapsed / args.steps)
@@ -254,15 +309,15 @@ def main():
     if world > 1 and args.scaling == "strong" and not args.no_weak_leg:
         ws = make_stream("weak", args.placement)
         rw = run_engine(ws, cap, local_rank, args.steps, 1, False, barrier)
-        w_el = fdist.max_over_ranks(dist, rw["elapsed"], device=dev)
-        w_ops = fdist.sum_over_ranks(dist, int(ws["batch"]["op_offsets"][-1]), device=dev)
+        w_el = node.max(rw["elapsed"])
+        w_ops = int(node.sum(int(ws["batch"]["op_offsets"][-1])))
         weak_leg = {"value": w_ops / (w_el / args.steps), "ms_per_step": w_el * 1000.0 / args.steps,
                     "docs_per_gpu": int(len(ws["inits"])), "scaling": "weak"}
         del rw, ws
 
     if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
+        if node is not None:
+            node.close()
         return
 
     cpu = None
@@ -297,6 +352,7 @@ def main():
                           "declaration checked per batch" if args.placement == "round_sync" else
                           "legacy-calc docs on the tree pass (reference B+tree placement)"),
             "parallelism": f"doc-sharded x{world} (no data-path collective)",
+            "collective": node.kind if node is not None else None,
         },
         "roofline": {
             "bound": "hbm",
@@ -327,8 +383,8 @@ def main():
         "gen_s": round(gen_s, 2),
     }
     print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    if node is not None:
+        node.close()
 
 
 def cpu_baseline(stream, gpu_digest, target_s):

@@ -5,14 +5,15 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# MTE_LIB_DIR: another in-tree build of the same libraries (the profiling
-# build of tools/tree_prof.py --prof); the product default is _lib/
-LIB_DIR = os.environ.get("MTE_LIB_DIR") or os.path.join(_HERE, "_lib")
+LIB_DIR = os.path.join(_HERE, "_lib")
+# MTE_LIB_DIR: another in-tree build of libmte.so (the profiling build of
+# tools/tree_prof.py --prof); the product default is _lib/
+MTE_DIR = os.environ.get("MTE_LIB_DIR") or LIB_DIR
 _cache = {}
 
 
 def lib_path(name):
-    return os.path.join(LIB_DIR, name)
+    return os.path.join(MTE_DIR if name == "libmte.so" else LIB_DIR, name)
 
 
 def _load(name):
@@ -51,6 +52,13 @@ def load_mte():
         "mte_doc_status": ([vp, vp, u32], C.c_int),
         "mte_stats_get": ([vp, vp], C.c_int),
         "mte_set_stats": ([vp, C.c_int], C.c_int),
+        "mte_comm_unique_id": ([vp], C.c_int),
+        "mte_comm_init": ([vp, C.c_int, C.c_int, vp], C.c_int),
+        "mte_comm_share": ([vp, vp], C.c_int),
+        "mte_comm_barrier": ([vp], C.c_int),
+        "mte_comm_allreduce_f64": ([vp, vp, C.c_int], C.c_int),
+        "mte_comm_gather_digests": ([vp, vp, u32], C.c_int),
+        "mte_comm_destroy": ([vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

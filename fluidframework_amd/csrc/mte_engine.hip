@@ -22,6 +22,8 @@
 #include "mte_tree.h"
 #include "mte_passes.h"
 
+#include <rccl/rccl.h>
+
 using namespace mte;
 
 namespace {
@@ -33,7 +35,7 @@ __global__ void begin_batch_kernel(DocHdr* hdr, unsigned long long* stats, uint3
   if (d == 0) *gdone = 0;
   if (d >= n_docs) return;
   hdr[d].resume = 0;
-  hdr[d].flags &= ~(kHdrNeedsEsc | kHdrTreeEsc);
+  hdr[d].flags &= ~(kHdrNeedsEsc | kHdrTreeEsc | kHdrTreeBig);
 #pragma unroll
   for (int t = 0; t < kNumStats; t++) stats[(size_t)d * kNumStats + t] = 0;
 }
@@ -380,6 +382,13 @@ struct mte_ctx {
   uint32_t n_tree = 0;
   std::vector<uint8_t> h_legacy;    // per doc
   uint32_t* d_rs_docs = nullptr;    // legacy documents declared MTE_DOC_ROUND_SYNC (flat)
+  int tree_rounds = 4;              // TIER 0 / TIER 1 alternations (MTE_TREE_ROUNDS)
+  // node level (mte_comm_*): the RCCL communicator and its staging buffers
+  ncclComm_t comm = nullptr;
+  bool comm_owner = false;
+  int world = 1, rank = 0;
+  uint64_t* d_comm = nullptr;  // digests of all ranks / scalar reductions
+  uint64_t comm_cap = 0;       // uint64 elements
   uint32_t n_rs = 0;
   uint64_t* d_off = nullptr;
   uint64_t off_cap = 0;
@@ -498,8 +507,9 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
     // tree document), so the two streams share no document state
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->tree_stream, c->ev_fork, 0));
-    TreeArgs t{c->d_tree, c->d_heap, c->d_tree_docs, c->n_tree, c->arena};
-    HIPCHK(c, (launch_tree<K, S>(a, t, (c->n_tree + kDocsPerBlock - 1) / kDocsPerBlock, c->tree_stream)));
+    TreeArgs t{c->d_tree, c->d_heap, c->d_tree_docs, c->n_tree, c->arena, 0u};
+    HIPCHK(c, (launch_tree<K, S>(a, t, (c->n_tree + kDocsPerBlock - 1) / kDocsPerBlock, c->tree_stream,
+                                 c->tree_rounds)));
     HIPCHK(c, hipEventRecord(c->ev_join, c->tree_stream));
   }
   // pass 1: two documents per wavefront (docs up to 126 segments)
@@ -645,6 +655,10 @@ int mte_create(const mte_config* cfg, mte_ctx** out) {
   c->kt = cfg->n_keys == 0 ? 0 : (cfg->n_keys <= 4 ? 4 : 8);
   c->cap = cfg->seg_capacity ? cfg->seg_capacity : 1024;
   c->wclock_path = std::getenv("MTE_WAVE_CLOCK");
+  if (const char* r = std::getenv("MTE_TREE_ROUNDS")) {
+    const int v = std::atoi(r);
+    c->tree_rounds = v < 1 ? 1 : (v > 64 ? 64 : v);
+  }
   if (c->cap < 64) c->cap = 64;
   if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
@@ -679,6 +693,8 @@ int mte_destroy(mte_ctx* c) {
     if (c->stage[i]) (void)hipHostFree(c->stage[i]);
     if (c->stage_ev[i]) (void)hipEventDestroy(c->stage_ev[i]);
   }
+  if (c->comm && c->comm_owner) (void)ncclCommDestroy(c->comm);
+  if (c->d_comm) (void)hipFree(c->d_comm);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->tree_stream) (void)hipStreamDestroy(c->tree_stream);
@@ -1192,6 +1208,103 @@ int mte_read_segments(mte_ctx* c, uint32_t doc, mte_seg_list* v) {
 int mte_set_stats(mte_ctx* c, int enable) {
   if (!c) return MTE_E_INVALID_ARG;
   c->stats_on = enable != 0;
+  return MTE_OK;
+}
+
+// ---- node level over RCCL (include/mte.h) ----------------------------------
+
+#define NCCLCHK(ctx, expr)                                                                        \
+  do {                                                                                            \
+    ncclResult_t r_ = (expr);                                                                     \
+    if (r_ != ncclSuccess) return set_err(ctx, MTE_E_HIP, "%s: %s", #expr, ncclGetErrorString(r_)); \
+  } while (0)
+
+int mte_comm_unique_id(uint8_t id[MTE_COMM_ID_BYTES]) {
+  if (!id) return MTE_E_INVALID_ARG;
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return MTE_E_HIP;
+  static_assert(sizeof(u) == MTE_COMM_ID_BYTES, "ncclUniqueId size");
+  std::memcpy(id, &u, MTE_COMM_ID_BYTES);
+  return MTE_OK;
+}
+
+int mte_comm_init(mte_ctx* c, int world, int rank, const uint8_t id[MTE_COMM_ID_BYTES]) {
+  if (!c || !id || world < 1 || rank < 0 || rank >= world) return MTE_E_INVALID_ARG;
+  if (c->comm) return set_err(c, MTE_E_STATE, "mte_comm_init: already initialised");
+  HIPCHK(c, hipSetDevice(c->device));
+  ncclUniqueId u;
+  std::memcpy(&u, id, MTE_COMM_ID_BYTES);
+  NCCLCHK(c, ncclCommInitRank(&c->comm, world, u, rank));
+  c->comm_owner = true;
+  c->world = world;
+  c->rank = rank;
+  return MTE_OK;
+}
+
+int mte_comm_share(mte_ctx* c, const mte_ctx* src) {
+  if (!c || !src || !src->comm || src->device != c->device) return MTE_E_INVALID_ARG;
+  if (c->comm) return set_err(c, MTE_E_STATE, "mte_comm_share: already has a communicator");
+  c->comm = src->comm;
+  c->comm_owner = false;
+  c->world = src->world;
+  c->rank = src->rank;
+  return MTE_OK;
+}
+
+namespace {
+int comm_staging(mte_ctx* c, uint64_t n) {
+  if (n <= c->comm_cap) return MTE_OK;
+  if (c->d_comm) HIPCHK(c, hipFree(c->d_comm));
+  c->d_comm = nullptr;
+  HIPCHK(c, hipMalloc((void**)&c->d_comm, n * sizeof(uint64_t)));
+  c->comm_cap = n;
+  return MTE_OK;
+}
+}  // namespace
+
+int mte_comm_allreduce_f64(mte_ctx* c, double* v, int op) {
+  if (!c || !v || (op != MTE_COMM_SUM && op != MTE_COMM_MAX)) return MTE_E_INVALID_ARG;
+  if (!c->comm) return set_err(c, MTE_E_STATE, "mte_comm_init first");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = comm_staging(c, 1);
+  if (rc) return rc;
+  double* d = reinterpret_cast<double*>(c->d_comm);
+  HIPCHK(c, hipMemcpyAsync(d, v, sizeof(double), hipMemcpyHostToDevice, c->stream));
+  NCCLCHK(c, ncclAllReduce(d, d, 1, ncclFloat64, op == MTE_COMM_SUM ? ncclSum : ncclMax, c->comm, c->stream));
+  HIPCHK(c, hipMemcpyAsync(v, d, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MTE_OK;
+}
+
+int mte_comm_barrier(mte_ctx* c) {
+  double one = 1.0;
+  return mte_comm_allreduce_f64(c, &one, MTE_COMM_SUM);
+}
+
+int mte_comm_gather_digests(mte_ctx* c, uint64_t* out, uint32_t docs_per_rank) {
+  if (!c || !out || docs_per_rank < c->n_docs) return MTE_E_INVALID_ARG;
+  if (!c->comm) return set_err(c, MTE_E_STATE, "mte_comm_init first");
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint64_t per = 4ull * docs_per_rank;
+  int rc = comm_staging(c, per * (uint64_t)(c->world + 1));
+  if (rc) return rc;
+  uint64_t* send = c->d_comm + per * (uint64_t)c->world;  // after the receive area
+  HIPCHK(c, hipMemsetAsync(send, 0, per * sizeof(uint64_t), c->stream));
+  if (c->n_docs && (rc = mte_digest_device(c, send, c->n_docs))) return rc;
+  NCCLCHK(c, ncclAllGather(send, c->d_comm, per, ncclUint64, c->comm, c->stream));
+  HIPCHK(c, hipMemcpyAsync(out, c->d_comm, per * (uint64_t)c->world * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MTE_OK;
+}
+
+int mte_comm_destroy(mte_ctx* c) {
+  if (!c) return MTE_E_INVALID_ARG;
+  if (c->comm && c->comm_owner) NCCLCHK(c, ncclCommDestroy(c->comm));
+  c->comm = nullptr;
+  c->comm_owner = false;
+  c->world = 1;
+  c->rank = 0;
   return MTE_OK;
 }
 

@@ -34,7 +34,8 @@
 namespace mte {
 
 constexpr int kTreeHeapCap = 255;  // entries per document (+ the unused index 0)
-constexpr uint32_t kHdrTreeEsc = 0x40000000u;  // tree pass: continue in the E = 8 / 16 kernel
+constexpr uint32_t kHdrTreeEsc = 0x40000000u;  // tree pass: the document is TIER 1's (E = 4)
+constexpr uint32_t kHdrTreeBig = 0x20000000u;  // tree pass: the document is TIER 2's (E = 8, 16)
 constexpr uint32_t kTH = 0x7u, kTCont = 0x8u, kTNsShift = 4, kTNs = 0x30u, kTPo = 0x40u, kTEmpty = 0x80u;
 constexpr uint32_t kTNl = 0x80000000u;
 constexpr uint16_t kRecNl = 0x8000u;  // op record flag (engine-internal): the insert's text holds a '\n'
@@ -62,6 +63,7 @@ struct TreeArgs {
   const uint32_t* docs;  // the legacy documents
   uint32_t n_docs;
   const uint16_t* arena; // text (an append-merge looks at the last unit of a leaf)
+  uint32_t final_round;  // TIER 1: keep documents that shrink (no return to TIER 0)
 };
 
 __device__ __forceinline__ uint32_t t_h(uint32_t t) { return t & kTH; }
@@ -149,7 +151,7 @@ struct TreeRun {
   int depth;
   uint32_t next_id;
   uint32_t hn;   // LRU heap entries
-  uint2* hp;     // LDS heap of this wave, hp[1 .. hn]
+  volatile uint2* hp;  // LDS heap of this wave, hp[1 .. hn] (16-byte aligned)
   const uint16_t* arena;
 };
 
@@ -273,53 +275,60 @@ __device__ __forceinline__ void split_cascade(uint32_t (&T)[E], int i, int n, Tr
 }
 
 // ---- LRU heap (collections/heap.ts), uniform code over the LDS array ------------
+// The sifts move a hole instead of swapping (the same comparisons as heap.ts's
+// fixup / fixdown, so the same final array): the element being placed stays
+// in registers, each level of fixdown is one 16-byte read of both children
+// and one write, and LDS accesses through the volatile pointer stay in order
+// (a wave's LDS operations complete in order), so only reads are waited on.
 
-__device__ __forceinline__ void hp_put(uint2* hp, uint32_t k, uint2 v) {
-  if (lane_id() == 0) hp[k] = v;
-  fence_wave();
+__device__ __forceinline__ void hp_put(volatile uint2* hp, uint32_t k, uint2 v) {
+  if (lane_id() == 0) {
+    hp[k].x = v.x;
+    hp[k].y = v.y;
+  }
 }
-__device__ __forceinline__ uint2 hp_get(const uint2* hp, uint32_t k) {
-  const uint2 v = hp[k];
-  return make_uint2(uni(v.x), uni(v.y));
+__device__ __forceinline__ uint2 hp_get(volatile uint2* hp, uint32_t k) {
+  const uint32_t x = hp[k].x, y = hp[k].y;
+  return make_uint2(uni(x), uni(y));
 }
 
 __device__ __forceinline__ int heap_add(TreeRun& tr, int32_t key, uint32_t id) {
   if (tr.hn >= (uint32_t)kTreeHeapCap) return MTE_E_CAPACITY;
   uint32_t k = ++tr.hn;
-  hp_put(tr.hp, k, make_uint2((uint32_t)key, id));
+  // fixup: while the parent compares greater, it moves down into the hole
   while (k > 1) {
     const uint2 par = hp_get(tr.hp, k >> 1);
     if (!((int32_t)par.x - key > 0)) break;
     hp_put(tr.hp, k, par);
-    hp_put(tr.hp, k >> 1, make_uint2((uint32_t)key, id));
     k >>= 1;
   }
+  hp_put(tr.hp, k, make_uint2((uint32_t)key, id));
   return 0;
 }
 
 __device__ __forceinline__ uint2 heap_pop(TreeRun& tr) {
   const uint2 x = hp_get(tr.hp, 1);
-  const uint2 last = hp_get(tr.hp, tr.hn);
-  hp_put(tr.hp, 1, last);
+  const uint2 cur = hp_get(tr.hp, tr.hn);  // the last entry, re-placed from the root
   tr.hn--;
   uint32_t k = 1;
   while ((k << 1) <= tr.hn) {
     uint32_t j = k << 1;
-    const uint2 cj = hp_get(tr.hp, j);
-    uint2 c = cj;
+    // both children in one read (entries 2k, 2k + 1 are 16-byte aligned)
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u cc = *reinterpret_cast<const volatile v4u*>(tr.hp + j);
+    uint2 c = make_uint2(uni(cc[0]), uni(cc[1]));
     if (j < tr.hn) {
-      const uint2 cj1 = hp_get(tr.hp, j + 1);
-      if ((int32_t)cj.x - (int32_t)cj1.x > 0) {
+      const uint2 c1 = make_uint2(uni(cc[2]), uni(cc[3]));
+      if ((int32_t)c.x - (int32_t)c1.x > 0) {
         j++;
-        c = cj1;
+        c = c1;
       }
     }
-    const uint2 cur = hp_get(tr.hp, k);
     if ((int32_t)cur.x - (int32_t)c.x <= 0) break;
     hp_put(tr.hp, k, c);
-    hp_put(tr.hp, j, cur);
     k = j;
   }
+  if (tr.hn > 0) hp_put(tr.hp, k, cur);
   return x;
 }
 
@@ -338,76 +347,144 @@ __device__ __forceinline__ int add_lru(uint32_t (&T)[E], int i, int32_t seq, int
 // ---- scour / pack (titems.c scour, drop_keep_starts, pack_parent) ----------------
 
 // scourNode over the leaf block [s, e]: sets drop[] on unlinked items and the
-// cont bit on appended leaves; returns the logical leaves held
+// cont bit on appended leaves; returns the logical leaves held.
+//
+// Vector form of mergeTree.ts:681-757 (titems.c scour): every leaf of the
+// block is summarised in parallel — removed / kept tombstone / below minSeq /
+// text, "same properties and text as the leaf before it", "the leaf before it
+// ends in '\n'", its prefix length — and the summaries are gathered through
+// LDS so that leaf r sits in lane r.  The append chain (TextSegment.canAppend
+// with the running length of the leaf appended to) then runs as a scalar loop
+// over those lanes, and its drop / append masks are applied in one pass.  The
+// leaf appended to is always the one just before: a run's leaves carry its
+// head's properties, and an append needs a match with the run.
+constexpr uint32_t kScRemoved = 1u, kScKeep = 2u, kScElig = 4u, kScText = 8u, kScMatch = 16u, kScNl = 32u;
+
 template <int E, int K>
-__device__ __forceinline__ int scour(TReg<E, K>& X, int s, int e, int32_t min_seq, bool (&drop)[E], const TreeRun& tr, int n_keys) {
-  const int base = lane_id() * E;
+__device__ __forceinline__ int scour(TReg<E, K>& X, int s, int e, int n, int32_t min_seq, bool (&drop)[E],
+                                     const TreeRun& tr, int n_keys, uint32_t* zlds) {
+  const int l = lane_id();
+  const int base = l * E;
+  // previous item's T / len / toff (item base + j - 1)
+  uint32_t pT[E], pO[E];
+  int32_t pL[E];
+  pT[0] = (uint32_t)lane_prev((int32_t)X.T[E - 1]);
+  pL[0] = lane_prev(X.R.len[E - 1]);
+  pO[0] = (uint32_t)lane_prev((int32_t)X.R.toff[E - 1]);
+#pragma unroll
+  for (int j = 1; j < E; j++) {
+    pT[j] = X.T[j - 1];
+    pL[j] = X.R.len[j - 1];
+    pO[j] = X.R.toff[j - 1];
+  }
   bool head[E];
+  int32_t hc = 0, lsum = 0, PX[E];
 #pragma unroll
-  for (int j = 0; j < E; j++) head[j] = (X.T[j] & (kTCont | kTEmpty)) == 0;
-  int held = 0;
-  int prev = -1, prev_last = -1;  // head and last item of the leaf appends go to
-  int32_t prev_len = 0;
-  for (int i = first_where<E>(head, s); i >= 0 && i <= e;) {
-    int xe = first_where<E>(head, i + 1);
-    {
-      // a leaf's texts end at the next head or placeholder, or the block end
-      bool stop[E];
+  for (int j = 0; j < E; j++) {
+    const int i = base + j;
+    head[j] = i >= s && i <= e && (X.T[j] & (kTCont | kTEmpty)) == 0;
+    hc += head[j] ? 1 : 0;
+    PX[j] = lsum;
+    lsum += i < n ? X.R.len[j] : 0;
+  }
+  const int32_t hin = wave_incl_scan(hc), lin = wave_incl_scan(lsum);
+  const int m = rdlane(hin, kWave - 1);
+  const int32_t ltot = rdlane(lin, kWave - 1);
 #pragma unroll
-      for (int j = 0; j < E; j++) stop[j] = (X.T[j] & kTCont) == 0;
-      const int st = first_where<E>(stop, i + 1);
-      xe = st < 0 || st > e + 1 ? e + 1 : st;
+  for (int j = 0; j < E; j++) PX[j] += lin - lsum;
+  if (m == 0) return 0;
+  // the leaf before a head ends in '\n' (only texts that held one are loaded)
+  bool nlc[E];
+  bool any_nl = false;
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    nlc[j] = head[j] && (pT[j] & kTNl) && pL[j] > 0;
+    any_nl = any_nl || nlc[j];
+  }
+  uint32_t nlb[E];
+#pragma unroll
+  for (int j = 0; j < E; j++) nlb[j] = 0;
+  if (__ballot(any_nl)) {
+#pragma unroll
+    for (int j = 0; j < E; j++)
+      nlb[j] = (nlc[j] && tr.arena[pO[j] + (uint32_t)pL[j] - 1u] == (uint16_t)'\n') ? kScNl : 0u;
+  }
+  // leaf records by rank: [bits, PX, po, props...] (W words)
+  constexpr int W = 3 + K;
+  int32_t r0 = hin - hc;
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    if (head[j]) {
+      uint32_t* rec = zlds + r0 * W;
+      const uint32_t meta = X.R.meta[j];
+      uint32_t bits = nlb[j];
+      bits |= X.R.rseq[j] != kNone ? kScRemoved : 0u;
+      bits |= X.R.rseq[j] > min_seq ? kScKeep : 0u;
+      bits |= X.R.seq[j] <= min_seq ? kScElig : 0u;
+      bits |= (meta >> 8) == 0 ? kScText : 0u;
+      rec[0] = bits;
+      rec[1] = (uint32_t)PX[j];
+      rec[2] = X.T[j] & kTPo;
+#pragma unroll
+      for (int k = 0; k < K; k++) rec[3 + k] = k < n_keys ? X.R.pr[k][j] : 0u;
+      r0++;
     }
-    const int32_t xl = sum_range<E>(X.R.len, i, xe);
-    const int32_t rseq = bcast<E>(X.R.rseq, i), seq = bcast<E>(X.R.seq, i);
-    if (rseq != kNone) {
-      if (rseq > min_seq) {
-        held++;
-      } else {
+  }
+  fence_wave();
+  // lane r: leaf r's bits, with the match against leaf r - 1
+  uint32_t bits = 0, pxh = 0;
+  if (l < m) {
+    const uint32_t* rc = zlds + l * W;
+    bits = rc[0];
+    pxh = rc[1];
+    if (l > 0) {
+      const uint32_t* rp = rc - W;
+      bool match = (rp[0] & kScText) && (bits & kScText) && rp[2] == rc[2];
 #pragma unroll
-        for (int j = 0; j < E; j++) drop[j] = drop[j] || (base + j >= i && base + j < xe);
-      }
-      prev = -1;
-    } else if (seq <= min_seq) {
-      bool app = false;
-      if (prev >= 0) {
-        const uint32_t pm = bcast<E>(X.R.meta, prev), xm = bcast<E>(X.R.meta, i);
-        const uint32_t pt = bcast<E>(X.T, prev), xt = bcast<E>(X.T, i);
-        bool match = ((pt ^ xt) & kTPo) == 0;
-#pragma unroll
-        for (int k = 0; k < K; k++)
-          if (k < n_keys) match = match && bcast<E>(X.R.pr[k], prev) == bcast<E>(X.R.pr[k], i);
-        const bool text = (pm >> 8) == 0 && (xm >> 8) == 0;
-        bool nl = false;
-        if (text && (bcast<E>(X.T, prev_last) & kTNl)) {
-          const int32_t ll = bcast<E>(X.R.len, prev_last);
-          const uint32_t lo = bcast<E>(X.R.toff, prev_last);
-          nl = ll > 0 && tr.arena[lo + (uint32_t)ll - 1] == (uint16_t)'\n';
-        }
-        app = text && !nl && (prev_len <= kTextGranularity || xl <= kTextGranularity) && match && xl > 0;
-      }
+      for (int k = 0; k < K; k++) match = match && rp[3 + k] == rc[3 + k];
+      bits |= match ? kScMatch : 0u;
+    }
+  }
+  fence_wave();
+  const int32_t pend = e + 1 < n ? bcast<E>(PX, e + 1) : ltot;
+  // the append chain, leaf by leaf (scalar)
+  int held = 0;
+  uint64_t dropm = 0, contm = 0;
+  bool run = false;  // the leaf before can be appended to
+  int32_t run_len = 0;
+  for (int r = 0; r < m; r++) {
+    const uint32_t b = rdlane(bits, r);
+    const int32_t xl = (int32_t)((r + 1 < m ? rdlane(pxh, r + 1) : (uint32_t)pend) - rdlane(pxh, r));
+    if (b & kScRemoved) {
+      if (b & kScKeep) held++;
+      else dropm |= 1ull << r;
+      run = false;
+    } else if (b & kScElig) {
+      const bool app = run && (b & kScMatch) && !(b & kScNl) &&
+                       (run_len <= kTextGranularity || xl <= kTextGranularity) && xl > 0;
       if (app) {
-        // TextSegment.append: the leaf becomes texts of the previous one
-#pragma unroll
-        for (int j = 0; j < E; j++)
-          if (base + j == i) X.T[j] = (X.T[j] & ((0xffu & ~kTNs) | kTNl)) | kTCont;
-        prev_len += xl;
-        prev_last = xe - 1;
+        contm |= 1ull << r;
+        run_len += xl;
       } else {
         held++;
-        if (xl > 0) {
-          prev = i;
-          prev_len = xl;
-          prev_last = xe - 1;
-        } else {
-          prev = -1;
-        }
+        run = xl > 0;
+        run_len = xl;
       }
     } else {
       held++;
-      prev = -1;
+      run = false;
     }
-    i = xe <= e ? first_where<E>(head, xe) : -1;
+  }
+  // apply: items of dropped leaves, heads of appended ones
+  const int32_t hex = hin - hc;  // heads before this lane
+  int32_t rk = hex - 1;          // rank of the leaf the item belongs to
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    const int i = base + j;
+    rk += head[j] ? 1 : 0;
+    const bool inb = i >= s && i <= e && rk >= 0;
+    drop[j] = drop[j] || (inb && ((dropm >> rk) & 1ull));
+    if (head[j] && ((contm >> rk) & 1ull)) X.T[j] = (X.T[j] & ((0xffu & ~kTNs) | kTNl)) | kTCont;
   }
   return held;
 }
@@ -468,7 +545,7 @@ __device__ __forceinline__ int pack_parent(TReg<E, K>& X, int s, int p, int n, i
       for (int j = 0; j < E; j++) drop[j] = false;
       for (int b = s; b <= e;) {
         const int be = span_end<E>(X.T, b, 1, n);
-        scour<E, K>(X, b, be, min_seq, drop, tr, n_keys);
+        scour<E, K>(X, b, be, n, min_seq, drop, tr, n_keys, zlds);
         b = be + 1;
       }
       // held leaves (placeholders go too), re-packed
@@ -579,7 +656,7 @@ __device__ __forceinline__ int zamboni(TReg<E, K>& X, int n, int32_t min_seq, Tr
     bool drop[E];
 #pragma unroll
     for (int j = 0; j < E; j++) drop[j] = false;
-    const int held = scour<E, K>(X, bs, be, min_seq, drop, tr, n_keys);
+    const int held = scour<E, K>(X, bs, be, n, min_seq, drop, tr, n_keys, zlds);
     set_ns<E>(X.T, bs, kNsFalse);
     if (held < before) {
       n = drop_block<E, K>(X, bs, be, drop, n, zlds);
@@ -664,7 +741,7 @@ __device__ __forceinline__ int tree_step(TReg<E, K>& X, DocRun& D, TreeRun& tr, 
   int n = D.n;
   int status = 0;
   const bool newcalc = (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
-  uint64_t tq0 = 0, tq1 = 0, tq2 = 0, tq3 = 0;
+  [[maybe_unused]] uint64_t tq0 = 0, tq1 = 0, tq2 = 0, tq3 = 0;
   TPROF(tq0 = wall_clock64(); tq1 = tq2 = tq3 = tq0;)
 
   if (type == MTE_OP_INSERT || type == MTE_OP_REMOVE || type == MTE_OP_ANNOTATE) {
@@ -816,7 +893,7 @@ __device__ __forceinline__ int tree_step(TReg<E, K>& X, DocRun& D, TreeRun& tr, 
     D.cur_seq = s;
     if (msn > D.min_seq) {
       D.min_seq = msn;
-      uint64_t tz = 0;
+      [[maybe_unused]] uint64_t tz = 0;
       TPROF(tz = wall_clock64();)
       D.n = zamboni<E, K>(X, D.n, D.min_seq, tr, zlds, a.n_keys, status);
       TPROF(st[kStMaxSegs] += (uint32_t)(wall_clock64() - tz);)
@@ -880,30 +957,37 @@ __device__ __forceinline__ void tree_burst(DocRun& D, TreeRun& tr, const ReplayA
   if constexpr (S) run_flush_stats(D, st, a);
 }
 
-// The tree pass, three launches.  A kernel's register allocation is that of
-// its largest tier, so the tiers are split by size: TIER 0 runs E = 1, 2
-// (documents up to 124 items, ~130 VGPRs: 3 waves per SIMD); a document that
-// outgrows it is flagged kHdrTreeEsc and continues in TIER 1 (E = 1, 2, 4, up
-// to 252 items), then TIER 2 (E = 8, 16, up to 1,020 items).
+// The tree pass.  A kernel's register allocation is that of its largest tier,
+// so the tiers are separate kernels: TIER 0 runs E = 1, 2 (documents up to 124
+// items, ~137 VGPRs: 3 waves per SIMD), TIER 1 E = 4 (up to 252 items, ~225
+// VGPRs: 2 waves), TIER 2 E = 8, 16 (up to 1,020 items).  A document that
+// outgrows TIER 0 is flagged kHdrTreeEsc and continues in the TIER 1 launch
+// that follows; one that shrinks back (20 items of slack) returns to the next
+// TIER 0 launch, so a passing peak does not keep it at low occupancy for the
+// rest of the batch.  The host alternates TIER 0 / TIER 1 a few rounds (the
+// last TIER 1 keeps its documents), then runs TIER 2 (kHdrTreeBig) once.
 template <int K, bool S, int TIER>
 __global__ __launch_bounds__(256) void tree_kernel(ReplayArgs a, TreeArgs t) {
   constexpr int EMAX = TIER == 2 ? 16 : TIER == 1 ? 4 : 2;
+  constexpr uint32_t kTierFlags = kHdrTreeEsc | kHdrTreeBig;
   __shared__ uint32_t zlds_all[kDocsPerBlock][kWave * EMAX];
-  __shared__ uint2 heap_all[kDocsPerBlock][kTreeHeapCap + 1];
+  __shared__ __attribute__((aligned(16))) uint2 heap_all[kDocsPerBlock][kTreeHeapCap + 1];
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
   const int idx = (int)blockIdx.x * kDocsPerBlock + w;
   if (idx >= (int)t.n_docs) return;
   const int doc = uni((int)t.docs[idx]);
   const uint4 h0 = reinterpret_cast<const uint4*>(a.hdr + doc)[0], h1 = reinterpret_cast<const uint4*>(a.hdr + doc)[1];
   const uint32_t hflags = uni(h1.x);
-  if (TIER > 0 && !(hflags & kHdrTreeEsc)) return;
+  if (TIER == 0 && (hflags & kTierFlags)) return;
+  if (TIER == 1 && (hflags & kTierFlags) != kHdrTreeEsc) return;
+  if (TIER == 2 && !(hflags & kHdrTreeBig)) return;
   DocRun D;
   D.doc = doc;
   D.n = uni((int32_t)h0.x);
   D.min_seq = uni((int32_t)h0.y);
   D.cur_seq = uni((int32_t)h0.z);
   D.status = uni((int32_t)h0.w);
-  D.flags = hflags & ~kHdrTreeEsc;
+  D.flags = hflags & ~kTierFlags;
   D.k = uni(h1.y);
   const uint64_t kb = uni64(a.op_off[doc]);
   D.recp = a.recs + 2 * kb;
@@ -917,7 +1001,11 @@ __global__ __launch_bounds__(256) void tree_kernel(ReplayArgs a, TreeArgs t) {
   tr.hp = heap_all[w];
   tr.arena = t.arena;
   const uint2* hg = t.heap + (uint64_t)doc * (kTreeHeapCap + 1);
-  for (uint32_t k = (uint32_t)lane_id(); k <= tr.hn; k += kWave) tr.hp[k] = hg[k];
+  for (uint32_t k = (uint32_t)lane_id(); k <= tr.hn; k += kWave) {
+    const uint2 v = hg[k];
+    tr.hp[k].x = v.x;
+    tr.hp[k].y = v.y;
+  }
   fence_wave();
   uint32_t* zlds = zlds_all[w];
   while (D.running) {
@@ -934,20 +1022,20 @@ __global__ __launch_bounds__(256) void tree_kernel(ReplayArgs a, TreeArgs t) {
         break;
       }
     } else if constexpr (TIER == 1) {
-      if (n + 4 <= kWave) tree_burst<1, K, S>(D, tr, a, t, zlds, 1);
-      else if (n + 4 <= 2 * kWave) tree_burst<2, K, S>(D, tr, a, t, zlds, 1);
-      else if (n + 4 <= 4 * kWave) tree_burst<4, K, S>(D, tr, a, t, zlds, 1);
-      else {
-        D.flags |= kHdrTreeEsc;
+      if (n + 4 > 4 * kWave) {
+        D.flags |= kHdrTreeBig;
         break;
       }
+      if (!t.final_round && n + 4 + 16 <= 2 * kWave) break;  // back to TIER 0
+      tree_burst<4, K, S>(D, tr, a, t, zlds, t.final_round ? 4 : 2);
     } else {
       if (n + 4 <= 8 * kWave) tree_burst<8, K, S>(D, tr, a, t, zlds, 8);
       else tree_burst<16, K, S>(D, tr, a, t, zlds, 8);
     }
   }
   uint2* hw = t.heap + (uint64_t)doc * (kTreeHeapCap + 1);
-  for (uint32_t k = (uint32_t)lane_id(); k <= tr.hn; k += kWave) hw[k] = tr.hp[k];
+  fence_wave();
+  for (uint32_t k = (uint32_t)lane_id(); k <= tr.hn; k += kWave) hw[k] = make_uint2(tr.hp[k].x, tr.hp[k].y);
   if (lane_id() == 0) {
     DocHdr o;
     o.nseg = D.n;

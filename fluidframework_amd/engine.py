@@ -166,6 +166,31 @@ class DeviceEngine(EngineBase):
         """Statistics accounting on (default) / off (mte_set_stats)."""
         self._check(self.lib.mte_set_stats(self.ctx, 1 if enable else 0), "set_stats")
 
+    # ---- node level over RCCL (mte_comm_*, include/mte.h) ----
+    def comm_init(self, world, rank, uid: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self._check(self.lib.mte_comm_init(self.ctx, world, rank, buf), "comm_init")
+
+    def comm_share(self, other):
+        self._check(self.lib.mte_comm_share(self.ctx, other.ctx), "comm_share")
+
+    def comm_barrier(self):
+        self._check(self.lib.mte_comm_barrier(self.ctx), "comm_barrier")
+
+    def comm_allreduce(self, value: float, op="sum") -> float:
+        v = C.c_double(value)
+        self._check(self.lib.mte_comm_allreduce_f64(self.ctx, C.byref(v), 0 if op == "sum" else 1),
+                    "comm_allreduce")
+        return v.value
+
+    def comm_gather_digests(self, world, docs_per_rank):
+        out = np.zeros(world * docs_per_rank * 4, np.uint64)
+        self._check(self.lib.mte_comm_gather_digests(self.ctx, ptr(out), docs_per_rank), "comm_gather_digests")
+        return out.reshape(world, docs_per_rank, 4)
+
+    def comm_destroy(self):
+        self._check(self.lib.mte_comm_destroy(self.ctx), "comm_destroy")
+
     def digest_device(self, device_ptr):
         self._check(self.lib.mte_digest_device(self.ctx, C.c_void_p(device_ptr), self.n_docs),
                     "digest_device")

@@ -265,6 +265,35 @@ int mte_stats_get(mte_ctx* ctx, mte_stats* out);
  * mte_stats_get reports zero counts (kernel_ms stays valid). */
 int mte_set_stats(mte_ctx* ctx, int enable);
 
+/* ---- Node level: one process per GPU, RCCL over xGMI ----------------------
+ * Documents are independent, so the host shards them over the GPUs (one
+ * context each) and no collective touches the replay.  These
+ * entry points carry what the node-level job needs beside it, over RCCL: a
+ * barrier and scalar reductions for timing, and the verification all-gather of
+ * every rank's per-document digests.  The reference has no multi-process
+ * merge-tree (one Client per document per process); this replaces running
+ * those Clients in many processes and comparing their texts.
+ *
+ * mte_comm_unique_id runs on one rank; the host hands the 128 bytes to the
+ * others (any side channel) before every rank calls mte_comm_init.           */
+#define MTE_COMM_ID_BYTES 128
+#define MTE_COMM_SUM 0
+#define MTE_COMM_MAX 1
+int mte_comm_unique_id(uint8_t id[MTE_COMM_ID_BYTES]);
+int mte_comm_init(mte_ctx* ctx, int world, int rank, const uint8_t id[MTE_COMM_ID_BYTES]);
+/* Let another context of this process use src's communicator (not owned:
+ * mte_comm_destroy / mte_destroy of ctx leave it to src).  Collectives of the
+ * contexts sharing one communicator must not overlap in time.                */
+int mte_comm_share(mte_ctx* ctx, const mte_ctx* src);
+int mte_comm_barrier(mte_ctx* ctx);
+/* In place, across ranks: op = MTE_COMM_SUM / MTE_COMM_MAX. */
+int mte_comm_allreduce_f64(mte_ctx* ctx, double* value, int op);
+/* Digests of this context's documents, padded with zero rows to docs_per_rank
+ * (>= n_docs, equal on all ranks), gathered in rank order into `out` (host,
+ * world * docs_per_rank * 4 uint64).                                          */
+int mte_comm_gather_digests(mte_ctx* ctx, uint64_t* out, uint32_t docs_per_rank);
+int mte_comm_destroy(mte_ctx* ctx);
+
 #ifdef __cplusplus
 }
 #endif
