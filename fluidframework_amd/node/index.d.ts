@@ -129,6 +129,16 @@ export class MergeTreeEngine {
   statuses(): Int32Array;
   stats(): EngineStats;
   close(): void;
+  /** Node level (one process per GPU, RCCL over xGMI, mte_comm_*). */
+  commUniqueId(): Uint8Array;
+  joinNode(world: number, rank: number, id: Uint8Array): void;
+  shareNode(other: MergeTreeEngine): void;
+  nodeBarrier(): void;
+  nodeAllreduce(value: number, op?: "sum" | "max"): number;
+  gatherDigests(docsPerRank: number): BigUint64Array;
+  leaveNode(): void;
+  /** Documents -> ranks by expected work (LPT). */
+  static shardByWork(work: number[], world: number): number[];
 }
 
 export interface BatchMergeTree {

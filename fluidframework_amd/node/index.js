@@ -181,6 +181,66 @@ class MergeTreeEngine {
     return this.addon.stats(this.ctx);
   }
 
+  // ---- node level: one process per GPU, RCCL over xGMI (mte_comm_*) ----
+
+  /** 128-byte RCCL id; draw it on one rank and hand it to the others. */
+  commUniqueId() {
+    return this.addon.commUniqueId();
+  }
+
+  /** Join the node's communicator (every rank, with the same id). */
+  joinNode(world, rank, id) {
+    this.addon.commInit(this.ctx, world, rank, id);
+    this.world = world;
+    this.rank = rank;
+  }
+
+  /** Use another engine's communicator (one per process). */
+  shareNode(other) {
+    this.addon.commShare(this.ctx, other.ctx);
+    this.world = other.world;
+    this.rank = other.rank;
+  }
+
+  nodeBarrier() {
+    this.addon.commBarrier(this.ctx);
+  }
+
+  /** value summed (op "sum") or maximised ("max") over the ranks. */
+  nodeAllreduce(value, op) {
+    return this.addon.commAllreduce(this.ctx, value, op === "max" ? 1 : 0);
+  }
+
+  /** Every rank's per-doc digests, rank-major, each rank padded to docsPerRank. */
+  gatherDigests(docsPerRank) {
+    this.flush();
+    const out = new BigUint64Array(this.world * docsPerRank * 4);
+    this.addon.commGatherDigests(this.ctx, out, docsPerRank);
+    return out;
+  }
+
+  leaveNode() {
+    this.addon.commDestroy(this.ctx);
+  }
+
+  /**
+   * Documents -> ranks, balanced by their expected replay work (SURVEY.md 8(e):
+   * ops x mean live segments per document): longest first onto the least
+   * loaded rank (LPT).  Returns the rank of every document.
+   */
+  static shardByWork(work, world) {
+    const order = Array.from(work.keys()).sort((a, b) => work[b] - work[a] || a - b);
+    const load = new Array(world).fill(0);
+    const rankOf = new Array(work.length).fill(0);
+    for (const d of order) {
+      let r = 0;
+      for (let k = 1; k < world; k++) if (load[k] < load[r]) r = k;
+      rankOf[d] = r;
+      load[r] += work[d];
+    }
+    return rankOf;
+  }
+
   close() {
     if (this.ctx) {
       this.addon.destroy(this.ctx);

@@ -432,6 +432,101 @@ static napi_value js_stats(napi_env env, napi_callback_info info) {
   return o;
 }
 
+/* ---- node level over RCCL (mte_comm_*) ---- */
+/* commUniqueId() -> Uint8Array(128) */
+static napi_value js_comm_unique_id(napi_env env, napi_callback_info info) {
+  (void)info;
+  napi_value ab, ta;
+  void* p = NULL;
+  NAPI_CALL(env, napi_create_arraybuffer(env, MTE_COMM_ID_BYTES, &p, &ab));
+  if (throw_rc(env, mte_comm_unique_id((uint8_t*)p), NULL, "mte_comm_unique_id")) return NULL;
+  NAPI_CALL(env, napi_create_typedarray(env, napi_uint8_array, MTE_COMM_ID_BYTES, ab, 0, &ta));
+  return ta;
+}
+
+/* commInit(ctx, world, rank, id Uint8Array(128)) */
+static napi_value js_comm_init(napi_env env, napi_callback_info info) {
+  napi_value argv[4];
+  if (!get_args(env, info, 4, argv)) return NULL;
+  mte_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  int32_t world = 0, rank = 0;
+  NAPI_CALL(env, napi_get_value_int32(env, argv[1], &world));
+  NAPI_CALL(env, napi_get_value_int32(env, argv[2], &rank));
+  void* id;
+  size_t n;
+  if (!get_bytes(env, argv[3], &id, &n)) return NULL;
+  if (n != MTE_COMM_ID_BYTES) {
+    throw_rc(env, MTE_E_INVALID_ARG, ctx, "commInit: id must be 128 bytes");
+    return NULL;
+  }
+  throw_rc(env, mte_comm_init(ctx, world, rank, (const uint8_t*)id), ctx, "mte_comm_init");
+  return NULL;
+}
+
+/* commShare(ctx, srcCtx) */
+static napi_value js_comm_share(napi_env env, napi_callback_info info) {
+  napi_value argv[2];
+  if (!get_args(env, info, 2, argv)) return NULL;
+  mte_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  mte_ctx* src = get_ctx(env, argv[1]);
+  if (!src) return NULL;
+  throw_rc(env, mte_comm_share(ctx, src), ctx, "mte_comm_share");
+  return NULL;
+}
+
+/* commBarrier(ctx) */
+static napi_value js_comm_barrier(napi_env env, napi_callback_info info) {
+  napi_value argv[1];
+  if (!get_args(env, info, 1, argv)) return NULL;
+  mte_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  throw_rc(env, mte_comm_barrier(ctx), ctx, "mte_comm_barrier");
+  return NULL;
+}
+
+/* commAllreduce(ctx, value, op 0 sum / 1 max) -> number */
+static napi_value js_comm_allreduce(napi_env env, napi_callback_info info) {
+  napi_value argv[3], r;
+  if (!get_args(env, info, 3, argv)) return NULL;
+  mte_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  double v = 0;
+  int32_t op = 0;
+  NAPI_CALL(env, napi_get_value_double(env, argv[1], &v));
+  NAPI_CALL(env, napi_get_value_int32(env, argv[2], &op));
+  if (throw_rc(env, mte_comm_allreduce_f64(ctx, &v, op), ctx, "mte_comm_allreduce_f64")) return NULL;
+  NAPI_CALL(env, napi_create_double(env, v, &r));
+  return r;
+}
+
+/* commGatherDigests(ctx, out BigUint64Array(world * docsPerRank * 4), docsPerRank) */
+static napi_value js_comm_gather_digests(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  if (!get_args(env, info, 3, argv)) return NULL;
+  mte_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  void* out;
+  size_t n;
+  if (!get_bytes(env, argv[1], &out, &n)) return NULL;
+  uint32_t per = 0;
+  NAPI_CALL(env, napi_get_value_uint32(env, argv[2], &per));
+  (void)n;
+  throw_rc(env, mte_comm_gather_digests(ctx, (uint64_t*)out, per), ctx, "mte_comm_gather_digests");
+  return NULL;
+}
+
+/* commDestroy(ctx) */
+static napi_value js_comm_destroy(napi_env env, napi_callback_info info) {
+  napi_value argv[1];
+  if (!get_args(env, info, 1, argv)) return NULL;
+  mte_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  throw_rc(env, mte_comm_destroy(ctx), ctx, "mte_comm_destroy");
+  return NULL;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
   const napi_property_descriptor d[] = {
       {"abiVersion", NULL, js_abi_version, NULL, NULL, NULL, napi_enumerable, NULL},
@@ -450,6 +545,13 @@ static napi_value init(napi_env env, napi_value exports) {
       {"readDoc", NULL, js_read_doc, NULL, NULL, NULL, napi_enumerable, NULL},
       {"readSegments", NULL, js_read_segments, NULL, NULL, NULL, napi_enumerable, NULL},
       {"stats", NULL, js_stats, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"commUniqueId", NULL, js_comm_unique_id, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"commInit", NULL, js_comm_init, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"commShare", NULL, js_comm_share, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"commBarrier", NULL, js_comm_barrier, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"commAllreduce", NULL, js_comm_allreduce, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"commGatherDigests", NULL, js_comm_gather_digests, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"commDestroy", NULL, js_comm_destroy, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   if (napi_define_properties(env, exports, sizeof d / sizeof d[0], d) != napi_ok) return NULL;
   return exports;

@@ -24,7 +24,8 @@ ADDON = os.path.join(ROOT, "fluidframework_amd", "_lib", "mte_napi.node")
 pytestmark = pytest.mark.skipif(NODE is None, reason="node not installed")
 
 EXPORTS = ["abiVersion", "strerror", "create", "destroy", "lastError", "loadDocs", "loadSegments", "readSegments", "submit", "run",
-           "sync", "reset", "digest", "docStatus", "readDoc", "stats"]
+           "sync", "reset", "digest", "docStatus", "readDoc", "stats", "commUniqueId", "commInit", "commShare",
+           "commBarrier", "commAllreduce", "commGatherDigests", "commDestroy"]
 
 
 def node(*args, timeout=300):
@@ -215,3 +216,38 @@ def test_node_read_outs_reject_wrong_nkeys_on_gpu():
                      "for(const f of ['readDoc','readSegments'])try{m[f](c,0,5)}catch(e){r.push(e.code)}"
                      "m.destroy(c);console.log(JSON.stringify(r))", ADDON)
     assert json.loads(out) == [-1, -1]
+
+
+def test_node_shard_by_work_balances():
+    out = node("-e", "const {MergeTreeEngine}=require('./fluidframework_amd/node');"
+                     "const w=[];for(let i=0;i<1000;i++)w.push(1+((i*7919)%97));"
+                     "const r=MergeTreeEngine.shardByWork(w,8);const l=new Array(8).fill(0);"
+                     "r.forEach((k,i)=>{l[k]+=w[i]});console.log(JSON.stringify(l))")
+    loads = json.loads(out)
+    assert max(loads) - min(loads) <= 97  # LPT: within the largest item
+
+
+@pytest.mark.gpu
+def test_node_one_rank_communicator_on_gpu():
+    # mte_comm_* through N-API on the box's one GPU: the gathered digests are the engine's
+    script = r"""
+const { MergeTreeEngine } = require("./fluidframework_amd/node");
+const node = new MergeTreeEngine({ nKeys: 0 });
+node.joinNode(1, 0, node.commUniqueId());
+node.nodeBarrier();
+const eng = new MergeTreeEngine({ nKeys: 4 });
+const c = eng.createClient("hello");
+c.applyMsg({ clientId: "b", sequenceNumber: 1, referenceSequenceNumber: 0, minimumSequenceNumber: 0, type: "op",
+  contents: { type: 0, pos1: 5, seg: " world" } });
+eng.shareNode(node);
+const g = eng.gatherDigests(4);
+const d = eng.digests();
+const out = { sum: node.nodeAllreduce(3, "sum"), max: node.nodeAllreduce(-2, "max"), text: c.getText(),
+  equal: [0, 1, 2, 3].every((i) => g[i] === d[i]), pad: g.slice(4).every((x) => x === 0n) };
+eng.close();
+node.leaveNode();
+node.close();
+process.stdout.write(JSON.stringify(out));
+"""
+    j = json.loads(node("-e", script))
+    assert j == {"sum": 3, "max": -2, "text": "hello world", "equal": True, "pad": True}
