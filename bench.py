@@ -208,6 +208,8 @@ def main():
                          "checked per batch) or on the tree pass")
     ap.add_argument("--no-tree-leg", action="store_true", help="skip the tree-placement side measurement")
     ap.add_argument("--no-weak-leg", action="store_true", help="skip the weak-scaling side measurement (N > 1)")
+    ap.add_argument("--no-node-leg", action="store_true", help="skip the Node host end-to-end measurement")
+    ap.add_argument("--node-docs", type=int, default=100, help="documents in the Node host sample")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stats", action="store_true",
@@ -320,6 +322,10 @@ def main():
             node.close()
         return
 
+    node_e2e = None
+    if world == 1 and not args.no_node_leg and stream.get("segs") is None:
+        node_e2e = node_end_to_end(stream, digest, args.node_docs)
+
     cpu = None
     parity = None
     if world == 1 and not args.no_cpu_baseline:
@@ -374,6 +380,7 @@ def main():
         },
         "end_to_end": {"ops_per_s": n_ops_rank / e2e_s, "ms": e2e_s * 1e3,
                        "includes": "mte_submit (host->HBM op upload) + reset + replay + digest read-back, rank 0"},
+        "end_to_end_node": node_e2e,
         "tree_placement": tree_leg,
         "weak_scaling": weak_leg,
         "cpu_baseline": cpu,
@@ -385,6 +392,38 @@ def main():
     print(json.dumps(out), flush=True)
     if node is not None:
         node.close()
+
+
+def node_end_to_end(stream, gpu_digest, n_docs):
+    """The Node host path on a bounded sample (fluidframework_amd/node/bench_e2e.js):
+    message objects -> BatchClient.applyMsg (JS packing) -> flush (mte_submit +
+    mte_run + mte_sync over N-API) -> digests, checked against the GPU run."""
+    import shutil
+    import subprocess
+
+    from fluidframework_amd import messages
+    node = shutil.which("node")
+    if node is None:
+        return {"skipped": "node not installed"}
+    m = min(n_docs, len(stream["inits"]))
+    docs = messages.stream_docs(stream, 0, m, segs=False)
+    t0 = time.perf_counter()
+    r = subprocess.run([node, "--max-old-space-size=8192", os.path.join(ROOT, "fluidframework_amd", "node",
+                                                                         "bench_e2e.js")],
+                       input=json.dumps({"docs": docs, "reps": 3}), capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"error": r.stderr[-2000:]}
+    j = json.loads(r.stdout)
+    got = np.array([int(x, 16) for x in j["digests"]], dtype=np.uint64).reshape(-1, 4)
+    b = j["best"]
+    return {"ops_per_s": j["ops_per_s"], "ms": b["pack_ms"] + b["flush_ms"], "pack_ms": b["pack_ms"],
+            "flush_ms": b["flush_ms"], "docs": m, "ops": j["ops"], "errors": b["errors"],
+            "digest_equal": bool(np.array_equal(got, gpu_digest[:m])),
+            "pipelined": j["pipelined"],
+            "includes": "BatchClient.applyMsg (JS packing) + flush (N-API mte_submit upload + mte_run + mte_sync); "
+                        "message objects built before the clock; 'pipelined': the messages in 4 slices, each "
+                        "flushed as packed (packing + upload of slice i+1 overlap the replay of slice i)",
+            "wall_s": round(time.perf_counter() - t0, 1)}
 
 
 def cpu_baseline(stream, gpu_digest, target_s):

@@ -58,10 +58,20 @@ def exchange_id(rank: int, timeout: float = 120.0) -> bytes:
 
 
 def join(engine, rank: int, world: int):
-    """Initialise engine's communicator; rank 0 removes the id file after all joined."""
+    """Initialise engine's communicator; rank 0 removes the id file after all joined.
+    RCCL prints a version banner on stdout at init: it goes to stderr, so the
+    job's stdout stays its own (bench.py prints one JSON line there)."""
     uid = exchange_id(rank)
-    engine.comm_init(world, rank, uid)
-    engine.comm_barrier()
+    import sys
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        engine.comm_init(world, rank, uid)
+        engine.comm_barrier()
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
     if rank == 0:
         try:
             os.remove(_id_path())

@@ -369,10 +369,29 @@ struct mte_ctx {
   std::vector<mte_prop> h_load_pe;
 
   // batch
+  // Two batch slots: mte_submit fills one (validation, pinned staging, DMA on
+  // up_stream) while a replay of the other may still run on `stream`; a slot is
+  // rewritten only after the last run that read it (slot_ev).  mte_run replays
+  // the slot last submitted (rslot).
+  hipStream_t up_stream = nullptr;
+  int rslot = 0;
+  hipEvent_t slot_ev[2] = {nullptr, nullptr};
+  mte_op* d_ops_s[2] = {nullptr, nullptr};
+  uint64_t ops_cap_s[2] = {0, 0};
+  uint4* d_cps_s[2] = {nullptr, nullptr};  // compiled propsets, 2 x uint4 each (props_kernel)
+  uint64_t cps_cap_s[2] = {0, 0};
+  uint64_t* d_off_s[2] = {nullptr, nullptr};
+  uint64_t off_cap_s[2] = {0, 0};
+  mte_propset* d_ps_s[2] = {nullptr, nullptr};
+  uint64_t ps_cap_s[2] = {0, 0};
+  mte_prop* d_pe_s[2] = {nullptr, nullptr};
+  uint64_t pe_cap_s[2] = {0, 0};
+  uint64_t n_ops_s[2] = {0, 0}, n_propsets_s[2] = {0, 0};
+  uint32_t text_base_s[2] = {0, 0};
+  // the batch mte_run replays (= slot rslot)
   mte_op* d_ops = nullptr;
-  uint64_t ops_cap = 0, n_ops = 0;
-  uint4* d_cps = nullptr;  // compiled propsets, 2 x uint4 each (props_kernel)
-  uint64_t cps_cap = 0, n_propsets = 0;
+  uint4* d_cps = nullptr;
+  uint64_t n_ops = 0, n_propsets = 0;
   uint32_t* d_pairs = nullptr;  // pass-1 doc pairs (new length calc documents)
   uint32_t n_pairs = 0;
   // tree pass (legacy length calc documents, mte_tree.h)
@@ -391,11 +410,8 @@ struct mte_ctx {
   uint64_t comm_cap = 0;       // uint64 elements
   uint32_t n_rs = 0;
   uint64_t* d_off = nullptr;
-  uint64_t off_cap = 0;
   mte_propset* d_ps = nullptr;
-  uint64_t ps_cap = 0;
   mte_prop* d_pe = nullptr;
-  uint64_t pe_cap = 0;
   uint32_t batch_text_base = 0;
 };
 
@@ -555,7 +571,7 @@ unsigned host_workers() {
 // threads into pinned staging buffers, each buffer's DMA overlapping the
 // filling of the next (pageable hipMemcpy runs at a fraction of PCIe speed).
 // Returns MTE_OK or MTE_E_INVALID_ARG with *bad = the first bad record.
-int upload_ops(mte_ctx* c, const mte_batch* b, uint64_t* bad, const char** why) {
+int upload_ops(mte_ctx* c, const mte_batch* b, int w, uint64_t* bad, const char** why) {
   for (int i = 0; i < mte_ctx::kStages; i++) {
     if (!c->stage[i]) HIPCHK(c, hipHostMalloc(&c->stage[i], mte_ctx::kStageBytes, hipHostMallocDefault));
     if (!c->stage_ev[i]) HIPCHK(c, hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
@@ -602,10 +618,10 @@ int upload_ops(mte_ctx* c, const mte_batch* b, uint64_t* bad, const char** why) 
     }
     for (auto& t : th) t.join();
     if (first_bad.load() != UINT64_MAX) break;
-    HIPCHK(c, hipMemcpyAsync(c->d_ops + k0, dst, n * sizeof(mte_op), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipEventRecord(c->stage_ev[si], c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_ops_s[w] + k0, dst, n * sizeof(mte_op), hipMemcpyHostToDevice, c->up_stream));
+    HIPCHK(c, hipEventRecord(c->stage_ev[si], c->up_stream));
   }
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->up_stream));
   if (first_bad.load() != UINT64_MAX) {
     *bad = first_bad.load();
     *why = "bad record";
@@ -686,9 +702,16 @@ int mte_destroy(mte_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   free_docs(c);
-  void* ps[] = {c->arena, c->d_ops, c->d_cps, c->d_off, c->d_ps, c->d_pe, c->d_pow, c->d_gdone};
+  void* ps[] = {c->arena, c->d_pow, c->d_gdone};
   for (void* p : ps)
     if (p) (void)hipFree(p);
+  for (int w = 0; w < 2; w++) {
+    void* sl[] = {c->d_ops_s[w], c->d_cps_s[w], c->d_off_s[w], c->d_ps_s[w], c->d_pe_s[w]};
+    for (void* p : sl)
+      if (p) (void)hipFree(p);
+    if (c->slot_ev[w]) (void)hipEventDestroy(c->slot_ev[w]);
+  }
+  if (c->up_stream) (void)hipStreamDestroy(c->up_stream);
   for (int i = 0; i < mte_ctx::kStages; i++) {
     if (c->stage[i]) (void)hipHostFree(c->stage[i]);
     if (c->stage_ev[i]) (void)hipEventDestroy(c->stage_ev[i]);
@@ -932,37 +955,58 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
   if (c->arena_n + b->text_units >= (1ull << 32)) return set_err(c, MTE_E_OOM, "text arena exceeds 2^32 units");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
+  if (!c->up_stream) {
+    HIPCHK(c, hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking));
+    for (int i = 0; i < 2; i++) HIPCHK(c, hipEventCreateWithFlags(&c->slot_ev[i], hipEventDisableTiming));
+  }
+  // the other slot than the one mte_run replays now; its buffers are written
+  // once the last run that read them is done
+  const int w = c->submitted ? c->rslot ^ 1 : c->rslot;
+  HIPCHK(c, hipStreamWaitEvent(c->up_stream, c->slot_ev[w], 0));
   // the replay kernels read the records in place; kRecPad zeroed records
   // follow the last one for the L2 prefetch that runs ahead
-  if ((rc = grow(c, &c->d_ops, &c->ops_cap, b->n_ops + kRecPad))) return rc;
-  HIPCHK(c, hipMemsetAsync(c->d_ops + b->n_ops, 0, kRecPad * sizeof(mte_op), c->stream));
-  if ((rc = grow(c, &c->d_off, &c->off_cap, (uint64_t)b->n_docs + 1))) return rc;
-  if ((rc = grow(c, &c->d_ps, &c->ps_cap, (uint64_t)b->n_propsets + 1))) return rc;
-  if ((rc = grow(c, &c->d_pe, &c->pe_cap, (uint64_t)b->n_props + 1))) return rc;
+  if ((rc = grow(c, &c->d_ops_s[w], &c->ops_cap_s[w], b->n_ops + kRecPad))) return rc;
+  HIPCHK(c, hipMemsetAsync(c->d_ops_s[w] + b->n_ops, 0, kRecPad * sizeof(mte_op), c->up_stream));
+  if ((rc = grow(c, &c->d_off_s[w], &c->off_cap_s[w], (uint64_t)b->n_docs + 1))) return rc;
+  if ((rc = grow(c, &c->d_ps_s[w], &c->ps_cap_s[w], (uint64_t)b->n_propsets + 1))) return rc;
+  if ((rc = grow(c, &c->d_pe_s[w], &c->pe_cap_s[w], (uint64_t)b->n_props + 1))) return rc;
+  if ((rc = grow(c, &c->d_cps_s[w], &c->cps_cap_s[w], 2 * ((uint64_t)b->n_propsets + 1)))) return rc;
   if (b->n_ops) {
-    // every record is validated on the way (no kernel may index out of bounds)
+    // every record is validated on the way (no kernel may index out of bounds);
+    // the host validates and stages while the previous batch may replay
     uint64_t bad = 0;
     const char* why = "";
-    c->submitted = false;
-    if ((rc = upload_ops(c, b, &bad, &why)))
+    if ((rc = upload_ops(c, b, w, &bad, &why)))
       return rc == MTE_E_INVALID_ARG ? set_err(c, rc, "op %llu: %s", (unsigned long long)bad, why) : rc;
   }
-  // append batch text to the arena
+  // append batch text to the arena (a running replay reads only below arena_n;
+  // growing it waits for the replay)
   if ((rc = grow(c, &c->arena, &c->arena_cap, c->arena_n + b->text_units + 1, true, c->arena_n))) return rc;
   if (b->text_units)
-    HIPCHK(c, hipMemcpyAsync(c->arena + c->arena_n, b->text, b->text_units * 2, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->arena + c->arena_n, b->text, b->text_units * 2, hipMemcpyHostToDevice, c->up_stream));
   c->h_arena.insert(c->h_arena.end(), b->text, b->text + b->text_units);
-  c->batch_text_base = (uint32_t)c->arena_n;
+  c->text_base_s[w] = (uint32_t)c->arena_n;
   c->arena_n += b->text_units;
-  HIPCHK(c, hipMemcpyAsync(c->d_off, b->op_offsets, ((uint64_t)b->n_docs + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_off_s[w], b->op_offsets, ((uint64_t)b->n_docs + 1) * 8, hipMemcpyHostToDevice,
+                           c->up_stream));
   if (b->n_propsets)
-    HIPCHK(c, hipMemcpyAsync(c->d_ps, b->propsets, b->n_propsets * sizeof(mte_propset), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_ps_s[w], b->propsets, b->n_propsets * sizeof(mte_propset), hipMemcpyHostToDevice,
+                             c->up_stream));
   if (b->n_props)
-    HIPCHK(c, hipMemcpyAsync(c->d_pe, b->props, b->n_props * sizeof(mte_prop), hipMemcpyHostToDevice, c->stream));
-  if ((rc = grow(c, &c->d_cps, &c->cps_cap, 2 * ((uint64_t)b->n_propsets + 1)))) return rc;
-  HIPCHK(c, hipStreamSynchronize(c->stream));  // host buffers may be freed after return
+    HIPCHK(c, hipMemcpyAsync(c->d_pe_s[w], b->props, b->n_props * sizeof(mte_prop), hipMemcpyHostToDevice,
+                             c->up_stream));
+  HIPCHK(c, hipStreamSynchronize(c->up_stream));  // host buffers may be freed after return
+  c->n_ops_s[w] = b->n_ops;
+  c->n_propsets_s[w] = b->n_propsets;
+  c->rslot = w;
+  c->d_ops = c->d_ops_s[w];
+  c->d_cps = c->d_cps_s[w];
+  c->d_off = c->d_off_s[w];
+  c->d_ps = c->d_ps_s[w];
+  c->d_pe = c->d_pe_s[w];
   c->n_ops = b->n_ops;
   c->n_propsets = b->n_propsets;
+  c->batch_text_base = c->text_base_s[w];
   c->submitted = true;
   return MTE_OK;
 }
@@ -1021,6 +1065,7 @@ int mte_run(mte_ctx* c) {
                     : (c->kt == 4 ? launch_replay<4, false>(c, a) : launch_replay<8, false>(c, a));
   if (rc) return rc;
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  HIPCHK(c, hipEventRecord(c->slot_ev[c->rslot], c->stream));  // the slot may be rewritten after this
   c->ran = true;
   return MTE_OK;
 }

@@ -113,6 +113,30 @@ def generate(config_id=2, n_docs=None, ops_per_doc=None, doc_base=0, n_threads=N
                       "propsets": ps, "props": pe}, "params": p}
 
 
+def split_ops(stream, k, parts):
+    """Batch k of `parts`: every document's ops [k/parts, (k+1)/parts) of its
+    count, cut at message ends (MTE_F_MSG_END) so windows stay whole."""
+    b = stream["batch"]
+    o = b["op_offsets"].astype(np.int64)
+    ops = b["ops"]
+    sel, offs = [], [0]
+    for d in range(len(o) - 1):
+        n = o[d + 1] - o[d]
+        ends = np.flatnonzero(ops["flags"][o[d]:o[d + 1]] & 2) + 1  # cut points after MSG_END records
+        def cut(x):
+            if x <= 0:
+                return 0
+            if x >= n:
+                return int(n)
+            i = np.searchsorted(ends, x)
+            return int(ends[i]) if i < len(ends) else int(n)
+        a, e = cut(n * k // parts), cut(n * (k + 1) // parts)
+        sel.append(np.arange(o[d] + a, o[d] + e))
+        offs.append(offs[-1] + (e - a))
+    idx = np.concatenate(sel) if sel else np.zeros(0, np.int64)
+    return dict(b, ops=ops[idx], op_offsets=np.array(offs, np.uint64))
+
+
 def preload_segments(inits, n_per_doc):
     """-> (seg_offsets, segs): every doc's load text as one-unit seq-0 segments
     (a summary body of n_per_doc segments, loaded with mte_load_segments)."""

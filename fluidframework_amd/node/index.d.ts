@@ -58,6 +58,10 @@ export interface ClientOptions {
   props?: PropertySet;
   minSeq?: number;
   currentSeq?: number;
+  /** Declare the document's stream round-synchronous (MTE_DOC_ROUND_SYNC): a
+   *  legacy length-calc document then replays on the flat passes; a batch
+   *  breaking the declaration stops it with code -9. */
+  roundSync?: boolean;
   /** Load a summary body instead of initialText (SnapshotLoader.loadBody). */
   segments?: SegmentWithMergeInfo[];
   /** Load a legacy summary (SnapshotLegacy blobs) and queue its catch-up ops. */
@@ -124,7 +128,10 @@ export class MergeTreeEngine {
   readonly nKeys: number;
   createClient(initialText?: string, options?: ClientOptions): BatchClient;
   start(): void;
+  /** Launch the replay of every queued message (returns before it ends). */
   flush(): void;
+  /** Wait for the launched replay (every read-out does). */
+  sync(): void;
   digests(): BigUint64Array;
   statuses(): Int32Array;
   stats(): EngineStats;

@@ -93,7 +93,7 @@ class MergeTreeEngine {
     if (o.summary) o = Object.assign({}, o, { legacy: o.summary });
     if (o.legacy) o = Object.assign({}, o, loadLegacy(o.legacy));
     const doc = this.docs.length;
-    this.docs.push({ text: initialText || "", newLengthCalc: !!o.newLengthCalc, props: o.props,
+    this.docs.push({ text: initialText || "", newLengthCalc: !!o.newLengthCalc, roundSync: !!o.roundSync, props: o.props,
       minSeq: o.minSeq || 0, currentSeq: o.currentSeq || 0, segments: o.segments });
     const c = new BatchClient(this, doc, o.observerId === undefined ? "A" : o.observerId);
     this.clients.push(c);
@@ -139,7 +139,10 @@ class MergeTreeEngine {
     return this.pending;
   }
 
-  /** Replay every queued message of every document on the GPU. */
+  /** Replay every queued message of every document on the GPU.  Returns once
+   *  the replay is launched: the next messages can be packed (and the next
+   *  flush uploaded, into the engine's other batch slot) while it runs; every
+   *  read-out waits for it. */
   flush() {
     this.start();
     if (this.pending.count === 0) return;
@@ -148,11 +151,20 @@ class MergeTreeEngine {
     this.views.fill(null);
     this.addon.submit(this.ctx, b.offsets, b.ops, b.text, b.propsets, b.props);
     this.addon.run(this.ctx);
-    this.addon.sync(this.ctx);
+    this.running = true;
+  }
+
+  /** Wait for the launched replay (read-outs call it). */
+  sync() {
+    if (this.running) {
+      this.running = false;
+      this.addon.sync(this.ctx);
+    }
   }
 
   _view(doc) {
     this.flush();
+    this.sync();
     let v = this.views[doc];
     if (v === null) {
       v = this.addon.readDoc(this.ctx, doc, this.nKeys);
@@ -165,6 +177,7 @@ class MergeTreeEngine {
   /** Per-doc canonical digests (4 x u64 each, DESIGN.md "Digest"). */
   digests() {
     this.flush();
+    this.sync();
     const out = new BigUint64Array(this.docs.length * 4);
     this.addon.digest(this.ctx, out);
     return out;
@@ -172,6 +185,7 @@ class MergeTreeEngine {
 
   statuses() {
     this.flush();
+    this.sync();
     const out = new Int32Array(this.docs.length);
     this.addon.docStatus(this.ctx, out);
     return out;
@@ -214,6 +228,7 @@ class MergeTreeEngine {
   /** Every rank's per-doc digests, rank-major, each rank padded to docsPerRank. */
   gatherDigests(docsPerRank) {
     this.flush();
+    this.sync();
     const out = new BigUint64Array(this.world * docsPerRank * 4);
     this.addon.commGatherDigests(this.ctx, out, docsPerRank);
     return out;
@@ -243,6 +258,7 @@ class MergeTreeEngine {
 
   close() {
     if (this.ctx) {
+      this.sync();
       this.addon.destroy(this.ctx);
       this.ctx = null;
     }

@@ -39,6 +39,7 @@ const DOC_NEW_LENGTH_CALC = 0x1;
 // MergeTreeDeltaType, ops.ts:43-48
 const INSERT = 0, REMOVE = 1, ANNOTATE = 2, GROUP = 3;
 
+const DOC_ROUND_SYNC = 0x2; // MTE_DOC_ROUND_SYNC (include/mte.h)
 const E_INVALID_ARG = -1, E_UNSUPPORTED = -9, E_CLIENT_RANGE = -12;
 
 class MergeTreeError extends Error {
@@ -336,7 +337,7 @@ function packDocInits(docs, interner) {
     const o = i * DOC_INIT_BYTES;
     buf.writeUInt32LE(off, o);
     buf.writeUInt32LE(d.text.length, o + 4);
-    buf.writeUInt32LE(d.newLengthCalc ? DOC_NEW_LENGTH_CALC : 0, o + 8);
+    buf.writeUInt32LE((d.newLengthCalc ? DOC_NEW_LENGTH_CALC : 0) | (d.roundSync ? DOC_ROUND_SYNC : 0), o + 8);
     buf.writeUInt32LE(props.add(d.props) >>> 0, o + 12);
     buf.writeInt32LE(d.minSeq || 0, o + 16);
     buf.writeInt32LE(d.currentSeq || 0, o + 20);

@@ -58,8 +58,8 @@ def test_strong_shards_cover_the_job():
 def test_gpu_one_rank_communicator():
     from fluidframework_amd.engine import DeviceEngine
     node = DeviceEngine(0)
-    node.comm_init(1, 0, fcomm.unique_id())
-    node.comm_barrier()
+    os.environ.setdefault("MASTER_PORT", "29501")
+    fcomm.join(node, 0, 1)
     assert node.comm_allreduce(2.5, "sum") == 2.5
     assert node.comm_allreduce(-1.0, "max") == -1.0
     s = gen.generate(3, n_docs=50, ops_per_doc=400, round_sync=True)

@@ -263,3 +263,30 @@ def test_gpu_matches_oracle_at_full_bench_size(cfg):
     o, d = replay_both_cap(s, gen.seg_capacity(cfg, s["params"]), threads=16)
     assert (o.statuses() == 0).all()
     assert_same(o, d)
+
+
+def test_gpu_pipelined_batches_equal_sequential():
+    # mte_submit of batch k+1 while batch k replays (two batch slots, upload
+    # stream): the same documents as one batch at a time with a sync between
+    s = gen.generate(3, n_docs=300, ops_per_doc=1600, round_sync=True)
+    parts = [gen.split_ops(s, k, 4) for k in range(4)] if hasattr(gen, "split_ops") else None
+    if parts is None:
+        pytest.skip("gen.split_ops missing")
+    seq = DeviceEngine(s["n_keys"])
+    gen.load_stream(seq, s)
+    for p in parts:
+        seq.submit(p)
+        seq.run()
+        seq.sync()
+    pipe = DeviceEngine(s["n_keys"])
+    gen.load_stream(pipe, s)
+    for p in parts:
+        pipe.submit(p)   # overlaps the previous run
+        pipe.run()
+    pipe.sync()
+    np.testing.assert_array_equal(pipe.statuses(), seq.statuses())
+    np.testing.assert_array_equal(pipe.digest(), seq.digest())
+    o = SpecOracle(s["n_keys"], threads=8)
+    gen.load_stream(o, s)
+    o.apply_batch(s["batch"])
+    np.testing.assert_array_equal(pipe.digest(), o.digest())

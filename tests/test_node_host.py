@@ -249,5 +249,5 @@ node.leaveNode();
 node.close();
 process.stdout.write(JSON.stringify(out));
 """
-    j = json.loads(node("-e", script))
+    j = json.loads(node("-e", script).strip().splitlines()[-1])  # RCCL prints a banner first
     assert j == {"sum": 3, "max": -2, "text": "hello world", "equal": True, "pad": True}
