@@ -18,6 +18,7 @@ const msgs = input.docs.map((d) => d.msgs.map((m) => ({
 const nOps = msgs.reduce((a, m) => a + m.length, 0);
 const runs = [];
 let digests = null;
+let texts = null;
 for (let rep = 0; rep < (input.reps || 2); rep++) {
   const eng = new MergeTreeEngine({ nKeys: 4, segCapacity: input.segCapacity || 0 });
   const clients = input.docs.map((d) => eng.createClient(d.initialText,
@@ -34,6 +35,7 @@ for (let rep = 0; rep < (input.reps || 2); rep++) {
   const t2 = process.hrtime.bigint();
   digests = eng.digests();
   const status = eng.statuses();
+  texts = clients.map((c) => c.getText());
   const t3 = process.hrtime.bigint();
   runs.push({ pack_ms: Number(t1 - t0) / 1e6, flush_ms: Number(t2 - t1) / 1e6, readout_ms: Number(t3 - t2) / 1e6,
     errors: status.reduce((a, x) => a + (x !== 0 ? 1 : 0), 0) });
@@ -71,4 +73,4 @@ const best = runs.reduce((a, r) => (a === null || r.pack_ms + r.flush_ms < a.pac
 process.stdout.write(JSON.stringify({ ops: nOps, docs: input.docs.length, runs, best,
   ops_per_s: nOps / ((best.pack_ms + best.flush_ms) / 1e3),
   pipelined: { parts, ms: bestPiped.ms, ops_per_s: nOps / (bestPiped.ms / 1e3), digest_equal: bestPiped.digest_equal },
-  digests: Array.from(digests, (x) => x.toString(16)) }));
+  texts }));
