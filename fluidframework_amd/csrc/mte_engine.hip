@@ -388,6 +388,7 @@ struct mte_ctx {
   uint64_t pe_cap_s[2] = {0, 0};
   uint64_t n_ops_s[2] = {0, 0}, n_propsets_s[2] = {0, 0};
   uint32_t text_base_s[2] = {0, 0};
+  uint64_t max_doc_ops_s[2] = {0, 0};  // the batch's largest per-document op count
   // the batch mte_run replays (= slot rslot)
   mte_op* d_ops = nullptr;
   uint4* d_cps = nullptr;
@@ -401,7 +402,7 @@ struct mte_ctx {
   uint32_t n_tree = 0;
   std::vector<uint8_t> h_legacy;    // per doc
   uint32_t* d_rs_docs = nullptr;    // legacy documents declared MTE_DOC_ROUND_SYNC (flat)
-  int tree_rounds = 4;              // TIER 0 / TIER 1 alternations (MTE_TREE_ROUNDS)
+  int tree_rounds = 0;              // TIER 0 / TIER 1 rounds (MTE_TREE_ROUNDS; 0 = from the batch)
   // node level (mte_comm_*): the RCCL communicator and its staging buffers
   ncclComm_t comm = nullptr;
   bool comm_owner = false;
@@ -523,9 +524,13 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
     // tree document), so the two streams share no document state
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->tree_stream, c->ev_fork, 0));
-    TreeArgs t{c->d_tree, c->d_heap, c->d_tree_docs, c->n_tree, c->arena, 0u};
-    HIPCHK(c, (launch_tree<K, S>(a, t, (c->n_tree + kDocsPerBlock - 1) / kDocsPerBlock, c->tree_stream,
-                                 c->tree_rounds)));
+    TreeArgs t{c->d_tree, c->d_heap, c->d_tree_docs, c->n_tree, c->arena, 0u, 0u};
+    // rounds of at most ~625 ops per document (MTE_TREE_ROUNDS overrides the count)
+    const uint64_t mx = c->max_doc_ops_s[c->rslot];
+    int rounds = c->tree_rounds > 0 ? c->tree_rounds : (int)std::min<uint64_t>(32, std::max<uint64_t>(1, (mx + 624) / 625));
+    const uint32_t per = (uint32_t)((mx + (uint64_t)rounds - 1) / (uint64_t)rounds);
+    HIPCHK(c, (launch_tree<K, S>(a, t, (c->n_tree + kDocsPerBlock - 1) / kDocsPerBlock, c->tree_stream, rounds,
+                                 per ? per : 1u)));
     HIPCHK(c, hipEventRecord(c->ev_join, c->tree_stream));
   }
   // pass 1: two documents per wavefront (docs up to 126 segments)
@@ -673,7 +678,7 @@ int mte_create(const mte_config* cfg, mte_ctx** out) {
   c->wclock_path = std::getenv("MTE_WAVE_CLOCK");
   if (const char* r = std::getenv("MTE_TREE_ROUNDS")) {
     const int v = std::atoi(r);
-    c->tree_rounds = v < 1 ? 1 : (v > 64 ? 64 : v);
+    c->tree_rounds = v < 0 ? 0 : (v > 64 ? 64 : v);
   }
   if (c->cap < 64) c->cap = 64;
   if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -998,6 +1003,9 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
   HIPCHK(c, hipStreamSynchronize(c->up_stream));  // host buffers may be freed after return
   c->n_ops_s[w] = b->n_ops;
   c->n_propsets_s[w] = b->n_propsets;
+  uint64_t mx = 0;
+  for (uint32_t d = 0; d < b->n_docs; d++) mx = std::max<uint64_t>(mx, b->op_offsets[d + 1] - b->op_offsets[d]);
+  c->max_doc_ops_s[w] = mx;
   c->rslot = w;
   c->d_ops = c->d_ops_s[w];
   c->d_cps = c->d_cps_s[w];

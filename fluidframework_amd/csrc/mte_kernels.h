@@ -155,7 +155,7 @@ __device__ __forceinline__ T pick(const T (&F)[E], int j) {
 template <int E, typename T>
 __device__ __forceinline__ T bcast(const T (&F)[E], int idx) {
   if constexpr (E == 1) return rdlane(F[0], idx);
-  else return rdlane(pick<E>(F, idx & (E - 1)), idx / E);
+  else return rdlane(pick<E>(F, (int)((uint32_t)idx % (uint32_t)E)), (int)((uint32_t)idx / (uint32_t)E));
 }
 
 template <int E, typename T>

@@ -17,7 +17,8 @@ struct ChunkArgs;
 // the tree pass over the legacy documents (mte_tree.h): `rounds` of TIER 0
 // (E <= 2) / TIER 1 (E = 4), then TIER 2 (E = 8, 16)
 template <int K, bool S>
-hipError_t launch_tree(const ReplayArgs& a, const TreeArgs& t, uint32_t blocks, hipStream_t s, int rounds);
+hipError_t launch_tree(const ReplayArgs& a, const TreeArgs& t, uint32_t blocks, hipStream_t s, int rounds,
+                       uint32_t per_round);
 // pass 1 (two documents per wavefront) and pass 2 (one per wavefront)
 template <int K, bool S>
 hipError_t launch_pair(const ReplayArgs& a, uint32_t blocks, hipStream_t s);

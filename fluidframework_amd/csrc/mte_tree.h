@@ -64,6 +64,7 @@ struct TreeArgs {
   uint32_t n_docs;
   const uint16_t* arena; // text (an append-merge looks at the last unit of a leaf)
   uint32_t final_round;  // TIER 1: keep documents that shrink (no return to TIER 0)
+  uint32_t k_cap;        // this round's op cursor limit (TIER 0 / 1): documents advance together
 };
 
 __device__ __forceinline__ uint32_t t_h(uint32_t t) { return t & kTH; }
@@ -992,6 +993,7 @@ __global__ __launch_bounds__(256) void tree_kernel(ReplayArgs a, TreeArgs t) {
   const uint64_t kb = uni64(a.op_off[doc]);
   D.recp = a.recs + 2 * kb;
   D.k1 = (uint32_t)(uni64(a.op_off[doc + 1]) - kb);
+  if (TIER < 2 && D.k1 > t.k_cap) D.k1 = t.k_cap;  // the round's share of the batch
   D.running = D.status == 0 && D.k < D.k1;
   if (!D.running) return;
   TreeRun tr;
