@@ -267,6 +267,7 @@ def main():
     r = run_engine(stream, cap, local_rank, args.steps, args.warmup, args.stats, barrier)
     eng, stats, digest = r["eng"], r["stats"], r["digest"]
     elapsed = r["elapsed"]
+    first_ms = r["first_ms"]
     total_ops = n_ops_rank * world
     fold = fdist.digest_fold(digest)
     if node is not None:
@@ -381,7 +382,7 @@ def main():
                                 "scanned (SURVEY.md 8(d))" if cap >= 8192 else "SURVEY.md 8(d) B_op"),
             "counters_in_timed_runs": bool(args.stats),
             "kernel_ms": avg_kernel_ms,
-            "first_run_kernel_ms": r["first_ms"],
+            "first_run_kernel_ms": first_ms,
             "algo_bytes_per_launch": algo_bytes,
             "algo_bytes_per_op": algo_bytes / max(1, stats["ops_applied"]),
         },
