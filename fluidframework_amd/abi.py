@@ -40,11 +40,13 @@ ERROR_NAMES = {
     MTE_E_CLIENT_RANGE: "too many clients in one document",
 }
 
-OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP = 0, 1, 2, 3
-F_MARKER, F_MSG_END, F_REWRITE = 0x1, 0x2, 0x4
+OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_ACK = 0, 1, 2, 3, 4
+F_MARKER, F_MSG_END, F_REWRITE, F_LOCAL = 0x1, 0x2, 0x4, 0x8
+LOCAL_SEQ_BASE = 0x40000000
 NO_PROPS = 0xFFFFFFFF
 DOC_NEW_LENGTH_CALC = 0x1
 DOC_ROUND_SYNC = 0x2
+DOC_LOCAL_CLIENT = 0x4
 
 # 32-byte mte_op record.
 OP_DTYPE = np.dtype([

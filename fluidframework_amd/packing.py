@@ -16,7 +16,12 @@ Reference behaviour mirrored here (packages/dds/merge-tree/src):
     textSegment.ts:40-48, mergeTreeNodes.ts:602-609); an insert without seg
     is a no-op (client.ts:481-487);
   * annotate props: null deletes, anything else sets; combiningOp "rewrite"
-    is supported, other combining ops are rejected.
+    is supported, other combining ops are rejected (DESIGN.md);
+  * a document whose own client sends (DocClients(local=True)): its local ops
+    become MTE_F_LOCAL records numbered by collabWindow.localSeq
+    (client.ts:131-229, mergeTree.ts:1590-1625), and the sequenced message of
+    each comes back as an MTE_OP_ACK record for the oldest pending localSeqs
+    (client.ts:925-928 -> ackPendingSegment, mergeTree.ts:1278-1331).
 Property keys are interned to plane indices and values to ids of their
 canonical JSON (sorted keys), so id equality == matchProperties
 (properties.ts:66-100).
@@ -25,9 +30,10 @@ import json
 
 import numpy as np
 
-from .abi import (F_MARKER, F_MSG_END, F_REWRITE, MTE_E_CLIENT_RANGE, MTE_E_INVALID_ARG,
-                  MTE_E_UNSUPPORTED, MTE_MAX_CLIENTS, NO_PROPS, OP_ANNOTATE, OP_DTYPE,
-                  OP_INSERT, OP_NOOP, OP_REMOVE, PROP_DTYPE, PROPSET_DTYPE, MergeTreeError)
+from .abi import (F_LOCAL, F_MARKER, F_MSG_END, F_REWRITE, LOCAL_SEQ_BASE, MTE_E_CLIENT_RANGE,
+                  MTE_E_INVALID_ARG, MTE_E_STATE, MTE_E_UNSUPPORTED, MTE_MAX_CLIENTS, NO_PROPS, OP_ACK,
+                  OP_ANNOTATE, OP_DTYPE, OP_INSERT, OP_NOOP, OP_REMOVE, PROP_DTYPE, PROPSET_DTYPE,
+                  MergeTreeError)
 
 INSERT, REMOVE, ANNOTATE, GROUP = 0, 1, 2, 3  # MergeTreeDeltaType, ops.ts:43-48
 I32_MIN, I32_MAX = -(1 << 31), (1 << 31) - 1
@@ -126,11 +132,17 @@ class DocClients:
 
     NEVER = I32_MAX  # slot held for good (observer, ids registered without a seq)
 
-    def __init__(self, observer_id: str, min_seq: int = 0):
+    def __init__(self, observer_id: str, min_seq: int = 0, local: bool = False):
         self.observer = observer_id
         self.ids = {observer_id: 0}
         self.last = {0: self.NEVER}  # slot -> highest seq its client used
         self.min_seq = min_seq       # the window's minSeq before the next message
+        # local client (MTE_DOC_LOCAL_CLIENT documents): collabWindow.localSeq and
+        # the (first, last) localSeqs of each unacked local message, oldest first
+        # (MergeTree.pendingSegments, mergeTree.ts:1333-1355)
+        self.local = local
+        self.local_seq = 0
+        self.pending = []
 
     def short(self, long_id, seq=None) -> int:
         i = self.ids.get(long_id)
@@ -197,8 +209,15 @@ class BatchBuilder:
         recs = []
         if msg.get("type", "op") == "op":
             if sender == clients.observer:
-                raise MergeTreeError(MTE_E_UNSUPPORTED, "ack of a local op (observer replay only)")
-            self._op_records(msg.get("contents"), recs)
+                # our own op, sequenced: ackPendingSegment (client.ts:925-928)
+                if not clients.local:
+                    raise MergeTreeError(MTE_E_UNSUPPORTED, "ack of a local op in an observer document")
+                if not clients.pending:
+                    raise MergeTreeError(MTE_E_STATE, "ack without a pending local op")
+                lo, hi = clients.pending.pop(0)
+                recs.append((OP_ACK, 0, lo, hi, 0, NO_PROPS))
+            else:
+                self._op_records(msg.get("contents"), recs)
         # the slot is taken only once the message has validated
         short = clients.short(sender, seq)
         if short >= MTE_MAX_CLIENTS:
@@ -213,6 +232,29 @@ class BatchBuilder:
                 flags |= F_MSG_END
             out.append((seq, ref, msn, t, short, flags, p1, p2, a, b))
         clients.advance(msn)
+
+    def add_local(self, doc: int, clients: DocClients, op: dict):
+        """A local op of the document's own client (insertSegmentLocal /
+        removeRangeLocal / annotateRangeLocal, client.ts:131-229): one MTE_F_LOCAL
+        record per (GROUP member) op, each with the next localSeq
+        (mergeTree.ts:1915, collabWindow.localSeq); the message's localSeqs join
+        the pending list, acked in order by add_message."""
+        if not clients.local:
+            raise MergeTreeError(MTE_E_UNSUPPORTED, "local op in an observer document")
+        recs = []
+        self._op_records(op, recs)
+        if not recs:
+            recs.append((OP_NOOP, 0, 0, 0, 0, NO_PROPS))
+        if any(f & F_REWRITE for _, f, *_ in recs):
+            raise MergeTreeError(MTE_E_UNSUPPORTED, "local combiningOp rewrite")
+        first = clients.local_seq + 1
+        if first + len(recs) >= LOCAL_SEQ_BASE:
+            raise MergeTreeError(MTE_E_INVALID_ARG, "localSeq overflow")
+        out = self.ops[doc]
+        for i, (t, flags, p1, p2, a, b) in enumerate(recs):
+            out.append((first + i, 0, 0, t, 0, flags | F_LOCAL, p1, p2, a, b))
+        clients.local_seq += len(recs)
+        clients.pending.append((first, clients.local_seq))
 
     def _op_records(self, op, recs):
         if not isinstance(op, dict):

@@ -69,10 +69,33 @@ extern "C" {
 #define MTE_OP_REMOVE 1
 #define MTE_OP_ANNOTATE 2
 #define MTE_OP_NOOP 3
+/* The sequenced message of an op this document's own (local) client sent:
+ * Client.applyMsg(msg) with msg.clientId == the local client -> ackPendingSegment
+ * (client.ts:925-928, mergeTree.ts:1278-1331, mergeTreeNodes.ts:475-503).  The
+ * pending segment groups of localSeq pos1 .. pos2 (FIFO, so always the oldest
+ * ones) take seq as their insert / removal seq and their pending property keys
+ * stop blocking remote annotates; then the window update as for any message.
+ * Only in MTE_DOC_LOCAL_CLIENT documents.                                    */
+#define MTE_OP_ACK 4
 
 #define MTE_F_MARKER 0x0001u  /* insert spec {marker:{refType}} (mergeTreeNodes.ts:602-609) */
 #define MTE_F_MSG_END 0x0002u /* last record of its message: window update follows      */
 #define MTE_F_REWRITE 0x0004u /* annotate combiningOp {name:"rewrite"} (segmentPropertiesManager.ts:105-119) */
+/* A local op of the document's own client (client 0), not yet sequenced:
+ * insertSegmentLocal / removeRangeLocal / annotateRangeLocal (client.ts:131-229)
+ * -> insertSegments / markRangeRemoved / annotateRange with seq =
+ * UnassignedSequenceNumber (constants.ts:12).  Positions are in the local
+ * client's view (every segment it holds, its own pending ones included, minus
+ * the removed ones: localNetLength, mergeTree.ts:553-573).  The record's seq is
+ * the op's localSeq (collabWindow.localSeq, > 0, strictly increasing per
+ * document, < MTE_LOCAL_SEQ_BASE); ref_seq and min_seq are ignored and the
+ * window does not move (no MSG_END).  Only in MTE_DOC_LOCAL_CLIENT documents;
+ * a local rewrite is MTE_E_UNSUPPORTED.                                       */
+#define MTE_F_LOCAL 0x0008u
+/* Pending (unacked) seqs are held as MTE_LOCAL_SEQ_BASE + localSeq, above any
+ * sequenced seq: UnassignedSequenceNumber normalised as in breakTie / nodeLength
+ * (mergeTree.ts:1009-1016, 1713-1714).  Sequenced seqs must stay below it.     */
+#define MTE_LOCAL_SEQ_BASE 0x40000000
 
 #define MTE_NO_PROPS 0xFFFFFFFFu
 
@@ -125,6 +148,14 @@ typedef struct mte_config {
  * with MTE_E_UNSUPPORTED before any of the batch's ops (its state stays that of
  * the previous batch).  Ignored with MTE_DOC_NEW_LENGTH_CALC (always flat). */
 #define MTE_DOC_ROUND_SYNC 0x2u
+/* The document is a collaborating client that sends ops of its own (short
+ * client id 0 = collabWindow.clientId): it takes MTE_F_LOCAL records and
+ * MTE_OP_ACK messages besides remote ones (the non-observer TestClients of the
+ * conflict farm, test/mergeTreeOperationRunner.ts:149-236).  Requires
+ * MTE_DOC_NEW_LENGTH_CALC (as the farm's clients, client.conflictFarm.spec.ts:84)
+ * and a context with seg_capacity < 8192; such documents replay on the
+ * HBM-streamed pass.                                                         */
+#define MTE_DOC_LOCAL_CLIENT 0x4u
 
 /* Initial document: one text segment inserted before collaboration starts, as
  * the reference replay harness does (client.replay.spec.ts:22-23): seq 0

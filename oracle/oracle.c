@@ -40,6 +40,12 @@ typedef struct {
   uint32_t flags;
   int32_t status;
   int32_t rs_ref, rs_seq; /* MTE_DOC_ROUND_SYNC: highest refSeq, highest live seq so far */
+  /* MTE_DOC_LOCAL_CLIENT: per segment and key, the localSeq of the last pending
+   * local annotate that set the key (0 = none pending), a row of MTE_MAX_KEYS
+   * per segment kept in step with s[] (the pendingKeyUpdateCount of
+   * segmentPropertiesManager.ts:20-60, see doc_apply_local); the last localSeq */
+  uint32_t* pk;
+  int32_t local_seq;
   /* stats */
   uint64_t ops, scanned, written, pwrites, units, max_segs;
   /* scratch */
@@ -81,6 +87,8 @@ static int arena_append(orc_ctx* c, const uint16_t* t, uint64_t n, uint64_t* bas
   return MTE_OK;
 }
 
+#define PK(d, i) ((d)->pk + (size_t)(i) * MTE_MAX_KEYS)
+
 static int doc_reserve(odoc* d, uint32_t need) {
   if (need <= d->cap) return MTE_OK;
   uint32_t nc = d->cap ? d->cap : 64;
@@ -88,6 +96,11 @@ static int doc_reserve(odoc* d, uint32_t need) {
   oseg* s = (oseg*)realloc(d->s, (size_t)nc * sizeof(oseg));
   if (!s) return MTE_E_OOM;
   d->s = s;
+  if (d->flags & MTE_DOC_LOCAL_CLIENT) {
+    uint32_t* pk = (uint32_t*)realloc(d->pk, (size_t)nc * MTE_MAX_KEYS * sizeof(uint32_t));
+    if (!pk) return MTE_E_OOM;
+    d->pk = pk;
+  }
   d->cap = nc;
   return MTE_OK;
 }
@@ -110,6 +123,10 @@ static int doc_open(odoc* d, uint32_t at, uint32_t cnt) {
   int rc = doc_reserve(d, d->n + cnt);
   if (rc) return rc;
   memmove(d->s + at + cnt, d->s + at, (size_t)(d->n - at) * sizeof(oseg));
+  if (d->pk) {
+    memmove(PK(d, at + cnt), PK(d, at), (size_t)(d->n - at) * MTE_MAX_KEYS * sizeof(uint32_t));
+    memset(PK(d, at), 0, (size_t)cnt * MTE_MAX_KEYS * sizeof(uint32_t));
+  }
   d->n += cnt;
   return MTE_OK;
 }
@@ -177,6 +194,9 @@ static int64_t doc_split_at(odoc* d, int64_t pos, uint64_t* written) {
       oseg* head = &d->s[i];
       oseg* tail = &d->s[i + 1];
       *tail = *head;
+      /* the tail keeps the pending key counts (copyPropertiesTo,
+       * mergeTreeNodes.ts:505-534 -> PropertiesManager.copyTo) */
+      if (d->pk) memcpy(PK(d, i + 1), PK(d, i), MTE_MAX_KEYS * sizeof(uint32_t));
       tail->len = head->len - (int32_t)off;
       tail->toff = head->toff + (uint32_t)off;
       head->len = (int32_t)off;
@@ -212,10 +232,155 @@ static void doc_compact(odoc* d) {
   uint32_t w = 0;
   for (uint32_t i = 0; i < d->n; i++) {
     if (d->s[i].rseq != NONE_SEQ && d->s[i].rseq <= d->min_seq) continue;
-    if (w != i) d->s[w] = d->s[i];
+    if (w != i) {
+      d->s[w] = d->s[i];
+      if (d->pk) memcpy(PK(d, w), PK(d, i), MTE_MAX_KEYS * sizeof(uint32_t));
+    }
     w++;
   }
   d->n = w;
+}
+
+#define LOCAL_BASE MTE_LOCAL_SEQ_BASE
+static inline int is_pending(int32_t seq) { return seq >= LOCAL_BASE && seq != NONE_SEQ; }
+
+/* annotateRange on one segment for a sequenced (remote) op in a document with
+ * a local client: PropertiesManager.addProperties skips every key with a
+ * pending local update (shouldModifyKey, segmentPropertiesManager.ts:94-102,
+ * 121-135), the rewrite's clear included (105-119). */
+static uint64_t apply_props_pending(uint32_t* props, const uint32_t* pk, uint32_t n_keys, const mte_propset* ps,
+                                    const mte_prop* pe, int rewrite) {
+  uint64_t w = 0;
+  if (rewrite) {
+    for (uint32_t k = 0; k < n_keys; k++)
+      if (!pk[k]) props[k] = 0;
+  }
+  for (uint32_t j = 0; j < ps->count; j++) {
+    const mte_prop* p = &pe[ps->first + j];
+    if (p->key < n_keys) {
+      if (!pk[p->key]) props[p->key] = p->value;
+      w++;
+    }
+  }
+  return w;
+}
+
+/* The local client's own view (nodeLength with clientId == collabWindow.clientId
+ * -> localNetLength without localSeq, mergeTree.ts:985-987, 553-573, new length
+ * calculation): every segment not removed counts its length, a removed one 0
+ * (its own pending removals included). */
+static int64_t doc_lengths_local(odoc* d) {
+  int64_t p = 0;
+  for (uint32_t i = 0; i < d->n; i++) {
+    const int32_t l = d->s[i].rseq != NONE_SEQ ? 0 : d->s[i].len;
+    d->L[i] = l;
+    d->P[i] = p;
+    p += l;
+  }
+  return p;
+}
+
+/* A local op (MTE_F_LOCAL, include/mte.h): insertSegmentLocal /
+ * removeRangeLocal / annotateRangeLocal (client.ts:131-229) with seq =
+ * UnassignedSequenceNumber, held as LOCAL_BASE + localSeq.
+ *   insert: ensureIntervalBoundary + insertingWalk in the local view; breakTie
+ *     normalises the new seq to MAX_SAFE_INTEGER (mergeTree.ts:1713), so the
+ *     segment goes before the first leaf at P >= pos, as a remote insert does;
+ *     no continuePredicate for a local insert (:1790).  The segment joins the
+ *     pending list (saveIfLocal, :1614-1619).
+ *   remove: markRemoved on the leaves the local view sees in [start, end):
+ *     removedSeq = Unassigned, removedClientIds = [local] (:1954-1959).
+ *   annotate: set / delete each key now and count it pending
+ *     (segmentPropertiesManager.ts:121-135); a local rewrite is unsupported. */
+static int doc_apply_local(odoc* d, const mte_op* op, const apply_env* env) {
+  const int32_t ls = op->seq;
+  int rc;
+  if (!(ls > d->local_seq && ls < LOCAL_BASE)) return MTE_E_INVALID_ARG;
+  if (op->client != 0) return MTE_E_INVALID_ARG;
+  if (op->type == MTE_OP_ANNOTATE && (op->flags & MTE_F_REWRITE)) return MTE_E_UNSUPPORTED;
+  d->local_seq = ls;
+  d->ops++;
+  if (d->n > d->max_segs) d->max_segs = d->n;
+  if (op->type == MTE_OP_NOOP) return MTE_OK;
+  d->scanned += d->n;
+  if ((rc = doc_scratch(d))) return rc;
+  const int64_t total = doc_lengths_local(d);
+  if (op->type == MTE_OP_INSERT) {
+    const int64_t pos = op->pos1;
+    const int64_t tail = doc_split_at(d, pos, &d->written);
+    if (tail == -2) return MTE_E_OOM;
+    const int is_marker = (op->flags & MTE_F_MARKER) != 0;
+    const int32_t len = is_marker ? 1 : op->pos2;
+    if (len <= 0) return MTE_OK;
+    uint32_t at = d->n;
+    if (tail >= 0) {
+      at = (uint32_t)tail;
+    } else {
+      for (uint32_t i = 0; i < d->n; i++)
+        if (d->P[i] >= pos) { at = i; break; }
+      if (at == d->n && pos > total) return MTE_E_INSERT_FAILED;
+    }
+    if ((rc = doc_open(d, at, 1))) return rc;
+    oseg* ns = &d->s[at];
+    memset(ns, 0, sizeof(*ns));
+    ns->len = len;
+    ns->seq = LOCAL_BASE + ls;
+    ns->cli = 0;
+    ns->rseq = NONE_SEQ;
+    if (is_marker) {
+      ns->kind = 1u + (uint32_t)op->pos2;
+    } else {
+      ns->toff = (uint32_t)(env->text_base + op->a);
+      d->units += (uint64_t)len;
+    }
+    if (op->b != MTE_NO_PROPS)
+      d->pwrites += orc_apply_props(ns->props, env->n_keys, &env->b->propsets[op->b], env->b->props, 0);
+    d->written += 1;
+    return MTE_OK;
+  }
+  if (op->type != MTE_OP_REMOVE && op->type != MTE_OP_ANNOTATE) return MTE_E_INVALID_ARG;
+  const int64_t start = op->pos1, end = op->pos2;
+  if (doc_split_at(d, start, &d->written) == -2) return MTE_E_OOM;
+  if (doc_split_at(d, end, &d->written) == -2) return MTE_E_OOM;
+  for (uint32_t i = 0; i < d->n && end > start; i++) {
+    const int32_t l = d->L[i];
+    if (l <= 0) continue;
+    if (d->P[i] >= end) break;
+    if (d->P[i] + l <= start) continue;
+    oseg* g = &d->s[i];
+    if (op->type == MTE_OP_REMOVE) {
+      g->rseq = LOCAL_BASE + ls;
+      g->rmask = 1u;
+    } else {
+      const mte_propset* ps = &env->b->propsets[op->a];
+      d->pwrites += orc_apply_props(g->props, env->n_keys, ps, env->b->props, 0);
+      for (uint32_t j = 0; j < ps->count; j++) {
+        const mte_prop* p = &env->b->props[ps->first + j];
+        if (p->key < env->n_keys) PK(d, i)[p->key] = (uint32_t)ls;
+      }
+    }
+    d->written += 1;
+  }
+  return MTE_OK;
+}
+
+/* MTE_OP_ACK: ackPendingSegment for the groups of localSeq pos1..pos2
+ * (mergeTree.ts:1278-1331, BaseSegment.ack mergeTreeNodes.ts:475-503): a
+ * pending insert takes the seq, a pending removal too unless a remote remove
+ * overtook it (then removedSeq is already that op's, :1928-1938), and the
+ * annotate's keys stop being pending (ackPendingProperties). */
+static int doc_ack(odoc* d, const mte_op* op) {
+  const int32_t lo = op->pos1, hi = op->pos2, s = op->seq;
+  if (!(lo > 0 && lo <= hi && hi <= d->local_seq)) return MTE_E_INVALID_ARG;
+  for (uint32_t i = 0; i < d->n; i++) {
+    oseg* g = &d->s[i];
+    if (g->seq >= LOCAL_BASE + lo && g->seq <= LOCAL_BASE + hi) g->seq = s;
+    if (g->rseq >= LOCAL_BASE + lo && g->rseq <= LOCAL_BASE + hi) g->rseq = s;
+    uint32_t* pk = PK(d, i);
+    for (uint32_t k = 0; k < MTE_MAX_KEYS; k++)
+      if (pk[k] && pk[k] <= (uint32_t)hi) pk[k] = 0;
+  }
+  return MTE_OK;
 }
 
 /* One op record.  Client.applyMsg -> applyRemoteOp (client.ts:918-935,
@@ -224,8 +389,12 @@ static int doc_apply(odoc* d, const mte_op* op, const apply_env* env) {
   const int newcalc = (d->flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
   const int32_t r = op->ref_seq, s = op->seq, m = d->min_seq;
   const int c = op->client;
+  const int local_doc = (d->flags & MTE_DOC_LOCAL_CLIENT) != 0;
   int rc;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
+  if (op->flags & MTE_F_LOCAL) return local_doc ? doc_apply_local(d, op, env) : MTE_E_UNSUPPORTED;
+  if (op->type == MTE_OP_ACK && !local_doc) return MTE_E_UNSUPPORTED;
+  if (local_doc && op->type != MTE_OP_ACK && op->type != MTE_OP_NOOP && c == 0) return MTE_E_INVALID_ARG;
   d->ops++;
   if (d->n > d->max_segs) d->max_segs = d->n;
   if (op->type != MTE_OP_NOOP) d->scanned += d->n;
@@ -249,8 +418,12 @@ static int doc_apply(odoc* d, const mte_op* op, const apply_env* env) {
       if (tail >= 0) {
         at = (uint32_t)tail;
       } else {
+        /* a pending local segment (zero-length for every remote view) is
+         * passed over: breakTie normalises its seq to MAX_SAFE_INTEGER - 1
+         * (mergeTree.ts:1714), and at a block's end continuePredicate's
+         * forward excursion moves on when it comes next (:1599-1611, 1790) */
         for (uint32_t i = 0; i < d->n; i++) {
-          if (d->L[i] >= 0 && d->P[i] >= pos) { at = i; break; }
+          if (d->L[i] >= 0 && d->P[i] >= pos && !(local_doc && is_pending(d->s[i].seq))) { at = i; break; }
         }
         if (at == d->n && pos > total) return MTE_E_INSERT_FAILED;
       }
@@ -298,8 +471,14 @@ static int doc_apply(odoc* d, const mte_op* op, const apply_env* env) {
             g->rseq = s;
             g->rmask = 1u << c;
           } else {
+            /* overtaking our pending removal: this op's seq becomes the
+             * removedSeq (1928-1938) */
+            if (is_pending(g->rseq)) g->rseq = s;
             g->rmask |= 1u << c;
           }
+        } else if (local_doc) {
+          d->pwrites += apply_props_pending(g->props, PK(d, i), env->n_keys, &env->b->propsets[op->a],
+                                            env->b->props, (op->flags & MTE_F_REWRITE) != 0);
         } else {
           d->pwrites += orc_apply_props(g->props, env->n_keys, &env->b->propsets[op->a], env->b->props,
                                     (op->flags & MTE_F_REWRITE) != 0);
@@ -307,6 +486,9 @@ static int doc_apply(odoc* d, const mte_op* op, const apply_env* env) {
         d->written += 1;
       }
     }
+    if ((rc = check_op_window(d, op))) return rc;
+  } else if (op->type == MTE_OP_ACK) {
+    if ((rc = doc_ack(d, op))) return rc;
     if ((rc = check_op_window(d, op))) return rc;
   } else if (op->type != MTE_OP_NOOP) {
     return MTE_E_INVALID_ARG;
@@ -342,6 +524,7 @@ static void free_docs(orc_ctx* c) {
     free(c->docs[i].s);
     free(c->docs[i].L);
     free(c->docs[i].P);
+    free(c->docs[i].pk);
   }
   free(c->docs);
   c->docs = NULL;
@@ -394,6 +577,7 @@ int orc_load_docs(orc_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     if ((uint64_t)in->text_off + in->text_len > text_units) return MTE_E_INVALID_ARG;
     d->init = *in;
     d->flags = in->flags;
+    if ((in->flags & MTE_DOC_LOCAL_CLIENT) && !(in->flags & MTE_DOC_NEW_LENGTH_CALC)) return MTE_E_UNSUPPORTED;
     d->min_seq = in->min_seq;
     d->cur_seq = in->cur_seq;
     d->rs_ref = INT32_MIN;
@@ -407,6 +591,7 @@ int orc_load_docs(orc_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
       g->cli = -1;  /* LocalClientId */
       g->rseq = NONE_SEQ;
       g->toff = (uint32_t)(base + in->text_off);
+      if (d->pk) memset(PK(d, 0), 0, MTE_MAX_KEYS * sizeof(uint32_t));
       if (in->propset != MTE_NO_PROPS) {
         if (in->propset >= n_propsets) return MTE_E_INVALID_ARG;
         orc_apply_props(g->props, c->n_keys, &propsets[in->propset], props, 0);
@@ -439,6 +624,7 @@ int orc_load_segments(orc_ctx* c, const uint64_t* seg_offsets, const mte_seg* se
         return MTE_E_INVALID_ARG;
       oseg* g = &d->s[k - b];
       memset(g, 0, sizeof(*g));
+      if (d->pk) memset(PK(d, k - b), 0, MTE_MAX_KEYS * sizeof(uint32_t));
       g->len = (int32_t)sg->len;
       g->seq = sg->seq;
       g->cli = sg->client;

@@ -1,0 +1,177 @@
+#!/usr/bin/env node
+// ref_farm.js — a conflict farm of REFERENCE merge-tree Clients with local ops,
+// acks and lagging clients (TEST INFRASTRUCTURE; runs only in the build
+// container, never on the GPU box).
+//
+// Like test/client.conflictFarm.spec.ts + test/mergeTreeOperationRunner.ts
+// (every client a collaborating Client with the new length calculation, :84;
+// ops made locally with insertSegmentLocal / removeRangeLocal /
+// annotateRangeLocal, client.ts:131-229, and their sequenced messages applied
+// by every client — its own as acks, client.ts:918-935), but the sequencer and
+// the clients run as a service does: a message is sequenced as soon as it is
+// sent, with refSeq = the sender's currentSeq and msn = the lowest currentSeq
+// of any client, and every client catches up with the sequenced log at its own
+// pace.  So ops see lagging refSeqs, a client's pending ops meet remote ops
+// (breakTie / continuePredicate, mergeTree.ts:1599-1611, 1705-1721, 1790;
+// overlapping removes, :1928-1938; pending property keys,
+// segmentPropertiesManager.ts:94-135) and the window trails far behind.
+//
+// stdin:  {"sets": [{"seed": int, "clients": int, "steps": int, "initialText": str,
+//                    "nCheckpoints": int, "maxText": int}]}
+// stdout: {"sets": [{..params, "names": [...], "log": [[clientId, seq, ref, msn, "op", contents]],
+//                    "events": [[["L"|"A", logIndex], ...] per client],
+//                    "checkpoints": [{"done": [events applied per client],
+//                                     "states": [{"text", "props": [[start, end, {..}]]}]}]}]}
+// Client 0 ("A") never sends: the observer.
+"use strict";
+const path = require("path");
+const fs = require("fs");
+
+const refdir = process.argv[2] || path.join(__dirname, "_ref", "ts");
+const { Client } = require(path.join(refdir, "client.js"));
+const { TextSegment } = require(path.join(refdir, "textSegment.js"));
+const { Marker } = require(path.join(refdir, "mergeTreeNodes.js"));
+const { MergeTreeTextHelper } = require(path.join(refdir, "MergeTreeTextHelper.js"));
+
+function specToSegment(spec) {
+  const t = TextSegment.fromJSONObject(spec);
+  if (t) return t;
+  const m = Marker.fromJSONObject(spec);
+  if (m) return m;
+  throw new Error(`Unrecognized IJSONSegment type: '${JSON.stringify(spec)}'`);
+}
+const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
+
+// mulberry32: a small seeded generator (the farm's random-js is not vendored)
+function rng(seed) {
+  let a = seed >>> 0;
+  const next = () => {
+    a = (a + 0x6d2b79f5) >>> 0;
+    let t = a;
+    t = Math.imul(t ^ (t >>> 15), t | 1);
+    t ^= t + Math.imul(t ^ (t >>> 7), t | 61);
+    return ((t ^ (t >>> 14)) >>> 0) / 4294967296;
+  };
+  return { next, int: (lo, hi) => lo + Math.floor(next() * (hi - lo + 1)) };
+}
+
+function sortKeys(v) {
+  if (v && typeof v === "object" && !Array.isArray(v)) {
+    const o = {};
+    for (const k of Object.keys(v).sort()) o[k] = sortKeys(v[k]);
+    return o;
+  }
+  return v;
+}
+
+function readOut(client) {
+  const helper = new MergeTreeTextHelper(client._mergeTree);
+  const text = helper.getText(client.getCurrentSeq(), client.getClientId(), "");
+  const length = client.getLength();
+  const props = [];
+  let cur = null;
+  let start = 0;
+  for (let p = 0; p < length; p++) {
+    const pr = client.getPropertiesAtPosition(p);
+    const key = pr && Object.keys(pr).length ? JSON.stringify(sortKeys(pr)) : "";
+    if (key !== cur) {
+      if (cur) props.push([start, p, JSON.parse(cur)]);
+      cur = key;
+      start = p;
+    }
+  }
+  if (cur) props.push([start, length, JSON.parse(cur)]);
+  return { text, length, props };
+}
+
+const KEYS = ["client", "bold", "color"];
+
+function runSet(p) {
+  const R = rng(p.seed);
+  const names = [];
+  for (let i = 0; i < p.clients; i++) names.push(String.fromCharCode(65 + i));
+  const clients = names.map((n) => {
+    const c = new Client(specToSegment, logger, { mergeTreeUseNewLengthCalculations: true });
+    if (p.initialText) c.insertSegmentLocal(0, new TextSegment(p.initialText));
+    c.startOrUpdateCollaboration(n);
+    return c;
+  });
+  const cursor = names.map(() => 0);
+  const events = names.map(() => []);
+  const log = [];
+  let seq = 0;
+  const checkpoints = [];
+  const every = Math.max(1, Math.floor(p.steps / Math.max(1, p.nCheckpoints)));
+
+  const applyNext = (i) => {
+    const m = log[cursor[i]];
+    clients[i].applyMsg({
+      clientId: m[0], sequenceNumber: m[1], referenceSequenceNumber: m[2], minimumSequenceNumber: m[3],
+      type: m[4], contents: m[5],
+    });
+    events[i].push(["A", cursor[i]]);
+    cursor[i]++;
+  };
+  const checkpoint = () => {
+    checkpoints.push({ done: events.map((e) => e.length), states: clients.map(readOut) });
+  };
+
+  for (let step = 0; step < p.steps; step++) {
+    if (R.next() < 0.55) {
+      // a local op of a sending client (client 0 only observes)
+      const i = R.int(1, p.clients - 1);
+      const c = clients[i];
+      const len = c.getLength();
+      const pick = R.next();
+      let op;
+      if (len < 4 || (pick < 0.4 && len < p.maxText)) {
+        const pos = R.int(0, len);
+        if (R.next() < 0.08) {
+          const props = R.next() < 0.5 ? { markerId: `m${seq}` } : undefined;
+          op = c.insertSegmentLocal(pos, Marker.make(1, props));
+        } else {
+          const text = names[i].repeat(R.int(1, 3));
+          const seg = new TextSegment(text);
+          if (R.next() < 0.2) seg.addProperties({ [KEYS[R.int(0, 2)]]: R.int(0, 3) });
+          op = c.insertSegmentLocal(pos, seg);
+        }
+      } else {
+        const start = R.int(0, len - 1);
+        const end = R.int(start + 1, Math.min(len, start + 1 + R.int(0, 24)));
+        if (pick < 0.7) {
+          op = c.removeRangeLocal(start, end);
+        } else {
+          const props = {};
+          const nk = R.int(1, 2);
+          for (let k = 0; k < nk; k++) props[KEYS[R.int(0, 2)]] = R.next() < 0.15 ? null : R.int(0, 5);
+          op = c.annotateRangeLocal(start, end, props, undefined);
+        }
+      }
+      if (op) {
+        let msn = Infinity;
+        for (const x of clients) msn = Math.min(msn, x.getCurrentSeq());
+        seq++;
+        log.push([names[i], seq, c.getCurrentSeq(), msn, "op", JSON.parse(JSON.stringify(op))]);
+        events[i].push(["L", log.length - 1]);
+      }
+    } else {
+      // a client catches up with a few sequenced messages
+      const i = R.int(0, p.clients - 1);
+      const k = R.int(1, 6);
+      for (let j = 0; j < k && cursor[i] < log.length; j++) applyNext(i);
+    }
+    if ((step + 1) % every === 0 && step + 1 < p.steps) checkpoint();
+  }
+  for (let i = 0; i < p.clients; i++) while (cursor[i] < log.length) applyNext(i);
+  checkpoint();
+  const t0 = checkpoints[checkpoints.length - 1].states[0];
+  for (const s of checkpoints[checkpoints.length - 1].states) {
+    if (s.text !== t0.text || JSON.stringify(s.props) !== JSON.stringify(t0.props)) {
+      throw new Error(`seed ${p.seed}: the reference clients did not converge`);
+    }
+  }
+  return Object.assign({}, p, { names, log, events, checkpoints });
+}
+
+const input = JSON.parse(fs.readFileSync(0, "utf8"));
+process.stdout.write(JSON.stringify({ sets: input.sets.map(runSet) }));

@@ -97,3 +97,140 @@ def replay_fixtures(engine_factory, files=None, check=True, rounds=None, fresh_c
                 else:
                     passed += 1
     return passed, failures, eng
+
+
+def farm_clients(f):
+    """The senders of a fixture file: the farm's non-observer TestClients."""
+    seen = []
+    for rd in f["rounds"]:
+        for m in rd["msgs"]:
+            if m[0] not in seen:
+                seen.append(m[0])
+    return seen
+
+
+def replay_farm(engine_factory, files=None, rounds=None):
+    """The conflict farm with every client on the engine
+    (test/mergeTreeOperationRunner.ts:100-236): per fixture an observer document
+    ("A", remote ops only) plus one MTE_DOC_LOCAL_CLIENT document per sender.
+    In each round every client first applies its own ops of the round locally
+    (they were generated against the round-start state plus the client's own
+    earlier ops, generateOperationMessagesForClients :149-199), then every
+    client applies every sequenced message — its own as acks (applyMessages
+    :217-236).  All documents must hold resultText after each round, with
+    the new length calculation the farm's clients use
+    (client.conflictFarm.spec.ts:84).  Returns (checkpoints_passed, failures, eng)."""
+    from fluidframework_amd.abi import DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC
+
+    fx = load_fixtures()
+    if files is not None:
+        fx = [fx[i] for i in files]
+    layout = []  # (fixture index, long id of the doc's own client or None)
+    for i, f in enumerate(fx):
+        layout.append((i, None))
+        layout += [(i, cid) for cid in farm_clients(f)]
+    texts = [fx[i]["rounds"][0]["initialText"] for i, _ in layout]
+    inits, text = doc_inits(texts)
+    for d, (_, cid) in enumerate(layout):
+        inits[d]["flags"] = DOC_NEW_LENGTH_CALC | (DOC_LOCAL_CLIENT if cid is not None else 0)
+    interner = Interner(8)
+    eng = engine_factory(8)
+    eng.load_docs(inits, text)
+    clients = [DocClients(cid if cid is not None else "A", local=cid is not None) for _, cid in layout]
+    n_rounds = max(len(f["rounds"]) for f in fx)
+    if rounds is not None:
+        n_rounds = min(n_rounds, rounds)
+    passed, failures = 0, []
+    for r in range(n_rounds):
+        bb = BatchBuilder(len(layout), interner)
+        for d, (i, cid) in enumerate(layout):
+            if r >= len(fx[i]["rounds"]):
+                continue
+            msgs = [as_msg(m) for m in fx[i]["rounds"][r]["msgs"]]
+            if cid is not None:
+                for m in msgs:
+                    if m["clientId"] == cid:
+                        bb.add_local(d, clients[d], m["contents"])
+            for m in msgs:
+                bb.add_message(d, clients[d], m)
+        eng.apply_batch(bb.build())
+        st = eng.statuses()
+        for d, (i, cid) in enumerate(layout):
+            if r >= len(fx[i]["rounds"]):
+                continue
+            if st[d] != 0:
+                failures.append((fx[i]["name"], cid, r, "status", int(st[d])))
+                continue
+            got = eng.read_doc(d)["text"]
+            if got != fx[i]["rounds"][r]["resultText"]:
+                failures.append((fx[i]["name"], cid, r, "result", got, fx[i]["rounds"][r]["resultText"]))
+            else:
+                passed += 1
+    return passed, failures, eng
+
+
+def prop_runs(view, interner):
+    """read_doc's visible segments -> per-position property runs
+    [[start, end, {..}], ...] (empty == undefined, testClientLogger.ts:33-42)."""
+    runs, pos = [], 0
+    for ln, _kind, planes in view["segs"]:
+        p = interner.decode_props(planes)
+        if ln:
+            if p and runs and runs[-1][1] == pos and runs[-1][2] == p:
+                runs[-1][1] = pos + ln
+            elif p:
+                runs.append([pos, pos + ln, p])
+        pos += ln
+    return runs
+
+
+def replay_ref_farm(engine_factory, sets, n_keys=8):
+    """Replay farms the reference ran (oracle/ref_farm.js -> tests/golden/
+    farm_vectors.json.gz): one MTE_DOC_LOCAL_CLIENT document per client of every
+    set (the observer "A" included), each fed its own events in order — "L" a
+    local op, "A" a sequenced message (its own: an ack) — in one batch per
+    checkpoint; text and per-position properties must equal the reference
+    client's at every checkpoint.  Returns (checkpoints_passed, failures)."""
+    from fluidframework_amd.abi import DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC
+
+    layout = [(si, ci) for si, s in enumerate(sets) for ci in range(len(s["names"]))]
+    inits, text = doc_inits([sets[si]["initialText"] for si, _ in layout],
+                            flags=DOC_NEW_LENGTH_CALC | DOC_LOCAL_CLIENT)
+    interner = Interner(n_keys)
+    eng = engine_factory(n_keys)
+    eng.load_docs(inits, text)
+    clients = [DocClients(sets[si]["names"][ci], local=True) for si, ci in layout]
+    n_cp = max(len(s["checkpoints"]) for s in sets)
+    prev = [0] * len(layout)
+    passed, failures = 0, []
+    for j in range(n_cp):
+        bb = BatchBuilder(len(layout), interner)
+        for d, (si, ci) in enumerate(layout):
+            s = sets[si]
+            if j >= len(s["checkpoints"]):
+                continue
+            done = s["checkpoints"][j]["done"][ci]
+            for kind, li in s["events"][ci][prev[d]:done]:
+                m = as_msg(s["log"][li])
+                if kind == "L":
+                    bb.add_local(d, clients[d], m["contents"])
+                else:
+                    bb.add_message(d, clients[d], m)
+            prev[d] = done
+        eng.apply_batch(bb.build())
+        st = eng.statuses()
+        for d, (si, ci) in enumerate(layout):
+            s = sets[si]
+            if j >= len(s["checkpoints"]):
+                continue
+            want = s["checkpoints"][j]["states"][ci]
+            if st[d] != 0:
+                failures.append((si, ci, j, "status", int(st[d])))
+                continue
+            v = eng.read_doc(d)
+            got = {"text": v["text"], "length": v["length"], "props": prop_runs(v, interner)}
+            if got["text"] != want["text"] or got["length"] != want["length"] or got["props"] != want["props"]:
+                failures.append((si, ci, j, "state", got, want))
+            else:
+                passed += 1
+    return passed, failures

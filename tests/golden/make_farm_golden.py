@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Golden farm vectors from the REFERENCE merge-tree itself
+(tests/golden/farm_vectors.json.gz).
+
+oracle/ref_farm.js runs conflict farms of reference Clients (type-erased into
+the git- and gpurun-ignored oracle/_ref/ts by oracle/ts_erase.py) with local
+ops, acks and clients that catch up with the sequenced log at their own pace,
+and records the sequenced messages, each client's order of events (its local
+ops and the messages it applied) and every client's text and per-position
+properties at checkpoints.  The file holds only that data — messages, event
+orders and expected read-outs — no reference source.  Run in the build
+container (the reference does not exist on the GPU box).
+
+Usage: python3 tests/golden/make_farm_golden.py
+"""
+import gzip
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+
+import ref_util  # noqa: E402
+
+OUT = os.path.join(HERE, "farm_vectors.json.gz")
+FARM_JS = os.path.join(ROOT, "oracle", "ref_farm.js")
+
+# (seed, clients incl. the observer, steps, initial text, checkpoints, text bound)
+SETS = [(1000 + i, 2 + i % 7, 300 + 150 * (i % 8), ["", "hello world", "x" * 40, "abc\ndef"][i % 4], 4,
+         [64, 200, 400][i % 3]) for i in range(40)]
+
+
+def main():
+    if not ref_util.ref_available():
+        sys.exit("the reference sources are not in this container")
+    out = ref_util.build_ref()
+    inp = {"sets": [{"seed": s, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m}
+                    for s, c, n, t, k, m in SETS]}
+    p = subprocess.run(["node", "--max-old-space-size=8192", FARM_JS, out], input=json.dumps(inp),
+                       capture_output=True, text=True, timeout=3600)
+    if p.returncode != 0:
+        sys.exit(p.stderr[-4000:])
+    res = json.loads(p.stdout)
+    res["generator"] = "oracle/ref_farm.js (reference Client, mulberry32 seeds)"
+    with gzip.open(OUT, "wt", encoding="utf-8") as fh:
+        json.dump(res, fh, separators=(",", ":"))
+    n_msgs = sum(len(s["log"]) for s in res["sets"])
+    print(f"wrote {OUT}: {len(res['sets'])} farms, {n_msgs} sequenced messages")
+
+
+if __name__ == "__main__":
+    main()
