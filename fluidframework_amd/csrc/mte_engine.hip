@@ -110,7 +110,7 @@ constexpr uint32_t kInitNl = 0x80000000u;
 
 __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_doc_init* inits,
                              const uint32_t* init_props, uint32_t n_keys, uint32_t n_docs,
-                             const uint64_t* img_off, uint32_t* tree) {
+                             const uint64_t* img_off, uint32_t* tree, uint32_t kt) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= n_docs) return;
   const mte_doc_init in = inits[d];
@@ -122,7 +122,7 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
   h.min_seq = in.min_seq;
   h.cur_seq = in.cur_seq;
   h.status = 0;
-  h.flags = in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC);
+  h.flags = in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC | MTE_DOC_LOCAL_CLIENT);
   h.resume = 0;
   h.pad0 = h.pad1 = 0;
   if (legacy) {
@@ -136,6 +136,11 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
     h.pad1 = (uint32_t)in.cur_seq;  // every later increase must reach it
   }
   hdr[d] = h;
+  if (in.flags & MTE_DOC_LOCAL_CLIENT) {  // no pending property keys (mte_stream.h)
+    const uint32_t nz = n_img ? n_img : 1u;
+    for (uint32_t k = 0; k < kt; k++)
+      for (uint32_t x = 0; x < nz; x++) soa.props[(kt + k) * soa.plane_stride + (uint64_t)d * cap + x] = 0u;
+  }
   if (n_img) return;  // image_kernel writes the segments
   const uint64_t i = (uint64_t)d * cap;
   soa.len[i] = (int32_t)in.text_len;
@@ -401,6 +406,7 @@ struct mte_ctx {
   uint32_t* d_tree_docs = nullptr;  // the legacy documents
   uint32_t n_tree = 0;
   std::vector<uint8_t> h_legacy;    // per doc
+  std::vector<uint8_t> h_local;     // per doc: MTE_DOC_LOCAL_CLIENT
   uint32_t* d_rs_docs = nullptr;    // legacy documents declared MTE_DOC_ROUND_SYNC (flat)
   int tree_rounds = 0;              // TIER 0 / TIER 1 rounds (MTE_TREE_ROUNDS; 0 = from the batch)
   // node level (mte_comm_*): the RCCL communicator and its staging buffers
@@ -497,7 +503,8 @@ int launch_reset(mte_ctx* c) {
   if (!c->n_docs) return MTE_OK;
   const uint32_t blocks = (c->n_docs + 255) / 256;
   hipLaunchKernelGGL(reset_kernel, dim3(blocks), dim3(256), 0, c->stream, c->hdr, c->soa, c->cap,
-                     c->d_inits, c->d_init_props, c->n_keys, c->n_docs, (const uint64_t*)c->d_img_off, c->d_tree);
+                     c->d_inits, c->d_init_props, c->n_keys, c->n_docs, (const uint64_t*)c->d_img_off, c->d_tree,
+                     c->kt);
   HIPCHK(c, hipGetLastError());
   if (c->n_img) {
     const uint64_t nb = std::min<uint64_t>((c->n_img + 255) / 256, 65536);
@@ -553,8 +560,15 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
 
 // Validation of one op record (the kernels index with these fields, so a bad
 // record must never reach them).  Returns nullptr or the reason.
-const char* bad_op(const mte_op& o, const mte_batch* b) {
-  if (o.type > MTE_OP_NOOP) return "type";
+const char* bad_op(const mte_op& o, const mte_batch* b, bool local_doc) {
+  if (o.type > MTE_OP_ACK) return "type";
+  if ((o.flags & MTE_F_LOCAL) || o.type == MTE_OP_ACK) {
+    if (!local_doc) return "local op or ack in a document without MTE_DOC_LOCAL_CLIENT";
+    if ((o.flags & MTE_F_LOCAL) && (o.type == MTE_OP_ACK || o.seq <= 0 || o.seq >= MTE_LOCAL_SEQ_BASE))
+      return "local record: type or localSeq out of range";
+    if (o.type == MTE_OP_ACK && (o.pos1 <= 0 || o.pos1 > o.pos2)) return "ack: localSeq range";
+  }
+  if (local_doc && !(o.flags & MTE_F_LOCAL) && o.seq >= MTE_LOCAL_SEQ_BASE) return "seq >= MTE_LOCAL_SEQ_BASE";
   if (o.type == MTE_OP_INSERT) {
     if (!(o.flags & MTE_F_MARKER) && o.pos2 > 0 && (uint64_t)o.a + (uint64_t)o.pos2 > b->text_units)
       return "text out of range";
@@ -594,9 +608,13 @@ int upload_ops(mte_ctx* c, const mte_batch* b, int w, uint64_t* bad, const char*
     for (unsigned w = 0; w < nw; w++) {
       th.emplace_back([&, w]() {
         const uint64_t a = n * w / nw, e = n * (w + 1) / nw;
+        // the document of record k0 + a, then a cursor over op_offsets
+        uint32_t d = (uint32_t)(std::upper_bound(b->op_offsets, b->op_offsets + b->n_docs + 1, k0 + a) -
+                                b->op_offsets) - 1;
         for (uint64_t k = a; k < e; k++) {
+          while (d + 1 < b->n_docs && b->op_offsets[d + 1] <= k0 + k) d++;
           const mte_op& o = b->ops[k0 + k];
-          if (const char* r = bad_op(o, b)) {
+          if (const char* r = bad_op(o, b, !c->h_local.empty() && c->h_local[d])) {
             uint64_t cur = first_bad.load();
             while (k0 + k < cur && !first_bad.compare_exchange_weak(cur, k0 + k)) {
             }
@@ -744,6 +762,9 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     const mte_doc_init& in = docs[d];
     if ((uint64_t)in.text_off + in.text_len > text_units || in.text_len > 0x7fffffffu)
       return set_err(c, MTE_E_INVALID_ARG, "doc %u: initial text out of range", d);
+    if ((in.flags & MTE_DOC_LOCAL_CLIENT) && (!(in.flags & MTE_DOC_NEW_LENGTH_CALC) || c->cap >= kChunkMinCap))
+      return set_err(c, MTE_E_UNSUPPORTED, "doc %u: a local client needs the new length calculation and a "
+                     "context below %u segments", d, kChunkMinCap);
     if (in.propset != MTE_NO_PROPS) {
       if (in.propset >= n_propsets || !propsets) return set_err(c, MTE_E_INVALID_ARG, "doc %u: bad propset", d);
       const mte_propset ps = propsets[in.propset];
@@ -760,11 +781,17 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
   c->n_ops = 0;
   const uint64_t nslots = (uint64_t)(n_docs ? n_docs : 1) * c->cap;
   c->soa.plane_stride = nslots;
+  c->h_local.assign(n_docs, 0);
+  bool any_local = false;
+  for (uint32_t d = 0; d < n_docs; d++)
+    if (docs[d].flags & MTE_DOC_LOCAL_CLIENT) c->h_local[d] = 1, any_local = true;
+  // documents with a local client hold kt more planes: the pending property keys (mte_stream.h)
+  const uint64_t prop_planes = (c->kt ? c->kt : 1) + (any_local ? c->kt : 0);
   HIPCHK(c, hipMalloc((void**)&c->hdr, sizeof(DocHdr) * (n_docs ? n_docs : 1)));
   // one allocation, planes at stride nslots: len seq rseq rmask meta toff props[kt]
   // (kt >= n_keys planes, so the register-resident kernels never index past it)
   {
-    const uint64_t planes = kFieldPlanes + (c->kt ? c->kt : 1);
+    const uint64_t planes = kFieldPlanes + prop_planes;
     uint32_t* base = nullptr;
     HIPCHK(c, hipMalloc((void**)&base, nslots * 4 * planes));
     c->soa.len = (int32_t*)base;
@@ -775,7 +802,7 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     c->soa.toff = base + 5 * nslots;
     c->soa.props = base + kFieldPlanes * nslots;
   }
-  HIPCHK(c, hipMemsetAsync(c->soa.props, 0, nslots * 4 * (c->kt ? c->kt : 1), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->soa.props, 0, nslots * 4 * prop_planes, c->stream));
   if (c->cap >= kChunkMinCap && n_docs) {
     // chunk arena: every doc can be re-laid out at kChFill segments per chunk
     const uint32_t nch_cap = c->cap / kChFill + 2;
@@ -810,7 +837,9 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     std::vector<uint32_t> flat_docs, tree_docs, rs_docs;
     c->h_legacy.assign(n_docs, 0);
     for (uint32_t d = 0; d < n_docs; d++) {
-      if (docs[d].flags & MTE_DOC_NEW_LENGTH_CALC) {
+      if (docs[d].flags & MTE_DOC_LOCAL_CLIENT) {
+        continue;  // the HBM-streamed pass replays them (mte_stream.h)
+      } else if (docs[d].flags & MTE_DOC_NEW_LENGTH_CALC) {
         flat_docs.push_back(d);
       } else if (docs[d].flags & MTE_DOC_ROUND_SYNC) {
         flat_docs.push_back(d);

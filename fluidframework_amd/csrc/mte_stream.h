@@ -54,15 +54,78 @@ __device__ __forceinline__ void tile_load_hot(Regs<kTileE, K>& R, const uint32_t
   }
 }
 
+// ---- documents with a local client (MTE_DOC_LOCAL_CLIENT, include/mte.h) ----
+// Pending seqs are kLocalBase + localSeq (UnassignedSequenceNumber, normalised
+// above every sequenced seq as breakTie / nodeLength do, mergeTree.ts:1009-1016,
+// 1713-1714).  K more planes after the property planes hold, per slot and key,
+// the localSeq of the last pending local annotate that set the key (0 = none):
+// the pendingKeyUpdateCount of segmentPropertiesManager.ts:94-135 (acks come in
+// order, so "count > 0" is "last pending localSeq not yet acked").
+constexpr int32_t kLocalBase = MTE_LOCAL_SEQ_BASE;
+
+// the local client's own view (localNetLength, mergeTree.ts:553-573, new
+// length calculation): removed -> 0, else the length; padding undefined
+template <int K>
+__device__ __forceinline__ void local_lengths(const Regs<kTileE, K>& R, int32_t (&L)[kTileE]) {
+#pragma unroll
+  for (int j = 0; j < kTileE; j++) L[j] = R.rseq[j] == kPad ? -1 : (R.rseq[j] != kNone ? 0 : R.len[j]);
+}
+
+// insertingWalk slot for a remote insert in a document with pending local
+// segments: as find_slot, passing over the pending ones (breakTie gives them
+// MAX_SAFE_INTEGER - 1, continuePredicate moves past them at a block's end,
+// mergeTree.ts:1599-1611, 1705-1721, 1790)
+template <int E>
+__device__ __forceinline__ int find_slot_remote(const int32_t (&L)[E], const int32_t (&P)[E],
+                                                const int32_t (&seq)[E], int32_t pos) {
+  int jsel = E;
+#pragma unroll
+  for (int j = E - 1; j >= 0; j--) jsel = (L[j] >= 0 && P[j] >= pos && seq[j] < kLocalBase) ? j : jsel;
+  const unsigned long long msk = __ballot(jsel < E);
+  if (!msk) return -1;
+  const int ls = __ffsll((long long)msk) - 1;
+  return ls * E + rdlane(jsel, ls);
+}
+
+// MTE_OP_ACK: ackPendingSegment for localSeqs lo..hi (mergeTree.ts:1278-1331,
+// BaseSegment.ack mergeTreeNodes.ts:475-503): pending inserts and removals of
+// those ops take seq (a removal a remote op overtook already has its seq,
+// :1928-1938), and their property keys stop being pending.
+template <int K>
+__device__ __forceinline__ void stream_ack(uint32_t* pl, uint64_t sd, int n, int32_t lo, int32_t hi, int32_t s) {
+  const int l = lane_id();
+  for (int tb = 0; tb < n; tb += kTile) {
+#pragma unroll
+    for (int j = 0; j < kTileE; j++) {
+      const int i = tb + l * kTileE + j;
+      if (i >= n) continue;
+#pragma unroll
+      for (int p = 1; p <= 2; p++) {  // seq, removedSeq
+        const int32_t v = (int32_t)ld_l2(pl + p * sd + i);
+        if (v >= kLocalBase + lo && v <= kLocalBase + hi) pl[p * sd + i] = (uint32_t)s;
+      }
+#pragma unroll
+      for (int kk = 0; kk < K; kk++) {
+        uint32_t* q = pl + (uint64_t)(kFieldPlanes + K + kk) * sd + i;
+        const uint32_t v = ld_l2(q);
+        if (v != 0u && v <= (uint32_t)hi) *q = 0u;
+      }
+    }
+  }
+  vm_drain();
+}
+
 // One op of one HBM-resident document (see the file comment).  Returns 0 or
-// a negative MTE_E_*.
+// a negative MTE_E_*.  lseq: the document's last localSeq (local-client docs).
 template <int K, bool S>
-__device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const ReplayArgs& a, uint32_t* zlds) {
+__device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const ReplayArgs& a, uint32_t* zlds,
+                           int32_t& lseq) {
   constexpr int E = kTileE;
   const int l = lane_id();
   uint32_t* pl = a.planes + (uint64_t)D.doc * a.cap;
   const uint64_t sd = a.stride;
-  const int nplanes = kFieldPlanes + K;
+  const bool ldoc = (D.flags & MTE_DOC_LOCAL_CLIENT) != 0;
+  const int nplanes = kFieldPlanes + K + (ldoc ? K : 0);  // + the pending-key planes
 
   const s8v op = cur;
   const uint4* rec = D.recp + 2 * D.k;
@@ -70,11 +133,20 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
-  if (type > MTE_OP_NOOP) return MTE_E_INVALID_ARG;
+  if (type > MTE_OP_ACK) return MTE_E_INVALID_ARG;
+  const bool lop = (flags & MTE_F_LOCAL) != 0;  // a local op: the local view, seq = localSeq
+  if ((lop || type == MTE_OP_ACK) && !ldoc) return MTE_E_UNSUPPORTED;
   MTE_STAT(st[kStOps]++;)
   MTE_STAT(st[kStMaxSegs] = (uint32_t)D.n > st[kStMaxSegs] ? (uint32_t)D.n : st[kStMaxSegs];)
   const int32_t s = op[0], r = op[1], msn = op[2];
   const int32_t pos1 = op[4], pos2 = op[5];
+  if (lop) {
+    if (!(s > lseq && s < kLocalBase) || c != 0) return MTE_E_INVALID_ARG;
+    if (type == MTE_OP_ANNOTATE && (flags & MTE_F_REWRITE)) return MTE_E_UNSUPPORTED;
+    lseq = s;
+  } else if (ldoc && type <= MTE_OP_ANNOTATE && c == 0) {
+    return MTE_E_INVALID_ARG;  // a remote op from the local client's own slot
+  }
   const bool ins = type == MTE_OP_INSERT;
   const bool marker = ins && (flags & MTE_F_MARKER) != 0;
   const int32_t nlen = marker ? 1 : pos2;  // insert: length of the new segment
@@ -82,6 +154,11 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   const bool newcalc = (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
   int n = D.n;
 
+  if (type == MTE_OP_ACK) {
+    if (!(pos1 > 0 && pos1 <= pos2 && pos2 <= lseq)) return MTE_E_INVALID_ARG;
+    MTE_STAT(st[kStScanned] += (uint32_t)n;)
+    stream_ack<K>(pl, sd, n, pos1, pos2, s);
+  }
   if (ins || rng) {
     MTE_STAT(st[kStScanned] += (uint32_t)n;)
     // ---- A: scan -----------------------------------------------------------
@@ -96,7 +173,8 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
       Regs<E, K> R;
       tile_load_hot<K>(R, pl, sd, tb, n);
       int32_t L[E], P[E];
-      leaf_lengths<E, K>(R, r, c + 1, (int)c, D.min_seq, newcalc, L);
+      if (lop) local_lengths<K>(R, L);
+      else leaf_lengths<E, K>(R, r, c + 1, (int)c, D.min_seq, newcalc, L);
       const int32_t tot = prefix<E>(L, P);
 #pragma unroll
       for (int j = 0; j < E; j++) P[j] += carry;
@@ -121,7 +199,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
         }
       }
       if (ins && gs < 0) {
-        const int x = find_slot<E>(L, P, pos1);
+        const int x = (ldoc && !lop) ? find_slot_remote<E>(L, P, R.seq, pos1) : find_slot<E>(L, P, pos1);
         if (x >= 0) gs = tb + x;
       }
       carry += tot;
@@ -221,7 +299,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
       }
       if (g >= 0) {
         pl[g] = (uint32_t)nlen;
-        pl[sd + g] = (uint32_t)s;
+        pl[sd + g] = (uint32_t)(lop ? kLocalBase + s : s);
         pl[2 * sd + g] = (uint32_t)kNone;
         pl[3 * sd + g] = 0u;
         pl[4 * sd + g] = (c + 1u) | (marker ? (1u + (uint32_t)pos2) << 8 : 0u);
@@ -242,6 +320,10 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
       if (l == 0) {
 #pragma unroll
         for (int kk = 0; kk < K; kk++) pl[(kFieldPlanes + kk) * sd + g] = pr[kk][0];
+        if (ldoc) {
+#pragma unroll
+          for (int kk = 0; kk < K; kk++) pl[(kFieldPlanes + K + kk) * sd + g] = 0u;  // nothing pending
+        }
       }
       MTE_STAT(if (!marker) st[kStUnits] += (uint32_t)pos2;)
     }
@@ -257,7 +339,8 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
         Regs<E, K> R;
         tile_load_hot<K>(R, pl, sd, tb, n);
         int32_t L[E], P[E];
-        leaf_lengths<E, K>(R, r, c + 1, (int)c, D.min_seq, newcalc, L);
+        if (lop) local_lengths<K>(R, L);
+        else leaf_lengths<E, K>(R, r, c + 1, (int)c, D.min_seq, newcalc, L);
         const int32_t tot = prefix<E>(L, P);
         bool in[E];
         uint32_t cnt = 0;
@@ -276,8 +359,12 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
 #pragma unroll
           for (int j = 0; j < E; j++) {
             if (in[j]) {
-              pl[2 * sd + base + j] = (uint32_t)(R.rseq[j] == kNone ? s : R.rseq[j]);
-              pl[3 * sd + base + j] = R.rmask[j] | (1u << c);
+              // a local removal: removedSeq Unassigned, removers [local]; a
+              // remote one keeps an earlier removedSeq but overtakes a pending
+              // local one (kNone and pending seqs are both >= kLocalBase)
+              pl[2 * sd + base + j] =
+                  (uint32_t)(lop ? kLocalBase + s : ((ldoc ? R.rseq[j] >= kLocalBase : R.rseq[j] == kNone) ? s : R.rseq[j]));
+              pl[3 * sd + base + j] = lop ? 1u : (R.rmask[j] | (1u << c));
             }
           }
         } else if (K > 0) {
@@ -291,7 +378,36 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
               pr[kk][j] = i < n ? ld_l2(pl + (kFieldPlanes + kk) * sd + i) : 0u;
               if (flags & MTE_F_REWRITE) pr[kk][j] = in[j] ? 0u : pr[kk][j];
             }
+          uint32_t old[K > 0 ? K : 1][E], pk[K > 0 ? K : 1][E];
+#pragma unroll
+          for (int kk = 0; kk < K; kk++)
+#pragma unroll
+            for (int j = 0; j < E; j++) {
+              const int i = base + j;
+              old[kk][j] = i < n ? ld_l2(pl + (kFieldPlanes + kk) * sd + i) : 0u;
+              pk[kk][j] = (ldoc && i < n) ? ld_l2(pl + (kFieldPlanes + K + kk) * sd + i) : 0u;
+            }
           apply_props<E, K>(pr, in, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], (uint32_t)op[6], a);
+          if (ldoc && !lop) {
+            // shouldModifyKey: a key with a pending local update keeps its
+            // value, the rewrite's clear included (segmentPropertiesManager.ts:94-135)
+#pragma unroll
+            for (int kk = 0; kk < K; kk++)
+#pragma unroll
+              for (int j = 0; j < E; j++) pr[kk][j] = pk[kk][j] ? old[kk][j] : pr[kk][j];
+          }
+          if (lop) {
+            // the local annotate's keys become pending on the marked slots
+            const mte_propset ps = a.ps[(uint32_t)op[6]];
+            for (uint32_t t = 0; t < ps.count; t++) {
+              const uint32_t key = uni(a.pe[ps.first + t].key);
+              if (key < (uint32_t)K) {
+#pragma unroll
+                for (int j = 0; j < E; j++)
+                  if (in[j]) pl[(kFieldPlanes + K + key) * sd + base + j] = (uint32_t)s;
+              }
+            }
+          }
 #pragma unroll
           for (int kk = 0; kk < K; kk++)
 #pragma unroll
@@ -306,6 +422,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   }
   D.n = n;
   D.k++;
+  if (lop) return 0;  // a local op moves no window
 
   if (type != MTE_OP_NOOP) {  // Client.completeAndLogOp (client.ts:525-528)
     if (!(D.cur_seq < s)) return MTE_E_SEQ_ORDER;
@@ -364,14 +481,17 @@ __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
   const int doc = (int)blockIdx.x * kDocsPerBlock + w;
   if (doc >= (int)a.n_docs) return;
-  if (!(a.hdr[doc].flags & kHdrNeedsEsc)) return;  // untouched doc: leave the header alone
+  // documents pass 2 escalated, and every document with a local client
+  const uint32_t hf = a.hdr[doc].flags;
+  if (!(hf & (kHdrNeedsEsc | MTE_DOC_LOCAL_CLIENT))) return;  // untouched doc: leave the header alone
   DocRun D;
-  run_init(D, a, doc, true);
+  run_init(D, a, doc, !(hf & MTE_DOC_LOCAL_CLIENT));
   uint32_t st[kNumStats] = {};
+  int32_t lseq = (int32_t)a.hdr[doc].pad0;  // local-client docs: the last localSeq
   if (D.running) {
     s8v cur = sload8(D.recp + 2 * D.k);
     while (D.running) {
-      const int rc = stream_step<K, S>(D, st, cur, a, zlds_all[w]);
+      const int rc = stream_step<K, S>(D, st, cur, a, zlds_all[w], lseq);
       if (rc < 0) {
         D.status = rc;
         D.running = false;
@@ -383,6 +503,7 @@ __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
     }
     if constexpr (S) run_flush_stats(D, st, a);
   }
+  if ((hf & MTE_DOC_LOCAL_CLIENT) && lane_id() == 0) a.hdr[doc].pad0 = (uint32_t)lseq;  // run_finish keeps it
   run_finish(D, a);
 }
 

@@ -54,6 +54,10 @@ export interface SegmentWithMergeInfo {
 
 export interface ClientOptions {
   observerId?: string;
+  /** This client sends ops of its own (MTE_DOC_LOCAL_CLIENT; needs newLengthCalc):
+   *  observerId / longClientId name it, its sequenced messages are acks. */
+  localClient?: boolean;
+  longClientId?: string;
   newLengthCalc?: boolean;
   props?: PropertySet;
   minSeq?: number;
@@ -167,7 +171,16 @@ export interface VisibleSegment {
 export class BatchClient {
   readonly mergeTree: BatchMergeTree;
   readonly longClientId: string;
+  /** A remote message, or (localClient documents) the sequenced message of an own op: its ack. */
   applyMsg(msg: ISequencedDocumentMessage, local?: boolean): void;
+  // local ops ({localClient: true, newLengthCalc: true} documents); each returns the op to send
+  insertTextLocal(pos: number, text: string, props?: PropertySet): IMergeTreeOp;
+  insertMarkerLocal(pos: number, refType: number, props?: PropertySet): IMergeTreeOp;
+  insertSegmentLocal(pos: number, segment: unknown): IMergeTreeOp;
+  removeRangeLocal(start: number, end: number): IMergeTreeOp;
+  annotateRangeLocal(start: number, end: number, props: PropertySet, combiningOp?: { name: string }): IMergeTreeOp;
+  makeOpMessage(op: IMergeTreeOp, seq?: number, refSeq?: number, minSeq?: number): ISequencedDocumentMessage;
+  getPendingCount(): number;
   getOrAddShortClientId(longId: string): number;
   getClientId(): number;
   getLongClientId(shortId: number): string | undefined;

@@ -93,9 +93,13 @@ class MergeTreeEngine {
     if (o.summary) o = Object.assign({}, o, { legacy: o.summary });
     if (o.legacy) o = Object.assign({}, o, loadLegacy(o.legacy));
     const doc = this.docs.length;
+    if (o.localClient && !o.newLengthCalc) {
+      throw new MergeTreeError(-9, "a local client needs the new length calculation (client.conflictFarm.spec.ts:84)");
+    }
     this.docs.push({ text: initialText || "", newLengthCalc: !!o.newLengthCalc, roundSync: !!o.roundSync, props: o.props,
-      minSeq: o.minSeq || 0, currentSeq: o.currentSeq || 0, segments: o.segments });
-    const c = new BatchClient(this, doc, o.observerId === undefined ? "A" : o.observerId);
+      minSeq: o.minSeq || 0, currentSeq: o.currentSeq || 0, segments: o.segments, localClient: !!o.localClient });
+    const c = new BatchClient(this, doc, o.observerId === undefined ? (o.longClientId || "A") : o.observerId,
+      !!o.localClient);
     this.clients.push(c);
     if (o.legacy && o.legacy.catchupOps) {
       // SharedSegmentSequence.loadCore (sequence.ts:588-609): catch-up ops above the window
@@ -266,11 +270,11 @@ class MergeTreeEngine {
 }
 
 class BatchClient {
-  constructor(engine, doc, observerId) {
+  constructor(engine, doc, observerId, local) {
     this.engine = engine;
     this.doc = doc;
     this.longClientId = observerId;
-    this.clients = new DocClients(observerId, engine.docs[doc].minSeq);
+    this.clients = new DocClients(observerId, engine.docs[doc].minSeq, local);
     this.lastMinSeq = 0;
     const self = this;
     // MergeTree-level entry points (clientId = short id, as in the reference)
@@ -296,11 +300,69 @@ class BatchClient {
     };
   }
 
-  /** Client.applyMsg (client.ts:918-935); remote messages only. */
+  /** Client.applyMsg (client.ts:918-935): a remote message, or — in a
+   *  document created with {localClient: true} — the sequenced message of one
+   *  of this client's own local ops, which acks its oldest pending op
+   *  (ackPendingSegment, mergeTree.ts:1278-1331). */
   applyMsg(msg, local) {
-    if (local) throw new MergeTreeError(-9, "local ops are not supported by the batch engine");
+    if (local) throw new MergeTreeError(-9, "applyMsg(msg, local = true): pass the sequenced message");
     this.engine._batch().addMessage(this.doc, this.clients, msg);
     if (msg.minimumSequenceNumber > this.lastMinSeq) this.lastMinSeq = msg.minimumSequenceNumber;
+  }
+
+  // ---- local ops (documents created with {localClient: true}) ----
+  // Each queues the op for this document's next replay, where it applies at
+  // once in this client's view with seq UnassignedSequenceNumber, and returns
+  // the op to send (client.ts:131-229).  Positions are in this client's view
+  // (getLength() etc. flush first, as any read-out).
+
+  _local(op) {
+    this.engine._batch().addLocal(this.doc, this.clients, op);
+    return op;
+  }
+
+  /** Client.insertSegmentLocal with a TextSegment (TestClient.insertTextLocal, test/testClient.ts:179-189). */
+  insertTextLocal(pos, text, props) {
+    return this._local({ type: 0, pos1: pos, seg: props ? { text, props } : text });
+  }
+
+  /** Client.insertSegmentLocal with a Marker (TestClient.insertMarkerLocal, test/testClient.ts:224-235). */
+  insertMarkerLocal(pos, refType, props) {
+    const seg = { marker: { refType } };
+    if (props) seg.props = props;
+    return this._local({ type: 0, pos1: pos, seg });
+  }
+
+  /** Client.insertSegmentLocal (client.ts:216-229) with a segment or its JSON spec. */
+  insertSegmentLocal(pos, segment) {
+    return this._local({ type: 0, pos1: pos, seg: segmentSpec(segment) });
+  }
+
+  /** Client.removeRangeLocal (client.ts:206-214). */
+  removeRangeLocal(start, end) {
+    return this._local({ type: 1, pos1: start, pos2: end });
+  }
+
+  /** Client.annotateRangeLocal (client.ts:183-204); combiningOp rewrite is not supported locally. */
+  annotateRangeLocal(start, end, props, combiningOp) {
+    const op = { type: 2, pos1: start, pos2: end, props };
+    if (combiningOp) op.combiningOp = combiningOp;
+    return this._local(op);
+  }
+
+  /** TestClient.makeOpMessage (test/testClient.ts:259-272): the message to
+   *  sequence for a local op. */
+  makeOpMessage(op, seq, refSeq, minSeq) {
+    return {
+      clientId: this.longClientId, sequenceNumber: seq === undefined ? -1 : seq,
+      referenceSequenceNumber: refSeq === undefined ? this.getCurrentSeq() : refSeq,
+      minimumSequenceNumber: minSeq === undefined ? 0 : minSeq, type: "op", contents: op,
+    };
+  }
+
+  /** Local ops sent but not acknowledged yet. */
+  getPendingCount() {
+    return this.clients.pending.length;
   }
 
   /** Client.getOrAddShortClientId (client.ts:683-698).  A short id handed out

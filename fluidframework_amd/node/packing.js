@@ -28,8 +28,9 @@
  * for record (tests/test_node_host.py checks the bytes are identical).
  */
 
-const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 3;
-const F_MARKER = 0x1, F_MSG_END = 0x2, F_REWRITE = 0x4;
+const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 3, OP_ACK = 4;
+const F_MARKER = 0x1, F_MSG_END = 0x2, F_REWRITE = 0x4, F_LOCAL = 0x8;
+const LOCAL_SEQ_BASE = 0x40000000; // MTE_LOCAL_SEQ_BASE
 const NO_PROPS = 0xffffffff;
 const MAX_CLIENTS = 32;
 const OP_BYTES = 32;
@@ -40,7 +41,8 @@ const DOC_NEW_LENGTH_CALC = 0x1;
 const INSERT = 0, REMOVE = 1, ANNOTATE = 2, GROUP = 3;
 
 const DOC_ROUND_SYNC = 0x2; // MTE_DOC_ROUND_SYNC (include/mte.h)
-const E_INVALID_ARG = -1, E_UNSUPPORTED = -9, E_CLIENT_RANGE = -12;
+const DOC_LOCAL_CLIENT = 0x4; // MTE_DOC_LOCAL_CLIENT
+const E_INVALID_ARG = -1, E_UNSUPPORTED = -9, E_STATE = -10, E_CLIENT_RANGE = -12;
 
 class MergeTreeError extends Error {
   constructor(code, message) {
@@ -117,11 +119,17 @@ class Interner {
  *  visibility rule any more (same rule as fluidframework_amd/packing.py). */
 const NEVER = 0x7fffffff;
 class DocClients {
-  constructor(observerId, minSeq) {
+  constructor(observerId, minSeq, local) {
     this.observer = observerId;
     this.ids = new Map([[observerId, 0]]);
     this.last = new Map([[0, NEVER]]); // slot -> highest seq its client used
     this.minSeq = minSeq || 0;          // the window's minSeq before the next message
+    // a document whose own client sends (MTE_DOC_LOCAL_CLIENT): collabWindow.localSeq
+    // and the [first, last] localSeqs of each unacked local message, oldest first
+    // (MergeTree.pendingSegments, mergeTree.ts:1333-1355)
+    this.local = !!local;
+    this.localSeq = 0;
+    this.pending = [];
   }
   short(longId, seq) {
     let i = this.ids.get(longId);
@@ -216,9 +224,14 @@ class BatchBuilder {
     const recs = [];
     if ((msg.type === undefined ? "op" : msg.type) === "op") {
       if (sender === clients.observer) {
-        throw new MergeTreeError(E_UNSUPPORTED, "ack of a local op (observer replay only)");
+        // our own op, sequenced: ackPendingSegment (client.ts:925-928)
+        if (!clients.local) throw new MergeTreeError(E_UNSUPPORTED, "ack of a local op in an observer document");
+        if (clients.pending.length === 0) throw new MergeTreeError(E_STATE, "ack without a pending local op");
+        const [lo, hi] = clients.pending.shift();
+        recs.push([OP_ACK, 0, lo, hi, 0, NO_PROPS]);
+      } else {
+        this._opRecords(msg.contents, recs);
       }
-      this._opRecords(msg.contents, recs);
     }
     // the slot is taken only once the message has validated
     const short = slotOf(clients, sender, seq);
@@ -227,6 +240,26 @@ class BatchBuilder {
     for (const r of recs) this.docOps[doc].push([seq, ref, msn, r[0], short, r[1], r[2], r[3], r[4], r[5]]);
     this.count += recs.length;
     clients.advance(msn);
+  }
+
+  /** A local op of the document's own client (insertSegmentLocal /
+   *  removeRangeLocal / annotateRangeLocal, client.ts:131-229): one F_LOCAL record
+   *  per (GROUP member) op, each with the next localSeq; the message's localSeqs
+   *  join the pending list, acked in order by addMessage (as packing.py add_local). */
+  addLocal(doc, clients, op) {
+    if (!clients.local) throw new MergeTreeError(E_UNSUPPORTED, "local op in an observer document");
+    const recs = [];
+    this._opRecords(op, recs);
+    if (recs.length === 0) recs.push([OP_NOOP, 0, 0, 0, 0, NO_PROPS]);
+    if (recs.some((r) => r[1] & F_REWRITE)) throw new MergeTreeError(E_UNSUPPORTED, "local combiningOp rewrite");
+    const first = clients.localSeq + 1;
+    if (first + recs.length >= LOCAL_SEQ_BASE) throw new MergeTreeError(E_INVALID_ARG, "localSeq overflow");
+    recs.forEach((r, i) => {
+      this.docOps[doc].push([first + i, 0, 0, r[0], 0, r[1] | F_LOCAL, r[2], r[3], r[4], r[5]]);
+    });
+    this.count += recs.length;
+    clients.localSeq += recs.length;
+    clients.pending.push([first, clients.localSeq]);
   }
 
   /** One MergeTree-level call (insertSegments / markRangeRemoved / annotateRange):
@@ -337,7 +370,8 @@ function packDocInits(docs, interner) {
     const o = i * DOC_INIT_BYTES;
     buf.writeUInt32LE(off, o);
     buf.writeUInt32LE(d.text.length, o + 4);
-    buf.writeUInt32LE((d.newLengthCalc ? DOC_NEW_LENGTH_CALC : 0) | (d.roundSync ? DOC_ROUND_SYNC : 0), o + 8);
+    buf.writeUInt32LE((d.newLengthCalc ? DOC_NEW_LENGTH_CALC : 0) | (d.roundSync ? DOC_ROUND_SYNC : 0) |
+      (d.localClient ? DOC_LOCAL_CLIENT : 0), o + 8);
     buf.writeUInt32LE(props.add(d.props) >>> 0, o + 12);
     buf.writeInt32LE(d.minSeq || 0, o + 16);
     buf.writeInt32LE(d.currentSeq || 0, o + 20);
@@ -416,7 +450,7 @@ function packSegments(docs, clientsOf, inits) {
 }
 
 module.exports = {
-  OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, F_MARKER, F_MSG_END, F_REWRITE, NO_PROPS, MAX_CLIENTS,
+  OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_ACK, F_MARKER, F_MSG_END, F_REWRITE, F_LOCAL, NO_PROPS, MAX_CLIENTS,
   INSERT, REMOVE, ANNOTATE, GROUP,
   MergeTreeError, Interner, DocClients, PropTable, BatchBuilder, canonicalJson, packDocInits, packSegments, utf16,
 };

@@ -695,8 +695,20 @@ static void* worker(void* p) {
 int orc_apply_batch(orc_ctx* c, const mte_batch* b, int n_threads) {
   if (!c || !b || b->n_docs != c->n_docs || !b->op_offsets) return MTE_E_INVALID_ARG;
   if (b->op_offsets[b->n_docs] != b->n_ops) return MTE_E_INVALID_ARG;
+  uint32_t dcur = 0;
   for (uint64_t k = 0; k < b->n_ops; k++) {
     const mte_op* op = &b->ops[k];
+    while (dcur + 1 < b->n_docs && b->op_offsets[dcur + 1] <= k) dcur++;
+    /* local records (as mte_submit validates them) */
+    const int local_doc = (c->docs[dcur].flags & MTE_DOC_LOCAL_CLIENT) != 0;
+    if (op->type > MTE_OP_ACK) return MTE_E_INVALID_ARG;
+    if ((op->flags & MTE_F_LOCAL) || op->type == MTE_OP_ACK) {
+      if (!local_doc) return MTE_E_INVALID_ARG;
+      if ((op->flags & MTE_F_LOCAL) && (op->type == MTE_OP_ACK || op->seq <= 0 || op->seq >= MTE_LOCAL_SEQ_BASE))
+        return MTE_E_INVALID_ARG;
+      if (op->type == MTE_OP_ACK && (op->pos1 <= 0 || op->pos1 > op->pos2)) return MTE_E_INVALID_ARG;
+    }
+    if (local_doc && !(op->flags & MTE_F_LOCAL) && op->seq >= MTE_LOCAL_SEQ_BASE) return MTE_E_INVALID_ARG;
     if (op->type == MTE_OP_INSERT && !(op->flags & MTE_F_MARKER) && op->pos2 > 0 &&
         (uint64_t)op->a + (uint64_t)op->pos2 > b->text_units)
       return MTE_E_INVALID_ARG;

@@ -1,0 +1,96 @@
+"use strict";
+// GPU test: conflict farms with EVERY client a BatchClient of its own
+// ({localClient: true}).  The sets are the ones the reference ran
+// (tests/golden/farm_vectors.json.gz, made by tests/golden/make_farm_golden.py
+// through oracle/ref_farm.js): each client replays its own events in order —
+// its local ops through insertSegmentLocal / removeRangeLocal /
+// annotateRangeLocal (the returned op must be the op the reference sent), the
+// sequenced messages through applyMsg (its own ones are acks) — and at every
+// checkpoint its text, length and per-position properties must be the
+// reference client's.  argv "sync": every local op reads the client's length
+// first, as the farm's op generator does (a flush + replay per op).
+// Prints one JSON line.
+const fs = require("fs");
+const path = require("path");
+const zlib = require("zlib");
+const { MergeTreeEngine } = require("../../fluidframework_amd/node");
+const { asMsg } = require("./fixtures");
+
+const sets = JSON.parse(zlib.gunzipSync(fs.readFileSync(path.join(__dirname, "..", "golden",
+  "farm_vectors.json.gz"))).toString("utf8")).sets;
+const nSets = process.argv[3] ? Number(process.argv[3]) : sets.length;
+const sync = process.argv[2] === "sync";
+
+function sortKeys(v) {
+  if (v && typeof v === "object" && !Array.isArray(v)) {
+    const o = {};
+    for (const k of Object.keys(v).sort()) o[k] = sortKeys(v[k]);
+    return o;
+  }
+  return v;
+}
+function propRuns(c) {
+  const runs = [];
+  let cur = null, start = 0;
+  const n = c.getLength();
+  for (let p = 0; p < n; p++) {
+    const pr = c.getPropertiesAtPosition(p);
+    const key = pr && Object.keys(pr).length ? JSON.stringify(sortKeys(pr)) : "";
+    if (key !== cur) {
+      if (cur) runs.push([start, p, JSON.parse(cur)]);
+      cur = key;
+      start = p;
+    }
+  }
+  if (cur) runs.push([start, n, JSON.parse(cur)]);
+  return runs;
+}
+
+const eng = new MergeTreeEngine({ nKeys: 8 });
+const layout = [];
+for (let si = 0; si < nSets; si++) {
+  sets[si].names.forEach((name, ci) => {
+    layout.push({ si, ci, client: eng.createClient(sets[si].initialText,
+      { newLengthCalc: true, localClient: true, longClientId: name }) });
+  });
+}
+let passed = 0, opsChecked = 0;
+const failures = [];
+const prev = layout.map(() => 0);
+const nCp = Math.max.apply(null, sets.slice(0, nSets).map((s) => s.checkpoints.length));
+for (let j = 0; j < nCp; j++) {
+  layout.forEach((L, d) => {
+    const s = sets[L.si];
+    if (j >= s.checkpoints.length) return;
+    const done = s.checkpoints[j].done[L.ci];
+    for (const [kind, li] of s.events[L.ci].slice(prev[d], done)) {
+      const m = asMsg(s.log[li]);
+      if (kind === "A") {
+        L.client.applyMsg(m);
+        continue;
+      }
+      if (sync) L.client.getLength();
+      const o = m.contents;
+      let op;
+      if (o.type === 0) op = L.client.insertSegmentLocal(o.pos1, o.seg);
+      else if (o.type === 1) op = L.client.removeRangeLocal(o.pos1, o.pos2);
+      else op = L.client.annotateRangeLocal(o.pos1, o.pos2, o.props);
+      if (JSON.stringify(sortKeys(op)) !== JSON.stringify(sortKeys(o))) failures.push([L.si, L.ci, j, "op", op, o]);
+      opsChecked++;
+    }
+    prev[d] = done;
+  });
+  layout.forEach((L) => {
+    const s = sets[L.si];
+    if (j >= s.checkpoints.length) return;
+    const want = s.checkpoints[j].states[L.ci];
+    const got = { text: L.client.getText(), length: L.client.getLength(), props: propRuns(L.client) };
+    if (got.text === want.text && got.length === want.length &&
+        JSON.stringify(got.props) === JSON.stringify(want.props)) passed++;
+    else failures.push([L.si, L.ci, j, "state"]);
+  });
+}
+const pending = layout.reduce((a, L) => a + L.client.getPendingCount(), 0);
+process.stdout.write(JSON.stringify({ passed, opsChecked, pending, failures: failures.slice(0, 5),
+  nFailures: failures.length, docs: layout.length }) + "\n");
+eng.close();

@@ -76,6 +76,38 @@ def test_js_packing_matches_python_packing_on_fixtures(fresh):
             assert base64.b64decode(j[key]) == np.ascontiguousarray(arr).tobytes(), (r, key)
 
 
+def test_js_packing_matches_python_packing_on_local_farms():
+    """Local ops and acks: the JS and Python packers emit the same bytes for
+    the reference farm vectors (tests/node/pack_farm.js)."""
+    import gzip
+    lines = node("tests/node/pack_farm.js").splitlines()
+    with gzip.open(os.path.join(ROOT, "tests", "golden", "farm_vectors.json.gz"), "rt") as fh:
+        sets = json.load(fh)["sets"]
+    interner = Interner(8)
+    layout = [(si, ci, DocClients(name, local=True)) for si, s in enumerate(sets) for ci, name in enumerate(s["names"])]
+    prev = [0] * len(layout)
+    assert len(lines) == max(len(s["checkpoints"]) for s in sets)
+    for j, line in enumerate(lines):
+        bb = BatchBuilder(len(layout), interner)
+        for d, (si, ci, cl) in enumerate(layout):
+            s = sets[si]
+            if j >= len(s["checkpoints"]):
+                continue
+            done = s["checkpoints"][j]["done"][ci]
+            for kind, li in s["events"][ci][prev[d]:done]:
+                m = as_msg(s["log"][li])
+                if kind == "L":
+                    bb.add_local(d, cl, m["contents"])
+                else:
+                    bb.add_message(d, cl, m)
+            prev[d] = done
+        b = bb.build()
+        jj = json.loads(line)
+        for key, arr in (("offsets", b["op_offsets"]), ("ops", b["ops"]), ("text", b["text"]),
+                         ("propsets", b["propsets"]), ("props", b["props"])):
+            assert base64.b64decode(jj[key]) == np.ascontiguousarray(arr).tobytes(), (j, key)
+
+
 @pytest.mark.gpu
 def test_node_batch_client_replays_fixtures_on_gpu():
     j = json.loads(node("tests/node/replay_fixtures_gpu.js", timeout=600))
@@ -251,3 +283,20 @@ process.stdout.write(JSON.stringify(out));
 """
     j = json.loads(node("-e", script).strip().splitlines()[-1])  # RCCL prints a banner first
     assert j == {"sum": 3, "max": -2, "text": "hello world", "equal": True, "pad": True}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["batched", "sync"])
+def test_node_farm_every_client_local_on_gpu(mode):
+    """Every farm client a BatchClient with local ops and acks (tests/node/farm_gpu.js)
+    against the reference's farm vectors; "sync" reads the length before every
+    local op (one replay per op), as the farm's generator does, on 6 farms."""
+    args = ["tests/node/farm_gpu.js", mode] + (["6"] if mode == "sync" else [])
+    j = json.loads(node(*args, timeout=600))
+    assert j["nFailures"] == 0, j["failures"]
+    assert j["pending"] == 0 and j["opsChecked"] > 0
+    if mode == "batched":
+        import gzip
+        with gzip.open(os.path.join(ROOT, "tests", "golden", "farm_vectors.json.gz"), "rt") as fh:
+            sets = json.load(fh)["sets"]
+        assert j["passed"] == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
