@@ -37,6 +37,12 @@
 #ifndef MTE_FAIR_PRIO  // pass-1 issue priority policy (below)
 #define MTE_FAIR_PRIO 4
 #endif
+#ifndef MTE_VREC  // 1: pass-1 op records fetched with vector loads (vmcnt), 0: scalar loads (lgkmcnt)
+#define MTE_VREC 0
+#endif
+#ifndef MTE_E1_DPP  // 1: the E = 1 shift moves slots with DPP instead of ds_bpermute
+#define MTE_E1_DPP 0
+#endif
 #ifndef MTE_OUTLINE  // 1: pass-1 tiers as out-of-line functions (measured: same time, 1.7x the HBM traffic)
 #define MTE_OUTLINE 0
 #endif
@@ -74,6 +80,20 @@ typedef const __attribute__((address_space(4))) s8v* cs8p;
 __device__ __forceinline__ s8v sload8(const uint4* p) { return *(cs8p)(const void*)p; }
 // compiled propset `psi` (mte_kernels.h)
 __device__ __forceinline__ s8v sload_props(const ReplayArgs& a, uint32_t psi) { return sload8(a.cps + 2 * psi); }
+
+// op record through a vector load: dword i in lane i < 8.  Its wait is on
+// vmcnt, so the LDS traffic of an op (shift permutes, zamboni) never waits for
+// the next record as it does for a scalar load in flight (SMEM and LDS share
+// lgkmcnt, and SMEM returns out of order, so any LDS wait becomes lgkmcnt(0)).
+__device__ __forceinline__ uint32_t vload_rec8(const uint4* rec) {
+  const int l = __lane_id();
+  return l < 8 ? reinterpret_cast<const uint32_t*>(rec)[l] : 0u;
+}
+#if MTE_VREC
+typedef uint32_t RecV;  // the prefetched record of the pass-1 tiers (doc_step_v)
+#else
+typedef s8v RecV;
+#endif
 __device__ __forceinline__ void swait(s8v&) {}
 
 // L2 prefetch: lane l touches record `from + 4 l` (one 128-B line per lane,
@@ -681,7 +701,17 @@ __device__ __forceinline__ void burst_run(DocRun& D, const ReplayArgs& a, uint32
   uint32_t st[kNumStats] = {};
   load_regs<E, K>(R, D, a);
   const uint32_t kend = D.k1 - D.k > limit ? D.k + limit : D.k1;
-  s8v cur = sload8(D.recp + 2 * D.k);
+  s8v cur;
+  RecV vcur;
+  if constexpr (E <= 4) {
+#if MTE_VREC
+    vcur = vload_rec8(D.recp + 2 * D.k);
+#else
+    vcur = sload8(D.recp + 2 * D.k);
+#endif
+  } else {
+    cur = sload8(D.recp + 2 * D.k);
+  }
   uint32_t pending = 0, sink = 0;
   // L2 prefetch of the records: short bursts (pass 1) touch the span after
   // this burst once, at its start (the first burst its own span too); long
@@ -692,7 +722,7 @@ __device__ __forceinline__ void burst_run(DocRun& D, const ReplayArgs& a, uint32
   for (;;) {
     if (!per_burst && (D.k & (kTouchSpan / 2 - 1)) == 0) touch_records(D, D.k + kTouchSpan / 2, pending, sink);
     int rc;
-    if constexpr (E <= 4) rc = doc_step_v<E, K, S>(R, D, st, cur, a, zlds, emin);
+    if constexpr (E <= 4) rc = doc_step_v<E, K, S>(R, D, st, vcur, a, zlds, emin);
     else rc = doc_step<E, K, S>(R, D, st, cur, a, zlds, emin);
     if (rc != 0) {
       if (rc < 0) {
@@ -704,7 +734,10 @@ __device__ __forceinline__ void burst_run(DocRun& D, const ReplayArgs& a, uint32
     if (D.k >= kend) break;
   }
   if (D.k >= D.k1) D.running = false;
-  swait(cur);  // no scalar load may be left in flight
+  if constexpr (E > 4) swait(cur);  // no scalar load may be left in flight
+#if !MTE_VREC
+  if constexpr (E <= 4) swait(vcur);
+#endif
   store_regs<E, K>(R, D, a);
   if constexpr (S) run_flush_stats(D, st, a);
   sink ^= pending;

@@ -60,13 +60,32 @@ __device__ __forceinline__ void perm_plane(T (&F)[E], int addr) {
   F[0] = perm1(F[0], addr);
 }
 
+template <typename T>
+__device__ __forceinline__ void shift1_dpp(T (&F)[1], bool g1, bool g2) {
+  const int32_t p1 = lane_prev((int32_t)F[0]);
+  const int32_t p2 = lane_prev(p1);
+  F[0] = g2 ? (T)p2 : (g1 ? (T)p1 : F[0]);
+}
+
 // new[i] = old[i - d(i)], d = g1 + g2 (g2 implies g1), for every plane and
 // the NX extra per-slot values X.  E == 1: one ds_bpermute per plane.  E > 1:
 // the two cross-lane moves of every plane first (DPP), then the selects.
 template <int E, int K, int NX>
 __device__ __forceinline__ void shift_v(Regs<E, K>& R, int32_t (&X)[NX > 0 ? NX : 1][E], const bool (&g1)[E],
                                         const bool (&g2)[E]) {
-  if constexpr (E == 1) {
+  if constexpr (E == 1 && MTE_E1_DPP) {
+    // new = d == 2 ? old[l-2] : d == 1 ? old[l-1] : old, two wave_shr:1 moves per plane
+    shift1_dpp(R.len, g1[0], g2[0]);
+    shift1_dpp(R.seq, g1[0], g2[0]);
+    shift1_dpp(R.rseq, g1[0], g2[0]);
+    shift1_dpp(R.rmask, g1[0], g2[0]);
+    shift1_dpp(R.meta, g1[0], g2[0]);
+    shift1_dpp(R.toff, g1[0], g2[0]);
+#pragma unroll
+    for (int k = 0; k < K; k++) shift1_dpp(R.pr[k], g1[0], g2[0]);
+#pragma unroll
+    for (int x = 0; x < NX; x++) shift1_dpp(X[x], g1[0], g2[0]);
+  } else if constexpr (E == 1) {
     const int addr = (lane_id() - (g1[0] ? 1 : 0) - (g2[0] ? 1 : 0)) << 2;
     perm_plane<E>(R.len, addr);
     perm_plane<E>(R.seq, addr);
@@ -339,7 +358,7 @@ __device__ __forceinline__ int seg_op_v(Regs<E, K>& R, int& n, const s8v& op, ui
 }
 
 template <int E, int K, bool S>
-__device__ __forceinline__ int doc_step_v(Regs<E, K>& R, DocRun& D, uint32_t (&st)[kNumStats], s8v& cur,
+__device__ __forceinline__ int doc_step_v(Regs<E, K>& R, DocRun& D, uint32_t (&st)[kNumStats], RecV& cur,
                                           const ReplayArgs& a, uint32_t* zlds, int emin) {
   const int l = lane_id();
   const int base = l * E;
@@ -350,11 +369,18 @@ __device__ __forceinline__ int doc_step_v(Regs<E, K>& R, DocRun& D, uint32_t (&s
   }
 
   // ---- op record (prefetched into `cur`; see doc_step) ----------------------
-  const s8v op = cur;
   const uint4* rec = D.recp + 2 * D.k;
+#if MTE_VREC
+  s8v op;
+#pragma unroll
+  for (int i = 0; i < 8; i++) op[i] = (int32_t)rdlane(cur, i);
+  cur = vload_rec8(rec + 2);  // the next record (zeroed pad after the last)
+#else
+  const s8v op = cur;
   uint64_t next = reinterpret_cast<uint64_t>(rec + 2);
   asm volatile("" : "+s"(next) : "s"(op));
   cur = sload8(reinterpret_cast<const uint4*>(next));
+#endif
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
