@@ -60,6 +60,8 @@ struct ChCtl {
   int32_t status;
   int32_t part[kChWaves];
   int32_t rr[MTE_MAX_CLIENTS];  // refSeq each summary column is valid for
+  int32_t pf_k;     // wave 0's current op (the prefetch wave runs ahead of it)
+  int32_t pf_stop;  // wave 0 left its op loop
 };
 
 // Data this kernel writes is read back with agent-scope loads (vector, L1
@@ -124,6 +126,20 @@ __device__ __forceinline__ void ch_store(const Regs<kChE, K>& R, const ChunkArgs
       for (int k = 0; k < K; k++) pl[(kFieldPlanes + k) * st + x] = R.pr[k][j];
     }
   }
+}
+
+// op records: 1 = 64 at a time through vector loads, 0 = scalar loads one ahead
+#ifndef MTE_CH_VREC
+#define MTE_CH_VREC 1
+#endif
+
+// 64 op records from record `base` on: lane l holds record base + l, one
+// dword per register
+__device__ __forceinline__ void ch_rec_batch(uint32_t (&b)[8], const uint4* recp, uint32_t base) {
+  const uint4* p = recp + 2 * (base + (uint32_t)lane_id());
+  const uint4 x = p[0], y = p[1];
+  b[0] = x.x, b[1] = x.y, b[2] = x.z, b[3] = x.w;
+  b[4] = y.x, b[5] = y.y, b[6] = y.z, b[7] = y.w;
 }
 
 // First chunk whose inclusive prefix (column c) is > x (strict) or >= x.
@@ -305,29 +321,125 @@ __device__ void ch_rebuild(const ChunkArgs& ch, int doc, uint32_t* Gc, int nch, 
   __syncthreads();
 }
 
+// ---- diagnostics: MTE_CH_PROF=1 phase clocks (tools/chunk_prof.py) ------------
+// Per document, in its stats slots at the end of the pass (s_memtime cycles):
+// 0 ops, 1 position lookups (ch_find), 2 chunk loads (issue -> data), 3 the
+// register step, 4 stores + summary updates, 5 the pass (max over docs),
+// 6 column rebuilds, 7 re-layouts.  A diagnostic build, never the product.
+#ifndef MTE_CH_PROF
+#define MTE_CH_PROF 0
+#endif
+#if MTE_CH_PROF
+#define CHPROF(...) __VA_ARGS__
+__device__ __forceinline__ uint64_t ch_clock() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  return __builtin_amdgcn_s_memtime();
+}
+#else
+#define CHPROF(...)
+#endif
+
+// ---- wave 1: chunk prefetch ---------------------------------------------------
+// While wave 0 applies op k, wave 1 resolves ops k+1 .. k+kPfAhead against the
+// summaries as they stand and touches their chunks, so wave 0's chunk loads
+// hit L2 instead of HBM.  A column only changes for its own client's ops, so
+// the guess is exact unless an op of the same client lies in between; a wrong
+// guess costs bandwidth only: this wave reads, never writes (the summaries
+// and G may be mid-update — every index it forms is range-checked).
+#ifndef MTE_CH_PREFETCH
+#define MTE_CH_PREFETCH 1
+#endif
+constexpr int kPfAhead = 4;
+
+template <int K>
+__device__ void ch_prefetch(const DocRun& D0, const ReplayArgs& a, const ChunkArgs& ch, const uint32_t* G,
+                            uint32_t ng_cap, ChCtl* ctl, int doc) {
+  const int nch = ctl->nch;
+  const uint32_t ng = (uint32_t)((nch + kChGroup - 1) / kChGroup);
+  const uint32_t* cnt = ch.cnt + (uint64_t)doc * ch.nch_cap;
+  const uint64_t kb = a.op_off[doc];
+  const uint4* recp = a.recs + 2 * kb;
+  const uint32_t k1 = (uint32_t)(a.op_off[doc + 1] - kb);
+  uint32_t done = 0;  // ops below this are prefetched
+  uint32_t sink = 0;
+  for (;;) {
+    if (*(volatile int32_t*)&ctl->pf_stop) break;
+    const uint32_t k = (uint32_t)uni(*(volatile int32_t*)&ctl->pf_k);
+    uint32_t j = done > k + 1 ? done : k + 1;
+    if (j >= k + 1 + kPfAhead || j >= k1) {
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    done = j + 1;
+    const uint32_t rw = lane_id() < 8 ? reinterpret_cast<const uint32_t*>(recp + 2 * j)[lane_id()] : 0u;
+    const uint32_t w3 = rdlane(rw, 3);
+    const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu;
+    if (type > MTE_OP_ANNOTATE || c >= MTE_MAX_CLIENTS) continue;
+    if (ctl->rr[c] != (int32_t)rdlane(rw, 1)) continue;  // column c not built for this refSeq
+    const int32_t pos1 = (int32_t)rdlane(rw, 4), pos2 = (int32_t)rdlane(rw, 5);
+    const int32_t x = type == MTE_OP_INSERT ? pos1 : (pos1 < pos2 ? pos1 : pos2);
+    const int32_t* sumc = ch.sum + ((uint64_t)doc * MTE_MAX_CLIENTS + c) * ch.nch_cap;
+    int32_t ex, total, cs;
+    int cn;
+    const int i = ch_find(G + c * ng_cap, ng, sumc, cnt, nch, x, type != MTE_OP_INSERT, &ex, &total, &cs, &cn);
+    if (i < 0 || i >= nch) continue;
+    const uint32_t* pl = ch.arena + ch_slot(ch, doc, i) + (uint32_t)lane_id() * kChE;
+#pragma unroll
+    for (int p = 0; p < kFieldPlanes + K; p++) sink ^= ld4(pl + p * ch.astride).x;
+  }
+  if (sink == 0x9e3779b9u && doc < 0) a.stats[0] = sink;  // keeps the touches alive
+  (void)D0;
+}
+
 // ---- wave 0: the op loop ------------------------------------------------------
 
 // Runs ops of the doc until the workgroup must act (re-layout, column
 // rebuild) or the batch ends.  Returns the request.
 template <int K, bool S>
 __device__ int ch_ops(DocRun& D, const ReplayArgs& a, const ChunkArgs& ch, uint32_t* G, uint32_t ng_cap, ChCtl* ctl,
-                      uint32_t (&st)[kNumStats]) {
+                      uint32_t (&st)[kNumStats], uint64_t* prof) {
   const int doc = D.doc;
   const int nch = ctl->nch;
   const uint32_t ng = (uint32_t)((nch + kChGroup - 1) / kChGroup);
   uint32_t* cnt = ch.cnt + (uint64_t)doc * ch.nch_cap;
   const bool newcalc = (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
+  // MTE_CH_VREC: op records 64 at a time through vector loads (lane l:
+  // record base + l), the next batch loading while this one is used, so the
+  // LDS scans never wait behind a scalar load in flight (SMEM and LDS share
+  // lgkmcnt).  Past the doc's last op the loads read the next doc's records
+  // or the zeroed tail (kRecPad).
+#if MTE_CH_VREC
+  uint32_t rbase = D.k & ~(uint32_t)(kWave - 1);
+  uint32_t rc0[8], rc1[8];
+  ch_rec_batch(rc0, D.recp, rbase);
+  ch_rec_batch(rc1, D.recp, rbase + kWave);
+#else
   s8v cur = sload8(D.recp + 2 * D.k);
+#endif
   while (D.k < D.k1) {
     if constexpr (S) {
       if (st[kStOps] >= 256) run_flush_stats(D, st, a);
     }
+#if MTE_CH_VREC
+    if (D.k - rbase >= (uint32_t)kWave) {  // the next batch; load the one after
+      rbase += kWave;
+#pragma unroll
+      for (int i = 0; i < 8; i++) rc0[i] = rc1[i];
+      ch_rec_batch(rc1, D.recp, rbase + kWave);
+    }
+    s8v op;
+#pragma unroll
+    for (int i = 0; i < 8; i++) op[i] = (int32_t)rdlane(rc0[i], (int)(D.k - rbase));
+#else
     // this op's record was prefetched; the next one is in flight meanwhile
     // (past the last op it reads the next doc's record or the zeroed tail)
     const s8v op = cur;
     uint64_t next = uni64(reinterpret_cast<uint64_t>(D.recp + 2 * (D.k + 1)));
     asm volatile("" : "+s"(next) : "s"(op));
     cur = sload8(reinterpret_cast<const uint4*>(next));
+#endif
+    CHPROF(uint64_t tq = ch_clock(); uint64_t tn;)
+    if (MTE_CH_PREFETCH && lane_id() == 0) *(volatile int32_t*)&ctl->pf_k = (int32_t)D.k;
     const uint32_t w3 = (uint32_t)op[3];
     const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
     const int32_t s = op[0], r = op[1], msn = op[2];
@@ -394,6 +506,7 @@ __device__ int ch_ops(DocRun& D, const ReplayArgs& a, const ChunkArgs& ch, uint3
         // only the two boundary chunks can grow (one split each)
         if (i1 >= i0 && (cn0 + 2 > kChSlots - 2 || cn1 + 2 > kChSlots - 2)) return kReqRelayout;
       }
+      CHPROF(tn = ch_clock(); prof[1] += tn - tq; tq = tn;)
       for (int i = i0; i <= i1; i++) {
         int ni = i == i0 ? cn0 : (int)ld_ag(cnt + i);
         // an insert touches one chunk and nothing is applied before this
@@ -403,11 +516,13 @@ __device__ int ch_ops(DocRun& D, const ReplayArgs& a, const ChunkArgs& ch, uint3
         const uint64_t x0 = ch_slot(ch, doc, i);
         Regs<kChE, K> R;
         ch_load<K>(R, ch, x0, ni);
+        CHPROF(tn = ch_clock(); prof[2] += tn - tq; tq = tn;)
         const int n0 = ni;
         scan += (uint32_t)ni;
         int32_t tot = 0, dlen = 0;
         const int rc = seg_op_v<kChE, K, S, true>(R, ni, op, type, c, flags, D.min_seq, newcalc, ex, i == nch - 1,
                                                   tot, dlen, a, st);
+        CHPROF(tn = ch_clock(); prof[3] += tn - tq; tq = tn;)
         if (rc == kNextChunk) {  // insert at the end of chunk i's perspective: the slot is further on
           ex = pos1;
           continue;
@@ -417,20 +532,24 @@ __device__ int ch_ops(DocRun& D, const ReplayArgs& a, const ChunkArgs& ch, uint3
           return kReqDone;
         }
         ch_store<K>(R, ch, x0, ni);
-        if (lane_id() == 0) {
-          cnt[i] = (uint32_t)ni;
-          if (dlen != 0) {
-            sumc[i] = ld_ag(sumc + i) + dlen;
+        if (dlen != 0) {
+          // chunk i0's sum came with ch_find: no second round trip for it
+          const int32_t prev = i == i0 ? cs0 : ld_ag(sumc + i);
+          if (lane_id() == 0) {
+            sumc[i] = prev + dlen;
             Gc[i / kChGroup] += (uint32_t)dlen;
           }
         }
+        if (lane_id() == 0) cnt[i] = (uint32_t)ni;
         D.n += ni - n0;
         ex += tot;
+        CHPROF(tn = ch_clock(); prof[4] += tn - tq; tq = tn;)
         if (type == MTE_OP_INSERT) break;
       }
       fence_wave();
     }
     // counted once the op is applied (a re-layout or rebuild retries it)
+    CHPROF(prof[0]++;)
     MTE_STAT(st[kStOps]++;)
     MTE_STAT(st[kStMaxSegs] = (uint32_t)n_before > st[kStMaxSegs] ? (uint32_t)n_before : st[kStMaxSegs];)
     MTE_STAT(if (type != MTE_OP_NOOP) {
@@ -471,6 +590,8 @@ __global__ __launch_bounds__(512) void chunk_kernel(ReplayArgs a, ChunkArgs ch) 
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
   DocRun D;
   uint32_t st[kNumStats] = {};
+  uint64_t prof[8] = {};
+  CHPROF(const uint64_t t_start = ch_clock(); uint64_t tph = 0;)
   if (w == 0) {
     run_init(D, a, doc, true);
     if (lane_id() == 0) {
@@ -484,6 +605,7 @@ __global__ __launch_bounds__(512) void chunk_kernel(ReplayArgs a, ChunkArgs ch) 
   bool chunked = false;  // the doc is in the chunk layout
   for (;;) {
     const int req = ctl->req;
+    CHPROF(tph = ch_clock();)
     if (req == kReqRelayout || req == kReqDone) {
       int n = ctl->n;
       if (chunked) n = ch_gather<K>(a, ch, doc, ctl, ctl->nch, ctl->min_seq);
@@ -496,6 +618,7 @@ __global__ __launch_bounds__(512) void chunk_kernel(ReplayArgs a, ChunkArgs ch) 
       if (threadIdx.x < MTE_MAX_CLIENTS) ctl->rr[threadIdx.x] = kColInvalid;
       if (threadIdx.x == 0) ctl->n = n;
       __syncthreads();
+      CHPROF(prof[7] += ch_clock() - tph;)
       if (req == kReqDone) break;
     } else if (req == kReqRebuild) {
       const int c = ctl->arg_c;
@@ -503,15 +626,24 @@ __global__ __launch_bounds__(512) void chunk_kernel(ReplayArgs a, ChunkArgs ch) 
                     (a.hdr[doc].flags & MTE_DOC_NEW_LENGTH_CALC) != 0);
       if (threadIdx.x == 0) ctl->rr[c] = ctl->arg_r;
       __syncthreads();
+      CHPROF(prof[6] += ch_clock() - tph;)
     }
+    if (MTE_CH_PREFETCH && threadIdx.x == 0) {
+      ctl->pf_stop = 0;
+      ctl->pf_k = D.k;
+    }
+    __syncthreads();
     if (w == 0) {
       D.n = ctl->n;
-      const int nreq = D.status == 0 ? ch_ops<K, S>(D, a, ch, G, ch.ng_cap, ctl, st) : (int)kReqDone;
+      const int nreq = D.status == 0 ? ch_ops<K, S>(D, a, ch, G, ch.ng_cap, ctl, st, prof) : (int)kReqDone;
       if (lane_id() == 0) {
         ctl->req = nreq;
         ctl->n = D.n;
         ctl->min_seq = D.min_seq;
+        if (MTE_CH_PREFETCH) *(volatile int32_t*)&ctl->pf_stop = 1;
       }
+    } else if (MTE_CH_PREFETCH && w == 1) {
+      ch_prefetch<K>(D, a, ch, G, ch.ng_cap, ctl, doc);
     }
     __syncthreads();
   }
@@ -520,6 +652,8 @@ __global__ __launch_bounds__(512) void chunk_kernel(ReplayArgs a, ChunkArgs ch) 
     D.running = false;
     if constexpr (S) run_flush_stats(D, st, a);
     run_finish(D, a);
+    CHPROF(prof[5] = ch_clock() - t_start;
+           if (lane_id() == 0) for (int t = 0; t < 8; t++) a.stats[(size_t)doc * kNumStats + t] = prof[t];)
   }
 }
 

@@ -2,7 +2,10 @@
  * mte.h — C-ABI of the MI355X batched sequence-merge engine (libmte.so).
  *
  * The engine replays *sequenced* merge-tree messages for many independent
- * documents at once, as an observer client would (every message is remote).
+ * documents at once, as an observer client would (every message is remote),
+ * and — for documents declared MTE_DOC_LOCAL_CLIENT — as a client that sends:
+ * its local ops (MTE_F_LOCAL) and the acks of their sequenced messages
+ * (MTE_OP_ACK) interleaved with the remote messages it receives.
  * It replaces, for that path, the following reference interfaces
  * (paths relative to /root/reference/packages/dds/merge-tree/src/):
  *
