@@ -122,7 +122,7 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
   h.min_seq = in.min_seq;
   h.cur_seq = in.cur_seq;
   h.status = 0;
-  h.flags = in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC | MTE_DOC_LOCAL_CLIENT);
+  h.flags = in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC | MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS);
   h.resume = 0;
   h.pad0 = h.pad1 = 0;
   if (legacy) {
@@ -407,6 +407,18 @@ struct mte_ctx {
   uint32_t n_tree = 0;
   std::vector<uint8_t> h_legacy;    // per doc
   std::vector<uint8_t> h_local;     // per doc: MTE_DOC_LOCAL_CLIENT
+  std::vector<uint8_t> h_events;    // per doc: MTE_DOC_EVENTS
+  // delta events per batch slot: region offsets (n_docs + 1, host and device),
+  // the events, their counts; ev_slot = the slot of the last mte_run
+  uint32_t ev_per_op = 8;
+  std::vector<uint64_t> h_dl_off_s[2];
+  uint64_t* d_dl_off_s[2] = {nullptr, nullptr};
+  uint64_t dl_off_cap_s[2] = {0, 0};
+  mte_delta* d_dl_s[2] = {nullptr, nullptr};
+  uint64_t dl_cap_s[2] = {0, 0};
+  uint32_t* d_dl_n_s[2] = {nullptr, nullptr};
+  uint64_t dl_n_cap_s[2] = {0, 0};
+  int ev_slot = -1;
   uint32_t* d_rs_docs = nullptr;    // legacy documents declared MTE_DOC_ROUND_SYNC (flat)
   int tree_rounds = 0;              // TIER 0 / TIER 1 rounds (MTE_TREE_ROUNDS; 0 = from the batch)
   // node level (mte_comm_*): the RCCL communicator and its staging buffers
@@ -729,7 +741,8 @@ int mte_destroy(mte_ctx* c) {
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int w = 0; w < 2; w++) {
-    void* sl[] = {c->d_ops_s[w], c->d_cps_s[w], c->d_off_s[w], c->d_ps_s[w], c->d_pe_s[w]};
+    void* sl[] = {c->d_ops_s[w], c->d_cps_s[w], c->d_off_s[w], c->d_ps_s[w], c->d_pe_s[w],
+                  c->d_dl_off_s[w], c->d_dl_s[w], c->d_dl_n_s[w]};
     for (void* p : sl)
       if (p) (void)hipFree(p);
     if (c->slot_ev[w]) (void)hipEventDestroy(c->slot_ev[w]);
@@ -762,9 +775,10 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     const mte_doc_init& in = docs[d];
     if ((uint64_t)in.text_off + in.text_len > text_units || in.text_len > 0x7fffffffu)
       return set_err(c, MTE_E_INVALID_ARG, "doc %u: initial text out of range", d);
-    if ((in.flags & MTE_DOC_LOCAL_CLIENT) && (!(in.flags & MTE_DOC_NEW_LENGTH_CALC) || c->cap >= kChunkMinCap))
-      return set_err(c, MTE_E_UNSUPPORTED, "doc %u: a local client needs the new length calculation and a "
-                     "context below %u segments", d, kChunkMinCap);
+    if ((in.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)) &&
+        (!(in.flags & MTE_DOC_NEW_LENGTH_CALC) || c->cap >= kChunkMinCap))
+      return set_err(c, MTE_E_UNSUPPORTED, "doc %u: a local client or delta events need the new length "
+                     "calculation and a context below %u segments", d, kChunkMinCap);
     if (in.propset != MTE_NO_PROPS) {
       if (in.propset >= n_propsets || !propsets) return set_err(c, MTE_E_INVALID_ARG, "doc %u: bad propset", d);
       const mte_propset ps = propsets[in.propset];
@@ -778,13 +792,17 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
   free_docs(c);
   c->n_docs = n_docs;
   c->submitted = false;
+  c->ev_slot = -1;
   c->n_ops = 0;
   const uint64_t nslots = (uint64_t)(n_docs ? n_docs : 1) * c->cap;
   c->soa.plane_stride = nslots;
   c->h_local.assign(n_docs, 0);
+  c->h_events.assign(n_docs, 0);
   bool any_local = false;
-  for (uint32_t d = 0; d < n_docs; d++)
+  for (uint32_t d = 0; d < n_docs; d++) {
     if (docs[d].flags & MTE_DOC_LOCAL_CLIENT) c->h_local[d] = 1, any_local = true;
+    if (docs[d].flags & MTE_DOC_EVENTS) c->h_events[d] = 1;
+  }
   // documents with a local client hold kt more planes: the pending property keys (mte_stream.h)
   const uint64_t prop_planes = (c->kt ? c->kt : 1) + (any_local ? c->kt : 0);
   HIPCHK(c, hipMalloc((void**)&c->hdr, sizeof(DocHdr) * (n_docs ? n_docs : 1)));
@@ -837,7 +855,7 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     std::vector<uint32_t> flat_docs, tree_docs, rs_docs;
     c->h_legacy.assign(n_docs, 0);
     for (uint32_t d = 0; d < n_docs; d++) {
-      if (docs[d].flags & MTE_DOC_LOCAL_CLIENT) {
+      if (docs[d].flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)) {
         continue;  // the HBM-streamed pass replays them (mte_stream.h)
       } else if (docs[d].flags & MTE_DOC_NEW_LENGTH_CALC) {
         flat_docs.push_back(d);
@@ -1030,6 +1048,27 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
     HIPCHK(c, hipMemcpyAsync(c->d_pe_s[w], b->props, b->n_props * sizeof(mte_prop), hipMemcpyHostToDevice,
                              c->up_stream));
   HIPCHK(c, hipStreamSynchronize(c->up_stream));  // host buffers may be freed after return
+  // delta event regions of the MTE_DOC_EVENTS docs (per_op x records + 256 each)
+  {
+    std::vector<uint64_t>& off = c->h_dl_off_s[w];
+    off.assign((size_t)b->n_docs + 1, 0);
+    bool any = false;
+    for (uint32_t d = 0; d < b->n_docs; d++) {
+      const bool e = d < c->h_events.size() && c->h_events[d];
+      any = any || e;
+      off[d + 1] = off[d] + (e ? (uint64_t)c->ev_per_op * (b->op_offsets[d + 1] - b->op_offsets[d]) + 256 : 0);
+    }
+    if (any) {
+      if ((rc = grow(c, &c->d_dl_off_s[w], &c->dl_off_cap_s[w], (uint64_t)b->n_docs + 1))) return rc;
+      if ((rc = grow(c, &c->d_dl_s[w], &c->dl_cap_s[w], off[b->n_docs] + 1))) return rc;
+      if ((rc = grow(c, &c->d_dl_n_s[w], &c->dl_n_cap_s[w], (uint64_t)b->n_docs + 1))) return rc;
+      HIPCHK(c, hipMemcpyAsync(c->d_dl_off_s[w], off.data(), off.size() * 8, hipMemcpyHostToDevice, c->up_stream));
+      HIPCHK(c, hipMemsetAsync(c->d_dl_n_s[w], 0, ((size_t)b->n_docs + 1) * 4, c->up_stream));
+      HIPCHK(c, hipStreamSynchronize(c->up_stream));
+    } else {
+      off.clear();
+    }
+  }
   c->n_ops_s[w] = b->n_ops;
   c->n_propsets_s[w] = b->n_propsets;
   uint64_t mx = 0;
@@ -1077,6 +1116,11 @@ int mte_run(mte_ctx* c) {
   a.wclock = nullptr;
   a.gdone = c->d_gdone;
   a.n_ops = c->n_ops;
+  const bool evs = !c->h_dl_off_s[c->rslot].empty();
+  a.dl = evs ? c->d_dl_s[c->rslot] : nullptr;
+  a.dl_off = evs ? c->d_dl_off_s[c->rslot] : nullptr;
+  a.dl_n = evs ? c->d_dl_n_s[c->rslot] : nullptr;
+  c->ev_slot = evs ? c->rslot : -1;
   // s_memrealtime runs at 100 MHz: ticks = ms x 1e5, scaled to this batch's ops
   a.eta = (c->last_ms > 0 && c->last_ops > 0) ? (unsigned long long)(c->last_ms * 1e5 * (double)c->n_ops / c->last_ops)
                                               : 0ull;
@@ -1227,6 +1271,31 @@ int mte_read_doc(mte_ctx* c, uint32_t doc, mte_doc_view* v) {
   v->length = length;
   v->n_text = nt;
   v->n_segs = ns;
+  return MTE_OK;
+}
+
+int mte_set_event_capacity(mte_ctx* c, uint32_t per_op) {
+  if (!c || per_op == 0 || per_op > (1u << 16)) return MTE_E_INVALID_ARG;
+  c->ev_per_op = per_op;
+  return MTE_OK;
+}
+
+int mte_read_deltas(mte_ctx* c, uint32_t doc, mte_delta* out, uint64_t cap, uint64_t* n) {
+  if (!c || !n || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  *n = 0;
+  if (c->h_events.empty() || !c->h_events[doc]) return set_err(c, MTE_E_INVALID_ARG, "doc %u: no MTE_DOC_EVENTS", doc);
+  if (c->ev_slot < 0) return MTE_OK;  // no batch with events ran yet
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const int sl = c->ev_slot;
+  uint32_t cnt = 0;
+  HIPCHK(c, hipMemcpy(&cnt, c->d_dl_n_s[sl] + doc, 4, hipMemcpyDeviceToHost));
+  const uint64_t b0 = c->h_dl_off_s[sl][doc], room = c->h_dl_off_s[sl][doc + 1] - b0;
+  *n = cnt;
+  if (cnt > room) return set_err(c, MTE_E_CAPACITY, "doc %u: %u delta events, room for %llu (mte_set_event_capacity)",
+                                 doc, cnt, (unsigned long long)room);
+  const uint64_t k = std::min<uint64_t>(cap, cnt);
+  if (out && k) HIPCHK(c, hipMemcpy(out, c->d_dl_s[sl] + b0, k * sizeof(mte_delta), hipMemcpyDeviceToHost));
   return MTE_OK;
 }
 

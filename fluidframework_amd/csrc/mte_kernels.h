@@ -95,6 +95,11 @@ struct ReplayArgs {
   unsigned long long* gdone;   // pass 1: ops applied so far by all waves (fair priority), zeroed per run
   unsigned long long n_ops;    // ops of the batch
   unsigned long long eta;      // expected pass-1 duration in s_memrealtime ticks (0 = unknown)
+  // MTE_DOC_EVENTS documents: delta events of doc d go to dl[dl_off[d] ..
+  // dl_off[d + 1]); dl_n[d] = how many the batch produced (more = overflow)
+  mte_delta* dl;
+  const uint64_t* dl_off;
+  uint32_t* dl_n;
 };
 
 // ---- wavefront primitives --------------------------------------------------

@@ -115,16 +115,45 @@ __device__ __forceinline__ void stream_ack(uint32_t* pl, uint64_t sd, int n, int
   vm_drain();
 }
 
+// ---- delta events (MTE_DOC_EVENTS, include/mte.h) ----------------------------
+// The doc's own view: removed -> 0, else the length (Client.getPosition,
+// client.ts:345-350, through nodeLength for the local client).
+struct EvOut {
+  mte_delta* p;   // the doc's region
+  uint64_t cap;   // its size
+  uint32_t n;     // events so far (may pass cap: overflow)
+  uint32_t op;    // the record being applied
+};
+__device__ __forceinline__ void ev_one(EvOut& ev, uint32_t kind, int32_t pos, int32_t len) {
+  if (lane_id() == 0 && ev.n < ev.cap) ev.p[ev.n] = mte_delta{ev.op, kind, pos, len, 0u};
+  ev.n++;
+}
+// the own view's length of slots [0, g)
+__device__ __forceinline__ int32_t own_prefix(const uint32_t* pl, uint64_t sd, int g) {
+  int32_t acc = 0;
+  for (int tb = 0; tb < g; tb += kTile) {
+#pragma unroll
+    for (int j = 0; j < kTileE; j++) {
+      const int i = tb + lane_id() * kTileE + j;
+      if (i < g) acc += (int32_t)ld_l2(pl + 2 * sd + i) == kNone ? (int32_t)ld_l2(pl + i) : 0;
+    }
+  }
+  return rdlane(wave_incl_scan(acc), kWave - 1);
+}
+
 // One op of one HBM-resident document (see the file comment).  Returns 0 or
-// a negative MTE_E_*.  lseq: the document's last localSeq (local-client docs).
+// a negative MTE_E_*.  lseq: the document's last localSeq (local-client docs);
+// ev: its delta events (MTE_DOC_EVENTS docs).
 template <int K, bool S>
 __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const ReplayArgs& a, uint32_t* zlds,
-                           int32_t& lseq) {
+                           int32_t& lseq, EvOut& ev) {
   constexpr int E = kTileE;
   const int l = lane_id();
   uint32_t* pl = a.planes + (uint64_t)D.doc * a.cap;
   const uint64_t sd = a.stride;
   const bool ldoc = (D.flags & MTE_DOC_LOCAL_CLIENT) != 0;
+  const bool evd = (D.flags & MTE_DOC_EVENTS) != 0;
+  ev.op = D.k;
   const int nplanes = kFieldPlanes + K + (ldoc ? K : 0);  // + the pending-key planes
 
   const s8v op = cur;
@@ -328,12 +357,16 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
       MTE_STAT(if (!marker) st[kStUnits] += (uint32_t)pos2;)
     }
     vm_drain();
+    if (evd && ins) {  // insertSegments' delta callback (mergeTree.ts:1409-1416)
+      if (g >= 0) ev_one(ev, MTE_OP_INSERT, own_prefix(pl, sd, g), nlen);
+      else if (nlen <= 0) ev_one(ev, MTE_OP_INSERT, -1, 0);  // a zero-length segment is never linked
+    }
     // ---- C: mark [start, end) on the new layout ---------------------------------
     if (rng && pos2 > pos1) {
       s8v q2 = {0, 0, 0, 0, 0, 0, 0, 0};
       if (type == MTE_OP_ANNOTATE) q2 = sload_props(a, (uint32_t)op[6]);
       const bool rem = type == MTE_OP_REMOVE;
-      int32_t cy = 0;
+      int32_t cy = 0, ocy = 0;  // ocy: the own view's prefix after the op (events)
       uint32_t cnt_all = 0;
       for (int tb = 0; tb < n && cy < pos2; tb += kTile) {
         Regs<E, K> R;
@@ -351,6 +384,35 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
           cnt += (uint32_t)__popcll(__ballot(in[j]));
         }
         cy += tot;
+        if (evd) {
+          // markRangeRemoved reports the segments it newly removes, annotateRange
+          // every one it visits (mergeTree.ts:1954-1959, 1893-1900), at their
+          // positions in the own view after the op, in document order
+          const bool rem0 = type == MTE_OP_REMOVE;
+          bool evf[E];
+          int32_t OL[E], OP[E];
+#pragma unroll
+          for (int j = 0; j < E; j++) {
+            evf[j] = in[j] && (!rem0 || lop || R.rseq[j] == kNone);
+            const bool gone = rem0 && in[j];
+            OL[j] = (R.rseq[j] == kNone && !gone) ? R.len[j] : 0;
+          }
+          const int32_t otot = prefix<E>(OL, OP);
+          uint32_t ecnt = 0;
+#pragma unroll
+          for (int j = 0; j < E; j++) ecnt += evf[j] ? 1u : 0u;
+          const int32_t eincl = wave_incl_scan((int32_t)ecnt);
+          uint32_t e = ev.n + (uint32_t)(eincl - (int32_t)ecnt);
+#pragma unroll
+          for (int j = 0; j < E; j++) {
+            if (evf[j]) {
+              if (e < ev.cap) ev.p[e] = mte_delta{ev.op, type, ocy + OP[j], R.len[j], OL[j] == 0 ? 1u : 0u};
+              e++;
+            }
+          }
+          ev.n += (uint32_t)rdlane(eincl, kWave - 1);
+          ocy += otot;
+        }
         if (cnt == 0) continue;
         cnt_all += cnt;
         const int base = tb + l * E;
@@ -483,15 +545,21 @@ __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
   if (doc >= (int)a.n_docs) return;
   // documents pass 2 escalated, and every document with a local client
   const uint32_t hf = a.hdr[doc].flags;
-  if (!(hf & (kHdrNeedsEsc | MTE_DOC_LOCAL_CLIENT))) return;  // untouched doc: leave the header alone
+  constexpr uint32_t kOwn = MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS;  // docs this pass always replays
+  if (!(hf & (kHdrNeedsEsc | kOwn))) return;  // untouched doc: leave the header alone
   DocRun D;
-  run_init(D, a, doc, !(hf & MTE_DOC_LOCAL_CLIENT));
+  run_init(D, a, doc, !(hf & kOwn));
   uint32_t st[kNumStats] = {};
   int32_t lseq = (int32_t)a.hdr[doc].pad0;  // local-client docs: the last localSeq
+  EvOut ev{nullptr, 0, 0u, 0u};
+  if ((hf & MTE_DOC_EVENTS) && a.dl_off) {
+    ev.p = a.dl + a.dl_off[doc];
+    ev.cap = a.dl_off[doc + 1] - a.dl_off[doc];
+  }
   if (D.running) {
     s8v cur = sload8(D.recp + 2 * D.k);
     while (D.running) {
-      const int rc = stream_step<K, S>(D, st, cur, a, zlds_all[w], lseq);
+      const int rc = stream_step<K, S>(D, st, cur, a, zlds_all[w], lseq, ev);
       if (rc < 0) {
         D.status = rc;
         D.running = false;
@@ -504,6 +572,7 @@ __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
     if constexpr (S) run_flush_stats(D, st, a);
   }
   if ((hf & MTE_DOC_LOCAL_CLIENT) && lane_id() == 0) a.hdr[doc].pad0 = (uint32_t)lseq;  // run_finish keeps it
+  if ((hf & MTE_DOC_EVENTS) && a.dl_n && lane_id() == 0) a.dl_n[doc] = ev.n;
   run_finish(D, a);
 }
 

@@ -10,7 +10,7 @@ import ctypes as C
 import numpy as np
 
 from . import _native
-from .abi import (DOC_INIT_DTYPE, EXPORTED_SYMBOLS, OP_DTYPE, PROP_DTYPE, PROPSET_DTYPE, SEG_DTYPE,
+from .abi import (DELTA_DTYPE, DOC_INIT_DTYPE, EXPORTED_SYMBOLS, OP_DTYPE, PROP_DTYPE, PROPSET_DTYPE, SEG_DTYPE,
                   MergeTreeError, MteBatch, MteConfig, MteDocView, MteSegList, MteStats, ptr)
 from .packing import units_to_str
 
@@ -66,6 +66,15 @@ class EngineBase:
                 for i in range(v.n_segs)]
         return {"status": v.status, "cur_seq": v.cur_seq, "min_seq": v.min_seq,
                 "length": v.length, "text": units_to_str(text[: v.n_text]), "segs": segs}
+
+    def read_deltas(self, doc):
+        """Delta events of the last batch of an MTE_DOC_EVENTS doc -> DELTA_DTYPE[n]
+        (op = record index in the doc's batch, kind, pos in the doc's own view, len)."""
+        n = C.c_uint64()
+        self._check(self._read_deltas(doc, None, 0, C.byref(n)), "read_deltas")
+        out = np.zeros(max(n.value, 1), DELTA_DTYPE)
+        self._check(self._read_deltas(doc, ptr(out), n.value, C.byref(n)), "read_deltas")
+        return out[: n.value]
 
     def read_segments(self, doc):
         """-> (segs SEG_DTYPE[n] with text_off into text, props uint32[n, n_keys], text uint16[])."""
@@ -197,6 +206,12 @@ class DeviceEngine(EngineBase):
 
     def _read_doc(self, doc, vptr):
         return self.lib.mte_read_doc(self.ctx, doc, vptr)
+
+    def _read_deltas(self, doc, p, cap, np_):
+        return self.lib.mte_read_deltas(self.ctx, doc, p, cap, np_)
+
+    def set_event_capacity(self, per_op):
+        self._check(self.lib.mte_set_event_capacity(self.ctx, per_op), "set_event_capacity")
 
     def _digest(self, p, n):
         return self.lib.mte_digest(self.ctx, p, n)

@@ -159,6 +159,15 @@ typedef struct mte_config {
  * and a context with seg_capacity < 8192; such documents replay on the
  * HBM-streamed pass.                                                         */
 #define MTE_DOC_LOCAL_CLIENT 0x4u
+/* Record the document's delta events: what MergeTree.mergeTreeDeltaCallback
+ * reports after each insert / remove / annotate (mergeTree.ts:1409-1416,
+ * 1893-1900, 1978-1985) and SharedString turns into "sequenceDelta" events
+ * (sequence.ts:203-211; SequenceEvent.ranges, sequenceDeltaEvent.ts): one
+ * mte_delta per affected segment, in document order, at its position in the
+ * document's own view right after the op (Client.getPosition, client.ts:345-350).
+ * Requires MTE_DOC_NEW_LENGTH_CALC and a context below 8192 segments; such
+ * documents replay on the HBM-streamed pass.  Read with mte_read_deltas.      */
+#define MTE_DOC_EVENTS 0x8u
 
 /* Initial document: one text segment inserted before collaboration starts, as
  * the reference replay harness does (client.replay.spec.ts:22-23): seq 0
@@ -275,6 +284,29 @@ int mte_digest(mte_ctx* ctx, uint64_t* out, uint32_t n_docs);
 int mte_digest_device(mte_ctx* ctx, void* device_out, uint32_t n_docs);
 
 int mte_read_doc(mte_ctx* ctx, uint32_t doc, mte_doc_view* view);
+
+/* One delta event range (ISequenceDeltaRange): the record (index in the doc's
+ * part of the last batch) whose op caused it, MergeTreeDeltaType (INSERT /
+ * REMOVE / ANNOTATE), the segment's position in the doc's own view right after
+ * the op (-1 for a zero-length insert, which links no segment) and its length
+ * (cachedLength).  A remove reports only segments it newly removed
+ * (removedSegments, mergeTree.ts:1954-1959); an annotate every segment it
+ * visited; no event when none (the deltaSegments.length > 0 checks).       */
+typedef struct mte_delta {
+  uint32_t op;
+  uint32_t kind;
+  int32_t pos;
+  int32_t len;
+  uint32_t removed; /* 1: the segment is removed in the doc's own view (an
+                       annotate of text another client removed since)      */
+} mte_delta;
+/* Events of the last mte_run for an MTE_DOC_EVENTS doc (query-size-then-fill:
+ * *n gets the count; up to cap are copied).  MTE_E_CAPACITY when the doc
+ * produced more than its event capacity (mte_set_event_capacity).            */
+int mte_read_deltas(mte_ctx* ctx, uint32_t doc, mte_delta* out, uint64_t cap, uint64_t* n);
+/* Event capacity of an MTE_DOC_EVENTS doc per batch: per_op x its records +
+ * 256 (default per_op 8); applies from the next mte_submit.                 */
+int mte_set_event_capacity(mte_ctx* ctx, uint32_t per_op);
 
 /* Every segment a document holds — removed ones above minSeq included — with
  * its merge info, in document order: the input of a summary writer

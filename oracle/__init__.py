@@ -54,6 +54,8 @@ def load():
         f = getattr(lib, name)
         f.argtypes = args
         f.restype = C.c_int
+    lib.orc_read_deltas.argtypes = [vp, u32, vp, u64, vp]
+    lib.orc_read_deltas.restype = C.c_int
     for pre in ("ort", "oti"):
         f = getattr(lib, f"{pre}_doc_shape")
         f.argtypes = [vp, u32, C.c_char_p, u32]
@@ -138,6 +140,9 @@ class OracleEngine(EngineBase):
 
     def _read_doc(self, doc, vptr):
         return self.f.read_doc(self.ctx, doc, vptr)
+
+    def _read_deltas(self, doc, p, cap, np_):
+        return self.lib.orc_read_deltas(self.ctx, doc, p, cap, np_)
 
     def _digest(self, p, n):
         return self.f.digest(self.ctx, p, n)

@@ -46,6 +46,10 @@ typedef struct {
    * segmentPropertiesManager.ts:20-60, see doc_apply_local); the last localSeq */
   uint32_t* pk;
   int32_t local_seq;
+  /* MTE_DOC_EVENTS: the last batch's delta events, and the record being applied */
+  mte_delta* dl;
+  uint64_t dl_n, dl_cap;
+  uint32_t cur_op;
   /* stats */
   uint64_t ops, scanned, written, pwrites, units, max_segs;
   /* scratch */
@@ -242,6 +246,31 @@ static void doc_compact(odoc* d) {
 }
 
 #define LOCAL_BASE MTE_LOCAL_SEQ_BASE
+
+/* ---- delta events (MTE_DOC_EVENTS, include/mte.h) --------------------------
+ * mergeTreeDeltaCallback after an insert / remove / annotate
+ * (mergeTree.ts:1409-1416, 1893-1900, 1978-1985) as SharedString's
+ * sequenceDelta listener reads it right away: per affected segment its
+ * position in the doc's own view (Client.getPosition, client.ts:345-350 ->
+ * nodeLength for the local client: removed 0, else the length) and its
+ * cachedLength. */
+static int delta_push(odoc* d, uint32_t kind, int64_t pos, int32_t len, uint32_t removed) {
+  if (d->dl_n == d->dl_cap) {
+    uint64_t nc = d->dl_cap ? 2 * d->dl_cap : 64;
+    mte_delta* x = (mte_delta*)realloc(d->dl, nc * sizeof(mte_delta));
+    if (!x) return MTE_E_OOM;
+    d->dl = x;
+    d->dl_cap = nc;
+  }
+  d->dl[d->dl_n++] = (mte_delta){d->cur_op, kind, (int32_t)pos, len, removed};
+  return MTE_OK;
+}
+static inline int32_t own_len(const oseg* g) { return g->rseq == NONE_SEQ ? g->len : 0; }
+static int64_t own_prefix(const odoc* d, uint32_t at) {
+  int64_t p = 0;
+  for (uint32_t i = 0; i < at; i++) p += own_len(&d->s[i]);
+  return p;
+}
 static inline int is_pending(int32_t seq) { return seq >= LOCAL_BASE && seq != NONE_SEQ; }
 
 /* annotateRange on one segment for a sequenced (remote) op in a document with
@@ -311,7 +340,7 @@ static int doc_apply_local(odoc* d, const mte_op* op, const apply_env* env) {
     if (tail == -2) return MTE_E_OOM;
     const int is_marker = (op->flags & MTE_F_MARKER) != 0;
     const int32_t len = is_marker ? 1 : op->pos2;
-    if (len <= 0) return MTE_OK;
+    if (len <= 0) return (d->flags & MTE_DOC_EVENTS) ? delta_push(d, MTE_OP_INSERT, -1, 0, 0) : MTE_OK;
     uint32_t at = d->n;
     if (tail >= 0) {
       at = (uint32_t)tail;
@@ -336,18 +365,23 @@ static int doc_apply_local(odoc* d, const mte_op* op, const apply_env* env) {
     if (op->b != MTE_NO_PROPS)
       d->pwrites += orc_apply_props(ns->props, env->n_keys, &env->b->propsets[op->b], env->b->props, 0);
     d->written += 1;
+    if (d->flags & MTE_DOC_EVENTS) return delta_push(d, MTE_OP_INSERT, own_prefix(d, at), len, 0);
     return MTE_OK;
   }
   if (op->type != MTE_OP_REMOVE && op->type != MTE_OP_ANNOTATE) return MTE_E_INVALID_ARG;
   const int64_t start = op->pos1, end = op->pos2;
   if (doc_split_at(d, start, &d->written) == -2) return MTE_E_OOM;
   if (doc_split_at(d, end, &d->written) == -2) return MTE_E_OOM;
-  for (uint32_t i = 0; i < d->n && end > start; i++) {
+  int64_t lp = 0;  /* the own view's prefix after the op, for the events */
+  for (uint32_t i = 0; i < d->n && end > start; lp += own_len(&d->s[i]), i++) {
     const int32_t l = d->L[i];
     if (l <= 0) continue;
     if (d->P[i] >= end) break;
     if (d->P[i] + l <= start) continue;
     oseg* g = &d->s[i];
+    if ((d->flags & MTE_DOC_EVENTS) &&
+        (rc = delta_push(d, op->type, lp, g->len, op->type == MTE_OP_REMOVE || g->rseq != NONE_SEQ)))
+      return rc;
     if (op->type == MTE_OP_REMOVE) {
       g->rseq = LOCAL_BASE + ls;
       g->rmask = 1u;
@@ -446,6 +480,9 @@ static int doc_apply(odoc* d, const mte_op* op, const apply_env* env) {
       if (op->b != MTE_NO_PROPS)
         d->pwrites += orc_apply_props(ns->props, env->n_keys, &env->b->propsets[op->b], env->b->props, 0);
       d->written += 1;
+      if ((d->flags & MTE_DOC_EVENTS) && (rc = delta_push(d, MTE_OP_INSERT, own_prefix(d, at), len, 0))) return rc;
+    } else if ((d->flags & MTE_DOC_EVENTS) && (rc = delta_push(d, MTE_OP_INSERT, -1, 0, 0))) {
+      return rc;  /* a zero-length segment is reported unlinked (getPosition -1) */
     }
     if ((rc = check_op_window(d, op))) return rc;
   } else if (op->type == MTE_OP_REMOVE || op->type == MTE_OP_ANNOTATE) {
@@ -458,12 +495,17 @@ static int doc_apply(odoc* d, const mte_op* op, const apply_env* env) {
     if (doc_split_at(d, start, &d->written) == -2) return MTE_E_OOM;
     if (doc_split_at(d, end, &d->written) == -2) return MTE_E_OOM;
     if (end != start) {
-      for (uint32_t i = 0; i < d->n; i++) {
+      int64_t lp = 0; /* the own view's prefix after the op, for the events */
+      const int ev = (d->flags & MTE_DOC_EVENTS) != 0;
+      for (uint32_t i = 0; i < d->n; lp += own_len(&d->s[i]), i++) {
         int32_t l = d->L[i];
         if (l <= 0) continue;
         if (d->P[i] >= end) break;
         if (d->P[i] + l <= start) continue;
         oseg* g = &d->s[i];
+        if (ev && (op->type == MTE_OP_ANNOTATE || g->rseq == NONE_SEQ) &&
+            (rc = delta_push(d, op->type, lp, g->len, op->type == MTE_OP_REMOVE || g->rseq != NONE_SEQ)))
+          return rc; /* a remove reports the segments it newly removes (removedSegments) */
         if (op->type == MTE_OP_REMOVE) {
           /* markRemoved closure (mergeTree.ts:1924-1962): keep the earlier
            * removedSeq and add the client to removedClientIds (1939-1942). */
@@ -525,6 +567,7 @@ static void free_docs(orc_ctx* c) {
     free(c->docs[i].L);
     free(c->docs[i].P);
     free(c->docs[i].pk);
+    free(c->docs[i].dl);
   }
   free(c->docs);
   c->docs = NULL;
@@ -577,7 +620,8 @@ int orc_load_docs(orc_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     if ((uint64_t)in->text_off + in->text_len > text_units) return MTE_E_INVALID_ARG;
     d->init = *in;
     d->flags = in->flags;
-    if ((in->flags & MTE_DOC_LOCAL_CLIENT) && !(in->flags & MTE_DOC_NEW_LENGTH_CALC)) return MTE_E_UNSUPPORTED;
+    if ((in->flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)) && !(in->flags & MTE_DOC_NEW_LENGTH_CALC))
+      return MTE_E_UNSUPPORTED;
     d->min_seq = in->min_seq;
     d->cur_seq = in->cur_seq;
     d->rs_ref = INT32_MIN;
@@ -681,7 +725,9 @@ static void* worker(void* p) {
       d->status = MTE_E_UNSUPPORTED;
       continue;
     }
+    d->dl_n = 0;
     for (uint64_t k = w->b->op_offsets[di]; k < w->b->op_offsets[di + 1]; k++) {
+      d->cur_op = (uint32_t)(k - w->b->op_offsets[di]);
       int rc = doc_apply(d, &w->b->ops[k], &env);
       if (rc) {
         d->status = rc;
@@ -853,5 +899,13 @@ int orc_stats_get(orc_ctx* c, mte_stats* o) {
 int orc_doc_nsegs(orc_ctx* c, uint32_t doc, uint32_t* out) {
   if (!c || !out || doc >= c->n_docs) return MTE_E_INVALID_ARG;
   *out = c->docs[doc].n;
+  return MTE_OK;
+}
+
+int orc_read_deltas(orc_ctx* c, uint32_t doc, mte_delta* out, uint64_t cap, uint64_t* n) {
+  if (!c || !n || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  const odoc* d = &c->docs[doc];
+  *n = d->dl_n;
+  if (out) memcpy(out, d->dl, (size_t)(cap < d->dl_n ? cap : d->dl_n) * sizeof(mte_delta));
   return MTE_OK;
 }

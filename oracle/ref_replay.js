@@ -54,6 +54,18 @@ function replayDoc(d) {
   client.startOrUpdateCollaboration("A");
   let error = null;
   let applied = 0;
+  // d.deltas: record every mergeTreeDeltaCallback (mergeTree.ts:1409-1416,
+  // 1893-1900, 1978-1985) as SharedString's sequenceDelta listener reads it
+  // (sequence.ts:203-211, 688-725; SequenceEvent.ranges, sequenceDeltaEvent.ts):
+  // [message index, operation, [[client.getPosition(segment), cachedLength, removed], ...]]
+  const deltas = [];
+  if (d.deltas) {
+    client.mergeTreeDeltaCallback = (opArgs, deltaArgs) => {
+      deltas.push([applied, deltaArgs.operation,
+        deltaArgs.deltaSegments.map((ds) => [client.getPosition(ds.segment), ds.segment.cachedLength,
+          ds.segment.removedSeq !== undefined ? 1 : 0])]);
+    };
+  }
   for (const m of d.msgs) {
     const msg = {
       clientId: m[0],
@@ -103,7 +115,7 @@ function replayDoc(d) {
       return true;
     });
   }
-  return { text, length, props, segs, error, applied, ms };
+  return { text, length, props, segs, error, applied, ms, deltas: d.deltas ? deltas : undefined };
 }
 
 const input = JSON.parse(fs.readFileSync(0, "utf8"));
