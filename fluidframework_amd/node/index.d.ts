@@ -58,6 +58,8 @@ export interface ClientOptions {
    *  observerId / longClientId name it, its sequenced messages are acks. */
   localClient?: boolean;
   longClientId?: string;
+  /** Record delta events (MTE_DOC_EVENTS; needs newLengthCalc): BatchClient.on("sequenceDelta"). */
+  events?: boolean;
   newLengthCalc?: boolean;
   props?: PropertySet;
   minSeq?: number;
@@ -168,6 +170,22 @@ export interface VisibleSegment {
   props?: PropertySet;
 }
 
+export interface SequenceDeltaRange {
+  position: number;   // Client.getPosition of the segment in this client's view after the op
+  length: number;     // cachedLength
+  removed: boolean;   // removed in this client's view
+  segment?: unknown;  // an insert's segment spec
+}
+export interface SequenceDeltaEvent {
+  deltaOperation: number;  // MergeTreeDeltaType
+  operation: "insert" | "remove" | "annotate";
+  isLocal: boolean;
+  message?: ISequencedDocumentMessage;
+  ranges: SequenceDeltaRange[];
+  first: SequenceDeltaRange;
+  last: SequenceDeltaRange;
+}
+
 export class BatchClient {
   readonly mergeTree: BatchMergeTree;
   readonly longClientId: string;
@@ -181,6 +199,10 @@ export class BatchClient {
   annotateRangeLocal(start: number, end: number, props: PropertySet, combiningOp?: { name: string }): IMergeTreeOp;
   makeOpMessage(op: IMergeTreeOp, seq?: number, refSeq?: number, minSeq?: number): ISequencedDocumentMessage;
   getPendingCount(): number;
+  /** SharedString "sequenceDelta" events ({events: true} documents), delivered at each flush in op order. */
+  on(name: "sequenceDelta", listener: (event: SequenceDeltaEvent, client: BatchClient) => void): this;
+  /** The catch-up stash of a legacy summary, ops rewritten to refSeq = seq - 1 (sequence.ts:688-725). */
+  getMessagesSinceMSNChange(): ISequencedDocumentMessage[];
   getOrAddShortClientId(longId: string): number;
   getClientId(): number;
   getLongClientId(shortId: number): string | undefined;

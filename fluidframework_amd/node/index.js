@@ -62,6 +62,30 @@ function segmentSpec(seg) {
   return seg;
 }
 
+/** SharedSegmentSequence.createOpsFromDelta (sequence.ts:116-161) for one
+ *  record's ranges: inserts as they landed, consecutive removes at one
+ *  position merged, annotates that continue the last merged (one op: the same
+ *  props, its keys with the values they now have). */
+function opsFromDelta(kind, ranges, op) {
+  const ops = [];
+  for (const r of ranges) {
+    if (kind === 0) {
+      ops.push({ pos1: r.position, seg: r.segment, type: 0 });
+    } else if (kind === 1) {
+      const last = ops[ops.length - 1];
+      if (last && last.pos1 === r.position) last.pos2 += r.length;
+      else ops.push({ pos1: r.position, pos2: r.position + r.length, type: 1 });
+    } else {
+      const props = {};
+      for (const key of Object.keys((op && op.props) || {})) props[key] = op.props[key] === undefined ? null : op.props[key];
+      const last = ops[ops.length - 1];
+      if (last && last.pos2 === r.position) last.pos2 += r.length;
+      else ops.push({ pos1: r.position, pos2: r.position + r.length, props, type: 2 });
+    }
+  }
+  return ops;
+}
+
 class MergeTreeEngine {
   /**
    * @param {{device?: number, nKeys?: number, segCapacity?: number}} [options]
@@ -93,11 +117,12 @@ class MergeTreeEngine {
     if (o.summary) o = Object.assign({}, o, { legacy: o.summary });
     if (o.legacy) o = Object.assign({}, o, loadLegacy(o.legacy));
     const doc = this.docs.length;
-    if (o.localClient && !o.newLengthCalc) {
-      throw new MergeTreeError(-9, "a local client needs the new length calculation (client.conflictFarm.spec.ts:84)");
+    if ((o.localClient || o.events) && !o.newLengthCalc) {
+      throw new MergeTreeError(-9, "a local client or delta events need the new length calculation");
     }
     this.docs.push({ text: initialText || "", newLengthCalc: !!o.newLengthCalc, roundSync: !!o.roundSync, props: o.props,
-      minSeq: o.minSeq || 0, currentSeq: o.currentSeq || 0, segments: o.segments, localClient: !!o.localClient });
+      minSeq: o.minSeq || 0, currentSeq: o.currentSeq || 0, segments: o.segments, localClient: !!o.localClient,
+      events: !!o.events });
     const c = new BatchClient(this, doc, o.observerId === undefined ? (o.longClientId || "A") : o.observerId,
       !!o.localClient);
     this.clients.push(c);
@@ -133,7 +158,8 @@ class MergeTreeEngine {
     this.addon.loadDocs(this.ctx, p.inits, p.text, p.propsets, p.props);
     if (body) this.addon.loadSegments(this.ctx, body.offsets, body.segs);
     this.started = true;
-    this.pending = new BatchBuilder(this.docs.length, this.interner);
+    this.track = this.docs.some((d) => d.events) ? this.docs.map((d) => !!d.events) : null;
+    this.pending = new BatchBuilder(this.docs.length, this.interner, this.track);
     this.views = new Array(this.docs.length).fill(null);
     this.docs.forEach((d, i) => { if (d.catchup) for (const m of d.catchup) this.clients[i].applyMsg(m); });
   }
@@ -151,7 +177,10 @@ class MergeTreeEngine {
     this.start();
     if (this.pending.count === 0) return;
     const b = this.pending.build();
-    this.pending = new BatchBuilder(this.docs.length, this.interner);
+    // a replay still running delivers its events before this batch takes the engine
+    this.sync();
+    this.inflightSrc = this.pending.recSrc;
+    this.pending = new BatchBuilder(this.docs.length, this.interner, this.track);
     this.views.fill(null);
     this.addon.submit(this.ctx, b.offsets, b.ops, b.text, b.propsets, b.props);
     this.addon.run(this.ctx);
@@ -163,6 +192,11 @@ class MergeTreeEngine {
     if (this.running) {
       this.running = false;
       this.addon.sync(this.ctx);
+      const src = this.inflightSrc;
+      this.inflightSrc = null;
+      if (src) {
+        src.forEach((recs, doc) => { if (recs && recs.length) this.clients[doc]._deliver(this.addon.readDeltas(this.ctx, doc), recs); });
+      }
     }
   }
 
@@ -358,6 +392,82 @@ class BatchClient {
       referenceSequenceNumber: refSeq === undefined ? this.getCurrentSeq() : refSeq,
       minimumSequenceNumber: minSeq === undefined ? 0 : minSeq, type: "op", contents: op,
     };
+  }
+
+  // ---- delta events (documents created with {events: true}) ----
+  // After each replay the document's mergeTreeDeltaCallback ranges come back
+  // from the engine (MTE_DOC_EVENTS) and are delivered in op order as
+  // SharedString's "sequenceDelta" events (sequence.ts:203-211,
+  // SequenceDeltaEvent / ISequenceDeltaRange, sequenceDeltaEvent.ts): one event
+  // per insert / remove / annotate that changed something, its ranges
+  // {position, length, removed, segment} in document order.  The segment is the
+  // inserted spec for an insert, else undefined: the engine keeps no segment
+  // objects.  They arrive at the flush, not synchronously with applyMsg.
+
+  /** on("sequenceDelta", listener(event, client)) */
+  on(name, listener) {
+    if (name !== "sequenceDelta") throw new MergeTreeError(-9, "only sequenceDelta events are delivered");
+    if (!this.engine.docs[this.doc].events) throw new MergeTreeError(-9, "createClient(..., {events: true}) first");
+    (this.listeners || (this.listeners = [])).push(listener);
+    return this;
+  }
+
+  /** Messages since the last minSeq change, catch-up ops rewritten as
+   *  SharedSegmentSequence.processMergeTreeMsg stashes them for a legacy
+   *  summary (sequence.ts:688-725, createOpsFromDelta :116-161): a message whose
+   *  refSeq is not seq - 1 becomes its effect as ops at refSeq = seq - 1. */
+  getMessagesSinceMSNChange() {
+    return (this.stash || []).slice();
+  }
+
+  _deliver(flat, recs) {
+    if (!this.stash) this.stash = [];
+    const kinds = ["insert", "remove", "annotate"];
+    let i = 0;
+    const n = flat.length / 5;
+    // one group of events per record, then one stash entry per message
+    let cur = null;  // {msg, ops: [...]} of the message being rewritten
+    const flushMsg = () => {
+      if (!cur) return;
+      const m = cur.msg;
+      if ((m.type === undefined ? "op" : m.type) !== "op") {  // only merge-tree ops reach processMergeTreeMsg
+        cur = null;
+        return;
+      }
+      if (m.referenceSequenceNumber !== m.sequenceNumber - 1) {
+        this.stash.push(Object.assign({}, m, { referenceSequenceNumber: m.sequenceNumber - 1,
+          contents: cur.ops.length !== 1 ? { type: 3, ops: cur.ops } : cur.ops[0] }));
+      } else {
+        this.stash.push(m);
+      }
+      // sequence.ts:719-723 / 727-738: drop what the window has passed
+      const msn = m.minimumSequenceNumber;
+      if (this.stash.length > 20 && this.stash[20].sequenceNumber < msn) {
+        this.stash = this.stash.filter((x) => x.sequenceNumber > msn);
+      }
+      cur = null;
+    };
+    for (let k = 0; k < recs.length; k++) {
+      const src = recs[k];
+      if (!src.local && (!cur || cur.msg !== src.msg)) {
+        flushMsg();
+        cur = { msg: src.msg, ops: [] };
+      }
+      const ranges = [];
+      let kind = -1;
+      while (i < n && flat[5 * i] === k) {
+        kind = flat[5 * i + 1];
+        ranges.push({ position: flat[5 * i + 2] | 0, length: flat[5 * i + 3], removed: flat[5 * i + 4] === 1,
+          segment: kind === 0 && src.op ? src.op.seg : undefined });
+        i++;
+      }
+      if (kind < 0) continue;
+      if (cur) cur.ops.push(...opsFromDelta(kind, ranges, src.op));
+      const ev = { deltaOperation: kind, operation: kinds[kind], isLocal: src.local,
+        message: src.local ? undefined : src.msg, ranges, first: ranges[0], last: ranges[ranges.length - 1] };
+      for (const fn of this.listeners || []) fn(ev, this);
+    }
+    flushMsg();
   }
 
   /** Local ops sent but not acknowledged yet. */

@@ -527,6 +527,46 @@ static napi_value js_comm_destroy(napi_env env, napi_callback_info info) {
   return NULL;
 }
 
+/* readDeltas(ctx, doc) -> Int32Array(5 n): op, kind, pos, len, removed per
+   event (mte_read_deltas) */
+static napi_value js_read_deltas(napi_env env, napi_callback_info info) {
+  napi_value argv[2];
+  if (!get_args(env, info, 2, argv)) return NULL;
+  mte_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  uint32_t doc = 0;
+  if (napi_get_value_uint32(env, argv[1], &doc) != napi_ok) {
+    napi_throw_type_error(env, NULL, "doc must be a number");
+    return NULL;
+  }
+  uint64_t n = 0;
+  if (throw_rc(env, mte_read_deltas(ctx, doc, NULL, 0, &n), ctx, "mte_read_deltas")) return NULL;
+  mte_delta* buf = (mte_delta*)malloc((size_t)(n ? n : 1) * sizeof(mte_delta));
+  if (!buf) {
+    napi_throw_error(env, NULL, "out of memory");
+    return NULL;
+  }
+  if (throw_rc(env, mte_read_deltas(ctx, doc, buf, n, &n), ctx, "mte_read_deltas")) {
+    free(buf);
+    return NULL;
+  }
+  napi_value out = u32_array(env, (const uint32_t*)buf, (size_t)n * 5);
+  free(buf);
+  return out;
+}
+
+/* setEventCapacity(ctx, perOp) (mte_set_event_capacity) */
+static napi_value js_set_event_capacity(napi_env env, napi_callback_info info) {
+  napi_value argv[2];
+  if (!get_args(env, info, 2, argv)) return NULL;
+  mte_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  uint32_t per = 0;
+  napi_get_value_uint32(env, argv[1], &per);
+  throw_rc(env, mte_set_event_capacity(ctx, per), ctx, "mte_set_event_capacity");
+  return NULL;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
   const napi_property_descriptor d[] = {
       {"abiVersion", NULL, js_abi_version, NULL, NULL, NULL, napi_enumerable, NULL},
@@ -552,6 +592,8 @@ static napi_value init(napi_env env, napi_value exports) {
       {"commAllreduce", NULL, js_comm_allreduce, NULL, NULL, NULL, napi_enumerable, NULL},
       {"commGatherDigests", NULL, js_comm_gather_digests, NULL, NULL, NULL, napi_enumerable, NULL},
       {"commDestroy", NULL, js_comm_destroy, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"readDeltas", NULL, js_read_deltas, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"setEventCapacity", NULL, js_set_event_capacity, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   if (napi_define_properties(env, exports, sizeof d / sizeof d[0], d) != napi_ok) return NULL;
   return exports;

@@ -42,6 +42,7 @@ const INSERT = 0, REMOVE = 1, ANNOTATE = 2, GROUP = 3;
 
 const DOC_ROUND_SYNC = 0x2; // MTE_DOC_ROUND_SYNC (include/mte.h)
 const DOC_LOCAL_CLIENT = 0x4; // MTE_DOC_LOCAL_CLIENT
+const DOC_EVENTS = 0x8; // MTE_DOC_EVENTS
 const E_INVALID_ARG = -1, E_UNSUPPORTED = -9, E_STATE = -10, E_CLIENT_RANGE = -12;
 
 class MergeTreeError extends Error {
@@ -191,9 +192,13 @@ function utf16(s) {
 
 /** Collects messages for nDocs documents and emits one mte_batch. */
 class BatchBuilder {
-  constructor(nDocs, interner) {
+  constructor(nDocs, interner, trackDocs) {
     this.nDocs = nDocs;
     this.interner = interner;
+    // documents whose delta events are read back (MTE_DOC_EVENTS): per record,
+    // {msg, op, local} — the message (or local op) and the (GROUP member) op
+    this.track = trackDocs || null;
+    this.recSrc = trackDocs ? trackDocs.map((t) => (t ? [] : null)) : null;
     this.props = new PropTable(interner);
     this.docOps = [];
     for (let d = 0; d < nDocs; d++) this.docOps.push([]);
@@ -222,6 +227,7 @@ class BatchBuilder {
       throw new MergeTreeError(E_INVALID_ARG, "referenceSequenceNumber " + ref + " < minSeq " + clients.minSeq);
     }
     const recs = [];
+    this._srcOps = null;
     if ((msg.type === undefined ? "op" : msg.type) === "op") {
       if (sender === clients.observer) {
         // our own op, sequenced: ackPendingSegment (client.ts:925-928)
@@ -230,12 +236,18 @@ class BatchBuilder {
         const [lo, hi] = clients.pending.shift();
         recs.push([OP_ACK, 0, lo, hi, 0, NO_PROPS]);
       } else {
-        this._opRecords(msg.contents, recs);
+        this._opRecords(msg.contents, recs, this._src(doc));
       }
     }
     // the slot is taken only once the message has validated
     const short = slotOf(clients, sender, seq);
     if (recs.length === 0) recs.push([OP_NOOP, 0, 0, 0, 0, NO_PROPS]);
+    const src = this._src(doc);
+    if (src) {  // one entry per record of this message
+      const ops = this._srcOps || [];
+      for (let i = 0; i < recs.length; i++) src.push({ msg, op: ops[i], local: false });
+      this._srcOps = null;
+    }
     recs[recs.length - 1][1] |= F_MSG_END;
     for (const r of recs) this.docOps[doc].push([seq, ref, msn, r[0], short, r[1], r[2], r[3], r[4], r[5]]);
     this.count += recs.length;
@@ -249,9 +261,16 @@ class BatchBuilder {
   addLocal(doc, clients, op) {
     if (!clients.local) throw new MergeTreeError(E_UNSUPPORTED, "local op in an observer document");
     const recs = [];
-    this._opRecords(op, recs);
+    this._srcOps = null;
+    this._opRecords(op, recs, this._src(doc));
     if (recs.length === 0) recs.push([OP_NOOP, 0, 0, 0, 0, NO_PROPS]);
     if (recs.some((r) => r[1] & F_REWRITE)) throw new MergeTreeError(E_UNSUPPORTED, "local combiningOp rewrite");
+    const src = this._src(doc);
+    if (src) {
+      const ops = this._srcOps || [];
+      for (let i = 0; i < recs.length; i++) src.push({ msg: null, op: ops[i], local: true });
+      this._srcOps = null;
+    }
     const first = clients.localSeq + 1;
     if (first + recs.length >= LOCAL_SEQ_BASE) throw new MergeTreeError(E_INVALID_ARG, "localSeq overflow");
     recs.forEach((r, i) => {
@@ -275,11 +294,19 @@ class BatchBuilder {
     this.count += recs.length;
   }
 
-  _opRecords(op, recs) {
+  _src(doc) {
+    return this.recSrc ? this.recSrc[doc] : null;
+  }
+
+  _opRecords(op, recs, track) {
+    if (track && op && typeof op === "object" && op.type !== GROUP) {
+      if (!this._srcOps) this._srcOps = [];
+      this._srcOps.push(op);  // the op behind the record pushed below
+    }
     if (op === null || typeof op !== "object") throw new MergeTreeError(E_INVALID_ARG, "op contents must be an object");
     const t = op.type;
     if (t === GROUP) {
-      for (const member of op.ops || []) this._opRecords(member, recs);
+      for (const member of op.ops || []) this._opRecords(member, recs, track);
       return;
     }
     if (!("pos1" in op) && op.relativePos1 !== undefined && op.relativePos1 !== null) {
@@ -371,7 +398,7 @@ function packDocInits(docs, interner) {
     buf.writeUInt32LE(off, o);
     buf.writeUInt32LE(d.text.length, o + 4);
     buf.writeUInt32LE((d.newLengthCalc ? DOC_NEW_LENGTH_CALC : 0) | (d.roundSync ? DOC_ROUND_SYNC : 0) |
-      (d.localClient ? DOC_LOCAL_CLIENT : 0), o + 8);
+      (d.localClient ? DOC_LOCAL_CLIENT : 0) | (d.events ? DOC_EVENTS : 0), o + 8);
     buf.writeUInt32LE(props.add(d.props) >>> 0, o + 12);
     buf.writeInt32LE(d.minSeq || 0, o + 16);
     buf.writeInt32LE(d.currentSeq || 0, o + 20);

@@ -25,7 +25,7 @@ pytestmark = pytest.mark.skipif(NODE is None, reason="node not installed")
 
 EXPORTS = ["abiVersion", "strerror", "create", "destroy", "lastError", "loadDocs", "loadSegments", "readSegments", "submit", "run",
            "sync", "reset", "digest", "docStatus", "readDoc", "stats", "commUniqueId", "commInit", "commShare",
-           "commBarrier", "commAllreduce", "commGatherDigests", "commDestroy"]
+           "commBarrier", "commAllreduce", "commGatherDigests", "commDestroy", "readDeltas", "setEventCapacity"]
 
 
 def node(*args, timeout=300):
@@ -300,3 +300,44 @@ def test_node_farm_every_client_local_on_gpu(mode):
         with gzip.open(os.path.join(ROOT, "tests", "golden", "farm_vectors.json.gz"), "rt") as fh:
             sets = json.load(fh)["sets"]
         assert j["passed"] == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i", range(3))
+def test_node_sequence_delta_events_on_gpu(i):
+    """BatchClient {events: true}: the sequenceDelta events of a flush equal the
+    reference's delta callbacks (tests/golden/delta_vectors.json.gz, compared as
+    in tests/test_deltas.py); on the set without annotates (config 2) the
+    rewritten catch-up stash equals createOpsFromDelta over the reference's own
+    events (sequence.ts:116-161, 688-725)."""
+    import test_deltas as T
+    from fluidframework_amd import gen
+    from fluidframework_amd.messages import stream_docs
+    S = T.golden()[i]
+    st = gen.generate(S["config"], n_docs=12, ops_per_doc=S["ops_per_doc"], **S["params"])
+    docs = stream_docs(st, 0, 12)
+    r = subprocess.run([NODE, "tests/node/deltas_gpu.js"], cwd=ROOT, input=json.dumps({"docs": docs}),
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = json.loads(r.stdout.strip().splitlines()[-1])["docs"]
+    for d in range(12):
+        assert T.compare(got[d]["events"], S["docs"][d]["events"]) is None, (d,)
+        if S["config"] == 2:
+            want = []
+            for mi, (cid, seq, ref, msn, typ, contents) in enumerate(docs[d]["msgs"]):
+                if typ != "op":
+                    continue
+                if ref == seq - 1:
+                    want.append((seq, ref, contents))
+                    continue
+                ops = []
+                for _, kind, pos, ln, _rm in (e for e in S["docs"][d]["events"] if e[0] == mi):
+                    if kind == 0:
+                        ops.append({"pos1": pos, "seg": contents["seg"], "type": 0})
+                    elif ops and ops[-1]["type"] == 1 and ops[-1]["pos1"] == pos:
+                        ops[-1]["pos2"] += ln
+                    else:
+                        ops.append({"pos1": pos, "pos2": pos + ln, "type": 1})
+                want.append((seq, seq - 1, ops[0] if len(ops) == 1 else {"type": 3, "ops": ops}))
+            have = [(m["sequenceNumber"], m["referenceSequenceNumber"], m["contents"]) for m in got[d]["stash"]]
+            assert have and have == want[len(want) - len(have):], (d, have[:2], want[len(want) - len(have):][:2])
