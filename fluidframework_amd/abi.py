@@ -40,7 +40,7 @@ ERROR_NAMES = {
     MTE_E_CLIENT_RANGE: "too many clients in one document",
 }
 
-OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_ACK = 0, 1, 2, 3, 4
+OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_ACK, OP_ROLLBACK = 0, 1, 2, 3, 4, 5
 F_MARKER, F_MSG_END, F_REWRITE, F_LOCAL = 0x1, 0x2, 0x4, 0x8
 LOCAL_SEQ_BASE = 0x40000000
 NO_PROPS = 0xFFFFFFFF

@@ -573,7 +573,8 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
 // Validation of one op record (the kernels index with these fields, so a bad
 // record must never reach them).  Returns nullptr or the reason.
 const char* bad_op(const mte_op& o, const mte_batch* b, bool local_doc) {
-  if (o.type > MTE_OP_ACK) return "type";
+  if (o.type > MTE_OP_ROLLBACK) return "type";
+  if (o.type == MTE_OP_ROLLBACK && !(o.flags & MTE_F_LOCAL)) return "rollback without MTE_F_LOCAL";
   if ((o.flags & MTE_F_LOCAL) || o.type == MTE_OP_ACK) {
     if (!local_doc) return "local op or ack in a document without MTE_DOC_LOCAL_CLIENT";
     if ((o.flags & MTE_F_LOCAL) && (o.type == MTE_OP_ACK || o.seq <= 0 || o.seq >= MTE_LOCAL_SEQ_BASE))

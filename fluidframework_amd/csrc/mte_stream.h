@@ -141,6 +141,63 @@ __device__ __forceinline__ int32_t own_prefix(const uint32_t* pl, uint64_t sd, i
   return rdlane(wave_incl_scan(acc), kWave - 1);
 }
 
+// MTE_OP_ROLLBACK: MergeTree.rollback of the pending op of localSeq ls, type t
+// (mergeTree.ts:2005-2083): its inserted segments get seq and removedSeq
+// UniversalSequenceNumber 0 (gone for every view), its removed ones are
+// restored; each one's delta event at its own-view position once done.
+__device__ __forceinline__ void stream_rollback(uint32_t* pl, uint64_t sd, int n, int32_t ls, uint32_t t, bool evd,
+                                                EvOut& ev) {
+  const int l = lane_id();
+  int32_t ocy = 0;
+  for (int tb = 0; tb < n; tb += kTile) {
+    bool hit[kTileE];
+    int32_t OL[kTileE], OP[kTileE], len[kTileE];
+#pragma unroll
+    for (int j = 0; j < kTileE; j++) {
+      const int i = tb + l * kTileE + j;
+      const bool v = i < n;
+      len[j] = v ? (int32_t)ld_l2(pl + i) : 0;
+      const int32_t sq = v ? (int32_t)ld_l2(pl + sd + i) : 0;
+      int32_t rs = v ? (int32_t)ld_l2(pl + 2 * sd + i) : kPad;
+      hit[j] = v && (t == MTE_OP_INSERT ? sq == kLocalBase + ls : rs == kLocalBase + ls);
+      if (hit[j]) {
+        if (t == MTE_OP_INSERT) {
+          pl[sd + i] = 0u;
+          pl[2 * sd + i] = 0u;
+          pl[3 * sd + i] = 1u;  // removed by the local client
+          rs = 0;
+        } else {
+          pl[2 * sd + i] = (uint32_t)kNone;
+          pl[3 * sd + i] = 0u;
+          rs = kNone;
+        }
+      }
+      OL[j] = (v && rs == kNone) ? len[j] : 0;
+    }
+    if (evd) {
+      const int32_t otot = prefix<kTileE>(OL, OP);
+      uint32_t ecnt = 0;
+#pragma unroll
+      for (int j = 0; j < kTileE; j++) ecnt += hit[j] ? 1u : 0u;
+      const int32_t eincl = wave_incl_scan((int32_t)ecnt);
+      uint32_t e = ev.n + (uint32_t)(eincl - (int32_t)ecnt);
+#pragma unroll
+      for (int j = 0; j < kTileE; j++) {
+        if (hit[j]) {
+          // a rolled-back insert is removed (REMOVE event), a rolled-back remove re-inserted
+          if (e < ev.cap)
+            ev.p[e] = mte_delta{ev.op, t == MTE_OP_INSERT ? (uint32_t)MTE_OP_REMOVE : (uint32_t)MTE_OP_INSERT,
+                                ocy + OP[j], len[j], t == MTE_OP_INSERT ? 1u : 0u};
+          e++;
+        }
+      }
+      ev.n += (uint32_t)rdlane(eincl, kWave - 1);
+      ocy += otot;
+    }
+  }
+  vm_drain();
+}
+
 // One op of one HBM-resident document (see the file comment).  Returns 0 or
 // a negative MTE_E_*.  lseq: the document's last localSeq (local-client docs);
 // ev: its delta events (MTE_DOC_EVENTS docs).
@@ -162,13 +219,21 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
-  if (type > MTE_OP_ACK) return MTE_E_INVALID_ARG;
+  if (type > MTE_OP_ROLLBACK) return MTE_E_INVALID_ARG;
   const bool lop = (flags & MTE_F_LOCAL) != 0;  // a local op: the local view, seq = localSeq
-  if ((lop || type == MTE_OP_ACK) && !ldoc) return MTE_E_UNSUPPORTED;
+  if ((lop || type >= MTE_OP_ACK) && !ldoc) return MTE_E_UNSUPPORTED;
   MTE_STAT(st[kStOps]++;)
   MTE_STAT(st[kStMaxSegs] = (uint32_t)D.n > st[kStMaxSegs] ? (uint32_t)D.n : st[kStMaxSegs];)
   const int32_t s = op[0], r = op[1], msn = op[2];
   const int32_t pos1 = op[4], pos2 = op[5];
+  if (type == MTE_OP_ROLLBACK) {
+    if (!lop || !(s > 0 && s <= lseq)) return MTE_E_INVALID_ARG;
+    if (pos1 != MTE_OP_INSERT && pos1 != MTE_OP_REMOVE) return MTE_E_UNSUPPORTED;
+    MTE_STAT(st[kStScanned] += (uint32_t)D.n;)
+    stream_rollback(pl, sd, D.n, s, (uint32_t)pos1, evd, ev);
+    D.k++;
+    return 0;
+  }
   if (lop) {
     if (!(s > lseq && s < kLocalBase) || c != 0) return MTE_E_INVALID_ARG;
     if (type == MTE_OP_ANNOTATE && (flags & MTE_F_REWRITE)) return MTE_E_UNSUPPORTED;

@@ -199,6 +199,8 @@ export class BatchClient {
   annotateRangeLocal(start: number, end: number, props: PropertySet, combiningOp?: { name: string }): IMergeTreeOp;
   makeOpMessage(op: IMergeTreeOp, seq?: number, refSeq?: number, minSeq?: number): ISequencedDocumentMessage;
   getPendingCount(): number;
+  /** Client.rollback of the latest pending local op (inserts and removes). */
+  rollback(op?: IMergeTreeOp): void;
   /** SharedString "sequenceDelta" events ({events: true} documents), delivered at each flush in op order. */
   on(name: "sequenceDelta", listener: (event: SequenceDeltaEvent, client: BatchClient) => void): this;
   /** The catch-up stash of a legacy summary, ops rewritten to refSeq = seq - 1 (sequence.ts:688-725). */

@@ -470,6 +470,14 @@ class BatchClient {
     flushMsg();
   }
 
+  /** Client.rollback (client.ts:396-398 -> MergeTree.rollback,
+   *  mergeTree.ts:2005-2083) of this client's latest pending op, which must not
+   *  have been sent: its inserts disappear, its removes are undone.  Rolling
+   *  back an annotate is not supported. */
+  rollback(op) {  // eslint-disable-line no-unused-vars
+    this.engine._batch().addRollback(this.doc, this.clients);
+  }
+
   /** Local ops sent but not acknowledged yet. */
   getPendingCount() {
     return this.clients.pending.length;

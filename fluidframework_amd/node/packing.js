@@ -28,7 +28,7 @@
  * for record (tests/test_node_host.py checks the bytes are identical).
  */
 
-const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 3, OP_ACK = 4;
+const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 3, OP_ACK = 4, OP_ROLLBACK = 5;
 const F_MARKER = 0x1, F_MSG_END = 0x2, F_REWRITE = 0x4, F_LOCAL = 0x8;
 const LOCAL_SEQ_BASE = 0x40000000; // MTE_LOCAL_SEQ_BASE
 const NO_PROPS = 0xffffffff;
@@ -131,6 +131,7 @@ class DocClients {
     this.local = !!local;
     this.localSeq = 0;
     this.pending = [];
+    this.pendingTypes = [];  // the record types of each pending message (rollback)
   }
   short(longId, seq) {
     let i = this.ids.get(longId);
@@ -234,6 +235,7 @@ class BatchBuilder {
         if (!clients.local) throw new MergeTreeError(E_UNSUPPORTED, "ack of a local op in an observer document");
         if (clients.pending.length === 0) throw new MergeTreeError(E_STATE, "ack without a pending local op");
         const [lo, hi] = clients.pending.shift();
+        clients.pendingTypes.shift();
         recs.push([OP_ACK, 0, lo, hi, 0, NO_PROPS]);
       } else {
         this._opRecords(msg.contents, recs, this._src(doc));
@@ -279,6 +281,27 @@ class BatchBuilder {
     this.count += recs.length;
     clients.localSeq += recs.length;
     clients.pending.push([first, clients.localSeq]);
+    clients.pendingTypes.push(recs.map((r) => r[0]));
+  }
+
+  /** Client.rollback of the latest pending local op (client.ts:396-398 ->
+   *  MergeTree.rollback, mergeTree.ts:2005-2083), as packing.py add_rollback. */
+  addRollback(doc, clients) {
+    if (!clients.local || clients.pending.length === 0) {
+      throw new MergeTreeError(E_STATE, "rollback without a pending local op");
+    }
+    const types = clients.pendingTypes[clients.pendingTypes.length - 1];
+    if (types.includes(OP_ANNOTATE)) throw new MergeTreeError(E_UNSUPPORTED, "rollback of an annotate");
+    const [lo, hi] = clients.pending.pop();
+    clients.pendingTypes.pop();
+    for (let ls = hi; ls >= lo; ls--) {
+      const t = types[ls - lo];
+      if (t === OP_NOOP) continue;
+      this.docOps[doc].push([ls, 0, 0, OP_ROLLBACK, 0, F_LOCAL, t, 0, 0, NO_PROPS]);
+      this.count++;
+      const src = this._src(doc);
+      if (src) src.push({ msg: null, op: undefined, local: true });
+    }
   }
 
   /** One MergeTree-level call (insertSegments / markRangeRemoved / annotateRange):

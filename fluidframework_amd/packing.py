@@ -31,7 +31,7 @@ import json
 import numpy as np
 
 from .abi import (F_LOCAL, F_MARKER, F_MSG_END, F_REWRITE, LOCAL_SEQ_BASE, MTE_E_CLIENT_RANGE,
-                  MTE_E_INVALID_ARG, MTE_E_STATE, MTE_E_UNSUPPORTED, MTE_MAX_CLIENTS, NO_PROPS, OP_ACK,
+                  MTE_E_INVALID_ARG, MTE_E_STATE, MTE_E_UNSUPPORTED, MTE_MAX_CLIENTS, NO_PROPS, OP_ACK, OP_ROLLBACK,
                   OP_ANNOTATE, OP_DTYPE, OP_INSERT, OP_NOOP, OP_REMOVE, PROP_DTYPE, PROPSET_DTYPE,
                   MergeTreeError)
 
@@ -143,6 +143,7 @@ class DocClients:
         self.local = local
         self.local_seq = 0
         self.pending = []
+        self.pending_types = []  # the record types of each pending message (rollback)
 
     def short(self, long_id, seq=None) -> int:
         i = self.ids.get(long_id)
@@ -215,6 +216,7 @@ class BatchBuilder:
                 if not clients.pending:
                     raise MergeTreeError(MTE_E_STATE, "ack without a pending local op")
                 lo, hi = clients.pending.pop(0)
+                clients.pending_types.pop(0)
                 recs.append((OP_ACK, 0, lo, hi, 0, NO_PROPS))
             else:
                 self._op_records(msg.get("contents"), recs)
@@ -255,6 +257,25 @@ class BatchBuilder:
             out.append((first + i, 0, 0, t, 0, flags | F_LOCAL, p1, p2, a, b))
         clients.local_seq += len(recs)
         clients.pending.append((first, clients.local_seq))
+        clients.pending_types.append(tuple(r[0] for r in recs))
+
+    def add_rollback(self, doc: int, clients: DocClients):
+        """Client.rollback of the latest pending local op (client.ts:396-398 ->
+        MergeTree.rollback, mergeTree.ts:2005-2083): one MTE_OP_ROLLBACK record
+        per record of that op, last first.  Rolling back an annotate is not
+        supported (MTE_E_UNSUPPORTED)."""
+        if not clients.local or not clients.pending:
+            raise MergeTreeError(MTE_E_STATE, "rollback without a pending local op")
+        types = clients.pending_types[-1]
+        if OP_ANNOTATE in types:
+            raise MergeTreeError(MTE_E_UNSUPPORTED, "rollback of an annotate")
+        lo, hi = clients.pending.pop()
+        clients.pending_types.pop()
+        out = self.ops[doc]
+        for ls in range(hi, lo - 1, -1):
+            t = types[ls - lo]
+            if t != OP_NOOP:
+                out.append((ls, 0, 0, OP_ROLLBACK, 0, F_LOCAL, t, 0, 0, NO_PROPS))
 
     def _op_records(self, op, recs):
         if not isinstance(op, dict):

@@ -80,6 +80,13 @@ extern "C" {
  * stop blocking remote annotates; then the window update as for any message.
  * Only in MTE_DOC_LOCAL_CLIENT documents.                                    */
 #define MTE_OP_ACK 4
+/* Client.rollback of the document's own latest pending op (client.ts:396-398
+ * -> MergeTree.rollback, mergeTree.ts:2005-2083), which is then never sent:
+ * seq = that op's localSeq, pos1 = its type.  A rolled-back insert becomes a
+ * removed segment of seq and removedSeq UniversalSequenceNumber (0), gone for
+ * every view; a rolled-back remove restores its segments.  A rollback of an
+ * annotate is MTE_E_UNSUPPORTED.  Only in MTE_DOC_LOCAL_CLIENT documents.    */
+#define MTE_OP_ROLLBACK 5
 
 #define MTE_F_MARKER 0x0001u  /* insert spec {marker:{refType}} (mergeTreeNodes.ts:602-609) */
 #define MTE_F_MSG_END 0x0002u /* last record of its message: window update follows      */

@@ -309,6 +309,8 @@ static int64_t doc_lengths_local(odoc* d) {
   return p;
 }
 
+static int doc_rollback(odoc* d, const mte_op* op);
+
 /* A local op (MTE_F_LOCAL, include/mte.h): insertSegmentLocal /
  * removeRangeLocal / annotateRangeLocal (client.ts:131-229) with seq =
  * UnassignedSequenceNumber, held as LOCAL_BASE + localSeq.
@@ -324,6 +326,7 @@ static int64_t doc_lengths_local(odoc* d) {
 static int doc_apply_local(odoc* d, const mte_op* op, const apply_env* env) {
   const int32_t ls = op->seq;
   int rc;
+  if (op->type == MTE_OP_ROLLBACK) return doc_rollback(d, op);
   if (!(ls > d->local_seq && ls < LOCAL_BASE)) return MTE_E_INVALID_ARG;
   if (op->client != 0) return MTE_E_INVALID_ARG;
   if (op->type == MTE_OP_ANNOTATE && (op->flags & MTE_F_REWRITE)) return MTE_E_UNSUPPORTED;
@@ -394,6 +397,38 @@ static int doc_apply_local(odoc* d, const mte_op* op, const apply_env* env) {
       }
     }
     d->written += 1;
+  }
+  return MTE_OK;
+}
+
+/* MTE_OP_ROLLBACK (a local record): MergeTree.rollback of the pending op of
+ * localSeq op->seq, type op->pos1 (mergeTree.ts:2005-2083).  Its inserted
+ * segments get seq and removedSeq UniversalSequenceNumber (markRangeRemoved
+ * at seq 0 by the local client: gone for every view, zamboni drops them);
+ * its removed ones are restored.  Each segment's delta event comes at its
+ * own-view position once it is done (findRollbackPosition :2088-2103). */
+static int doc_rollback(odoc* d, const mte_op* op) {
+  const int32_t ls = op->seq;
+  int rc;
+  if (!(ls > 0 && ls <= d->local_seq)) return MTE_E_INVALID_ARG;
+  if (op->pos1 != MTE_OP_INSERT && op->pos1 != MTE_OP_REMOVE) return MTE_E_UNSUPPORTED;
+  d->ops++;
+  d->scanned += d->n;
+  int64_t lp = 0;
+  for (uint32_t i = 0; i < d->n; lp += own_len(&d->s[i]), i++) {
+    oseg* g = &d->s[i];
+    if (op->pos1 == MTE_OP_INSERT && g->seq == LOCAL_BASE + ls) {
+      g->seq = 0;
+      g->rseq = 0;
+      g->rmask = 1u;
+      if ((d->flags & MTE_DOC_EVENTS) && (rc = delta_push(d, MTE_OP_REMOVE, lp, g->len, 1))) return rc;
+      d->written += 1;
+    } else if (op->pos1 == MTE_OP_REMOVE && g->rseq == LOCAL_BASE + ls) {
+      g->rseq = NONE_SEQ;
+      g->rmask = 0;
+      if ((d->flags & MTE_DOC_EVENTS) && (rc = delta_push(d, MTE_OP_INSERT, lp, g->len, 0))) return rc;
+      d->written += 1;
+    }
   }
   return MTE_OK;
 }
@@ -747,7 +782,8 @@ int orc_apply_batch(orc_ctx* c, const mte_batch* b, int n_threads) {
     while (dcur + 1 < b->n_docs && b->op_offsets[dcur + 1] <= k) dcur++;
     /* local records (as mte_submit validates them) */
     const int local_doc = (c->docs[dcur].flags & MTE_DOC_LOCAL_CLIENT) != 0;
-    if (op->type > MTE_OP_ACK) return MTE_E_INVALID_ARG;
+    if (op->type > MTE_OP_ROLLBACK) return MTE_E_INVALID_ARG;
+    if (op->type == MTE_OP_ROLLBACK && !(op->flags & MTE_F_LOCAL)) return MTE_E_INVALID_ARG;
     if ((op->flags & MTE_F_LOCAL) || op->type == MTE_OP_ACK) {
       if (!local_doc) return MTE_E_INVALID_ARG;
       if ((op->flags & MTE_F_LOCAL) && (op->type == MTE_OP_ACK || op->seq <= 0 || op->seq >= MTE_LOCAL_SEQ_BASE))

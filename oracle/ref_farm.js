@@ -17,9 +17,12 @@
 // segmentPropertiesManager.ts:94-135) and the window trails far behind.
 //
 // stdin:  {"sets": [{"seed": int, "clients": int, "steps": int, "initialText": str,
-//                    "nCheckpoints": int, "maxText": int}]}
+//                    "nCheckpoints": int, "maxText": int, "rollback": p}]}
+//         (rollback: the chance that a local insert / remove is rolled back
+//         instead of sent; the event is ["R", op]: the client made the op
+//         locally, then rolled it back)
 // stdout: {"sets": [{..params, "names": [...], "log": [[clientId, seq, ref, msn, "op", contents]],
-//                    "events": [[["L"|"A", logIndex], ...] per client],
+//                    "events": [[["L"|"A", logIndex] | ["R", op], ...] per client],
 //                    "checkpoints": [{"done": [events applied per client],
 //                                     "states": [{"text", "props": [[start, end, {..}]]}]}]}]}
 // Client 0 ("A") never sends: the observer.
@@ -147,7 +150,13 @@ function runSet(p) {
           op = c.annotateRangeLocal(start, end, props, undefined);
         }
       }
-      if (op) {
+      if (op && p.rollback && (p.rollbackInserts ? op.type !== 2 : op.type === 1) && R.next() < p.rollback) {
+        // Client.rollback of the op just made (client.ts:396-398 ->
+        // MergeTree.rollback, mergeTree.ts:2005-2083): it is never sent
+        const opJson = JSON.parse(JSON.stringify(op));
+        c.rollback(op, c.peekPendingSegmentGroups());
+        events[i].push(["R", opJson]);
+      } else if (op) {
         let msn = Infinity;
         for (const x of clients) msn = Math.min(msn, x.getCurrentSeq());
         seq++;

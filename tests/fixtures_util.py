@@ -188,7 +188,8 @@ def replay_ref_farm(engine_factory, sets, n_keys=8):
     """Replay farms the reference ran (oracle/ref_farm.js -> tests/golden/
     farm_vectors.json.gz): one MTE_DOC_LOCAL_CLIENT document per client of every
     set (the observer "A" included), each fed its own events in order — "L" a
-    local op, "A" a sequenced message (its own: an ack) — in one batch per
+    local op, "A" a sequenced message (its own: an ack), "R" a local op made and
+    rolled back at once (Client.rollback) — in one batch per
     checkpoint; text and per-position properties must equal the reference
     client's at every checkpoint.  Returns (checkpoints_passed, failures)."""
     from fluidframework_amd.abi import DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC
@@ -211,6 +212,10 @@ def replay_ref_farm(engine_factory, sets, n_keys=8):
                 continue
             done = s["checkpoints"][j]["done"][ci]
             for kind, li in s["events"][ci][prev[d]:done]:
+                if kind == "R":  # the op (li) made locally, then rolled back
+                    bb.add_local(d, clients[d], li)
+                    bb.add_rollback(d, clients[d])
+                    continue
                 m = as_msg(s["log"][li])
                 if kind == "L":
                     bb.add_local(d, clients[d], m["contents"])

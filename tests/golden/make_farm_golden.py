@@ -30,21 +30,38 @@ FARM_JS = os.path.join(ROOT, "oracle", "ref_farm.js")
 
 # (seed, clients incl. the observer, steps, initial text, checkpoints, text bound)
 SETS = [(1000 + i, 2 + i % 7, 300 + 150 * (i % 8), ["", "hello world", "x" * 40, "abc\ndef"][i % 4], 4,
-         [64, 200, 400][i % 3]) for i in range(40)]
+         [64, 200, 400][i % 3], 0.0) for i in range(40)]
+# with rollbacks: a local remove is rolled back instead of sent (Client.rollback)
+SETS += [(2000 + i, 2 + i % 7, 400 + 100 * (i % 5), ["", "hello world"][i % 2], 4, [64, 200][i % 2], 0.15)
+         for i in range(16)]
+# removes and inserts rolled back: the reference's own farm stops on some seeds
+# ("MergeTree insert failed" in another client after a rolled-back insert);
+# those seeds are left out and counted in the file
+ROLLBACK_INSERT_SETS = [(3000 + i, 2 + i % 5, 400, ["", "hello world"][i % 2], 4, 200, 0.15) for i in range(24)]
 
 
 def main():
     if not ref_util.ref_available():
         sys.exit("the reference sources are not in this container")
     out = ref_util.build_ref()
-    inp = {"sets": [{"seed": s, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m}
-                    for s, c, n, t, k, m in SETS]}
+    inp = {"sets": [{"seed": s, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
+                     "rollback": rb} for s, c, n, t, k, m, rb in SETS]}
     p = subprocess.run(["node", "--max-old-space-size=8192", FARM_JS, out], input=json.dumps(inp),
                        capture_output=True, text=True, timeout=3600)
     if p.returncode != 0:
         sys.exit(p.stderr[-4000:])
     res = json.loads(p.stdout)
     res["generator"] = "oracle/ref_farm.js (reference Client, mulberry32 seeds)"
+    failed = []
+    for sd, c, n, t, k, m, rb in ROLLBACK_INSERT_SETS:
+        one = {"sets": [{"seed": sd, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
+                         "rollback": rb, "rollbackInserts": True}]}
+        q = subprocess.run(["node", FARM_JS, out], input=json.dumps(one), capture_output=True, text=True, timeout=600)
+        if q.returncode == 0:
+            res["sets"] += json.loads(q.stdout)["sets"]
+        else:
+            failed.append(sd)
+    res["rollback_insert_seeds_the_reference_failed"] = failed
     with gzip.open(OUT, "wt", encoding="utf-8") as fh:
         json.dump(res, fh, separators=(",", ":"))
     n_msgs = sum(len(s["log"]) for s in res["sets"])

@@ -64,6 +64,14 @@ for (let j = 0; j < nCp; j++) {
     if (j >= s.checkpoints.length) return;
     const done = s.checkpoints[j].done[L.ci];
     for (const [kind, li] of s.events[L.ci].slice(prev[d], done)) {
+      if (kind === "R") {  // the op made locally, then rolled back (Client.rollback)
+        if (sync) L.client.getLength();
+        const o = li;
+        const op = o.type === 0 ? L.client.insertSegmentLocal(o.pos1, o.seg) : L.client.removeRangeLocal(o.pos1, o.pos2);
+        L.client.rollback(op);
+        opsChecked++;
+        continue;
+      }
       const m = asMsg(s.log[li]);
       if (kind === "A") {
         L.client.applyMsg(m);

@@ -25,6 +25,11 @@ for (let j = 0; j < nCp; j++) {
     if (j >= s.checkpoints.length) return;
     const done = s.checkpoints[j].done[ci];
     for (const [kind, li] of s.events[ci].slice(prev[d], done)) {
+      if (kind === "R") {  // made locally, then rolled back
+        bb.addLocal(d, cl, li);
+        bb.addRollback(d, cl);
+        continue;
+      }
       const m = asMsg(s.log[li]);
       if (kind === "L") bb.addLocal(d, cl, m.contents);
       else bb.addMessage(d, cl, m);

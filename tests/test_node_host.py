@@ -95,6 +95,10 @@ def test_js_packing_matches_python_packing_on_local_farms():
                 continue
             done = s["checkpoints"][j]["done"][ci]
             for kind, li in s["events"][ci][prev[d]:done]:
+                if kind == "R":
+                    bb.add_local(d, cl, li)
+                    bb.add_rollback(d, cl)
+                    continue
                 m = as_msg(s["log"][li])
                 if kind == "L":
                     bb.add_local(d, cl, m["contents"])
