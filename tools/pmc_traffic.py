@@ -20,7 +20,8 @@ import json
 import os
 import sys
 
-PATH_KERNELS = ("begin_batch_kernel", "props_kernel", "pair_kernel", "big_kernel", "stream_kernel")
+PATH_KERNELS = ("begin_batch_kernel", "props_kernel", "round_sync_kernel", "pair_kernel", "big_kernel", "stream_kernel",
+                "chunk_kernel", "tree_kernel")
 
 
 def last_dispatch(d, counter):
