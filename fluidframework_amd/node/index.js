@@ -177,8 +177,10 @@ class MergeTreeEngine {
     this.start();
     if (this.pending.count === 0) return;
     const b = this.pending.build();
-    // a replay still running delivers its events before this batch takes the engine
-    this.sync();
+    // documents with delta events: the running replay delivers its events
+    // before this batch takes the engine (the events of one run are read
+    // back before the next run); otherwise this batch uploads while it runs
+    if (this.track) this.sync();
     this.inflightSrc = this.pending.recSrc;
     this.pending = new BatchBuilder(this.docs.length, this.interner, this.track);
     this.views.fill(null);
