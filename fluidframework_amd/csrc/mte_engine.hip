@@ -140,6 +140,7 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
     const uint32_t nz = n_img ? n_img : 1u;
     for (uint32_t k = 0; k < kt; k++)
       for (uint32_t x = 0; x < nz; x++) soa.props[(kt + k) * soa.plane_stride + (uint64_t)d * cap + x] = 0u;
+    for (uint32_t x = 0; x < nz; x++) soa.props[2ull * kt * soa.plane_stride + (uint64_t)d * cap + x] = 0u;  // no groups
   }
   if (n_img) return;  // image_kernel writes the segments
   const uint64_t i = (uint64_t)d * cap;
@@ -573,8 +574,10 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
 // Validation of one op record (the kernels index with these fields, so a bad
 // record must never reach them).  Returns nullptr or the reason.
 const char* bad_op(const mte_op& o, const mte_batch* b, bool local_doc) {
-  if (o.type > MTE_OP_ROLLBACK) return "type";
-  if (o.type == MTE_OP_ROLLBACK && !(o.flags & MTE_F_LOCAL)) return "rollback without MTE_F_LOCAL";
+  if (o.type > MTE_OP_REGEN) return "type";
+  if (o.type >= MTE_OP_ROLLBACK && !(o.flags & MTE_F_LOCAL)) return "rollback / regen without MTE_F_LOCAL";
+  if ((o.flags & MTE_F_LOCAL) && o.type == MTE_OP_ANNOTATE && o.b != MTE_NO_PROPS && o.b >= MTE_ANNOTATE_SLOTS)
+    return "annotate group slot out of range";
   if ((o.flags & MTE_F_LOCAL) || o.type == MTE_OP_ACK) {
     if (!local_doc) return "local op or ack in a document without MTE_DOC_LOCAL_CLIENT";
     if ((o.flags & MTE_F_LOCAL) && (o.type == MTE_OP_ACK || o.seq <= 0 || o.seq >= MTE_LOCAL_SEQ_BASE))
@@ -805,7 +808,8 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     if (docs[d].flags & MTE_DOC_EVENTS) c->h_events[d] = 1;
   }
   // documents with a local client hold kt more planes: the pending property keys (mte_stream.h)
-  const uint64_t prop_planes = (c->kt ? c->kt : 1) + (any_local ? c->kt : 0);
+  // + per local doc: the pending-key planes and the annotate-group plane (mte_stream.h)
+  const uint64_t prop_planes = (c->kt ? c->kt : 1) + (any_local ? c->kt + 1 : 0);
   HIPCHK(c, hipMalloc((void**)&c->hdr, sizeof(DocHdr) * (n_docs ? n_docs : 1)));
   // one allocation, planes at stride nslots: len seq rseq rmask meta toff props[kt]
   // (kt >= n_keys planes, so the register-resident kernels never index past it)

@@ -60,8 +60,12 @@ __device__ __forceinline__ void tile_load_hot(Regs<kTileE, K>& R, const uint32_t
 // 1713-1714).  K more planes after the property planes hold, per slot and key,
 // the localSeq of the last pending local annotate that set the key (0 = none):
 // the pendingKeyUpdateCount of segmentPropertiesManager.ts:94-135 (acks come in
-// order, so "count > 0" is "last pending localSeq not yet acked").
+// order, so "count > 0" is "last pending localSeq not yet acked").  One more
+// plane after them holds the mask of the pending annotate segment groups the
+// slot belongs to (MTE_ANNOTATE_SLOTS, include/mte.h).
 constexpr int32_t kLocalBase = MTE_LOCAL_SEQ_BASE;
+template <int K>
+constexpr int kAnnPlane = kFieldPlanes + 2 * K;
 
 // the local client's own view (localNetLength, mergeTree.ts:553-573, new
 // length calculation): removed -> 0, else the length; padding undefined
@@ -92,7 +96,8 @@ __device__ __forceinline__ int find_slot_remote(const int32_t (&L)[E], const int
 // those ops take seq (a removal a remote op overtook already has its seq,
 // :1928-1938), and their property keys stop being pending.
 template <int K>
-__device__ __forceinline__ void stream_ack(uint32_t* pl, uint64_t sd, int n, int32_t lo, int32_t hi, int32_t s) {
+__device__ __forceinline__ void stream_ack(uint32_t* pl, uint64_t sd, int n, int32_t lo, int32_t hi, int32_t s,
+                                           uint32_t ann_mask) {
   const int l = lane_id();
   for (int tb = 0; tb < n; tb += kTile) {
 #pragma unroll
@@ -109,6 +114,11 @@ __device__ __forceinline__ void stream_ack(uint32_t* pl, uint64_t sd, int n, int
         uint32_t* q = pl + (uint64_t)(kFieldPlanes + K + kk) * sd + i;
         const uint32_t v = ld_l2(q);
         if (v != 0u && v <= (uint32_t)hi) *q = 0u;
+      }
+      if (ann_mask) {  // the acked annotates' segment groups
+        uint32_t* q = pl + (uint64_t)kAnnPlane<K> * sd + i;
+        const uint32_t v = ld_l2(q);
+        if (v & ann_mask) *q = v & ~ann_mask;
       }
     }
   }
@@ -198,6 +208,59 @@ __device__ __forceinline__ void stream_rollback(uint32_t* pl, uint64_t sd, int n
   vm_drain();
 }
 
+// MTE_OP_REGEN: Client.regeneratePendingOp of the pending op of localSeq ls,
+// type t (client.ts:972-1002 -> resetPendingDeltaToOps :788-860): its segment
+// group in document order, each at its position in the view at localSeq ls
+// (findReconnectionPosition :709-713 -> localNetLength with localSeq,
+// mergeTree.ts:575-593) with its length, as MTE_DELTA_REGEN | t records.
+// Inserts: the segments ls inserted (their text offset rides in `removed`);
+// removes: the ones ls still holds removed (no remote remove overtook it);
+// annotates: the members of group slot `slot` not removed, or removed only by
+// a pending local remove.  The document does not change.
+template <int K>
+__device__ __forceinline__ void stream_regen(const uint32_t* pl, uint64_t sd, int n, int32_t ls, uint32_t t,
+                                             uint32_t slot, EvOut& ev) {
+  const int l = lane_id();
+  int32_t cy = 0;
+  for (int tb = 0; tb < n; tb += kTile) {
+    bool hit[kTileE];
+    int32_t LL[kTileE], PP[kTileE], len[kTileE];
+    uint32_t tf[kTileE];
+#pragma unroll
+    for (int j = 0; j < kTileE; j++) {
+      const int i = tb + l * kTileE + j;
+      const bool v = i < n;
+      len[j] = v ? (int32_t)ld_l2(pl + i) : 0;
+      const int32_t sq = v ? (int32_t)ld_l2(pl + sd + i) : 0;
+      const int32_t rs = v ? (int32_t)ld_l2(pl + 2 * sd + i) : kPad;
+      tf[j] = v ? ld_l2(pl + 5 * sd + i) : 0u;
+      const bool rp = rs >= kLocalBase && rs != kNone;  // a pending local removal
+      if (t == MTE_OP_INSERT) hit[j] = v && sq == kLocalBase + ls;
+      else if (t == MTE_OP_REMOVE) hit[j] = v && rs == kLocalBase + ls;
+      else hit[j] = v && ((ld_l2(pl + (uint64_t)kAnnPlane<K> * sd + i) >> slot) & 1u) && (rs == kNone || rp);
+      const bool later = sq >= kLocalBase && sq - kLocalBase > ls;  // inserted after ls
+      const bool gone = rs != kNone && (!rp || rs - kLocalBase <= ls);
+      LL[j] = (v && !later && !gone) ? len[j] : 0;
+    }
+    const int32_t tot = prefix<kTileE>(LL, PP);
+    uint32_t ecnt = 0;
+#pragma unroll
+    for (int j = 0; j < kTileE; j++) ecnt += hit[j] ? 1u : 0u;
+    const int32_t eincl = wave_incl_scan((int32_t)ecnt);
+    uint32_t e = ev.n + (uint32_t)(eincl - (int32_t)ecnt);
+#pragma unroll
+    for (int j = 0; j < kTileE; j++) {
+      if (hit[j]) {
+        if (e < ev.cap)
+          ev.p[e] = mte_delta{ev.op, MTE_DELTA_REGEN | t, cy + PP[j], len[j], t == MTE_OP_INSERT ? tf[j] : 0u};
+        e++;
+      }
+    }
+    ev.n += (uint32_t)rdlane(eincl, kWave - 1);
+    cy += tot;
+  }
+}
+
 // One op of one HBM-resident document (see the file comment).  Returns 0 or
 // a negative MTE_E_*.  lseq: the document's last localSeq (local-client docs);
 // ev: its delta events (MTE_DOC_EVENTS docs).
@@ -211,7 +274,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   const bool ldoc = (D.flags & MTE_DOC_LOCAL_CLIENT) != 0;
   const bool evd = (D.flags & MTE_DOC_EVENTS) != 0;
   ev.op = D.k;
-  const int nplanes = kFieldPlanes + K + (ldoc ? K : 0);  // + the pending-key planes
+  const int nplanes = kFieldPlanes + K + (ldoc ? K + 1 : 0);  // + the pending-key and group planes
 
   const s8v op = cur;
   const uint4* rec = D.recp + 2 * D.k;
@@ -219,7 +282,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
-  if (type > MTE_OP_ROLLBACK) return MTE_E_INVALID_ARG;
+  if (type > MTE_OP_REGEN) return MTE_E_INVALID_ARG;
   const bool lop = (flags & MTE_F_LOCAL) != 0;  // a local op: the local view, seq = localSeq
   if ((lop || type >= MTE_OP_ACK) && !ldoc) return MTE_E_UNSUPPORTED;
   MTE_STAT(st[kStOps]++;)
@@ -234,9 +297,21 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
     D.k++;
     return 0;
   }
+  if (type == MTE_OP_REGEN) {
+    if (!lop || !(s > 0 && s <= lseq)) return MTE_E_INVALID_ARG;
+    if (pos1 != MTE_OP_INSERT && pos1 != MTE_OP_REMOVE && pos1 != MTE_OP_ANNOTATE) return MTE_E_INVALID_ARG;
+    if (pos1 == MTE_OP_ANNOTATE && (uint32_t)op[6] >= MTE_ANNOTATE_SLOTS) return MTE_E_INVALID_ARG;
+    if (!evd) return MTE_E_UNSUPPORTED;
+    MTE_STAT(st[kStScanned] += (uint32_t)D.n;)
+    stream_regen<K>(pl, sd, D.n, s, (uint32_t)pos1, (uint32_t)op[6], ev);
+    D.k++;
+    return 0;
+  }
   if (lop) {
     if (!(s > lseq && s < kLocalBase) || c != 0) return MTE_E_INVALID_ARG;
     if (type == MTE_OP_ANNOTATE && (flags & MTE_F_REWRITE)) return MTE_E_UNSUPPORTED;
+    if (type == MTE_OP_ANNOTATE && (uint32_t)op[7] != MTE_NO_PROPS && (uint32_t)op[7] >= MTE_ANNOTATE_SLOTS)
+      return MTE_E_INVALID_ARG;
     lseq = s;
   } else if (ldoc && type <= MTE_OP_ANNOTATE && c == 0) {
     return MTE_E_INVALID_ARG;  // a remote op from the local client's own slot
@@ -251,7 +326,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   if (type == MTE_OP_ACK) {
     if (!(pos1 > 0 && pos1 <= pos2 && pos2 <= lseq)) return MTE_E_INVALID_ARG;
     MTE_STAT(st[kStScanned] += (uint32_t)n;)
-    stream_ack<K>(pl, sd, n, pos1, pos2, s);
+    stream_ack<K>(pl, sd, n, pos1, pos2, s, (uint32_t)op[6]);
   }
   if (ins || rng) {
     MTE_STAT(st[kStScanned] += (uint32_t)n;)
@@ -417,6 +492,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
         if (ldoc) {
 #pragma unroll
           for (int kk = 0; kk < K; kk++) pl[(kFieldPlanes + K + kk) * sd + g] = 0u;  // nothing pending
+          pl[(uint64_t)kAnnPlane<K> * sd + g] = 0u;  // in no annotate group
         }
       }
       MTE_STAT(if (!marker) st[kStUnits] += (uint32_t)pos2;)
@@ -481,6 +557,16 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
         if (cnt == 0) continue;
         cnt_all += cnt;
         const int base = tb + l * E;
+        if (lop && type == MTE_OP_ANNOTATE && (uint32_t)op[7] < MTE_ANNOTATE_SLOTS) {
+          // the visited slots join the annotate's segment group (mergeTree.ts:1874-1880)
+#pragma unroll
+          for (int j = 0; j < E; j++) {
+            if (in[j]) {
+              uint32_t* q = pl + (uint64_t)kAnnPlane<K> * sd + base + j;
+              *q = ld_l2(q) | (1u << (uint32_t)op[7]);
+            }
+          }
+        }
         if (rem) {
           // markRemoved (mergeTree.ts:1924-1962)
 #pragma unroll

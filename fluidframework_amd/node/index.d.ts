@@ -199,6 +199,9 @@ export class BatchClient {
   annotateRangeLocal(start: number, end: number, props: PropertySet, combiningOp?: { name: string }): IMergeTreeOp;
   makeOpMessage(op: IMergeTreeOp, seq?: number, refSeq?: number, minSeq?: number): ISequencedDocumentMessage;
   getPendingCount(): number;
+  /** Client.regeneratePendingOp for reconnection: the op re-sending the oldest
+   *  pending op (resetOp as sent); needs {localClient: true, events: true}. */
+  regeneratePendingOp(resetOp: IMergeTreeOp): IMergeTreeOp;
   /** Client.rollback of the latest pending local op (inserts and removes). */
   rollback(op?: IMergeTreeOp): void;
   /** SharedString "sequenceDelta" events ({events: true} documents), delivered at each flush in op order. */

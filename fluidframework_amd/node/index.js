@@ -451,6 +451,14 @@ class BatchClient {
     };
     for (let k = 0; k < recs.length; k++) {
       const src = recs[k];
+      if (src.regen) {  // a regenerated op (regeneratePendingOp): no event
+        while (i < n && flat[5 * i] === k) {
+          (this.regenRecs || (this.regenRecs = [])).push([k, flat[5 * i + 1], flat[5 * i + 2] | 0, flat[5 * i + 3],
+            flat[5 * i + 4]]);
+          i++;
+        }
+        continue;
+      }
       if (!src.local && (!cur || cur.msg !== src.msg)) {
         flushMsg();
         cur = { msg: src.msg, ops: [] };
@@ -478,6 +486,24 @@ class BatchClient {
    *  back an annotate is not supported. */
   rollback(op) {  // eslint-disable-line no-unused-vars
     this.engine._batch().addRollback(this.doc, this.clients);
+  }
+
+  /** Client.regeneratePendingOp (client.ts:972-1002 -> resetPendingDeltaToOps
+   *  :788-860) for reconnection: the op that re-sends the oldest pending op
+   *  (resetOp, as it was sent), one member per segment of its group, at
+   *  positions in the view at its localSeq; the op stays pending (acked by the
+   *  sequenced message of the returned op).  Needs {localClient, events};
+   *  replays what is queued (flush + sync). */
+  regeneratePendingOp(resetOp) {
+    if (!this.engine.docs[this.doc].events) throw new MergeTreeError(-9, "createClient(..., {events: true}) first");
+    const idx = this.engine._batch().addRegen(this.doc, this.clients);
+    this.regenRecs = [];
+    this.engine.flush();
+    this.engine.sync();
+    if (this.engine.statuses()[this.doc] !== 0) throw docError(this.engine.statuses()[this.doc], this.doc);
+    const op = packing.regenOps(resetOp, idx, this.regenRecs);
+    this.regenRecs = null;
+    return op;
   }
 
   /** Local ops sent but not acknowledged yet. */

@@ -28,7 +28,9 @@
  * for record (tests/test_node_host.py checks the bytes are identical).
  */
 
-const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 3, OP_ACK = 4, OP_ROLLBACK = 5;
+const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 3, OP_ACK = 4, OP_ROLLBACK = 5, OP_REGEN = 6;
+const DELTA_REGEN = 0x10;    // MTE_DELTA_REGEN: kind flag of a regenerated op's records
+const ANNOTATE_SLOTS = 32;   // MTE_ANNOTATE_SLOTS: pending local annotate groups tracked per document
 const F_MARKER = 0x1, F_MSG_END = 0x2, F_REWRITE = 0x4, F_LOCAL = 0x8;
 const LOCAL_SEQ_BASE = 0x40000000; // MTE_LOCAL_SEQ_BASE
 const NO_PROPS = 0xffffffff;
@@ -132,6 +134,9 @@ class DocClients {
     this.localSeq = 0;
     this.pending = [];
     this.pendingTypes = [];  // the record types of each pending message (rollback)
+    // segment groups of pending local annotates: localSeq -> group slot; an
+    // annotate made while all are taken is not tracked (cannot be regenerated)
+    this.annSlot = new Map();
   }
   short(longId, seq) {
     let i = this.ids.get(longId);
@@ -236,7 +241,14 @@ class BatchBuilder {
         if (clients.pending.length === 0) throw new MergeTreeError(E_STATE, "ack without a pending local op");
         const [lo, hi] = clients.pending.shift();
         clients.pendingTypes.shift();
-        recs.push([OP_ACK, 0, lo, hi, 0, NO_PROPS]);
+        let mask = 0;
+        for (let ls = lo; ls <= hi; ls++) {
+          if (clients.annSlot.has(ls)) {
+            mask |= 1 << clients.annSlot.get(ls);
+            clients.annSlot.delete(ls);
+          }
+        }
+        recs.push([OP_ACK, 0, lo, hi, mask >>> 0, NO_PROPS]);
       } else {
         this._opRecords(msg.contents, recs, this._src(doc));
       }
@@ -276,7 +288,17 @@ class BatchBuilder {
     const first = clients.localSeq + 1;
     if (first + recs.length >= LOCAL_SEQ_BASE) throw new MergeTreeError(E_INVALID_ARG, "localSeq overflow");
     recs.forEach((r, i) => {
-      this.docOps[doc].push([first + i, 0, 0, r[0], 0, r[1] | F_LOCAL, r[2], r[3], r[4], r[5]]);
+      let b = r[5];
+      if (r[0] === OP_ANNOTATE) {
+        const used = new Set(clients.annSlot.values());
+        let free = -1;
+        for (let x = 0; x < ANNOTATE_SLOTS && free < 0; x++) if (!used.has(x)) free = x;
+        if (free >= 0) {
+          clients.annSlot.set(first + i, free);
+          b = free;
+        }
+      }
+      this.docOps[doc].push([first + i, 0, 0, r[0], 0, r[1] | F_LOCAL, r[2], r[3], r[4], b]);
     });
     this.count += recs.length;
     clients.localSeq += recs.length;
@@ -302,6 +324,39 @@ class BatchBuilder {
       const src = this._src(doc);
       if (src) src.push({ msg: null, op: undefined, local: true });
     }
+  }
+
+  /** Client.regeneratePendingOp of the oldest pending local message
+   *  (client.ts:972-1002), as packing.py add_regen: one MTE_OP_REGEN record per
+   *  record of it; the message moves to the end of the pending list.  Returns
+   *  [[record index in the doc's part of the batch, localSeq, type], ...]. */
+  addRegen(doc, clients) {
+    if (!clients.local || clients.pending.length === 0) {
+      throw new MergeTreeError(E_STATE, "regenerate without a pending local op");
+    }
+    const [lo, hi] = clients.pending[0];
+    const types = clients.pendingTypes[0];
+    const idx = [];
+    for (let ls = lo; ls <= hi; ls++) {
+      const t = types[ls - lo];
+      if (t === OP_NOOP) continue;
+      let slot = 0;
+      if (t === OP_ANNOTATE) {
+        if (!clients.annSlot.has(ls)) {
+          throw new MergeTreeError(E_UNSUPPORTED, "regenerate an untracked annotate (more than " + ANNOTATE_SLOTS +
+            " pending)");
+        }
+        slot = clients.annSlot.get(ls);
+      }
+      idx.push([this.docOps[doc].length, ls, t]);
+      this.docOps[doc].push([ls, 0, 0, OP_REGEN, 0, F_LOCAL, t, 0, slot, NO_PROPS]);
+      this.count++;
+      const src = this._src(doc);
+      if (src) src.push({ msg: null, op: undefined, local: true, regen: true });
+    }
+    clients.pending.push(clients.pending.shift());
+    clients.pendingTypes.push(clients.pendingTypes.shift());
+    return idx;
   }
 
   /** One MergeTree-level call (insertSegments / markRangeRemoved / annotateRange):
@@ -499,8 +554,60 @@ function packSegments(docs, clientsOf, inits) {
   return { offsets, segs: new Uint8Array(buf.buffer, buf.byteOffset, buf.length), extraText: extra.join("") };
 }
 
+/** The op Client.regeneratePendingOp returns (client.ts:972-1002,
+ *  resetPendingDeltaToOps :788-860), from the engine's MTE_DELTA_REGEN records,
+ *  as packing.py regen_ops: op = the pending message's original contents, idx =
+ *  addRegen's result, recs = [[record, kind, pos, len, textOffset], ...].  One
+ *  op per segment of each member's group in document order: an insert re-sends
+ *  its part of the original text (with the original seg.props, :829-832). */
+function regenOps(op, idx, recs) {
+  const flat = [];
+  const walk = (o) => {
+    if (o && o.type === GROUP) for (const m of o.ops || []) walk(m);
+    else if (!(o.type === INSERT && (o.seg === undefined || o.seg === null))) flat.push(o);
+  };
+  walk(op);
+  const byRec = new Map();
+  for (const r of recs) {
+    if (!(r[1] & DELTA_REGEN)) continue;
+    if (!byRec.has(r[0])) byRec.set(r[0], []);
+    byRec.get(r[0]).push(r);
+  }
+  const out = [];
+  idx.forEach(([k, , t], j) => {
+    const m = flat[j];
+    const rs = byRec.get(k) || [];
+    if (t === OP_INSERT) {
+      const seg = m.seg;
+      let base = Infinity;
+      for (const r of rs) base = Math.min(base, r[4]);
+      for (const r of rs) {
+        const text = typeof seg === "string" ? seg : seg.text;
+        if (text === undefined) {  // a marker
+          out.push({ pos1: r[2], seg, type: INSERT });
+          continue;
+        }
+        const piece = text.substr(r[4] - base, r[3]);
+        out.push({ pos1: r[2], seg: typeof seg === "string" || seg.props === undefined ? piece :
+          { text: piece, props: seg.props }, type: INSERT });
+      }
+    } else if (t === OP_REMOVE) {
+      for (const r of rs) out.push({ pos1: r[2], pos2: r[2] + r[3], type: REMOVE });
+    } else {
+      for (const r of rs) {
+        const a = { pos1: r[2], pos2: r[2] + r[3], props: m.props, type: ANNOTATE };
+        if (m.combiningOp) a.combiningOp = m.combiningOp;
+        out.push(a);
+      }
+    }
+  });
+  return out.length === 1 ? out[0] : { ops: out, type: GROUP };
+}
+
 module.exports = {
-  OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_ACK, F_MARKER, F_MSG_END, F_REWRITE, F_LOCAL, NO_PROPS, MAX_CLIENTS,
+  OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_ACK, OP_REGEN, DELTA_REGEN, ANNOTATE_SLOTS, F_MARKER, F_MSG_END, F_REWRITE,
+  F_LOCAL, NO_PROPS, MAX_CLIENTS,
   INSERT, REMOVE, ANNOTATE, GROUP,
   MergeTreeError, Interner, DocClients, PropTable, BatchBuilder, canonicalJson, packDocInits, packSegments, utf16,
+  regenOps,
 };

@@ -32,6 +32,7 @@ import numpy as np
 
 from .abi import (F_LOCAL, F_MARKER, F_MSG_END, F_REWRITE, LOCAL_SEQ_BASE, MTE_E_CLIENT_RANGE,
                   MTE_E_INVALID_ARG, MTE_E_STATE, MTE_E_UNSUPPORTED, MTE_MAX_CLIENTS, NO_PROPS, OP_ACK, OP_ROLLBACK,
+                  OP_REGEN, ANNOTATE_SLOTS,
                   OP_ANNOTATE, OP_DTYPE, OP_INSERT, OP_NOOP, OP_REMOVE, PROP_DTYPE, PROPSET_DTYPE,
                   MergeTreeError)
 
@@ -144,6 +145,10 @@ class DocClients:
         self.local_seq = 0
         self.pending = []
         self.pending_types = []  # the record types of each pending message (rollback)
+        # segment groups of pending local annotates: localSeq -> group slot
+        # (MTE_ANNOTATE_SLOTS, include/mte.h); an annotate made while all are
+        # taken is not tracked and cannot be regenerated
+        self.ann_slot = {}
 
     def short(self, long_id, seq=None) -> int:
         i = self.ids.get(long_id)
@@ -217,7 +222,11 @@ class BatchBuilder:
                     raise MergeTreeError(MTE_E_STATE, "ack without a pending local op")
                 lo, hi = clients.pending.pop(0)
                 clients.pending_types.pop(0)
-                recs.append((OP_ACK, 0, lo, hi, 0, NO_PROPS))
+                mask = 0
+                for ls in range(lo, hi + 1):
+                    if ls in clients.ann_slot:
+                        mask |= 1 << clients.ann_slot.pop(ls)
+                recs.append((OP_ACK, 0, lo, hi, mask, NO_PROPS))
             else:
                 self._op_records(msg.get("contents"), recs)
         # the slot is taken only once the message has validated
@@ -254,6 +263,12 @@ class BatchBuilder:
             raise MergeTreeError(MTE_E_INVALID_ARG, "localSeq overflow")
         out = self.ops[doc]
         for i, (t, flags, p1, p2, a, b) in enumerate(recs):
+            if t == OP_ANNOTATE:
+                used = set(clients.ann_slot.values())
+                free = next((x for x in range(ANNOTATE_SLOTS) if x not in used), None)
+                if free is not None:
+                    clients.ann_slot[first + i] = free
+                    b = free
             out.append((first + i, 0, 0, t, 0, flags | F_LOCAL, p1, p2, a, b))
         clients.local_seq += len(recs)
         clients.pending.append((first, clients.local_seq))
@@ -276,6 +291,36 @@ class BatchBuilder:
             t = types[ls - lo]
             if t != OP_NOOP:
                 out.append((ls, 0, 0, OP_ROLLBACK, 0, F_LOCAL, t, 0, 0, NO_PROPS))
+
+    def add_regen(self, doc: int, clients: DocClients):
+        """Client.regeneratePendingOp of the oldest pending local message
+        (client.ts:972-1002): one MTE_OP_REGEN record per record of it; the
+        message moves to the end of the pending list (its groups are re-queued
+        under the same localSeqs, resetPendingDeltaToOps :851-855).  Returns
+        [(record index in the doc's part of the batch, localSeq, type)]; the
+        engine reports the regenerated ops as MTE_DELTA_REGEN delta records of
+        those indices (regen_ops turns them into ops)."""
+        if not clients.local or not clients.pending:
+            raise MergeTreeError(MTE_E_STATE, "regenerate without a pending local op")
+        lo, hi = clients.pending[0]
+        types = clients.pending_types[0]
+        out = self.ops[doc]
+        idx = []
+        for ls in range(lo, hi + 1):
+            t = types[ls - lo]
+            if t == OP_NOOP:
+                continue
+            slot = 0
+            if t == OP_ANNOTATE:
+                if ls not in clients.ann_slot:
+                    raise MergeTreeError(MTE_E_UNSUPPORTED, "regenerate an untracked annotate "
+                                         f"(more than {ANNOTATE_SLOTS} pending)")
+                slot = clients.ann_slot[ls]
+            idx.append((len(out), ls, t))
+            out.append((ls, 0, 0, OP_REGEN, 0, F_LOCAL, t, 0, slot, NO_PROPS))
+        clients.pending.append(clients.pending.pop(0))
+        clients.pending_types.append(clients.pending_types.pop(0))
+        return idx
 
     def _op_records(self, op, recs):
         if not isinstance(op, dict):
@@ -333,3 +378,59 @@ class BatchBuilder:
         ps, pe = self.props.arrays()
         return {"op_offsets": offsets, "ops": ops, "text": text.astype("<u2"),
                 "propsets": ps, "props": pe}
+
+
+def _members(op):
+    """The merge-tree ops of a message's contents, GROUP flattened (one localSeq each)."""
+    if isinstance(op, dict) and op.get("type") == GROUP:
+        return [m for x in op.get("ops", []) for m in _members(x)]
+    return [op]
+
+
+def regen_ops(op, idx, deltas):
+    """The regenerated op of Client.regeneratePendingOp (client.ts:972-1002,
+    resetPendingDeltaToOps :788-860) from the engine's MTE_DELTA_REGEN records.
+
+    op: the pending message's original contents; idx: add_regen's result;
+    deltas: the doc's delta records (DELTA_DTYPE) of that batch.  One op per
+    segment of each member's group, in document order: an insert re-sends the
+    segment's part of the original text (with the original seg.props, if any,
+    :829-832), a remove / annotate its range.  Returns one op, or a GROUP."""
+    from .abi import DELTA_REGEN
+    members = [m for m in _members(op) if not (m.get("type") == INSERT and m.get("seg") is None)]
+    by_rec = {}
+    for dl in deltas:
+        if int(dl["kind"]) & DELTA_REGEN:
+            by_rec.setdefault(int(dl["op"]), []).append(dl)
+    out = []
+    for (k, _ls, t), m in zip(idx, [m for m in members if m.get("type") in (INSERT, REMOVE, ANNOTATE)]):
+        recs = by_rec.get(k, [])
+        if t == INSERT:
+            seg = m["seg"]
+            base = min((int(r["removed"]) for r in recs), default=0)
+            for r in recs:
+                p, n = int(r["pos"]), int(r["len"])
+                if isinstance(seg, str):
+                    u = utf16_units(seg)
+                    o = int(r["removed"]) - base
+                    s = u[o:o + n].tobytes().decode("utf-16-le")
+                    out.append({"pos1": p, "seg": s, "type": INSERT})
+                elif "text" in seg:
+                    u = utf16_units(seg["text"])
+                    o = int(r["removed"]) - base
+                    s = {"text": u[o:o + n].tobytes().decode("utf-16-le")}
+                    if seg.get("props") is not None:
+                        s["props"] = seg["props"]
+                    out.append({"pos1": p, "seg": s, "type": INSERT})
+                else:
+                    out.append({"pos1": p, "seg": seg, "type": INSERT})
+        elif t == REMOVE:
+            out += [{"pos1": int(r["pos"]), "pos2": int(r["pos"]) + int(r["len"]), "type": REMOVE} for r in recs]
+        else:
+            for r in recs:
+                a = {"pos1": int(r["pos"]), "pos2": int(r["pos"]) + int(r["len"]), "props": m.get("props", {}),
+                     "type": ANNOTATE}
+                if m.get("combiningOp") is not None:
+                    a["combiningOp"] = m["combiningOp"]
+                out.append(a)
+    return out[0] if len(out) == 1 else {"ops": out, "type": GROUP}

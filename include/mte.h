@@ -87,6 +87,32 @@ extern "C" {
  * every view; a rolled-back remove restores its segments.  A rollback of an
  * annotate is MTE_E_UNSUPPORTED.  Only in MTE_DOC_LOCAL_CLIENT documents.    */
 #define MTE_OP_ROLLBACK 5
+/* Client.regeneratePendingOp for reconnection (client.ts:972-1002 ->
+ * resetPendingDeltaToOps :788-860): a local record with seq = the localSeq L of
+ * a pending op and pos1 = its type.  The document does not change; it reports,
+ * as MTE_DELTA_REGEN | type delta records, one per segment of L's segment group
+ * in document order, the op that re-sends that segment: its position in the
+ * view at localSeq L (findReconnectionPosition :709-713 -> localNetLength with
+ * localSeq, mergeTree.ts:575-593: acked text plus own pending inserts up to L,
+ * minus acked removals and own pending removals up to L) and its cachedLength.
+ *   insert: every segment L inserted (`removed` holds its text offset, whose
+ *     difference from the lowest of the group is the segment's offset in the
+ *     op's text);
+ *   remove: every segment L removes that no remote remove overtook;
+ *   annotate: every segment L visited (a = the annotate's group slot, see
+ *     MTE_OP_ANNOTATE below) that is not removed, or only by a pending local
+ *     remove.
+ * The host re-sends the ops and keeps the group pending under the same L
+ * (acked by MTE_OP_ACK as before).  Only in MTE_DOC_LOCAL_CLIENT documents
+ * that record events (MTE_DOC_EVENTS).                                       */
+#define MTE_OP_REGEN 6
+#define MTE_DELTA_REGEN 0x10u
+/* Segment groups of pending local annotates (mergeTree.ts:1874-1880): a local
+ * annotate record with b = a slot 0..31 marks every segment it visits with
+ * that slot (MTE_NO_PROPS: not tracked); an MTE_OP_ACK record's a is the mask
+ * of the slots its groups free.  At most 32 tracked annotates are pending at
+ * once per document (the host assigns the slots).                           */
+#define MTE_ANNOTATE_SLOTS 32
 
 #define MTE_F_MARKER 0x0001u  /* insert spec {marker:{refType}} (mergeTreeNodes.ts:602-609) */
 #define MTE_F_MSG_END 0x0002u /* last record of its message: window update follows      */
@@ -305,7 +331,8 @@ typedef struct mte_delta {
   int32_t pos;
   int32_t len;
   uint32_t removed; /* 1: the segment is removed in the doc's own view (an
-                       annotate of text another client removed since)      */
+                       annotate of text another client removed since);
+                       MTE_DELTA_REGEN | INSERT records: the text offset    */
 } mte_delta;
 /* Events of the last mte_run for an MTE_DOC_EVENTS doc (query-size-then-fill:
  * *n gets the count; up to cap are copied).  MTE_E_CAPACITY when the doc

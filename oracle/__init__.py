@@ -144,6 +144,9 @@ class OracleEngine(EngineBase):
     def _read_deltas(self, doc, p, cap, np_):
         return self.lib.orc_read_deltas(self.ctx, doc, p, cap, np_)
 
+    def set_event_capacity(self, per_op):
+        """The restatement's event buffers grow as needed (mte_set_event_capacity's bound is the engine's)."""
+
     def _digest(self, p, n):
         return self.f.digest(self.ctx, p, n)
 

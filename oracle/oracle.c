@@ -91,7 +91,11 @@ static int arena_append(orc_ctx* c, const uint16_t* t, uint64_t n, uint64_t* bas
   return MTE_OK;
 }
 
-#define PK(d, i) ((d)->pk + (size_t)(i) * MTE_MAX_KEYS)
+/* a pk row: MTE_MAX_KEYS pending-key localSeqs, then the mask of the pending
+ * annotate groups (MTE_ANNOTATE_SLOTS) the segment belongs to */
+#define PKW (MTE_MAX_KEYS + 1)
+#define PK(d, i) ((d)->pk + (size_t)(i) * PKW)
+#define AM(d, i) (PK(d, i)[MTE_MAX_KEYS])
 
 static int doc_reserve(odoc* d, uint32_t need) {
   if (need <= d->cap) return MTE_OK;
@@ -101,7 +105,7 @@ static int doc_reserve(odoc* d, uint32_t need) {
   if (!s) return MTE_E_OOM;
   d->s = s;
   if (d->flags & MTE_DOC_LOCAL_CLIENT) {
-    uint32_t* pk = (uint32_t*)realloc(d->pk, (size_t)nc * MTE_MAX_KEYS * sizeof(uint32_t));
+    uint32_t* pk = (uint32_t*)realloc(d->pk, (size_t)nc * PKW * sizeof(uint32_t));
     if (!pk) return MTE_E_OOM;
     d->pk = pk;
   }
@@ -128,8 +132,8 @@ static int doc_open(odoc* d, uint32_t at, uint32_t cnt) {
   if (rc) return rc;
   memmove(d->s + at + cnt, d->s + at, (size_t)(d->n - at) * sizeof(oseg));
   if (d->pk) {
-    memmove(PK(d, at + cnt), PK(d, at), (size_t)(d->n - at) * MTE_MAX_KEYS * sizeof(uint32_t));
-    memset(PK(d, at), 0, (size_t)cnt * MTE_MAX_KEYS * sizeof(uint32_t));
+    memmove(PK(d, at + cnt), PK(d, at), (size_t)(d->n - at) * PKW * sizeof(uint32_t));
+    memset(PK(d, at), 0, (size_t)cnt * PKW * sizeof(uint32_t));
   }
   d->n += cnt;
   return MTE_OK;
@@ -200,7 +204,7 @@ static int64_t doc_split_at(odoc* d, int64_t pos, uint64_t* written) {
       *tail = *head;
       /* the tail keeps the pending key counts (copyPropertiesTo,
        * mergeTreeNodes.ts:505-534 -> PropertiesManager.copyTo) */
-      if (d->pk) memcpy(PK(d, i + 1), PK(d, i), MTE_MAX_KEYS * sizeof(uint32_t));
+      if (d->pk) memcpy(PK(d, i + 1), PK(d, i), PKW * sizeof(uint32_t));
       tail->len = head->len - (int32_t)off;
       tail->toff = head->toff + (uint32_t)off;
       head->len = (int32_t)off;
@@ -238,7 +242,7 @@ static void doc_compact(odoc* d) {
     if (d->s[i].rseq != NONE_SEQ && d->s[i].rseq <= d->min_seq) continue;
     if (w != i) {
       d->s[w] = d->s[i];
-      if (d->pk) memcpy(PK(d, w), PK(d, i), MTE_MAX_KEYS * sizeof(uint32_t));
+      if (d->pk) memcpy(PK(d, w), PK(d, i), PKW * sizeof(uint32_t));
     }
     w++;
   }
@@ -310,6 +314,7 @@ static int64_t doc_lengths_local(odoc* d) {
 }
 
 static int doc_rollback(odoc* d, const mte_op* op);
+static int doc_regen(odoc* d, const mte_op* op);
 
 /* A local op (MTE_F_LOCAL, include/mte.h): insertSegmentLocal /
  * removeRangeLocal / annotateRangeLocal (client.ts:131-229) with seq =
@@ -327,6 +332,7 @@ static int doc_apply_local(odoc* d, const mte_op* op, const apply_env* env) {
   const int32_t ls = op->seq;
   int rc;
   if (op->type == MTE_OP_ROLLBACK) return doc_rollback(d, op);
+  if (op->type == MTE_OP_REGEN) return doc_regen(d, op);
   if (!(ls > d->local_seq && ls < LOCAL_BASE)) return MTE_E_INVALID_ARG;
   if (op->client != 0) return MTE_E_INVALID_ARG;
   if (op->type == MTE_OP_ANNOTATE && (op->flags & MTE_F_REWRITE)) return MTE_E_UNSUPPORTED;
@@ -395,6 +401,8 @@ static int doc_apply_local(odoc* d, const mte_op* op, const apply_env* env) {
         const mte_prop* p = &env->b->props[ps->first + j];
         if (p->key < env->n_keys) PK(d, i)[p->key] = (uint32_t)ls;
       }
+      /* the segment joins the annotate's segment group (addToPendingList) */
+      if (op->b != MTE_NO_PROPS) AM(d, i) |= 1u << op->b;
     }
     d->written += 1;
   }
@@ -433,6 +441,51 @@ static int doc_rollback(odoc* d, const mte_op* op) {
   return MTE_OK;
 }
 
+/* The length of a segment in the local client's view at localSeq ls
+ * (localNetLength with localSeq and refSeq = currentSeq, mergeTree.ts:575-593):
+ * an own pending insert after ls is not there yet, an own pending removal up to
+ * ls is; a sequenced removal always is (removedSeq <= currentSeq). */
+static inline int32_t len_at_local_seq(const oseg* g, int32_t ls) {
+  if (is_pending(g->seq) && g->seq - LOCAL_BASE > ls) return 0;
+  if (g->rseq != NONE_SEQ && (!is_pending(g->rseq) || g->rseq - LOCAL_BASE <= ls)) return 0;
+  return g->len;
+}
+
+/* MTE_OP_REGEN (a local record): Client.regeneratePendingOp of the pending op
+ * of localSeq op->seq, type op->pos1 (client.ts:972-1002 ->
+ * resetPendingDeltaToOps :788-860).  Its segment group, sorted by ordinal
+ * (document order), each at findReconnectionPosition (:709-713) -- the view at
+ * that localSeq -- with its cachedLength, as MTE_DELTA_REGEN | type records:
+ *   insert: every segment the op inserted (the record's removed field: its
+ *     text offset);
+ *   remove: only while the removal is still pending (a remote remove that
+ *     overtook it leaves nothing to send, :839-845);
+ *   annotate: the segments of group slot op->a not removed, or removed only by
+ *     a pending local remove (:809-823).
+ * The document itself does not change. */
+static int doc_regen(odoc* d, const mte_op* op) {
+  const int32_t ls = op->seq;
+  const uint32_t t = (uint32_t)op->pos1;
+  int rc;
+  if (!(ls > 0 && ls <= d->local_seq)) return MTE_E_INVALID_ARG;
+  if (t != MTE_OP_INSERT && t != MTE_OP_REMOVE && t != MTE_OP_ANNOTATE) return MTE_E_INVALID_ARG;
+  if (t == MTE_OP_ANNOTATE && op->a >= MTE_ANNOTATE_SLOTS) return MTE_E_INVALID_ARG;
+  if (!(d->flags & MTE_DOC_EVENTS)) return MTE_E_UNSUPPORTED;
+  d->ops++;
+  d->scanned += d->n;
+  int64_t p = 0;
+  for (uint32_t i = 0; i < d->n; i++) {
+    const oseg* g = &d->s[i];
+    int hit;
+    if (t == MTE_OP_INSERT) hit = g->seq == LOCAL_BASE + ls;
+    else if (t == MTE_OP_REMOVE) hit = g->rseq == LOCAL_BASE + ls;
+    else hit = ((AM(d, i) >> op->a) & 1u) && (g->rseq == NONE_SEQ || is_pending(g->rseq));
+    if (hit && (rc = delta_push(d, MTE_DELTA_REGEN | t, p, g->len, t == MTE_OP_INSERT ? g->toff : 0u))) return rc;
+    p += len_at_local_seq(g, ls);
+  }
+  return MTE_OK;
+}
+
 /* MTE_OP_ACK: ackPendingSegment for the groups of localSeq pos1..pos2
  * (mergeTree.ts:1278-1331, BaseSegment.ack mergeTreeNodes.ts:475-503): a
  * pending insert takes the seq, a pending removal too unless a remote remove
@@ -448,6 +501,7 @@ static int doc_ack(odoc* d, const mte_op* op) {
     uint32_t* pk = PK(d, i);
     for (uint32_t k = 0; k < MTE_MAX_KEYS; k++)
       if (pk[k] && pk[k] <= (uint32_t)hi) pk[k] = 0;
+    pk[MTE_MAX_KEYS] &= ~op->a; /* the acked annotates' groups */
   }
   return MTE_OK;
 }
@@ -670,7 +724,7 @@ int orc_load_docs(orc_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
       g->cli = -1;  /* LocalClientId */
       g->rseq = NONE_SEQ;
       g->toff = (uint32_t)(base + in->text_off);
-      if (d->pk) memset(PK(d, 0), 0, MTE_MAX_KEYS * sizeof(uint32_t));
+      if (d->pk) memset(PK(d, 0), 0, PKW * sizeof(uint32_t));
       if (in->propset != MTE_NO_PROPS) {
         if (in->propset >= n_propsets) return MTE_E_INVALID_ARG;
         orc_apply_props(g->props, c->n_keys, &propsets[in->propset], props, 0);
@@ -703,7 +757,7 @@ int orc_load_segments(orc_ctx* c, const uint64_t* seg_offsets, const mte_seg* se
         return MTE_E_INVALID_ARG;
       oseg* g = &d->s[k - b];
       memset(g, 0, sizeof(*g));
-      if (d->pk) memset(PK(d, k - b), 0, MTE_MAX_KEYS * sizeof(uint32_t));
+      if (d->pk) memset(PK(d, k - b), 0, PKW * sizeof(uint32_t));
       g->len = (int32_t)sg->len;
       g->seq = sg->seq;
       g->cli = sg->client;
@@ -782,8 +836,11 @@ int orc_apply_batch(orc_ctx* c, const mte_batch* b, int n_threads) {
     while (dcur + 1 < b->n_docs && b->op_offsets[dcur + 1] <= k) dcur++;
     /* local records (as mte_submit validates them) */
     const int local_doc = (c->docs[dcur].flags & MTE_DOC_LOCAL_CLIENT) != 0;
-    if (op->type > MTE_OP_ROLLBACK) return MTE_E_INVALID_ARG;
-    if (op->type == MTE_OP_ROLLBACK && !(op->flags & MTE_F_LOCAL)) return MTE_E_INVALID_ARG;
+    if (op->type > MTE_OP_REGEN) return MTE_E_INVALID_ARG;
+    if (op->type >= MTE_OP_ROLLBACK && !(op->flags & MTE_F_LOCAL)) return MTE_E_INVALID_ARG;
+    if ((op->flags & MTE_F_LOCAL) && op->type == MTE_OP_ANNOTATE && op->b != MTE_NO_PROPS &&
+        op->b >= MTE_ANNOTATE_SLOTS)
+      return MTE_E_INVALID_ARG;
     if ((op->flags & MTE_F_LOCAL) || op->type == MTE_OP_ACK) {
       if (!local_doc) return MTE_E_INVALID_ARG;
       if ((op->flags & MTE_F_LOCAL) && (op->type == MTE_OP_ACK || op->seq <= 0 || op->seq >= MTE_LOCAL_SEQ_BASE))

@@ -20,7 +20,13 @@
 //                    "nCheckpoints": int, "maxText": int, "rollback": p}]}
 //         (rollback: the chance that a local insert / remove is rolled back
 //         instead of sent; the event is ["R", op]: the client made the op
-//         locally, then rolled it back)
+//         locally, then rolled it back.
+//          reconnect: the chance per step that a sending client goes offline,
+//         or, when offline, reconnects.  Offline, its local ops are held
+//         (["H", op]); reconnecting, it catches up with the whole log, then
+//         re-sends every held op through Client.regeneratePendingOp
+//         (client.ts:972-1002), as test/client.reconnectFarm.spec.ts:25-59
+//         does: ["G", logIndex], the log entry holding the regenerated op)
 // stdout: {"sets": [{..params, "names": [...], "log": [[clientId, seq, ref, msn, "op", contents]],
 //                    "events": [[["L"|"A", logIndex] | ["R", op], ...] per client],
 //                    "checkpoints": [{"done": [events applied per client],
@@ -100,6 +106,8 @@ function runSet(p) {
     return c;
   });
   const cursor = names.map(() => 0);
+  const offline = names.map(() => false);
+  const held = names.map(() => []);  // [op, segment group] per held op
   const events = names.map(() => []);
   const log = [];
   let seq = 0;
@@ -115,12 +123,30 @@ function runSet(p) {
     events[i].push(["A", cursor[i]]);
     cursor[i]++;
   };
+  const reconnect = (i) => {
+    const c = clients[i];
+    while (cursor[i] < log.length) applyNext(i);  // every op it sent is acked
+    for (const [op, sg] of held[i]) {
+      const regen = c.regeneratePendingOp(op, sg);
+      let msn = Infinity;
+      for (const x of clients) msn = Math.min(msn, x.getCurrentSeq());
+      seq++;
+      log.push([names[i], seq, c.getCurrentSeq(), msn, "op", JSON.parse(JSON.stringify(regen))]);
+      events[i].push(["G", log.length - 1]);
+    }
+    held[i] = [];
+    offline[i] = false;
+  };
   const checkpoint = () => {
     checkpoints.push({ done: events.map((e) => e.length), states: clients.map(readOut) });
   };
 
   for (let step = 0; step < p.steps; step++) {
-    if (R.next() < 0.55) {
+    if (p.reconnect && R.next() < p.reconnect) {
+      const i = R.int(1, p.clients - 1);
+      if (offline[i]) reconnect(i);
+      else offline[i] = true;
+    } else if (R.next() < 0.55) {
       // a local op of a sending client (client 0 only observes)
       const i = R.int(1, p.clients - 1);
       const c = clients[i];
@@ -150,7 +176,11 @@ function runSet(p) {
           op = c.annotateRangeLocal(start, end, props, undefined);
         }
       }
-      if (op && p.rollback && (p.rollbackInserts ? op.type !== 2 : op.type === 1) && R.next() < p.rollback) {
+      if (op && offline[i]) {
+        // made while offline: pending, not sent
+        events[i].push(["H", JSON.parse(JSON.stringify(op))]);
+        held[i].push([op, c.peekPendingSegmentGroups()]);
+      } else if (op && p.rollback && (p.rollbackInserts ? op.type !== 2 : op.type === 1) && R.next() < p.rollback) {
         // Client.rollback of the op just made (client.ts:396-398 ->
         // MergeTree.rollback, mergeTree.ts:2005-2083): it is never sent
         const opJson = JSON.parse(JSON.stringify(op));
@@ -171,15 +201,20 @@ function runSet(p) {
     }
     if ((step + 1) % every === 0 && step + 1 < p.steps) checkpoint();
   }
+  for (let i = 0; i < p.clients; i++) if (offline[i]) reconnect(i);
   for (let i = 0; i < p.clients; i++) while (cursor[i] < log.length) applyNext(i);
   checkpoint();
+  let diverged = null;  // allowDiverge: the clients' final documents differ (recorded, not thrown)
   const t0 = checkpoints[checkpoints.length - 1].states[0];
   for (const s of checkpoints[checkpoints.length - 1].states) {
     if (s.text !== t0.text || JSON.stringify(s.props) !== JSON.stringify(t0.props)) {
-      throw new Error(`seed ${p.seed}: the reference clients did not converge`);
+      const what = s.text !== t0.text ? `text ${JSON.stringify(s.text)} vs ${JSON.stringify(t0.text)}`
+        : `props ${JSON.stringify(s.props)} vs ${JSON.stringify(t0.props)}`;
+      if (!p.allowDiverge) throw new Error(`seed ${p.seed}: the reference clients did not converge: ${what}`);
+      diverged = what;
     }
   }
-  return Object.assign({}, p, { names, log, events, checkpoints });
+  return Object.assign({}, p, { names, log, events, checkpoints }, diverged ? { diverged } : {});
 }
 
 const input = JSON.parse(fs.readFileSync(0, "utf8"));

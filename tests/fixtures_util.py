@@ -184,28 +184,84 @@ def prop_runs(view, interner):
     return runs
 
 
-def replay_ref_farm(engine_factory, sets, n_keys=8):
+def canon_regen(op, orig):
+    """A regenerated op as compared with the reference's: an insert of a segment
+    whose original spec had no props carries, in the reference, the segment's
+    props at regeneration time (createInsertSegmentOp(pos, segment),
+    client.ts:828-836) -- the props of the op's own later annotates, which it
+    re-sends right after; those are dropped (the documents end up the same).
+    Adjacent ops that make one edit are merged (see merge).  Keys sorted."""
+    def one(o, src):
+        if o.get("type") == 0 and isinstance(src, dict) and src.get("type") == 0:
+            seg, sseg = o.get("seg"), src.get("seg")
+            no_props = isinstance(sseg, str) or (isinstance(sseg, dict) and sseg.get("props") is None)
+            if no_props and isinstance(seg, dict):
+                seg = {k: v for k, v in seg.items() if k != "props"}
+                if isinstance(sseg, str):
+                    seg = seg.get("text", seg)
+                o = dict(o, seg=seg)
+        return o
+
+    def merge(out, o):
+        # the same edit in fewer ops: the reference append-merges adjacent acked
+        # segments (zamboni, mergeTree.ts:681-747) that the flat state keeps apart,
+        # so its segment groups -- one op per segment -- can be coarser
+        q = out[-1] if out else None
+        if q is not None and q["type"] == o["type"]:
+            if o["type"] == 1 and o["pos1"] == q["pos1"]:
+                q["pos2"] += o["pos2"] - o["pos1"]
+                return
+            if o["type"] == 2 and o["pos1"] == q["pos2"] and o.get("props") == q.get("props") and \
+                    o.get("combiningOp") == q.get("combiningOp"):
+                q["pos2"] = o["pos2"]
+                return
+            if o["type"] == 0 and isinstance(o["seg"], str) and isinstance(q["seg"], str) and \
+                    o["pos1"] == q["pos1"] + len(q["seg"].encode("utf-16-le")) // 2:
+                q["seg"] += o["seg"]
+                return
+        out.append(dict(o))
+
+    srcs = orig.get("ops", [orig]) if orig.get("type") == 3 else [orig]
+    ops = op.get("ops", [op]) if op.get("type") == 3 else [op]
+    src = srcs[0] if len(srcs) == 1 else None
+    out = []
+    for o in ops:
+        merge(out, one(o, src))
+    return json.dumps(out, sort_keys=True)
+
+
+def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None):
     """Replay farms the reference ran (oracle/ref_farm.js -> tests/golden/
     farm_vectors.json.gz): one MTE_DOC_LOCAL_CLIENT document per client of every
     set (the observer "A" included), each fed its own events in order — "L" a
     local op, "A" a sequenced message (its own: an ack), "R" a local op made and
-    rolled back at once (Client.rollback) — in one batch per
-    checkpoint; text and per-position properties must equal the reference
-    client's at every checkpoint.  Returns (checkpoints_passed, failures)."""
-    from fluidframework_amd.abi import DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC
+    rolled back at once (Client.rollback), "H" a local op held while offline,
+    "G" the oldest pending op regenerated on reconnect (Client.regeneratePendingOp;
+    the engine's regenerated op must equal the reference's, which the log holds
+    and every client then applies) — in one batch per checkpoint; text and
+    per-position properties must equal the reference client's at every
+    checkpoint.  regen_checks (a list) collects one entry per "G" event compared.
+    Returns (checkpoints_passed, failures)."""
+    from fluidframework_amd.abi import DOC_EVENTS, DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC
+    from fluidframework_amd.packing import regen_ops
 
     layout = [(si, ci) for si, s in enumerate(sets) for ci in range(len(s["names"]))]
+    has_regen = any(e[0] == "G" for s in sets for ev in s["events"] for e in ev)
     inits, text = doc_inits([sets[si]["initialText"] for si, _ in layout],
-                            flags=DOC_NEW_LENGTH_CALC | DOC_LOCAL_CLIENT)
+                            flags=DOC_NEW_LENGTH_CALC | DOC_LOCAL_CLIENT | (DOC_EVENTS if has_regen else 0))
     interner = Interner(n_keys)
     eng = engine_factory(n_keys)
+    if has_regen:
+        eng.set_event_capacity(64)
     eng.load_docs(inits, text)
+    held = [[] for _ in layout]
     clients = [DocClients(sets[si]["names"][ci], local=True) for si, ci in layout]
     n_cp = max(len(s["checkpoints"]) for s in sets)
     prev = [0] * len(layout)
     passed, failures = 0, []
     for j in range(n_cp):
         bb = BatchBuilder(len(layout), interner)
+        regens = []  # (doc, add_regen result, original op, log index)
         for d, (si, ci) in enumerate(layout):
             s = sets[si]
             if j >= len(s["checkpoints"]):
@@ -216,6 +272,13 @@ def replay_ref_farm(engine_factory, sets, n_keys=8):
                     bb.add_local(d, clients[d], li)
                     bb.add_rollback(d, clients[d])
                     continue
+                if kind == "H":  # the op (li) made locally while offline
+                    bb.add_local(d, clients[d], li)
+                    held[d].append(li)
+                    continue
+                if kind == "G":
+                    regens.append((d, bb.add_regen(d, clients[d]), held[d].pop(0), li))
+                    continue
                 m = as_msg(s["log"][li])
                 if kind == "L":
                     bb.add_local(d, clients[d], m["contents"])
@@ -224,6 +287,17 @@ def replay_ref_farm(engine_factory, sets, n_keys=8):
             prev[d] = done
         eng.apply_batch(bb.build())
         st = eng.statuses()
+        for d, idx, orig, li in regens:
+            si, ci = layout[d]
+            if st[d] != 0:
+                continue
+            want_op = sets[si]["log"][li][5]
+            got_op = regen_ops(orig, idx, eng.read_deltas(d))
+            ok = canon_regen(got_op, orig) == canon_regen(want_op, orig)
+            if regen_checks is not None:
+                regen_checks.append(ok)
+            if not ok:
+                failures.append((si, ci, j, "regen", got_op, want_op))
         for d, (si, ci) in enumerate(layout):
             s = sets[si]
             if j >= len(s["checkpoints"]):

@@ -10,8 +10,10 @@ const zlib = require("zlib");
 const packing = require("../../fluidframework_amd/node/packing");
 const { asMsg } = require("./fixtures");
 
+// argv: the vectors file (farm_vectors.json.gz, or reconnect_vectors.json.gz:
+// ops held offline "H" and regeneratePendingOp "G" as MTE_OP_REGEN records)
 const sets = JSON.parse(zlib.gunzipSync(fs.readFileSync(path.join(__dirname, "..", "golden",
-  "farm_vectors.json.gz"))).toString("utf8")).sets;
+  process.argv[2] || "farm_vectors.json.gz"))).toString("utf8")).sets;
 const interner = new packing.Interner(8);
 const layout = [];
 sets.forEach((s, si) => s.names.forEach((name, ci) => layout.push([si, ci, new packing.DocClients(name, 0, true)])));
@@ -28,6 +30,14 @@ for (let j = 0; j < nCp; j++) {
       if (kind === "R") {  // made locally, then rolled back
         bb.addLocal(d, cl, li);
         bb.addRollback(d, cl);
+        continue;
+      }
+      if (kind === "H") {
+        bb.addLocal(d, cl, li);
+        continue;
+      }
+      if (kind === "G") {
+        bb.addRegen(d, cl);
         continue;
       }
       const m = asMsg(s.log[li]);

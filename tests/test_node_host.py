@@ -76,12 +76,14 @@ def test_js_packing_matches_python_packing_on_fixtures(fresh):
             assert base64.b64decode(j[key]) == np.ascontiguousarray(arr).tobytes(), (r, key)
 
 
-def test_js_packing_matches_python_packing_on_local_farms():
-    """Local ops and acks: the JS and Python packers emit the same bytes for
-    the reference farm vectors (tests/node/pack_farm.js)."""
+@pytest.mark.parametrize("vectors", ["farm_vectors.json.gz", "reconnect_vectors.json.gz"])
+def test_js_packing_matches_python_packing_on_local_farms(vectors):
+    """Local ops and acks (and, on the reconnect farms, ops held offline and
+    regeneratePendingOp's MTE_OP_REGEN records): the JS and Python packers emit
+    the same bytes for the reference farm vectors (tests/node/pack_farm.js)."""
     import gzip
-    lines = node("tests/node/pack_farm.js").splitlines()
-    with gzip.open(os.path.join(ROOT, "tests", "golden", "farm_vectors.json.gz"), "rt") as fh:
+    lines = node("tests/node/pack_farm.js", vectors).splitlines()
+    with gzip.open(os.path.join(ROOT, "tests", "golden", vectors), "rt") as fh:
         sets = json.load(fh)["sets"]
     interner = Interner(8)
     layout = [(si, ci, DocClients(name, local=True)) for si, s in enumerate(sets) for ci, name in enumerate(s["names"])]
@@ -98,6 +100,12 @@ def test_js_packing_matches_python_packing_on_local_farms():
                 if kind == "R":
                     bb.add_local(d, cl, li)
                     bb.add_rollback(d, cl)
+                    continue
+                if kind == "H":
+                    bb.add_local(d, cl, li)
+                    continue
+                if kind == "G":
+                    bb.add_regen(d, cl)
                     continue
                 m = as_msg(s["log"][li])
                 if kind == "L":
