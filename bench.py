@@ -151,6 +151,8 @@ def run_engine(stream, cap, device, steps, warmup, stats_on, barrier=lambda: Non
     from fluidframework_amd.engine import DeviceEngine
 
     eng = DeviceEngine(stream["n_keys"], device=device, seg_capacity=cap)
+    if stream.get("event_capacity"):
+        eng.set_event_capacity(stream["event_capacity"])
     gen.load_stream(eng, stream)
     eng.submit(stream["batch"])
 
@@ -215,6 +217,10 @@ def main():
     ap.add_argument("--no-tree-leg", action="store_true", help="skip the tree-placement side measurement")
     ap.add_argument("--no-weak-leg", action="store_true", help="skip the weak-scaling side measurement (N > 1)")
     ap.add_argument("--no-node-leg", action="store_true", help="skip the Node host end-to-end measurement")
+    ap.add_argument("--no-local-leg", action="store_true",
+                    help="skip the local-client side measurement (reference farms: local ops, acks, rollback, "
+                         "reconnect, delta events)")
+    ap.add_argument("--local-docs", type=int, default=10000, help="documents in the local-client side measurement")
     ap.add_argument("--node-docs", type=int, default=100, help="documents in the Node host sample")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -313,6 +319,12 @@ def main():
                     "note": "legacy-calc documents on the tree pass (reference B+tree placement, mte_tree.h)"}
         del rt, ts
 
+    # side measurement: documents with a local client (the 8(f) rows: local ops
+    # + acks, rollback, reconnect, delta events) on the HBM-streamed pass
+    local_leg = None
+    if not args.no_local_leg and world == 1:
+        local_leg = local_client_leg(args.local_docs, local_rank, max(1, args.steps // 2), threads)
+
     # side measurement at N > 1: weak scaling (every rank the config's docs)
     weak_leg = None
     if world > 1 and args.scaling == "strong" and not args.no_weak_leg:
@@ -390,6 +402,7 @@ def main():
                        "includes": "mte_submit (host->HBM op upload) + reset + replay + digest read-back, rank 0"},
         "end_to_end_node": node_e2e,
         "tree_placement": tree_leg,
+        "local_client": local_leg,
         "weak_scaling": weak_leg,
         "cpu_baseline": cpu,
         "cpu_baseline_reference": ref_cpu,
@@ -400,6 +413,108 @@ def main():
     print(json.dumps(out), flush=True)
     if node is not None:
         node.close()
+
+
+LOCAL_KEYS = 4  # the farms' property keys: client, bold, color, markerId
+
+
+def local_client_stream(n_docs):
+    """Documents whose own client sends, at bench scale: every client of the
+    farms the reference itself ran (tests/golden/farm_vectors.json.gz: local ops,
+    acks, lagging remote ops, rollbacks; reconnect_vectors.json.gz: ops held
+    offline and regeneratePendingOp) as one MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS
+    document with all its events in one batch, the set of documents repeated
+    to n_docs (copies share the property tables; text offsets shift).  Returns
+    (stream, base stream of the distinct documents, copies)."""
+    import gzip
+
+    from fluidframework_amd.abi import DOC_EVENTS, DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC, F_MARKER, OP_INSERT
+    from fluidframework_amd.packing import BatchBuilder, DocClients, Interner
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from fixtures_util import as_msg, doc_inits
+
+    sets = []
+    for name in ("farm_vectors.json.gz", "reconnect_vectors.json.gz"):
+        with gzip.open(os.path.join(ROOT, "tests", "golden", name), "rt", encoding="utf-8") as fh:
+            sets += json.load(fh)["sets"]
+    layout = [(si, ci) for si, st in enumerate(sets) for ci in range(len(st["names"]))]
+    inits, text = doc_inits([sets[si]["initialText"] for si, _ in layout],
+                            flags=DOC_NEW_LENGTH_CALC | DOC_LOCAL_CLIENT | DOC_EVENTS)
+    it = Interner(LOCAL_KEYS)
+    bb = BatchBuilder(len(layout), it)
+    for d, (si, ci) in enumerate(layout):
+        st, cl = sets[si], DocClients(sets[si]["names"][ci], local=True)
+        for kind, li in st["events"][ci]:
+            if kind == "R":
+                bb.add_local(d, cl, li)
+                bb.add_rollback(d, cl)
+            elif kind == "H":
+                bb.add_local(d, cl, li)
+            elif kind == "G":
+                bb.add_regen(d, cl)
+            elif kind == "L":
+                bb.add_local(d, cl, as_msg(st["log"][li])["contents"])
+            else:
+                bb.add_message(d, cl, as_msg(st["log"][li]))
+    base_batch = bb.build()
+    base = {"n_keys": LOCAL_KEYS, "inits": inits, "init_text": text, "batch": base_batch, "event_capacity": 64}
+    nb = len(layout)
+    copies = max(1, (n_docs + nb - 1) // nb)
+    ops, offs = base_batch["ops"], base_batch["op_offsets"].astype(np.int64)
+    tu, iu = len(base_batch["text"]), len(text)
+    shifted = []
+    txt_rec = (ops["type"] == OP_INSERT) & ((ops["flags"] & F_MARKER) == 0)
+    for c in range(copies):
+        o = ops.copy()
+        o["a"][txt_rec] += np.uint32(c * tu)
+        shifted.append(o)
+    all_ops = np.concatenate(shifted)
+    cnt = offs[1:] - offs[:-1]
+    # document order: copy-major, each copy's documents in base order
+    all_offs = np.zeros(nb * copies + 1, np.uint64)
+    all_offs[1:] = np.cumsum(np.tile(cnt, copies))
+    # each copy's records are contiguous in all_ops in base-doc order: the same order
+    all_inits = np.concatenate([inits] * copies)
+    for c in range(copies):
+        all_inits["text_off"][c * nb:(c + 1) * nb] += np.uint32(c * iu)
+    batch = dict(base_batch, ops=all_ops, op_offsets=all_offs, text=np.tile(base_batch["text"], copies))
+    stream = {"n_keys": LOCAL_KEYS, "inits": all_inits, "init_text": np.tile(text, copies), "batch": batch,
+              "event_capacity": 64}
+    return stream, base, copies
+
+
+def local_client_leg(n_docs, device, steps, threads):
+    """The local-client side line: replay rate of local_client_stream on the
+    GPU (HIP-event kernel time, algorithmic bytes as the headline's), every
+    copy's digest equal to the flat restatement's for its base document, and
+    the restatement's own rate on the base documents (kind "port")."""
+    from oracle import OracleEngine
+    t0 = time.time()
+    stream, base, copies = local_client_stream(n_docs)
+    build_s = time.time() - t0
+    r = run_engine(stream, 0, device, steps, 1, False)
+    nb = len(base["inits"])
+    n_ops = int(stream["batch"]["op_offsets"][-1])
+    o = OracleEngine(LOCAL_KEYS, threads=threads)
+    o.load_docs(base["inits"], base["init_text"])
+    tc = time.perf_counter()
+    o.apply_batch(base["batch"])
+    cpu_s = time.perf_counter() - tc
+    od = o.digest()
+    equal = bool((o.statuses() == 0).all() and all(np.array_equal(r["digest"][c * nb:(c + 1) * nb], od)
+                                                   for c in range(copies)))
+    kms = float(np.mean(r["kernel_ms"]))
+    gbs = r["stats"]["algo_bytes"] / (kms * 1e-3) / 1e9
+    ms = r["elapsed"] * 1000.0 / steps
+    base_ops = int(base["batch"]["op_offsets"][-1])
+    return {"docs": int(len(stream["inits"])), "distinct_docs": nb, "ops": n_ops, "ms_per_step": ms,
+            "ops_per_s": n_ops / (ms * 1e-3), "kernel_ms": kms, "first_run_kernel_ms": r["first_ms"],
+            "achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS, "digest_equal_restatement": equal,
+            "cpu_port": {"ops_per_s": base_ops / cpu_s, "cores": threads, "ops": base_ops},
+            "build_s": round(build_s, 1),
+            "note": ("every client of the 76 farm + 35 reconnect farm sets the reference ran (local ops, acks, "
+                     "rollbacks, regeneratePendingOp, lagging remote ops), MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS, "
+                     "repeated to the doc count; HBM-streamed pass (mte_stream.h)")}
 
 
 def node_end_to_end(stream, gpu_digest, n_docs):

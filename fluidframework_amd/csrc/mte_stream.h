@@ -29,6 +29,11 @@ constexpr int kTile = kWave * kTileE;  // slots per tile
 __device__ __forceinline__ uint32_t ld_l2(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// plane p, slot i of a doc's planes as a 32-bit offset from the doc's base
+// (global_load saddr + voffset: no 64-bit address per lane and plane)
+__device__ __forceinline__ uint32_t ld_l2o(const uint32_t* pl, uint32_t off) {
+  return __hip_atomic_load(pl + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Every slot index this path computes is checked against the doc's capacity
@@ -66,6 +71,7 @@ __device__ __forceinline__ void tile_load_hot(Regs<kTileE, K>& R, const uint32_t
 constexpr int32_t kLocalBase = MTE_LOCAL_SEQ_BASE;
 template <int K>
 constexpr int kAnnPlane = kFieldPlanes + 2 * K;
+constexpr int kPlaneGroup = 3;  // planes moved per batch of loads (all in flight, then the stores)
 
 // the local client's own view (localNetLength, mergeTree.ts:553-573, new
 // length calculation): removed -> 0, else the length; padding undefined
@@ -99,27 +105,31 @@ template <int K>
 __device__ __forceinline__ void stream_ack(uint32_t* pl, uint64_t sd, int n, int32_t lo, int32_t hi, int32_t s,
                                            uint32_t ann_mask) {
   const int l = lane_id();
+  // per tile: every load first (all in flight at once), then the stores
   for (int tb = 0; tb < n; tb += kTile) {
+    int32_t sr[2][kTileE];
+    uint32_t pk[K > 0 ? K : 1][kTileE], am[kTileE];
+#pragma unroll
+    for (int j = 0; j < kTileE; j++) {
+      const int i = tb + l * kTileE + j;
+      const bool v = i < n;
+#pragma unroll
+      for (int p = 0; p < 2; p++) sr[p][j] = v ? (int32_t)ld_l2(pl + (p + 1) * sd + i) : 0;  // seq, removedSeq
+#pragma unroll
+      for (int kk = 0; kk < K; kk++) pk[kk][j] = v ? ld_l2(pl + (uint64_t)(kFieldPlanes + K + kk) * sd + i) : 0u;
+      am[j] = (v && ann_mask) ? ld_l2(pl + (uint64_t)kAnnPlane<K> * sd + i) : 0u;
+    }
 #pragma unroll
     for (int j = 0; j < kTileE; j++) {
       const int i = tb + l * kTileE + j;
       if (i >= n) continue;
 #pragma unroll
-      for (int p = 1; p <= 2; p++) {  // seq, removedSeq
-        const int32_t v = (int32_t)ld_l2(pl + p * sd + i);
-        if (v >= kLocalBase + lo && v <= kLocalBase + hi) pl[p * sd + i] = (uint32_t)s;
-      }
+      for (int p = 0; p < 2; p++)
+        if (sr[p][j] >= kLocalBase + lo && sr[p][j] <= kLocalBase + hi) pl[(p + 1) * sd + i] = (uint32_t)s;
 #pragma unroll
-      for (int kk = 0; kk < K; kk++) {
-        uint32_t* q = pl + (uint64_t)(kFieldPlanes + K + kk) * sd + i;
-        const uint32_t v = ld_l2(q);
-        if (v != 0u && v <= (uint32_t)hi) *q = 0u;
-      }
-      if (ann_mask) {  // the acked annotates' segment groups
-        uint32_t* q = pl + (uint64_t)kAnnPlane<K> * sd + i;
-        const uint32_t v = ld_l2(q);
-        if (v & ann_mask) *q = v & ~ann_mask;
-      }
+      for (int kk = 0; kk < K; kk++)
+        if (pk[kk][j] != 0u && pk[kk][j] <= (uint32_t)hi) pl[(uint64_t)(kFieldPlanes + K + kk) * sd + i] = 0u;
+      if (am[j] & ann_mask) pl[(uint64_t)kAnnPlane<K> * sd + i] = am[j] & ~ann_mask;  // the acked groups
     }
   }
   vm_drain();
@@ -431,27 +441,39 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
     // ---- B: shift back to front, then patches and the new segment --------------
     if (t1 != INT32_MAX) {
       const int lo = t1 + 1;
+      // back to front: a tile's sources lie in it or the tile below, which is
+      // moved later, so a tile's planes move kPlaneGroup at a time: their loads
+      // all in flight at once, then their stores
       for (int tb = ((n - 1) / kTile) * kTile; tb + kTile > lo; tb -= kTile) {
         const int base = tb + l * E;
-        for (int p = 0; p < nplanes; p++) {
-          uint32_t* q = pl + (uint64_t)p * sd;
-          uint32_t v[E];
+#pragma nounroll
+        for (int p0 = 0; p0 < nplanes; p0 += kPlaneGroup) {
+          uint32_t v[kPlaneGroup][E];
 #pragma unroll
-          for (int j = 0; j < E; j++) {
-            const int i = base + j;
-            const int src = i - ((i > t1 ? 1 : 0) + (i > t2 ? 1 : 0));
-            // src is -1 only for the new segment's slot 0 (t1 == -1), which the
-            // new-segment stores below overwrite: never read before the doc
-            v[j] = (i < n && i >= lo && MTE_SLOT_OK(src, a.cap)) ? ld_l2(q + src) : 0u;
+          for (int g = 0; g < kPlaneGroup; g++) {
+            const uint32_t pb = (uint32_t)((uint64_t)(p0 + g) * sd);
+#pragma unroll
+            for (int j = 0; j < E; j++) {
+              const int i = base + j;
+              const int src = i - ((i > t1 ? 1 : 0) + (i > t2 ? 1 : 0));
+              // src is -1 only for the new segment's slot 0 (t1 == -1), which the
+              // new-segment stores below overwrite: never read before the doc
+              v[g][j] = (p0 + g < nplanes && i < n && i >= lo && MTE_SLOT_OK(src, a.cap))
+                            ? ld_l2o(pl, pb + (uint32_t)src) : 0u;
+            }
           }
 #pragma unroll
-          for (int j = 0; j < E; j++) {
-            const int i = base + j;
-            if (i < n && i >= lo && MTE_SLOT_OK(i, a.cap)) q[i] = v[j];
+          for (int g = 0; g < kPlaneGroup; g++) {
+            const uint32_t pb = (uint32_t)((uint64_t)(p0 + g) * sd);
+#pragma unroll
+            for (int j = 0; j < E; j++) {
+              const int i = base + j;
+              if (p0 + g < nplanes && i < n && i >= lo && MTE_SLOT_OK(i, a.cap)) pl[pb + (uint32_t)i] = v[g][j];
+            }
           }
         }
-        vm_drain();
       }
+      vm_drain();
     }
     if ((pa.h >= 0 && !(MTE_SLOT_OK(pa.h, a.cap) && MTE_SLOT_OK(pa.tl, a.cap))) ||
         (pb.h >= 0 && !(MTE_SLOT_OK(pb.h, a.cap) && MTE_SLOT_OK(pb.tl, a.cap))) || (g >= 0 && !MTE_SLOT_OK(g, a.cap)))
@@ -559,13 +581,13 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
         const int base = tb + l * E;
         if (lop && type == MTE_OP_ANNOTATE && (uint32_t)op[7] < MTE_ANNOTATE_SLOTS) {
           // the visited slots join the annotate's segment group (mergeTree.ts:1874-1880)
+          uint32_t* q = pl + (uint64_t)kAnnPlane<K> * sd + base;
+          uint32_t gm[E];
 #pragma unroll
-          for (int j = 0; j < E; j++) {
-            if (in[j]) {
-              uint32_t* q = pl + (uint64_t)kAnnPlane<K> * sd + base + j;
-              *q = ld_l2(q) | (1u << (uint32_t)op[7]);
-            }
-          }
+          for (int j = 0; j < E; j++) gm[j] = in[j] ? ld_l2(q + j) : 0u;
+#pragma unroll
+          for (int j = 0; j < E; j++)
+            if (in[j]) q[j] = gm[j] | (1u << (uint32_t)op[7]);
         }
         if (rem) {
           // markRemoved (mergeTree.ts:1924-1962)
@@ -665,16 +687,27 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
         const int32_t tot = rdlane(incl, kWave - 1);
         if (tot != kTile || w != tb) {
           int32_t dst = w + incl - cntl;
-          for (int p = 0; p < nplanes; p++) {
-            uint32_t* q = pl + (uint64_t)p * sd;
-            uint32_t v[E];
+          // kPlaneGroup planes' loads in flight at once, then their stores (dst
+          // <= src: a tile's stores land at or below it, after its own loads)
+  #pragma nounroll
+        for (int p0 = 0; p0 < nplanes; p0 += kPlaneGroup) {
+            uint32_t v[kPlaneGroup][E];
 #pragma unroll
-            for (int j = 0; j < E; j++) v[j] = keep[j] ? ld_l2(q + base + j) : 0u;
-            int32_t d0 = dst;
+            for (int g = 0; g < kPlaneGroup; g++) {
+              const uint32_t pb = (uint32_t)((uint64_t)(p0 + g) * sd);
 #pragma unroll
-            for (int j = 0; j < E; j++) {
-              if (keep[j] && MTE_SLOT_OK(d0, a.cap)) q[d0] = v[j];
-              d0 += keep[j] ? 1 : 0;
+              for (int j = 0; j < E; j++)
+                v[g][j] = (p0 + g < nplanes && keep[j]) ? ld_l2o(pl, pb + (uint32_t)(base + j)) : 0u;
+            }
+#pragma unroll
+            for (int g = 0; g < kPlaneGroup; g++) {
+              const uint32_t pb = (uint32_t)((uint64_t)(p0 + g) * sd);
+              int32_t d0 = dst;
+#pragma unroll
+              for (int j = 0; j < E; j++) {
+                if (p0 + g < nplanes && keep[j] && MTE_SLOT_OK(d0, a.cap)) pl[pb + (uint32_t)d0] = v[g][j];
+                d0 += keep[j] ? 1 : 0;
+              }
             }
           }
           vm_drain();

@@ -235,3 +235,22 @@ def test_js_regen_ops_match_python():
     got = json.loads(r.stdout)
     for g, c in zip(got, cases):
         assert json.dumps(g, sort_keys=True) == json.dumps(c["want"], sort_keys=True), c
+
+
+def test_bench_local_client_stream_copies_replay_alike():
+    """bench.py's local-client side line: the farm documents repeated with
+    shifted text offsets replay to the same state in every copy (the
+    restatement on two copies), with no error status."""
+    import sys
+    sys.path.insert(0, os.path.dirname(HERE))
+    import numpy as np
+
+    import bench
+    st, base, copies = bench.local_client_stream(2 * 506)
+    assert copies == 2 and len(st["inits"]) == 2 * len(base["inits"])
+    o = oracle_factory(st["n_keys"])
+    o.load_docs(st["inits"], st["init_text"])
+    o.apply_batch(st["batch"])
+    assert (o.statuses() == 0).all()
+    d, nb = o.digest(), len(base["inits"])
+    assert np.array_equal(d[:nb], d[nb:])
