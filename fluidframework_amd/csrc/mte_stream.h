@@ -49,13 +49,17 @@ __device__ __forceinline__ void tile_load_hot(Regs<kTileE, K>& R, const uint32_t
   for (int j = 0; j < kTileE; j++) {
     const int i = base + j;
     const bool v = i < n;
+    // unconditional loads (slot 0 stands in for padding), selected after:
+    // no branch around each load
     const uint32_t x = (uint32_t)(v ? i : 0);
-    R.len[j] = v ? (int32_t)ld_l2(pl + x) : 0;
-    R.seq[j] = v ? (int32_t)ld_l2(pl + st + x) : 0;
-    R.rseq[j] = v ? (int32_t)ld_l2(pl + 2 * st + x) : kPad;
-    R.rmask[j] = v ? ld_l2(pl + 3 * st + x) : 0u;
-    R.meta[j] = v ? ld_l2(pl + 4 * st + x) : 0u;
-    R.toff[j] = v ? ld_l2(pl + 5 * st + x) : 0u;
+    const uint32_t l0 = ld_l2(pl + x), l1 = ld_l2(pl + st + x), l2 = ld_l2(pl + 2 * st + x);
+    const uint32_t l3 = ld_l2(pl + 3 * st + x), l4 = ld_l2(pl + 4 * st + x), l5 = ld_l2(pl + 5 * st + x);
+    R.len[j] = v ? (int32_t)l0 : 0;
+    R.seq[j] = v ? (int32_t)l1 : 0;
+    R.rseq[j] = v ? (int32_t)l2 : kPad;
+    R.rmask[j] = v ? l3 : 0u;
+    R.meta[j] = v ? l4 : 0u;
+    R.toff[j] = v ? l5 : 0u;
   }
 }
 
@@ -113,11 +117,20 @@ __device__ __forceinline__ void stream_ack(uint32_t* pl, uint64_t sd, int n, int
     for (int j = 0; j < kTileE; j++) {
       const int i = tb + l * kTileE + j;
       const bool v = i < n;
+      // unconditional loads (padding reads slot 0), then selects
+      const int ic = v ? i : 0;
 #pragma unroll
-      for (int p = 0; p < 2; p++) sr[p][j] = v ? (int32_t)ld_l2(pl + (p + 1) * sd + i) : 0;  // seq, removedSeq
+      for (int p = 0; p < 2; p++) {  // seq, removedSeq
+        const int32_t x = (int32_t)ld_l2(pl + (p + 1) * sd + ic);
+        sr[p][j] = v ? x : 0;
+      }
 #pragma unroll
-      for (int kk = 0; kk < K; kk++) pk[kk][j] = v ? ld_l2(pl + (uint64_t)(kFieldPlanes + K + kk) * sd + i) : 0u;
-      am[j] = (v && ann_mask) ? ld_l2(pl + (uint64_t)kAnnPlane<K> * sd + i) : 0u;
+      for (int kk = 0; kk < K; kk++) {
+        const uint32_t x = ld_l2(pl + (uint64_t)(kFieldPlanes + K + kk) * sd + ic);
+        pk[kk][j] = v ? x : 0u;
+      }
+      const uint32_t xa = ld_l2(pl + (uint64_t)kAnnPlane<K> * sd + ic);
+      am[j] = (v && ann_mask) ? xa : 0u;
     }
 #pragma unroll
     for (int j = 0; j < kTileE; j++) {
@@ -155,7 +168,9 @@ __device__ __forceinline__ int32_t own_prefix(const uint32_t* pl, uint64_t sd, i
 #pragma unroll
     for (int j = 0; j < kTileE; j++) {
       const int i = tb + lane_id() * kTileE + j;
-      if (i < g) acc += (int32_t)ld_l2(pl + 2 * sd + i) == kNone ? (int32_t)ld_l2(pl + i) : 0;
+      const int ic = i < g ? i : 0;  // unconditional loads, selected after
+      const int32_t rs = (int32_t)ld_l2(pl + 2 * sd + ic), ln = (int32_t)ld_l2(pl + ic);
+      acc += (i < g && rs == kNone) ? ln : 0;
     }
   }
   return rdlane(wave_incl_scan(acc), kWave - 1);
@@ -176,9 +191,11 @@ __device__ __forceinline__ void stream_rollback(uint32_t* pl, uint64_t sd, int n
     for (int j = 0; j < kTileE; j++) {
       const int i = tb + l * kTileE + j;
       const bool v = i < n;
-      len[j] = v ? (int32_t)ld_l2(pl + i) : 0;
-      const int32_t sq = v ? (int32_t)ld_l2(pl + sd + i) : 0;
-      int32_t rs = v ? (int32_t)ld_l2(pl + 2 * sd + i) : kPad;
+      const int ic = v ? i : 0;  // unconditional loads, selected after
+      const int32_t l0 = (int32_t)ld_l2(pl + ic), l1 = (int32_t)ld_l2(pl + sd + ic), l2 = (int32_t)ld_l2(pl + 2 * sd + ic);
+      len[j] = v ? l0 : 0;
+      const int32_t sq = v ? l1 : 0;
+      int32_t rs = v ? l2 : kPad;
       hit[j] = v && (t == MTE_OP_INSERT ? sq == kLocalBase + ls : rs == kLocalBase + ls);
       if (hit[j]) {
         if (t == MTE_OP_INSERT) {
@@ -240,14 +257,17 @@ __device__ __forceinline__ void stream_regen(const uint32_t* pl, uint64_t sd, in
     for (int j = 0; j < kTileE; j++) {
       const int i = tb + l * kTileE + j;
       const bool v = i < n;
-      len[j] = v ? (int32_t)ld_l2(pl + i) : 0;
-      const int32_t sq = v ? (int32_t)ld_l2(pl + sd + i) : 0;
-      const int32_t rs = v ? (int32_t)ld_l2(pl + 2 * sd + i) : kPad;
-      tf[j] = v ? ld_l2(pl + 5 * sd + i) : 0u;
+      const int ic = v ? i : 0;  // unconditional loads, selected after
+      const int32_t l0 = (int32_t)ld_l2(pl + ic), l1 = (int32_t)ld_l2(pl + sd + ic), l2 = (int32_t)ld_l2(pl + 2 * sd + ic);
+      const uint32_t l5 = ld_l2(pl + 5 * sd + ic), am = ld_l2(pl + (uint64_t)kAnnPlane<K> * sd + ic);
+      len[j] = v ? l0 : 0;
+      const int32_t sq = v ? l1 : 0;
+      const int32_t rs = v ? l2 : kPad;
+      tf[j] = v ? l5 : 0u;
       const bool rp = rs >= kLocalBase && rs != kNone;  // a pending local removal
       if (t == MTE_OP_INSERT) hit[j] = v && sq == kLocalBase + ls;
       else if (t == MTE_OP_REMOVE) hit[j] = v && rs == kLocalBase + ls;
-      else hit[j] = v && ((ld_l2(pl + (uint64_t)kAnnPlane<K> * sd + i) >> slot) & 1u) && (rs == kNone || rp);
+      else hit[j] = v && ((am >> slot) & 1u) && (rs == kNone || rp);
       const bool later = sq >= kLocalBase && sq - kLocalBase > ls;  // inserted after ls
       const bool gone = rs != kNone && (!rp || rs - kLocalBase <= ls);
       LL[j] = (v && !later && !gone) ? len[j] : 0;
@@ -451,15 +471,18 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
           uint32_t v[kPlaneGroup][E];
 #pragma unroll
           for (int g = 0; g < kPlaneGroup; g++) {
-            const uint32_t pb = (uint32_t)((uint64_t)(p0 + g) * sd);
+            // unconditional loads from a valid plane and slot, selected after
+            const int pg = p0 + g < nplanes ? p0 + g : nplanes - 1;
+            const uint32_t pb = (uint32_t)((uint64_t)pg * sd);
 #pragma unroll
             for (int j = 0; j < E; j++) {
               const int i = base + j;
               const int src = i - ((i > t1 ? 1 : 0) + (i > t2 ? 1 : 0));
               // src is -1 only for the new segment's slot 0 (t1 == -1), which the
               // new-segment stores below overwrite: never read before the doc
-              v[g][j] = (p0 + g < nplanes && i < n && i >= lo && MTE_SLOT_OK(src, a.cap))
-                            ? ld_l2o(pl, pb + (uint32_t)src) : 0u;
+              const bool ok = p0 + g < nplanes && i < n && i >= lo && MTE_SLOT_OK(src, a.cap);
+              const uint32_t x = ld_l2o(pl, pb + (uint32_t)(ok ? src : 0));
+              v[g][j] = ok ? x : 0u;
             }
           }
 #pragma unroll
@@ -581,13 +604,13 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
         const int base = tb + l * E;
         if (lop && type == MTE_OP_ANNOTATE && (uint32_t)op[7] < MTE_ANNOTATE_SLOTS) {
           // the visited slots join the annotate's segment group (mergeTree.ts:1874-1880)
-          uint32_t* q = pl + (uint64_t)kAnnPlane<K> * sd + base;
+          uint32_t* q = pl + (uint64_t)kAnnPlane<K> * sd;
           uint32_t gm[E];
 #pragma unroll
-          for (int j = 0; j < E; j++) gm[j] = in[j] ? ld_l2(q + j) : 0u;
+          for (int j = 0; j < E; j++) gm[j] = ld_l2(q + (in[j] ? base + j : 0));  // only in[] slots are stored
 #pragma unroll
           for (int j = 0; j < E; j++)
-            if (in[j]) q[j] = gm[j] | (1u << (uint32_t)op[7]);
+            if (in[j]) q[base + j] = gm[j] | (1u << (uint32_t)op[7]);
         }
         if (rem) {
           // markRemoved (mergeTree.ts:1924-1962)
@@ -604,24 +627,33 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
           }
         } else if (K > 0) {
           // PropertiesManager.addProperties (segmentPropertiesManager.ts:63-151)
-          uint32_t pr[K > 0 ? K : 1][E];
+          // loads unconditional (padding reads slot 0), padding selected away
+          // after: no branch per load
+          uint32_t pr[K > 0 ? K : 1][E], old[K > 0 ? K : 1][E], pk[K > 0 ? K : 1][E];
 #pragma unroll
           for (int kk = 0; kk < K; kk++)
 #pragma unroll
             for (int j = 0; j < E; j++) {
               const int i = base + j;
-              pr[kk][j] = i < n ? ld_l2(pl + (kFieldPlanes + kk) * sd + i) : 0u;
-              if (flags & MTE_F_REWRITE) pr[kk][j] = in[j] ? 0u : pr[kk][j];
+              const uint32_t o = ld_l2(pl + (kFieldPlanes + kk) * sd + (i < n ? i : 0));
+              old[kk][j] = i < n ? o : 0u;
+              pr[kk][j] = ((flags & MTE_F_REWRITE) && in[j]) ? 0u : old[kk][j];
             }
-          uint32_t old[K > 0 ? K : 1][E], pk[K > 0 ? K : 1][E];
+          if (ldoc) {
 #pragma unroll
-          for (int kk = 0; kk < K; kk++)
+            for (int kk = 0; kk < K; kk++)
 #pragma unroll
-            for (int j = 0; j < E; j++) {
-              const int i = base + j;
-              old[kk][j] = i < n ? ld_l2(pl + (kFieldPlanes + kk) * sd + i) : 0u;
-              pk[kk][j] = (ldoc && i < n) ? ld_l2(pl + (kFieldPlanes + K + kk) * sd + i) : 0u;
-            }
+              for (int j = 0; j < E; j++) {
+                const int i = base + j;
+                const uint32_t q = ld_l2(pl + (kFieldPlanes + K + kk) * sd + (i < n ? i : 0));
+                pk[kk][j] = i < n ? q : 0u;
+              }
+          } else {
+#pragma unroll
+            for (int kk = 0; kk < K; kk++)
+#pragma unroll
+              for (int j = 0; j < E; j++) pk[kk][j] = 0u;
+          }
           apply_props<E, K>(pr, in, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], (uint32_t)op[6], a);
           if (ldoc && !lop) {
             // shouldModifyKey: a key with a pending local update keeps its
@@ -680,7 +712,8 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
 #pragma unroll
         for (int j = 0; j < E; j++) {
           const int i = base + j;
-          keep[j] = i < n && (int32_t)ld_l2(pl + 2 * sd + i) > msn;
+          const int32_t rs = (int32_t)ld_l2(pl + 2 * sd + (i < n ? i : 0));  // unconditional, selected after
+          keep[j] = i < n && rs > msn;
           cntl += keep[j] ? 1 : 0;
         }
         const int32_t incl = wave_incl_scan(cntl);
@@ -694,10 +727,14 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
             uint32_t v[kPlaneGroup][E];
 #pragma unroll
             for (int g = 0; g < kPlaneGroup; g++) {
-              const uint32_t pb = (uint32_t)((uint64_t)(p0 + g) * sd);
+              const int pg = p0 + g < nplanes ? p0 + g : nplanes - 1;
+              const uint32_t pb = (uint32_t)((uint64_t)pg * sd);
 #pragma unroll
-              for (int j = 0; j < E; j++)
-                v[g][j] = (p0 + g < nplanes && keep[j]) ? ld_l2o(pl, pb + (uint32_t)(base + j)) : 0u;
+              for (int j = 0; j < E; j++) {
+                const bool ok = p0 + g < nplanes && keep[j];  // keep implies base + j < n
+                const uint32_t x = ld_l2o(pl, pb + (uint32_t)(ok ? base + j : 0));
+                v[g][j] = ok ? x : 0u;
+              }
             }
 #pragma unroll
             for (int g = 0; g < kPlaneGroup; g++) {
