@@ -254,3 +254,48 @@ def test_bench_local_client_stream_copies_replay_alike():
     assert (o.statuses() == 0).all()
     d, nb = o.digest(), len(base["inits"])
     assert np.array_equal(d[:nb], d[nb:])
+
+
+def _regen_mixed(factory, n_keys):
+    """Inserts, removes and annotates (props {} when the context has no keys),
+    regenerated: the MTE_DELTA_REGEN records, text offsets taken per group."""
+    it = Interner(n_keys)
+    eng = factory(n_keys)
+    inits, text = doc_inits(["hello world, hello again"], flags=DOC_NEW_LENGTH_CALC | DOC_LOCAL_CLIENT | DOC_EVENTS)
+    eng.load_docs(inits, text)
+    me = DocClients("me", local=True)
+    props = {"k": 1} if n_keys else {}
+    ops = [{"type": 0, "pos1": 3, "seg": "XYZ"}, {"type": 2, "pos1": 1, "pos2": 9, "props": props},
+           {"type": 1, "pos1": 5, "pos2": 12}, {"type": 0, "pos1": 6, "seg": "QQ"},
+           {"type": 2, "pos1": 0, "pos2": 20, "props": props}]
+    bb = BatchBuilder(1, it)
+    for op in ops:
+        bb.add_local(0, me, op)
+    eng.apply_batch(bb.build())
+    bb = BatchBuilder(1, it)
+    for _ in ops:
+        bb.add_regen(0, me)
+    eng.apply_batch(bb.build())
+    assert eng.statuses()[0] == 0
+    out, base = [], {}
+    dl = eng.read_deltas(0)
+    for d in dl:
+        base[int(d["op"])] = min(base.get(int(d["op"]), 1 << 32), int(d["removed"]))
+    for d in dl:
+        out.append((int(d["op"]), int(d["kind"]), int(d["pos"]), int(d["len"]), int(d["removed"]) - base[int(d["op"])]))
+    return out
+
+
+def test_oracle_regen_mixed_shape():
+    got = _regen_mixed(oracle_factory, 4)
+    kinds = {k & 0xF for _, k, _, _, _ in got}
+    assert kinds == {0, 1, 2}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_keys", [0, 4, 8])
+def test_gpu_regen_mixed_matches_oracle(n_keys):
+    """Every key-plane layout of the stream pass (the group-mask plane follows
+    the K property and K pending-key planes; with K = 0 it is the one spare
+    props plane): GPU records equal the restatement's."""
+    assert _regen_mixed(device_factory, n_keys) == _regen_mixed(oracle_factory, n_keys)
