@@ -320,7 +320,8 @@ int mte_read_doc(mte_ctx* ctx, uint32_t doc, mte_doc_view* view);
 
 /* One delta event range (ISequenceDeltaRange): the record (index in the doc's
  * part of the last batch) whose op caused it, MergeTreeDeltaType (INSERT /
- * REMOVE / ANNOTATE), the segment's position in the doc's own view right after
+ * REMOVE / ANNOTATE; MTE_DELTA_REGEN | type for the segments an MTE_OP_REGEN
+ * record re-sends, positioned as that record describes), the segment's position in the doc's own view right after
  * the op (-1 for a zero-length insert, which links no segment) and its length
  * (cachedLength).  A remove reports only segments it newly removed
  * (removedSegments, mergeTree.ts:1954-1959); an annotate every segment it
