@@ -1,7 +1,9 @@
 // mte_stream.h — pass 3: documents beyond the register tiers (> 1,022
-// segments), replayed one wavefront per document with the segment planes
-// left in HBM and streamed per op in tiles of 256 slots (4 per lane,
-// lane-major, coalesced).
+// segments) and every document with a local client or delta events, replayed
+// one wavefront per document with the segment planes left in HBM and streamed
+// per op in tiles of 128 slots (2 per lane, lane-major, coalesced; 2 per lane
+// keeps the registers low enough for 5-8 waves per SIMD, which hide the
+// per-op chain of L2 round trips better than wider tiles).
 //
 // Per op, the same algorithm as doc_step (mte_replay.h), restated over tiles:
 //   A  scan tiles front to back: perspective lengths, running prefix, the
@@ -23,7 +25,7 @@
 
 namespace mte {
 
-constexpr int kTileE = 4;
+constexpr int kTileE = 2;
 constexpr int kTile = kWave * kTileE;  // slots per tile
 
 __device__ __forceinline__ uint32_t ld_l2(const uint32_t* p) {
