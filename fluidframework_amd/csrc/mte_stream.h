@@ -77,7 +77,7 @@ __device__ __forceinline__ void tile_load_hot(Regs<kTileE, K>& R, const uint32_t
 constexpr int32_t kLocalBase = MTE_LOCAL_SEQ_BASE;
 template <int K>
 constexpr int kAnnPlane = kFieldPlanes + 2 * K;
-constexpr int kPlaneGroup = 3;  // planes moved per batch of loads (all in flight, then the stores)
+constexpr int kPlaneGroup = 5;  // planes moved per batch of loads (all in flight, then the stores)
 
 // the local client's own view (localNetLength, mergeTree.ts:553-573, new
 // length calculation): removed -> 0, else the length; padding undefined
