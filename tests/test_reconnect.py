@@ -299,3 +299,43 @@ def test_gpu_regen_mixed_matches_oracle(n_keys):
     the K property and K pending-key planes; with K = 0 it is the one spare
     props plane): GPU records equal the restatement's."""
     assert _regen_mixed(device_factory, n_keys) == _regen_mixed(oracle_factory, n_keys)
+
+
+@pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
+def test_js_packer_regen_slot_overflow_matches_python():
+    """33 pending annotates: both packers leave the 33rd untracked (record b =
+    MTE_NO_PROPS), refuse to regenerate it, and free a slot per ack."""
+    root = os.path.dirname(HERE)
+    script = r"""
+const p = require('./fluidframework_amd/node/packing');
+const it = new p.Interner(4), cl = new p.DocClients('me', 0, true);
+const bb = new p.BatchBuilder(1, it);
+for (let i = 0; i < 33; i++) bb.addLocal(0, cl, {type: 2, pos1: 0, pos2: 1, props: {a: 1}});
+const bs = bb.docOps[0].map((r) => r[9]);
+const bb2 = new p.BatchBuilder(1, it);
+for (let i = 0; i < 32; i++) bb2.addRegen(0, cl);
+let code = 0;
+try { bb2.addRegen(0, cl); } catch (e) { code = e.code; }
+const bb3 = new p.BatchBuilder(1, it);
+for (let s = 1; s <= 2; s++)
+  bb3.addMessage(0, cl, {clientId: 'me', sequenceNumber: s, referenceSequenceNumber: 0, minimumSequenceNumber: 0,
+                         type: 'op', contents: {}});
+process.stdout.write(JSON.stringify({bs, code, acks: bb3.docOps[0].map((r) => r.slice(6, 9)),
+                                     free: 32 - cl.annSlot.size}));
+"""
+    r = subprocess.run([shutil.which("node"), "-e", script], cwd=root, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    j = json.loads(r.stdout)
+    from fluidframework_amd.abi import NO_PROPS
+    assert j["bs"] == list(range(32)) + [NO_PROPS]
+    assert j["code"] == MTE_E_UNSUPPORTED
+    # the 32 regenerated messages moved behind the untracked one: the first ack
+    # is localSeq 33 (no slot), the second localSeq 1 (slot 0: mask 1 << 0)
+    assert j["acks"] == [[33, 33, 0], [1, 1, 1]] and j["free"] == 1
+    # the Python packer, the same sequence
+    it = Interner(4)
+    me = DocClients("me", local=True)
+    bb = BatchBuilder(1, it)
+    for _ in range(33):
+        bb.add_local(0, me, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1}})
+    assert [int(r[9]) for r in bb.ops[0]] == j["bs"]
