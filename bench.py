@@ -5,12 +5,16 @@ One step = replay of one batch (every doc x every op of the workload) from the
 documents' initial state: mte_reset + mte_run (device-resident inputs: ops,
 text and property tables are uploaded to HBM before the timed region).
 
-N GPUs: one process per GPU (torch.distributed.run), documents sharded with no
+N GPUs: one process per GPU (launched by torch.distributed.run, which only
+sets RANK / WORLD_SIZE; nothing here imports torch), documents sharded with no
 data-path collective.  Default "strong": the config's documents (BASELINE: 10k
-per node) split over the ranks (doc seeds are global doc indices); at N > 1 a
-"weak" side line replays the config's documents on every rank.  After the
-timed region the per-doc digests are all-gathered over RCCL for verification
-(the only collective).
+per node) assigned to ranks by expected work, longest first onto the least
+loaded rank (fluidframework_amd/dist.py, the Node host's shardByWork rule; doc
+seeds are global doc indices); at N > 1 a "weak" side line replays the
+config's document count on every rank.  After the timed region the per-doc
+digests are all-gathered over RCCL (libmte.so mte_comm_*, the only
+collective) and put back in global order for verification.  If RCCL cannot
+start, the job exits non-zero.
 
 Legacy length-calc documents of the round-model workloads are declared
 round-synchronous (MTE_DOC_ROUND_SYNC: flat passes, declaration checked per
@@ -70,11 +74,23 @@ def pmc_traffic(config, n_docs, ops_per_doc):
     if not preset_ok:
         return None, "non-default workload size"
     rec = json.load(open(path))
-    lib = os.path.join(ROOT, "fluidframework_amd", "_lib", "libmte.so")
-    sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+    from fluidframework_amd import _native
+    sha = hashlib.sha256(open(_native.lib_path("libmte.so"), "rb").read()).hexdigest()
     if rec.get("libmte_sha256") != sha:
         return None, "PMC summary was taken on a different libmte.so build"
     return rec["traffic_bytes_per_launch"], os.path.relpath(path, ROOT) + " (" + rec["correction"] + ")"
+
+
+def library_build():
+    """Which libmte.so ran: its sha256 and file time (a rebuild on the box shows as a
+    new time and, if the sources changed, a new hash)."""
+    import hashlib
+    from fluidframework_amd import _native
+    p = _native.lib_path("libmte.so")
+    st = os.stat(p)
+    return {"libmte_sha256": hashlib.sha256(open(p, "rb").read()).hexdigest(),
+            "libmte_mtime_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(st.st_mtime)),
+            "libmte_path": os.path.relpath(p, ROOT)}
 
 
 REF_BASELINE_JSON = os.path.join(ROOT, "profiles", "r02", "ref_cpu_baseline.json")
@@ -92,55 +108,38 @@ def reference_cpu_baseline(config):
 class NodeComm:
     """Barrier, scalar reductions and the digest gather of an N-GPU job: RCCL
     through libmte.so's mte_comm_* on a context of its own (fluidframework_amd/
-    comm.py bootstraps the unique id), or torch.distributed if that cannot start."""
+    comm.py bootstraps the unique id).  No fallback: a job whose communicator
+    cannot start exits non-zero."""
 
     def __init__(self, rank, world, local_rank):
         from fluidframework_amd import comm as fcomm
         from fluidframework_amd.engine import DeviceEngine
         self.rank, self.world = rank, world
-        self.dist = None
         try:
             self.eng = DeviceEngine(0, device=local_rank)
             fcomm.join(self.eng, rank, world)
-            self.kind = "rccl via libmte.so mte_comm_* (no torch)"
         except Exception as e:  # pragma: no cover - hardware dependent
-            import torch
-            import torch.distributed as dist
-            torch.cuda.set_device(local_rank)
-            dist.init_process_group("nccl")
-            self.dist, self.dev = dist, f"cuda:{local_rank}"
-            self.kind = f"torch.distributed nccl (mte_comm failed: {e})"
+            raise SystemExit(f"rank {rank}: RCCL communicator (mte_comm_init) failed: {e}")
+        self.kind = "rccl via libmte.so mte_comm_* (no torch)"
 
     def barrier(self):
-        if self.dist is not None:
-            self.dist.barrier()
-        else:
-            self.eng.comm_barrier()
+        self.eng.comm_barrier()
 
     def max(self, v):
-        from fluidframework_amd import dist as fdist
-        if self.dist is not None:
-            return fdist.max_over_ranks(self.dist, v, device=self.dev)
         return self.eng.comm_allreduce(float(v), "max")
 
     def sum(self, v):
-        from fluidframework_amd import dist as fdist
-        if self.dist is not None:
-            return fdist.sum_over_ranks(self.dist, v, device=self.dev)
         return self.eng.comm_allreduce(float(v), "sum")
 
     def gather_digests(self, eng, docs_per_rank):
-        from fluidframework_amd import dist as fdist
-        if self.dist is not None:
-            return fdist.gather_digests(self.dist, engine=eng, device=self.dev)
+        """Every rank's digests, rank-major (world, docs_per_rank, 4)."""
         eng.comm_share(self.eng)
-        return eng.comm_gather_digests(self.world, docs_per_rank).reshape(-1, 4)
+        g = eng.comm_gather_digests(docs_per_rank)
+        eng.comm_destroy()  # drops eng's reference; the communicator stays with self.eng
+        return g
 
     def close(self):
-        if self.dist is not None:
-            self.dist.destroy_process_group()
-        else:
-            self.eng.comm_destroy()
+        self.eng.comm_destroy()
 
 
 def run_engine(stream, cap, device, steps, warmup, stats_on, barrier=lambda: None):
@@ -237,7 +236,7 @@ def main():
     from fluidframework_amd.engine import DeviceEngine
 
     # node level: RCCL through libmte.so (mte_comm_*), one communicator per
-    # process on a context of its own; torch.distributed only if that fails
+    # process on a context of its own
     node = None
     if world > 1:
         node = NodeComm(rank, world, local_rank)
@@ -247,19 +246,21 @@ def main():
     ops_per_doc = args.ops or preset["ops_per_doc"]
     threads = max(1, host_threads() // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", world))))
 
+    # strong scaling: the job's documents onto ranks by expected work (every
+    # document of a preset has the same op count and expected live segments,
+    # so LPT deals them out round-robin); weak: rank r replays global documents
+    # [r * docs_job, (r + 1) * docs_job)
+    rank_of = fdist.shard_by_work(np.full(docs_job, float(ops_per_doc)), world)
+
     def shard(scaling):
-        """(first global doc, docs) of this rank."""
+        """Global indices of this rank's documents."""
         if scaling == "weak":
-            return fdist.shard_doc_base(rank, docs_job), docs_job
-        per = (docs_job + world - 1) // world
-        b = min(docs_job, rank * per)
-        return b, max(0, min(docs_job, b + per) - b)
+            return np.arange(rank * docs_job, (rank + 1) * docs_job, dtype=np.uint32)
+        return fdist.rank_docs(rank_of, rank)
 
     def make_stream(scaling, placement):
-        base, n = shard(scaling)
         kw = {"round_sync": True} if placement == "round_sync" and not preset.get("max_lag") else {}
-        return gen.generate(args.config, n_docs=n, ops_per_doc=ops_per_doc, doc_base=base, n_threads=threads,
-                            **kw)
+        return gen.generate(args.config, ops_per_doc=ops_per_doc, doc_ids=shard(scaling), n_threads=threads, **kw)
 
     def barrier():
         if node is not None:
@@ -279,9 +280,13 @@ def main():
     if node is not None:
         elapsed = node.max(r["elapsed"])
         total_ops = int(node.sum(n_ops_rank))
-        # the verification collective: every rank's per-doc digests over RCCL
-        per = docs_job if args.scaling == "weak" else (docs_job + world - 1) // world
-        fold = fdist.digest_fold(node.gather_digests(eng, per))
+        # the verification collective: every rank's per-doc digests over RCCL,
+        # back in global document order
+        if args.scaling == "weak":
+            fold = fdist.digest_fold(node.gather_digests(eng, docs_job))
+        else:
+            g = node.gather_digests(eng, fdist.docs_per_rank(rank_of, world))
+            fold = fdist.digest_fold(fdist.unshard_digests(g, rank_of, world))
 
     ms_per_step = elapsed * 1000.0 / args.steps
     value = total_ops / (elapsed / args.steps)
@@ -376,7 +381,7 @@ def main():
             "placement": ("legacy-calc docs declared round-synchronous (MTE_DOC_ROUND_SYNC): flat passes, "
                           "declaration checked per batch" if args.placement == "round_sync" else
                           "legacy-calc docs on the tree pass (reference B+tree placement)"),
-            "parallelism": f"doc-sharded x{world} (no data-path collective)",
+            "parallelism": f"doc-sharded x{world} by expected work (LPT), no data-path collective",
             "collective": node.kind if node is not None else None,
         },
         "roofline": {
@@ -409,6 +414,7 @@ def main():
         "digest_fold": f"{fold:016x}",
         "parity_sample": parity,
         "gen_s": round(gen_s, 2),
+        "build": library_build(),
     }
     print(json.dumps(out), flush=True)
     if node is not None:

@@ -59,7 +59,8 @@ def load_mte():
         "mte_comm_share": ([vp, vp], C.c_int),
         "mte_comm_barrier": ([vp], C.c_int),
         "mte_comm_allreduce_f64": ([vp, vp, C.c_int], C.c_int),
-        "mte_comm_gather_digests": ([vp, vp, u32], C.c_int),
+        "mte_comm_gather_digests": ([vp, vp, C.c_uint64, u32], C.c_int),
+        "mte_comm_world": ([vp, vp, vp], C.c_int),
         "mte_comm_destroy": ([vp], C.c_int),
     }
     for name, (args, res) in sig.items():

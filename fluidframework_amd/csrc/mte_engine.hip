@@ -321,6 +321,12 @@ const uint64_t kDigB2 = 0x0a0761d6478bd642ull % kM61;
 // C-ABI
 // ---------------------------------------------------------------------------
 
+// An RCCL communicator and the number of contexts using it (mte_comm_share).
+struct CommRef {
+  ncclComm_t comm = nullptr;
+  std::atomic<int> refs{1};
+};
+
 struct mte_ctx {
   int device = 0;
   uint32_t n_keys = 0, kt = 0;  // kt: template planes (0/4/8)
@@ -423,8 +429,10 @@ struct mte_ctx {
   uint32_t* d_rs_docs = nullptr;    // legacy documents declared MTE_DOC_ROUND_SYNC (flat)
   int tree_rounds = 0;              // TIER 0 / TIER 1 rounds (MTE_TREE_ROUNDS; 0 = from the batch)
   // node level (mte_comm_*): the RCCL communicator and its staging buffers
-  ncclComm_t comm = nullptr;
-  bool comm_owner = false;
+  // the communicator is shared by reference count (mte_comm_share): the last
+  // context to release it destroys it, whatever order contexts go in
+  CommRef* cref = nullptr;
+  ncclComm_t comm = nullptr;  // cref->comm, or null
   int world = 1, rank = 0;
   uint64_t* d_comm = nullptr;  // digests of all ranks / scalar reductions
   uint64_t comm_cap = 0;       // uint64 elements
@@ -445,6 +453,20 @@ int set_err(mte_ctx* c, int code, const char* fmt, ...) {
   va_end(ap);
   if (c) c->err = buf;
   return code;
+}
+
+// drop this context's reference to its communicator; the last one destroys it
+ncclResult_t comm_release(mte_ctx* c) {
+  ncclResult_t r = ncclSuccess;
+  if (c->cref && c->cref->refs.fetch_sub(1) == 1) {
+    r = ncclCommDestroy(c->cref->comm);
+    delete c->cref;
+  }
+  c->cref = nullptr;
+  c->comm = nullptr;
+  c->world = 1;
+  c->rank = 0;
+  return r;
 }
 
 #define HIPCHK(ctx, expr)                                                                  \
@@ -756,7 +778,7 @@ int mte_destroy(mte_ctx* c) {
     if (c->stage[i]) (void)hipHostFree(c->stage[i]);
     if (c->stage_ev[i]) (void)hipEventDestroy(c->stage_ev[i]);
   }
-  if (c->comm && c->comm_owner) (void)ncclCommDestroy(c->comm);
+  comm_release(c);
   if (c->d_comm) (void)hipFree(c->d_comm);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
@@ -1390,8 +1412,11 @@ int mte_comm_init(mte_ctx* c, int world, int rank, const uint8_t id[MTE_COMM_ID_
   HIPCHK(c, hipSetDevice(c->device));
   ncclUniqueId u;
   std::memcpy(&u, id, MTE_COMM_ID_BYTES);
-  NCCLCHK(c, ncclCommInitRank(&c->comm, world, u, rank));
-  c->comm_owner = true;
+  ncclComm_t comm = nullptr;
+  NCCLCHK(c, ncclCommInitRank(&comm, world, u, rank));
+  c->cref = new CommRef;
+  c->cref->comm = comm;
+  c->comm = comm;
   c->world = world;
   c->rank = rank;
   return MTE_OK;
@@ -1400,8 +1425,9 @@ int mte_comm_init(mte_ctx* c, int world, int rank, const uint8_t id[MTE_COMM_ID_
 int mte_comm_share(mte_ctx* c, const mte_ctx* src) {
   if (!c || !src || !src->comm || src->device != c->device) return MTE_E_INVALID_ARG;
   if (c->comm) return set_err(c, MTE_E_STATE, "mte_comm_share: already has a communicator");
+  src->cref->refs.fetch_add(1);
+  c->cref = src->cref;
   c->comm = src->comm;
-  c->comm_owner = false;
   c->world = src->world;
   c->rank = src->rank;
   return MTE_OK;
@@ -1437,9 +1463,19 @@ int mte_comm_barrier(mte_ctx* c) {
   return mte_comm_allreduce_f64(c, &one, MTE_COMM_SUM);
 }
 
-int mte_comm_gather_digests(mte_ctx* c, uint64_t* out, uint32_t docs_per_rank) {
+int mte_comm_world(const mte_ctx* c, int32_t* world, int32_t* rank) {
+  if (!c || !world || !rank) return MTE_E_INVALID_ARG;
+  *world = c->world;
+  *rank = c->rank;
+  return MTE_OK;
+}
+
+int mte_comm_gather_digests(mte_ctx* c, uint64_t* out, uint64_t out_cap, uint32_t docs_per_rank) {
   if (!c || !out || docs_per_rank < c->n_docs) return MTE_E_INVALID_ARG;
   if (!c->comm) return set_err(c, MTE_E_STATE, "mte_comm_init first");
+  if (out_cap < 4ull * docs_per_rank * (uint64_t)c->world)
+    return set_err(c, MTE_E_INVALID_ARG, "mte_comm_gather_digests: out holds %llu uint64, needs world %d x %u docs x 4",
+                   (unsigned long long)out_cap, c->world, docs_per_rank);
   HIPCHK(c, hipSetDevice(c->device));
   const uint64_t per = 4ull * docs_per_rank;
   int rc = comm_staging(c, per * (uint64_t)(c->world + 1));
@@ -1456,9 +1492,9 @@ int mte_comm_gather_digests(mte_ctx* c, uint64_t* out, uint32_t docs_per_rank) {
 
 int mte_comm_destroy(mte_ctx* c) {
   if (!c) return MTE_E_INVALID_ARG;
-  if (c->comm && c->comm_owner) NCCLCHK(c, ncclCommDestroy(c->comm));
-  c->comm = nullptr;
-  c->comm_owner = false;
+  HIPCHK(c, hipSetDevice(c->device));
+  const ncclResult_t r = comm_release(c);
+  if (r != ncclSuccess) return set_err(c, MTE_E_HIP, "ncclCommDestroy: %s", ncclGetErrorString(r));
   c->world = 1;
   c->rank = 0;
   return MTE_OK;

@@ -199,7 +199,7 @@ int32_t gen_insert(const mteg_config& cfg, MT& rng, uint32_t author, int32_t s, 
 // [0, bound] instead of [0, L].  Ranges are short (1..max_range units).
 void gen_doc_long(const mteg_config& cfg, uint32_t d, DocOut& out) {
   MT rng;
-  const uint32_t key[4] = {0xDEADBEEFu, 0xFEEDBEDu, cfg.config_id, cfg.doc_base + d};
+  const uint32_t key[4] = {0xDEADBEEFu, 0xFEEDBEDu, cfg.config_id, cfg.doc_ids ? cfg.doc_ids[d] : cfg.doc_base + d};
   rng.init_by_array(key, 4);
   const uint32_t C = cfg.clients < 1 ? 1 : (cfg.clients > 31 ? 31 : cfg.clients);
   if (cfg.length_mode == 0) out.flags = (rng.next() & 1u) ? MTE_DOC_NEW_LENGTH_CALC : 0u;
@@ -273,7 +273,7 @@ void gen_doc(const mteg_config& cfg, uint32_t d, DocOut& out) {
     return;
   }
   MT rng;
-  const uint32_t key[4] = {0xDEADBEEFu, 0xFEEDBEDu, cfg.config_id, cfg.doc_base + d};
+  const uint32_t key[4] = {0xDEADBEEFu, 0xFEEDBEDu, cfg.config_id, cfg.doc_ids ? cfg.doc_ids[d] : cfg.doc_base + d};
   rng.init_by_array(key, 4);
   const uint32_t C = cfg.clients < 1 ? 1 : (cfg.clients > 31 ? 31 : cfg.clients);
   if (cfg.length_mode == 0) out.flags = (rng.next() & 1u) ? MTE_DOC_NEW_LENGTH_CALC : 0u;

@@ -57,6 +57,9 @@ typedef struct mteg_config {
                             rule, deli clientSeqManager.ts:130-137), so ops
                             see each other's concurrent edits partially */
   uint32_t newline_every; /* 1 in N inserted texts holds a '\n' (0 = none) */
+  const uint32_t* doc_ids; /* NULL: doc d is global doc doc_base + d; else the
+                              global index of doc d (seed word 4), e.g. a
+                              rank's shard from a work-balanced assignment   */
 } mteg_config;
 
 typedef struct mteg_stream mteg_stream;

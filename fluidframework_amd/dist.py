@@ -1,58 +1,55 @@
-"""Multi-GPU sharding of documents.
+"""Multi-GPU sharding of documents.  No torch.
 
-Documents are independent: rank r of a world of N replays its own shard of
-`docs_per_rank` documents whose seeds are the global doc indices
-[r * docs_per_rank, (r + 1) * docs_per_rank) — weak scaling, no collective on
-the data path.  The only collective is the verification gather of the per-doc
-32-byte digests (RCCL `all_gather` over xGMI under the "nccl" backend, gloo on
-CPU in the tests).
+Documents are independent, so a node job assigns each document to one rank
+(one process per GPU) and no collective touches the replay.  The assignment
+is by expected work: documents longest first onto the least
+loaded rank (LPT), the same rule as the Node host's
+MergeTreeEngine.shardByWork (node/index.js).  The only collective is the
+verification all-gather of the per-doc digests (libmte.so mte_comm_gather_
+digests over RCCL): rank-major, every rank's rows padded with zero rows to
+`docs_per_rank`.  `unshard_digests` turns that layout back into global
+document order.
 """
 import numpy as np
 
 
-def shard_doc_base(rank: int, docs_per_rank: int) -> int:
-    """Global index of the first document of `rank`'s shard."""
-    return rank * docs_per_rank
+def shard_by_work(work, world: int) -> np.ndarray:
+    """Rank of every document: longest first onto the least loaded rank
+    (ties: the lower document index first, the lower rank first)."""
+    work = np.asarray(work, dtype=np.float64)
+    order = sorted(range(len(work)), key=lambda d: (-work[d], d))
+    load = np.zeros(world, np.float64)
+    rank_of = np.zeros(len(work), np.int32)
+    for d in order:
+        r = int(np.argmin(load))  # argmin returns the first (lowest) rank on ties
+        rank_of[d] = r
+        load[r] += work[d]
+    return rank_of
 
 
-def gather_digests(dist, local_digest=None, engine=None, device=None):
-    """All-gather every rank's (n_docs, 4) uint64 digests -> (world * n_docs, 4).
+def rank_docs(rank_of, rank: int) -> np.ndarray:
+    """Global indices of `rank`'s documents, ascending (its local order)."""
+    return np.flatnonzero(np.asarray(rank_of) == rank).astype(np.uint32)
 
-    Under a device backend pass `engine` and `device`: the digest kernel writes
-    straight into a device tensor (mte_digest_device) that RCCL gathers.  On
-    CPU (gloo) pass `local_digest` (numpy)."""
-    import torch
 
-    world = dist.get_world_size()
-    if engine is not None:
-        n = engine.n_docs
-        mine = torch.empty((n, 4), dtype=torch.int64, device=device)
-        engine.digest_device(mine.data_ptr())
-        engine.sync()
-    else:
-        mine = torch.from_numpy(np.ascontiguousarray(local_digest).view(np.int64).copy())
-    parts = [torch.empty_like(mine) for _ in range(world)]
-    dist.all_gather(parts, mine)
-    return torch.cat(parts).cpu().numpy().view(np.uint64)
+def docs_per_rank(rank_of, world: int) -> int:
+    """Rows per rank of the gathered digest layout (the largest shard)."""
+    return int(np.bincount(np.asarray(rank_of), minlength=world).max()) if len(rank_of) else 0
+
+
+def unshard_digests(gathered, rank_of, world: int) -> np.ndarray:
+    """(world, docs_per_rank, 4) or (world * docs_per_rank, 4) gathered digests
+    (rank-major, zero-padded rows) -> (n_docs, 4) in global document order."""
+    rank_of = np.asarray(rank_of)
+    g = np.asarray(gathered, dtype=np.uint64).reshape(world, -1, 4)
+    out = np.zeros((len(rank_of), 4), np.uint64)
+    for r in range(world):
+        ids = rank_docs(rank_of, r)
+        out[ids] = g[r, :len(ids)]
+    return out
 
 
 def digest_fold(d) -> int:
     """A single 64-bit checksum of checksums for logging (xor of h1 ^ h2)."""
     d = np.asarray(d, dtype=np.uint64).reshape(-1, 4)
     return int(np.bitwise_xor.reduce(d[:, 1] ^ d[:, 2])) if len(d) else 0
-
-
-def max_over_ranks(dist, value: float, device=None) -> float:
-    import torch
-
-    t = torch.tensor([value], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def sum_over_ranks(dist, value: int, device=None) -> int:
-    import torch
-
-    t = torch.tensor([value], dtype=torch.int64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return int(t.item())

@@ -192,9 +192,18 @@ class DeviceEngine(EngineBase):
                     "comm_allreduce")
         return v.value
 
-    def comm_gather_digests(self, world, docs_per_rank):
+    def comm_world(self):
+        """(world, rank) of this context's communicator (mte_comm_world)."""
+        w, r = C.c_int32(), C.c_int32()
+        self._check(self.lib.mte_comm_world(self.ctx, C.byref(w), C.byref(r)), "comm_world")
+        return w.value, r.value
+
+    def comm_gather_digests(self, docs_per_rank):
+        """Every rank's digests in rank order, sized from the context's own world."""
+        world, _ = self.comm_world()
         out = np.zeros(world * docs_per_rank * 4, np.uint64)
-        self._check(self.lib.mte_comm_gather_digests(self.ctx, ptr(out), docs_per_rank), "comm_gather_digests")
+        self._check(self.lib.mte_comm_gather_digests(self.ctx, ptr(out), out.size, docs_per_rank),
+                    "comm_gather_digests")
         return out.reshape(world, docs_per_rank, 4)
 
     def comm_destroy(self):

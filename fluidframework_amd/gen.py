@@ -20,7 +20,7 @@ class GenConfig(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in (
         "config_id", "n_docs", "ops_per_doc", "doc_base", "clients", "min_length", "round_ops",
         "mix", "marker_every", "length_mode", "init_len", "n_threads", "init_segs", "max_range",
-        "max_lag", "newline_every")]
+        "max_lag", "newline_every")] + [("doc_ids", C.c_void_p)]
 
 
 class GenSizes(C.Structure):
@@ -64,9 +64,16 @@ def default_threads():
     return max(1, min(n, 16))
 
 
-def generate(config_id=2, n_docs=None, ops_per_doc=None, doc_base=0, n_threads=None, **over):
-    """-> dict(inits, init_text, batch={op_offsets, ops, text, propsets, props})."""
+def generate(config_id=2, n_docs=None, ops_per_doc=None, doc_base=0, n_threads=None, doc_ids=None, **over):
+    """-> dict(inits, init_text, batch={op_offsets, ops, text, propsets, props}).
+
+    Documents are the global documents doc_base .. doc_base + n_docs - 1, or
+    the global indices `doc_ids` (a rank's shard, fluidframework_amd/dist.py)."""
     p = dict(PRESETS.get(config_id, PRESETS[2]))
+    ids = None
+    if doc_ids is not None:
+        ids = np.ascontiguousarray(doc_ids, dtype=np.uint32)
+        n_docs = len(ids)
     if n_docs is not None:
         p["n_docs"] = n_docs
     if ops_per_doc is not None:
@@ -77,7 +84,7 @@ def generate(config_id=2, n_docs=None, ops_per_doc=None, doc_base=0, n_threads=N
                     p["min_length"], p["round_ops"], p["mix"], p["marker_every"],
                     p["length_mode"], p.get("init_len", 0), n_threads or default_threads(),
                     p.get("init_segs", 0), p.get("max_range", 0), p.get("max_lag", 0),
-                    p.get("newline_every", 0))
+                    p.get("newline_every", 0), ids.ctypes.data if ids is not None and len(ids) else None)
     h = C.c_void_p()
     rc = lib.mteg_generate(C.byref(cfg), C.byref(h))
     if rc:

@@ -138,6 +138,8 @@ export class MergeTreeEngine {
   flush(): void;
   /** Wait for the launched replay (every read-out does). */
   sync(): void;
+  /** Delta-event records per op record of {events: true} documents (mte_set_event_capacity). */
+  setEventCapacity(perOp: number): void;
   digests(): BigUint64Array;
   statuses(): Int32Array;
   stats(): EngineStats;

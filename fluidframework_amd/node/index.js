@@ -189,17 +189,45 @@ class MergeTreeEngine {
     this.running = true;
   }
 
-  /** Wait for the launched replay (read-outs call it). */
+  /** Wait for the launched replay (read-outs call it).  Every document's
+   *  delta events are read and delivered before any error is raised: a
+   *  document whose event region overflowed (MTE_E_CAPACITY, see
+   *  setEventCapacity) loses its events and is marked, so its later
+   *  getMessagesSinceMSNChange / summarizeLegacy throw instead of returning an
+   *  incomplete stash; the other documents of the batch are unaffected. */
   sync() {
-    if (this.running) {
-      this.running = false;
-      this.addon.sync(this.ctx);
-      const src = this.inflightSrc;
-      this.inflightSrc = null;
-      if (src) {
-        src.forEach((recs, doc) => { if (recs && recs.length) this.clients[doc]._deliver(this.addon.readDeltas(this.ctx, doc), recs); });
+    if (!this.running) return;
+    this.addon.sync(this.ctx);
+    this.running = false;
+    const src = this.inflightSrc;
+    this.inflightSrc = null;
+    if (!src) return;
+    let first = null;
+    src.forEach((recs, doc) => {
+      if (!recs || !recs.length) return;
+      const c = this.clients[doc];
+      let flat;
+      try {
+        flat = this.addon.readDeltas(this.ctx, doc);
+      } catch (e) {
+        c.eventsLost = e;
+        if (!first) first = e;
+        return;
       }
-    }
+      try {
+        c._deliver(flat, recs);
+      } catch (e) {  // a listener threw: the other documents still get theirs
+        if (!first) first = e;
+      }
+    });
+    if (first) throw first;
+  }
+
+  /** Delta-event records per op record of MTE_DOC_EVENTS documents (+ 256 per
+   *  document; mte_set_event_capacity, default 8).  Takes effect at the next
+   *  flush; raise it before replaying ops that touch many segments. */
+  setEventCapacity(perOp) {
+    this.addon.setEventCapacity(this.ctx, perOp);
   }
 
   _view(doc) {
@@ -419,6 +447,7 @@ class BatchClient {
    *  summary (sequence.ts:688-725, createOpsFromDelta :116-161): a message whose
    *  refSeq is not seq - 1 becomes its effect as ops at refSeq = seq - 1. */
   getMessagesSinceMSNChange() {
+    if (this.eventsLost) throw this.eventsLost;
     return (this.stash || []).slice();
   }
 

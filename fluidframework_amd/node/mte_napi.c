@@ -512,8 +512,9 @@ static napi_value js_comm_gather_digests(napi_env env, napi_callback_info info) 
   if (!get_bytes(env, argv[1], &out, &n)) return NULL;
   uint32_t per = 0;
   NAPI_CALL(env, napi_get_value_uint32(env, argv[2], &per));
-  (void)n;
-  throw_rc(env, mte_comm_gather_digests(ctx, (uint64_t*)out, per), ctx, "mte_comm_gather_digests");
+  /* the byte length of the caller's array bounds the gather (mte.h) */
+  throw_rc(env, mte_comm_gather_digests(ctx, (uint64_t*)out, (uint64_t)(n / sizeof(uint64_t)), per), ctx,
+           "mte_comm_gather_digests");
   return NULL;
 }
 
@@ -562,7 +563,10 @@ static napi_value js_set_event_capacity(napi_env env, napi_callback_info info) {
   mte_ctx* ctx = get_ctx(env, argv[0]);
   if (!ctx) return NULL;
   uint32_t per = 0;
-  napi_get_value_uint32(env, argv[1], &per);
+  if (napi_get_value_uint32(env, argv[1], &per) != napi_ok) {
+    napi_throw_type_error(env, NULL, "setEventCapacity: the per-op capacity must be a number");
+    return NULL;
+  }
   throw_rc(env, mte_set_event_capacity(ctx, per), ctx, "mte_set_event_capacity");
   return NULL;
 }

@@ -239,7 +239,15 @@ class BatchBuilder {
         // our own op, sequenced: ackPendingSegment (client.ts:925-928)
         if (!clients.local) throw new MergeTreeError(E_UNSUPPORTED, "ack of a local op in an observer document");
         if (clients.pending.length === 0) throw new MergeTreeError(E_STATE, "ack without a pending local op");
-        const [lo, hi] = clients.pending.shift();
+        const [lo, hi] = clients.pending[0];
+        // as packing.py: an earlier annotate still pending would lose its keys
+        for (let q = 1; q < clients.pending.length; q++) {
+          if (clients.pending[q][0] < lo && clients.pendingTypes[q].includes(OP_ANNOTATE)) {
+            throw new MergeTreeError(E_UNSUPPORTED,
+              "ack out of localSeq order past a pending annotate (regenerate every pending op, in order)");
+          }
+        }
+        clients.pending.shift();
         clients.pendingTypes.shift();
         let mask = 0;
         for (let ls = lo; ls <= hi; ls++) {
@@ -279,14 +287,15 @@ class BatchBuilder {
     this._opRecords(op, recs, this._src(doc));
     if (recs.length === 0) recs.push([OP_NOOP, 0, 0, 0, 0, NO_PROPS]);
     if (recs.some((r) => r[1] & F_REWRITE)) throw new MergeTreeError(E_UNSUPPORTED, "local combiningOp rewrite");
+    const first = clients.localSeq + 1;
+    if (first + recs.length >= LOCAL_SEQ_BASE) throw new MergeTreeError(E_INVALID_ARG, "localSeq overflow");
+    // every check that can throw is above: the event sources stay aligned with the records
     const src = this._src(doc);
     if (src) {
       const ops = this._srcOps || [];
       for (let i = 0; i < recs.length; i++) src.push({ msg: null, op: ops[i], local: true });
-      this._srcOps = null;
     }
-    const first = clients.localSeq + 1;
-    if (first + recs.length >= LOCAL_SEQ_BASE) throw new MergeTreeError(E_INVALID_ARG, "localSeq overflow");
+    this._srcOps = null;
     recs.forEach((r, i) => {
       let b = r[5];
       if (r[0] === OP_ANNOTATE) {

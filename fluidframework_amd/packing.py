@@ -220,7 +220,16 @@ class BatchBuilder:
                     raise MergeTreeError(MTE_E_UNSUPPORTED, "ack of a local op in an observer document")
                 if not clients.pending:
                     raise MergeTreeError(MTE_E_STATE, "ack without a pending local op")
-                lo, hi = clients.pending.pop(0)
+                lo, hi = clients.pending[0]
+                # the engine clears pending property keys up to hi (acks in
+                # localSeq order, the runtime regenerating every pending op in
+                # order); after a partial regeneration an earlier annotate can
+                # still be pending here, whose keys that would clear
+                if any(plo < lo and OP_ANNOTATE in pt
+                       for (plo, _), pt in zip(clients.pending[1:], clients.pending_types[1:])):
+                    raise MergeTreeError(MTE_E_UNSUPPORTED, "ack out of localSeq order past a pending annotate "
+                                         "(regenerate every pending op, in order)")
+                clients.pending.pop(0)
                 clients.pending_types.pop(0)
                 mask = 0
                 for ls in range(lo, hi + 1):

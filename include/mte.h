@@ -382,17 +382,22 @@ int mte_set_stats(mte_ctx* ctx, int enable);
 #define MTE_COMM_MAX 1
 int mte_comm_unique_id(uint8_t id[MTE_COMM_ID_BYTES]);
 int mte_comm_init(mte_ctx* ctx, int world, int rank, const uint8_t id[MTE_COMM_ID_BYTES]);
-/* Let another context of this process use src's communicator (not owned:
- * mte_comm_destroy / mte_destroy of ctx leave it to src).  Collectives of the
- * contexts sharing one communicator must not overlap in time.                */
+/* Let another context of this process use src's communicator.  The contexts
+ * sharing it hold it by reference count: mte_comm_destroy / mte_destroy of any
+ * of them (in any order) releases that context's reference, and the last one
+ * destroys the communicator.  Collectives of the contexts sharing one
+ * communicator must not overlap in time.                                     */
 int mte_comm_share(mte_ctx* ctx, const mte_ctx* src);
+/* The context's world size and rank (1 / 0 without a communicator).         */
+int mte_comm_world(const mte_ctx* ctx, int32_t* world, int32_t* rank);
 int mte_comm_barrier(mte_ctx* ctx);
 /* In place, across ranks: op = MTE_COMM_SUM / MTE_COMM_MAX. */
 int mte_comm_allreduce_f64(mte_ctx* ctx, double* value, int op);
 /* Digests of this context's documents, padded with zero rows to docs_per_rank
  * (>= n_docs, equal on all ranks), gathered in rank order into `out` (host,
- * world * docs_per_rank * 4 uint64).                                          */
-int mte_comm_gather_digests(mte_ctx* ctx, uint64_t* out, uint32_t docs_per_rank);
+ * world * docs_per_rank * 4 uint64; out_cap = the uint64 elements `out` holds,
+ * MTE_E_INVALID_ARG when that is fewer).                                      */
+int mte_comm_gather_digests(mte_ctx* ctx, uint64_t* out, uint64_t out_cap, uint32_t docs_per_rank);
 int mte_comm_destroy(mte_ctx* ctx);
 
 #ifdef __cplusplus

@@ -1,71 +1,33 @@
-// ref_stubs.js — the few values the erased reference merge-tree (oracle/ts_erase.py)
-// imports from Fluid packages outside packages/dds/merge-tree (TEST INFRASTRUCTURE).
-// Semantics follow the reference packages they stand in for:
-//   assert(cond, msg)            common/lib/common-utils/src/assert.ts:15
-//   Trace                        common/lib/common-utils/src/trace.ts:12-32
-//   unreachableCase, bufferToString
-//   UsageError / LoggingError    container-utils, telemetry-utils
-//   MessageType.Operation = "op" protocol-definitions/src/protocol.ts:58
+// ref_stubs.js — what the erased reference merge-tree (oracle/ts_erase.py) imports
+// from Fluid packages that cannot be erased here (TEST INFRASTRUCTURE).  Every
+// other imported value — assert, Trace, unreachableCase, bufferToString,
+// MessageType, AttachState — is erased from the reference's own sources
+// (ts_erase.py EXTERNAL).  What stays here carries none of the merge arithmetic:
+//   ChildLogger                  telemetry-utils: a logger factory (no-op sink)
+//   LoggingError / UsageError    telemetry-utils errorLogging.ts:360 / container-utils
+//                                error.ts:77 — their module needs the third-party
+//                                `uuid`, absent offline; raised only on failure
+//                                paths (message + props kept)
+//   SummaryTreeBuilder           runtime-utils summaryUtils.ts:128 — needs
+//                                protocol-base; on no path the oracle runs
+//   bufferToString               common-utils bufferNode.ts:58 (the same one-liner
+//                                over Node's Buffer; that file's ambient class
+//                                declaration defeats the eraser); summary load only
 "use strict";
-
-function assert(condition, message) {
-  if (!condition) {
-    const m = typeof message === "number" ? `0x${message.toString(16).padStart(3, "0")}` : message;
-    throw new Error(m);
-  }
-}
-
-class Trace {
-  static start() {
-    return new Trace(Date.now());
-  }
-  constructor(startTick) {
-    this.startTick = startTick;
-    this.lastTick = startTick;
-  }
-  trace() {
-    const tick = Date.now();
-    const event = { totalTimeElapsed: tick - this.startTick, duration: tick - this.lastTick, tick };
-    this.lastTick = tick;
-    return event;
-  }
-}
-
-function unreachableCase(x, message = "Unreachable Case") {
-  throw new Error(message);
-}
-
-function bufferToString(blob, encoding) {
-  return Buffer.from(blob).toString(encoding);
-}
-
-class UsageError extends Error {}
-class LoggingError extends Error {
-  constructor(message, props) {
-    super(message);
-    Object.assign(this, props || {});
-  }
-}
-
-const MessageType = {
-  NoOp: "noop",
-  ClientJoin: "join",
-  ClientLeave: "leave",
-  Propose: "propose",
-  Reject: "reject",
-  Summarize: "summarize",
-  SummaryAck: "summaryAck",
-  SummaryNack: "summaryNack",
-  Operation: "op",
-};
-
-const AttachState = { Detached: "Detached", Attaching: "Attaching", Attached: "Attached" };
 
 class ChildLogger {
   static create(logger) {
     return logger || { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
   }
 }
+
+class LoggingError extends Error {
+  constructor(message, props) {
+    super(message);
+    Object.assign(this, props || {});
+  }
+}
+class UsageError extends LoggingError {}
 
 class SummaryTreeBuilder {
   constructor() {
@@ -82,15 +44,6 @@ class SummaryTreeBuilder {
   }
 }
 
-module.exports = {
-  assert,
-  Trace,
-  unreachableCase,
-  bufferToString,
-  UsageError,
-  LoggingError,
-  MessageType,
-  AttachState,
-  ChildLogger,
-  SummaryTreeBuilder,
-};
+const bufferToString = (blob, encoding) => Buffer.from(blob).toString(encoding);
+
+module.exports = { ChildLogger, LoggingError, UsageError, SummaryTreeBuilder, bufferToString };

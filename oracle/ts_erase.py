@@ -14,9 +14,18 @@ constructor assignments, ES imports / exports into CommonJS, and downlevels
 Output goes to oracle/_ref/ts/ (git-ignored and gpurun-ignored: the reference
 never enters the repository's history and never travels to the GPU box).  Only
 its *outputs* (golden vectors under tests/golden/) are committed.  The
-packages outside merge-tree that the sources import (common-utils assert /
-Trace, protocol-definitions, telemetry-utils, container-utils ...) are not
-transpiled: oracle/ref_stubs.js supplies the few values the replay path uses.
+modules outside merge-tree whose values the sources use are erased from the
+reference too, into oracle/_ref/ts/node_modules/@fluidframework/<package>/
+(EXTERNAL below): common-utils assert / Trace / unreachableCase,
+protocol-definitions MessageType, container-definitions AttachState.
+oracle/ref_stubs.js supplies only what cannot be erased here:
+the telemetry loggers, the error classes of telemetry-utils / container-utils
+(whose module needs the third-party `uuid`, absent offline; they are raised
+only on failure paths) and runtime-utils' SummaryTreeBuilder (needs
+protocol-base) and common-utils' bufferToString (bufferNode.ts declares an
+ambient Buffer class this eraser does not handle); neither is on a path the
+oracle runs (summary emit / load).  Packages imported for types only
+become empty modules.
 
 Usage: python3 oracle/ts_erase.py [--src DIR] [--out DIR]
 """
@@ -28,6 +37,26 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_SRC = "/root/reference/packages/dds/merge-tree/src"
 DEFAULT_OUT = os.path.join(HERE, "_ref", "ts")
+REF_ROOT = "/root/reference"
+
+# package -> (module name, reference source file) erased into
+# node_modules/@fluidframework/<package>/<module>.js, plus the package's
+# index.js re-exporting them (the reference package's own index re-exports the
+# same names).  trace.ts imports { performance } from "./indexNode", which the
+# reference wires to performanceNode.ts.
+EXTERNAL = {
+    "common-utils": [("assert", "common/lib/common-utils/src/assert.ts"),
+                     ("trace", "common/lib/common-utils/src/trace.ts"),
+                     ("unreachable", "common/lib/common-utils/src/unreachable.ts"),
+                     ("performanceNode", "common/lib/common-utils/src/performanceNode.ts")],
+    "protocol-definitions": [("protocol", "common/lib/protocol-definitions/src/protocol.ts")],
+    "container-definitions": [("runtime", "packages/common/container-definitions/src/runtime.ts")],
+}
+INDEX_ALIASES = {"common-utils": {"indexNode": "performanceNode"}}
+STUBBED = ("telemetry-utils", "container-utils", "runtime-utils")  # oracle/ref_stubs.js
+STUB_EXTRA = ("common-utils",)  # + bufferToString from oracle/ref_stubs.js
+TYPE_ONLY = ("core-interfaces", "shared-object-base", "datastore-definitions", "runtime-definitions",
+             "common-definitions", "driver-definitions")
 
 PUNCTS = sorted("""
 >>>= ... === !== **= <<= >>= >>> ??= ?. ?? => == != <= >= && || ++ -- += -= *= /= %= &= |= ^= << >> ** &&= ||=
@@ -1158,15 +1187,31 @@ def main():
             os.makedirs(os.path.dirname(dst), exist_ok=True)
             open(dst, "w", encoding="utf-8").write(js)
             n += 1
-    # the packages the sources import but this script does not transpile
+    # the packages the sources import: erased from the reference where their
+    # values are used, the loggers / error classes / summary builder from
+    # ref_stubs.js, the type-only ones empty
     stubs = os.path.join(HERE, "ref_stubs.js")
     nm = os.path.join(args.out, "node_modules", "@fluidframework")
-    for pkg in ("common-utils", "container-utils", "telemetry-utils", "protocol-definitions", "core-interfaces",
-                "shared-object-base", "datastore-definitions", "runtime-definitions", "common-definitions",
-                "container-definitions", "driver-definitions", "runtime-utils"):
+    for pkg, mods in EXTERNAL.items():
+        d = os.path.join(nm, pkg)
+        os.makedirs(d, exist_ok=True)
+        for name, rel in mods:
+            open(os.path.join(d, name + ".js"), "w", encoding="utf-8").write(
+                erase_file(os.path.join(REF_ROOT, rel)))
+            n += 1
+        for alias, target in INDEX_ALIASES.get(pkg, {}).items():
+            open(os.path.join(d, alias + ".js"), "w").write(f"module.exports = require(\"./{target}\");\n")
+        reqs = ", ".join(f"require(\"./{name}\")" for name, _ in mods)
+        extra = f", require({stubs!r})" if pkg in STUB_EXTRA else ""
+        open(os.path.join(d, "index.js"), "w").write(f"module.exports = Object.assign({{}}, {reqs}{extra});\n")
+    for pkg in STUBBED:
         d = os.path.join(nm, pkg)
         os.makedirs(d, exist_ok=True)
         open(os.path.join(d, "index.js"), "w").write(f"module.exports = require({stubs!r});\n")
+    for pkg in TYPE_ONLY:
+        d = os.path.join(nm, pkg)
+        os.makedirs(d, exist_ok=True)
+        open(os.path.join(d, "index.js"), "w").write("module.exports = {};\n")
     print(f"erased {n} files -> {args.out}")
 
 

@@ -27,8 +27,11 @@ def ref_available():
 
 
 def build_ref():
-    """Type-erase the reference into oracle/_ref/ts (idempotent)."""
-    if not os.path.exists(os.path.join(REF_OUT, "client.js")):
+    """Type-erase the reference into oracle/_ref/ts (again when the eraser or the
+    stubs changed since)."""
+    stamp = os.path.join(REF_OUT, "client.js")
+    newest = max(os.path.getmtime(os.path.join(ROOT, "oracle", f)) for f in ("ts_erase.py", "ref_stubs.js"))
+    if not os.path.exists(stamp) or os.path.getmtime(stamp) < newest:
         subprocess.check_call(["python3", os.path.join(ROOT, "oracle", "ts_erase.py"), "--out", REF_OUT],
                               stdout=subprocess.DEVNULL)
     return REF_OUT

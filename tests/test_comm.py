@@ -43,15 +43,13 @@ def test_unique_id_exchange_between_processes(tmp_path, monkeypatch):
 
 
 def test_strong_shards_cover_the_job():
-    # bench.py's strong scaling: 10k docs over N ranks, ceil-sized shards
+    # bench.py's strong scaling: 10k docs over N ranks by expected work (LPT)
+    from fluidframework_amd import dist as fdist
     for world in (1, 2, 3, 4, 8):
-        per = (10000 + world - 1) // world
-        shards = []
-        for rank in range(world):
-            b = min(10000, rank * per)
-            shards.append((b, max(0, min(10000, b + per) - b)))
-        assert sum(n for _, n in shards) == 10000
-        assert [b for b, _ in shards] == sorted(b for b, _ in shards)
+        rank_of = fdist.shard_by_work(np.full(10000, 10000.0), world)
+        sizes = [len(fdist.rank_docs(rank_of, r)) for r in range(world)]
+        assert sum(sizes) == 10000 and max(sizes) - min(sizes) <= 1
+        assert fdist.docs_per_rank(rank_of, world) == max(sizes)
 
 
 @pytest.mark.gpu
@@ -67,7 +65,7 @@ def test_gpu_one_rank_communicator():
     gen.load_stream(e, s)
     e.apply_batch(s["batch"])
     e.comm_share(node)
-    g = e.comm_gather_digests(1, 64)
+    g = e.comm_gather_digests(64)
     np.testing.assert_array_equal(g[0, :50], e.digest())
     assert (g[0, 50:] == 0).all()
     e.comm_destroy()

@@ -317,11 +317,12 @@ for (let i = 0; i < 32; i++) bb2.addRegen(0, cl);
 let code = 0;
 try { bb2.addRegen(0, cl); } catch (e) { code = e.code; }
 const bb3 = new p.BatchBuilder(1, it);
-for (let s = 1; s <= 2; s++)
-  bb3.addMessage(0, cl, {clientId: 'me', sequenceNumber: s, referenceSequenceNumber: 0, minimumSequenceNumber: 0,
+let ackCode = 0;
+try {
+  bb3.addMessage(0, cl, {clientId: 'me', sequenceNumber: 1, referenceSequenceNumber: 0, minimumSequenceNumber: 0,
                          type: 'op', contents: {}});
-process.stdout.write(JSON.stringify({bs, code, acks: bb3.docOps[0].map((r) => r.slice(6, 9)),
-                                     free: 32 - cl.annSlot.size}));
+} catch (e) { ackCode = e.code; }
+process.stdout.write(JSON.stringify({bs, code, ackCode, free: 32 - cl.annSlot.size}));
 """
     r = subprocess.run([shutil.which("node"), "-e", script], cwd=root, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -329,9 +330,10 @@ process.stdout.write(JSON.stringify({bs, code, acks: bb3.docOps[0].map((r) => r.
     from fluidframework_amd.abi import NO_PROPS
     assert j["bs"] == list(range(32)) + [NO_PROPS]
     assert j["code"] == MTE_E_UNSUPPORTED
-    # the 32 regenerated messages moved behind the untracked one: the first ack
-    # is localSeq 33 (no slot), the second localSeq 1 (slot 0: mask 1 << 0)
-    assert j["acks"] == [[33, 33, 0], [1, 1, 1]] and j["free"] == 1
+    # the 32 regenerated messages moved behind the untracked one: the next ack
+    # would be localSeq 33's while 1..32 are pending annotates, whose pending
+    # keys an ack up to 33 would clear: refused
+    assert j["ackCode"] == MTE_E_UNSUPPORTED and j["free"] == 0
     # the Python packer, the same sequence
     it = Interner(4)
     me = DocClients("me", local=True)
@@ -339,3 +341,49 @@ process.stdout.write(JSON.stringify({bs, code, acks: bb3.docOps[0].map((r) => r.
     for _ in range(33):
         bb.add_local(0, me, {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1}})
     assert [int(r[9]) for r in bb.ops[0]] == j["bs"]
+
+
+def test_ack_order_after_partial_regen_is_refused_in_both_packers():
+    """Regenerating only the oldest of two pending annotates moves it behind the
+    second, so the second is acked first; the engine clears pending keys up to
+    the acked localSeq, which would drop the first's keys: both packers refuse
+    that ack.  Regenerating every pending op in order (the runtime's reconnect)
+    keeps the acks in order and is accepted."""
+    ann = {"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1}}
+    ack = {"clientId": "me", "sequenceNumber": 1, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
+           "type": "op", "contents": {}}
+    for full in (False, True):
+        it = Interner(4)
+        me = DocClients("me", local=True)
+        bb = BatchBuilder(1, it)
+        bb.add_local(0, me, ann)
+        bb.add_local(0, me, ann)
+        bb.add_regen(0, me)
+        if full:
+            bb.add_regen(0, me)
+            bb.add_message(0, me, ack)
+        else:
+            with pytest.raises(MergeTreeError) as ei:
+                bb.add_message(0, me, ack)
+            assert ei.value.code == MTE_E_UNSUPPORTED
+    root = os.path.dirname(HERE)
+    script = r"""
+const p = require('./fluidframework_amd/node/packing');
+const out = [];
+for (const full of [false, true]) {
+  const it = new p.Interner(4), cl = new p.DocClients('me', 0, true), bb = new p.BatchBuilder(1, it);
+  const ann = {type: 2, pos1: 0, pos2: 1, props: {a: 1}};
+  bb.addLocal(0, cl, ann); bb.addLocal(0, cl, ann); bb.addRegen(0, cl);
+  if (full) bb.addRegen(0, cl);
+  let code = 0;
+  try {
+    bb.addMessage(0, cl, {clientId: 'me', sequenceNumber: 1, referenceSequenceNumber: 0, minimumSequenceNumber: 0,
+                          type: 'op', contents: {}});
+  } catch (e) { code = e.code; }
+  out.push(code);
+}
+process.stdout.write(JSON.stringify(out));
+"""
+    r = subprocess.run([shutil.which("node"), "-e", script], cwd=root, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads(r.stdout) == [MTE_E_UNSUPPORTED, 0]
