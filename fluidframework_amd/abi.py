@@ -42,6 +42,7 @@ ERROR_NAMES = {
 
 OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_ACK, OP_ROLLBACK = 0, 1, 2, 3, 4, 5
 OP_REGEN = 6          # Client.regeneratePendingOp (a local record; include/mte.h)
+OP_RBKEY = 7          # an annotate rollback's previous-value candidates (include/mte.h)
 DELTA_REGEN = 0x10    # kind flag of its output records
 ANNOTATE_SLOTS = 32   # pending local annotate groups tracked per document
 F_MARKER, F_MSG_END, F_REWRITE, F_LOCAL = 0x1, 0x2, 0x4, 0x8

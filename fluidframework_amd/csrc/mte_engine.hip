@@ -141,6 +141,8 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
     for (uint32_t k = 0; k < kt; k++)
       for (uint32_t x = 0; x < nz; x++) soa.props[(kt + k) * soa.plane_stride + (uint64_t)d * cap + x] = 0u;
     for (uint32_t x = 0; x < nz; x++) soa.props[2ull * kt * soa.plane_stride + (uint64_t)d * cap + x] = 0u;  // no groups
+    for (uint32_t k = 0; k < kt; k++)
+      for (uint32_t x = 0; x < nz; x++) soa.props[(2ull * kt + 1 + k) * soa.plane_stride + (uint64_t)d * cap + x] = 0u;
   }
   if (n_img) return;  // image_kernel writes the segments
   const uint64_t i = (uint64_t)d * cap;
@@ -406,7 +408,8 @@ struct mte_ctx {
   uint4* d_cps = nullptr;
   uint64_t n_ops = 0, n_propsets = 0;
   uint32_t* d_pairs = nullptr;  // pass-1 doc pairs (new length calc documents)
-  uint32_t n_pairs = 0;
+  uint32_t n_pairs = 0;         // pass-1 waves
+  uint32_t pass1_group = 1;     // documents per pass-1 wave
   // tree pass (legacy length calc documents, mte_tree.h)
   uint32_t* d_tree = nullptr;       // tree word per slot
   uint2* d_heap = nullptr;          // LRU heap per document
@@ -596,14 +599,21 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
 // Validation of one op record (the kernels index with these fields, so a bad
 // record must never reach them).  Returns nullptr or the reason.
 const char* bad_op(const mte_op& o, const mte_batch* b, bool local_doc) {
-  if (o.type > MTE_OP_REGEN) return "type";
+  if (o.type > MTE_OP_RBKEY) return "type";
   if (o.type >= MTE_OP_ROLLBACK && !(o.flags & MTE_F_LOCAL)) return "rollback / regen without MTE_F_LOCAL";
   if ((o.flags & MTE_F_LOCAL) && o.type == MTE_OP_ANNOTATE && o.b != MTE_NO_PROPS && o.b >= MTE_ANNOTATE_SLOTS)
     return "annotate group slot out of range";
   if ((o.flags & MTE_F_LOCAL) || o.type == MTE_OP_ACK) {
     if (!local_doc) return "local op or ack in a document without MTE_DOC_LOCAL_CLIENT";
-    if ((o.flags & MTE_F_LOCAL) && (o.type == MTE_OP_ACK || o.seq <= 0 || o.seq >= MTE_LOCAL_SEQ_BASE))
+    if ((o.flags & MTE_F_LOCAL) && o.type != MTE_OP_RBKEY &&
+        (o.type == MTE_OP_ACK || o.seq <= 0 || o.seq >= MTE_LOCAL_SEQ_BASE))
       return "local record: type or localSeq out of range";
+    if (o.type == MTE_OP_RBKEY && (o.seq < 0 || o.seq >= MTE_LOCAL_SEQ_BASE || o.pos1 < 0 ||
+                                   o.pos1 >= MTE_MAX_KEYS || o.pos2 < 0 || o.pos2 > MTE_ANNOTATE_SLOTS))
+      return "rollback key record out of range";
+    if (o.type == MTE_OP_ROLLBACK && o.pos1 == MTE_OP_ANNOTATE &&
+        (o.a >= MTE_ANNOTATE_SLOTS || o.pos2 < 0 || o.pos2 > MTE_MAX_KEYS * (MTE_ANNOTATE_SLOTS + 1)))
+      return "annotate rollback: group slot or key record count out of range";
     if (o.type == MTE_OP_ACK && (o.pos1 <= 0 || o.pos1 > o.pos2)) return "ack: localSeq range";
   }
   if (local_doc && !(o.flags & MTE_F_LOCAL) && o.seq >= MTE_LOCAL_SEQ_BASE) return "seq >= MTE_LOCAL_SEQ_BASE";
@@ -829,9 +839,10 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     if (docs[d].flags & MTE_DOC_LOCAL_CLIENT) c->h_local[d] = 1, any_local = true;
     if (docs[d].flags & MTE_DOC_EVENTS) c->h_events[d] = 1;
   }
-  // documents with a local client hold kt more planes: the pending property keys (mte_stream.h)
-  // + per local doc: the pending-key planes and the annotate-group plane (mte_stream.h)
-  const uint64_t prop_planes = (c->kt ? c->kt : 1) + (any_local ? c->kt + 1 : 0);
+  // documents with a local client hold 2 kt + 1 more planes (mte_stream.h): the
+  // pending property keys, the annotate-group mask and the keys' values before
+  // their first pending annotate
+  const uint64_t prop_planes = (c->kt ? c->kt : 1) + (any_local ? 2 * c->kt + 1 : 0);
   HIPCHK(c, hipMalloc((void**)&c->hdr, sizeof(DocHdr) * (n_docs ? n_docs : 1)));
   // one allocation, planes at stride nslots: len seq rseq rmask meta toff props[kt]
   // (kt >= n_keys planes, so the register-resident kernels never index past it)
@@ -872,10 +883,11 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
   HIPCHK(c, hipMalloc((void**)&c->d_init_props, sizeof(uint32_t) * iprops.size() + 4));
   HIPCHK(c, hipMalloc((void**)&c->d_digest, sizeof(uint64_t) * 4 * (n_docs ? n_docs : 1)));
   {
-    // pass-1 pairs: docs (2p, 2p+1), an odd last doc alone.  A batch that fits
-    // the chip at one document per wave (<= CUs x 4 SIMDs x MTE_PAIR_WAVES,
-    // e.g. config 2's 1k docs) runs one per wave instead: pairing it would
-    // leave SIMDs idle and serialise two documents per wave.
+    // pass-1 groups: g consecutive documents per wave, g the smallest count
+    // that puts the whole batch on the chip at once (CUs x 4 SIMDs x
+    // pass1_waves() waves), so a batch that fits at one document per wave
+    // (config 2's 1k docs, the 1,250 per GPU of an 8-GPU 10k job) runs one per
+    // wave: grouping it would leave SIMDs idle and serialise its documents.
     // Legacy length-calc documents go to the tree pass instead (mte_tree.h).
     // Round-synchronous legacy documents (MTE_DOC_ROUND_SYNC) stay flat, behind
     // the per-batch check of round_sync_kernel.
@@ -897,10 +909,12 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     const uint32_t nf = (uint32_t)flat_docs.size();
     int n_cu = 0;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) n_cu = 0;
-    const bool solo = n_cu > 0 && (uint64_t)nf <= (uint64_t)n_cu * 4 * MTE_PAIR_WAVES;
-    c->n_pairs = solo ? nf : (nf + 1) / 2;
-    std::vector<uint32_t> pairs((size_t)c->n_pairs * 2 + 2, 0xffffffffu);
-    for (uint32_t i = 0; i < nf; i++) pairs[solo ? 2 * (size_t)i : i] = flat_docs[i];
+    const uint64_t resident = (n_cu > 0 ? (uint64_t)n_cu : 256) * 4 * (uint64_t)pass1_waves();
+    const uint32_t g = (uint32_t)std::min<uint64_t>(kGroupMax, std::max<uint64_t>(1, (nf + resident - 1) / resident));
+    c->pass1_group = g;
+    c->n_pairs = (nf + g - 1) / g;
+    std::vector<uint32_t> pairs((size_t)c->n_pairs * g + g, 0xffffffffu);
+    for (uint32_t i = 0; i < nf; i++) pairs[i] = flat_docs[i];
     HIPCHK(c, hipMalloc((void**)&c->d_pairs, pairs.size() * 4));
     HIPCHK(c, hipMemcpy(c->d_pairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice));
     c->n_rs = (uint32_t)rs_docs.size();
@@ -1140,6 +1154,7 @@ int mte_run(mte_ctx* c) {
   a.stats = c->stats;
   a.pair_docs = c->d_pairs;
   a.n_pairs = c->n_pairs;
+  a.group = c->pass1_group;
   a.wclock = nullptr;
   a.gdone = c->d_gdone;
   a.n_ops = c->n_ops;

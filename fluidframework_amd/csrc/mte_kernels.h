@@ -23,7 +23,8 @@ constexpr int kWave = 64;
 constexpr int32_t kNone = INT32_MAX;  // removedSeq undefined (not removed)
 constexpr int32_t kPad = INT32_MIN;   // removedSeq of a padding slot
 constexpr int kDocsPerBlock = 4;      // big-doc kernel: 4 waves (docs) per workgroup
-constexpr int kPairsPerBlock = 4;     // pair kernel: 4 waves x 2 docs per workgroup
+constexpr int kPairsPerBlock = 4;     // pass-1 kernel: 4 waves per workgroup
+constexpr int kGroupMax = 8;          // pass 1: at most this many documents per wave
 
 // per-doc header in HBM (32 B)
 struct DocHdr {
@@ -89,8 +90,9 @@ struct ReplayArgs {
   uint32_t n_keys;
   uint32_t text_base;      // arena offset of the batch's text (mte_op.a of inserts)
   unsigned long long* stats;  // n_docs * kNumStats
-  const uint32_t* pair_docs;  // pair kernel: doc index per pair half (2 per pair)
-  uint32_t n_pairs;
+  const uint32_t* pair_docs;  // pass 1: `group` document indices per wave (-1: none)
+  uint32_t n_pairs;           // pass-1 waves
+  uint32_t group;             // pass 1: documents per wave (1 .. kGroupMax)
   unsigned long long* wclock;  // diagnostics (MTE_WAVE_CLOCK): pass-1 start / end time per pair, or null
   unsigned long long* gdone;   // pass 1: ops applied so far by all waves (fair priority), zeroed per run
   unsigned long long n_ops;    // ops of the batch

@@ -8,9 +8,12 @@ namespace mte {
 
 template <int K, bool S>
 hipError_t launch_pair(const ReplayArgs& a, uint32_t blocks, hipStream_t s) {
-  hipLaunchKernelGGL((pair_kernel<K, S, kPairsPerBlock>), dim3(blocks), dim3(kPairsPerBlock * kWave), 0, s, a);
+  hipLaunchKernelGGL((pair_kernel<K, S, kPairsPerBlock, MTE_PAIR_WAVES>), dim3(blocks), dim3(kPairsPerBlock * kWave),
+                     0, s, a);
   return hipGetLastError();
 }
+
+int pass1_waves() { return MTE_PAIR_WAVES; }
 
 template <int K, bool S>
 hipError_t launch_big(const ReplayArgs& a, uint32_t blocks, hipStream_t s) {

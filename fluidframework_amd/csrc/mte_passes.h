@@ -19,9 +19,12 @@ struct ChunkArgs;
 template <int K, bool S>
 hipError_t launch_tree(const ReplayArgs& a, const TreeArgs& t, uint32_t blocks, hipStream_t s, int rounds,
                        uint32_t per_round);
-// pass 1 (two documents per wavefront) and pass 2 (one per wavefront)
+// pass 1 (ReplayArgs::group documents per wavefront) and pass 2 (one per
+// wavefront); pass1_waves() = the waves per SIMD pass 1's register budget is
+// built for (the host sizes the groups so the batch is resident at once)
 template <int K, bool S>
 hipError_t launch_pair(const ReplayArgs& a, uint32_t blocks, hipStream_t s);
+int pass1_waves();
 template <int K, bool S>
 hipError_t launch_big(const ReplayArgs& a, uint32_t blocks, hipStream_t s);
 // pass 3: HBM-streamed (mte_stream.h) or chunked (mte_chunk.h)

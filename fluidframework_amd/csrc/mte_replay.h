@@ -25,7 +25,7 @@
 // 3 = bands around the global progress (one returning atomic per burst; measured 33.9 ms vs
 // 23.9 ms on config 3: the single contended counter costs more than the balance gains),
 // 4 = bands around the previous run's schedule (product: 22.6 ms; band 1 on the first run).
-#ifndef MTE_PAIR_WAVES
+#ifndef MTE_PAIR_WAVES  // pass-1 waves per SIMD the register budget is sized for (5: 96 VGPRs, 4: 128)
 #define MTE_PAIR_WAVES 5
 #endif
 #ifndef MTE_BURST
@@ -45,6 +45,9 @@
 #endif
 #ifndef MTE_OUTLINE  // 1: pass-1 tiers as out-of-line functions (measured: same time, 1.7x the HBM traffic)
 #define MTE_OUTLINE 0
+#endif
+#ifndef MTE_OUTLINE_E4  // 1: only the rare E = 4 tier out of line (the E <= 2 loops get the registers)
+#define MTE_OUTLINE_E4 0
 #endif
 
 namespace mte {
@@ -846,11 +849,17 @@ __device__ __forceinline__ void pass1_burst(DocRun& D, const ReplayArgs& a, uint
   else if constexpr (MTE_PASS1_EMAX >= 4) {
     if (e == 4) burst_out<4, K, S>(D, a, zlds);
   }
+#elif defined(MTE_ISA_STUDY)  // ISA inspection only: one tier
+  if (e) burst_run<MTE_ISA_STUDY, K, S>(D, a, zlds, 1, kBurst);
 #else
   if (e == 1) burst_run<1, K, S>(D, a, zlds, 1, kBurst);
   else if (e == 2) burst_run<2, K, S>(D, a, zlds, 1, kBurst);
   else if constexpr (MTE_PASS1_EMAX >= 4) {
+#if MTE_OUTLINE_E4
+    if (e == 4) burst_out<4, K, S>(D, a, zlds);
+#else
     if (e == 4) burst_run<4, K, S>(D, a, zlds, 1, kBurst);
+#endif
   }
 #endif
 }
@@ -908,47 +917,44 @@ __device__ __forceinline__ void fair_prio(uint32_t left, uint32_t total) {
   }
 }
 
-// pass 1: two documents per wavefront, replayed in alternating bursts, so a
-// 10k-document batch is resident on the chip at once with the register
-// budget of one document (E <= 4)
-template <int K, bool S, int WPB>
-__global__ __launch_bounds__(WPB * kWave, MTE_PAIR_WAVES * 4 / WPB) void pair_kernel(ReplayArgs a) {
+// pass 1: `a.group` documents per wavefront (1 when the batch fits the chip
+// at one per wave), replayed in turn one burst each, so a 10k-document batch is
+// resident on the chip at once with the register budget of one document
+// (E <= 4); W = waves per SIMD the register budget is sized for
+template <int K, bool S, int WPB, int W>
+__global__ __launch_bounds__(WPB * kWave, W * 4 / WPB) void pair_kernel(ReplayArgs a) {
   __shared__ uint32_t zlds_all[WPB][kWave * 4];
-  __shared__ DocHdr hl_all[WPB][2];
+  __shared__ DocHdr hl_all[WPB][kGroupMax];
   const int w = WPB == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
   const int pair = (int)blockIdx.x * WPB + w;
   if (pair >= (int)a.n_pairs) return;
   if (a.wclock && lane_id() == 0) a.wclock[2 * pair] = __builtin_amdgcn_s_memrealtime();
-  int docs[2] = {(int)a.pair_docs[2 * pair], (int)a.pair_docs[2 * pair + 1]};
-  if (docs[1] == docs[0]) docs[1] = -1;
+  const int g = (int)a.group;
   DocHdr* hl = hl_all[w];
   uint32_t* zlds = zlds_all[w];
   uint32_t live = 0;  // bit t: document t still has ops to run in this pass
-#pragma unroll
-  for (int t = 0; t < 2; t++) {
-    if (docs[t] >= 0) {
-      DocHdr h = a.hdr[docs[t]];
+  uint32_t total = 0;  // ops of the group in this pass, and those left (for fair_prio)
+  for (int t = 0; t < g; t++) {
+    const int doc = (int)a.pair_docs[(uint32_t)g * (uint32_t)pair + (uint32_t)t];
+    if (doc >= 0) {
+      DocHdr h = a.hdr[doc];
       h.flags &= ~kHdrNeedsEsc;
       if (lane_id() == 0) hl[t] = h;
       live |= 1u << t;
+      total += (uint32_t)(a.op_off[doc + 1] - a.op_off[doc]) - h.resume;
     }
   }
   fence_wave();
-  // ops of the pair in this pass, and those left (for fair_prio)
-  uint32_t total = 0;
-#pragma unroll
-  for (int t = 0; t < 2; t++)
-    if (docs[t] >= 0) total += (uint32_t)(a.op_off[docs[t] + 1] - a.op_off[docs[t]]) - hl[t].resume;
   total = uni(total);
   uint32_t left = total;
   [[maybe_unused]] const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   if constexpr (MTE_FAIR_PRIO == 4) __builtin_amdgcn_s_setprio(2);
   else fair_prio(left, total);
-  // one burst per iteration, alternating between the two documents; a single
-  // copy of the burst code serves both (the document is a runtime index)
-  for (int t = 0; live; t ^= 1) {
+  // one burst per iteration, the documents in turn; a single copy of the
+  // burst code serves them all (the document is a runtime index)
+  for (int t = 0; live; t = (t + 1 == g) ? 0 : t + 1) {
     if (!(live & (1u << t))) continue;
-    const int doc = t ? docs[1] : docs[0];
+    const int doc = (int)a.pair_docs[(uint32_t)g * (uint32_t)pair + (uint32_t)t];
     DocRun D;
     const uint32_t k0 = hl[t].resume;
     if (run_from_lds(D, &hl[t], doc, a)) pass1_burst<K, S>(D, a, zlds);
@@ -959,11 +965,11 @@ __global__ __launch_bounds__(WPB * kWave, MTE_PAIR_WAVES * 4 / WPB) void pair_ke
     if constexpr (MTE_FAIR_PRIO == 3) {
       // progress relative to all waves: the global count of applied ops comes
       // back from the atomic that adds this burst (its old value)
-      unsigned long long g = 0;
-      if (lane_id() == 0) g = atomicAdd(a.gdone, (unsigned long long)ran);
-      g = ((unsigned long long)uni((uint32_t)(g >> 32)) << 32) | uni((uint32_t)g);
+      unsigned long long gl = 0;
+      if (lane_id() == 0) gl = atomicAdd(a.gdone, (unsigned long long)ran);
+      gl = ((unsigned long long)uni((uint32_t)(gl >> 32)) << 32) | uni((uint32_t)gl);
       const unsigned long long mine = (unsigned long long)(total - left) * a.n_ops;  // my fraction x n_ops x total
-      const unsigned long long all = g * total;
+      const unsigned long long all = gl * total;
       const unsigned long long band = (unsigned long long)total * a.n_ops / 64;  // 1/64 of the work
       if (mine + band < all) __builtin_amdgcn_s_setprio(3);
       else if (mine < all) __builtin_amdgcn_s_setprio(2);
@@ -989,9 +995,10 @@ __global__ __launch_bounds__(WPB * kWave, MTE_PAIR_WAVES * 4 / WPB) void pair_ke
     }
   }
   if (lane_id() == 0) {
-#pragma unroll
-    for (int t = 0; t < 2; t++)
-      if (docs[t] >= 0) a.hdr[docs[t]] = hl[t];  // resume = the op cursor
+    for (int t = 0; t < g; t++) {
+      const int doc = (int)a.pair_docs[(uint32_t)g * (uint32_t)pair + (uint32_t)t];
+      if (doc >= 0) a.hdr[doc] = hl[t];  // resume = the op cursor
+    }
     if (a.wclock) a.wclock[2 * pair + 1] = __builtin_amdgcn_s_memrealtime();
   }
 }

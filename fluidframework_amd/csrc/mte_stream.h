@@ -77,6 +77,10 @@ __device__ __forceinline__ void tile_load_hot(Regs<kTileE, K>& R, const uint32_t
 constexpr int32_t kLocalBase = MTE_LOCAL_SEQ_BASE;
 template <int K>
 constexpr int kAnnPlane = kFieldPlanes + 2 * K;
+// K more after it: per key, the value before the first pending local annotate
+// set it (what that annotate's rollback puts back, MTE_OP_RBKEY)
+template <int K>
+constexpr int kBasePlane = kFieldPlanes + 2 * K + 1;
 constexpr int kPlaneGroup = 5;  // planes moved per batch of loads (all in flight, then the stores)
 
 // the local client's own view (localNetLength, mergeTree.ts:553-573, new
@@ -237,6 +241,119 @@ __device__ __forceinline__ void stream_rollback(uint32_t* pl, uint64_t sd, int n
   vm_drain();
 }
 
+// MTE_OP_ROLLBACK of a local annotate (group slot b), followed by its n_aux
+// MTE_OP_RBKEY records at aux: MergeTree.rollback -> annotateRange of each
+// segment of the group with its previousProps under PropertiesRollback.Rollback
+// (mergeTree.ts:2036-2072, segmentPropertiesManager.ts:63-151): per key the
+// annotate set, the value of the first candidate (latest older pending annotate
+// of the key) whose group holds the segment -- its localSeq the key's pending
+// one -- else the base plane's value, no longer pending.  Each segment's
+// annotate event at its own-view position.  A segment of the group removed
+// since: MTE_E_UNSUPPORTED (include/mte.h).
+template <int K>
+__device__ __forceinline__ int stream_rollback_annotate(uint32_t* pl, uint64_t sd, int n, uint32_t b,
+                                                        const uint4* aux, uint32_t n_aux, bool evd, EvOut& ev) {
+  const int l = lane_id();
+  int32_t ocy = 0;
+  for (int tb = 0; tb < n; tb += kTile) {
+    bool hit[kTileE], bad = false;
+    int32_t OL[kTileE], OP[kTileE], len[kTileE];
+    uint32_t am[kTileE];
+#pragma unroll
+    for (int j = 0; j < kTileE; j++) {
+      const int i = tb + l * kTileE + j;
+      const bool v = i < n;
+      const int ic = v ? i : 0;  // unconditional loads, selected after
+      const int32_t l0 = (int32_t)ld_l2(pl + ic), l2 = (int32_t)ld_l2(pl + 2 * sd + ic);
+      const uint32_t xa = ld_l2(pl + (uint64_t)kAnnPlane<K> * sd + ic);
+      len[j] = v ? l0 : 0;
+      const int32_t rs = v ? l2 : kPad;
+      am[j] = v ? xa : 0u;
+      hit[j] = v && ((am[j] >> b) & 1u);
+      bad = bad || (hit[j] && rs != kNone);
+      OL[j] = (v && rs == kNone) ? len[j] : 0;
+    }
+    if (__ballot(bad)) {
+      vm_drain();
+      return MTE_E_UNSUPPORTED;
+    }
+    for (uint32_t q = 0; q < n_aux;) {
+      const uint32_t key = uni((uint32_t)sload8(aux + 2 * q)[4]);
+      if (key >= (uint32_t)K) {
+        vm_drain();
+        return MTE_E_INVALID_ARG;
+      }
+      bool done[kTileE];
+      uint32_t val[kTileE], pk[kTileE];
+#pragma unroll
+      for (int j = 0; j < kTileE; j++) {
+        done[j] = false;
+        val[j] = 0u;
+        pk[j] = 0u;
+      }
+      for (;;) {  // the key's candidates, latest first, then its base entry
+        if (q >= n_aux) {
+          vm_drain();
+          return MTE_E_INVALID_ARG;
+        }
+        const s8v rr = sload8(aux + 2 * q);
+        q++;
+        const uint32_t slot = (uint32_t)rr[5];
+        if ((uint32_t)rr[4] != key) {
+          vm_drain();
+          return MTE_E_INVALID_ARG;
+        }
+        if (slot >= MTE_ANNOTATE_SLOTS) {
+#pragma unroll
+          for (int j = 0; j < kTileE; j++) {
+            const int i = tb + l * kTileE + j;
+            const uint32_t bv = ld_l2(pl + (uint64_t)(kBasePlane<K> + key) * sd + (hit[j] ? i : 0));
+            val[j] = done[j] ? val[j] : bv;
+          }
+          break;
+        }
+#pragma unroll
+        for (int j = 0; j < kTileE; j++) {
+          const bool take = hit[j] && !done[j] && ((am[j] >> slot) & 1u);
+          val[j] = take ? (uint32_t)rr[6] : val[j];
+          pk[j] = take ? (uint32_t)rr[0] : pk[j];
+          done[j] = done[j] || take;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kTileE; j++) {
+        const int i = tb + l * kTileE + j;
+        if (hit[j]) {
+          pl[(uint64_t)(kFieldPlanes + key) * sd + i] = val[j];
+          pl[(uint64_t)(kFieldPlanes + K + key) * sd + i] = pk[j];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kTileE; j++)
+      if (hit[j]) pl[(uint64_t)kAnnPlane<K> * sd + tb + l * kTileE + j] = am[j] & ~(1u << b);
+    if (evd) {
+      const int32_t otot = prefix<kTileE>(OL, OP);
+      uint32_t ecnt = 0;
+#pragma unroll
+      for (int j = 0; j < kTileE; j++) ecnt += hit[j] ? 1u : 0u;
+      const int32_t eincl = wave_incl_scan((int32_t)ecnt);
+      uint32_t e = ev.n + (uint32_t)(eincl - (int32_t)ecnt);
+#pragma unroll
+      for (int j = 0; j < kTileE; j++) {
+        if (hit[j]) {
+          if (e < ev.cap) ev.p[e] = mte_delta{ev.op, (uint32_t)MTE_OP_ANNOTATE, ocy + OP[j], len[j], 0u};
+          e++;
+        }
+      }
+      ev.n += (uint32_t)rdlane(eincl, kWave - 1);
+      ocy += otot;
+    }
+  }
+  vm_drain();
+  return 0;
+}
+
 // MTE_OP_REGEN: Client.regeneratePendingOp of the pending op of localSeq ls,
 // type t (client.ts:972-1002 -> resetPendingDeltaToOps :788-860): its segment
 // group in document order, each at its position in the view at localSeq ls
@@ -306,7 +423,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   const bool ldoc = (D.flags & MTE_DOC_LOCAL_CLIENT) != 0;
   const bool evd = (D.flags & MTE_DOC_EVENTS) != 0;
   ev.op = D.k;
-  const int nplanes = kFieldPlanes + K + (ldoc ? K + 1 : 0);  // + the pending-key and group planes
+  const int nplanes = kFieldPlanes + K + (ldoc ? 2 * K + 1 : 0);  // + the pending-key, group and base planes
 
   const s8v op = cur;
   const uint4* rec = D.recp + 2 * D.k;
@@ -314,7 +431,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
-  if (type > MTE_OP_REGEN) return MTE_E_INVALID_ARG;
+  if (type > MTE_OP_REGEN) return MTE_E_INVALID_ARG;  // MTE_OP_RBKEY only after an annotate's rollback
   const bool lop = (flags & MTE_F_LOCAL) != 0;  // a local op: the local view, seq = localSeq
   if ((lop || type >= MTE_OP_ACK) && !ldoc) return MTE_E_UNSUPPORTED;
   MTE_STAT(st[kStOps]++;)
@@ -323,7 +440,17 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   const int32_t pos1 = op[4], pos2 = op[5];
   if (type == MTE_OP_ROLLBACK) {
     if (!lop || !(s > 0 && s <= lseq)) return MTE_E_INVALID_ARG;
-    if (pos1 != MTE_OP_INSERT && pos1 != MTE_OP_REMOVE) return MTE_E_UNSUPPORTED;
+    if (pos1 == MTE_OP_ANNOTATE) {
+      const uint32_t n_aux = (uint32_t)pos2;
+      if ((uint64_t)D.k + 1 + n_aux > D.k1 || (uint32_t)op[6] >= MTE_ANNOTATE_SLOTS) return MTE_E_INVALID_ARG;
+      MTE_STAT(st[kStScanned] += (uint32_t)D.n;)
+      const int rc = stream_rollback_annotate<K>(pl, sd, D.n, (uint32_t)op[6], rec + 2, n_aux, evd, ev);
+      if (rc) return rc;
+      D.k += 1 + n_aux;
+      if (D.k < D.k1) cur = sload8(D.recp + 2 * D.k);
+      return 0;
+    }
+    if (pos1 != MTE_OP_INSERT && pos1 != MTE_OP_REMOVE) return MTE_E_INVALID_ARG;
     MTE_STAT(st[kStScanned] += (uint32_t)D.n;)
     stream_rollback(pl, sd, D.n, s, (uint32_t)pos1, evd, ev);
     D.k++;
@@ -666,11 +793,20 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
               for (int j = 0; j < E; j++) pr[kk][j] = pk[kk][j] ? old[kk][j] : pr[kk][j];
           }
           if (lop) {
-            // the local annotate's keys become pending on the marked slots
+            // the local annotate's keys become pending on the marked slots; a key
+            // not pending yet keeps its value in the base plane (what this
+            // annotate's rollback puts back when no older one set the key)
             const mte_propset ps = a.ps[(uint32_t)op[6]];
             for (uint32_t t = 0; t < ps.count; t++) {
               const uint32_t key = uni(a.pe[ps.first + t].key);
               if (key < (uint32_t)K) {
+#pragma unroll
+                for (int kk = 0; kk < K; kk++) {
+                  if ((uint32_t)kk != key) continue;
+#pragma unroll
+                  for (int j = 0; j < E; j++)
+                    if (in[j] && pk[kk][j] == 0u) pl[(uint64_t)(kBasePlane<K> + kk) * sd + base + j] = old[kk][j];
+                }
 #pragma unroll
                 for (int j = 0; j < E; j++)
                   if (in[j]) pl[(kFieldPlanes + K + key) * sd + base + j] = (uint32_t)s;

@@ -204,7 +204,7 @@ export class BatchClient {
   /** Client.regeneratePendingOp for reconnection: the op re-sending the oldest
    *  pending op (resetOp as sent); needs {localClient: true, events: true}. */
   regeneratePendingOp(resetOp: IMergeTreeOp): IMergeTreeOp;
-  /** Client.rollback of the latest pending local op (inserts and removes). */
+  /** Client.rollback of the latest pending local op (inserts, removes and annotates). */
   rollback(op?: IMergeTreeOp): void;
   /** SharedString "sequenceDelta" events ({events: true} documents), delivered at each flush in op order. */
   on(name: "sequenceDelta", listener: (event: SequenceDeltaEvent, client: BatchClient) => void): this;

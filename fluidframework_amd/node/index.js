@@ -511,8 +511,8 @@ class BatchClient {
 
   /** Client.rollback (client.ts:396-398 -> MergeTree.rollback,
    *  mergeTree.ts:2005-2083) of this client's latest pending op, which must not
-   *  have been sent: its inserts disappear, its removes are undone.  Rolling
-   *  back an annotate is not supported. */
+   *  have been sent: its inserts disappear, its removes are undone, its
+   *  annotates put the previous values back (previousProps). */
   rollback(op) {  // eslint-disable-line no-unused-vars
     this.engine._batch().addRollback(this.doc, this.clients);
   }

@@ -29,6 +29,7 @@
  */
 
 const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 3, OP_ACK = 4, OP_ROLLBACK = 5, OP_REGEN = 6;
+const OP_RBKEY = 7;          // MTE_OP_RBKEY: an annotate rollback's previous-value candidates
 const DELTA_REGEN = 0x10;    // MTE_DELTA_REGEN: kind flag of a regenerated op's records
 const ANNOTATE_SLOTS = 32;   // MTE_ANNOTATE_SLOTS: pending local annotate groups tracked per document
 const F_MARKER = 0x1, F_MSG_END = 0x2, F_REWRITE = 0x4, F_LOCAL = 0x8;
@@ -137,6 +138,11 @@ class DocClients {
     // segment groups of pending local annotates: localSeq -> group slot; an
     // annotate made while all are taken is not tracked (cannot be regenerated)
     this.annSlot = new Map();
+    // the key -> value id each pending local annotate set (its rollback puts the
+    // older values back), and the annotates whose rollback the engine cannot
+    // restate exactly (as packing.py)
+    this.annProps = new Map();
+    this.noRollback = new Set();
   }
   short(longId, seq) {
     let i = this.ids.get(longId);
@@ -255,6 +261,15 @@ class BatchBuilder {
             mask |= 1 << clients.annSlot.get(ls);
             clients.annSlot.delete(ls);
           }
+          // an annotate acked under a later pending one on the same key (packing.py)
+          const keys = clients.annProps.get(ls);
+          if (keys) {
+            clients.annProps.delete(ls);
+            for (const [ls2, kv] of clients.annProps) {
+              if (ls2 > hi && Array.from(keys.keys()).some((k) => kv.has(k))) clients.noRollback.add(ls2);
+            }
+          }
+          clients.noRollback.delete(ls);
         }
         recs.push([OP_ACK, 0, lo, hi, mask >>> 0, NO_PROPS]);
       } else {
@@ -306,6 +321,10 @@ class BatchBuilder {
           clients.annSlot.set(first + i, free);
           b = free;
         }
+        const kv = new Map();
+        const f0 = this.props.sets[2 * r[4]], cnt = this.props.sets[2 * r[4] + 1];
+        for (let t = f0; t < f0 + cnt; t++) kv.set(this.props.entries[2 * t], this.props.entries[2 * t + 1]);
+        clients.annProps.set(first + i, kv);
       }
       this.docOps[doc].push([first + i, 0, 0, r[0], 0, r[1] | F_LOCAL, r[2], r[3], r[4], b]);
     });
@@ -322,16 +341,55 @@ class BatchBuilder {
       throw new MergeTreeError(E_STATE, "rollback without a pending local op");
     }
     const types = clients.pendingTypes[clients.pendingTypes.length - 1];
-    if (types.includes(OP_ANNOTATE)) throw new MergeTreeError(E_UNSUPPORTED, "rollback of an annotate");
-    const [lo, hi] = clients.pending.pop();
+    const [lo, hi] = clients.pending[clients.pending.length - 1];
+    // an annotate's MTE_OP_RBKEY records (packing.py add_rollback): per key it
+    // set, the older pending annotates that set the key, latest first, then the
+    // base entry; every check that can throw comes before any record
+    const aux = new Map();
+    for (let ls = hi; ls >= lo; ls--) {
+      if (types[ls - lo] !== OP_ANNOTATE) continue;
+      if (!clients.annSlot.has(ls) || clients.noRollback.has(ls)) {
+        throw new MergeTreeError(E_UNSUPPORTED, "rollback of an annotate the engine does not track");
+      }
+      const mine = clients.annProps.get(ls);
+      for (const [x, kv] of clients.annProps) {
+        if (x > ls && (x < lo || x > hi) && Array.from(mine.keys()).some((k) => kv.has(k))) {
+          throw new MergeTreeError(E_UNSUPPORTED, "rollback under a newer pending annotate of the same key");
+        }
+      }
+      const recs = [];
+      for (const k of mine.keys()) {
+        const older = Array.from(clients.annProps.keys()).filter((x) => x < ls && clients.annProps.get(x).has(k))
+          .sort((p, q) => q - p);
+        if (older.some((x) => !clients.annSlot.has(x))) {
+          throw new MergeTreeError(E_UNSUPPORTED, "rollback past an untracked pending annotate");
+        }
+        for (const x of older) {
+          recs.push([x, 0, 0, OP_RBKEY, 0, F_LOCAL, k, clients.annSlot.get(x), clients.annProps.get(x).get(k), NO_PROPS]);
+        }
+        recs.push([0, 0, 0, OP_RBKEY, 0, F_LOCAL, k, ANNOTATE_SLOTS, 0, NO_PROPS]);
+      }
+      aux.set(ls, recs);
+    }
+    clients.pending.pop();
     clients.pendingTypes.pop();
+    const src = this._src(doc);
+    const push = (rec) => {
+      this.docOps[doc].push(rec);
+      this.count++;
+      if (src) src.push({ msg: null, op: undefined, local: true });
+    };
     for (let ls = hi; ls >= lo; ls--) {
       const t = types[ls - lo];
-      if (t === OP_NOOP) continue;
-      this.docOps[doc].push([ls, 0, 0, OP_ROLLBACK, 0, F_LOCAL, t, 0, 0, NO_PROPS]);
-      this.count++;
-      const src = this._src(doc);
-      if (src) src.push({ msg: null, op: undefined, local: true });
+      if (t === OP_ANNOTATE) {
+        const recs = aux.get(ls);
+        push([ls, 0, 0, OP_ROLLBACK, 0, F_LOCAL, t, recs.length, clients.annSlot.get(ls), NO_PROPS]);
+        recs.forEach(push);
+        clients.annSlot.delete(ls);
+        clients.annProps.delete(ls);
+      } else if (t !== OP_NOOP) {
+        push([ls, 0, 0, OP_ROLLBACK, 0, F_LOCAL, t, 0, 0, NO_PROPS]);
+      }
     }
   }
 

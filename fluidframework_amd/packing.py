@@ -32,7 +32,7 @@ import numpy as np
 
 from .abi import (F_LOCAL, F_MARKER, F_MSG_END, F_REWRITE, LOCAL_SEQ_BASE, MTE_E_CLIENT_RANGE,
                   MTE_E_INVALID_ARG, MTE_E_STATE, MTE_E_UNSUPPORTED, MTE_MAX_CLIENTS, NO_PROPS, OP_ACK, OP_ROLLBACK,
-                  OP_REGEN, ANNOTATE_SLOTS,
+                  OP_REGEN, OP_RBKEY, ANNOTATE_SLOTS,
                   OP_ANNOTATE, OP_DTYPE, OP_INSERT, OP_NOOP, OP_REMOVE, PROP_DTYPE, PROPSET_DTYPE,
                   MergeTreeError)
 
@@ -149,6 +149,11 @@ class DocClients:
         # (MTE_ANNOTATE_SLOTS, include/mte.h); an annotate made while all are
         # taken is not tracked and cannot be regenerated
         self.ann_slot = {}
+        # the keys -> value ids each pending local annotate set (its rollback
+        # puts the older values back), and the annotates whose rollback the
+        # engine cannot restate exactly (see BatchBuilder.add_rollback)
+        self.ann_props = {}
+        self.no_rollback = set()
 
     def short(self, long_id, seq=None) -> int:
         i = self.ids.get(long_id)
@@ -235,6 +240,15 @@ class BatchBuilder:
                 for ls in range(lo, hi + 1):
                     if ls in clients.ann_slot:
                         mask |= 1 << clients.ann_slot.pop(ls)
+                    # an annotate acked under a later pending one on the same key:
+                    # the engine keeps the value from before the first pending
+                    # annotate, not this one's, so the later one's rollback
+                    # could not put this value back
+                    keys = clients.ann_props.pop(ls, {})
+                    for ls2, kv in clients.ann_props.items():
+                        if ls2 > hi and keys.keys() & kv.keys():
+                            clients.no_rollback.add(ls2)
+                    clients.no_rollback.discard(ls)
                 recs.append((OP_ACK, 0, lo, hi, mask, NO_PROPS))
             else:
                 self._op_records(msg.get("contents"), recs)
@@ -278,6 +292,8 @@ class BatchBuilder:
                 if free is not None:
                     clients.ann_slot[first + i] = free
                     b = free
+                f0, cnt = self.props.sets[a]
+                clients.ann_props[first + i] = dict(self.props.entries[f0:f0 + cnt])
             out.append((first + i, 0, 0, t, 0, flags | F_LOCAL, p1, p2, a, b))
         clients.local_seq += len(recs)
         clients.pending.append((first, clients.local_seq))
@@ -286,19 +302,48 @@ class BatchBuilder:
     def add_rollback(self, doc: int, clients: DocClients):
         """Client.rollback of the latest pending local op (client.ts:396-398 ->
         MergeTree.rollback, mergeTree.ts:2005-2083): one MTE_OP_ROLLBACK record
-        per record of that op, last first.  Rolling back an annotate is not
-        supported (MTE_E_UNSUPPORTED)."""
+        per record of that op, last first.  An annotate's carries its group slot
+        and is followed by its MTE_OP_RBKEY records (include/mte.h): per key it
+        set, the older pending annotates that set the key, latest first, then
+        the base entry.  MTE_E_UNSUPPORTED for an annotate the engine cannot
+        restate: untracked (no group slot), an older untracked annotate on one
+        of its keys, or an older annotate on one of its keys acked meanwhile."""
         if not clients.local or not clients.pending:
             raise MergeTreeError(MTE_E_STATE, "rollback without a pending local op")
         types = clients.pending_types[-1]
-        if OP_ANNOTATE in types:
-            raise MergeTreeError(MTE_E_UNSUPPORTED, "rollback of an annotate")
-        lo, hi = clients.pending.pop()
+        lo, hi = clients.pending[-1]
+        aux = {}
+        for ls in range(hi, lo - 1, -1):
+            if types[ls - lo] != OP_ANNOTATE:
+                continue
+            if ls not in clients.ann_slot or ls in clients.no_rollback:
+                raise MergeTreeError(MTE_E_UNSUPPORTED, "rollback of an annotate the engine does not track")
+            # a regenerated message moves behind newer ones; rolling it back under a
+            # newer pending annotate of the same key leaves that key pending in the
+            # reference (its count drops by one), which the engine does not restate
+            if any(x > ls and x not in range(lo, hi + 1) and kv.keys() & clients.ann_props[ls].keys()
+                   for x, kv in clients.ann_props.items()):
+                raise MergeTreeError(MTE_E_UNSUPPORTED, "rollback under a newer pending annotate of the same key")
+            recs = []
+            for k, _ in clients.ann_props[ls].items():
+                older = sorted((x for x, kv in clients.ann_props.items() if x < ls and k in kv), reverse=True)
+                if any(x not in clients.ann_slot for x in older):
+                    raise MergeTreeError(MTE_E_UNSUPPORTED, "rollback past an untracked pending annotate")
+                for x in older:
+                    recs.append((x, 0, 0, OP_RBKEY, 0, F_LOCAL, k, clients.ann_slot[x], clients.ann_props[x][k],
+                                 NO_PROPS))
+                recs.append((0, 0, 0, OP_RBKEY, 0, F_LOCAL, k, ANNOTATE_SLOTS, 0, NO_PROPS))
+            aux[ls] = recs
+        clients.pending.pop()
         clients.pending_types.pop()
         out = self.ops[doc]
         for ls in range(hi, lo - 1, -1):
             t = types[ls - lo]
-            if t != OP_NOOP:
+            if t == OP_ANNOTATE:
+                out.append((ls, 0, 0, OP_ROLLBACK, 0, F_LOCAL, t, len(aux[ls]), clients.ann_slot.pop(ls), NO_PROPS))
+                out.extend(aux[ls])
+                del clients.ann_props[ls]
+            elif t != OP_NOOP:
                 out.append((ls, 0, 0, OP_ROLLBACK, 0, F_LOCAL, t, 0, 0, NO_PROPS))
 
     def add_regen(self, doc: int, clients: DocClients):

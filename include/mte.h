@@ -84,8 +84,16 @@ extern "C" {
  * -> MergeTree.rollback, mergeTree.ts:2005-2083), which is then never sent:
  * seq = that op's localSeq, pos1 = its type.  A rolled-back insert becomes a
  * removed segment of seq and removedSeq UniversalSequenceNumber (0), gone for
- * every view; a rolled-back remove restores its segments.  A rollback of an
- * annotate is MTE_E_UNSUPPORTED.  Only in MTE_DOC_LOCAL_CLIENT documents.    */
+ * every view; a rolled-back remove restores its segments.  A rolled-back
+ * annotate (a = its group slot, see MTE_ANNOTATE_SLOTS; pos2 = the number of
+ * MTE_OP_RBKEY records that follow it) puts back, on every segment of its
+ * group, the previous value of each key it set (the group's previousProps,
+ * mergeTree.ts:2056-2072, segmentPropertiesManager.ts:63-151): the value of
+ * the latest older pending annotate of the segment's groups that set the key,
+ * else the value the key had before the first pending annotate set it.  A
+ * segment of the group removed since stops the document with
+ * MTE_E_UNSUPPORTED (the reference would re-annotate the range after it).
+ * Only in MTE_DOC_LOCAL_CLIENT documents.                                    */
 #define MTE_OP_ROLLBACK 5
 /* Client.regeneratePendingOp for reconnection (client.ts:972-1002 ->
  * resetPendingDeltaToOps :788-860): a local record with seq = the localSeq L of
@@ -107,6 +115,13 @@ extern "C" {
  * that record events (MTE_DOC_EVENTS).                                       */
 #define MTE_OP_REGEN 6
 #define MTE_DELTA_REGEN 0x10u
+/* Follows an annotate's MTE_OP_ROLLBACK (a local record): for each key k the
+ * rolled-back annotate set (pos1 = k), the older pending annotates that set k
+ * too, latest first -- pos2 = its group slot, a = the value id it set, seq =
+ * its localSeq -- then one record with pos2 = MTE_ANNOTATE_SLOTS (the value
+ * before the first pending annotate, kept per segment).  A segment takes the
+ * first candidate whose group it belongs to.                                 */
+#define MTE_OP_RBKEY 7
 /* Segment groups of pending local annotates (mergeTree.ts:1874-1880): a local
  * annotate record with b = a slot 0..31 marks every segment it visits with
  * that slot (MTE_NO_PROPS: not tracked); an MTE_OP_ACK record's a is the mask

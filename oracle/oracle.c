@@ -91,11 +91,14 @@ static int arena_append(orc_ctx* c, const uint16_t* t, uint64_t n, uint64_t* bas
   return MTE_OK;
 }
 
-/* a pk row: MTE_MAX_KEYS pending-key localSeqs, then the mask of the pending
- * annotate groups (MTE_ANNOTATE_SLOTS) the segment belongs to */
-#define PKW (MTE_MAX_KEYS + 1)
+/* a pk row: MTE_MAX_KEYS pending-key localSeqs, the mask of the pending
+ * annotate groups (MTE_ANNOTATE_SLOTS) the segment belongs to, then per key the
+ * value it had before the first pending annotate set it (what an annotate
+ * rollback puts back when no older pending annotate set the key) */
+#define PKW (2 * MTE_MAX_KEYS + 1)
 #define PK(d, i) ((d)->pk + (size_t)(i) * PKW)
 #define AM(d, i) (PK(d, i)[MTE_MAX_KEYS])
+#define BASEV(d, i) (PK(d, i) + MTE_MAX_KEYS + 1)
 
 static int doc_reserve(odoc* d, uint32_t need) {
   if (need <= d->cap) return MTE_OK;
@@ -223,6 +226,7 @@ typedef struct {
   uint64_t text_base;
   uint32_t n_keys;
   const uint16_t* arena;
+  const mte_op* aux;  /* the records after the one applied (an annotate rollback's MTE_OP_RBKEY) */
 } apply_env;
 
 /* Client.completeAndLogOp asserts (client.ts:525-528). */
@@ -313,7 +317,7 @@ static int64_t doc_lengths_local(odoc* d) {
   return p;
 }
 
-static int doc_rollback(odoc* d, const mte_op* op);
+static int doc_rollback(odoc* d, const mte_op* op, const apply_env* env);
 static int doc_regen(odoc* d, const mte_op* op);
 
 /* A local op (MTE_F_LOCAL, include/mte.h): insertSegmentLocal /
@@ -331,7 +335,7 @@ static int doc_regen(odoc* d, const mte_op* op);
 static int doc_apply_local(odoc* d, const mte_op* op, const apply_env* env) {
   const int32_t ls = op->seq;
   int rc;
-  if (op->type == MTE_OP_ROLLBACK) return doc_rollback(d, op);
+  if (op->type == MTE_OP_ROLLBACK) return doc_rollback(d, op, env);
   if (op->type == MTE_OP_REGEN) return doc_regen(d, op);
   if (!(ls > d->local_seq && ls < LOCAL_BASE)) return MTE_E_INVALID_ARG;
   if (op->client != 0) return MTE_E_INVALID_ARG;
@@ -396,6 +400,12 @@ static int doc_apply_local(odoc* d, const mte_op* op, const apply_env* env) {
       g->rmask = 1u;
     } else {
       const mte_propset* ps = &env->b->propsets[op->a];
+      /* the value a key had before the first pending annotate set it (the
+       * previousProps of that annotate, mergeTree.ts:1874-1880) */
+      for (uint32_t j = 0; j < ps->count; j++) {
+        const mte_prop* p = &env->b->props[ps->first + j];
+        if (p->key < env->n_keys && !PK(d, i)[p->key]) BASEV(d, i)[p->key] = g->props[p->key];
+      }
       d->pwrites += orc_apply_props(g->props, env->n_keys, ps, env->b->props, 0);
       for (uint32_t j = 0; j < ps->count; j++) {
         const mte_prop* p = &env->b->props[ps->first + j];
@@ -409,17 +419,71 @@ static int doc_apply_local(odoc* d, const mte_op* op, const apply_env* env) {
   return MTE_OK;
 }
 
+/* MTE_OP_ROLLBACK of an annotate (group slot op->a), followed by its op->pos2
+ * MTE_OP_RBKEY records (env->aux): MergeTree.rollback -> annotateRange of
+ * each segment of the group with its previousProps under
+ * PropertiesRollback.Rollback (mergeTree.ts:2036-2072): the pending count of
+ * each key drops (decrementPendingCounts, segmentPropertiesManager.ts:73-84)
+ * and the key takes its value from before the annotate -- the latest older
+ * pending annotate of the segment's groups that set it (its localSeq becomes
+ * the key's pending one), else the value before the first pending annotate.
+ * Each segment's annotate event at its own-view position (findRollbackPosition
+ * :2088-2103).  A segment of the group removed since would make the reference
+ * re-annotate the range after it (its local length is 0): MTE_E_UNSUPPORTED. */
+static int doc_rollback_annotate(odoc* d, const mte_op* op, const apply_env* env) {
+  const uint32_t b = op->a;
+  const mte_op* aux = env->aux;
+  const uint32_t n_aux = (uint32_t)op->pos2;
+  int rc;
+  if (b >= MTE_ANNOTATE_SLOTS || !aux) return MTE_E_INVALID_ARG;
+  d->ops++;
+  d->scanned += d->n;
+  int64_t lp = 0;
+  for (uint32_t i = 0; i < d->n; lp += own_len(&d->s[i]), i++) {
+    if (!((AM(d, i) >> b) & 1u)) continue;
+    oseg* g = &d->s[i];
+    if (g->rseq != NONE_SEQ) return MTE_E_UNSUPPORTED;
+    uint32_t j = 0;
+    while (j < n_aux) {
+      const uint32_t key = (uint32_t)aux[j].pos1;
+      if (key >= env->n_keys) return MTE_E_INVALID_ARG;
+      uint32_t val = BASEV(d, i)[key], pk = 0;
+      for (; j < n_aux; j++) {  /* the key's candidates, latest first, then the base entry */
+        const uint32_t slot = (uint32_t)aux[j].pos2;
+        if ((uint32_t)aux[j].pos1 != key) return MTE_E_INVALID_ARG;
+        if (slot >= MTE_ANNOTATE_SLOTS) break;
+        if ((AM(d, i) >> slot) & 1u) {
+          val = aux[j].a;
+          pk = (uint32_t)aux[j].seq;
+          break;
+        }
+      }
+      while (j < n_aux && (uint32_t)aux[j].pos2 < MTE_ANNOTATE_SLOTS) j++;  /* to the run's base entry */
+      if (j >= n_aux) return MTE_E_INVALID_ARG;
+      j++;
+      g->props[key] = val;
+      PK(d, i)[key] = pk;
+      d->pwrites += 1;
+    }
+    AM(d, i) &= ~(1u << b);
+    if ((d->flags & MTE_DOC_EVENTS) && (rc = delta_push(d, MTE_OP_ANNOTATE, lp, g->len, 0))) return rc;
+    d->written += 1;
+  }
+  return MTE_OK;
+}
+
 /* MTE_OP_ROLLBACK (a local record): MergeTree.rollback of the pending op of
  * localSeq op->seq, type op->pos1 (mergeTree.ts:2005-2083).  Its inserted
  * segments get seq and removedSeq UniversalSequenceNumber (markRangeRemoved
  * at seq 0 by the local client: gone for every view, zamboni drops them);
  * its removed ones are restored.  Each segment's delta event comes at its
  * own-view position once it is done (findRollbackPosition :2088-2103). */
-static int doc_rollback(odoc* d, const mte_op* op) {
+static int doc_rollback(odoc* d, const mte_op* op, const apply_env* env) {
   const int32_t ls = op->seq;
   int rc;
   if (!(ls > 0 && ls <= d->local_seq)) return MTE_E_INVALID_ARG;
-  if (op->pos1 != MTE_OP_INSERT && op->pos1 != MTE_OP_REMOVE) return MTE_E_UNSUPPORTED;
+  if (op->pos1 == MTE_OP_ANNOTATE) return doc_rollback_annotate(d, op, env);
+  if (op->pos1 != MTE_OP_INSERT && op->pos1 != MTE_OP_REMOVE) return MTE_E_INVALID_ARG;
   d->ops++;
   d->scanned += d->n;
   int64_t lp = 0;
@@ -805,7 +869,7 @@ static int round_sync_ok(odoc* d, const mte_op* ops, uint64_t k0, uint64_t k1) {
 
 static void* worker(void* p) {
   worker_arg* w = (worker_arg*)p;
-  apply_env env = {w->b, w->base, w->c->n_keys, w->c->arena};
+  apply_env env = {w->b, w->base, w->c->n_keys, w->c->arena, NULL};
   for (uint32_t di = w->d0; di < w->d1; di += w->stride) {
     odoc* d = &w->c->docs[di];
     if (d->status) continue;
@@ -816,12 +880,15 @@ static void* worker(void* p) {
     }
     d->dl_n = 0;
     for (uint64_t k = w->b->op_offsets[di]; k < w->b->op_offsets[di + 1]; k++) {
+      const mte_op* op = &w->b->ops[k];
       d->cur_op = (uint32_t)(k - w->b->op_offsets[di]);
-      int rc = doc_apply(d, &w->b->ops[k], &env);
+      env.aux = op + 1;
+      int rc = doc_apply(d, op, &env);
       if (rc) {
         d->status = rc;
         break;
       }
+      if (op->type == MTE_OP_ROLLBACK && op->pos1 == MTE_OP_ANNOTATE) k += (uint64_t)op->pos2;  /* its RBKEY records */
     }
   }
   return NULL;
@@ -831,19 +898,29 @@ int orc_apply_batch(orc_ctx* c, const mte_batch* b, int n_threads) {
   if (!c || !b || b->n_docs != c->n_docs || !b->op_offsets) return MTE_E_INVALID_ARG;
   if (b->op_offsets[b->n_docs] != b->n_ops) return MTE_E_INVALID_ARG;
   uint32_t dcur = 0;
+  uint64_t rbkey_end = 0;  /* records up to here are an annotate rollback's MTE_OP_RBKEY */
   for (uint64_t k = 0; k < b->n_ops; k++) {
     const mte_op* op = &b->ops[k];
     while (dcur + 1 < b->n_docs && b->op_offsets[dcur + 1] <= k) dcur++;
     /* local records (as mte_submit validates them) */
     const int local_doc = (c->docs[dcur].flags & MTE_DOC_LOCAL_CLIENT) != 0;
-    if (op->type > MTE_OP_REGEN) return MTE_E_INVALID_ARG;
+    if ((op->type == MTE_OP_RBKEY) != (k < rbkey_end)) return MTE_E_INVALID_ARG;
+    if (op->type == MTE_OP_ROLLBACK && op->pos1 == MTE_OP_ANNOTATE) {
+      if (op->pos2 < 0 || k + 1 + (uint64_t)op->pos2 > b->op_offsets[dcur + 1]) return MTE_E_INVALID_ARG;
+      rbkey_end = k + 1 + (uint64_t)op->pos2;
+    }
+    if (op->type > MTE_OP_RBKEY) return MTE_E_INVALID_ARG;
     if (op->type >= MTE_OP_ROLLBACK && !(op->flags & MTE_F_LOCAL)) return MTE_E_INVALID_ARG;
     if ((op->flags & MTE_F_LOCAL) && op->type == MTE_OP_ANNOTATE && op->b != MTE_NO_PROPS &&
         op->b >= MTE_ANNOTATE_SLOTS)
       return MTE_E_INVALID_ARG;
     if ((op->flags & MTE_F_LOCAL) || op->type == MTE_OP_ACK) {
       if (!local_doc) return MTE_E_INVALID_ARG;
-      if ((op->flags & MTE_F_LOCAL) && (op->type == MTE_OP_ACK || op->seq <= 0 || op->seq >= MTE_LOCAL_SEQ_BASE))
+      if ((op->flags & MTE_F_LOCAL) && op->type != MTE_OP_RBKEY &&
+          (op->type == MTE_OP_ACK || op->seq <= 0 || op->seq >= MTE_LOCAL_SEQ_BASE))
+        return MTE_E_INVALID_ARG;
+      if (op->type == MTE_OP_RBKEY && (op->seq < 0 || op->seq >= MTE_LOCAL_SEQ_BASE || op->pos1 < 0 ||
+                                       op->pos1 >= MTE_MAX_KEYS || op->pos2 < 0 || op->pos2 > MTE_ANNOTATE_SLOTS))
         return MTE_E_INVALID_ARG;
       if (op->type == MTE_OP_ACK && (op->pos1 <= 0 || op->pos1 > op->pos2)) return MTE_E_INVALID_ARG;
     }

@@ -18,9 +18,11 @@
 //
 // stdin:  {"sets": [{"seed": int, "clients": int, "steps": int, "initialText": str,
 //                    "nCheckpoints": int, "maxText": int, "rollback": p}]}
-//         (rollback: the chance that a local insert / remove is rolled back
-//         instead of sent; the event is ["R", op]: the client made the op
-//         locally, then rolled it back.
+//         (rollback: the chance that a local remove -- with rollbackInserts
+//         also an insert, with rollbackTypes [MergeTreeDeltaType, ...] those
+//         types, annotates included -- is rolled back instead of sent; the
+//         event is ["R", op]: the client made the op locally, then rolled it
+//         back.
 //          reconnect: the chance per step that a sending client goes offline,
 //         or, when offline, reconnects.  Offline, its local ops are held
 //         (["H", op]); reconnecting, it catches up with the whole log, then
@@ -180,7 +182,8 @@ function runSet(p) {
         // made while offline: pending, not sent
         events[i].push(["H", JSON.parse(JSON.stringify(op))]);
         held[i].push([op, c.peekPendingSegmentGroups()]);
-      } else if (op && p.rollback && (p.rollbackInserts ? op.type !== 2 : op.type === 1) && R.next() < p.rollback) {
+      } else if (op && p.rollback && (p.rollbackTypes ? p.rollbackTypes.includes(op.type)
+        : (p.rollbackInserts ? op.type !== 2 : op.type === 1)) && R.next() < p.rollback) {
         // Client.rollback of the op just made (client.ts:396-398 ->
         // MergeTree.rollback, mergeTree.ts:2005-2083): it is never sent
         const opJson = JSON.parse(JSON.stringify(op));

@@ -38,6 +38,13 @@ SETS += [(2000 + i, 2 + i % 7, 400 + 100 * (i % 5), ["", "hello world"][i % 2], 
 # ("MergeTree insert failed" in another client after a rolled-back insert);
 # those seeds are left out and counted in the file
 ROLLBACK_INSERT_SETS = [(3000 + i, 2 + i % 5, 400, ["", "hello world"][i % 2], 4, 200, 0.15) for i in range(24)]
+# annotates rolled back too (previousProps, mergeTree.ts:2036-2072), beside
+# removes.  Inserts stay out of these sets: after a rolled-back insert the
+# reference's block partial lengths can still count the segment (seed 4016 with
+# inserts: a later remote insert lands one unit early in one client), which is
+# the reference's own defect, not a rule to restate
+ROLLBACK_ANNOTATE_SETS = [(4000 + i, 2 + i % 6, 400 + 100 * (i % 3), ["", "hello world", "abc\ndef"][i % 3], 4,
+                           [64, 200][i % 2], 0.25, [1, 2]) for i in range(24)]
 
 
 def main():
@@ -62,6 +69,16 @@ def main():
         else:
             failed.append(sd)
     res["rollback_insert_seeds_the_reference_failed"] = failed
+    failed = []
+    for sd, c, n, t, k, m, rb, types in ROLLBACK_ANNOTATE_SETS:
+        one = {"sets": [{"seed": sd, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
+                         "rollback": rb, "rollbackTypes": types}]}
+        q = subprocess.run(["node", FARM_JS, out], input=json.dumps(one), capture_output=True, text=True, timeout=600)
+        if q.returncode == 0:
+            res["sets"] += json.loads(q.stdout)["sets"]
+        else:
+            failed.append(sd)
+    res["rollback_annotate_seeds_the_reference_failed"] = failed
     with gzip.open(OUT, "wt", encoding="utf-8") as fh:
         json.dump(res, fh, separators=(",", ":"))
     n_msgs = sum(len(s["log"]) for s in res["sets"])

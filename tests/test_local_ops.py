@@ -161,3 +161,114 @@ def test_gpu_reference_farms():
     passed, failures = replay_ref_farm(device_factory, sets)
     assert not failures, failures[:2]
     assert passed == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
+
+
+def _annotate_rollback_scenario(factory):
+    """Annotate rollback (MTE_OP_ROLLBACK of an annotate + MTE_OP_RBKEY,
+    mergeTree.ts:2036-2072): B annotates k=1 on [0, 4) and sends it (pending),
+    a remote k=9 over everything is ignored on B's pending keys, then B annotates
+    k=2 on [2, 6) and rolls it back: [2, 4) gets k=1 again (the older pending
+    annotate's value, still pending), [4, 6) the value from before (k=9 from
+    the remote annotate, not pending)."""
+    inits, text = doc_inits(["abcdefgh"], flags=DOC_NEW_LENGTH_CALC | DOC_LOCAL_CLIENT)
+    it = Interner(4)
+    e = factory(4)
+    e.load_docs(inits, text)
+    cl = DocClients("B", local=True)
+    bb = BatchBuilder(1, it)
+    bb.add_local(0, cl, {"type": 2, "pos1": 0, "pos2": 4, "props": {"k": 1}})
+    bb.add_message(0, cl, {"clientId": "C", "sequenceNumber": 1, "referenceSequenceNumber": 0,
+                           "minimumSequenceNumber": 0, "type": "op",
+                           "contents": {"type": 2, "pos1": 0, "pos2": 8, "props": {"k": 9}}})
+    bb.add_local(0, cl, {"type": 2, "pos1": 2, "pos2": 6, "props": {"k": 2, "j": 5}})
+    bb.add_rollback(0, cl)
+    # a remote annotate now: [0, 4) still pending (B's first annotate), the rest not
+    bb.add_message(0, cl, {"clientId": "C", "sequenceNumber": 2, "referenceSequenceNumber": 1,
+                           "minimumSequenceNumber": 0, "type": "op",
+                           "contents": {"type": 2, "pos1": 0, "pos2": 8, "props": {"k": 7}}})
+    e.apply_batch(bb.build())
+    v = e.read_doc(0)
+    per_pos = []
+    for ln, _, p in v["segs"]:
+        per_pos += [it.decode_props(p)] * ln
+    return e, per_pos
+
+
+def test_oracle_annotate_rollback_scenario():
+    e, per_pos = _annotate_rollback_scenario(oracle_factory)
+    assert (e.statuses() == 0).all()
+    assert per_pos == [{"k": 1}] * 4 + [{"k": 7}] * 4
+
+
+@pytest.mark.gpu
+def test_gpu_annotate_rollback_scenario():
+    e, per_pos = _annotate_rollback_scenario(device_factory)
+    assert (e.statuses() == 0).all()
+    assert per_pos == [{"k": 1}] * 4 + [{"k": 7}] * 4
+
+
+def test_annotate_rollback_farms_hold_annotate_rollbacks():
+    sets = farm_sets()
+    n = sum(1 for s in sets for ev in s["events"] for e in ev if e[0] == "R" and e[1]["type"] == 2)
+    assert n >= 400
+
+
+def test_packer_refuses_annotate_rollbacks_it_cannot_restate():
+    ann = {"type": 2, "pos1": 0, "pos2": 1, "props": {"k": 1}}
+    ack = {"clientId": "B", "sequenceNumber": 1, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
+           "type": "op", "contents": ann}
+    # an older annotate on the same key acked under it: the base value is stale
+    cl = DocClients("B", local=True)
+    bb = BatchBuilder(1, Interner(4))
+    bb.add_local(0, cl, ann)
+    bb.add_local(0, cl, ann)
+    bb.add_message(0, cl, ack)
+    with pytest.raises(MergeTreeError) as ei:
+        bb.add_rollback(0, cl)
+    assert ei.value.code == MTE_E_UNSUPPORTED
+    # the 33rd pending annotate has no group slot
+    cl = DocClients("B", local=True)
+    bb = BatchBuilder(1, Interner(4))
+    for _ in range(33):
+        bb.add_local(0, cl, ann)
+    with pytest.raises(MergeTreeError) as ei:
+        bb.add_rollback(0, cl)
+    assert ei.value.code == MTE_E_UNSUPPORTED
+    # a different key under it is fine, and emits one base record per key
+    cl = DocClients("B", local=True)
+    bb = BatchBuilder(1, Interner(4))
+    bb.add_local(0, cl, {"type": 2, "pos1": 0, "pos2": 1, "props": {"j": 1}})
+    bb.add_local(0, cl, ann)
+    bb.add_rollback(0, cl)
+    from fluidframework_amd.abi import OP_RBKEY, OP_ROLLBACK
+    recs = bb.ops[0][2:]
+    assert recs[0][3] == OP_ROLLBACK and recs[0][7] == 1 and [r[3] for r in recs[1:]] == [OP_RBKEY]
+
+
+def test_annotate_rollback_mutation_is_caught():
+    """Without the older-candidate records (every key back to its base value)
+    the reference farms fail: the chain of pending annotates matters."""
+    from fluidframework_amd import packing
+    sets = farm_sets()[76:]
+    orig = packing.BatchBuilder.add_rollback
+
+    def base_only(self, doc, clients):
+        n0 = len(self.ops[doc])
+        orig(self, doc, clients)
+        out = self.ops[doc]
+        new = [r for r in out[n0:] if not (r[3] == packing.OP_RBKEY and r[7] < packing.ANNOTATE_SLOTS)]
+        for i, r in enumerate(new):  # recount each rollback's key records
+            if r[3] == packing.OP_ROLLBACK and r[6] == packing.OP_ANNOTATE:
+                n = 0
+                while i + 1 + n < len(new) and new[i + 1 + n][3] == packing.OP_RBKEY:
+                    n += 1
+                new[i] = r[:7] + (n,) + r[8:]
+        del out[n0:]
+        out.extend(new)
+
+    packing.BatchBuilder.add_rollback = base_only
+    try:
+        passed, failures = replay_ref_farm(oracle_factory, sets)
+    finally:
+        packing.BatchBuilder.add_rollback = orig
+    assert len(failures) > 20 and {f[3] for f in failures} == {"state"}
