@@ -46,6 +46,9 @@
 #ifndef MTE_OUTLINE  // 1: pass-1 tiers as out-of-line functions (measured: same time, 1.7x the HBM traffic)
 #define MTE_OUTLINE 0
 #endif
+#ifndef MTE_STEPV_EMAX  // tiers up to this E run the per-slot-flag step (doc_step_v), larger ones doc_step
+#define MTE_STEPV_EMAX 4
+#endif
 #ifndef MTE_OUTLINE_E4  // 1: only the rare E = 4 tier out of line (the E <= 2 loops get the registers)
 #define MTE_OUTLINE_E4 0
 #endif
@@ -706,7 +709,7 @@ __device__ __forceinline__ void burst_run(DocRun& D, const ReplayArgs& a, uint32
   const uint32_t kend = D.k1 - D.k > limit ? D.k + limit : D.k1;
   s8v cur;
   RecV vcur;
-  if constexpr (E <= 4) {
+  if constexpr (E <= MTE_STEPV_EMAX) {
 #if MTE_VREC
     vcur = vload_rec8(D.recp + 2 * D.k);
 #else
@@ -725,7 +728,7 @@ __device__ __forceinline__ void burst_run(DocRun& D, const ReplayArgs& a, uint32
   for (;;) {
     if (!per_burst && (D.k & (kTouchSpan / 2 - 1)) == 0) touch_records(D, D.k + kTouchSpan / 2, pending, sink);
     int rc;
-    if constexpr (E <= 4) rc = doc_step_v<E, K, S>(R, D, st, vcur, a, zlds, emin);
+    if constexpr (E <= MTE_STEPV_EMAX) rc = doc_step_v<E, K, S>(R, D, st, vcur, a, zlds, emin);
     else rc = doc_step<E, K, S>(R, D, st, cur, a, zlds, emin);
     if (rc != 0) {
       if (rc < 0) {
@@ -737,9 +740,9 @@ __device__ __forceinline__ void burst_run(DocRun& D, const ReplayArgs& a, uint32
     if (D.k >= kend) break;
   }
   if (D.k >= D.k1) D.running = false;
-  if constexpr (E > 4) swait(cur);  // no scalar load may be left in flight
+  if constexpr (E > MTE_STEPV_EMAX) swait(cur);  // no scalar load may be left in flight
 #if !MTE_VREC
-  if constexpr (E <= 4) swait(vcur);
+  if constexpr (E <= MTE_STEPV_EMAX) swait(vcur);
 #endif
   store_regs<E, K>(R, D, a);
   if constexpr (S) run_flush_stats(D, st, a);

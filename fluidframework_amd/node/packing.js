@@ -63,6 +63,7 @@ function canonicalJson(v) {
 }
 
 function checkI32(v, what) {
+  if ((v | 0) === v) return v;  // an int32 number (fast path; the test below gives the same answer)
   if (typeof v !== "number" || !Number.isInteger(v) || v < -2147483648 || v > 2147483647) {
     throw new MergeTreeError(E_INVALID_ARG, what + "=" + String(v) + " is not an int32");
   }
@@ -77,6 +78,8 @@ class Interner {
     this.keyNames = [];
     this.values = new Map();
     this.valueJson = [null];
+    this.numIds = new Map();
+    this.strIds = new Map();
   }
   key(name) {
     let k = this.keys.get(name);
@@ -92,6 +95,13 @@ class Interner {
   }
   value(v) {
     if (v === null || v === undefined) return 0;
+    // numbers and strings: their canonical JSON is a function of the value, so
+    // a map keyed by the value skips the stringify (same ids)
+    const prim = typeof v === "number" ? this.numIds : (typeof v === "string" ? this.strIds : null);
+    if (prim !== null) {
+      const id = prim.get(v);
+      if (id !== undefined) return id;
+    }
     const cj = canonicalJson(v);
     let i = this.values.get(cj);
     if (i === undefined) {
@@ -99,6 +109,7 @@ class Interner {
       this.values.set(cj, i);
       this.valueJson.push(cj);
     }
+    if (prim !== null && !(typeof v === "number" && Object.is(v, -0))) prim.set(v, i);
     return i;
   }
   /** plane values of one segment -> PropertySet (undefined when empty) */
@@ -126,7 +137,9 @@ class DocClients {
   constructor(observerId, minSeq, local) {
     this.observer = observerId;
     this.ids = new Map([[observerId, 0]]);
-    this.last = new Map([[0, NEVER]]); // slot -> highest seq its client used
+    this.last = new Int32Array(MAX_CLIENTS).fill(NEVER); // slot -> highest seq its client used
+    this.lastId = observerId;  // the last sender and its slot (messages come in runs per sender)
+    this.lastSlot = 0;
     this.minSeq = minSeq || 0;          // the window's minSeq before the next message
     // a document whose own client sends (MTE_DOC_LOCAL_CLIENT): collabWindow.localSeq
     // and the [first, last] localSeqs of each unacked local message, oldest first
@@ -145,15 +158,17 @@ class DocClients {
     this.noRollback = new Set();
   }
   short(longId, seq) {
-    let i = this.ids.get(longId);
+    let i = longId === this.lastId ? this.lastSlot : this.ids.get(longId);
     if (i === undefined) {
       i = this._freeSlot();
       if (i >= MAX_CLIENTS) return i; // the caller throws E_CLIENT_RANGE
       this.ids.set(longId, i);
-      this.last.set(i, seq === undefined ? NEVER : seq);
-    } else if (seq !== undefined && this.last.get(i) !== NEVER) {
-      this.last.set(i, Math.max(this.last.get(i), seq));
+      this.last[i] = seq === undefined ? NEVER : seq;
+    } else if (seq !== undefined && this.last[i] !== NEVER) {
+      if (seq > this.last[i]) this.last[i] = seq;
     }
+    this.lastId = longId;
+    this.lastSlot = i;
     return i;
   }
   _freeSlot() {
@@ -161,13 +176,14 @@ class DocClients {
     for (let s = 1; s < MAX_CLIENTS; s++) if (!used.has(s)) return s;
     let best = -1, bestSeq = NEVER;
     for (const v of used) {
-      if (v !== 0 && (best < 0 || this.last.get(v) < bestSeq || (this.last.get(v) === bestSeq && v < best))) {
+      if (v !== 0 && (best < 0 || this.last[v] < bestSeq || (this.last[v] === bestSeq && v < best))) {
         best = v;
-        bestSeq = this.last.get(v);
+        bestSeq = this.last[v];
       }
     }
     if (best < 0 || bestSeq > this.minSeq) return MAX_CLIENTS;
     for (const [k, v] of this.ids) if (v === best) { this.ids.delete(k); break; }
+    if (this.lastSlot === best) this.lastId = undefined;  // its client leaves the cache with its slot
     return best;
   }
   advance(msn) {
@@ -212,19 +228,76 @@ class BatchBuilder {
     this.track = trackDocs || null;
     this.recSrc = trackDocs ? trackDocs.map((t) => (t ? [] : null)) : null;
     this.props = new PropTable(interner);
-    this.docOps = [];
-    for (let d = 0; d < nDocs; d++) this.docOps.push([]);
-    this.text = [];
-    this.textUnits = 0;
+    // records in arrival order, 8 int32 words each (the mte_op layout), and
+    // their documents; build() sorts them by document (counting sort)
+    this.cap = 1024;
+    this.rec = new Int32Array(this.cap * 8);
+    this.recDoc = new Uint32Array(this.cap);
+    this.docCount = new Uint32Array(nDocs);
     this.count = 0;
+    this.textBuf = new Uint16Array(4096);
+    this.textUnits = 0;
+  }
+
+  _grow() {
+    this.cap *= 2;
+    const r = new Int32Array(this.cap * 8);
+    r.set(this.rec);
+    this.rec = r;
+    const d = new Uint32Array(this.cap);
+    d.set(this.recDoc);
+    this.recDoc = d;
+  }
+
+  /** one record (mte_op): seq, ref_seq, min_seq, type | client << 8 | flags << 16, pos1, pos2, a, b */
+  _put(doc, seq, ref, msn, type, client, flags, p1, p2, a, b) {
+    if (this.count === this.cap) this._grow();
+    const w = this.count * 8, R = this.rec;
+    R[w] = seq;
+    R[w + 1] = ref;
+    R[w + 2] = msn;
+    R[w + 3] = type | (client << 8) | (flags << 16);
+    R[w + 4] = p1;
+    R[w + 5] = p2;
+    R[w + 6] = a;
+    R[w + 7] = b;
+    this.recDoc[this.count] = doc;
+    this.docCount[doc]++;
+    this.count++;
+  }
+
+  _truncate(k0) {
+    for (let k = k0; k < this.count; k++) this.docCount[this.recDoc[k]]--;
+    this.count = k0;
+  }
+
+  /** the records of document d as [seq, ref, msn, type, client, flags, pos1, pos2, a, b] (tests) */
+  get docOps() {
+    const out = [];
+    for (let d = 0; d < this.nDocs; d++) out.push([]);
+    const R = this.rec;
+    for (let k = 0; k < this.count; k++) {
+      const w = k * 8, w3 = R[w + 3];
+      out[this.recDoc[k]].push([R[w], R[w + 1], R[w + 2], w3 & 0xff, (w3 >>> 8) & 0xff, w3 >>> 16, R[w + 4],
+        R[w + 5], R[w + 6] >>> 0, R[w + 7] >>> 0]);
+    }
+    return out;
   }
 
   _text(s) {
     if (typeof s !== "string") throw new MergeTreeError(E_INVALID_ARG, "text must be a string");
-    const off = this.textUnits;
-    this.text.push(s);
-    this.textUnits += s.length;
-    return [off, s.length];
+    const off = this.textUnits, n = s.length;
+    if (off + n > this.textBuf.length) {
+      let c = this.textBuf.length * 2;
+      while (c < off + n) c *= 2;
+      const t = new Uint16Array(c);
+      t.set(this.textBuf.subarray(0, off));
+      this.textBuf = t;
+    }
+    const T = this.textBuf;
+    for (let i = 0; i < n; i++) T[off + i] = s.charCodeAt(i);  // UTF-16 code units (textSegment.ts:52-55)
+    this.textUnits = off + n;
+    return [off, n];
   }
 
   /** Client.applyMsg(msg, local=false) for one document (client.ts:918-935). */
@@ -238,7 +311,7 @@ class BatchBuilder {
     if (ref < clients.minSeq) {
       throw new MergeTreeError(E_INVALID_ARG, "referenceSequenceNumber " + ref + " < minSeq " + clients.minSeq);
     }
-    const recs = [];
+    const k0 = this.count;
     this._srcOps = null;
     if ((msg.type === undefined ? "op" : msg.type) === "op") {
       if (sender === clients.observer) {
@@ -271,24 +344,92 @@ class BatchBuilder {
           }
           clients.noRollback.delete(ls);
         }
-        recs.push([OP_ACK, 0, lo, hi, mask >>> 0, NO_PROPS]);
+        this._put(doc, seq, ref, msn, OP_ACK, 0, 0, lo, hi, mask, NO_PROPS);
       } else {
-        this._opRecords(msg.contents, recs, this._src(doc));
+        try {
+          this._opPut(doc, seq, ref, msn, msg.contents, this._src(doc));
+        } catch (e) {
+          this._truncate(k0);
+          throw e;
+        }
       }
     }
     // the slot is taken only once the message has validated
-    const short = slotOf(clients, sender, seq);
-    if (recs.length === 0) recs.push([OP_NOOP, 0, 0, 0, 0, NO_PROPS]);
+    let short;
+    try {
+      short = slotOf(clients, sender, seq);
+    } catch (e) {
+      this._truncate(k0);
+      throw e;
+    }
+    if (this.count === k0) this._put(doc, seq, ref, msn, OP_NOOP, 0, 0, 0, 0, 0, NO_PROPS);
     const src = this._src(doc);
     if (src) {  // one entry per record of this message
       const ops = this._srcOps || [];
-      for (let i = 0; i < recs.length; i++) src.push({ msg, op: ops[i], local: false });
+      for (let i = 0; i < this.count - k0; i++) src.push({ msg, op: ops[i], local: false });
       this._srcOps = null;
     }
-    recs[recs.length - 1][1] |= F_MSG_END;
-    for (const r of recs) this.docOps[doc].push([seq, ref, msn, r[0], short, r[1], r[2], r[3], r[4], r[5]]);
-    this.count += recs.length;
+    const R = this.rec;
+    for (let k = k0; k < this.count; k++) R[k * 8 + 3] |= short << 8;
+    R[(this.count - 1) * 8 + 3] |= F_MSG_END << 16;
     clients.advance(msn);
+  }
+
+  /** the records of a remote op (client.ts:862-889), as _opRecords, written
+   *  straight into the batch (client 0, no MSG_END: addMessage sets both) */
+  _opPut(doc, seq, ref, msn, op, track) {
+    if (track && op && typeof op === "object" && op.type !== GROUP) {
+      if (!this._srcOps) this._srcOps = [];
+      this._srcOps.push(op);
+    }
+    if (op === null || typeof op !== "object") throw new MergeTreeError(E_INVALID_ARG, "op contents must be an object");
+    const t = op.type;
+    if (t === GROUP) {
+      for (const member of op.ops || []) this._opPut(doc, seq, ref, msn, member, track);
+      return;
+    }
+    if (!("pos1" in op) && op.relativePos1 !== undefined && op.relativePos1 !== null) {
+      throw new MergeTreeError(E_UNSUPPORTED, "relativePos1");
+    }
+    if (t === INSERT) {
+      const seg = op.seg;
+      if (seg === undefined || seg === null) { // applyInsertOp returns false: no segment
+        this._put(doc, seq, ref, msn, OP_NOOP, 0, 0, 0, 0, 0, NO_PROPS);
+        return;
+      }
+      const pos = checkI32(op.pos1 === undefined ? 0 : op.pos1, "pos1");
+      if (typeof seg === "string") {
+        const off = this._text(seg)[0];
+        this._put(doc, seq, ref, msn, OP_INSERT, 0, 0, pos, seg.length, off, NO_PROPS);
+      } else if (typeof seg === "object" && "text" in seg) {
+        const tx = this._text(seg.text);
+        this._put(doc, seq, ref, msn, OP_INSERT, 0, 0, pos, tx[1], tx[0], this.props.add(seg.props));
+      } else if (typeof seg === "object" && "marker" in seg) {
+        const rt = checkI32(seg.marker.refType === undefined ? 0 : seg.marker.refType, "refType");
+        this._put(doc, seq, ref, msn, OP_INSERT, 0, F_MARKER, pos, rt, 0, this.props.add(seg.props));
+      } else {
+        throw new MergeTreeError(E_INVALID_ARG, "Unrecognized IJSONSegment type: " + JSON.stringify(seg));
+      }
+      return;
+    }
+    if ((t === REMOVE || t === ANNOTATE) && !("pos2" in op)) {
+      throw new MergeTreeError(E_UNSUPPORTED, "range op without pos2");
+    }
+    if (t === REMOVE) {
+      this._put(doc, seq, ref, msn, OP_REMOVE, 0, 0, checkI32(op.pos1, "pos1"), checkI32(op.pos2, "pos2"), 0, NO_PROPS);
+    } else if (t === ANNOTATE) {
+      let flags = 0;
+      const comb = op.combiningOp;
+      if (comb !== undefined && comb !== null) {
+        if (comb.name !== "rewrite") throw new MergeTreeError(E_UNSUPPORTED, "combiningOp " + String(comb.name));
+        flags = F_REWRITE;
+      }
+      const ps = this.props.add(op.props === undefined ? {} : op.props);  // before the checks, as packing.py
+      this._put(doc, seq, ref, msn, OP_ANNOTATE, 0, flags, checkI32(op.pos1, "pos1"), checkI32(op.pos2, "pos2"), ps,
+        NO_PROPS);
+    } else {
+      throw new MergeTreeError(E_INVALID_ARG, "unknown op type " + String(t));
+    }
   }
 
   /** A local op of the document's own client (insertSegmentLocal /
@@ -326,9 +467,8 @@ class BatchBuilder {
         for (let t = f0; t < f0 + cnt; t++) kv.set(this.props.entries[2 * t], this.props.entries[2 * t + 1]);
         clients.annProps.set(first + i, kv);
       }
-      this.docOps[doc].push([first + i, 0, 0, r[0], 0, r[1] | F_LOCAL, r[2], r[3], r[4], b]);
+      this._put(doc, first + i, 0, 0, r[0], 0, r[1] | F_LOCAL, r[2], r[3], r[4], b);
     });
-    this.count += recs.length;
     clients.localSeq += recs.length;
     clients.pending.push([first, clients.localSeq]);
     clients.pendingTypes.push(recs.map((r) => r[0]));
@@ -374,9 +514,8 @@ class BatchBuilder {
     clients.pending.pop();
     clients.pendingTypes.pop();
     const src = this._src(doc);
-    const push = (rec) => {
-      this.docOps[doc].push(rec);
-      this.count++;
+    const push = (r) => {
+      this._put(doc, r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7], r[8], r[9]);
       if (src) src.push({ msg: null, op: undefined, local: true });
     };
     for (let ls = hi; ls >= lo; ls--) {
@@ -415,9 +554,8 @@ class BatchBuilder {
         }
         slot = clients.annSlot.get(ls);
       }
-      idx.push([this.docOps[doc].length, ls, t]);
-      this.docOps[doc].push([ls, 0, 0, OP_REGEN, 0, F_LOCAL, t, 0, slot, NO_PROPS]);
-      this.count++;
+      idx.push([this.docCount[doc], ls, t]);
+      this._put(doc, ls, 0, 0, OP_REGEN, 0, F_LOCAL, t, 0, slot, NO_PROPS);
       const src = this._src(doc);
       if (src) src.push({ msg: null, op: undefined, local: true, regen: true });
     }
@@ -433,10 +571,8 @@ class BatchBuilder {
     const recs = [];
     this._opRecords(op, recs);
     for (const r of recs) {
-      this.docOps[doc].push([checkI32(seq, "seq"), checkI32(ref, "refSeq"), msn, r[0], client, r[1], r[2], r[3],
-        r[4], r[5]]);
+      this._put(doc, checkI32(seq, "seq"), checkI32(ref, "refSeq"), msn, r[0], client, r[1], r[2], r[3], r[4], r[5]);
     }
-    this.count += recs.length;
   }
 
   _src(doc) {
@@ -497,37 +633,36 @@ class BatchBuilder {
 
   /** -> {offsets: BigUint64Array, ops: Uint8Array, text: Uint16Array, propsets, props: Uint32Array} */
   build() {
-    const offsets = new BigUint64Array(this.nDocs + 1);
-    const ops = Buffer.alloc(this.count * OP_BYTES);
-    let k = 0;
-    for (let d = 0; d < this.nDocs; d++) {
-      for (const r of this.docOps[d]) {
-        const o = k * OP_BYTES;
-        ops.writeInt32LE(r[0], o);
-        ops.writeInt32LE(r[1], o + 4);
-        ops.writeInt32LE(r[2], o + 8);
-        ops.writeUInt8(r[3], o + 12);
-        ops.writeUInt8(r[4], o + 13);
-        ops.writeUInt16LE(r[5], o + 14);
-        ops.writeInt32LE(r[6], o + 16);
-        ops.writeInt32LE(r[7], o + 20);
-        ops.writeUInt32LE(r[8] >>> 0, o + 24);
-        ops.writeUInt32LE(r[9] >>> 0, o + 28);
-        k++;
-      }
-      offsets[d + 1] = BigInt(k);
+    // counting sort of the records by document, arrival order kept within one
+    const nd = this.nDocs, n = this.count;
+    const offsets = new BigUint64Array(nd + 1);
+    const cur = new Uint32Array(nd);
+    let acc = 0;
+    for (let d = 0; d < nd; d++) {
+      offsets[d] = BigInt(acc);
+      cur[d] = acc;
+      acc += this.docCount[d];
     }
-    const text = new Uint16Array(this.textUnits);
-    let t = 0;
-    for (const s of this.text) {
-      for (let i = 0; i < s.length; i++) text[t++] = s.charCodeAt(i);
+    offsets[nd] = BigInt(acc);
+    const out = new Int32Array(n * 8), R = this.rec, D = this.recDoc;
+    for (let k = 0; k < n; k++) {
+      const o = cur[D[k]]++ * 8, w = k * 8;
+      out[o] = R[w];
+      out[o + 1] = R[w + 1];
+      out[o + 2] = R[w + 2];
+      out[o + 3] = R[w + 3];
+      out[o + 4] = R[w + 4];
+      out[o + 5] = R[w + 5];
+      out[o + 6] = R[w + 6];
+      out[o + 7] = R[w + 7];
     }
+    const text = this.textBuf.slice(0, this.textUnits);
     return {
       offsets,
-      ops: new Uint8Array(ops.buffer, ops.byteOffset, ops.length),
+      ops: new Uint8Array(out.buffer, 0, n * OP_BYTES),
       text,
-      propsets: Uint32Array.from(this.props.sets),
-      props: Uint32Array.from(this.props.entries),
+      propsets: new Uint32Array(this.props.sets),
+      props: new Uint32Array(this.props.entries),
     };
   }
 }
