@@ -50,6 +50,8 @@ def load_mte():
         "mte_read_doc": ([vp, u32, vp], C.c_int),
         "mte_read_deltas": ([vp, u32, vp, u64, vp], C.c_int),
         "mte_set_event_capacity": ([vp, u32], C.c_int),
+        "mte_set_ref_capacity": ([vp, u32], C.c_int),
+        "mte_read_refs": ([vp, u32, vp, u32], C.c_int),
         "mte_read_segments": ([vp, u32, vp], C.c_int),
         "mte_doc_status": ([vp, vp, u32], C.c_int),
         "mte_stats_get": ([vp, vp], C.c_int),

@@ -43,6 +43,8 @@ ERROR_NAMES = {
 OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_ACK, OP_ROLLBACK = 0, 1, 2, 3, 4, 5
 OP_REGEN = 6          # Client.regeneratePendingOp (a local record; include/mte.h)
 OP_RBKEY = 7          # an annotate rollback's previous-value candidates (include/mte.h)
+OP_REF = 8            # create / remove a local reference (a local record; include/mte.h)
+REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE, REF_TRANSIENT = 0x40, 0x80, 0x100  # ReferenceType (ops.ts)
 DELTA_REGEN = 0x10    # kind flag of its output records
 ANNOTATE_SLOTS = 32   # pending local annotate groups tracked per document
 F_MARKER, F_MSG_END, F_REWRITE, F_LOCAL = 0x1, 0x2, 0x4, 0x8
@@ -119,9 +121,11 @@ EXPORTED_SYMBOLS = [
     "mte_digest_device", "mte_read_doc", "mte_read_segments", "mte_doc_status", "mte_stats_get", "mte_set_stats",
     "mte_comm_unique_id", "mte_comm_init", "mte_comm_share", "mte_comm_barrier", "mte_comm_allreduce_f64",
     "mte_comm_gather_digests", "mte_comm_world", "mte_comm_destroy", "mte_read_deltas", "mte_set_event_capacity",
+    "mte_set_ref_capacity", "mte_read_refs",
 ]
 
 DOC_EVENTS = 0x8
+DOC_REFS = 0x10
 DELTA_DTYPE = np.dtype([("op", "<u4"), ("kind", "<u4"), ("pos", "<i4"), ("len", "<i4"), ("removed", "<u4")])
 
 

@@ -122,7 +122,7 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
   h.min_seq = in.min_seq;
   h.cur_seq = in.cur_seq;
   h.status = 0;
-  h.flags = in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC | MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS);
+  h.flags = in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC | MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS | MTE_DOC_REFS);
   h.resume = 0;
   h.pad0 = h.pad1 = 0;
   if (legacy) {
@@ -429,6 +429,11 @@ struct mte_ctx {
   uint32_t* d_dl_n_s[2] = {nullptr, nullptr};
   uint64_t dl_n_cap_s[2] = {0, 0};
   int ev_slot = -1;
+  // local references of the MTE_DOC_REFS documents (mte_stream.h): ref_cap slots
+  // per document, zeroed at every reset
+  std::vector<uint8_t> h_refs;      // per doc: MTE_DOC_REFS
+  uint32_t ref_cap = 1024;
+  uint2* d_refs = nullptr;
   uint32_t* d_rs_docs = nullptr;    // legacy documents declared MTE_DOC_ROUND_SYNC (flat)
   int tree_rounds = 0;              // TIER 0 / TIER 1 rounds (MTE_TREE_ROUNDS; 0 = from the batch)
   // node level (mte_comm_*): the RCCL communicator and its staging buffers
@@ -517,9 +522,10 @@ void free_docs(mte_ctx* c) {
   if (c->d_wclock) (void)hipFree(c->d_wclock);
   c->d_wclock = nullptr;
   void* ps[] = {c->hdr, c->soa.len, c->stats, c->d_inits, c->d_init_props, c->d_digest, c->d_pairs,
-                c->d_tree, c->d_heap, c->d_tree_docs, c->d_rs_docs};
+                c->d_tree, c->d_heap, c->d_tree_docs, c->d_rs_docs, c->d_refs};
   for (void* p : ps)
     if (p) (void)hipFree(p);
+  c->d_refs = nullptr;
   c->d_rs_docs = nullptr;
   c->n_rs = 0;
   c->d_tree = nullptr;
@@ -544,6 +550,8 @@ int launch_reset(mte_ctx* c) {
                      c->d_inits, c->d_init_props, c->n_keys, c->n_docs, (const uint64_t*)c->d_img_off, c->d_tree,
                      c->kt);
   HIPCHK(c, hipGetLastError());
+  if (c->d_refs)
+    HIPCHK(c, hipMemsetAsync(c->d_refs, 0, sizeof(uint2) * (size_t)c->ref_cap * c->n_docs, c->stream));
   if (c->n_img) {
     const uint64_t nb = std::min<uint64_t>((c->n_img + 255) / 256, 65536);
     hipLaunchKernelGGL(image_kernel, dim3((uint32_t)nb), dim3(256), 0, c->stream, c->soa, c->cap,
@@ -598,9 +606,15 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
 
 // Validation of one op record (the kernels index with these fields, so a bad
 // record must never reach them).  Returns nullptr or the reason.
-const char* bad_op(const mte_op& o, const mte_batch* b, bool local_doc) {
-  if (o.type > MTE_OP_RBKEY) return "type";
+const char* bad_op(const mte_op& o, const mte_batch* b, bool local_doc, bool refs_doc, uint32_t ref_cap) {
+  if (o.type > MTE_OP_REF) return "type";
   if (o.type >= MTE_OP_ROLLBACK && !(o.flags & MTE_F_LOCAL)) return "rollback / regen without MTE_F_LOCAL";
+  if (o.type == MTE_OP_REF) {
+    if (!refs_doc) return "local reference record in a document without MTE_DOC_REFS";
+    if (o.seq != 0 || o.pos2 < 0 || (uint32_t)o.pos2 >= ref_cap || o.b > 1)
+      return "local reference record: seq, slot (mte_set_ref_capacity) or b out of range";
+    return nullptr;
+  }
   if ((o.flags & MTE_F_LOCAL) && o.type == MTE_OP_ANNOTATE && o.b != MTE_NO_PROPS && o.b >= MTE_ANNOTATE_SLOTS)
     return "annotate group slot out of range";
   if ((o.flags & MTE_F_LOCAL) || o.type == MTE_OP_ACK) {
@@ -662,7 +676,8 @@ int upload_ops(mte_ctx* c, const mte_batch* b, int w, uint64_t* bad, const char*
         for (uint64_t k = a; k < e; k++) {
           while (d + 1 < b->n_docs && b->op_offsets[d + 1] <= k0 + k) d++;
           const mte_op& o = b->ops[k0 + k];
-          if (const char* r = bad_op(o, b, !c->h_local.empty() && c->h_local[d])) {
+          if (const char* r = bad_op(o, b, !c->h_local.empty() && c->h_local[d], !c->h_refs.empty() && c->h_refs[d],
+                                     c->ref_cap)) {
             uint64_t cur = first_bad.load();
             while (k0 + k < cur && !first_bad.compare_exchange_weak(cur, k0 + k)) {
             }
@@ -811,6 +826,8 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     const mte_doc_init& in = docs[d];
     if ((uint64_t)in.text_off + in.text_len > text_units || in.text_len > 0x7fffffffu)
       return set_err(c, MTE_E_INVALID_ARG, "doc %u: initial text out of range", d);
+    if ((in.flags & MTE_DOC_REFS) && !(in.flags & MTE_DOC_LOCAL_CLIENT))
+      return set_err(c, MTE_E_UNSUPPORTED, "doc %u: local references need MTE_DOC_LOCAL_CLIENT", d);
     if ((in.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)) &&
         (!(in.flags & MTE_DOC_NEW_LENGTH_CALC) || c->cap >= kChunkMinCap))
       return set_err(c, MTE_E_UNSUPPORTED, "doc %u: a local client or delta events need the new length "
@@ -834,11 +851,14 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
   c->soa.plane_stride = nslots;
   c->h_local.assign(n_docs, 0);
   c->h_events.assign(n_docs, 0);
-  bool any_local = false;
+  c->h_refs.assign(n_docs, 0);
+  bool any_local = false, any_refs = false;
   for (uint32_t d = 0; d < n_docs; d++) {
     if (docs[d].flags & MTE_DOC_LOCAL_CLIENT) c->h_local[d] = 1, any_local = true;
     if (docs[d].flags & MTE_DOC_EVENTS) c->h_events[d] = 1;
+    if (docs[d].flags & MTE_DOC_REFS) c->h_refs[d] = 1, any_refs = true;
   }
+  if (any_refs) HIPCHK(c, hipMalloc((void**)&c->d_refs, sizeof(uint2) * (size_t)c->ref_cap * n_docs));
   // documents with a local client hold 2 kt + 1 more planes (mte_stream.h): the
   // pending property keys, the annotate-group mask and the keys' values before
   // their first pending annotate
@@ -994,7 +1014,9 @@ int mte_load_segments(mte_ctx* c, const uint64_t* seg_offsets, const mte_seg* se
       img[2 * n_segs + g] = (uint32_t)(sg.removed_seq == MTE_NOT_REMOVED ? kNone : sg.removed_seq);
       img[3 * n_segs + g] = sg.removed_seq == MTE_NOT_REMOVED ? 0u : sg.removers;
       img[4 * n_segs + g] = (uint32_t)(sg.client + 1) | (sg.kind << 8);
-      img[5 * n_segs + g] = marker ? 0u : sg.text_off;
+      // a marker of an MTE_DOC_REFS document is named by its index in the load
+      // (above every arena offset), as an inserted one by its reserved unit
+      img[5 * n_segs + g] = marker ? (c->h_refs[d] ? 0x80000000u + (uint32_t)(g - b) : 0u) : sg.text_off;
       {
         const uint64_t nd = e - b, k = g - b;
         int depth = 1;
@@ -1046,6 +1068,8 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
     if ((uint64_t)b->propsets[i].first + b->propsets[i].count > b->n_props)
       return set_err(c, MTE_E_INVALID_ARG, "propset %u out of range", i);
   if (c->arena_n + b->text_units >= (1ull << 32)) return set_err(c, MTE_E_OOM, "text arena exceeds 2^32 units");
+  if (c->d_refs && c->arena_n + b->text_units >= (1ull << 31))  // loaded markers are named above 2^31
+    return set_err(c, MTE_E_OOM, "text arena of a context with local references exceeds 2^31 units");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
   if (!c->up_stream) {
@@ -1163,6 +1187,8 @@ int mte_run(mte_ctx* c) {
   a.dl_off = evs ? c->d_dl_off_s[c->rslot] : nullptr;
   a.dl_n = evs ? c->d_dl_n_s[c->rslot] : nullptr;
   c->ev_slot = evs ? c->rslot : -1;
+  a.refs = c->d_refs;
+  a.ref_cap = c->ref_cap;
   // s_memrealtime runs at 100 MHz: ticks = ms x 1e5, scaled to this batch's ops
   a.eta = (c->last_ms > 0 && c->last_ops > 0) ? (unsigned long long)(c->last_ms * 1e5 * (double)c->n_ops / c->last_ops)
                                               : 0ull;
@@ -1319,6 +1345,54 @@ int mte_read_doc(mte_ctx* c, uint32_t doc, mte_doc_view* v) {
 int mte_set_event_capacity(mte_ctx* c, uint32_t per_op) {
   if (!c || per_op == 0 || per_op > (1u << 16)) return MTE_E_INVALID_ARG;
   c->ev_per_op = per_op;
+  return MTE_OK;
+}
+
+int mte_set_ref_capacity(mte_ctx* c, uint32_t per_doc) {
+  if (!c || per_doc == 0 || per_doc > (1u << 20)) return MTE_E_INVALID_ARG;
+  if (c->d_refs) return set_err(c, MTE_E_STATE, "mte_set_ref_capacity after mte_load_docs of MTE_DOC_REFS documents");
+  c->ref_cap = per_doc;
+  return MTE_OK;
+}
+
+// referencePositionToLocalPosition (mergeTree.ts:1095-1112) of slots [0, n):
+// the own-view position of the segment holding the reference's unit plus its
+// offset there (0 on a removed segment); -1 for a detached or unused slot or a
+// unit no segment holds any more (a tombstone compacted at minSeq)
+int mte_read_refs(mte_ctx* c, uint32_t doc, int32_t* pos, uint32_t n) {
+  if (!c || (n && !pos) || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  if (c->h_refs.empty() || !c->h_refs[doc]) return set_err(c, MTE_E_INVALID_ARG, "doc %u: no MTE_DOC_REFS", doc);
+  if (n > c->ref_cap) return set_err(c, MTE_E_INVALID_ARG, "%u reference slots > capacity %u", n, c->ref_cap);
+  HIPCHK(c, hipSetDevice(c->device));
+  DocHdr h;
+  HIPCHK(c, hipMemcpyAsync(&h, c->hdr + doc, sizeof(DocHdr), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint32_t ns = (uint32_t)std::max(h.nseg, 0);
+  const uint64_t db = (uint64_t)doc * c->cap;
+  std::vector<int32_t> len(ns + 1), rseq(ns + 1);
+  std::vector<uint32_t> toff(ns + 1);
+  std::vector<uint2> rt(n + 1);
+  if (ns) {
+    HIPCHK(c, hipMemcpyAsync(len.data(), c->soa.len + db, ns * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(rseq.data(), c->soa.rseq + db, ns * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(toff.data(), c->soa.toff + db, ns * 4, hipMemcpyDeviceToHost, c->stream));
+  }
+  if (n)
+    HIPCHK(c, hipMemcpyAsync(rt.data(), c->d_refs + (uint64_t)doc * c->ref_cap, n * sizeof(uint2),
+                             hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (uint32_t r = 0; r < n; r++) {
+    pos[r] = -1;
+    if (!(rt[r].y & kRefLive) || (rt[r].y & kRefDetached)) continue;
+    int64_t p = 0;
+    for (uint32_t i = 0; i < ns; i++) {
+      if (rt[r].x - toff[i] < (uint32_t)len[i]) {
+        pos[r] = (int32_t)(p + (rseq[i] != kNone ? 0 : (int64_t)(rt[r].x - toff[i])));
+        break;
+      }
+      p += rseq[i] == kNone ? len[i] : 0;
+    }
+  }
   return MTE_OK;
 }
 

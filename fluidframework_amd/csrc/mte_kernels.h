@@ -102,6 +102,11 @@ struct ReplayArgs {
   mte_delta* dl;
   const uint64_t* dl_off;
   uint32_t* dl_n;
+  // MTE_DOC_REFS documents: local reference slots of doc d at refs[d * ref_cap ..]
+  // (x = the arena offset of the unit the reference sits on, y = kRefLive |
+  // kRefDetached | refType; mte_stream.h)
+  uint2* refs;
+  uint32_t ref_cap;
 };
 
 // ---- wavefront primitives --------------------------------------------------

@@ -760,6 +760,7 @@ __device__ __forceinline__ int pick_pass1_tier(DocRun& D, uint32_t cap) {
   }
   if (D.n + 2 <= kWave) return 1;
   if (D.n + 2 <= 2 * kWave) return 2;
+  if (MTE_PASS1_EMAX == 3 && D.n + 2 <= 3 * kWave) return 3;
   if (MTE_PASS1_EMAX >= 4 && D.n + 2 <= 4 * kWave) return 4;
   D.flags |= kHdrNeedsEsc;  // continue in the big-doc pass
   D.running = false;
@@ -857,7 +858,9 @@ __device__ __forceinline__ void pass1_burst(DocRun& D, const ReplayArgs& a, uint
 #else
   if (e == 1) burst_run<1, K, S>(D, a, zlds, 1, kBurst);
   else if (e == 2) burst_run<2, K, S>(D, a, zlds, 1, kBurst);
-  else if constexpr (MTE_PASS1_EMAX >= 4) {
+  else if constexpr (MTE_PASS1_EMAX == 3) {
+    if (e == 3) burst_run<3, K, S>(D, a, zlds, 1, kBurst);
+  } else if constexpr (MTE_PASS1_EMAX >= 4) {
 #if MTE_OUTLINE_E4
     if (e == 4) burst_out<4, K, S>(D, a, zlds);
 #else

@@ -65,6 +65,26 @@ __device__ __forceinline__ void perm_plane(T (&F)[E], int addr) {
   F[0] = perm1(F[0], addr);
 }
 
+#ifndef MTE_SHIFT_SEQ_EMIN  // tiers with E >= this shift one plane at a time (register-light)
+#define MTE_SHIFT_SEQ_EMIN 4
+#endif
+
+// one plane of shift_v: its two cross-lane moves, then its selects.  The E = 4
+// tier shifts plane by plane: moving all 13 planes' neighbours first needs 52
+// temporaries on top of 40 state registers, which spilled the whole pass-1
+// kernel (its register budget is that of its largest tier)
+template <int E, typename T>
+__device__ __forceinline__ void shift_plane(T (&F)[E], const bool (&g1)[E], const bool (&g2)[E]) {
+  const T p1 = (T)lane_prev((int32_t)F[E - 1]);
+  const T p2 = (T)lane_prev((int32_t)F[E >= 2 ? E - 2 : 0]);
+#pragma unroll
+  for (int j = E - 1; j >= 0; j--) {
+    const T m1 = (j >= 1) ? F[j >= 1 ? j - 1 : 0] : p1;
+    const T m2 = (j >= 2) ? F[j >= 2 ? j - 2 : 0] : ((j == 1) ? p1 : p2);
+    F[j] = g2[j] ? m2 : (g1[j] ? m1 : F[j]);
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ void shift1_dpp(T (&F)[1], bool g1, bool g2) {
   const int32_t p1 = lane_prev((int32_t)F[0]);
@@ -102,6 +122,17 @@ __device__ __forceinline__ void shift_v(Regs<E, K>& R, int32_t (&X)[NX > 0 ? NX 
     for (int k = 0; k < K; k++) perm_plane<E>(R.pr[k], addr);
 #pragma unroll
     for (int x = 0; x < NX; x++) perm_plane<E>(X[x], addr);
+  } else if constexpr (E >= MTE_SHIFT_SEQ_EMIN) {
+    shift_plane<E>(R.len, g1, g2);
+    shift_plane<E>(R.seq, g1, g2);
+    shift_plane<E>(R.rseq, g1, g2);
+    shift_plane<E>(R.rmask, g1, g2);
+    shift_plane<E>(R.meta, g1, g2);
+    shift_plane<E>(R.toff, g1, g2);
+#pragma unroll
+    for (int k = 0; k < K; k++) shift_plane<E>(R.pr[k], g1, g2);
+#pragma unroll
+    for (int x = 0; x < NX; x++) shift_plane<E>(X[x], g1, g2);
   } else {
     constexpr int NF = kFieldPlanes + K + NX;
     uint32_t last[NF], last2[NF];

@@ -410,12 +410,138 @@ __device__ __forceinline__ void stream_regen(const uint32_t* pl, uint64_t sd, in
   }
 }
 
+// ---- local references (MTE_DOC_REFS, include/mte.h) -------------------------
+// A reference is kept as the text unit it sits on -- its arena offset (a
+// marker's is its reserved unit): splits never copy text, so the unit names the
+// same place in whatever segment holds it, which is what LocalReferenceCollection
+// keeps as (segment, offset) and moves on split (localReference.ts:391-416).
+constexpr uint32_t kRefLive = 0x80000000u, kRefDetached = 0x40000000u;
+
+// a segment references may slide to (_getSlideToSegment, mergeTree.ts:893-913):
+// not a pending insert and not removed-and-acked (a pending removal is fine)
+__device__ __forceinline__ bool slide_ok(int32_t sq, int32_t rs) { return sq < kLocalBase && rs >= kLocalBase; }
+
+// the first slot a reference may slide to after x (dir > 0) or before it
+// (dir < 0), or -1; x is wave-uniform
+__device__ int find_slide_target(const uint32_t* pl, uint64_t sd, int n, int x, int dir) {
+  const int l = lane_id();
+  if (dir > 0) {
+    for (int b = x + 1; b < n; b += kWave) {
+      const int i = b + l;
+      const int ic = i < n ? i : 0;  // unconditional loads, selected after
+      const int32_t sq = (int32_t)ld_l2(pl + sd + ic), rs = (int32_t)ld_l2(pl + 2 * sd + ic);
+      const uint64_t m = __ballot(i < n && slide_ok(sq, rs));
+      if (m) return b + __ffsll((long long)m) - 1;
+    }
+  } else {
+    for (int e = x; e > 0; e -= kWave) {  // slots [e - 64, e)
+      const int i = e - kWave + l;
+      const int ic = i >= 0 ? i : 0;
+      const int32_t sq = (int32_t)ld_l2(pl + sd + ic), rs = (int32_t)ld_l2(pl + 2 * sd + ic);
+      const uint64_t m = __ballot(i >= 0 && slide_ok(sq, rs));
+      if (m) return e - kWave + (63 - __builtin_clzll(m));
+    }
+  }
+  return -1;
+}
+
+// slideAckedRemovedSegmentReferences (mergeTree.ts:921-950) for every segment
+// the op of seq s made removed-and-acked -- its removedSeq is now s: a remote
+// remove's new removals and the pending ones it overtook (:1936-1938,
+// 1986-1993), or the local removals an ack sequenced (:1302-1304).  Each such
+// segment's SlideOnRemove references move to offset 0 of the first following
+// segment they may slide to (addBeforeTombstones), else to the last offset of
+// the last preceding one (addAfterTombstones), else detach; Simple references
+// detach (localReference.ts:422-485).  Slots [0, rhi) of the table rt.
+__device__ void stream_slide(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t rhi, int32_t s) {
+  const int l = lane_id();
+  for (int tb = 0; tb < n; tb += kWave) {
+    const int i = tb + l;
+    const int32_t rs = (int32_t)ld_l2(pl + 2 * sd + (i < n ? i : 0));
+    uint64_t m = __ballot(i < n && rs == s);
+    while (m) {
+      const int x = tb + __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const uint32_t toff = uni(ld_l2(pl + 5 * sd + x)), len = uni(ld_l2(pl + x));
+      int t = find_slide_target(pl, sd, n, x, 1);
+      bool after = false;
+      if (t < 0) {
+        t = find_slide_target(pl, sd, n, x, -1);
+        after = t >= 0;
+      }
+      uint32_t to = 0;
+      if (t >= 0) {
+        const uint32_t tt = uni(ld_l2(pl + 5 * sd + t)), tl = uni(ld_l2(pl + t));
+        to = after ? tt + tl - 1u : tt;
+      }
+      for (uint32_t rb = 0; rb < rhi; rb += kWave) {
+        const uint32_t r = rb + (uint32_t)l;
+        const uint32_t rc = r < rhi ? r : 0u;  // unconditional loads, selected after
+        const uint32_t anc = ld_l2(&rt[rc].x), st = ld_l2(&rt[rc].y);
+        if (r < rhi && (st & kRefLive) && !(st & kRefDetached) && anc - toff < len) {
+          if ((st & MTE_REF_SLIDE_ON_REMOVE) && t >= 0) rt[r].x = to;
+          else rt[r].y = st | kRefDetached;
+        }
+      }
+      vm_drain();
+    }
+  }
+}
+
+// MTE_OP_REF (a local record): createLocalReferencePosition on the segment and
+// offset getContainingSegment(pos1) finds in the local view (client.ts:360-364,
+// 1107-1110; mergeTree.ts:872-885, 2124-2143), or removeLocalReferencePosition
+// (b = 1, mergeTree.ts:2113-2123).  rhi: slots in use so far.
+__device__ int stream_ref(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t& rhi, const s8v& op) {
+  const uint32_t slot = (uint32_t)op[5];
+  if ((uint32_t)op[7] == 1u) {
+    if (lane_id() == 0) rt[slot] = make_uint2(0u, 0u);
+    vm_drain();
+    return 0;
+  }
+  if ((uint32_t)op[6] & (MTE_REF_STAY_ON_REMOVE | MTE_REF_TRANSIENT)) return MTE_E_UNSUPPORTED;
+  const int32_t pos = op[4];
+  const int l = lane_id();
+  int32_t carry = 0;
+  for (int tb = 0; tb < n; tb += kTile) {
+    int32_t L[kTileE], P[kTileE];
+    uint32_t tf[kTileE];
+#pragma unroll
+    for (int j = 0; j < kTileE; j++) {
+      const int i = tb + l * kTileE + j;
+      const int ic = i < n ? i : 0;  // unconditional loads, selected after
+      const int32_t ln = (int32_t)ld_l2(pl + ic), rs = (int32_t)ld_l2(pl + 2 * sd + ic);
+      tf[j] = ld_l2(pl + 5 * sd + ic);
+      L[j] = (i < n && rs == kNone) ? ln : 0;  // the local view: removed -> 0
+    }
+    const int32_t tot = prefix<kTileE>(L, P);
+    bool hit = false;
+    uint32_t anc = 0;
+#pragma unroll
+    for (int j = 0; j < kTileE; j++) {
+      const bool h = L[j] > 0 && pos >= carry + P[j] && pos < carry + P[j] + L[j];
+      anc = h ? tf[j] + (uint32_t)(pos - carry - P[j]) : anc;
+      hit = hit || h;
+    }
+    const uint64_t m = __ballot(hit);
+    if (m) {
+      const uint32_t a0 = rdlane(anc, __ffsll((long long)m) - 1);
+      if (l == 0) rt[slot] = make_uint2(a0, kRefLive | ((uint32_t)op[6] & 0xffffu));
+      vm_drain();
+      if (slot + 1 > rhi) rhi = slot + 1;
+      return 0;
+    }
+    carry += tot;
+  }
+  return MTE_E_INVALID_ARG;  // no segment holds pos in the local view
+}
+
 // One op of one HBM-resident document (see the file comment).  Returns 0 or
 // a negative MTE_E_*.  lseq: the document's last localSeq (local-client docs);
 // ev: its delta events (MTE_DOC_EVENTS docs).
 template <int K, bool S>
 __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const ReplayArgs& a, uint32_t* zlds,
-                           int32_t& lseq, EvOut& ev) {
+                           int32_t& lseq, EvOut& ev, uint32_t& rhi) {
   constexpr int E = kTileE;
   const int l = lane_id();
   uint32_t* pl = a.planes + (uint64_t)D.doc * a.cap;
@@ -431,6 +557,18 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
+  const bool refd = (D.flags & MTE_DOC_REFS) != 0 && a.refs != nullptr;
+  uint2* const rt = refd ? a.refs + (uint64_t)D.doc * a.ref_cap : nullptr;
+  if (type == MTE_OP_REF) {
+    if (!(flags & MTE_F_LOCAL) || !ldoc || !refd) return MTE_E_UNSUPPORTED;
+    if ((uint32_t)op[5] >= a.ref_cap || (uint32_t)op[7] > 1u) return MTE_E_INVALID_ARG;
+    MTE_STAT(st[kStOps]++;)
+    MTE_STAT(if ((uint32_t)op[7] == 0u) st[kStScanned] += (uint32_t)D.n;)
+    const int rc = stream_ref(pl, sd, D.n, rt, rhi, op);
+    if (rc) return rc;
+    D.k++;
+    return 0;
+  }
   if (type > MTE_OP_REGEN) return MTE_E_INVALID_ARG;  // MTE_OP_RBKEY only after an annotate's rollback
   const bool lop = (flags & MTE_F_LOCAL) != 0;  // a local op: the local view, seq = localSeq
   if ((lop || type >= MTE_OP_ACK) && !ldoc) return MTE_E_UNSUPPORTED;
@@ -486,6 +624,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
     if (!(pos1 > 0 && pos1 <= pos2 && pos2 <= lseq)) return MTE_E_INVALID_ARG;
     MTE_STAT(st[kStScanned] += (uint32_t)n;)
     stream_ack<K>(pl, sd, n, pos1, pos2, s, (uint32_t)op[6]);
+    if (refd && rhi) stream_slide(pl, sd, n, rt, rhi, s);
   }
   if (ins || rng) {
     MTE_STAT(st[kStScanned] += (uint32_t)n;)
@@ -646,7 +785,8 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
         pl[2 * sd + g] = (uint32_t)kNone;
         pl[3 * sd + g] = 0u;
         pl[4 * sd + g] = (c + 1u) | (marker ? (1u + (uint32_t)pos2) << 8 : 0u);
-        pl[5 * sd + g] = marker ? 0u : a.text_base + (uint32_t)op[6];
+        // a marker of an MTE_DOC_REFS document takes its reserved text unit (its name)
+        pl[5 * sd + g] = (marker && !refd) ? 0u : a.text_base + (uint32_t)op[6];
       }
     }
     if (g >= 0) {
@@ -823,6 +963,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
       MTE_STAT(st[kStWritten] += cnt_all;)
       if (type == MTE_OP_ANNOTATE) st[kStPwrites] += cnt_all * (uint32_t)q2[3];
       vm_drain();
+      if (rem && !lop && refd && rhi) stream_slide(pl, sd, n, rt, rhi, s);
     }
   }
   D.n = n;
@@ -910,6 +1051,7 @@ __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
   run_init(D, a, doc, !(hf & kOwn));
   uint32_t st[kNumStats] = {};
   int32_t lseq = (int32_t)a.hdr[doc].pad0;  // local-client docs: the last localSeq
+  uint32_t rhi = (hf & MTE_DOC_REFS) ? a.hdr[doc].pad1 : 0u;  // MTE_DOC_REFS docs: reference slots in use
   EvOut ev{nullptr, 0, 0u, 0u};
   if ((hf & MTE_DOC_EVENTS) && a.dl_off) {
     ev.p = a.dl + a.dl_off[doc];
@@ -918,7 +1060,7 @@ __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
   if (D.running) {
     s8v cur = sload8(D.recp + 2 * D.k);
     while (D.running) {
-      const int rc = stream_step<K, S>(D, st, cur, a, zlds_all[w], lseq, ev);
+      const int rc = stream_step<K, S>(D, st, cur, a, zlds_all[w], lseq, ev, rhi);
       if (rc < 0) {
         D.status = rc;
         D.running = false;
@@ -931,6 +1073,7 @@ __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
     if constexpr (S) run_flush_stats(D, st, a);
   }
   if ((hf & MTE_DOC_LOCAL_CLIENT) && lane_id() == 0) a.hdr[doc].pad0 = (uint32_t)lseq;  // run_finish keeps it
+  if ((hf & MTE_DOC_REFS) && lane_id() == 0) a.hdr[doc].pad1 = rhi;
   if ((hf & MTE_DOC_EVENTS) && a.dl_n && lane_id() == 0) a.dl_n[doc] = ev.n;
   run_finish(D, a);
 }

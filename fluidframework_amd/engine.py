@@ -76,6 +76,13 @@ class EngineBase:
         self._check(self._read_deltas(doc, ptr(out), n.value, C.byref(n)), "read_deltas")
         return out[: n.value]
 
+    def read_refs(self, doc, n):
+        """Positions of local reference slots [0, n) of an MTE_DOC_REFS doc in its
+        own view (localReferencePositionToPosition; -1 = detached / unused)."""
+        out = np.zeros(max(n, 1), np.int32)
+        self._check(self._read_refs(doc, ptr(out), n), "read_refs")
+        return out[:n]
+
     def read_segments(self, doc):
         """-> (segs SEG_DTYPE[n] with text_off into text, props uint32[n, n_keys], text uint16[])."""
         v = MteSegList()
@@ -221,6 +228,12 @@ class DeviceEngine(EngineBase):
 
     def set_event_capacity(self, per_op):
         self._check(self.lib.mte_set_event_capacity(self.ctx, per_op), "set_event_capacity")
+
+    def set_ref_capacity(self, per_doc):
+        self._check(self.lib.mte_set_ref_capacity(self.ctx, per_doc), "set_ref_capacity")
+
+    def _read_refs(self, doc, p, n):
+        return self.lib.mte_read_refs(self.ctx, doc, p, n)
 
     def _digest(self, p, n):
         return self.lib.mte_digest(self.ctx, p, n)

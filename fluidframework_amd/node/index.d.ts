@@ -60,6 +60,8 @@ export interface ClientOptions {
   longClientId?: string;
   /** Record delta events (MTE_DOC_EVENTS; needs newLengthCalc): BatchClient.on("sequenceDelta"). */
   events?: boolean;
+  /** Hold local references (MTE_DOC_REFS; needs localClient): createLocalReferencePosition. */
+  refs?: boolean;
   newLengthCalc?: boolean;
   props?: PropertySet;
   minSeq?: number;
@@ -188,8 +190,30 @@ export interface SequenceDeltaEvent {
   last: SequenceDeltaRange;
 }
 
+/** ReferenceType flags (ops.ts): Simple 0, SlideOnRemove 0x40 (StayOnRemove / Transient unsupported). */
+export class LocalReferencePosition {
+  readonly refType: number;
+  properties?: PropertySet;
+  addProperties(newProps: PropertySet): void;
+  getProperties(): PropertySet | undefined;
+}
+
+/** getContainingSegment's snapshot of a visible segment. */
+export interface SegmentSnapshot {
+  start: number;
+  length: number;
+  kind: number;
+}
+
 export class BatchClient {
   readonly mergeTree: BatchMergeTree;
+  // local references ({localClient: true, refs: true} documents)
+  getContainingSegment(pos: number): { segment: SegmentSnapshot | undefined; offset: number | undefined };
+  createLocalReferencePosition(segment: SegmentSnapshot | number, offset: number | undefined, refType: number,
+    properties?: PropertySet): LocalReferencePosition;
+  removeLocalReferencePosition(lref: LocalReferencePosition): LocalReferencePosition | undefined;
+  /** -1 (DetachedReferencePosition) once detached or removed. */
+  localReferencePositionToPosition(lref: LocalReferencePosition): number;
   readonly longClientId: string;
   /** A remote message, or (localClient documents) the sequenced message of an own op: its ack. */
   applyMsg(msg: ISequencedDocumentMessage, local?: boolean): void;

@@ -120,9 +120,10 @@ class MergeTreeEngine {
     if ((o.localClient || o.events) && !o.newLengthCalc) {
       throw new MergeTreeError(-9, "a local client or delta events need the new length calculation");
     }
+    if (o.refs && !o.localClient) throw new MergeTreeError(-9, "local references need {localClient: true}");
     this.docs.push({ text: initialText || "", newLengthCalc: !!o.newLengthCalc, roundSync: !!o.roundSync, props: o.props,
       minSeq: o.minSeq || 0, currentSeq: o.currentSeq || 0, segments: o.segments, localClient: !!o.localClient,
-      events: !!o.events });
+      events: !!o.events, refs: !!o.refs });
     const c = new BatchClient(this, doc, o.observerId === undefined ? (o.longClientId || "A") : o.observerId,
       !!o.localClient);
     this.clients.push(c);
@@ -161,6 +162,7 @@ class MergeTreeEngine {
     this.track = this.docs.some((d) => d.events) ? this.docs.map((d) => !!d.events) : null;
     this.pending = new BatchBuilder(this.docs.length, this.interner, this.track);
     this.views = new Array(this.docs.length).fill(null);
+    this.refViews = new Array(this.docs.length).fill(null);
     this.docs.forEach((d, i) => { if (d.catchup) for (const m of d.catchup) this.clients[i].applyMsg(m); });
   }
 
@@ -184,6 +186,7 @@ class MergeTreeEngine {
     this.inflightSrc = this.pending.recSrc;
     this.pending = new BatchBuilder(this.docs.length, this.interner, this.track);
     this.views.fill(null);
+    this.refViews.fill(null);
     this.addon.submit(this.ctx, b.offsets, b.ops, b.text, b.propsets, b.props);
     this.addon.run(this.ctx);
     this.running = true;
@@ -239,6 +242,19 @@ class MergeTreeEngine {
       this.views[doc] = v;
     }
     if (v.status !== 0) throw docError(v.status, doc);
+    return v;
+  }
+
+  /** Positions of a document's local reference slots after the last replay
+   *  (mte_read_refs), read once per flush. */
+  _refView(doc) {
+    this.flush();
+    this.sync();
+    let v = this.refViews[doc];
+    if (v === null) {
+      v = new Int32Array(this.addon.readRefs(this.ctx, doc, this.clients[doc].clients.refNext).buffer);
+      this.refViews[doc] = v;
+    }
     return v;
   }
 
@@ -330,6 +346,24 @@ class MergeTreeEngine {
       this.addon.destroy(this.ctx);
       this.ctx = null;
     }
+  }
+}
+
+/** A local reference (LocalReferencePosition, localReference.ts:44-118): its
+ *  engine slot, ReferenceType and properties. */
+class LocalReferencePosition {
+  constructor(client, slot, refType, properties) {
+    this.client = client;
+    this.slot = slot;
+    this.refType = refType;
+    this.properties = properties;
+  }
+  addProperties(newProps) {
+    this.properties = Object.assign({}, this.properties || {}, newProps);
+    for (const k of Object.keys(newProps)) if (newProps[k] === null) delete this.properties[k];
+  }
+  getProperties() {
+    return this.properties;
   }
 }
 
@@ -533,6 +567,59 @@ class BatchClient {
     const op = packing.regenOps(resetOp, idx, this.regenRecs);
     this.regenRecs = null;
     return op;
+  }
+
+  // ---- local references (documents created with {localClient: true, refs: true}) ----
+  // LocalReferenceCollection (localReference.ts:139-567) held by the engine
+  // (MTE_DOC_REFS): a reference sits on a text unit of this client's view and
+  // slides with it (slideAckedRemovedSegmentReferences, mergeTree.ts:893-950).
+
+  /** Client.getContainingSegment (client.ts:1107-1110) in this client's view:
+   *  {segment: {start, length, kind}, offset}, or {segment: undefined} past the
+   *  end.  The segment is a snapshot of the visible segment holding pos (the
+   *  engine keeps no segment objects); pass it to createLocalReferencePosition
+   *  before queuing another op. */
+  getContainingSegment(pos) {
+    const v = this.engine._view(this.doc);
+    let start = 0;
+    for (let i = 0; i < v.segLen.length; i++) {
+      const n = v.segLen[i];
+      if (pos >= start && pos < start + n) {
+        return { segment: { start, length: n, kind: v.segKind[i] }, offset: pos - start };
+      }
+      start += n;
+    }
+    return { segment: undefined, offset: undefined };
+  }
+
+  /** Client.createLocalReferencePosition (client.ts:360-364): a reference at
+   *  offset of segment (from getContainingSegment; a number is taken as a
+   *  position of this client's view).  refType: ReferenceType flags --
+   *  SlideOnRemove (0x40) or Simple (0), with any label bits; StayOnRemove and
+   *  Transient throw.  Queued with the document's next replay. */
+  createLocalReferencePosition(segment, offset, refType, properties) {
+    if (!this.engine.docs[this.doc].refs) throw new MergeTreeError(-9, "createClient(..., {refs: true}) first");
+    const base = typeof segment === "number" ? segment : (segment && typeof segment.start === "number" ? segment.start : NaN);
+    if (Number.isNaN(base)) throw new MergeTreeError(-1, "createLocalReferencePosition: no segment");
+    const rt = refType === undefined ? 0 : refType;
+    const slot = this.engine._batch().addRef(this.doc, this.clients, base + (offset || 0), rt);
+    return new LocalReferencePosition(this, slot, rt, properties);
+  }
+
+  /** Client.removeLocalReferencePosition (client.ts:369-371). */
+  removeLocalReferencePosition(lref) {
+    if (!lref || lref.client !== this || lref.slot < 0) return undefined;
+    this.engine._batch().removeRef(this.doc, this.clients, lref.slot);
+    lref.slot = -1;
+    return lref;
+  }
+
+  /** Client.localReferencePositionToPosition (client.ts:376-378): the
+   *  reference's position in this client's view, -1 (DetachedReferencePosition)
+   *  once it is detached or removed. */
+  localReferencePositionToPosition(lref) {
+    if (!lref || lref.client !== this || lref.slot < 0) return -1;
+    return this.engine._refView(this.doc)[lref.slot];
   }
 
   /** Local ops sent but not acknowledged yet. */
@@ -840,4 +927,4 @@ function loadLegacy(blobs) {
   return { segments: specs, minSeq: md.minSequenceNumber !== undefined ? md.minSequenceNumber : seq, currentSeq: seq };
 }
 
-module.exports = { MergeTreeEngine, BatchClient, MergeTreeError, loadAddon, loadLegacy, packing };
+module.exports = { MergeTreeEngine, BatchClient, LocalReferencePosition, MergeTreeError, loadAddon, loadLegacy, packing };

@@ -571,6 +571,47 @@ static napi_value js_set_event_capacity(napi_env env, napi_callback_info info) {
   return NULL;
 }
 
+/* setRefCapacity(ctx, perDoc) (mte_set_ref_capacity) */
+static napi_value js_set_ref_capacity(napi_env env, napi_callback_info info) {
+  napi_value argv[2];
+  if (!get_args(env, info, 2, argv)) return NULL;
+  mte_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  uint32_t per = 0;
+  if (napi_get_value_uint32(env, argv[1], &per) != napi_ok) {
+    napi_throw_type_error(env, NULL, "setRefCapacity: the per-document capacity must be a number");
+    return NULL;
+  }
+  throw_rc(env, mte_set_ref_capacity(ctx, per), ctx, "mte_set_ref_capacity");
+  return NULL;
+}
+
+/* readRefs(ctx, doc, n) -> Int32Array(n): positions of reference slots [0, n)
+   (mte_read_refs; -1 detached / unused) */
+static napi_value js_read_refs(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  if (!get_args(env, info, 3, argv)) return NULL;
+  mte_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  uint32_t doc = 0, n = 0;
+  if (napi_get_value_uint32(env, argv[1], &doc) != napi_ok || napi_get_value_uint32(env, argv[2], &n) != napi_ok) {
+    napi_throw_type_error(env, NULL, "readRefs: doc and n must be numbers");
+    return NULL;
+  }
+  int32_t* buf = (int32_t*)malloc((size_t)(n ? n : 1) * sizeof(int32_t));
+  if (!buf) {
+    napi_throw_error(env, NULL, "out of memory");
+    return NULL;
+  }
+  if (throw_rc(env, mte_read_refs(ctx, doc, buf, n), ctx, "mte_read_refs")) {
+    free(buf);
+    return NULL;
+  }
+  napi_value out = u32_array(env, (const uint32_t*)buf, (size_t)n);
+  free(buf);
+  return out;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
   const napi_property_descriptor d[] = {
       {"abiVersion", NULL, js_abi_version, NULL, NULL, NULL, napi_enumerable, NULL},
@@ -598,6 +639,8 @@ static napi_value init(napi_env env, napi_value exports) {
       {"commDestroy", NULL, js_comm_destroy, NULL, NULL, NULL, napi_enumerable, NULL},
       {"readDeltas", NULL, js_read_deltas, NULL, NULL, NULL, napi_enumerable, NULL},
       {"setEventCapacity", NULL, js_set_event_capacity, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"setRefCapacity", NULL, js_set_ref_capacity, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"readRefs", NULL, js_read_refs, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   if (napi_define_properties(env, exports, sizeof d / sizeof d[0], d) != napi_ok) return NULL;
   return exports;

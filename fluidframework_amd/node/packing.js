@@ -30,6 +30,8 @@
 
 const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 3, OP_ACK = 4, OP_ROLLBACK = 5, OP_REGEN = 6;
 const OP_RBKEY = 7;          // MTE_OP_RBKEY: an annotate rollback's previous-value candidates
+const OP_REF = 8;            // MTE_OP_REF: create / remove a local reference
+const REF_SLIDE_ON_REMOVE = 0x40, REF_STAY_ON_REMOVE = 0x80, REF_TRANSIENT = 0x100;  // ReferenceType (ops.ts)
 const DELTA_REGEN = 0x10;    // MTE_DELTA_REGEN: kind flag of a regenerated op's records
 const ANNOTATE_SLOTS = 32;   // MTE_ANNOTATE_SLOTS: pending local annotate groups tracked per document
 const F_MARKER = 0x1, F_MSG_END = 0x2, F_REWRITE = 0x4, F_LOCAL = 0x8;
@@ -45,6 +47,7 @@ const INSERT = 0, REMOVE = 1, ANNOTATE = 2, GROUP = 3;
 
 const DOC_ROUND_SYNC = 0x2; // MTE_DOC_ROUND_SYNC (include/mte.h)
 const DOC_LOCAL_CLIENT = 0x4; // MTE_DOC_LOCAL_CLIENT
+const DOC_REFS = 0x10;       // MTE_DOC_REFS
 const DOC_EVENTS = 0x8; // MTE_DOC_EVENTS
 const E_INVALID_ARG = -1, E_UNSUPPORTED = -9, E_STATE = -10, E_CLIENT_RANGE = -12;
 
@@ -156,6 +159,10 @@ class DocClients {
     // restate exactly (as packing.py)
     this.annProps = new Map();
     this.noRollback = new Set();
+    // local reference slots (MTE_DOC_REFS documents): the next unused one and the
+    // removed ones, reused first (as packing.py)
+    this.refNext = 0;
+    this.refFree = [];
   }
   short(longId, seq) {
     let i = longId === this.lastId ? this.lastSlot : this.ids.get(longId);
@@ -406,7 +413,8 @@ class BatchBuilder {
         this._put(doc, seq, ref, msn, OP_INSERT, 0, 0, pos, tx[1], tx[0], this.props.add(seg.props));
       } else if (typeof seg === "object" && "marker" in seg) {
         const rt = checkI32(seg.marker.refType === undefined ? 0 : seg.marker.refType, "refType");
-        this._put(doc, seq, ref, msn, OP_INSERT, 0, F_MARKER, pos, rt, 0, this.props.add(seg.props));
+        const off = this._text("\ufffc")[0];  // one reserved unit names the marker in MTE_DOC_REFS documents
+        this._put(doc, seq, ref, msn, OP_INSERT, 0, F_MARKER, pos, rt, off, this.props.add(seg.props));
       } else {
         throw new MergeTreeError(E_INVALID_ARG, "Unrecognized IJSONSegment type: " + JSON.stringify(seg));
       }
@@ -564,6 +572,35 @@ class BatchBuilder {
     return idx;
   }
 
+  /** Client.createLocalReferencePosition on getContainingSegment(pos) in the
+   *  local view (client.ts:360-364, 1107-1110): an MTE_OP_REF record in an
+   *  MTE_DOC_REFS document (as packing.py add_ref).  Returns the slot. */
+  addRef(doc, clients, pos, refType) {
+    if (!clients.local) throw new MergeTreeError(E_UNSUPPORTED, "local reference in an observer document");
+    const rt = checkI32(refType === undefined ? REF_SLIDE_ON_REMOVE : refType, "refType");
+    if (rt < 0 || (rt & (REF_STAY_ON_REMOVE | REF_TRANSIENT))) {
+      throw new MergeTreeError(E_UNSUPPORTED, "StayOnRemove / Transient local references");
+    }
+    const p = checkI32(pos, "pos");
+    const slot = clients.refFree.length ? clients.refFree.pop() : clients.refNext;
+    if (slot === clients.refNext) clients.refNext++;
+    this._put(doc, 0, 0, 0, OP_REF, 0, F_LOCAL, p, slot, rt, 0);
+    const src = this._src(doc);
+    if (src) src.push({ msg: null, op: undefined, local: true });
+    return slot;
+  }
+
+  /** removeLocalReferencePosition (mergeTree.ts:2113-2123). */
+  removeRef(doc, clients, slot) {
+    if (!(slot >= 0 && slot < clients.refNext) || clients.refFree.includes(slot)) {
+      throw new MergeTreeError(E_INVALID_ARG, "no local reference in slot " + slot);
+    }
+    clients.refFree.push(slot);
+    this._put(doc, 0, 0, 0, OP_REF, 0, F_LOCAL, -1, slot, 0, 1);
+    const src = this._src(doc);
+    if (src) src.push({ msg: null, op: undefined, local: true });
+  }
+
   /** One MergeTree-level call (insertSegments / markRangeRemoved / annotateRange):
    *  a record that does not close a message (no window update). */
   addRaw(doc, seq, ref, msn, client, op) {
@@ -611,7 +648,8 @@ class BatchBuilder {
         recs.push([OP_INSERT, 0, pos, tx[1], tx[0], this.props.add(seg.props)]);
       } else if (typeof seg === "object" && "marker" in seg) {
         const rt = checkI32(seg.marker.refType === undefined ? 0 : seg.marker.refType, "refType");
-        recs.push([OP_INSERT, F_MARKER, pos, rt, 0, this.props.add(seg.props)]);
+        const off = this._text("\ufffc")[0];  // one reserved unit names the marker in MTE_DOC_REFS documents
+        recs.push([OP_INSERT, F_MARKER, pos, rt, off, this.props.add(seg.props)]);
       } else {
         throw new MergeTreeError(E_INVALID_ARG, "Unrecognized IJSONSegment type: " + JSON.stringify(seg));
       }
@@ -678,7 +716,7 @@ function packDocInits(docs, interner) {
     buf.writeUInt32LE(off, o);
     buf.writeUInt32LE(d.text.length, o + 4);
     buf.writeUInt32LE((d.newLengthCalc ? DOC_NEW_LENGTH_CALC : 0) | (d.roundSync ? DOC_ROUND_SYNC : 0) |
-      (d.localClient ? DOC_LOCAL_CLIENT : 0) | (d.events ? DOC_EVENTS : 0), o + 8);
+      (d.localClient ? DOC_LOCAL_CLIENT : 0) | (d.events ? DOC_EVENTS : 0) | (d.refs ? DOC_REFS : 0), o + 8);
     buf.writeUInt32LE(props.add(d.props) >>> 0, o + 12);
     buf.writeInt32LE(d.minSeq || 0, o + 16);
     buf.writeInt32LE(d.currentSeq || 0, o + 20);
@@ -808,7 +846,7 @@ function regenOps(op, idx, recs) {
 
 module.exports = {
   OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_ACK, OP_REGEN, DELTA_REGEN, ANNOTATE_SLOTS, F_MARKER, F_MSG_END, F_REWRITE,
-  F_LOCAL, NO_PROPS, MAX_CLIENTS,
+  F_LOCAL, NO_PROPS, MAX_CLIENTS, OP_REF, REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE, REF_TRANSIENT,
   INSERT, REMOVE, ANNOTATE, GROUP,
   MergeTreeError, Interner, DocClients, PropTable, BatchBuilder, canonicalJson, packDocInits, packSegments, utf16,
   regenOps,

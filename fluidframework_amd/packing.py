@@ -32,7 +32,8 @@ import numpy as np
 
 from .abi import (F_LOCAL, F_MARKER, F_MSG_END, F_REWRITE, LOCAL_SEQ_BASE, MTE_E_CLIENT_RANGE,
                   MTE_E_INVALID_ARG, MTE_E_STATE, MTE_E_UNSUPPORTED, MTE_MAX_CLIENTS, NO_PROPS, OP_ACK, OP_ROLLBACK,
-                  OP_REGEN, OP_RBKEY, ANNOTATE_SLOTS,
+                  OP_REGEN, OP_RBKEY, OP_REF, ANNOTATE_SLOTS, REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE,
+                  REF_TRANSIENT,
                   OP_ANNOTATE, OP_DTYPE, OP_INSERT, OP_NOOP, OP_REMOVE, PROP_DTYPE, PROPSET_DTYPE,
                   MergeTreeError)
 
@@ -154,6 +155,10 @@ class DocClients:
         # engine cannot restate exactly (see BatchBuilder.add_rollback)
         self.ann_props = {}
         self.no_rollback = set()
+        # local reference slots (MTE_DOC_REFS documents): the next unused one and
+        # the removed ones, reused first
+        self.ref_next = 0
+        self.ref_free = []
 
     def short(self, long_id, seq=None) -> int:
         i = self.ids.get(long_id)
@@ -376,6 +381,29 @@ class BatchBuilder:
         clients.pending_types.append(clients.pending_types.pop(0))
         return idx
 
+    def add_ref(self, doc: int, clients: DocClients, pos: int, ref_type: int = REF_SLIDE_ON_REMOVE) -> int:
+        """Client.createLocalReferencePosition on the segment and offset that
+        getContainingSegment(pos) finds in the local view (client.ts:360-364,
+        1107-1110; mergeTree.ts:872-885, 2124-2143): an MTE_OP_REF record in an
+        MTE_DOC_REFS document.  Returns the reference's slot (mte_read_refs)."""
+        if not clients.local:
+            raise MergeTreeError(MTE_E_UNSUPPORTED, "local reference in an observer document")
+        ref_type = _check_i32(ref_type, "refType")
+        if ref_type & (REF_STAY_ON_REMOVE | REF_TRANSIENT) or ref_type < 0:
+            raise MergeTreeError(MTE_E_UNSUPPORTED, "StayOnRemove / Transient local references")
+        slot = clients.ref_free.pop() if clients.ref_free else clients.ref_next
+        if slot == clients.ref_next:
+            clients.ref_next += 1
+        self.ops[doc].append((0, 0, 0, OP_REF, 0, F_LOCAL, _check_i32(pos, "pos"), slot, ref_type, 0))
+        return slot
+
+    def remove_ref(self, doc: int, clients: DocClients, slot: int):
+        """removeLocalReferencePosition (mergeTree.ts:2113-2123)."""
+        if not 0 <= slot < clients.ref_next or slot in clients.ref_free:
+            raise MergeTreeError(MTE_E_INVALID_ARG, f"no local reference in slot {slot}")
+        clients.ref_free.append(slot)
+        self.ops[doc].append((0, 0, 0, OP_REF, 0, F_LOCAL, -1, slot, 0, 1))
+
     def _op_records(self, op, recs):
         if not isinstance(op, dict):
             raise MergeTreeError(MTE_E_INVALID_ARG, "op contents must be an object")
@@ -402,7 +430,9 @@ class BatchBuilder:
                 recs.append((OP_INSERT, 0, pos, n, off, self.props.add(seg.get("props"))))
             elif isinstance(seg, dict) and "marker" in seg:
                 ref_type = _check_i32(seg["marker"].get("refType", 0), "refType")
-                recs.append((OP_INSERT, F_MARKER, pos, ref_type, 0, self.props.add(seg.get("props"))))
+                # one reserved text unit names the marker in MTE_DOC_REFS documents
+                off, _ = self._text("\ufffc")
+                recs.append((OP_INSERT, F_MARKER, pos, ref_type, off, self.props.add(seg.get("props"))))
             else:
                 raise MergeTreeError(MTE_E_INVALID_ARG, f"Unrecognized IJSONSegment type: {seg!r}")
         elif t == REMOVE:

@@ -122,6 +122,33 @@ extern "C" {
  * before the first pending annotate, kept per segment).  A segment takes the
  * first candidate whose group it belongs to.                                 */
 #define MTE_OP_RBKEY 7
+/* Local references (LocalReferenceCollection, localReference.ts:139-567) in an
+ * MTE_DOC_REFS document: a local record (MTE_F_LOCAL, seq 0: it takes no
+ * localSeq and moves no window) with pos2 = the reference's slot (0 ..
+ * mte_set_ref_capacity - 1, assigned by the host) and b = 0 to create, 1 to
+ * remove it.
+ *   create: Client.createLocalReferencePosition(segment, offset, refType)
+ *     (client.ts:360-364, mergeTree.ts:2124-2143) on the segment and offset
+ *     that getContainingSegment(pos1) finds in the local view
+ *     (mergeTree.ts:872-885); a = the ReferenceType flags (ops.ts): Simple (0)
+ *     or SlideOnRemove (0x40) plus any of the label bits; StayOnRemove and
+ *     Transient are MTE_E_UNSUPPORTED; pos1 outside the local view
+ *     MTE_E_INVALID_ARG.
+ *   remove: removeLocalReferencePosition (mergeTree.ts:2113-2123).
+ * The engine slides references as the reference does
+ * (slideAckedRemovedSegmentReferences, mergeTree.ts:893-950): when a segment
+ * becomes removed and acked -- a remote remove newly removing it or
+ * overtaking the local client's pending removal (:1936-1938, 1986-1993), or
+ * the ack of the local client's removal (:1302-1304) -- its SlideOnRemove
+ * references move to the first following segment that is neither removed and
+ * acked nor a pending insert (offset 0), else to the last such preceding one
+ * (its last offset), else detach; its Simple references detach.  Positions
+ * come from mte_read_refs (referencePositionToLocalPosition,
+ * mergeTree.ts:1095-1112).                                                     */
+#define MTE_OP_REF 8
+#define MTE_REF_SLIDE_ON_REMOVE 0x40u /* ReferenceType.SlideOnRemove             */
+#define MTE_REF_STAY_ON_REMOVE 0x80u  /* ReferenceType.StayOnRemove (unsupported) */
+#define MTE_REF_TRANSIENT 0x100u      /* ReferenceType.Transient (unsupported)    */
 /* Segment groups of pending local annotates (mergeTree.ts:1874-1880): a local
  * annotate record with b = a slot 0..31 marks every segment it visits with
  * that slot (MTE_NO_PROPS: not tracked); an MTE_OP_ACK record's a is the mask
@@ -216,6 +243,12 @@ typedef struct mte_config {
  * Requires MTE_DOC_NEW_LENGTH_CALC and a context below 8192 segments; such
  * documents replay on the HBM-streamed pass.  Read with mte_read_deltas.      */
 #define MTE_DOC_EVENTS 0x8u
+/* The document holds local references (MTE_OP_REF records; mte_read_refs).
+ * Requires MTE_DOC_LOCAL_CLIENT.  Each of its markers takes the text offset of
+ * its insert record (mte_op.a: the host reserves one unit of the batch text per
+ * marker insert), which identifies the marker as a text unit's arena offset
+ * identifies that unit.                                                        */
+#define MTE_DOC_REFS 0x10u
 
 /* Initial document: one text segment inserted before collaboration starts, as
  * the reference replay harness does (client.replay.spec.ts:22-23): seq 0
@@ -357,6 +390,17 @@ int mte_read_deltas(mte_ctx* ctx, uint32_t doc, mte_delta* out, uint64_t cap, ui
 /* Event capacity of an MTE_DOC_EVENTS doc per batch: per_op x its records +
  * 256 (default per_op 8); applies from the next mte_submit.                 */
 int mte_set_event_capacity(mte_ctx* ctx, uint32_t per_op);
+
+/* Local reference slots per MTE_DOC_REFS document (default 1024).  Set before
+ * mte_load_docs; references live until removed or the next mte_load_docs /
+ * mte_reset.                                                                   */
+int mte_set_ref_capacity(mte_ctx* ctx, uint32_t per_doc);
+/* Positions of reference slots [0, n) of doc in its own view after the last
+ * mte_run: Client.localReferencePositionToPosition -> MergeTree.
+ * referencePositionToLocalPosition (client.ts:376-378, mergeTree.ts:1095-1112):
+ * the segment's position (Client.getPosition) plus the offset, 0 on a removed
+ * segment; -1 (DetachedReferencePosition) for a detached or unused slot.      */
+int mte_read_refs(mte_ctx* ctx, uint32_t doc, int32_t* pos, uint32_t n);
 
 /* Every segment a document holds — removed ones above minSeq included — with
  * its merge info, in document order: the input of a summary writer

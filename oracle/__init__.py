@@ -56,6 +56,8 @@ def load():
         f.restype = C.c_int
     lib.orc_read_deltas.argtypes = [vp, u32, vp, u64, vp]
     lib.orc_read_deltas.restype = C.c_int
+    lib.orc_read_refs.argtypes = [vp, u32, vp, u32]
+    lib.orc_read_refs.restype = C.c_int
     for pre in ("ort", "oti"):
         f = getattr(lib, f"{pre}_doc_shape")
         f.argtypes = [vp, u32, C.c_char_p, u32]
@@ -146,6 +148,12 @@ class OracleEngine(EngineBase):
 
     def set_event_capacity(self, per_op):
         """The restatement's event buffers grow as needed (mte_set_event_capacity's bound is the engine's)."""
+
+    def set_ref_capacity(self, per_doc):
+        """The restatement's reference slots grow as needed."""
+
+    def _read_refs(self, doc, p, n):
+        return self.lib.orc_read_refs(self.ctx, doc, p, n)
 
     def _digest(self, p, n):
         return self.f.digest(self.ctx, p, n)
@@ -246,6 +254,10 @@ class SpecOracle:
     def nsegs(self, doc):
         e, i = self.where[doc]
         return self._engines()[e].nsegs(int(i))
+
+    def read_refs(self, doc, n):
+        e, i = self.where[doc]
+        return self._engines()[e].read_refs(int(i), n)
 
     def stats(self):
         zero = {"ops_applied": 0, "segs_scanned": 0, "segs_written": 0, "prop_writes": 0, "units_inserted": 0,

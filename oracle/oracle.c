@@ -46,6 +46,12 @@ typedef struct {
    * segmentPropertiesManager.ts:20-60, see doc_apply_local); the last localSeq */
   uint32_t* pk;
   int32_t local_seq;
+  /* MTE_DOC_REFS: local reference slots -- the arena offset of the unit the
+   * reference sits on (a marker's is its reserved unit) and REF_LIVE |
+   * REF_DETACHED | refType; slots [0, ref_hi) were ever used */
+  uint32_t* ref_anchor;
+  uint32_t* ref_state;
+  uint32_t ref_cap, ref_hi;
   /* MTE_DOC_EVENTS: the last batch's delta events, and the record being applied */
   mte_delta* dl;
   uint64_t dl_n, dl_cap;
@@ -320,6 +326,92 @@ static int64_t doc_lengths_local(odoc* d) {
 static int doc_rollback(odoc* d, const mte_op* op, const apply_env* env);
 static int doc_regen(odoc* d, const mte_op* op);
 
+/* ---- local references (MTE_DOC_REFS, include/mte.h) --------------------------
+ * A reference is kept as the text unit it sits on (its arena offset: splits
+ * never copy text, so the unit names the same place in whatever segment holds
+ * it) -- LocalReferenceCollection keeps it as (segment, offset) and moves it on
+ * split / append (localReference.ts:330-416), which names the same unit. */
+#define REF_LIVE 0x80000000u
+#define REF_DETACHED 0x40000000u
+#define REF_LIMIT (1u << 24)
+
+/* a segment references may slide to (_getSlideToSegment, mergeTree.ts:893-913):
+ * not a pending insert and not removed-and-acked (a pending removal is fine) */
+static inline int slide_target_ok(const oseg* g) { return g->seq < LOCAL_BASE && g->rseq >= LOCAL_BASE; }
+
+/* MTE_OP_REF: createLocalReferencePosition on getContainingSegment(pos1) in the
+ * local view (client.ts:360-364, 1107-1110; mergeTree.ts:872-885, 2124-2143) or
+ * removeLocalReferencePosition (mergeTree.ts:2113-2123). */
+static int doc_ref(odoc* d, const mte_op* op) {
+  if (!(d->flags & MTE_DOC_REFS)) return MTE_E_UNSUPPORTED;
+  if (op->pos2 < 0 || (uint32_t)op->pos2 >= REF_LIMIT || op->b > 1) return MTE_E_INVALID_ARG;
+  const uint32_t slot = (uint32_t)op->pos2;
+  if (slot >= d->ref_cap) {
+    uint32_t nc = d->ref_cap ? d->ref_cap : 64;
+    while (nc <= slot) nc *= 2;
+    uint32_t* a = (uint32_t*)realloc(d->ref_anchor, (size_t)nc * sizeof(uint32_t));
+    if (!a) return MTE_E_OOM;
+    d->ref_anchor = a;
+    uint32_t* st = (uint32_t*)realloc(d->ref_state, (size_t)nc * sizeof(uint32_t));
+    if (!st) return MTE_E_OOM;
+    d->ref_state = st;
+    memset(d->ref_state + d->ref_cap, 0, (size_t)(nc - d->ref_cap) * sizeof(uint32_t));
+    d->ref_cap = nc;
+  }
+  d->ops++;
+  if (op->b == 1) {
+    d->ref_state[slot] = 0;
+    return MTE_OK;
+  }
+  if (op->a & (MTE_REF_STAY_ON_REMOVE | MTE_REF_TRANSIENT)) return MTE_E_UNSUPPORTED;
+  d->scanned += d->n;
+  int64_t p = 0;
+  for (uint32_t i = 0; i < d->n; i++) {
+    const int32_t l = own_len(&d->s[i]);
+    if (l > 0 && op->pos1 >= p && op->pos1 < p + l) {
+      d->ref_anchor[slot] = d->s[i].toff + (uint32_t)(op->pos1 - p);
+      d->ref_state[slot] = REF_LIVE | (op->a & 0xffffu);
+      if (slot + 1 > d->ref_hi) d->ref_hi = slot + 1;
+      return MTE_OK;
+    }
+    p += l;
+  }
+  return MTE_E_INVALID_ARG; /* no segment holds pos1 in the local view */
+}
+
+/* slideAckedRemovedSegmentReferences (mergeTree.ts:921-950) for every segment
+ * the op of seq s made removed-and-acked (its removedSeq is now s: a remote
+ * remove's new removals and overtaken pending ones, :1936-1938 / 1986-1993, or
+ * the ack of a local removal, :1302-1304): SlideOnRemove references go to
+ * offset 0 of the first following segment a reference may slide to
+ * (forwardExcursion, addBeforeTombstones), else to the last offset of the last
+ * preceding one (backwardExcursion, addAfterTombstones), else detach; Simple
+ * references detach (localReference.ts:422-485). */
+static void doc_slide_refs(odoc* d, int32_t s) {
+  if (!(d->flags & MTE_DOC_REFS) || !d->ref_hi) return;
+  for (uint32_t i = 0; i < d->n; i++) {
+    const oseg* g = &d->s[i];
+    if (g->rseq != s) continue;
+    int64_t t = -1;
+    int after = 0;
+    for (uint32_t j = i + 1; j < d->n && t < 0; j++)
+      if (slide_target_ok(&d->s[j])) t = j;
+    for (int64_t j = (int64_t)i - 1; j >= 0 && t < 0; j--)
+      if (slide_target_ok(&d->s[j])) t = j, after = 1;
+    for (uint32_t r = 0; r < d->ref_hi; r++) {
+      const uint32_t st = d->ref_state[r];
+      if (!(st & REF_LIVE) || (st & REF_DETACHED)) continue;
+      if (d->ref_anchor[r] - g->toff >= (uint32_t)g->len) continue;
+      if ((st & MTE_REF_SLIDE_ON_REMOVE) && t >= 0) {
+        const oseg* tg = &d->s[t];
+        d->ref_anchor[r] = after ? tg->toff + (uint32_t)tg->len - 1u : tg->toff;
+      } else {
+        d->ref_state[r] = st | REF_DETACHED;
+      }
+    }
+  }
+}
+
 /* A local op (MTE_F_LOCAL, include/mte.h): insertSegmentLocal /
  * removeRangeLocal / annotateRangeLocal (client.ts:131-229) with seq =
  * UnassignedSequenceNumber, held as LOCAL_BASE + localSeq.
@@ -337,6 +429,7 @@ static int doc_apply_local(odoc* d, const mte_op* op, const apply_env* env) {
   int rc;
   if (op->type == MTE_OP_ROLLBACK) return doc_rollback(d, op, env);
   if (op->type == MTE_OP_REGEN) return doc_regen(d, op);
+  if (op->type == MTE_OP_REF) return doc_ref(d, op);
   if (!(ls > d->local_seq && ls < LOCAL_BASE)) return MTE_E_INVALID_ARG;
   if (op->client != 0) return MTE_E_INVALID_ARG;
   if (op->type == MTE_OP_ANNOTATE && (op->flags & MTE_F_REWRITE)) return MTE_E_UNSUPPORTED;
@@ -371,6 +464,7 @@ static int doc_apply_local(odoc* d, const mte_op* op, const apply_env* env) {
     ns->rseq = NONE_SEQ;
     if (is_marker) {
       ns->kind = 1u + (uint32_t)op->pos2;
+      if (d->flags & MTE_DOC_REFS) ns->toff = (uint32_t)(env->text_base + op->a); /* its reserved unit */
     } else {
       ns->toff = (uint32_t)(env->text_base + op->a);
       d->units += (uint64_t)len;
@@ -624,7 +718,7 @@ static int doc_apply(odoc* d, const mte_op* op, const apply_env* env) {
       ns->rmask = 0;
       if (is_marker) {
         ns->kind = 1u + (uint32_t)op->pos2;
-        ns->toff = 0;
+        ns->toff = (d->flags & MTE_DOC_REFS) ? (uint32_t)(env->text_base + op->a) : 0u; /* its reserved unit */
       } else {
         ns->kind = 0;
         ns->toff = (uint32_t)(env->text_base + op->a);
@@ -681,9 +775,11 @@ static int doc_apply(odoc* d, const mte_op* op, const apply_env* env) {
         d->written += 1;
       }
     }
+    if (op->type == MTE_OP_REMOVE) doc_slide_refs(d, s);
     if ((rc = check_op_window(d, op))) return rc;
   } else if (op->type == MTE_OP_ACK) {
     if ((rc = doc_ack(d, op))) return rc;
+    doc_slide_refs(d, s);
     if ((rc = check_op_window(d, op))) return rc;
   } else if (op->type != MTE_OP_NOOP) {
     return MTE_E_INVALID_ARG;
@@ -721,6 +817,8 @@ static void free_docs(orc_ctx* c) {
     free(c->docs[i].P);
     free(c->docs[i].pk);
     free(c->docs[i].dl);
+    free(c->docs[i].ref_anchor);
+    free(c->docs[i].ref_state);
   }
   free(c->docs);
   c->docs = NULL;
@@ -775,6 +873,7 @@ int orc_load_docs(orc_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     d->flags = in->flags;
     if ((in->flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)) && !(in->flags & MTE_DOC_NEW_LENGTH_CALC))
       return MTE_E_UNSUPPORTED;
+    if ((in->flags & MTE_DOC_REFS) && !(in->flags & MTE_DOC_LOCAL_CLIENT)) return MTE_E_UNSUPPORTED;
     d->min_seq = in->min_seq;
     d->cur_seq = in->cur_seq;
     d->rs_ref = INT32_MIN;
@@ -828,7 +927,9 @@ int orc_load_segments(orc_ctx* c, const uint64_t* seg_offsets, const mte_seg* se
       g->rseq = sg->removed_seq == MTE_NOT_REMOVED ? NONE_SEQ : sg->removed_seq;
       g->rmask = sg->removed_seq == MTE_NOT_REMOVED ? 0u : sg->removers;
       g->kind = sg->kind;
-      g->toff = marker ? 0u : sg->text_off;
+      /* a marker of an MTE_DOC_REFS document is named by its index in the load
+       * (above every arena offset), as an inserted one by its reserved unit */
+      g->toff = marker ? ((d->flags & MTE_DOC_REFS) ? 0x80000000u + (uint32_t)(k - b) : 0u) : sg->text_off;
       if (sg->propset != MTE_NO_PROPS) {
         if (sg->propset >= c->n_load_ps) return MTE_E_INVALID_ARG;
         orc_apply_props(g->props, c->n_keys, &c->load_ps[sg->propset], c->load_pe, 0);
@@ -909,8 +1010,13 @@ int orc_apply_batch(orc_ctx* c, const mte_batch* b, int n_threads) {
       if (op->pos2 < 0 || k + 1 + (uint64_t)op->pos2 > b->op_offsets[dcur + 1]) return MTE_E_INVALID_ARG;
       rbkey_end = k + 1 + (uint64_t)op->pos2;
     }
-    if (op->type > MTE_OP_RBKEY) return MTE_E_INVALID_ARG;
+    if (op->type > MTE_OP_REF) return MTE_E_INVALID_ARG;
     if (op->type >= MTE_OP_ROLLBACK && !(op->flags & MTE_F_LOCAL)) return MTE_E_INVALID_ARG;
+    if (op->type == MTE_OP_REF) {
+      if (!(c->docs[dcur].flags & MTE_DOC_REFS) || op->seq != 0 || op->pos2 < 0 || op->b > 1)
+        return MTE_E_INVALID_ARG;
+      continue;
+    }
     if ((op->flags & MTE_F_LOCAL) && op->type == MTE_OP_ANNOTATE && op->b != MTE_NO_PROPS &&
         op->b >= MTE_ANNOTATE_SLOTS)
       return MTE_E_INVALID_ARG;
@@ -1077,5 +1183,30 @@ int orc_read_deltas(orc_ctx* c, uint32_t doc, mte_delta* out, uint64_t cap, uint
   const odoc* d = &c->docs[doc];
   *n = d->dl_n;
   if (out) memcpy(out, d->dl, (size_t)(cap < d->dl_n ? cap : d->dl_n) * sizeof(mte_delta));
+  return MTE_OK;
+}
+
+/* referencePositionToLocalPosition (mergeTree.ts:1095-1112) of slots [0, n):
+ * the own-view position of the segment holding the reference's unit plus its
+ * offset there (0 on a removed segment); -1 for a detached or unused slot or a
+ * unit no segment holds any more. */
+int orc_read_refs(orc_ctx* c, uint32_t doc, int32_t* pos, uint32_t n) {
+  if (!c || (n && !pos) || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  const odoc* d = &c->docs[doc];
+  for (uint32_t r = 0; r < n; r++) {
+    pos[r] = -1;
+    if (r >= d->ref_hi) continue;
+    const uint32_t st = d->ref_state[r], u = d->ref_anchor[r];
+    if (!(st & REF_LIVE) || (st & REF_DETACHED)) continue;
+    int64_t p = 0;
+    for (uint32_t i = 0; i < d->n; i++) {
+      const oseg* g = &d->s[i];
+      if (u - g->toff < (uint32_t)g->len) {
+        pos[r] = (int32_t)(p + (g->rseq != NONE_SEQ ? 0 : (int64_t)(u - g->toff)));
+        break;
+      }
+      p += own_len(g);
+    }
+  }
   return MTE_OK;
 }

@@ -29,6 +29,13 @@
 //         re-sends every held op through Client.regeneratePendingOp
 //         (client.ts:972-1002), as test/client.reconnectFarm.spec.ts:25-59
 //         does: ["G", logIndex], the log entry holding the regenerated op)
+//          refs: the chance per step that a client (the observer included)
+//         creates a local reference -- Client.createLocalReferencePosition on
+//         getContainingSegment(pos) in its own view, SlideOnRemove or Simple
+//         (client.ts:360-364, 1107-1110) -- or removes one of its own
+//         (removeLocalReferencePosition): ["F", pos, refType] / ["X", index];
+//         each checkpoint state then holds "refs", the client's references'
+//         localReferencePositionToPosition in creation order (null: removed)
 // stdout: {"sets": [{..params, "names": [...], "log": [[clientId, seq, ref, msn, "op", contents]],
 //                    "events": [[["L"|"A", logIndex] | ["R", op], ...] per client],
 //                    "checkpoints": [{"done": [events applied per client],
@@ -43,6 +50,7 @@ const { Client } = require(path.join(refdir, "client.js"));
 const { TextSegment } = require(path.join(refdir, "textSegment.js"));
 const { Marker } = require(path.join(refdir, "mergeTreeNodes.js"));
 const { MergeTreeTextHelper } = require(path.join(refdir, "MergeTreeTextHelper.js"));
+const { ReferenceType } = require(path.join(refdir, "ops.js"));
 
 function specToSegment(spec) {
   const t = TextSegment.fromJSONObject(spec);
@@ -111,6 +119,7 @@ function runSet(p) {
   const offline = names.map(() => false);
   const held = names.map(() => []);  // [op, segment group] per held op
   const events = names.map(() => []);
+  const refs = names.map(() => []);  // per client, in creation order (null: removed)
   const log = [];
   let seq = 0;
   const checkpoints = [];
@@ -140,10 +149,38 @@ function runSet(p) {
     offline[i] = false;
   };
   const checkpoint = () => {
-    checkpoints.push({ done: events.map((e) => e.length), states: clients.map(readOut) });
+    const states = clients.map(readOut);
+    if (p.refs) {
+      states.forEach((st, i) => {
+        st.refs = refs[i].map((r) => (r === null ? null : clients[i].localReferencePositionToPosition(r)));
+      });
+    }
+    checkpoints.push({ done: events.map((e) => e.length), states });
   };
 
   for (let step = 0; step < p.steps; step++) {
+    if (p.refs && R.next() < p.refs) {
+      // a local reference made or dropped by any client (its own, not sequenced)
+      const i = R.int(0, p.clients - 1);
+      const c = clients[i];
+      const live = [];
+      refs[i].forEach((r, k) => { if (r !== null) live.push(k); });
+      const len = c.getLength();
+      if (len > 0 && (live.length === 0 || R.next() < 0.75)) {
+        const pos = R.int(0, len - 1);
+        const type = R.next() < 0.8 ? ReferenceType.SlideOnRemove : ReferenceType.Simple;
+        const { segment, offset } = c.getContainingSegment(pos);
+        refs[i].push(c.createLocalReferencePosition(segment, offset, type, undefined));
+        events[i].push(["F", pos, type]);
+      } else if (live.length > 0) {
+        const k = live[R.int(0, live.length - 1)];
+        c.removeLocalReferencePosition(refs[i][k]);
+        refs[i][k] = null;
+        events[i].push(["X", k]);
+      }
+      if ((step + 1) % every === 0 && step + 1 < p.steps) checkpoint();
+      continue;
+    }
     if (p.reconnect && R.next() < p.reconnect) {
       const i = R.int(1, p.clients - 1);
       if (offline[i]) reconnect(i);

@@ -238,23 +238,29 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None):
     rolled back at once (Client.rollback), "H" a local op held while offline,
     "G" the oldest pending op regenerated on reconnect (Client.regeneratePendingOp;
     the engine's regenerated op must equal the reference's, which the log holds
-    and every client then applies) — in one batch per checkpoint; text and
-    per-position properties must equal the reference client's at every
-    checkpoint.  regen_checks (a list) collects one entry per "G" event compared.
+    and every client then applies), "F" / "X" a local reference created at a
+    position of the client's own view / removed (createLocalReferencePosition /
+    removeLocalReferencePosition) — in one batch per checkpoint; text,
+    per-position properties and, for sets with references, every reference's
+    position (localReferencePositionToPosition) must equal the reference
+    client's at every checkpoint.  regen_checks (a list) collects one entry per "G" event compared.
     Returns (checkpoints_passed, failures)."""
-    from fluidframework_amd.abi import DOC_EVENTS, DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC
+    from fluidframework_amd.abi import DOC_EVENTS, DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC, DOC_REFS
     from fluidframework_amd.packing import regen_ops
 
     layout = [(si, ci) for si, s in enumerate(sets) for ci in range(len(s["names"]))]
     has_regen = any(e[0] == "G" for s in sets for ev in s["events"] for e in ev)
+    has_refs = any(s.get("refs") for s in sets)
     inits, text = doc_inits([sets[si]["initialText"] for si, _ in layout],
-                            flags=DOC_NEW_LENGTH_CALC | DOC_LOCAL_CLIENT | (DOC_EVENTS if has_regen else 0))
+                            flags=DOC_NEW_LENGTH_CALC | DOC_LOCAL_CLIENT | (DOC_EVENTS if has_regen else 0) |
+                            (DOC_REFS if has_refs else 0))
     interner = Interner(n_keys)
     eng = engine_factory(n_keys)
     if has_regen:
         eng.set_event_capacity(64)
     eng.load_docs(inits, text)
     held = [[] for _ in layout]
+    ref_slots = [[] for _ in layout]  # the farm's reference index -> engine slot
     clients = [DocClients(sets[si]["names"][ci], local=True) for si, ci in layout]
     n_cp = max(len(s["checkpoints"]) for s in sets)
     prev = [0] * len(layout)
@@ -267,7 +273,15 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None):
             if j >= len(s["checkpoints"]):
                 continue
             done = s["checkpoints"][j]["done"][ci]
-            for kind, li in s["events"][ci][prev[d]:done]:
+            for ev in s["events"][ci][prev[d]:done]:
+                kind, li = ev[0], ev[1]
+                if kind == "F":  # a local reference at position li (ev[2]: its ReferenceType)
+                    ref_slots[d].append(bb.add_ref(d, clients[d], li, ev[2]))
+                    continue
+                if kind == "X":
+                    bb.remove_ref(d, clients[d], ref_slots[d][li])
+                    ref_slots[d][li] = None
+                    continue
                 if kind == "R":  # the op (li) made locally, then rolled back
                     bb.add_local(d, clients[d], li)
                     bb.add_rollback(d, clients[d])
@@ -308,7 +322,12 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None):
                 continue
             v = eng.read_doc(d)
             got = {"text": v["text"], "length": v["length"], "props": prop_runs(v, interner)}
-            if got["text"] != want["text"] or got["length"] != want["length"] or got["props"] != want["props"]:
+            if "refs" in want:
+                slots = ref_slots[d]
+                pos = eng.read_refs(d, 1 + max([x for x in slots if x is not None], default=-1))
+                got["refs"] = [None if x is None else int(pos[x]) for x in slots]
+            if got["text"] != want["text"] or got["length"] != want["length"] or got["props"] != want["props"] or \
+                    got.get("refs") != want.get("refs"):
                 failures.append((si, ci, j, "state", got, want))
             else:
                 passed += 1

@@ -11,7 +11,13 @@ properties at checkpoints.  The file holds only that data — messages, event
 orders and expected read-outs — no reference source.  Run in the build
 container (the reference does not exist on the GPU box).
 
-Usage: python3 tests/golden/make_farm_golden.py
+With --refs it writes tests/golden/localref_vectors.json.gz instead: farms in
+which every client (the observer included) also creates local references at
+positions of its own view and removes some (Client.createLocalReferencePosition
+/ removeLocalReferencePosition, SlideOnRemove or Simple), each checkpoint
+holding every reference's localReferencePositionToPosition.
+
+Usage: python3 tests/golden/make_farm_golden.py [--refs]
 """
 import gzip
 import json
@@ -26,6 +32,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
 import ref_util  # noqa: E402
 
 OUT = os.path.join(HERE, "farm_vectors.json.gz")
+OUT_REFS = os.path.join(HERE, "localref_vectors.json.gz")
 FARM_JS = os.path.join(ROOT, "oracle", "ref_farm.js")
 
 # (seed, clients incl. the observer, steps, initial text, checkpoints, text bound)
@@ -47,10 +54,40 @@ ROLLBACK_ANNOTATE_SETS = [(4000 + i, 2 + i % 6, 400 + 100 * (i % 3), ["", "hello
                            [64, 200][i % 2], 0.25, [1, 2]) for i in range(24)]
 
 
+# local references: (seed, clients, steps, initial text, checkpoints, text bound,
+# rollback chance, rollback types or None, reference-op chance)
+REF_SETS = [(7000 + i, 2 + i % 6, 300 + 100 * (i % 5), ["", "hello world", "abc\ndef"][i % 3], 5, [64, 200, 400][i % 3],
+             [0.0, 0.2][i % 2], [1, 2] if i % 4 == 3 else None, [0.1, 0.25][(i % 2) if i < 20 else 1 - i % 2])
+            for i in range(40)]
+
+
+def main_refs(out):
+    res = {"sets": [], "generator": "oracle/ref_farm.js with refs (reference Client, mulberry32 seeds)"}
+    failed = []
+    for sd, c, n, t, k, m, rb, types, refs in REF_SETS:
+        one = {"seed": sd, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
+               "rollback": rb, "refs": refs}
+        if types:
+            one["rollbackTypes"] = types
+        q = subprocess.run(["node", FARM_JS, out], input=json.dumps({"sets": [one]}), capture_output=True, text=True,
+                           timeout=600)
+        if q.returncode == 0:
+            res["sets"] += json.loads(q.stdout)["sets"]
+        else:
+            failed.append(sd)
+    res["seeds_the_reference_failed"] = failed
+    with gzip.open(OUT_REFS, "wt", encoding="utf-8") as fh:
+        json.dump(res, fh, separators=(",", ":"))
+    n_refs = sum(1 for s in res["sets"] for ev in s["events"] for e in ev if e[0] == "F")
+    print(f"wrote {OUT_REFS}: {len(res['sets'])} farms, {n_refs} local references")
+
+
 def main():
     if not ref_util.ref_available():
         sys.exit("the reference sources are not in this container")
     out = ref_util.build_ref()
+    if "--refs" in sys.argv[1:]:
+        return main_refs(out)
     inp = {"sets": [{"seed": s, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
                      "rollback": rb} for s, c, n, t, k, m, rb in SETS]}
     p = subprocess.run(["node", "--max-old-space-size=8192", FARM_JS, out], input=json.dumps(inp),

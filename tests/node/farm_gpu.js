@@ -8,7 +8,10 @@
 // sequenced messages through applyMsg (its own ones are acks) — and at every
 // checkpoint its text, length and per-position properties must be the
 // reference client's.  argv "sync": every local op reads the client's length
-// first, as the farm's op generator does (a flush + replay per op).
+// first, as the farm's op generator does (a flush + replay per op).  argv[4]:
+// the vectors file (default farm_vectors.json.gz; localref_vectors.json.gz adds
+// local references "F" / "X" through createLocalReferencePosition /
+// removeLocalReferencePosition, their positions checked at every checkpoint).
 // Prints one JSON line.
 const fs = require("fs");
 const path = require("path");
@@ -17,8 +20,9 @@ const { MergeTreeEngine } = require("../../fluidframework_amd/node");
 const { asMsg } = require("./fixtures");
 
 const sets = JSON.parse(zlib.gunzipSync(fs.readFileSync(path.join(__dirname, "..", "golden",
-  "farm_vectors.json.gz"))).toString("utf8")).sets;
-const nSets = process.argv[3] ? Number(process.argv[3]) : sets.length;
+  process.argv[4] || "farm_vectors.json.gz"))).toString("utf8")).sets;
+const nSets = process.argv[3] && process.argv[3] !== "all" ? Number(process.argv[3]) : sets.length;
+const withRefs = sets.some((s) => s.refs);
 const sync = process.argv[2] === "sync";
 
 function sortKeys(v) {
@@ -50,8 +54,8 @@ const eng = new MergeTreeEngine({ nKeys: 8 });
 const layout = [];
 for (let si = 0; si < nSets; si++) {
   sets[si].names.forEach((name, ci) => {
-    layout.push({ si, ci, client: eng.createClient(sets[si].initialText,
-      { newLengthCalc: true, localClient: true, longClientId: name }) });
+    layout.push({ si, ci, refs: [], client: eng.createClient(sets[si].initialText,
+      { newLengthCalc: true, localClient: true, longClientId: name, refs: withRefs }) });
   });
 }
 let passed = 0, opsChecked = 0;
@@ -63,11 +67,22 @@ for (let j = 0; j < nCp; j++) {
     const s = sets[L.si];
     if (j >= s.checkpoints.length) return;
     const done = s.checkpoints[j].done[L.ci];
-    for (const [kind, li] of s.events[L.ci].slice(prev[d], done)) {
+    for (const ev of s.events[L.ci].slice(prev[d], done)) {
+      const kind = ev[0], li = ev[1];
+      if (kind === "F") {  // a local reference at position li of the client's view
+        L.refs.push(L.client.createLocalReferencePosition(li, 0, ev[2]));
+        continue;
+      }
+      if (kind === "X") {
+        L.client.removeLocalReferencePosition(L.refs[li]);
+        L.refs[li] = null;
+        continue;
+      }
       if (kind === "R") {  // the op made locally, then rolled back (Client.rollback)
         if (sync) L.client.getLength();
         const o = li;
-        const op = o.type === 0 ? L.client.insertSegmentLocal(o.pos1, o.seg) : L.client.removeRangeLocal(o.pos1, o.pos2);
+        const op = o.type === 0 ? L.client.insertSegmentLocal(o.pos1, o.seg)
+          : (o.type === 1 ? L.client.removeRangeLocal(o.pos1, o.pos2) : L.client.annotateRangeLocal(o.pos1, o.pos2, o.props));
         L.client.rollback(op);
         opsChecked++;
         continue;
@@ -93,8 +108,10 @@ for (let j = 0; j < nCp; j++) {
     if (j >= s.checkpoints.length) return;
     const want = s.checkpoints[j].states[L.ci];
     const got = { text: L.client.getText(), length: L.client.getLength(), props: propRuns(L.client) };
+    if (want.refs) got.refs = L.refs.map((r) => (r === null ? null : L.client.localReferencePositionToPosition(r)));
     if (got.text === want.text && got.length === want.length &&
-        JSON.stringify(got.props) === JSON.stringify(want.props)) passed++;
+        JSON.stringify(got.props) === JSON.stringify(want.props) &&
+        JSON.stringify(got.refs) === JSON.stringify(want.refs)) passed++;
     else failures.push([L.si, L.ci, j, "state"]);
   });
 }

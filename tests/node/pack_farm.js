@@ -10,14 +10,16 @@ const zlib = require("zlib");
 const packing = require("../../fluidframework_amd/node/packing");
 const { asMsg } = require("./fixtures");
 
-// argv: the vectors file (farm_vectors.json.gz, or reconnect_vectors.json.gz:
-// ops held offline "H" and regeneratePendingOp "G" as MTE_OP_REGEN records)
+// argv: the vectors file (farm_vectors.json.gz, reconnect_vectors.json.gz: ops
+// held offline "H" and regeneratePendingOp "G" as MTE_OP_REGEN records, or
+// localref_vectors.json.gz: local references "F" / "X" as MTE_OP_REF records)
 const sets = JSON.parse(zlib.gunzipSync(fs.readFileSync(path.join(__dirname, "..", "golden",
   process.argv[2] || "farm_vectors.json.gz"))).toString("utf8")).sets;
 const interner = new packing.Interner(8);
 const layout = [];
 sets.forEach((s, si) => s.names.forEach((name, ci) => layout.push([si, ci, new packing.DocClients(name, 0, true)])));
 const prev = layout.map(() => 0);
+const refSlots = layout.map(() => []);
 const nCp = Math.max.apply(null, sets.map((s) => s.checkpoints.length));
 const b64 = (a) => Buffer.from(a.buffer, a.byteOffset, a.byteLength).toString("base64");
 for (let j = 0; j < nCp; j++) {
@@ -26,7 +28,16 @@ for (let j = 0; j < nCp; j++) {
     const s = sets[si];
     if (j >= s.checkpoints.length) return;
     const done = s.checkpoints[j].done[ci];
-    for (const [kind, li] of s.events[ci].slice(prev[d], done)) {
+    for (const ev of s.events[ci].slice(prev[d], done)) {
+      const kind = ev[0], li = ev[1];
+      if (kind === "F") {
+        refSlots[d].push(bb.addRef(d, cl, li, ev[2]));
+        continue;
+      }
+      if (kind === "X") {
+        bb.removeRef(d, cl, refSlots[d][li]);
+        continue;
+      }
       if (kind === "R") {  // made locally, then rolled back
         bb.addLocal(d, cl, li);
         bb.addRollback(d, cl);

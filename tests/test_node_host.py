@@ -25,7 +25,8 @@ pytestmark = pytest.mark.skipif(NODE is None, reason="node not installed")
 
 EXPORTS = ["abiVersion", "strerror", "create", "destroy", "lastError", "loadDocs", "loadSegments", "readSegments", "submit", "run",
            "sync", "reset", "digest", "docStatus", "readDoc", "stats", "commUniqueId", "commInit", "commShare",
-           "commBarrier", "commAllreduce", "commGatherDigests", "commDestroy", "readDeltas", "setEventCapacity"]
+           "commBarrier", "commAllreduce", "commGatherDigests", "commDestroy", "readDeltas", "setEventCapacity",
+           "setRefCapacity", "readRefs"]
 
 
 def node(*args, timeout=300):
@@ -76,7 +77,7 @@ def test_js_packing_matches_python_packing_on_fixtures(fresh):
             assert base64.b64decode(j[key]) == np.ascontiguousarray(arr).tobytes(), (r, key)
 
 
-@pytest.mark.parametrize("vectors", ["farm_vectors.json.gz", "reconnect_vectors.json.gz"])
+@pytest.mark.parametrize("vectors", ["farm_vectors.json.gz", "reconnect_vectors.json.gz", "localref_vectors.json.gz"])
 def test_js_packing_matches_python_packing_on_local_farms(vectors):
     """Local ops and acks (and, on the reconnect farms, ops held offline and
     regeneratePendingOp's MTE_OP_REGEN records): the JS and Python packers emit
@@ -88,6 +89,7 @@ def test_js_packing_matches_python_packing_on_local_farms(vectors):
     interner = Interner(8)
     layout = [(si, ci, DocClients(name, local=True)) for si, s in enumerate(sets) for ci, name in enumerate(s["names"])]
     prev = [0] * len(layout)
+    ref_slots = [[] for _ in layout]
     assert len(lines) == max(len(s["checkpoints"]) for s in sets)
     for j, line in enumerate(lines):
         bb = BatchBuilder(len(layout), interner)
@@ -96,7 +98,14 @@ def test_js_packing_matches_python_packing_on_local_farms(vectors):
             if j >= len(s["checkpoints"]):
                 continue
             done = s["checkpoints"][j]["done"][ci]
-            for kind, li in s["events"][ci][prev[d]:done]:
+            for ev in s["events"][ci][prev[d]:done]:
+                kind, li = ev[0], ev[1]
+                if kind == "F":
+                    ref_slots[d].append(bb.add_ref(d, cl, li, ev[2]))
+                    continue
+                if kind == "X":
+                    bb.remove_ref(d, cl, ref_slots[d][li])
+                    continue
                 if kind == "R":
                     bb.add_local(d, cl, li)
                     bb.add_rollback(d, cl)
@@ -312,6 +321,21 @@ def test_node_farm_every_client_local_on_gpu(mode):
         with gzip.open(os.path.join(ROOT, "tests", "golden", "farm_vectors.json.gz"), "rt") as fh:
             sets = json.load(fh)["sets"]
         assert j["passed"] == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
+
+
+@pytest.mark.gpu
+def test_node_local_references_on_gpu():
+    """BatchClient {localClient, refs}: every client of the 40 local-reference
+    farms the reference ran creates / removes its references through
+    createLocalReferencePosition / removeLocalReferencePosition, and at every
+    checkpoint localReferencePositionToPosition of each equals the reference's
+    (tests/node/farm_gpu.js over localref_vectors.json.gz)."""
+    import gzip
+    j = json.loads(node("tests/node/farm_gpu.js", "batched", "all", "localref_vectors.json.gz", timeout=600))
+    assert j["nFailures"] == 0, j["failures"]
+    with gzip.open(os.path.join(ROOT, "tests", "golden", "localref_vectors.json.gz"), "rt") as fh:
+        sets = json.load(fh)["sets"]
+    assert j["passed"] == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
 
 
 @pytest.mark.gpu
