@@ -221,6 +221,8 @@ def main():
                          "reconnect, delta events)")
     ap.add_argument("--local-docs", type=int, default=10000, help="documents in the local-client side measurement")
     ap.add_argument("--node-docs", type=int, default=100, help="documents in the Node host sample")
+    ap.add_argument("--node-sharded-docs", type=int, default=1000,
+                    help="documents in the Node host sample with parallel packing (ShardedHost)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stats", action="store_true",
@@ -349,6 +351,7 @@ def main():
     node_e2e = None
     if world == 1 and not args.no_node_leg and stream.get("segs") is None:
         node_e2e = node_end_to_end(stream, digest, args.node_docs)
+        node_e2e["sharded"] = node_sharded(stream, args.node_sharded_docs, host_threads())
 
     cpu = None
     parity = None
@@ -560,6 +563,76 @@ def node_end_to_end(stream, gpu_digest, n_docs):
             "includes": "BatchClient.applyMsg (JS packing) + flush (N-API mte_submit upload + mte_run + mte_sync); "
                         "message objects built before the clock; 'pipelined': the messages in 4 slices, each "
                         "flushed as packed (packing + upload of slice i+1 overlap the replay of slice i)",
+            "wall_s": round(time.perf_counter() - t0, 1)}
+
+
+def write_stream_dir(stream, d, n_docs):
+    """Docs [0, n_docs) of a generated stream as the files stream_source.js reads
+    (fluidframework_amd/node/stream_source.js)."""
+    from fluidframework_amd import gen
+    from fluidframework_amd.packing import units_to_str
+    os.makedirs(d, exist_ok=True)
+    b = stream["batch"]
+    o = np.asarray(b["op_offsets"], np.uint64)[: n_docs + 1]
+    o.tofile(os.path.join(d, "offsets.u64"))
+    np.asarray(b["ops"])[: int(o[-1])].tofile(os.path.join(d, "ops.bin"))
+    np.asarray(b["text"], np.uint16).tofile(os.path.join(d, "text.u16"))
+    np.asarray(b["propsets"]).tofile(os.path.join(d, "propsets.u32"))
+    np.asarray(b["props"]).tofile(os.path.join(d, "props.u32"))
+    vids = sorted(set(int(x) for x in np.asarray(b["props"])["value"]) - {0})
+    with open(os.path.join(d, "tables.json"), "w") as fh:
+        json.dump({"keys": gen.KEY_NAMES, "values": {str(v): gen.value_json(v) for v in vids}}, fh)
+    init = stream["init_text"]
+    inits = []
+    for k in range(n_docs):
+        it = stream["inits"][k]
+        inits.append({"text": units_to_str(init[int(it["text_off"]):int(it["text_off"]) + int(it["text_len"])]),
+                      "newCalc": bool(int(it["flags"]) & 1), "roundSync": bool(int(it["flags"]) & 2),
+                      "nMsgs": int(o[k + 1] - o[k])})
+    with open(os.path.join(d, "inits.json"), "w") as fh:
+        json.dump(inits, fh)
+
+
+def node_sharded(stream, n_docs, workers):
+    """The Node host with parallel packing (fluidframework_amd/node/bench_shards.js):
+    ShardedHost workers, one per host thread, pack their document shards'
+    messages into one shared batch; submit + replay in 4 slices, packing slice
+    i + 1 while slice i replays.  Texts of a sample checked against the
+    restatement."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    from fluidframework_amd import gen
+    node = shutil.which("node")
+    if node is None:
+        return {"skipped": "node not installed"}
+    m = min(n_docs, len(stream["inits"]))
+    d = tempfile.mkdtemp(prefix="mte_stream_")
+    t0 = time.perf_counter()
+    try:
+        write_stream_dir(stream, d, m)
+        r = subprocess.run([node, "--max-old-space-size=16384", os.path.join(ROOT, "fluidframework_amd", "node",
+                                                                          "bench_shards.js"), d, str(workers), "4"],
+                           capture_output=True, text=True, timeout=900)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    if r.returncode != 0:
+        return {"error": r.stderr[-2000:]}
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    from oracle import OracleEngine
+    k = len(j.get("texts", []))
+    sub = gen.slice_docs(stream, 0, k)
+    o = OracleEngine(stream["n_keys"], threads=4)
+    gen.load_stream(o, sub)
+    o.apply_batch(sub["batch"])
+    want = [o.read_doc(x)["text"] for x in range(k)]
+    return {"ops_per_s": j["ops_per_s"], "ms": j["ms"], "docs": m, "ops": j["ops"], "workers": j["workers"],
+            "parts": j["parts"], "errors": j.get("errors"), "timing_ms": j.get("timing"),
+            "texts_equal_restatement": want == j.get("texts"), "texts_checked": k,
+            "includes": "ShardedHost: worker threads pack their document shards (JS) into one shared batch, the host "
+                        "merges the interned property ids and submits (N-API mte_submit upload + mte_run), 4 slices "
+                        "pipelined, final mte_sync; message objects built in the workers before the clock",
             "wall_s": round(time.perf_counter() - t0, 1)}
 
 

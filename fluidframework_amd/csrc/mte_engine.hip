@@ -611,8 +611,9 @@ const char* bad_op(const mte_op& o, const mte_batch* b, bool local_doc, bool ref
   if (o.type >= MTE_OP_ROLLBACK && !(o.flags & MTE_F_LOCAL)) return "rollback / regen without MTE_F_LOCAL";
   if (o.type == MTE_OP_REF) {
     if (!refs_doc) return "local reference record in a document without MTE_DOC_REFS";
-    if (o.seq != 0 || o.pos2 < 0 || (uint32_t)o.pos2 >= ref_cap || o.b > 1)
-      return "local reference record: seq, slot (mte_set_ref_capacity) or b out of range";
+    if (o.seq != 0 || o.pos2 < 0 || (uint32_t)o.pos2 >= ref_cap || o.b > 3 || o.client >= MTE_MAX_CLIENTS ||
+        (o.b == 2 && o.client == 0))
+      return "local reference record: seq, slot (mte_set_ref_capacity), b or client out of range";
     return nullptr;
   }
   if ((o.flags & MTE_F_LOCAL) && o.type == MTE_OP_ANNOTATE && o.b != MTE_NO_PROPS && o.b >= MTE_ANNOTATE_SLOTS)

@@ -478,7 +478,7 @@ __device__ void stream_slide(const uint32_t* pl, uint64_t sd, int n, uint2* rt, 
         const uint32_t r = rb + (uint32_t)l;
         const uint32_t rc = r < rhi ? r : 0u;  // unconditional loads, selected after
         const uint32_t anc = ld_l2(&rt[rc].x), st = ld_l2(&rt[rc].y);
-        if (r < rhi && (st & kRefLive) && !(st & kRefDetached) && anc - toff < len) {
+        if (r < rhi && (st & kRefLive) && !(st & (kRefDetached | MTE_REF_STAY_ON_REMOVE)) && anc - toff < len) {
           if ((st & MTE_REF_SLIDE_ON_REMOVE) && t >= 0) rt[r].x = to;
           else rt[r].y = st | kRefDetached;
         }
@@ -488,52 +488,116 @@ __device__ void stream_slide(const uint32_t* pl, uint64_t sd, int n, uint2* rt, 
   }
 }
 
-// MTE_OP_REF (a local record): createLocalReferencePosition on the segment and
-// offset getContainingSegment(pos1) finds in the local view (client.ts:360-364,
-// 1107-1110; mergeTree.ts:872-885, 2124-2143), or removeLocalReferencePosition
-// (b = 1, mergeTree.ts:2113-2123).  rhi: slots in use so far.
-__device__ int stream_ref(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t& rhi, const s8v& op) {
-  const uint32_t slot = (uint32_t)op[5];
-  if ((uint32_t)op[7] == 1u) {
-    if (lane_id() == 0) rt[slot] = make_uint2(0u, 0u);
+// the anchor a reference on slot x moves to when x is removed and acked
+// (_getSlideToSegment, mergeTree.ts:893-913; Client.getSlideToSegment's offset,
+// client.ts:1117-1130), or false when there is none; x is wave-uniform
+__device__ bool slide_anchor(const uint32_t* pl, uint64_t sd, int n, int x, uint32_t& to) {
+  int t = find_slide_target(pl, sd, n, x, 1);
+  bool after = false;
+  if (t < 0) {
+    t = find_slide_target(pl, sd, n, x, -1);
+    after = true;
+  }
+  if (t < 0) return false;
+  const uint32_t tt = uni(ld_l2(pl + 5 * sd + t)), tl = uni(ld_l2(pl + t));
+  to = after ? tt + tl - 1u : tt;
+  return true;
+}
+
+// MTE_OP_REF (include/mte.h):
+//   b = 0: createLocalReferencePosition on the segment and offset
+//     getContainingSegment(pos1) finds in the local view (client.ts:360-364,
+//     1107-1110; mergeTree.ts:872-885, 2124-2143);
+//   b = 1: removeLocalReferencePosition (mergeTree.ts:2113-2123);
+//   b = 2: a reference a sequenced op creates (createPositionReference with an
+//     op, intervalCollection.ts:639-658): getContainingSegment in the op's
+//     perspective (ref_seq, client), then getSlideToSegment; no segment: detached;
+//   b = 3: the reference becomes SlideOnRemove (a = its new type) and slides if
+//     its segment is removed and acked (ackInterval, :1805-1902).
+// rhi: slots in use so far.
+template <int K>
+__device__ int stream_ref(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t& rhi, const s8v& op,
+                          int32_t m, bool newcalc) {
+  const uint32_t slot = (uint32_t)op[5], b = (uint32_t)op[7], typ = (uint32_t)op[6];
+  const int l = lane_id();
+  if (b == 1u) {
+    if (l == 0) rt[slot] = make_uint2(0u, 0u);
     vm_drain();
     return 0;
   }
-  if ((uint32_t)op[6] & (MTE_REF_STAY_ON_REMOVE | MTE_REF_TRANSIENT)) return MTE_E_UNSUPPORTED;
-  const int32_t pos = op[4];
-  const int l = lane_id();
+  if (typ & MTE_REF_TRANSIENT) return MTE_E_UNSUPPORTED;
+  if ((typ & MTE_REF_SLIDE_ON_REMOVE) && (typ & MTE_REF_STAY_ON_REMOVE)) return MTE_E_INVALID_ARG;
+  if (b == 3u) {
+    const uint32_t st0 = ld_l2(&rt[slot].y), anc = ld_l2(&rt[slot].x);
+    if (!(st0 & kRefLive)) return MTE_E_INVALID_ARG;
+    uint32_t st = (st0 & (kRefLive | kRefDetached)) | (typ & 0xffffu), to = anc;
+    if (!(st & kRefDetached) && (st & MTE_REF_SLIDE_ON_REMOVE)) {
+      // the slot holding the reference's unit
+      for (int tb = 0; tb < n; tb += kWave) {
+        const int i = tb + l;
+        const int ic = i < n ? i : 0;  // unconditional loads, selected after
+        const uint32_t tf = ld_l2(pl + 5 * sd + ic), ln = ld_l2(pl + ic);
+        const uint64_t mk = __ballot(i < n && anc - tf < ln);
+        if (mk) {
+          const int x = tb + __ffsll((long long)mk) - 1;
+          const int32_t rs = (int32_t)uni(ld_l2(pl + 2 * sd + x));
+          if (rs != kNone && rs < kLocalBase && !slide_anchor(pl, sd, n, x, to)) st |= kRefDetached;
+          break;
+        }
+      }
+    }
+    if (l == 0) rt[slot] = make_uint2(to, st);
+    vm_drain();
+    return 0;
+  }
+  const bool remote = b == 2u;
+  const int32_t pos = op[4], r = op[1];
+  const uint32_t c = ((uint32_t)op[3] >> 8) & 0xffu;
   int32_t carry = 0;
   for (int tb = 0; tb < n; tb += kTile) {
+    Regs<kTileE, K> R;
+    tile_load_hot<K>(R, pl, sd, tb, n);
     int32_t L[kTileE], P[kTileE];
-    uint32_t tf[kTileE];
+    if (remote) {
+      leaf_lengths<kTileE, K>(R, r, c + 1, (int)c, m, newcalc, L);
+    } else {
 #pragma unroll
-    for (int j = 0; j < kTileE; j++) {
-      const int i = tb + l * kTileE + j;
-      const int ic = i < n ? i : 0;  // unconditional loads, selected after
-      const int32_t ln = (int32_t)ld_l2(pl + ic), rs = (int32_t)ld_l2(pl + 2 * sd + ic);
-      tf[j] = ld_l2(pl + 5 * sd + ic);
-      L[j] = (i < n && rs == kNone) ? ln : 0;  // the local view: removed -> 0
+      for (int j = 0; j < kTileE; j++) L[j] = R.rseq[j] == kNone ? R.len[j] : 0;  // the local view: removed -> 0
     }
+#pragma unroll
+    for (int j = 0; j < kTileE; j++) L[j] = L[j] > 0 ? L[j] : 0;  // padding / undefined: nothing
     const int32_t tot = prefix<kTileE>(L, P);
     bool hit = false;
     uint32_t anc = 0;
+    int jx = 0;
 #pragma unroll
     for (int j = 0; j < kTileE; j++) {
       const bool h = L[j] > 0 && pos >= carry + P[j] && pos < carry + P[j] + L[j];
-      anc = h ? tf[j] + (uint32_t)(pos - carry - P[j]) : anc;
+      anc = h ? R.toff[j] + (uint32_t)(pos - carry - P[j]) : anc;
+      jx = h ? j : jx;
       hit = hit || h;
     }
-    const uint64_t m = __ballot(hit);
-    if (m) {
-      const uint32_t a0 = rdlane(anc, __ffsll((long long)m) - 1);
-      if (l == 0) rt[slot] = make_uint2(a0, kRefLive | ((uint32_t)op[6] & 0xffffu));
+    const uint64_t mk = __ballot(hit);
+    if (mk) {
+      const int ls = __ffsll((long long)mk) - 1;
+      uint32_t a0 = rdlane(anc, ls), st = kRefLive | (typ & 0xffffu);
+      if (remote) {
+        const int x = tb + ls * kTileE + rdlane(jx, ls);
+        const int32_t rs = (int32_t)uni(ld_l2(pl + 2 * sd + x));
+        if (rs != kNone && rs < kLocalBase && !slide_anchor(pl, sd, n, x, a0)) st |= kRefDetached;
+      }
+      if (l == 0) rt[slot] = make_uint2(a0, st);
       vm_drain();
       if (slot + 1 > rhi) rhi = slot + 1;
       return 0;
     }
     carry += tot;
   }
-  return MTE_E_INVALID_ARG;  // no segment holds pos in the local view
+  if (!remote) return MTE_E_INVALID_ARG;  // no segment holds pos in the local view
+  if (l == 0) rt[slot] = make_uint2(0u, kRefLive | kRefDetached | (typ & 0xffffu));  // detached
+  vm_drain();
+  if (slot + 1 > rhi) rhi = slot + 1;
+  return 0;
 }
 
 // One op of one HBM-resident document (see the file comment).  Returns 0 or
@@ -561,10 +625,11 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   uint2* const rt = refd ? a.refs + (uint64_t)D.doc * a.ref_cap : nullptr;
   if (type == MTE_OP_REF) {
     if (!(flags & MTE_F_LOCAL) || !ldoc || !refd) return MTE_E_UNSUPPORTED;
-    if ((uint32_t)op[5] >= a.ref_cap || (uint32_t)op[7] > 1u) return MTE_E_INVALID_ARG;
+    if ((uint32_t)op[5] >= a.ref_cap || (uint32_t)op[7] > 3u) return MTE_E_INVALID_ARG;
+    if ((uint32_t)op[7] == 2u && c == 0) return MTE_E_INVALID_ARG;  // a sequenced op of another client
     MTE_STAT(st[kStOps]++;)
-    MTE_STAT(if ((uint32_t)op[7] == 0u) st[kStScanned] += (uint32_t)D.n;)
-    const int rc = stream_ref(pl, sd, D.n, rt, rhi, op);
+    MTE_STAT(if ((uint32_t)op[7] != 1u) st[kStScanned] += (uint32_t)D.n;)
+    const int rc = stream_ref<K>(pl, sd, D.n, rt, rhi, op, D.min_seq, (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0);
     if (rc) return rc;
     D.k++;
     return 0;

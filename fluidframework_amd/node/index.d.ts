@@ -190,7 +190,7 @@ export interface SequenceDeltaEvent {
   last: SequenceDeltaRange;
 }
 
-/** ReferenceType flags (ops.ts): Simple 0, SlideOnRemove 0x40 (StayOnRemove / Transient unsupported). */
+/** ReferenceType flags (ops.ts): Simple 0, SlideOnRemove 0x40, StayOnRemove 0x80 (Transient unsupported). */
 export class LocalReferencePosition {
   readonly refType: number;
   properties?: PropertySet;
@@ -205,8 +205,44 @@ export interface SegmentSnapshot {
   kind: number;
 }
 
+/** IntervalType (intervalCollection.ts:48-66) and ReferenceType (merge-tree ops.ts) flags. */
+export const IntervalType: { Simple: 0; Nest: 1; SlideOnRemove: 2; Transient: 4 };
+export const RefType: { Simple: 0; Tile: 1; NestBegin: 2; NestEnd: 4; RangeBegin: 16; RangeEnd: 32;
+  SlideOnRemove: 64; StayOnRemove: 128; Transient: 256 };
+
+/** SequenceInterval (intervalCollection.ts:387-619): its ends are engine references. */
+export class SequenceInterval {
+  start: LocalReferencePosition;
+  end: LocalReferencePosition;
+  intervalType: number;
+  properties: PropertySet;
+  getIntervalId(): string;
+  /** [start, end] in the client's view (-1: slid off the string). */
+  positions(): [number, number];
+  serialize(): { start: number; end: number; intervalType: number; sequenceNumber: number; properties: PropertySet };
+}
+
+/** IntervalCollection (intervalCollection.ts:1309-2102) over a {localClient, refs} BatchClient. */
+export class IntervalCollection implements Iterable<SequenceInterval> {
+  readonly label: string;
+  add(start: number, end: number, intervalType: number, props?: PropertySet): SequenceInterval;
+  change(id: string, start?: number, end?: number): SequenceInterval | undefined;
+  changeProperties(id: string, props: PropertySet): void;
+  removeIntervalById(id: string): SequenceInterval | undefined;
+  getIntervalById(id: string): SequenceInterval | undefined;
+  /** A sequenced interval op (makeOpsMap): ackAdd / ackChange / ackDelete. */
+  process(opName: "add" | "change" | "delete", value: any, local: boolean, op: ISequencedDocumentMessage): void;
+  findOverlappingIntervals(startPosition: number, endPosition: number): SequenceInterval[];
+  [Symbol.iterator](): Iterator<SequenceInterval>;
+}
+
 export class BatchClient {
   readonly mergeTree: BatchMergeTree;
+  /** SharedString.getIntervalCollection; emitter.emit(opName, undefined, value) receives the ops to send. */
+  getIntervalCollection(label: string, emitter?: { emit(opName: string, prev: undefined, value: any, meta: any): void }):
+    IntervalCollection;
+  /** A sequenced {key: label, type: "act", value: {opName, value}} interval message (applyMsg routes them too). */
+  applyIntervalMsg(msg: ISequencedDocumentMessage): void;
   // local references ({localClient: true, refs: true} documents)
   getContainingSegment(pos: number): { segment: SegmentSnapshot | undefined; offset: number | undefined };
   createLocalReferencePosition(segment: SegmentSnapshot | number, offset: number | undefined, refType: number,

@@ -26,6 +26,7 @@
  */
 const path = require("path");
 const packing = require("./packing");
+const { IntervalCollection, IntervalType, RefType } = require("./intervals");
 
 const { BatchBuilder, DocClients, Interner, MergeTreeError, packDocInits, packSegments, utf16 } = packing;
 
@@ -93,7 +94,7 @@ class MergeTreeEngine {
   constructor(options) {
     const o = options || {};
     this.nKeys = o.nKeys === undefined ? 8 : o.nKeys;
-    this.addon = loadAddon();
+    this.addon = o.addon || loadAddon();  // o.addon: another binding of the same functions (tests)
     this.ctx = this.addon.create(o.device || 0, this.nKeys, o.segCapacity || 0);
     this.interner = new Interner(this.nKeys);
     this.docs = [];
@@ -404,6 +405,10 @@ class BatchClient {
    *  (ackPendingSegment, mergeTree.ts:1278-1331). */
   applyMsg(msg, local) {
     if (local) throw new MergeTreeError(-9, "applyMsg(msg, local = true): pass the sequenced message");
+    if (msg.contents && msg.contents.type === "act") {  // an interval op (SharedString's map kernel)
+      this.applyIntervalMsg(msg);
+      return;
+    }
     this.engine._batch().addMessage(this.doc, this.clients, msg);
     if (msg.minimumSequenceNumber > this.lastMinSeq) this.lastMinSeq = msg.minimumSequenceNumber;
   }
@@ -595,8 +600,8 @@ class BatchClient {
   /** Client.createLocalReferencePosition (client.ts:360-364): a reference at
    *  offset of segment (from getContainingSegment; a number is taken as a
    *  position of this client's view).  refType: ReferenceType flags --
-   *  SlideOnRemove (0x40) or Simple (0), with any label bits; StayOnRemove and
-   *  Transient throw.  Queued with the document's next replay. */
+   *  SlideOnRemove (0x40), StayOnRemove (0x80) or Simple (0), with any label
+   *  bits; Transient throws.  Queued with the document's next replay. */
   createLocalReferencePosition(segment, offset, refType, properties) {
     if (!this.engine.docs[this.doc].refs) throw new MergeTreeError(-9, "createClient(..., {refs: true}) first");
     const base = typeof segment === "number" ? segment : (segment && typeof segment.start === "number" ? segment.start : NaN);
@@ -604,6 +609,47 @@ class BatchClient {
     const rt = refType === undefined ? 0 : refType;
     const slot = this.engine._batch().addRef(this.doc, this.clients, base + (offset || 0), rt);
     return new LocalReferencePosition(this, slot, rt, properties);
+  }
+
+  /** A reference a sequenced op creates in its own perspective (refSeq and
+   *  sender): createPositionReference with an op (intervalCollection.ts:639-658),
+   *  SlideOnRemove, detached when no segment holds pos there. */
+  _createRefFromOp(msg, pos, refType) {
+    if (!this.engine.docs[this.doc].refs) throw new MergeTreeError(-9, "createClient(..., {refs: true}) first");
+    const slot = this.engine._batch().addRefRemote(this.doc, this.clients, msg, pos, refType);
+    return new LocalReferencePosition(this, slot, refType, undefined);
+  }
+
+  /** The reference becomes refType (SlideOnRemove) and slides if its segment is
+   *  removed and acked (ackInterval's setSlideOnRemove + getSlideToSegment). */
+  _setRefSlide(lref, refType) {
+    if (!lref || lref.client !== this || lref.slot < 0) return;
+    this.engine._batch().setRefSlide(this.doc, this.clients, lref.slot, refType);
+    lref.refType = refType;
+  }
+
+  /** SharedString.getIntervalCollection(label) (sequence.ts): the label's
+   *  IntervalCollection over this client's references ({localClient, refs}
+   *  documents); emitter.emit(opName, undefined, value) receives its ops. */
+  getIntervalCollection(label, emitter) {
+    if (!this.intervalCollections) this.intervalCollections = new Map();
+    let c = this.intervalCollections.get(label);
+    if (!c) {
+      if (!this.engine.docs[this.doc].refs) throw new MergeTreeError(-9, "createClient(..., {refs: true}) first");
+      c = new IntervalCollection(this, label, emitter);
+      this.intervalCollections.set(label, c);
+    } else if (emitter) {
+      c.emitter = emitter;
+    }
+    return c;
+  }
+
+  /** A sequenced interval op as SharedString's map kernel carries it
+   *  ({key: label, type: "act", value: {opName, value}}): processed by the
+   *  label's collection; the merge-tree window does not move (sequence.ts:628-648). */
+  applyIntervalMsg(msg) {
+    const c = msg.contents;
+    this.getIntervalCollection(c.key).process(c.value.opName, c.value.value, msg.clientId === this.longClientId, msg);
   }
 
   /** Client.removeLocalReferencePosition (client.ts:369-371). */
@@ -927,4 +973,5 @@ function loadLegacy(blobs) {
   return { segments: specs, minSeq: md.minSequenceNumber !== undefined ? md.minSequenceNumber : seq, currentSeq: seq };
 }
 
-module.exports = { MergeTreeEngine, BatchClient, LocalReferencePosition, MergeTreeError, loadAddon, loadLegacy, packing };
+module.exports = { MergeTreeEngine, BatchClient, LocalReferencePosition, IntervalCollection, IntervalType, RefType,
+  MergeTreeError, loadAddon, loadLegacy, packing };

@@ -115,6 +115,16 @@ class Interner {
     if (prim !== null && !(typeof v === "number" && Object.is(v, -0))) prim.set(v, i);
     return i;
   }
+  /** the id of a value given as its canonical JSON (a shard's interned value, shards.js) */
+  valueOfJson(cj) {
+    let i = this.values.get(cj);
+    if (i === undefined) {
+      i = this.valueJson.length;
+      this.values.set(cj, i);
+      this.valueJson.push(cj);
+    }
+    return i;
+  }
   /** plane values of one segment -> PropertySet (undefined when empty) */
   decode(planes) {
     let out;
@@ -227,7 +237,7 @@ function utf16(s) {
 
 /** Collects messages for nDocs documents and emits one mte_batch. */
 class BatchBuilder {
-  constructor(nDocs, interner, trackDocs) {
+  constructor(nDocs, interner, trackDocs, capHint) {
     this.nDocs = nDocs;
     this.interner = interner;
     // documents whose delta events are read back (MTE_DOC_EVENTS): per record,
@@ -237,7 +247,7 @@ class BatchBuilder {
     this.props = new PropTable(interner);
     // records in arrival order, 8 int32 words each (the mte_op layout), and
     // their documents; build() sorts them by document (counting sort)
-    this.cap = 1024;
+    this.cap = Math.max(1024, capHint || 0);  // records (capHint: the expected count, no regrowth)
     this.rec = new Int32Array(this.cap * 8);
     this.recDoc = new Uint32Array(this.cap);
     this.docCount = new Uint32Array(nDocs);
@@ -380,6 +390,7 @@ class BatchBuilder {
     for (let k = k0; k < this.count; k++) R[k * 8 + 3] |= short << 8;
     R[(this.count - 1) * 8 + 3] |= F_MSG_END << 16;
     clients.advance(msn);
+    clients.mergeSeq = seq;  // collabWindow.currentSeq after updateSeqNumbers (client.ts:937-945)
   }
 
   /** the records of a remote op (client.ts:862-889), as _opRecords, written
@@ -578,16 +589,62 @@ class BatchBuilder {
   addRef(doc, clients, pos, refType) {
     if (!clients.local) throw new MergeTreeError(E_UNSUPPORTED, "local reference in an observer document");
     const rt = checkI32(refType === undefined ? REF_SLIDE_ON_REMOVE : refType, "refType");
-    if (rt < 0 || (rt & (REF_STAY_ON_REMOVE | REF_TRANSIENT))) {
-      throw new MergeTreeError(E_UNSUPPORTED, "StayOnRemove / Transient local references");
+    if (rt < 0 || (rt & REF_TRANSIENT)) {
+      throw new MergeTreeError(E_UNSUPPORTED, "Transient local references (positions are not tracked)");
+    }
+    if ((rt & REF_SLIDE_ON_REMOVE) && (rt & REF_STAY_ON_REMOVE)) {
+      throw new MergeTreeError(E_INVALID_ARG, "SlideOnRemove and StayOnRemove together");
     }
     const p = checkI32(pos, "pos");
-    const slot = clients.refFree.length ? clients.refFree.pop() : clients.refNext;
-    if (slot === clients.refNext) clients.refNext++;
+    const slot = this._refSlot(clients);
     this._put(doc, 0, 0, 0, OP_REF, 0, F_LOCAL, p, slot, rt, 0);
     const src = this._src(doc);
     if (src) src.push({ msg: null, op: undefined, local: true });
     return slot;
+  }
+
+  _refSlot(clients) {
+    const slot = clients.refFree.length ? clients.refFree.pop() : clients.refNext;
+    if (slot === clients.refNext) clients.refNext++;
+    return slot;
+  }
+
+  /** A reference a sequenced op creates (createPositionReference with an op,
+   *  intervalCollection.ts:639-658): getContainingSegment(pos) in the op's
+   *  perspective (its refSeq and sender), then getSlideToSegment; detached when
+   *  no segment holds pos there (MTE_OP_REF, b = 2).  The sender takes a short
+   *  id as for a message (getClientSequenceArgsForMessage).  Returns the slot. */
+  addRefRemote(doc, clients, msg, pos, refType) {
+    if (!clients.local) throw new MergeTreeError(E_UNSUPPORTED, "local reference in an observer document");
+    const rt = checkI32(refType, "refType");
+    if (!(rt & REF_SLIDE_ON_REMOVE) || (rt & (REF_STAY_ON_REMOVE | REF_TRANSIENT))) {
+      throw new MergeTreeError(E_INVALID_ARG, "an op creates SlideOnRemove references");
+    }
+    const seq = checkI32(msg.sequenceNumber, "sequenceNumber");
+    const ref = checkI32(msg.referenceSequenceNumber, "referenceSequenceNumber");
+    if (ref < clients.minSeq) {
+      throw new MergeTreeError(E_INVALID_ARG, "referenceSequenceNumber " + ref + " < minSeq " + clients.minSeq);
+    }
+    if (msg.clientId === clients.observer) throw new MergeTreeError(E_INVALID_ARG, "a remote op of the local client");
+    const short = slotOf(clients, msg.clientId, seq);
+    const slot = this._refSlot(clients);
+    this._put(doc, 0, ref, 0, OP_REF, short, F_LOCAL, checkI32(pos, "pos"), slot, rt, 2);
+    const src = this._src(doc);
+    if (src) src.push({ msg: null, op: undefined, local: true });
+    return slot;
+  }
+
+  /** The reference in slot becomes refType (SlideOnRemove) and slides if its
+   *  segment is removed and acked (ackInterval, intervalCollection.ts:1819-1902;
+   *  MTE_OP_REF, b = 3). */
+  setRefSlide(doc, clients, slot, refType) {
+    const rt = checkI32(refType, "refType");
+    if (!(rt & REF_SLIDE_ON_REMOVE) || (rt & (REF_STAY_ON_REMOVE | REF_TRANSIENT))) {
+      throw new MergeTreeError(E_INVALID_ARG, "setRefSlide takes a SlideOnRemove type");
+    }
+    this._put(doc, 0, 0, 0, OP_REF, 0, F_LOCAL, 0, slot, rt, 3);
+    const src = this._src(doc);
+    if (src) src.push({ msg: null, op: undefined, local: true });
   }
 
   /** removeLocalReferencePosition (mergeTree.ts:2113-2123). */

@@ -389,8 +389,10 @@ class BatchBuilder:
         if not clients.local:
             raise MergeTreeError(MTE_E_UNSUPPORTED, "local reference in an observer document")
         ref_type = _check_i32(ref_type, "refType")
-        if ref_type & (REF_STAY_ON_REMOVE | REF_TRANSIENT) or ref_type < 0:
-            raise MergeTreeError(MTE_E_UNSUPPORTED, "StayOnRemove / Transient local references")
+        if ref_type & REF_TRANSIENT or ref_type < 0:
+            raise MergeTreeError(MTE_E_UNSUPPORTED, "Transient local references (positions are not tracked)")
+        if ref_type & REF_SLIDE_ON_REMOVE and ref_type & REF_STAY_ON_REMOVE:
+            raise MergeTreeError(MTE_E_INVALID_ARG, "SlideOnRemove and StayOnRemove together")
         slot = clients.ref_free.pop() if clients.ref_free else clients.ref_next
         if slot == clients.ref_next:
             clients.ref_next += 1

@@ -339,12 +339,40 @@ static int doc_regen(odoc* d, const mte_op* op);
  * not a pending insert and not removed-and-acked (a pending removal is fine) */
 static inline int slide_target_ok(const oseg* g) { return g->seq < LOCAL_BASE && g->rseq >= LOCAL_BASE; }
 
-/* MTE_OP_REF: createLocalReferencePosition on getContainingSegment(pos1) in the
- * local view (client.ts:360-364, 1107-1110; mergeTree.ts:872-885, 2124-2143) or
- * removeLocalReferencePosition (mergeTree.ts:2113-2123). */
+/* where a reference on segment i slides to when that segment is removed and
+ * acked (_getSlideToSegment, mergeTree.ts:893-913; Client.getSlideToSegment's
+ * offset, client.ts:1117-1130): the first following segment it may slide to at
+ * offset 0, else the last preceding one at its last offset; -1: nowhere */
+static int64_t slide_to(const odoc* d, uint32_t i, uint32_t* anchor) {
+  for (uint32_t j = i + 1; j < d->n; j++)
+    if (slide_target_ok(&d->s[j])) {
+      *anchor = d->s[j].toff;
+      return j;
+    }
+  for (int64_t j = (int64_t)i - 1; j >= 0; j--)
+    if (slide_target_ok(&d->s[j])) {
+      *anchor = d->s[j].toff + (uint32_t)d->s[j].len - 1u;
+      return j;
+    }
+  return -1;
+}
+static inline int removed_and_acked(const oseg* g) { return g->rseq != NONE_SEQ && !is_pending(g->rseq); }
+
+/* MTE_OP_REF (include/mte.h):
+ *   b = 0: createLocalReferencePosition on getContainingSegment(pos1) in the
+ *     local view (client.ts:360-364, 1107-1110; mergeTree.ts:872-885, 2124-2143);
+ *   b = 1: removeLocalReferencePosition (mergeTree.ts:2113-2123);
+ *   b = 2: a reference a sequenced op creates (createPositionReference with an
+ *     op, intervalCollection.ts:639-658): getContainingSegment(pos1, op) in the
+ *     op's perspective (ref_seq, client), then getSlideToSegment -- a segment
+ *     removed and acked since hands it on at once; no segment: detached
+ *     (createDetachedLocalReferencePosition, :621-637);
+ *   b = 3: the reference becomes SlideOnRemove (a = its new type) and slides
+ *     if its segment is removed and acked (ackInterval's setSlideOnRemove and
+ *     getSlideToSegment, :1805-1902). */
 static int doc_ref(odoc* d, const mte_op* op) {
   if (!(d->flags & MTE_DOC_REFS)) return MTE_E_UNSUPPORTED;
-  if (op->pos2 < 0 || (uint32_t)op->pos2 >= REF_LIMIT || op->b > 1) return MTE_E_INVALID_ARG;
+  if (op->pos2 < 0 || (uint32_t)op->pos2 >= REF_LIMIT || op->b > 3) return MTE_E_INVALID_ARG;
   const uint32_t slot = (uint32_t)op->pos2;
   if (slot >= d->ref_cap) {
     uint32_t nc = d->ref_cap ? d->ref_cap : 64;
@@ -363,18 +391,49 @@ static int doc_ref(odoc* d, const mte_op* op) {
     d->ref_state[slot] = 0;
     return MTE_OK;
   }
-  if (op->a & (MTE_REF_STAY_ON_REMOVE | MTE_REF_TRANSIENT)) return MTE_E_UNSUPPORTED;
+  if (op->a & MTE_REF_TRANSIENT) return MTE_E_UNSUPPORTED;
+  if ((op->a & MTE_REF_SLIDE_ON_REMOVE) && (op->a & MTE_REF_STAY_ON_REMOVE)) return MTE_E_INVALID_ARG;
   d->scanned += d->n;
+  if (op->b == 3) {
+    uint32_t st = d->ref_state[slot];
+    if (!(st & REF_LIVE)) return MTE_E_INVALID_ARG;
+    d->ref_state[slot] = st = (st & (REF_LIVE | REF_DETACHED)) | (op->a & 0xffffu);
+    if (st & REF_DETACHED) return MTE_OK;
+    for (uint32_t i = 0; i < d->n; i++) {
+      const oseg* g = &d->s[i];
+      if (d->ref_anchor[slot] - g->toff >= (uint32_t)g->len) continue;
+      if (removed_and_acked(g) && (st & MTE_REF_SLIDE_ON_REMOVE)) {
+        uint32_t to = 0;
+        if (slide_to(d, i, &to) >= 0) d->ref_anchor[slot] = to;
+        else d->ref_state[slot] = st | REF_DETACHED;
+      }
+      break;
+    }
+    return MTE_OK;
+  }
+  const int remote = op->b == 2;
+  if (remote && (op->client >= MTE_MAX_CLIENTS || op->client == 0)) return MTE_E_INVALID_ARG;
+  int rc;
+  if (remote && (rc = doc_scratch(d))) return rc;
+  if (remote) doc_lengths(d, op->ref_seq, op->client, d->min_seq, (d->flags & MTE_DOC_NEW_LENGTH_CALC) != 0);
   int64_t p = 0;
+  if (slot + 1 > d->ref_hi) d->ref_hi = slot + 1;
   for (uint32_t i = 0; i < d->n; i++) {
-    const int32_t l = own_len(&d->s[i]);
+    const int32_t l = remote ? d->L[i] : own_len(&d->s[i]);
     if (l > 0 && op->pos1 >= p && op->pos1 < p + l) {
-      d->ref_anchor[slot] = d->s[i].toff + (uint32_t)(op->pos1 - p);
-      d->ref_state[slot] = REF_LIVE | (op->a & 0xffffu);
-      if (slot + 1 > d->ref_hi) d->ref_hi = slot + 1;
+      uint32_t anchor = d->s[i].toff + (uint32_t)(op->pos1 - p);
+      uint32_t st = REF_LIVE | (op->a & 0xffffu);
+      if (remote && removed_and_acked(&d->s[i]) && slide_to(d, i, &anchor) < 0) st |= REF_DETACHED;
+      d->ref_anchor[slot] = anchor;
+      d->ref_state[slot] = st;
       return MTE_OK;
     }
-    p += l;
+    if (l > 0) p += l;
+  }
+  if (remote) {  /* no segment holds pos1 in the op's view: a detached reference */
+    d->ref_anchor[slot] = 0;
+    d->ref_state[slot] = REF_LIVE | REF_DETACHED | (op->a & 0xffffu);
+    return MTE_OK;
   }
   return MTE_E_INVALID_ARG; /* no segment holds pos1 in the local view */
 }
@@ -392,22 +451,14 @@ static void doc_slide_refs(odoc* d, int32_t s) {
   for (uint32_t i = 0; i < d->n; i++) {
     const oseg* g = &d->s[i];
     if (g->rseq != s) continue;
-    int64_t t = -1;
-    int after = 0;
-    for (uint32_t j = i + 1; j < d->n && t < 0; j++)
-      if (slide_target_ok(&d->s[j])) t = j;
-    for (int64_t j = (int64_t)i - 1; j >= 0 && t < 0; j--)
-      if (slide_target_ok(&d->s[j])) t = j, after = 1;
+    uint32_t to = 0;
+    const int64_t t = slide_to(d, i, &to);
     for (uint32_t r = 0; r < d->ref_hi; r++) {
       const uint32_t st = d->ref_state[r];
-      if (!(st & REF_LIVE) || (st & REF_DETACHED)) continue;
+      if (!(st & REF_LIVE) || (st & REF_DETACHED) || (st & MTE_REF_STAY_ON_REMOVE)) continue;
       if (d->ref_anchor[r] - g->toff >= (uint32_t)g->len) continue;
-      if ((st & MTE_REF_SLIDE_ON_REMOVE) && t >= 0) {
-        const oseg* tg = &d->s[t];
-        d->ref_anchor[r] = after ? tg->toff + (uint32_t)tg->len - 1u : tg->toff;
-      } else {
-        d->ref_state[r] = st | REF_DETACHED;
-      }
+      if ((st & MTE_REF_SLIDE_ON_REMOVE) && t >= 0) d->ref_anchor[r] = to;
+      else d->ref_state[r] = st | REF_DETACHED;
     }
   }
 }
@@ -1013,7 +1064,8 @@ int orc_apply_batch(orc_ctx* c, const mte_batch* b, int n_threads) {
     if (op->type > MTE_OP_REF) return MTE_E_INVALID_ARG;
     if (op->type >= MTE_OP_ROLLBACK && !(op->flags & MTE_F_LOCAL)) return MTE_E_INVALID_ARG;
     if (op->type == MTE_OP_REF) {
-      if (!(c->docs[dcur].flags & MTE_DOC_REFS) || op->seq != 0 || op->pos2 < 0 || op->b > 1)
+      if (!(c->docs[dcur].flags & MTE_DOC_REFS) || op->seq != 0 || op->pos2 < 0 || op->b > 3 ||
+          op->client >= MTE_MAX_CLIENTS)
         return MTE_E_INVALID_ARG;
       continue;
     }

@@ -1,0 +1,193 @@
+#!/usr/bin/env node
+// ref_interval_farm.js — conflict farms of REFERENCE merge-tree Clients that
+// also edit a SharedString interval collection (TEST INFRASTRUCTURE; build
+// container only, never on the GPU box).
+//
+// Every client holds the reference's IntervalCollection over its Client
+// (packages/dds/sequence/src/intervalCollection.ts, erased by oracle/ts_erase.py
+// into _ref/ts/sequence/), attached as SharedString attaches it
+// (attachGraph(client, label), intervalCollection.ts:1337-1374), and processes
+// interval messages as SharedSegmentSequence.processCore does: through the
+// value type's ops map (makeOpsMap: ackAdd / ackChange / ackDelete,
+// :1163-1221) without touching the merge-tree window (sequence.ts:628-648).
+// Merge-tree ops are made and sequenced as in oracle/ref_farm.js.  Interval
+// ops: add (with an explicit intervalId), change of one or both ends,
+// changeProperties, removeIntervalById, by any client but the observer.  A
+// message's refSeq is the sender's last processed seq (any kind), msn the
+// lowest of those over the clients.
+//
+// stdin:  {"sets": [{"seed", "clients", "steps", "initialText", "nCheckpoints",
+//                    "maxText", "intervals": p (the chance a step is an interval op)}]}
+// stdout: {"sets": [{..params, "names", "log": [[clientId, seq, ref, msn, kind, contents]]
+//                    (kind "op": a merge-tree op; "iv": {opName, value}),
+//                    "events": per client [["L"|"A", logIndex] | ["I", logIndex]
+//                    (an interval op it made: the log entry holds it)],
+//                    "checkpoints": [{"done", "states": [{"text", "intervals":
+//                    [[id, start, end, props]] sorted by id}]}]}]}
+"use strict";
+const path = require("path");
+const fs = require("fs");
+
+const refdir = process.argv[2] || path.join(__dirname, "_ref", "ts");
+const { Client } = require(path.join(refdir, "client.js"));
+const { TextSegment } = require(path.join(refdir, "textSegment.js"));
+const { Marker } = require(path.join(refdir, "mergeTreeNodes.js"));
+const { MergeTreeTextHelper } = require(path.join(refdir, "MergeTreeTextHelper.js"));
+const iv = require(path.join(refdir, "sequence", "intervalCollection.js"));
+
+function specToSegment(spec) {
+  const t = TextSegment.fromJSONObject(spec);
+  if (t) return t;
+  const m = Marker.fromJSONObject(spec);
+  if (m) return m;
+  throw new Error(`Unrecognized IJSONSegment type: '${JSON.stringify(spec)}'`);
+}
+const logger = { send() {}, sendTelemetryEvent() {}, sendErrorEvent() {}, sendPerformanceEvent() {} };
+
+// mulberry32 (as oracle/ref_farm.js)
+function rng(seed) {
+  let a = seed >>> 0;
+  const next = () => {
+    a = (a + 0x6d2b79f5) >>> 0;
+    let t = a;
+    t = Math.imul(t ^ (t >>> 15), t | 1);
+    t ^= t + Math.imul(t ^ (t >>> 7), t | 61);
+    return ((t ^ (t >>> 14)) >>> 0) / 4294967296;
+  };
+  return { next, int: (lo, hi) => lo + Math.floor(next() * (hi - lo + 1)) };
+}
+function sortKeys(v) {
+  if (v && typeof v === "object" && !Array.isArray(v)) {
+    const o = {};
+    for (const k of Object.keys(v).sort()) o[k] = sortKeys(v[k]);
+    return o;
+  }
+  return v;
+}
+const clone = (v) => JSON.parse(JSON.stringify(v));
+const LABEL = "farm";
+const KEYS = ["client", "bold", "color"];
+
+function runSet(p) {
+  const R = rng(p.seed);
+  const names = [];
+  for (let i = 0; i < p.clients; i++) names.push(String.fromCharCode(65 + i));
+  const ops = new iv.SequenceIntervalCollectionValueType().ops;
+  const factory = new iv.SequenceIntervalCollectionValueType().factory;
+  const sent = [];  // the interval op each emitter captures, per client
+  const clients = names.map((n, i) => {
+    const c = new Client(specToSegment, logger, { mergeTreeUseNewLengthCalculations: true });
+    if (p.initialText) c.insertSegmentLocal(0, new TextSegment(p.initialText));
+    c.startOrUpdateCollaboration(n);
+    const emitter = { emit(opName, _prev, params) { sent[i] = { opName, value: clone(params) }; } };
+    const coll = factory.load(emitter, []);
+    coll.attachGraph(c, LABEL);
+    return { c, coll, lastSeq: 0, ids: [] };
+  });
+  const cursor = names.map(() => 0);
+  const events = names.map(() => []);
+  const log = [];
+  let seq = 0, nextId = 0;
+  const checkpoints = [];
+  const every = Math.max(1, Math.floor(p.steps / Math.max(1, p.nCheckpoints)));
+  const msnNow = () => clients.reduce((a, x) => Math.min(a, x.lastSeq), Infinity);
+
+  const applyNext = (i) => {
+    const m = log[cursor[i]];
+    const msg = { clientId: m[0], sequenceNumber: m[1], referenceSequenceNumber: m[2], minimumSequenceNumber: m[3],
+      type: "op", contents: m[5] };
+    const X = clients[i];
+    if (m[4] === "op") {
+      X.c.applyMsg(msg);
+    } else {
+      ops.get(m[5].opName).process(X.coll, clone(m[5].value), m[0] === names[i], msg);
+    }
+    X.lastSeq = m[1];
+    events[i].push(["A", cursor[i]]);
+    cursor[i]++;
+  };
+  const readOut = (X) => {
+    const helper = new MergeTreeTextHelper(X.c._mergeTree);
+    const text = helper.getText(X.c.getCurrentSeq(), X.c.getClientId(), "");
+    const out = [];
+    for (const ival of X.coll) {
+      const props = Object.assign({}, ival.properties);
+      out.push([ival.getIntervalId(), X.c.localReferencePositionToPosition(ival.start),
+        X.c.localReferencePositionToPosition(ival.end), sortKeys(props)]);
+    }
+    out.sort((a, b) => (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0));
+    return { text, intervals: out };
+  };
+  const checkpoint = () => {
+    checkpoints.push({ done: events.map((e) => e.length), states: clients.map(readOut) });
+  };
+  const send = (i, kind, contents) => {
+    seq++;
+    log.push([names[i], seq, clients[i].lastSeq, msnNow(), kind, contents]);
+    events[i].push([kind === "op" ? "L" : "I", log.length - 1]);
+  };
+
+  for (let step = 0; step < p.steps; step++) {
+    const i = R.int(1, p.clients - 1);
+    const X = clients[i];
+    const len = X.c.getLength();
+    if (R.next() < p.intervals) {
+      // an interval op of client i (SharedString.getIntervalCollection(label).add / change / ...)
+      const live = Array.from(X.coll).map((x) => x.getIntervalId());
+      const pick = R.next();
+      sent[i] = undefined;
+      if (live.length === 0 || pick < 0.35) {
+        if (len === 0) continue;
+        const s0 = R.int(0, len - 1), e0 = R.int(s0, Math.min(len - 1, s0 + R.int(0, 12)));
+        const id = `iv${nextId++}`;
+        const props = { intervalId: id };
+        if (R.next() < 0.3) props[KEYS[R.int(0, 2)]] = R.int(0, 3);
+        X.coll.add(s0, e0, iv.IntervalType.SlideOnRemove, props);
+      } else {
+        const id = live[R.int(0, live.length - 1)];
+        if (pick < 0.6) {
+          if (len === 0) continue;
+          const s0 = R.int(0, len - 1), e0 = R.int(s0, Math.min(len - 1, s0 + R.int(0, 12)));
+          const which = R.int(0, 2);
+          X.coll.change(id, which === 2 ? undefined : s0, which === 1 ? undefined : e0);
+        } else if (pick < 0.8) {
+          X.coll.changeProperties(id, { [KEYS[R.int(0, 2)]]: R.next() < 0.2 ? null : R.int(0, 5) });
+        } else {
+          X.coll.removeIntervalById(id);
+        }
+      }
+      if (sent[i]) send(i, "iv", sent[i]);
+    } else if (R.next() < 0.5) {
+      // a merge-tree op (as oracle/ref_farm.js)
+      let op;
+      if (len < 4 || (R.next() < 0.4 && len < p.maxText)) {
+        const pos = R.int(0, len);
+        const seg = new TextSegment(names[i].repeat(R.int(1, 3)));
+        op = X.c.insertSegmentLocal(pos, seg);
+      } else {
+        const start = R.int(0, len - 1);
+        const end = R.int(start + 1, Math.min(len, start + 1 + R.int(0, 24)));
+        if (R.next() < 0.7) op = X.c.removeRangeLocal(start, end);
+        else op = X.c.annotateRangeLocal(start, end, { [KEYS[R.int(0, 2)]]: R.int(0, 5) }, undefined);
+      }
+      if (op) send(i, "op", clone(op));
+    } else {
+      const j = R.int(0, p.clients - 1);
+      const k = R.int(1, 6);
+      for (let q = 0; q < k && cursor[j] < log.length; q++) applyNext(j);
+    }
+    if ((step + 1) % every === 0 && step + 1 < p.steps) checkpoint();
+  }
+  for (let i = 0; i < p.clients; i++) while (cursor[i] < log.length) applyNext(i);
+  checkpoint();
+  const last = checkpoints[checkpoints.length - 1].states;
+  for (const s of last) {
+    if (s.text !== last[0].text || JSON.stringify(s.intervals) !== JSON.stringify(last[0].intervals)) {
+      throw new Error(`seed ${p.seed}: the reference clients did not converge`);
+    }
+  }
+  return Object.assign({}, p, { names, log, events, checkpoints });
+}
+
+const input = JSON.parse(fs.readFileSync(0, "utf8"));
+process.stdout.write(JSON.stringify({ sets: input.sets.map(runSet) }));

@@ -47,6 +47,7 @@ REF_ROOT = "/root/reference"
 EXTERNAL = {
     "common-utils": [("assert", "common/lib/common-utils/src/assert.ts"),
                      ("trace", "common/lib/common-utils/src/trace.ts"),
+                     ("typedEventEmitter", "common/lib/common-utils/src/typedEventEmitter.ts"),
                      ("unreachable", "common/lib/common-utils/src/unreachable.ts"),
                      ("performanceNode", "common/lib/common-utils/src/performanceNode.ts")],
     "protocol-definitions": [("protocol", "common/lib/protocol-definitions/src/protocol.ts")],
@@ -55,6 +56,13 @@ EXTERNAL = {
 INDEX_ALIASES = {"common-utils": {"indexNode": "performanceNode"}}
 STUBBED = ("telemetry-utils", "container-utils", "runtime-utils")  # oracle/ref_stubs.js
 STUB_EXTRA = ("common-utils",)  # + bufferToString from oracle/ref_stubs.js
+# the sequence package's interval collection over the erased merge-tree
+# (oracle/ref_interval_farm.js): erased into <out>/sequence/, with
+# @fluidframework/merge-tree resolving to the erased merge-tree itself.  Its
+# only third-party import, uuid, makes the ids of intervals added without one;
+# the farm always passes ids, and node_modules/uuid throws if it is ever called.
+SEQUENCE_SRC = "packages/dds/sequence/src"
+SEQUENCE_FILES = ("intervalCollection.ts", "intervalTree.ts")
 TYPE_ONLY = ("core-interfaces", "shared-object-base", "datastore-definitions", "runtime-definitions",
              "common-definitions", "driver-definitions")
 
@@ -1208,6 +1216,19 @@ def main():
         d = os.path.join(nm, pkg)
         os.makedirs(d, exist_ok=True)
         open(os.path.join(d, "index.js"), "w").write(f"module.exports = require({stubs!r});\n")
+    seq_out = os.path.join(args.out, "sequence")
+    os.makedirs(seq_out, exist_ok=True)
+    for f in SEQUENCE_FILES:
+        open(os.path.join(seq_out, f[:-3] + ".js"), "w", encoding="utf-8").write(
+            erase_file(os.path.join(REF_ROOT, SEQUENCE_SRC, f)))
+        n += 1
+    d = os.path.join(nm, "merge-tree")
+    os.makedirs(d, exist_ok=True)
+    open(os.path.join(d, "index.js"), "w").write("module.exports = require(\"../../../index\");\n")
+    d = os.path.join(args.out, "node_modules", "uuid")
+    os.makedirs(d, exist_ok=True)
+    open(os.path.join(d, "index.js"), "w").write(
+        "module.exports = { v4() { throw new Error(\"uuid is not available offline: pass interval ids\"); } };\n")
     for pkg in TYPE_ONLY:
         d = os.path.join(nm, pkg)
         os.makedirs(d, exist_ok=True)

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Golden interval-collection farm vectors from the REFERENCE itself
+(tests/golden/interval_vectors.json.gz).
+
+oracle/ref_interval_farm.js runs conflict farms of reference merge-tree Clients
+that also edit a SharedString interval collection -- the reference's own
+IntervalCollection (packages/dds/sequence/src/intervalCollection.ts, erased by
+oracle/ts_erase.py into the git- and gpurun-ignored oracle/_ref/ts/sequence)
+-- with local and remote interval adds, changes of one or both ends, property
+changes and deletes among merge-tree inserts, removes and annotates, every
+client catching up with the sequenced log at its own pace.  The file holds the
+messages, each client's event order and, at checkpoints, each client's text
+and intervals (id, start and end positions, properties).  Build container only.
+
+Usage: python3 tests/golden/make_interval_golden.py
+"""
+import gzip
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+
+import ref_util  # noqa: E402
+
+OUT = os.path.join(HERE, "interval_vectors.json.gz")
+FARM_JS = os.path.join(ROOT, "oracle", "ref_interval_farm.js")
+# (seed, clients incl. the observer, steps, initial text, checkpoints, text bound, interval-op chance)
+SETS = [(9000 + i, 2 + i % 5, 300 + 100 * (i % 4), ["", "hello world", "abc\ndef"][i % 3], 5, [64, 200][i % 2],
+         [0.2, 0.35, 0.5][i % 3]) for i in range(30)]
+
+
+def main():
+    if not ref_util.ref_available():
+        sys.exit("the reference sources are not in this container")
+    out = ref_util.build_ref()
+    res = {"sets": [], "generator": "oracle/ref_interval_farm.js (reference Client + IntervalCollection)"}
+    failed = []
+    for sd, c, n, t, k, m, iv in SETS:
+        one = {"seed": sd, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
+               "intervals": iv}
+        q = subprocess.run(["node", FARM_JS, out], input=json.dumps({"sets": [one]}), capture_output=True,
+                           text=True, timeout=600)
+        if q.returncode == 0:
+            res["sets"] += json.loads(q.stdout)["sets"]
+        else:
+            failed.append((sd, q.stderr.strip().splitlines()[-1:]))
+    res["seeds_the_reference_failed"] = failed
+    with gzip.open(OUT, "wt", encoding="utf-8") as fh:
+        json.dump(res, fh, separators=(",", ":"))
+    n_iv = sum(1 for s in res["sets"] for e in s["log"] if e[4] == "iv")
+    print(f"wrote {OUT}: {len(res['sets'])} farms, {n_iv} interval ops, failed {failed}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,149 @@
+"use strict";
+// Interval-collection farms (tests/golden/interval_vectors.json.gz, made by
+// tests/golden/make_interval_golden.py through oracle/ref_interval_farm.js)
+// replayed through the Node host: every client a BatchClient
+// ({localClient, refs}) with the label's IntervalCollection
+// (fluidframework_amd/node/intervals.js).  Each client replays its own events
+// in order: "L" a local merge-tree op, "I" a local interval op (re-made through
+// add / change / changeProperties / removeIntervalById; the op it emits must be
+// the one the reference sent), "A" a sequenced message (merge-tree ops through
+// applyMsg, interval ops through the collection's process).
+//   argv[2] "gpu":  on the engine; at every checkpoint each client's text and
+//                   intervals (id, start, end, properties) must equal the
+//                   reference client's.  Prints one JSON line.
+//   argv[2] "pack": no device (a recording addon): prints one JSON line per
+//                   checkpoint with the batch (base64) and, per client, its
+//                   intervals as [id, start slot, end slot, properties], for
+//                   tests/test_intervals.py to replay on the restatement.
+const fs = require("fs");
+const path = require("path");
+const zlib = require("zlib");
+const { MergeTreeEngine } = require("../../fluidframework_amd/node");
+
+const mode = process.argv[2] || "gpu";
+const sets = JSON.parse(zlib.gunzipSync(fs.readFileSync(path.join(__dirname, "..", "golden",
+  "interval_vectors.json.gz"))).toString("utf8")).sets;
+const nSets = process.argv[3] && process.argv[3] !== "all" ? Number(process.argv[3]) : sets.length;
+const LABEL = "farm";
+
+function sortKeys(v) {
+  if (v && typeof v === "object" && !Array.isArray(v)) {
+    const o = {};
+    for (const k of Object.keys(v).sort()) o[k] = sortKeys(v[k]);
+    return o;
+  }
+  return v;
+}
+const b64 = (a) => Buffer.from(a.buffer, a.byteOffset, a.byteLength).toString("base64");
+
+// pack mode: the N-API surface the engine uses, recording the submitted batches
+let lastBatch = null;
+const recorder = {
+  create() { return {}; }, destroy() {}, loadDocs() {}, loadSegments() {},
+  submit(ctx, offsets, ops, text, propsets, props) {
+    lastBatch = { offsets: b64(offsets), ops: b64(ops), text: b64(text), propsets: b64(propsets), props: b64(props) };
+  },
+  run() {}, sync() {}, readDeltas() { return new Uint32Array(0); },
+};
+
+const eng = new MergeTreeEngine(mode === "pack" ? { nKeys: 8, addon: recorder } : { nKeys: 8 });
+const layout = [];
+for (let si = 0; si < nSets; si++) {
+  sets[si].names.forEach((name, ci) => {
+    const L = { si, ci, sent: null };
+    L.client = eng.createClient(sets[si].initialText, { newLengthCalc: true, localClient: true, refs: true,
+      longClientId: name });
+    L.coll = L.client.getIntervalCollection(LABEL, { emit(opName, _p, value) { L.sent = { opName, value }; } });
+    layout.push(L);
+  });
+}
+eng.start();
+const prev = layout.map(() => 0);
+const failures = [];
+let passed = 0, opsChecked = 0;
+const clone = (v) => JSON.parse(JSON.stringify(v));
+const nCp = Math.max.apply(null, sets.slice(0, nSets).map((s) => s.checkpoints.length));
+for (let j = 0; j < nCp; j++) {
+  layout.forEach((L, d) => {
+    const s = sets[L.si];
+    if (j >= s.checkpoints.length) return;
+    const done = s.checkpoints[j].done[L.ci];
+    for (const [kind, li] of s.events[L.ci].slice(prev[d], done)) {
+      const m = s.log[li];
+      const msg = { clientId: m[0], sequenceNumber: m[1], referenceSequenceNumber: m[2], minimumSequenceNumber: m[3],
+        type: "op", contents: m[5] };
+      if (kind === "A") {
+        if (m[4] === "op") L.client.applyMsg(msg);
+        else L.coll.process(m[5].opName, clone(m[5].value), m[0] === s.names[L.ci], msg);
+        continue;
+      }
+      if (kind === "L") {
+        const o = m[5];
+        if (o.type === 0) L.client.insertSegmentLocal(o.pos1, o.seg);
+        else if (o.type === 1) L.client.removeRangeLocal(o.pos1, o.pos2);
+        else L.client.annotateRangeLocal(o.pos1, o.pos2, o.props);
+        continue;
+      }
+      // "I": the client's own interval op, re-made through the collection API
+      const { opName, value } = m[5];
+      const id = value.properties && value.properties.intervalId;
+      L.sent = null;
+      if (opName === "add") {
+        L.coll.add(value.start, value.end, value.intervalType, value.properties);
+      } else if (opName === "delete") {
+        L.coll.removeIntervalById(id);
+      } else if (value.start !== undefined || value.end !== undefined) {
+        L.coll.change(id, value.start, value.end);
+      } else {
+        const props = Object.assign({}, value.properties);
+        delete props.intervalId;
+        L.coll.changeProperties(id, props);
+      }
+      // the op the reference sent (a delete's positions are informational)
+      const want = clone(value), got = L.sent ? clone(L.sent.value) : null;
+      if (opName === "delete" && got) {
+        delete want.start;
+        delete want.end;
+      }
+      if (!L.sent || L.sent.opName !== opName || JSON.stringify(sortKeys(got)) !== JSON.stringify(sortKeys(want))) {
+        failures.push([L.si, L.ci, j, "op", L.sent, m[5]]);
+      }
+      opsChecked++;
+    }
+    prev[d] = done;
+  });
+  if (mode === "pack") {
+    eng.flush();
+    const states = layout.map((L) => {
+      if (j >= sets[L.si].checkpoints.length) return null;
+      const ivs = Array.from(L.coll.byId.values()).map((x) => [x.getIntervalId(), x.start.slot, x.end.slot,
+        sortKeys(x.properties)]);
+      ivs.sort((a, b) => (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0));
+      return { intervals: ivs, nRefs: L.client.clients.refNext };
+    });
+    process.stdout.write(JSON.stringify({ batch: lastBatch, states }) + "\n");
+    lastBatch = null;
+    continue;
+  }
+  layout.forEach((L) => {
+    const s = sets[L.si];
+    if (j >= s.checkpoints.length) return;
+    const want = s.checkpoints[j].states[L.ci];
+    const ivs = Array.from(L.coll.byId.values()).map((x) => {
+      const [a, b] = x.positions();
+      return [x.getIntervalId(), a, b, sortKeys(x.properties)];
+    });
+    ivs.sort((a, b) => (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0));
+    const text = L.client.getText();
+    if (text === want.text && JSON.stringify(ivs) === JSON.stringify(want.intervals)) passed++;
+    else failures.push([L.si, L.ci, j, "state", ivs.slice(0, 3), want.intervals.slice(0, 3)]);
+  });
+}
+if (mode !== "pack") {
+  process.stdout.write(JSON.stringify({ passed, opsChecked, failures: failures.slice(0, 4), nFailures: failures.length,
+    docs: layout.length }) + "\n");
+} else {
+  process.stdout.write(JSON.stringify({ done: true, opsChecked, failures: failures.slice(0, 4),
+    nFailures: failures.length }) + "\n");
+}
+eng.close();

@@ -1,0 +1,146 @@
+"""SharedString interval collections: IntervalCollection
+(packages/dds/sequence/src/intervalCollection.ts) in the Node host
+(fluidframework_amd/node/intervals.js) over the engine's local references
+(MTE_DOC_REFS): StayOnRemove ends for pending local adds / changes,
+SlideOnRemove ends created in a sequenced op's perspective and slid at once
+(MTE_OP_REF b = 2), the conversion at the ack (b = 3), pending changes per end,
+pending property keys.
+
+Pinned by 29 farms the reference itself ran with its own IntervalCollection
+(oracle/ref_interval_farm.js -> tests/golden/interval_vectors.json.gz, made by
+tests/golden/make_interval_golden.py): every interval op the host emits must be
+the op the reference sent, and at every checkpoint every client's text and
+intervals (id, start and end positions, properties) must equal the reference
+client's -- on the restatement (the host's batches replayed, test below), on the
+GPU through Python and through Node.
+"""
+import base64
+import gzip
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from fixtures_util import doc_inits
+from fluidframework_amd.abi import (DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC, DOC_REFS, OP_DTYPE, PROP_DTYPE,
+                                    PROPSET_DTYPE)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+VECTORS = os.path.join(HERE, "golden", "interval_vectors.json.gz")
+
+
+def interval_sets():
+    with gzip.open(VECTORS, "rt", encoding="utf-8") as fh:
+        return json.load(fh)["sets"]
+
+
+def node(*args, timeout=600):
+    r = subprocess.run(["node", *args], cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return r.stdout
+
+
+def _batch(b):
+    dec = lambda k: base64.b64decode(b[k])  # noqa: E731
+    return {"op_offsets": np.frombuffer(dec("offsets"), np.uint64).copy(),
+            "ops": np.frombuffer(dec("ops"), OP_DTYPE).copy(),
+            "text": np.frombuffer(dec("text"), np.uint16).copy(),
+            "propsets": np.frombuffer(dec("propsets"), PROPSET_DTYPE).copy(),
+            "props": np.frombuffer(dec("props"), PROP_DTYPE).copy()}
+
+
+def replay_packed(factory, sets, lines):
+    """The Node host's batches (tests/node/interval_farm.js pack) on an engine:
+    every client's text and intervals at every checkpoint against the reference."""
+    layout = [(si, ci) for si, s in enumerate(sets) for ci in range(len(s["names"]))]
+    inits, text = doc_inits([sets[si]["initialText"] for si, _ in layout],
+                            flags=DOC_NEW_LENGTH_CALC | DOC_LOCAL_CLIENT | DOC_REFS)
+    eng = factory(8)
+    eng.load_docs(inits, text)
+    passed, failures = 0, []
+    for j, line in enumerate(lines):
+        rec = json.loads(line)
+        if rec["batch"] is not None:
+            eng.apply_batch(_batch(rec["batch"]))
+        st = eng.statuses()
+        for d, (si, ci) in enumerate(layout):
+            have = rec["states"][d]
+            if have is None:
+                continue
+            want = sets[si]["checkpoints"][j]["states"][ci]
+            if st[d] != 0:
+                failures.append((si, ci, j, "status", int(st[d])))
+                continue
+            pos = eng.read_refs(d, have["nRefs"]) if have["nRefs"] else []
+            got = [[i, int(pos[a]), int(pos[b]), p] for i, a, b, p in have["intervals"]]
+            if eng.read_doc(d)["text"] != want["text"] or got != want["intervals"]:
+                failures.append((si, ci, j, "state", got[:3], want["intervals"][:3]))
+            else:
+                passed += 1
+    return passed, failures
+
+
+@pytest.fixture(scope="module")
+def packed():
+    out = node("tests/node/interval_farm.js", "pack").splitlines()
+    tail = json.loads(out[-1])
+    return out[:-1], tail
+
+
+def test_interval_vectors_shape():
+    sets = interval_sets()
+    assert len(sets) == 29
+    ops = [e[5]["opName"] for s in sets for e in s["log"] if e[4] == "iv"]
+    assert len(ops) > 4000 and {"add", "change", "delete"} <= set(ops)
+    ends = [x for s in sets for cp in s["checkpoints"] for st in cp["states"] for iv in st["intervals"]
+            for x in iv[1:3]]
+    assert ends.count(-1) > 0  # ends that slid off the string
+
+
+def test_host_emits_the_reference_interval_ops(packed):
+    _, tail = packed
+    assert tail["nFailures"] == 0, tail["failures"]
+    assert tail["opsChecked"] > 2000
+
+
+def test_oracle_interval_farms(packed):
+    from oracle import OracleEngine
+    sets = interval_sets()
+    passed, failures = replay_packed(lambda k: OracleEngine(k), sets, packed[0])
+    assert not failures, failures[:2]
+    assert passed == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
+
+
+def test_interval_farm_live():
+    """The committed vectors are what the erased reference computes now (build
+    container only)."""
+    import ref_util
+    if not ref_util.ref_available():
+        pytest.skip("reference sources not in this container")
+    keys = ("seed", "clients", "steps", "initialText", "nCheckpoints", "maxText", "intervals")
+    for s in interval_sets()[:3]:
+        p = subprocess.run(["node", os.path.join(ROOT, "oracle", "ref_interval_farm.js"), ref_util.build_ref()],
+                           input=json.dumps({"sets": [{k: s[k] for k in keys}]}), capture_output=True, text=True,
+                           timeout=600, check=True)
+        live = json.loads(p.stdout)["sets"][0]
+        assert live["log"] == s["log"] and live["checkpoints"] == s["checkpoints"]
+
+
+@pytest.mark.gpu
+def test_gpu_interval_farms(packed):
+    from fluidframework_amd.engine import DeviceEngine
+    sets = interval_sets()
+    passed, failures = replay_packed(lambda k: DeviceEngine(k), sets, packed[0])
+    assert not failures, failures[:2]
+    assert passed == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
+
+
+@pytest.mark.gpu
+def test_node_interval_farms_on_gpu():
+    j = json.loads(node("tests/node/interval_farm.js", "gpu").strip().splitlines()[-1])
+    assert j["nFailures"] == 0, j["failures"]
+    sets = interval_sets()
+    assert j["passed"] == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)

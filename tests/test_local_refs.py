@@ -25,7 +25,8 @@ import pytest
 
 from fixtures_util import doc_inits, replay_ref_farm
 from fluidframework_amd.abi import (DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC, DOC_REFS, MTE_E_INVALID_ARG,
-                                    MTE_E_UNSUPPORTED, REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE, MergeTreeError)
+                                    MTE_E_UNSUPPORTED, REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE, REF_TRANSIENT,
+                                    MergeTreeError)
 from fluidframework_amd.packing import BatchBuilder, DocClients, Interner
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -132,8 +133,11 @@ def test_packer_ref_rules():
     cl = DocClients("B", local=True)
     bb = BatchBuilder(1, Interner(4))
     with pytest.raises(MergeTreeError) as ei:
-        bb.add_ref(0, cl, 0, REF_STAY_ON_REMOVE)
+        bb.add_ref(0, cl, 0, REF_TRANSIENT)
     assert ei.value.code == MTE_E_UNSUPPORTED
+    with pytest.raises(MergeTreeError) as ei:
+        bb.add_ref(0, cl, 0, REF_STAY_ON_REMOVE | REF_SLIDE_ON_REMOVE)
+    assert ei.value.code == MTE_E_INVALID_ARG
     assert bb.add_ref(0, cl, 0) == 0 and bb.add_ref(0, cl, 1) == 1
     bb.remove_ref(0, cl, 0)
     assert bb.add_ref(0, cl, 2) == 0  # a removed slot is reused

@@ -377,3 +377,58 @@ def test_node_sequence_delta_events_on_gpu(i):
                 want.append((seq, seq - 1, ops[0] if len(ops) == 1 else {"type": 3, "ops": ops}))
             have = [(m["sequenceNumber"], m["referenceSequenceNumber"], m["contents"]) for m in got[d]["stash"]]
             assert have and have == want[len(want) - len(have):], (d, have[:2], want[len(want) - len(have):][:2])
+
+
+def test_sharded_host_packs_what_one_packer_packs(tmp_path):
+    """ShardedHost (fluidframework_amd/node/shards.js): 3 worker threads pack a
+    60-document config-3 stream in 3 flushes into shared batches; replayed on
+    the restatement, every document's text and per-position properties equal
+    one Python packer's batch of the same messages (the interned ids differ:
+    properties are compared decoded)."""
+    import base64
+    import sys
+    sys.path.insert(0, ROOT)
+    from bench import write_stream_dir
+    from fluidframework_amd import gen, messages
+    from fluidframework_amd.abi import OP_DTYPE, PROP_DTYPE, PROPSET_DTYPE
+    from fluidframework_amd.packing import BatchBuilder, DocClients, Interner
+    stream = gen.generate(3, n_docs=60, ops_per_doc=600)
+    write_stream_dir(stream, str(tmp_path), 60)
+    out = node("tests/node/shard_pack.js", str(tmp_path), "3", "3").splitlines()
+    tables = json.loads(out[-1])
+    sharded = OracleEngine(4)
+    gen.load_stream(sharded, stream)
+    for line in out[:-1]:
+        j = json.loads(line)
+        dec = lambda k: base64.b64decode(j[k])  # noqa: E731
+        sharded.apply_batch({"op_offsets": np.frombuffer(dec("offsets"), np.uint64).copy(),
+                             "ops": np.frombuffer(dec("ops"), OP_DTYPE).copy(),
+                             "text": np.frombuffer(dec("text"), np.uint16).copy(),
+                             "propsets": np.frombuffer(dec("propsets"), PROPSET_DTYPE).copy(),
+                             "props": np.frombuffer(dec("props"), PROP_DTYPE).copy()})
+    assert (sharded.statuses() == 0).all()
+    it = Interner(4)
+    bb = BatchBuilder(60, it)
+    docs = messages.stream_docs(stream, 0, 60, segs=False)
+    for d, doc in enumerate(docs):
+        cl = DocClients("A")
+        for m in doc["msgs"]:
+            bb.add_message(d, cl, as_msg(m))
+    one = OracleEngine(4)
+    gen.load_stream(one, stream)
+    one.apply_batch(bb.build())
+
+    def runs(v, keys, values):
+        out, pos = [], 0
+        for ln, _k, planes in v["segs"]:
+            p = {keys[k]: json.loads(values[x]) for k, x in enumerate(planes) if x}
+            out.append((pos, ln, json.dumps(p, sort_keys=True)))
+            pos += ln
+        flat = []
+        for pos, ln, p in out:
+            flat += [p] * ln
+        return flat
+    for d in range(60):
+        a, b = sharded.read_doc(d), one.read_doc(d)
+        assert a["text"] == b["text"], d
+        assert runs(a, tables["keys"], tables["values"]) == runs(b, it.key_names, it.value_json), d
