@@ -445,6 +445,11 @@ struct mte_ctx {
   uint64_t* d_comm = nullptr;  // digests of all ranks / scalar reductions
   uint64_t comm_cap = 0;       // uint64 elements
   uint32_t n_rs = 0;
+  // the largest property value id the context was given (load + every batch):
+  // below 256 pass 1 packs the 4 property planes into one (kPack4);
+  // MTE_PACK_PROPS=0 turns that off
+  uint32_t max_vid = 0;
+  bool pack_props = true;
   uint64_t* d_off = nullptr;
   mte_propset* d_ps = nullptr;
   mte_prop* d_pe = nullptr;
@@ -588,7 +593,16 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   }
   // pass 1: two documents per wavefront (docs up to 126 segments)
   const uint32_t b1 = (c->n_pairs + kPairsPerBlock - 1) / kPairsPerBlock;
-  if (b1) HIPCHK(c, (launch_pair<K, S>(a, b1, c->stream)));
+  // with 4 keys whose value ids all fit in a byte (every value the context was
+  // ever given), pass 1 holds the four planes as one packed register plane
+  if (b1) {
+    if constexpr (K == 4) {
+      if (c->max_vid < 256 && c->pack_props) HIPCHK(c, (launch_pair<kPack4, S>(a, b1, c->stream)));
+      else HIPCHK(c, (launch_pair<K, S>(a, b1, c->stream)));
+    } else {
+      HIPCHK(c, (launch_pair<K, S>(a, b1, c->stream)));
+    }
+  }
   // pass 2: docs that outgrew pass 1 continue one per wavefront (up to 1022 segments)
   const uint32_t b2 = (c->n_docs + kDocsPerBlock - 1) / kDocsPerBlock;
   HIPCHK(c, (launch_big<K, S>(a, b2, c->stream)));
@@ -758,6 +772,7 @@ int mte_create(const mte_config* cfg, mte_ctx** out) {
   c->kt = cfg->n_keys == 0 ? 0 : (cfg->n_keys <= 4 ? 4 : 8);
   c->cap = cfg->seg_capacity ? cfg->seg_capacity : 1024;
   c->wclock_path = std::getenv("MTE_WAVE_CLOCK");
+  if (const char* pp = std::getenv("MTE_PACK_PROPS")) c->pack_props = std::atoi(pp) != 0;
   if (const char* r = std::getenv("MTE_TREE_ROUNDS")) {
     const int v = std::atoi(r);
     c->tree_rounds = v < 0 ? 0 : (v > 64 ? 64 : v);
@@ -846,6 +861,8 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
   free_docs(c);
   c->n_docs = n_docs;
   c->submitted = false;
+  c->max_vid = 0;
+  for (uint32_t i = 0; props && i < n_props; i++) c->max_vid = std::max(c->max_vid, props[i].value);
   c->ev_slot = -1;
   c->n_ops = 0;
   const uint64_t nslots = (uint64_t)(n_docs ? n_docs : 1) * c->cap;
@@ -1135,6 +1152,7 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
       off.clear();
     }
   }
+  for (uint32_t i = 0; b->props && i < b->n_props; i++) c->max_vid = std::max(c->max_vid, b->props[i].value);
   c->n_ops_s[w] = b->n_ops;
   c->n_propsets_s[w] = b->n_propsets;
   uint64_t mx = 0;

@@ -198,11 +198,23 @@ __device__ __forceinline__ void pull_shift(T (&F)[E], int t1, int t2) {
 
 // ---- register-resident document --------------------------------------------
 
+// Property planes in registers.  K = kPack4: four keys whose value ids all fit
+// in 8 bits held as the bytes of ONE register plane (pass 1 when the context's
+// values allow it): shifts, inserts and compactions move one plane instead of
+// four; HBM keeps the four planes (load_regs / store_regs pack and unpack).
+constexpr int kPack4 = -4;
+template <int K>
+constexpr int kRegPlanes = K == kPack4 ? 1 : K;  // register planes
+template <int K>
+constexpr int kRP = kRegPlanes<K> > 0 ? kRegPlanes<K> : 1;  // array extent
+template <int K>
+constexpr int kKeys = K == kPack4 ? 4 : K;  // keys (HBM planes)
+
 template <int E, int K>
 struct Regs {
   int32_t len[E], seq[E], rseq[E];
   uint32_t rmask[E], meta[E], toff[E];
-  uint32_t pr[K > 0 ? K : 1][E];
+  uint32_t pr[kRP<K>][E];
 };
 
 // Perspective length of every slot (mergeTree.ts:1003-1026 new calc,

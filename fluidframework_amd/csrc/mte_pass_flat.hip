@@ -33,5 +33,8 @@ hipError_t launch_stream(const ReplayArgs& a, uint32_t blocks, hipStream_t s) {
   template hipError_t launch_stream<K, S>(const ReplayArgs&, uint32_t, hipStream_t);
 MTE_INST(0, false) MTE_INST(0, true) MTE_INST(4, false) MTE_INST(4, true) MTE_INST(8, false) MTE_INST(8, true)
 #undef MTE_INST
+// pass 1 with the four property planes packed into one register (kPack4)
+template hipError_t launch_pair<kPack4, false>(const ReplayArgs&, uint32_t, hipStream_t);
+template hipError_t launch_pair<kPack4, true>(const ReplayArgs&, uint32_t, hipStream_t);
 
 }  // namespace mte

@@ -132,8 +132,15 @@ __device__ __forceinline__ void set_one_plane(uint32_t (&p)[E], const bool (&sel
 }
 
 template <int E, int K>
-__device__ __forceinline__ void set_plane(uint32_t (&pr)[K > 0 ? K : 1][E], const bool (&sel)[E], uint32_t key,
+__device__ __forceinline__ void set_plane(uint32_t (&pr)[kRP<K>][E], const bool (&sel)[E], uint32_t key,
                                           uint32_t val) {
+  if constexpr (K == kPack4) {
+    // byte `key` of the packed plane (key < 4 and val < 256: the host's choice)
+    const uint32_t sh = key * 8u, keep = ~(0xffu << sh), v = val << sh;
+#pragma unroll
+    for (int jj = 0; jj < E; jj++) pr[0][jj] = sel[jj] ? ((pr[0][jj] & keep) | v) : pr[0][jj];
+    return;
+  }
 #if MTE_SET_PLANE_SWITCH
   // `key` is wave-uniform: one scalar branch picks the plane, so only that
   // plane's E selects issue (the branch-free form costs K x E selects)
@@ -161,7 +168,7 @@ __device__ __forceinline__ void set_plane(uint32_t (&pr)[K > 0 ? K : 1][E], cons
 }
 
 template <int E, int K>
-__device__ __forceinline__ void apply_props(uint32_t (&pr)[K > 0 ? K : 1][E], const bool (&sel)[E], uint32_t pk,
+__device__ __forceinline__ void apply_props(uint32_t (&pr)[kRP<K>][E], const bool (&sel)[E], uint32_t pk,
                                             uint32_t v0, uint32_t v1, uint32_t psi, const ReplayArgs& a) {
   const uint32_t k0 = pk & 0xffu, k1 = (pk >> 8) & 0xffu;
   if (k0 != kNoKey) set_plane<E, K>(pr, sel, k0, v0);
@@ -232,14 +239,14 @@ __device__ __forceinline__ void shift_all(Regs<E, K>& R, int32_t (&L)[E], int32_
     shift_perm<E>(R.meta, addr);
     shift_perm<E>(R.toff, addr);
 #pragma unroll
-    for (int k = 0; k < K; k++) shift_perm<E>(R.pr[k], addr);
+    for (int k = 0; k < kRegPlanes<K>; k++) shift_perm<E>(R.pr[k], addr);
     if constexpr (LP) {
       shift_perm<E>(L, addr);
       shift_perm<E>(P, addr);
     }
     return;
   }
-  constexpr int NF = kFieldPlanes + K + (LP ? 2 : 0);
+  constexpr int NF = kFieldPlanes + kRegPlanes<K> + (LP ? 2 : 0);
   uint32_t last[NF], last2[NF];
   shift_grab<E, NF>(last, last2, 0, R.len);
   shift_grab<E, NF>(last, last2, 1, R.seq);
@@ -248,7 +255,7 @@ __device__ __forceinline__ void shift_all(Regs<E, K>& R, int32_t (&L)[E], int32_
   shift_grab<E, NF>(last, last2, 4, R.meta);
   shift_grab<E, NF>(last, last2, 5, R.toff);
 #pragma unroll
-  for (int k = 0; k < K; k++) shift_grab<E, NF>(last, last2, kFieldPlanes + k, R.pr[k]);
+  for (int k = 0; k < kRegPlanes<K>; k++) shift_grab<E, NF>(last, last2, kFieldPlanes + k, R.pr[k]);
   if constexpr (LP) {
     shift_grab<E, NF>(last, last2, NF - 2, L);
     shift_grab<E, NF>(last, last2, NF - 1, P);
@@ -272,7 +279,7 @@ __device__ __forceinline__ void shift_all(Regs<E, K>& R, int32_t (&L)[E], int32_
   shift_apply<E, NF>(R.meta, p1, p2, 4, g1, g2);
   shift_apply<E, NF>(R.toff, p1, p2, 5, g1, g2);
 #pragma unroll
-  for (int k = 0; k < K; k++) shift_apply<E, NF>(R.pr[k], p1, p2, kFieldPlanes + k, g1, g2);
+  for (int k = 0; k < kRegPlanes<K>; k++) shift_apply<E, NF>(R.pr[k], p1, p2, kFieldPlanes + k, g1, g2);
   if constexpr (LP) {
     shift_apply<E, NF>(L, p1, p2, NF - 2, g1, g2);
     shift_apply<E, NF>(P, p1, p2, NF - 1, g1, g2);
@@ -295,8 +302,15 @@ __device__ __forceinline__ void load_regs(Regs<E, K>& R, const DocRun& D, const 
     R.rmask[j] = v ? pl[3 * st + x] : 0u;
     R.meta[j] = v ? pl[4 * st + x] : 0u;
     R.toff[j] = v ? pl[5 * st + x] : 0u;
+    if constexpr (K == kPack4) {
+      uint32_t w = 0;
 #pragma unroll
-    for (int k = 0; k < K; k++) R.pr[k][j] = v ? pl[(kFieldPlanes + k) * st + x] : 0u;
+      for (int k = 0; k < 4; k++) w |= (v ? pl[(kFieldPlanes + k) * st + x] : 0u) << (8 * k);
+      R.pr[0][j] = w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < K; k++) R.pr[k][j] = v ? pl[(kFieldPlanes + k) * st + x] : 0u;
+    }
   }
 }
 
@@ -316,8 +330,13 @@ __device__ __forceinline__ void store_regs(const Regs<E, K>& R, const DocRun& D,
       pl[3 * st + x] = R.rmask[j];
       pl[4 * st + x] = R.meta[j];
       pl[5 * st + x] = R.toff[j];
+      if constexpr (K == kPack4) {
 #pragma unroll
-      for (int k = 0; k < K; k++) pl[(kFieldPlanes + k) * st + x] = R.pr[k][j];
+        for (int k = 0; k < 4; k++) pl[(kFieldPlanes + k) * st + x] = (R.pr[0][j] >> (8 * k)) & 0xffu;
+      } else {
+#pragma unroll
+        for (int k = 0; k < K; k++) pl[(kFieldPlanes + k) * st + x] = R.pr[k][j];
+      }
     }
   }
 }
@@ -511,10 +530,10 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
       const uint32_t meta = (c + 1u) | (marker ? (1u + (uint32_t)pos2) << 8 : 0u);
       const uint32_t toff = marker ? 0u : a.text_base + (uint32_t)op[6];
       const uint32_t psi = (uint32_t)op[7];
-      uint32_t pr[K > 0 ? K : 1][1];
+      uint32_t pr[kRP<K>][1];
       const bool one[1] = {true};
 #pragma unroll
-      for (int kk = 0; kk < (K > 0 ? K : 1); kk++) pr[kk][0] = 0;
+      for (int kk = 0; kk < kRP<K>; kk++) pr[kk][0] = 0;
       if (K > 0 && psi != MTE_NO_PROPS) {
         const s8v q2 = sload_props(a, psi);
         apply_props<1, K>(pr, one, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], psi, a);
@@ -532,7 +551,7 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
         R.meta[jj] = at ? meta : R.meta[jj];
         R.toff[jj] = at ? toff : R.toff[jj];
 #pragma unroll
-        for (int kk = 0; kk < K; kk++) R.pr[kk][jj] = at ? pr[kk][0] : R.pr[kk][jj];
+        for (int kk = 0; kk < kRegPlanes<K>; kk++) R.pr[kk][jj] = at ? pr[kk][0] : R.pr[kk][jj];
       }
     }
     if (!ins && pos2 != pos1) {
@@ -561,7 +580,7 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
         const s8v q2 = sload_props(a, psi);
         if (flags & MTE_F_REWRITE) {
 #pragma unroll
-          for (int kk = 0; kk < K; kk++)
+          for (int kk = 0; kk < kRegPlanes<K>; kk++)
 #pragma unroll
             for (int jj = 0; jj < E; jj++) R.pr[kk][jj] = in[jj] ? 0u : R.pr[kk][jj];
         }
@@ -612,7 +631,7 @@ __device__ __forceinline__ int doc_step(Regs<E, K>& R, DocRun& D, uint32_t (&st)
         compact_plane<E>(R.meta, keep, dst, zlds);
         compact_plane<E>(R.toff, keep, dst, zlds);
 #pragma unroll
-        for (int kk = 0; kk < K; kk++) compact_plane<E>(R.pr[kk], keep, dst, zlds);
+        for (int kk = 0; kk < kRegPlanes<K>; kk++) compact_plane<E>(R.pr[kk], keep, dst, zlds);
 #pragma unroll
         for (int jj = 0; jj < E; jj++) {
           const bool pad = base + jj >= n_new;

@@ -107,7 +107,7 @@ __device__ __forceinline__ void shift_v(Regs<E, K>& R, int32_t (&X)[NX > 0 ? NX 
     shift1_dpp(R.meta, g1[0], g2[0]);
     shift1_dpp(R.toff, g1[0], g2[0]);
 #pragma unroll
-    for (int k = 0; k < K; k++) shift1_dpp(R.pr[k], g1[0], g2[0]);
+    for (int k = 0; k < kRegPlanes<K>; k++) shift1_dpp(R.pr[k], g1[0], g2[0]);
 #pragma unroll
     for (int x = 0; x < NX; x++) shift1_dpp(X[x], g1[0], g2[0]);
   } else if constexpr (E == 1) {
@@ -119,7 +119,7 @@ __device__ __forceinline__ void shift_v(Regs<E, K>& R, int32_t (&X)[NX > 0 ? NX 
     perm_plane<E>(R.meta, addr);
     perm_plane<E>(R.toff, addr);
 #pragma unroll
-    for (int k = 0; k < K; k++) perm_plane<E>(R.pr[k], addr);
+    for (int k = 0; k < kRegPlanes<K>; k++) perm_plane<E>(R.pr[k], addr);
 #pragma unroll
     for (int x = 0; x < NX; x++) perm_plane<E>(X[x], addr);
   } else if constexpr (E >= MTE_SHIFT_SEQ_EMIN) {
@@ -130,11 +130,11 @@ __device__ __forceinline__ void shift_v(Regs<E, K>& R, int32_t (&X)[NX > 0 ? NX 
     shift_plane<E>(R.meta, g1, g2);
     shift_plane<E>(R.toff, g1, g2);
 #pragma unroll
-    for (int k = 0; k < K; k++) shift_plane<E>(R.pr[k], g1, g2);
+    for (int k = 0; k < kRegPlanes<K>; k++) shift_plane<E>(R.pr[k], g1, g2);
 #pragma unroll
     for (int x = 0; x < NX; x++) shift_plane<E>(X[x], g1, g2);
   } else {
-    constexpr int NF = kFieldPlanes + K + NX;
+    constexpr int NF = kFieldPlanes + kRegPlanes<K> + NX;
     uint32_t last[NF], last2[NF];
     shift_grab<E, NF>(last, last2, 0, R.len);
     shift_grab<E, NF>(last, last2, 1, R.seq);
@@ -143,9 +143,9 @@ __device__ __forceinline__ void shift_v(Regs<E, K>& R, int32_t (&X)[NX > 0 ? NX 
     shift_grab<E, NF>(last, last2, 4, R.meta);
     shift_grab<E, NF>(last, last2, 5, R.toff);
 #pragma unroll
-    for (int k = 0; k < K; k++) shift_grab<E, NF>(last, last2, kFieldPlanes + k, R.pr[k]);
+    for (int k = 0; k < kRegPlanes<K>; k++) shift_grab<E, NF>(last, last2, kFieldPlanes + k, R.pr[k]);
 #pragma unroll
-    for (int x = 0; x < NX; x++) shift_grab<E, NF>(last, last2, kFieldPlanes + K + x, X[x]);
+    for (int x = 0; x < NX; x++) shift_grab<E, NF>(last, last2, kFieldPlanes + kRegPlanes<K> + x, X[x]);
     uint32_t p1[NF], p2[NF];
 #pragma unroll
     for (int f = 0; f < NF; f++) p1[f] = (uint32_t)lane_prev((int32_t)last[f]);
@@ -158,9 +158,9 @@ __device__ __forceinline__ void shift_v(Regs<E, K>& R, int32_t (&X)[NX > 0 ? NX 
     shift_apply<E, NF>(R.meta, p1, p2, 4, g1, g2);
     shift_apply<E, NF>(R.toff, p1, p2, 5, g1, g2);
 #pragma unroll
-    for (int k = 0; k < K; k++) shift_apply<E, NF>(R.pr[k], p1, p2, kFieldPlanes + k, g1, g2);
+    for (int k = 0; k < kRegPlanes<K>; k++) shift_apply<E, NF>(R.pr[k], p1, p2, kFieldPlanes + k, g1, g2);
 #pragma unroll
-    for (int x = 0; x < NX; x++) shift_apply<E, NF>(X[x], p1, p2, kFieldPlanes + K + x, g1, g2);
+    for (int x = 0; x < NX; x++) shift_apply<E, NF>(X[x], p1, p2, kFieldPlanes + kRegPlanes<K> + x, g1, g2);
   }
 }
 
@@ -175,11 +175,11 @@ __device__ __forceinline__ void put_new_v(Regs<E, K>& R, const bool (&at)[E], co
   const uint32_t meta = (c + 1u) | (marker ? (1u + (uint32_t)pos2) << 8 : 0u);
   const uint32_t toff = marker ? 0u : a.text_base + (uint32_t)op[6];
   const uint32_t psi = (uint32_t)op[7];
-  uint32_t pr[K > 0 ? K : 1][1];
+  uint32_t pr[kRP<K>][1];
   const bool one[1] = {true};
 #pragma unroll
-  for (int kk = 0; kk < (K > 0 ? K : 1); kk++) pr[kk][0] = 0;
-  if (K > 0 && psi != MTE_NO_PROPS) {
+  for (int kk = 0; kk < kRP<K>; kk++) pr[kk][0] = 0;
+  if (kKeys<K> > 0 && psi != MTE_NO_PROPS) {
     const s8v q2 = sload_props(a, psi);
     apply_props<1, K>(pr, one, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], psi, a);
     MTE_STAT(st[kStPwrites] += (uint32_t)q2[3];)
@@ -194,7 +194,7 @@ __device__ __forceinline__ void put_new_v(Regs<E, K>& R, const bool (&at)[E], co
     R.meta[j] = at[j] ? meta : R.meta[j];
     R.toff[j] = at[j] ? toff : R.toff[j];
 #pragma unroll
-    for (int kk = 0; kk < K; kk++) R.pr[kk][j] = at[j] ? pr[kk][0] : R.pr[kk][j];
+    for (int kk = 0; kk < kRegPlanes<K>; kk++) R.pr[kk][j] = at[j] ? pr[kk][0] : R.pr[kk][j];
   }
 }
 
@@ -381,7 +381,7 @@ __device__ __forceinline__ int seg_op_v(Regs<E, K>& R, int& n, const s8v& op, ui
         const s8v q2 = sload_props(a, psi);
         if (flags & MTE_F_REWRITE) {
 #pragma unroll
-          for (int kk = 0; kk < K; kk++)
+          for (int kk = 0; kk < kRegPlanes<K>; kk++)
 #pragma unroll
             for (int j = 0; j < E; j++) R.pr[kk][j] = in[j] ? 0u : R.pr[kk][j];
         }
@@ -468,7 +468,7 @@ __device__ __forceinline__ int doc_step_v(Regs<E, K>& R, DocRun& D, uint32_t (&s
           R.meta[0] = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int32_t)R.meta[0]);
           R.toff[0] = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int32_t)R.toff[0]);
 #pragma unroll
-          for (int kk = 0; kk < K; kk++)
+          for (int kk = 0; kk < kRegPlanes<K>; kk++)
             R.pr[kk][0] = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int32_t)R.pr[kk][0]);
           const bool pad = l >= n_new;
           R.rseq[0] = pad ? kPad : R.rseq[0];
@@ -501,7 +501,7 @@ __device__ __forceinline__ int doc_step_v(Regs<E, K>& R, DocRun& D, uint32_t (&s
           compact_plane<E>(R.meta, keep, dst, zlds);
           compact_plane<E>(R.toff, keep, dst, zlds);
 #pragma unroll
-          for (int kk = 0; kk < K; kk++) compact_plane<E>(R.pr[kk], keep, dst, zlds);
+          for (int kk = 0; kk < kRegPlanes<K>; kk++) compact_plane<E>(R.pr[kk], keep, dst, zlds);
 #pragma unroll
           for (int jj = 0; jj < E; jj++) {
             const bool pad = base + jj >= n_new;

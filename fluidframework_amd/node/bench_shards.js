@@ -5,7 +5,7 @@
 // from the generated stream in data.dir by stream_source.js before the clock,
 // as a server holds them from its delta streams — into one shared batch; the
 // host submits and replays it (mte_submit + mte_run over N-API), in `parts`
-// slices so that packing slice i + 1 overlaps the replay of slice i.
+// slices so that packing slice i + 1 overlaps the submit and replay of slice i.
 // argv: dir workers parts [recorder] ("recorder": no device, the N-API calls
 // recorded — a CPU run of the packing alone).  Prints one JSON line.
 "use strict";
@@ -30,8 +30,9 @@ async function main() {
   const tl1 = process.hrtime.bigint();
   const maxLen = inits.reduce((a, d) => Math.max(a, d.nMsgs), 0);
   const t0 = process.hrtime.bigint();
-  let nrec = 0;
-  for (let p = 1; p <= parts; p++) nrec += await host.flush(Math.floor((maxLen * p) / parts));
+  const uptos = [];
+  for (let p = 1; p <= parts; p++) uptos.push(Math.floor((maxLen * p) / parts));
+  const nrec = await host.flushParts(uptos);
   eng.sync();
   const t1 = process.hrtime.bigint();
   const ms = Number(t1 - t0) / 1e6;

@@ -10,7 +10,7 @@
 //                   text / propset offsets moved by the bases and the keys /
 //                   values renamed to the engine's ids
 const { parentPort, workerData } = require("worker_threads");
-const { BatchBuilder, DocClients, Interner, OP_INSERT, OP_ANNOTATE, NO_PROPS } = require("./packing");
+const { BatchBuilder, DocClients, Interner } = require("./packing");
 
 const { d0, d1, observers, minSeq, nKeys } = workerData;
 const n = d1 - d0;
@@ -59,32 +59,24 @@ function pack(upto) {
 
 function emit(base, map, sab) {
   const t0 = process.hrtime.bigint();
-  const b = bb.build();  // records sorted by document
-  const out = new Int32Array(sab.ops, base.rec * 32, b.ops.length / 4);
-  out.set(new Int32Array(b.ops.buffer, b.ops.byteOffset, b.ops.length / 4));
-  // text offsets (inserts: a) and propset indices (insert b, annotate a) move by the bases
-  for (let k = 0; k < out.length; k += 8) {
-    const t = out[k + 3] & 0xff;
-    if (t === OP_INSERT) {
-      out[k + 6] += base.text;
-      if ((out[k + 7] >>> 0) !== NO_PROPS) out[k + 7] += base.ps;
-    } else if (t === OP_ANNOTATE) {
-      out[k + 6] += base.ps;
-    }
-  }
-  new Uint16Array(sab.text, base.text * 2, b.text.length).set(b.text);
-  const ps = new Uint32Array(sab.propsets, base.ps * 8, b.propsets.length);
+  // records sorted by document, text / propset offsets moved by the bases
+  const out = new Int32Array(sab.ops, base.rec * 32, bb.count * 8);
+  const rel = bb.buildInto(out, base.text, base.ps);
+  new Uint16Array(sab.text, base.text * 2, bb.textUnits).set(bb.textBuf.subarray(0, bb.textUnits));
+  const sets = bb.props.sets, ents = bb.props.entries;
+  const ps = new Uint32Array(sab.propsets, base.ps * 8, sets.length);
   for (let i = 0; i < ps.length; i += 2) {
-    ps[i] = b.propsets[i] + base.pe;
-    ps[i + 1] = b.propsets[i + 1];
+    ps[i] = sets[i] + base.pe;
+    ps[i + 1] = sets[i + 1];
   }
-  const pe = new Uint32Array(sab.props, base.pe * 8, b.props.length);
+  // keys / values renamed to the engine's ids
+  const pe = new Uint32Array(sab.props, base.pe * 8, ents.length);
   for (let i = 0; i < pe.length; i += 2) {
-    pe[i] = map.keys[b.props[i]];
-    pe[i + 1] = map.values[b.props[i + 1]];
+    pe[i] = map.keys[ents[i]];
+    pe[i + 1] = map.values[ents[i + 1]];
   }
   const offs = new BigUint64Array(sab.offsets);
-  for (let d = 0; d < n; d++) offs[d0 + d] = BigInt(base.rec) + b.offsets[d];
+  for (let d = 0; d < n; d++) offs[d0 + d] = BigInt(base.rec + rel[d]);
   bb = null;
   return { ok: true, ms: Number(process.hrtime.bigint() - t0) / 1e6 };
 }

@@ -760,6 +760,44 @@ class BatchBuilder {
       props: new Uint32Array(this.props.entries),
     };
   }
+
+  /** build() straight into a shared batch: the records sorted by document into
+   *  `out` (an Int32Array of count * 8), their text offsets (insert a) moved by
+   *  textBase and their propset indices (insert b, annotate a) by psBase.
+   *  Returns the per-document record offsets relative to `out`. */
+  buildInto(out, textBase, psBase) {
+    const nd = this.nDocs, n = this.count;
+    const offsets = new Uint32Array(nd + 1);
+    const cur = new Uint32Array(nd);
+    let acc = 0;
+    for (let d = 0; d < nd; d++) {
+      offsets[d] = acc;
+      cur[d] = acc;
+      acc += this.docCount[d];
+    }
+    offsets[nd] = acc;
+    const R = this.rec, D = this.recDoc;
+    for (let k = 0; k < n; k++) {
+      const o = cur[D[k]]++ * 8, w = k * 8;
+      const w3 = R[w + 3], t = w3 & 0xff;
+      let a = R[w + 6], b = R[w + 7];
+      if (t === OP_INSERT) {
+        a += textBase;
+        if ((b >>> 0) !== NO_PROPS) b += psBase;
+      } else if (t === OP_ANNOTATE) {
+        a += psBase;
+      }
+      out[o] = R[w];
+      out[o + 1] = R[w + 1];
+      out[o + 2] = R[w + 2];
+      out[o + 3] = w3;
+      out[o + 4] = R[w + 4];
+      out[o + 5] = R[w + 5];
+      out[o + 6] = a;
+      out[o + 7] = b;
+    }
+    return offsets;
+  }
 }
 
 /** mte_doc_init records + load text for documents created before start(). */

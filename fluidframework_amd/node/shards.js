@@ -59,13 +59,62 @@ class ShardedHost {
    *  the workers write the batch into shared memory, then submit + run it.
    *  Returns the number of records. */
   async flush(upto) {
+    return this.flushParts([upto]);
+  }
+
+  /** flush(uptos[0]), flush(uptos[1]), ... pipelined: the workers pack part
+   *  i + 1 while the host thread submits part i (mte_submit's upload runs on
+   *  the host thread, the packing on the workers) and the device replays it.
+   *  Returns the number of records of all parts. */
+  async flushParts(uptos) {
     const eng = this.engine;
-    eng.sync();  // the previous replay may still read the other batch slot
-    const tp = process.hrtime.bigint();
-    const parts = await Promise.all(this.workers.map((_, w) => this._call(w, { cmd: "pack", upto })));
-    const tm = process.hrtime.bigint();
-    // the engine's interner is the single id space (its read-outs decode with it)
-    const it = eng.interner;
+    const t = this.timing || (this.timing = { pack_ms: 0, pack_max_worker_ms: 0, merge_ms: 0, emit_ms: 0, submit_ms: 0 });
+    const packAll = (upto) => Promise.all(this.workers.map((_, w) => this._call(w, { cmd: "pack", upto })));
+    let total = 0;
+    let tp = process.hrtime.bigint();
+    let next = packAll(uptos[0]);
+    for (let i = 0; i < uptos.length; i++) {
+      const parts = await next;
+      const tm = process.hrtime.bigint();
+      t.pack_ms += Number(tm - tp) / 1e6;
+      t.pack_max_worker_ms += Math.max(...parts.map((p) => p.ms));
+      const { maps, bases, nrec, ntext, nps, npe } = this._merge(parts);
+      const nDocs = eng.docs.length;
+      const sab = {
+        ops: new SharedArrayBuffer(Math.max(1, nrec) * OP_BYTES),
+        text: new SharedArrayBuffer(Math.max(1, ntext) * 2),
+        propsets: new SharedArrayBuffer(Math.max(1, nps) * 8),
+        props: new SharedArrayBuffer(Math.max(1, npe) * 8),
+        offsets: new SharedArrayBuffer((nDocs + 1) * 8),
+      };
+      const te = process.hrtime.bigint();
+      await Promise.all(this.workers.map((_, w) => this._call(w, { cmd: "emit", base: bases[w], map: maps[w], sab })));
+      const ts = process.hrtime.bigint();
+      // the workers go on with the next part while this thread submits
+      tp = ts;
+      if (i + 1 < uptos.length) next = packAll(uptos[i + 1]);
+      new BigUint64Array(sab.offsets)[nDocs] = BigInt(nrec);
+      eng.sync();  // the previous replay may still read the other batch slot
+      eng.views.fill(null);
+      eng.refViews.fill(null);
+      eng.addon.submit(eng.ctx, new BigUint64Array(sab.offsets), new Uint8Array(sab.ops, 0, nrec * OP_BYTES),
+        new Uint16Array(sab.text, 0, ntext), new Uint32Array(sab.propsets, 0, 2 * nps),
+        new Uint32Array(sab.props, 0, 2 * npe));
+      eng.addon.run(eng.ctx);
+      eng.running = true;
+      t.merge_ms += Number(te - tm) / 1e6;
+      t.emit_ms += Number(ts - te) / 1e6;
+      t.submit_ms += Number(process.hrtime.bigint() - ts) / 1e6;
+      total += nrec;
+    }
+    return total;
+  }
+
+  // the shards' keys / values interned since the last part -> the engine's
+  // interner (the single id space its read-outs decode with); each shard's
+  // base in the shared batch
+  _merge(parts) {
+    const it = this.engine.interner;
     if (!this.maps) this.maps = this.workers.map(() => ({ keys: [], values: [0] }));
     const maps = parts.map((p, w) => {
       const m = this.maps[w];  // a shard's key / value ids -> the engine's
@@ -82,32 +131,7 @@ class ShardedHost {
       npe += p.npe;
       return b;
     });
-    const nDocs = eng.docs.length;
-    const sab = {
-      ops: new SharedArrayBuffer(Math.max(1, nrec) * OP_BYTES),
-      text: new SharedArrayBuffer(Math.max(1, ntext) * 2),
-      propsets: new SharedArrayBuffer(Math.max(1, nps) * 8),
-      props: new SharedArrayBuffer(Math.max(1, npe) * 8),
-      offsets: new SharedArrayBuffer((nDocs + 1) * 8),
-    };
-    const te = process.hrtime.bigint();
-    const emits = await Promise.all(this.workers.map((_, w) => this._call(w, { cmd: "emit", base: bases[w], map: maps[w],
-      sab })));
-    const ts = process.hrtime.bigint();
-    new BigUint64Array(sab.offsets)[nDocs] = BigInt(nrec);
-    eng.views.fill(null);
-    eng.refViews.fill(null);
-    eng.addon.submit(eng.ctx, new BigUint64Array(sab.offsets), new Uint8Array(sab.ops, 0, nrec * OP_BYTES),
-      new Uint16Array(sab.text, 0, ntext), new Uint32Array(sab.propsets, 0, 2 * nps), new Uint32Array(sab.props, 0, 2 * npe));
-    eng.addon.run(eng.ctx);
-    eng.running = true;
-    const t = this.timing || (this.timing = { pack_ms: 0, pack_max_worker_ms: 0, merge_ms: 0, emit_ms: 0, submit_ms: 0 });
-    t.pack_ms += Number(tm - tp) / 1e6;
-    t.pack_max_worker_ms += Math.max(...parts.map((p) => p.ms));
-    t.merge_ms += Number(te - tm) / 1e6;
-    t.emit_ms += Number(ts - te) / 1e6;
-    t.submit_ms += Number(process.hrtime.bigint() - ts) / 1e6;
-    return nrec;
+    return { maps, bases, nrec, ntext, nps, npe };
   }
 
   async close() {

@@ -125,16 +125,23 @@ extern "C" {
 /* Local references (LocalReferenceCollection, localReference.ts:139-567) in an
  * MTE_DOC_REFS document: a local record (MTE_F_LOCAL, seq 0: it takes no
  * localSeq and moves no window) with pos2 = the reference's slot (0 ..
- * mte_set_ref_capacity - 1, assigned by the host) and b = 0 to create, 1 to
- * remove it.
- *   create: Client.createLocalReferencePosition(segment, offset, refType)
+ * mte_set_ref_capacity - 1, assigned by the host) and b one of:
+ *   0 create: Client.createLocalReferencePosition(segment, offset, refType)
  *     (client.ts:360-364, mergeTree.ts:2124-2143) on the segment and offset
  *     that getContainingSegment(pos1) finds in the local view
- *     (mergeTree.ts:872-885); a = the ReferenceType flags (ops.ts): Simple (0)
- *     or SlideOnRemove (0x40) plus any of the label bits; StayOnRemove and
- *     Transient are MTE_E_UNSUPPORTED; pos1 outside the local view
- *     MTE_E_INVALID_ARG.
- *   remove: removeLocalReferencePosition (mergeTree.ts:2113-2123).
+ *     (mergeTree.ts:872-885); a = the ReferenceType flags (ops.ts): Simple (0),
+ *     SlideOnRemove (0x40) or StayOnRemove (0x80), plus any of the label bits;
+ *     SlideOnRemove with StayOnRemove is MTE_E_INVALID_ARG, Transient
+ *     MTE_E_UNSUPPORTED; pos1 outside the local view MTE_E_INVALID_ARG.
+ *   1 remove: removeLocalReferencePosition (mergeTree.ts:2113-2123).
+ *   2 create in a sequenced op's perspective (the interval collection's
+ *     remote add / change, intervalCollection.ts:639-658): ref_seq and client
+ *     (non-zero) are the op's; getContainingSegment(pos1) in that view, then
+ *     getSlideToSegment (mergeTree.ts:893-950); no segment: the reference is
+ *     detached.
+ *   3 retype: the reference takes type a; if it becomes SlideOnRemove and its
+ *     segment is already removed and acked it slides now (ackInterval's
+ *     StayOnRemove -> SlideOnRemove conversion, intervalCollection.ts:1805-1902).
  * The engine slides references as the reference does
  * (slideAckedRemovedSegmentReferences, mergeTree.ts:893-950): when a segment
  * becomes removed and acked -- a remote remove newly removing it or
@@ -142,12 +149,13 @@ extern "C" {
  * the ack of the local client's removal (:1302-1304) -- its SlideOnRemove
  * references move to the first following segment that is neither removed and
  * acked nor a pending insert (offset 0), else to the last such preceding one
- * (its last offset), else detach; its Simple references detach.  Positions
+ * (its last offset), else detach; its Simple references detach; its
+ * StayOnRemove references stay on the removed segment.  Positions
  * come from mte_read_refs (referencePositionToLocalPosition,
  * mergeTree.ts:1095-1112).                                                     */
 #define MTE_OP_REF 8
 #define MTE_REF_SLIDE_ON_REMOVE 0x40u /* ReferenceType.SlideOnRemove             */
-#define MTE_REF_STAY_ON_REMOVE 0x80u  /* ReferenceType.StayOnRemove (unsupported) */
+#define MTE_REF_STAY_ON_REMOVE 0x80u  /* ReferenceType.StayOnRemove              */
 #define MTE_REF_TRANSIENT 0x100u      /* ReferenceType.Transient (unsupported)    */
 /* Segment groups of pending local annotates (mergeTree.ts:1874-1880): a local
  * annotate record with b = a slot 0..31 marks every segment it visits with
