@@ -690,6 +690,7 @@ def cpu_baseline_prefix(stream, cap, target_s, threads):
         k = int(k * min(16.0, max(2.0, target_s / max(dt, 1e-3))))
     ops = int(sub["batch"]["op_offsets"][-1])
     d = DeviceEngine(stream["n_keys"], seg_capacity=cap)
+    d.set_stats(False)  # the timed path (round phases: statistics runs replay op after op)
     gen.load_stream(d, sub)
     d.apply_batch(sub["batch"])
     parity = bool(np.array_equal(o.digest(), d.digest()) and (o.statuses() == 0).all()

@@ -47,7 +47,13 @@ struct ChunkArgs {
   uint32_t* cnt;     // [doc][nch_cap] segments per chunk
   uint32_t* kc;      // [doc][nch_cap] re-layout scratch
   int32_t* sum;      // [doc][MTE_MAX_CLIENTS][nch_cap]
+  // round phases (mte_round.h): with a plan, chunk_kernel replays only the
+  // documents the plan sends op after op, up to their run's end
+  const uint4* plan;      // [doc] x mode, y k0, z k1, w M (null: every escalated doc to its end)
+  const uint32_t* rflag;  // [doc] non-zero: the round phases left the run to this pass
 };
+
+enum : uint32_t { kModeIdle = 0, kModeRound = 1, kModeSeq = 2 };
 
 // wave-0 -> workgroup requests
 enum ChReq : int32_t { kReqNone = 0, kReqRelayout, kReqRebuild, kReqDone };
@@ -585,6 +591,12 @@ __global__ __launch_bounds__(512) void chunk_kernel(ReplayArgs a, ChunkArgs ch) 
   const int doc = (int)blockIdx.x;
   if (doc >= (int)a.n_docs) return;
   if (!(a.hdr[doc].flags & kHdrNeedsEsc)) return;  // untouched doc: leave the header alone
+  uint32_t kend = 0xffffffffu;
+  if (ch.plan) {
+    const uint4 pp = ch.plan[doc];
+    if (!(pp.x == kModeSeq || (pp.x == kModeRound && ch.rflag[doc] != 0u))) return;
+    kend = pp.z;
+  }
   uint32_t* G = ch_lds;  // [MTE_MAX_CLIENTS][ng_cap]
   ChCtl* ctl = reinterpret_cast<ChCtl*>(ch_lds + (size_t)MTE_MAX_CLIENTS * ch.ng_cap);
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
@@ -592,8 +604,12 @@ __global__ __launch_bounds__(512) void chunk_kernel(ReplayArgs a, ChunkArgs ch) 
   uint32_t st[kNumStats] = {};
   uint64_t prof[8] = {};
   CHPROF(const uint64_t t_start = ch_clock(); uint64_t tph = 0;)
+  uint32_t ktot = 0;
   if (w == 0) {
     run_init(D, a, doc, true);
+    ktot = D.k1;
+    if (D.k1 > kend) D.k1 = kend;
+    D.running = D.running && D.k < D.k1;
     if (lane_id() == 0) {
       ctl->n = D.n;
       ctl->min_seq = D.min_seq;
@@ -652,6 +668,8 @@ __global__ __launch_bounds__(512) void chunk_kernel(ReplayArgs a, ChunkArgs ch) 
     D.running = false;
     if constexpr (S) run_flush_stats(D, st, a);
     run_finish(D, a);
+    // a plan's run ended before the batch: the document stays escalated
+    if (ch.plan && lane_id() == 0 && D.status == 0 && D.k < ktot) a.hdr[doc].flags |= kHdrNeedsEsc;
     CHPROF(prof[5] = ch_clock() - t_start;
            if (lane_id() == 0) for (int t = 0; t < 8; t++) a.stats[(size_t)doc * kNumStats + t] = prof[t];)
   }

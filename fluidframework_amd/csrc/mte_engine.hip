@@ -450,6 +450,10 @@ struct mte_ctx {
   // MTE_PACK_PROPS=0 turns that off
   uint32_t max_vid = 0;
   bool pack_props = true;
+  // round phases of the chunked pass (mte_round.h); MTE_ROUND_PHASES=0 turns them off
+  RoundArgs rd{};
+  bool round_phases = true;
+  uint32_t* h_rcount = nullptr;  // pinned: the plan's counts
   uint64_t* d_off = nullptr;
   mte_propset* d_ps = nullptr;
   mte_prop* d_pe = nullptr;
@@ -519,10 +523,12 @@ void free_image(mte_ctx* c) {
 
 void free_docs(mte_ctx* c) {
   free_image(c);
-  void* cs[] = {c->ch.arena, c->ch.cnt, c->ch.kc, c->ch.sum};
+  void* cs[] = {c->ch.arena, c->ch.cnt, c->ch.kc, c->ch.sum, c->rd.plan, c->rd.rcnt, c->rd.rbuf, c->rd.rflag,
+                c->rd.nch, c->rd.count};
   for (void* p : cs)
     if (p) (void)hipFree(p);
   c->ch = ChunkArgs{};
+  c->rd = RoundArgs{};
   c->chunked = false;
   if (c->d_wclock) (void)hipFree(c->d_wclock);
   c->d_wclock = nullptr;
@@ -610,7 +616,33 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   // contexts, otherwise HBM-resident and streamed per op
   if (c->chunked) {
     const size_t lds = sizeof(uint32_t) * MTE_MAX_CLIENTS * c->ch.ng_cap + sizeof(ChCtl);
-    HIPCHK(c, (launch_chunk<K, S>(a, c->ch, c->n_docs, lds, c->stream)));
+    if (!S && c->round_phases) {
+      // round phases (mte_round.h): each phase plans every escalated
+      // document's next run, replays the round-shaped runs chunk-parallel and
+      // the rest op after op; the host reads the plan's counts to stop
+      ChunkArgs ch = c->ch;
+      RoundArgs rd = c->rd;
+      ch.plan = rd.plan;
+      ch.rflag = rd.rflag;
+      const uint64_t nch_all = (uint64_t)c->n_docs * ch.nch_cap;
+      for (int ph = 0; ph < kMaxPhases; ph++) {
+        rd.last = ph == kMaxPhases - 1 ? 1u : 0u;
+        HIPCHK(c, hipMemsetAsync(rd.count, 0, 16, c->stream));
+        HIPCHK(c, launch_round_plan(a, rd, c->n_docs, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_rcount, rd.count, 16, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        const uint32_t n_round = c->h_rcount[0], n_active = c->h_rcount[2];
+        if (n_active == 0) break;
+        if (n_round) {
+          HIPCHK(c, hipMemsetAsync(rd.rcnt, 0, nch_all * 4, c->stream));
+          HIPCHK(c, hipMemsetAsync(rd.rflag, 0, 4 * (uint64_t)c->n_docs, c->stream));
+          HIPCHK(c, (launch_round_run<K>(a, ch, rd, c->n_docs, c->stream)));
+        }
+        HIPCHK(c, (launch_chunk<K, S>(a, ch, c->n_docs, lds, c->stream)));
+      }
+    } else {
+      HIPCHK(c, (launch_chunk<K, S>(a, c->ch, c->n_docs, lds, c->stream)));
+    }
   } else {
     HIPCHK(c, (launch_stream<K, S>(a, b2, c->stream)));
   }
@@ -773,6 +805,7 @@ int mte_create(const mte_config* cfg, mte_ctx** out) {
   c->cap = cfg->seg_capacity ? cfg->seg_capacity : 1024;
   c->wclock_path = std::getenv("MTE_WAVE_CLOCK");
   if (const char* pp = std::getenv("MTE_PACK_PROPS")) c->pack_props = std::atoi(pp) != 0;
+  if (const char* rp = std::getenv("MTE_ROUND_PHASES")) c->round_phases = std::atoi(rp) != 0;
   if (const char* r = std::getenv("MTE_TREE_ROUNDS")) {
     const int v = std::atoi(r);
     c->tree_rounds = v < 0 ? 0 : (v > 64 ? 64 : v);
@@ -820,6 +853,7 @@ int mte_destroy(mte_ctx* c) {
     if (c->stage_ev[i]) (void)hipEventDestroy(c->stage_ev[i]);
   }
   comm_release(c);
+  if (c->h_rcount) (void)hipHostFree(c->h_rcount);
   if (c->d_comm) (void)hipFree(c->d_comm);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
@@ -912,6 +946,14 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
       HIPCHK(c, hipMalloc((void**)&ch.cnt, nch_all * 4));
       HIPCHK(c, hipMalloc((void**)&ch.kc, nch_all * 4));
       HIPCHK(c, hipMalloc((void**)&ch.sum, nch_all * 4 * MTE_MAX_CLIENTS));
+      RoundArgs& rd = c->rd;
+      HIPCHK(c, hipMalloc((void**)&rd.plan, sizeof(uint4) * n_docs));
+      HIPCHK(c, hipMalloc((void**)&rd.rcnt, nch_all * 4));
+      HIPCHK(c, hipMalloc((void**)&rd.rbuf, nch_all * kRB * sizeof(uint2)));
+      HIPCHK(c, hipMalloc((void**)&rd.rflag, 4 * (uint64_t)n_docs));
+      HIPCHK(c, hipMalloc((void**)&rd.nch, 4 * (uint64_t)n_docs));
+      HIPCHK(c, hipMalloc((void**)&rd.count, 16));
+      if (!c->h_rcount) HIPCHK(c, hipHostMalloc((void**)&c->h_rcount, 16, 0));
       c->chunked = true;
     }
   }

@@ -14,6 +14,20 @@ struct ReplayArgs;
 struct TreeArgs;
 struct ChunkArgs;
 
+// round phases of the chunked pass (mte_round.h)
+constexpr int kRB = 62;              // sub-ops per chunk and run: 128 + 2 x 62 slots <= 254
+constexpr uint32_t kRoundMin = 256;  // the shortest run the round phases take
+constexpr int kMaxPhases = 16;       // phases per launch before the rest runs op after op
+struct RoundArgs {
+  uint4* plan;      // [doc] x mode, y k0, z k1, w M
+  uint32_t* rcnt;   // [doc][nch_cap] sub-ops per chunk
+  uint2* rbuf;      // [doc][nch_cap][kRB] (op index - k0, chunk start in the op's perspective)
+  uint32_t* rflag;  // [doc] non-zero: the run replays op after op
+  uint32_t* nch;    // [doc] chunks after rnd_scatter
+  uint32_t* count;  // [0] round docs, [1] op-after-op docs, [2] active docs
+  uint32_t last;    // this phase sends every active document op after op
+};
+
 // the tree pass over the legacy documents (mte_tree.h): `rounds` of TIER 0
 // (E <= 2) / TIER 1 (E = 4), then TIER 2 (E = 8, 16)
 template <int K, bool S>
@@ -32,5 +46,11 @@ template <int K, bool S>
 hipError_t launch_stream(const ReplayArgs& a, uint32_t blocks, hipStream_t s);
 template <int K, bool S>
 hipError_t launch_chunk(const ReplayArgs& a, const ChunkArgs& ch, uint32_t n_docs, size_t lds, hipStream_t s);
+// the round phases: plan, then (scatter, resolve, apply, gather) for the
+// documents the plan gives a run
+hipError_t launch_round_plan(const ReplayArgs& a, const RoundArgs& rd, uint32_t n_docs, hipStream_t s);
+template <int K>
+hipError_t launch_round_run(const ReplayArgs& a, const ChunkArgs& ch, const RoundArgs& rd, uint32_t n_docs,
+                            hipStream_t s);
 
 }  // namespace mte

@@ -201,3 +201,149 @@ def test_gpu_config5_full_size_batching_invariance():
     p = gen.prefix_ops(s, 8, 512)
     o, dd = both(p, cap)
     assert_same(o, dd)
+
+
+# ---- round phases (mte_round.h): runs replayed chunk-parallel ----------------
+# Statistics runs take the op-after-op chunk pass, so these run with
+# statistics off and compare statuses, digests and read-outs with the
+# restatement (which replays op after op).
+
+def round_both(stream, cap, threads=8):
+    o = SpecOracle(stream["n_keys"], threads=threads, cap=cap)
+    gen.load_stream(o, stream)
+    o.apply_batch(stream["batch"])
+    d = DeviceEngine(stream["n_keys"], seg_capacity=cap)
+    d.set_stats(False)
+    gen.load_stream(d, stream)
+    d.apply_batch(stream["batch"])
+    return o, d
+
+
+def assert_same_state(o, d, sample_docs=8):
+    np.testing.assert_array_equal(d.statuses(), o.statuses())
+    np.testing.assert_array_equal(d.digest(), o.digest())
+    n = o.n_docs
+    for doc in sorted(set(np.linspace(0, n - 1, min(n, sample_docs)).astype(int).tolist())):
+        assert d.read_doc(doc) == o.read_doc(doc)
+
+
+def test_gpu_round_phases_config5_shaped():
+    # 8 docs x 20,000 preloaded segments, 4 rounds of 2,000 concurrent ops: every
+    # round one run (zamboni at each round start)
+    s = gen.generate(5, n_docs=8, ops_per_doc=8000, init_segs=20000, round_ops=2000)
+    cap = gen.seg_capacity(5, s["params"])
+    o, d = round_both(s, cap)
+    assert (o.statuses() == 0).all()
+    assert_same_state(o, d)
+
+
+def test_gpu_round_phases_long_ranges():
+    # farm-rule ranges cross many chunks: sub-ops in every chunk of the range
+    s = gen.generate(5, n_docs=6, ops_per_doc=3000, init_segs=6000, round_ops=300, max_range=0)
+    o, d = round_both(s, 16384)
+    assert (o.statuses() == 0).all()
+    assert_same_state(o, d, sample_docs=6)
+
+
+def test_gpu_round_phases_batches_split_mid_round():
+    # the same ops in 3 batches cut inside rounds: a batch that starts mid-round
+    # is not a run (its refSeq is not the document's currentSeq) and replays op
+    # after op, the next whole rounds as runs
+    s = gen.generate(5, n_docs=4, ops_per_doc=4000, init_segs=5000, round_ops=1000)
+    cap = 16384
+    o = SpecOracle(s["n_keys"], threads=4, cap=cap)
+    gen.load_stream(o, s)
+    o.apply_batch(s["batch"])
+    d = DeviceEngine(s["n_keys"], seg_capacity=cap)
+    d.set_stats(False)
+    gen.load_stream(d, s)
+    b = s["batch"]
+    offs = b["op_offsets"].astype(np.int64)
+    for lo, hi in ((0, 1500), (1500, 2000), (2000, 4000)):
+        sub = dict(b)
+        sub["ops"] = np.concatenate([b["ops"][int(x) + lo:int(x) + hi] for x in offs[:-1]])
+        sub["op_offsets"] = np.arange(len(offs), dtype=np.uint64) * (hi - lo)
+        d.apply_batch(sub)
+    assert_same_state(o, d, sample_docs=4)
+
+
+def _one_run(n0, n_ops, pos, mix_remove=False, past_end=None):
+    """One document of n0 one-unit segments and one run of n_ops concurrent ops
+    (refSeq 0, 4 clients) inserting at `pos` (or removing one unit there on odd
+    ops); past_end: the op index that inserts past the end."""
+    inits = np.zeros(1, gen.DOC_INIT_DTYPE)
+    inits["text_len"] = n0
+    inits["propset"] = 0xFFFFFFFF
+    inits["flags"] = 1  # new length calc
+    text = np.full(n0, ord("a"), np.uint16)
+    offs_s, segs = gen.preload_segments(inits, n0)
+    ops = np.zeros(n_ops, OP_DTYPE)
+    ops["seq"] = np.arange(1, n_ops + 1)
+    ops["ref_seq"] = 0
+    ops["min_seq"] = 0
+    ops["client"] = 1 + (np.arange(n_ops) % 4)
+    ops["flags"] = 2  # MSG_END
+    ops["pos1"] = pos
+    ops["pos2"] = 1
+    ops["a"] = np.arange(n_ops) % 26
+    ops["b"] = 0xFFFFFFFF
+    if mix_remove:
+        odd = np.arange(n_ops) % 2 == 1
+        ops["type"][odd] = 1
+        ops["pos2"][odd] = ops["pos1"][odd] + 1
+    if past_end is not None:
+        ops["pos1"][past_end] = n0 + 10 ** 6
+    batch = {"op_offsets": np.array([0, n_ops], np.uint64), "ops": ops,
+             "text": np.arange(ord("A"), ord("A") + 26, dtype=np.uint16)}
+    res = []
+    for eng in (OracleEngine(0), DeviceEngine(0, seg_capacity=8192)):
+        if isinstance(eng, DeviceEngine):
+            eng.set_stats(False)
+        eng.load_docs(inits, text)
+        eng.load_segments(offs_s, segs)
+        eng.apply_batch(batch)
+        res.append(eng)
+    return res
+
+
+def test_gpu_round_phases_hotspot_falls_back():
+    # 600 inserts at one position: one chunk's bucket overflows (> 62 sub-ops),
+    # so the run replays op after op — same state
+    o, d = _one_run(3000, 600, 1500)
+    assert_same_state(o, d, sample_docs=1)
+
+
+def test_gpu_round_phases_spread_run():
+    # inserts and removes of 4 clients spread over the document (each client's
+    # own earlier ops move its later positions), including several at one spot
+    pos = (np.arange(1200) * 53) % 2950
+    pos[::40] = 1500
+    o, d = _one_run(3000, 1200, pos, mix_remove=True)
+    assert_same_state(o, d, sample_docs=1)
+
+
+def test_gpu_round_phases_insert_past_end_status():
+    # an insert past the end inside a run: the run replays op after op and the
+    # document stops at that op with MTE_E_INSERT_FAILED, as the restatement
+    o, d = _one_run(3000, 400, (np.arange(400) * 37) % 2900, past_end=333)
+    assert o.statuses()[0] != 0
+    assert_same_state(o, d, sample_docs=1)
+
+
+def test_gpu_config5_full_size_round_phases_equal_op_after_op():
+    # BASELINE config 5 at full size: the round phases (statistics off) and the
+    # op-after-op chunk pass (statistics on) end in identical digests
+    s = gen.generate(5)
+    cap = gen.seg_capacity(5, s["params"])
+    d = DeviceEngine(s["n_keys"], seg_capacity=cap)
+    gen.load_stream(d, s)
+    d.apply_batch(s["batch"])
+    assert (d.statuses() == 0).all()
+    seq = d.digest()
+    d.set_stats(False)
+    d.reset()
+    d.run()
+    d.sync()
+    assert (d.statuses() == 0).all()
+    np.testing.assert_array_equal(d.digest(), seq)
+    d.close()
