@@ -454,6 +454,7 @@ struct mte_ctx {
   RoundArgs rd{};
   bool round_phases = true;
   uint32_t* h_rcount = nullptr;  // pinned: the plan's counts
+  uint64_t rl_alloc = 0;         // rd.rlist entries allocated
   uint64_t* d_off = nullptr;
   mte_propset* d_ps = nullptr;
   mte_prop* d_pe = nullptr;
@@ -524,11 +525,12 @@ void free_image(mte_ctx* c) {
 void free_docs(mte_ctx* c) {
   free_image(c);
   void* cs[] = {c->ch.arena, c->ch.cnt, c->ch.kc, c->ch.sum, c->rd.plan, c->rd.rcnt, c->rd.rbuf, c->rd.rflag,
-                c->rd.nch, c->rd.count};
+                c->rd.nch, c->rd.nnew, c->rd.count, c->rd.rlist, c->rd.rchain};
   for (void* p : cs)
     if (p) (void)hipFree(p);
   c->ch = ChunkArgs{};
   c->rd = RoundArgs{};
+  c->rl_alloc = 0;
   c->chunked = false;
   if (c->d_wclock) (void)hipFree(c->d_wclock);
   c->d_wclock = nullptr;
@@ -616,10 +618,22 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   // contexts, otherwise HBM-resident and streamed per op
   if (c->chunked) {
     const size_t lds = sizeof(uint32_t) * MTE_MAX_CLIENTS * c->ch.ng_cap + sizeof(ChCtl);
-    if (!S && c->round_phases) {
+    if (!S && c->round_phases && (uint64_t)(c->ch.nch_cap + c->ch.ng_cap) * 4 <= kRoundLdsMax) {
       // round phases (mte_round.h): each phase plans every escalated
       // document's next run, replays the round-shaped runs chunk-parallel and
       // the rest op after op; the host reads the plan's counts to stop
+      // the client chains' sub-op lists: 2 x ops + 8 per client, per document
+      const uint64_t rl_cap = 2 * c->max_doc_ops_s[c->rslot] + 8 * MTE_MAX_CLIENTS;
+      if (rl_cap * c->n_docs > c->rl_alloc) {
+        if (c->rd.rlist) {
+          HIPCHK(c, hipStreamSynchronize(c->stream));
+          HIPCHK(c, hipFree(c->rd.rlist));
+        }
+        c->rd.rlist = nullptr;
+        HIPCHK(c, hipMalloc((void**)&c->rd.rlist, sizeof(uint4) * rl_cap * c->n_docs));
+        c->rl_alloc = rl_cap * c->n_docs;
+      }
+      c->rd.rl_cap = rl_cap;
       ChunkArgs ch = c->ch;
       RoundArgs rd = c->rd;
       ch.plan = rd.plan;
@@ -952,6 +966,8 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
       HIPCHK(c, hipMalloc((void**)&rd.rbuf, nch_all * kRB * sizeof(uint2)));
       HIPCHK(c, hipMalloc((void**)&rd.rflag, 4 * (uint64_t)n_docs));
       HIPCHK(c, hipMalloc((void**)&rd.nch, 4 * (uint64_t)n_docs));
+      HIPCHK(c, hipMalloc((void**)&rd.nnew, 4 * (uint64_t)n_docs));
+      HIPCHK(c, hipMalloc((void**)&rd.rchain, sizeof(uint2) * MTE_MAX_CLIENTS * (uint64_t)n_docs));
       HIPCHK(c, hipMalloc((void**)&rd.count, 16));
       if (!c->h_rcount) HIPCHK(c, hipHostMalloc((void**)&c->h_rcount, 16, 0));
       c->chunked = true;

@@ -24,12 +24,34 @@ hipError_t launch_round_plan(const ReplayArgs& a, const RoundArgs& rd, uint32_t 
 template <int K>
 hipError_t launch_round_run(const ReplayArgs& a, const ChunkArgs& ch, const RoundArgs& rd, uint32_t n_docs,
                             hipStream_t s) {
-  const dim3 blk(kChWaves * kWave);
-  hipLaunchKernelGGL((rnd_scatter_kernel<K>), dim3(n_docs), blk, 0, s, a, ch, rd);
-  hipLaunchKernelGGL((rnd_resolve_kernel<K>), dim3(n_docs), blk, 0, s, a, ch, rd);
-  const uint64_t waves = (uint64_t)n_docs * ch.nch_cap;
-  hipLaunchKernelGGL((rnd_apply_kernel<K>), dim3((uint32_t)((waves + 3) / 4)), dim3(4 * kWave), 0, s, a, ch, rd);
-  hipLaunchKernelGGL((rnd_gather_kernel<K>), dim3(n_docs), blk, 0, s, a, ch, rd);
+  const uint32_t tpd = (a.cap + kT - 1) / kT;  // flat tiles per document
+  const uint64_t tiles = (uint64_t)n_docs * tpd, chunks = (uint64_t)n_docs * ch.nch_cap;
+  const dim3 w4(4 * kWave);
+  // re-layout: flat -> chunks (zamboni at M), the round-start column
+  hipLaunchKernelGGL((rnd_count_kernel<K>), dim3((uint32_t)((tiles + 3) / 4)), w4, 0, s, a, ch, rd, tpd);
+  hipLaunchKernelGGL(rnd_scan_kernel, dim3(n_docs), dim3(kChWaves * kWave), 0, s, a, ch, rd, 0);
+  hipLaunchKernelGGL((rnd_move_kernel<K>), dim3((uint32_t)((tiles + 3) / 4)), w4, 0, s, a, ch, rd, tpd);
+  hipLaunchKernelGGL(rnd_cols_kernel, dim3((uint32_t)((chunks + 3) / 4)), w4, 0, s, a, ch, rd);
+  // resolve: the client chains, columns in LDS (two waves per workgroup when they fit)
+  const size_t col = (size_t)(ch.nch_cap + ch.ng_cap) * 4;
+  if (2 * col <= kRoundLdsMax) {
+    hipError_t e = hipFuncSetAttribute((const void*)rnd_resolve_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)(2 * col));
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(rnd_resolve_kernel<2>, dim3(n_docs * (kChWaves / 2)), dim3(2 * kWave), 2 * col, s, a, ch, rd);
+  } else {
+    hipError_t e = hipFuncSetAttribute((const void*)rnd_resolve_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)col);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(rnd_resolve_kernel<1>, dim3(n_docs * kChWaves), dim3(kWave), col, s, a, ch, rd);
+  }
+  const uint32_t bpd = (uint32_t)((rd.rl_cap + 255) / 256);
+  hipLaunchKernelGGL(rnd_bucket_kernel, dim3(n_docs * bpd), dim3(256), 0, s, a, ch, rd, bpd);
+  // apply: every chunk with sub-ops on its own wave
+  hipLaunchKernelGGL((rnd_apply_kernel<K>), dim3((uint32_t)((chunks + 3) / 4)), w4, 0, s, a, ch, rd);
+  // gather: chunks -> flat, the header past the run
+  hipLaunchKernelGGL(rnd_scan_kernel, dim3(n_docs), dim3(kChWaves * kWave), 0, s, a, ch, rd, 1);
+  hipLaunchKernelGGL((rnd_gmove_kernel<K>), dim3((uint32_t)((chunks + 3) / 4)), w4, 0, s, a, ch, rd);
   return hipGetLastError();
 }
 template hipError_t launch_round_run<0>(const ReplayArgs&, const ChunkArgs&, const RoundArgs&, uint32_t, hipStream_t);

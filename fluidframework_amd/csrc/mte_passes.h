@@ -23,10 +23,17 @@ struct RoundArgs {
   uint32_t* rcnt;   // [doc][nch_cap] sub-ops per chunk
   uint2* rbuf;      // [doc][nch_cap][kRB] (op index - k0, chunk start in the op's perspective)
   uint32_t* rflag;  // [doc] non-zero: the run replays op after op
-  uint32_t* nch;    // [doc] chunks after rnd_scatter
+  uint32_t* nch;    // [doc] chunks after the re-layout
+  uint32_t* nnew;   // [doc] segments after the re-layout
   uint32_t* count;  // [0] round docs, [1] op-after-op docs, [2] active docs
+  uint4* rlist;     // [doc][rl_cap] the client chains' sub-ops (chunk, op index - k0, chunk start)
+  uint64_t rl_cap;  // list entries per document: 2 x its ops + 8 per client
+  uint2* rchain;    // [doc][MTE_MAX_CLIENTS] (list offset, entries) of each client chain
   uint32_t last;    // this phase sends every active document op after op
 };
+// the round phases fit a context whose per-wave column (nch_cap + ng_cap
+// entries) fits this much LDS
+constexpr uint32_t kRoundLdsMax = 150u * 1024u;
 
 // the tree pass over the legacy documents (mte_tree.h): `rounds` of TIER 0
 // (E <= 2) / TIER 1 (E = 4), then TIER 2 (E = 8, 16)

@@ -35,14 +35,19 @@
 // Phases per launch of the chunked pass (host loop, mte_engine.hip):
 //   rnd_plan     one wave per document: the run at its op cursor (mode kRound
 //                if long enough, else the rest goes to the sequential pass);
-//   rnd_scatter  flat planes -> chunks of kChFill segments, dropping
-//                removedSeq <= M (zamboni, mergeTree.ts:1077-1093), and the
-//                round-start column (visible length per chunk);
-//   rnd_resolve  one wave per client chain: positions -> (chunk, start) on the
-//                client's column, each sub-op into the chunk's bucket;
+//   re-layout    flat planes -> chunks of kChFill segments, dropping
+//                removedSeq <= M (zamboni, mergeTree.ts:1077-1093): keep
+//                counts per 256-slot tile (rnd_count, a wave per tile), their
+//                prefix per document (rnd_scan), the moves (rnd_move, a wave
+//                per tile), then per chunk its count and round-start column
+//                entry, the visible length (rnd_cols, a wave per chunk);
+//   rnd_resolve  one wave per client chain, its column in LDS: positions ->
+//                (chunk, start), appended to the chain's sub-op list;
+//   rnd_bucket   a thread per sub-op: into its chunk's bucket;
 //   rnd_apply    one wave per chunk with sub-ops: sort them by op index, load
 //                the chunk into registers, seg_op_v each, store;
-//   rnd_gather   chunks -> flat planes, the document header advanced to k1.
+//   gather       chunk counts -> prefix (rnd_scan), chunks -> flat planes
+//                (rnd_gmove, a wave per chunk), the header advanced to k1.
 // Anything the run cannot take — an insert past the end (the op-after-op pass
 // reports MTE_E_INSERT_FAILED at that op), a bucket over kRB sub-ops — sets
 // the document's flag before any segment is written, and the sequential chunk
@@ -115,198 +120,353 @@ __global__ __launch_bounds__(256) void rnd_plan_kernel(ReplayArgs a, RoundArgs r
   if (l == 0) rd.plan[doc] = p;
 }
 
-// flat planes -> chunks of kChFill, dropping removedSeq <= M; the round-start
-// column (visible length of each chunk) into ch.kc
+// ---- re-layout and gather: many waves per document ---------------------------
+
+constexpr int kT = kChE * kWave;  // flat slots per tile
+
+// keep counts of the flat tiles (removedSeq > M), one wave per tile
 template <int K>
-__global__ __launch_bounds__(512) void rnd_scatter_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
+__global__ __launch_bounds__(256) void rnd_count_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd, uint32_t tpd) {
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
+  const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
+  const int doc = (int)(wi / tpd), t = (int)(wi % tpd);
+  if (doc >= (int)a.n_docs) return;
+  const uint4 p = rd.plan[doc];
+  const int n = a.hdr[doc].nseg;
+  if (p.x != kModeRound || t * kT >= n) return;
+  const int32_t M = (int32_t)p.w;
+  const uint32_t* rs = a.planes + 2 * a.stride + (uint64_t)doc * a.cap;
+  int32_t k = 0;
+#pragma unroll
+  for (int j = 0; j < kChE; j++) {
+    const int i = t * kT + j * kWave + l;
+    k += (i < n && (int32_t)rs[i] > M) ? 1 : 0;
+  }
+  const int32_t tot = rdlane(wave_incl_scan(k), kWave - 1);
+  if (l == 0) ch.kc[(uint64_t)doc * ch.nch_cap + t] = (uint32_t)tot;
+}
+
+// per document: exclusive prefix of kc (scatter: the tiles' keep counts) or of
+// cnt (gather: the chunks' segment counts, into kc); the gather also advances
+// the header past the run
+__global__ __launch_bounds__(512) void rnd_scan_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd, int gather) {
   __shared__ ChCtl ctl;
   const int doc = (int)blockIdx.x;
   const uint4 p = rd.plan[doc];
-  if (p.x != kModeRound) return;
-  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
-  const int32_t M = (int32_t)p.w;
-  const int n = a.hdr[doc].nseg;
-  const uint32_t* pl = a.planes + (uint64_t)doc * a.cap;
+  if (p.x != kModeRound || (gather && rd.rflag[doc] != 0u)) return;
   uint32_t* kc = ch.kc + (uint64_t)doc * ch.nch_cap;
-  uint32_t* cnt = ch.cnt + (uint64_t)doc * ch.nch_cap;
-  constexpr int kT = kChE * kWave;  // 256 flat slots per tile
-  const int ntile = (n + kT - 1) / kT;
-  for (int t = w; t < ntile; t += kChWaves) {
-    int32_t k = 0;
-#pragma unroll
-    for (int j = 0; j < kChE; j++) {
-      const int i = t * kT + l * kChE + j;
-      k += (i < n && (int32_t)pl[2 * a.stride + i] > M) ? 1 : 0;
-    }
-    const int32_t tot = rdlane(wave_incl_scan(k), kWave - 1);
-    if (l == 0) kc[t] = (uint32_t)tot;
+  int m;
+  if (gather) {
+    m = (int)rd.nch[doc];
+    const uint32_t* cnt = ch.cnt + (uint64_t)doc * ch.nch_cap;
+    for (int i = (int)threadIdx.x; i < m; i += (int)blockDim.x) kc[i] = cnt[i];
+    __syncthreads();
+  } else {
+    m = (a.hdr[doc].nseg + kT - 1) / kT;
   }
-  __syncthreads();
-  const int32_t n_new = ch_block_scan(kc, ntile, &ctl);
-  const int nplanes = kFieldPlanes + K;
-  for (int t = w; t < ntile; t += kChWaves) {
-    bool keep[kChE];
-    int32_t k = 0;
-#pragma unroll
-    for (int j = 0; j < kChE; j++) {
-      const int i = t * kT + l * kChE + j;
-      keep[j] = i < n && (int32_t)pl[2 * a.stride + i] > M;
-      k += keep[j] ? 1 : 0;
-    }
-    const int32_t d0 = (int32_t)ld_ag(kc + t) + wave_incl_scan(k) - k;
-    for (int q = 0; q < nplanes; q++) {
-      int32_t d = d0;
-#pragma unroll
-      for (int j = 0; j < kChE; j++) {
-        const int i = t * kT + l * kChE + j;
-        if (keep[j] && d < (int32_t)(ch.nch_cap * kChFill)) {
-          const uint64_t x = ch_slot(ch, doc, d / kChFill) + (uint32_t)(d % kChFill);
-          ch.arena[(uint64_t)q * ch.astride + x] = pl[(uint64_t)q * a.stride + i];
-        }
-        d += keep[j] ? 1 : 0;
-      }
+  const int32_t total = ch_block_scan(kc, m, &ctl);
+  if (threadIdx.x == 0) {
+    if (!gather) {
+      int nch = (total + kChFill - 1) / kChFill;
+      nch = nch < 1 ? 1 : (nch > (int)ch.nch_cap ? (int)ch.nch_cap : nch);
+      rd.nch[doc] = (uint32_t)nch;
+      rd.nnew[doc] = (uint32_t)total;
+    } else {
+      const uint64_t kb = a.op_off[doc];
+      const uint32_t ktot = (uint32_t)(a.op_off[doc + 1] - kb);
+      DocHdr h = a.hdr[doc];
+      h.nseg = total;
+      h.min_seq = (int32_t)p.w;
+      h.cur_seq = (int32_t)reinterpret_cast<const uint32_t*>(a.recs + 2 * (kb + p.z - 1))[0];
+      h.resume = p.z;
+      if (p.z >= ktot) h.flags &= ~kHdrNeedsEsc;
+      a.hdr[doc] = h;
     }
   }
-  __syncthreads();  // (every wave has read its tile's prefix before kc is reused)
-  int nch = (n_new + kChFill - 1) / kChFill;
-  nch = nch < 1 ? 1 : (nch > (int)ch.nch_cap ? (int)ch.nch_cap : nch);
-  for (int q = w; q < nch; q += kChWaves) {
-    const int cn = n_new - q * kChFill < kChFill ? (n_new - q * kChFill > 0 ? n_new - q * kChFill : 0) : kChFill;
-    const uint64_t x0 = ch_slot(ch, doc, q);
-    int32_t v = 0;
-#pragma unroll
-    for (int j = 0; j < kChFill / kWave; j++) {
-      const int s = j * kWave + l;
-      if (s < cn) {
-        const int32_t rs = (int32_t)ld_ag(ch.arena + 2 * ch.astride + x0 + s);
-        v += rs == kNone ? (int32_t)ld_ag(ch.arena + x0 + s) : 0;
-      }
-    }
-    const int32_t tot = rdlane(wave_incl_scan(v), kWave - 1);
-    if (l == 0) {
-      cnt[q] = (uint32_t)cn;
-      kc[q] = (uint32_t)tot;
-    }
-  }
-  if (threadIdx.x == 0) rd.nch[doc] = (uint32_t)nch;
 }
 
-// one sub-op into chunk i's bucket (any lane; returns false on overflow)
-__device__ __forceinline__ void rnd_emit(const RoundArgs& rd, uint32_t* rcnt, uint2* rbuf, int doc, int i,
-                                         uint32_t k, int32_t ex) {
-  const uint32_t pos = atomicAdd(rcnt + i, 1u);
-  if (pos < (uint32_t)kRB) rbuf[(uint64_t)i * kRB + pos] = make_uint2(k, (uint32_t)ex);
-  else atomicOr(rd.rflag + doc, 1u);
-}
-
-// one wave per client chain (clients c = w, w + 8, ... with ops in the run)
+// flat tile -> its kept segments at kChFill per chunk, one wave per tile
 template <int K>
-__global__ __launch_bounds__(512) void rnd_resolve_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
-  __shared__ uint32_t Gs[kChWaves][kChMaxGroups];
-  __shared__ uint32_t present;
-  const int doc = (int)blockIdx.x;
+__global__ __launch_bounds__(256) void rnd_move_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd, uint32_t tpd) {
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
+  const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
+  const int doc = (int)(wi / tpd), t = (int)(wi % tpd);
+  if (doc >= (int)a.n_docs) return;
+  const uint4 p = rd.plan[doc];
+  const int n = a.hdr[doc].nseg;
+  if (p.x != kModeRound || t * kT >= n) return;
+  const int32_t M = (int32_t)p.w;
+  const uint32_t* pl = a.planes + (uint64_t)doc * a.cap;
+  bool keep[kChE];
+#pragma unroll
+  for (int j = 0; j < kChE; j++) {
+    const int i = t * kT + j * kWave + l;
+    keep[j] = i < n && (int32_t)pl[2 * a.stride + i] > M;
+  }
+  // destinations in document order: slot j * 64 + l of the tile
+  int32_t dst[kChE];
+  int32_t run = (int32_t)ch.kc[(uint64_t)doc * ch.nch_cap + t];
+#pragma unroll
+  for (int j = 0; j < kChE; j++) {
+    const uint64_t mk = __ballot(keep[j]);
+    dst[j] = run + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+    run += __popcll(mk);
+  }
+  const uint32_t lim = ch.nch_cap * kChFill;
+  for (int q = 0; q < kFieldPlanes + K; q++) {
+#pragma unroll
+    for (int j = 0; j < kChE; j++) {
+      const int i = t * kT + j * kWave + l;
+      if (keep[j] && (uint32_t)dst[j] < lim) {
+        const uint64_t x = ch_slot(ch, doc, dst[j] / kChFill) + (uint32_t)(dst[j] % kChFill);
+        ch.arena[(uint64_t)q * ch.astride + x] = pl[(uint64_t)q * a.stride + i];
+      }
+    }
+  }
+}
+
+// per chunk after the moves: its segment count and its round-start column
+// entry (the visible length: every segment is seen at refSeq R), into kc
+__global__ __launch_bounds__(256) void rnd_cols_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
+  const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
+  const int doc = (int)(wi / ch.nch_cap), q = (int)(wi % ch.nch_cap);
+  if (doc >= (int)a.n_docs) return;
+  const uint4 p = rd.plan[doc];
+  if (p.x != kModeRound || q >= (int)rd.nch[doc]) return;
+  const int n_new = (int)rd.nnew[doc];
+  const int cn = n_new - q * kChFill < kChFill ? (n_new - q * kChFill > 0 ? n_new - q * kChFill : 0) : kChFill;
+  const uint64_t x0 = ch_slot(ch, doc, q);
+  int32_t v = 0;
+#pragma unroll
+  for (int j = 0; j < kChFill / kWave; j++) {
+    const int s = j * kWave + l;
+    if (s < cn) v += (int32_t)ch.arena[2 * ch.astride + x0 + s] == kNone ? (int32_t)ch.arena[x0 + s] : 0;
+  }
+  const int32_t tot = rdlane(wave_incl_scan(v), kWave - 1);
+  if (l == 0) {
+    ch.cnt[(uint64_t)doc * ch.nch_cap + q] = (uint32_t)cn;
+    ch.kc[(uint64_t)doc * ch.nch_cap + q] = (uint32_t)tot;
+  }
+}
+
+// chunk -> flat planes at its prefix (nothing is dropped: the run's
+// tombstones have removedSeq > R >= M), one wave per chunk
+template <int K>
+__global__ __launch_bounds__(256) void rnd_gmove_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
+  const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
+  const int doc = (int)(wi / ch.nch_cap), q = (int)(wi % ch.nch_cap);
+  if (doc >= (int)a.n_docs) return;
+  const uint4 p = rd.plan[doc];
+  if (p.x != kModeRound || rd.rflag[doc] != 0u || q >= (int)rd.nch[doc]) return;
+  const int cn = (int)ch.cnt[(uint64_t)doc * ch.nch_cap + q];
+  const uint32_t d0 = ch.kc[(uint64_t)doc * ch.nch_cap + q];
+  const uint64_t x0 = ch_slot(ch, doc, q);
+  uint32_t* pl = a.planes + (uint64_t)doc * a.cap;
+  for (int qq = 0; qq < kFieldPlanes + K; qq++) {
+#pragma unroll
+    for (int j = 0; j < kChE; j++) {
+      const int s = j * kWave + l;
+      if (s < cn && d0 + (uint32_t)s < a.cap)
+        pl[(uint64_t)qq * a.stride + d0 + (uint32_t)s] = ch.arena[(uint64_t)qq * ch.astride + x0 + s];
+    }
+  }
+}
+
+// ---- resolve: one wave per client chain, the column in LDS -------------------
+
+// ch_find (mte_chunk.h) over a column in LDS: the first chunk whose inclusive
+// prefix is > x (strict) or >= x; nch if none
+__device__ __forceinline__ int col_find(const uint32_t* G, uint32_t ng, const int32_t* col, int nch, int32_t x,
+                                        bool strict, int32_t* excl, int32_t* total, int32_t* csum) {
+  const int l = lane_id();
+  const uint32_t gpl = (ng + kWave - 1) / kWave;
+  int32_t s = 0;
+  for (uint32_t k = 0; k < gpl; k++) {
+    const uint32_t g = (uint32_t)l * gpl + k;
+    s += g < ng ? (int32_t)G[g] : 0;
+  }
+  const int32_t incl = wave_incl_scan(s);
+  *total = rdlane(incl, kWave - 1);
+  const uint64_t hm = __ballot(strict ? incl > x : incl >= x);
+  if (!hm) {
+    *excl = *total;
+    *csum = 0;
+    return nch;
+  }
+  const int ls = __ffsll((long long)hm) - 1;
+  int32_t run = rdlane(incl - s, ls);
+  uint32_t g = (uint32_t)ls * gpl;
+  for (uint32_t k = 0; k < gpl; k++, g++) {
+    const int32_t v = (int32_t)G[g];
+    if (strict ? run + v > x : run + v >= x) break;
+    run += v;
+  }
+  const int i = (int)g * kChGroup + l;
+  const int32_t v = i < nch ? col[i] : 0;
+  const int32_t ci = wave_incl_scan(v) + run;
+  const uint64_t cm = __ballot(strict ? ci > x : ci >= x);
+  const int lc = cm ? __ffsll((long long)cm) - 1 : kWave - 1;
+  *excl = rdlane(ci - v, lc);
+  *csum = rdlane(v, lc);
+  return (int)g * kChGroup + lc;
+}
+
+// WPB waves per workgroup, 8 / WPB workgroups per document; wave u = 0..7 of
+// the document takes the clients c = u, u + 8, ...; dynamic LDS: per wave a
+// column of nch_cap entries and its group sums
+template <int WPB>
+__global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
+  extern __shared__ uint32_t rs_lds[];
+  __shared__ uint32_t ccount[MTE_MAX_CLIENTS];
+  constexpr int kBlocksPerDoc = kChWaves / WPB;
+  const int doc = (int)blockIdx.x / kBlocksPerDoc;
   const uint4 p = rd.plan[doc];
   if (p.x != kModeRound) return;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
-  const uint32_t k0 = p.y, nops = p.z - p.y;
-  const uint4* recp = a.recs + 2 * (a.op_off[doc] + k0);
+  const int u = ((int)blockIdx.x % kBlocksPerDoc) * WPB + w;
+  const uint32_t nops = p.z - p.y;
+  const uint4* recp = a.recs + 2 * (a.op_off[doc] + p.y);
   const int nch = (int)rd.nch[doc];
   const uint32_t ng = (uint32_t)((nch + kChGroup - 1) / kChGroup);
-  const uint32_t* cnt = ch.cnt + (uint64_t)doc * ch.nch_cap;
+  const uint32_t stride = ch.nch_cap + ch.ng_cap;
+  int32_t* col = reinterpret_cast<int32_t*>(rs_lds + (uint32_t)w * stride);
+  uint32_t* G = rs_lds + (uint32_t)w * stride + ch.nch_cap;
   const int32_t* sum0 = reinterpret_cast<const int32_t*>(ch.kc + (uint64_t)doc * ch.nch_cap);
-  uint32_t* rcnt = rd.rcnt + (uint64_t)doc * ch.nch_cap;
-  uint2* rbuf = rd.rbuf + (uint64_t)doc * ch.nch_cap * kRB;
-  uint32_t* G = Gs[w];
-  // the clients with ops in the run
-  if (threadIdx.x == 0) present = 0u;
+  uint4* list = rd.rlist + (uint64_t)doc * rd.rl_cap;
+  // ops per client (every workgroup of the document counts them all)
+  for (int c = (int)threadIdx.x; c < MTE_MAX_CLIENTS; c += (int)blockDim.x) ccount[c] = 0u;
   __syncthreads();
-  uint32_t mask = 0u;
-  for (uint32_t base = (uint32_t)w * kWave; base < nops; base += kChWaves * kWave) {
-    const uint32_t i = base + (uint32_t)l;
-    const uint32_t w3 = i < nops ? reinterpret_cast<const uint32_t*>(recp + 2 * i)[3] : 0u;
-    mask |= i < nops ? 1u << ((w3 >> 8) & 31u) : 0u;
+  for (uint32_t i = threadIdx.x; i < nops; i += blockDim.x) {
+    const uint32_t w3 = reinterpret_cast<const uint32_t*>(recp + 2 * i)[3];
+    atomicAdd(&ccount[(w3 >> 8) & 31u], 1u);
   }
-  for (int off = 32; off >= 1; off >>= 1) mask |= (uint32_t)__shfl_xor((int)mask, off);
-  if (l == 0 && mask) atomicOr(&present, mask);
   __syncthreads();
-  const uint32_t pres = present;
-  for (int c = w; c < MTE_MAX_CLIENTS; c += kChWaves) {
-    if (!((pres >> c) & 1u)) continue;
-    int32_t* sumc = ch.sum + ((uint64_t)doc * MTE_MAX_CLIENTS + (uint32_t)c) * ch.nch_cap;
-    // column c = the round-start column
-    for (int i = l; i < nch; i += kWave) sumc[i] = ld_ag(sum0 + i);
-    for (uint32_t g = 0; g < ng; g++) {
-      const int i = (int)g * kChGroup + l;
-      const int32_t v = i < nch ? ld_ag(sum0 + i) : 0;
-      const int32_t tot = rdlane(wave_incl_scan(v), kWave - 1);
-      if (l == 0) G[g] = (uint32_t)tot;
-    }
-    vm_wait();
-    fence_wave();
-    bool failed = false;
-    for (uint32_t base = 0; base < nops && !failed; base += kWave) {
-      uint32_t b[8];
-      ch_rec_batch(b, recp, base);
-      uint64_t mine = __ballot(base + (uint32_t)l < nops && ((b[3] >> 8) & 0xffu) == (uint32_t)c);
-      while (mine) {
-        const int j = __ffsll((long long)mine) - 1;
-        mine &= mine - 1;
-        const uint32_t k = base + (uint32_t)j;
-        const uint32_t w3 = rdlane(b[3], j);
-        const uint32_t type = w3 & 0xffu, flags = w3 >> 16;
-        const int32_t pos1 = (int32_t)rdlane(b[4], j), pos2 = (int32_t)rdlane(b[5], j);
-        int32_t ex = 0, total = 0, cs = 0;
-        int cn = 0;
-        if (type == MTE_OP_INSERT) {
-          const int i0 = ch_find(G, ng, sumc, cnt, nch, pos1, false, &ex, &total, &cs, &cn);
-          if (pos1 > total || i0 >= nch) {  // MTE_E_INSERT_FAILED at this op: the run goes op after op
-            if (l == 0) atomicOr(rd.rflag + doc, 2u);
-            failed = true;
-            break;
-          }
-          const int32_t nlen = (flags & MTE_F_MARKER) ? 1 : pos2;
-          if (l == 0) {
-            rnd_emit(rd, rcnt, rbuf, doc, i0, k, ex);
-            if (nlen > 0) {
-              sumc[i0] = cs + nlen;
-              G[(uint32_t)i0 / kChGroup] += (uint32_t)nlen;
+  // each chain's list region: twice its ops (+ 8) from the prefix over clients
+  uint32_t off = 0;
+  for (int c = 0; c < MTE_MAX_CLIENTS; c++) {
+    const uint32_t nc = ccount[c];
+    const uint32_t cap_c = nc ? 2u * nc + 8u : 0u;
+    if ((c % kChWaves) == u && nc) {
+      // column c = the round-start column, its group sums
+      for (int i = l; i < nch; i += kWave) col[i] = sum0[i];
+      for (uint32_t g = 0; g < ng; g++) {
+        const int i = (int)g * kChGroup + l;
+        const int32_t v = i < nch ? sum0[i] : 0;
+        const int32_t tot = rdlane(wave_incl_scan(v), kWave - 1);
+        if (l == 0) G[g] = (uint32_t)tot;
+      }
+      fence_wave();
+      uint32_t m = 0;  // entries in the chain's list
+      bool failed = false;
+      uint32_t b[8], nb[8];
+      ch_rec_batch(b, recp, 0);
+      for (uint32_t base = 0; base < nops && !failed; base += kWave) {
+        if (base + kWave < nops) ch_rec_batch(nb, recp, base + kWave);  // the next batch, in flight meanwhile
+        uint64_t mine = __ballot(base + (uint32_t)l < nops && ((b[3] >> 8) & 0xffu) == (uint32_t)c);
+        while (mine) {
+          const int j = __ffsll((long long)mine) - 1;
+          mine &= mine - 1;
+          const uint32_t k = base + (uint32_t)j;
+          const uint32_t w3 = rdlane(b[3], j);
+          const uint32_t type = w3 & 0xffu, flags = w3 >> 16;
+          const int32_t pos1 = (int32_t)rdlane(b[4], j), pos2 = (int32_t)rdlane(b[5], j);
+          int32_t ex = 0, total = 0, cs = 0;
+          if (type == MTE_OP_INSERT) {
+            const int i0 = col_find(G, ng, col, nch, pos1, false, &ex, &total, &cs);
+            if (pos1 > total || i0 >= nch || m >= cap_c) {  // MTE_E_INSERT_FAILED here: op after op
+              failed = true;
+              break;
             }
-          }
-        } else {
-          const int32_t b1 = pos1 < pos2 ? pos1 : pos2, b2 = pos1 < pos2 ? pos2 : pos1;
-          const int i0 = ch_find(G, ng, sumc, cnt, nch, b1, true, &ex, &total, &cs, &cn);
-          if (i0 < nch) {
-            if (b1 == b2) {
-              // ensureIntervalBoundary alone: a split strictly inside a leaf
-              if (ex < b1 && l == 0) rnd_emit(rd, rcnt, rbuf, doc, i0, k, ex);
-            } else {
-              // chunks i0 .. while their start is before b2, 64 at a time
-              int32_t run = ex;
-              for (int cb = i0; cb < nch; cb += kWave) {
-                const int i = cb + l;
-                const int32_t v = i < nch ? ld_ag(sumc + i) : 0;
-                const int32_t incl = wave_incl_scan(v) + run;
-                const int32_t st = incl - v;
-                const bool hit = i < nch && v > 0 && st < b2;
-                if (hit) {
-                  rnd_emit(rd, rcnt, rbuf, doc, i, k, st);
-                  if (type == MTE_OP_REMOVE) {
-                    const int32_t lo = b1 > st ? b1 : st, hi = b2 < incl ? b2 : incl;
-                    sumc[i] = v - (hi - lo);
-                    atomicSub(&G[(uint32_t)i / kChGroup], (uint32_t)(hi - lo));
+            const int32_t nlen = (flags & MTE_F_MARKER) ? 1 : pos2;
+            if (l == 0) {
+              list[off + m] = make_uint4((uint32_t)i0, k, (uint32_t)ex, 0u);
+              if (nlen > 0) {
+                col[i0] = cs + nlen;
+                G[(uint32_t)i0 / kChGroup] += (uint32_t)nlen;
+              }
+            }
+            m++;
+          } else {
+            const int32_t b1 = pos1 < pos2 ? pos1 : pos2, b2 = pos1 < pos2 ? pos2 : pos1;
+            const int i0 = col_find(G, ng, col, nch, b1, true, &ex, &total, &cs);
+            if (i0 < nch) {
+              if (b1 == b2) {
+                // ensureIntervalBoundary alone: a split strictly inside a leaf
+                if (ex < b1) {
+                  if (m >= cap_c) {
+                    failed = true;
+                    break;
                   }
+                  if (l == 0) list[off + m] = make_uint4((uint32_t)i0, k, (uint32_t)ex, 0u);
+                  m++;
                 }
-                run = rdlane(incl, kWave - 1);
-                if (run >= b2) break;
+              } else {
+                // chunks i0 .. while their start is before b2, 64 at a time
+                int32_t run = ex;
+                for (int cb = i0; cb < nch; cb += kWave) {
+                  const int i = cb + l;
+                  const int32_t v = i < nch ? col[i] : 0;
+                  const int32_t incl = wave_incl_scan(v) + run;
+                  const int32_t st = incl - v;
+                  const bool hit = i < nch && v > 0 && st < b2;
+                  const uint64_t hm = __ballot(hit);
+                  const uint32_t at = m + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32),
+                                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+                  m += (uint32_t)__popcll(hm);
+                  if (m > cap_c) {
+                    failed = true;
+                    break;
+                  }
+                  if (hit) {
+                    list[off + at] = make_uint4((uint32_t)i, k, (uint32_t)st, 0u);
+                    if (type == MTE_OP_REMOVE) {
+                      const int32_t lo = b1 > st ? b1 : st, hi = b2 < incl ? b2 : incl;
+                      col[i] = v - (hi - lo);
+                      atomicSub(&G[(uint32_t)i / kChGroup], (uint32_t)(hi - lo));
+                    }
+                  }
+                  run = rdlane(incl, kWave - 1);
+                  if (run >= b2) break;
+                }
+                if (failed) break;
               }
             }
           }
+          fence_wave();
         }
-        vm_wait();
-        fence_wave();
+#pragma unroll
+        for (int q = 0; q < 8; q++) b[q] = nb[q];
       }
+      if (l == 0) {
+        if (failed) atomicOr(rd.rflag + doc, 2u);
+        rd.rchain[(uint64_t)doc * MTE_MAX_CLIENTS + (uint32_t)c] = make_uint2(off, failed ? 0u : m);
+      }
+    } else if ((c % kChWaves) == u && l == 0) {
+      rd.rchain[(uint64_t)doc * MTE_MAX_CLIENTS + (uint32_t)c] = make_uint2(off, 0u);
     }
+    off += cap_c;
   }
+}
+
+// every chain's sub-ops into their chunks' buckets: a thread per list entry
+__global__ __launch_bounds__(256) void rnd_bucket_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd, uint32_t bpd) {
+  __shared__ uint2 chains[MTE_MAX_CLIENTS];
+  const int doc = (int)(blockIdx.x / bpd);
+  const uint4 p = rd.plan[doc];
+  if (p.x != kModeRound || rd.rflag[doc] != 0u) return;
+  if (threadIdx.x < MTE_MAX_CLIENTS) chains[threadIdx.x] = rd.rchain[(uint64_t)doc * MTE_MAX_CLIENTS + threadIdx.x];
+  __syncthreads();
+  const uint32_t e = (blockIdx.x % bpd) * blockDim.x + threadIdx.x;
+  bool mine = false;
+  for (int c = 0; c < MTE_MAX_CLIENTS; c++) mine = mine || (e >= chains[c].x && e < chains[c].x + chains[c].y);
+  if (!mine) return;
+  const uint4 en = rd.rlist[(uint64_t)doc * rd.rl_cap + e];
+  uint32_t* rcnt = rd.rcnt + (uint64_t)doc * ch.nch_cap;
+  const uint32_t pos = atomicAdd(rcnt + en.x, 1u);
+  if (pos < (uint32_t)kRB) rd.rbuf[((uint64_t)doc * ch.nch_cap + en.x) * kRB + pos] = make_uint2(en.y, en.z);
+  else atomicOr(rd.rflag + doc, 1u);
 }
 
 // one wave per chunk of a run: its sub-ops in op order through seg_op_v
@@ -350,28 +510,6 @@ __global__ __launch_bounds__(256) void rnd_apply_kernel(ReplayArgs a, ChunkArgs 
   if (l == 0) {
     cntp[i] = (uint32_t)ni;
     if (rcs != 0) a.hdr[doc].status = MTE_E_STATE;  // resolve guarantees every sub-op fits: an engine bug
-  }
-}
-
-// chunks -> flat planes; the header advanced past the run
-template <int K>
-__global__ __launch_bounds__(512) void rnd_gather_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
-  __shared__ ChCtl ctl;
-  const int doc = (int)blockIdx.x;
-  const uint4 p = rd.plan[doc];
-  if (p.x != kModeRound || rd.rflag[doc] != 0u) return;
-  const int32_t M = (int32_t)p.w;
-  const int32_t n_new = ch_gather<K>(a, ch, doc, &ctl, (int)rd.nch[doc], M);
-  if (threadIdx.x == 0) {
-    const uint64_t kb = a.op_off[doc];
-    const uint32_t ktot = (uint32_t)(a.op_off[doc + 1] - kb);
-    DocHdr h = a.hdr[doc];
-    h.nseg = n_new;
-    h.min_seq = M;
-    h.cur_seq = (int32_t)reinterpret_cast<const uint32_t*>(a.recs + 2 * (kb + p.z - 1))[0];
-    h.resume = p.z;
-    if (p.z >= ktot) h.flags &= ~kHdrNeedsEsc;
-    a.hdr[doc] = h;
   }
 }
 

@@ -2,7 +2,7 @@
 # and without the round phases, kernel stats of the round-phase run
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r03round
+O=gpurun_out/r03round2
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_chunk.py -x -v --timeout 300 --timeout-method thread > $O/chunk_tests.log 2>&1 || exit 1
 timeout -k 10 400 python -u bench.py --config 5 --steps 3 --warmup 1 > $O/bench5_round.json 2> $O/bench5_round.err || exit 1
