@@ -455,6 +455,13 @@ struct mte_ctx {
   bool round_phases = true;
   uint32_t* h_rcount = nullptr;  // pinned: the plan's counts
   uint64_t rl_alloc = 0;         // rd.rlist entries allocated
+  // the round phases can run document slices on their own streams
+  // (MTE_ROUND_STREAMS = slices; default 1, the engine stream alone: 4 slices
+  // measured 72.4 against 49.0 ms per config-5 step, profiles/r03/config5)
+  static constexpr int kRoundStreams = 8;
+  int round_streams = 1;
+  hipStream_t rstream[kRoundStreams] = {};
+  hipEvent_t rev_fork = nullptr, rev_join[kRoundStreams] = {};
   uint64_t* d_off = nullptr;
   mte_propset* d_ps = nullptr;
   mte_prop* d_pe = nullptr;
@@ -618,7 +625,8 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   // contexts, otherwise HBM-resident and streamed per op
   if (c->chunked) {
     const size_t lds = sizeof(uint32_t) * MTE_MAX_CLIENTS * c->ch.ng_cap + sizeof(ChCtl);
-    if (!S && c->round_phases && (uint64_t)(c->ch.nch_cap + c->ch.ng_cap) * 4 <= kRoundLdsMax) {
+    const uint64_t col_bytes = (uint64_t)(c->ch.nch_cap + (c->ch.ng_cap + 63) / 64 * 64 + 64) * 4;
+    if (!S && c->round_phases && col_bytes <= kRoundLdsMax) {
       // round phases (mte_round.h): each phase plans every escalated
       // document's next run, replays the round-shaped runs chunk-parallel and
       // the rest op after op; the host reads the plan's counts to stop
@@ -650,7 +658,29 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
         if (n_round) {
           HIPCHK(c, hipMemsetAsync(rd.rcnt, 0, nch_all * 4, c->stream));
           HIPCHK(c, hipMemsetAsync(rd.rflag, 0, 4 * (uint64_t)c->n_docs, c->stream));
-          HIPCHK(c, (launch_round_run<K>(a, ch, rd, c->n_docs, c->stream)));
+          const int ns = (int)std::min<uint32_t>((uint32_t)c->round_streams, c->n_docs);
+          if (ns <= 1) {
+            rd.d0 = 0;
+            rd.nd = c->n_docs;
+            HIPCHK(c, (launch_round_run<K>(a, ch, rd, c->n_docs, c->stream)));
+          } else {
+            if (!c->rev_fork) {
+              HIPCHK(c, hipEventCreateWithFlags(&c->rev_fork, hipEventDisableTiming));
+              for (int q = 0; q < mte_ctx::kRoundStreams; q++) {
+                HIPCHK(c, hipStreamCreateWithFlags(&c->rstream[q], hipStreamNonBlocking));
+                HIPCHK(c, hipEventCreateWithFlags(&c->rev_join[q], hipEventDisableTiming));
+              }
+            }
+            HIPCHK(c, hipEventRecord(c->rev_fork, c->stream));
+            for (int q = 0; q < ns; q++) {
+              rd.d0 = (uint32_t)((uint64_t)c->n_docs * q / ns);
+              rd.nd = (uint32_t)((uint64_t)c->n_docs * (q + 1) / ns) - rd.d0;
+              HIPCHK(c, hipStreamWaitEvent(c->rstream[q], c->rev_fork, 0));
+              if (rd.nd) HIPCHK(c, (launch_round_run<K>(a, ch, rd, rd.nd, c->rstream[q])));
+              HIPCHK(c, hipEventRecord(c->rev_join[q], c->rstream[q]));
+            }
+            for (int q = 0; q < ns; q++) HIPCHK(c, hipStreamWaitEvent(c->stream, c->rev_join[q], 0));
+          }
         }
         HIPCHK(c, (launch_chunk<K, S>(a, ch, c->n_docs, lds, c->stream)));
       }
@@ -820,6 +850,8 @@ int mte_create(const mte_config* cfg, mte_ctx** out) {
   c->wclock_path = std::getenv("MTE_WAVE_CLOCK");
   if (const char* pp = std::getenv("MTE_PACK_PROPS")) c->pack_props = std::atoi(pp) != 0;
   if (const char* rp = std::getenv("MTE_ROUND_PHASES")) c->round_phases = std::atoi(rp) != 0;
+  if (const char* rs = std::getenv("MTE_ROUND_STREAMS"))
+    c->round_streams = std::max(1, std::min(mte_ctx::kRoundStreams, std::atoi(rs)));
   if (const char* r = std::getenv("MTE_TREE_ROUNDS")) {
     const int v = std::atoi(r);
     c->tree_rounds = v < 0 ? 0 : (v > 64 ? 64 : v);
@@ -868,6 +900,11 @@ int mte_destroy(mte_ctx* c) {
   }
   comm_release(c);
   if (c->h_rcount) (void)hipHostFree(c->h_rcount);
+  for (int q = 0; q < mte_ctx::kRoundStreams; q++) {
+    if (c->rstream[q]) (void)hipStreamDestroy(c->rstream[q]);
+    if (c->rev_join[q]) (void)hipEventDestroy(c->rev_join[q]);
+  }
+  if (c->rev_fork) (void)hipEventDestroy(c->rev_fork);
   if (c->d_comm) (void)hipFree(c->d_comm);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);

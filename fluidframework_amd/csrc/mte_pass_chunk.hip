@@ -17,13 +17,14 @@ MTE_INST(0, false) MTE_INST(0, true) MTE_INST(4, false) MTE_INST(4, true) MTE_IN
 #undef MTE_INST
 
 hipError_t launch_round_plan(const ReplayArgs& a, const RoundArgs& rd, uint32_t n_docs, hipStream_t s) {
-  hipLaunchKernelGGL(rnd_plan_kernel, dim3((n_docs + 3) / 4), dim3(256), 0, s, a, rd);
+  hipLaunchKernelGGL(rnd_plan_kernel, dim3(n_docs), dim3(kChWaves * kWave), 0, s, a, rd);
   return hipGetLastError();
 }
 
 template <int K>
-hipError_t launch_round_run(const ReplayArgs& a, const ChunkArgs& ch, const RoundArgs& rd, uint32_t n_docs,
+hipError_t launch_round_run(const ReplayArgs& a, const ChunkArgs& ch, const RoundArgs& rd, uint32_t,
                             hipStream_t s) {
+  const uint32_t n_docs = rd.nd;  // this launch's slice of the documents
   const uint32_t tpd = (a.cap + kT - 1) / kT;  // flat tiles per document
   const uint64_t tiles = (uint64_t)n_docs * tpd, chunks = (uint64_t)n_docs * ch.nch_cap;
   const dim3 w4(4 * kWave);
@@ -33,7 +34,7 @@ hipError_t launch_round_run(const ReplayArgs& a, const ChunkArgs& ch, const Roun
   hipLaunchKernelGGL((rnd_move_kernel<K>), dim3((uint32_t)((tiles + 3) / 4)), w4, 0, s, a, ch, rd, tpd);
   hipLaunchKernelGGL(rnd_cols_kernel, dim3((uint32_t)((chunks + 3) / 4)), w4, 0, s, a, ch, rd);
   // resolve: the client chains, columns in LDS (two waves per workgroup when they fit)
-  const size_t col = (size_t)(ch.nch_cap + ch.ng_cap) * 4;
+  const size_t col = (size_t)(ch.nch_cap + (ch.ng_cap + kWave - 1) / kWave * kWave + kWave) * 4;
   if (2 * col <= kRoundLdsMax) {
     hipError_t e = hipFuncSetAttribute((const void*)rnd_resolve_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)(2 * col));

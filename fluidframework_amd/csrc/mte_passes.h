@@ -30,6 +30,7 @@ struct RoundArgs {
   uint64_t rl_cap;  // list entries per document: 2 x its ops + 8 per client
   uint2* rchain;    // [doc][MTE_MAX_CLIENTS] (list offset, entries) of each client chain
   uint32_t last;    // this phase sends every active document op after op
+  uint32_t d0, nd;  // the documents [d0, d0 + nd) one launch_round_run covers
 };
 // the round phases fit a context whose per-wave column (nch_cap + ng_cap
 // entries) fits this much LDS

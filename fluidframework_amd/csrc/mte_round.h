@@ -33,7 +33,7 @@
 // lands in the same place relative to every segment that stays.
 //
 // Phases per launch of the chunked pass (host loop, mte_engine.hip):
-//   rnd_plan     one wave per document: the run at its op cursor (mode kRound
+//   rnd_plan     a workgroup per document: the run at its op cursor (mode kRound
 //                if long enough, else the rest goes to the sequential pass);
 //   re-layout    flat planes -> chunks of kChFill segments, dropping
 //                removedSeq <= M (zamboni, mergeTree.ts:1077-1093): keep
@@ -62,62 +62,61 @@ namespace mte {
 
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// one wave per document
-__global__ __launch_bounds__(256) void rnd_plan_kernel(ReplayArgs a, RoundArgs rd) {
+// one workgroup per document: its 8 waves scan the records from the cursor
+// in interleaved batches of 64 for the first op that ends the run
+__global__ __launch_bounds__(512) void rnd_plan_kernel(ReplayArgs a, RoundArgs rd) {
+  __shared__ uint32_t first_bad;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
-  const int doc = (int)blockIdx.x * 4 + w;
-  if (doc >= (int)a.n_docs) return;
+  const int doc = (int)blockIdx.x;
   const DocHdr h = a.hdr[doc];
   const uint64_t kb = a.op_off[doc];
   const uint32_t ktot = (uint32_t)(a.op_off[doc + 1] - kb);
   const bool active = (h.flags & kHdrNeedsEsc) && h.status == 0 && h.resume < ktot;
+  const uint32_t k0 = h.resume, nleft = active ? ktot - k0 : 0u;
+  const bool newcalc = (h.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
+  if (threadIdx.x == 0) first_bad = nleft;
+  __syncthreads();
+  const uint4* recp = a.recs + 2 * (kb + k0);
+  const int32_t M = active ? (int32_t)reinterpret_cast<const uint32_t*>(recp)[2] : 0;
+  if (active && !rd.last && newcalc) {
+    const int32_t R = h.cur_seq;
+    constexpr uint32_t kAllowed = MTE_F_MSG_END | MTE_F_MARKER | MTE_F_REWRITE;
+    for (uint32_t base = (uint32_t)w * kWave; base < nleft; base += kChWaves * kWave) {
+      if (base >= *(volatile uint32_t*)&first_bad) break;  // an earlier op already ends the run
+      uint32_t b[8];
+      ch_rec_batch(b, recp, base);
+      const int32_t s = (int32_t)b[0], r = (int32_t)b[1], m = (int32_t)b[2];
+      const uint32_t type = b[3] & 0xffu, c = (b[3] >> 8) & 0xffu, fl = b[3] >> 16;
+      // the seq of the op before (lane 0: the record before the batch)
+      const int32_t up = __shfl_up(s, 1);
+      const int32_t before = base > 0 ? (int32_t)reinterpret_cast<const uint32_t*>(recp + 2 * (base - 1))[0] : R;
+      const int32_t below = l == 0 ? before : up;
+      const bool in = base + (uint32_t)l < nleft;
+      const bool ok = r == R && m == M && type <= MTE_OP_ANNOTATE && c < MTE_MAX_CLIENTS &&
+                      (fl & MTE_F_MSG_END) && !(fl & ~kAllowed) && s > below && M >= h.min_seq && M <= R &&
+                      (int32_t)b[4] >= 0 && (int32_t)b[5] >= 0;
+      const uint64_t bad = __ballot(in && !ok);
+      if (bad) {
+        if (l == 0) atomicMin(&first_bad, base + (uint32_t)(__ffsll((long long)bad) - 1));
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
   uint4 p = make_uint4(kModeIdle, 0u, 0u, 0u);
   if (active) {
-    const uint32_t k0 = h.resume;
-    uint32_t k1 = k0;
-    int32_t M = 0;
-    const bool newcalc = (h.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
-    if (!rd.last && newcalc) {
-      const uint4* recp = a.recs + 2 * (kb + k0);
-      const int32_t R = h.cur_seq;
-      const uint32_t nleft = ktot - k0;
-      int32_t prev = R;  // seq of the op before this batch of 64
-      constexpr uint32_t kAllowed = MTE_F_MSG_END | MTE_F_MARKER | MTE_F_REWRITE;
-      for (uint32_t base = 0; base < nleft; base += kWave) {
-        uint32_t b[8];
-        ch_rec_batch(b, recp, base);
-        const int32_t s = (int32_t)b[0], r = (int32_t)b[1], m = (int32_t)b[2];
-        const uint32_t type = b[3] & 0xffu, c = (b[3] >> 8) & 0xffu, fl = b[3] >> 16;
-        if (base == 0) M = rdlane(m, 0);
-        // the seq of the lane below (lane 0: the previous batch's last)
-        int32_t below = __shfl_up(s, 1);
-        below = l == 0 ? prev : below;
-        const bool in = base + (uint32_t)l < nleft;
-        const bool ok = r == R && m == M && type <= MTE_OP_ANNOTATE && c < MTE_MAX_CLIENTS &&
-                        (fl & MTE_F_MSG_END) && !(fl & ~kAllowed) && s > below && M >= h.min_seq && M <= R &&
-                        (int32_t)b[4] >= 0 && (int32_t)b[5] >= 0;
-        const uint64_t bad = __ballot(in && !ok);
-        if (bad) {
-          k1 = k0 + base + (uint32_t)(__ffsll((long long)bad) - 1);
-          break;
-        }
-        prev = rdlane(s, kWave - 1);
-        k1 = k0 + base + kWave;
-      }
-      k1 = k1 < ktot ? k1 : ktot;
-    }
-    const uint32_t len = k1 - k0;
+    const uint32_t len = (!rd.last && newcalc) ? first_bad : 0u;
+    const uint32_t k1 = k0 + len;
     // room for every op's segments (an insert or a range op adds at most 3)
     const bool room = (uint64_t)h.nseg + 3ull * len + 2ull <= (uint64_t)a.cap;
     if (len >= kRoundMin && room) p = make_uint4(kModeRound, k0, k1, (uint32_t)M);
     else if (len >= kRoundMin) p = make_uint4(kModeSeq, k0, k1, 0u);  // this run, op after op
     else p = make_uint4(kModeSeq, k0, ktot, 0u);  // not round-shaped: the rest op after op
-    if (l == 0) {
-      atomicAdd(rd.count + (p.x == kModeRound ? 0 : 1), 1u);
-      atomicAdd(rd.count + 2, 1u);
-    }
+    atomicAdd(rd.count + (p.x == kModeRound ? 0 : 1), 1u);
+    atomicAdd(rd.count + 2, 1u);
   }
-  if (l == 0) rd.plan[doc] = p;
+  rd.plan[doc] = p;
 }
 
 // ---- re-layout and gather: many waves per document ---------------------------
@@ -129,8 +128,8 @@ template <int K>
 __global__ __launch_bounds__(256) void rnd_count_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd, uint32_t tpd) {
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
   const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
-  const int doc = (int)(wi / tpd), t = (int)(wi % tpd);
-  if (doc >= (int)a.n_docs) return;
+  const int doc = (int)rd.d0 + (int)(wi / tpd), t = (int)(wi % tpd);
+  if (doc >= (int)(rd.d0 + rd.nd)) return;
   const uint4 p = rd.plan[doc];
   const int n = a.hdr[doc].nseg;
   if (p.x != kModeRound || t * kT >= n) return;
@@ -151,7 +150,7 @@ __global__ __launch_bounds__(256) void rnd_count_kernel(ReplayArgs a, ChunkArgs 
 // the header past the run
 __global__ __launch_bounds__(512) void rnd_scan_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd, int gather) {
   __shared__ ChCtl ctl;
-  const int doc = (int)blockIdx.x;
+  const int doc = (int)rd.d0 + (int)blockIdx.x;
   const uint4 p = rd.plan[doc];
   if (p.x != kModeRound || (gather && rd.rflag[doc] != 0u)) return;
   uint32_t* kc = ch.kc + (uint64_t)doc * ch.nch_cap;
@@ -190,8 +189,8 @@ template <int K>
 __global__ __launch_bounds__(256) void rnd_move_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd, uint32_t tpd) {
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
   const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
-  const int doc = (int)(wi / tpd), t = (int)(wi % tpd);
-  if (doc >= (int)a.n_docs) return;
+  const int doc = (int)rd.d0 + (int)(wi / tpd), t = (int)(wi % tpd);
+  if (doc >= (int)(rd.d0 + rd.nd)) return;
   const uint4 p = rd.plan[doc];
   const int n = a.hdr[doc].nseg;
   if (p.x != kModeRound || t * kT >= n) return;
@@ -230,8 +229,8 @@ __global__ __launch_bounds__(256) void rnd_move_kernel(ReplayArgs a, ChunkArgs c
 __global__ __launch_bounds__(256) void rnd_cols_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
   const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
-  const int doc = (int)(wi / ch.nch_cap), q = (int)(wi % ch.nch_cap);
-  if (doc >= (int)a.n_docs) return;
+  const int doc = (int)rd.d0 + (int)(wi / ch.nch_cap), q = (int)(wi % ch.nch_cap);
+  if (doc >= (int)(rd.d0 + rd.nd)) return;
   const uint4 p = rd.plan[doc];
   if (p.x != kModeRound || q >= (int)rd.nch[doc]) return;
   const int n_new = (int)rd.nnew[doc];
@@ -256,8 +255,8 @@ template <int K>
 __global__ __launch_bounds__(256) void rnd_gmove_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
   const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
-  const int doc = (int)(wi / ch.nch_cap), q = (int)(wi % ch.nch_cap);
-  if (doc >= (int)a.n_docs) return;
+  const int doc = (int)rd.d0 + (int)(wi / ch.nch_cap), q = (int)(wi % ch.nch_cap);
+  if (doc >= (int)(rd.d0 + rd.nd)) return;
   const uint4 p = rd.plan[doc];
   if (p.x != kModeRound || rd.rflag[doc] != 0u || q >= (int)rd.nch[doc]) return;
   const int cn = (int)ch.cnt[(uint64_t)doc * ch.nch_cap + q];
@@ -274,65 +273,114 @@ __global__ __launch_bounds__(256) void rnd_gmove_kernel(ReplayArgs a, ChunkArgs 
   }
 }
 
-// ---- resolve: one wave per client chain, the column in LDS -------------------
+// ---- resolve: one wave per client chain, the column as prefix sums -----------
+// The column is kept in LDS as three levels of inclusive prefix sums over rows
+// of 64: CI[i] = chunk i's prefix within its group of 64 chunks, GS[g] = group
+// g's prefix within its supergroup of 64 groups, SS[s] = supergroup s's prefix
+// over the document.  A position resolves with one LDS read and one ballot
+// per level and no scan; a change d to chunk i adds d to the later entries of
+// the three rows it lies in (one LDS write per lane and level, from the values
+// the search just read).
+struct Col {
+  int32_t* CI;  // nch_cap entries
+  int32_t* GS;  // ng_cap rounded up to 64
+  int32_t* SS;  // 64
+  int nch;
+  int ng, nsg;
+};
 
-// ch_find (mte_chunk.h) over a column in LDS: the first chunk whose inclusive
-// prefix is > x (strict) or >= x; nch if none
-__device__ __forceinline__ int col_find(const uint32_t* G, uint32_t ng, const int32_t* col, int nch, int32_t x,
-                                        bool strict, int32_t* excl, int32_t* total, int32_t* csum) {
+struct ColHit {
+  int i, g, sg;          // chunk, its group and supergroup (i = nch: none)
+  int lc, lg;            // lane of the chunk in its group row, of the group in its supergroup row
+  int32_t excl, csum;    // the chunk's exclusive prefix and length
+  int32_t total;         // the column's total
+  int32_t ci, gs, ss;    // this lane's entries of the three rows, as read
+};
+
+// the first chunk whose inclusive prefix is > x (strict) or >= x
+__device__ __forceinline__ ColHit col_find(const Col& C, int32_t x, bool strict) {
   const int l = lane_id();
-  const uint32_t gpl = (ng + kWave - 1) / kWave;
-  int32_t s = 0;
-  for (uint32_t k = 0; k < gpl; k++) {
-    const uint32_t g = (uint32_t)l * gpl + k;
-    s += g < ng ? (int32_t)G[g] : 0;
+  ColHit h;
+  h.g = h.sg = h.lc = h.lg = 0;
+  h.ci = h.gs = 0;
+  h.ss = l < C.nsg ? C.SS[l] : INT32_MAX / 2;
+  h.total = C.nsg > 0 ? rdlane(h.ss, C.nsg - 1) : 0;
+  const uint64_t ms = __ballot(l < C.nsg && (strict ? h.ss > x : h.ss >= x));
+  if (!ms) {
+    h.i = C.nch;
+    h.excl = h.total;
+    h.csum = 0;
+    return h;
   }
-  const int32_t incl = wave_incl_scan(s);
-  *total = rdlane(incl, kWave - 1);
-  const uint64_t hm = __ballot(strict ? incl > x : incl >= x);
-  if (!hm) {
-    *excl = *total;
-    *csum = 0;
-    return nch;
-  }
-  const int ls = __ffsll((long long)hm) - 1;
-  int32_t run = rdlane(incl - s, ls);
-  uint32_t g = (uint32_t)ls * gpl;
-  for (uint32_t k = 0; k < gpl; k++, g++) {
-    const int32_t v = (int32_t)G[g];
-    if (strict ? run + v > x : run + v >= x) break;
-    run += v;
-  }
-  const int i = (int)g * kChGroup + l;
-  const int32_t v = i < nch ? col[i] : 0;
-  const int32_t ci = wave_incl_scan(v) + run;
-  const uint64_t cm = __ballot(strict ? ci > x : ci >= x);
-  const int lc = cm ? __ffsll((long long)cm) - 1 : kWave - 1;
-  *excl = rdlane(ci - v, lc);
-  *csum = rdlane(v, lc);
-  return (int)g * kChGroup + lc;
+  h.sg = __ffsll((long long)ms) - 1;
+  const int32_t es = h.sg > 0 ? rdlane(h.ss, h.sg - 1) : 0;
+  const int gi = h.sg * kWave + l;
+  h.gs = gi < C.ng ? C.GS[gi] : INT32_MAX / 2;
+  const uint64_t mg = __ballot(gi < C.ng && (strict ? es + h.gs > x : es + h.gs >= x));
+  h.lg = mg ? __ffsll((long long)mg) - 1 : 0;
+  h.g = h.sg * kWave + h.lg;
+  const int32_t eg = es + (h.lg > 0 ? rdlane(h.gs, h.lg - 1) : 0);
+  const int ci = h.g * kChGroup + l;
+  h.ci = ci < C.nch ? C.CI[ci] : INT32_MAX / 2;
+  const uint64_t mc = __ballot(ci < C.nch && (strict ? eg + h.ci > x : eg + h.ci >= x));
+  h.lc = mc ? __ffsll((long long)mc) - 1 : 0;
+  h.i = h.g * kChGroup + h.lc;
+  const int32_t prev = h.lc > 0 ? rdlane(h.ci, h.lc - 1) : 0;
+  h.excl = eg + prev;
+  h.csum = rdlane(h.ci, h.lc) - prev;
+  return h;
+}
+
+// chunk h.i changed by d: the later entries of its three rows
+__device__ __forceinline__ void col_add(const Col& C, const ColHit& h, int32_t d) {
+  const int l = lane_id();
+  const int ci = h.g * kChGroup + l, gi = h.sg * kWave + l;
+  if (l >= h.lc && ci < C.nch) C.CI[ci] = h.ci + d;
+  if (l >= h.lg && gi < C.ng) C.GS[gi] = h.gs + d;
+  if (l >= h.sg && l < C.nsg) C.SS[l] = h.ss + d;
+}
+
+// group gg's row changed by the per-lane amounts o (lane j: chunk gg * 64 + j):
+// CI of the row minus their running sum, the group's and later groups' GS /
+// SS minus their total
+__device__ __forceinline__ void col_sub_row(const Col& C, int gg, int32_t ci_row, int32_t o) {
+  const int l = lane_id();
+  const int32_t oi = wave_incl_scan(o);
+  const int32_t og = rdlane(oi, kWave - 1);
+  const int ci = gg * kChGroup + l;
+  if (ci < C.nch) C.CI[ci] = ci_row - oi;
+  const int sg = gg / kWave, lg = gg % kWave;
+  const int gi = sg * kWave + l;
+  if (l >= lg && gi < C.ng) C.GS[gi] = C.GS[gi] - og;
+  if (l >= sg && l < C.nsg) C.SS[l] = C.SS[l] - og;
 }
 
 // WPB waves per workgroup, 8 / WPB workgroups per document; wave u = 0..7 of
 // the document takes the clients c = u, u + 8, ...; dynamic LDS: per wave a
-// column of nch_cap entries and its group sums
+// CI column of nch_cap entries
 template <int WPB>
 __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
   extern __shared__ uint32_t rs_lds[];
   __shared__ uint32_t ccount[MTE_MAX_CLIENTS];
   constexpr int kBlocksPerDoc = kChWaves / WPB;
-  const int doc = (int)blockIdx.x / kBlocksPerDoc;
+  const int doc = (int)rd.d0 + (int)blockIdx.x / kBlocksPerDoc;
   const uint4 p = rd.plan[doc];
   if (p.x != kModeRound) return;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
   const int u = ((int)blockIdx.x % kBlocksPerDoc) * WPB + w;
   const uint32_t nops = p.z - p.y;
   const uint4* recp = a.recs + 2 * (a.op_off[doc] + p.y);
-  const int nch = (int)rd.nch[doc];
-  const uint32_t ng = (uint32_t)((nch + kChGroup - 1) / kChGroup);
-  const uint32_t stride = ch.nch_cap + ch.ng_cap;
-  int32_t* col = reinterpret_cast<int32_t*>(rs_lds + (uint32_t)w * stride);
-  uint32_t* G = rs_lds + (uint32_t)w * stride + ch.nch_cap;
+  Col C;
+  C.nch = (int)rd.nch[doc];
+  C.ng = (C.nch + kChGroup - 1) / kChGroup;
+  C.nsg = (C.ng + kWave - 1) / kWave;
+  {
+    const uint32_t gs_cap = (ch.ng_cap + kWave - 1) / kWave * kWave;
+    int32_t* base = reinterpret_cast<int32_t*>(rs_lds) + (uint64_t)w * (ch.nch_cap + gs_cap + kWave);
+    C.CI = base;
+    C.GS = base + ch.nch_cap;
+    C.SS = base + ch.nch_cap + gs_cap;
+  }
   const int32_t* sum0 = reinterpret_cast<const int32_t*>(ch.kc + (uint64_t)doc * ch.nch_cap);
   uint4* list = rd.rlist + (uint64_t)doc * rd.rl_cap;
   // ops per client (every workgroup of the document counts them all)
@@ -349,13 +397,28 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
     const uint32_t nc = ccount[c];
     const uint32_t cap_c = nc ? 2u * nc + 8u : 0u;
     if ((c % kChWaves) == u && nc) {
-      // column c = the round-start column, its group sums
-      for (int i = l; i < nch; i += kWave) col[i] = sum0[i];
-      for (uint32_t g = 0; g < ng; g++) {
-        const int i = (int)g * kChGroup + l;
-        const int32_t v = i < nch ? sum0[i] : 0;
-        const int32_t tot = rdlane(wave_incl_scan(v), kWave - 1);
-        if (l == 0) G[g] = (uint32_t)tot;
+      // column c = the round-start column as prefix sums: the chunk rows, then
+      // the group rows from the chunk rows' totals, then the supergroup row
+      for (int g = 0; g < C.ng; g++) {
+        const int i = g * kChGroup + l;
+        const int32_t v = i < C.nch ? sum0[i] : 0;
+        const int32_t incl = wave_incl_scan(v);
+        if (i < C.nch) C.CI[i] = incl;
+        if (l == 0) C.GS[g] = rdlane(incl, kWave - 1);  // the group's total, for now
+      }
+      fence_wave();
+      for (int sg = 0; sg < C.nsg; sg++) {
+        const int g = sg * kWave + l;
+        const int32_t v = g < C.ng ? C.GS[g] : 0;
+        const int32_t incl = wave_incl_scan(v);
+        if (g < C.ng) C.GS[g] = incl;
+        if (l == 0) C.SS[sg] = rdlane(incl, kWave - 1);
+      }
+      fence_wave();
+      {
+        const int32_t v = l < C.nsg ? C.SS[l] : 0;
+        const int32_t incl = wave_incl_scan(v);
+        if (l < C.nsg) C.SS[l] = incl;
       }
       fence_wave();
       uint32_t m = 0;  // entries in the chain's list
@@ -372,63 +435,61 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
           const uint32_t w3 = rdlane(b[3], j);
           const uint32_t type = w3 & 0xffu, flags = w3 >> 16;
           const int32_t pos1 = (int32_t)rdlane(b[4], j), pos2 = (int32_t)rdlane(b[5], j);
-          int32_t ex = 0, total = 0, cs = 0;
           if (type == MTE_OP_INSERT) {
-            const int i0 = col_find(G, ng, col, nch, pos1, false, &ex, &total, &cs);
-            if (pos1 > total || i0 >= nch || m >= cap_c) {  // MTE_E_INSERT_FAILED here: op after op
+            const ColHit h = col_find(C, pos1, false);
+            if (pos1 > h.total || h.i >= C.nch || m >= cap_c) {  // MTE_E_INSERT_FAILED here: op after op
               failed = true;
               break;
             }
             const int32_t nlen = (flags & MTE_F_MARKER) ? 1 : pos2;
-            if (l == 0) {
-              list[off + m] = make_uint4((uint32_t)i0, k, (uint32_t)ex, 0u);
-              if (nlen > 0) {
-                col[i0] = cs + nlen;
-                G[(uint32_t)i0 / kChGroup] += (uint32_t)nlen;
-              }
-            }
+            if (l == 0) list[off + m] = make_uint4((uint32_t)h.i, k, (uint32_t)h.excl, 0u);
             m++;
+            if (nlen > 0) col_add(C, h, nlen);
           } else {
             const int32_t b1 = pos1 < pos2 ? pos1 : pos2, b2 = pos1 < pos2 ? pos2 : pos1;
-            const int i0 = col_find(G, ng, col, nch, b1, true, &ex, &total, &cs);
-            if (i0 < nch) {
+            const ColHit h = col_find(C, b1, true);
+            if (h.i < C.nch) {
               if (b1 == b2) {
                 // ensureIntervalBoundary alone: a split strictly inside a leaf
-                if (ex < b1) {
+                if (h.excl < b1) {
                   if (m >= cap_c) {
                     failed = true;
                     break;
                   }
-                  if (l == 0) list[off + m] = make_uint4((uint32_t)i0, k, (uint32_t)ex, 0u);
+                  if (l == 0) list[off + m] = make_uint4((uint32_t)h.i, k, (uint32_t)h.excl, 0u);
                   m++;
                 }
               } else {
-                // chunks i0 .. while their start is before b2, 64 at a time
-                int32_t run = ex;
-                for (int cb = i0; cb < nch; cb += kWave) {
-                  const int i = cb + l;
-                  const int32_t v = i < nch ? col[i] : 0;
-                  const int32_t incl = wave_incl_scan(v) + run;
-                  const int32_t st = incl - v;
-                  const bool hit = i < nch && v > 0 && st < b2;
+                // group by group from the first chunk's while the chunk starts
+                // are before b2, in the op's perspective before it (eg: the
+                // group's start then)
+                int32_t eg = h.excl - (h.lc > 0 ? rdlane(h.ci, h.lc - 1) : 0);
+                for (int gg = h.g; gg < C.ng; gg++) {
+                  const int i = gg * kChGroup + l;
+                  const int32_t ci = i < C.nch ? C.CI[i] : 0;
+                  const int32_t cprev0 = __shfl_up(ci, 1);
+                  const int32_t cprev = l == 0 ? 0 : cprev0;
+                  const int32_t st = eg + cprev, incl = eg + ci, v = ci - cprev;
+                  const bool hit = i < C.nch && i >= h.i && v > 0 && st < b2;
                   const uint64_t hm = __ballot(hit);
-                  const uint32_t at = m + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32),
-                                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+                  const uint32_t at = m + (uint32_t)__builtin_amdgcn_mbcnt_hi(
+                                              (uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
                   m += (uint32_t)__popcll(hm);
                   if (m > cap_c) {
                     failed = true;
                     break;
                   }
-                  if (hit) {
-                    list[off + at] = make_uint4((uint32_t)i, k, (uint32_t)st, 0u);
-                    if (type == MTE_OP_REMOVE) {
-                      const int32_t lo = b1 > st ? b1 : st, hi = b2 < incl ? b2 : incl;
-                      col[i] = v - (hi - lo);
-                      atomicSub(&G[(uint32_t)i / kChGroup], (uint32_t)(hi - lo));
-                    }
+                  if (hit) list[off + at] = make_uint4((uint32_t)i, k, (uint32_t)st, 0u);
+                  // the group's end before this op
+                  const int last = C.nch - gg * kChGroup < kWave ? C.nch - gg * kChGroup - 1 : kWave - 1;
+                  const int32_t gend = eg + rdlane(ci, last);
+                  if (type == MTE_OP_REMOVE && hm) {
+                    const int32_t lo = b1 > st ? b1 : st, hi = b2 < incl ? b2 : incl;
+                    col_sub_row(C, gg, ci, hit ? hi - lo : 0);
+                    fence_wave();
                   }
-                  run = rdlane(incl, kWave - 1);
-                  if (run >= b2) break;
+                  eg = gend;
+                  if (gend >= b2) break;
                 }
                 if (failed) break;
               }
@@ -453,7 +514,7 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
 // every chain's sub-ops into their chunks' buckets: a thread per list entry
 __global__ __launch_bounds__(256) void rnd_bucket_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd, uint32_t bpd) {
   __shared__ uint2 chains[MTE_MAX_CLIENTS];
-  const int doc = (int)(blockIdx.x / bpd);
+  const int doc = (int)rd.d0 + (int)(blockIdx.x / bpd);
   const uint4 p = rd.plan[doc];
   if (p.x != kModeRound || rd.rflag[doc] != 0u) return;
   if (threadIdx.x < MTE_MAX_CLIENTS) chains[threadIdx.x] = rd.rchain[(uint64_t)doc * MTE_MAX_CLIENTS + threadIdx.x];
@@ -474,8 +535,8 @@ template <int K>
 __global__ __launch_bounds__(256) void rnd_apply_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
   const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
-  const int doc = (int)(wi / ch.nch_cap), i = (int)(wi % ch.nch_cap);
-  if (doc >= (int)a.n_docs) return;
+  const int doc = (int)rd.d0 + (int)(wi / ch.nch_cap), i = (int)(wi % ch.nch_cap);
+  if (doc >= (int)(rd.d0 + rd.nd)) return;
   const uint4 p = rd.plan[doc];
   if (p.x != kModeRound || rd.rflag[doc] != 0u || i >= (int)rd.nch[doc]) return;
   const uint32_t nb = rd.rcnt[(uint64_t)doc * ch.nch_cap + i];
@@ -487,6 +548,13 @@ __global__ __launch_bounds__(256) void rnd_apply_kernel(ReplayArgs a, ChunkArgs 
   const int dst = (l < (int)nb ? (int)rank : l) << 2;
   const uint32_t ks = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)e.x);
   const int32_t exs = __builtin_amdgcn_ds_permute(dst, (int)e.y);
+  // every sub-op's record at once: lane j loads the j-th one (in op order)
+  const uint4* recp = a.recs + 2 * (a.op_off[doc] + p.y);
+  uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0;
+  if (l < (int)nb) {
+    r0 = recp[2 * ks];
+    r1 = recp[2 * ks + 1];
+  }
   uint32_t* cntp = ch.cnt + (uint64_t)doc * ch.nch_cap;
   int ni = (int)cntp[i];
   const uint64_t x0 = ch_slot(ch, doc, i);
@@ -494,12 +562,18 @@ __global__ __launch_bounds__(256) void rnd_apply_kernel(ReplayArgs a, ChunkArgs 
   ch_load<K>(R, ch, x0, ni);
   uint32_t st[kNumStats] = {};
   const int32_t M = (int32_t)p.w;
-  const uint4* recp = a.recs + 2 * (a.op_off[doc] + p.y);
   int rcs = 0;
   for (uint32_t j = 0; j < nb; j++) {
-    const uint32_t k = uni(rdlane(ks, (int)j));
     const int32_t ex = rdlane(exs, (int)j);
-    const s8v op = sload8(recp + 2 * k);
+    s8v op;
+    op[0] = (int32_t)rdlane(r0.x, (int)j);
+    op[1] = (int32_t)rdlane(r0.y, (int)j);
+    op[2] = (int32_t)rdlane(r0.z, (int)j);
+    op[3] = (int32_t)rdlane(r0.w, (int)j);
+    op[4] = (int32_t)rdlane(r1.x, (int)j);
+    op[5] = (int32_t)rdlane(r1.y, (int)j);
+    op[6] = (int32_t)rdlane(r1.z, (int)j);
+    op[7] = (int32_t)rdlane(r1.w, (int)j);
     const uint32_t w3 = (uint32_t)op[3];
     int32_t tot = 0, dlen = 0;
     const int rc = seg_op_v<kChE, K, false, true>(R, ni, op, w3 & 0xffu, (w3 >> 8) & 0xffu, w3 >> 16, M, true, ex,

@@ -1,10 +1,10 @@
-# round phases of the chunked pass: chunk GPU tests, then config 5 bench with
-# and without the round phases, kernel stats of the round-phase run
+# round phases of the chunked pass: chunk GPU tests, then config 5 bench
+# (round phases on 4 streams / 1 stream / off), kernel stats of the default
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r03round2
+O=gpurun_out/r03round6
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_chunk.py -x -v --timeout 300 --timeout-method thread > $O/chunk_tests.log 2>&1 || exit 1
 timeout -k 10 400 python -u bench.py --config 5 --steps 3 --warmup 1 > $O/bench5_round.json 2> $O/bench5_round.err || exit 1
-MTE_ROUND_PHASES=0 timeout -k 10 300 python -u bench.py --config 5 --steps 2 --warmup 1 --no-cpu-baseline > $O/bench5_seq.json 2> $O/bench5_seq.err || exit 1
+MTE_ROUND_STREAMS=1 timeout -k 10 300 python -u bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline > $O/bench5_round1.json 2> $O/bench5_round1.err || exit 1
 timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $O/stats5 -o run --output-format csv -- python3 bench.py --config 5 --steps 2 --warmup 1 --no-cpu-baseline > $O/stats5.json 2> $O/stats5.err || exit 1
