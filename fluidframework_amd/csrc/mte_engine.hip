@@ -428,6 +428,12 @@ struct mte_ctx {
   uint64_t dl_cap_s[2] = {0, 0};
   uint32_t* d_dl_n_s[2] = {nullptr, nullptr};
   uint64_t dl_n_cap_s[2] = {0, 0};
+  // the streamed pass's document order (longest batch first, so the longest
+  // chains start first): the local-client / event documents by this batch's op
+  // count, then the rest; empty without such documents
+  std::vector<uint32_t> h_sdocs;
+  uint32_t* d_sorder_s[2] = {nullptr, nullptr};
+  uint64_t sorder_cap_s[2] = {0, 0};
   int ev_slot = -1;
   // local references of the MTE_DOC_REFS documents (mte_stream.h): ref_cap slots
   // per document, zeroed at every reset
@@ -888,7 +894,7 @@ int mte_destroy(mte_ctx* c) {
     if (p) (void)hipFree(p);
   for (int w = 0; w < 2; w++) {
     void* sl[] = {c->d_ops_s[w], c->d_cps_s[w], c->d_off_s[w], c->d_ps_s[w], c->d_pe_s[w],
-                  c->d_dl_off_s[w], c->d_dl_s[w], c->d_dl_n_s[w]};
+                  c->d_dl_off_s[w], c->d_dl_s[w], c->d_dl_n_s[w], c->d_sorder_s[w]};
     for (void* p : sl)
       if (p) (void)hipFree(p);
     if (c->slot_ev[w]) (void)hipEventDestroy(c->slot_ev[w]);
@@ -956,7 +962,9 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
   c->h_events.assign(n_docs, 0);
   c->h_refs.assign(n_docs, 0);
   bool any_local = false, any_refs = false;
+  c->h_sdocs.clear();
   for (uint32_t d = 0; d < n_docs; d++) {
+    if (docs[d].flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)) c->h_sdocs.push_back(d);
     if (docs[d].flags & MTE_DOC_LOCAL_CLIENT) c->h_local[d] = 1, any_local = true;
     if (docs[d].flags & MTE_DOC_EVENTS) c->h_events[d] = 1;
     if (docs[d].flags & MTE_DOC_REFS) c->h_refs[d] = 1, any_refs = true;
@@ -1225,6 +1233,20 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
   if (b->n_props)
     HIPCHK(c, hipMemcpyAsync(c->d_pe_s[w], b->props, b->n_props * sizeof(mte_prop), hipMemcpyHostToDevice,
                              c->up_stream));
+  if (!c->h_sdocs.empty()) {
+    std::vector<uint32_t> order(c->h_sdocs);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+      return b->op_offsets[x + 1] - b->op_offsets[x] > b->op_offsets[y + 1] - b->op_offsets[y];
+    });
+    std::vector<uint8_t> in(b->n_docs, 0);
+    for (uint32_t d : order) in[d] = 1;
+    for (uint32_t d = 0; d < b->n_docs; d++)
+      if (!in[d]) order.push_back(d);
+    if ((rc = grow(c, &c->d_sorder_s[w], &c->sorder_cap_s[w], (uint64_t)b->n_docs))) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->d_sorder_s[w], order.data(), (size_t)b->n_docs * 4, hipMemcpyHostToDevice,
+                             c->up_stream));
+    HIPCHK(c, hipStreamSynchronize(c->up_stream));  // `order` goes out of scope
+  }
   HIPCHK(c, hipStreamSynchronize(c->up_stream));  // host buffers may be freed after return
   // delta event regions of the MTE_DOC_EVENTS docs (per_op x records + 256 each)
   {
@@ -1303,6 +1325,7 @@ int mte_run(mte_ctx* c) {
   c->ev_slot = evs ? c->rslot : -1;
   a.refs = c->d_refs;
   a.ref_cap = c->ref_cap;
+  a.sorder = c->h_sdocs.empty() ? nullptr : c->d_sorder_s[c->rslot];
   // s_memrealtime runs at 100 MHz: ticks = ms x 1e5, scaled to this batch's ops
   a.eta = (c->last_ms > 0 && c->last_ops > 0) ? (unsigned long long)(c->last_ms * 1e5 * (double)c->n_ops / c->last_ops)
                                               : 0ull;

@@ -107,6 +107,9 @@ struct ReplayArgs {
   // kRefDetached | refType; mte_stream.h)
   uint2* refs;
   uint32_t ref_cap;
+  // the streamed pass's document order (stream_kernel: wave i replays document
+  // sorder[i]), or null for index order
+  const uint32_t* sorder;
 };
 
 // ---- wavefront primitives --------------------------------------------------

@@ -1106,8 +1106,10 @@ template <int K, bool S>
 __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
   __shared__ uint32_t zlds_all[kDocsPerBlock][kWave];
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
-  const int doc = (int)blockIdx.x * kDocsPerBlock + w;
-  if (doc >= (int)a.n_docs) return;
+  const int idx = (int)blockIdx.x * kDocsPerBlock + w;
+  if (idx >= (int)a.n_docs) return;
+  // longest batch first (a.sorder): the long local-client chains start first
+  const int doc = a.sorder ? (int)__builtin_amdgcn_readfirstlane((int)a.sorder[idx]) : idx;
   // documents pass 2 escalated, and every document with a local client
   const uint32_t hf = a.hdr[doc].flags;
   constexpr uint32_t kOwn = MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS;  // docs this pass always replays
