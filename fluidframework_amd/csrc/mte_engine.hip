@@ -19,6 +19,13 @@
 #include "mte_replay.h"
 #include "mte_stream.h"
 #include "mte_chunk.h"
+
+namespace mte {
+// round phases for pass-1-sized documents (mte_pass_rsmall.hip, mte_rsmall.h)
+template <int K>
+hipError_t launch_rsmall(const ReplayArgs& a, uint32_t blocks, hipStream_t s);
+constexpr uint32_t kRsmallMaxDocs = 2560;  // up to ~2.5 documents per SIMD
+}  // namespace mte
 #include "mte_tree.h"
 #include "mte_passes.h"
 
@@ -456,6 +463,9 @@ struct mte_ctx {
   // MTE_PACK_PROPS=0 turns that off
   uint32_t max_vid = 0;
   bool pack_props = true;
+  // round phases for small batches of pass-1 documents (mte_rsmall.h): opt-in
+  // (MTE_RSMALL=1), measured slower than pass 1 at 1,250 documents
+  bool rsmall = false;
   // round phases of the chunked pass (mte_round.h); MTE_ROUND_PHASES=0 turns them off
   RoundArgs rd{};
   bool round_phases = true;
@@ -614,6 +624,11 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   }
   // pass 1: two documents per wavefront (docs up to 126 segments)
   const uint32_t b1 = (c->n_pairs + kPairsPerBlock - 1) / kPairsPerBlock;
+  // a batch too small to fill the SIMDs at one document per wave: its
+  // round-shaped runs first, four waves per document (mte_rsmall.h); pass 1
+  // goes on from where each document stopped
+  if (!S && b1 && c->rsmall && c->pass1_group == 1 && c->n_pairs <= kRsmallMaxDocs)
+    HIPCHK(c, (launch_rsmall<K == kPack4 ? 4 : K>(a, c->n_pairs, c->stream)));
   // with 4 keys whose value ids all fit in a byte (every value the context was
   // ever given), pass 1 holds the four planes as one packed register plane
   if (b1) {
@@ -856,6 +871,7 @@ int mte_create(const mte_config* cfg, mte_ctx** out) {
   c->wclock_path = std::getenv("MTE_WAVE_CLOCK");
   if (const char* pp = std::getenv("MTE_PACK_PROPS")) c->pack_props = std::atoi(pp) != 0;
   if (const char* rp = std::getenv("MTE_ROUND_PHASES")) c->round_phases = std::atoi(rp) != 0;
+  if (const char* rs = std::getenv("MTE_RSMALL")) c->rsmall = std::atoi(rs) != 0;
   if (const char* rs = std::getenv("MTE_ROUND_STREAMS"))
     c->round_streams = std::max(1, std::min(mte_ctx::kRoundStreams, std::atoi(rs)));
   if (const char* r = std::getenv("MTE_TREE_ROUNDS")) {
