@@ -43,7 +43,6 @@ constexpr int kRsE = 2;                          // chunk registers: 128 slots p
 constexpr int kRsCap = kRsW * kRsE * kWave;      // 512 LDS slots per document
 constexpr int kRsChunkMax = kRsE * kWave - 2;    // 126
 constexpr int kRsBucket = 60;                    // sub-ops per chunk and run
-constexpr int kRsSeqMax = 4 * kWave - 2;         // op-after-op fallback: E = 4 registers
 constexpr int kRsGrowMax = 400;                  // past this the document goes back to pass 1 / 2
 
 template <int K>
@@ -54,7 +53,9 @@ struct RsLds {
   int32_t cnt[kRsW];          // chunk sizes after the apply / kept slots in the zamboni
   int32_t vis[kRsW];          // run-start visible length per chunk
   int32_t bn[kRsW];           // sub-ops per chunk
+  int32_t col[MTE_MAX_CLIENTS][kRsW];  // each client's column during the resolve
   int32_t n, k, cur, minq, status, flag, stop;
+  int32_t seqr;     // a run left part-way by the op-after-op path: its refSeq (else INT32_MIN)
   int32_t diag[4];  // diagnostics (MTE_WAVE_CLOCK runs): parallel runs, op-after-op runs, stop reason, ops
 };
 
@@ -148,14 +149,14 @@ __device__ __forceinline__ void rs_zamboni(RsLds<K>& S, int32_t M) {
 // one document per workgroup of kRsW waves: a.pair_docs[blockIdx.x] (pass 1
 // with one document per slot)
 template <int K>
-__global__ __launch_bounds__(kRsW * kWave) void rsmall_kernel(ReplayArgs a) {
+__global__ __launch_bounds__(kRsW * kWave, 5) void rsmall_kernel(ReplayArgs a) {
   __shared__ RsLds<K> S;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
   const int doc = (int)a.pair_docs[blockIdx.x];
   if (doc < 0) return;
   DocRun D;
   run_init(D, a, doc, false);
-  if (!D.running || (D.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)) || D.n + 2 > kRsSeqMax) return;
+  if (!D.running || (D.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)) || D.n > kRsGrowMax) return;
   const bool newcalc = (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
   uint32_t* hp = a.planes + (uint64_t)doc * a.cap;
   for (int i = (int)threadIdx.x; i < D.n; i += kRsW * kWave) {
@@ -169,6 +170,7 @@ __global__ __launch_bounds__(kRsW * kWave) void rsmall_kernel(ReplayArgs a) {
     S.minq = D.min_seq;
     S.status = 0;
     S.stop = 0;
+    S.seqr = INT32_MIN;
     S.diag[0] = S.diag[1] = S.diag[2] = S.diag[3] = 0;
   }
   __syncthreads();
@@ -177,6 +179,10 @@ __global__ __launch_bounds__(kRsW * kWave) void rsmall_kernel(ReplayArgs a) {
   for (;;) {
     const uint32_t k = (uint32_t)S.k;
     const int32_t R = S.cur, m0 = S.minq;
+    // a run the op-after-op path left part-way goes on op after op: its ops
+    // carry the run's refSeq, below the document's currentSeq by now
+    const bool cont = S.seqr != INT32_MIN;
+    const int32_t Rr = cont ? S.seqr : R;
     if (S.stop || S.status || k >= D.k1) break;
     // ---- the run: up to 64 records from the cursor (every wave holds them)
     uint32_t rb[8];
@@ -194,9 +200,9 @@ __global__ __launch_bounds__(kRsW * kWave) void rsmall_kernel(ReplayArgs a) {
       const int32_t up = __shfl_up(s, 1);
       const int32_t below = l == 0 ? R : up;
       const bool in = k + (uint32_t)l < D.k1;
-      const bool ok = in && (int32_t)rb[1] == R && (int32_t)rb[2] == M && type <= MTE_OP_ANNOTATE &&
+      const bool ok = in && (int32_t)rb[1] == Rr && (int32_t)rb[2] == M && type <= MTE_OP_ANNOTATE &&
                       c < MTE_MAX_CLIENTS && (fl & MTE_F_MSG_END) && !(fl & ~kAllowed) && s > below && M >= m0 &&
-                      M <= R && (int32_t)rb[4] >= 0 && (int32_t)rb[5] >= 0;
+                      M <= Rr && (int32_t)rb[4] >= 0 && (int32_t)rb[5] >= 0;
       const uint64_t stopm = __ballot(!ok);
       len = stopm ? __ffsll((long long)stopm) - 1 : kWave;
     }
@@ -226,116 +232,137 @@ __global__ __launch_bounds__(kRsW * kWave) void rsmall_kernel(ReplayArgs a) {
       if (l == 0) S.vis[w] = t;
     }
     __syncthreads();
-    // ---- resolve (wave 0): lane c holds client c's column
-    if (w == 0) {
-      int32_t col[kRsW];
+    // ---- resolve (wave 0), all clients at once: step t takes every client's
+    // t-th op of the run (lane j: op j), each against its client's column
+    if (w == 0 && cont) {
+      if (l == 0) S.flag = 4;  // the rest of a run op after op
+    } else if (w == 0) {
+      const uint32_t w3 = rb[3];
+      const int cj = (int)((w3 >> 8) & 31u);
+      const bool inrun = l < len;
+      // the clients of the run, and each op's rank among its client's ops
+      uint32_t pres = inrun ? 1u << cj : 0u;
+      for (int off = 32; off >= 1; off >>= 1) pres |= (uint32_t)__shfl_xor((int)pres, off);
+      pres = __builtin_amdgcn_readfirstlane(pres);
+      int rank = 0, maxrank = 0;
+      for (uint32_t m = pres; m; m &= m - 1) {
+        const int c = __ffs((int)m) - 1;
+        const uint64_t mc = __ballot(inrun && cj == c);
+        if (inrun && cj == c)
+          rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mc >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mc, 0u));
+        const int nc = __popcll(mc);
+        maxrank = nc > maxrank ? nc : maxrank;
+      }
+      // every present client's column = the run-start visible lengths
+      if (l < MTE_MAX_CLIENTS && ((pres >> l) & 1u)) {
 #pragma unroll
-      for (int u = 0; u < kRsW; u++) col[u] = S.vis[u];
-      int32_t bn[kRsW] = {0, 0, 0, 0};
-      int fail = 0;
-      for (int j = 0; j < len && !fail; j++) {
-        const uint32_t w3 = rdlane(rb[3], j);
-        const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
-        const int32_t pos1 = (int32_t)rdlane(rb[4], j), pos2 = (int32_t)rdlane(rb[5], j);
-        int32_t cc[kRsW];
+        for (int u = 0; u < kRsW; u++) S.col[l][u] = S.vis[u];
+      }
+      if (l < kRsW) S.bn[l] = 0;
+      if (l == 0) S.flag = 0;
+      fence_wave();
+      const uint32_t type = w3 & 0xffu, flags = w3 >> 16;
+      const int32_t pos1 = (int32_t)rb[4], pos2 = (int32_t)rb[5];
+      for (int t = 0; t < maxrank; t++) {
+        if (inrun && rank == t) {
+          int32_t cc[kRsW];
 #pragma unroll
-        for (int u = 0; u < kRsW; u++) cc[u] = rdlane(col[u], (int)c);
-        if (type == MTE_OP_INSERT) {
-          int i0 = -1;
-          int32_t ex = 0, run = 0;
+          for (int u = 0; u < kRsW; u++) cc[u] = S.col[cj][u];
+          if (type == MTE_OP_INSERT) {
+            int i0 = -1;
+            int32_t ex = 0, run = 0;
 #pragma unroll
-          for (int u = 0; u < kRsW; u++) {
-            const int32_t incl = run + cc[u];
-            if (i0 < 0 && incl >= pos1) {
-              i0 = u;
-              ex = run;
-            }
-            run = incl;
-          }
-          if (i0 < 0 || pos1 > run || bn[i0] >= kRsBucket) {
-            fail = 1;
-            break;
-          }
-          if (l == 0) S.bk[i0][bn[i0]] = make_uint2((uint32_t)j, (uint32_t)ex);
-          bn[i0]++;
-          const int32_t nlen = (flags & MTE_F_MARKER) ? 1 : pos2;
-#pragma unroll
-          for (int u = 0; u < kRsW; u++) col[u] += (l == (int)c && u == i0) ? nlen : 0;
-        } else {
-          const int32_t b1 = pos1 < pos2 ? pos1 : pos2, b2 = pos1 < pos2 ? pos2 : pos1;
-          int32_t run = 0;
-          bool first = true;
-#pragma unroll
-          for (int u = 0; u < kRsW; u++) {
-            const int32_t stu = run, incl = run + cc[u];
-            run = incl;
-            if (b1 == b2) {
-              // ensureIntervalBoundary alone: the first chunk reaching past b1, a split strictly inside it
-              if (first && incl > b1) {
-                first = false;
-                if (stu < b1) {
-                  if (bn[u] >= kRsBucket) fail = 1;
-                  else {
-                    if (l == 0) S.bk[u][bn[u]] = make_uint2((uint32_t)j, (uint32_t)stu);
-                    bn[u]++;
-                  }
-                }
+            for (int u = 0; u < kRsW; u++) {
+              const int32_t incl = run + cc[u];
+              if (i0 < 0 && incl >= pos1) {
+                i0 = u;
+                ex = run;
               }
-            } else if (cc[u] > 0 && incl > b1 && stu < b2) {
-              if (bn[u] >= kRsBucket) {
-                fail = 1;
-              } else {
-                if (l == 0) S.bk[u][bn[u]] = make_uint2((uint32_t)j, (uint32_t)stu);
-                bn[u]++;
+              run = incl;
+            }
+            if (i0 < 0 || pos1 > run) {
+              atomicOr(&S.flag, 1);  // MTE_E_INSERT_FAILED at this op: pass 1 replays it
+            } else {
+              const int q = atomicAdd(&S.bn[i0], 1);
+              if (q < kRsBucket) S.bk[i0][q] = make_uint2((uint32_t)l, (uint32_t)ex);
+              const int32_t nlen = (flags & MTE_F_MARKER) ? 1 : pos2;
+              S.col[cj][i0] = cc[i0] + nlen;
+            }
+          } else {
+            const int32_t b1 = pos1 < pos2 ? pos1 : pos2, b2 = pos1 < pos2 ? pos2 : pos1;
+            int32_t run = 0;
+            bool first = true;
+#pragma unroll
+            for (int u = 0; u < kRsW; u++) {
+              const int32_t stu = run, incl = run + cc[u];
+              run = incl;
+              bool emit = false;
+              if (b1 == b2) {
+                // ensureIntervalBoundary alone: the first chunk reaching past b1, a split strictly inside it
+                if (first && incl > b1) {
+                  first = false;
+                  emit = stu < b1;
+                }
+              } else if (cc[u] > 0 && incl > b1 && stu < b2) {
+                emit = true;
                 if (type == MTE_OP_REMOVE) {
                   const int32_t lo = b1 > stu ? b1 : stu, hi = b2 < incl ? b2 : incl;
-                  col[u] -= l == (int)c ? hi - lo : 0;
+                  S.col[cj][u] = cc[u] - (hi - lo);
                 }
+              }
+              if (emit) {
+                const int q = atomicAdd(&S.bn[u], 1);
+                if (q < kRsBucket) S.bk[u][q] = make_uint2((uint32_t)l, (uint32_t)stu);
               }
             }
           }
         }
+        fence_wave();
       }
-      for (int u = 0; u < kRsW; u++)
-        if (S.b[u + 1] - S.b[u] + 2 * bn[u] > kRsChunkMax) fail = 1;
-      if (l == 0) {
-#pragma unroll
-        for (int u = 0; u < kRsW; u++) S.bn[u] = bn[u];
-        S.flag = fail;
-      }
+      if (l < kRsW && (S.bn[l] > kRsBucket || S.b[l + 1] - S.b[l] + 2 * S.bn[l] > kRsChunkMax)) atomicOr(&S.flag, 2);
     }
     __syncthreads();
     if (S.flag) {
-      // ---- op after op on wave 0, the whole document in registers
+      // a run the chunks cannot take (a young document's first rounds land in
+      // one chunk): op after op on wave 0 with the whole document in one
+      // chunk's registers while it fits, else pass 1 goes on from this run
       if (w == 0) {
-        if (n + 2 + 2 * len > kRsSeqMax) {
+        if (n + 2 > kRsChunkMax) {
           if (l == 0) {
             S.stop = 1;
             S.diag[2] = 2;
           }
         } else {
-          Regs<4, K> Rg;
-          rs_load<4, K>(Rg, S, 0, n);
+          // as many of the run's ops as the chunk's registers hold (the rest
+          // start the next run)
+          Regs<kRsE, K> Rg;
+          rs_load<kRsE, K>(Rg, S, 0, n);
           int nn = n;
           int32_t cur = R;
           int done = 0, rc = 0;
           for (int j = 0; j < len; j++) {
+            if (nn + 2 > kRsChunkMax) break;
             const s8v op = rs_rec(rb, j);
             const uint32_t w3 = (uint32_t)op[3];
             int32_t tot = 0, dlen = 0;
-            rc = seg_op_v<4, K, false, false>(Rg, nn, op, w3 & 0xffu, (w3 >> 8) & 0xffu, w3 >> 16, M, newcalc, 0,
-                                              true, tot, dlen, a, st);
+            rc = seg_op_v<kRsE, K, false, false>(Rg, nn, op, w3 & 0xffu, (w3 >> 8) & 0xffu, w3 >> 16, M, newcalc, 0,
+                                                 true, tot, dlen, a, st);
             if (rc < 0) break;
             cur = op[0];
             done++;
           }
-          rs_store<4, K>(Rg, S, 0, nn);
+          rs_store<kRsE, K>(Rg, S, 0, nn);
           if (l == 0) {
             S.n = nn;
             S.k = (int32_t)(k + (uint32_t)done);
             S.cur = cur;
             if (done > 0) S.minq = M;  // the window moves after the run's first op
             if (rc < 0) S.status = rc;
+            S.seqr = done < len ? Rr : INT32_MIN;
+            if (done == 0 && rc == 0) {
+              S.stop = 1;
+              S.diag[2] = 2;
+            }
             S.diag[1]++;
             S.diag[3] += done;
           }
@@ -346,18 +373,30 @@ __global__ __launch_bounds__(kRsW * kWave) void rsmall_kernel(ReplayArgs a) {
       if (S.minq == M && M > m0) rs_zamboni<K>(S, M);
     } else {
       // ---- each wave its chunk and its bucket, in op order
+      const int nb = S.bn[w];
+      // the bucket sorted by op index: lane q holds entry q, its rank among them
+      const uint2 e = l < nb ? S.bk[w][l] : make_uint2(0xffffffffu, 0u);
+      uint32_t rk = 0;
+      for (int q = 0; q < nb; q++) rk += rdlane(e.x, q) < e.x ? 1u : 0u;
+      const int dst = (l < nb ? (int)rk : l) << 2;
+      const uint32_t ks = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)e.x);
+      const int32_t exs = __builtin_amdgcn_ds_permute(dst, (int)e.y);
       Regs<kRsE, K> Rg;
       int ni = ce - cb;
       rs_load<kRsE, K>(Rg, S, cb, ni);
-      const int nb = S.bn[w];
       int rcs = 0;
       for (int q = 0; q < nb; q++) {
-        const uint2 e = S.bk[w][q];
-        const s8v op = rs_rec(rb, (int)e.x);
+        const int j = (int)uni(rdlane(ks, q));
+        const int32_t ex = rdlane(exs, q);
+        s8v op = rs_rec(rb, j);
         const uint32_t w3 = (uint32_t)op[3];
+        const uint32_t type = w3 & 0xffu;
+        // positions relative to the chunk start: the whole-document step on the chunk
+        op[4] -= ex;
+        if (type != MTE_OP_INSERT) op[5] -= ex;
         int32_t tot = 0, dlen = 0;
-        const int rc = seg_op_v<kRsE, K, false, true>(Rg, ni, op, w3 & 0xffu, (w3 >> 8) & 0xffu, w3 >> 16, M,
-                                                      newcalc, (int32_t)e.y, true, tot, dlen, a, st);
+        const int rc = seg_op_v<kRsE, K, false, false>(Rg, ni, op, type, (w3 >> 8) & 0xffu, w3 >> 16, M, newcalc, 0,
+                                                       true, tot, dlen, a, st);
         rcs = rc != 0 ? rc : rcs;
       }
       if (l == 0) S.cnt[w] = ni;

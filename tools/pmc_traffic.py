@@ -1,11 +1,15 @@
 #!/usr/bin/env python3
 """HBM traffic per replay launch from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
 
-Usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON [--workload config3]
+Usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON [--workload config3] [--sum-last-run]
 
 Both passes run `bench.py --steps 1 --warmup 0 --no-cpu-baseline`, so the
 replay kernels are dispatched twice (the accounting run with counters on, then
 the timed run without): the LAST dispatch of each kernel is the timed one.
+With --sum-last-run (a launch that dispatches kernels many times: the chunked
+pass's round phases, config 5) every path kernel dispatched after the last
+begin_batch_kernel (the timed launch's first kernel) is summed instead; run
+bench.py without its side legs so the timed launch is the last one.
 The counters are in KiB.  Corrections per MI355X_MICROARCH.md (HBM/rocprofv3):
 FETCH_SIZE counts half the bytes of wide coalesced reads on gfx950, so it is
 doubled; WRITE_SIZE is taken as is.  The op records are read by scalar loads
@@ -21,7 +25,25 @@ import os
 import sys
 
 PATH_KERNELS = ("begin_batch_kernel", "props_kernel", "round_sync_kernel", "pair_kernel", "big_kernel", "stream_kernel",
-                "chunk_kernel", "tree_kernel")
+                "chunk_kernel", "tree_kernel", "rsmall_kernel", "rnd_plan_kernel", "rnd_count_kernel", "rnd_scan_kernel",
+                "rnd_move_kernel", "rnd_cols_kernel", "rnd_resolve_kernel", "rnd_bucket_kernel", "rnd_apply_kernel",
+                "rnd_gmove_kernel")
+
+
+def last_run_sum(d, counter):
+    """Every path kernel dispatched after the last begin_batch_kernel, summed per kernel."""
+    rows = [r for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv")))
+            if r["Counter_Name"] == counter]
+    starts = [int(r["Dispatch_Id"]) for r in rows if "begin_batch_kernel" in r["Kernel_Name"]]
+    first = max(starts) if starts else -1
+    out = {}
+    for r in rows:
+        name = r["Kernel_Name"]
+        short = next((k for k in PATH_KERNELS if k in name), None)
+        if short is None or int(r["Dispatch_Id"]) < first:
+            continue
+        out[short] = out.get(short, 0.0) + float(r["Counter_Value"])
+    return out
 
 
 def last_dispatch(d, counter):
@@ -42,12 +64,13 @@ def last_dispatch(d, counter):
 
 def main():
     fetch_dir, write_dir, out_json = sys.argv[1:4]
-    workload = sys.argv[5] if len(sys.argv) > 5 and sys.argv[4] == "--workload" else "config3"
+    workload = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else "config3"
+    pick = last_run_sum if "--sum-last-run" in sys.argv else last_dispatch
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     lib = os.path.join(root, "fluidframework_amd", "_lib", "libmte.so")
     sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()
-    f = last_dispatch(fetch_dir, "FETCH_SIZE")
-    w = last_dispatch(write_dir, "WRITE_SIZE")
+    f = pick(fetch_dir, "FETCH_SIZE")
+    w = pick(write_dir, "WRITE_SIZE")
     kern = {}
     for k in sorted(set(f) | set(w)):
         fb = f.get(k, 0.0) * 1024.0
