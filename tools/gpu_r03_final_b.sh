@@ -2,7 +2,7 @@
 # 1,250-document point
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r03final
+O=gpurun_out/r03final2
 mkdir -p $O
 timeout -k 10 400 python -u bench.py --config 5 --steps 3 --warmup 1 > $O/bench5.json 2> $O/bench5.err || exit 1
 P5="python3 bench.py --config 5 --no-cpu-baseline --steps 1 --warmup 0"
