@@ -3,13 +3,14 @@
 // generated stream on disk, with a recording addon instead of the device:
 // prints one JSON line per flush (the shared batch, base64) and a last line
 // with the engine interner's key names and value JSON (to decode properties).
-// argv: dir workers parts
+// argv: dir workers parts [pipelined] (pipelined: one flushParts call, the
+// workers packing part i + 1 while part i is submitted)
 const path = require("path");
 const { MergeTreeEngine } = require("../../fluidframework_amd/node");
 const { ShardedHost } = require("../../fluidframework_amd/node/shards");
 const fs = require("fs");
 
-const [dir, workers, parts] = process.argv.slice(2);
+const [dir, workers, parts, mode] = process.argv.slice(2);
 const b64 = (a) => Buffer.from(a.buffer, a.byteOffset, a.byteLength).toString("base64");
 const lines = [];
 const recorder = {
@@ -27,7 +28,10 @@ const recorder = {
     "fluidframework_amd", "node", "stream_source.js"), sourceData: { dir } });
   await host.start();
   const maxLen = inits.reduce((a, d) => Math.max(a, d.nMsgs), 0);
-  for (let p = 1; p <= Number(parts); p++) await host.flush(Math.floor((maxLen * p) / Number(parts)));
+  const uptos = [];
+  for (let p = 1; p <= Number(parts); p++) uptos.push(Math.floor((maxLen * p) / Number(parts)));
+  if (mode === "pipelined") await host.flushParts(uptos);
+  else for (const u of uptos) await host.flush(u);
   await host.close();
   for (const l of lines) process.stdout.write(JSON.stringify(l) + "\n");
   process.stdout.write(JSON.stringify({ keys: eng.interner.keyNames, values: eng.interner.valueJson }) + "\n");

@@ -379,12 +379,14 @@ def test_node_sequence_delta_events_on_gpu(i):
             assert have and have == want[len(want) - len(have):], (d, have[:2], want[len(want) - len(have):][:2])
 
 
-def test_sharded_host_packs_what_one_packer_packs(tmp_path):
+@pytest.mark.parametrize("mode", ["flush", "pipelined"])
+def test_sharded_host_packs_what_one_packer_packs(tmp_path, mode):
     """ShardedHost (fluidframework_amd/node/shards.js): 3 worker threads pack a
-    60-document config-3 stream in 3 flushes into shared batches; replayed on
-    the restatement, every document's text and per-position properties equal
-    one Python packer's batch of the same messages (the interned ids differ:
-    properties are compared decoded)."""
+    60-document config-3 stream in 3 flushes (or one pipelined flushParts:
+    part i + 1 packed while part i is submitted) into shared batches; replayed
+    on the restatement, every document's text and per-position properties
+    equal one Python packer's batch of the same messages (the interned ids
+    differ: properties are compared decoded)."""
     import base64
     import sys
     sys.path.insert(0, ROOT)
@@ -394,7 +396,7 @@ def test_sharded_host_packs_what_one_packer_packs(tmp_path):
     from fluidframework_amd.packing import BatchBuilder, DocClients, Interner
     stream = gen.generate(3, n_docs=60, ops_per_doc=600)
     write_stream_dir(stream, str(tmp_path), 60)
-    out = node("tests/node/shard_pack.js", str(tmp_path), "3", "3").splitlines()
+    out = node("tests/node/shard_pack.js", str(tmp_path), "3", "3", mode).splitlines()
     tables = json.loads(out[-1])
     sharded = OracleEngine(4)
     gen.load_stream(sharded, stream)
