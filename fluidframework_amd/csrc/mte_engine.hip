@@ -11,6 +11,7 @@
 #include <new>
 #include <type_traits>
 #include <atomic>
+#include <functional>
 #include <string>
 #include <thread>
 #include <vector>
@@ -21,10 +22,6 @@
 #include "mte_chunk.h"
 
 namespace mte {
-// round phases for pass-1-sized documents (mte_pass_rsmall.hip, mte_rsmall.h)
-template <int K>
-hipError_t launch_rsmall(const ReplayArgs& a, uint32_t blocks, hipStream_t s);
-constexpr uint32_t kRsmallMaxDocs = 2560;  // up to ~2.5 documents per SIMD
 }  // namespace mte
 #include "mte_tree.h"
 #include "mte_passes.h"
@@ -463,21 +460,20 @@ struct mte_ctx {
   // MTE_PACK_PROPS=0 turns that off
   uint32_t max_vid = 0;
   bool pack_props = true;
-  // round phases for small batches of pass-1 documents (mte_rsmall.h): opt-in
-  // (MTE_RSMALL=1), measured slower than pass 1 at 1,250 documents
-  bool rsmall = false;
   // round phases of the chunked pass (mte_round.h); MTE_ROUND_PHASES=0 turns them off
   RoundArgs rd{};
   bool round_phases = true;
   uint32_t* h_rcount = nullptr;  // pinned: the plan's counts
   uint64_t rl_alloc = 0;         // rd.rlist entries allocated
-  // the round phases can run document slices on their own streams
-  // (MTE_ROUND_STREAMS = slices; default 1, the engine stream alone: 4 slices
-  // measured 72.4 against 49.0 ms per config-5 step, profiles/r03/config5)
-  static constexpr int kRoundStreams = 8;
-  int round_streams = 1;
-  hipStream_t rstream[kRoundStreams] = {};
-  hipEvent_t rev_fork = nullptr, rev_join[kRoundStreams] = {};
+  // The round phases' host loop (launch_replay) reads each phase's counts back
+  // before launching the next, so it cannot be enqueued ahead: mte_run starts
+  // it on this thread and returns (include/mte.h: mte_run does not wait); every
+  // later call that uses the context's stream or state joins it first
+  // (join_tail), and its error, if any, is returned there.
+  std::thread tail;
+  std::function<int()> tail_fn;
+  int tail_rc = 0;
+  int tail_slot = -1;  // the batch slot the running tail replays
   uint64_t* d_off = nullptr;
   mte_propset* d_ps = nullptr;
   mte_prop* d_pe = nullptr;
@@ -495,6 +491,19 @@ int set_err(mte_ctx* c, int code, const char* fmt, ...) {
   if (c) c->err = buf;
   return code;
 }
+
+// Join the round phases' tail thread of the last mte_run, if any, and hand on
+// its status (mte_ctx::tail).
+int join_tail(mte_ctx* c) {
+  if (c->tail.joinable()) c->tail.join();
+  const int rc = c->tail_rc;
+  c->tail_rc = 0;
+  return rc;
+}
+#define JOIN_TAIL(c)                              \
+  do {                                            \
+    if (const int jr_ = join_tail(c)) return jr_; \
+  } while (0)
 
 // drop this context's reference to its communicator; the last one destroys it
 ncclResult_t comm_release(mte_ctx* c) {
@@ -599,6 +608,49 @@ int launch_reset(mte_ctx* c) {
   return MTE_OK;
 }
 
+// The round phases of the chunked pass (mte_round.h), run by the context's tail
+// thread (mte_ctx::tail): per phase the plan's counts come back to the host,
+// which stops when no document is left or launches the phase's runs.
+template <int K>
+int round_phase_loop(mte_ctx* c, const ReplayArgs& a, size_t lds, uint64_t max_ops) {
+  HIPCHK(c, hipSetDevice(c->device));
+  // the client chains' sub-op lists: 2 x ops + 8 per client, per document
+  const uint64_t rl_cap = 2 * max_ops + 8 * MTE_MAX_CLIENTS;
+  if (rl_cap * c->n_docs > c->rl_alloc) {
+    if (c->rd.rlist) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      HIPCHK(c, hipFree(c->rd.rlist));
+    }
+    c->rd.rlist = nullptr;
+    HIPCHK(c, hipMalloc((void**)&c->rd.rlist, sizeof(uint4) * rl_cap * c->n_docs));
+    c->rl_alloc = rl_cap * c->n_docs;
+  }
+  c->rd.rl_cap = rl_cap;
+  ChunkArgs ch = c->ch;
+  RoundArgs rd = c->rd;
+  ch.plan = rd.plan;
+  ch.rflag = rd.rflag;
+  const uint64_t nch_all = (uint64_t)c->n_docs * ch.nch_cap;
+  for (int ph = 0; ph < kMaxPhases; ph++) {
+    rd.last = ph == kMaxPhases - 1 ? 1u : 0u;
+    HIPCHK(c, hipMemsetAsync(rd.count, 0, 16, c->stream));
+    HIPCHK(c, launch_round_plan(a, rd, c->n_docs, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_rcount, rd.count, 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint32_t n_round = c->h_rcount[0], n_active = c->h_rcount[2];
+    if (n_active == 0) break;
+    if (n_round) {
+      HIPCHK(c, hipMemsetAsync(rd.rcnt, 0, nch_all * 4, c->stream));
+      HIPCHK(c, hipMemsetAsync(rd.rflag, 0, 4 * (uint64_t)c->n_docs, c->stream));
+      rd.d0 = 0;
+      rd.nd = c->n_docs;
+      HIPCHK(c, (launch_round_run<K>(a, ch, rd, c->n_docs, c->stream)));
+    }
+    HIPCHK(c, (launch_chunk<K, false>(a, ch, c->n_docs, lds, c->stream)));
+  }
+  return MTE_OK;
+}
+
 template <int K, bool S>
 int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   // the tree pass: legacy length calc documents (mte_tree.h), up to 252
@@ -624,11 +676,6 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   }
   // pass 1: two documents per wavefront (docs up to 126 segments)
   const uint32_t b1 = (c->n_pairs + kPairsPerBlock - 1) / kPairsPerBlock;
-  // a batch too small to fill the SIMDs at one document per wave: its
-  // round-shaped runs first, four waves per document (mte_rsmall.h); pass 1
-  // goes on from where each document stopped
-  if (!S && b1 && c->rsmall && c->pass1_group == 1 && c->n_pairs <= kRsmallMaxDocs)
-    HIPCHK(c, (launch_rsmall<K == kPack4 ? 4 : K>(a, c->n_pairs, c->stream)));
   // with 4 keys whose value ids all fit in a byte (every value the context was
   // ever given), pass 1 holds the four planes as one packed register plane
   if (b1) {
@@ -650,69 +697,18 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
     if (!S && c->round_phases && col_bytes <= kRoundLdsMax) {
       // round phases (mte_round.h): each phase plans every escalated
       // document's next run, replays the round-shaped runs chunk-parallel and
-      // the rest op after op; the host reads the plan's counts to stop
-      // the client chains' sub-op lists: 2 x ops + 8 per client, per document
-      const uint64_t rl_cap = 2 * c->max_doc_ops_s[c->rslot] + 8 * MTE_MAX_CLIENTS;
-      if (rl_cap * c->n_docs > c->rl_alloc) {
-        if (c->rd.rlist) {
-          HIPCHK(c, hipStreamSynchronize(c->stream));
-          HIPCHK(c, hipFree(c->rd.rlist));
-        }
-        c->rd.rlist = nullptr;
-        HIPCHK(c, hipMalloc((void**)&c->rd.rlist, sizeof(uint4) * rl_cap * c->n_docs));
-        c->rl_alloc = rl_cap * c->n_docs;
-      }
-      c->rd.rl_cap = rl_cap;
-      ChunkArgs ch = c->ch;
-      RoundArgs rd = c->rd;
-      ch.plan = rd.plan;
-      ch.rflag = rd.rflag;
-      const uint64_t nch_all = (uint64_t)c->n_docs * ch.nch_cap;
-      for (int ph = 0; ph < kMaxPhases; ph++) {
-        rd.last = ph == kMaxPhases - 1 ? 1u : 0u;
-        HIPCHK(c, hipMemsetAsync(rd.count, 0, 16, c->stream));
-        HIPCHK(c, launch_round_plan(a, rd, c->n_docs, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->h_rcount, rd.count, 16, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        const uint32_t n_round = c->h_rcount[0], n_active = c->h_rcount[2];
-        if (n_active == 0) break;
-        if (n_round) {
-          HIPCHK(c, hipMemsetAsync(rd.rcnt, 0, nch_all * 4, c->stream));
-          HIPCHK(c, hipMemsetAsync(rd.rflag, 0, 4 * (uint64_t)c->n_docs, c->stream));
-          const int ns = (int)std::min<uint32_t>((uint32_t)c->round_streams, c->n_docs);
-          if (ns <= 1) {
-            rd.d0 = 0;
-            rd.nd = c->n_docs;
-            HIPCHK(c, (launch_round_run<K>(a, ch, rd, c->n_docs, c->stream)));
-          } else {
-            if (!c->rev_fork) {
-              HIPCHK(c, hipEventCreateWithFlags(&c->rev_fork, hipEventDisableTiming));
-              for (int q = 0; q < mte_ctx::kRoundStreams; q++) {
-                HIPCHK(c, hipStreamCreateWithFlags(&c->rstream[q], hipStreamNonBlocking));
-                HIPCHK(c, hipEventCreateWithFlags(&c->rev_join[q], hipEventDisableTiming));
-              }
-            }
-            HIPCHK(c, hipEventRecord(c->rev_fork, c->stream));
-            for (int q = 0; q < ns; q++) {
-              rd.d0 = (uint32_t)((uint64_t)c->n_docs * q / ns);
-              rd.nd = (uint32_t)((uint64_t)c->n_docs * (q + 1) / ns) - rd.d0;
-              HIPCHK(c, hipStreamWaitEvent(c->rstream[q], c->rev_fork, 0));
-              if (rd.nd) HIPCHK(c, (launch_round_run<K>(a, ch, rd, rd.nd, c->rstream[q])));
-              HIPCHK(c, hipEventRecord(c->rev_join[q], c->rstream[q]));
-            }
-            for (int q = 0; q < ns; q++) HIPCHK(c, hipStreamWaitEvent(c->stream, c->rev_join[q], 0));
-          }
-        }
-        HIPCHK(c, (launch_chunk<K, S>(a, ch, c->n_docs, lds, c->stream)));
-      }
+      // the rest op after op; the host reads the plan's counts to stop.  The
+      // loop runs on the context's tail thread (mte_run returns at once).
+      const uint64_t max_ops = c->max_doc_ops_s[c->rslot];
+      c->tail_fn = [c, a, lds, max_ops]() -> int { return round_phase_loop<K>(c, a, lds, max_ops); };
+      return MTE_OK;  // the tail joins the tree stream after the loop
     } else {
       HIPCHK(c, (launch_chunk<K, S>(a, c->ch, c->n_docs, lds, c->stream)));
     }
   } else {
     HIPCHK(c, (launch_stream<K, S>(a, b2, c->stream)));
   }
-  if (c->n_tree) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
-  return MTE_OK;
+  return MTE_OK;  // mte_run joins the tree stream (finish)
 }
 
 // Validation of one op record (the kernels index with these fields, so a bad
@@ -871,9 +867,6 @@ int mte_create(const mte_config* cfg, mte_ctx** out) {
   c->wclock_path = std::getenv("MTE_WAVE_CLOCK");
   if (const char* pp = std::getenv("MTE_PACK_PROPS")) c->pack_props = std::atoi(pp) != 0;
   if (const char* rp = std::getenv("MTE_ROUND_PHASES")) c->round_phases = std::atoi(rp) != 0;
-  if (const char* rs = std::getenv("MTE_RSMALL")) c->rsmall = std::atoi(rs) != 0;
-  if (const char* rs = std::getenv("MTE_ROUND_STREAMS"))
-    c->round_streams = std::max(1, std::min(mte_ctx::kRoundStreams, std::atoi(rs)));
   if (const char* r = std::getenv("MTE_TREE_ROUNDS")) {
     const int v = std::atoi(r);
     c->tree_rounds = v < 0 ? 0 : (v > 64 ? 64 : v);
@@ -902,6 +895,7 @@ int mte_create(const mte_config* cfg, mte_ctx** out) {
 
 int mte_destroy(mte_ctx* c) {
   if (!c) return MTE_E_INVALID_ARG;
+  (void)join_tail(c);
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   free_docs(c);
@@ -922,11 +916,6 @@ int mte_destroy(mte_ctx* c) {
   }
   comm_release(c);
   if (c->h_rcount) (void)hipHostFree(c->h_rcount);
-  for (int q = 0; q < mte_ctx::kRoundStreams; q++) {
-    if (c->rstream[q]) (void)hipStreamDestroy(c->rstream[q]);
-    if (c->rev_join[q]) (void)hipEventDestroy(c->rev_join[q]);
-  }
-  if (c->rev_fork) (void)hipEventDestroy(c->rev_fork);
   if (c->d_comm) (void)hipFree(c->d_comm);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
@@ -942,6 +931,7 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
                   uint64_t text_units, const mte_propset* propsets, uint32_t n_propsets,
                   const mte_prop* props, uint32_t n_props) {
   if (!c || (n_docs && !docs) || (text_units && !text)) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   std::vector<uint32_t> iprops((size_t)n_docs * MTE_MAX_KEYS, 0u);
@@ -1122,6 +1112,7 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
 
 int mte_load_segments(mte_ctx* c, const uint64_t* seg_offsets, const mte_seg* segs, uint64_t n_segs) {
   if (!c || !seg_offsets || (n_segs && !segs)) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   if (!c->n_docs) return MTE_OK;
   if (seg_offsets[0] != 0 || seg_offsets[c->n_docs] != n_segs)
     return set_err(c, MTE_E_INVALID_ARG, "seg_offsets must run from 0 to n_segs");
@@ -1216,6 +1207,7 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
   // the other slot than the one mte_run replays now; its buffers are written
   // once the last run that read them is done
   const int w = c->submitted ? c->rslot ^ 1 : c->rslot;
+  if (c->tail.joinable() && w == c->tail_slot) JOIN_TAIL(c);  // a second submit without mte_run
   HIPCHK(c, hipStreamWaitEvent(c->up_stream, c->slot_ev[w], 0));
   // the replay kernels read the records in place; kRecPad zeroed records
   // follow the last one for the L2 prefetch that runs ahead
@@ -1306,6 +1298,7 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
 
 int mte_run(mte_ctx* c) {
   if (!c) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   if (!c->submitted) return set_err(c, MTE_E_STATE, "mte_run before mte_submit");
   if (!c->n_docs) return MTE_OK;
   HIPCHK(c, hipSetDevice(c->device));
@@ -1366,14 +1359,30 @@ int mte_run(mte_ctx* c) {
     rc = c->kt == 0 ? launch_replay<0, false>(c, a)
                     : (c->kt == 4 ? launch_replay<4, false>(c, a) : launch_replay<8, false>(c, a));
   if (rc) return rc;
-  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-  HIPCHK(c, hipEventRecord(c->slot_ev[c->rslot], c->stream));  // the slot may be rewritten after this
   c->ran = true;
+  const int slot = c->rslot;
+  auto finish = [c, slot]() -> int {
+    if (c->n_tree) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipEventRecord(c->slot_ev[slot], c->stream));  // the slot may be rewritten after this
+    return MTE_OK;
+  };
+  if (!c->tail_fn) return finish();
+  // the round phases' host loop goes on on the tail thread; mte_run returns
+  std::function<int()> fn = std::move(c->tail_fn);
+  c->tail_fn = nullptr;
+  c->tail_slot = slot;
+  c->tail = std::thread([c, fn, finish]() {
+    int r = fn();
+    if (!r) r = finish();
+    c->tail_rc = r;
+  });
   return MTE_OK;
 }
 
 int mte_sync(mte_ctx* c) {
   if (!c) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (c->ran) {
@@ -1396,12 +1405,14 @@ int mte_sync(mte_ctx* c) {
 
 int mte_reset(mte_ctx* c) {
   if (!c) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   HIPCHK(c, hipSetDevice(c->device));
   return launch_reset(c);
 }
 
 int mte_digest_device(mte_ctx* c, void* out, uint32_t n_docs) {
   if (!c || !out || n_docs != c->n_docs) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   if (!n_docs) return MTE_OK;
   HIPCHK(c, hipSetDevice(c->device));
   DigestArgs a;
@@ -1421,6 +1432,7 @@ int mte_digest_device(mte_ctx* c, void* out, uint32_t n_docs) {
 
 int mte_digest(mte_ctx* c, uint64_t* out, uint32_t n_docs) {
   if (!c || !out || n_docs != c->n_docs) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   if (!n_docs) return MTE_OK;
   int rc = mte_digest_device(c, c->d_digest, n_docs);
   if (rc) return rc;
@@ -1431,6 +1443,7 @@ int mte_digest(mte_ctx* c, uint64_t* out, uint32_t n_docs) {
 
 int mte_doc_status(mte_ctx* c, int32_t* out, uint32_t n_docs) {
   if (!c || !out || n_docs != c->n_docs) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   if (!n_docs) return MTE_OK;
   HIPCHK(c, hipSetDevice(c->device));
   std::vector<DocHdr> h(n_docs);
@@ -1442,6 +1455,7 @@ int mte_doc_status(mte_ctx* c, int32_t* out, uint32_t n_docs) {
 
 int mte_read_doc(mte_ctx* c, uint32_t doc, mte_doc_view* v) {
   if (!c || !v || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   HIPCHK(c, hipSetDevice(c->device));
   DocHdr h;
   HIPCHK(c, hipMemcpyAsync(&h, c->hdr + doc, sizeof(DocHdr), hipMemcpyDeviceToHost, c->stream));
@@ -1497,12 +1511,14 @@ int mte_read_doc(mte_ctx* c, uint32_t doc, mte_doc_view* v) {
 
 int mte_set_event_capacity(mte_ctx* c, uint32_t per_op) {
   if (!c || per_op == 0 || per_op > (1u << 16)) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   c->ev_per_op = per_op;
   return MTE_OK;
 }
 
 int mte_set_ref_capacity(mte_ctx* c, uint32_t per_doc) {
   if (!c || per_doc == 0 || per_doc > (1u << 20)) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   if (c->d_refs) return set_err(c, MTE_E_STATE, "mte_set_ref_capacity after mte_load_docs of MTE_DOC_REFS documents");
   c->ref_cap = per_doc;
   return MTE_OK;
@@ -1514,6 +1530,7 @@ int mte_set_ref_capacity(mte_ctx* c, uint32_t per_doc) {
 // unit no segment holds any more (a tombstone compacted at minSeq)
 int mte_read_refs(mte_ctx* c, uint32_t doc, int32_t* pos, uint32_t n) {
   if (!c || (n && !pos) || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   if (c->h_refs.empty() || !c->h_refs[doc]) return set_err(c, MTE_E_INVALID_ARG, "doc %u: no MTE_DOC_REFS", doc);
   if (n > c->ref_cap) return set_err(c, MTE_E_INVALID_ARG, "%u reference slots > capacity %u", n, c->ref_cap);
   HIPCHK(c, hipSetDevice(c->device));
@@ -1551,6 +1568,7 @@ int mte_read_refs(mte_ctx* c, uint32_t doc, int32_t* pos, uint32_t n) {
 
 int mte_read_deltas(mte_ctx* c, uint32_t doc, mte_delta* out, uint64_t cap, uint64_t* n) {
   if (!c || !n || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   *n = 0;
   if (c->h_events.empty() || !c->h_events[doc]) return set_err(c, MTE_E_INVALID_ARG, "doc %u: no MTE_DOC_EVENTS", doc);
   if (c->ev_slot < 0) return MTE_OK;  // no batch with events ran yet
@@ -1570,6 +1588,7 @@ int mte_read_deltas(mte_ctx* c, uint32_t doc, mte_delta* out, uint64_t cap, uint
 
 int mte_read_segments(mte_ctx* c, uint32_t doc, mte_seg_list* v) {
   if (!c || !v || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   HIPCHK(c, hipSetDevice(c->device));
   DocHdr h;
   HIPCHK(c, hipMemcpyAsync(&h, c->hdr + doc, sizeof(DocHdr), hipMemcpyDeviceToHost, c->stream));
@@ -1627,6 +1646,7 @@ int mte_read_segments(mte_ctx* c, uint32_t doc, mte_seg_list* v) {
 
 int mte_set_stats(mte_ctx* c, int enable) {
   if (!c) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   c->stats_on = enable != 0;
   return MTE_OK;
 }
@@ -1650,6 +1670,7 @@ int mte_comm_unique_id(uint8_t id[MTE_COMM_ID_BYTES]) {
 
 int mte_comm_init(mte_ctx* c, int world, int rank, const uint8_t id[MTE_COMM_ID_BYTES]) {
   if (!c || !id || world < 1 || rank < 0 || rank >= world) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   if (c->comm) return set_err(c, MTE_E_STATE, "mte_comm_init: already initialised");
   HIPCHK(c, hipSetDevice(c->device));
   ncclUniqueId u;
@@ -1666,6 +1687,7 @@ int mte_comm_init(mte_ctx* c, int world, int rank, const uint8_t id[MTE_COMM_ID_
 
 int mte_comm_share(mte_ctx* c, const mte_ctx* src) {
   if (!c || !src || !src->comm || src->device != c->device) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   if (c->comm) return set_err(c, MTE_E_STATE, "mte_comm_share: already has a communicator");
   src->cref->refs.fetch_add(1);
   c->cref = src->cref;
@@ -1688,6 +1710,7 @@ int comm_staging(mte_ctx* c, uint64_t n) {
 
 int mte_comm_allreduce_f64(mte_ctx* c, double* v, int op) {
   if (!c || !v || (op != MTE_COMM_SUM && op != MTE_COMM_MAX)) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   if (!c->comm) return set_err(c, MTE_E_STATE, "mte_comm_init first");
   HIPCHK(c, hipSetDevice(c->device));
   int rc = comm_staging(c, 1);
@@ -1714,6 +1737,7 @@ int mte_comm_world(const mte_ctx* c, int32_t* world, int32_t* rank) {
 
 int mte_comm_gather_digests(mte_ctx* c, uint64_t* out, uint64_t out_cap, uint32_t docs_per_rank) {
   if (!c || !out || docs_per_rank < c->n_docs) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   if (!c->comm) return set_err(c, MTE_E_STATE, "mte_comm_init first");
   if (out_cap < 4ull * docs_per_rank * (uint64_t)c->world)
     return set_err(c, MTE_E_INVALID_ARG, "mte_comm_gather_digests: out holds %llu uint64, needs world %d x %u docs x 4",
@@ -1734,6 +1758,7 @@ int mte_comm_gather_digests(mte_ctx* c, uint64_t* out, uint64_t out_cap, uint32_
 
 int mte_comm_destroy(mte_ctx* c) {
   if (!c) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   HIPCHK(c, hipSetDevice(c->device));
   const ncclResult_t r = comm_release(c);
   if (r != ncclSuccess) return set_err(c, MTE_E_HIP, "ncclCommDestroy: %s", ncclGetErrorString(r));
@@ -1744,6 +1769,7 @@ int mte_comm_destroy(mte_ctx* c) {
 
 int mte_stats_get(mte_ctx* c, mte_stats* o) {
   if (!c || !o) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
   std::memset(o, 0, sizeof(*o));
   if (!c->n_docs) return MTE_OK;
   HIPCHK(c, hipSetDevice(c->device));

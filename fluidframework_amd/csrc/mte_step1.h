@@ -14,11 +14,6 @@
 #pragma once
 
 #include "mte_kernels.h"
-#include "mte_lean.h"
-
-#ifndef MTE_LEAN  // 1: the E = 1 / 2 tiers run lean_seg_op (mte_lean.h; an A/B variant, measured slower)
-#define MTE_LEAN 0
-#endif
 
 namespace mte {
 
@@ -428,15 +423,9 @@ __device__ __forceinline__ int doc_step_v(Regs<E, K>& R, DocRun& D, uint32_t (&s
 
   if (type <= MTE_OP_ANNOTATE) {
     MTE_STAT(st[kStScanned] += (uint32_t)n;)
-    int rc;
-    if constexpr (MTE_LEAN && E <= 2) {
-      rc = lean_seg_op<E, K, S>(R, n, op, type, c, flags, D.min_seq, (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0, a,
-                                st);
-    } else {
-      int32_t tot, dlen;
-      rc = seg_op_v<E, K, S, false>(R, n, op, type, c, flags, D.min_seq, (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0, 0,
-                                    true, tot, dlen, a, st);
-    }
+    int32_t tot, dlen;
+    const int rc = seg_op_v<E, K, S, false>(R, n, op, type, c, flags, D.min_seq, (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0,
+                                            0, true, tot, dlen, a, st);
     if (rc) return rc;
   } else if (type != MTE_OP_NOOP) {
     return MTE_E_INVALID_ARG;

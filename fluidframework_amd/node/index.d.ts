@@ -40,6 +40,9 @@ export interface EngineOptions {
   device?: number;
   nKeys?: number;
   segCapacity?: number;
+  /** local reference slots per document (mte_set_ref_capacity, default 1024); a
+   *  reference past it throws for its document (MergeTreeError code -4) */
+  refCapacity?: number;
 }
 
 /** IJSONSegmentWithMergeInfo (snapshotChunks.ts:48-78): one segment of a summary body. */

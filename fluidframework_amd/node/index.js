@@ -96,6 +96,10 @@ class MergeTreeEngine {
     this.nKeys = o.nKeys === undefined ? 8 : o.nKeys;
     this.addon = o.addon || loadAddon();  // o.addon: another binding of the same functions (tests)
     this.ctx = this.addon.create(o.device || 0, this.nKeys, o.segCapacity || 0);
+    // reference slots per document (mte_set_ref_capacity, default 1024): every
+    // document's packer refuses a reference past it
+    this.refCapacity = o.refCapacity === undefined ? 1024 : o.refCapacity;
+    if (o.refCapacity !== undefined) this.addon.setRefCapacity(this.ctx, o.refCapacity);
     this.interner = new Interner(this.nKeys);
     this.docs = [];
     this.clients = [];
@@ -374,6 +378,7 @@ class BatchClient {
     this.doc = doc;
     this.longClientId = observerId;
     this.clients = new DocClients(observerId, engine.docs[doc].minSeq, local);
+    this.clients.refCap = engine.refCapacity;
     this.lastMinSeq = 0;
     const self = this;
     // MergeTree-level entry points (clientId = short id, as in the reference)

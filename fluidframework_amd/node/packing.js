@@ -49,7 +49,8 @@ const DOC_ROUND_SYNC = 0x2; // MTE_DOC_ROUND_SYNC (include/mte.h)
 const DOC_LOCAL_CLIENT = 0x4; // MTE_DOC_LOCAL_CLIENT
 const DOC_REFS = 0x10;       // MTE_DOC_REFS
 const DOC_EVENTS = 0x8; // MTE_DOC_EVENTS
-const E_INVALID_ARG = -1, E_UNSUPPORTED = -9, E_STATE = -10, E_CLIENT_RANGE = -12;
+const E_INVALID_ARG = -1, E_CAPACITY = -4, E_UNSUPPORTED = -9, E_STATE = -10, E_CLIENT_RANGE = -12;
+const DEFAULT_REF_CAPACITY = 1024;  // mte_set_ref_capacity's default (include/mte.h)
 
 class MergeTreeError extends Error {
   constructor(code, message) {
@@ -173,6 +174,10 @@ class DocClients {
     // removed ones, reused first (as packing.py)
     this.refNext = 0;
     this.refFree = [];
+    // the context's reference slots per document (MergeTreeEngine refCapacity,
+    // mte_set_ref_capacity): a slot past it would fail the whole batch at
+    // mte_submit, so the packer refuses the reference for this document alone
+    this.refCap = DEFAULT_REF_CAPACITY;
   }
   short(longId, seq) {
     let i = longId === this.lastId ? this.lastSlot : this.ids.get(longId);
@@ -604,9 +609,12 @@ class BatchBuilder {
   }
 
   _refSlot(clients) {
-    const slot = clients.refFree.length ? clients.refFree.pop() : clients.refNext;
-    if (slot === clients.refNext) clients.refNext++;
-    return slot;
+    if (clients.refFree.length) return clients.refFree.pop();
+    if (clients.refNext >= clients.refCap) {
+      throw new MergeTreeError(E_CAPACITY, "more than " + clients.refCap +
+        " live local references in one document (MergeTreeEngine refCapacity)");
+    }
+    return clients.refNext++;
   }
 
   /** A reference a sequenced op creates (createPositionReference with an op,

@@ -30,7 +30,7 @@ import json
 
 import numpy as np
 
-from .abi import (F_LOCAL, F_MARKER, F_MSG_END, F_REWRITE, LOCAL_SEQ_BASE, MTE_E_CLIENT_RANGE,
+from .abi import (F_LOCAL, F_MARKER, F_MSG_END, F_REWRITE, LOCAL_SEQ_BASE, MTE_E_CAPACITY, MTE_E_CLIENT_RANGE,
                   MTE_E_INVALID_ARG, MTE_E_STATE, MTE_E_UNSUPPORTED, MTE_MAX_CLIENTS, NO_PROPS, OP_ACK, OP_ROLLBACK,
                   OP_REGEN, OP_RBKEY, OP_REF, ANNOTATE_SLOTS, REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE,
                   REF_TRANSIENT,
@@ -119,6 +119,21 @@ class PropTable:
         return ps, pe
 
 
+DEFAULT_REF_CAPACITY = 1024  # mte_set_ref_capacity's default (include/mte.h)
+
+
+def _ref_slot(clients) -> int:
+    """The next reference slot of a document: a removed one first, else a new one,
+    which must stay below the context's per-document capacity (clients.ref_cap)."""
+    if clients.ref_free:
+        return clients.ref_free.pop()
+    if clients.ref_next >= clients.ref_cap:
+        raise MergeTreeError(MTE_E_CAPACITY, f"more than {clients.ref_cap} live local references in one "
+                             "document (mte_set_ref_capacity)")
+    clients.ref_next += 1
+    return clients.ref_next - 1
+
+
 class DocClients:
     """Per-document long -> short client id map (client.ts:683-698).
 
@@ -159,6 +174,10 @@ class DocClients:
         # the removed ones, reused first
         self.ref_next = 0
         self.ref_free = []
+        # the context's reference slots per document (mte_set_ref_capacity); a slot
+        # at or past it would fail the whole batch at mte_submit, so the packer
+        # refuses the reference for this document alone
+        self.ref_cap = DEFAULT_REF_CAPACITY
 
     def short(self, long_id, seq=None) -> int:
         i = self.ids.get(long_id)
@@ -393,9 +412,7 @@ class BatchBuilder:
             raise MergeTreeError(MTE_E_UNSUPPORTED, "Transient local references (positions are not tracked)")
         if ref_type & REF_SLIDE_ON_REMOVE and ref_type & REF_STAY_ON_REMOVE:
             raise MergeTreeError(MTE_E_INVALID_ARG, "SlideOnRemove and StayOnRemove together")
-        slot = clients.ref_free.pop() if clients.ref_free else clients.ref_next
-        if slot == clients.ref_next:
-            clients.ref_next += 1
+        slot = _ref_slot(clients)
         self.ops[doc].append((0, 0, 0, OP_REF, 0, F_LOCAL, _check_i32(pos, "pos"), slot, ref_type, 0))
         return slot
 

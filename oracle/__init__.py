@@ -50,6 +50,7 @@ def load():
         "oti_load_segments": [vp, vp, vp, u64], "oti_apply_batch": [vp, vp, C.c_int],
         "oti_read_doc": [vp, u32, vp], "oti_digest": [vp, vp, u32], "oti_doc_status": [vp, vp, u32],
         "oti_doc_nsegs": [vp, u32, vp], "oti_stats_get": [vp, vp], "oti_read_segments": [vp, u32, vp], "oti_set_limit": [vp, u32],
+        "oti_read_deltas": [vp, u32, vp, u64, vp], "oti_read_refs": [vp, u32, vp, u32],
     }.items():
         f = getattr(lib, name)
         f.argtypes = args
@@ -144,7 +145,8 @@ class OracleEngine(EngineBase):
         return self.f.read_doc(self.ctx, doc, vptr)
 
     def _read_deltas(self, doc, p, cap, np_):
-        return self.lib.orc_read_deltas(self.ctx, doc, p, cap, np_)
+        f = self.lib.oti_read_deltas if self.tree == "items" else self.lib.orc_read_deltas
+        return f(self.ctx, doc, p, cap, np_)
 
     def set_event_capacity(self, per_op):
         """The restatement's event buffers grow as needed (mte_set_event_capacity's bound is the engine's)."""
@@ -153,7 +155,8 @@ class OracleEngine(EngineBase):
         """The restatement's reference slots grow as needed."""
 
     def _read_refs(self, doc, p, n):
-        return self.lib.orc_read_refs(self.ctx, doc, p, n)
+        f = self.lib.oti_read_refs if self.tree == "items" else self.lib.orc_read_refs
+        return f(self.ctx, doc, p, n)
 
     def _digest(self, p, n):
         return self.f.digest(self.ctx, p, n)

@@ -18,6 +18,16 @@
  * and the heap itself as an array (collections/heap.ts).  Every rule cites the
  * reference in tree.c; this file only re-expresses them over the item array.
  * It must agree with tree.c on every document (tests/test_tree_items.py).
+ *
+ * Documents with a local client (MTE_DOC_LOCAL_CLIENT) run here too, with the
+ * flat restatement's local records (oracle.c: local ops, acks, rollback,
+ * regeneration, references, delta events) on the tree: the reference places
+ * a remote insert next to the client's pending segments by its block edges
+ * (continuePredicate's forward excursion, mergeTree.ts:1599-1611, 1788-1797),
+ * holds every segment of a pending group in scourNode (:686-688), runs the
+ * lazy zamboni after acks and rollbacks (:1329, 2052-2061) and adds acked
+ * segments to the LRU set (:1303-1305).  This is the spec of the GPU's HBM
+ * tree pass (csrc/mte_htree.h).
  */
 #include <limits.h>
 #include <pthread.h>
@@ -45,6 +55,17 @@ typedef struct {
   uint32_t props[MTE_MAX_KEYS];
   uint8_t h, cont, ns, po, empty, drop;
   uint32_t id;
+  /* MTE_DOC_LOCAL_CLIENT (as oracle.c's pk rows): per key the localSeq of the
+   * last pending local annotate that set it, the mask of the pending annotate
+   * segment groups the item belongs to, per key the value before the first
+   * pending annotate set it */
+  uint32_t pk[MTE_MAX_KEYS];
+  uint32_t am;
+  uint32_t basev[MTE_MAX_KEYS];
+  /* localRemovedSeq: the localSeq of the client's pending removal, kept when
+   * a remote remove overtakes it (the segment stays in that removal's group
+   * until the ack, mergeTreeNodes.ts:487-497), 0 = none */
+  int32_t lrs;
 } item;
 
 typedef struct {
@@ -68,6 +89,15 @@ typedef struct {
   /* the GPU tree pass's statistics (mte_stats), counted the same way */
   uint64_t ops, scanned, written, pwrites, units, max_segs;
   mte_doc_init init;
+  /* MTE_DOC_LOCAL_CLIENT: the last localSeq */
+  int32_t local_seq;
+  /* MTE_DOC_REFS: reference slots (as oracle.c) */
+  uint32_t *ref_anchor, *ref_state;
+  uint32_t ref_cap, ref_hi;
+  /* MTE_DOC_EVENTS: the last batch's delta events, the record being applied */
+  mte_delta* dl;
+  uint64_t dl_n, dl_cap;
+  uint32_t cur_op;
 } __attribute__((aligned(128))) idoc;
 
 struct oti_ctx {
@@ -88,7 +118,11 @@ typedef struct {
   uint32_t n_keys;
   const uint16_t* arena;
   uint32_t limit;
+  const mte_op* aux; /* the records after the one applied (an annotate rollback's MTE_OP_RBKEY) */
 } env_t;
+
+#define LOCAL_BASE MTE_LOCAL_SEQ_BASE
+static inline int is_pending(int32_t seq) { return seq >= LOCAL_BASE && seq != NONE_SEQ; }
 
 /* ---- storage --------------------------------------------------------------- */
 
@@ -155,13 +189,37 @@ static inline int32_t leaf_len(const item* s, int32_t r, int c, int32_t m, int n
   }
   if (removed && s->rseq <= r) return -1;
   if (s->cli == c || s->seq <= r) return (removed && by_c) ? 0 : s->len;
-  return removed ? -1 : 0;
+  /* inserted and removed before this perspective: undefined, unless the
+   * removal is the local client's pending one (removedSeq Unassigned,
+   * mergeTree.ts:1049-1052) */
+  return (removed && !is_pending(s->rseq)) ? -1 : 0;
 }
 
 static int64_t lengths(idoc* d, int32_t r, int c, int32_t m, int newcalc) {
   int64_t p = 0;
   for (uint32_t i = 0; i < d->n; i++) {
     const int32_t l = leaf_len(&d->it[i], r, c, m, newcalc);
+    d->L[i] = l;
+    d->P[i] = p;
+    if (l > 0) p += l;
+  }
+  return p;
+}
+
+/* The local client's own view (nodeLength with clientId == collabWindow.clientId
+ * -> localNetLength without localSeq, mergeTree.ts:985-987, 553-573): a segment
+ * not removed counts its length; a removed one 0 -- with the legacy calculation
+ * undefined once its (sequenced) removal is at or below minSeq; a placeholder
+ * is no segment. */
+static int64_t lengths_local(idoc* d) {
+  const int newcalc = (d->flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
+  int64_t p = 0;
+  for (uint32_t i = 0; i < d->n; i++) {
+    const item* s = &d->it[i];
+    int32_t l;
+    if (s->empty) l = -1;
+    else if (s->rseq == NONE_SEQ) l = s->len;
+    else l = (newcalc || is_pending(s->rseq) || s->rseq > d->min_seq) ? 0 : -1;
     d->L[i] = l;
     d->P[i] = p;
     if (l > 0) p += l;
@@ -291,7 +349,12 @@ static int scour(idoc* d, uint32_t s, uint32_t e, const uint16_t* arena, uint32_
     }
     const uint32_t xe = leaf_end(d, i);
     const int64_t xl = leaf_total(d, i, xe);
-    if (x->rseq != NONE_SEQ) {
+    if (is_pending(x->seq) || x->lrs || x->am) {
+      /* a segment of a pending group (segmentGroups not empty, mergeTree.ts:686,
+       * 736-739) is held and ends the append run */
+      held++;
+      prev = -1;
+    } else if (x->rseq != NONE_SEQ) {
       if (x->rseq > d->min_seq) {
         held++;
       } else {
@@ -492,115 +555,603 @@ static int check_op_window(const idoc* d, const mte_op* op) {
   return MTE_OK;
 }
 
-static int doc_apply(idoc* d, const mte_op* op, const env_t* env) {
+/* ---- delta events (MTE_DOC_EVENTS, as oracle.c) ------------------------------
+ * One record per segment of the reference: a merged leaf (a head and its
+ * continuations) is one segment, so its items' records are joined. */
+static int delta_push(idoc* d, uint32_t kind, int64_t pos, int32_t len, uint32_t removed) {
+  if (d->dl_n == d->dl_cap) {
+    uint64_t nc = d->dl_cap ? 2 * d->dl_cap : 64;
+    mte_delta* x = (mte_delta*)realloc(d->dl, nc * sizeof(mte_delta));
+    if (!x) return MTE_E_OOM;
+    d->dl = x;
+    d->dl_cap = nc;
+  }
+  d->dl[d->dl_n++] = (mte_delta){d->cur_op, kind, (int32_t)pos, len, removed};
+  return MTE_OK;
+}
+static inline int32_t own_len(const item* g) { return g->rseq == NONE_SEQ ? g->len : 0; }
+static int64_t own_prefix(const idoc* d, uint32_t at) {
+  int64_t p = 0;
+  for (uint32_t i = 0; i < at; i++) p += own_len(&d->it[i]);
+  return p;
+}
+
+/* annotateRange on one item for a sequenced op in a document with a local
+ * client: keys with a pending local update keep their value (shouldModifyKey,
+ * segmentPropertiesManager.ts:94-102, 105-135) */
+static uint64_t apply_props_pending(uint32_t* props, const uint32_t* pk, uint32_t n_keys, const mte_propset* ps,
+                                    const mte_prop* pe, int rewrite) {
+  uint64_t w = 0;
+  if (rewrite)
+    for (uint32_t k = 0; k < n_keys; k++)
+      if (!pk[k]) props[k] = 0;
+  for (uint32_t j = 0; j < ps->count; j++) {
+    const mte_prop* p = &pe[ps->first + j];
+    if (p->key < n_keys) {
+      if (!pk[p->key]) props[p->key] = p->value;
+      w++;
+    }
+  }
+  return w;
+}
+
+/* ---- local references (MTE_DOC_REFS, as oracle.c) ---------------------------- */
+#define REF_LIVE 0x80000000u
+#define REF_DETACHED 0x40000000u
+#define REF_LIMIT (1u << 24)
+
+/* a segment references may slide to (_getSlideToSegment, mergeTree.ts:893-913):
+ * not a pending insert, not removed-and-acked (a pending removal is fine), not
+ * a placeholder */
+static inline int slide_target_ok(const item* g) { return !g->empty && g->seq < LOCAL_BASE && g->rseq >= LOCAL_BASE; }
+static inline int removed_and_acked(const item* g) { return g->rseq != NONE_SEQ && !is_pending(g->rseq) && !g->empty; }
+
+/* where a reference on item i slides to (forwardExcursion / backwardExcursion,
+ * client.ts:1117-1130): offset 0 of the first following segment, else the last
+ * unit of the last preceding one; -1: nowhere */
+static int64_t slide_to(const idoc* d, uint32_t i, uint32_t* anchor) {
+  for (uint32_t j = i + 1; j < d->n; j++)
+    if (slide_target_ok(&d->it[j])) {
+      *anchor = d->it[j].toff;
+      return j;
+    }
+  for (int64_t j = (int64_t)i - 1; j >= 0; j--)
+    if (slide_target_ok(&d->it[j])) {
+      *anchor = d->it[j].toff + (uint32_t)d->it[j].len - 1u;
+      return j;
+    }
+  return -1;
+}
+
+static int ref_reserve(idoc* d, uint32_t slot) {
+  if (slot < d->ref_cap) return MTE_OK;
+  uint32_t nc = d->ref_cap ? d->ref_cap : 64;
+  while (nc <= slot) nc *= 2;
+  uint32_t* a = (uint32_t*)realloc(d->ref_anchor, (size_t)nc * sizeof(uint32_t));
+  if (!a) return MTE_E_OOM;
+  d->ref_anchor = a;
+  uint32_t* st = (uint32_t*)realloc(d->ref_state, (size_t)nc * sizeof(uint32_t));
+  if (!st) return MTE_E_OOM;
+  d->ref_state = st;
+  memset(d->ref_state + d->ref_cap, 0, (size_t)(nc - d->ref_cap) * sizeof(uint32_t));
+  d->ref_cap = nc;
+  return MTE_OK;
+}
+
+/* MTE_OP_REF (oracle.c doc_ref): b = 0 create in the local view, 1 remove,
+ * 2 create in a sequenced op's perspective, 3 become SlideOnRemove */
+static int doc_ref(idoc* d, const mte_op* op) {
+  if (!(d->flags & MTE_DOC_REFS)) return MTE_E_UNSUPPORTED;
+  if (op->pos2 < 0 || (uint32_t)op->pos2 >= REF_LIMIT || op->b > 3) return MTE_E_INVALID_ARG;
+  const uint32_t slot = (uint32_t)op->pos2;
+  int rc;
+  if ((rc = ref_reserve(d, slot))) return rc;
+  d->ops++;
+  if (op->b == 1) {
+    d->ref_state[slot] = 0;
+    return MTE_OK;
+  }
+  if (op->a & MTE_REF_TRANSIENT) return MTE_E_UNSUPPORTED;
+  if ((op->a & MTE_REF_SLIDE_ON_REMOVE) && (op->a & MTE_REF_STAY_ON_REMOVE)) return MTE_E_INVALID_ARG;
+  d->scanned += d->n;
+  if (op->b == 3) {
+    uint32_t st = d->ref_state[slot];
+    if (!(st & REF_LIVE)) return MTE_E_INVALID_ARG;
+    d->ref_state[slot] = st = (st & (REF_LIVE | REF_DETACHED)) | (op->a & 0xffffu);
+    if (st & REF_DETACHED) return MTE_OK;
+    for (uint32_t i = 0; i < d->n; i++) {
+      const item* g = &d->it[i];
+      if (g->empty || d->ref_anchor[slot] - g->toff >= (uint32_t)g->len) continue;
+      if (removed_and_acked(g) && (st & MTE_REF_SLIDE_ON_REMOVE)) {
+        uint32_t to = 0;
+        if (slide_to(d, i, &to) >= 0) d->ref_anchor[slot] = to;
+        else d->ref_state[slot] = st | REF_DETACHED;
+      }
+      break;
+    }
+    return MTE_OK;
+  }
+  const int remote = op->b == 2;
+  if (remote && (op->client >= MTE_MAX_CLIENTS || op->client == 0)) return MTE_E_INVALID_ARG;
+  if (remote) lengths(d, op->ref_seq, op->client, d->min_seq, (d->flags & MTE_DOC_NEW_LENGTH_CALC) != 0);
+  int64_t p = 0;
+  if (slot + 1 > d->ref_hi) d->ref_hi = slot + 1;
+  for (uint32_t i = 0; i < d->n; i++) {
+    const int32_t l = remote ? d->L[i] : (d->it[i].empty ? 0 : own_len(&d->it[i]));
+    if (l > 0 && op->pos1 >= p && op->pos1 < p + l) {
+      uint32_t anchor = d->it[i].toff + (uint32_t)(op->pos1 - p);
+      uint32_t st = REF_LIVE | (op->a & 0xffffu);
+      if (remote && removed_and_acked(&d->it[i]) && slide_to(d, i, &anchor) < 0) st |= REF_DETACHED;
+      d->ref_anchor[slot] = anchor;
+      d->ref_state[slot] = st;
+      return MTE_OK;
+    }
+    if (l > 0) p += l;
+  }
+  if (remote) {
+    d->ref_anchor[slot] = 0;
+    d->ref_state[slot] = REF_LIVE | REF_DETACHED | (op->a & 0xffffu);
+    return MTE_OK;
+  }
+  return MTE_E_INVALID_ARG;
+}
+
+/* slideAckedRemovedSegmentReferences for every item whose removedSeq is now s
+ * (oracle.c doc_slide_refs) */
+static void doc_slide_refs(idoc* d, int32_t s) {
+  if (!(d->flags & MTE_DOC_REFS) || !d->ref_hi) return;
+  for (uint32_t i = 0; i < d->n; i++) {
+    const item* g = &d->it[i];
+    if (g->rseq != s || g->empty) continue;
+    uint32_t to = 0;
+    const int64_t t = slide_to(d, i, &to);
+    for (uint32_t r = 0; r < d->ref_hi; r++) {
+      const uint32_t st = d->ref_state[r];
+      if (!(st & REF_LIVE) || (st & REF_DETACHED) || (st & MTE_REF_STAY_ON_REMOVE)) continue;
+      if (d->ref_anchor[r] - g->toff >= (uint32_t)g->len) continue;
+      if ((st & MTE_REF_SLIDE_ON_REMOVE) && t >= 0) d->ref_anchor[r] = to;
+      else d->ref_state[r] = st | REF_DETACHED;
+    }
+  }
+}
+
+/* ---- insert, range ops (remote and local) -------------------------------------------------------- */
+
+/* insertSegments -> blockInsert -> insertingWalk (mergeTree.ts:1394-1422,
+ * 1590-1680, 1723-1825) for a remote op (local = 0: lengths in the op's
+ * perspective, seq s) or a local one (local = 1: the local view, seq
+ * Unassigned = LOCAL_BASE + localSeq).  Returns the new item's index through
+ * *at (-1 when nothing was linked). */
+static int tree_insert(idoc* d, const mte_op* op, const env_t* env, int local, int64_t* at) {
   const int newcalc = (d->flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
   const int32_t r = op->ref_seq, s = op->seq, m = d->min_seq;
   const int c = op->client;
   int rc;
+  *at = -1;
+  if ((rc = reserve(d, d->n + 3))) return rc;
+  if (local) lengths_local(d);
+  else lengths(d, r, c, m, newcalc);
+  if ((rc = boundary(d, op->pos1))) return rc;
+  const int64_t total = local ? lengths_local(d) : lengths(d, r, c, m, newcalc);
+  const int is_marker = (op->flags & MTE_F_MARKER) != 0;
+  const int32_t len = is_marker ? 1 : op->pos2;
+  if (len <= 0) return MTE_OK; /* blockInsert skips zero-length segments (:1645) */
+  const int64_t pos = op->pos1;
+  /* the leaf block insertingWalk enters: the first whose end reaches pos */
+  uint32_t ks = d->n;
+  for (uint32_t i = 0; i < d->n; i++)
+    if (d->P[i] + (d->L[i] > 0 ? d->L[i] : 0) >= pos) {
+      ks = i;
+      break;
+    }
+  if (ks == d->n || pos > total) return MTE_E_INSERT_FAILED;
+  uint32_t bs = span_start(d, ks, 1), be = span_end(d, bs, 1);
+  uint32_t slot;
+  int replace = 0;
+  for (;;) {
+    slot = UINT32_MAX;
+    if (!d->it[bs].empty) {
+      /* before the first defined leaf at pos (pos < len, or a zero-length leaf
+       * breakTie prefers: every sequenced one, but a pending one only for a
+       * local insert -- Unassigned normalises to MAX vs MAX - 1, :1705-1721) */
+      for (uint32_t i = ks; i <= be; i++) {
+        const item* g = &d->it[i];
+        if (d->L[i] >= 0 && d->P[i] >= pos && !g->empty && !(!local && d->L[i] == 0 && is_pending(g->seq))) {
+          slot = i;
+          break;
+        }
+      }
+      if (slot != UINT32_MAX) break;
+    }
+    /* _pos == 0 at the block's end: a sequenced insert asks continuePredicate,
+     * whose forward excursion looks at the first segment after the block and
+     * moves on past the block when it is a pending local one (:1599-1611,
+     * 1788-1793); otherwise the segment goes at the block's end */
+    if (!local) {
+      uint32_t x = be + 1;
+      while (x < d->n && d->it[x].empty) x++;
+      if (x < d->n && is_pending(d->it[x].seq)) {
+        ks = x;
+        bs = span_start(d, x, 1);
+        be = span_end(d, bs, 1);
+        continue;
+      }
+    }
+    if (d->it[bs].empty) {
+      slot = bs;
+      replace = 1;
+    } else {
+      slot = be + 1;
+    }
+    break;
+  }
+  item nw;
+  memset(&nw, 0, sizeof nw);
+  nw.len = len;
+  nw.seq = local ? LOCAL_BASE + s : s;
+  nw.cli = c;
+  nw.rseq = NONE_SEQ;
+  nw.id = new_id(d);
+  d->written += 1;
+  if (is_marker) {
+    nw.kind = 1u + (uint32_t)op->pos2;
+    if (d->flags & MTE_DOC_REFS) nw.toff = (uint32_t)(env->text_base + op->a); /* its reserved unit */
+  } else {
+    nw.toff = (uint32_t)(env->text_base + op->a);
+    d->units += (uint64_t)len;
+  }
+  if (op->b != MTE_NO_PROPS) {
+    nw.po = 1;
+    d->pwrites += orc_apply_props(nw.props, env->n_keys, &env->b->propsets[op->b], env->b->props, 0);
+  }
+  if (replace) {
+    nw.h = d->it[slot].h;
+    nw.ns = d->it[slot].ns;
+    d->it[slot] = nw;
+  } else {
+    if ((rc = open_slot(d, slot))) return rc;
+    if (slot == bs) { /* the new leaf becomes the block's first child */
+      nw.h = d->it[slot + 1].h;
+      nw.ns = d->it[slot + 1].ns;
+      d->it[slot + 1].h = 0;
+    }
+    d->it[slot] = nw;
+    split_cascade(d, slot);
+  }
+  /* saveIfLocal (:1614-1627): a local segment joins the pending list, a
+   * sequenced one the LRU set */
+  if (!local && (rc = add_lru(d, slot, s))) return rc;
+  *at = slot;
+  return MTE_OK;
+}
+
+/* markRangeRemoved / annotateRange (mergeTree.ts:1864-2000) for a remote op or
+ * a local one (the local view, removedSeq / pending keys Unassigned) */
+static int tree_range(idoc* d, const mte_op* op, const env_t* env, int local) {
+  const int newcalc = (d->flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
+  const int32_t r = op->ref_seq, s = op->seq, m = d->min_seq;
+  const int c = op->client;
+  const int local_doc = (d->flags & MTE_DOC_LOCAL_CLIENT) != 0;
+  const int ev = (d->flags & MTE_DOC_EVENTS) != 0;
+  const int64_t start = op->pos1, end = op->pos2;
+  int rc;
+  if ((rc = reserve(d, d->n + 3))) return rc;
+  if (local) lengths_local(d);
+  else lengths(d, r, c, m, newcalc);
+  if ((rc = boundary(d, start))) return rc;
+  if (local) lengths_local(d);
+  else lengths(d, r, c, m, newcalc);
+  if ((rc = boundary(d, end))) return rc;
+  if (end == start) return MTE_OK;
+  if (local) lengths_local(d);
+  else lengths(d, r, c, m, newcalc);
+  int64_t lp = 0;         /* the own view's prefix after the op, for the events */
+  int64_t last_ev = -2;   /* the item of the last event (a continuation joins it) */
+  for (uint32_t i = 0; i < d->n; lp += own_len(&d->it[i]), i++) {
+    const int32_t l = d->L[i];
+    if (l <= 0) continue;
+    if (d->P[i] >= end) break;
+    if (d->P[i] + l <= start) continue;
+    item* g = &d->it[i];
+    d->written += 1;
+    const int is_rem = op->type == MTE_OP_REMOVE;
+    /* a remove reports the segments it newly removes, an annotate every one it
+     * visits (removedSegments / deltaSegments, :1954-1959, 1893-1900) */
+    if (ev && (!is_rem || g->rseq == NONE_SEQ)) {
+      const uint32_t removed = is_rem || g->rseq != NONE_SEQ;
+      if (g->cont && last_ev == (int64_t)i - 1 && d->dl_n) {
+        d->dl[d->dl_n - 1].len += g->len;
+      } else if ((rc = delta_push(d, op->type, lp, g->len, removed))) {
+        return rc;
+      }
+      last_ev = i;
+    }
+    if (is_rem) {
+      if (local) {
+        g->rseq = LOCAL_BASE + s;
+        g->rmask = 1u;
+        g->lrs = s;
+      } else if (g->rseq == NONE_SEQ) {
+        g->rseq = s;
+        g->rmask = 1u << c;
+      } else {
+        if (is_pending(g->rseq)) g->rseq = s; /* overtaking our pending removal (:1928-1938) */
+        g->rmask |= 1u << c;
+      }
+    } else {
+      const mte_propset* ps = &env->b->propsets[op->a];
+      g->po = 1;
+      if (local) {
+        for (uint32_t j = 0; j < ps->count; j++) {
+          const mte_prop* p = &env->b->props[ps->first + j];
+          if (p->key < env->n_keys && !g->pk[p->key]) g->basev[p->key] = g->props[p->key];
+        }
+        d->pwrites += orc_apply_props(g->props, env->n_keys, ps, env->b->props, 0);
+        for (uint32_t j = 0; j < ps->count; j++) {
+          const mte_prop* p = &env->b->props[ps->first + j];
+          if (p->key < env->n_keys) g->pk[p->key] = (uint32_t)s;
+        }
+        if (op->b != MTE_NO_PROPS) g->am |= 1u << op->b; /* the annotate's segment group */
+      } else if (local_doc) {
+        d->pwrites += apply_props_pending(g->props, g->pk, env->n_keys, ps, env->b->props,
+                                          (op->flags & MTE_F_REWRITE) != 0);
+      } else {
+        d->pwrites += orc_apply_props(g->props, env->n_keys, ps, env->b->props, (op->flags & MTE_F_REWRITE) != 0);
+      }
+    }
+    /* a sequenced op adds each visited segment to the LRU set (:1881-1884, 1955-1958) */
+    if (!local && !g->cont && (rc = add_lru(d, i, s))) return rc;
+  }
+  return MTE_OK;
+}
+
+/* ---- local records --------------------------------------------------------------------------------- */
+
+static int doc_rollback(idoc* d, const mte_op* op, const env_t* env);
+static int doc_regen(idoc* d, const mte_op* op);
+
+/* A local op (MTE_F_LOCAL): insertSegmentLocal / removeRangeLocal /
+ * annotateRangeLocal (client.ts:131-229) with seq Unassigned, or one of the
+ * local records (rollback, regeneration, reference). */
+static int doc_apply_local(idoc* d, const mte_op* op, const env_t* env) {
+  const int32_t ls = op->seq;
+  int rc;
+  if (op->type == MTE_OP_ROLLBACK) return doc_rollback(d, op, env);
+  if (op->type == MTE_OP_REGEN) return doc_regen(d, op);
+  if (op->type == MTE_OP_REF) return doc_ref(d, op);
+  if (!(ls > d->local_seq && ls < LOCAL_BASE)) return MTE_E_INVALID_ARG;
+  if (op->client != 0) return MTE_E_INVALID_ARG;
+  if (op->type == MTE_OP_ANNOTATE && (op->flags & MTE_F_REWRITE)) return MTE_E_UNSUPPORTED;
+  d->local_seq = ls;
+  d->ops++;
+  if (d->n > d->max_segs) d->max_segs = d->n;
+  if (op->type == MTE_OP_NOOP) return MTE_OK;
+  d->scanned += d->n;
+  if (op->type == MTE_OP_INSERT) {
+    int64_t at;
+    if ((rc = tree_insert(d, op, env, 1, &at))) return rc;
+    if (d->flags & MTE_DOC_EVENTS) {
+      const int is_marker = (op->flags & MTE_F_MARKER) != 0;
+      return at >= 0 ? delta_push(d, MTE_OP_INSERT, own_prefix(d, (uint32_t)at), is_marker ? 1 : op->pos2, 0)
+                     : delta_push(d, MTE_OP_INSERT, -1, 0, 0);
+    }
+    return MTE_OK;
+  }
+  if (op->type != MTE_OP_REMOVE && op->type != MTE_OP_ANNOTATE) return MTE_E_INVALID_ARG;
+  return tree_range(d, op, env, 1);
+}
+
+/* the next item of a pending group, from i on: an insert / remove group by its
+ * seq / removedSeq, an annotate group by its slot bit */
+static int64_t next_member(const idoc* d, uint32_t i, uint32_t t, int32_t ls, uint32_t slot) {
+  for (; i < d->n; i++) {
+    const item* g = &d->it[i];
+    if (g->empty) continue;
+    if (t == MTE_OP_INSERT ? g->seq == LOCAL_BASE + ls
+                           : (t == MTE_OP_REMOVE ? g->rseq == LOCAL_BASE + ls : ((g->am >> slot) & 1u) != 0))
+      return i;
+  }
+  return -1;
+}
+
+/* MTE_OP_ROLLBACK of an annotate (as oracle.c doc_rollback_annotate), each
+ * segment re-annotated by annotateRange at seq UniversalSequenceNumber, which
+ * runs zamboniSegments after it (mergeTree.ts:2036-2072, 1901-1905) */
+static int doc_rollback_annotate(idoc* d, const mte_op* op, const env_t* env) {
+  const uint32_t b = op->a;
+  const mte_op* aux = env->aux;
+  const uint32_t n_aux = (uint32_t)op->pos2;
+  int rc;
+  if (b >= MTE_ANNOTATE_SLOTS || !aux) return MTE_E_INVALID_ARG;
+  d->ops++;
+  d->scanned += d->n;
+  for (int64_t i = next_member(d, 0, MTE_OP_ANNOTATE, 0, b); i >= 0; i = next_member(d, 0, MTE_OP_ANNOTATE, 0, b)) {
+    item* g = &d->it[i];
+    if (g->rseq != NONE_SEQ) return MTE_E_UNSUPPORTED;
+    /* a merged leaf of the group is one segment: its items together */
+    uint32_t e = (uint32_t)i + 1;
+    while (e < d->n && d->it[e].cont) e++;
+    uint32_t j = 0;
+    while (j < n_aux) {
+      const uint32_t key = (uint32_t)aux[j].pos1;
+      if (key >= env->n_keys) return MTE_E_INVALID_ARG;
+      uint32_t val = g->basev[key], pk = 0;
+      for (; j < n_aux; j++) {
+        const uint32_t slot = (uint32_t)aux[j].pos2;
+        if ((uint32_t)aux[j].pos1 != key) return MTE_E_INVALID_ARG;
+        if (slot >= MTE_ANNOTATE_SLOTS) break;
+        if ((g->am >> slot) & 1u) {
+          val = aux[j].a;
+          pk = (uint32_t)aux[j].seq;
+          break;
+        }
+      }
+      while (j < n_aux && (uint32_t)aux[j].pos2 < MTE_ANNOTATE_SLOTS) j++;
+      if (j >= n_aux) return MTE_E_INVALID_ARG;
+      j++;
+      for (uint32_t q = (uint32_t)i; q < e; q++) {
+        d->it[q].props[key] = val;
+        d->it[q].pk[key] = pk;
+      }
+      d->pwrites += 1;
+    }
+    int32_t tl = 0;
+    for (uint32_t q = (uint32_t)i; q < e; q++) {
+      d->it[q].am &= ~(1u << b);
+      tl += d->it[q].len;
+    }
+    if ((d->flags & MTE_DOC_EVENTS) && (rc = delta_push(d, MTE_OP_ANNOTATE, own_prefix(d, (uint32_t)i), tl, 0)))
+      return rc;
+    d->written += 1;
+    zamboni(d, env->arena, env->n_keys);
+  }
+  return MTE_OK;
+}
+
+/* MTE_OP_ROLLBACK (MergeTree.rollback, mergeTree.ts:2005-2083): an insert's
+ * segments get seq and removedSeq UniversalSequenceNumber through
+ * markRangeRemoved at seq 0, which runs zamboniSegments after each; a remove's
+ * are restored */
+static int doc_rollback(idoc* d, const mte_op* op, const env_t* env) {
+  const int32_t ls = op->seq;
+  int rc;
+  if (!(ls > 0 && ls <= d->local_seq)) return MTE_E_INVALID_ARG;
+  if (op->pos1 == MTE_OP_ANNOTATE) return doc_rollback_annotate(d, op, env);
+  if (op->pos1 != MTE_OP_INSERT && op->pos1 != MTE_OP_REMOVE) return MTE_E_INVALID_ARG;
+  d->ops++;
+  d->scanned += d->n;
+  const uint32_t t = (uint32_t)op->pos1;
+  for (int64_t i = next_member(d, 0, t, ls, 0); i >= 0; i = next_member(d, t == MTE_OP_INSERT ? 0 : (uint32_t)i + 1, t, ls, 0)) {
+    item* g = &d->it[i];
+    const int64_t lp = own_prefix(d, (uint32_t)i);
+    if (t == MTE_OP_INSERT) {
+      g->seq = 0;
+      g->rseq = 0;
+      g->rmask = 1u;
+      if ((d->flags & MTE_DOC_EVENTS) && (rc = delta_push(d, MTE_OP_REMOVE, lp, g->len, 1))) return rc;
+      d->written += 1;
+      zamboni(d, env->arena, env->n_keys);
+    } else {
+      g->rseq = NONE_SEQ;
+      g->rmask = 0;
+      g->lrs = 0;
+      if ((d->flags & MTE_DOC_EVENTS) && (rc = delta_push(d, MTE_OP_INSERT, lp, g->len, 0))) return rc;
+      d->written += 1;
+    }
+  }
+  return MTE_OK;
+}
+
+/* the length of an item in the local view at localSeq ls (localNetLength with
+ * localSeq, mergeTree.ts:575-593) */
+static inline int32_t len_at_local_seq(const item* g, int32_t ls) {
+  if (g->empty) return 0;
+  if (is_pending(g->seq) && g->seq - LOCAL_BASE > ls) return 0;
+  if (g->lrs && g->lrs <= ls) return 0;
+  if (g->rseq != NONE_SEQ && (!is_pending(g->rseq) || g->rseq - LOCAL_BASE <= ls)) return 0;
+  return g->len;
+}
+
+/* MTE_OP_REGEN (as oracle.c doc_regen): the group's segments in document order
+ * at their positions in the view at that localSeq -- a merged leaf one record */
+static int doc_regen(idoc* d, const mte_op* op) {
+  const int32_t ls = op->seq;
+  const uint32_t t = (uint32_t)op->pos1;
+  int rc;
+  if (!(ls > 0 && ls <= d->local_seq)) return MTE_E_INVALID_ARG;
+  if (t != MTE_OP_INSERT && t != MTE_OP_REMOVE && t != MTE_OP_ANNOTATE) return MTE_E_INVALID_ARG;
+  if (t == MTE_OP_ANNOTATE && op->a >= MTE_ANNOTATE_SLOTS) return MTE_E_INVALID_ARG;
+  if (!(d->flags & MTE_DOC_EVENTS)) return MTE_E_UNSUPPORTED;
+  d->ops++;
+  d->scanned += d->n;
+  int64_t p = 0;
+  int64_t last = -2;
+  for (uint32_t i = 0; i < d->n; i++) {
+    const item* g = &d->it[i];
+    int hit;
+    if (g->empty) hit = 0;
+    else if (t == MTE_OP_INSERT) hit = g->seq == LOCAL_BASE + ls;
+    else if (t == MTE_OP_REMOVE) hit = g->rseq == LOCAL_BASE + ls;
+    else hit = ((g->am >> op->a) & 1u) && (g->rseq == NONE_SEQ || is_pending(g->rseq));
+    if (hit) {
+      if (g->cont && last == (int64_t)i - 1 && d->dl_n) d->dl[d->dl_n - 1].len += g->len;
+      else if ((rc = delta_push(d, MTE_DELTA_REGEN | t, p, g->len, t == MTE_OP_INSERT ? g->toff : 0u))) return rc;
+      last = i;
+    }
+    p += len_at_local_seq(g, ls);
+  }
+  return MTE_OK;
+}
+
+/* MTE_OP_ACK for localSeqs pos1..pos2 (client.ts:640-672 acks a GROUP's members
+ * one by one): per localSeq, ackPendingSegment (mergeTree.ts:1278-1331) acks its
+ * group's segments, slides the references of the acked removals, adds each
+ * segment to the LRU set, then runs zamboniSegments.  The slot mask op->a frees
+ * the annotate groups (all of them with the last localSeq of the record). */
+static int doc_ack(idoc* d, const mte_op* op, const env_t* env) {
+  const int32_t lo = op->pos1, hi = op->pos2, s = op->seq;
+  int rc;
+  if (!(lo > 0 && lo <= hi && hi <= d->local_seq)) return MTE_E_INVALID_ARG;
+  for (int32_t ls = lo; ls <= hi; ls++) {
+    const uint32_t am_mask = ls == hi ? op->a : 0u;
+    for (uint32_t i = 0; i < d->n; i++) {
+      item* g = &d->it[i];
+      if (g->empty) continue;
+      int member = 0;
+      if (g->seq == LOCAL_BASE + ls) {
+        g->seq = s;
+        member = 1;
+      }
+      if (g->rseq == LOCAL_BASE + ls) g->rseq = s;
+      if (g->lrs == ls) { /* acked, or overtaken by a remote remove before (:1928-1938) */
+        g->lrs = 0;
+        member = 1;
+      }
+      for (uint32_t k = 0; k < MTE_MAX_KEYS; k++)
+        if (g->pk[k] && g->pk[k] <= (uint32_t)ls) g->pk[k] = 0;
+      if (g->am & am_mask) {
+        g->am &= ~am_mask;
+        member = 1;
+      }
+      if (member && !g->cont && (rc = add_lru(d, i, s))) return rc;
+    }
+    doc_slide_refs(d, s);
+    zamboni(d, env->arena, env->n_keys);
+  }
+  return MTE_OK;
+}
+
+static int doc_apply(idoc* d, const mte_op* op, const env_t* env) {
+  const int32_t s = op->seq;
+  const int c = op->client;
+  const int local_doc = (d->flags & MTE_DOC_LOCAL_CLIENT) != 0;
+  int rc;
   if (d->n + 4 > env->limit) return MTE_E_CAPACITY;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
+  if (op->flags & MTE_F_LOCAL) return local_doc ? doc_apply_local(d, op, env) : MTE_E_UNSUPPORTED;
+  if (op->type == MTE_OP_ACK && !local_doc) return MTE_E_UNSUPPORTED;
+  if (local_doc && op->type != MTE_OP_ACK && op->type != MTE_OP_NOOP && c == 0) return MTE_E_INVALID_ARG;
   d->ops++;
   if (d->n > d->max_segs) d->max_segs = d->n;
   if (op->type != MTE_OP_NOOP) d->scanned += d->n;
   if (op->type == MTE_OP_INSERT) {
-    if ((rc = reserve(d, d->n + 3))) return rc;
-    lengths(d, r, c, m, newcalc);
-    if ((rc = boundary(d, op->pos1))) return rc;
-    const int64_t total = lengths(d, r, c, m, newcalc);
-    const int is_marker = (op->flags & MTE_F_MARKER) != 0;
-    const int32_t len = is_marker ? 1 : op->pos2;
-    if (len > 0) {
-      const int64_t pos = op->pos1;
-      /* the leaf block insertingWalk enters: the first whose end reaches pos */
-      uint32_t ks = d->n;
-      for (uint32_t i = 0; i < d->n; i++)
-        if (d->P[i] + (d->L[i] > 0 ? d->L[i] : 0) >= pos) {
-          ks = i;
-          break;
-        }
-      if (ks == d->n || pos > total) return MTE_E_INSERT_FAILED;
-      const uint32_t bs = span_start(d, ks, 1), be = span_end(d, bs, 1);
-      uint32_t slot;
-      int replace = 0;
-      if (d->it[bs].empty) {
-        slot = bs;
-        replace = 1;
-      } else {
-        slot = be + 1;
-        for (uint32_t i = ks; i <= be; i++)
-          if (d->L[i] >= 0 && d->P[i] >= pos && !d->it[i].empty) {
-            slot = i;
-            break;
-          }
-      }
-      item nw;
-      memset(&nw, 0, sizeof nw);
-      nw.len = len;
-      nw.seq = s;
-      nw.cli = c;
-      nw.rseq = NONE_SEQ;
-      nw.id = new_id(d);
-      d->written += 1;
-      if (is_marker) {
-        nw.kind = 1u + (uint32_t)op->pos2;
-      } else {
-        nw.toff = (uint32_t)(env->text_base + op->a);
-        d->units += (uint64_t)len;
-      }
-      if (op->b != MTE_NO_PROPS) {
-        nw.po = 1;
-        d->pwrites += orc_apply_props(nw.props, env->n_keys, &env->b->propsets[op->b], env->b->props, 0);
-      }
-      if (replace) {
-        nw.h = d->it[slot].h;
-        nw.ns = d->it[slot].ns;
-        d->it[slot] = nw;
-      } else {
-        if ((rc = open_slot(d, slot))) return rc;
-        if (slot == bs) { /* the new leaf becomes the block's first child */
-          nw.h = d->it[slot + 1].h;
-          nw.ns = d->it[slot + 1].ns;
-          d->it[slot + 1].h = 0;
-        }
-        d->it[slot] = nw;
-        split_cascade(d, slot);
-      }
-      if ((rc = add_lru(d, slot, s))) return rc;
+    int64_t at;
+    if ((rc = tree_insert(d, op, env, 0, &at))) return rc;
+    if (d->flags & MTE_DOC_EVENTS) {
+      const int is_marker = (op->flags & MTE_F_MARKER) != 0;
+      rc = at >= 0 ? delta_push(d, MTE_OP_INSERT, own_prefix(d, (uint32_t)at), is_marker ? 1 : op->pos2, 0)
+                   : delta_push(d, MTE_OP_INSERT, -1, 0, 0);
+      if (rc) return rc;
     }
     zamboni(d, env->arena, env->n_keys);
     if ((rc = check_op_window(d, op))) return rc;
   } else if (op->type == MTE_OP_REMOVE || op->type == MTE_OP_ANNOTATE) {
-    const int64_t start = op->pos1, end = op->pos2;
-    if ((rc = reserve(d, d->n + 3))) return rc;
-    lengths(d, r, c, m, newcalc);
-    if ((rc = boundary(d, start))) return rc;
-    lengths(d, r, c, m, newcalc);
-    if ((rc = boundary(d, end))) return rc;
-    if (end != start) {
-      lengths(d, r, c, m, newcalc);
-      for (uint32_t i = 0; i < d->n; i++) {
-        const int32_t l = d->L[i];
-        if (l <= 0) continue;
-        if (d->P[i] >= end) break;
-        if (d->P[i] + l <= start) continue;
-        item* g = &d->it[i];
-        d->written += 1;
-        if (op->type == MTE_OP_REMOVE) {
-          if (g->rseq == NONE_SEQ) {
-            g->rseq = s;
-            g->rmask = 1u << c;
-          } else {
-            g->rmask |= 1u << c;
-          }
-        } else {
-          g->po = 1;
-          d->pwrites += orc_apply_props(g->props, env->n_keys, &env->b->propsets[op->a], env->b->props,
-                                        (op->flags & MTE_F_REWRITE) != 0);
-        }
-        if (!g->cont && (rc = add_lru(d, i, s))) return rc;
-      }
-    }
+    if ((rc = tree_range(d, op, env, 0))) return rc;
+    if (op->type == MTE_OP_REMOVE) doc_slide_refs(d, s);
     zamboni(d, env->arena, env->n_keys);
+    if ((rc = check_op_window(d, op))) return rc;
+  } else if (op->type == MTE_OP_ACK) {
+    if ((rc = doc_ack(d, op, env))) return rc;
     if ((rc = check_op_window(d, op))) return rc;
   } else if (op->type != MTE_OP_NOOP) {
     return MTE_E_INVALID_ARG;
@@ -651,6 +1202,9 @@ static void free_docs(oti_ctx* c) {
     free(c->docs[i].heap);
     free(c->docs[i].L);
     free(c->docs[i].P);
+    free(c->docs[i].ref_anchor);
+    free(c->docs[i].ref_state);
+    free(c->docs[i].dl);
   }
   free(c->docs);
   free(c->load_ps);
@@ -785,16 +1339,21 @@ typedef struct {
 
 static void* worker(void* p) {
   worker_arg* w = (worker_arg*)p;
-  env_t env = {w->b, w->base, w->c->n_keys, w->c->arena, w->c->limit};
+  env_t env = {w->b, w->base, w->c->n_keys, w->c->arena, w->c->limit, NULL};
   for (uint32_t di = w->d0; di < w->d1; di += w->stride) {
     idoc* d = &w->c->docs[di];
     if (d->status) continue;
+    d->dl_n = 0;
     for (uint64_t k = w->b->op_offsets[di]; k < w->b->op_offsets[di + 1]; k++) {
-      int rc = doc_apply(d, &w->b->ops[k], &env);
+      const mte_op* op = &w->b->ops[k];
+      d->cur_op = (uint32_t)(k - w->b->op_offsets[di]);
+      env.aux = op + 1;
+      int rc = doc_apply(d, op, &env);
       if (rc) {
         d->status = rc;
         break;
       }
+      if (op->type == MTE_OP_ROLLBACK && op->pos1 == MTE_OP_ANNOTATE) k += (uint64_t)op->pos2; /* its RBKEY records */
     }
   }
   return NULL;
@@ -803,6 +1362,46 @@ static void* worker(void* p) {
 int oti_apply_batch(oti_ctx* c, const mte_batch* b, int n_threads) {
   if (!c || !b || b->n_docs != c->n_docs || !b->op_offsets) return MTE_E_INVALID_ARG;
   if (b->op_offsets[b->n_docs] != b->n_ops) return MTE_E_INVALID_ARG;
+  /* the records as mte_submit validates them (oracle.c orc_apply_batch) */
+  uint32_t dcur = 0;
+  uint64_t rbkey_end = 0;
+  for (uint64_t k = 0; k < b->n_ops; k++) {
+    const mte_op* op = &b->ops[k];
+    while (dcur + 1 < b->n_docs && b->op_offsets[dcur + 1] <= k) dcur++;
+    const int local_doc = (c->docs[dcur].flags & MTE_DOC_LOCAL_CLIENT) != 0;
+    if ((op->type == MTE_OP_RBKEY) != (k < rbkey_end)) return MTE_E_INVALID_ARG;
+    if (op->type == MTE_OP_ROLLBACK && op->pos1 == MTE_OP_ANNOTATE) {
+      if (op->pos2 < 0 || k + 1 + (uint64_t)op->pos2 > b->op_offsets[dcur + 1]) return MTE_E_INVALID_ARG;
+      rbkey_end = k + 1 + (uint64_t)op->pos2;
+    }
+    if (op->type > MTE_OP_REF) return MTE_E_INVALID_ARG;
+    if (op->type >= MTE_OP_ROLLBACK && !(op->flags & MTE_F_LOCAL)) return MTE_E_INVALID_ARG;
+    if (op->type == MTE_OP_REF) {
+      if (!(c->docs[dcur].flags & MTE_DOC_REFS) || op->seq != 0 || op->pos2 < 0 || op->b > 3 ||
+          op->client >= MTE_MAX_CLIENTS)
+        return MTE_E_INVALID_ARG;
+      continue;
+    }
+    if ((op->flags & MTE_F_LOCAL) && op->type == MTE_OP_ANNOTATE && op->b != MTE_NO_PROPS &&
+        op->b >= MTE_ANNOTATE_SLOTS)
+      return MTE_E_INVALID_ARG;
+    if ((op->flags & MTE_F_LOCAL) || op->type == MTE_OP_ACK) {
+      if (!local_doc) return MTE_E_INVALID_ARG;
+      if ((op->flags & MTE_F_LOCAL) && op->type != MTE_OP_RBKEY &&
+          (op->type == MTE_OP_ACK || op->seq <= 0 || op->seq >= MTE_LOCAL_SEQ_BASE))
+        return MTE_E_INVALID_ARG;
+      if (op->type == MTE_OP_RBKEY && (op->seq < 0 || op->seq >= MTE_LOCAL_SEQ_BASE || op->pos1 < 0 ||
+                                       op->pos1 >= MTE_MAX_KEYS || op->pos2 < 0 || op->pos2 > MTE_ANNOTATE_SLOTS))
+        return MTE_E_INVALID_ARG;
+      if (op->type == MTE_OP_ACK && (op->pos1 <= 0 || op->pos1 > op->pos2)) return MTE_E_INVALID_ARG;
+    }
+    if (local_doc && !(op->flags & MTE_F_LOCAL) && op->seq >= MTE_LOCAL_SEQ_BASE) return MTE_E_INVALID_ARG;
+    if (op->type == MTE_OP_INSERT && !(op->flags & MTE_F_MARKER) && op->pos2 > 0 &&
+        (uint64_t)op->a + (uint64_t)op->pos2 > b->text_units)
+      return MTE_E_INVALID_ARG;
+    if (op->type == MTE_OP_INSERT && op->b != MTE_NO_PROPS && op->b >= b->n_propsets) return MTE_E_INVALID_ARG;
+    if (op->type == MTE_OP_ANNOTATE && op->a >= b->n_propsets) return MTE_E_INVALID_ARG;
+  }
   uint64_t base = 0;
   int rc = arena_append(c, b->text, b->text_units, &base);
   if (rc) return rc;
@@ -987,5 +1586,37 @@ int oti_read_segments(oti_ctx* c, uint32_t doc, mte_seg_list* v) {
 int oti_set_limit(oti_ctx* c, uint32_t limit) {
   if (!c || limit < 8) return MTE_E_INVALID_ARG;
   c->limit = limit;
+  return MTE_OK;
+}
+
+int oti_read_deltas(oti_ctx* c, uint32_t doc, mte_delta* out, uint64_t cap, uint64_t* n) {
+  if (!c || !n || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  const idoc* d = &c->docs[doc];
+  *n = d->dl_n;
+  if (out) memcpy(out, d->dl, (size_t)(cap < d->dl_n ? cap : d->dl_n) * sizeof(mte_delta));
+  return MTE_OK;
+}
+
+/* referencePositionToLocalPosition (mergeTree.ts:1095-1112) of slots [0, n),
+ * as oracle.c: -1 for a detached or unused slot or a unit no item holds (its
+ * segment unlinked by the zamboni) */
+int oti_read_refs(oti_ctx* c, uint32_t doc, int32_t* pos, uint32_t n) {
+  if (!c || (n && !pos) || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  const idoc* d = &c->docs[doc];
+  for (uint32_t r = 0; r < n; r++) {
+    pos[r] = -1;
+    if (r >= d->ref_hi) continue;
+    const uint32_t st = d->ref_state[r], u = d->ref_anchor[r];
+    if (!(st & REF_LIVE) || (st & REF_DETACHED)) continue;
+    int64_t p = 0;
+    for (uint32_t i = 0; i < d->n; i++) {
+      const item* g = &d->it[i];
+      if (!g->empty && u - g->toff < (uint32_t)g->len) {
+        pos[r] = (int32_t)(p + (g->rseq != NONE_SEQ ? 0 : (int64_t)(u - g->toff)));
+        break;
+      }
+      p += g->empty ? 0 : own_len(g);
+    }
+  }
   return MTE_OK;
 }

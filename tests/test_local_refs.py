@@ -24,7 +24,7 @@ import os
 import pytest
 
 from fixtures_util import doc_inits, replay_ref_farm
-from fluidframework_amd.abi import (DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC, DOC_REFS, MTE_E_INVALID_ARG,
+from fluidframework_amd.abi import (DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC, DOC_REFS, MTE_E_CAPACITY, MTE_E_INVALID_ARG,
                                     MTE_E_UNSUPPORTED, REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE, REF_TRANSIENT,
                                     MergeTreeError)
 from fluidframework_amd.packing import BatchBuilder, DocClients, Interner
@@ -146,6 +146,21 @@ def test_packer_ref_rules():
     assert ei.value.code == MTE_E_INVALID_ARG
     with pytest.raises(MergeTreeError):
         bb.add_ref(0, DocClients("A"), 0)  # observer documents have no local view
+
+
+def test_packer_ref_capacity_refuses_only_that_document():
+    # a slot >= the context's ref capacity made mte_submit fail the
+    # whole batch; the packer now refuses the reference for its document alone
+    cl, other = DocClients("B", local=True), DocClients("B", local=True)
+    cl.ref_cap = other.ref_cap = 3
+    bb = BatchBuilder(2, Interner(4))
+    assert [bb.add_ref(0, cl, i) for i in range(3)] == [0, 1, 2]
+    with pytest.raises(MergeTreeError) as ei:
+        bb.add_ref(0, cl, 0)
+    assert ei.value.code == MTE_E_CAPACITY
+    assert bb.add_ref(1, other, 0) == 0  # the other document is unaffected
+    bb.remove_ref(0, cl, 1)
+    assert bb.add_ref(0, cl, 0) == 1  # a freed slot is below the capacity
 
 
 def test_oracle_rejects_refs_outside_refs_docs():

@@ -434,3 +434,22 @@ def test_sharded_host_packs_what_one_packer_packs(tmp_path, mode):
         a, b = sharded.read_doc(d), one.read_doc(d)
         assert a["text"] == b["text"], d
         assert runs(a, tables["keys"], tables["values"]) == runs(b, it.key_names, it.value_json), d
+
+
+def test_js_packer_ref_capacity_refuses_only_that_document():
+    # the JS packer refuses a reference past the context's capacity
+    # for its own document instead of letting mte_submit fail the whole batch
+    out = node("-e", """
+const p = require('./fluidframework_amd/node/packing.js');
+const bb = new p.BatchBuilder(2, new p.Interner(4));
+const a = new p.DocClients('B', 0, true), b = new p.DocClients('B', 0, true);
+a.refCap = b.refCap = 2;
+const slots = [bb.addRef(0, a, 0), bb.addRef(0, a, 1)];
+let code = null;
+try { bb.addRef(0, a, 0); } catch (e) { code = e.code; }
+slots.push(bb.addRef(1, b, 0));
+bb.removeRef(0, a, 0);
+slots.push(bb.addRef(0, a, 0));
+console.log(JSON.stringify({slots, code}));
+""")
+    assert json.loads(out) == {"slots": [0, 1, 0, 0], "code": -4}
