@@ -24,6 +24,7 @@
 namespace mte {
 }  // namespace mte
 #include "mte_tree.h"
+#include "mte_htree.h"
 #include "mte_passes.h"
 
 #include <rccl/rccl.h>
@@ -114,13 +115,17 @@ constexpr uint32_t kInitNl = 0x80000000u;
 
 __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_doc_init* inits,
                              const uint32_t* init_props, uint32_t n_keys, uint32_t n_docs,
-                             const uint64_t* img_off, uint32_t* tree, uint32_t kt) {
+                             const uint64_t* img_off, uint32_t* tree, uint32_t kt, uint32_t* hst) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= n_docs) return;
   const mte_doc_init in = inits[d];
   const uint32_t n_img = img_off ? (uint32_t)(img_off[d + 1] - img_off[d]) : 0u;
   const bool flat_legacy = (in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC)) == MTE_DOC_ROUND_SYNC;
-  const bool legacy = !(in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC)) && tree != nullptr;
+  // documents with the reference's tree: legacy ones (register tiers, then the
+  // HBM tree pass) and the HBM tree pass's own (a local client, or legacy with
+  // delta events)
+  const bool legacy = tree != nullptr && (!(in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC)) ||
+                                          (in.flags & MTE_DOC_LOCAL_CLIENT));
   DocHdr h;
   h.nseg = n_img ? (int32_t)n_img : (in.text_len > 0 || legacy ? 1 : 0);
   h.min_seq = in.min_seq;
@@ -140,13 +145,19 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
     h.pad1 = (uint32_t)in.cur_seq;  // every later increase must reach it
   }
   hdr[d] = h;
-  if (in.flags & MTE_DOC_LOCAL_CLIENT) {  // no pending property keys (mte_stream.h)
+  if (hst) {  // the HBM tree pass's state (mte_htree.h): a legacy doc enters it from the register tiers
+    uint32_t* st = hst + (uint64_t)d * kHtState;
+    st[kHsDepth] = h.pad1 & 0xffu;
+    st[kHsNextId] = h.pad0;
+    st[kHsHeapN] = 0u;
+    st[kHsLseq] = 0u;
+    st[kHsRhi] = 0u;
+    st[kHsEntered] = (in.flags & MTE_DOC_LOCAL_CLIENT) ? 1u : 0u;
+  }
+  if (in.flags & MTE_DOC_LOCAL_CLIENT) {  // nothing pending (mte_htree.h planes)
     const uint32_t nz = n_img ? n_img : 1u;
-    for (uint32_t k = 0; k < kt; k++)
+    for (uint32_t k = 0; k < 2 * kt + 2; k++)
       for (uint32_t x = 0; x < nz; x++) soa.props[(kt + k) * soa.plane_stride + (uint64_t)d * cap + x] = 0u;
-    for (uint32_t x = 0; x < nz; x++) soa.props[2ull * kt * soa.plane_stride + (uint64_t)d * cap + x] = 0u;  // no groups
-    for (uint32_t k = 0; k < kt; k++)
-      for (uint32_t x = 0; x < nz; x++) soa.props[(2ull * kt + 1 + k) * soa.plane_stride + (uint64_t)d * cap + x] = 0u;
   }
   if (n_img) return;  // image_kernel writes the segments
   const uint64_t i = (uint64_t)d * cap;
@@ -419,6 +430,14 @@ struct mte_ctx {
   uint2* d_heap = nullptr;          // LRU heap per document
   uint32_t* d_tree_docs = nullptr;  // the legacy documents
   uint32_t n_tree = 0;
+  // the HBM tree pass (mte_htree.h): legacy documents past the register tiers
+  // and every document with a local client (or legacy with delta events)
+  uint2* d_hheap = nullptr;         // heaps, hcap + 1 entries per document
+  uint32_t hcap = 0;
+  uint32_t* d_hst = nullptr;        // kHtState words per document
+  int32_t* d_hscr = nullptr;        // L / P scratch, 2 x cap per document
+  uint32_t* d_htree_docs = nullptr; // the candidates
+  uint32_t n_htree = 0;
   std::vector<uint8_t> h_legacy;    // per doc
   std::vector<uint8_t> h_local;     // per doc: MTE_DOC_LOCAL_CLIENT
   std::vector<uint8_t> h_events;    // per doc: MTE_DOC_EVENTS
@@ -455,6 +474,14 @@ struct mte_ctx {
   uint64_t* d_comm = nullptr;  // digests of all ranks / scalar reductions
   uint64_t comm_cap = 0;       // uint64 elements
   uint32_t n_rs = 0;
+  // per key, the largest property value id the context was given (load +
+  // every batch) and whether any text segment or annotate ever carried it:
+  // pass 1 packs the 4 property planes into one (kPack4) when every key's ids
+  // fit a byte, or all but a side key that only marker inserts ever set
+  // (ReplayArgs::side_key, config 3's markerId); sticky per context
+  uint32_t max_vid_k[MTE_MAX_KEYS] = {};
+  uint8_t key_text[MTE_MAX_KEYS] = {};
+  std::vector<uint8_t> h_text_ps;  // the batch's propsets a text insert or an annotate used
   // the largest property value id the context was given (load + every batch):
   // below 256 pass 1 packs the 4 property planes into one (kPack4);
   // MTE_PACK_PROPS=0 turns that off
@@ -567,7 +594,8 @@ void free_docs(mte_ctx* c) {
   if (c->d_wclock) (void)hipFree(c->d_wclock);
   c->d_wclock = nullptr;
   void* ps[] = {c->hdr, c->soa.len, c->stats, c->d_inits, c->d_init_props, c->d_digest, c->d_pairs,
-                c->d_tree, c->d_heap, c->d_tree_docs, c->d_rs_docs, c->d_refs};
+                c->d_tree, c->d_heap, c->d_tree_docs, c->d_rs_docs, c->d_refs, c->d_hheap, c->d_hst, c->d_hscr,
+                c->d_htree_docs};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   c->d_refs = nullptr;
@@ -577,6 +605,11 @@ void free_docs(mte_ctx* c) {
   c->d_heap = nullptr;
   c->d_tree_docs = nullptr;
   c->n_tree = 0;
+  c->d_hheap = nullptr;
+  c->d_hst = nullptr;
+  c->d_hscr = nullptr;
+  c->d_htree_docs = nullptr;
+  c->n_htree = 0;
   c->hdr = nullptr;
   c->soa = SegSoA{};
   c->stats = nullptr;
@@ -593,7 +626,7 @@ int launch_reset(mte_ctx* c) {
   const uint32_t blocks = (c->n_docs + 255) / 256;
   hipLaunchKernelGGL(reset_kernel, dim3(blocks), dim3(256), 0, c->stream, c->hdr, c->soa, c->cap,
                      c->d_inits, c->d_init_props, c->n_keys, c->n_docs, (const uint64_t*)c->d_img_off, c->d_tree,
-                     c->kt);
+                     c->kt, c->d_hst);
   HIPCHK(c, hipGetLastError());
   if (c->d_refs)
     HIPCHK(c, hipMemsetAsync(c->d_refs, 0, sizeof(uint2) * (size_t)c->ref_cap * c->n_docs, c->stream));
@@ -654,8 +687,10 @@ int round_phase_loop(mte_ctx* c, const ReplayArgs& a, size_t lds, uint64_t max_o
 template <int K, bool S>
 int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   // the tree pass: legacy length calc documents (mte_tree.h), up to 252
-  // items at E <= 4, then up to 1,020 at E = 8 / 16
-  if (c->n_tree) {
+  // items at E <= 4, then up to 1,020 at E = 8 / 16; then the HBM tree pass
+  // (mte_htree.h): the legacy documents past that and every document with a
+  // local client
+  if (c->n_tree || c->n_htree) {
     if (!c->tree_stream) {
       HIPCHK(c, hipStreamCreateWithFlags(&c->tree_stream, hipStreamNonBlocking));
       HIPCHK(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
@@ -665,13 +700,20 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
     // tree document), so the two streams share no document state
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->tree_stream, c->ev_fork, 0));
-    TreeArgs t{c->d_tree, c->d_heap, c->d_tree_docs, c->n_tree, c->arena, 0u, 0u};
-    // rounds of at most ~625 ops per document (MTE_TREE_ROUNDS overrides the count)
-    const uint64_t mx = c->max_doc_ops_s[c->rslot];
-    int rounds = c->tree_rounds > 0 ? c->tree_rounds : (int)std::min<uint64_t>(32, std::max<uint64_t>(1, (mx + 624) / 625));
-    const uint32_t per = (uint32_t)((mx + (uint64_t)rounds - 1) / (uint64_t)rounds);
-    HIPCHK(c, (launch_tree<K, S>(a, t, (c->n_tree + kDocsPerBlock - 1) / kDocsPerBlock, c->tree_stream, rounds,
-                                 per ? per : 1u)));
+    if (c->n_tree) {
+      TreeArgs t{c->d_tree, c->d_heap, c->d_tree_docs, c->n_tree, c->arena, 0u, 0u};
+      // rounds of at most ~625 ops per document (MTE_TREE_ROUNDS overrides the count)
+      const uint64_t mx = c->max_doc_ops_s[c->rslot];
+      int rounds = c->tree_rounds > 0 ? c->tree_rounds : (int)std::min<uint64_t>(32, std::max<uint64_t>(1, (mx + 624) / 625));
+      const uint32_t per = (uint32_t)((mx + (uint64_t)rounds - 1) / (uint64_t)rounds);
+      HIPCHK(c, (launch_tree<K, S>(a, t, (c->n_tree + kDocsPerBlock - 1) / kDocsPerBlock, c->tree_stream, rounds,
+                                   per ? per : 1u)));
+    }
+    if (c->n_htree) {
+      HtreeArgs ht{c->d_tree, c->d_heap, c->d_hheap, c->hcap, c->d_hst, c->d_hscr, c->d_htree_docs, c->n_htree,
+                   c->arena};
+      HIPCHK(c, (launch_htree<K, S>(a, ht, c->tree_stream)));
+    }
     HIPCHK(c, hipEventRecord(c->ev_join, c->tree_stream));
   }
   // pass 1: two documents per wavefront (docs up to 126 segments)
@@ -680,7 +722,17 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   // ever given), pass 1 holds the four planes as one packed register plane
   if (b1) {
     if constexpr (K == 4) {
-      if (c->max_vid < 256 && c->pack_props) HIPCHK(c, (launch_pair<kPack4, S>(a, b1, c->stream)));
+      uint32_t side = kNoKey;
+      bool pack = c->pack_props;
+      for (uint32_t k = 0; k < 4 && pack; k++) {
+        if (c->max_vid_k[k] < 256) continue;
+        if (side == kNoKey && !c->key_text[k]) side = k;  // set on markers only
+        else pack = false;
+      }
+      for (uint32_t k = 4; k < MTE_MAX_KEYS; k++) pack = pack && c->max_vid_k[k] == 0;  // kt = 4: 4 keys at most
+      ReplayArgs ap = a;
+      ap.side_key = side;
+      if (pack) HIPCHK(c, (launch_pair<kPack4, S>(ap, b1, c->stream)));
       else HIPCHK(c, (launch_pair<K, S>(a, b1, c->stream)));
     } else {
       HIPCHK(c, (launch_pair<K, S>(a, b1, c->stream)));
@@ -769,6 +821,8 @@ int upload_ops(mte_ctx* c, const mte_batch* b, int w, uint64_t* bad, const char*
   const unsigned nw = host_workers();
   std::atomic<uint64_t> first_bad{UINT64_MAX};
   std::vector<const char*> reasons(nw, nullptr);
+  // per worker: the propsets a text insert or an annotate used (kPack4 side key)
+  std::vector<std::vector<uint8_t>> tps(nw, std::vector<uint8_t>(b->n_propsets, 0));
   for (uint64_t k0 = 0, it = 0; k0 < b->n_ops; k0 += per_stage, it++) {
     const int si = (int)(it % mte_ctx::kStages);
     const uint64_t n = std::min(per_stage, b->n_ops - k0);
@@ -796,8 +850,12 @@ int upload_ops(mte_ctx* c, const mte_batch* b, int w, uint64_t* bad, const char*
         std::memcpy(dst + a, b->ops + k0 + a, (e - a) * sizeof(mte_op));
         // kRecNl: the insert's text holds a '\n' (the tree pass's append-merge
         // looks at a leaf's last unit only then, mte_tree.h)
+        std::vector<uint8_t>& tp = tps[w];
         for (uint64_t k = a; k < e; k++) {
           mte_op& o = dst[k];
+          if (o.type == MTE_OP_ANNOTATE && o.a < b->n_propsets) tp[o.a] = 1;
+          if (o.type == MTE_OP_INSERT && !(o.flags & MTE_F_MARKER) && o.b != MTE_NO_PROPS && o.b < b->n_propsets)
+            tp[o.b] = 1;
           o.flags = (uint16_t)(o.flags & ~kRecNl);
           if (o.type == MTE_OP_INSERT && !(o.flags & MTE_F_MARKER) && o.pos2 > 0) {
             const uint16_t* t = b->text + o.a;
@@ -823,6 +881,9 @@ int upload_ops(mte_ctx* c, const mte_batch* b, int w, uint64_t* bad, const char*
       if (r) *why = r;
     return MTE_E_INVALID_ARG;
   }
+  c->h_text_ps.assign(b->n_propsets, 0);
+  for (const auto& v : tps)
+    for (uint32_t i = 0; i < b->n_propsets; i++) c->h_text_ps[i] |= v[i];
   return MTE_OK;
 }
 
@@ -941,10 +1002,14 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
       return set_err(c, MTE_E_INVALID_ARG, "doc %u: initial text out of range", d);
     if ((in.flags & MTE_DOC_REFS) && !(in.flags & MTE_DOC_LOCAL_CLIENT))
       return set_err(c, MTE_E_UNSUPPORTED, "doc %u: local references need MTE_DOC_LOCAL_CLIENT", d);
-    if ((in.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)) &&
-        (!(in.flags & MTE_DOC_NEW_LENGTH_CALC) || c->cap >= kChunkMinCap))
-      return set_err(c, MTE_E_UNSUPPORTED, "doc %u: a local client or delta events need the new length "
-                     "calculation and a context below %u segments", d, kChunkMinCap);
+    // delta events of a new length-calc document without a local client come
+    // from the HBM-streamed flat pass, which big-document contexts do not run
+    if ((in.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)) == MTE_DOC_EVENTS &&
+        (in.flags & MTE_DOC_NEW_LENGTH_CALC) && c->cap >= kChunkMinCap)
+      return set_err(c, MTE_E_UNSUPPORTED, "doc %u: delta events of a document without a local client need a "
+                     "context below %u segments", d, kChunkMinCap);
+    if ((in.flags & MTE_DOC_ROUND_SYNC) && (in.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)))
+      return set_err(c, MTE_E_UNSUPPORTED, "doc %u: MTE_DOC_ROUND_SYNC with a local client or delta events", d);
     if (in.propset != MTE_NO_PROPS) {
       if (in.propset >= n_propsets || !propsets) return set_err(c, MTE_E_INVALID_ARG, "doc %u: bad propset", d);
       const mte_propset ps = propsets[in.propset];
@@ -960,6 +1025,15 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
   c->submitted = false;
   c->max_vid = 0;
   for (uint32_t i = 0; props && i < n_props; i++) c->max_vid = std::max(c->max_vid, props[i].value);
+  for (uint32_t k = 0; k < MTE_MAX_KEYS; k++) c->max_vid_k[k] = 0, c->key_text[k] = 0;
+  for (uint32_t i = 0; props && i < n_props; i++)
+    if (props[i].key < MTE_MAX_KEYS) c->max_vid_k[props[i].key] = std::max(c->max_vid_k[props[i].key], props[i].value);
+  for (uint32_t d = 0; d < n_docs; d++)  // the initial text's properties
+    if (docs[d].propset != MTE_NO_PROPS) {
+      const mte_propset ps = propsets[docs[d].propset];
+      for (uint32_t t = 0; t < ps.count; t++)
+        if (props[ps.first + t].key < MTE_MAX_KEYS) c->key_text[props[ps.first + t].key] = 1;
+    }
   c->ev_slot = -1;
   c->n_ops = 0;
   const uint64_t nslots = (uint64_t)(n_docs ? n_docs : 1) * c->cap;
@@ -970,7 +1044,10 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
   bool any_local = false, any_refs = false;
   c->h_sdocs.clear();
   for (uint32_t d = 0; d < n_docs; d++) {
-    if (docs[d].flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)) c->h_sdocs.push_back(d);
+    // the flat HBM-streamed pass's own: new length-calc documents with delta events and no local client
+    if ((docs[d].flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS | MTE_DOC_NEW_LENGTH_CALC)) ==
+        (MTE_DOC_EVENTS | MTE_DOC_NEW_LENGTH_CALC))
+      c->h_sdocs.push_back(d);
     if (docs[d].flags & MTE_DOC_LOCAL_CLIENT) c->h_local[d] = 1, any_local = true;
     if (docs[d].flags & MTE_DOC_EVENTS) c->h_events[d] = 1;
     if (docs[d].flags & MTE_DOC_REFS) c->h_refs[d] = 1, any_refs = true;
@@ -979,7 +1056,7 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
   // documents with a local client hold 2 kt + 1 more planes (mte_stream.h): the
   // pending property keys, the annotate-group mask and the keys' values before
   // their first pending annotate
-  const uint64_t prop_planes = (c->kt ? c->kt : 1) + (any_local ? 2 * c->kt + 1 : 0);
+  const uint64_t prop_planes = (c->kt ? c->kt : 1) + (any_local ? 2 * c->kt + 2 : 0);  // + localRemovedSeq
   HIPCHK(c, hipMalloc((void**)&c->hdr, sizeof(DocHdr) * (n_docs ? n_docs : 1)));
   // one allocation, planes at stride nslots: len seq rseq rmask meta toff props[kt]
   // (kt >= n_keys planes, so the register-resident kernels never index past it)
@@ -1038,11 +1115,15 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     // Legacy length-calc documents go to the tree pass instead (mte_tree.h).
     // Round-synchronous legacy documents (MTE_DOC_ROUND_SYNC) stay flat, behind
     // the per-batch check of round_sync_kernel.
-    std::vector<uint32_t> flat_docs, tree_docs, rs_docs;
-    c->h_legacy.assign(n_docs, 0);
+    std::vector<uint32_t> flat_docs, tree_docs, rs_docs, htree_docs;
+    c->h_legacy.assign(n_docs, 0);  // the document carries tree words (read-outs join merged leaves)
     for (uint32_t d = 0; d < n_docs; d++) {
-      if (docs[d].flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)) {
-        continue;  // the HBM-streamed pass replays them (mte_stream.h)
+      const uint32_t f = docs[d].flags;
+      if ((f & MTE_DOC_LOCAL_CLIENT) || ((f & MTE_DOC_EVENTS) && !(f & MTE_DOC_NEW_LENGTH_CALC))) {
+        htree_docs.push_back(d);  // the HBM tree pass's own (mte_htree.h)
+        c->h_legacy[d] = 1;
+      } else if (f & MTE_DOC_EVENTS) {
+        continue;  // the HBM-streamed flat pass replays them (mte_stream.h)
       } else if (docs[d].flags & MTE_DOC_NEW_LENGTH_CALC) {
         flat_docs.push_back(d);
       } else if (docs[d].flags & MTE_DOC_ROUND_SYNC) {
@@ -1071,11 +1152,26 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     }
     c->n_tree = (uint32_t)tree_docs.size();
     if (c->n_tree) {
-      HIPCHK(c, hipMalloc((void**)&c->d_tree, nslots * 4));
-      HIPCHK(c, hipMemsetAsync(c->d_tree, 0, nslots * 4, c->stream));
       HIPCHK(c, hipMalloc((void**)&c->d_heap, sizeof(uint2) * (kTreeHeapCap + 1) * (size_t)n_docs));
       HIPCHK(c, hipMalloc((void**)&c->d_tree_docs, tree_docs.size() * 4));
       HIPCHK(c, hipMemcpy(c->d_tree_docs, tree_docs.data(), tree_docs.size() * 4, hipMemcpyHostToDevice));
+    }
+    // the HBM tree pass takes its own documents and the legacy ones the
+    // register tiers hand over (past 1,020 items)
+    for (uint32_t d : tree_docs)
+      if (c->cap > 16 * kWave - 4) htree_docs.push_back(d);
+    c->n_htree = (uint32_t)htree_docs.size();
+    if (c->n_tree || c->n_htree) {
+      HIPCHK(c, hipMalloc((void**)&c->d_tree, nslots * 4));
+      HIPCHK(c, hipMemsetAsync(c->d_tree, 0, nslots * 4, c->stream));
+    }
+    if (c->n_htree) {
+      c->hcap = c->cap;  // one heap entry per slot
+      HIPCHK(c, hipMalloc((void**)&c->d_hheap, sizeof(uint2) * ((size_t)c->hcap + 1) * n_docs));
+      HIPCHK(c, hipMalloc((void**)&c->d_hst, sizeof(uint32_t) * kHtState * (size_t)n_docs));
+      HIPCHK(c, hipMalloc((void**)&c->d_hscr, sizeof(int32_t) * 2 * nslots));
+      HIPCHK(c, hipMalloc((void**)&c->d_htree_docs, htree_docs.size() * 4));
+      HIPCHK(c, hipMemcpy(c->d_htree_docs, htree_docs.data(), htree_docs.size() * 4, hipMemcpyHostToDevice));
     }
   }
   if (n_docs) {
@@ -1167,6 +1263,7 @@ int mte_load_segments(mte_ctx* c, const uint64_t* seg_offsets, const mte_seg* se
         for (uint32_t t = 0; t < ps.count; t++) {
           const mte_prop p = c->h_load_pe[ps.first + t];
           if (p.key < c->n_keys) img[(uint64_t)(kFieldPlanes + p.key) * n_segs + g] = p.value;
+          if (p.key < MTE_MAX_KEYS && sg.kind == 0) c->key_text[p.key] = 1;  // a text segment's key (kPack4 side key)
         }
       }
       doc[g] = d;
@@ -1224,6 +1321,8 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
     const char* why = "";
     if ((rc = upload_ops(c, b, w, &bad, &why)))
       return rc == MTE_E_INVALID_ARG ? set_err(c, rc, "op %llu: %s", (unsigned long long)bad, why) : rc;
+  } else {
+    c->h_text_ps.clear();
   }
   // append batch text to the arena (a running replay reads only below arena_n;
   // growing it waits for the replay)
@@ -1277,7 +1376,18 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
       off.clear();
     }
   }
-  for (uint32_t i = 0; b->props && i < b->n_props; i++) c->max_vid = std::max(c->max_vid, b->props[i].value);
+  for (uint32_t i = 0; b->props && i < b->n_props; i++) {
+    c->max_vid = std::max(c->max_vid, b->props[i].value);
+    if (b->props[i].key < MTE_MAX_KEYS)
+      c->max_vid_k[b->props[i].key] = std::max(c->max_vid_k[b->props[i].key], b->props[i].value);
+  }
+  // the keys of every propset a text insert or an annotate used (upload_ops)
+  for (uint32_t i = 0; i < b->n_propsets && i < c->h_text_ps.size(); i++)
+    if (c->h_text_ps[i]) {
+      const mte_propset ps = b->propsets[i];
+      for (uint32_t t = 0; t < ps.count; t++)
+        if (b->props[ps.first + t].key < MTE_MAX_KEYS) c->key_text[b->props[ps.first + t].key] = 1;
+    }
   c->n_ops_s[w] = b->n_ops;
   c->n_propsets_s[w] = b->n_propsets;
   uint64_t mx = 0;
@@ -1335,9 +1445,22 @@ int mte_run(mte_ctx* c) {
   a.refs = c->d_refs;
   a.ref_cap = c->ref_cap;
   a.sorder = c->h_sdocs.empty() ? nullptr : c->d_sorder_s[c->rslot];
-  // s_memrealtime runs at 100 MHz: ticks = ms x 1e5, scaled to this batch's ops
-  a.eta = (c->last_ms > 0 && c->last_ops > 0) ? (unsigned long long)(c->last_ms * 1e5 * (double)c->n_ops / c->last_ops)
-                                              : 0ull;
+  // s_memrealtime runs at 100 MHz: ticks = ms x 1e5, scaled to this batch's
+  // ops.  A context's first run has no previous duration: it is estimated from
+  // the batch, the larger of a saturated chip's throughput (0.215 ns per op,
+  // configs 3 and 4 on one MI355X) and one wave's chain over its documents'
+  // ops (0.85 us per op alone on its SIMD, the 1,250-document and config-2
+  // batches) -- within a few per cent of the measured pass-1 times
+  // (DESIGN.md §6), which is what the schedule's bands need
+  double eta_ms = 0.0;
+  if (c->last_ms > 0 && c->last_ops > 0) {
+    eta_ms = c->last_ms * (double)c->n_ops / c->last_ops;
+  } else if (c->n_ops) {
+    const double thr = 2.15e-7 * (double)c->n_ops;
+    const double chain = 8.5e-4 * (double)c->max_doc_ops_s[c->rslot] * (double)c->pass1_group;
+    eta_ms = std::max(thr, chain);
+  }
+  a.eta = (unsigned long long)(eta_ms * 1e5);
   if (c->wclock_path) {
     if (!c->d_wclock) HIPCHK(c, hipMalloc((void**)&c->d_wclock, 16ull * (c->n_pairs + 1)));
     a.wclock = c->d_wclock;
@@ -1362,7 +1485,7 @@ int mte_run(mte_ctx* c) {
   c->ran = true;
   const int slot = c->rslot;
   auto finish = [c, slot]() -> int {
-    if (c->n_tree) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    if (c->n_tree || c->n_htree) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     HIPCHK(c, hipEventRecord(c->slot_ev[slot], c->stream));  // the slot may be rewritten after this
     return MTE_OK;

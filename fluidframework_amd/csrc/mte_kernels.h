@@ -97,6 +97,11 @@ struct ReplayArgs {
   unsigned long long* gdone;   // pass 1: ops applied so far by all waves (fair priority), zeroed per run
   unsigned long long n_ops;    // ops of the batch
   unsigned long long eta;      // expected pass-1 duration in s_memrealtime ticks (0 = unknown)
+  // kPack4 with a side key: the key (< 4) whose value ids may exceed a byte
+  // because only marker inserts ever set it (markerId); pass 1 holds a
+  // marker's value of it in the marker's toff register (a marker has no text)
+  // and the key's byte stays 0.  kNoKey: none.
+  uint32_t side_key;
   // MTE_DOC_EVENTS documents: delta events of doc d go to dl[dl_off[d] ..
   // dl_off[d + 1]); dl_n[d] = how many the batch produced (more = overflow)
   mte_delta* dl;

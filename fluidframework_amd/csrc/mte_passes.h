@@ -12,6 +12,7 @@ namespace mte {
 
 struct ReplayArgs;
 struct TreeArgs;
+struct HtreeArgs;
 struct ChunkArgs;
 
 // round phases of the chunked pass (mte_round.h)
@@ -41,6 +42,9 @@ constexpr uint32_t kRoundLdsMax = 150u * 1024u;
 template <int K, bool S>
 hipError_t launch_tree(const ReplayArgs& a, const TreeArgs& t, uint32_t blocks, hipStream_t s, int rounds,
                        uint32_t per_round);
+// the HBM tree pass (mte_htree.h): one wavefront per candidate document
+template <int K, bool S>
+hipError_t launch_htree(const ReplayArgs& a, const HtreeArgs& t, hipStream_t s);
 // pass 1 (ReplayArgs::group documents per wavefront) and pass 2 (one per
 // wavefront); pass1_waves() = the waves per SIMD pass 1's register budget is
 // built for (the host sizes the groups so the batch is resident at once)

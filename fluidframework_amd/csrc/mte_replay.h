@@ -171,13 +171,15 @@ template <int E, int K>
 __device__ __forceinline__ void apply_props(uint32_t (&pr)[kRP<K>][E], const bool (&sel)[E], uint32_t pk,
                                             uint32_t v0, uint32_t v1, uint32_t psi, const ReplayArgs& a) {
   const uint32_t k0 = pk & 0xffu, k1 = (pk >> 8) & 0xffu;
-  if (k0 != kNoKey) set_plane<E, K>(pr, sel, k0, v0);
-  if (k1 != kNoKey) set_plane<E, K>(pr, sel, k1, v1);
+  // kPack4: the side key never goes into the packed bytes (ReplayArgs::side_key)
+  const uint32_t skip = K == kPack4 ? a.side_key : kNoKey;
+  if (k0 != kNoKey && k0 != skip) set_plane<E, K>(pr, sel, k0, v0);
+  if (k1 != kNoKey && k1 != skip) set_plane<E, K>(pr, sel, k1, v1);
   if (pk >> 16) {
     const mte_propset ps = a.ps[psi];
     for (uint32_t t = 2; t < ps.count; t++) {
       const mte_prop p = a.pe[ps.first + t];
-      if (p.key < a.n_keys) set_plane<E, K>(pr, sel, uni(p.key), uni(p.value));
+      if (p.key < a.n_keys && p.key != skip) set_plane<E, K>(pr, sel, uni(p.key), uni(p.value));
     }
   }
 }
@@ -303,9 +305,14 @@ __device__ __forceinline__ void load_regs(Regs<E, K>& R, const DocRun& D, const 
     R.meta[j] = v ? pl[4 * st + x] : 0u;
     R.toff[j] = v ? pl[5 * st + x] : 0u;
     if constexpr (K == kPack4) {
+      // the side key's value of a marker rides in its toff register
       uint32_t w = 0;
 #pragma unroll
-      for (int k = 0; k < 4; k++) w |= (v ? pl[(kFieldPlanes + k) * st + x] : 0u) << (8 * k);
+      for (int k = 0; k < 4; k++) {
+        const uint32_t pv = v ? pl[(kFieldPlanes + k) * st + x] : 0u;
+        if ((uint32_t)k == a.side_key) R.toff[j] = (R.meta[j] >> 8) ? pv : R.toff[j];
+        else w |= pv << (8 * k);
+      }
       R.pr[0][j] = w;
     } else {
 #pragma unroll
@@ -329,11 +336,15 @@ __device__ __forceinline__ void store_regs(const Regs<E, K>& R, const DocRun& D,
       pl[2 * st + x] = (uint32_t)R.rseq[j];
       pl[3 * st + x] = R.rmask[j];
       pl[4 * st + x] = R.meta[j];
-      pl[5 * st + x] = R.toff[j];
       if constexpr (K == kPack4) {
+        const bool mk = (R.meta[j] >> 8) != 0 && a.side_key < 4u;
+        pl[5 * st + x] = mk ? 0u : R.toff[j];
 #pragma unroll
-        for (int k = 0; k < 4; k++) pl[(kFieldPlanes + k) * st + x] = (R.pr[0][j] >> (8 * k)) & 0xffu;
+        for (int k = 0; k < 4; k++)
+          pl[(kFieldPlanes + k) * st + x] =
+              (uint32_t)k == a.side_key ? (mk ? R.toff[j] : 0u) : (R.pr[0][j] >> (8 * k)) & 0xffu;
       } else {
+        pl[5 * st + x] = R.toff[j];
 #pragma unroll
         for (int k = 0; k < K; k++) pl[(kFieldPlanes + k) * st + x] = R.pr[k][j];
       }

@@ -168,7 +168,7 @@ __device__ __forceinline__ void put_new_v(Regs<E, K>& R, const bool (&at)[E], co
   const bool marker = (flags & MTE_F_MARKER) != 0;
   const int32_t nlen = marker ? 1 : pos2;
   const uint32_t meta = (c + 1u) | (marker ? (1u + (uint32_t)pos2) << 8 : 0u);
-  const uint32_t toff = marker ? 0u : a.text_base + (uint32_t)op[6];
+  uint32_t toff = marker ? 0u : a.text_base + (uint32_t)op[6];
   const uint32_t psi = (uint32_t)op[7];
   uint32_t pr[kRP<K>][1];
   const bool one[1] = {true};
@@ -178,6 +178,21 @@ __device__ __forceinline__ void put_new_v(Regs<E, K>& R, const bool (&at)[E], co
     const s8v q2 = sload_props(a, psi);
     apply_props<1, K>(pr, one, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], psi, a);
     MTE_STAT(st[kStPwrites] += (uint32_t)q2[3];)
+    if constexpr (K == kPack4) {
+      // a marker's side-key value goes to its toff register (ReplayArgs::side_key)
+      if (marker && a.side_key < 4u) {
+        const uint32_t pk = (uint32_t)q2[0];
+        if ((pk & 0xffu) == a.side_key) toff = (uint32_t)q2[1];
+        if (((pk >> 8) & 0xffu) == a.side_key) toff = (uint32_t)q2[2];
+        if (pk >> 16) {
+          const mte_propset ps = a.ps[psi];
+          for (uint32_t t = 2; t < ps.count; t++) {
+            const mte_prop p = a.pe[ps.first + t];
+            if (p.key == a.side_key) toff = uni(p.value);
+          }
+        }
+      }
+    }
   }
   MTE_STAT(if (!marker) st[kStUnits] += (uint32_t)pos2;)
 #pragma unroll

@@ -1110,12 +1110,14 @@ __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
   if (idx >= (int)a.n_docs) return;
   // longest batch first (a.sorder): the long local-client chains start first
   const int doc = a.sorder ? (int)__builtin_amdgcn_readfirstlane((int)a.sorder[idx]) : idx;
-  // documents pass 2 escalated, and every document with a local client
+  // documents pass 2 escalated, and the new length-calc documents with delta
+  // events and no local client (a local client's go to the HBM tree pass)
   const uint32_t hf = a.hdr[doc].flags;
-  constexpr uint32_t kOwn = MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS;  // docs this pass always replays
-  if (!(hf & (kHdrNeedsEsc | kOwn))) return;  // untouched doc: leave the header alone
+  if (hf & MTE_DOC_LOCAL_CLIENT) return;
+  const bool own = (hf & (MTE_DOC_EVENTS | MTE_DOC_NEW_LENGTH_CALC)) == (MTE_DOC_EVENTS | MTE_DOC_NEW_LENGTH_CALC);
+  if (!(hf & kHdrNeedsEsc) && !own) return;  // untouched doc: leave the header alone
   DocRun D;
-  run_init(D, a, doc, !(hf & kOwn));
+  run_init(D, a, doc, !own);
   uint32_t st[kNumStats] = {};
   int32_t lseq = (int32_t)a.hdr[doc].pad0;  // local-client docs: the last localSeq
   uint32_t rhi = (hf & MTE_DOC_REFS) ? a.hdr[doc].pad1 : 0u;  // MTE_DOC_REFS docs: reference slots in use

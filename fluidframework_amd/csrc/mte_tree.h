@@ -36,6 +36,7 @@ namespace mte {
 constexpr int kTreeHeapCap = 255;  // entries per document (+ the unused index 0)
 constexpr uint32_t kHdrTreeEsc = 0x40000000u;  // tree pass: the document is TIER 1's (E = 4)
 constexpr uint32_t kHdrTreeBig = 0x20000000u;  // tree pass: the document is TIER 2's (E = 8, 16)
+constexpr uint32_t kHdrTreeHbmFlag = 0x10000000u;  // past TIER 2: the HBM tree pass (mte_htree.h kHdrTreeHbm)
 constexpr uint32_t kTH = 0x7u, kTCont = 0x8u, kTNsShift = 4, kTNs = 0x30u, kTPo = 0x40u, kTEmpty = 0x80u;
 constexpr uint32_t kTNl = 0x80000000u;
 constexpr uint16_t kRecNl = 0x8000u;  // op record flag (engine-internal): the insert's text holds a '\n'
@@ -970,7 +971,7 @@ __device__ __forceinline__ void tree_burst(DocRun& D, TreeRun& tr, const ReplayA
 template <int K, bool S, int TIER>
 __global__ __launch_bounds__(256) void tree_kernel(ReplayArgs a, TreeArgs t) {
   constexpr int EMAX = TIER == 2 ? 16 : TIER == 1 ? 4 : 2;
-  constexpr uint32_t kTierFlags = kHdrTreeEsc | kHdrTreeBig;
+  constexpr uint32_t kTierFlags = kHdrTreeEsc | kHdrTreeBig | kHdrTreeHbmFlag;
   __shared__ uint32_t zlds_all[kDocsPerBlock][kWave * EMAX];
   __shared__ __attribute__((aligned(16))) uint2 heap_all[kDocsPerBlock][kTreeHeapCap + 1];
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
@@ -1012,8 +1013,12 @@ __global__ __launch_bounds__(256) void tree_kernel(ReplayArgs a, TreeArgs t) {
   uint32_t* zlds = zlds_all[w];
   while (D.running) {
     const int n = D.n;
-    if (n + 4 > (int)a.cap || n + 4 > 16 * kWave) {
+    if (n + 4 > (int)a.cap) {
       D.status = MTE_E_CAPACITY;
+      break;
+    }
+    if (n + 4 > 16 * kWave) {  // past the registers: the HBM tree pass goes on (mte_htree.h)
+      D.flags |= kHdrTreeHbmFlag;
       break;
     }
     if constexpr (TIER == 0) {

@@ -122,8 +122,8 @@ class MergeTreeEngine {
     if (o.summary) o = Object.assign({}, o, { legacy: o.summary });
     if (o.legacy) o = Object.assign({}, o, loadLegacy(o.legacy));
     const doc = this.docs.length;
-    if ((o.localClient || o.events) && !o.newLengthCalc) {
-      throw new MergeTreeError(-9, "a local client or delta events need the new length calculation");
+    if ((o.localClient || o.events) && o.roundSync) {
+      throw new MergeTreeError(-9, "roundSync with a local client or delta events");
     }
     if (o.refs && !o.localClient) throw new MergeTreeError(-9, "local references need {localClient: true}");
     this.docs.push({ text: initialText || "", newLengthCalc: !!o.newLengthCalc, roundSync: !!o.roundSync, props: o.props,

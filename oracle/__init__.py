@@ -11,7 +11,7 @@ import subprocess
 
 import numpy as np
 
-from fluidframework_amd.abi import DOC_INIT_DTYPE, PROP_DTYPE, PROPSET_DTYPE, SEG_DTYPE, ptr  # noqa: F401
+from fluidframework_amd.abi import DOC_INIT_DTYPE, DOC_LOCAL_CLIENT, PROP_DTYPE, PROPSET_DTYPE, SEG_DTYPE, ptr  # noqa: F401
 from fluidframework_amd.engine import EngineBase, _arr, make_batch_struct
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -51,6 +51,10 @@ def load():
         "oti_read_doc": [vp, u32, vp], "oti_digest": [vp, vp, u32], "oti_doc_status": [vp, vp, u32],
         "oti_doc_nsegs": [vp, u32, vp], "oti_stats_get": [vp, vp], "oti_read_segments": [vp, u32, vp], "oti_set_limit": [vp, u32],
         "oti_read_deltas": [vp, u32, vp, u64, vp], "oti_read_refs": [vp, u32, vp, u32],
+        "och_create": [u32, vp], "och_destroy": [vp], "och_load_docs": [vp, u32, vp, vp, u64, vp, u32, vp, u32],
+        "och_load_segments": [vp, vp, vp, u64], "och_apply_batch": [vp, vp, C.c_int], "och_read_doc": [vp, u32, vp],
+        "och_digest": [vp, vp, u32], "och_doc_status": [vp, vp, u32], "och_doc_nsegs": [vp, u32, vp],
+        "och_stats_get": [vp, vp],
     }.items():
         f = getattr(lib, name)
         f.argtypes = args
@@ -84,11 +88,12 @@ class OracleEngine(EngineBase):
     (tree.c), which keeps the reference's B+tree, its lazy zamboni and therefore
     its insert placement next to tombstones in legacy length-calc documents.
     tree="items": the same tree on a flat item array (titems.c), the spec of
-    the GPU tree pass."""
+    the GPU tree pass.  tree="chunked": the flat restatement with a chunk index
+    (chunked.c), for config 5's documents of millions of segments."""
 
     def __init__(self, n_keys=0, threads=1, tree=False):
         self.lib = load()
-        self.f = _Fn(self.lib, "oti" if tree == "items" else ("ort" if tree else "orc"))
+        self.f = _Fn(self.lib, {"items": "oti", "chunked": "och"}.get(tree, "ort" if tree else "orc"))
         self.tree = tree
         self.n_keys = n_keys
         self.threads = threads
@@ -194,15 +199,18 @@ class SpecOracle:
         self.n_keys = n_keys
         self.flat = OracleEngine(n_keys, threads)
         self.tree = OracleEngine(n_keys, threads, tree="items")
-        # the tree pass holds a document in registers: at most 16 x 64 slots
-        # (or the ctx capacity), 4 kept free for one op's new items
+        # the tree pass holds a document in registers up to 1,020 items, then
+        # in HBM (mte_htree.h) up to the ctx capacity, 4 slots kept free for
+        # one op's new items
         cap = cap or 1024
-        self.tree.lib.oti_set_limit(self.tree.ctx, min(1024, max(cap, 64)))
+        self.tree.lib.oti_set_limit(self.tree.ctx, max(cap, 64))
         self.n_docs = 0
 
     def load_docs(self, inits, text=None, propsets=None, props=None):
         inits = _arr(inits, DOC_INIT_DTYPE)
-        flat = (inits["flags"] & 3) != 0  # MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC
+        # flat: MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC without a local client;
+        # the tree: legacy documents and every document with a local client
+        flat = ((inits["flags"] & 3) != 0) & ((inits["flags"] & DOC_LOCAL_CLIENT) == 0)
         self.sub = [np.where(flat)[0], np.where(~flat)[0]]  # flat, tree
         self.where = np.zeros((len(inits), 2), np.int64)
         for e, idx in enumerate(self.sub):
@@ -261,6 +269,16 @@ class SpecOracle:
     def read_refs(self, doc, n):
         e, i = self.where[doc]
         return self._engines()[e].read_refs(int(i), n)
+
+    def read_deltas(self, doc):
+        e, i = self.where[doc]
+        return self._engines()[e].read_deltas(int(i))
+
+    def set_event_capacity(self, per_op):
+        """The restatements' event buffers grow as needed."""
+
+    def set_ref_capacity(self, per_doc):
+        """The restatements' reference slots grow as needed."""
 
     def stats(self):
         zero = {"ops_applied": 0, "segs_scanned": 0, "segs_written": 0, "prop_writes": 0, "units_inserted": 0,

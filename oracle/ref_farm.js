@@ -40,6 +40,8 @@
 //                    "events": [[["L"|"A", logIndex] | ["R", op], ...] per client],
 //                    "checkpoints": [{"done": [events applied per client],
 //                                     "states": [{"text", "props": [[start, end, {..}]]}]}]}]}
+//          legacy: the clients keep the default (legacy) length calculation
+//         instead of mergeTreeUseNewLengthCalculations
 // Client 0 ("A") never sends: the observer.
 "use strict";
 const path = require("path");
@@ -110,7 +112,8 @@ function runSet(p) {
   const names = [];
   for (let i = 0; i < p.clients; i++) names.push(String.fromCharCode(65 + i));
   const clients = names.map((n) => {
-    const c = new Client(specToSegment, logger, { mergeTreeUseNewLengthCalculations: true });
+    // legacy: the default length calculation (mergeTree.ts:386-399)
+    const c = new Client(specToSegment, logger, { mergeTreeUseNewLengthCalculations: !p.legacy });
     if (p.initialText) c.insertSegmentLocal(0, new TextSegment(p.initialText));
     c.startOrUpdateCollaboration(n);
     return c;

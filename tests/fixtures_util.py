@@ -184,7 +184,7 @@ def prop_runs(view, interner):
     return runs
 
 
-def canon_regen(op, orig):
+def canon_regen(op, orig, merge=True):
     """A regenerated op as compared with the reference's: an insert of a segment
     whose original spec had no props carries, in the reference, the segment's
     props at regeneration time (createInsertSegmentOp(pos, segment),
@@ -202,7 +202,7 @@ def canon_regen(op, orig):
                 o = dict(o, seg=seg)
         return o
 
-    def merge(out, o):
+    def merge_into(out, o):
         # the same edit in fewer ops: the reference append-merges adjacent acked
         # segments (zamboni, mergeTree.ts:681-747) that the flat state keeps apart,
         # so its segment groups -- one op per segment -- can be coarser
@@ -226,11 +226,14 @@ def canon_regen(op, orig):
     src = srcs[0] if len(srcs) == 1 else None
     out = []
     for o in ops:
-        merge(out, one(o, src))
+        if merge:
+            merge_into(out, one(o, src))
+        else:
+            out.append(one(o, src))
     return json.dumps(out, sort_keys=True)
 
 
-def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None):
+def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_regen=False):
     """Replay farms the reference ran (oracle/ref_farm.js -> tests/golden/
     farm_vectors.json.gz): one MTE_DOC_LOCAL_CLIENT document per client of every
     set (the observer "A" included), each fed its own events in order — "L" a
@@ -243,7 +246,9 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None):
     removeLocalReferencePosition) — in one batch per checkpoint; text,
     per-position properties and, for sets with references, every reference's
     position (localReferencePositionToPosition) must equal the reference
-    client's at every checkpoint.  regen_checks (a list) collects one entry per "G" event compared.
+    client's at every checkpoint.  regen_checks (a list) collects one entry per "G" event compared;
+    exact_regen compares the regenerated ops one for one (the tree keeps the
+    reference's segment groups), else in merged form (canon_regen).
     Returns (checkpoints_passed, failures)."""
     from fluidframework_amd.abi import DOC_EVENTS, DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC, DOC_REFS
     from fluidframework_amd.packing import regen_ops
@@ -254,6 +259,9 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None):
     inits, text = doc_inits([sets[si]["initialText"] for si, _ in layout],
                             flags=DOC_NEW_LENGTH_CALC | DOC_LOCAL_CLIENT | (DOC_EVENTS if has_regen else 0) |
                             (DOC_REFS if has_refs else 0))
+    for d, (si, _) in enumerate(layout):  # sets the reference ran with the legacy length calculation
+        if sets[si].get("legacy"):
+            inits[d]["flags"] = int(inits[d]["flags"]) & ~DOC_NEW_LENGTH_CALC & 0xffffffff
     interner = Interner(n_keys)
     eng = engine_factory(n_keys)
     if has_regen:
@@ -307,7 +315,7 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None):
                 continue
             want_op = sets[si]["log"][li][5]
             got_op = regen_ops(orig, idx, eng.read_deltas(d))
-            ok = canon_regen(got_op, orig) == canon_regen(want_op, orig)
+            ok = canon_regen(got_op, orig, not exact_regen) == canon_regen(want_op, orig, not exact_regen)
             if regen_checks is not None:
                 regen_checks.append(ok)
             if not ok:

@@ -11,13 +11,17 @@ properties at checkpoints.  The file holds only that data — messages, event
 orders and expected read-outs — no reference source.  Run in the build
 container (the reference does not exist on the GPU box).
 
+With --legacy it writes tests/golden/legacy_farm_vectors.json.gz: farms whose
+clients keep the default (legacy) length calculation, with lagging clients,
+rollbacks of removes, reconnects and local references among the sets.
+
 With --refs it writes tests/golden/localref_vectors.json.gz instead: farms in
 which every client (the observer included) also creates local references at
 positions of its own view and removes some (Client.createLocalReferencePosition
 / removeLocalReferencePosition, SlideOnRemove or Simple), each checkpoint
 holding every reference's localReferencePositionToPosition.
 
-Usage: python3 tests/golden/make_farm_golden.py [--refs]
+Usage: python3 tests/golden/make_farm_golden.py [--refs | --legacy]
 """
 import gzip
 import json
@@ -33,6 +37,7 @@ import ref_util  # noqa: E402
 
 OUT = os.path.join(HERE, "farm_vectors.json.gz")
 OUT_REFS = os.path.join(HERE, "localref_vectors.json.gz")
+OUT_LEGACY = os.path.join(HERE, "legacy_farm_vectors.json.gz")
 FARM_JS = os.path.join(ROOT, "oracle", "ref_farm.js")
 
 # (seed, clients incl. the observer, steps, initial text, checkpoints, text bound)
@@ -59,6 +64,39 @@ ROLLBACK_ANNOTATE_SETS = [(4000 + i, 2 + i % 6, 400 + 100 * (i % 3), ["", "hello
 REF_SETS = [(7000 + i, 2 + i % 6, 300 + 100 * (i % 5), ["", "hello world", "abc\ndef"][i % 3], 5, [64, 200, 400][i % 3],
              [0.0, 0.2][i % 2], [1, 2] if i % 4 == 3 else None, [0.1, 0.25][(i % 2) if i < 20 else 1 - i % 2])
             for i in range(40)]
+
+
+# legacy length calculation: (seed, clients, steps, initial text, checkpoints,
+# text bound, extra parameters)
+LEGACY_SETS = ([(8000 + i, 2 + i % 7, 300 + 150 * (i % 6), ["", "hello world", "abc\ndef"][i % 3], 4,
+                 [64, 200, 400][i % 3], {}) for i in range(16)] +
+               [(8100 + i, 3 + i % 4, 400, ["hello world", ""][i % 2], 4, 200, {"rollback": 0.15})
+                for i in range(8)] +
+               [(8200 + i, 3 + i % 4, 400, "hello world", 5, 200, {"reconnect": 0.1, "allowDiverge": True})
+                for i in range(10)] +
+               [(8300 + i, 2 + i % 5, 300 + 100 * (i % 3), ["", "hello world"][i % 2], 5, 200, {"refs": 0.2})
+                for i in range(8)])
+
+
+def main_legacy(out):
+    res = {"sets": [], "generator": "oracle/ref_farm.js, legacy length calculation (reference Client, mulberry32 seeds)"}
+    failed = []
+    for sd, c, n, t, k, m, extra in LEGACY_SETS:
+        # the reference's legacy-calc clients do not always converge (a reason the
+        # new calculation exists): each client of ours must equal its reference
+        # client, whatever the others hold
+        one = dict({"seed": sd, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
+                    "legacy": True, "allowDiverge": True}, **extra)
+        q = subprocess.run(["node", FARM_JS, out], input=json.dumps({"sets": [one]}), capture_output=True, text=True,
+                           timeout=600)
+        if q.returncode == 0:
+            res["sets"] += json.loads(q.stdout)["sets"]
+        else:
+            failed.append(sd)
+    res["seeds_the_reference_failed"] = failed
+    with gzip.open(OUT_LEGACY, "wt", encoding="utf-8") as fh:
+        json.dump(res, fh, separators=(",", ":"))
+    print(f"{len(res['sets'])} legacy sets, reference failed on {failed}")
 
 
 def main_refs(out):
@@ -88,6 +126,8 @@ def main():
     out = ref_util.build_ref()
     if "--refs" in sys.argv[1:]:
         return main_refs(out)
+    if "--legacy" in sys.argv[1:]:
+        return main_legacy(out)
     inp = {"sets": [{"seed": s, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
                      "rollback": rb} for s, c, n, t, k, m, rb in SETS]}
     p = subprocess.run(["node", "--max-old-space-size=8192", FARM_JS, out], input=json.dumps(inp),

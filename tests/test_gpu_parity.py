@@ -172,14 +172,25 @@ def test_gpu_stream_pass_long_docs_all_ops():
     assert_same(o, d, sample_docs=6)
 
 
-def test_gpu_tree_pass_capacity_for_long_legacy_docs():
-    # the same legacy documents outgrow the tree pass (1,020 items) and stop
-    # with MTE_E_CAPACITY, as the specification does, never diverging
+def test_gpu_tree_pass_long_legacy_docs_go_on_in_hbm():
+    # the same legacy documents outgrow the register tiers (1,020 items) and go
+    # on in the HBM tree pass (mte_htree.h) to the end of the batch, equal to
+    # the specification (titems.c) in statuses, digests, statistics and read-outs
     s = gen.generate(3, n_docs=6, ops_per_doc=4000, init_len=20000, round_ops=1024, min_length=16,
                      length_mode=1)
     o, d = replay_both_cap(s, 16384)
-    assert (o.statuses() == MTE_E_CAPACITY).all()
+    assert (o.statuses() == 0).all()
+    assert o.stats()["max_segs"] > 1020
     assert_same(o, d, sample_docs=6)
+
+
+def test_gpu_tree_pass_capacity_is_the_context_capacity():
+    # a legacy document stops with MTE_E_CAPACITY only at the ctx capacity
+    s = gen.generate(3, n_docs=4, ops_per_doc=4000, init_len=20000, round_ops=1024, min_length=16,
+                     length_mode=1)
+    o, d = replay_both_cap(s, 1536)
+    assert (o.statuses() == MTE_E_CAPACITY).all()
+    assert_same(o, d, sample_docs=4)
 
 
 def test_gpu_stream_pass_annotate_heavy():

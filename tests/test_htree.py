@@ -1,0 +1,134 @@
+"""The HBM tree pass (csrc/mte_htree.h) and its specification, the tree
+restatement with local records (oracle/titems.c).
+
+Two classes of documents replay on the reference's B+tree beyond what the
+register tiers hold:
+  * legacy length-calc documents past 1,020 items: lagging streams that grow to
+    ~10-20k items, checked against titems.c and the linked-block tree.c;
+  * documents with a local client, in either length mode: the reference's own
+    farms (tests/golden/*_vectors.json.gz, made by oracle/ref_farm.js) with
+    every client on the engine -- new length calculation (farm, reconnect,
+    local-reference sets) and the legacy one (legacy_farm_vectors.json.gz:
+    plain, rollback, reconnect and reference farms; the reference's legacy
+    clients need not converge, so each client is held to its own reference
+    client, and the six seeds where the reference throws "MergeTree insert
+    failed" are left out and listed in the file).
+"""
+import gzip
+import json
+import os
+
+import numpy as np
+import pytest
+
+from fixtures_util import replay_ref_farm
+from fluidframework_amd import gen
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def vector_sets(name):
+    with gzip.open(os.path.join(HERE, "golden", name), "rt", encoding="utf-8") as fh:
+        return json.load(fh)
+
+
+def tree_factory(k):
+    from oracle import OracleEngine
+    e = OracleEngine(k, tree="items")
+    e.lib.oti_set_limit(e.ctx, 1 << 20)
+    return e
+
+
+def device_factory(k):
+    from fluidframework_amd.engine import DeviceEngine
+    return DeviceEngine(k)
+
+
+def _farms(factory, name):
+    sets = vector_sets(name)["sets"]
+    checks = []
+    passed, failures = replay_ref_farm(factory, sets, regen_checks=checks, exact_regen=True)
+    assert not failures, failures[:2]
+    assert passed == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
+    assert all(checks)
+    return passed, len(checks)
+
+
+def test_legacy_farm_vectors_shape():
+    v = vector_sets("legacy_farm_vectors.json.gz")
+    sets = v["sets"]
+    assert len(sets) == 36 and all(s["legacy"] for s in sets)
+    assert sorted(v["seeds_the_reference_failed"]) == [8004, 8009, 8010, 8107, 8202, 8301]
+    kinds = {"R" for s in sets for ev in s["events"] for e in ev if e[0] == "R"}
+    kinds |= {"G" for s in sets for ev in s["events"] for e in ev if e[0] == "G"}
+    kinds |= {"F" for s in sets for ev in s["events"] for e in ev if e[0] == "F"}
+    assert kinds == {"R", "G", "F"}
+
+
+@pytest.mark.parametrize("name", ["legacy_farm_vectors.json.gz", "farm_vectors.json.gz",
+                                  "localref_vectors.json.gz"])
+def test_tree_oracle_local_farms(name):
+    passed, _ = _farms(tree_factory, name)
+    assert passed > 700
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["legacy_farm_vectors.json.gz", "farm_vectors.json.gz",
+                                  "localref_vectors.json.gz", "reconnect_vectors.json.gz"])
+def test_gpu_local_farms_on_the_tree(name):
+    g = _farms(device_factory, name)
+    assert g == _farms(tree_factory, name)
+
+
+def _long_legacy(mix, n_docs, ops, lag, init_len=0, cap=32768):
+    s = gen.generate(3, n_docs=n_docs, ops_per_doc=ops, length_mode=1, max_lag=lag, mix=mix,
+                     min_length=16 if not init_len else 0, init_len=init_len)
+    return s, cap
+
+
+# (mix, docs, ops per doc, max lag, initial text, items the documents reach at least)
+LONG = [(gen.MIX_INSERT | gen.MIX_ANNOTATE, 8, 20000, 32, 0, 4000),
+        (gen.MIX_INSERT | gen.MIX_ANNOTATE, 8, 14000, 64, 4000, 4000),
+        (gen.MIX_INSERT | gen.MIX_REMOVE | gen.MIX_ANNOTATE, 8, 12000, 8, 0, 0)]
+
+
+@pytest.mark.parametrize("mix,nd,ops,lag,init_len,reach", LONG[:1])
+def test_tree_oracles_agree_on_long_legacy_docs(mix, nd, ops, lag, init_len, reach):
+    # the item array (titems.c, the HBM tree pass's spec) and the linked blocks
+    # (tree.c) on documents far past the register tiers
+    from oracle import OracleEngine
+    s, cap = _long_legacy(mix, 4, ops // 2, lag, init_len)
+    t = tree_factory(s["n_keys"])
+    r = OracleEngine(s["n_keys"], threads=4, tree=True)
+    for e in (t, r):
+        gen.load_stream(e, s)
+        e.apply_batch(s["batch"])
+    np.testing.assert_array_equal(t.statuses(), r.statuses())
+    np.testing.assert_array_equal(t.digest(), r.digest())
+    assert t.stats()["max_segs"] > 4000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mix,nd,ops,lag,init_len,reach", LONG)
+def test_gpu_htree_long_lagging_legacy_docs(mix, nd, ops, lag, init_len, reach):
+    """Lagging legacy documents that grow to thousands of items: the register
+    tiers hand them to the HBM tree pass at 1,020 items; statuses, digests,
+    read-outs and segment lists equal titems.c (and tree.c's digests)."""
+    from fluidframework_amd.engine import DeviceEngine
+    from oracle import OracleEngine, SpecOracle
+    s, cap = _long_legacy(mix, nd, ops, lag, init_len)
+    o = SpecOracle(s["n_keys"], threads=8, cap=cap)
+    d = DeviceEngine(s["n_keys"], seg_capacity=cap)
+    r = OracleEngine(s["n_keys"], threads=8, tree=True)
+    for e in (o, d, r):
+        gen.load_stream(e, s)
+        e.apply_batch(s["batch"])
+    np.testing.assert_array_equal(d.statuses(), o.statuses())
+    np.testing.assert_array_equal(d.digest(), o.digest())
+    np.testing.assert_array_equal(d.digest(), r.digest())
+    assert o.stats()["max_segs"] >= reach
+    for doc in range(0, nd, 3):
+        assert d.read_doc(doc) == o.read_doc(doc)
+        a, b = o.read_segments(doc), d.read_segments(doc)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)

@@ -10,16 +10,14 @@ Pinned by:
   * tests/golden/reconnect_vectors.json.gz (tests/golden/make_reconnect_golden.py
     through oracle/ref_farm.js): 35 farms the reference itself ran with clients
     going offline, editing, catching up and re-sending every held op through its
-    own regeneratePendingOp.  Every regenerated op must equal the reference's (in
-    merged form: the reference's segment groups can be coarser, fixtures_util.
-    canon_regen) and every client's text and properties must equal the
-    reference client's at every checkpoint.  Three seeds (KNOWN_TREE_PLACEMENT)
-    differ: there a remote insert met pending local segments right after a block
-    of the reference's B+tree whose next leaf is a tombstone its lazy zamboni has
-    not scoured yet; continuePredicate looks at that one leaf only
-    (mergeTree.ts:1599-1611, 1788-1797), so the reference inserts before the
-    pending segments, while the flat state (tombstones compacted at minSeq, no
-    blocks) passes over them as breakTie does everywhere else.
+    own regeneratePendingOp.  Every regenerated op must equal the reference's
+    one for one and every client's text and properties must equal the reference
+    client's at every checkpoint -- on the tree restatement (titems.c), the GPU's
+    HBM tree pass and the Node host.  The reference places a remote insert
+    beside pending local segments by its B+tree's block edges (continuePredicate
+    looks at the one leaf after a block, mergeTree.ts:1599-1611, 1788-1797) and
+    keeps segments of pending groups unscoured (:686-688); the flat restatement
+    has neither, and diverges on three of the farms (FLAT_DIVERGES).
   * the resetPendingSegmentsToOp.spec.ts:23-96 case: five nested local inserts
     regenerate into 2 x 5 - 1 ops that rebuild the same text elsewhere.
 """
@@ -38,8 +36,9 @@ from fluidframework_amd.packing import BatchBuilder, DocClients, Interner, regen
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 VECTORS = os.path.join(HERE, "golden", "reconnect_vectors.json.gz")
-# seeds where the reference's placement depends on its tree's block edges (see above)
-KNOWN_TREE_PLACEMENT = {4015, 4024, 4025}
+# the farms where the flat restatement (no block edges, tombstones compacted at
+# minSeq) differs from the reference
+FLAT_DIVERGES = {4015, 4024, 4025}
 
 
 def reconnect_sets():
@@ -48,6 +47,14 @@ def reconnect_sets():
 
 
 def oracle_factory(k):
+    """The specification of a local-client document: the tree restatement."""
+    from oracle import OracleEngine
+    e = OracleEngine(k, tree="items")
+    e.lib.oti_set_limit(e.ctx, 1 << 20)
+    return e
+
+
+def flat_factory(k):
     from oracle import OracleEngine
     return OracleEngine(k)
 
@@ -60,16 +67,11 @@ def device_factory(k):
 def _reconnect_farms(factory):
     sets = reconnect_sets()
     checks = []
-    passed, failures = replay_ref_farm(factory, sets, regen_checks=checks)
-    bad = {sets[f[0]]["seed"] for f in failures}
-    assert bad <= KNOWN_TREE_PLACEMENT, [f for f in failures if sets[f[0]]["seed"] not in KNOWN_TREE_PLACEMENT][:2]
-    # every other farm: all checkpoints of all clients and every regenerated op
-    clean = [s for s in sets if s["seed"] not in KNOWN_TREE_PLACEMENT]
-    n_clean = sum(len(s["names"]) * len(s["checkpoints"]) for s in clean)
+    passed, failures = replay_ref_farm(factory, sets, regen_checks=checks, exact_regen=True)
+    assert not failures, failures[:2]
+    n_cp = sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
     n_regen = sum(1 for s in sets for ev in s["events"] for e in ev if e[0] == "G")
-    assert len(checks) == n_regen
-    assert sum(checks) >= n_regen - sum(1 for f in failures if f[3] == "regen")
-    assert passed >= n_clean
+    assert passed == n_cp and len(checks) == n_regen and all(checks)
     return passed, sum(checks), n_regen
 
 
@@ -82,7 +84,15 @@ def test_reconnect_vectors_shape():
 
 def test_oracle_reconnect_farms():
     passed, ok, n = _reconnect_farms(oracle_factory)
-    assert ok >= 0.99 * n
+    assert n > 5000
+
+
+def test_flat_restatement_diverges_where_block_edges_decide():
+    # why local-client documents replay on the tree: the flat rule fails exactly
+    # the three farms where a block edge of the reference decides a placement
+    sets = reconnect_sets()
+    _, failures = replay_ref_farm(flat_factory, sets)
+    assert {sets[f[0]]["seed"] for f in failures} == FLAT_DIVERGES
 
 
 def _nested_inserts(factory):
@@ -185,20 +195,19 @@ def test_gpu_regenerate_nested_inserts_match_oracle():
 @pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
 def test_node_reconnect_farms_on_gpu():
     """BatchClient.regeneratePendingOp through the N-API host
-    (tests/node/reconnect_gpu.js) on the first 12 reconnect farms: every
-    regenerated op equal to the reference's (merged form) and every client's
-    state at every checkpoint, outside the KNOWN_TREE_PLACEMENT seeds."""
+    (tests/node/reconnect_gpu.js) on all 35 reconnect farms: every
+    regenerated op equal to the reference's and every client's state at every
+    checkpoint."""
     from fixtures_util import canon_regen
     root = os.path.dirname(HERE)
-    r = subprocess.run([shutil.which("node"), "tests/node/reconnect_gpu.js", "12"], cwd=root, capture_output=True,
+    r = subprocess.run([shutil.which("node"), "tests/node/reconnect_gpu.js", "35"], cwd=root, capture_output=True,
                        text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     j = json.loads(r.stdout.strip().splitlines()[-1])
     assert j["pending"] == 0
-    bad_states = [x for x in j["states"] if not x[3] and x[0] not in KNOWN_TREE_PLACEMENT]
+    bad_states = [x for x in j["states"] if not x[3]]
     assert not bad_states, bad_states[:3]
-    bad_regen = [x for x in j["regens"] if x[0] not in KNOWN_TREE_PLACEMENT and
-                 canon_regen(x[2], x[4]) != canon_regen(x[3], x[4])]
+    bad_regen = [x for x in j["regens"] if canon_regen(x[2], x[4], False) != canon_regen(x[3], x[4], False)]
     assert not bad_regen, bad_regen[:2]
     assert len(j["regens"]) > 1000
 
