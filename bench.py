@@ -183,12 +183,15 @@ def run_engine(stream, cap, device, steps, warmup, stats_on, barrier=lambda: Non
     eng.sync()
     kernel_ms = []
     t_start = time.perf_counter()
+    round_bytes = []
     for _ in range(steps):
         step()
         # the library brackets its replay kernels with HIP events on its own
         # stream; read them after the step (waits only for that step)
         eng.sync()
-        kernel_ms.append(eng.stats()["kernel_ms"])
+        st = eng.stats()
+        kernel_ms.append(st["kernel_ms"])
+        round_bytes.append(st.get("round_bytes", 0.0))
     eng.sync()
     t_elapsed = time.perf_counter() - t_start
     barrier()
@@ -196,7 +199,7 @@ def run_engine(stream, cap, device, steps, warmup, stats_on, barrier=lambda: Non
     if (eng.statuses() != 0).any() or not np.array_equal(digest, stats_digest):
         raise SystemExit("timed runs disagree with the accounting run")
     return {"eng": eng, "elapsed": t_elapsed, "kernel_ms": kernel_ms, "stats": stats, "digest": digest,
-            "first_ms": first_ms}
+            "first_ms": first_ms, "round_bytes": float(np.mean(round_bytes)) if round_bytes else 0.0}
 
 
 def main():
@@ -294,7 +297,12 @@ def main():
     value = total_ops / (elapsed / args.steps)
     avg_kernel_ms = float(np.mean(r["kernel_ms"])) if r["kernel_ms"] else None
     algo_bytes = stats["algo_bytes"]
-    achieved_gbs = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9 if avg_kernel_ms else None
+    # the chunked pass's timed runs take the round phases, whose own bytes the
+    # library counts in every run (mte_stats.round_bytes); the statistics run
+    # replays op after op, so its algo_bytes describe that pass, not the timed one
+    round_bytes = r.get("round_bytes", 0.0)
+    timed_bytes = round_bytes if cap >= 8192 and round_bytes > 0 else algo_bytes
+    achieved_gbs = timed_bytes / (avg_kernel_ms * 1e-3) / 1e9 if avg_kernel_ms else None
 
     traffic, traffic_src = pmc_traffic(args.config, args.docs, args.ops)
 
@@ -357,7 +365,7 @@ def main():
     parity = None
     if world == 1 and not args.no_cpu_baseline:
         if stream.get("segs") is not None:
-            cpu, parity = cpu_baseline_prefix(stream, cap, args.cpu_seconds, threads)
+            cpu, parity = cpu_baseline(stream, digest, args.cpu_seconds, tree="chunked")
         else:
             cpu, parity = cpu_baseline(stream, digest, args.cpu_seconds)
     ref_cpu = reference_cpu_baseline(args.config)
@@ -398,13 +406,17 @@ def main():
             "traffic_frac_of_algo": (traffic / algo_bytes) if traffic else None,
             "kernel": ("tree + pair + big + " + ("chunk" if cap >= 8192 else "stream") +
                        " replay passes, HIP events on the engine stream"),
-            "algo_bytes_note": ("S_live of chunk-pass ops replaced by the chunk slots + summary entries they "
-                                "scanned (SURVEY.md 8(d))" if cap >= 8192 else "SURVEY.md 8(d) B_op"),
+            "algo_bytes_note": ("the round phases' own bytes, counted by the library in the timed runs "
+                                "(mte_stats.round_bytes: records, planes re-laid out / applied / gathered, sub-op "
+                                "lists); algo_bytes_op_after_op = SURVEY.md 8(d) with S_live replaced by the chunk "
+                                "slots + summary entries the op-after-op chunk pass scans"
+                                if cap >= 8192 and round_bytes > 0 else "SURVEY.md 8(d) B_op"),
             "counters_in_timed_runs": bool(args.stats),
             "kernel_ms": avg_kernel_ms,
             "first_run_kernel_ms": first_ms,
-            "algo_bytes_per_launch": algo_bytes,
-            "algo_bytes_per_op": algo_bytes / max(1, stats["ops_applied"]),
+            "algo_bytes_per_launch": timed_bytes,
+            "algo_bytes_per_op": timed_bytes / max(1, stats["ops_applied"]),
+            "algo_bytes_op_after_op": algo_bytes if timed_bytes != algo_bytes else None,
         },
         "end_to_end": {"ops_per_s": n_ops_rank / e2e_s, "ms": e2e_s * 1e3,
                        "includes": "mte_submit (host->HBM op upload) + reset + replay + digest read-back, rank 0"},
@@ -495,8 +507,9 @@ def local_client_stream(n_docs):
 def local_client_leg(n_docs, device, steps, threads):
     """The local-client side line: replay rate of local_client_stream on the
     GPU (HIP-event kernel time, algorithmic bytes as the headline's), every
-    copy's digest equal to the flat restatement's for its base document, and
-    the restatement's own rate on the base documents (kind "port")."""
+    copy's digest equal to the tree restatement's (oracle/titems.c, the HBM
+    tree pass's specification) for its base document, and the restatement's
+    own rate on the base documents (kind "port")."""
     from oracle import OracleEngine
     t0 = time.time()
     stream, base, copies = local_client_stream(n_docs)
@@ -504,7 +517,9 @@ def local_client_leg(n_docs, device, steps, threads):
     r = run_engine(stream, 0, device, steps, 1, False)
     nb = len(base["inits"])
     n_ops = int(stream["batch"]["op_offsets"][-1])
-    o = OracleEngine(LOCAL_KEYS, threads=threads)
+    o = OracleEngine(LOCAL_KEYS, threads=threads, tree="items")
+    o.lib.oti_set_limit(o.ctx, 1 << 20)
+    o.set_event_capacity(base["event_capacity"])
     o.load_docs(base["inits"], base["init_text"])
     tc = time.perf_counter()
     o.apply_batch(base["batch"])
@@ -523,7 +538,7 @@ def local_client_leg(n_docs, device, steps, threads):
             "build_s": round(build_s, 1),
             "note": ("every client of the 76 farm + 35 reconnect farm sets the reference ran (local ops, acks, "
                      "rollbacks, regeneratePendingOp, lagging remote ops), MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS, "
-                     "repeated to the doc count; HBM-streamed pass (mte_stream.h)")}
+                     "repeated to the doc count; HBM tree pass (mte_htree.h)")}
 
 
 def node_end_to_end(stream, gpu_digest, n_docs):
@@ -636,69 +651,44 @@ def node_sharded(stream, n_docs, workers):
             "wall_s": round(time.perf_counter() - t0, 1)}
 
 
-def cpu_baseline(stream, gpu_digest, target_s):
-    """Time the CPU restatement (oracle/, kind 'port') on a bounded doc sample."""
+def cpu_baseline(stream, gpu_digest, target_s, tree=False):
+    """Time the CPU restatement (oracle/, kind 'port') on a bounded doc sample:
+    the flat restatement (oracle.c), or for documents of millions of segments
+    (config 5) the same rules with a chunk index (tree="chunked", chunked.c),
+    whose per-op cost is O(chunks + chunk), not O(S)."""
     from fluidframework_amd import gen
     from oracle import OracleEngine
 
     threads = host_threads()
     n_docs = len(stream["inits"])
+    src = "oracle/chunked.c flat restatement with a chunk index" if tree == "chunked" else \
+        "oracle/oracle.c flat restatement"
     # calibrate on a small slice, then size the sample for ~target_s
-    cal = max(threads, min(n_docs, 64))
+    cal = max(min(threads, n_docs), min(n_docs, 64 if not tree else threads))
     sub = gen.slice_docs(stream, 0, cal)
-    o = OracleEngine(stream["n_keys"], threads=threads)
-    o.load_docs(sub["inits"], sub["init_text"])
+    o = OracleEngine(stream["n_keys"], threads=threads, tree=tree)
+    gen.load_stream(o, sub)
     t0 = time.perf_counter()
     o.apply_batch(sub["batch"])
     t_cal = time.perf_counter() - t0
     per_doc = t_cal / cal
     m = int(min(n_docs, max(cal, target_s / max(per_doc, 1e-9))))
-    sub = gen.slice_docs(stream, 0, m)
-    o = OracleEngine(stream["n_keys"], threads=threads)
-    o.load_docs(sub["inits"], sub["init_text"])
-    t0 = time.perf_counter()
-    o.apply_batch(sub["batch"])
-    dt = time.perf_counter() - t0
-    ops = int(sub["batch"]["op_offsets"][-1])
-    parity = bool(np.array_equal(o.digest(), gpu_digest[:m]) and (o.statuses() == 0).all())
-    return ({"value": ops / dt, "unit": "ops/s", "cores": threads, "kind": "port",
-             "sample": f"first {m} of {n_docs} docs (all their ops, {ops} ops), {dt:.1f} s, "
-                       f"oracle/oracle.c flat restatement, {threads} pthreads"},
-            {"docs": m, "digest_equal": parity})
-
-
-def cpu_baseline_prefix(stream, cap, target_s, threads):
-    """Long documents (config 5): the flat restatement costs O(S) per op, so the
-    sample is the first k ops of `threads` docs (k sized for ~target_s); its
-    digests are checked against a GPU replay of the same prefix."""
-    from fluidframework_amd import gen
-    from fluidframework_amd.engine import DeviceEngine
-    from oracle import OracleEngine
-
-    n_docs = len(stream["inits"])
-    m = min(n_docs, threads)
-    k = 64
-    while True:
-        sub = gen.prefix_ops(stream, m, k)
-        o = OracleEngine(stream["n_keys"], threads=threads)
+    if m != cal:
+        del o
+        sub = gen.slice_docs(stream, 0, m)
+        o = OracleEngine(stream["n_keys"], threads=threads, tree=tree)
         gen.load_stream(o, sub)
         t0 = time.perf_counter()
         o.apply_batch(sub["batch"])
         dt = time.perf_counter() - t0
-        if dt >= target_s / 4 or k >= int(np.diff(stream["batch"]["op_offsets"].astype(np.int64)).min()):
-            break
-        k = int(k * min(16.0, max(2.0, target_s / max(dt, 1e-3))))
+    else:
+        dt = t_cal
     ops = int(sub["batch"]["op_offsets"][-1])
-    d = DeviceEngine(stream["n_keys"], seg_capacity=cap)
-    d.set_stats(False)  # the timed path (round phases: statistics runs replay op after op)
-    gen.load_stream(d, sub)
-    d.apply_batch(sub["batch"])
-    parity = bool(np.array_equal(o.digest(), d.digest()) and (o.statuses() == 0).all()
-                  and (d.statuses() == 0).all())
+    parity = bool(np.array_equal(o.digest(), gpu_digest[:m]) and (o.statuses() == 0).all())
     return ({"value": ops / dt, "unit": "ops/s", "cores": threads, "kind": "port",
-             "sample": f"first {k} ops of the first {m} of {n_docs} docs ({ops} ops at ~2^20 segments/doc), "
-                       f"{dt:.1f} s, oracle/oracle.c flat restatement, {threads} pthreads"},
-            {"docs": m, "ops_per_doc": k, "digest_equal": parity, "checked_against": "GPU replay of the same prefix"})
+             "sample": f"first {m} of {n_docs} docs (all their ops, {ops} ops), {dt:.1f} s, {src}, "
+                       f"{threads} pthreads"},
+            {"docs": m, "digest_equal": parity, "checked_against": "the timed GPU runs' digests"})
 
 
 if __name__ == "__main__":

@@ -95,7 +95,7 @@ class MteStats(C.Structure):
                 ("segs_written", C.c_uint64), ("prop_writes", C.c_uint64),
                 ("units_inserted", C.c_uint64), ("max_segs", C.c_uint64),
                 ("kernel_ms", C.c_double), ("algo_bytes", C.c_double),
-                ("chunk_scanned", C.c_uint64)]
+                ("chunk_scanned", C.c_uint64), ("round_bytes", C.c_double)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

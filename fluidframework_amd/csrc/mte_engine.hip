@@ -583,7 +583,7 @@ void free_image(mte_ctx* c) {
 
 void free_docs(mte_ctx* c) {
   free_image(c);
-  void* cs[] = {c->ch.arena, c->ch.cnt, c->ch.kc, c->ch.sum, c->rd.plan, c->rd.rcnt, c->rd.rbuf, c->rd.rflag,
+  void* cs[] = {c->ch.arena, c->ch.cnt, c->ch.kc, c->ch.sum, c->rd.plan, c->rd.acct, c->rd.rcnt, c->rd.rbuf, c->rd.rflag,
                 c->rd.nch, c->rd.nnew, c->rd.count, c->rd.rlist, c->rd.rchain};
   for (void* p : cs)
     if (p) (void)hipFree(p);
@@ -663,6 +663,8 @@ int round_phase_loop(mte_ctx* c, const ReplayArgs& a, size_t lds, uint64_t max_o
   RoundArgs rd = c->rd;
   ch.plan = rd.plan;
   ch.rflag = rd.rflag;
+  rd.planes = kFieldPlanes + (uint32_t)(K > 0 ? K : 0);
+  HIPCHK(c, hipMemsetAsync(rd.acct, 0, sizeof(unsigned long long) * c->n_docs, c->stream));
   const uint64_t nch_all = (uint64_t)c->n_docs * ch.nch_cap;
   for (int ph = 0; ph < kMaxPhases; ph++) {
     rd.last = ph == kMaxPhases - 1 ? 1u : 0u;
@@ -1090,6 +1092,8 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
       HIPCHK(c, hipMalloc((void**)&ch.sum, nch_all * 4 * MTE_MAX_CLIENTS));
       RoundArgs& rd = c->rd;
       HIPCHK(c, hipMalloc((void**)&rd.plan, sizeof(uint4) * n_docs));
+      HIPCHK(c, hipMalloc((void**)&rd.acct, sizeof(unsigned long long) * n_docs));
+      HIPCHK(c, hipMemsetAsync(rd.acct, 0, sizeof(unsigned long long) * n_docs, c->stream));
       HIPCHK(c, hipMalloc((void**)&rd.rcnt, nch_all * 4));
       HIPCHK(c, hipMalloc((void**)&rd.rbuf, nch_all * kRB * sizeof(uint2)));
       HIPCHK(c, hipMalloc((void**)&rd.rflag, 4 * (uint64_t)n_docs));
@@ -1917,6 +1921,15 @@ int mte_stats_get(mte_ctx* c, mte_stats* o) {
   }
   // ops of the chunked pass count the slots and summary
   // entries they scanned instead of the document's S_live
+  // the round phases' own bytes of the last run (RoundArgs::acct)
+  o->round_bytes = 0.0;
+  if (c->chunked && c->rd.acct && c->n_docs) {
+    std::vector<unsigned long long> ac(c->n_docs);
+    HIPCHK(c, hipMemcpyAsync(ac.data(), c->rd.acct, sizeof(unsigned long long) * c->n_docs, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (unsigned long long v : ac) o->round_bytes += (double)v;
+  }
   const double scanned = (double)(o->segs_scanned - chunk_canon) + (double)o->chunk_scanned;
   o->algo_bytes = 32.0 * (double)o->ops_applied + 20.0 * scanned + 20.0 * (double)o->segs_written +
                   4.0 * (double)o->prop_writes + 2.0 * (double)o->units_inserted;

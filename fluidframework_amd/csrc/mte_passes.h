@@ -32,6 +32,12 @@ struct RoundArgs {
   uint2* rchain;    // [doc][MTE_MAX_CLIENTS] (list offset, entries) of each client chain
   uint32_t last;    // this phase sends every active document op after op
   uint32_t d0, nd;  // the documents [d0, d0 + nd) one launch_round_run covers
+  // [doc] the bytes the round phases of the last mte_run had to read and write
+  // (their algorithmic bytes: records, planes re-laid out / applied /
+  // gathered, sub-op lists), added per document and phase; planes = the
+  // segment planes a move carries (kFieldPlanes + K)
+  unsigned long long* acct;
+  uint32_t planes;
 };
 // the round phases fit a context whose per-wave column (nch_cap + ng_cap
 // entries) fits this much LDS

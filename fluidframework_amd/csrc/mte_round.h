@@ -165,12 +165,21 @@ __global__ __launch_bounds__(512) void rnd_scan_kernel(ReplayArgs a, ChunkArgs c
   }
   const int32_t total = ch_block_scan(kc, m, &ctl);
   if (threadIdx.x == 0) {
+    const unsigned long long pb = 4ull * rd.planes;  // bytes of one segment's planes
     if (!gather) {
       int nch = (total + kChFill - 1) / kChFill;
       nch = nch < 1 ? 1 : (nch > (int)ch.nch_cap ? (int)ch.nch_cap : nch);
       rd.nch[doc] = (uint32_t)nch;
       rd.nnew[doc] = (uint32_t)total;
+      // the plan's record scan, the keep counts' removedSeq reads, the kept
+      // segments' planes moved into the chunks, the columns' length and
+      // removedSeq reads, the chunk counts and column entries
+      const unsigned long long n_old = (unsigned long long)a.hdr[doc].nseg;
+      atomicAdd(rd.acct + doc, 32ull * (p.z - p.y) + 4ull * n_old + 2ull * pb * (unsigned long long)total +
+                                   8ull * (unsigned long long)total + 8ull * (unsigned long long)nch);
     } else {
+      // the chunks' planes back into the flat planes, the counts and their prefix
+      atomicAdd(rd.acct + doc, 2ull * pb * (unsigned long long)total + 8ull * (unsigned long long)m);
       const uint64_t kb = a.op_off[doc];
       const uint32_t ktot = (uint32_t)(a.op_off[doc + 1] - kb);
       DocHdr h = a.hdr[doc];
@@ -503,6 +512,9 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
       if (l == 0) {
         if (failed) atomicOr(rd.rflag + doc, 2u);
         rd.rchain[(uint64_t)doc * MTE_MAX_CLIENTS + (uint32_t)c] = make_uint2(off, failed ? 0u : m);
+        // the chain's records and its sub-op list: written here, read and
+        // bucketed (8 B) by rnd_bucket
+        atomicAdd(rd.acct + doc, 32ull * nc + 40ull * m);
       }
     } else if ((c % kChWaves) == u && l == 0) {
       rd.rchain[(uint64_t)doc * MTE_MAX_CLIENTS + (uint32_t)c] = make_uint2(off, 0u);
@@ -580,8 +592,11 @@ __global__ __launch_bounds__(256) void rnd_apply_kernel(ReplayArgs a, ChunkArgs 
                                                   true, tot, dlen, a, st);
     rcs = rc != 0 ? rc : rcs;
   }
+  const int n_before = (int)cntp[i];
   ch_store<K>(R, ch, x0, ni);
   if (l == 0) {
+    // the chunk's sub-ops (record + bucket entry), its planes in and out, its count
+    atomicAdd(rd.acct + doc, 40ull * nb + 4ull * rd.planes * (unsigned long long)(n_before + ni) + 8ull);
     cntp[i] = (uint32_t)ni;
     if (rcs != 0) a.hdr[doc].status = MTE_E_STATE;  // resolve guarantees every sub-op fits: an engine bug
   }

@@ -1,5 +1,5 @@
-// mte_stream.h — pass 3: documents beyond the register tiers (> 1,022
-// segments) and every document with a local client or delta events, replayed
+// mte_stream.h — pass 3: documents pass 2 escalated (> 1,022 segments) and
+// new length-calc documents of remote clients with delta events, replayed
 // one wavefront per document with the segment planes left in HBM and streamed
 // per op in tiles of 128 slots (2 per lane, lane-major, coalesced; 2 per lane
 // keeps the registers low enough for 5-8 waves per SIMD, which hide the
@@ -66,7 +66,8 @@ __device__ __forceinline__ void tile_load_hot(Regs<kTileE, K>& R, const uint32_t
 }
 
 // ---- documents with a local client (MTE_DOC_LOCAL_CLIENT, include/mte.h) ----
-// Pending seqs are kLocalBase + localSeq (UnassignedSequenceNumber, normalised
+// They replay on the HBM tree pass (mte_htree.h); the plane layout and the
+// event / reference helpers below are shared with it.  Pending seqs are kLocalBase + localSeq (UnassignedSequenceNumber, normalised
 // above every sequenced seq as breakTie / nodeLength do, mergeTree.ts:1009-1016,
 // 1713-1714).  K more planes after the property planes hold, per slot and key,
 // the localSeq of the last pending local annotate that set the key (0 = none):
@@ -77,82 +78,7 @@ __device__ __forceinline__ void tile_load_hot(Regs<kTileE, K>& R, const uint32_t
 constexpr int32_t kLocalBase = MTE_LOCAL_SEQ_BASE;
 template <int K>
 constexpr int kAnnPlane = kFieldPlanes + 2 * K;
-// K more after it: per key, the value before the first pending local annotate
-// set it (what that annotate's rollback puts back, MTE_OP_RBKEY)
-template <int K>
-constexpr int kBasePlane = kFieldPlanes + 2 * K + 1;
 constexpr int kPlaneGroup = 5;  // planes moved per batch of loads (all in flight, then the stores)
-
-// the local client's own view (localNetLength, mergeTree.ts:553-573, new
-// length calculation): removed -> 0, else the length; padding undefined
-template <int K>
-__device__ __forceinline__ void local_lengths(const Regs<kTileE, K>& R, int32_t (&L)[kTileE]) {
-#pragma unroll
-  for (int j = 0; j < kTileE; j++) L[j] = R.rseq[j] == kPad ? -1 : (R.rseq[j] != kNone ? 0 : R.len[j]);
-}
-
-// insertingWalk slot for a remote insert in a document with pending local
-// segments: as find_slot, passing over the pending ones (breakTie gives them
-// MAX_SAFE_INTEGER - 1, continuePredicate moves past them at a block's end,
-// mergeTree.ts:1599-1611, 1705-1721, 1790)
-template <int E>
-__device__ __forceinline__ int find_slot_remote(const int32_t (&L)[E], const int32_t (&P)[E],
-                                                const int32_t (&seq)[E], int32_t pos) {
-  int jsel = E;
-#pragma unroll
-  for (int j = E - 1; j >= 0; j--) jsel = (L[j] >= 0 && P[j] >= pos && seq[j] < kLocalBase) ? j : jsel;
-  const unsigned long long msk = __ballot(jsel < E);
-  if (!msk) return -1;
-  const int ls = __ffsll((long long)msk) - 1;
-  return ls * E + rdlane(jsel, ls);
-}
-
-// MTE_OP_ACK: ackPendingSegment for localSeqs lo..hi (mergeTree.ts:1278-1331,
-// BaseSegment.ack mergeTreeNodes.ts:475-503): pending inserts and removals of
-// those ops take seq (a removal a remote op overtook already has its seq,
-// :1928-1938), and their property keys stop being pending.
-template <int K>
-__device__ __forceinline__ void stream_ack(uint32_t* pl, uint64_t sd, int n, int32_t lo, int32_t hi, int32_t s,
-                                           uint32_t ann_mask) {
-  const int l = lane_id();
-  // per tile: every load first (all in flight at once), then the stores
-  for (int tb = 0; tb < n; tb += kTile) {
-    int32_t sr[2][kTileE];
-    uint32_t pk[K > 0 ? K : 1][kTileE], am[kTileE];
-#pragma unroll
-    for (int j = 0; j < kTileE; j++) {
-      const int i = tb + l * kTileE + j;
-      const bool v = i < n;
-      // unconditional loads (padding reads slot 0), then selects
-      const int ic = v ? i : 0;
-#pragma unroll
-      for (int p = 0; p < 2; p++) {  // seq, removedSeq
-        const int32_t x = (int32_t)ld_l2(pl + (p + 1) * sd + ic);
-        sr[p][j] = v ? x : 0;
-      }
-#pragma unroll
-      for (int kk = 0; kk < K; kk++) {
-        const uint32_t x = ld_l2(pl + (uint64_t)(kFieldPlanes + K + kk) * sd + ic);
-        pk[kk][j] = v ? x : 0u;
-      }
-      const uint32_t xa = ld_l2(pl + (uint64_t)kAnnPlane<K> * sd + ic);
-      am[j] = (v && ann_mask) ? xa : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < kTileE; j++) {
-      const int i = tb + l * kTileE + j;
-      if (i >= n) continue;
-#pragma unroll
-      for (int p = 0; p < 2; p++)
-        if (sr[p][j] >= kLocalBase + lo && sr[p][j] <= kLocalBase + hi) pl[(p + 1) * sd + i] = (uint32_t)s;
-#pragma unroll
-      for (int kk = 0; kk < K; kk++)
-        if (pk[kk][j] != 0u && pk[kk][j] <= (uint32_t)hi) pl[(uint64_t)(kFieldPlanes + K + kk) * sd + i] = 0u;
-      if (am[j] & ann_mask) pl[(uint64_t)kAnnPlane<K> * sd + i] = am[j] & ~ann_mask;  // the acked groups
-    }
-  }
-  vm_drain();
-}
 
 // ---- delta events (MTE_DOC_EVENTS, include/mte.h) ----------------------------
 // The doc's own view: removed -> 0, else the length (Client.getPosition,
@@ -180,234 +106,6 @@ __device__ __forceinline__ int32_t own_prefix(const uint32_t* pl, uint64_t sd, i
     }
   }
   return rdlane(wave_incl_scan(acc), kWave - 1);
-}
-
-// MTE_OP_ROLLBACK: MergeTree.rollback of the pending op of localSeq ls, type t
-// (mergeTree.ts:2005-2083): its inserted segments get seq and removedSeq
-// UniversalSequenceNumber 0 (gone for every view), its removed ones are
-// restored; each one's delta event at its own-view position once done.
-__device__ __forceinline__ void stream_rollback(uint32_t* pl, uint64_t sd, int n, int32_t ls, uint32_t t, bool evd,
-                                                EvOut& ev) {
-  const int l = lane_id();
-  int32_t ocy = 0;
-  for (int tb = 0; tb < n; tb += kTile) {
-    bool hit[kTileE];
-    int32_t OL[kTileE], OP[kTileE], len[kTileE];
-#pragma unroll
-    for (int j = 0; j < kTileE; j++) {
-      const int i = tb + l * kTileE + j;
-      const bool v = i < n;
-      const int ic = v ? i : 0;  // unconditional loads, selected after
-      const int32_t l0 = (int32_t)ld_l2(pl + ic), l1 = (int32_t)ld_l2(pl + sd + ic), l2 = (int32_t)ld_l2(pl + 2 * sd + ic);
-      len[j] = v ? l0 : 0;
-      const int32_t sq = v ? l1 : 0;
-      int32_t rs = v ? l2 : kPad;
-      hit[j] = v && (t == MTE_OP_INSERT ? sq == kLocalBase + ls : rs == kLocalBase + ls);
-      if (hit[j]) {
-        if (t == MTE_OP_INSERT) {
-          pl[sd + i] = 0u;
-          pl[2 * sd + i] = 0u;
-          pl[3 * sd + i] = 1u;  // removed by the local client
-          rs = 0;
-        } else {
-          pl[2 * sd + i] = (uint32_t)kNone;
-          pl[3 * sd + i] = 0u;
-          rs = kNone;
-        }
-      }
-      OL[j] = (v && rs == kNone) ? len[j] : 0;
-    }
-    if (evd) {
-      const int32_t otot = prefix<kTileE>(OL, OP);
-      uint32_t ecnt = 0;
-#pragma unroll
-      for (int j = 0; j < kTileE; j++) ecnt += hit[j] ? 1u : 0u;
-      const int32_t eincl = wave_incl_scan((int32_t)ecnt);
-      uint32_t e = ev.n + (uint32_t)(eincl - (int32_t)ecnt);
-#pragma unroll
-      for (int j = 0; j < kTileE; j++) {
-        if (hit[j]) {
-          // a rolled-back insert is removed (REMOVE event), a rolled-back remove re-inserted
-          if (e < ev.cap)
-            ev.p[e] = mte_delta{ev.op, t == MTE_OP_INSERT ? (uint32_t)MTE_OP_REMOVE : (uint32_t)MTE_OP_INSERT,
-                                ocy + OP[j], len[j], t == MTE_OP_INSERT ? 1u : 0u};
-          e++;
-        }
-      }
-      ev.n += (uint32_t)rdlane(eincl, kWave - 1);
-      ocy += otot;
-    }
-  }
-  vm_drain();
-}
-
-// MTE_OP_ROLLBACK of a local annotate (group slot b), followed by its n_aux
-// MTE_OP_RBKEY records at aux: MergeTree.rollback -> annotateRange of each
-// segment of the group with its previousProps under PropertiesRollback.Rollback
-// (mergeTree.ts:2036-2072, segmentPropertiesManager.ts:63-151): per key the
-// annotate set, the value of the first candidate (latest older pending annotate
-// of the key) whose group holds the segment -- its localSeq the key's pending
-// one -- else the base plane's value, no longer pending.  Each segment's
-// annotate event at its own-view position.  A segment of the group removed
-// since: MTE_E_UNSUPPORTED (include/mte.h).
-template <int K>
-__device__ __forceinline__ int stream_rollback_annotate(uint32_t* pl, uint64_t sd, int n, uint32_t b,
-                                                        const uint4* aux, uint32_t n_aux, bool evd, EvOut& ev) {
-  const int l = lane_id();
-  int32_t ocy = 0;
-  for (int tb = 0; tb < n; tb += kTile) {
-    bool hit[kTileE], bad = false;
-    int32_t OL[kTileE], OP[kTileE], len[kTileE];
-    uint32_t am[kTileE];
-#pragma unroll
-    for (int j = 0; j < kTileE; j++) {
-      const int i = tb + l * kTileE + j;
-      const bool v = i < n;
-      const int ic = v ? i : 0;  // unconditional loads, selected after
-      const int32_t l0 = (int32_t)ld_l2(pl + ic), l2 = (int32_t)ld_l2(pl + 2 * sd + ic);
-      const uint32_t xa = ld_l2(pl + (uint64_t)kAnnPlane<K> * sd + ic);
-      len[j] = v ? l0 : 0;
-      const int32_t rs = v ? l2 : kPad;
-      am[j] = v ? xa : 0u;
-      hit[j] = v && ((am[j] >> b) & 1u);
-      bad = bad || (hit[j] && rs != kNone);
-      OL[j] = (v && rs == kNone) ? len[j] : 0;
-    }
-    if (__ballot(bad)) {
-      vm_drain();
-      return MTE_E_UNSUPPORTED;
-    }
-    for (uint32_t q = 0; q < n_aux;) {
-      const uint32_t key = uni((uint32_t)sload8(aux + 2 * q)[4]);
-      if (key >= (uint32_t)K) {
-        vm_drain();
-        return MTE_E_INVALID_ARG;
-      }
-      bool done[kTileE];
-      uint32_t val[kTileE], pk[kTileE];
-#pragma unroll
-      for (int j = 0; j < kTileE; j++) {
-        done[j] = false;
-        val[j] = 0u;
-        pk[j] = 0u;
-      }
-      for (;;) {  // the key's candidates, latest first, then its base entry
-        if (q >= n_aux) {
-          vm_drain();
-          return MTE_E_INVALID_ARG;
-        }
-        const s8v rr = sload8(aux + 2 * q);
-        q++;
-        const uint32_t slot = (uint32_t)rr[5];
-        if ((uint32_t)rr[4] != key) {
-          vm_drain();
-          return MTE_E_INVALID_ARG;
-        }
-        if (slot >= MTE_ANNOTATE_SLOTS) {
-#pragma unroll
-          for (int j = 0; j < kTileE; j++) {
-            const int i = tb + l * kTileE + j;
-            const uint32_t bv = ld_l2(pl + (uint64_t)(kBasePlane<K> + key) * sd + (hit[j] ? i : 0));
-            val[j] = done[j] ? val[j] : bv;
-          }
-          break;
-        }
-#pragma unroll
-        for (int j = 0; j < kTileE; j++) {
-          const bool take = hit[j] && !done[j] && ((am[j] >> slot) & 1u);
-          val[j] = take ? (uint32_t)rr[6] : val[j];
-          pk[j] = take ? (uint32_t)rr[0] : pk[j];
-          done[j] = done[j] || take;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < kTileE; j++) {
-        const int i = tb + l * kTileE + j;
-        if (hit[j]) {
-          pl[(uint64_t)(kFieldPlanes + key) * sd + i] = val[j];
-          pl[(uint64_t)(kFieldPlanes + K + key) * sd + i] = pk[j];
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < kTileE; j++)
-      if (hit[j]) pl[(uint64_t)kAnnPlane<K> * sd + tb + l * kTileE + j] = am[j] & ~(1u << b);
-    if (evd) {
-      const int32_t otot = prefix<kTileE>(OL, OP);
-      uint32_t ecnt = 0;
-#pragma unroll
-      for (int j = 0; j < kTileE; j++) ecnt += hit[j] ? 1u : 0u;
-      const int32_t eincl = wave_incl_scan((int32_t)ecnt);
-      uint32_t e = ev.n + (uint32_t)(eincl - (int32_t)ecnt);
-#pragma unroll
-      for (int j = 0; j < kTileE; j++) {
-        if (hit[j]) {
-          if (e < ev.cap) ev.p[e] = mte_delta{ev.op, (uint32_t)MTE_OP_ANNOTATE, ocy + OP[j], len[j], 0u};
-          e++;
-        }
-      }
-      ev.n += (uint32_t)rdlane(eincl, kWave - 1);
-      ocy += otot;
-    }
-  }
-  vm_drain();
-  return 0;
-}
-
-// MTE_OP_REGEN: Client.regeneratePendingOp of the pending op of localSeq ls,
-// type t (client.ts:972-1002 -> resetPendingDeltaToOps :788-860): its segment
-// group in document order, each at its position in the view at localSeq ls
-// (findReconnectionPosition :709-713 -> localNetLength with localSeq,
-// mergeTree.ts:575-593) with its length, as MTE_DELTA_REGEN | t records.
-// Inserts: the segments ls inserted (their text offset rides in `removed`);
-// removes: the ones ls still holds removed (no remote remove overtook it);
-// annotates: the members of group slot `slot` not removed, or removed only by
-// a pending local remove.  The document does not change.
-template <int K>
-__device__ __forceinline__ void stream_regen(const uint32_t* pl, uint64_t sd, int n, int32_t ls, uint32_t t,
-                                             uint32_t slot, EvOut& ev) {
-  const int l = lane_id();
-  int32_t cy = 0;
-  for (int tb = 0; tb < n; tb += kTile) {
-    bool hit[kTileE];
-    int32_t LL[kTileE], PP[kTileE], len[kTileE];
-    uint32_t tf[kTileE];
-#pragma unroll
-    for (int j = 0; j < kTileE; j++) {
-      const int i = tb + l * kTileE + j;
-      const bool v = i < n;
-      const int ic = v ? i : 0;  // unconditional loads, selected after
-      const int32_t l0 = (int32_t)ld_l2(pl + ic), l1 = (int32_t)ld_l2(pl + sd + ic), l2 = (int32_t)ld_l2(pl + 2 * sd + ic);
-      const uint32_t l5 = ld_l2(pl + 5 * sd + ic), am = ld_l2(pl + (uint64_t)kAnnPlane<K> * sd + ic);
-      len[j] = v ? l0 : 0;
-      const int32_t sq = v ? l1 : 0;
-      const int32_t rs = v ? l2 : kPad;
-      tf[j] = v ? l5 : 0u;
-      const bool rp = rs >= kLocalBase && rs != kNone;  // a pending local removal
-      if (t == MTE_OP_INSERT) hit[j] = v && sq == kLocalBase + ls;
-      else if (t == MTE_OP_REMOVE) hit[j] = v && rs == kLocalBase + ls;
-      else hit[j] = v && ((am >> slot) & 1u) && (rs == kNone || rp);
-      const bool later = sq >= kLocalBase && sq - kLocalBase > ls;  // inserted after ls
-      const bool gone = rs != kNone && (!rp || rs - kLocalBase <= ls);
-      LL[j] = (v && !later && !gone) ? len[j] : 0;
-    }
-    const int32_t tot = prefix<kTileE>(LL, PP);
-    uint32_t ecnt = 0;
-#pragma unroll
-    for (int j = 0; j < kTileE; j++) ecnt += hit[j] ? 1u : 0u;
-    const int32_t eincl = wave_incl_scan((int32_t)ecnt);
-    uint32_t e = ev.n + (uint32_t)(eincl - (int32_t)ecnt);
-#pragma unroll
-    for (int j = 0; j < kTileE; j++) {
-      if (hit[j]) {
-        if (e < ev.cap)
-          ev.p[e] = mte_delta{ev.op, MTE_DELTA_REGEN | t, cy + PP[j], len[j], t == MTE_OP_INSERT ? tf[j] : 0u};
-        e++;
-      }
-    }
-    ev.n += (uint32_t)rdlane(eincl, kWave - 1);
-    cy += tot;
-  }
 }
 
 // ---- local references (MTE_DOC_REFS, include/mte.h) -------------------------
@@ -600,20 +298,18 @@ __device__ int stream_ref(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uin
   return 0;
 }
 
-// One op of one HBM-resident document (see the file comment).  Returns 0 or
-// a negative MTE_E_*.  lseq: the document's last localSeq (local-client docs);
-// ev: its delta events (MTE_DOC_EVENTS docs).
+// One op of one HBM-resident document of remote clients (see the file
+// comment).  Returns 0 or a negative MTE_E_*.  ev: its delta events
+// (MTE_DOC_EVENTS docs).
 template <int K, bool S>
-__device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const ReplayArgs& a, uint32_t* zlds,
-                           int32_t& lseq, EvOut& ev, uint32_t& rhi) {
+__device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const ReplayArgs& a, EvOut& ev) {
   constexpr int E = kTileE;
   const int l = lane_id();
   uint32_t* pl = a.planes + (uint64_t)D.doc * a.cap;
   const uint64_t sd = a.stride;
-  const bool ldoc = (D.flags & MTE_DOC_LOCAL_CLIENT) != 0;
   const bool evd = (D.flags & MTE_DOC_EVENTS) != 0;
   ev.op = D.k;
-  const int nplanes = kFieldPlanes + K + (ldoc ? 2 * K + 1 : 0);  // + the pending-key, group and base planes
+  const int nplanes = kFieldPlanes + K;
 
   const s8v op = cur;
   const uint4* rec = D.recp + 2 * D.k;
@@ -621,63 +317,13 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
-  const bool refd = (D.flags & MTE_DOC_REFS) != 0 && a.refs != nullptr;
-  uint2* const rt = refd ? a.refs + (uint64_t)D.doc * a.ref_cap : nullptr;
-  if (type == MTE_OP_REF) {
-    if (!(flags & MTE_F_LOCAL) || !ldoc || !refd) return MTE_E_UNSUPPORTED;
-    if ((uint32_t)op[5] >= a.ref_cap || (uint32_t)op[7] > 3u) return MTE_E_INVALID_ARG;
-    if ((uint32_t)op[7] == 2u && c == 0) return MTE_E_INVALID_ARG;  // a sequenced op of another client
-    MTE_STAT(st[kStOps]++;)
-    MTE_STAT(if ((uint32_t)op[7] != 1u) st[kStScanned] += (uint32_t)D.n;)
-    const int rc = stream_ref<K>(pl, sd, D.n, rt, rhi, op, D.min_seq, (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0);
-    if (rc) return rc;
-    D.k++;
-    return 0;
-  }
-  if (type > MTE_OP_REGEN) return MTE_E_INVALID_ARG;  // MTE_OP_RBKEY only after an annotate's rollback
-  const bool lop = (flags & MTE_F_LOCAL) != 0;  // a local op: the local view, seq = localSeq
-  if ((lop || type >= MTE_OP_ACK) && !ldoc) return MTE_E_UNSUPPORTED;
+  // local ops, acks, rollbacks, regenerations and references belong to a
+  // local client's document (the HBM tree pass)
+  if (type == MTE_OP_REF || (flags & MTE_F_LOCAL) || type >= MTE_OP_ACK) return MTE_E_UNSUPPORTED;
   MTE_STAT(st[kStOps]++;)
   MTE_STAT(st[kStMaxSegs] = (uint32_t)D.n > st[kStMaxSegs] ? (uint32_t)D.n : st[kStMaxSegs];)
   const int32_t s = op[0], r = op[1], msn = op[2];
   const int32_t pos1 = op[4], pos2 = op[5];
-  if (type == MTE_OP_ROLLBACK) {
-    if (!lop || !(s > 0 && s <= lseq)) return MTE_E_INVALID_ARG;
-    if (pos1 == MTE_OP_ANNOTATE) {
-      const uint32_t n_aux = (uint32_t)pos2;
-      if ((uint64_t)D.k + 1 + n_aux > D.k1 || (uint32_t)op[6] >= MTE_ANNOTATE_SLOTS) return MTE_E_INVALID_ARG;
-      MTE_STAT(st[kStScanned] += (uint32_t)D.n;)
-      const int rc = stream_rollback_annotate<K>(pl, sd, D.n, (uint32_t)op[6], rec + 2, n_aux, evd, ev);
-      if (rc) return rc;
-      D.k += 1 + n_aux;
-      if (D.k < D.k1) cur = sload8(D.recp + 2 * D.k);
-      return 0;
-    }
-    if (pos1 != MTE_OP_INSERT && pos1 != MTE_OP_REMOVE) return MTE_E_INVALID_ARG;
-    MTE_STAT(st[kStScanned] += (uint32_t)D.n;)
-    stream_rollback(pl, sd, D.n, s, (uint32_t)pos1, evd, ev);
-    D.k++;
-    return 0;
-  }
-  if (type == MTE_OP_REGEN) {
-    if (!lop || !(s > 0 && s <= lseq)) return MTE_E_INVALID_ARG;
-    if (pos1 != MTE_OP_INSERT && pos1 != MTE_OP_REMOVE && pos1 != MTE_OP_ANNOTATE) return MTE_E_INVALID_ARG;
-    if (pos1 == MTE_OP_ANNOTATE && (uint32_t)op[6] >= MTE_ANNOTATE_SLOTS) return MTE_E_INVALID_ARG;
-    if (!evd) return MTE_E_UNSUPPORTED;
-    MTE_STAT(st[kStScanned] += (uint32_t)D.n;)
-    stream_regen<K>(pl, sd, D.n, s, (uint32_t)pos1, (uint32_t)op[6], ev);
-    D.k++;
-    return 0;
-  }
-  if (lop) {
-    if (!(s > lseq && s < kLocalBase) || c != 0) return MTE_E_INVALID_ARG;
-    if (type == MTE_OP_ANNOTATE && (flags & MTE_F_REWRITE)) return MTE_E_UNSUPPORTED;
-    if (type == MTE_OP_ANNOTATE && (uint32_t)op[7] != MTE_NO_PROPS && (uint32_t)op[7] >= MTE_ANNOTATE_SLOTS)
-      return MTE_E_INVALID_ARG;
-    lseq = s;
-  } else if (ldoc && type <= MTE_OP_ANNOTATE && c == 0) {
-    return MTE_E_INVALID_ARG;  // a remote op from the local client's own slot
-  }
   const bool ins = type == MTE_OP_INSERT;
   const bool marker = ins && (flags & MTE_F_MARKER) != 0;
   const int32_t nlen = marker ? 1 : pos2;  // insert: length of the new segment
@@ -685,12 +331,6 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   const bool newcalc = (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
   int n = D.n;
 
-  if (type == MTE_OP_ACK) {
-    if (!(pos1 > 0 && pos1 <= pos2 && pos2 <= lseq)) return MTE_E_INVALID_ARG;
-    MTE_STAT(st[kStScanned] += (uint32_t)n;)
-    stream_ack<K>(pl, sd, n, pos1, pos2, s, (uint32_t)op[6]);
-    if (refd && rhi) stream_slide(pl, sd, n, rt, rhi, s);
-  }
   if (ins || rng) {
     MTE_STAT(st[kStScanned] += (uint32_t)n;)
     // ---- A: scan -----------------------------------------------------------
@@ -705,8 +345,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
       Regs<E, K> R;
       tile_load_hot<K>(R, pl, sd, tb, n);
       int32_t L[E], P[E];
-      if (lop) local_lengths<K>(R, L);
-      else leaf_lengths<E, K>(R, r, c + 1, (int)c, D.min_seq, newcalc, L);
+      leaf_lengths<E, K>(R, r, c + 1, (int)c, D.min_seq, newcalc, L);
       const int32_t tot = prefix<E>(L, P);
 #pragma unroll
       for (int j = 0; j < E; j++) P[j] += carry;
@@ -731,7 +370,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
         }
       }
       if (ins && gs < 0) {
-        const int x = (ldoc && !lop) ? find_slot_remote<E>(L, P, R.seq, pos1) : find_slot<E>(L, P, pos1);
+        const int x = find_slot<E>(L, P, pos1);
         if (x >= 0) gs = tb + x;
       }
       carry += tot;
@@ -846,12 +485,11 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
       }
       if (g >= 0) {
         pl[g] = (uint32_t)nlen;
-        pl[sd + g] = (uint32_t)(lop ? kLocalBase + s : s);
+        pl[sd + g] = (uint32_t)s;
         pl[2 * sd + g] = (uint32_t)kNone;
         pl[3 * sd + g] = 0u;
         pl[4 * sd + g] = (c + 1u) | (marker ? (1u + (uint32_t)pos2) << 8 : 0u);
-        // a marker of an MTE_DOC_REFS document takes its reserved text unit (its name)
-        pl[5 * sd + g] = (marker && !refd) ? 0u : a.text_base + (uint32_t)op[6];
+        pl[5 * sd + g] = marker ? 0u : a.text_base + (uint32_t)op[6];
       }
     }
     if (g >= 0) {
@@ -868,11 +506,6 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
       if (l == 0) {
 #pragma unroll
         for (int kk = 0; kk < K; kk++) pl[(kFieldPlanes + kk) * sd + g] = pr[kk][0];
-        if (ldoc) {
-#pragma unroll
-          for (int kk = 0; kk < K; kk++) pl[(kFieldPlanes + K + kk) * sd + g] = 0u;  // nothing pending
-          pl[(uint64_t)kAnnPlane<K> * sd + g] = 0u;  // in no annotate group
-        }
       }
       MTE_STAT(if (!marker) st[kStUnits] += (uint32_t)pos2;)
     }
@@ -892,8 +525,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
         Regs<E, K> R;
         tile_load_hot<K>(R, pl, sd, tb, n);
         int32_t L[E], P[E];
-        if (lop) local_lengths<K>(R, L);
-        else leaf_lengths<E, K>(R, r, c + 1, (int)c, D.min_seq, newcalc, L);
+        leaf_lengths<E, K>(R, r, c + 1, (int)c, D.min_seq, newcalc, L);
         const int32_t tot = prefix<E>(L, P);
         bool in[E];
         uint32_t cnt = 0;
@@ -913,7 +545,7 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
           int32_t OL[E], OP[E];
 #pragma unroll
           for (int j = 0; j < E; j++) {
-            evf[j] = in[j] && (!rem0 || lop || R.rseq[j] == kNone);
+            evf[j] = in[j] && (!rem0 || R.rseq[j] == kNone);
             const bool gone = rem0 && in[j];
             OL[j] = (R.rseq[j] == kNone && !gone) ? R.len[j] : 0;
           }
@@ -936,88 +568,30 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
         if (cnt == 0) continue;
         cnt_all += cnt;
         const int base = tb + l * E;
-        if (lop && type == MTE_OP_ANNOTATE && (uint32_t)op[7] < MTE_ANNOTATE_SLOTS) {
-          // the visited slots join the annotate's segment group (mergeTree.ts:1874-1880)
-          uint32_t* q = pl + (uint64_t)kAnnPlane<K> * sd;
-          uint32_t gm[E];
-#pragma unroll
-          for (int j = 0; j < E; j++) gm[j] = ld_l2(q + (in[j] ? base + j : 0));  // only in[] slots are stored
-#pragma unroll
-          for (int j = 0; j < E; j++)
-            if (in[j]) q[base + j] = gm[j] | (1u << (uint32_t)op[7]);
-        }
         if (rem) {
           // markRemoved (mergeTree.ts:1924-1962)
 #pragma unroll
           for (int j = 0; j < E; j++) {
             if (in[j]) {
-              // a local removal: removedSeq Unassigned, removers [local]; a
-              // remote one keeps an earlier removedSeq but overtakes a pending
-              // local one (kNone and pending seqs are both >= kLocalBase)
-              pl[2 * sd + base + j] =
-                  (uint32_t)(lop ? kLocalBase + s : ((ldoc ? R.rseq[j] >= kLocalBase : R.rseq[j] == kNone) ? s : R.rseq[j]));
-              pl[3 * sd + base + j] = lop ? 1u : (R.rmask[j] | (1u << c));
+              // an earlier removedSeq stays; the remover joins the mask
+              pl[2 * sd + base + j] = (uint32_t)(R.rseq[j] == kNone ? s : R.rseq[j]);
+              pl[3 * sd + base + j] = R.rmask[j] | (1u << c);
             }
           }
         } else if (K > 0) {
           // PropertiesManager.addProperties (segmentPropertiesManager.ts:63-151)
           // loads unconditional (padding reads slot 0), padding selected away
           // after: no branch per load
-          uint32_t pr[K > 0 ? K : 1][E], old[K > 0 ? K : 1][E], pk[K > 0 ? K : 1][E];
+          uint32_t pr[K > 0 ? K : 1][E];
 #pragma unroll
           for (int kk = 0; kk < K; kk++)
 #pragma unroll
             for (int j = 0; j < E; j++) {
               const int i = base + j;
               const uint32_t o = ld_l2(pl + (kFieldPlanes + kk) * sd + (i < n ? i : 0));
-              old[kk][j] = i < n ? o : 0u;
-              pr[kk][j] = ((flags & MTE_F_REWRITE) && in[j]) ? 0u : old[kk][j];
+              pr[kk][j] = ((flags & MTE_F_REWRITE) && in[j]) ? 0u : (i < n ? o : 0u);
             }
-          if (ldoc) {
-#pragma unroll
-            for (int kk = 0; kk < K; kk++)
-#pragma unroll
-              for (int j = 0; j < E; j++) {
-                const int i = base + j;
-                const uint32_t q = ld_l2(pl + (kFieldPlanes + K + kk) * sd + (i < n ? i : 0));
-                pk[kk][j] = i < n ? q : 0u;
-              }
-          } else {
-#pragma unroll
-            for (int kk = 0; kk < K; kk++)
-#pragma unroll
-              for (int j = 0; j < E; j++) pk[kk][j] = 0u;
-          }
           apply_props<E, K>(pr, in, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], (uint32_t)op[6], a);
-          if (ldoc && !lop) {
-            // shouldModifyKey: a key with a pending local update keeps its
-            // value, the rewrite's clear included (segmentPropertiesManager.ts:94-135)
-#pragma unroll
-            for (int kk = 0; kk < K; kk++)
-#pragma unroll
-              for (int j = 0; j < E; j++) pr[kk][j] = pk[kk][j] ? old[kk][j] : pr[kk][j];
-          }
-          if (lop) {
-            // the local annotate's keys become pending on the marked slots; a key
-            // not pending yet keeps its value in the base plane (what this
-            // annotate's rollback puts back when no older one set the key)
-            const mte_propset ps = a.ps[(uint32_t)op[6]];
-            for (uint32_t t = 0; t < ps.count; t++) {
-              const uint32_t key = uni(a.pe[ps.first + t].key);
-              if (key < (uint32_t)K) {
-#pragma unroll
-                for (int kk = 0; kk < K; kk++) {
-                  if ((uint32_t)kk != key) continue;
-#pragma unroll
-                  for (int j = 0; j < E; j++)
-                    if (in[j] && pk[kk][j] == 0u) pl[(uint64_t)(kBasePlane<K> + kk) * sd + base + j] = old[kk][j];
-                }
-#pragma unroll
-                for (int j = 0; j < E; j++)
-                  if (in[j]) pl[(kFieldPlanes + K + key) * sd + base + j] = (uint32_t)s;
-              }
-            }
-          }
 #pragma unroll
           for (int kk = 0; kk < K; kk++)
 #pragma unroll
@@ -1028,12 +602,10 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
       MTE_STAT(st[kStWritten] += cnt_all;)
       if (type == MTE_OP_ANNOTATE) st[kStPwrites] += cnt_all * (uint32_t)q2[3];
       vm_drain();
-      if (rem && !lop && refd && rhi) stream_slide(pl, sd, n, rt, rhi, s);
     }
   }
   D.n = n;
   D.k++;
-  if (lop) return 0;  // a local op moves no window
 
   if (type != MTE_OP_NOOP) {  // Client.completeAndLogOp (client.ts:525-528)
     if (!(D.cur_seq < s)) return MTE_E_SEQ_ORDER;
@@ -1104,7 +676,6 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
 // pass 3: documents pass 2 escalated (more than 1,022 segments)
 template <int K, bool S>
 __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
-  __shared__ uint32_t zlds_all[kDocsPerBlock][kWave];
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
   const int idx = (int)blockIdx.x * kDocsPerBlock + w;
   if (idx >= (int)a.n_docs) return;
@@ -1119,8 +690,6 @@ __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
   DocRun D;
   run_init(D, a, doc, !own);
   uint32_t st[kNumStats] = {};
-  int32_t lseq = (int32_t)a.hdr[doc].pad0;  // local-client docs: the last localSeq
-  uint32_t rhi = (hf & MTE_DOC_REFS) ? a.hdr[doc].pad1 : 0u;  // MTE_DOC_REFS docs: reference slots in use
   EvOut ev{nullptr, 0, 0u, 0u};
   if ((hf & MTE_DOC_EVENTS) && a.dl_off) {
     ev.p = a.dl + a.dl_off[doc];
@@ -1129,7 +698,7 @@ __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
   if (D.running) {
     s8v cur = sload8(D.recp + 2 * D.k);
     while (D.running) {
-      const int rc = stream_step<K, S>(D, st, cur, a, zlds_all[w], lseq, ev, rhi);
+      const int rc = stream_step<K, S>(D, st, cur, a, ev);
       if (rc < 0) {
         D.status = rc;
         D.running = false;
@@ -1141,8 +710,6 @@ __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
     }
     if constexpr (S) run_flush_stats(D, st, a);
   }
-  if ((hf & MTE_DOC_LOCAL_CLIENT) && lane_id() == 0) a.hdr[doc].pad0 = (uint32_t)lseq;  // run_finish keeps it
-  if ((hf & MTE_DOC_REFS) && lane_id() == 0) a.hdr[doc].pad1 = rhi;
   if ((hf & MTE_DOC_EVENTS) && a.dl_n && lane_id() == 0) a.dl_n[doc] = ev.n;
   run_finish(D, a);
 }

@@ -126,6 +126,8 @@ export interface EngineStats {
   opsApplied: number;
   segsScanned: number;
   chunkScanned?: number;
+  /** the round phases' bytes read and written in the last run (mte_stats.round_bytes) */
+  roundBytes?: number;
   segsWritten: number;
   propWrites: number;
   unitsInserted: number;

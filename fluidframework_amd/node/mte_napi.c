@@ -429,6 +429,7 @@ static napi_value js_stats(napi_env env, napi_callback_info info) {
   set_f64(env, o, "kernelMs", s.kernel_ms);
   set_f64(env, o, "algoBytes", s.algo_bytes);
   set_f64(env, o, "chunkScanned", (double)s.chunk_scanned);
+  set_f64(env, o, "roundBytes", s.round_bytes);
   return o;
 }
 

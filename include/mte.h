@@ -313,6 +313,10 @@ typedef struct mte_stats {
   double algo_bytes;        /* sum of B_op of the last run   */
   uint64_t chunk_scanned;   /* chunked pass: chunk slots + summary entries its
                                ops scanned (replaces their S_live in algo_bytes) */
+  double round_bytes;       /* chunked pass, round phases: the bytes they had to
+                               read and write in the last run (records, planes
+                               re-laid out / applied / gathered, sub-op lists),
+                               counted with statistics off too               */
 } mte_stats;
 
 /* Per-doc read-out (query-size-then-fill).  On input the *_cap fields give the

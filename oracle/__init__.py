@@ -54,7 +54,7 @@ def load():
         "och_create": [u32, vp], "och_destroy": [vp], "och_load_docs": [vp, u32, vp, vp, u64, vp, u32, vp, u32],
         "och_load_segments": [vp, vp, vp, u64], "och_apply_batch": [vp, vp, C.c_int], "och_read_doc": [vp, u32, vp],
         "och_digest": [vp, vp, u32], "och_doc_status": [vp, vp, u32], "och_doc_nsegs": [vp, u32, vp],
-        "och_stats_get": [vp, vp],
+        "och_stats_get": [vp, vp], "och_read_segments": [vp, u32, vp],
     }.items():
         f = getattr(lib, name)
         f.argtypes = args
@@ -282,7 +282,8 @@ class SpecOracle:
 
     def stats(self):
         zero = {"ops_applied": 0, "segs_scanned": 0, "segs_written": 0, "prop_writes": 0, "units_inserted": 0,
-                "max_segs": 0, "kernel_ms": 0.0, "algo_bytes": 0.0, "chunk_scanned": 0}
+                "max_segs": 0, "kernel_ms": 0.0, "algo_bytes": 0.0, "chunk_scanned": 0,
+                "round_bytes": 0.0}
         a = self.flat.stats() if len(self.sub[0]) else zero
         b = self.tree.stats() if len(self.sub[1]) else zero
         out = {k: a[k] + b[k] for k in a if k not in ("max_segs", "kernel_ms")}

@@ -686,6 +686,40 @@ int och_read_doc(och_ctx* c, uint32_t doc, mte_doc_view* v) {
   return MTE_OK;
 }
 
+/* every held segment, tombstones included, in document order (as
+ * mte_read_segments / orc_read_segments) */
+int och_read_segments(och_ctx* c, uint32_t doc, mte_seg_list* v) {
+  if (!c || !v || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  const cdoc* d = &c->docs[doc];
+  uint64_t nt = 0;
+  uint32_t i = 0;
+  for (uint32_t k = 0; k < d->nch; k++) {
+    const chunk* ck = d->ch[k];
+    for (uint32_t j = 0; j < ck->n; j++, i++) {
+      const cseg* g = &ck->s[j];
+      if (i < v->seg_cap && v->segs) {
+        mte_seg* s = &v->segs[i];
+        s->text_off = g->kind == 0 ? (uint32_t)nt : 0u;
+        s->len = (uint32_t)g->len;
+        s->seq = g->seq;
+        s->removed_seq = g->rseq == NONE_SEQ ? MTE_NOT_REMOVED : g->rseq;
+        s->removers = g->rseq == NONE_SEQ ? 0u : g->rmask;
+        s->client = g->cli;
+        s->kind = g->kind;
+        s->propset = MTE_NO_PROPS;
+        if (v->props)
+          for (uint32_t q = 0; q < c->n_keys; q++) v->props[(size_t)i * c->n_keys + q] = g->props[q];
+      }
+      if (g->kind == 0)
+        for (int32_t u = 0; u < g->len; u++, nt++)
+          if (nt < v->text_cap && v->text) v->text[nt] = c->arena[g->toff + (uint32_t)u];
+    }
+  }
+  v->n_segs = i;
+  v->n_text = nt;
+  return MTE_OK;
+}
+
 int och_stats_get(och_ctx* c, mte_stats* o) {
   if (!c || !o) return MTE_E_INVALID_ARG;
   memset(o, 0, sizeof(*o));

@@ -25,6 +25,7 @@ int och_read_doc(och_ctx* c, uint32_t doc, mte_doc_view* v);
 int och_digest(och_ctx* c, uint64_t* out, uint32_t n_docs);
 int och_doc_status(och_ctx* c, int32_t* out, uint32_t n_docs);
 int och_doc_nsegs(och_ctx* c, uint32_t doc, uint32_t* out);
+int och_read_segments(och_ctx* c, uint32_t doc, mte_seg_list* v);
 int och_stats_get(och_ctx* c, mte_stats* out);
 
 #ifdef __cplusplus

@@ -3,8 +3,9 @@ seg_capacity >= 8192) and of snapshot-body loading (mte_load_segments), against
 the CPU restatement: digests, statuses, op statistics and read-outs bit-exact.
 
 Config 5 (64 docs x 2^20 preloaded segments, 4 rounds of 65,536 concurrent
-ops) is exercised here at scaled sizes the flat oracle replays in seconds; the
-full size runs in bench.py --config 5 with a prefix parity sample."""
+ops) is exercised at scaled sizes against the flat oracle, and at full size
+against the same restatement with a chunk index (oracle/chunked.c), which
+replays the whole workload in ~20 s on 8 host threads."""
 import numpy as np
 import pytest
 
@@ -30,16 +31,13 @@ def both(stream, cap, threads=8):
 @pytest.mark.parametrize("mode", [1, 2])
 def test_gpu_chunk_config5_shaped(mode):
     # 8 docs x 20,000 preloaded segments, 4 rounds of 2,000 concurrent ops;
-    # legacy documents of that size are beyond the tree pass (MTE_E_CAPACITY)
+    # legacy documents of that size replay on the HBM tree pass (mte_htree.h)
     s = gen.generate(5, n_docs=8, ops_per_doc=8000, init_segs=20000, round_ops=2000, length_mode=mode)
     cap = gen.seg_capacity(5, s["params"])
     assert cap >= 8192
     o, d = both(s, cap)
-    if mode == 1:
-        assert (o.statuses() == MTE_E_CAPACITY).all()
-    else:
-        assert (o.statuses() == 0).all()
-        assert o.stats()["max_segs"] > 20000
+    assert (o.statuses() == 0).all()
+    assert o.stats()["max_segs"] > 20000
     assert_same(o, d, sample_docs=8)
 
 
@@ -346,4 +344,25 @@ def test_gpu_config5_full_size_round_phases_equal_op_after_op():
     d.sync()
     assert (d.statuses() == 0).all()
     np.testing.assert_array_equal(d.digest(), seq)
+    d.close()
+
+
+def test_gpu_config5_full_size_equals_chunked_restatement():
+    # BASELINE config 5 at full size, every op: the timed path (round phases,
+    # statistics off) against oracle/chunked.c -- statuses, digests of all 64
+    # documents, and the text and segment lists of three of them
+    s = gen.generate(5)
+    cap = gen.seg_capacity(5, s["params"])
+    o = OracleEngine(s["n_keys"], threads=16, tree="chunked")
+    gen.load_stream(o, s)
+    o.apply_batch(s["batch"])
+    assert (o.statuses() == 0).all()
+    d = DeviceEngine(s["n_keys"], seg_capacity=cap)
+    d.set_stats(False)
+    gen.load_stream(d, s)
+    d.apply_batch(s["batch"])
+    np.testing.assert_array_equal(d.statuses(), o.statuses())
+    np.testing.assert_array_equal(d.digest(), o.digest())
+    for doc in (0, 31, 63):
+        assert d.read_doc(doc) == o.read_doc(doc)
     d.close()

@@ -186,10 +186,11 @@ def test_gpu_tree_pass_long_legacy_docs_go_on_in_hbm():
 
 def test_gpu_tree_pass_capacity_is_the_context_capacity():
     # a legacy document stops with MTE_E_CAPACITY only at the ctx capacity
-    s = gen.generate(3, n_docs=4, ops_per_doc=4000, init_len=20000, round_ops=1024, min_length=16,
-                     length_mode=1)
+    s = gen.generate(3, n_docs=4, ops_per_doc=4000, max_lag=32, mix=gen.MIX_INSERT | gen.MIX_ANNOTATE,
+                     min_length=16, length_mode=1)
     o, d = replay_both_cap(s, 1536)
     assert (o.statuses() == MTE_E_CAPACITY).all()
+    assert o.stats()["max_segs"] > 1020
     assert_same(o, d, sample_docs=4)
 
 
