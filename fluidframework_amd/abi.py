@@ -44,6 +44,8 @@ OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_ACK, OP_ROLLBACK = 0, 1, 2, 3, 4,
 OP_REGEN = 6          # Client.regeneratePendingOp (a local record; include/mte.h)
 OP_RBKEY = 7          # an annotate rollback's previous-value candidates (include/mte.h)
 OP_REF = 8            # create / remove a local reference (a local record; include/mte.h)
+OP_RELPOS = 9         # relative positions of the record that follows (include/mte.h)
+RP_POS1, RP_BEFORE1, RP_POS2, RP_BEFORE2 = 0x100, 0x200, 0x400, 0x800
 REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE, REF_TRANSIENT = 0x40, 0x80, 0x100  # ReferenceType (ops.ts)
 DELTA_REGEN = 0x10    # kind flag of its output records
 ANNOTATE_SLOTS = 32   # pending local annotate groups tracked per document

@@ -40,7 +40,7 @@ __global__ void begin_batch_kernel(DocHdr* hdr, unsigned long long* stats, uint3
   if (d == 0) *gdone = 0;
   if (d >= n_docs) return;
   hdr[d].resume = 0;
-  hdr[d].flags &= ~(kHdrNeedsEsc | kHdrTreeEsc | kHdrTreeBig);
+  hdr[d].flags &= ~(kHdrNeedsEsc | kHdrTreeEsc | kHdrTreeBig | kHdrRel);
 #pragma unroll
   for (int t = 0; t < kNumStats; t++) stats[(size_t)d * kNumStats + t] = 0;
 }
@@ -80,7 +80,8 @@ __global__ __launch_bounds__(256) void round_sync_kernel(DocHdr* hdr, const uint
   for (uint64_t k = k0; k < k1 && !bad; k += kWave) {
     const bool in = k + (uint64_t)l < k1;
     const uint4 w0 = in ? recs[2 * (k + (uint64_t)l)] : make_uint4(0u, 0u, 0u, (uint32_t)MTE_OP_NOOP);
-    const bool live = in && (w0.w & 0xffu) != MTE_OP_NOOP;
+    const uint32_t ty = w0.w & 0xffu;
+    const bool live = in && ty != MTE_OP_NOOP && ty != MTE_OP_RELPOS;  // RELPOS: seq / ref_seq are offsets
     const int32_t r = (int32_t)w0.y, sq = (int32_t)w0.x;
     // maxima over the live records before this one (exclusive scans)
     const int32_t rin = wave_incl_max(live ? r : INT32_MIN), sin = wave_incl_max(live ? sq : INT32_MIN);
@@ -101,6 +102,26 @@ __global__ __launch_bounds__(256) void round_sync_kernel(DocHdr* hdr, const uint
       hdr[doc].pad1 = (uint32_t)seq;
     }
   }
+}
+
+// Documents whose batch holds MTE_OP_RELPOS records (include/mte.h): the flat
+// ones replay this batch on the HBM-streamed pass (kHdrRel: passes 1 and 2
+// hand them on), the legacy tree ones move to the HBM tree pass for good
+// (their state enters it as from TIER 2, mte_htree.h); the HBM tree pass's own
+// already resolve them.  The chunked pass does not: MTE_E_UNSUPPORTED.
+__global__ void rel_route_kernel(DocHdr* hdr, const uint32_t* docs, uint32_t n, int chunked) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  DocHdr* h = hdr + docs[i];
+  if (h->status != 0) return;
+  const uint32_t f = h->flags;
+  if (f & MTE_DOC_LOCAL_CLIENT) return;
+  if (!(f & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC))) {
+    if (!(f & MTE_DOC_EVENTS)) h->flags = f | kHdrTreeHbmFlag;
+    return;
+  }
+  if (chunked) h->status = MTE_E_UNSUPPORTED;
+  else h->flags = f | kHdrRel | kHdrNeedsEsc;
 }
 
 // (re)initialise docs from their load description: one seq-0 LocalClientId
@@ -457,6 +478,10 @@ struct mte_ctx {
   std::vector<uint32_t> h_sdocs;
   uint32_t* d_sorder_s[2] = {nullptr, nullptr};
   uint64_t sorder_cap_s[2] = {0, 0};
+  // per batch slot: the documents with MTE_OP_RELPOS records (upload_ops)
+  std::vector<uint32_t> h_rel_s[2];
+  uint32_t* d_rel_s[2] = {nullptr, nullptr};
+  uint64_t rel_cap_s[2] = {0, 0};
   int ev_slot = -1;
   // local references of the MTE_DOC_REFS documents (mte_stream.h): ref_cap slots
   // per document, zeroed at every reset
@@ -768,7 +793,12 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
 // Validation of one op record (the kernels index with these fields, so a bad
 // record must never reach them).  Returns nullptr or the reason.
 const char* bad_op(const mte_op& o, const mte_batch* b, bool local_doc, bool refs_doc, uint32_t ref_cap) {
-  if (o.type > MTE_OP_REF) return "type";
+  if (o.type > MTE_OP_RELPOS) return "type";
+  if (o.type == MTE_OP_RELPOS) {  // the record after it is checked by the caller
+    const uint32_t rp = MTE_RP_POS1 | MTE_RP_BEFORE1 | MTE_RP_POS2 | MTE_RP_BEFORE2;
+    if ((o.flags & ~rp) || !(o.flags & (MTE_RP_POS1 | MTE_RP_POS2))) return "relative position record: flags";
+    return nullptr;
+  }
   if (o.type >= MTE_OP_ROLLBACK && !(o.flags & MTE_F_LOCAL)) return "rollback / regen without MTE_F_LOCAL";
   if (o.type == MTE_OP_REF) {
     if (!refs_doc) return "local reference record in a document without MTE_DOC_REFS";
@@ -825,6 +855,8 @@ int upload_ops(mte_ctx* c, const mte_batch* b, int w, uint64_t* bad, const char*
   std::vector<const char*> reasons(nw, nullptr);
   // per worker: the propsets a text insert or an annotate used (kPack4 side key)
   std::vector<std::vector<uint8_t>> tps(nw, std::vector<uint8_t>(b->n_propsets, 0));
+  // per worker: the documents with MTE_OP_RELPOS records
+  std::vector<std::vector<uint32_t>> rels(nw);
   for (uint64_t k0 = 0, it = 0; k0 < b->n_ops; k0 += per_stage, it++) {
     const int si = (int)(it % mte_ctx::kStages);
     const uint64_t n = std::min(per_stage, b->n_ops - k0);
@@ -840,8 +872,15 @@ int upload_ops(mte_ctx* c, const mte_batch* b, int w, uint64_t* bad, const char*
         for (uint64_t k = a; k < e; k++) {
           while (d + 1 < b->n_docs && b->op_offsets[d + 1] <= k0 + k) d++;
           const mte_op& o = b->ops[k0 + k];
-          if (const char* r = bad_op(o, b, !c->h_local.empty() && c->h_local[d], !c->h_refs.empty() && c->h_refs[d],
-                                     c->ref_cap)) {
+          const char* r = bad_op(o, b, !c->h_local.empty() && c->h_local[d], !c->h_refs.empty() && c->h_refs[d],
+                                 c->ref_cap);
+          if (!r && o.type == MTE_OP_RELPOS) {
+            const mte_op* nx = k0 + k + 1 < b->op_offsets[d + 1] ? &b->ops[k0 + k + 1] : nullptr;
+            if (!nx || nx->type > MTE_OP_ANNOTATE) r = "relative position record not followed by an insert, remove "
+                                                      "or annotate of its document";
+            else if (rels[w].empty() || rels[w].back() != d) rels[w].push_back(d);
+          }
+          if (r) {
             uint64_t cur = first_bad.load();
             while (k0 + k < cur && !first_bad.compare_exchange_weak(cur, k0 + k)) {
             }
@@ -886,6 +925,11 @@ int upload_ops(mte_ctx* c, const mte_batch* b, int w, uint64_t* bad, const char*
   c->h_text_ps.assign(b->n_propsets, 0);
   for (const auto& v : tps)
     for (uint32_t i = 0; i < b->n_propsets; i++) c->h_text_ps[i] |= v[i];
+  std::vector<uint32_t>& rd = c->h_rel_s[w];
+  rd.clear();
+  for (const auto& v : rels) rd.insert(rd.end(), v.begin(), v.end());
+  std::sort(rd.begin(), rd.end());
+  rd.erase(std::unique(rd.begin(), rd.end()), rd.end());
   return MTE_OK;
 }
 
@@ -967,7 +1011,7 @@ int mte_destroy(mte_ctx* c) {
     if (p) (void)hipFree(p);
   for (int w = 0; w < 2; w++) {
     void* sl[] = {c->d_ops_s[w], c->d_cps_s[w], c->d_off_s[w], c->d_ps_s[w], c->d_pe_s[w],
-                  c->d_dl_off_s[w], c->d_dl_s[w], c->d_dl_n_s[w], c->d_sorder_s[w]};
+                  c->d_dl_off_s[w], c->d_dl_s[w], c->d_dl_n_s[w], c->d_sorder_s[w], c->d_rel_s[w]};
     for (void* p : sl)
       if (p) (void)hipFree(p);
     if (c->slot_ev[w]) (void)hipEventDestroy(c->slot_ev[w]);
@@ -1162,8 +1206,8 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     }
     // the HBM tree pass takes its own documents and the legacy ones the
     // register tiers hand over (past 1,020 items)
-    for (uint32_t d : tree_docs)
-      if (c->cap > 16 * kWave - 4) htree_docs.push_back(d);
+    // (past 1,020 items, or from a batch with relative positions)
+    for (uint32_t d : tree_docs) htree_docs.push_back(d);
     c->n_htree = (uint32_t)htree_docs.size();
     if (c->n_tree || c->n_htree) {
       HIPCHK(c, hipMalloc((void**)&c->d_tree, nslots * 4));
@@ -1327,6 +1371,7 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
       return rc == MTE_E_INVALID_ARG ? set_err(c, rc, "op %llu: %s", (unsigned long long)bad, why) : rc;
   } else {
     c->h_text_ps.clear();
+    c->h_rel_s[w].clear();
   }
   // append batch text to the arena (a running replay reads only below arena_n;
   // growing it waits for the replay)
@@ -1357,6 +1402,11 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
     HIPCHK(c, hipMemcpyAsync(c->d_sorder_s[w], order.data(), (size_t)b->n_docs * 4, hipMemcpyHostToDevice,
                              c->up_stream));
     HIPCHK(c, hipStreamSynchronize(c->up_stream));  // `order` goes out of scope
+  }
+  if (!c->h_rel_s[w].empty()) {
+    if ((rc = grow(c, &c->d_rel_s[w], &c->rel_cap_s[w], (uint64_t)c->h_rel_s[w].size()))) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->d_rel_s[w], c->h_rel_s[w].data(), c->h_rel_s[w].size() * 4, hipMemcpyHostToDevice,
+                             c->up_stream));
   }
   HIPCHK(c, hipStreamSynchronize(c->up_stream));  // host buffers may be freed after return
   // delta event regions of the MTE_DOC_EVENTS docs (per_op x records + 256 each)
@@ -1472,6 +1522,11 @@ int mte_run(mte_ctx* c) {
   if (c->n_rs) {
     hipLaunchKernelGGL(round_sync_kernel, dim3((c->n_rs + 3) / 4), dim3(256), 0, c->stream, c->hdr, a.recs, c->d_off,
                        c->d_rs_docs, c->n_rs);
+    HIPCHK(c, hipGetLastError());
+  }
+  if (const uint32_t nr = (uint32_t)c->h_rel_s[c->rslot].size()) {
+    hipLaunchKernelGGL(rel_route_kernel, dim3((nr + 255) / 256), dim3(256), 0, c->stream, c->hdr,
+                       c->d_rel_s[c->rslot], nr, c->chunked ? 1 : 0);
     HIPCHK(c, hipGetLastError());
   }
   if (c->n_propsets) {

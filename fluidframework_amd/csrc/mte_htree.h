@@ -80,6 +80,9 @@ struct HT {
   int lp_n;
   int32_t lp_carry;
   const uint16_t* arena;
+  // MTE_OP_RELPOS: positions for the next record (rpf: MTE_RP_POS1 / POS2 given)
+  uint32_t rpf;
+  int32_t rp1, rp2;
 };
 
 // ---- single-item access (wave-uniform) ----------------------------------------
@@ -1271,6 +1274,12 @@ __device__ void ht_regen(const HT& h, int32_t ls, uint32_t t, uint32_t slot, EvO
         if (t == MTE_OP_INSERT) hit = sq == kLocalBase + ls;
         else if (t == MTE_OP_REMOVE) hit = rs == kLocalBase + ls;
         else hit = ((am >> slot) & 1u) && (rs == kNone || rp);
+        // a member that re-sends nothing leaves the group (resetPendingDeltaToOps
+        // enqueues only the segments with a new op, client.ts:803-852): the
+        // zamboni stops holding it for the group (titems.c doc_regen)
+        if (!hit && t == MTE_OP_REMOVE && lr == ls) h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = 0u;
+        if (!hit && t == MTE_OP_ANNOTATE && ((am >> slot) & 1u))
+          h.pl[(uint64_t)kAnnPlane<K> * h.sd + i] = am & ~(1u << slot);
       }
       // localNetLength with localSeq (mergeTree.ts:575-593)
       int32_t ll = (v && !(tt & kTEmpty)) ? len : 0;
@@ -1304,13 +1313,37 @@ __device__ void ht_regen(const HT& h, int32_t ls, uint32_t t, uint32_t slot, EvO
 
 // ---- one record (titems.c doc_apply / doc_apply_local) ----------------------------------
 
+// MTE_OP_RELPOS (include/mte.h): the position of the first marker whose key
+// plane `key` holds `vid` in the view of the record it serves (getPosition,
+// mergeTree.ts:853-870, the lengths before it; posFromRelativePos :1369-1392),
+// -1 when no held marker carries the id
+template <int K>
+__device__ int32_t ht_marker_pos(HT& h, uint32_t key, uint32_t vid, bool local, int32_t r, int c) {
+  if (key >= (uint32_t)K || vid == 0u) return -1;
+  const uint32_t* kp = h.pl + (uint64_t)(kFieldPlanes + key) * h.sd;
+  const uint32_t* mp = h.pl + 4 * h.sd;
+  const uint32_t* tw = h.tw;
+  const int x = ht_first(0, h.n, [&](int i) {
+    return (ld_l2(mp + i) >> 8) != 0u && ld_l2(kp + i) == vid && !(ld_l2(tw + i) & kTEmpty);
+  });
+  if (x < 0) return -1;
+  ht_persp(h, local, r, c);
+  ht_ensure(h, x);
+  return (int32_t)uld((const uint32_t*)h.P + x);
+}
+
 template <int K, bool S>
 __device__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStats], const ReplayArgs& a, int32_t& lseq, EvOut& ev,
                        uint32_t& rhi) {
-  const s8v op = sload8(D.recp + 2 * D.k);
+  s8v op = sload8(D.recp + 2 * D.k);
   const uint4* rec = D.recp + 2 * D.k;
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
+  if (h.rpf) {  // the positions an MTE_OP_RELPOS record resolved for this one
+    if (h.rpf & MTE_RP_POS1) op[4] = h.rp1;
+    if (h.rpf & MTE_RP_POS2) op[5] = h.rp2;
+    h.rpf = 0;
+  }
   const bool ldoc = h.ldoc;
   const bool evd = (D.flags & MTE_DOC_EVENTS) != 0;
   const bool refd = (D.flags & MTE_DOC_REFS) != 0 && a.refs != nullptr;
@@ -1323,6 +1356,33 @@ __device__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStats], const Replay
   int rc;
   h.min_seq = D.min_seq;
   h.cur_seq = D.cur_seq;
+  if (type == MTE_OP_RELPOS) {
+    // the next record's positions, in its view (the engine checked that an
+    // insert, remove or annotate of this document follows)
+    if (D.k + 1 >= D.k1) return MTE_E_INVALID_ARG;
+    const s8v nx = sload8(rec + 2);
+    const uint32_t nw3 = (uint32_t)nx[3];
+    const uint32_t nt = nw3 & 0xffu, nc = (nw3 >> 8) & 0xffu;
+    const bool nloc = ((nw3 >> 16) & MTE_F_LOCAL) != 0;
+    if (nt > MTE_OP_ANNOTATE || nc >= MTE_MAX_CLIENTS) return MTE_E_INVALID_ARG;
+    const uint32_t key = (uint32_t)op[6];
+    h.rpf = 0;
+    if (flags & MTE_RP_POS1) {
+      int32_t p = ht_marker_pos<K>(h, key, (uint32_t)op[4], nloc, nx[1], (int)nc);
+      if (p >= 0) p = (flags & MTE_RP_BEFORE1) ? p - op[0] : p + 1 + op[0];
+      else if (nt == MTE_OP_INSERT) return MTE_E_UNSUPPORTED;
+      h.rp1 = p;
+      h.rpf |= MTE_RP_POS1;
+    }
+    if ((flags & MTE_RP_POS2) && nt != MTE_OP_INSERT) {
+      int32_t p = ht_marker_pos<K>(h, key, (uint32_t)op[5], nloc, nx[1], (int)nc);
+      if (p >= 0) p = (flags & MTE_RP_BEFORE2) ? p - op[1] : p + 1 + op[1];
+      h.rp2 = p;
+      h.rpf |= MTE_RP_POS2;
+    }
+    D.k++;
+    return 0;
+  }
   if (type == MTE_OP_REF) {
     if (!lop || !ldoc || !refd) return MTE_E_UNSUPPORTED;
     if ((uint32_t)op[5] >= a.ref_cap || (uint32_t)op[7] > 3u) return MTE_E_INVALID_ARG;
@@ -1446,6 +1506,7 @@ __global__ __launch_bounds__(64) void htree_kernel(ReplayArgs a, HtreeArgs t) {
   h.plocal = false;
   h.pr = 0;
   h.pc = 0;
+  h.rpf = 0;
   if (!ldoc && uld(stp + kHsEntered) == 0u) {
     // a legacy document leaves the register tiers: its depth / next id / heap
     // (DocHdr pad0 / pad1, TreeArgs::heap) move to the HBM tree's state

@@ -37,6 +37,9 @@ struct DocHdr {
   uint32_t pad0, pad1;
 };
 constexpr uint32_t kHdrNeedsEsc = 0x80000000u;
+// the document's batch holds MTE_OP_RELPOS records: passes 1 and 2 leave it to
+// the HBM-streamed pass (set per batch by the engine, mte_engine.hip)
+constexpr uint32_t kHdrRel = 0x08000000u;
 
 // kStChunkCanon / kStChunkScan (chunk pass only): the canonical S_live of its
 // ops, and the chunk slots + summary entries those ops actually scanned

@@ -974,10 +974,13 @@ __global__ __launch_bounds__(WPB * kWave, W * 4 / WPB) void pair_kernel(ReplayAr
     const int doc = (int)a.pair_docs[(uint32_t)g * (uint32_t)pair + (uint32_t)t];
     if (doc >= 0) {
       DocHdr h = a.hdr[doc];
-      h.flags &= ~kHdrNeedsEsc;
+      const bool rel = (h.flags & kHdrRel) != 0;  // the streamed pass's this batch
+      if (!rel) h.flags &= ~kHdrNeedsEsc;
       if (lane_id() == 0) hl[t] = h;
-      live |= 1u << t;
-      total += (uint32_t)(a.op_off[doc + 1] - a.op_off[doc]) - h.resume;
+      if (!rel) {
+        live |= 1u << t;
+        total += (uint32_t)(a.op_off[doc + 1] - a.op_off[doc]) - h.resume;
+      }
     }
   }
   fence_wave();
@@ -1049,6 +1052,10 @@ __global__ __launch_bounds__(256) void big_kernel(ReplayArgs a) {
   DocRun D;
   run_init(D, a, doc, true);
   if (!D.running && !(a.hdr[doc].flags & kHdrNeedsEsc)) return;  // untouched doc: leave the header alone
+  if (D.flags & kHdrRel) {  // relative positions: on to the streamed pass
+    D.flags |= kHdrNeedsEsc;
+    D.running = false;
+  }
   uint32_t* zlds = zlds_all[w];
   while (D.running) {
     const int n = D.n;

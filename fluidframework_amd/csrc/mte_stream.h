@@ -298,6 +298,44 @@ __device__ int stream_ref(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uin
   return 0;
 }
 
+// MTE_OP_RELPOS (include/mte.h): the position of the first marker whose key
+// plane `key` holds `vid`, in the view (r, c) -- getPosition (mergeTree.ts:
+// 853-870) sums the lengths of everything before it; undefined leaves count 0
+// -- or -1 when no held marker carries the id (posFromRelativePos,
+// mergeTree.ts:1369-1392).  One front-to-back tile scan with early exit.
+template <int K>
+__device__ int32_t stream_marker_pos(const uint32_t* pl, uint64_t sd, int n, uint32_t key, uint32_t vid, int32_t r,
+                                     uint32_t c, int32_t m, bool newcalc) {
+  if (key >= (uint32_t)K || vid == 0u) return -1;
+  constexpr int E = kTileE;
+  const uint32_t* kp = pl + (uint64_t)(kFieldPlanes + key) * sd;
+  int32_t carry = 0;
+  for (int tb = 0; tb < n; tb += kTile) {
+    Regs<E, K> R;
+    tile_load_hot<K>(R, pl, sd, tb, n);
+    int32_t L[E], P[E];
+    leaf_lengths<E, K>(R, r, c + 1, (int)c, m, newcalc, L);
+    const int32_t tot = prefix<E>(L, P);
+    int jsel = E;
+#pragma unroll
+    for (int j = E - 1; j >= 0; j--) {
+      const int i = tb + lane_id() * E + j;
+      const uint32_t v = ld_l2(kp + (i < n ? i : 0));  // unconditional, selected after
+      jsel = (i < n && (R.meta[j] >> 8) != 0u && v == vid) ? j : jsel;
+    }
+    const uint64_t msk = __ballot(jsel < E);
+    if (msk) {
+      const int ls = __ffsll((long long)msk) - 1;
+      int32_t pv = P[0];
+#pragma unroll
+      for (int j = 1; j < E; j++) pv = jsel == j ? P[j] : pv;
+      return carry + (int32_t)rdlane(pv, ls);
+    }
+    carry += tot;
+  }
+  return -1;
+}
+
 // One op of one HBM-resident document of remote clients (see the file
 // comment).  Returns 0 or a negative MTE_E_*.  ev: its delta events
 // (MTE_DOC_EVENTS docs).
@@ -317,6 +355,29 @@ __device__ int stream_step(DocRun& D, uint32_t (&st)[kNumStats], s8v& cur, const
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
+  if (type == MTE_OP_RELPOS) {
+    // the next record's positions, in its view (the engine checked that an
+    // insert, remove or annotate of this document follows)
+    if (D.k + 1 >= D.k1) return MTE_E_INVALID_ARG;
+    const uint32_t nw3 = (uint32_t)cur[3];
+    const uint32_t nt = nw3 & 0xffu, nc = (nw3 >> 8) & 0xffu;
+    if (nt > MTE_OP_ANNOTATE || nc >= MTE_MAX_CLIENTS || ((nw3 >> 16) & MTE_F_LOCAL)) return MTE_E_INVALID_ARG;
+    const bool newcalc = (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
+    const uint32_t key = (uint32_t)op[6];
+    if (flags & MTE_RP_POS1) {
+      int32_t p = stream_marker_pos<K>(pl, sd, D.n, key, (uint32_t)op[4], cur[1], nc, D.min_seq, newcalc);
+      if (p >= 0) p = (flags & MTE_RP_BEFORE1) ? p - op[0] : p + 1 + op[0];
+      else if (nt == MTE_OP_INSERT) return MTE_E_UNSUPPORTED;
+      cur[4] = p;
+    }
+    if ((flags & MTE_RP_POS2) && nt != MTE_OP_INSERT) {
+      int32_t p = stream_marker_pos<K>(pl, sd, D.n, key, (uint32_t)op[5], cur[1], nc, D.min_seq, newcalc);
+      if (p >= 0) p = (flags & MTE_RP_BEFORE2) ? p - op[1] : p + 1 + op[1];
+      cur[5] = p;
+    }
+    D.k++;
+    return 0;
+  }
   // local ops, acks, rollbacks, regenerations and references belong to a
   // local client's document (the HBM tree pass)
   if (type == MTE_OP_REF || (flags & MTE_F_LOCAL) || type >= MTE_OP_ACK) return MTE_E_UNSUPPORTED;

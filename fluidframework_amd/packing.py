@@ -32,13 +32,15 @@ import numpy as np
 
 from .abi import (F_LOCAL, F_MARKER, F_MSG_END, F_REWRITE, LOCAL_SEQ_BASE, MTE_E_CAPACITY, MTE_E_CLIENT_RANGE,
                   MTE_E_INVALID_ARG, MTE_E_STATE, MTE_E_UNSUPPORTED, MTE_MAX_CLIENTS, NO_PROPS, OP_ACK, OP_ROLLBACK,
-                  OP_REGEN, OP_RBKEY, OP_REF, ANNOTATE_SLOTS, REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE,
+                  OP_REGEN, OP_RBKEY, OP_REF, OP_RELPOS, RP_BEFORE1, RP_BEFORE2, RP_POS1, RP_POS2,
+                  ANNOTATE_SLOTS, REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE,
                   REF_TRANSIENT,
                   OP_ANNOTATE, OP_DTYPE, OP_INSERT, OP_NOOP, OP_REMOVE, PROP_DTYPE, PROPSET_DTYPE,
                   MergeTreeError)
 
 INSERT, REMOVE, ANNOTATE, GROUP = 0, 1, 2, 3  # MergeTreeDeltaType, ops.ts:43-48
 I32_MIN, I32_MAX = -(1 << 31), (1 << 31) - 1
+MARKER_ID_KEY = "markerId"  # reservedMarkerIdKey (mergeTreeNodes.ts)
 
 
 def canonical_json(v) -> str:
@@ -286,6 +288,9 @@ class BatchBuilder:
         out = self.ops[doc]
         last = len(recs) - 1
         for i, (t, flags, p1, p2, a, b) in enumerate(recs):
+            if t == OP_RELPOS:  # seq / ref_seq carry the offsets
+                out.append((b[0], b[1], 0, t, short, flags, p1, p2, a, 0))
+                continue
             if i == last:
                 flags |= F_MSG_END
             out.append((seq, ref, msn, t, short, flags, p1, p2, a, b))
@@ -303,13 +308,18 @@ class BatchBuilder:
         self._op_records(op, recs)
         if not recs:
             recs.append((OP_NOOP, 0, 0, 0, 0, NO_PROPS))
-        if any(f & F_REWRITE for _, f, *_ in recs):
+        if any(t != OP_RELPOS and f & F_REWRITE for t, f, *_ in recs):
             raise MergeTreeError(MTE_E_UNSUPPORTED, "local combiningOp rewrite")
         first = clients.local_seq + 1
-        if first + len(recs) >= LOCAL_SEQ_BASE:
+        n_ops = sum(1 for r in recs if r[0] != OP_RELPOS)
+        if first + n_ops >= LOCAL_SEQ_BASE:
             raise MergeTreeError(MTE_E_INVALID_ARG, "localSeq overflow")
         out = self.ops[doc]
-        for i, (t, flags, p1, p2, a, b) in enumerate(recs):
+        i = 0
+        for t, flags, p1, p2, a, b in recs:
+            if t == OP_RELPOS:  # takes no localSeq
+                out.append((b[0], b[1], 0, t, 0, flags, p1, p2, a, 0))
+                continue
             if t == OP_ANNOTATE:
                 used = set(clients.ann_slot.values())
                 free = next((x for x in range(ANNOTATE_SLOTS) if x not in used), None)
@@ -319,9 +329,10 @@ class BatchBuilder:
                 f0, cnt = self.props.sets[a]
                 clients.ann_props[first + i] = dict(self.props.entries[f0:f0 + cnt])
             out.append((first + i, 0, 0, t, 0, flags | F_LOCAL, p1, p2, a, b))
-        clients.local_seq += len(recs)
+            i += 1
+        clients.local_seq += n_ops
         clients.pending.append((first, clients.local_seq))
-        clients.pending_types.append(tuple(r[0] for r in recs))
+        clients.pending_types.append(tuple(r[0] for r in recs if r[0] != OP_RELPOS))
 
     def add_rollback(self, doc: int, clients: DocClients):
         """Client.rollback of the latest pending local op (client.ts:396-398 ->
@@ -431,16 +442,21 @@ class BatchBuilder:
             for member in op.get("ops", []):
                 self._op_records(member, recs)
             return
-        if "pos1" not in op and op.get("relativePos1") is not None:
-            raise MergeTreeError(MTE_E_UNSUPPORTED, "relativePos1")
-        if t in (REMOVE, ANNOTATE) and "pos2" not in op:
+        rel = self._relpos(op, t)
+        if t in (REMOVE, ANNOTATE) and "pos2" not in op and not (rel and rel[1] & RP_POS2):
             raise MergeTreeError(MTE_E_UNSUPPORTED, "range op without pos2")
+        if rel and (t != INSERT or op.get("seg") is not None):
+            recs.append(rel)
+        p1 = op.get("pos1", 0 if (t == INSERT or (rel and rel[1] & RP_POS1)) else None)
+        p2 = op.get("pos2", 0)
+        if p1 is None:
+            raise MergeTreeError(MTE_E_UNSUPPORTED, "range op without pos1")
         if t == INSERT:
             seg = op.get("seg")
             if seg is None:  # applyInsertOp returns false: no segment
                 recs.append((OP_NOOP, 0, 0, 0, 0, NO_PROPS))
                 return
-            pos = _check_i32(op.get("pos1", 0), "pos1")
+            pos = _check_i32(p1, "pos1")
             if isinstance(seg, str):
                 off, n = self._text(seg)
                 recs.append((OP_INSERT, 0, pos, n, off, NO_PROPS))
@@ -455,7 +471,7 @@ class BatchBuilder:
             else:
                 raise MergeTreeError(MTE_E_INVALID_ARG, f"Unrecognized IJSONSegment type: {seg!r}")
         elif t == REMOVE:
-            recs.append((OP_REMOVE, 0, _check_i32(op["pos1"], "pos1"), _check_i32(op["pos2"], "pos2"),
+            recs.append((OP_REMOVE, 0, _check_i32(p1, "pos1"), _check_i32(p2, "pos2"),
                          0, NO_PROPS))
         elif t == ANNOTATE:
             comb = op.get("combiningOp")
@@ -465,10 +481,34 @@ class BatchBuilder:
                     raise MergeTreeError(MTE_E_UNSUPPORTED, f"combiningOp {comb.get('name')!r}")
                 flags = F_REWRITE
             ps = self.props.add(op.get("props", {}))
-            recs.append((OP_ANNOTATE, flags, _check_i32(op["pos1"], "pos1"),
-                         _check_i32(op["pos2"], "pos2"), ps, NO_PROPS))
+            recs.append((OP_ANNOTATE, flags, _check_i32(p1, "pos1"), _check_i32(p2, "pos2"), ps, NO_PROPS))
         else:
             raise MergeTreeError(MTE_E_INVALID_ARG, f"unknown op type {t!r}")
+
+    def _relpos(self, op, t):
+        """getValidOpRange (client.ts:541-560): a position given as relativePos
+        (no pos1 / pos2) -> an MTE_OP_RELPOS record for the engine to resolve
+        (posFromRelativePos, mergeTree.ts:1369-1392), or None."""
+        flags, vids, offs = 0, [0, 0], [0, 0]
+        for i, (pk, rk, pf, bf) in enumerate((("pos1", "relativePos1", RP_POS1, RP_BEFORE1),
+                                               ("pos2", "relativePos2", RP_POS2, RP_BEFORE2))):
+            rp = op.get(rk)
+            if pk in op or rp is None or (i == 1 and t == INSERT):
+                continue
+            if not isinstance(rp, dict):
+                raise MergeTreeError(MTE_E_INVALID_ARG, f"{rk} must be an object")
+            flags |= pf
+            if rp.get("before"):
+                flags |= bf
+            if rp.get("offset") is not None:
+                offs[i] = _check_i32(rp["offset"], f"{rk}.offset")
+            mid = rp.get("id")
+            # an id no marker was ever given cannot match (value 0)
+            vids[i] = self.interner.values.get(canonical_json(mid), 0) if mid else 0
+        if not flags:
+            return None
+        key = self.interner.keys.get(MARKER_ID_KEY, NO_PROPS)
+        return (OP_RELPOS, flags, vids[0], vids[1], key, (offs[0], offs[1]))
 
     def build(self):
         """-> dict of numpy arrays forming one mte_batch."""

@@ -58,7 +58,8 @@ extern "C" {
 #define MTE_E_MSN_GT_SEQ (-7)  /* msn > seq                  (0x039, 0x04e)     */
 #define MTE_E_INSERT_FAILED (-8) /* "MergeTree insert failed" mergeTree.ts:1666-1672 */
 #define MTE_E_UNSUPPORTED (-9) /* op shape outside the engine (combiningOp other
-                                  than rewrite, relativePos, local/ack ops)     */
+                                  than rewrite, local/ack ops without
+                                  MTE_DOC_LOCAL_CLIENT)                        */
 #define MTE_E_STATE (-10)      /* call out of order (e.g. run before submit)    */
 #define MTE_E_OOM (-11)        /* device or host allocation failed              */
 #define MTE_E_CLIENT_RANGE (-12) /* short client id >= MTE_MAX_CLIENTS          */
@@ -97,7 +98,7 @@ extern "C" {
 #define MTE_OP_ROLLBACK 5
 /* Client.regeneratePendingOp for reconnection (client.ts:972-1002 ->
  * resetPendingDeltaToOps :788-860): a local record with seq = the localSeq L of
- * a pending op and pos1 = its type.  The document does not change; it reports,
+ * a pending op and pos1 = its type.  The text does not change; it reports,
  * as MTE_DELTA_REGEN | type delta records, one per segment of L's segment group
  * in document order, the op that re-sends that segment: its position in the
  * view at localSeq L (findReconnectionPosition :709-713 -> localNetLength with
@@ -110,6 +111,8 @@ extern "C" {
  *   annotate: every segment L visited (a = the annotate's group slot, see
  *     MTE_OP_ANNOTATE below) that is not removed, or only by a pending local
  *     remove.
+ * A member that re-sends nothing (a removal a remote remove overtook, an
+ * annotated segment removed since) leaves the group, as :803-852 dequeue it.
  * The host re-sends the ops and keeps the group pending under the same L
  * (acked by MTE_OP_ACK as before).  Only in MTE_DOC_LOCAL_CLIENT documents
  * that record events (MTE_DOC_EVENTS).                                       */
@@ -154,6 +157,28 @@ extern "C" {
  * come from mte_read_refs (referencePositionToLocalPosition,
  * mergeTree.ts:1095-1112).                                                     */
 #define MTE_OP_REF 8
+/* Relative positions (IRelativePosition, ops.ts:62-76) of the insert, remove
+ * or annotate record that follows in the same document (getValidOpRange,
+ * client.ts:541-560 -> posFromRelativePos, mergeTree.ts:1369-1392), resolved
+ * in that record's own view: its ref_seq and client, the local view for a
+ * local record.  a = the property key holding marker ids
+ * (reservedMarkerIdKey "markerId"; MTE_NO_PROPS: the context has none), pos1
+ * / pos2 = the value ids of relativePos1 / relativePos2's `id` (0: none),
+ * seq / ref_seq = their `offset`s (0 when absent), flags MTE_RP_*: which of
+ * the two are given and their `before`.  The marker is the first marker
+ * segment in document order whose key-a value is the id (idToSegment,
+ * mergeTree.ts:490, 597-599; ids are unique per document); with P its
+ * position in the view (getPosition, :853-870), the record's position becomes
+ * P - offset (before) or P + 1 + offset.  An id no held marker carries gives
+ * -1, as the reference's "not found" (a remove or annotate of [-1, -1) does
+ * nothing; an insert there stops the document with MTE_E_UNSUPPORTED).  An
+ * insert takes relativePos1 only.  Contexts of >= 8192 segments replay such
+ * a document of the new length calculation with MTE_E_UNSUPPORTED.         */
+#define MTE_OP_RELPOS 9
+#define MTE_RP_POS1 0x0100u
+#define MTE_RP_BEFORE1 0x0200u
+#define MTE_RP_POS2 0x0400u
+#define MTE_RP_BEFORE2 0x0800u
 #define MTE_REF_SLIDE_ON_REMOVE 0x40u /* ReferenceType.SlideOnRemove             */
 #define MTE_REF_STAY_ON_REMOVE 0x80u  /* ReferenceType.StayOnRemove              */
 #define MTE_REF_TRANSIENT 0x100u      /* ReferenceType.Transient (unsupported)    */

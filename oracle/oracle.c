@@ -326,6 +326,41 @@ static int64_t doc_lengths_local(odoc* d) {
 static int doc_rollback(odoc* d, const mte_op* op, const apply_env* env);
 static int doc_regen(odoc* d, const mte_op* op);
 
+/* ---- relative positions (MTE_OP_RELPOS, include/mte.h) ------------------------
+ * posFromRelativePos (mergeTree.ts:1369-1392) for the record nx that follows:
+ * the marker idToSegment holds for the id -- the first marker segment whose
+ * key-`key` value is vid (ids unique per document, :490, 597-599) -- at
+ * getPosition (:853-870), the length of everything before it in nx's view
+ * (undefined leaves count 0), minus the offset (before) or plus 1 + offset;
+ * -1 when no held marker carries the id.  nx's pos1 / pos2 are replaced. */
+static int32_t marker_pos(odoc* d, const mte_op* nx, uint32_t key, uint32_t vid, uint32_t n_keys) {
+  if (key >= n_keys || vid == 0) return -1;
+  uint32_t x = d->n;
+  for (uint32_t i = 0; i < d->n && x == d->n; i++)
+    if (d->s[i].kind != 0 && d->s[i].props[key] == vid) x = i;
+  if (x == d->n) return -1;
+  if (nx->flags & MTE_F_LOCAL) doc_lengths_local(d);
+  else doc_lengths(d, nx->ref_seq, nx->client, d->min_seq, (d->flags & MTE_DOC_NEW_LENGTH_CALC) != 0);
+  return (int32_t)d->P[x];
+}
+
+static int doc_relpos(odoc* d, const mte_op* rp, mte_op* nx, uint32_t n_keys) {
+  int rc;
+  if ((rc = doc_scratch(d))) return rc;
+  if (rp->flags & MTE_RP_POS1) {
+    int32_t p = marker_pos(d, nx, rp->a, (uint32_t)rp->pos1, n_keys);
+    if (p >= 0) p = (rp->flags & MTE_RP_BEFORE1) ? p - rp->seq : p + 1 + rp->seq;
+    else if (nx->type == MTE_OP_INSERT) return MTE_E_UNSUPPORTED;
+    nx->pos1 = p;
+  }
+  if ((rp->flags & MTE_RP_POS2) && nx->type != MTE_OP_INSERT) {
+    int32_t p = marker_pos(d, nx, rp->a, (uint32_t)rp->pos2, n_keys);
+    if (p >= 0) p = (rp->flags & MTE_RP_BEFORE2) ? p - rp->ref_seq : p + 1 + rp->ref_seq;
+    nx->pos2 = p;
+  }
+  return MTE_OK;
+}
+
 /* ---- local references (MTE_DOC_REFS, include/mte.h) --------------------------
  * A reference is kept as the text unit it sits on (its arena offset: splits
  * never copy text, so the unit names the same place in whatever segment holds
@@ -1006,7 +1041,7 @@ static int round_sync_ok(odoc* d, const mte_op* ops, uint64_t k0, uint64_t k1) {
   int32_t ref = d->rs_ref, seq = d->rs_seq;
   for (uint64_t k = k0; k < k1; k++) {
     const mte_op* o = &ops[k];
-    if (o->type == MTE_OP_NOOP) continue;
+    if (o->type == MTE_OP_NOOP || o->type == MTE_OP_RELPOS) continue;
     if (o->ref_seq < ref) return 0;
     if (o->ref_seq > ref) {
       if (o->ref_seq < seq) return 0;
@@ -1033,9 +1068,17 @@ static void* worker(void* p) {
     d->dl_n = 0;
     for (uint64_t k = w->b->op_offsets[di]; k < w->b->op_offsets[di + 1]; k++) {
       const mte_op* op = &w->b->ops[k];
+      mte_op nx;
+      int rc = 0;
+      if (op->type == MTE_OP_RELPOS) {  /* the next record, at the resolved positions */
+        nx = op[1];
+        rc = doc_relpos(d, op, &nx, env.n_keys);
+        op = &nx;
+        k++;
+      }
       d->cur_op = (uint32_t)(k - w->b->op_offsets[di]);
-      env.aux = op + 1;
-      int rc = doc_apply(d, op, &env);
+      env.aux = &w->b->ops[k] + 1;
+      if (!rc) rc = doc_apply(d, op, &env);
       if (rc) {
         d->status = rc;
         break;
@@ -1061,7 +1104,14 @@ int orc_apply_batch(orc_ctx* c, const mte_batch* b, int n_threads) {
       if (op->pos2 < 0 || k + 1 + (uint64_t)op->pos2 > b->op_offsets[dcur + 1]) return MTE_E_INVALID_ARG;
       rbkey_end = k + 1 + (uint64_t)op->pos2;
     }
-    if (op->type > MTE_OP_REF) return MTE_E_INVALID_ARG;
+    if (op->type > MTE_OP_RELPOS) return MTE_E_INVALID_ARG;
+    if (op->type == MTE_OP_RELPOS) {
+      const uint32_t rp = MTE_RP_POS1 | MTE_RP_BEFORE1 | MTE_RP_POS2 | MTE_RP_BEFORE2;
+      if ((op->flags & ~rp) || !(op->flags & (MTE_RP_POS1 | MTE_RP_POS2)) || k + 1 >= b->op_offsets[dcur + 1] ||
+          op[1].type > MTE_OP_ANNOTATE)
+        return MTE_E_INVALID_ARG;
+      continue;
+    }
     if (op->type >= MTE_OP_ROLLBACK && !(op->flags & MTE_F_LOCAL)) return MTE_E_INVALID_ARG;
     if (op->type == MTE_OP_REF) {
       if (!(c->docs[dcur].flags & MTE_DOC_REFS) || op->seq != 0 || op->pos2 < 0 || op->b > 3 ||

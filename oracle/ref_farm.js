@@ -42,6 +42,14 @@
 //                                     "states": [{"text", "props": [[start, end, {..}]]}]}]}]}
 //          legacy: the clients keep the default (legacy) length calculation
 //         instead of mergeTreeUseNewLengthCalculations
+//          relpos: the chance that a local op addresses a marker by its id
+//         (IRelativePosition, ops.ts:62-76, resolved by posFromRelativePos,
+//         mergeTree.ts:1369-1392, from getValidOpRange, client.ts:541-560):
+//         Client.annotateMarker (client.ts:166-174, opBuilder.ts:26-40), or a
+//         remove / insert whose relativePos1 / relativePos2 name a marker the
+//         client sees, applied through the Client's own op path
+//         (applyRemoveRangeOp / applyInsertOp, client.ts:405-500); with relpos
+//         the marker ids are unique ("mk<n>")
 // Client 0 ("A") never sends: the observer.
 "use strict";
 const path = require("path");
@@ -127,6 +135,47 @@ function runSet(p) {
   let seq = 0;
   const checkpoints = [];
   const every = Math.max(1, Math.floor(p.steps / Math.max(1, p.nCheckpoints)));
+  let markerNo = 0;
+  // the id'd markers a client's own view holds
+  const idMarkers = (c) => {
+    const out = [];
+    const len = c.getLength();
+    for (let pos = 0; pos < len; pos++) {
+      const { segment } = c.getContainingSegment(pos);
+      if (segment && Marker.is(segment) && segment.getId()) out.push(segment);
+    }
+    return out;
+  };
+  const relPos = (id) => {
+    const rp = { id };
+    if (R.next() < 0.5) rp.before = true;
+    if (R.next() < 0.5) rp.offset = R.int(0, 3);
+    return rp;
+  };
+  // a local op through a relative position; undefined when the range is not
+  // valid in the client's view (getValidOpRange throws)
+  const relOp = (c, i) => {
+    const ms = idMarkers(c);
+    if (!ms.length) return undefined;
+    const m = ms[R.int(0, ms.length - 1)];
+    const pick = R.next();
+    try {
+      if (pick < 0.5) {
+        const props = { [KEYS[R.int(0, 2)]]: R.next() < 0.15 ? null : R.int(0, 5) };
+        return c.annotateMarker(m, props, undefined);
+      }
+      if (pick < 0.75) {
+        const op = { type: 1, relativePos1: relPos(m.getId()), relativePos2: relPos(m.getId()) };
+        if (R.next() < 0.5) op.relativePos1.before = true;
+        return c.applyRemoveRangeOp({ op }) ? op : undefined;
+      }
+      const op = { type: 0, relativePos1: relPos(m.getId()), seg: new TextSegment(names[i].toLowerCase()).toJSONObject() };
+      return c.applyInsertOp({ op }) ? op : undefined;
+    } catch (e) {
+      if (e && (e.message === "RangeOutOfBounds" || /RangeOutOfBounds/.test(String(e.message)))) return undefined;
+      throw e;
+    }
+  };
 
   const applyNext = (i) => {
     const m = log[cursor[i]];
@@ -195,10 +244,12 @@ function runSet(p) {
       const len = c.getLength();
       const pick = R.next();
       let op;
-      if (len < 4 || (pick < 0.4 && len < p.maxText)) {
+      if (p.relpos && len >= 4 && R.next() < p.relpos) {
+        op = relOp(c, i);
+      } else if (len < 4 || (pick < 0.4 && len < p.maxText)) {
         const pos = R.int(0, len);
-        if (R.next() < 0.08) {
-          const props = R.next() < 0.5 ? { markerId: `m${seq}` } : undefined;
+        if (R.next() < (p.relpos ? 0.2 : 0.08)) {
+          const props = R.next() < 0.5 ? { markerId: p.relpos ? `mk${markerNo++}` : `m${seq}` } : undefined;
           op = c.insertSegmentLocal(pos, Marker.make(1, props));
         } else {
           const text = names[i].repeat(R.int(1, 3));

@@ -227,6 +227,38 @@ static int64_t lengths_local(idoc* d) {
   return p;
 }
 
+/* ---- relative positions (MTE_OP_RELPOS, include/mte.h) ---------------------------
+ * posFromRelativePos (mergeTree.ts:1369-1392) for the record nx that follows:
+ * the first marker whose key-`key` value is vid (idToSegment, :490, 597-599),
+ * at getPosition (:853-870) -- the length before it in nx's view, undefined
+ * leaves 0 -- minus the offset (before) or plus 1 + offset; -1 when no held
+ * marker carries the id.  nx's pos1 / pos2 are replaced (as oracle.c). */
+static int32_t marker_pos(idoc* d, const mte_op* nx, uint32_t key, uint32_t vid, uint32_t n_keys) {
+  if (key >= n_keys || vid == 0) return -1;
+  uint32_t x = d->n;
+  for (uint32_t i = 0; i < d->n && x == d->n; i++)
+    if (!d->it[i].empty && d->it[i].kind != 0 && d->it[i].props[key] == vid) x = i;
+  if (x == d->n) return -1;
+  if (nx->flags & MTE_F_LOCAL) lengths_local(d);
+  else lengths(d, nx->ref_seq, nx->client, d->min_seq, (d->flags & MTE_DOC_NEW_LENGTH_CALC) != 0);
+  return (int32_t)d->P[x];
+}
+
+static int doc_relpos(idoc* d, const mte_op* rp, mte_op* nx, uint32_t n_keys) {
+  if (rp->flags & MTE_RP_POS1) {
+    int32_t p = marker_pos(d, nx, rp->a, (uint32_t)rp->pos1, n_keys);
+    if (p >= 0) p = (rp->flags & MTE_RP_BEFORE1) ? p - rp->seq : p + 1 + rp->seq;
+    else if (nx->type == MTE_OP_INSERT) return MTE_E_UNSUPPORTED;
+    nx->pos1 = p;
+  }
+  if ((rp->flags & MTE_RP_POS2) && nx->type != MTE_OP_INSERT) {
+    int32_t p = marker_pos(d, nx, rp->a, (uint32_t)rp->pos2, n_keys);
+    if (p >= 0) p = (rp->flags & MTE_RP_BEFORE2) ? p - rp->ref_seq : p + 1 + rp->ref_seq;
+    nx->pos2 = p;
+  }
+  return MTE_OK;
+}
+
 /* ---- block spans ------------------------------------------------------------------ */
 
 static uint32_t span_start(const idoc* d, uint32_t i, int k) {
@@ -1067,12 +1099,20 @@ static int doc_regen(idoc* d, const mte_op* op) {
   int64_t p = 0;
   int64_t last = -2;
   for (uint32_t i = 0; i < d->n; i++) {
-    const item* g = &d->it[i];
+    item* g = &d->it[i];
     int hit;
     if (g->empty) hit = 0;
     else if (t == MTE_OP_INSERT) hit = g->seq == LOCAL_BASE + ls;
     else if (t == MTE_OP_REMOVE) hit = g->rseq == LOCAL_BASE + ls;
     else hit = ((g->am >> op->a) & 1u) && (g->rseq == NONE_SEQ || is_pending(g->rseq));
+    /* a member that re-sends nothing leaves the group (resetPendingDeltaToOps
+     * dequeues every segment and enqueues only those with a new op,
+     * client.ts:803-852): a removal a remote remove overtook, an annotated
+     * segment removed since -- the zamboni no longer holds it for the group */
+    if (!g->empty && !hit) {
+      if (t == MTE_OP_REMOVE && g->lrs == ls) g->lrs = 0;
+      if (t == MTE_OP_ANNOTATE) g->am &= ~(1u << op->a);
+    }
     if (hit) {
       if (g->cont && last == (int64_t)i - 1 && d->dl_n) d->dl[d->dl_n - 1].len += g->len;
       else if ((rc = delta_push(d, MTE_DELTA_REGEN | t, p, g->len, t == MTE_OP_INSERT ? g->toff : 0u))) return rc;
@@ -1346,9 +1386,18 @@ static void* worker(void* p) {
     d->dl_n = 0;
     for (uint64_t k = w->b->op_offsets[di]; k < w->b->op_offsets[di + 1]; k++) {
       const mte_op* op = &w->b->ops[k];
+      mte_op nx;
+      int rc = 0;
+      if (op->type == MTE_OP_RELPOS) {  /* the next record, at the resolved positions */
+        if (d->n + 4 > env.limit) rc = MTE_E_CAPACITY;
+        nx = op[1];
+        if (!rc) rc = doc_relpos(d, op, &nx, env.n_keys);
+        op = &nx;
+        k++;
+      }
       d->cur_op = (uint32_t)(k - w->b->op_offsets[di]);
-      env.aux = op + 1;
-      int rc = doc_apply(d, op, &env);
+      env.aux = &w->b->ops[k] + 1;
+      if (!rc) rc = doc_apply(d, op, &env);
       if (rc) {
         d->status = rc;
         break;
@@ -1374,7 +1423,14 @@ int oti_apply_batch(oti_ctx* c, const mte_batch* b, int n_threads) {
       if (op->pos2 < 0 || k + 1 + (uint64_t)op->pos2 > b->op_offsets[dcur + 1]) return MTE_E_INVALID_ARG;
       rbkey_end = k + 1 + (uint64_t)op->pos2;
     }
-    if (op->type > MTE_OP_REF) return MTE_E_INVALID_ARG;
+    if (op->type > MTE_OP_RELPOS) return MTE_E_INVALID_ARG;
+    if (op->type == MTE_OP_RELPOS) {
+      const uint32_t rp = MTE_RP_POS1 | MTE_RP_BEFORE1 | MTE_RP_POS2 | MTE_RP_BEFORE2;
+      if ((op->flags & ~rp) || !(op->flags & (MTE_RP_POS1 | MTE_RP_POS2)) || k + 1 >= b->op_offsets[dcur + 1] ||
+          op[1].type > MTE_OP_ANNOTATE)
+        return MTE_E_INVALID_ARG;
+      continue;
+    }
     if (op->type >= MTE_OP_ROLLBACK && !(op->flags & MTE_F_LOCAL)) return MTE_E_INVALID_ARG;
     if (op->type == MTE_OP_REF) {
       if (!(c->docs[dcur].flags & MTE_DOC_REFS) || op->seq != 0 || op->pos2 < 0 || op->b > 3 ||

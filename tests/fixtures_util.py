@@ -233,7 +233,7 @@ def canon_regen(op, orig, merge=True):
     return json.dumps(out, sort_keys=True)
 
 
-def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_regen=False):
+def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_regen=False, observers_only=False):
     """Replay farms the reference ran (oracle/ref_farm.js -> tests/golden/
     farm_vectors.json.gz): one MTE_DOC_LOCAL_CLIENT document per client of every
     set (the observer "A" included), each fed its own events in order — "L" a
@@ -249,16 +249,19 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_reg
     client's at every checkpoint.  regen_checks (a list) collects one entry per "G" event compared;
     exact_regen compares the regenerated ops one for one (the tree keeps the
     reference's segment groups), else in merged form (canon_regen).
+    observers_only: only each set's observer "A" (it never sends), as a
+    document of remote clients alone (no MTE_DOC_LOCAL_CLIENT: the flat passes
+    with the new length calculation, the tree passes with the legacy one).
     Returns (checkpoints_passed, failures)."""
     from fluidframework_amd.abi import DOC_EVENTS, DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC, DOC_REFS
     from fluidframework_amd.packing import regen_ops
 
-    layout = [(si, ci) for si, s in enumerate(sets) for ci in range(len(s["names"]))]
-    has_regen = any(e[0] == "G" for s in sets for ev in s["events"] for e in ev)
-    has_refs = any(s.get("refs") for s in sets)
+    layout = [(si, ci) for si, s in enumerate(sets) for ci in range(1 if observers_only else len(s["names"]))]
+    has_regen = not observers_only and any(e[0] == "G" for s in sets for ev in s["events"] for e in ev)
+    has_refs = not observers_only and any(s.get("refs") for s in sets)
     inits, text = doc_inits([sets[si]["initialText"] for si, _ in layout],
-                            flags=DOC_NEW_LENGTH_CALC | DOC_LOCAL_CLIENT | (DOC_EVENTS if has_regen else 0) |
-                            (DOC_REFS if has_refs else 0))
+                            flags=DOC_NEW_LENGTH_CALC | (0 if observers_only else DOC_LOCAL_CLIENT) |
+                            (DOC_EVENTS if has_regen else 0) | (DOC_REFS if has_refs else 0))
     for d, (si, _) in enumerate(layout):  # sets the reference ran with the legacy length calculation
         if sets[si].get("legacy"):
             inits[d]["flags"] = int(inits[d]["flags"]) & ~DOC_NEW_LENGTH_CALC & 0xffffffff
@@ -269,7 +272,7 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_reg
     eng.load_docs(inits, text)
     held = [[] for _ in layout]
     ref_slots = [[] for _ in layout]  # the farm's reference index -> engine slot
-    clients = [DocClients(sets[si]["names"][ci], local=True) for si, ci in layout]
+    clients = [DocClients(sets[si]["names"][ci], local=not observers_only) for si, ci in layout]
     n_cp = max(len(s["checkpoints"]) for s in sets)
     prev = [0] * len(layout)
     passed, failures = 0, []

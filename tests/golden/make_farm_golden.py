@@ -21,7 +21,13 @@ positions of its own view and removes some (Client.createLocalReferencePosition
 / removeLocalReferencePosition, SlideOnRemove or Simple), each checkpoint
 holding every reference's localReferencePositionToPosition.
 
-Usage: python3 tests/golden/make_farm_golden.py [--refs | --legacy]
+With --relpos it writes tests/golden/relpos_farm_vectors.json.gz: farms in
+which local ops also address id'd markers through relative positions
+(Client.annotateMarker, and removes / inserts whose relativePos1 / relativePos2
+name a marker), in both length calculations, with lagging clients, rollbacks
+and reconnects among the sets.
+
+Usage: python3 tests/golden/make_farm_golden.py [--refs | --legacy | --relpos]
 """
 import gzip
 import json
@@ -38,6 +44,7 @@ import ref_util  # noqa: E402
 OUT = os.path.join(HERE, "farm_vectors.json.gz")
 OUT_REFS = os.path.join(HERE, "localref_vectors.json.gz")
 OUT_LEGACY = os.path.join(HERE, "legacy_farm_vectors.json.gz")
+OUT_RELPOS = os.path.join(HERE, "relpos_farm_vectors.json.gz")
 FARM_JS = os.path.join(ROOT, "oracle", "ref_farm.js")
 
 # (seed, clients incl. the observer, steps, initial text, checkpoints, text bound)
@@ -76,6 +83,37 @@ LEGACY_SETS = ([(8000 + i, 2 + i % 7, 300 + 150 * (i % 6), ["", "hello world", "
                 for i in range(10)] +
                [(8300 + i, 2 + i % 5, 300 + 100 * (i % 3), ["", "hello world"][i % 2], 5, 200, {"refs": 0.2})
                 for i in range(8)])
+
+
+# relative positions: (seed, clients, steps, initial text, checkpoints, text
+# bound, extra parameters); the legacy sets may diverge (as LEGACY_SETS)
+RELPOS_SETS = ([(9000 + i, 2 + i % 6, 300 + 100 * (i % 4), ["", "hello world", "abc\ndef"][i % 3], 4,
+                 [64, 200][i % 2], {"relpos": [0.2, 0.35][i % 2]}) for i in range(16)] +
+               [(9100 + i, 3 + i % 4, 400, "hello world", 4, 200,
+                 {"relpos": 0.3, "rollback": 0.15, "rollbackTypes": [1, 2]}) for i in range(8)] +
+               [(9200 + i, 3 + i % 4, 400, "hello world", 5, 200, {"relpos": 0.3, "reconnect": 0.1, "allowDiverge": True})
+                for i in range(8)] +
+               [(9300 + i, 2 + i % 6, 300 + 100 * (i % 4), ["", "hello world"][i % 2], 4, 200,
+                 {"relpos": 0.3, "legacy": True, "allowDiverge": True}) for i in range(12)])
+
+
+def main_relpos(out):
+    res = {"sets": [], "generator": "oracle/ref_farm.js with relpos (reference Client, mulberry32 seeds)"}
+    failed = []
+    for sd, c, n, t, k, m, extra in RELPOS_SETS:
+        one = dict({"seed": sd, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m},
+                   **extra)
+        q = subprocess.run(["node", FARM_JS, out], input=json.dumps({"sets": [one]}), capture_output=True, text=True,
+                           timeout=600)
+        if q.returncode == 0:
+            res["sets"] += json.loads(q.stdout)["sets"]
+        else:
+            failed.append(sd)
+    res["seeds_the_reference_failed"] = failed
+    with gzip.open(OUT_RELPOS, "wt", encoding="utf-8") as fh:
+        json.dump(res, fh, separators=(",", ":"))
+    n_rel = sum(1 for s in res["sets"] for e in s["log"] if "relativePos1" in e[5])
+    print(f"wrote {OUT_RELPOS}: {len(res['sets'])} farms, {n_rel} relative-position ops, reference failed on {failed}")
 
 
 def main_legacy(out):
@@ -128,6 +166,8 @@ def main():
         return main_refs(out)
     if "--legacy" in sys.argv[1:]:
         return main_legacy(out)
+    if "--relpos" in sys.argv[1:]:
+        return main_relpos(out)
     inp = {"sets": [{"seed": s, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
                      "rollback": rb} for s, c, n, t, k, m, rb in SETS]}
     p = subprocess.run(["node", "--max-old-space-size=8192", FARM_JS, out], input=json.dumps(inp),

@@ -70,6 +70,6 @@ def test_packer_rejects_ref_below_min_seq_and_takes_no_slot_on_error():
     # a message that fails validation leaves DocClients untouched
     with pytest.raises(MergeTreeError) as e:
         bb.add_message(0, c, dict(clientId="d", sequenceNumber=2, referenceSequenceNumber=1,
-                                  minimumSequenceNumber=1, contents={"type": 0, "relativePos1": {"id": "m"}}))
+                                  minimumSequenceNumber=1, contents={"type": 1, "pos1": 0}))
     assert e.value.code == MTE_E_UNSUPPORTED
     assert set(c.ids) == {"A", "b"}
