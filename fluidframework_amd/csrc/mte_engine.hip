@@ -515,6 +515,15 @@ struct mte_ctx {
   // round phases of the chunked pass (mte_round.h); MTE_ROUND_PHASES=0 turns them off
   RoundArgs rd{};
   bool round_phases = true;
+  uint32_t htree_lds = 40u << 10;  // LDS bytes a document of the HBM tree pass may hold (MTE_HTREE_LDS)
+  std::vector<uint32_t> h_htree_docs, h_hord;
+  uint32_t* d_hord_s[2] = {nullptr, nullptr};  // per batch slot: the candidates, most records first
+  uint64_t hord_cap_s[2] = {0, 0};
+  bool hord_ok_s[2] = {false, false};  // the slot's order is of the loaded documents
+  // MTE_HTREE_PROF=<file>: the HBM tree pass's phase clocks (a `make prof`
+  // build) appended to <file> at each mte_stats_get
+  const char* hprof_path = nullptr;
+  unsigned long long* d_hprof = nullptr;
   uint32_t* h_rcount = nullptr;  // pinned: the plan's counts
   uint64_t rl_alloc = 0;         // rd.rlist entries allocated
   // The round phases' host loop (launch_replay) reads each phase's counts back
@@ -635,6 +644,8 @@ void free_docs(mte_ctx* c) {
   c->d_hscr = nullptr;
   c->d_htree_docs = nullptr;
   c->n_htree = 0;
+  c->h_htree_docs.clear();
+  c->hord_ok_s[0] = c->hord_ok_s[1] = false;
   c->hdr = nullptr;
   c->soa = SegSoA{};
   c->stats = nullptr;
@@ -737,8 +748,17 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
                                    per ? per : 1u)));
     }
     if (c->n_htree) {
-      HtreeArgs ht{c->d_tree, c->d_heap, c->d_hheap, c->hcap, c->d_hst, c->d_hscr, c->d_htree_docs, c->n_htree,
-                   c->arena};
+      // LDS residency: (nP + 5) words per item (mte_htree.h ht_to_lds), whole wavefronts' worth
+      const uint32_t words = (uint32_t)(kFieldPlanes + 3 * K + 2 + 5);
+      uint32_t lcap = c->htree_lds >= 8 ? (c->htree_lds / 4 - 2) / words / kWave * kWave : 0u;
+      if (lcap > c->cap) lcap = c->cap / kWave * kWave;
+      const uint32_t* order = c->hord_ok_s[c->rslot] ? c->d_hord_s[c->rslot] : c->d_htree_docs;
+      if (c->hprof_path && !c->d_hprof) {
+        HIPCHK(c, hipMalloc((void**)&c->d_hprof, kHtProf * 8));
+        HIPCHK(c, hipMemsetAsync(c->d_hprof, 0, kHtProf * 8, c->tree_stream));
+      }
+      HtreeArgs ht{c->d_tree, c->d_heap, c->d_hheap, c->hcap, lcap, c->d_hst, c->d_hscr, order, c->n_htree,
+                   c->arena, c->d_hprof};
       HIPCHK(c, (launch_htree<K, S>(a, ht, c->tree_stream)));
     }
     HIPCHK(c, hipEventRecord(c->ev_join, c->tree_stream));
@@ -974,6 +994,8 @@ int mte_create(const mte_config* cfg, mte_ctx** out) {
   c->wclock_path = std::getenv("MTE_WAVE_CLOCK");
   if (const char* pp = std::getenv("MTE_PACK_PROPS")) c->pack_props = std::atoi(pp) != 0;
   if (const char* rp = std::getenv("MTE_ROUND_PHASES")) c->round_phases = std::atoi(rp) != 0;
+  c->hprof_path = std::getenv("MTE_HTREE_PROF");
+  if (const char* hl = std::getenv("MTE_HTREE_LDS")) c->htree_lds = (uint32_t)std::min(160l << 10, std::max(0l, std::atol(hl)));
   if (const char* r = std::getenv("MTE_TREE_ROUNDS")) {
     const int v = std::atoi(r);
     c->tree_rounds = v < 0 ? 0 : (v > 64 ? 64 : v);
@@ -1006,12 +1028,12 @@ int mte_destroy(mte_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   free_docs(c);
-  void* ps[] = {c->arena, c->d_pow, c->d_gdone};
+  void* ps[] = {c->arena, c->d_pow, c->d_gdone, c->d_hprof};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int w = 0; w < 2; w++) {
     void* sl[] = {c->d_ops_s[w], c->d_cps_s[w], c->d_off_s[w], c->d_ps_s[w], c->d_pe_s[w],
-                  c->d_dl_off_s[w], c->d_dl_s[w], c->d_dl_n_s[w], c->d_sorder_s[w], c->d_rel_s[w]};
+                  c->d_dl_off_s[w], c->d_dl_s[w], c->d_dl_n_s[w], c->d_sorder_s[w], c->d_rel_s[w], c->d_hord_s[w]};
     for (void* p : sl)
       if (p) (void)hipFree(p);
     if (c->slot_ev[w]) (void)hipEventDestroy(c->slot_ev[w]);
@@ -1218,6 +1240,7 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
       HIPCHK(c, hipMalloc((void**)&c->d_hheap, sizeof(uint2) * ((size_t)c->hcap + 1) * n_docs));
       HIPCHK(c, hipMalloc((void**)&c->d_hst, sizeof(uint32_t) * kHtState * (size_t)n_docs));
       HIPCHK(c, hipMalloc((void**)&c->d_hscr, sizeof(int32_t) * 2 * nslots));
+      c->h_htree_docs = htree_docs;
       HIPCHK(c, hipMalloc((void**)&c->d_htree_docs, htree_docs.size() * 4));
       HIPCHK(c, hipMemcpy(c->d_htree_docs, htree_docs.data(), htree_docs.size() * 4, hipMemcpyHostToDevice));
     }
@@ -1403,6 +1426,17 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
                              c->up_stream));
     HIPCHK(c, hipStreamSynchronize(c->up_stream));  // `order` goes out of scope
   }
+  if (!c->h_htree_docs.empty()) {
+    // the HBM tree pass's documents, most records first (the long chains start first)
+    std::vector<uint32_t>& ho = c->h_hord;
+    ho = c->h_htree_docs;
+    std::stable_sort(ho.begin(), ho.end(), [&](uint32_t x, uint32_t y) {
+      return b->op_offsets[x + 1] - b->op_offsets[x] > b->op_offsets[y + 1] - b->op_offsets[y];
+    });
+    if ((rc = grow(c, &c->d_hord_s[w], &c->hord_cap_s[w], (uint64_t)ho.size()))) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->d_hord_s[w], ho.data(), ho.size() * 4, hipMemcpyHostToDevice, c->up_stream));
+  }
+  c->hord_ok_s[w] = !c->h_htree_docs.empty();
   if (!c->h_rel_s[w].empty()) {
     if ((rc = grow(c, &c->d_rel_s[w], &c->rel_cap_s[w], (uint64_t)c->h_rel_s[w].size()))) return rc;
     HIPCHK(c, hipMemcpyAsync(c->d_rel_s[w], c->h_rel_s[w].data(), c->h_rel_s[w].size() * 4, hipMemcpyHostToDevice,
@@ -1748,6 +1782,43 @@ int mte_read_refs(mte_ctx* c, uint32_t doc, int32_t* pos, uint32_t n) {
   return MTE_OK;
 }
 
+int mte_read_ref_order(mte_ctx* c, uint32_t doc, int64_t* key, uint32_t n) {
+  if (!c || (n && !key) || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  JOIN_TAIL(c);
+  if (c->h_refs.empty() || !c->h_refs[doc]) return set_err(c, MTE_E_INVALID_ARG, "doc %u: no MTE_DOC_REFS", doc);
+  if (n > c->ref_cap) return set_err(c, MTE_E_INVALID_ARG, "%u reference slots > capacity %u", n, c->ref_cap);
+  HIPCHK(c, hipSetDevice(c->device));
+  DocHdr h;
+  HIPCHK(c, hipMemcpyAsync(&h, c->hdr + doc, sizeof(DocHdr), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint32_t ns = (uint32_t)std::max(h.nseg, 0);
+  const uint64_t db = (uint64_t)doc * c->cap;
+  std::vector<int32_t> len(ns + 1);
+  std::vector<uint32_t> toff(ns + 1);
+  std::vector<uint2> rt(n + 1);
+  if (ns) {
+    HIPCHK(c, hipMemcpyAsync(len.data(), c->soa.len + db, ns * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(toff.data(), c->soa.toff + db, ns * 4, hipMemcpyDeviceToHost, c->stream));
+  }
+  if (n)
+    HIPCHK(c, hipMemcpyAsync(rt.data(), c->d_refs + (uint64_t)doc * c->ref_cap, n * sizeof(uint2),
+                             hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (uint32_t r = 0; r < n; r++) {
+    key[r] = -1;
+    if (!(rt[r].y & kRefLive) || (rt[r].y & kRefDetached)) continue;
+    int64_t p = 0;
+    for (uint32_t i = 0; i < ns; i++) {
+      if (rt[r].x - toff[i] < (uint32_t)len[i]) {
+        key[r] = p + (int64_t)(rt[r].x - toff[i]);
+        break;
+      }
+      p += len[i];
+    }
+  }
+  return MTE_OK;
+}
+
 int mte_read_deltas(mte_ctx* c, uint32_t doc, mte_delta* out, uint64_t cap, uint64_t* n) {
   if (!c || !n || doc >= c->n_docs) return MTE_E_INVALID_ARG;
   JOIN_TAIL(c);
@@ -1973,6 +2044,17 @@ int mte_stats_get(mte_ctx* c, mte_stats* o) {
   if (c->ran) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) o->kernel_ms = ms;
+  }
+  if (c->d_hprof) {  // MTE_HTREE_PROF: one line of phase clocks, then zeroed
+    unsigned long long hp[kHtProf];
+    HIPCHK(c, hipMemcpyAsync(hp, c->d_hprof, sizeof(hp), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_hprof, 0, sizeof(hp), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (FILE* f = std::fopen(c->hprof_path, "a")) {
+      for (int q = 0; q < kHtProf; q++) std::fprintf(f, q ? " %llu" : "%llu", hp[q]);
+      std::fprintf(f, "\n");
+      std::fclose(f);
+    }
   }
   // ops of the chunked pass count the slots and summary
   // entries they scanned instead of the document's S_live

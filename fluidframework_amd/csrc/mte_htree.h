@@ -42,16 +42,32 @@ constexpr int kHtState = 8;            // state words per document
 // state words (HtreeArgs::st)
 enum HtSt { kHsDepth = 0, kHsNextId, kHsHeapN, kHsLseq, kHsRhi, kHsEntered };
 
+// MTE_HTREE_PROF (a profiling build only, `make prof`): per-phase clocks
+// (s_memrealtime ticks, 100 MHz) summed over every document into
+// HtreeArgs::prof: 0 insert, 1 remove / annotate, 2 ack, 3 zamboni (inside the
+// others too), 4 rollback / regen, 5 references / relative positions, 6 every
+// record, 7 records.
+constexpr int kHtProf = 8;
+#ifdef MTE_HTREE_PROF
+#define HPROF_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime();
+#define HPROF_END(h, i, v) (h).prof[i] += __builtin_amdgcn_s_memrealtime() - (v);
+#else
+#define HPROF_BEGIN(v)
+#define HPROF_END(h, i, v)
+#endif
+
 struct HtreeArgs {
   uint32_t* tree;        // tree words: tree[doc * cap + i]
   const uint2* rheap;    // the register tiers' heaps (kTreeHeapCap + 1 per doc): an escalating doc's
   uint2* heap;           // HBM tree heaps: heap[doc * (hcap + 1) + k], k = 1 .. hn
   uint32_t hcap;
+  uint32_t lcap;         // items a document may hold in LDS (0: none; the launch's dynamic LDS)
   uint32_t* st;          // kHtState words per document
   int32_t* scr;          // L at scr[doc * 2 cap + i], P at scr[doc * 2 cap + cap + i]
   const uint32_t* docs;  // the documents this pass may replay
   uint32_t n_docs;
   const uint16_t* arena;
+  unsigned long long* prof;  // kHtProf phase clocks (MTE_HTREE_PROF builds), or nullptr
 };
 
 // plane indices of a local-client document (after the K property planes)
@@ -83,6 +99,21 @@ struct HT {
   // MTE_OP_RELPOS: positions for the next record (rpf: MTE_RP_POS1 / POS2 given)
   uint32_t rpf;
   int32_t rp1, rp2;
+  // LDS residency: the document's planes, tree words, L / P and heap in the
+  // workgroup's LDS while they fit (every access goes through the pointers
+  // above); its HBM home below
+  bool lds;
+  uint32_t* g_pl;
+  uint64_t g_sd;
+  uint32_t* g_tw;
+  int32_t* g_L;
+  int32_t* g_P;
+  uint32_t* g_hp;
+  uint32_t g_hcap;
+  int g_cap;
+#ifdef MTE_HTREE_PROF
+  unsigned long long prof[kHtProf];
+#endif
 };
 
 // ---- single-item access (wave-uniform) ----------------------------------------
@@ -638,7 +669,16 @@ __device__ int ht_pack_parent(HT& h, int s, int p, uint32_t n_keys, int& status)
 
 // zamboniSegments (titems.c zamboni): at most two scours
 template <int K>
+__device__ int ht_zamboni_body(HT& h, uint32_t n_keys);
+template <int K>
 __device__ int ht_zamboni(HT& h, uint32_t n_keys) {
+  HPROF_BEGIN(t0)
+  const int rc = ht_zamboni_body<K>(h, n_keys);
+  HPROF_END(h, 3, t0)
+  return rc;
+}
+template <int K>
+__device__ int ht_zamboni_body(HT& h, uint32_t n_keys) {
   int status = 0;
   for (int z = 0; z < 2; z++) {
     if (h.hn == 0) break;
@@ -1311,6 +1351,77 @@ __device__ void ht_regen(const HT& h, int32_t ls, uint32_t t, uint32_t slot, EvO
   vm_drain();
 }
 
+// ---- LDS residency -------------------------------------------------------------------------
+// A document's state is moved whole: rows [0, n) of its nP planes and tree
+// words, and heap entries 1 .. hn.  L / P are scratch (recomputed lazily).
+// Items a record may add at most (splits, a new leaf, placeholders): the
+// document leaves LDS before a record that could pass its LDS capacity.
+constexpr int kLdsMargin = 16;
+
+__device__ void ht_move(uint32_t* dpl, uint64_t dsd, uint32_t* dtw, uint32_t* dhp, const uint32_t* spl, uint64_t ssd,
+                        const uint32_t* stw, const uint32_t* shp, int nP, int n, uint32_t hn) {
+  const int l = lane_id();
+  for (int p = 0; p <= nP; p++) {
+    const uint32_t* sp = p < nP ? spl + (uint64_t)p * ssd : stw;
+    uint32_t* dp = p < nP ? dpl + (uint64_t)p * dsd : dtw;
+    for (int i = l; i < n; i += kWave) dp[i] = ld_l2(sp + i);
+  }
+  for (uint32_t k = 1 + (uint32_t)l; k <= hn; k += kWave) {
+    dhp[2 * k] = ld_l2(shp + 2 * k);
+    dhp[2 * k + 1] = ld_l2(shp + 2 * k + 1);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
+// into the workgroup's LDS (lds: (nP + 5) x lcap + 2 words)
+__device__ void ht_to_lds(HT& h, uint32_t* lds, uint32_t lcap) {
+  h.g_pl = h.pl;
+  h.g_sd = h.sd;
+  h.g_tw = h.tw;
+  h.g_L = h.L;
+  h.g_P = h.P;
+  h.g_hp = h.hp;
+  h.g_hcap = h.hcap;
+  h.g_cap = h.cap;
+  uint32_t* pl = lds;
+  uint32_t* tw = pl + (uint64_t)h.nP * lcap;
+  int32_t* L = reinterpret_cast<int32_t*>(tw + lcap);
+  int32_t* P = L + lcap;
+  uint32_t* hp = reinterpret_cast<uint32_t*>(P + lcap);
+  ht_move(pl, lcap, tw, hp, h.pl, h.sd, h.tw, h.hp, h.nP, h.n, h.hn);
+  h.pl = pl;
+  h.sd = lcap;
+  h.tw = tw;
+  h.L = L;
+  h.P = P;
+  h.hp = hp;
+  h.hcap = lcap;
+  h.cap = (int)lcap;
+  h.lds = true;
+  h.lp_n = 0;
+  h.lp_carry = 0;
+}
+
+// back to HBM (before a record that could outgrow LDS, and at the end)
+__device__ void ht_spill(HT& h) {
+  ht_move(h.g_pl, h.g_sd, h.g_tw, h.g_hp, h.pl, h.sd, h.tw, h.hp, h.nP, h.n, h.hn);
+  h.pl = h.g_pl;
+  h.sd = h.g_sd;
+  h.tw = h.g_tw;
+  h.L = h.g_L;
+  h.P = h.g_P;
+  h.hp = h.g_hp;
+  h.hcap = h.g_hcap;
+  h.cap = h.g_cap;
+  h.lds = false;
+  h.lp_n = 0;
+  h.lp_carry = 0;
+}
+
+__device__ __forceinline__ bool ht_lds_room(const HT& h) {
+  return h.n + kLdsMargin <= h.cap && (int)h.hn + h.n + kLdsMargin <= (int)h.hcap;
+}
+
 // ---- one record (titems.c doc_apply / doc_apply_local) ----------------------------------
 
 // MTE_OP_RELPOS (include/mte.h): the position of the first marker whose key
@@ -1360,6 +1471,7 @@ __device__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStats], const Replay
     // the next record's positions, in its view (the engine checked that an
     // insert, remove or annotate of this document follows)
     if (D.k + 1 >= D.k1) return MTE_E_INVALID_ARG;
+    HPROF_BEGIN(t0)
     const s8v nx = sload8(rec + 2);
     const uint32_t nw3 = (uint32_t)nx[3];
     const uint32_t nt = nw3 & 0xffu, nc = (nw3 >> 8) & 0xffu;
@@ -1380,6 +1492,7 @@ __device__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStats], const Replay
       h.rp2 = p;
       h.rpf |= MTE_RP_POS2;
     }
+    HPROF_END(h, 5, t0)
     D.k++;
     return 0;
   }
@@ -1389,7 +1502,10 @@ __device__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStats], const Replay
     if ((uint32_t)op[7] == 2u && c == 0) return MTE_E_INVALID_ARG;
     MTE_STAT(st[kStOps]++;)
     MTE_STAT(if ((uint32_t)op[7] != 1u) st[kStScanned] += (uint32_t)h.n;)
-    if ((rc = stream_ref<K>(h.pl, h.sd, h.n, rt, rhi, op, D.min_seq, h.newcalc))) return rc;
+    HPROF_BEGIN(t0)
+    rc = stream_ref<K>(h.pl, h.sd, h.n, rt, rhi, op, D.min_seq, h.newcalc);
+    HPROF_END(h, 5, t0)
+    if (rc) return rc;
     D.k++;
     return 0;
   }
@@ -1404,12 +1520,18 @@ __device__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStats], const Replay
     if (t == MTE_OP_ANNOTATE) {
       const uint32_t n_aux = (uint32_t)op[5];
       if ((uint64_t)D.k + 1 + n_aux > D.k1 || (uint32_t)op[6] >= MTE_ANNOTATE_SLOTS) return MTE_E_INVALID_ARG;
-      if ((rc = ht_rollback_annotate<K>(h, (uint32_t)op[6], rec + 2, n_aux, a, evd, ev))) return rc;
+      HPROF_BEGIN(t0)
+      rc = ht_rollback_annotate<K>(h, (uint32_t)op[6], rec + 2, n_aux, a, evd, ev);
+      HPROF_END(h, 4, t0)
+      if (rc) return rc;
       D.k += 1 + n_aux;
       return 0;
     }
     if (t != MTE_OP_INSERT && t != MTE_OP_REMOVE) return MTE_E_INVALID_ARG;
-    if ((rc = ht_rollback<K>(h, op, a, evd, ev))) return rc;
+    HPROF_BEGIN(t0)
+    rc = ht_rollback<K>(h, op, a, evd, ev);
+    HPROF_END(h, 4, t0)
+    if (rc) return rc;
     D.k++;
     return 0;
   }
@@ -1419,7 +1541,9 @@ __device__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStats], const Replay
     if (t != MTE_OP_INSERT && t != MTE_OP_REMOVE && t != MTE_OP_ANNOTATE) return MTE_E_INVALID_ARG;
     if (t == MTE_OP_ANNOTATE && (uint32_t)op[6] >= MTE_ANNOTATE_SLOTS) return MTE_E_INVALID_ARG;
     if (!evd) return MTE_E_UNSUPPORTED;
+    HPROF_BEGIN(t0)
     ht_regen<K>(h, s, (uint32_t)t, (uint32_t)op[6], ev);
+    HPROF_END(h, 4, t0)
     D.k++;
     return 0;
   }
@@ -1434,16 +1558,25 @@ __device__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStats], const Replay
   }
   if (type == MTE_OP_INSERT) {
     int at = -1;
-    if ((rc = ht_insert<K, S>(h, op, lop, refd, a, st, at))) return rc;
+    HPROF_BEGIN(t0)
+    rc = ht_insert<K, S>(h, op, lop, refd, a, st, at);
+    HPROF_END(h, 0, t0)
+    if (rc) return rc;
     if (evd) {  // insertSegments' delta callback (mergeTree.ts:1409-1416)
       if (at >= 0) ev_one(ev, MTE_OP_INSERT, own_prefix(h.pl, h.sd, at), (flags & MTE_F_MARKER) ? 1 : op[5]);
       else ev_one(ev, MTE_OP_INSERT, -1, 0);  // a zero-length segment is never linked
     }
   } else if (type == MTE_OP_REMOVE || type == MTE_OP_ANNOTATE) {
-    if ((rc = ht_range<K, S>(h, op, lop, a, st, ev, evd, rt, rhi))) return rc;
+    HPROF_BEGIN(t0)
+    rc = ht_range<K, S>(h, op, lop, a, st, ev, evd, rt, rhi);
+    HPROF_END(h, 1, t0)
+    if (rc) return rc;
   } else if (type == MTE_OP_ACK) {
     if (!(op[4] > 0 && op[4] <= op[5] && op[5] <= lseq)) return MTE_E_INVALID_ARG;
-    if ((rc = ht_ack<K>(h, op, a, rt, refd ? rhi : 0u))) return rc;
+    HPROF_BEGIN(t0)
+    rc = ht_ack<K>(h, op, a, rt, refd ? rhi : 0u);
+    HPROF_END(h, 2, t0)
+    if (rc) return rc;
   } else if (type != MTE_OP_NOOP) {
     return MTE_E_INVALID_ARG;
   }
@@ -1507,6 +1640,10 @@ __global__ __launch_bounds__(64) void htree_kernel(ReplayArgs a, HtreeArgs t) {
   h.pr = 0;
   h.pc = 0;
   h.rpf = 0;
+  h.lds = false;
+#ifdef MTE_HTREE_PROF
+  for (int q = 0; q < kHtProf; q++) h.prof[q] = 0;
+#endif
   if (!ldoc && uld(stp + kHsEntered) == 0u) {
     // a legacy document leaves the register tiers: its depth / next id / heap
     // (DocHdr pad0 / pad1, TreeArgs::heap) move to the HBM tree's state
@@ -1536,8 +1673,18 @@ __global__ __launch_bounds__(64) void htree_kernel(ReplayArgs a, HtreeArgs t) {
     ev.cap = a.dl_off[doc + 1] - a.dl_off[doc];
   }
   D.running = D.status == 0 && D.k < D.k1;
+  extern __shared__ uint32_t ht_lds[];
+  // LDS-resident while the document fits (ht_lds_room's margins)
+  if (D.running && t.lcap && h.n + kLdsMargin <= (int)t.lcap && (int)h.hn + h.n + kLdsMargin <= (int)t.lcap)
+    ht_to_lds(h, ht_lds, t.lcap);
   while (D.running) {
+    if (h.lds && !ht_lds_room(h)) ht_spill(h);
+    HPROF_BEGIN(t_rec)
     const int rc = ht_step<K, S>(h, D, st, a, lseq, ev, rhi);
+    HPROF_END(h, 6, t_rec)
+#ifdef MTE_HTREE_PROF
+    h.prof[7]++;
+#endif
     D.n = h.n;
     if (rc < 0) {
       D.status = rc;
@@ -1549,6 +1696,11 @@ __global__ __launch_bounds__(64) void htree_kernel(ReplayArgs a, HtreeArgs t) {
     }
   }
   if constexpr (S) run_flush_stats(D, st, a);
+  if (h.lds) ht_spill(h);
+#ifdef MTE_HTREE_PROF
+  if (t.prof && lane_id() == 0)
+    for (int q = 0; q < kHtProf; q++) atomicAdd(t.prof + q, h.prof[q]);
+#endif
   lane0_st(stp + kHsDepth, (uint32_t)h.depth);
   lane0_st(stp + kHsNextId, h.next_id);
   lane0_st(stp + kHsHeapN, h.hn);

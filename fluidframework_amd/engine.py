@@ -83,6 +83,13 @@ class EngineBase:
         self._check(self._read_refs(doc, ptr(out), n), "read_refs")
         return out[:n]
 
+    def read_ref_order(self, doc, n):
+        """Document order of local reference slots [0, n) (mte_read_ref_order:
+        the index of the held text unit each sits on; -1 = detached / unused)."""
+        out = np.zeros(max(n, 1), np.int64)
+        self._check(self.lib.mte_read_ref_order(self.ctx, doc, ptr(out), n), "read_ref_order")
+        return out[:n]
+
     def read_segments(self, doc):
         """-> (segs SEG_DTYPE[n] with text_off into text, props uint32[n, n_keys], text uint16[])."""
         v = MteSegList()

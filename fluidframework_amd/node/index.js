@@ -168,6 +168,8 @@ class MergeTreeEngine {
     this.pending = new BatchBuilder(this.docs.length, this.interner, this.track);
     this.views = new Array(this.docs.length).fill(null);
     this.refViews = new Array(this.docs.length).fill(null);
+    this.orderViews = new Array(this.docs.length).fill(null);
+    this.unitViews = new Array(this.docs.length).fill(null);
     this.docs.forEach((d, i) => { if (d.catchup) for (const m of d.catchup) this.clients[i].applyMsg(m); });
   }
 
@@ -192,6 +194,8 @@ class MergeTreeEngine {
     this.pending = new BatchBuilder(this.docs.length, this.interner, this.track);
     this.views.fill(null);
     this.refViews.fill(null);
+    this.orderViews.fill(null);
+    this.unitViews.fill(null);
     this.addon.submit(this.ctx, b.offsets, b.ops, b.text, b.propsets, b.props);
     this.addon.run(this.ctx);
     this.running = true;
@@ -259,6 +263,38 @@ class MergeTreeEngine {
     if (v === null) {
       v = new Int32Array(this.addon.readRefs(this.ctx, doc, this.clients[doc].clients.refNext).buffer);
       this.refViews[doc] = v;
+    }
+    return v;
+  }
+
+  /** Document order of a document's reference slots (mte_read_ref_order: the
+   *  index of the held text unit each sits on, -1 detached), once per flush. */
+  _refOrderView(doc) {
+    this.flush();
+    this.sync();
+    let v = this.orderViews[doc];
+    if (v === null) {
+      v = this.addon.readRefOrder(this.ctx, doc, this.clients[doc].clients.refNext);
+      this.orderViews[doc] = v;
+    }
+    return v;
+  }
+
+  /** Per held segment of a document: [length, removed] (mte_read_segments),
+   *  once per flush: the units behind positions of the document's own view. */
+  _unitView(doc) {
+    let v = this.unitViews[doc];
+    if (v === null) {
+      this._view(doc);
+      const r = this.addon.readSegments(this.ctx, doc, this.nKeys);
+      const dv = new DataView(r.segs.buffer, r.segs.byteOffset, r.segs.byteLength);
+      const n = r.segs.byteLength / 32;
+      v = new Int32Array(2 * n);
+      for (let i = 0; i < n; i++) {
+        v[2 * i] = dv.getUint32(i * 32 + 4, true);
+        v[2 * i + 1] = dv.getInt32(i * 32 + 12, true) !== 0x7fffffff ? 1 : 0;
+      }
+      this.unitViews[doc] = v;
     }
     return v;
   }
@@ -458,6 +494,28 @@ class BatchClient {
     return this._local(op);
   }
 
+  /** Client.annotateMarker (client.ts:166-174): the op createAnnotateMarkerOp
+   *  makes (opBuilder.ts:26-40, relativePos1 {id, before: true} and
+   *  relativePos2 {id}), resolved by the engine in this client's view
+   *  (posFromRelativePos, mergeTree.ts:1369-1392).  marker: the marker's id,
+   *  or an object with getId() / properties.markerId; undefined without an id. */
+  annotateMarker(marker, props, combiningOp) {
+    const id = typeof marker === "string" ? marker
+      : (marker && typeof marker.getId === "function" ? marker.getId()
+        : (marker && marker.properties ? marker.properties.markerId : undefined));
+    if (!id) return undefined;
+    const op = { props, relativePos1: { id, before: true }, relativePos2: { id }, type: 2 };
+    if (combiningOp) op.combiningOp = combiningOp;
+    return this._local(op);
+  }
+
+  /** A local op given as its IMergeTreeDeltaOp JSON -- the Client's own op
+   *  path, applyInsertOp / applyRemoveRangeOp / applyAnnotateRangeOp({op})
+   *  (client.ts:405-500) -- relative positions included.  Returns the op. */
+  applyLocalOp(op) {
+    return this._local(op);
+  }
+
   /** TestClient.makeOpMessage (test/testClient.ts:259-272): the message to
    *  sequence for a local op. */
   makeOpMessage(op, seq, refSeq, minSeq) {
@@ -636,12 +694,12 @@ class BatchClient {
   /** SharedString.getIntervalCollection(label) (sequence.ts): the label's
    *  IntervalCollection over this client's references ({localClient, refs}
    *  documents); emitter.emit(opName, undefined, value) receives its ops. */
-  getIntervalCollection(label, emitter) {
+  getIntervalCollection(label, emitter, serialized) {
     if (!this.intervalCollections) this.intervalCollections = new Map();
     let c = this.intervalCollections.get(label);
     if (!c) {
       if (!this.engine.docs[this.doc].refs) throw new MergeTreeError(-9, "createClient(..., {refs: true}) first");
-      c = new IntervalCollection(this, label, emitter);
+      c = new IntervalCollection(this, label, emitter, serialized);
       this.intervalCollections.set(label, c);
     } else if (emitter) {
       c.emitter = emitter;
@@ -665,10 +723,35 @@ class BatchClient {
     return lref;
   }
 
+  /** The document-order key of a reference (mte_read_ref_order; -1 detached). */
+  _refOrder(lref) {
+    if (!lref || lref.client !== this || lref.slot < 0) return -1;
+    return this.engine._refOrderView(this.doc)[lref.slot];
+  }
+
+  /** The document-order key of the unit at pos of this client's view, as a
+   *  Transient reference there would have it (createPositionReference ->
+   *  getContainingSegment, intervalCollection.ts:639-658): -1 outside. */
+  _unitKeyAt(pos) {
+    const v = this.engine._unitView(this.doc);
+    if (!(pos >= 0)) return -1;
+    let p = 0, k = 0;
+    for (let i = 0; i < v.length; i += 2) {
+      const len = v[i];
+      if (!v[i + 1]) {
+        if (pos < p + len) return k + (pos - p);
+        p += len;
+      }
+      k += len;
+    }
+    return -1;
+  }
+
   /** Client.localReferencePositionToPosition (client.ts:376-378): the
    *  reference's position in this client's view, -1 (DetachedReferencePosition)
    *  once it is detached or removed. */
   localReferencePositionToPosition(lref) {
+    if (lref && lref.snapshot) return lref.position;  // an interval event's previousInterval end
     if (!lref || lref.client !== this || lref.slot < 0) return -1;
     return this.engine._refView(this.doc)[lref.slot];
   }

@@ -4,9 +4,9 @@
 // local references of its document (MTE_DOC_REFS, include/mte.h), so the
 // engine moves them with their text and slides them on removal; this module
 // keeps the collection's bookkeeping -- ids, pending changes, the interval
-// properties' pending keys, which end is which reference -- as the reference's
-// IntervalCollection does, and turns each interval op into the reference
-// records the engine needs:
+// properties' pending keys, which end is which reference, the order of the
+// interval tree, events, the summary -- as the reference's IntervalCollection
+// does, and turns each interval op into the reference records the engine needs:
 //   local add / change           StayOnRemove references in the local view
 //                                (createSequenceInterval / modify without an op,
 //                                intervalCollection.ts:573-609, 660-707)
@@ -18,7 +18,15 @@
 //                                become SlideOnRemove and slide if their
 //                                segment is removed and acked (ackInterval,
 //                                :1826-1902; MTE_OP_REF b = 3)
-// Positions are read back from the engine (localReferencePositionToPosition).
+//   load from a summary          SlideOnRemove references in the local view
+//                                (attachGraph with fromSnapshot, :1337-1374)
+// Positions are read back from the engine (localReferencePositionToPosition),
+// the tree order from the units the ends sit on (mte_read_ref_order, as
+// compareReferencePositions orders them).  Events (IIntervalCollectionEvent,
+// :1257-1300) fire for the collection's own edits and the interval ops it
+// processes; an end the engine slides off a removed segment inside a merge-tree
+// op moves without a "changeInterval" event (the reference raises one from the
+// reference's position-change listeners, :1023-1058, mid-op).
 const { MergeTreeError } = require("./packing");
 
 // ReferenceType (merge-tree ops.ts) and IntervalType (intervalCollection.ts:48-66)
@@ -28,6 +36,10 @@ const IntervalType = { Simple: 0x0, Nest: 0x1, SlideOnRemove: 0x2, Transient: 0x
 const reservedIntervalIdKey = "intervalId";            // intervalCollection.ts:46
 const reservedRangeLabelsKey = "referenceRangeLabels";  // merge-tree referencePositions.ts
 const UnassignedSequenceNumber = -1;                   // merge-tree constants.ts
+
+// Client.getCurrentSeq without a replay: the last sequenced message the host
+// packed (collabWindow.currentSeq after it, client.ts:937-945)
+const curSeq = (client) => client.clients.mergeSeq || 0;
 
 /** PropertiesManager (merge-tree segmentPropertiesManager.ts:29-160) for the
  *  interval properties: a key with a pending local change keeps its value
@@ -63,6 +75,16 @@ class PropertiesManager {
   }
 }
 
+/** compareReferencePositions (merge-tree referencePositions.ts:81-89) on the
+ *  engine's order keys: the same unit compares equal; a detached end (-1, no
+ *  segment) before every other. */
+function compareKeys(a, b) {
+  if (a === b) return 0;
+  if (a < 0) return -1;
+  if (b < 0) return 1;
+  return a < b ? -1 : 1;
+}
+
 /** SequenceInterval (intervalCollection.ts:387-619): two local references and
  *  the interval's properties. */
 class SequenceInterval {
@@ -77,6 +99,9 @@ class SequenceInterval {
   getIntervalId() {
     return this.properties[reservedIntervalIdKey];
   }
+  getProperties() {
+    return this.properties;
+  }
   addProperties(newProps, collab, seq) {
     return this.propertyManager.addProperties(this.properties, newProps, seq, !!collab);
   }
@@ -85,32 +110,94 @@ class SequenceInterval {
     const c = this.collection.client;
     return [c.localReferencePositionToPosition(this.start), c.localReferencePositionToPosition(this.end)];
   }
+  _keys() {
+    const c = this.collection.client;
+    return [c._refOrder(this.start), c._refOrder(this.end)];
+  }
+  /** compare (:483-506): start, then end, then id. */
+  compare(b) {
+    const x = this._keys(), y = b._keys();
+    const r = compareKeys(x[0], y[0]) || compareKeys(x[1], y[1]);
+    if (r) return r;
+    const i = this.getIntervalId(), j = b.getIntervalId();
+    return i && j ? (i > j ? 1 : i < j ? -1 : 0) : 0;
+  }
+  compareStart(b) {
+    return compareKeys(this._keys()[0], b._keys()[0]);
+  }
+  compareEnd(b) {
+    return compareKeys(this._keys()[1], b._keys()[1]);
+  }
+  /** overlaps (:522-527): ends inclusive. */
+  overlaps(b) {
+    const x = this._keys(), y = b._keys();
+    return compareKeys(x[0], y[1]) <= 0 && compareKeys(x[1], y[0]) >= 0;
+  }
+  /** serialize (:456-474). */
   serialize() {
     const [start, end] = this.positions();
-    return { end, intervalType: this.intervalType, sequenceNumber: this.collection.client.clients.mergeSeq || 0,
-      start, properties: this.properties };
+    const out = { end, intervalType: this.intervalType, sequenceNumber: curSeq(this.collection.client), start };
+    if (this.properties) out.properties = this.properties;
+    return out;
   }
 }
 
-function endpointTypes(intervalType, op) {
+/** A Transient interval at positions of the client's view, for queries
+ *  (createPositionReference with Transient, :639-658: no unit there ->
+ *  detached). */
+class TransientInterval {
+  constructor(client, start, end) {
+    this.k = [start === undefined ? undefined : client._unitKeyAt(start),
+      end === undefined ? undefined : client._unitKeyAt(end)];
+  }
+  _keys() {
+    return this.k;
+  }
+}
+
+/** The ends of an interval as they were, for a "changeInterval" event's
+ *  previousInterval (position information only, as the reference's Transient
+ *  copies, :1387-1410). */
+function snapshotInterval(ival) {
+  const c = ival.collection.client;
+  const ref = (r) => ({ snapshot: true, position: c.localReferencePositionToPosition(r), refType: RefType.Transient });
+  const prev = new SequenceInterval(ival.collection, ref(ival.start), ref(ival.end), ival.intervalType);
+  prev.properties = Object.assign({}, ival.properties);
+  return prev;
+}
+
+function endpointTypes(intervalType, op, fromSnapshot) {
   if (intervalType & IntervalType.Transient) throw new MergeTreeError(-9, "Can not add transient intervals");
   let b = RefType.RangeBegin, e = RefType.RangeEnd;
   if (intervalType === IntervalType.Nest) {
     b = RefType.NestBegin;
     e = RefType.NestEnd;
   }
-  // createSequenceInterval (:679-689): SlideOnRemove once created by an op,
-  // StayOnRemove while a local creation is pending
-  const slide = op ? RefType.SlideOnRemove : RefType.StayOnRemove;
+  // createSequenceInterval (:679-689): SlideOnRemove once created by an op or
+  // from a summary, StayOnRemove while a local creation is pending
+  const slide = op || fromSnapshot ? RefType.SlideOnRemove : RefType.StayOnRemove;
   return [b | slide, e | slide];
+}
+
+/** decompressInterval / compressInterval (:123-149). */
+function decompressInterval(x, label) {
+  return { start: x[0], end: x[1], sequenceNumber: x[2], intervalType: x[3],
+    properties: Object.assign({}, x[4], { [reservedRangeLabelsKey]: [label] }) };
+}
+function compressInterval(v) {
+  const props = Object.assign({}, v.properties);
+  delete props[reservedRangeLabelsKey];  // {..., referenceRangeLabels: undefined} drops it from the JSON
+  return [v.start, v.end, v.sequenceNumber, v.intervalType, props];
 }
 
 /** IntervalCollection (intervalCollection.ts:1309-2102) of one label on one
  *  BatchClient ({localClient, refs} document).  emitter.emit(opName, undefined,
  *  value, metadata) receives the ops to send, as SharedString's value-type
- *  emitter does; the sequenced messages come back through process(). */
+ *  emitter does; the sequenced messages come back through process().
+ *  serialized: a summary of the collection (serializeInternal's
+ *  ISerializedIntervalCollectionV2, or a V1 array) to load. */
 class IntervalCollection {
-  constructor(client, label, emitter) {
+  constructor(client, label, emitter, serialized) {
     this.client = client;
     this.label = label;
     this.emitter = emitter || { emit() {} };
@@ -118,6 +205,32 @@ class IntervalCollection {
     this.pendingStart = new Map();  // id -> pending local changes of the start (FIFO)
     this.pendingEnd = new Map();
     this.nextLocalId = 0;
+    this.listeners = new Map();
+    this.stamp = 0;  // index insertion order (the end tree keeps the last put, rbTree.ts:249-300)
+    if (serialized) this._load(serialized);
+  }
+
+  // ---- events (TypedEventEmitter<IIntervalCollectionEvent>) ------------------------
+  on(event, listener) {
+    if (!this.listeners.has(event)) this.listeners.set(event, []);
+    this.listeners.get(event).push(listener);
+    return this;
+  }
+  off(event, listener) {
+    const l = this.listeners.get(event);
+    if (l) {
+      const i = l.indexOf(listener);
+      if (i >= 0) l.splice(i, 1);
+    }
+    return this;
+  }
+  _has(event) {
+    const l = this.listeners.get(event);
+    return !!l && l.length > 0;
+  }
+  _emit(event, ...args) {
+    const l = this.listeners.get(event);
+    if (l) for (const f of l.slice()) f(...args);
   }
 
   // ---- references ------------------------------------------------------------
@@ -133,8 +246,8 @@ class IntervalCollection {
     if (ref) this.client.removeLocalReferencePosition(ref);
   }
 
-  _create(start, end, intervalType, op) {
-    const [bt, et] = endpointTypes(intervalType, op);
+  _create(start, end, intervalType, op, fromSnapshot) {
+    const [bt, et] = endpointTypes(intervalType, op, fromSnapshot);
     const s = op ? this._opRef(start, bt, op) : this._localRef(start, bt);
     const e = op ? this._opRef(end, et, op) : this._localRef(end, et);
     const ival = new SequenceInterval(this, s, e, intervalType);
@@ -142,14 +255,32 @@ class IntervalCollection {
     return ival;
   }
 
-  _addInterval(start, end, intervalType, props, op) {
-    const ival = this._create(start, end, intervalType, op);
+  _index(ival) {
+    ival.stamp = ++this.stamp;
+    this.byId.set(ival.getIntervalId(), ival);
+  }
+
+  _addInterval(start, end, intervalType, props, op, fromSnapshot) {
+    const ival = this._create(start, end, intervalType, op, fromSnapshot);
     if (props) ival.addProperties(props);
     if (ival.properties[reservedIntervalIdKey] === undefined) {
       ival.properties[reservedIntervalIdKey] = `${this.client.longClientId}-${this.label}-${this.nextLocalId++}`;
     }
-    this.byId.set(ival.getIntervalId(), ival);
+    this._index(ival);
     return ival;
+  }
+
+  /** attachGraph with saved intervals (:1337-1374): each end a SlideOnRemove
+   *  reference at its position in the local view; no events. */
+  _load(serialized) {
+    const list = Array.isArray(serialized) ? serialized
+      : serialized.intervals.map((x) => decompressInterval(x, serialized.label));
+    for (const v of list) {
+      this._ensureId(v);
+      const ival = this._create(v.start, v.end, v.intervalType, undefined, true);
+      if (v.properties) ival.addProperties(v.properties);
+      this._index(ival);
+    }
   }
 
   /** LocalIntervalCollection.changeInterval -> SequenceInterval.modify
@@ -167,6 +298,7 @@ class IntervalCollection {
       ival.end = op ? this._opRef(end, retype(old.refType), op) : this._localRef(end, retype(old.refType));
       this._drop(old);
     }
+    ival.stamp = ++this.stamp;
     return ival;
   }
 
@@ -185,18 +317,22 @@ class IntervalCollection {
   add(start, end, intervalType, props) {
     const ival = this._addInterval(start, end, intervalType, props);
     this.emitter.emit("add", undefined, { end, intervalType, properties: Object.assign({}, ival.properties),
-      sequenceNumber: this.client.clients.mergeSeq || 0, start }, {});
+      sequenceNumber: curSeq(this.client), start }, {});
+    this._emit("addInterval", ival, true, undefined);
     return ival;
   }
 
-  /** IntervalCollection.removeIntervalById (:1493-1502). */
+  /** IntervalCollection.removeIntervalById (:1493-1502) -> deleteExistingInterval (:1462-1491). */
   removeIntervalById(id) {
     const ival = this.byId.get(id);
     if (ival) {
-      const v = { intervalType: ival.intervalType, sequenceNumber: this.client.clients.mergeSeq || 0,
+      // serialize() without the ends' positions (a replay per delete; receivers
+      // look the interval up by id, ackDelete :1943-1963)
+      const v = { intervalType: ival.intervalType, sequenceNumber: curSeq(this.client),
         properties: Object.assign({}, ival.properties) };
       this._remove(ival);
       this.emitter.emit("delete", undefined, v, {});
+      this._emit("deleteInterval", ival, true, undefined);
     }
     return ival;
   }
@@ -207,10 +343,11 @@ class IntervalCollection {
     if (!props) throw new MergeTreeError(-1, "changeProperties should be called with a property set");
     const ival = this.byId.get(id);
     if (ival) {
-      ival.addProperties(props, true, UnassignedSequenceNumber);
+      const deltas = ival.addProperties(props, true, UnassignedSequenceNumber);
       this.emitter.emit("change", undefined, { intervalType: ival.intervalType,
-        sequenceNumber: this.client.clients.mergeSeq || 0,
+        sequenceNumber: curSeq(this.client),
         properties: Object.assign({}, props, { [reservedIntervalIdKey]: id }) }, {});
+      this._emit("propertyChanged", ival, deltas, true, undefined);
     }
   }
 
@@ -220,11 +357,13 @@ class IntervalCollection {
     if (typeof id !== "string") throw new MergeTreeError(-1, "Change API requires an ID that is a string");
     const ival = this.byId.get(id);
     if (!ival) return undefined;
+    const prev = this._has("changeInterval") ? snapshotInterval(ival) : null;
     this._changeInterval(ival, start, end);
-    const v = { start, end, intervalType: ival.intervalType, sequenceNumber: this.client.clients.mergeSeq || 0,
+    const v = { start, end, intervalType: ival.intervalType, sequenceNumber: curSeq(this.client),
       properties: { [reservedIntervalIdKey]: id } };
     this.emitter.emit("change", undefined, v, {});
     this._addPending(id, v);
+    if (prev) this._emit("changeInterval", ival, prev, true, undefined);
     return ival;
   }
 
@@ -274,18 +413,22 @@ class IntervalCollection {
   ackAdd(v, local, op) {
     if (local) {
       const ival = this.byId.get(v.properties && v.properties[reservedIntervalIdKey]);
-      if (ival) this._ackInterval(ival);
+      if (ival) this._ackInterval(ival, op);
       return;
     }
     this._ensureId(v);
-    this._addInterval(v.start, v.end, v.intervalType, v.properties, op);
+    const ival = this._addInterval(v.start, v.end, v.intervalType, v.properties, op);
+    this._emit("addInterval", ival, false, op);
   }
 
   /** ackDelete (:1943-1963). */
-  ackDelete(v, local) {
+  ackDelete(v, local, op) {
     if (local) return;
     const ival = this.byId.get(this._ensureId(v));
-    if (ival) this._remove(ival);
+    if (ival) {
+      this._remove(ival);
+      this._emit("deleteInterval", ival, false, op);
+    }
   }
 
   /** ackChange (:1641-1704). */
@@ -299,46 +442,139 @@ class IntervalCollection {
     if (!ival) return;  // removed locally
     if (local) {
       ival.propertyManager.ackPendingProperties(v.properties || {});
-      this._ackInterval(ival);
+      this._ackInterval(ival, op);
       return;
     }
     const start = this.pendingStart.has(id) ? undefined : v.start;
     const end = this.pendingEnd.has(id) ? undefined : v.end;
-    if (start !== undefined || end !== undefined) this._changeInterval(ival, start, end, op);
-    ival.addProperties(props, true, op.sequenceNumber);
+    let prev = null;
+    if (start !== undefined || end !== undefined) {
+      prev = this._has("changeInterval") ? snapshotInterval(ival) : null;
+      this._changeInterval(ival, start, end, op);
+    }
+    const deltas = ival.addProperties(props, true, op.sequenceNumber);
+    if (prev) this._emit("changeInterval", ival, prev, false, op);
+    if (Object.keys(props).length > 0) this._emit("propertyChanged", ival, deltas, false, op);
   }
 
   /** ackInterval (:1826-1902): the StayOnRemove ends no pending change holds
-   *  become SlideOnRemove and slide if their segment is removed and acked. */
-  _ackInterval(ival) {
+   *  become SlideOnRemove and slide if their segment is removed and acked;
+   *  "changeInterval" when one slid. */
+  _ackInterval(ival, op) {
     const stay = (r) => (r.refType & RefType.StayOnRemove) !== 0;
     if (!stay(ival.start) && !stay(ival.end)) return;
     const id = ival.getIntervalId();
+    const watch = this._has("changeInterval");
+    const prev = watch ? snapshotInterval(ival) : null;
+    const before = watch ? ival._keys() : null;
     const slide = (r) => (r.refType & ~RefType.StayOnRemove) | RefType.SlideOnRemove;
     if (!this.pendingStart.has(id) && stay(ival.start)) this.client._setRefSlide(ival.start, slide(ival.start));
     if (!this.pendingEnd.has(id) && stay(ival.end)) this.client._setRefSlide(ival.end, slide(ival.end));
-  }
-
-  // ---- queries -----------------------------------------------------------------
-  /** Every interval in (start, end, id) order of their positions. */
-  [Symbol.iterator]() {
-    const all = Array.from(this.byId.values()).map((x) => [x.positions(), x]);
-    all.sort((a, b) => a[0][0] - b[0][0] || a[0][1] - b[0][1] ||
-      (a[1].getIntervalId() < b[1].getIntervalId() ? -1 : a[1].getIntervalId() > b[1].getIntervalId() ? 1 : 0));
-    return all.map((x) => x[1])[Symbol.iterator]();
-  }
-
-  /** findOverlappingIntervals (:881-895): the intervals overlapping
-   *  [startPosition, endPosition] (ends inclusive). */
-  findOverlappingIntervals(startPosition, endPosition) {
-    if (endPosition < startPosition) return [];
-    const out = [];
-    for (const x of this) {
-      const [s, e] = x.positions();
-      if (s <= endPosition && e >= startPosition) out.push(x);
+    if (watch) {
+      const after = ival._keys();
+      if (after[0] !== before[0] || after[1] !== before[1]) {
+        ival.stamp = ++this.stamp;
+        this._emit("changeInterval", ival, prev, true, op);
+      }
     }
+  }
+
+  // ---- queries (LocalIntervalCollection, :760-913) ------------------------------
+  /** The interval tree's order (compare, :483-506). */
+  _sorted() {
+    return Array.from(this.byId.values()).sort((a, b) => a.compare(b));
+  }
+
+  [Symbol.iterator]() {
+    return this._sorted()[Symbol.iterator]();
+  }
+
+  map(fn) {
+    for (const x of this._sorted()) fn(x);
+  }
+
+  /** gatherIterationResults (:802-879): whole tree, or the intervals whose start
+   *  (and end) equal those of a Transient interval at the positions given. */
+  gatherIterationResults(results, iteratesForward, start, end) {
+    let all = this._sorted();
+    if (!iteratesForward) all = all.reverse();
+    if (start === undefined && end === undefined) {
+      results.push(...all);
+      return;
+    }
+    const t = new TransientInterval(this.client, start, end);
+    for (const x of all) {
+      const k = x._keys();
+      if (start !== undefined && compareKeys(t.k[0], k[0]) !== 0) continue;
+      if (end !== undefined && compareKeys(t.k[1], k[1]) !== 0) continue;
+      results.push(x);
+    }
+  }
+
+  CreateForwardIteratorWithStartPosition(startPosition) {
+    const r = [];
+    this.gatherIterationResults(r, true, startPosition);
+    return r[Symbol.iterator]();
+  }
+  CreateBackwardIteratorWithStartPosition(startPosition) {
+    const r = [];
+    this.gatherIterationResults(r, false, startPosition);
+    return r[Symbol.iterator]();
+  }
+  CreateForwardIteratorWithEndPosition(endPosition) {
+    const r = [];
+    this.gatherIterationResults(r, true, undefined, endPosition);
+    return r[Symbol.iterator]();
+  }
+  CreateBackwardIteratorWithEndPosition(endPosition) {
+    const r = [];
+    this.gatherIterationResults(r, false, undefined, endPosition);
+    return r[Symbol.iterator]();
+  }
+
+  /** findOverlappingIntervals (:881-895): the intervals overlapping a
+   *  Transient interval at [startPosition, endPosition] (ends inclusive), in
+   *  tree order. */
+  findOverlappingIntervals(startPosition, endPosition) {
+    if (endPosition < startPosition || this.byId.size === 0) return [];
+    const t = new TransientInterval(this.client, startPosition, endPosition);
+    return this._sorted().filter((x) => {
+      const k = x._keys();
+      return compareKeys(k[0], t.k[1]) <= 0 && compareKeys(k[1], t.k[0]) >= 0;
+    });
+  }
+
+  /** previousInterval / nextInterval (:897-913): floor / ceil of a Transient
+   *  interval at pos in the end tree (ordered by end; of the intervals whose
+   *  ends sit on one unit it holds the one put last, rbTree.ts:249-300). */
+  _endTree() {
+    const byEnd = new Map();
+    for (const x of this.byId.values()) {
+      const k = x._keys()[1];
+      const cur = byEnd.get(k);
+      if (!cur || cur.stamp < x.stamp) byEnd.set(k, x);
+    }
+    return Array.from(byEnd.entries()).sort((a, b) => compareKeys(a[0], b[0]));
+  }
+  previousInterval(pos) {
+    const k = this.client._unitKeyAt(pos);
+    let out;
+    for (const [ek, x] of this._endTree()) if (compareKeys(ek, k) <= 0) out = x;
     return out;
+  }
+  nextInterval(pos) {
+    const k = this.client._unitKeyAt(pos);
+    for (const [ek, x] of this._endTree()) if (compareKeys(ek, k) >= 0) return x;
+    return undefined;
+  }
+
+  // ---- summary --------------------------------------------------------------------
+  /** serializeInternal (:1968-1977) -> LocalIntervalCollection.serialize
+   *  (:1014-1021): the intervals in tree order, compressed. */
+  serializeInternal() {
+    return { label: this.label, intervals: this._sorted().map((x) => compressInterval(x.serialize())), version: 2 };
   }
 }
 
-module.exports = { IntervalCollection, SequenceInterval, PropertiesManager, RefType, IntervalType };
+module.exports = { IntervalCollection, SequenceInterval, PropertiesManager, RefType, IntervalType, compressInterval,
+  decompressInterval };

@@ -613,6 +613,40 @@ static napi_value js_read_refs(napi_env env, napi_callback_info info) {
   return out;
 }
 
+/* readRefOrder(ctx, doc, n) -> Float64Array(n): document order of reference
+   slots [0, n) (mte_read_ref_order; -1 detached / unused) */
+static napi_value js_read_ref_order(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  if (!get_args(env, info, 3, argv)) return NULL;
+  mte_ctx* ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  uint32_t doc = 0, n = 0;
+  if (napi_get_value_uint32(env, argv[1], &doc) != napi_ok || napi_get_value_uint32(env, argv[2], &n) != napi_ok) {
+    napi_throw_type_error(env, NULL, "readRefOrder: doc and n must be numbers");
+    return NULL;
+  }
+  int64_t* buf = (int64_t*)malloc((size_t)(n ? n : 1) * sizeof(int64_t));
+  if (!buf) {
+    napi_throw_error(env, NULL, "out of memory");
+    return NULL;
+  }
+  if (throw_rc(env, mte_read_ref_order(ctx, doc, buf, n), ctx, "mte_read_ref_order")) {
+    free(buf);
+    return NULL;
+  }
+  napi_value ab, out;
+  void* data = NULL;
+  if (napi_create_arraybuffer(env, (size_t)n * 8, &data, &ab) != napi_ok ||
+      napi_create_typedarray(env, napi_float64_array, n, ab, 0, &out) != napi_ok) {
+    free(buf);
+    napi_throw_error(env, NULL, "readRefOrder: allocation");
+    return NULL;
+  }
+  for (uint32_t i = 0; i < n; i++) ((double*)data)[i] = (double)buf[i];
+  free(buf);
+  return out;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
   const napi_property_descriptor d[] = {
       {"abiVersion", NULL, js_abi_version, NULL, NULL, NULL, napi_enumerable, NULL},
@@ -642,6 +676,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"setEventCapacity", NULL, js_set_event_capacity, NULL, NULL, NULL, napi_enumerable, NULL},
       {"setRefCapacity", NULL, js_set_ref_capacity, NULL, NULL, NULL, napi_enumerable, NULL},
       {"readRefs", NULL, js_read_refs, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"readRefOrder", NULL, js_read_ref_order, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   if (napi_define_properties(env, exports, sizeof d / sizeof d[0], d) != napi_ok) return NULL;
   return exports;

@@ -31,6 +31,9 @@
 const OP_INSERT = 0, OP_REMOVE = 1, OP_ANNOTATE = 2, OP_NOOP = 3, OP_ACK = 4, OP_ROLLBACK = 5, OP_REGEN = 6;
 const OP_RBKEY = 7;          // MTE_OP_RBKEY: an annotate rollback's previous-value candidates
 const OP_REF = 8;            // MTE_OP_REF: create / remove a local reference
+const OP_RELPOS = 9;         // MTE_OP_RELPOS: relative positions of the record that follows
+const RP_POS1 = 0x100, RP_BEFORE1 = 0x200, RP_POS2 = 0x400, RP_BEFORE2 = 0x800;
+const MARKER_ID_KEY = "markerId";  // reservedMarkerIdKey (mergeTreeNodes.ts)
 const REF_SLIDE_ON_REMOVE = 0x40, REF_STAY_ON_REMOVE = 0x80, REF_TRANSIENT = 0x100;  // ReferenceType (ops.ts)
 const DELTA_REGEN = 0x10;    // MTE_DELTA_REGEN: kind flag of a regenerated op's records
 const ANNOTATE_SLOTS = 32;   // MTE_ANNOTATE_SLOTS: pending local annotate groups tracked per document
@@ -411,8 +414,16 @@ class BatchBuilder {
       for (const member of op.ops || []) this._opPut(doc, seq, ref, msn, member, track);
       return;
     }
-    if (!("pos1" in op) && op.relativePos1 !== undefined && op.relativePos1 !== null) {
-      throw new MergeTreeError(E_UNSUPPORTED, "relativePos1");
+    const rel = this._relpos(op, t);
+    if ((t === REMOVE || t === ANNOTATE) && !("pos2" in op) && !(rel && (rel[0] & RP_POS2))) {
+      throw new MergeTreeError(E_UNSUPPORTED, "range op without pos2");
+    }
+    if ((t === REMOVE || t === ANNOTATE) && !("pos1" in op) && !(rel && (rel[0] & RP_POS1))) {
+      throw new MergeTreeError(E_UNSUPPORTED, "range op without pos1");
+    }
+    if (rel && (t !== INSERT || (op.seg !== undefined && op.seg !== null))) {
+      this._put(doc, rel[4], rel[5], 0, OP_RELPOS, 0, rel[0], rel[1], rel[2], rel[3], 0);
+      if (track) this._srcOps.push(op);  // the RELPOS record's entry
     }
     if (t === INSERT) {
       const seg = op.seg;
@@ -436,11 +447,9 @@ class BatchBuilder {
       }
       return;
     }
-    if ((t === REMOVE || t === ANNOTATE) && !("pos2" in op)) {
-      throw new MergeTreeError(E_UNSUPPORTED, "range op without pos2");
-    }
+    const p1 = op.pos1 === undefined ? 0 : op.pos1, p2 = op.pos2 === undefined ? 0 : op.pos2;
     if (t === REMOVE) {
-      this._put(doc, seq, ref, msn, OP_REMOVE, 0, 0, checkI32(op.pos1, "pos1"), checkI32(op.pos2, "pos2"), 0, NO_PROPS);
+      this._put(doc, seq, ref, msn, OP_REMOVE, 0, 0, checkI32(p1, "pos1"), checkI32(p2, "pos2"), 0, NO_PROPS);
     } else if (t === ANNOTATE) {
       let flags = 0;
       const comb = op.combiningOp;
@@ -449,8 +458,7 @@ class BatchBuilder {
         flags = F_REWRITE;
       }
       const ps = this.props.add(op.props === undefined ? {} : op.props);  // before the checks, as packing.py
-      this._put(doc, seq, ref, msn, OP_ANNOTATE, 0, flags, checkI32(op.pos1, "pos1"), checkI32(op.pos2, "pos2"), ps,
-        NO_PROPS);
+      this._put(doc, seq, ref, msn, OP_ANNOTATE, 0, flags, checkI32(p1, "pos1"), checkI32(p2, "pos2"), ps, NO_PROPS);
     } else {
       throw new MergeTreeError(E_INVALID_ARG, "unknown op type " + String(t));
     }
@@ -466,9 +474,12 @@ class BatchBuilder {
     this._srcOps = null;
     this._opRecords(op, recs, this._src(doc));
     if (recs.length === 0) recs.push([OP_NOOP, 0, 0, 0, 0, NO_PROPS]);
-    if (recs.some((r) => r[1] & F_REWRITE)) throw new MergeTreeError(E_UNSUPPORTED, "local combiningOp rewrite");
+    if (recs.some((r) => r[0] !== OP_RELPOS && (r[1] & F_REWRITE))) {
+      throw new MergeTreeError(E_UNSUPPORTED, "local combiningOp rewrite");
+    }
     const first = clients.localSeq + 1;
-    if (first + recs.length >= LOCAL_SEQ_BASE) throw new MergeTreeError(E_INVALID_ARG, "localSeq overflow");
+    const nOps = recs.filter((r) => r[0] !== OP_RELPOS).length;  // a RELPOS record takes no localSeq
+    if (first + nOps >= LOCAL_SEQ_BASE) throw new MergeTreeError(E_INVALID_ARG, "localSeq overflow");
     // every check that can throw is above: the event sources stay aligned with the records
     const src = this._src(doc);
     if (src) {
@@ -476,7 +487,12 @@ class BatchBuilder {
       for (let i = 0; i < recs.length; i++) src.push({ msg: null, op: ops[i], local: true });
     }
     this._srcOps = null;
-    recs.forEach((r, i) => {
+    let i = 0;
+    for (const r of recs) {
+      if (r[0] === OP_RELPOS) {
+        this._put(doc, r[5][0], r[5][1], 0, OP_RELPOS, 0, r[1], r[2], r[3], r[4], 0);
+        continue;
+      }
       let b = r[5];
       if (r[0] === OP_ANNOTATE) {
         const used = new Set(clients.annSlot.values());
@@ -492,10 +508,11 @@ class BatchBuilder {
         clients.annProps.set(first + i, kv);
       }
       this._put(doc, first + i, 0, 0, r[0], 0, r[1] | F_LOCAL, r[2], r[3], r[4], b);
-    });
-    clients.localSeq += recs.length;
+      i++;
+    }
+    clients.localSeq += nOps;
     clients.pending.push([first, clients.localSeq]);
-    clients.pendingTypes.push(recs.map((r) => r[0]));
+    clients.pendingTypes.push(recs.filter((r) => r[0] !== OP_RELPOS).map((r) => r[0]));
   }
 
   /** Client.rollback of the latest pending local op (client.ts:396-398 ->
@@ -681,6 +698,33 @@ class BatchBuilder {
     return this.recSrc ? this.recSrc[doc] : null;
   }
 
+  /** getValidOpRange (client.ts:541-560): a position given as relativePos (no
+   *  pos1 / pos2) -> [flags, vid1, vid2, key, offset1, offset2] of an
+   *  MTE_OP_RELPOS record the engine resolves (posFromRelativePos,
+   *  mergeTree.ts:1369-1392), or null (as packing.py _relpos) */
+  _relpos(op, t) {
+    let flags = 0;
+    const vids = [0, 0], offs = [0, 0];
+    const spec = [["pos1", "relativePos1", RP_POS1, RP_BEFORE1], ["pos2", "relativePos2", RP_POS2, RP_BEFORE2]];
+    for (let i = 0; i < 2; i++) {
+      const [pk, rk, pf, bf] = spec[i];
+      const rp = op[rk];
+      if (pk in op || rp === undefined || rp === null || (i === 1 && op.type === INSERT)) continue;
+      if (typeof rp !== "object") throw new MergeTreeError(E_INVALID_ARG, rk + " must be an object");
+      flags |= pf;
+      if (rp.before) flags |= bf;
+      if (rp.offset !== undefined && rp.offset !== null) offs[i] = checkI32(rp.offset, rk + ".offset");
+      // an id no marker was ever given cannot match (value 0)
+      if (rp.id) {
+        const v = this.interner.values.get(canonicalJson(rp.id));
+        vids[i] = v === undefined ? 0 : v;
+      }
+    }
+    if (!flags) return null;
+    const key = this.interner.keys.get(MARKER_ID_KEY);
+    return [flags, vids[0], vids[1], key === undefined ? NO_PROPS : key, offs[0], offs[1]];
+  }
+
   _opRecords(op, recs, track) {
     if (track && op && typeof op === "object" && op.type !== GROUP) {
       if (!this._srcOps) this._srcOps = [];
@@ -692,11 +736,16 @@ class BatchBuilder {
       for (const member of op.ops || []) this._opRecords(member, recs, track);
       return;
     }
-    if (!("pos1" in op) && op.relativePos1 !== undefined && op.relativePos1 !== null) {
-      throw new MergeTreeError(E_UNSUPPORTED, "relativePos1");
-    }
-    if ((t === REMOVE || t === ANNOTATE) && !("pos2" in op)) {
+    const rel = this._relpos(op, t);
+    if ((t === REMOVE || t === ANNOTATE) && !("pos2" in op) && !(rel && (rel[0] & RP_POS2))) {
       throw new MergeTreeError(E_UNSUPPORTED, "range op without pos2");
+    }
+    if ((t === REMOVE || t === ANNOTATE) && !("pos1" in op) && !(rel && (rel[0] & RP_POS1))) {
+      throw new MergeTreeError(E_UNSUPPORTED, "range op without pos1");
+    }
+    if (rel && (t !== INSERT || (op.seg !== undefined && op.seg !== null))) {
+      recs.push([OP_RELPOS, rel[0], rel[1], rel[2], rel[3], [rel[4], rel[5]]]);
+      if (track) this._srcOps.push(op);  // the RELPOS record's entry
     }
     if (t === INSERT) {
       const seg = op.seg;
@@ -719,7 +768,8 @@ class BatchBuilder {
         throw new MergeTreeError(E_INVALID_ARG, "Unrecognized IJSONSegment type: " + JSON.stringify(seg));
       }
     } else if (t === REMOVE) {
-      recs.push([OP_REMOVE, 0, checkI32(op.pos1, "pos1"), checkI32(op.pos2, "pos2"), 0, NO_PROPS]);
+      recs.push([OP_REMOVE, 0, checkI32(op.pos1 === undefined ? 0 : op.pos1, "pos1"),
+        checkI32(op.pos2 === undefined ? 0 : op.pos2, "pos2"), 0, NO_PROPS]);
     } else if (t === ANNOTATE) {
       let flags = 0;
       const comb = op.combiningOp;
@@ -728,7 +778,8 @@ class BatchBuilder {
         flags = F_REWRITE;
       }
       const ps = this.props.add(op.props === undefined ? {} : op.props);
-      recs.push([OP_ANNOTATE, flags, checkI32(op.pos1, "pos1"), checkI32(op.pos2, "pos2"), ps, NO_PROPS]);
+      recs.push([OP_ANNOTATE, flags, checkI32(op.pos1 === undefined ? 0 : op.pos1, "pos1"),
+        checkI32(op.pos2 === undefined ? 0 : op.pos2, "pos2"), ps, NO_PROPS]);
     } else {
       throw new MergeTreeError(E_INVALID_ARG, "unknown op type " + String(t));
     }

@@ -262,10 +262,10 @@ typedef struct mte_config {
 /* The document is a collaborating client that sends ops of its own (short
  * client id 0 = collabWindow.clientId): it takes MTE_F_LOCAL records and
  * MTE_OP_ACK messages besides remote ones (the non-observer TestClients of the
- * conflict farm, test/mergeTreeOperationRunner.ts:149-236).  Requires
- * MTE_DOC_NEW_LENGTH_CALC (as the farm's clients, client.conflictFarm.spec.ts:84)
- * and a context with seg_capacity < 8192; such documents replay on the
- * HBM-streamed pass.                                                         */
+ * conflict farm, test/mergeTreeOperationRunner.ts:149-236), in either length
+ * calculation.  Such documents replay on the HBM tree pass (the reference's
+ * B+tree with its continuePredicate placement, mergeTree.ts:1664, 1790-1791),
+ * LDS-resident while they fit.                                               */
 #define MTE_DOC_LOCAL_CLIENT 0x4u
 /* Record the document's delta events: what MergeTree.mergeTreeDeltaCallback
  * reports after each insert / remove / annotate (mergeTree.ts:1409-1416,
@@ -273,8 +273,9 @@ typedef struct mte_config {
  * (sequence.ts:203-211; SequenceEvent.ranges, sequenceDeltaEvent.ts): one
  * mte_delta per affected segment, in document order, at its position in the
  * document's own view right after the op (Client.getPosition, client.ts:345-350).
- * Requires MTE_DOC_NEW_LENGTH_CALC and a context below 8192 segments; such
- * documents replay on the HBM-streamed pass.  Read with mte_read_deltas.      */
+ * New length-calc documents of remote clients replay on the HBM-streamed pass
+ * (refused in contexts of >= 8192 segments), the others on the HBM tree pass.
+ * Read with mte_read_deltas.                                                  */
 #define MTE_DOC_EVENTS 0x8u
 /* The document holds local references (MTE_OP_REF records; mte_read_refs).
  * Requires MTE_DOC_LOCAL_CLIENT.  Each of its markers takes the text offset of
@@ -438,6 +439,13 @@ int mte_set_ref_capacity(mte_ctx* ctx, uint32_t per_doc);
  * the segment's position (Client.getPosition) plus the offset, 0 on a removed
  * segment; -1 (DetachedReferencePosition) for a detached or unused slot.      */
 int mte_read_refs(mte_ctx* ctx, uint32_t doc, int32_t* pos, uint32_t n);
+/* Document order of reference slots [0, n): the index, among every text unit
+ * the document holds (removed segments included), of the unit the reference
+ * sits on; -1 for a detached or unused slot.  Two references compare as
+ * compareReferencePositions does (referencePositions.ts:81-89: the same
+ * segment by offset, else by segment ordinal; detached first) -- the order of
+ * an interval collection's tree (intervalCollection.ts:483-520).            */
+int mte_read_ref_order(mte_ctx* ctx, uint32_t doc, int64_t* key, uint32_t n);
 
 /* Every segment a document holds — removed ones above minSeq included — with
  * its merge info, in document order: the input of a summary writer

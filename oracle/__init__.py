@@ -50,7 +50,7 @@ def load():
         "oti_load_segments": [vp, vp, vp, u64], "oti_apply_batch": [vp, vp, C.c_int],
         "oti_read_doc": [vp, u32, vp], "oti_digest": [vp, vp, u32], "oti_doc_status": [vp, vp, u32],
         "oti_doc_nsegs": [vp, u32, vp], "oti_stats_get": [vp, vp], "oti_read_segments": [vp, u32, vp], "oti_set_limit": [vp, u32],
-        "oti_read_deltas": [vp, u32, vp, u64, vp], "oti_read_refs": [vp, u32, vp, u32],
+        "oti_read_deltas": [vp, u32, vp, u64, vp], "oti_read_refs": [vp, u32, vp, u32], "oti_read_ref_order": [vp, u32, vp, u32],
         "och_create": [u32, vp], "och_destroy": [vp], "och_load_docs": [vp, u32, vp, vp, u64, vp, u32, vp, u32],
         "och_load_segments": [vp, vp, vp, u64], "och_apply_batch": [vp, vp, C.c_int], "och_read_doc": [vp, u32, vp],
         "och_digest": [vp, vp, u32], "och_doc_status": [vp, vp, u32], "och_doc_nsegs": [vp, u32, vp],
@@ -63,6 +63,8 @@ def load():
     lib.orc_read_deltas.restype = C.c_int
     lib.orc_read_refs.argtypes = [vp, u32, vp, u32]
     lib.orc_read_refs.restype = C.c_int
+    lib.orc_read_ref_order.argtypes = [vp, u32, vp, u32]
+    lib.orc_read_ref_order.restype = C.c_int
     for pre in ("ort", "oti"):
         f = getattr(lib, f"{pre}_doc_shape")
         f.argtypes = [vp, u32, C.c_char_p, u32]
@@ -162,6 +164,12 @@ class OracleEngine(EngineBase):
     def _read_refs(self, doc, p, n):
         f = self.lib.oti_read_refs if self.tree == "items" else self.lib.orc_read_refs
         return f(self.ctx, doc, p, n)
+
+    def read_ref_order(self, doc, n):
+        f = self.lib.oti_read_ref_order if self.tree == "items" else self.lib.orc_read_ref_order
+        out = np.zeros(max(n, 1), np.int64)
+        self._check(f(self.ctx, doc, ptr(out), n), "read_ref_order")
+        return out[:n]
 
     def _digest(self, p, n):
         return self.f.digest(self.ctx, p, n)
@@ -269,6 +277,10 @@ class SpecOracle:
     def read_refs(self, doc, n):
         e, i = self.where[doc]
         return self._engines()[e].read_refs(int(i), n)
+
+    def read_ref_order(self, doc, n):
+        e, i = self.where[doc]
+        return self._engines()[e].read_ref_order(int(i), n)
 
     def read_deltas(self, doc):
         e, i = self.where[doc]

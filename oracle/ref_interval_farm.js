@@ -18,6 +18,17 @@
 //
 // stdin:  {"sets": [{"seed", "clients", "steps", "initialText", "nCheckpoints",
 //                    "maxText", "intervals": p (the chance a step is an interval op)}]}
+//          ext: true also records, per client and checkpoint, the
+//         collection's events since the previous checkpoint (addInterval /
+//         deleteInterval / changeInterval / propertyChanged, with local and the
+//         ends before and after, IIntervalCollectionEvent :1257-1300), its
+//         iteration order (the interval tree's compare order, :276-316, 483-520),
+//         serializeInternal() (:1968-1977, compressInterval :137-149), and
+//         (each event's last field true when a merge-tree op raised it: an end
+//         sliding off a removed segment, the position change listeners :1023-1058)
+//         queries at seeded positions: findOverlappingIntervals, previousInterval,
+//         nextInterval and the start / end position iterators (:881-913,
+//         :1987-2067); the queries draw from their own generator
 // stdout: {"sets": [{..params, "names", "log": [[clientId, seq, ref, msn, kind, contents]]
 //                    (kind "op": a merge-tree op; "iv": {opName, value}),
 //                    "events": per client [["L"|"A", logIndex] | ["I", logIndex]
@@ -82,8 +93,19 @@ function runSet(p) {
     const emitter = { emit(opName, _prev, params) { sent[i] = { opName, value: clone(params) }; } };
     const coll = factory.load(emitter, []);
     coll.attachGraph(c, LABEL);
-    return { c, coll, lastSeq: 0, ids: [] };
+    const X = { c, coll, lastSeq: 0, ids: [], ev: [], mt: false };
+    if (p.ext) {
+      const pos = (r) => c.localReferencePositionToPosition(r);
+      coll.on("addInterval", (ival, local, op) => X.ev.push(["add", ival.getIntervalId(), local, !!op, X.mt]));
+      coll.on("deleteInterval", (ival, local, op) => X.ev.push(["delete", ival.getIntervalId(), local, !!op, X.mt]));
+      coll.on("changeInterval", (ival, prev, local, op) => X.ev.push(["change", ival.getIntervalId(), local, !!op,
+        pos(prev.start), pos(prev.end), pos(ival.start), pos(ival.end), X.mt]));
+      coll.on("propertyChanged", (ival, deltas, local, op) => X.ev.push(["props", ival.getIntervalId(), local, !!op,
+        sortKeys(clone(deltas)), X.mt]));
+    }
+    return X;
   });
+  const Q = rng(p.seed ^ 0x5bd1e995);
   const cursor = names.map(() => 0);
   const events = names.map(() => []);
   const log = [];
@@ -98,7 +120,9 @@ function runSet(p) {
       type: "op", contents: m[5] };
     const X = clients[i];
     if (m[4] === "op") {
+      X.mt = true;
       X.c.applyMsg(msg);
+      X.mt = false;
     } else {
       ops.get(m[5].opName).process(X.coll, clone(m[5].value), m[0] === names[i], msg);
     }
@@ -116,7 +140,22 @@ function runSet(p) {
         X.c.localReferencePositionToPosition(ival.end), sortKeys(props)]);
     }
     out.sort((a, b) => (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0));
-    return { text, intervals: out };
+    if (!p.ext) return { text, intervals: out };
+    const ids = (xs) => xs.map((x) => x.getIntervalId());
+    const n = X.c.getLength();
+    const queries = [];
+    for (let q = 0; q < 4; q++) {
+      const a = Q.int(0, n + 1), b = Q.int(a - 1, n + 2);
+      const it = (f) => ids(Array.from(f));
+      queries.push([a, b, ids(X.coll.findOverlappingIntervals(a, b)),
+        ids([X.coll.previousInterval(a)].filter(Boolean)), ids([X.coll.nextInterval(a)].filter(Boolean)),
+        it(X.coll.CreateForwardIteratorWithStartPosition(a)), it(X.coll.CreateBackwardIteratorWithStartPosition(a)),
+        it(X.coll.CreateForwardIteratorWithEndPosition(b)), it(X.coll.CreateBackwardIteratorWithEndPosition(b))]);
+    }
+    const st = { text, intervals: out, order: ids(Array.from(X.coll)), events: X.ev,
+      summary: clone(X.coll.serializeInternal()), queries };
+    X.ev = [];
+    return st;
   };
   const checkpoint = () => {
     checkpoints.push({ done: events.map((e) => e.length), states: clients.map(readOut) });
@@ -160,6 +199,7 @@ function runSet(p) {
     } else if (R.next() < 0.5) {
       // a merge-tree op (as oracle/ref_farm.js)
       let op;
+      X.mt = true;
       if (len < 4 || (R.next() < 0.4 && len < p.maxText)) {
         const pos = R.int(0, len);
         const seg = new TextSegment(names[i].repeat(R.int(1, 3)));
@@ -170,6 +210,7 @@ function runSet(p) {
         if (R.next() < 0.7) op = X.c.removeRangeLocal(start, end);
         else op = X.c.annotateRangeLocal(start, end, { [KEYS[R.int(0, 2)]]: R.int(0, 5) }, undefined);
       }
+      X.mt = false;
       if (op) send(i, "op", clone(op));
     } else {
       const j = R.int(0, p.clients - 1);

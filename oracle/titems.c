@@ -1656,6 +1656,29 @@ int oti_read_deltas(oti_ctx* c, uint32_t doc, mte_delta* out, uint64_t cap, uint
 /* referencePositionToLocalPosition (mergeTree.ts:1095-1112) of slots [0, n),
  * as oracle.c: -1 for a detached or unused slot or a unit no item holds (its
  * segment unlinked by the zamboni) */
+/* mte_read_ref_order: the index, among every unit the document holds, of the
+ * unit each reference sits on (-1 detached / unused) */
+int oti_read_ref_order(oti_ctx* c, uint32_t doc, int64_t* key, uint32_t n) {
+  if (!c || (n && !key) || doc >= c->n_docs) return MTE_E_INVALID_ARG;
+  const idoc* d = &c->docs[doc];
+  for (uint32_t r = 0; r < n; r++) {
+    key[r] = -1;
+    if (r >= d->ref_hi) continue;
+    const uint32_t st = d->ref_state[r], u = d->ref_anchor[r];
+    if (!(st & REF_LIVE) || (st & REF_DETACHED)) continue;
+    int64_t p = 0;
+    for (uint32_t i = 0; i < d->n; i++) {
+      const item* g = &d->it[i];
+      if (!g->empty && u - g->toff < (uint32_t)g->len) {
+        key[r] = p + (int64_t)(u - g->toff);
+        break;
+      }
+      p += g->empty ? 0 : g->len;
+    }
+  }
+  return MTE_OK;
+}
+
 int oti_read_refs(oti_ctx* c, uint32_t doc, int32_t* pos, uint32_t n) {
   if (!c || (n && !pos) || doc >= c->n_docs) return MTE_E_INVALID_ARG;
   const idoc* d = &c->docs[doc];

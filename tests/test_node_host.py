@@ -26,7 +26,7 @@ pytestmark = pytest.mark.skipif(NODE is None, reason="node not installed")
 EXPORTS = ["abiVersion", "strerror", "create", "destroy", "lastError", "loadDocs", "loadSegments", "readSegments", "submit", "run",
            "sync", "reset", "digest", "docStatus", "readDoc", "stats", "commUniqueId", "commInit", "commShare",
            "commBarrier", "commAllreduce", "commGatherDigests", "commDestroy", "readDeltas", "setEventCapacity",
-           "setRefCapacity", "readRefs"]
+           "setRefCapacity", "readRefs", "readRefOrder"]
 
 
 def node(*args, timeout=300):
@@ -77,7 +77,8 @@ def test_js_packing_matches_python_packing_on_fixtures(fresh):
             assert base64.b64decode(j[key]) == np.ascontiguousarray(arr).tobytes(), (r, key)
 
 
-@pytest.mark.parametrize("vectors", ["farm_vectors.json.gz", "reconnect_vectors.json.gz", "localref_vectors.json.gz"])
+@pytest.mark.parametrize("vectors", ["farm_vectors.json.gz", "reconnect_vectors.json.gz", "localref_vectors.json.gz",
+                                     "relpos_farm_vectors.json.gz"])
 def test_js_packing_matches_python_packing_on_local_farms(vectors):
     """Local ops and acks (and, on the reconnect farms, ops held offline and
     regeneratePendingOp's MTE_OP_REGEN records): the JS and Python packers emit

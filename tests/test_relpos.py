@@ -207,3 +207,28 @@ def test_gpu_relpos_chunked_context():
     d2.load_docs(inits2, np.zeros(0, np.uint16))
     d2.apply_batch(sub)
     assert d2.statuses()[0] == 0 and d2.read_doc(0)["text"] == "helo"
+
+
+@pytest.mark.gpu
+def test_node_relpos_every_client_on_gpu():
+    """Every client a BatchClient ({localClient, events}) through the N-API host
+    (tests/node/reconnect_gpu.js): annotateMarker and relative-position ops
+    through applyLocalOp return the reference's ops, every state at every
+    checkpoint and every regenerated op equal the reference's."""
+    import shutil
+    import subprocess
+
+    from fixtures_util import canon_regen
+    if shutil.which("node") is None:
+        pytest.skip("node not installed")
+    r = subprocess.run([shutil.which("node"), "tests/node/reconnect_gpu.js", "all", NAME], cwd=os.path.dirname(HERE),
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    assert j["pending"] == 0 and j["nBadOps"] == 0, j["badOps"]
+    bad = [x for x in j["states"] if not x[3]]
+    assert not bad, bad[:3]
+    assert len(j["states"]) == 768
+    bad_regen = [x for x in j["regens"] if canon_regen(x[2], x[4], False) != canon_regen(x[3], x[4], False)]
+    assert not bad_regen, bad_regen[:2]
+    assert len(j["regens"]) == 658
