@@ -275,6 +275,13 @@ class IntervalCollection {
   _load(serialized) {
     const list = Array.isArray(serialized) ? serialized
       : serialized.intervals.map((x) => decompressInterval(x, serialized.label));
+    const n = list.length ? this.client.getLength() : 0;
+    for (const v of list) {
+      // createPositionReferenceFromSegoff without a segment (:629-636)
+      if (!(v.start >= 0 && v.start < n && v.end >= 0 && v.end < n)) {
+        throw new MergeTreeError(-1, "Non-transient references need segment");
+      }
+    }
     for (const v of list) {
       this._ensureId(v);
       const ival = this._create(v.start, v.end, v.intervalType, undefined, true);

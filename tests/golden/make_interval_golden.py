@@ -12,7 +12,12 @@ client catching up with the sequenced log at its own pace.  The file holds the
 messages, each client's event order and, at checkpoints, each client's text
 and intervals (id, start and end positions, properties).  Build container only.
 
-Usage: python3 tests/golden/make_interval_golden.py
+With --ext it writes tests/golden/interval_ext_vectors.json.gz: farms that also
+record, per client and checkpoint, the collection's events, its iteration
+order, serializeInternal() and seeded queries (findOverlappingIntervals,
+previousInterval / nextInterval, the start / end position iterators).
+
+Usage: python3 tests/golden/make_interval_golden.py [--ext]
 """
 import gzip
 import json
@@ -27,21 +32,30 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
 import ref_util  # noqa: E402
 
 OUT = os.path.join(HERE, "interval_vectors.json.gz")
+OUT_EXT = os.path.join(HERE, "interval_ext_vectors.json.gz")
 FARM_JS = os.path.join(ROOT, "oracle", "ref_interval_farm.js")
 # (seed, clients incl. the observer, steps, initial text, checkpoints, text bound, interval-op chance)
 SETS = [(9000 + i, 2 + i % 5, 300 + 100 * (i % 4), ["", "hello world", "abc\ndef"][i % 3], 5, [64, 200][i % 2],
          [0.2, 0.35, 0.5][i % 3]) for i in range(30)]
 
 
+# ext: (seed, clients, steps, initial text, checkpoints, text bound, interval-op chance)
+EXT_SETS = [(9500 + i, 2 + i % 4, 200 + 100 * (i % 3), ["hello world", "", "abc\ndef"][i % 3], 4, [64, 200][i % 2],
+             [0.3, 0.45][i % 2]) for i in range(12)]
+
+
 def main():
     if not ref_util.ref_available():
         sys.exit("the reference sources are not in this container")
     out = ref_util.build_ref()
+    ext = "--ext" in sys.argv[1:]
     res = {"sets": [], "generator": "oracle/ref_interval_farm.js (reference Client + IntervalCollection)"}
     failed = []
-    for sd, c, n, t, k, m, iv in SETS:
+    for sd, c, n, t, k, m, iv in (EXT_SETS if ext else SETS):
         one = {"seed": sd, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
                "intervals": iv}
+        if ext:
+            one["ext"] = True
         q = subprocess.run(["node", FARM_JS, out], input=json.dumps({"sets": [one]}), capture_output=True,
                            text=True, timeout=600)
         if q.returncode == 0:
@@ -49,10 +63,10 @@ def main():
         else:
             failed.append((sd, q.stderr.strip().splitlines()[-1:]))
     res["seeds_the_reference_failed"] = failed
-    with gzip.open(OUT, "wt", encoding="utf-8") as fh:
+    with gzip.open(OUT_EXT if ext else OUT, "wt", encoding="utf-8") as fh:
         json.dump(res, fh, separators=(",", ":"))
     n_iv = sum(1 for s in res["sets"] for e in s["log"] if e[4] == "iv")
-    print(f"wrote {OUT}: {len(res['sets'])} farms, {n_iv} interval ops, failed {failed}")
+    print(f"wrote {OUT_EXT if ext else OUT}: {len(res['sets'])} farms, {n_iv} interval ops, failed {failed}")
 
 
 if __name__ == "__main__":

@@ -15,14 +15,22 @@
 //                   checkpoint with the batch (base64) and, per client, its
 //                   intervals as [id, start slot, end slot, properties], for
 //                   tests/test_intervals.py to replay on the restatement.
+//   argv[2] "ext":  as "gpu" on interval_ext_vectors.json.gz (argv[4]), and at
+//                   every checkpoint also the collection's events since the
+//                   last one (those a merge-tree op raises excepted: ends that
+//                   slid, see intervals.js), its iteration order,
+//                   serializeInternal() and the recorded queries; then each
+//                   set's final summary loads into a fresh client whose
+//                   intervals must equal the reference's.
 const fs = require("fs");
 const path = require("path");
 const zlib = require("zlib");
 const { MergeTreeEngine } = require("../../fluidframework_amd/node");
 
 const mode = process.argv[2] || "gpu";
+const ext = mode === "ext";
 const sets = JSON.parse(zlib.gunzipSync(fs.readFileSync(path.join(__dirname, "..", "golden",
-  "interval_vectors.json.gz"))).toString("utf8")).sets;
+  process.argv[4] || (ext ? "interval_ext_vectors.json.gz" : "interval_vectors.json.gz")))).toString("utf8")).sets;
 const nSets = process.argv[3] && process.argv[3] !== "all" ? Number(process.argv[3]) : sets.length;
 const LABEL = "farm";
 
@@ -34,6 +42,7 @@ function sortKeys(v) {
   }
   return v;
 }
+const clone = (v) => JSON.parse(JSON.stringify(v));
 const b64 = (a) => Buffer.from(a.buffer, a.byteOffset, a.byteLength).toString("base64");
 
 // pack mode: the N-API surface the engine uses, recording the submitted batches
@@ -54,14 +63,34 @@ for (let si = 0; si < nSets; si++) {
     L.client = eng.createClient(sets[si].initialText, { newLengthCalc: true, localClient: true, refs: true,
       longClientId: name });
     L.coll = L.client.getIntervalCollection(LABEL, { emit(opName, _p, value) { L.sent = { opName, value }; } });
+    if (ext) {
+      L.ev = [];
+      const pos = (r) => L.client.localReferencePositionToPosition(r);
+      L.coll.on("addInterval", (x, local, op) => L.ev.push(["add", x.getIntervalId(), local, !!op, false]));
+      L.coll.on("deleteInterval", (x, local, op) => L.ev.push(["delete", x.getIntervalId(), local, !!op, false]));
+      L.coll.on("changeInterval", (x, prev, local, op) => L.ev.push(["change", x.getIntervalId(), local, !!op,
+        pos(prev.start), pos(prev.end), pos(x.start), pos(x.end), false]));
+      L.coll.on("propertyChanged", (x, deltas, local, op) => L.ev.push(["props", x.getIntervalId(), local, !!op,
+        sortKeys(clone(deltas)), false]));
+    }
     layout.push(L);
   });
+}
+// ext: a loader client per set, of its final text, for the summary load below
+const loaders = [];
+if (ext) {
+  for (let si = 0; si < nSets; si++) {
+    const s = sets[si];
+    const last = s.checkpoints[s.checkpoints.length - 1].states[0];
+    loaders.push(eng.createClient(last.text, { newLengthCalc: true, localClient: true, refs: true,
+      longClientId: "loader" + si }));
+  }
 }
 eng.start();
 const prev = layout.map(() => 0);
 const failures = [];
+const extFail = {};
 let passed = 0, opsChecked = 0;
-const clone = (v) => JSON.parse(JSON.stringify(v));
 const nCp = Math.max.apply(null, sets.slice(0, nSets).map((s) => s.checkpoints.length));
 for (let j = 0; j < nCp; j++) {
   layout.forEach((L, d) => {
@@ -135,13 +164,60 @@ for (let j = 0; j < nCp; j++) {
     });
     ivs.sort((a, b) => (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0));
     const text = L.client.getText();
-    if (text === want.text && JSON.stringify(ivs) === JSON.stringify(want.intervals)) passed++;
-    else failures.push([L.si, L.ci, j, "state", ivs.slice(0, 3), want.intervals.slice(0, 3)]);
+    let ok = text === want.text && JSON.stringify(ivs) === JSON.stringify(want.intervals);
+    if (!ok) failures.push([L.si, L.ci, j, "state", ivs.slice(0, 3), want.intervals.slice(0, 3)]);
+    if (ext && ok) {
+      const ids = (xs) => xs.map((x) => x.getIntervalId());
+      const evWant = want.events.filter((e) => !e[e.length - 1]);
+      const got = { events: L.ev, order: ids(Array.from(L.coll)), summary: clone(L.coll.serializeInternal()),
+        queries: want.queries.map(([a, b]) => [a, b, ids(L.coll.findOverlappingIntervals(a, b)),
+          ids([L.coll.previousInterval(a)].filter(Boolean)), ids([L.coll.nextInterval(a)].filter(Boolean)),
+          ids(Array.from(L.coll.CreateForwardIteratorWithStartPosition(a))),
+          ids(Array.from(L.coll.CreateBackwardIteratorWithStartPosition(a))),
+          ids(Array.from(L.coll.CreateForwardIteratorWithEndPosition(b))),
+          ids(Array.from(L.coll.CreateBackwardIteratorWithEndPosition(b)))]) };
+      for (const k of ["events", "order", "summary", "queries"]) {
+        const w = k === "events" ? evWant : want[k];
+        if (JSON.stringify(sortKeys(got[k])) !== JSON.stringify(sortKeys(w))) {
+          ok = false;
+          extFail[k] = (extFail[k] || 0) + 1;
+          failures.push([L.si, L.ci, j, k, got[k], w]);
+          break;
+        }
+      }
+      L.ev = [];
+    }
+    if (ok) passed++;
   });
 }
+let loaded = 0, unloadable = 0;
+if (ext) {
+  // each set's observer summary (serializeInternal at the last checkpoint)
+  // loaded into a fresh client of the same text: the reference's intervals
+  for (let si = 0; si < nSets; si++) {
+    const s = sets[si];
+    const last = s.checkpoints[s.checkpoints.length - 1].states[0];
+    // an end outside the text (detached) makes the reference's load throw
+    // ("Non-transient references need segment", :629-636): those sets load nothing
+    if (last.intervals.some((x) => x[1] < 0 || x[2] < 0 || x[1] >= last.text.length || x[2] >= last.text.length)) {
+      unloadable++;
+      continue;
+    }
+    const c = loaders[si];
+    const coll = c.getIntervalCollection(LABEL, null, last.summary);
+    const ivs = Array.from(coll.byId.values()).map((x) => {
+      const [a, b] = x.positions();
+      return [x.getIntervalId(), a, b, sortKeys(x.properties)];
+    });
+    ivs.sort((a, b) => (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0));
+    if (JSON.stringify(ivs) === JSON.stringify(last.intervals) &&
+        JSON.stringify(sortKeys(clone(coll.serializeInternal()))) === JSON.stringify(sortKeys(last.summary))) loaded++;
+    else failures.push([si, "load", ivs.slice(0, 3), last.intervals.slice(0, 3)]);
+  }
+}
 if (mode !== "pack") {
-  process.stdout.write(JSON.stringify({ passed, opsChecked, failures: failures.slice(0, 4), nFailures: failures.length,
-    docs: layout.length }) + "\n");
+  process.stdout.write(JSON.stringify({ passed, opsChecked, loaded, unloadable, extFail, failures: failures.slice(0, 4),
+    nFailures: failures.length, docs: layout.length }) + "\n");
 } else {
   process.stdout.write(JSON.stringify({ done: true, opsChecked, failures: failures.slice(0, 4),
     nFailures: failures.length }) + "\n");

@@ -144,3 +144,33 @@ def test_node_interval_farms_on_gpu():
     assert j["nFailures"] == 0, j["failures"]
     sets = interval_sets()
     assert j["passed"] == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
+
+
+def ext_sets():
+    with gzip.open(os.path.join(HERE, "golden", "interval_ext_vectors.json.gz"), "rt", encoding="utf-8") as fh:
+        return json.load(fh)
+
+
+def test_interval_ext_vectors_shape():
+    v = ext_sets()
+    sets = v["sets"]
+    assert len(sets) == 11 and [x[0] for x in v["seeds_the_reference_failed"]] == [9508]
+    states = [st for s in sets for cp in s["checkpoints"] for st in cp["states"]]
+    assert all({"events", "order", "summary", "queries"} <= set(st) for st in states)
+    kinds = {(e[0], e[-1]) for st in states for e in st["events"]}
+    assert {("add", False), ("delete", False), ("change", False), ("props", False), ("change", True)} <= kinds
+
+
+@pytest.mark.gpu
+def test_node_interval_events_order_queries_summaries_on_gpu():
+    """IntervalCollection events (addInterval / deleteInterval / changeInterval /
+    propertyChanged, except those a merge-tree op raises), the tree's order,
+    serializeInternal() and findOverlappingIntervals / previousInterval /
+    nextInterval / the position iterators equal the reference's at every
+    checkpoint of the ext farms, and every loadable final summary loads into a
+    fresh client with the reference's intervals."""
+    j = json.loads(node("tests/node/interval_farm.js", "ext").strip().splitlines()[-1])
+    assert j["nFailures"] == 0, (j["extFail"], j["failures"])
+    sets = ext_sets()["sets"]
+    assert j["passed"] == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
+    assert j["loaded"] + j["unloadable"] == len(sets) and j["loaded"] > 0
