@@ -302,23 +302,40 @@ __device__ __forceinline__ int ht_first_lp(HT& h, int lo, F pred) {
 
 // ---- moves -------------------------------------------------------------------------
 
+// planes moved per batch of loads: kHtGroup planes' loads in flight at once,
+// then their stores (one memory round trip per group, not per plane)
+constexpr int kHtGroup = 8;
+
+__device__ __forceinline__ uint32_t* ht_plane(const HT& h, int p) {  // p == nP: the tree word
+  return p < h.nP ? h.pl + (uint64_t)p * h.sd : h.tw;
+}
+
 // open an empty slot at g: items [g, n) move up by one (titems.c open_slot)
 __device__ void ht_open(HT& h, int g) {
   const int l = lane_id();
   for (int te = h.n; te > g; te -= kHT) {
     const int tb = te - kHT > g ? te - kHT : g;
-    for (int p = 0; p <= h.nP; p++) {  // p == nP: the tree word
-      uint32_t* base = p < h.nP ? h.pl + (uint64_t)p * h.sd : h.tw;
-      uint32_t v[kHE];
+    for (int p0 = 0; p0 <= h.nP; p0 += kHtGroup) {
+      uint32_t v[kHtGroup][kHE];
 #pragma unroll
-      for (int j = 0; j < kHE; j++) {
-        const int i = tb + j * kWave + l;
-        v[j] = ld_l2(base + (i < te ? i : tb));
+      for (int q = 0; q < kHtGroup; q++) {
+        const int p = p0 + q <= h.nP ? p0 + q : h.nP;  // past the last plane: reload it, stored never
+        const uint32_t* base = ht_plane(h, p);
+#pragma unroll
+        for (int j = 0; j < kHE; j++) {
+          const int i = tb + j * kWave + l;
+          v[q][j] = ld_l2(base + (i < te ? i : tb));
+        }
       }
 #pragma unroll
-      for (int j = 0; j < kHE; j++) {
-        const int i = tb + j * kWave + l;
-        if (i < te) base[i + 1] = v[j];
+      for (int q = 0; q < kHtGroup; q++) {
+        if (p0 + q > h.nP) break;
+        uint32_t* base = ht_plane(h, p0 + q);
+#pragma unroll
+        for (int j = 0; j < kHE; j++) {
+          const int i = tb + j * kWave + l;
+          if (i < te) base[i + 1] = v[q][j];
+        }
       }
     }
   }
@@ -356,17 +373,26 @@ __device__ void ht_compact(HT& h, int lo, int hi) {
       kept += rdlane(incl, kWave - 1);
     }
     if (w != tb || kept != (h.n - tb < kHT ? h.n - tb : kHT)) {
-      for (int p = 0; p <= h.nP; p++) {
-        uint32_t* base = p < h.nP ? h.pl + (uint64_t)p * h.sd : h.tw;
-        uint32_t v[kHE];
+      for (int p0 = 0; p0 <= h.nP; p0 += kHtGroup) {
+        uint32_t v[kHtGroup][kHE];
 #pragma unroll
-        for (int j = 0; j < kHE; j++) {
-          const int i = tb + j * kWave + l;
-          v[j] = ld_l2(base + (keep[j] ? i : tb));
+        for (int q = 0; q < kHtGroup; q++) {
+          const int p = p0 + q <= h.nP ? p0 + q : h.nP;
+          const uint32_t* base = ht_plane(h, p);
+#pragma unroll
+          for (int j = 0; j < kHE; j++) {
+            const int i = tb + j * kWave + l;
+            v[q][j] = ld_l2(base + (keep[j] ? i : tb));
+          }
         }
 #pragma unroll
-        for (int j = 0; j < kHE; j++)
-          if (keep[j]) base[dst[j]] = v[j];
+        for (int q = 0; q < kHtGroup; q++) {
+          if (p0 + q > h.nP) break;
+          uint32_t* base = ht_plane(h, p0 + q);
+#pragma unroll
+          for (int j = 0; j < kHE; j++)
+            if (keep[j]) base[dst[j]] = v[q][j];
+        }
       }
     }
     w += kept;
@@ -1361,10 +1387,32 @@ constexpr int kLdsMargin = 16;
 __device__ void ht_move(uint32_t* dpl, uint64_t dsd, uint32_t* dtw, uint32_t* dhp, const uint32_t* spl, uint64_t ssd,
                         const uint32_t* stw, const uint32_t* shp, int nP, int n, uint32_t hn) {
   const int l = lane_id();
-  for (int p = 0; p <= nP; p++) {
-    const uint32_t* sp = p < nP ? spl + (uint64_t)p * ssd : stw;
-    uint32_t* dp = p < nP ? dpl + (uint64_t)p * dsd : dtw;
-    for (int i = l; i < n; i += kWave) dp[i] = ld_l2(sp + i);
+  // tiles of kHT items, kHtGroup planes' loads in flight before their stores
+  for (int tb = 0; tb < n; tb += kHT) {
+    for (int p0 = 0; p0 <= nP; p0 += kHtGroup) {
+      uint32_t v[kHtGroup][kHE];
+#pragma unroll
+      for (int q = 0; q < kHtGroup; q++) {
+        const int p = p0 + q <= nP ? p0 + q : nP;
+        const uint32_t* sp = p < nP ? spl + (uint64_t)p * ssd : stw;
+#pragma unroll
+        for (int j = 0; j < kHE; j++) {
+          const int i = tb + j * kWave + l;
+          v[q][j] = ld_l2(sp + (i < n ? i : 0));
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kHtGroup; q++) {
+        if (p0 + q > nP) break;
+        const int p = p0 + q;
+        uint32_t* dp = p < nP ? dpl + (uint64_t)p * dsd : dtw;
+#pragma unroll
+        for (int j = 0; j < kHE; j++) {
+          const int i = tb + j * kWave + l;
+          if (i < n) dp[i] = v[q][j];
+        }
+      }
+    }
   }
   for (uint32_t k = 1 + (uint32_t)l; k <= hn; k += kWave) {
     dhp[2 * k] = ld_l2(shp + 2 * k);

@@ -146,7 +146,12 @@ function runSet(p) {
     const queries = [];
     for (let q = 0; q < 4; q++) {
       const a = Q.int(0, n + 1), b = Q.int(a - 1, n + 2);
-      const it = (f) => ids(Array.from(f));
+      // IntervalCollectionIterator is an Iterator, not an Iterable (:1222-1250): drain it with next()
+      const it = (f) => {
+        const out = [];
+        for (let r = f.next(); !r.done; r = f.next()) out.push(r.value);
+        return ids(out);
+      };
       queries.push([a, b, ids(X.coll.findOverlappingIntervals(a, b)),
         ids([X.coll.previousInterval(a)].filter(Boolean)), ids([X.coll.nextInterval(a)].filter(Boolean)),
         it(X.coll.CreateForwardIteratorWithStartPosition(a)), it(X.coll.CreateBackwardIteratorWithStartPosition(a)),

@@ -89,7 +89,7 @@ if (ext) {
 eng.start();
 const prev = layout.map(() => 0);
 const failures = [];
-const extFail = {};
+const extFail = {}, extFirst = {};
 let passed = 0, opsChecked = 0;
 const nCp = Math.max.apply(null, sets.slice(0, nSets).map((s) => s.checkpoints.length));
 for (let j = 0; j < nCp; j++) {
@@ -181,6 +181,7 @@ for (let j = 0; j < nCp; j++) {
         if (JSON.stringify(sortKeys(got[k])) !== JSON.stringify(sortKeys(w))) {
           ok = false;
           extFail[k] = (extFail[k] || 0) + 1;
+          if (!extFirst[k]) extFirst[k] = [L.si, L.ci, j, got[k], w];
           failures.push([L.si, L.ci, j, k, got[k], w]);
           break;
         }
@@ -216,7 +217,7 @@ if (ext) {
   }
 }
 if (mode !== "pack") {
-  process.stdout.write(JSON.stringify({ passed, opsChecked, loaded, unloadable, extFail, failures: failures.slice(0, 4),
+  process.stdout.write(JSON.stringify({ passed, opsChecked, loaded, unloadable, extFail, extFirst, failures: failures.slice(0, 4),
     nFailures: failures.length, docs: layout.length }) + "\n");
 } else {
   process.stdout.write(JSON.stringify({ done: true, opsChecked, failures: failures.slice(0, 4),

@@ -170,7 +170,7 @@ def test_node_interval_events_order_queries_summaries_on_gpu():
     checkpoint of the ext farms, and every loadable final summary loads into a
     fresh client with the reference's intervals."""
     j = json.loads(node("tests/node/interval_farm.js", "ext").strip().splitlines()[-1])
-    assert j["nFailures"] == 0, (j["extFail"], j["failures"])
+    assert j["nFailures"] == 0, (j["extFail"], j["extFirst"], j["failures"][:2])
     sets = ext_sets()["sets"]
     assert j["passed"] == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
     assert j["loaded"] + j["unloadable"] == len(sets) and j["loaded"] > 0
