@@ -34,7 +34,10 @@
 
 namespace mte {
 
-constexpr int kHE = 4;                 // items per lane per tile
+#ifndef MTE_HTREE_KHE
+#define MTE_HTREE_KHE 4
+#endif
+constexpr int kHE = MTE_HTREE_KHE;     // items per lane per tile
 constexpr int kHT = kWave * kHE;       // items per tile
 constexpr uint32_t kHdrTreeHbm = kHdrTreeHbmFlag;  // a legacy document continues on the HBM tree pass
 constexpr int kHtState = 8;            // state words per document
@@ -172,7 +175,7 @@ __device__ __forceinline__ void ht_inval(HT& h, int from) {
 }
 
 // L / P valid through item `upto` (or the document's end)
-__device__ void ht_ensure(HT& h, int upto) {
+__device__ __forceinline__ void ht_ensure(HT& h, int upto) {
   const int l = lane_id();
   bool wrote = false;
   while (h.lp_n <= upto && h.lp_n < h.n) {
@@ -311,7 +314,7 @@ __device__ __forceinline__ uint32_t* ht_plane(const HT& h, int p) {  // p == nP:
 }
 
 // open an empty slot at g: items [g, n) move up by one (titems.c open_slot)
-__device__ void ht_open(HT& h, int g) {
+__device__ __forceinline__ void ht_open(HT& h, int g) {
   const int l = lane_id();
   for (int te = h.n; te > g; te -= kHT) {
     const int tb = te - kHT > g ? te - kHT : g;
@@ -356,7 +359,7 @@ __device__ __forceinline__ void ht_copy_item(HT& h, int from, int to) {
 
 // drop the items i in [lo, hi] whose flag (L scratch) is set; the others keep
 // their order (titems.c compact)
-__device__ void ht_compact(HT& h, int lo, int hi) {
+__device__ __forceinline__ void ht_compact(HT& h, int lo, int hi) {
   const int l = lane_id();
   int w = lo;
   for (int tb = lo; tb < h.n; tb += kHT) {
@@ -433,7 +436,7 @@ __device__ __forceinline__ void ht_set_h(HT& h, int i, uint32_t hv, bool clear_n
 }
 
 // split_cascade (titems.c): a leaf block gained a child at item i
-__device__ void ht_split_cascade(HT& h, int i) {
+__device__ __forceinline__ void ht_split_cascade(HT& h, int i) {
   for (int k = 1;; k++) {
     const int s = ht_span_start(h, i, k), e = ht_span_end(h, s, k);
     if (ht_children(h, s, e, k) < kMaxNodes) return;
@@ -460,7 +463,7 @@ __device__ __forceinline__ void ht_hput(HT& h, uint32_t k, uint2 v) {
   }
 }
 
-__device__ int ht_heap_add(HT& h, int32_t key, uint32_t id) {
+__device__ __forceinline__ int ht_heap_add(HT& h, int32_t key, uint32_t id) {
   if (h.hn >= h.hcap) return MTE_E_CAPACITY;
   uint32_t k = ++h.hn;
   while (k > 1) {  // the same comparisons as heap.ts fixup, moving a hole
@@ -475,7 +478,7 @@ __device__ int ht_heap_add(HT& h, int32_t key, uint32_t id) {
   return 0;
 }
 
-__device__ uint2 ht_heap_pop(HT& h) {
+__device__ __forceinline__ uint2 ht_heap_pop(HT& h) {
   const uint2 x = ht_hget(h, 1);
   const uint2 cur = ht_hget(h, h.hn);
   h.hn--;
@@ -501,7 +504,7 @@ __device__ uint2 ht_heap_pop(HT& h) {
 }
 
 // add_lru (titems.c): addToLRUSet for the leaf headed at item i
-__device__ int ht_add_lru(HT& h, int i, int32_t seq, int& bs_cache, int& be_cache) {
+__device__ __forceinline__ int ht_add_lru(HT& h, int i, int32_t seq, int& bs_cache, int& be_cache) {
   int bs;
   if (i >= bs_cache && i <= be_cache) {
     bs = bs_cache;
@@ -555,7 +558,7 @@ __device__ __forceinline__ void ht_mark(HT& h, int a, int b, int32_t f) {
 // unlinked items, turns appended leaves into continuations; returns the
 // logical leaves held.  The caller cleared the flags of [s, e].
 template <int K>
-__device__ int ht_scour(HT& h, int s, int e, uint32_t n_keys) {
+__device__ __forceinline__ int ht_scour(HT& h, int s, int e, uint32_t n_keys) {
   int held = 0;
   int prev = -1;             // head of the leaf appends go to
   int32_t prev_len = 0;
@@ -624,7 +627,7 @@ __device__ int ht_scour(HT& h, int s, int e, uint32_t n_keys) {
 
 // titems.c drop_keep_starts over [s, e]: every block start moves to a kept
 // item of its block; a block left with no leaf keeps a placeholder
-__device__ void ht_drop_keep_starts(HT& h, int s, int e) {
+__device__ __forceinline__ void ht_drop_keep_starts(HT& h, int s, int e) {
   const int32_t* Lf = h.L;
   for (int b = s; b <= e;) {
     const int be = ht_span_end(h, b, 1);
@@ -661,7 +664,7 @@ __device__ __forceinline__ bool group_start_h(int r, int base, int rem) {
 // mergeTree.ts:764-786), setting h = top for the first, else `hv`, and `other`
 // on the rest of the ranked items (other < 0: left alone)
 template <typename F>
-__device__ void ht_regroup(HT& h, int s, int e, int total, uint32_t top, uint32_t hv, int other, bool clear_ns,
+__device__ __forceinline__ void ht_regroup(HT& h, int s, int e, int total, uint32_t top, uint32_t hv, int other, bool clear_ns,
                            F pred) {
   int cc = total / (kMaxNodes / 2) < kMaxNodes - 1 ? total / (kMaxNodes / 2) : kMaxNodes - 1;
   if (cc < 1) cc = 1;
@@ -691,20 +694,20 @@ __device__ void ht_regroup(HT& h, int s, int e, int total, uint32_t top, uint32_
 }
 
 template <int K>
-__device__ int ht_pack_parent(HT& h, int s, int p, uint32_t n_keys, int& status);
+__device__ __forceinline__ int ht_pack_parent(HT& h, int s, int p, uint32_t n_keys, int& status);
 
 // zamboniSegments (titems.c zamboni): at most two scours
 template <int K>
-__device__ int ht_zamboni_body(HT& h, uint32_t n_keys);
+__device__ __forceinline__ int ht_zamboni_body(HT& h, uint32_t n_keys);
 template <int K>
-__device__ int ht_zamboni(HT& h, uint32_t n_keys) {
+__device__ __forceinline__ int ht_zamboni(HT& h, uint32_t n_keys) {
   HPROF_BEGIN(t0)
   const int rc = ht_zamboni_body<K>(h, n_keys);
   HPROF_END(h, 3, t0)
   return rc;
 }
 template <int K>
-__device__ int ht_zamboni_body(HT& h, uint32_t n_keys) {
+__device__ __forceinline__ int ht_zamboni_body(HT& h, uint32_t n_keys) {
   int status = 0;
   for (int z = 0; z < 2; z++) {
     if (h.hn == 0) break;
@@ -743,7 +746,7 @@ __device__ int ht_zamboni_body(HT& h, uint32_t n_keys) {
 
 // packParent (mergeTree.ts:750-798) of the level-p block starting at s
 template <int K>
-__device__ int ht_pack_parent(HT& h, int s, int p, uint32_t n_keys, int& status) {
+__device__ __forceinline__ int ht_pack_parent(HT& h, int s, int p, uint32_t n_keys, int& status) {
   for (;;) {
     int e = ht_span_end(h, s, p);
     const uint32_t top = t_h(ht_T(h, s));
@@ -814,7 +817,7 @@ __device__ int ht_pack_parent(HT& h, int s, int p, uint32_t n_keys, int& status)
 // ---- ensureIntervalBoundary (titems.c boundary) ---------------------------------------
 
 template <int K, bool S>
-__device__ int ht_boundary(HT& h, int32_t pos, uint32_t (&st)[kNumStats]) {
+__device__ __forceinline__ int ht_boundary(HT& h, int32_t pos, uint32_t (&st)[kNumStats]) {
   const int32_t* Lp = h.L;
   const int32_t* Pp = h.P;
   const int i = ht_first_lp(h, 0, [&](int x) {
@@ -857,7 +860,7 @@ __device__ int ht_boundary(HT& h, int32_t pos, uint32_t (&st)[kNumStats]) {
 // insert's spec (textSegment.ts:40-48, mergeTreeNodes.ts:602-609), its props,
 // nothing pending
 template <int K>
-__device__ void ht_put_new(HT& h, int g, const s8v& op, bool local, uint32_t refd, const ReplayArgs& a) {
+__device__ __forceinline__ void ht_put_new(HT& h, int g, const s8v& op, bool local, uint32_t refd, const ReplayArgs& a) {
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   const bool marker = (flags & MTE_F_MARKER) != 0;
@@ -887,7 +890,7 @@ __device__ void ht_put_new(HT& h, int g, const s8v& op, bool local, uint32_t ref
 // insertSegments -> blockInsert -> insertingWalk (mergeTree.ts:1394-1422,
 // 1590-1680, 1723-1825); *at = the new item or -1
 template <int K, bool S>
-__device__ int ht_insert(HT& h, const s8v& op, bool local, bool refd, const ReplayArgs& a, uint32_t (&st)[kNumStats],
+__device__ __forceinline__ int ht_insert(HT& h, const s8v& op, bool local, bool refd, const ReplayArgs& a, uint32_t (&st)[kNumStats],
                          int& at) {
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
@@ -994,7 +997,7 @@ struct EvRun {
 };
 
 template <int K, bool S>
-__device__ int ht_range(HT& h, const s8v& op, bool local, const ReplayArgs& a, uint32_t (&st)[kNumStats], EvOut& ev,
+__device__ __forceinline__ int ht_range(HT& h, const s8v& op, bool local, const ReplayArgs& a, uint32_t (&st)[kNumStats], EvOut& ev,
                         bool evd, uint2* rt, uint32_t rhi) {
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
@@ -1161,7 +1164,7 @@ __device__ int ht_range(HT& h, const s8v& op, bool local, const ReplayArgs& a, u
 // references of the acked removals, adds each segment to the LRU set and runs
 // zamboniSegments
 template <int K>
-__device__ int ht_ack(HT& h, const s8v& op, const ReplayArgs& a, uint2* rt, uint32_t rhi) {
+__device__ __forceinline__ int ht_ack(HT& h, const s8v& op, const ReplayArgs& a, uint2* rt, uint32_t rhi) {
   const int32_t lo = op[4], hi = op[5], s = op[0];
   const uint32_t mask = (uint32_t)op[6];
   const int l = lane_id();
@@ -1240,7 +1243,7 @@ __device__ __forceinline__ int ht_member(const HT& h, int from, uint32_t t, int3
 // markRangeRemoved at seq 0, each followed by zamboniSegments; a remove's are
 // restored
 template <int K>
-__device__ int ht_rollback(HT& h, const s8v& op, const ReplayArgs& a, bool evd, EvOut& ev) {
+__device__ __forceinline__ int ht_rollback(HT& h, const s8v& op, const ReplayArgs& a, bool evd, EvOut& ev) {
   const int32_t ls = op[0];
   const uint32_t t = (uint32_t)op[4];
   int rc;
@@ -1271,7 +1274,7 @@ __device__ int ht_rollback(HT& h, const s8v& op, const ReplayArgs& a, bool evd, 
 // aux (titems.c doc_rollback_annotate): each segment of the group re-annotated
 // by annotateRange at seq 0, which runs zamboniSegments after it
 template <int K>
-__device__ int ht_rollback_annotate(HT& h, uint32_t b, const uint4* aux, uint32_t n_aux, const ReplayArgs& a,
+__device__ __forceinline__ int ht_rollback_annotate(HT& h, uint32_t b, const uint4* aux, uint32_t n_aux, const ReplayArgs& a,
                                     bool evd, EvOut& ev) {
   int rc;
   for (int i = ht_member<K>(h, 0, MTE_OP_ANNOTATE, 0, b); i >= 0; i = ht_member<K>(h, 0, MTE_OP_ANNOTATE, 0, b)) {
@@ -1318,7 +1321,7 @@ __device__ int ht_rollback_annotate(HT& h, uint32_t b, const uint4* aux, uint32_
 // MTE_OP_REGEN (titems.c doc_regen): the group's segments in document order at
 // their positions in the view at localSeq ls, a merged leaf one record
 template <int K>
-__device__ void ht_regen(const HT& h, int32_t ls, uint32_t t, uint32_t slot, EvOut& ev) {
+__device__ __forceinline__ void ht_regen(const HT& h, int32_t ls, uint32_t t, uint32_t slot, EvOut& ev) {
   const int l = lane_id();
   int32_t cy = 0;
   bool prev_hit = false;  // the tile's last item was a record's item (a continuation joins it)
@@ -1384,7 +1387,7 @@ __device__ void ht_regen(const HT& h, int32_t ls, uint32_t t, uint32_t slot, EvO
 // document leaves LDS before a record that could pass its LDS capacity.
 constexpr int kLdsMargin = 16;
 
-__device__ void ht_move(uint32_t* dpl, uint64_t dsd, uint32_t* dtw, uint32_t* dhp, const uint32_t* spl, uint64_t ssd,
+__device__ __forceinline__ void ht_move(uint32_t* dpl, uint64_t dsd, uint32_t* dtw, uint32_t* dhp, const uint32_t* spl, uint64_t ssd,
                         const uint32_t* stw, const uint32_t* shp, int nP, int n, uint32_t hn) {
   const int l = lane_id();
   // tiles of kHT items, kHtGroup planes' loads in flight before their stores
@@ -1422,7 +1425,7 @@ __device__ void ht_move(uint32_t* dpl, uint64_t dsd, uint32_t* dtw, uint32_t* dh
 }
 
 // into the workgroup's LDS (lds: (nP + 5) x lcap + 2 words)
-__device__ void ht_to_lds(HT& h, uint32_t* lds, uint32_t lcap) {
+__device__ __forceinline__ void ht_to_lds(HT& h, uint32_t* lds, uint32_t lcap) {
   h.g_pl = h.pl;
   h.g_sd = h.sd;
   h.g_tw = h.tw;
@@ -1451,7 +1454,7 @@ __device__ void ht_to_lds(HT& h, uint32_t* lds, uint32_t lcap) {
 }
 
 // back to HBM (before a record that could outgrow LDS, and at the end)
-__device__ void ht_spill(HT& h) {
+__device__ __forceinline__ void ht_spill(HT& h) {
   ht_move(h.g_pl, h.g_sd, h.g_tw, h.g_hp, h.pl, h.sd, h.tw, h.hp, h.nP, h.n, h.hn);
   h.pl = h.g_pl;
   h.sd = h.g_sd;
@@ -1477,7 +1480,7 @@ __device__ __forceinline__ bool ht_lds_room(const HT& h) {
 // mergeTree.ts:853-870, the lengths before it; posFromRelativePos :1369-1392),
 // -1 when no held marker carries the id
 template <int K>
-__device__ int32_t ht_marker_pos(HT& h, uint32_t key, uint32_t vid, bool local, int32_t r, int c) {
+__device__ __forceinline__ int32_t ht_marker_pos(HT& h, uint32_t key, uint32_t vid, bool local, int32_t r, int c) {
   if (key >= (uint32_t)K || vid == 0u) return -1;
   const uint32_t* kp = h.pl + (uint64_t)(kFieldPlanes + key) * h.sd;
   const uint32_t* mp = h.pl + 4 * h.sd;
@@ -1492,7 +1495,7 @@ __device__ int32_t ht_marker_pos(HT& h, uint32_t key, uint32_t vid, bool local, 
 }
 
 template <int K, bool S>
-__device__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStats], const ReplayArgs& a, int32_t& lseq, EvOut& ev,
+__device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStats], const ReplayArgs& a, int32_t& lseq, EvOut& ev,
                        uint32_t& rhi) {
   s8v op = sload8(D.recp + 2 * D.k);
   const uint4* rec = D.recp + 2 * D.k;

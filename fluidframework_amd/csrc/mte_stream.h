@@ -121,7 +121,7 @@ __device__ __forceinline__ bool slide_ok(int32_t sq, int32_t rs) { return sq < k
 
 // the first slot a reference may slide to after x (dir > 0) or before it
 // (dir < 0), or -1; x is wave-uniform
-__device__ int find_slide_target(const uint32_t* pl, uint64_t sd, int n, int x, int dir) {
+__device__ __forceinline__ int find_slide_target(const uint32_t* pl, uint64_t sd, int n, int x, int dir) {
   const int l = lane_id();
   if (dir > 0) {
     for (int b = x + 1; b < n; b += kWave) {
@@ -151,7 +151,7 @@ __device__ int find_slide_target(const uint32_t* pl, uint64_t sd, int n, int x, 
 // segment they may slide to (addBeforeTombstones), else to the last offset of
 // the last preceding one (addAfterTombstones), else detach; Simple references
 // detach (localReference.ts:422-485).  Slots [0, rhi) of the table rt.
-__device__ void stream_slide(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t rhi, int32_t s) {
+__device__ __forceinline__ void stream_slide(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t rhi, int32_t s) {
   const int l = lane_id();
   for (int tb = 0; tb < n; tb += kWave) {
     const int i = tb + l;
@@ -189,7 +189,7 @@ __device__ void stream_slide(const uint32_t* pl, uint64_t sd, int n, uint2* rt, 
 // the anchor a reference on slot x moves to when x is removed and acked
 // (_getSlideToSegment, mergeTree.ts:893-913; Client.getSlideToSegment's offset,
 // client.ts:1117-1130), or false when there is none; x is wave-uniform
-__device__ bool slide_anchor(const uint32_t* pl, uint64_t sd, int n, int x, uint32_t& to) {
+__device__ __forceinline__ bool slide_anchor(const uint32_t* pl, uint64_t sd, int n, int x, uint32_t& to) {
   int t = find_slide_target(pl, sd, n, x, 1);
   bool after = false;
   if (t < 0) {
@@ -214,7 +214,7 @@ __device__ bool slide_anchor(const uint32_t* pl, uint64_t sd, int n, int x, uint
 //     its segment is removed and acked (ackInterval, :1805-1902).
 // rhi: slots in use so far.
 template <int K>
-__device__ int stream_ref(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t& rhi, const s8v& op,
+__device__ __forceinline__ int stream_ref(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t& rhi, const s8v& op,
                           int32_t m, bool newcalc) {
   const uint32_t slot = (uint32_t)op[5], b = (uint32_t)op[7], typ = (uint32_t)op[6];
   const int l = lane_id();
