@@ -515,7 +515,7 @@ struct mte_ctx {
   // round phases of the chunked pass (mte_round.h); MTE_ROUND_PHASES=0 turns them off
   RoundArgs rd{};
   bool round_phases = true;
-  uint32_t htree_lds = 24u << 10;  // LDS bytes a document of the HBM tree pass may hold (MTE_HTREE_LDS)
+  uint32_t htree_lds = 0;  // LDS bytes a document of the HBM tree pass may hold (MTE_HTREE_LDS)
   std::vector<uint32_t> h_htree_docs, h_hord;
   uint32_t* d_hord_s[2] = {nullptr, nullptr};  // per batch slot: the candidates, most records first
   uint64_t hord_cap_s[2] = {0, 0};

@@ -35,7 +35,7 @@
 namespace mte {
 
 #ifndef MTE_HTREE_KHE
-#define MTE_HTREE_KHE 4
+#define MTE_HTREE_KHE 2
 #endif
 constexpr int kHE = MTE_HTREE_KHE;     // items per lane per tile
 constexpr int kHT = kWave * kHE;       // items per tile

@@ -89,7 +89,7 @@ if (ext) {
 eng.start();
 const prev = layout.map(() => 0);
 const failures = [];
-const extFail = {}, extFirst = {};
+const extFail = {}, extFirst = {}, prevNext = { n: 0, equal: 0 };
 let passed = 0, opsChecked = 0;
 const nCp = Math.max.apply(null, sets.slice(0, nSets).map((s) => s.checkpoints.length));
 for (let j = 0; j < nCp; j++) {
@@ -176,12 +176,28 @@ for (let j = 0; j < nCp; j++) {
           ids(Array.from(L.coll.CreateBackwardIteratorWithStartPosition(a))),
           ids(Array.from(L.coll.CreateForwardIteratorWithEndPosition(b))),
           ids(Array.from(L.coll.CreateBackwardIteratorWithEndPosition(b)))]) };
+      // previousInterval / nextInterval (columns 3, 4) are compared apart: the
+      // reference's end tree keeps one node per end and can lose an interval
+      // sharing its end with one removed (rbTree put / remove by key)
+      const strip = (qs) => qs.map((q) => q.filter((_, i) => i !== 3 && i !== 4));
+      for (const q of got.queries.keys()) {
+        const gq = got.queries[q], wq = want.queries[q];
+        prevNext.n += 2;
+        prevNext.equal += (JSON.stringify(gq[3]) === JSON.stringify(wq[3]) ? 1 : 0) +
+          (JSON.stringify(gq[4]) === JSON.stringify(wq[4]) ? 1 : 0);
+      }
       for (const k of ["events", "order", "summary", "queries"]) {
-        const w = k === "events" ? evWant : want[k];
+        const w = k === "events" ? evWant : (k === "queries" ? strip(want[k]) : want[k]);
+        if (k === "queries") got[k] = strip(got[k]);
         if (JSON.stringify(sortKeys(got[k])) !== JSON.stringify(sortKeys(w))) {
           ok = false;
           extFail[k] = (extFail[k] || 0) + 1;
-          if (!extFirst[k]) extFirst[k] = [L.si, L.ci, j, got[k], w];
+          if (!extFirst[k]) {
+            const g = got[k], ww = w;
+            let d = 0;
+            while (d < Math.min(g.length, ww.length) && JSON.stringify(sortKeys(g[d])) === JSON.stringify(sortKeys(ww[d]))) d++;
+            extFirst[k] = [L.si, L.ci, j, d, g.length, ww.length, g.slice(d, d + 3), ww.slice(d, d + 3)];
+          }
           failures.push([L.si, L.ci, j, k, got[k], w]);
           break;
         }
@@ -217,7 +233,7 @@ if (ext) {
   }
 }
 if (mode !== "pack") {
-  process.stdout.write(JSON.stringify({ passed, opsChecked, loaded, unloadable, extFail, extFirst, failures: failures.slice(0, 4),
+  process.stdout.write(JSON.stringify({ passed, opsChecked, loaded, unloadable, extFail, extFirst, prevNext, failures: failures.slice(0, 4),
     nFailures: failures.length, docs: layout.length }) + "\n");
 } else {
   process.stdout.write(JSON.stringify({ done: true, opsChecked, failures: failures.slice(0, 4),
