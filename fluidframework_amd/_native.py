@@ -52,6 +52,7 @@ def load_mte():
         "mte_set_event_capacity": ([vp, u32], C.c_int),
         "mte_set_ref_capacity": ([vp, u32], C.c_int),
         "mte_read_refs": ([vp, u32, vp, u32], C.c_int),
+        "mte_read_refs_transient": ([vp, u32, vp, u32], C.c_int),
         "mte_read_ref_order": ([vp, u32, vp, u32], C.c_int),
         "mte_read_segments": ([vp, u32, vp], C.c_int),
         "mte_doc_status": ([vp, vp, u32], C.c_int),

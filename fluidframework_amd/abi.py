@@ -123,7 +123,7 @@ EXPORTED_SYMBOLS = [
     "mte_digest_device", "mte_read_doc", "mte_read_segments", "mte_doc_status", "mte_stats_get", "mte_set_stats",
     "mte_comm_unique_id", "mte_comm_init", "mte_comm_share", "mte_comm_barrier", "mte_comm_allreduce_f64",
     "mte_comm_gather_digests", "mte_comm_world", "mte_comm_destroy", "mte_read_deltas", "mte_set_event_capacity",
-    "mte_set_ref_capacity", "mte_read_refs", "mte_read_ref_order",
+    "mte_set_ref_capacity", "mte_read_refs", "mte_read_refs_transient", "mte_read_ref_order",
 ]
 
 DOC_EVENTS = 0x8

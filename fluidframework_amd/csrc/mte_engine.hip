@@ -1744,7 +1744,7 @@ int mte_set_ref_capacity(mte_ctx* c, uint32_t per_doc) {
 // the own-view position of the segment holding the reference's unit plus its
 // offset there (0 on a removed segment); -1 for a detached or unused slot or a
 // unit no segment holds any more (a tombstone compacted at minSeq)
-int mte_read_refs(mte_ctx* c, uint32_t doc, int32_t* pos, uint32_t n) {
+static int read_refs_view(mte_ctx* c, uint32_t doc, int32_t* pos, uint32_t n, bool transient) {
   if (!c || (n && !pos) || doc >= c->n_docs) return MTE_E_INVALID_ARG;
   JOIN_TAIL(c);
   if (c->h_refs.empty() || !c->h_refs[doc]) return set_err(c, MTE_E_INVALID_ARG, "doc %u: no MTE_DOC_REFS", doc);
@@ -1769,7 +1769,7 @@ int mte_read_refs(mte_ctx* c, uint32_t doc, int32_t* pos, uint32_t n) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   for (uint32_t r = 0; r < n; r++) {
     pos[r] = -1;
-    if (!(rt[r].y & kRefLive) || (rt[r].y & kRefDetached)) continue;
+    if (!(rt[r].y & kRefLive) || ((rt[r].y & kRefDetached) && !(transient && (rt[r].y & kRefOff)))) continue;
     int64_t p = 0;
     for (uint32_t i = 0; i < ns; i++) {
       if (rt[r].x - toff[i] < (uint32_t)len[i]) {
@@ -1780,6 +1780,12 @@ int mte_read_refs(mte_ctx* c, uint32_t doc, int32_t* pos, uint32_t n) {
     }
   }
   return MTE_OK;
+}
+
+int mte_read_refs(mte_ctx* c, uint32_t doc, int32_t* pos, uint32_t n) { return read_refs_view(c, doc, pos, n, false); }
+
+int mte_read_refs_transient(mte_ctx* c, uint32_t doc, int32_t* pos, uint32_t n) {
+  return read_refs_view(c, doc, pos, n, true);
 }
 
 int mte_read_ref_order(mte_ctx* c, uint32_t doc, int64_t* key, uint32_t n) {

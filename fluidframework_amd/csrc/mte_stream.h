@@ -113,7 +113,11 @@ __device__ __forceinline__ int32_t own_prefix(const uint32_t* pl, uint64_t sd, i
 // marker's is its reserved unit): splits never copy text, so the unit names the
 // same place in whatever segment holds it, which is what LocalReferenceCollection
 // keeps as (segment, offset) and moves on split (localReference.ts:391-416).
-constexpr uint32_t kRefLive = 0x80000000u, kRefDetached = 0x40000000u;
+// kRefOff (with kRefDetached): a reference slideAckedRemovedSegmentReferences
+// took off its segment's list for want of a segment to slide to
+// (mergeTree.ts:935-942, removeLocalRef keeps the segment): detached for
+// every read but mte_read_refs_transient, which still finds its segment.
+constexpr uint32_t kRefLive = 0x80000000u, kRefDetached = 0x40000000u, kRefOff = 0x20000000u;
 
 // a segment references may slide to (_getSlideToSegment, mergeTree.ts:893-913):
 // not a pending insert and not removed-and-acked (a pending removal is fine)
@@ -149,8 +153,9 @@ __device__ __forceinline__ int find_slide_target(const uint32_t* pl, uint64_t sd
 // 1986-1993), or the local removals an ack sequenced (:1302-1304).  Each such
 // segment's SlideOnRemove references move to offset 0 of the first following
 // segment they may slide to (addBeforeTombstones), else to the last offset of
-// the last preceding one (addAfterTombstones), else detach; Simple references
-// detach (localReference.ts:422-485).  Slots [0, rhi) of the table rt.
+// the last preceding one (addAfterTombstones), else come off the segment's list
+// (kRefOff); Simple references detach, or come off the list when there is no
+// segment to slide to (localReference.ts:422-485).  Slots [0, rhi) of the table rt.
 __device__ __forceinline__ void stream_slide(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t rhi, int32_t s) {
   const int l = lane_id();
   for (int tb = 0; tb < n; tb += kWave) {
@@ -178,7 +183,7 @@ __device__ __forceinline__ void stream_slide(const uint32_t* pl, uint64_t sd, in
         const uint32_t anc = ld_l2(&rt[rc].x), st = ld_l2(&rt[rc].y);
         if (r < rhi && (st & kRefLive) && !(st & (kRefDetached | MTE_REF_STAY_ON_REMOVE)) && anc - toff < len) {
           if ((st & MTE_REF_SLIDE_ON_REMOVE) && t >= 0) rt[r].x = to;
-          else rt[r].y = st | kRefDetached;
+          else rt[r].y = st | kRefDetached | (t < 0 ? kRefOff : 0u);
         }
       }
       vm_drain();
@@ -228,7 +233,7 @@ __device__ __forceinline__ int stream_ref(const uint32_t* pl, uint64_t sd, int n
   if (b == 3u) {
     const uint32_t st0 = ld_l2(&rt[slot].y), anc = ld_l2(&rt[slot].x);
     if (!(st0 & kRefLive)) return MTE_E_INVALID_ARG;
-    uint32_t st = (st0 & (kRefLive | kRefDetached)) | (typ & 0xffffu), to = anc;
+    uint32_t st = (st0 & (kRefLive | kRefDetached | kRefOff)) | (typ & 0xffffu), to = anc;
     if (!(st & kRefDetached) && (st & MTE_REF_SLIDE_ON_REMOVE)) {
       // the slot holding the reference's unit
       for (int tb = 0; tb < n; tb += kWave) {

@@ -76,11 +76,12 @@ class EngineBase:
         self._check(self._read_deltas(doc, ptr(out), n.value, C.byref(n)), "read_deltas")
         return out[: n.value]
 
-    def read_refs(self, doc, n):
+    def read_refs(self, doc, n, transient=False):
         """Positions of local reference slots [0, n) of an MTE_DOC_REFS doc in its
-        own view (localReferencePositionToPosition; -1 = detached / unused)."""
+        own view (localReferencePositionToPosition; -1 = detached / unused);
+        transient: as Transient references (mte_read_refs_transient)."""
         out = np.zeros(max(n, 1), np.int32)
-        self._check(self._read_refs(doc, ptr(out), n), "read_refs")
+        self._check(self._read_refs(doc, ptr(out), n, transient), "read_refs")
         return out[:n]
 
     def read_ref_order(self, doc, n):
@@ -239,8 +240,9 @@ class DeviceEngine(EngineBase):
     def set_ref_capacity(self, per_doc):
         self._check(self.lib.mte_set_ref_capacity(self.ctx, per_doc), "set_ref_capacity")
 
-    def _read_refs(self, doc, p, n):
-        return self.lib.mte_read_refs(self.ctx, doc, p, n)
+    def _read_refs(self, doc, p, n, transient=False):
+        f = self.lib.mte_read_refs_transient if transient else self.lib.mte_read_refs
+        return f(self.ctx, doc, p, n)
 
     def _digest(self, p, n):
         return self.lib.mte_digest(self.ctx, p, n)

@@ -168,6 +168,7 @@ class MergeTreeEngine {
     this.pending = new BatchBuilder(this.docs.length, this.interner, this.track);
     this.views = new Array(this.docs.length).fill(null);
     this.refViews = new Array(this.docs.length).fill(null);
+    this.refViewsT = new Array(this.docs.length).fill(null);
     this.orderViews = new Array(this.docs.length).fill(null);
     this.unitViews = new Array(this.docs.length).fill(null);
     this.docs.forEach((d, i) => { if (d.catchup) for (const m of d.catchup) this.clients[i].applyMsg(m); });
@@ -194,6 +195,7 @@ class MergeTreeEngine {
     this.pending = new BatchBuilder(this.docs.length, this.interner, this.track);
     this.views.fill(null);
     this.refViews.fill(null);
+    this.refViewsT.fill(null);
     this.orderViews.fill(null);
     this.unitViews.fill(null);
     this.addon.submit(this.ctx, b.offsets, b.ops, b.text, b.propsets, b.props);
@@ -256,13 +258,14 @@ class MergeTreeEngine {
 
   /** Positions of a document's local reference slots after the last replay
    *  (mte_read_refs), read once per flush. */
-  _refView(doc) {
+  _refView(doc, transient) {
     this.flush();
     this.sync();
-    let v = this.refViews[doc];
+    const views = transient ? this.refViewsT : this.refViews;
+    let v = views[doc];
     if (v === null) {
-      v = new Int32Array(this.addon.readRefs(this.ctx, doc, this.clients[doc].clients.refNext).buffer);
-      this.refViews[doc] = v;
+      v = new Int32Array(this.addon.readRefs(this.ctx, doc, this.clients[doc].clients.refNext, !!transient).buffer);
+      views[doc] = v;
     }
     return v;
   }
@@ -753,7 +756,9 @@ class BatchClient {
   localReferencePositionToPosition(lref) {
     if (lref && lref.snapshot) return lref.position;  // an interval event's previousInterval end
     if (!lref || lref.client !== this || lref.slot < 0) return -1;
-    return this.engine._refView(this.doc)[lref.slot];
+    // transientRead: an end an interval event's previousInterval shares, read
+    // as the reference reads it while emitChange holds it Transient
+    return this.engine._refView(this.doc, lref.transientRead)[lref.slot];
   }
 
   /** Local ops sent but not acknowledged yet. */

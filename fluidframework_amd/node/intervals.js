@@ -156,13 +156,22 @@ class TransientInterval {
 }
 
 /** The ends of an interval as they were, for a "changeInterval" event's
- *  previousInterval (position information only, as the reference's Transient
- *  copies, :1387-1410). */
+ *  previousInterval (position information only): read as Transient references,
+ *  as emitChange makes them (:1387-1410) -- an end that slid off the string
+ *  still finds its removed segment while the document holds it
+ *  (mte_read_refs_transient).  _src: the ends themselves, for the ones the
+ *  changed interval keeps. */
 function snapshotInterval(ival) {
   const c = ival.collection.client;
-  const ref = (r) => ({ snapshot: true, position: c.localReferencePositionToPosition(r), refType: RefType.Transient });
+  const ref = (r) => {
+    r.transientRead = true;
+    const position = c.localReferencePositionToPosition(r);
+    delete r.transientRead;
+    return { snapshot: true, position, refType: RefType.Transient };
+  };
   const prev = new SequenceInterval(ival.collection, ref(ival.start), ref(ival.end), ival.intervalType);
   prev.properties = Object.assign({}, ival.properties);
+  prev._src = [ival.start, ival.end];
   return prev;
 }
 
@@ -232,6 +241,18 @@ class IntervalCollection {
     const l = this.listeners.get(event);
     if (l) for (const f of l.slice()) f(...args);
   }
+  /** emitChange (:1387-1410): while the listeners run, the ends the changed
+   *  interval shares with the previous one are Transient too. */
+  _emitChange(ival, prev, local, op) {
+    const shared = [ival.start, ival.end].filter((r) => prev._src && prev._src.includes(r));
+    for (const r of shared) r.transientRead = true;
+    try {
+      this._emit("changeInterval", ival, prev, local, op);
+    } finally {
+      for (const r of shared) delete r.transientRead;
+    }
+  }
+
 
   // ---- references ------------------------------------------------------------
   _localRef(pos, type) {
@@ -370,7 +391,7 @@ class IntervalCollection {
       properties: { [reservedIntervalIdKey]: id } };
     this.emitter.emit("change", undefined, v, {});
     this._addPending(id, v);
-    if (prev) this._emit("changeInterval", ival, prev, true, undefined);
+    if (prev) this._emitChange(ival, prev, true, undefined);
     return ival;
   }
 
@@ -460,7 +481,7 @@ class IntervalCollection {
       this._changeInterval(ival, start, end, op);
     }
     const deltas = ival.addProperties(props, true, op.sequenceNumber);
-    if (prev) this._emit("changeInterval", ival, prev, false, op);
+    if (prev) this._emitChange(ival, prev, false, op);
     if (Object.keys(props).length > 0) this._emit("propertyChanged", ival, deltas, false, op);
   }
 
@@ -481,7 +502,7 @@ class IntervalCollection {
       const after = ival._keys();
       if (after[0] !== before[0] || after[1] !== before[1]) {
         ival.stamp = ++this.stamp;
-        this._emit("changeInterval", ival, prev, true, op);
+        this._emitChange(ival, prev, true, op);
       }
     }
   }

@@ -587,11 +587,19 @@ static napi_value js_set_ref_capacity(napi_env env, napi_callback_info info) {
   return NULL;
 }
 
-/* readRefs(ctx, doc, n) -> Int32Array(n): positions of reference slots [0, n)
-   (mte_read_refs; -1 detached / unused) */
+/* readRefs(ctx, doc, n[, transient]) -> Int32Array(n): positions of reference
+   slots [0, n) (mte_read_refs; -1 detached / unused); transient true: as
+   Transient references (mte_read_refs_transient) */
 static napi_value js_read_refs(napi_env env, napi_callback_info info) {
-  napi_value argv[3];
-  if (!get_args(env, info, 3, argv)) return NULL;
+  napi_value argv[4];
+  size_t argc = 4;
+  if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok) return NULL;
+  if (argc < 3) {
+    napi_throw_type_error(env, NULL, "too few arguments");
+    return NULL;
+  }
+  bool transient = false;
+  if (argc > 3 && napi_get_value_bool(env, argv[3], &transient) != napi_ok) transient = false;
   mte_ctx* ctx = get_ctx(env, argv[0]);
   if (!ctx) return NULL;
   uint32_t doc = 0, n = 0;
@@ -604,7 +612,7 @@ static napi_value js_read_refs(napi_env env, napi_callback_info info) {
     napi_throw_error(env, NULL, "out of memory");
     return NULL;
   }
-  if (throw_rc(env, mte_read_refs(ctx, doc, buf, n), ctx, "mte_read_refs")) {
+  if (throw_rc(env, (transient ? mte_read_refs_transient : mte_read_refs)(ctx, doc, buf, n), ctx, "mte_read_refs")) {
     free(buf);
     return NULL;
   }

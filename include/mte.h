@@ -439,6 +439,14 @@ int mte_set_ref_capacity(mte_ctx* ctx, uint32_t per_doc);
  * the segment's position (Client.getPosition) plus the offset, 0 on a removed
  * segment; -1 (DetachedReferencePosition) for a detached or unused slot.      */
 int mte_read_refs(mte_ctx* ctx, uint32_t doc, int32_t* pos, uint32_t n);
+/* As mte_read_refs with every reference Transient, as an interval
+ * collection's emitChange reads a changeInterval event's previous interval
+ * (intervalCollection.ts:1387-1410; mergeTree.ts:1106-1109): a reference that
+ * slid off the string -- its segment removed and acked with no segment to
+ * slide to, so slideAckedRemovedSegmentReferences took it off the segment's
+ * list but left it pointing there (mergeTree.ts:935-942) -- still gives the
+ * position of that segment while the document holds it.                     */
+int mte_read_refs_transient(mte_ctx* ctx, uint32_t doc, int32_t* pos, uint32_t n);
 /* Document order of reference slots [0, n): the index, among every text unit
  * the document holds (removed segments included), of the unit the reference
  * sits on; -1 for a detached or unused slot.  Two references compare as

@@ -50,7 +50,7 @@ def load():
         "oti_load_segments": [vp, vp, vp, u64], "oti_apply_batch": [vp, vp, C.c_int],
         "oti_read_doc": [vp, u32, vp], "oti_digest": [vp, vp, u32], "oti_doc_status": [vp, vp, u32],
         "oti_doc_nsegs": [vp, u32, vp], "oti_stats_get": [vp, vp], "oti_read_segments": [vp, u32, vp], "oti_set_limit": [vp, u32],
-        "oti_read_deltas": [vp, u32, vp, u64, vp], "oti_read_refs": [vp, u32, vp, u32], "oti_read_ref_order": [vp, u32, vp, u32],
+        "oti_read_deltas": [vp, u32, vp, u64, vp], "oti_read_refs": [vp, u32, vp, u32], "oti_read_refs_transient": [vp, u32, vp, u32], "oti_read_ref_order": [vp, u32, vp, u32],
         "och_create": [u32, vp], "och_destroy": [vp], "och_load_docs": [vp, u32, vp, vp, u64, vp, u32, vp, u32],
         "och_load_segments": [vp, vp, vp, u64], "och_apply_batch": [vp, vp, C.c_int], "och_read_doc": [vp, u32, vp],
         "och_digest": [vp, vp, u32], "och_doc_status": [vp, vp, u32], "och_doc_nsegs": [vp, u32, vp],
@@ -63,6 +63,8 @@ def load():
     lib.orc_read_deltas.restype = C.c_int
     lib.orc_read_refs.argtypes = [vp, u32, vp, u32]
     lib.orc_read_refs.restype = C.c_int
+    lib.orc_read_refs_transient.argtypes = [vp, u32, vp, u32]
+    lib.orc_read_refs_transient.restype = C.c_int
     lib.orc_read_ref_order.argtypes = [vp, u32, vp, u32]
     lib.orc_read_ref_order.restype = C.c_int
     for pre in ("ort", "oti"):
@@ -161,9 +163,9 @@ class OracleEngine(EngineBase):
     def set_ref_capacity(self, per_doc):
         """The restatement's reference slots grow as needed."""
 
-    def _read_refs(self, doc, p, n):
-        f = self.lib.oti_read_refs if self.tree == "items" else self.lib.orc_read_refs
-        return f(self.ctx, doc, p, n)
+    def _read_refs(self, doc, p, n, transient=False):
+        pre = "oti" if self.tree == "items" else "orc"
+        return getattr(self.lib, f"{pre}_read_refs{'_transient' if transient else ''}")(self.ctx, doc, p, n)
 
     def read_ref_order(self, doc, n):
         f = self.lib.oti_read_ref_order if self.tree == "items" else self.lib.orc_read_ref_order
@@ -274,9 +276,9 @@ class SpecOracle:
         e, i = self.where[doc]
         return self._engines()[e].nsegs(int(i))
 
-    def read_refs(self, doc, n):
+    def read_refs(self, doc, n, transient=False):
         e, i = self.where[doc]
-        return self._engines()[e].read_refs(int(i), n)
+        return self._engines()[e].read_refs(int(i), n, transient)
 
     def read_ref_order(self, doc, n):
         e, i = self.where[doc]

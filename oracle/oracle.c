@@ -368,6 +368,9 @@ static int doc_relpos(odoc* d, const mte_op* rp, mte_op* nx, uint32_t n_keys) {
  * split / append (localReference.ts:330-416), which names the same unit. */
 #define REF_LIVE 0x80000000u
 #define REF_DETACHED 0x40000000u
+/* with REF_DETACHED: taken off its segment's list for want of a segment to
+ * slide to (mergeTree.ts:935-942; removeLocalRef keeps the segment) */
+#define REF_OFF 0x20000000u
 #define REF_LIMIT (1u << 24)
 
 /* a segment references may slide to (_getSlideToSegment, mergeTree.ts:893-913):
@@ -432,7 +435,7 @@ static int doc_ref(odoc* d, const mte_op* op) {
   if (op->b == 3) {
     uint32_t st = d->ref_state[slot];
     if (!(st & REF_LIVE)) return MTE_E_INVALID_ARG;
-    d->ref_state[slot] = st = (st & (REF_LIVE | REF_DETACHED)) | (op->a & 0xffffu);
+    d->ref_state[slot] = st = (st & (REF_LIVE | REF_DETACHED | REF_OFF)) | (op->a & 0xffffu);
     if (st & REF_DETACHED) return MTE_OK;
     for (uint32_t i = 0; i < d->n; i++) {
       const oseg* g = &d->s[i];
@@ -493,7 +496,7 @@ static void doc_slide_refs(odoc* d, int32_t s) {
       if (!(st & REF_LIVE) || (st & REF_DETACHED) || (st & MTE_REF_STAY_ON_REMOVE)) continue;
       if (d->ref_anchor[r] - g->toff >= (uint32_t)g->len) continue;
       if ((st & MTE_REF_SLIDE_ON_REMOVE) && t >= 0) d->ref_anchor[r] = to;
-      else d->ref_state[r] = st | REF_DETACHED;
+      else d->ref_state[r] = st | REF_DETACHED | (t < 0 ? REF_OFF : 0u);
     }
   }
 }
@@ -1315,14 +1318,14 @@ int orc_read_ref_order(orc_ctx* c, uint32_t doc, int64_t* key, uint32_t n) {
   return MTE_OK;
 }
 
-int orc_read_refs(orc_ctx* c, uint32_t doc, int32_t* pos, uint32_t n) {
+static int read_refs_view(orc_ctx* c, uint32_t doc, int32_t* pos, uint32_t n, int transient) {
   if (!c || (n && !pos) || doc >= c->n_docs) return MTE_E_INVALID_ARG;
   const odoc* d = &c->docs[doc];
   for (uint32_t r = 0; r < n; r++) {
     pos[r] = -1;
     if (r >= d->ref_hi) continue;
     const uint32_t st = d->ref_state[r], u = d->ref_anchor[r];
-    if (!(st & REF_LIVE) || (st & REF_DETACHED)) continue;
+    if (!(st & REF_LIVE) || ((st & REF_DETACHED) && !(transient && (st & REF_OFF)))) continue;
     int64_t p = 0;
     for (uint32_t i = 0; i < d->n; i++) {
       const oseg* g = &d->s[i];
@@ -1334,4 +1337,13 @@ int orc_read_refs(orc_ctx* c, uint32_t doc, int32_t* pos, uint32_t n) {
     }
   }
   return MTE_OK;
+}
+
+int orc_read_refs(orc_ctx* c, uint32_t doc, int32_t* pos, uint32_t n) { return read_refs_view(c, doc, pos, n, 0); }
+
+/* mte_read_refs_transient: as orc_read_refs with every reference Transient
+ * (emitChange, intervalCollection.ts:1387-1410): a reference taken off its
+ * segment's list still finds the segment while it is held */
+int orc_read_refs_transient(orc_ctx* c, uint32_t doc, int32_t* pos, uint32_t n) {
+  return read_refs_view(c, doc, pos, n, 1);
 }

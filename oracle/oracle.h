@@ -40,6 +40,7 @@ int orc_read_doc(orc_ctx* c, uint32_t doc, mte_doc_view* v);
 /* Delta events of the last batch of an MTE_DOC_EVENTS doc (as mte_read_deltas, no cap). */
 int orc_read_deltas(orc_ctx* c, uint32_t doc, mte_delta* out, uint64_t cap, uint64_t* n);
 int orc_read_refs(orc_ctx* c, uint32_t doc, int32_t* pos, uint32_t n);
+int orc_read_refs_transient(orc_ctx* c, uint32_t doc, int32_t* pos, uint32_t n);
 int orc_read_ref_order(orc_ctx* c, uint32_t doc, int64_t* key, uint32_t n);
 int orc_read_segments(orc_ctx* c, uint32_t doc, mte_seg_list* v);
 int orc_digest(orc_ctx* c, uint64_t* out, uint32_t n_docs);

@@ -32,6 +32,7 @@ int oti_set_limit(oti_ctx* c, uint32_t limit);
 int oti_read_segments(oti_ctx* c, uint32_t doc, mte_seg_list* v);
 int oti_read_deltas(oti_ctx* c, uint32_t doc, mte_delta* out, uint64_t cap, uint64_t* n);
 int oti_read_refs(oti_ctx* c, uint32_t doc, int32_t* pos, uint32_t n);
+int oti_read_refs_transient(oti_ctx* c, uint32_t doc, int32_t* pos, uint32_t n);
 int oti_read_ref_order(oti_ctx* c, uint32_t doc, int64_t* key, uint32_t n);
 
 #ifdef __cplusplus

@@ -227,16 +227,30 @@ if (ext) {
       return [x.getIntervalId(), a, b, sortKeys(x.properties)];
     });
     ivs.sort((a, b) => (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0));
-    if (JSON.stringify(ivs) === JSON.stringify(last.intervals) &&
-        JSON.stringify(sortKeys(clone(coll.serializeInternal()))) === JSON.stringify(sortKeys(last.summary))) loaded++;
-    else failures.push([si, "load", ivs.slice(0, 3), last.intervals.slice(0, 3)]);
+    const gotSum = JSON.stringify(sortKeys(clone(coll.serializeInternal())));
+    // serialize() stamps each interval with the serializing client's current
+    // seq (intervalCollection.ts:456-470): the fresh loader's, not the observer's
+    const want = clone(last.summary);
+    for (const x of want.intervals) x[2] = c.getCurrentSeq();
+    const wantSum = JSON.stringify(sortKeys(want));
+    if (JSON.stringify(ivs) === JSON.stringify(last.intervals) && gotSum === wantSum) loaded++;
+    else {
+      // the first differing interval, or the summaries from their first difference
+      let d = 0;
+      while (d < ivs.length && JSON.stringify(ivs[d]) === JSON.stringify(last.intervals[d])) d++;
+      let e = 0;
+      while (e < gotSum.length && gotSum[e] === wantSum[e]) e++;
+      failures.push([si, "load", d, ivs.length, last.intervals.length, ivs.slice(d, d + 2),
+        last.intervals.slice(d, d + 2), gotSum.slice(Math.max(0, e - 80), e + 120),
+        wantSum.slice(Math.max(0, e - 80), e + 120)]);
+    }
   }
 }
 if (mode !== "pack") {
-  process.stdout.write(JSON.stringify({ passed, opsChecked, loaded, unloadable, extFail, extFirst, prevNext, failures: failures.slice(0, 4),
+  process.stdout.write(JSON.stringify({ passed, opsChecked, loaded, unloadable, extFail, extFirst, prevNext, failures: failures.slice(0, 16),
     nFailures: failures.length, docs: layout.length }) + "\n");
 } else {
-  process.stdout.write(JSON.stringify({ done: true, opsChecked, failures: failures.slice(0, 4),
+  process.stdout.write(JSON.stringify({ done: true, opsChecked, failures: failures.slice(0, 16),
     nFailures: failures.length }) + "\n");
 }
 eng.close();

@@ -121,6 +121,43 @@ def test_gpu_localref_scenario():
     assert mid == [2, -1, 3] and end == [1, -1, 1]
 
 
+def _off_scenario(factory):
+    """A remote remove of the whole text "abc" leaves no segment to slide to:
+    the SlideOnRemove reference on 'b' and the Simple one on 'c' come off the
+    removed segment's list but keep pointing at it (mergeTree.ts:935-942) --
+    detached for localReferencePositionToPosition, the segment's position (0,
+    offset 0 on a removed segment) read as Transient references
+    (mte_read_refs_transient, mergeTree.ts:1106-1109).  The Simple reference
+    of _scenario, detached beside a segment to slide to (link(undefined),
+    localReference.ts:447-449), stays detached either way."""
+    inits, text = doc_inits(["abc"], flags=DOC_NEW_LENGTH_CALC | DOC_LOCAL_CLIENT | DOC_REFS)
+    e = factory(4)
+    e.load_docs(inits, text)
+    cl = DocClients("B", local=True)
+    bb = BatchBuilder(1, Interner(4))
+    bb.add_ref(0, cl, 1, REF_SLIDE_ON_REMOVE)
+    bb.add_ref(0, cl, 2, 0)
+    bb.add_message(0, cl, {"clientId": "C", "sequenceNumber": 1, "referenceSequenceNumber": 0,
+                           "minimumSequenceNumber": 0, "type": "op", "contents": {"type": 1, "pos1": 0, "pos2": 3}})
+    e.apply_batch(bb.build())
+    e2 = _scenario(factory)[0]
+    return (e, list(e.read_refs(0, 2)), list(e.read_refs(0, 2, transient=True)),
+            list(e2.read_refs(0, 3, transient=True)))
+
+
+def test_oracle_refs_off_the_string_transient():
+    e, plain, transient, simple = _off_scenario(oracle_factory)
+    assert (e.statuses() == 0).all()
+    assert plain == [-1, -1] and transient == [0, 0] and simple == [1, -1, 1]
+
+
+@pytest.mark.gpu
+def test_gpu_refs_off_the_string_transient():
+    e, plain, transient, simple = _off_scenario(device_factory)
+    assert (e.statuses() == 0).all()
+    assert plain == [-1, -1] and transient == [0, 0] and simple == [1, -1, 1]
+
+
 @pytest.mark.gpu
 def test_gpu_localref_farms():
     sets = ref_sets()
