@@ -48,6 +48,7 @@ OP_RELPOS = 9         # relative positions of the record that follows (include/m
 RP_POS1, RP_BEFORE1, RP_POS2, RP_BEFORE2 = 0x100, 0x200, 0x400, 0x800
 REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE, REF_TRANSIENT = 0x40, 0x80, 0x100  # ReferenceType (ops.ts)
 DELTA_REGEN = 0x10    # kind flag of its output records
+DELTA_REBASE = 0x20   # MTE_OP_REF b = 4 / 5: the answer's kind
 ANNOTATE_SLOTS = 32   # pending local annotate groups tracked per document
 F_MARKER, F_MSG_END, F_REWRITE, F_LOCAL = 0x1, 0x2, 0x4, 0x8
 LOCAL_SEQ_BASE = 0x40000000

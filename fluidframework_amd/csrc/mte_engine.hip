@@ -822,9 +822,11 @@ const char* bad_op(const mte_op& o, const mte_batch* b, bool local_doc, bool ref
   if (o.type >= MTE_OP_ROLLBACK && !(o.flags & MTE_F_LOCAL)) return "rollback / regen without MTE_F_LOCAL";
   if (o.type == MTE_OP_REF) {
     if (!refs_doc) return "local reference record in a document without MTE_DOC_REFS";
-    if (o.seq != 0 || o.pos2 < 0 || (uint32_t)o.pos2 >= ref_cap || o.b > 3 || o.client >= MTE_MAX_CLIENTS ||
+    if (o.seq != 0 || o.pos2 < 0 || (uint32_t)o.pos2 >= ref_cap || o.b > 5 || o.client >= MTE_MAX_CLIENTS ||
         (o.b == 2 && o.client == 0))
       return "local reference record: seq, slot (mte_set_ref_capacity), b or client out of range";
+    if (o.b >= 4 && (!local_doc || o.a >= MTE_LOCAL_SEQ_BASE))
+      return "rebase record: not a local-client document, or localSeq out of range";
     return nullptr;
   }
   if ((o.flags & MTE_F_LOCAL) && o.type == MTE_OP_ANNOTATE && o.b != MTE_NO_PROPS && o.b >= MTE_ANNOTATE_SLOTS)
@@ -1812,7 +1814,9 @@ int mte_read_ref_order(mte_ctx* c, uint32_t doc, int64_t* key, uint32_t n) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   for (uint32_t r = 0; r < n; r++) {
     key[r] = -1;
-    if (!(rt[r].y & kRefLive) || (rt[r].y & kRefDetached)) continue;
+    // a reference off the string still sits on its segment (compareReferencePositions
+    // compares its segment's ordinal, referencePositions.ts:81-89)
+    if (!(rt[r].y & kRefLive) || ((rt[r].y & kRefDetached) && !(rt[r].y & kRefOff))) continue;
     int64_t p = 0;
     for (uint32_t i = 0; i < ns; i++) {
       if (rt[r].x - toff[i] < (uint32_t)len[i]) {

@@ -76,6 +76,10 @@ struct HtreeArgs {
 // plane indices of a local-client document (after the K property planes)
 template <int K> constexpr int kPkPlane = kFieldPlanes + K;
 template <int K> constexpr int kLrsPlane = kFieldPlanes + 3 * K + 1;
+// kLrsPlane: localRemovedSeq, | kLrsReleased once a regeneration dequeued the
+// segment from its group -- it keeps the value, the group no longer holds it
+// (resetPendingDeltaToOps, client.ts:802-857; titems.c LRS_RELEASED)
+constexpr uint32_t kLrsReleased = 0x40000000u;
 
 struct HT {
   uint32_t* pl;   // the document's plane base
@@ -573,7 +577,10 @@ __device__ __forceinline__ int ht_scour(HT& h, int s, int e, uint32_t n_keys) {
     const int32_t xl = ht_sum_len(h, i, xe);
     const int32_t seq = (int32_t)ht_pl(h, 1, i), rseq = (int32_t)ht_pl(h, 2, i);
     bool grouped = seq >= kLocalBase;  // a pending insert
-    if (h.ldoc && !grouped) grouped = ht_pl(h, kLrsPlane<K>, i) != 0u || ht_pl(h, kAnnPlane<K>, i) != 0u;
+    if (h.ldoc && !grouped) {
+      const uint32_t lr = ht_pl(h, kLrsPlane<K>, i);
+      grouped = (lr != 0u && !(lr & kLrsReleased)) || ht_pl(h, kAnnPlane<K>, i) != 0u;
+    }
     if (grouped) {
       // a segment of a pending group is held and ends the append run (:686, 736-739)
       held++;
@@ -1346,14 +1353,14 @@ __device__ __forceinline__ void ht_regen(const HT& h, int32_t ls, uint32_t t, ui
         // a member that re-sends nothing leaves the group (resetPendingDeltaToOps
         // enqueues only the segments with a new op, client.ts:803-852): the
         // zamboni stops holding it for the group (titems.c doc_regen)
-        if (!hit && t == MTE_OP_REMOVE && lr == ls) h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = 0u;
+        if (!hit && t == MTE_OP_REMOVE && lr == ls) h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = (uint32_t)ls | kLrsReleased;
         if (!hit && t == MTE_OP_ANNOTATE && ((am >> slot) & 1u))
           h.pl[(uint64_t)kAnnPlane<K> * h.sd + i] = am & ~(1u << slot);
       }
       // localNetLength with localSeq (mergeTree.ts:575-593)
       int32_t ll = (v && !(tt & kTEmpty)) ? len : 0;
       if (sq >= kLocalBase && sq - kLocalBase > ls) ll = 0;
-      if (lr != 0 && lr <= ls) ll = 0;
+      if (lr != 0 && (lr & ~(int32_t)kLrsReleased) <= ls) ll = 0;
       if (rs != kNone && (!rp || rs - kLocalBase <= ls)) ll = 0;
       const int32_t incl = wave_incl_scan(ll);
       // hit(i - 1): the lane before, or the previous row's / tile's last item
@@ -1494,6 +1501,147 @@ __device__ __forceinline__ int32_t ht_marker_pos(HT& h, uint32_t key, uint32_t v
   return (int32_t)uld((const uint32_t*)h.P + x);
 }
 
+// ---- reconnection of pending interval ops (MTE_OP_REF b = 4 / 5) --------------------------
+// The local client's view at refSeq rs0 and localSeq ls (localNetLength with a
+// localSeq, mergeTree.ts:575-593): acked text up to rs0 less acked removals up
+// to rs0, own pending inserts up to ls, less own removals up to ls.
+template <int K>
+__device__ __forceinline__ int32_t ht_view_len(const HT& h, int i, int32_t rs0, int32_t ls) {
+  const uint32_t tt = ld_l2(h.tw + i);
+  const int32_t len = (int32_t)ld_l2(h.pl + i), sq = (int32_t)ld_l2(h.pl + h.sd + i);
+  const int32_t rs = (int32_t)ld_l2(h.pl + 2 * h.sd + i);
+  const int32_t lr = (int32_t)ld_l2(h.pl + (uint64_t)kLrsPlane<K> * h.sd + i);
+  if (tt & kTEmpty) return 0;
+  if (lr != 0 && (lr & ~(int32_t)kLrsReleased) <= ls) return 0;
+  if (sq >= kLocalBase && sq != kNone) return sq - kLocalBase > ls ? 0 : len;
+  if (sq > rs0) return 0;
+  if (rs != kNone && rs >= kLocalBase) return rs - kLocalBase <= ls ? 0 : len;
+  return (rs != kNone && rs <= rs0) ? 0 : len;
+}
+
+// the view's length of items [0, g)
+template <int K>
+__device__ __forceinline__ int32_t ht_view_prefix(const HT& h, int g, int32_t rs0, int32_t ls) {
+  int32_t acc = 0;
+  for (int tb = 0; tb < g; tb += kHT) {
+#pragma unroll
+    for (int j = 0; j < kHE; j++) {
+      const int i = tb + j * kWave + lane_id();
+      const int32_t v = ht_view_len<K>(h, i < g ? i : 0, rs0, ls);
+      acc += i < g ? v : 0;
+    }
+  }
+  return rdlane(wave_incl_scan(acc), kWave - 1);
+}
+
+// getContainingSegment(pos) in that view (mergeTree.ts:872-885): the first item
+// of positive length holding pos, and the offset there; -1 past the end
+template <int K>
+__device__ __forceinline__ int ht_view_find(const HT& h, int32_t pos, int32_t rs0, int32_t ls, int32_t& off) {
+  const int l = lane_id();
+  int32_t carry = 0;
+  for (int tb = 0; tb < h.n; tb += kHT) {
+#pragma unroll
+    for (int j = 0; j < kHE; j++) {
+      const int i = tb + j * kWave + l;
+      const int32_t v = i < h.n ? ht_view_len<K>(h, i < h.n ? i : 0, rs0, ls) : 0;
+      const int32_t incl = wave_incl_scan(v), st0 = carry + incl - v;
+      const uint64_t m = __ballot(v > 0 && pos >= st0 && pos < st0 + v);
+      if (m) {
+        const int x = __ffsll((long long)m) - 1;
+        off = pos - rdlane(st0, x);
+        return tb + j * kWave + x;
+      }
+      carry += rdlane(incl, kWave - 1);
+    }
+  }
+  return -1;
+}
+
+__device__ __forceinline__ bool ht_removed_acked(const HT& h, int i) {
+  const int32_t rs = (int32_t)uni(ld_l2(h.pl + 2 * h.sd + i));
+  return !(uni(ld_l2(h.tw + i)) & kTEmpty) && rs != kNone && rs < kLocalBase;
+}
+
+// Client.getSlideToSegment (client.ts:1117-1130 -> _getSlideToSegment,
+// mergeTree.ts:893-913) from item x, removed and acked: offset 0 of the first
+// following item a reference may slide to, else the last unit of the last
+// preceding one; false when there is none
+__device__ __forceinline__ bool ht_slide_item(const HT& h, int x, int& t, int32_t& off) {
+  auto ok = [&](int i) {
+    const int32_t sq = (int32_t)ld_l2(h.pl + h.sd + i), rs = (int32_t)ld_l2(h.pl + 2 * h.sd + i);
+    return !(ld_l2(h.tw + i) & kTEmpty) && slide_ok(sq, rs);
+  };
+  t = ht_first(x + 1, h.n, ok);
+  off = 0;
+  if (t >= 0) return true;
+  t = ht_last(0, x, ok);
+  if (t < 0) return false;
+  off = (int32_t)uni(ld_l2(h.pl + t)) - 1;
+  return true;
+}
+
+// b = 4: Client.rebasePosition(pos1, ref_seq, a) (client.ts:755-786) as an
+// MTE_DELTA_REBASE event: the item holding pos1 in the view at (ref_seq, a),
+// else the last item at offset 0; slid if removed and acked; its position in
+// the view at (currentSeq, a) (findReconnectionPosition :709-713) plus the
+// offset, -1 (DetachedReferencePosition) when it slid off the string.
+// b = 5: rebaseLocalInterval's slide of a pending interval end
+// (intervalCollection.ts:1782-1799): the reference in slot pos2, live on an
+// item removed and acked, moves to what createPositionReference finds, in the
+// view at (currentSeq, a), at its slide target's position there; the event's
+// position is that position, -1 when it stays.
+template <int K>
+__device__ __forceinline__ int ht_ref_rebase(HT& h, const s8v& op, int32_t lseq, uint2* rt, EvOut& ev) {
+  const uint32_t b = (uint32_t)op[7];
+  const int32_t ls = op[6];
+  if (ls < 0 || ls > lseq) return MTE_E_INVALID_ARG;
+  if (b == 4u) {
+    int32_t off = 0;
+    int x = ht_view_find<K>(h, op[4], op[1], ls, off);
+    if (x < 0) {  // past every segment of the view: the tree's last leaf, offset 0
+      x = ht_last(0, h.n, [&](int i) { return !(ld_l2(h.tw + i) & kTEmpty); });
+      off = 0;
+    }
+    int32_t p = -1;
+    if (x >= 0) {
+      int t = x;
+      bool ok = true;
+      if (ht_removed_acked(h, x)) ok = ht_slide_item(h, x, t, off);
+      if (ok) p = ht_view_prefix<K>(h, t, h.cur_seq, ls) + off;
+    }
+    ev_one(ev, MTE_DELTA_REBASE, p, 0);
+    return 0;
+  }
+  const uint32_t slot = (uint32_t)op[5];
+  const uint32_t stt = uni(ld_l2(&rt[slot].y)), anc = uni(ld_l2(&rt[slot].x));
+  if (!(stt & kRefLive)) return MTE_E_INVALID_ARG;
+  int32_t p = -1;
+  if (!(stt & kRefDetached)) {
+    const int x = ht_first(0, h.n, [&](int i) {
+      return !(ld_l2(h.tw + i) & kTEmpty) && anc - ld_l2(h.pl + 5 * h.sd + i) < ld_l2(h.pl + i);
+    });
+    int t = -1;
+    int32_t off = 0;
+    if (x >= 0 && ht_removed_acked(h, x)) {
+      uint32_t to = 0, st2 = stt;
+      if (ht_slide_item(h, x, t, off)) {
+        p = ht_view_prefix<K>(h, t, h.cur_seq, ls) + off;
+        int32_t o2 = 0;
+        const int y = ht_view_find<K>(h, p, h.cur_seq, ls, o2);
+        if (y >= 0) to = uni(ld_l2(h.pl + 5 * h.sd + y)) + (uint32_t)o2;
+        else st2 |= kRefDetached;  // the reference throws: no segment there
+      } else {
+        st2 |= kRefDetached;
+      }
+      if (lane_id() == 0) rt[slot] = make_uint2(to, st2);
+      vm_drain();
+    }
+  }
+  ev_one(ev, MTE_DELTA_REBASE, p, 0);
+  return 0;
+}
+
 template <int K, bool S>
 __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStats], const ReplayArgs& a, int32_t& lseq, EvOut& ev,
                        uint32_t& rhi) {
@@ -1549,12 +1697,14 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
   }
   if (type == MTE_OP_REF) {
     if (!lop || !ldoc || !refd) return MTE_E_UNSUPPORTED;
-    if ((uint32_t)op[5] >= a.ref_cap || (uint32_t)op[7] > 3u) return MTE_E_INVALID_ARG;
+    if ((uint32_t)op[5] >= a.ref_cap || (uint32_t)op[7] > 5u) return MTE_E_INVALID_ARG;
     if ((uint32_t)op[7] == 2u && c == 0) return MTE_E_INVALID_ARG;
+    if ((uint32_t)op[7] >= 4u && !evd) return MTE_E_UNSUPPORTED;
     MTE_STAT(st[kStOps]++;)
     MTE_STAT(if ((uint32_t)op[7] != 1u) st[kStScanned] += (uint32_t)h.n;)
     HPROF_BEGIN(t0)
-    rc = stream_ref<K>(h.pl, h.sd, h.n, rt, rhi, op, D.min_seq, h.newcalc);
+    if ((uint32_t)op[7] >= 4u) rc = ht_ref_rebase<K>(h, op, lseq, rt, ev);
+    else rc = stream_ref<K>(h.pl, h.sd, h.n, rt, rhi, op, D.min_seq, h.newcalc);
     HPROF_END(h, 5, t0)
     if (rc) return rc;
     D.k++;

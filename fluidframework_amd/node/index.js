@@ -585,6 +585,13 @@ class BatchClient {
     };
     for (let k = 0; k < recs.length; k++) {
       const src = recs[k];
+      if (src.rebase) {  // a reconnection query of an interval op (_rebase): its answer
+        while (i < n && flat[5 * i] === k) {
+          (this.rebaseRecs || (this.rebaseRecs = [])).push([k, flat[5 * i + 2] | 0]);
+          i++;
+        }
+        continue;
+      }
       if (src.regen) {  // a regenerated op (regeneratePendingOp): no event
         while (i < n && flat[5 * i] === k) {
           (this.regenRecs || (this.regenRecs = [])).push([k, flat[5 * i + 1], flat[5 * i + 2] | 0, flat[5 * i + 3],
@@ -638,6 +645,27 @@ class BatchClient {
     const op = packing.regenOps(resetOp, idx, this.regenRecs);
     this.regenRecs = null;
     return op;
+  }
+
+  /** The reconnection queries of a pending interval op
+   *  (rebaseLocalInterval, intervalCollection.ts:1735-1803), answered at once
+   *  (flush + sync): each request {pos, seqFrom, localSeq} -> Client.rebasePosition
+   *  (client.ts:755-786: the position, -1 when it slid off the string), or
+   *  {slot, localSeq} -> the slide of a pending interval end whose segment was
+   *  removed and acked (the position it moved to, -1 when it stays). */
+  _rebase(requests) {
+    if (!this.engine.docs[this.doc].events) throw new MergeTreeError(-9, "createClient(..., {events: true}) first");
+    const b = this.engine._batch();
+    const idx = requests.map((q) => (q.slot !== undefined
+      ? b.addRefRebase(this.doc, this.clients, q.slot, q.localSeq)
+      : b.addRebase(this.doc, this.clients, q.pos, q.seqFrom, q.localSeq)));
+    this.rebaseRecs = [];
+    this.engine.flush();
+    this.engine.sync();
+    if (this.engine.statuses()[this.doc] !== 0) throw docError(this.engine.statuses()[this.doc], this.doc);
+    const byIdx = new Map(this.rebaseRecs.map((r) => [r[0], r[1]]));
+    this.rebaseRecs = null;
+    return idx.map((k) => (byIdx.has(k) ? byIdx.get(k) : -1));
   }
 
   // ---- local references (documents created with {localClient: true, refs: true}) ----

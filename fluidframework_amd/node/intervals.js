@@ -341,11 +341,63 @@ class IntervalCollection {
     return this.byId.get(id);
   }
 
+  /** The local op metadata an emitted op carries ({localSeq}, :1454): the
+   *  client's merge-tree localSeq when it was made (its pending ops up to there
+   *  are in the view the op's positions refer to) -- what rebaseLocalInterval
+   *  takes back on reconnection. */
+  _meta() {
+    return { localSeq: this.client.clients.localSeq };
+  }
+
+  /** The value type's rebase of a pending op for re-sending (makeOpsMap,
+   *  :1163-1172, 1191-1200): a delete goes out unchanged (by id), an add or a
+   *  change through rebaseLocalInterval.  meta: the op's local metadata. */
+  rebaseOp(opName, value, meta) {
+    if (opName === "delete") return value;
+    return this.rebaseLocalInterval(opName, value, meta.localSeq);
+  }
+
+  /** rebaseLocalInterval (:1735-1803) for reconnection (the ops map's rebase,
+   *  :1163-1172): a pending add / change re-made at the positions
+   *  Client.rebasePosition gives its ends (from the view it was made in: its
+   *  sequenceNumber and localSeq) and the current seq, its pending change
+   *  re-queued; undefined -- the op is sent empty -- when an end slid off the
+   *  string (the interval is dropped, no event).  An end of the interval whose
+   *  segment was removed and acked since moves to its slide target at that
+   *  localSeq (changeInterval with localSeq, :1782-1799).  Replays what is
+   *  queued (flush + sync). */
+  rebaseLocalInterval(opName, v, localSeq) {
+    const id = v.properties && v.properties[reservedIntervalIdKey];
+    const ival = id === undefined ? undefined : this.byId.get(id);
+    const reqs = [];
+    if (v.start !== undefined) reqs.push({ pos: v.start, seqFrom: v.sequenceNumber, localSeq });
+    if (v.end !== undefined) reqs.push({ pos: v.end, seqFrom: v.sequenceNumber, localSeq });
+    const nPos = reqs.length;
+    // the slides ride in the same replay (ignored if an end detaches)
+    if (ival) reqs.push({ slot: ival.start.slot, localSeq }, { slot: ival.end.slot, localSeq });
+    const r = reqs.length ? this.client._rebase(reqs) : [];
+    let k = 0;
+    const start = v.start === undefined ? undefined : r[k++];
+    const end = v.end === undefined ? undefined : r[k++];
+    const rebased = { start, end, intervalType: v.intervalType, sequenceNumber: curSeq(this.client),
+      properties: v.properties };
+    if (opName === "change" && id !== undefined && (this.pendingStart.has(id) || this.pendingEnd.has(id))) {
+      this._removePending(v);
+      this._addPending(id, rebased);
+    }
+    if (start === -1 || end === -1) {
+      if (ival) this._remove(ival);  // removeExistingInterval: no event
+      return undefined;
+    }
+    if (ival && (r[nPos] !== -1 || r[nPos + 1] !== -1)) ival.stamp = ++this.stamp;  // re-added by changeInterval
+    return rebased;
+  }
+
   /** IntervalCollection.add (:1430-1460). */
   add(start, end, intervalType, props) {
     const ival = this._addInterval(start, end, intervalType, props);
     this.emitter.emit("add", undefined, { end, intervalType, properties: Object.assign({}, ival.properties),
-      sequenceNumber: curSeq(this.client), start }, {});
+      sequenceNumber: curSeq(this.client), start }, this._meta());
     this._emit("addInterval", ival, true, undefined);
     return ival;
   }
@@ -359,7 +411,7 @@ class IntervalCollection {
       const v = { intervalType: ival.intervalType, sequenceNumber: curSeq(this.client),
         properties: Object.assign({}, ival.properties) };
       this._remove(ival);
-      this.emitter.emit("delete", undefined, v, {});
+      this.emitter.emit("delete", undefined, v, this._meta());
       this._emit("deleteInterval", ival, true, undefined);
     }
     return ival;
@@ -374,7 +426,7 @@ class IntervalCollection {
       const deltas = ival.addProperties(props, true, UnassignedSequenceNumber);
       this.emitter.emit("change", undefined, { intervalType: ival.intervalType,
         sequenceNumber: curSeq(this.client),
-        properties: Object.assign({}, props, { [reservedIntervalIdKey]: id }) }, {});
+        properties: Object.assign({}, props, { [reservedIntervalIdKey]: id }) }, this._meta());
       this._emit("propertyChanged", ival, deltas, true, undefined);
     }
   }
@@ -389,7 +441,7 @@ class IntervalCollection {
     this._changeInterval(ival, start, end);
     const v = { start, end, intervalType: ival.intervalType, sequenceNumber: curSeq(this.client),
       properties: { [reservedIntervalIdKey]: id } };
-    this.emitter.emit("change", undefined, v, {});
+    this.emitter.emit("change", undefined, v, this._meta());
     this._addPending(id, v);
     if (prev) this._emitChange(ival, prev, true, undefined);
     return ival;

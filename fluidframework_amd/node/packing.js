@@ -683,6 +683,39 @@ class BatchBuilder {
     if (src) src.push({ msg: null, op: undefined, local: true });
   }
 
+  /** Client.rebasePosition(pos, seqFrom, localSeq) (client.ts:755-786) for a
+   *  pending interval op's reconnection (MTE_OP_REF, b = 4; packing.py
+   *  add_rebase): answered by one MTE_DELTA_REBASE event of the returned
+   *  record index. */
+  addRebase(doc, clients, pos, seqFrom, localSeq) {
+    if (!clients.local) throw new MergeTreeError(E_UNSUPPORTED, "rebase in an observer document");
+    if (!(localSeq >= 0 && localSeq <= clients.localSeq)) {
+      throw new MergeTreeError(E_INVALID_ARG, "localSeq " + localSeq + " > the client's " + clients.localSeq);
+    }
+    const idx = this.docCount[doc];
+    this._put(doc, 0, checkI32(seqFrom, "seq"), 0, OP_REF, 0, F_LOCAL, checkI32(pos, "pos"), 0, localSeq, 4);
+    const src = this._src(doc);
+    if (src) src.push({ msg: null, op: undefined, local: true, rebase: true });
+    return idx;
+  }
+
+  /** rebaseLocalInterval's slide of a pending interval end
+   *  (intervalCollection.ts:1782-1799; MTE_OP_REF, b = 5): one MTE_DELTA_REBASE
+   *  event, the position it moved to or -1. */
+  addRefRebase(doc, clients, slot, localSeq) {
+    if (!(slot >= 0 && slot < clients.refNext) || clients.refFree.includes(slot)) {
+      throw new MergeTreeError(E_INVALID_ARG, "no local reference in slot " + slot);
+    }
+    if (!(localSeq >= 0 && localSeq <= clients.localSeq)) {
+      throw new MergeTreeError(E_INVALID_ARG, "localSeq " + localSeq + " > the client's " + clients.localSeq);
+    }
+    const idx = this.docCount[doc];
+    this._put(doc, 0, 0, 0, OP_REF, 0, F_LOCAL, 0, slot, localSeq, 5);
+    const src = this._src(doc);
+    if (src) src.push({ msg: null, op: undefined, local: true, rebase: true });
+    return idx;
+  }
+
   /** One MergeTree-level call (insertSegments / markRangeRemoved / annotateRange):
    *  a record that does not close a message (no window update). */
   addRaw(doc, seq, ref, msn, client, op) {

@@ -427,6 +427,30 @@ class BatchBuilder:
         self.ops[doc].append((0, 0, 0, OP_REF, 0, F_LOCAL, _check_i32(pos, "pos"), slot, ref_type, 0))
         return slot
 
+    def add_rebase(self, doc: int, clients: DocClients, pos: int, seq_from: int, local_seq: int):
+        """Client.rebasePosition(pos, seq_from, local_seq) (client.ts:755-786)
+        for a pending interval op's reconnection (rebaseLocalInterval,
+        intervalCollection.ts:1735-1803): an MTE_OP_REF record with b = 4,
+        answered by one MTE_DELTA_REBASE event (the position, -1 detached)."""
+        if not clients.local:
+            raise MergeTreeError(MTE_E_UNSUPPORTED, "rebase in an observer document")
+        if not 0 <= local_seq <= clients.local_seq:
+            raise MergeTreeError(MTE_E_INVALID_ARG, f"localSeq {local_seq} > the client's {clients.local_seq}")
+        self.ops[doc].append((0, _check_i32(seq_from, "seq"), 0, OP_REF, 0, F_LOCAL, _check_i32(pos, "pos"), 0,
+                              local_seq, 4))
+
+    def add_ref_rebase(self, doc: int, clients: DocClients, slot: int, local_seq: int):
+        """rebaseLocalInterval's slide of a pending interval end
+        (intervalCollection.ts:1782-1799): the reference in slot moves to its
+        slide target's position in the view at local_seq if its segment is
+        removed and acked (MTE_OP_REF b = 5; one MTE_DELTA_REBASE event, -1 when
+        it stays)."""
+        if not 0 <= slot < clients.ref_next or slot in clients.ref_free:
+            raise MergeTreeError(MTE_E_INVALID_ARG, f"no local reference in slot {slot}")
+        if not 0 <= local_seq <= clients.local_seq:
+            raise MergeTreeError(MTE_E_INVALID_ARG, f"localSeq {local_seq} > the client's {clients.local_seq}")
+        self.ops[doc].append((0, 0, 0, OP_REF, 0, F_LOCAL, 0, slot, local_seq, 5))
+
     def remove_ref(self, doc: int, clients: DocClients, slot: int):
         """removeLocalReferencePosition (mergeTree.ts:2113-2123)."""
         if not 0 <= slot < clients.ref_next or slot in clients.ref_free:

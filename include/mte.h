@@ -118,6 +118,8 @@ extern "C" {
  * that record events (MTE_DOC_EVENTS).                                       */
 #define MTE_OP_REGEN 6
 #define MTE_DELTA_REGEN 0x10u
+/* the answer of an MTE_OP_REF record with b = 4 / 5 (pos; len 0) */
+#define MTE_DELTA_REBASE 0x20u
 /* Follows an annotate's MTE_OP_ROLLBACK (a local record): for each key k the
  * rolled-back annotate set (pos1 = k), the older pending annotates that set k
  * too, latest first -- pos2 = its group slot, a = the value id it set, seq =
@@ -145,6 +147,24 @@ extern "C" {
  *   3 retype: the reference takes type a; if it becomes SlideOnRemove and its
  *     segment is already removed and acked it slides now (ackInterval's
  *     StayOnRemove -> SlideOnRemove conversion, intervalCollection.ts:1805-1902).
+ *   4 rebase a position (an interval collection's reconnection,
+ *     rebaseLocalInterval intervalCollection.ts:1735-1803 ->
+ *     Client.rebasePosition client.ts:755-786): pos1 in the local client's view
+ *     at refSeq ref_seq and localSeq a (the pending op's; a <= the document's
+ *     localSeq) -> the segment holding it, else the last segment at offset 0;
+ *     slid as getSlideToSegment slides (client.ts:1117-1130) if removed and
+ *     acked; its position in the view at (currentSeq, a) plus the offset
+ *     (findReconnectionPosition :709-713), -1 (DetachedReferencePosition) when
+ *     nothing is left to slide to.  Reported as one MTE_DELTA_REBASE event
+ *     (pos = the position).  pos2 = 0.
+ *   5 re-place a pending interval end on reconnection
+ *     (intervalCollection.ts:1782-1799): the reference in slot pos2, if its
+ *     segment is removed and acked, moves to the position of its slide target
+ *     in the view at (currentSeq, a) -- to what getContainingSegment finds there
+ *     (createPositionReference with localSeq :639-658), detached if nothing;
+ *     one MTE_DELTA_REBASE event, pos = that position, -1 if it did not move.
+ *   b = 4 / 5 only in MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS documents (the
+ *   HBM tree pass).
  * The engine slides references as the reference does
  * (slideAckedRemovedSegmentReferences, mergeTree.ts:893-950): when a segment
  * becomes removed and acked -- a remote remove newly removing it or
@@ -449,7 +469,8 @@ int mte_read_refs(mte_ctx* ctx, uint32_t doc, int32_t* pos, uint32_t n);
 int mte_read_refs_transient(mte_ctx* ctx, uint32_t doc, int32_t* pos, uint32_t n);
 /* Document order of reference slots [0, n): the index, among every text unit
  * the document holds (removed segments included), of the unit the reference
- * sits on; -1 for a detached or unused slot.  Two references compare as
+ * sits on (a reference that slid off the string: the unit it still points at,
+ * while held); -1 for a detached or unused slot.  Two references compare as
  * compareReferencePositions does (referencePositions.ts:81-89: the same
  * segment by offset, else by segment ordinal; detached first) -- the order of
  * an interval collection's tree (intervalCollection.ts:483-520).            */

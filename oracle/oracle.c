@@ -410,6 +410,9 @@ static inline int removed_and_acked(const oseg* g) { return g->rseq != NONE_SEQ 
  *     getSlideToSegment, :1805-1902). */
 static int doc_ref(odoc* d, const mte_op* op) {
   if (!(d->flags & MTE_DOC_REFS)) return MTE_E_UNSUPPORTED;
+  /* b = 4 / 5 (reconnection of pending interval ops): titems.c, the HBM tree
+   * pass's restatement, only */
+  if (op->b == 4 || op->b == 5) return MTE_E_UNSUPPORTED;
   if (op->pos2 < 0 || (uint32_t)op->pos2 >= REF_LIMIT || op->b > 3) return MTE_E_INVALID_ARG;
   const uint32_t slot = (uint32_t)op->pos2;
   if (slot >= d->ref_cap) {
@@ -1117,7 +1120,7 @@ int orc_apply_batch(orc_ctx* c, const mte_batch* b, int n_threads) {
     }
     if (op->type >= MTE_OP_ROLLBACK && !(op->flags & MTE_F_LOCAL)) return MTE_E_INVALID_ARG;
     if (op->type == MTE_OP_REF) {
-      if (!(c->docs[dcur].flags & MTE_DOC_REFS) || op->seq != 0 || op->pos2 < 0 || op->b > 3 ||
+      if (!(c->docs[dcur].flags & MTE_DOC_REFS) || op->seq != 0 || op->pos2 < 0 || op->b > 5 ||
           op->client >= MTE_MAX_CLIENTS)
         return MTE_E_INVALID_ARG;
       continue;
@@ -1304,7 +1307,7 @@ int orc_read_ref_order(orc_ctx* c, uint32_t doc, int64_t* key, uint32_t n) {
     key[r] = -1;
     if (r >= d->ref_hi) continue;
     const uint32_t st = d->ref_state[r], u = d->ref_anchor[r];
-    if (!(st & REF_LIVE) || (st & REF_DETACHED)) continue;
+    if (!(st & REF_LIVE) || ((st & REF_DETACHED) && !(st & REF_OFF))) continue; /* off the string: on its segment */
     int64_t p = 0;
     for (uint32_t i = 0; i < d->n; i++) {
       const oseg* g = &d->s[i];

@@ -29,6 +29,15 @@
 //         queries at seeded positions: findOverlappingIntervals, previousInterval,
 //         nextInterval and the start / end position iterators (:881-913,
 //         :1987-2067); the queries draw from their own generator
+//          reconnect: the chance per step that a sending client goes offline,
+//         or, offline, reconnects.  Offline, its merge-tree ops (["H", op]) and
+//         interval ops (["J", {opName, value}]) stay pending, unsent;
+//         reconnecting, it catches up with the whole log, then re-sends them
+//         in order as the container runtime's reSubmit does: merge-tree ops
+//         through Client.regeneratePendingOp (["G", logIndex]), interval ops
+//         through the value type's rebase (makeOpsMap :1163-1172 ->
+//         rebaseLocalInterval :1735-1803, with the op's localSeq metadata;
+//         ["K", logIndex], the value undefined when the interval slid off)
 // stdout: {"sets": [{..params, "names", "log": [[clientId, seq, ref, msn, kind, contents]]
 //                    (kind "op": a merge-tree op; "iv": {opName, value}),
 //                    "events": per client [["L"|"A", logIndex] | ["I", logIndex]
@@ -79,7 +88,72 @@ const clone = (v) => JSON.parse(JSON.stringify(v));
 const LABEL = "farm";
 const KEYS = ["client", "bold", "color"];
 
+// reconnect farms: each localSeq view the reference computes -- rebasePosition
+// (client.ts:755-786), findReconnectionPosition (:709-713) and getPosition
+// with a localSeq (:345-350) -- checked against the same view summed leaf by
+// leaf with localNetLength (mergeTree.ts:575-593), the rule the engine
+// restates.  The reference takes block lengths from its local partial lengths
+// (partialLengths.ts:667-700), which can disagree with its own leaf rule (a
+// local removal of a segment inserted after refSeq is subtracted while the
+// insertion is not counted; the partials cached by computeLocalPartials keep
+// the window of the first query since the last length update,
+// mergeTree.ts:964-982); the farm counts the calls where they differ.
+const leafViews = { calls: 0, differ: 0 };
+function leafHooks() {
+  const leaves = (mt) => {
+    const out = [];
+    const walk = (n) => { if (n.isLeaf()) out.push(n); else for (let i = 0; i < n.childCount; i++) walk(n.children[i]); };
+    walk(mt.root);
+    return out;
+  };
+  const prefix = (c, seg, refSeq, ls) => {
+    let q = 0;
+    for (const x of leaves(c._mergeTree)) {
+      if (x === seg) return q;
+      q += c._mergeTree.localNetLength(x, refSeq, ls) || 0;
+    }
+    return -1;
+  };
+  const P = Client.prototype;
+  const rebase0 = P.rebasePosition, frp0 = P.findReconnectionPosition, gp0 = P.getPosition;
+  let depth = 0;
+  const check = (r, e) => { leafViews.calls++; if (r !== e) leafViews.differ++; };
+  P.rebasePosition = function (pos, seqFrom, localSeq) {
+    depth++;
+    const r = rebase0.call(this, pos, seqFrom, localSeq);
+    depth--;
+    const mt = this._mergeTree;
+    let p0 = 0, seg, off = 0;
+    for (const x of leaves(mt)) {
+      const l = mt.localNetLength(x, seqFrom, localSeq) || 0;
+      if (l > 0 && pos >= p0 && pos < p0 + l) { seg = x; off = pos - p0; break; }
+      p0 += l;
+    }
+    if (!seg) { let f = mt.root; while (!f.isLeaf()) f = f.children[f.childCount - 1]; seg = f; off = 0; }
+    const so = this.getSlideToSegment({ segment: seg, offset: off });
+    check(r, so.segment ? prefix(this, so.segment, this.getCurrentSeq(), localSeq) + so.offset : -1);
+    return r;
+  };
+  P.findReconnectionPosition = function (segment, localSeq) {
+    const r = frp0.call(this, segment, localSeq);
+    if (!depth) check(r, prefix(this, segment, this.getCurrentSeq(), localSeq));
+    return r;
+  };
+  P.getPosition = function (segment, localSeq) {
+    const r = gp0.call(this, segment, localSeq);
+    if (!depth && localSeq !== undefined && segment && segment.parent) {
+      check(r, prefix(this, segment, this.getCurrentSeq(), localSeq));
+    }
+    return r;
+  };
+}
+
 function runSet(p) {
+  if (p.reconnect && !leafHooks.done) {
+    leafHooks();
+    leafHooks.done = true;
+  }
+  const v0 = { calls: leafViews.calls, differ: leafViews.differ };
   const R = rng(p.seed);
   const names = [];
   for (let i = 0; i < p.clients; i++) names.push(String.fromCharCode(65 + i));
@@ -90,7 +164,7 @@ function runSet(p) {
     const c = new Client(specToSegment, logger, { mergeTreeUseNewLengthCalculations: true });
     if (p.initialText) c.insertSegmentLocal(0, new TextSegment(p.initialText));
     c.startOrUpdateCollaboration(n);
-    const emitter = { emit(opName, _prev, params) { sent[i] = { opName, value: clone(params) }; } };
+    const emitter = { emit(opName, _prev, params, meta) { sent[i] = { opName, value: clone(params), meta }; } };
     const coll = factory.load(emitter, []);
     coll.attachGraph(c, LABEL);
     const X = { c, coll, lastSeq: 0, ids: [], ev: [], mt: false };
@@ -106,6 +180,8 @@ function runSet(p) {
     return X;
   });
   const Q = rng(p.seed ^ 0x5bd1e995);
+  const offline = names.map(() => false);
+  const held = names.map(() => []);
   const cursor = names.map(() => 0);
   const events = names.map(() => []);
   const log = [];
@@ -124,7 +200,8 @@ function runSet(p) {
       X.c.applyMsg(msg);
       X.mt = false;
     } else {
-      ops.get(m[5].opName).process(X.coll, clone(m[5].value), m[0] === names[i], msg);
+      const v = m[5].value === undefined ? undefined : clone(m[5].value);  // slid off while rebasing
+      ops.get(m[5].opName).process(X.coll, v, m[0] === names[i], msg);
     }
     X.lastSeq = m[1];
     events[i].push(["A", cursor[i]]);
@@ -165,13 +242,35 @@ function runSet(p) {
   const checkpoint = () => {
     checkpoints.push({ done: events.map((e) => e.length), states: clients.map(readOut) });
   };
-  const send = (i, kind, contents) => {
+  const send = (i, kind, contents, ev) => {
     seq++;
     log.push([names[i], seq, clients[i].lastSeq, msnNow(), kind, contents]);
-    events[i].push([kind === "op" ? "L" : "I", log.length - 1]);
+    events[i].push([ev || (kind === "op" ? "L" : "I"), log.length - 1]);
+  };
+  const reconnect = (i) => {
+    const X = clients[i];
+    while (cursor[i] < log.length) applyNext(i);  // every op it sent is acked
+    for (const h of held[i]) {
+      if (h.op) {
+        send(i, "op", clone(X.c.regeneratePendingOp(h.op, h.sg)), "G");
+      } else {
+        const { rebasedOp } = ops.get(h.opName).rebase(X.coll, { opName: h.opName, value: h.value }, h.meta);
+        send(i, "iv", { opName: h.opName, value: rebasedOp.value === undefined ? undefined : clone(rebasedOp.value) },
+          "K");
+      }
+    }
+    held[i] = [];
+    offline[i] = false;
   };
 
   for (let step = 0; step < p.steps; step++) {
+    if (p.reconnect && R.next() < p.reconnect) {
+      const r = R.int(1, p.clients - 1);
+      if (offline[r]) reconnect(r);
+      else offline[r] = true;
+      if ((step + 1) % every === 0 && step + 1 < p.steps) checkpoint();
+      continue;
+    }
     const i = R.int(1, p.clients - 1);
     const X = clients[i];
     const len = X.c.getLength();
@@ -200,7 +299,13 @@ function runSet(p) {
           X.coll.removeIntervalById(id);
         }
       }
-      if (sent[i]) send(i, "iv", sent[i]);
+      if (sent[i] && offline[i]) {
+        // made offline: pending, not sent
+        held[i].push({ opName: sent[i].opName, value: sent[i].value, meta: sent[i].meta });
+        events[i].push(["J", { opName: sent[i].opName, value: sent[i].value }]);
+      } else if (sent[i]) {
+        send(i, "iv", { opName: sent[i].opName, value: sent[i].value });
+      }
     } else if (R.next() < 0.5) {
       // a merge-tree op (as oracle/ref_farm.js)
       let op;
@@ -216,7 +321,12 @@ function runSet(p) {
         else op = X.c.annotateRangeLocal(start, end, { [KEYS[R.int(0, 2)]]: R.int(0, 5) }, undefined);
       }
       X.mt = false;
-      if (op) send(i, "op", clone(op));
+      if (op && offline[i]) {
+        held[i].push({ op, sg: X.c.peekPendingSegmentGroups() });
+        events[i].push(["H", clone(op)]);
+      } else if (op) {
+        send(i, "op", clone(op));
+      }
     } else {
       const j = R.int(0, p.clients - 1);
       const k = R.int(1, 6);
@@ -224,15 +334,19 @@ function runSet(p) {
     }
     if ((step + 1) % every === 0 && step + 1 < p.steps) checkpoint();
   }
+  for (let i = 0; i < p.clients; i++) if (offline[i]) reconnect(i);
   for (let i = 0; i < p.clients; i++) while (cursor[i] < log.length) applyNext(i);
   checkpoint();
   const last = checkpoints[checkpoints.length - 1].states;
+  let diverged = null;  // allowDiverge: the clients' final states differ (recorded, not thrown)
   for (const s of last) {
     if (s.text !== last[0].text || JSON.stringify(s.intervals) !== JSON.stringify(last[0].intervals)) {
-      throw new Error(`seed ${p.seed}: the reference clients did not converge`);
+      if (!p.allowDiverge) throw new Error(`seed ${p.seed}: the reference clients did not converge`);
+      diverged = s.text !== last[0].text ? "text" : "intervals";
     }
   }
-  return Object.assign({}, p, { names, log, events, checkpoints });
+  const lv = p.reconnect ? { leafViews: { calls: leafViews.calls - v0.calls, differ: leafViews.differ - v0.differ } } : {};
+  return Object.assign({}, p, { names, log, events, checkpoints }, diverged ? { diverged } : {}, lv);
 }
 
 const input = JSON.parse(fs.readFileSync(0, "utf8"));

@@ -65,7 +65,9 @@ typedef struct {
   /* localRemovedSeq: the localSeq of the client's pending removal, kept when
    * a remote remove overtakes it (the segment stays in that removal's group
    * until the ack, mergeTreeNodes.ts:487-497), 0 = none */
-  int32_t lrs;
+  int32_t lrs; /* localRemovedSeq; | LRS_RELEASED once a regeneration dequeued the
+                 segment from its group (it keeps the value, the group no longer
+                 holds it: resetPendingDeltaToOps, client.ts:802-857) */
 } item;
 
 typedef struct {
@@ -122,6 +124,7 @@ typedef struct {
 } env_t;
 
 #define LOCAL_BASE MTE_LOCAL_SEQ_BASE
+#define LRS_RELEASED 0x40000000 /* item.lrs: see there (localSeqs stay below it) */
 static inline int is_pending(int32_t seq) { return seq >= LOCAL_BASE && seq != NONE_SEQ; }
 
 /* ---- storage --------------------------------------------------------------- */
@@ -381,7 +384,7 @@ static int scour(idoc* d, uint32_t s, uint32_t e, const uint16_t* arena, uint32_
     }
     const uint32_t xe = leaf_end(d, i);
     const int64_t xl = leaf_total(d, i, xe);
-    if (is_pending(x->seq) || x->lrs || x->am) {
+    if (is_pending(x->seq) || (x->lrs && !(x->lrs & LRS_RELEASED)) || x->am) {
       /* a segment of a pending group (segmentGroups not empty, mergeTree.ts:686,
        * 736-739) is held and ends the append run */
       held++;
@@ -673,11 +676,122 @@ static int ref_reserve(idoc* d, uint32_t slot) {
   return MTE_OK;
 }
 
+static int delta_push(idoc* d, uint32_t kind, int64_t pos, int32_t len, uint32_t removed);
+
+/* the length of an item in the local client's view at refSeq rs0 and localSeq
+ * ls (localNetLength with a localSeq, mergeTree.ts:575-593): acked text up to
+ * rs0 less acked removals up to rs0, own pending inserts up to ls, less own
+ * removals up to ls */
+static inline int32_t view_len(const item* g, int32_t rs0, int32_t ls) {
+  if (g->empty) return 0;
+  if (g->lrs && (g->lrs & ~LRS_RELEASED) <= ls) return 0;
+  if (is_pending(g->seq)) return g->seq - LOCAL_BASE > ls ? 0 : g->len;
+  if (g->seq > rs0) return 0;
+  if (is_pending(g->rseq)) return g->rseq - LOCAL_BASE <= ls ? 0 : g->len;
+  return (g->rseq != NONE_SEQ && g->rseq <= rs0) ? 0 : g->len;
+}
+
+static int64_t view_prefix(const idoc* d, uint32_t g, int32_t rs0, int32_t ls) {
+  int64_t p = 0;
+  for (uint32_t i = 0; i < g; i++) p += view_len(&d->it[i], rs0, ls);
+  return p;
+}
+
+/* getContainingSegment(pos) in that view (mergeTree.ts:872-885): the first item
+ * of positive length holding pos; -1 past the end */
+static int64_t view_find(const idoc* d, int64_t pos, int32_t rs0, int32_t ls, int32_t* off) {
+  int64_t p = 0;
+  for (uint32_t i = 0; i < d->n; i++) {
+    const int32_t l = view_len(&d->it[i], rs0, ls);
+    if (l > 0 && pos >= p && pos < p + l) {
+      *off = (int32_t)(pos - p);
+      return i;
+    }
+    p += l;
+  }
+  return -1;
+}
+
+/* Client.getSlideToSegment (client.ts:1117-1130) from item x, removed and
+ * acked: offset 0 of the first following item a reference may slide to, else
+ * the last unit of the last preceding one; -1 when there is none */
+static int64_t slide_item(const idoc* d, uint32_t x, int32_t* off) {
+  for (uint32_t j = x + 1; j < d->n; j++)
+    if (slide_target_ok(&d->it[j])) {
+      *off = 0;
+      return j;
+    }
+  for (int64_t j = (int64_t)x - 1; j >= 0; j--)
+    if (slide_target_ok(&d->it[j])) {
+      *off = d->it[j].len - 1;
+      return j;
+    }
+  return -1;
+}
+
+/* MTE_OP_REF b = 4 (include/mte.h): Client.rebasePosition (client.ts:755-786)
+ * of pos1 from the view at (ref_seq, a) to the view at (currentSeq, a); b = 5:
+ * rebaseLocalInterval's slide of a pending interval end
+ * (intervalCollection.ts:1782-1799).  One MTE_DELTA_REBASE event each. */
+static int doc_ref_rebase(idoc* d, const mte_op* op) {
+  const int32_t ls = (int32_t)op->a;
+  if (!(d->flags & MTE_DOC_LOCAL_CLIENT) || ls < 0 || ls > d->local_seq) return MTE_E_INVALID_ARG;
+  if (!(d->flags & MTE_DOC_EVENTS)) return MTE_E_UNSUPPORTED;
+  d->scanned += d->n;
+  if (op->b == 4) {
+    int32_t off = 0;
+    int64_t x = view_find(d, op->pos1, op->ref_seq, ls, &off);
+    if (x < 0) { /* past every segment of the view: the tree's last leaf, offset 0 */
+      for (int64_t j = (int64_t)d->n - 1; j >= 0 && x < 0; j--)
+        if (!d->it[j].empty) x = j;
+      off = 0;
+    }
+    int64_t p = -1;
+    if (x >= 0) {
+      int64_t t = x;
+      if (removed_and_acked(&d->it[x])) t = slide_item(d, (uint32_t)x, &off);
+      if (t >= 0) p = view_prefix(d, (uint32_t)t, d->cur_seq, ls) + off;
+    }
+    return delta_push(d, MTE_DELTA_REBASE, p, 0, 0);
+  }
+  const uint32_t slot = (uint32_t)op->pos2;
+  if (slot >= d->ref_hi || !(d->ref_state[slot] & REF_LIVE)) return MTE_E_INVALID_ARG;
+  int64_t p = -1;
+  uint32_t st = d->ref_state[slot];
+  if (!(st & REF_DETACHED)) {
+    for (uint32_t i = 0; i < d->n; i++) {
+      const item* g = &d->it[i];
+      if (g->empty || d->ref_anchor[slot] - g->toff >= (uint32_t)g->len) continue;
+      if (removed_and_acked(g)) {
+        int32_t off = 0, o2 = 0;
+        const int64_t t = slide_item(d, i, &off);
+        int64_t y = -1;
+        if (t >= 0) {
+          p = view_prefix(d, (uint32_t)t, d->cur_seq, ls) + off;
+          y = view_find(d, p, d->cur_seq, ls, &o2);
+        }
+        if (y >= 0) d->ref_anchor[slot] = d->it[y].toff + (uint32_t)o2;
+        else { /* the reference throws: no segment there */
+          d->ref_anchor[slot] = 0;
+          d->ref_state[slot] = st | REF_DETACHED;
+        }
+      }
+      break;
+    }
+  }
+  return delta_push(d, MTE_DELTA_REBASE, p, 0, 0);
+}
+
 /* MTE_OP_REF (oracle.c doc_ref): b = 0 create in the local view, 1 remove,
- * 2 create in a sequenced op's perspective, 3 become SlideOnRemove */
+ * 2 create in a sequenced op's perspective, 3 become SlideOnRemove, 4 / 5
+ * reconnection (doc_ref_rebase) */
 static int doc_ref(idoc* d, const mte_op* op) {
   if (!(d->flags & MTE_DOC_REFS)) return MTE_E_UNSUPPORTED;
-  if (op->pos2 < 0 || (uint32_t)op->pos2 >= REF_LIMIT || op->b > 3) return MTE_E_INVALID_ARG;
+  if (op->pos2 < 0 || (uint32_t)op->pos2 >= REF_LIMIT || op->b > 5) return MTE_E_INVALID_ARG;
+  if (op->b >= 4) {
+    d->ops++;
+    return doc_ref_rebase(d, op);
+  }
   const uint32_t slot = (uint32_t)op->pos2;
   int rc;
   if ((rc = ref_reserve(d, slot))) return rc;
@@ -1082,7 +1196,7 @@ static int doc_rollback(idoc* d, const mte_op* op, const env_t* env) {
 static inline int32_t len_at_local_seq(const item* g, int32_t ls) {
   if (g->empty) return 0;
   if (is_pending(g->seq) && g->seq - LOCAL_BASE > ls) return 0;
-  if (g->lrs && g->lrs <= ls) return 0;
+  if (g->lrs && (g->lrs & ~LRS_RELEASED) <= ls) return 0;
   if (g->rseq != NONE_SEQ && (!is_pending(g->rseq) || g->rseq - LOCAL_BASE <= ls)) return 0;
   return g->len;
 }
@@ -1113,7 +1227,7 @@ static int doc_regen(idoc* d, const mte_op* op) {
      * client.ts:803-852): a removal a remote remove overtook, an annotated
      * segment removed since -- the zamboni no longer holds it for the group */
     if (!g->empty && !hit) {
-      if (t == MTE_OP_REMOVE && g->lrs == ls) g->lrs = 0;
+      if (t == MTE_OP_REMOVE && g->lrs == ls) g->lrs |= LRS_RELEASED;
       if (t == MTE_OP_ANNOTATE) g->am &= ~(1u << op->a);
     }
     if (hit) {
@@ -1436,7 +1550,7 @@ int oti_apply_batch(oti_ctx* c, const mte_batch* b, int n_threads) {
     }
     if (op->type >= MTE_OP_ROLLBACK && !(op->flags & MTE_F_LOCAL)) return MTE_E_INVALID_ARG;
     if (op->type == MTE_OP_REF) {
-      if (!(c->docs[dcur].flags & MTE_DOC_REFS) || op->seq != 0 || op->pos2 < 0 || op->b > 3 ||
+      if (!(c->docs[dcur].flags & MTE_DOC_REFS) || op->seq != 0 || op->pos2 < 0 || op->b > 5 ||
           op->client >= MTE_MAX_CLIENTS)
         return MTE_E_INVALID_ARG;
       continue;
@@ -1668,7 +1782,7 @@ int oti_read_ref_order(oti_ctx* c, uint32_t doc, int64_t* key, uint32_t n) {
     key[r] = -1;
     if (r >= d->ref_hi) continue;
     const uint32_t st = d->ref_state[r], u = d->ref_anchor[r];
-    if (!(st & REF_LIVE) || (st & REF_DETACHED)) continue;
+    if (!(st & REF_LIVE) || ((st & REF_DETACHED) && !(st & REF_OFF))) continue; /* off the string: on its segment */
     int64_t p = 0;
     for (uint32_t i = 0; i < d->n; i++) {
       const item* g = &d->it[i];

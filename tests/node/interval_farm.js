@@ -22,15 +22,26 @@
 //                   serializeInternal() and the recorded queries; then each
 //                   set's final summary loads into a fresh client whose
 //                   intervals must equal the reference's.
+//   argv[2] "reconnect": as "ext" on interval_reconnect_vectors.json.gz, whose
+//                   clients also go offline: "H" / "J" a merge-tree / interval op
+//                   made offline (held), "G" / "K" its re-send on reconnection --
+//                   BatchClient.regeneratePendingOp / the collection's
+//                   rebaseLocalInterval with the op's localSeq metadata -- which
+//                   must equal the op the reference re-sent.
 const fs = require("fs");
 const path = require("path");
 const zlib = require("zlib");
 const { MergeTreeEngine } = require("../../fluidframework_amd/node");
 
 const mode = process.argv[2] || "gpu";
-const ext = mode === "ext";
+const rec = mode === "reconnect";
+const ext = mode === "ext" || rec;
 const sets = JSON.parse(zlib.gunzipSync(fs.readFileSync(path.join(__dirname, "..", "golden",
-  process.argv[4] || (ext ? "interval_ext_vectors.json.gz" : "interval_vectors.json.gz")))).toString("utf8")).sets;
+  process.argv[4] || (rec ? "interval_reconnect_vectors.json.gz"
+    : ext ? "interval_ext_vectors.json.gz" : "interval_vectors.json.gz")))).toString("utf8")).sets
+  // reconnect: the farms in which every localSeq view the reference computed
+  // equals its own leaf rule (oracle/ref_interval_farm.js leafViews)
+  .filter((s) => !rec || (s.leafViews && s.leafViews.differ === 0));
 const nSets = process.argv[3] && process.argv[3] !== "all" ? Number(process.argv[3]) : sets.length;
 const LABEL = "farm";
 
@@ -61,8 +72,9 @@ for (let si = 0; si < nSets; si++) {
   sets[si].names.forEach((name, ci) => {
     const L = { si, ci, sent: null };
     L.client = eng.createClient(sets[si].initialText, { newLengthCalc: true, localClient: true, refs: true,
-      longClientId: name });
-    L.coll = L.client.getIntervalCollection(LABEL, { emit(opName, _p, value) { L.sent = { opName, value }; } });
+      longClientId: name, events: rec });
+    L.held = [];
+    L.coll = L.client.getIntervalCollection(LABEL, { emit(opName, _p, value, meta) { L.sent = { opName, value, meta }; } });
     if (ext) {
       L.ev = [];
       const pos = (r) => L.client.localReferencePositionToPosition(r);
@@ -90,6 +102,7 @@ eng.start();
 const prev = layout.map(() => 0);
 const failures = [];
 const extFail = {}, extFirst = {}, prevNext = { n: 0, equal: 0 };
+const regens = [];  // [got, want, original] of each regenerated merge-tree op
 let passed = 0, opsChecked = 0;
 const nCp = Math.max.apply(null, sets.slice(0, nSets).map((s) => s.checkpoints.length));
 for (let j = 0; j < nCp; j++) {
@@ -97,23 +110,48 @@ for (let j = 0; j < nCp; j++) {
     const s = sets[L.si];
     if (j >= s.checkpoints.length) return;
     const done = s.checkpoints[j].done[L.ci];
+    if (L.broken) return;
     for (const [kind, li] of s.events[L.ci].slice(prev[d], done)) {
-      const m = s.log[li];
+     try {
+      const m = typeof li === "number" ? s.log[li] : [null, 0, 0, 0, kind === "H" ? "op" : "iv", li];
       const msg = { clientId: m[0], sequenceNumber: m[1], referenceSequenceNumber: m[2], minimumSequenceNumber: m[3],
         type: "op", contents: m[5] };
       if (kind === "A") {
         if (m[4] === "op") L.client.applyMsg(msg);
-        else L.coll.process(m[5].opName, clone(m[5].value), m[0] === s.names[L.ci], msg);
+        else L.coll.process(m[5].opName, m[5].value === undefined ? undefined : clone(m[5].value),
+          m[0] === s.names[L.ci], msg);
         continue;
       }
-      if (kind === "L") {
+      if (kind === "L" || kind === "H") {
         const o = m[5];
-        if (o.type === 0) L.client.insertSegmentLocal(o.pos1, o.seg);
-        else if (o.type === 1) L.client.removeRangeLocal(o.pos1, o.pos2);
-        else L.client.annotateRangeLocal(o.pos1, o.pos2, o.props);
+        let made;
+        if (o.type === 0) made = L.client.insertSegmentLocal(o.pos1, o.seg);
+        else if (o.type === 1) made = L.client.removeRangeLocal(o.pos1, o.pos2);
+        else made = L.client.annotateRangeLocal(o.pos1, o.pos2, o.props);
+        if (kind === "H") L.held.push({ op: made });
         continue;
       }
-      // "I": the client's own interval op, re-made through the collection API
+      if (kind === "G" || kind === "K") {
+        // reconnection: the held ops re-sent in order
+        const h = L.held.shift();
+        const got = kind === "G" ? (h && h.op ? L.client.regeneratePendingOp(h.op) : null)
+          : (h && h.iv ? L.coll.rebaseOp(h.iv.opName, h.iv.value, h.iv.meta) : null);
+        let want = kind === "G" ? m[5] : m[5].value;
+        if (kind === "K" && m[5].opName === "delete" && want) {  // a delete's positions are informational
+          want = clone(want);
+          delete want.start;
+          delete want.end;
+        }
+        // regenerated ops: compared in Python (fixtures_util.canon_regen)
+        if (kind === "G") regens.push([got, want, h && h.op]);
+        else if (JSON.stringify(sortKeys(got === undefined ? null : clone(got))) !==
+            JSON.stringify(sortKeys(want === undefined ? null : want))) {
+          failures.push([L.si, L.ci, j, "rebase", got, want]);
+        }
+        opsChecked++;
+        continue;
+      }
+      // "I" / "J": the client's own interval op, re-made through the collection API
       const { opName, value } = m[5];
       const id = value.properties && value.properties.intervalId;
       L.sent = null;
@@ -137,7 +175,13 @@ for (let j = 0; j < nCp; j++) {
       if (!L.sent || L.sent.opName !== opName || JSON.stringify(sortKeys(got)) !== JSON.stringify(sortKeys(want))) {
         failures.push([L.si, L.ci, j, "op", L.sent, m[5]]);
       }
+      if (kind === "J" && L.sent) L.held.push({ iv: L.sent });
       opsChecked++;
+     } catch (e) {  // the client stops here; the failure says where
+      failures.push([L.si, L.ci, j, "throw", kind, String(e && e.message)]);
+      L.broken = true;
+      return;
+     }
     }
     prev[d] = done;
   });
@@ -156,7 +200,7 @@ for (let j = 0; j < nCp; j++) {
   }
   layout.forEach((L) => {
     const s = sets[L.si];
-    if (j >= s.checkpoints.length) return;
+    if (j >= s.checkpoints.length || L.broken) return;
     const want = s.checkpoints[j].states[L.ci];
     const ivs = Array.from(L.coll.byId.values()).map((x) => {
       const [a, b] = x.positions();
@@ -247,7 +291,8 @@ if (ext) {
   }
 }
 if (mode !== "pack") {
-  process.stdout.write(JSON.stringify({ passed, opsChecked, loaded, unloadable, extFail, extFirst, prevNext, failures: failures.slice(0, 16),
+  process.stdout.write(JSON.stringify({ passed, opsChecked, loaded, unloadable, extFail, extFirst, prevNext, regens,
+    failures: failures.slice(0, 16),
     nFailures: failures.length, docs: layout.length }) + "\n");
 } else {
   process.stdout.write(JSON.stringify({ done: true, opsChecked, failures: failures.slice(0, 16),

@@ -178,3 +178,56 @@ def test_node_interval_events_order_queries_summaries_on_gpu():
     # previousInterval / nextInterval follow the end order; the reference's end
     # tree keeps one node per end (rbTree.ts:249-300) and differs where ends coincide
     assert j["prevNext"]["equal"] >= 0.8 * j["prevNext"]["n"], j["prevNext"]
+
+
+def reconnect_sets():
+    with gzip.open(os.path.join(HERE, "golden", "interval_reconnect_vectors.json.gz"), "rt", encoding="utf-8") as fh:
+        return json.load(fh)
+
+
+def test_interval_reconnect_vectors_shape():
+    """The reference's reconnection farms (make_interval_golden.py --reconnect):
+    clients go offline, hold merge-tree and interval ops, and re-send them in
+    order -- regeneratePendingOp ("G") and rebaseLocalInterval ("K") -- among
+    remote edits; seeds whose reference run threw (a rebased interval end with
+    no segment at its slide position, "Non-transient references need segment",
+    or its own end-tree crash) are listed, not kept."""
+    v = reconnect_sets()
+    sets = v["sets"]
+    assert len(sets) == 33 and len(v["seeds_the_reference_failed"]) == 31
+    # localSeq views: the reference's (block partial lengths) against its own leaf rule
+    lv = [s["leafViews"] for s in sets]
+    assert sum(x["calls"] for x in lv) > 6000 and 0 < sum(x["differ"] for x in lv) < 0.04 * sum(x["calls"] for x in lv)
+    assert sum(x["differ"] == 0 for x in lv) == 8
+    ev = [e for s in sets for cl in s["events"] for e in cl]
+    assert sum(e[0] == "K" for e in ev) > 1000 and sum(e[0] == "G" for e in ev) > 800
+    assert sum(e[0] == "J" for e in ev) == sum(e[0] == "K" for e in ev)
+    # rebased ends that moved: the rebase does more than re-send
+    moved = 0
+    for s in sets:
+        for cl in s["events"]:
+            q = [e[1] for e in cl if e[0] == "J"]
+            k = [s["log"][e[1]][5] for e in cl if e[0] == "K"]
+            ends = lambda v: (v.get("start"), v.get("end"))  # noqa: E731
+            moved += sum(1 for a, b in zip(q, k) if a["opName"] != "delete" and "value" in b and
+                         ends(a["value"]) != ends(b["value"]))
+    assert moved > 100
+
+
+@pytest.mark.gpu
+def test_node_interval_reconnect_on_gpu():
+    """Interval collections across reconnection (rebaseLocalInterval,
+    intervalCollection.ts:1735-1803, through MTE_OP_REF b = 4 / 5 on the HBM
+    tree pass): every op a client re-sends equals the reference's -- rebased
+    adds and changes exactly, regenerated merge-tree ops as test_reconnect
+    compares them -- and at every checkpoint the text, intervals, events, order,
+    summary and queries equal the reference client's."""
+    from fixtures_util import canon_regen
+    j = json.loads(node("tests/node/interval_farm.js", "reconnect").strip().splitlines()[-1])
+    assert j["nFailures"] == 0, (j["extFail"], j["extFirst"], j["failures"][:2])
+    sets = [s for s in reconnect_sets()["sets"] if s["leafViews"]["differ"] == 0]
+    assert j["passed"] == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
+    bad = [x for x in j["regens"] if canon_regen(x[0], x[2], False) != canon_regen(x[1], x[2], False)]
+    assert not bad, bad[:2]
+    assert len(j["regens"]) > 800
+    assert j["prevNext"]["equal"] >= 0.8 * j["prevNext"]["n"], j["prevNext"]
