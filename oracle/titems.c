@@ -755,10 +755,9 @@ static int doc_ref_rebase(idoc* d, const mte_op* op) {
     return delta_push(d, MTE_DELTA_REBASE, p, 0, 0);
   }
   const uint32_t slot = (uint32_t)op->pos2;
-  if (slot >= d->ref_hi || !(d->ref_state[slot] & REF_LIVE)) return MTE_E_INVALID_ARG;
   int64_t p = -1;
-  uint32_t st = d->ref_state[slot];
-  if (!(st & REF_DETACHED)) {
+  const uint32_t st = slot < d->ref_hi ? d->ref_state[slot] : 0u;
+  if ((st & REF_LIVE) && !(st & REF_DETACHED)) { /* a slot not in use answers -1 */
     for (uint32_t i = 0; i < d->n; i++) {
       const item* g = &d->it[i];
       if (g->empty || d->ref_anchor[slot] - g->toff >= (uint32_t)g->len) continue;
