@@ -174,6 +174,7 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
     st[kHsLseq] = 0u;
     st[kHsRhi] = 0u;
     st[kHsEntered] = (in.flags & MTE_DOC_LOCAL_CLIENT) ? 1u : 0u;
+    st[kHsWin] = 0u;  // no cached local partials
   }
   if (in.flags & MTE_DOC_LOCAL_CLIENT) {  // nothing pending (mte_htree.h planes)
     const uint32_t nz = n_img ? n_img : 1u;

@@ -43,7 +43,7 @@ constexpr uint32_t kHdrTreeHbm = kHdrTreeHbmFlag;  // a legacy document continue
 constexpr int kHtState = 8;            // state words per document
 
 // state words (HtreeArgs::st)
-enum HtSt { kHsDepth = 0, kHsNextId, kHsHeapN, kHsLseq, kHsRhi, kHsEntered };
+enum HtSt { kHsDepth = 0, kHsNextId, kHsHeapN, kHsLseq, kHsRhi, kHsEntered, kHsWin };
 
 // MTE_HTREE_PROF (a profiling build only, `make prof`): per-phase clocks
 // (s_memrealtime ticks, 100 MHz) summed over every document into
@@ -105,6 +105,8 @@ struct HT {
   const uint16_t* arena;
   // MTE_OP_RELPOS: positions for the next record (rpf: MTE_RP_POS1 / POS2 given)
   uint32_t rpf;
+  // the window of the reference's cached local partial lengths (ht_view_window), -1: none
+  int32_t wcache;
   int32_t rp1, rp2;
   // LDS residency: the document's planes, tree words, L / P and heap in the
   // workgroup's LDS while they fit (every access goes through the pointers
@@ -1325,68 +1327,6 @@ __device__ __forceinline__ int ht_rollback_annotate(HT& h, uint32_t b, const uin
   return 0;
 }
 
-// MTE_OP_REGEN (titems.c doc_regen): the group's segments in document order at
-// their positions in the view at localSeq ls, a merged leaf one record
-template <int K>
-__device__ __forceinline__ void ht_regen(const HT& h, int32_t ls, uint32_t t, uint32_t slot, EvOut& ev) {
-  const int l = lane_id();
-  int32_t cy = 0;
-  bool prev_hit = false;  // the tile's last item was a record's item (a continuation joins it)
-  for (int tb = 0; tb < h.n; tb += kHT) {
-#pragma unroll
-    for (int j = 0; j < kHE; j++) {
-      const int i = tb + j * kWave + l;
-      const bool v = i < h.n;
-      const int ic = v ? i : 0;
-      const uint32_t tt = ld_l2(h.tw + ic);
-      const int32_t len = (int32_t)ld_l2(h.pl + ic), sq = (int32_t)ld_l2(h.pl + h.sd + ic);
-      const int32_t rs = (int32_t)ld_l2(h.pl + 2 * h.sd + ic);
-      const int32_t lr = (int32_t)ld_l2(h.pl + (uint64_t)kLrsPlane<K> * h.sd + ic);
-      const uint32_t am = ld_l2(h.pl + (uint64_t)kAnnPlane<K> * h.sd + ic);
-      const uint32_t tf = ld_l2(h.pl + 5 * h.sd + ic);
-      const bool rp = rs >= kLocalBase && rs != kNone;  // a pending local removal
-      bool hit = false;
-      if (v && !(tt & kTEmpty)) {
-        if (t == MTE_OP_INSERT) hit = sq == kLocalBase + ls;
-        else if (t == MTE_OP_REMOVE) hit = rs == kLocalBase + ls;
-        else hit = ((am >> slot) & 1u) && (rs == kNone || rp);
-        // a member that re-sends nothing leaves the group (resetPendingDeltaToOps
-        // enqueues only the segments with a new op, client.ts:803-852): the
-        // zamboni stops holding it for the group (titems.c doc_regen)
-        if (!hit && t == MTE_OP_REMOVE && lr == ls) h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = (uint32_t)ls | kLrsReleased;
-        if (!hit && t == MTE_OP_ANNOTATE && ((am >> slot) & 1u))
-          h.pl[(uint64_t)kAnnPlane<K> * h.sd + i] = am & ~(1u << slot);
-      }
-      // localNetLength with localSeq (mergeTree.ts:575-593)
-      int32_t ll = (v && !(tt & kTEmpty)) ? len : 0;
-      if (sq >= kLocalBase && sq - kLocalBase > ls) ll = 0;
-      if (lr != 0 && (lr & ~(int32_t)kLrsReleased) <= ls) ll = 0;
-      if (rs != kNone && (!rp || rs - kLocalBase <= ls)) ll = 0;
-      const int32_t incl = wave_incl_scan(ll);
-      // hit(i - 1): the lane before, or the previous row's / tile's last item
-      const uint64_t hm = __ballot(hit);
-      const bool hprev = l > 0 ? ((hm >> (l - 1)) & 1ull) != 0 : prev_hit;
-      const bool ext = hit && (tt & kTCont) && hprev;
-      const bool st0 = hit && !ext;
-      const int32_t sincl = wave_incl_scan(st0 ? 1 : 0);
-      const uint32_t base = ev.n;
-      if (st0) {
-        const uint32_t idx = base + (uint32_t)(sincl - 1);
-        if (idx < ev.cap) ev.p[idx] = mte_delta{ev.op, MTE_DELTA_REGEN | t, cy + incl - ll, len, t == MTE_OP_INSERT ? tf : 0u};
-      }
-      vm_drain();
-      if (ext) {
-        const uint32_t idx = base + (uint32_t)sincl - 1u;
-        if (idx < ev.cap) atomicAdd((int*)&ev.p[idx].len, len);
-      }
-      ev.n += (uint32_t)rdlane(sincl, kWave - 1);
-      cy += rdlane(incl, kWave - 1);
-      prev_hit = ((hm >> 63) & 1ull) != 0;
-    }
-  }
-  vm_drain();
-}
-
 // ---- LDS residency -------------------------------------------------------------------------
 // A document's state is moved whole: rows [0, n) of its nP planes and tree
 // words, and heap entries 1 .. hn.  L / P are scratch (recomputed lazily).
@@ -1519,43 +1459,174 @@ __device__ __forceinline__ int32_t ht_view_len(const HT& h, int i, int32_t rs0, 
   return (rs != kNone && rs <= rs0) ? 0 : len;
 }
 
-// the view's length of items [0, g)
+// The reference takes a block's length in these views from its local partial
+// lengths (titems.c item_partial / block_len, which cite the rules): per item
+// a sequenced part, a local part counted only when the block holds a local
+// record at or below localSeq, less the overlapping removes; W the window of
+// the cached partials (ht_view_window).
 template <int K>
-__device__ __forceinline__ int32_t ht_view_prefix(const HT& h, int g, int32_t rs0, int32_t ls) {
-  int32_t acc = 0;
-  for (int tb = 0; tb < g; tb += kHT) {
+__device__ __forceinline__ void ht_item_partial(const HT& h, int i, int32_t R, int32_t L, int32_t W, int32_t& a, int32_t& b,
+                                                int32_t& o, bool& fl) {
+  const uint32_t tt = ld_l2(h.tw + i);
+  const int32_t c = (int32_t)ld_l2(h.pl + i), sq = (int32_t)ld_l2(h.pl + h.sd + i);
+  const int32_t rs = (int32_t)ld_l2(h.pl + 2 * h.sd + i);
+  const uint32_t rm = ld_l2(h.pl + 3 * h.sd + i);
+  const int32_t lr = (int32_t)(ld_l2(h.pl + (uint64_t)kLrsPlane<K> * h.sd + i) & ~kLrsReleased);
+  if (tt & kTEmpty) return;
+  if (sq < kLocalBase) {
+    if (sq <= W || sq <= R) a += c;
+  } else if (sq - kLocalBase <= L) {
+    b += c;
+    fl = true;
+  }
+  if (rs == kNone) return;
+  if (rs >= kLocalBase) {
+    if (rs - kLocalBase <= L) {
+      b -= c;
+      fl = true;
+    }
+    return;
+  }
+  if (rs <= W) {
+    a -= c;
+    return;
+  }
+  if (rs <= R) a -= c;
+  if (__popc(rm) > 1 && lr != 0 && lr <= L) {
+    b -= c;
+    fl = true;
+    if (rs <= R) o -= c;
+  }
+}
+
+// the window of the reference's cached local partials: the first block length
+// a query evaluates since the last length update computes them, with that
+// query's refSeq (nodeLength :984-995 -> computeLocalPartials :964-982)
+__device__ __forceinline__ int32_t ht_view_window(HT& h, int32_t R) {
+  if (h.wcache < 0) h.wcache = h.min_seq < R ? h.min_seq : R;
+  return h.wcache;
+}
+
+template <int K>
+__device__ __forceinline__ int32_t ht_block_len(HT& h, int s, int e, int32_t R, int32_t L) {
+  const int32_t W = ht_view_window(h, R);
+  int32_t a = 0, b = 0, o = 0;
+  bool fl = false;
+  for (int tb = s; tb <= e; tb += kHT) {
 #pragma unroll
     for (int j = 0; j < kHE; j++) {
       const int i = tb + j * kWave + lane_id();
-      const int32_t v = ht_view_len<K>(h, i < g ? i : 0, rs0, ls);
-      acc += i < g ? v : 0;
+      if (i <= e) ht_item_partial<K>(h, i, R, L, W, a, b, o, fl);
+    }
+  }
+  a = rdlane(wave_incl_scan(a), kWave - 1);
+  b = rdlane(wave_incl_scan(b), kWave - 1);
+  o = rdlane(wave_incl_scan(o), kWave - 1);
+  return a + (__ballot(fl) ? b - o : 0);
+}
+
+// the leaf-rule length of items [s, e]
+template <int K>
+__device__ __forceinline__ int32_t ht_range_view(const HT& h, int s, int e, int32_t R, int32_t L) {
+  int32_t acc = 0;
+  for (int tb = s; tb <= e; tb += kHT) {
+#pragma unroll
+    for (int j = 0; j < kHE; j++) {
+      const int i = tb + j * kWave + lane_id();
+      const int32_t v = ht_view_len<K>(h, i <= e ? i : s, R, L);
+      acc += i <= e ? v : 0;
     }
   }
   return rdlane(wave_incl_scan(acc), kWave - 1);
 }
 
-// getContainingSegment(pos) in that view (mergeTree.ts:872-885): the first item
-// of positive length holding pos, and the offset there; -1 past the end
+// the last item of the child of a level-k block (ending at e) that starts at c
+__device__ __forceinline__ int ht_child_last(const HT& h, int c, int e, int k) {
+  if (k == 1) return ht_leaf_end(h, c) - 1;
+  const uint32_t* tw = h.tw;
+  const int j = ht_first(c + 1, e + 1, [&](int x) { return (int)t_h(ld_l2(tw + x)) >= k - 1; });
+  return j < 0 ? e : j - 1;
+}
+
 template <int K>
-__device__ __forceinline__ int ht_view_find(const HT& h, int32_t pos, int32_t rs0, int32_t ls, int32_t& off) {
-  const int l = lane_id();
-  int32_t carry = 0;
-  for (int tb = 0; tb < h.n; tb += kHT) {
-#pragma unroll
-    for (int j = 0; j < kHE; j++) {
-      const int i = tb + j * kWave + l;
-      const int32_t v = i < h.n ? ht_view_len<K>(h, i < h.n ? i : 0, rs0, ls) : 0;
-      const int32_t incl = wave_incl_scan(v), st0 = carry + incl - v;
-      const uint64_t m = __ballot(v > 0 && pos >= st0 && pos < st0 + v);
-      if (m) {
-        const int x = __ffsll((long long)m) - 1;
-        off = pos - rdlane(st0, x);
-        return tb + j * kWave + x;
-      }
-      carry += rdlane(incl, kWave - 1);
+__device__ __forceinline__ int32_t ht_child_len(HT& h, int c, int ce, int k, int32_t R, int32_t L) {
+  return k > 1 ? ht_block_len<K>(h, c, ce, R, L) : ht_range_view<K>(h, c, ce, R, L);
+}
+
+
+// getPosition of the leaf starting at item x (mergeTree.ts:853-870): the
+// lengths of the children before it at every level
+template <int K>
+__device__ __forceinline__ int32_t ht_view_prefix(HT& h, int x, int32_t R, int32_t L) {
+  const int s1 = ht_span_start(h, x, 1);
+  int32_t pos = s1 < x ? ht_range_view<K>(h, s1, x - 1, R, L) : 0;
+  for (int k = 2; k <= h.depth; k++) {
+    const int s = ht_span_start(h, x, k), cx = ht_span_start(h, x, k - 1), e = ht_span_end(h, s, k);
+    for (int c = s; c < cx;) {
+      const int ce = ht_child_last(h, c, e, k);
+      pos += ht_block_len<K>(h, c, ce, R, L);
+      c = ce + 1;
     }
   }
-  return -1;
+  return pos;
+}
+
+// getContainingSegment(pos) in the view (mergeTree.ts:872-885 -> nodeMap
+// :2274-2330, depth first from the root's children): a zero length skips a
+// child, a negative one moves the running position back.  The item holding pos
+// and the offset there; -1 past the end.
+template <int K>
+__device__ __forceinline__ int ht_view_find(HT& h, int32_t pos, int32_t R, int32_t L, int32_t& off) {
+  int k = h.depth, e = h.n - 1, c = 0, found = -1;
+  int32_t p = 0;
+  while (h.n > 0) {
+    if (c > e) {  // this block's children are done: its parent goes on after it
+      if (k >= h.depth) break;
+      k++;
+      e = ht_span_end(h, ht_span_start(h, c - 1, k), k);
+      continue;
+    }
+    if (!is_child_t(uni(ld_l2(h.tw + c)), k)) {  // a continuation or a placeholder
+      c++;
+      continue;
+    }
+    if (pos + 1 <= p) break;
+    const int ce = ht_child_last(h, c, e, k);
+    const int32_t len = ht_child_len<K>(h, c, ce, k, R, L);
+    if (len != 0) {
+      if (pos >= p + len) {
+        p += len;
+      } else if (k == 1) {
+        found = c;
+        off = pos - p;
+        break;
+      } else {
+        k--;
+        e = ce;
+        continue;
+      }
+    }
+    c = ce + 1;
+  }
+  if (found < 0) return -1;
+  // the offset within the leaf -> the item of the leaf holding it
+  const int le = ht_leaf_end(h, found);
+  while (found + 1 < le && off >= (int32_t)uni(ld_l2(h.pl + found))) {
+    off -= (int32_t)uni(ld_l2(h.pl + found));
+    found++;
+  }
+  return found;
+}
+
+// the item a leaf starts at; the units of its leaf before item i
+__device__ __forceinline__ int ht_leaf_start(const HT& h, int i) {
+  const uint32_t* tw = h.tw;
+  const int s = ht_last(0, i + 1, [&](int x) { return (ld_l2(tw + x) & kTCont) == 0; });
+  return s < 0 ? 0 : s;
+}
+__device__ __forceinline__ int32_t ht_leaf_offset(const HT& h, int i) {
+  const int s = ht_leaf_start(h, i);
+  return s < i ? ht_sum_len(h, s, i) : 0;
 }
 
 __device__ __forceinline__ bool ht_removed_acked(const HT& h, int i) {
@@ -1591,6 +1662,85 @@ __device__ __forceinline__ bool ht_slide_item(const HT& h, int x, int& t, int32_
 // item removed and acked, moves to what createPositionReference finds, in the
 // view at (currentSeq, a), at its slide target's position there; the event's
 // position is that position, -1 when it stays.
+// MTE_OP_REGEN (titems.c doc_regen): the group's segments in document order at
+// their positions in the view at localSeq ls, a merged leaf one record
+template <int K>
+__device__ __forceinline__ void ht_regen(HT& h, int32_t ls, uint32_t t, uint32_t slot, EvOut& ev) {
+  const int l = lane_id();
+  bool prev_hit = false;  // the tile's last item was a record's item (a continuation joins it)
+  for (int tb = 0; tb < h.n; tb += kHT) {
+#pragma unroll
+    for (int j = 0; j < kHE; j++) {
+      const int i = tb + j * kWave + l;
+      const bool v = i < h.n;
+      const int ic = v ? i : 0;
+      const uint32_t tt = ld_l2(h.tw + ic);
+      const int32_t len = (int32_t)ld_l2(h.pl + ic), sq = (int32_t)ld_l2(h.pl + h.sd + ic);
+      const int32_t rs = (int32_t)ld_l2(h.pl + 2 * h.sd + ic);
+      const int32_t lr = (int32_t)ld_l2(h.pl + (uint64_t)kLrsPlane<K> * h.sd + ic);
+      const uint32_t am = ld_l2(h.pl + (uint64_t)kAnnPlane<K> * h.sd + ic);
+      const uint32_t tf = ld_l2(h.pl + 5 * h.sd + ic);
+      const bool rp = rs >= kLocalBase && rs != kNone;  // a pending local removal
+      bool hit = false;
+      if (v && !(tt & kTEmpty)) {
+        if (t == MTE_OP_INSERT) hit = sq == kLocalBase + ls;
+        else if (t == MTE_OP_REMOVE) hit = rs == kLocalBase + ls;
+        else hit = ((am >> slot) & 1u) && (rs == kNone || rp);
+        // a member that re-sends nothing leaves the group (resetPendingDeltaToOps
+        // enqueues only the segments with a new op, client.ts:803-852): the
+        // zamboni stops holding it for the group; it keeps its localRemovedSeq
+        // (titems.c doc_regen)
+        if (!hit && t == MTE_OP_REMOVE && lr == ls)
+          h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = (uint32_t)ls | kLrsReleased;
+        if (!hit && t == MTE_OP_ANNOTATE && ((am >> slot) & 1u))
+          h.pl[(uint64_t)kAnnPlane<K> * h.sd + i] = am & ~(1u << slot);
+      }
+      // a member that leaves has its position taken all the same
+      // (resetPendingDeltaToOps :806, before the op is chosen), which may compute
+      // the cached local partials (titems.c doc_regen)
+      const bool gone = v && !(tt & kTEmpty) && !hit && !(tt & kTCont) &&
+                        ((t == MTE_OP_REMOVE && lr == ls) || (t == MTE_OP_ANNOTATE && ((am >> slot) & 1u)));
+      uint64_t gm = h.wcache < 0 ? __ballot(gone) : 0ull;
+      while (gm && h.wcache < 0) {
+        const int ln = __ffsll((long long)gm) - 1;
+        gm &= gm - 1;
+        (void)ht_view_prefix<K>(h, tb + j * kWave + ln, h.cur_seq, ls);
+      }
+      // hit(i - 1): the lane before, or the previous row's / tile's last item
+      const uint64_t hm = __ballot(hit);
+      const bool hprev = l > 0 ? ((hm >> (l - 1)) & 1ull) != 0 : prev_hit;
+      const bool ext = hit && (tt & kTCont) && hprev;
+      const bool st0 = hit && !ext;
+      const int32_t sincl = wave_incl_scan(st0 ? 1 : 0);
+      const uint32_t base = ev.n;
+      if (st0) {
+        const uint32_t idx = base + (uint32_t)(sincl - 1);
+        if (idx < ev.cap) ev.p[idx] = mte_delta{ev.op, MTE_DELTA_REGEN | t, 0, len, t == MTE_OP_INSERT ? tf : 0u};
+      }
+      vm_drain();
+      if (ext) {
+        const uint32_t idx = base + (uint32_t)sincl - 1u;
+        if (idx < ev.cap) atomicAdd((int*)&ev.p[idx].len, len);
+      }
+      // positions: findReconnectionPosition (client.ts:709-713), getPosition with
+      // the localSeq, block lengths from the local partials (ht_view_prefix)
+      uint64_t sm = __ballot(st0);
+      while (sm) {
+        const int ln = __ffsll((long long)sm) - 1;
+        sm &= sm - 1;
+        const int x = tb + j * kWave + ln;
+        const int32_t pos = ht_view_prefix<K>(h, ht_leaf_start(h, x), h.cur_seq, ls) + ht_leaf_offset(h, x);
+        const uint32_t idx = base + (uint32_t)rdlane(sincl, ln) - 1u;
+        if (l == 0 && idx < ev.cap) ev.p[idx].pos = pos;
+      }
+      vm_drain();
+      ev.n += (uint32_t)rdlane(sincl, kWave - 1);
+      prev_hit = ((hm >> 63) & 1ull) != 0;
+    }
+  }
+  vm_drain();
+}
+
 template <int K>
 __device__ __forceinline__ int ht_ref_rebase(HT& h, const s8v& op, int32_t lseq, uint2* rt, EvOut& ev) {
   const uint32_t b = (uint32_t)op[7];
@@ -1608,7 +1758,7 @@ __device__ __forceinline__ int ht_ref_rebase(HT& h, const s8v& op, int32_t lseq,
       int t = x;
       bool ok = true;
       if (ht_removed_acked(h, x)) ok = ht_slide_item(h, x, t, off);
-      if (ok) p = ht_view_prefix<K>(h, t, h.cur_seq, ls) + off;
+      if (ok) p = ht_view_prefix<K>(h, ht_leaf_start(h, t), h.cur_seq, ls) + ht_leaf_offset(h, t) + off;
     }
     ev_one(ev, MTE_DELTA_REBASE, p, 0);
     return 0;
@@ -1628,7 +1778,7 @@ __device__ __forceinline__ int ht_ref_rebase(HT& h, const s8v& op, int32_t lseq,
     if (x >= 0 && ht_removed_acked(h, x)) {
       uint32_t to = 0, st2 = stt;
       if (ht_slide_item(h, x, t, off)) {
-        p = ht_view_prefix<K>(h, t, h.cur_seq, ls) + off;
+        p = ht_view_prefix<K>(h, ht_leaf_start(h, t), h.cur_seq, ls) + ht_leaf_offset(h, t) + off;
         int32_t o2 = 0;
         const int y = ht_view_find<K>(h, p, h.cur_seq, ls, o2);
         if (y >= 0) to = uni(ld_l2(h.pl + 5 * h.sd + y)) + (uint32_t)o2;
@@ -1638,6 +1788,7 @@ __device__ __forceinline__ int ht_ref_rebase(HT& h, const s8v& op, int32_t lseq,
       }
       if (lane_id() == 0) rt[slot] = make_uint2(to, st2);
       vm_drain();
+      h.wcache = -1;  // createLocalReferencePosition updates lengths (mergeTree.ts:2124-2143)
     }
   }
   ev_one(ev, MTE_DELTA_REBASE, p, 0);
@@ -1697,6 +1848,10 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
     D.k++;
     return 0;
   }
+  // a length update drops the reference's cached local partials
+  // (mergeTree.ts:2105-2110, 2188-2191; ht_view_window): every record but a
+  // regeneration; references below
+  if (type != MTE_OP_REF && type != MTE_OP_REGEN) h.wcache = -1;
   if (type == MTE_OP_REF) {
     if (!lop || !ldoc || !refd) return MTE_E_UNSUPPORTED;
     if ((uint32_t)op[5] >= a.ref_cap || (uint32_t)op[7] > 5u) return MTE_E_INVALID_ARG;
@@ -1705,8 +1860,20 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
     MTE_STAT(st[kStOps]++;)
     MTE_STAT(if ((uint32_t)op[7] != 1u) st[kStScanned] += (uint32_t)h.n;)
     HPROF_BEGIN(t0)
-    if ((uint32_t)op[7] >= 4u) rc = ht_ref_rebase<K>(h, op, lseq, rt, ev);
-    else rc = stream_ref<K>(h.pl, h.sd, h.n, rt, rhi, op, D.min_seq, h.newcalc);
+    if ((uint32_t)op[7] >= 4u) {
+      rc = ht_ref_rebase<K>(h, op, lseq, rt, ev);
+    } else {
+      // createLocalReferencePosition updates lengths (mergeTree.ts:2124-2143): a
+      // reference made on a segment (b = 0 / 2), or one ackInterval re-makes (b = 3)
+      const uint32_t slot = (uint32_t)op[5];
+      const uint2 before = make_uint2(uni(ld_l2(&rt[slot].x)), uni(ld_l2(&rt[slot].y)));
+      rc = stream_ref<K>(h.pl, h.sd, h.n, rt, rhi, op, D.min_seq, h.newcalc);
+      const uint2 after = make_uint2(uni(ld_l2(&rt[slot].x)), uni(ld_l2(&rt[slot].y)));
+      const uint32_t b = (uint32_t)op[7];
+      if ((b == 0u || b == 2u) ? !(after.y & kRefDetached)
+                               : (b == 3u && (after.x != before.x || ((after.y ^ before.y) & kRefDetached))))
+        h.wcache = -1;
+    }
     HPROF_END(h, 5, t0)
     if (rc) return rc;
     D.k++;
@@ -1869,6 +2036,7 @@ __global__ __launch_bounds__(64) void htree_kernel(ReplayArgs a, HtreeArgs t) {
   }
   int32_t lseq = (int32_t)uld(stp + kHsLseq);
   uint32_t rhi = uld(stp + kHsRhi);
+  h.wcache = (int32_t)uld(stp + kHsWin) - 1;
   uint32_t st[kNumStats] = {};
   EvOut ev{nullptr, 0, 0u, 0u};
   if ((hf & MTE_DOC_EVENTS) && a.dl_off) {
@@ -1909,6 +2077,7 @@ __global__ __launch_bounds__(64) void htree_kernel(ReplayArgs a, HtreeArgs t) {
   lane0_st(stp + kHsHeapN, h.hn);
   lane0_st(stp + kHsLseq, (uint32_t)lseq);
   lane0_st(stp + kHsRhi, rhi);
+  lane0_st(stp + kHsWin, (uint32_t)(h.wcache + 1));
   if ((hf & MTE_DOC_EVENTS) && a.dl_n && lane_id() == 0) a.dl_n[doc] = ev.n;
   vm_drain();
   run_finish(D, a);

@@ -101,9 +101,11 @@ extern "C" {
  * a pending op and pos1 = its type.  The text does not change; it reports,
  * as MTE_DELTA_REGEN | type delta records, one per segment of L's segment group
  * in document order, the op that re-sends that segment: its position in the
- * view at localSeq L (findReconnectionPosition :709-713 -> localNetLength with
- * localSeq, mergeTree.ts:575-593: acked text plus own pending inserts up to L,
- * minus acked removals and own pending removals up to L) and its cachedLength.
+ * view at localSeq L (findReconnectionPosition :709-713 -> getPosition with
+ * localSeq: leaves by localNetLength, mergeTree.ts:575-593 -- acked text plus
+ * own pending inserts up to L, minus acked removals and own pending removals
+ * up to L -- blocks by the reference's local partial lengths, see MTE_OP_REF
+ * b = 4) and its cachedLength.
  *   insert: every segment L inserted (`removed` holds its text offset, whose
  *     difference from the lowest of the group is the segment's offset in the
  *     op's text);
@@ -164,7 +166,10 @@ extern "C" {
  *     (createPositionReference with localSeq :639-658), detached if nothing;
  *     one MTE_DELTA_REBASE event, pos = that position, -1 if it did not move.
  *   b = 4 / 5 only in MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS documents (the
- *   HBM tree pass).
+ *   HBM tree pass).  These views -- and MTE_OP_REGEN's positions -- are the
+ *   reference's: block lengths from its local partial lengths (partialLengths.ts:
+ *   667-700), cached as computeLocalPartials caches them (mergeTree.ts:964-982;
+ *   DESIGN.md §4 "Reconnection").
  * The engine slides references as the reference does
  * (slideAckedRemovedSegmentReferences, mergeTree.ts:893-950): when a segment
  * becomes removed and acked -- a remote remove newly removing it or

@@ -91,8 +91,10 @@ typedef struct {
   /* the GPU tree pass's statistics (mte_stats), counted the same way */
   uint64_t ops, scanned, written, pwrites, units, max_segs;
   mte_doc_init init;
-  /* MTE_DOC_LOCAL_CLIENT: the last localSeq */
+  /* MTE_DOC_LOCAL_CLIENT: the last localSeq; the window the reference's
+   * cached local partial lengths were computed with (block_views), -1: none */
   int32_t local_seq;
+  int64_t wcache;
   /* MTE_DOC_REFS: reference slots (as oracle.c) */
   uint32_t *ref_anchor, *ref_state;
   uint32_t ref_cap, ref_hi;
@@ -691,25 +693,155 @@ static inline int32_t view_len(const item* g, int32_t rs0, int32_t ls) {
   return (g->rseq != NONE_SEQ && g->rseq <= rs0) ? 0 : g->len;
 }
 
-static int64_t view_prefix(const idoc* d, uint32_t g, int32_t rs0, int32_t ls) {
-  int64_t p = 0;
-  for (uint32_t i = 0; i < g; i++) p += view_len(&d->it[i], rs0, ls);
-  return p;
+/* ---- the reference's localSeq views at block level -----------------------------
+ * getContainingSegment / getPosition with a localSeq (mergeTree.ts:853-885, 2274-2330)
+ * take a block's length from its local partial lengths (nodeLength :984-995 ->
+ * PartialSequenceLengths.getPartialLength, partialLengths.ts:667-700): minLength
+ * plus the sequenced records up to refSeq, and -- when the block holds a local
+ * record at or below localSeq -- the local records up to localSeq less the
+ * overlapping removes (a remote remove that overtook a local one).  Summed per
+ * item (fromLeaves / insertSegment :330-505), which can disagree with the leaf
+ * rule view_len: a local removal of a segment inserted after refSeq is
+ * subtracted while its insertion is not counted (a block can come out
+ * negative).  The partials are computed by the first such query after a length
+ * update, with the window's minSeq lowered to that query's refSeq
+ * (computeLocalPartials :964-982): W, kept in idoc.wcache. */
+typedef struct {
+  int64_t a, b, o;
+  int flag;
+} pl_acc;
+
+static void item_partial(const item* g, int32_t R, int32_t L, int64_t W, pl_acc* x) {
+  if (g->empty) return;
+  const int64_t c = g->len;
+  if (!is_pending(g->seq)) {
+    if (g->seq <= W || g->seq <= R) x->a += c;
+  } else if (g->seq - LOCAL_BASE <= L) {
+    x->b += c;
+    x->flag = 1;
+  }
+  if (g->rseq == NONE_SEQ) return;
+  if (is_pending(g->rseq)) {
+    if (g->rseq - LOCAL_BASE <= L) {
+      x->b -= c;
+      x->flag = 1;
+    }
+    return;
+  }
+  if (g->rseq <= W) {
+    x->a -= c;
+    return;
+  }
+  if (g->rseq <= R) x->a -= c;
+  const int32_t lrs = g->lrs & ~LRS_RELEASED;
+  if (__builtin_popcount(g->rmask) > 1 && lrs != 0 && lrs <= L) { /* an overlapping remove */
+    x->b -= c;
+    x->flag = 1;
+    if (g->rseq <= R) x->o -= c;
+  }
 }
 
-/* getContainingSegment(pos) in that view (mergeTree.ts:872-885): the first item
- * of positive length holding pos; -1 past the end */
-static int64_t view_find(const idoc* d, int64_t pos, int32_t rs0, int32_t ls, int32_t* off) {
-  int64_t p = 0;
-  for (uint32_t i = 0; i < d->n; i++) {
-    const int32_t l = view_len(&d->it[i], rs0, ls);
-    if (l > 0 && pos >= p && pos < p + l) {
-      *off = (int32_t)(pos - p);
-      return i;
+/* the window of the cached local partials: the first block length a query
+ * evaluates computes them, with that query's refSeq (nodeLength :984-995) */
+static int64_t view_window(idoc* d, int32_t R) {
+  if (d->wcache < 0) d->wcache = d->min_seq < R ? d->min_seq : R;
+  return d->wcache;
+}
+
+static int64_t block_len(idoc* d, uint32_t s, uint32_t e, int32_t R, int32_t L) {
+  const int64_t W = view_window(d, R);
+  pl_acc x = {0, 0, 0, 0};
+  for (uint32_t i = s; i <= e; i++) item_partial(&d->it[i], R, L, W, &x);
+  return x.a + (x.flag ? x.b - x.o : 0);
+}
+
+/* the last item of the child of the level-k block [.., e] that starts at c */
+static uint32_t child_last(const idoc* d, uint32_t c, uint32_t e, int k) {
+  if (k == 1) return leaf_end(d, c) - 1;
+  uint32_t j = c + 1;
+  while (j <= e && d->it[j].h < k - 1) j++;
+  return j - 1;
+}
+
+/* a child's length in the view: a leaf by the leaf rule, a block by its partials */
+static int64_t child_len(idoc* d, uint32_t c, uint32_t ce, int k, int32_t R, int32_t L) {
+  if (k > 1) return block_len(d, c, ce, R, L);
+  int64_t v = 0;
+  for (uint32_t i = c; i <= ce; i++) v += view_len(&d->it[i], R, L);
+  return v;
+}
+
+/* nodeMap from the root's children (depthFirstNodeWalk): a zero length skips,
+ * a negative one moves the running position back */
+static int walk_find(idoc* d, uint32_t s, uint32_t e, int k, int64_t pos, int32_t R, int32_t L, int64_t* p,
+                     int64_t* leaf, int64_t* off) {
+  for (uint32_t c = s; c <= e; c++) {
+    if (!is_child(&d->it[c], k)) continue;
+    if (pos + 1 <= *p) return 1;
+    const uint32_t ce = child_last(d, c, e, k);
+    const int64_t len = child_len(d, c, ce, k, R, L);
+    if (len != 0) {
+      if (pos >= *p + len) {
+        *p += len;
+      } else if (k == 1) {
+        *leaf = c;
+        *off = pos - *p;
+        return 1;
+      } else if (walk_find(d, c, ce, k - 1, pos, R, L, p, leaf, off)) {
+        return 1;
+      }
     }
-    p += l;
+    c = ce;
   }
-  return -1;
+  return 0;
+}
+
+/* getContainingSegment(pos) in the view at (R, L) (mergeTree.ts:872-885): the
+ * item holding pos and the offset there; -1 past the end */
+static int64_t view_find(idoc* d, int64_t pos, int32_t R, int32_t L, int32_t* off) {
+  if (!d->n) return -1;
+  int64_t p = 0, leaf = -1, o = 0;
+  walk_find(d, 0, d->n - 1, d->depth, pos, R, L, &p, &leaf, &o);
+  if (leaf < 0) return -1;
+  /* the offset within the leaf -> the item of the leaf holding it */
+  uint32_t i = (uint32_t)leaf;
+  const uint32_t le = leaf_end(d, i);
+  while (i + 1 < le && o >= d->it[i].len) {
+    o -= d->it[i].len;
+    i++;
+  }
+  *off = (int32_t)o;
+  return i;
+}
+
+/* getPosition of the leaf starting at item x (mergeTree.ts:853-870): the
+ * lengths of the children before it at every level */
+static int64_t view_prefix(idoc* d, uint32_t x, int32_t R, int32_t L) {
+  int64_t pos = 0;
+  for (int k = 1; k <= d->depth; k++) {
+    const uint32_t s = span_start(d, x, k), e = span_end(d, s, k);
+    const uint32_t cx = k == 1 ? x : span_start(d, x, k - 1);
+    for (uint32_t c = s; c < cx; c++) {
+      if (!is_child(&d->it[c], k)) continue;
+      const uint32_t ce = child_last(d, c, e, k);
+      pos += child_len(d, c, ce, k, R, L);
+      c = ce;
+    }
+  }
+  return pos;
+}
+
+
+/* the item a leaf starts at */
+static uint32_t leaf_start(const idoc* d, uint32_t i) {
+  while (i > 0 && d->it[i].cont) i--;
+  return i;
+}
+/* the units of its leaf before item i */
+static int32_t leaf_offset(const idoc* d, uint32_t i) {
+  int32_t o = 0;
+  for (uint32_t j = leaf_start(d, i); j < i; j++) o += d->it[j].len;
+  return o;
 }
 
 /* Client.getSlideToSegment (client.ts:1117-1130) from item x, removed and
@@ -750,7 +882,7 @@ static int doc_ref_rebase(idoc* d, const mte_op* op) {
     if (x >= 0) {
       int64_t t = x;
       if (removed_and_acked(&d->it[x])) t = slide_item(d, (uint32_t)x, &off);
-      if (t >= 0) p = view_prefix(d, (uint32_t)t, d->cur_seq, ls) + off;
+      if (t >= 0) p = view_prefix(d, leaf_start(d, (uint32_t)t), d->cur_seq, ls) + leaf_offset(d, (uint32_t)t) + off;
     }
     return delta_push(d, MTE_DELTA_REBASE, p, 0, 0);
   }
@@ -766,7 +898,7 @@ static int doc_ref_rebase(idoc* d, const mte_op* op) {
         const int64_t t = slide_item(d, i, &off);
         int64_t y = -1;
         if (t >= 0) {
-          p = view_prefix(d, (uint32_t)t, d->cur_seq, ls) + off;
+          p = view_prefix(d, leaf_start(d, (uint32_t)t), d->cur_seq, ls) + leaf_offset(d, (uint32_t)t) + off;
           y = view_find(d, p, d->cur_seq, ls, &o2);
         }
         if (y >= 0) d->ref_anchor[slot] = d->it[y].toff + (uint32_t)o2;
@@ -774,6 +906,7 @@ static int doc_ref_rebase(idoc* d, const mte_op* op) {
           d->ref_anchor[slot] = 0;
           d->ref_state[slot] = st | REF_DETACHED;
         }
+        d->wcache = -1; /* createLocalReferencePosition updates lengths (mergeTree.ts:2124-2143) */
       }
       break;
     }
@@ -814,6 +947,7 @@ static int doc_ref(idoc* d, const mte_op* op) {
         uint32_t to = 0;
         if (slide_to(d, i, &to) >= 0) d->ref_anchor[slot] = to;
         else d->ref_state[slot] = st | REF_DETACHED;
+        d->wcache = -1; /* ackInterval re-creates the end (createLocalReferencePosition) */
       }
       break;
     }
@@ -830,6 +964,7 @@ static int doc_ref(idoc* d, const mte_op* op) {
       uint32_t anchor = d->it[i].toff + (uint32_t)(op->pos1 - p);
       uint32_t st = REF_LIVE | (op->a & 0xffffu);
       if (remote && removed_and_acked(&d->it[i]) && slide_to(d, i, &anchor) < 0) st |= REF_DETACHED;
+      else d->wcache = -1; /* createLocalReferencePosition (mergeTree.ts:2124-2143) */
       d->ref_anchor[slot] = anchor;
       d->ref_state[slot] = st;
       return MTE_OK;
@@ -1064,6 +1199,9 @@ static int doc_regen(idoc* d, const mte_op* op);
 static int doc_apply_local(idoc* d, const mte_op* op, const env_t* env) {
   const int32_t ls = op->seq;
   int rc;
+  /* a length update drops the cached local partials (mergeTree.ts:2105-2110,
+   * 2188-2191): every local op; references: doc_ref */
+  if (op->type != MTE_OP_REGEN && op->type != MTE_OP_REF) d->wcache = -1;
   if (op->type == MTE_OP_ROLLBACK) return doc_rollback(d, op, env);
   if (op->type == MTE_OP_REGEN) return doc_regen(d, op);
   if (op->type == MTE_OP_REF) return doc_ref(d, op);
@@ -1190,15 +1328,6 @@ static int doc_rollback(idoc* d, const mte_op* op, const env_t* env) {
   return MTE_OK;
 }
 
-/* the length of an item in the local view at localSeq ls (localNetLength with
- * localSeq, mergeTree.ts:575-593) */
-static inline int32_t len_at_local_seq(const item* g, int32_t ls) {
-  if (g->empty) return 0;
-  if (is_pending(g->seq) && g->seq - LOCAL_BASE > ls) return 0;
-  if (g->lrs && (g->lrs & ~LRS_RELEASED) <= ls) return 0;
-  if (g->rseq != NONE_SEQ && (!is_pending(g->rseq) || g->rseq - LOCAL_BASE <= ls)) return 0;
-  return g->len;
-}
 
 /* MTE_OP_REGEN (as oracle.c doc_regen): the group's segments in document order
  * at their positions in the view at that localSeq -- a merged leaf one record */
@@ -1212,7 +1341,6 @@ static int doc_regen(idoc* d, const mte_op* op) {
   if (!(d->flags & MTE_DOC_EVENTS)) return MTE_E_UNSUPPORTED;
   d->ops++;
   d->scanned += d->n;
-  int64_t p = 0;
   int64_t last = -2;
   for (uint32_t i = 0; i < d->n; i++) {
     item* g = &d->it[i];
@@ -1226,15 +1354,23 @@ static int doc_regen(idoc* d, const mte_op* op) {
      * client.ts:803-852): a removal a remote remove overtook, an annotated
      * segment removed since -- the zamboni no longer holds it for the group */
     if (!g->empty && !hit) {
+      const int member = (t == MTE_OP_REMOVE && g->lrs == ls) || (t == MTE_OP_ANNOTATE && ((g->am >> op->a) & 1u));
       if (t == MTE_OP_REMOVE && g->lrs == ls) g->lrs |= LRS_RELEASED;
       if (t == MTE_OP_ANNOTATE) g->am &= ~(1u << op->a);
+      /* its position is taken all the same (resetPendingDeltaToOps :806, before
+       * the op is chosen): that may compute the cached local partials */
+      if (member && !g->cont && d->wcache < 0) (void)view_prefix(d, i, d->cur_seq, ls);
     }
     if (hit) {
+      /* findReconnectionPosition (client.ts:709-713): getPosition with the
+       * localSeq, block lengths from the local partials (view_prefix) */
       if (g->cont && last == (int64_t)i - 1 && d->dl_n) d->dl[d->dl_n - 1].len += g->len;
-      else if ((rc = delta_push(d, MTE_DELTA_REGEN | t, p, g->len, t == MTE_OP_INSERT ? g->toff : 0u))) return rc;
+      else if ((rc = delta_push(d, MTE_DELTA_REGEN | t,
+                                view_prefix(d, leaf_start(d, i), d->cur_seq, ls) + leaf_offset(d, i), g->len,
+                                t == MTE_OP_INSERT ? g->toff : 0u)))
+        return rc;
       last = i;
     }
-    p += len_at_local_seq(g, ls);
   }
   return MTE_OK;
 }
@@ -1285,6 +1421,7 @@ static int doc_apply(idoc* d, const mte_op* op, const env_t* env) {
   if (d->n + 4 > env->limit) return MTE_E_CAPACITY;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
   if (op->flags & MTE_F_LOCAL) return local_doc ? doc_apply_local(d, op, env) : MTE_E_UNSUPPORTED;
+  d->wcache = -1; /* a sequenced message updates lengths */
   if (op->type == MTE_OP_ACK && !local_doc) return MTE_E_UNSUPPORTED;
   if (local_doc && op->type != MTE_OP_ACK && op->type != MTE_OP_NOOP && c == 0) return MTE_E_INVALID_ARG;
   d->ops++;
@@ -1414,6 +1551,7 @@ int oti_load_docs(oti_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     d->cur_seq = in->cur_seq;
     d->depth = 1;
     d->next_id = 1;
+    d->wcache = -1;
     if ((rc = reserve(d, 64))) return rc;
     d->n = 1;
     if (in->text_len > 0) {
