@@ -238,6 +238,22 @@ export class IntervalCollection implements Iterable<SequenceInterval> {
   /** A sequenced interval op (makeOpsMap): ackAdd / ackChange / ackDelete. */
   process(opName: "add" | "change" | "delete", value: any, local: boolean, op: ISequencedDocumentMessage): void;
   findOverlappingIntervals(startPosition: number, endPosition: number): SequenceInterval[];
+  previousInterval(pos: number): SequenceInterval | undefined;
+  nextInterval(pos: number): SequenceInterval | undefined;
+  CreateForwardIteratorWithStartPosition(startPosition: number): Iterator<SequenceInterval>;
+  CreateBackwardIteratorWithStartPosition(startPosition: number): Iterator<SequenceInterval>;
+  CreateForwardIteratorWithEndPosition(endPosition: number): Iterator<SequenceInterval>;
+  CreateBackwardIteratorWithEndPosition(endPosition: number): Iterator<SequenceInterval>;
+  /** addInterval / deleteInterval / changeInterval / propertyChanged (intervalCollection.ts:1257-1300). */
+  on(event: "addInterval" | "deleteInterval" | "changeInterval" | "propertyChanged", listener: (...args: any[]) => void): this;
+  off(event: string, listener: (...args: any[]) => void): this;
+  /** ISerializedIntervalCollectionV2 (:1968-1977); loads back through getIntervalCollection(label, emitter, serialized). */
+  serializeInternal(): { label: string; intervals: any[]; version: 2 };
+  /** The value type's rebase of a pending op for re-sending (makeOpsMap :1163-1172): deletes unchanged,
+   *  adds / changes through rebaseLocalInterval; undefined: send the op empty. meta: the emitter's 4th argument. */
+  rebaseOp(opName: "add" | "change" | "delete", value: any, meta: { localSeq: number }): any;
+  /** rebaseLocalInterval (:1735-1803); needs an {events: true} document. */
+  rebaseLocalInterval(opName: "add" | "change", value: any, localSeq: number): any;
   [Symbol.iterator](): Iterator<SequenceInterval>;
 }
 

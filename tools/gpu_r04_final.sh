@@ -4,7 +4,7 @@
 # local-client leg (side legs off where a profile needs the timed launch last)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r04final
+O=gpurun_out/r04final2
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
 echo "tests rc=$?" > $O/rc.txt
@@ -23,4 +23,7 @@ timeout -k 10 300 $P --config 2 > $O/bench2.json 2> $O/bench2.err || exit 1
 timeout -k 10 300 $P --config 4 > $O/bench4.json 2> $O/bench4.err || exit 1
 timeout -k 10 300 $P --docs 1250 > $O/bench_1250.json 2> $O/bench_1250.err || exit 1
 timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $O/stats_local -o run --output-format csv -- python3 tools/local_leg.py 0 > $O/local.json 2> $O/local.err || exit 1
+for L in 0 65536; do
+  MTE_HTREE_LDS=$L timeout -k 10 300 python3 -u tools/lc_probe.py > $O/probe_lds_$L.json 2> $O/probe_lds_$L.err || exit 1
+done
 echo done >> $O/rc.txt
