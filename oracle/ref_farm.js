@@ -35,7 +35,9 @@
 //         (client.ts:360-364, 1107-1110) -- or removes one of its own
 //         (removeLocalReferencePosition): ["F", pos, refType] / ["X", index];
 //         each checkpoint state then holds "refs", the client's references'
-//         localReferencePositionToPosition in creation order (null: removed)
+//         localReferencePositionToPosition in creation order (null: removed);
+//          stay: the chance that a reference made is StayOnRemove (drawn from
+//         the same number, so the farms without it are unchanged)
 // stdout: {"sets": [{..params, "names": [...], "log": [[clientId, seq, ref, msn, "op", contents]],
 //                    "events": [[["L"|"A", logIndex] | ["R", op], ...] per client],
 //                    "checkpoints": [{"done": [events applied per client],
@@ -220,7 +222,9 @@ function runSet(p) {
       const len = c.getLength();
       if (len > 0 && (live.length === 0 || R.next() < 0.75)) {
         const pos = R.int(0, len - 1);
-        const type = R.next() < 0.8 ? ReferenceType.SlideOnRemove : ReferenceType.Simple;
+        const u = R.next();
+        const type = p.stay && u < p.stay ? ReferenceType.StayOnRemove
+          : u < 0.8 ? ReferenceType.SlideOnRemove : ReferenceType.Simple;
         const { segment, offset } = c.getContainingSegment(pos);
         refs[i].push(c.createLocalReferencePosition(segment, offset, type, undefined));
         events[i].push(["F", pos, type]);

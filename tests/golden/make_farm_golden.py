@@ -27,7 +27,12 @@ which local ops also address id'd markers through relative positions
 name a marker), in both length calculations, with lagging clients, rollbacks
 and reconnects among the sets.
 
-Usage: python3 tests/golden/make_farm_golden.py [--refs | --legacy | --relpos]
+With --stay it writes tests/golden/localref_stay_vectors.json.gz: farms as
+--refs in which a third to three fifths of the references made are
+StayOnRemove -- they stay on their removed segment (localReference.ts:434,
+469) until the lazy zamboni unlinks it, then read detached.
+
+Usage: python3 tests/golden/make_farm_golden.py [--refs | --stay | --legacy | --relpos]
 """
 import gzip
 import json
@@ -43,6 +48,7 @@ import ref_util  # noqa: E402
 
 OUT = os.path.join(HERE, "farm_vectors.json.gz")
 OUT_REFS = os.path.join(HERE, "localref_vectors.json.gz")
+OUT_STAY = os.path.join(HERE, "localref_stay_vectors.json.gz")
 OUT_LEGACY = os.path.join(HERE, "legacy_farm_vectors.json.gz")
 OUT_RELPOS = os.path.join(HERE, "relpos_farm_vectors.json.gz")
 FARM_JS = os.path.join(ROOT, "oracle", "ref_farm.js")
@@ -71,6 +77,12 @@ ROLLBACK_ANNOTATE_SETS = [(4000 + i, 2 + i % 6, 400 + 100 * (i % 3), ["", "hello
 REF_SETS = [(7000 + i, 2 + i % 6, 300 + 100 * (i % 5), ["", "hello world", "abc\ndef"][i % 3], 5, [64, 200, 400][i % 3],
              [0.0, 0.2][i % 2], [1, 2] if i % 4 == 3 else None, [0.1, 0.25][(i % 2) if i < 20 else 1 - i % 2])
             for i in range(40)]
+
+# StayOnRemove references among them (--stay): (seed, clients, steps, initial
+# text, checkpoints, text bound, rollback, rollback types, refs, stay)
+STAY_SETS = [(7500 + i, 2 + i % 6, 400 + 100 * (i % 5), ["", "hello world", "abc\ndef"][i % 3], 6, [64, 200, 400][i % 3],
+              [0.0, 0.2][i % 2], [1, 2] if i % 4 == 3 else None, [0.15, 0.3][i % 2], [0.35, 0.6][(i // 2) % 2])
+             for i in range(32)]
 
 
 # legacy length calculation: (seed, clients, steps, initial text, checkpoints,
@@ -137,12 +149,15 @@ def main_legacy(out):
     print(f"{len(res['sets'])} legacy sets, reference failed on {failed}")
 
 
-def main_refs(out):
+def main_refs(out, stay=False):
     res = {"sets": [], "generator": "oracle/ref_farm.js with refs (reference Client, mulberry32 seeds)"}
     failed = []
-    for sd, c, n, t, k, m, rb, types, refs in REF_SETS:
+    for row in (STAY_SETS if stay else REF_SETS):
+        sd, c, n, t, k, m, rb, types, refs = row[:9]
         one = {"seed": sd, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
                "rollback": rb, "refs": refs}
+        if stay:
+            one["stay"] = row[9]
         if types:
             one["rollbackTypes"] = types
         q = subprocess.run(["node", FARM_JS, out], input=json.dumps({"sets": [one]}), capture_output=True, text=True,
@@ -152,10 +167,11 @@ def main_refs(out):
         else:
             failed.append(sd)
     res["seeds_the_reference_failed"] = failed
-    with gzip.open(OUT_REFS, "wt", encoding="utf-8") as fh:
+    dst = OUT_STAY if stay else OUT_REFS
+    with gzip.open(dst, "wt", encoding="utf-8") as fh:
         json.dump(res, fh, separators=(",", ":"))
     n_refs = sum(1 for s in res["sets"] for ev in s["events"] for e in ev if e[0] == "F")
-    print(f"wrote {OUT_REFS}: {len(res['sets'])} farms, {n_refs} local references")
+    print(f"wrote {dst}: {len(res['sets'])} farms, {n_refs} local references, reference failed on {failed}")
 
 
 def main():
@@ -164,6 +180,8 @@ def main():
     out = ref_util.build_ref()
     if "--refs" in sys.argv[1:]:
         return main_refs(out)
+    if "--stay" in sys.argv[1:]:
+        return main_refs(out, stay=True)
     if "--legacy" in sys.argv[1:]:
         return main_legacy(out)
     if "--relpos" in sys.argv[1:]:

@@ -66,7 +66,7 @@ def test_legacy_farm_vectors_shape():
 
 
 @pytest.mark.parametrize("name", ["legacy_farm_vectors.json.gz", "farm_vectors.json.gz",
-                                  "localref_vectors.json.gz"])
+                                  "localref_vectors.json.gz", "localref_stay_vectors.json.gz"])
 def test_tree_oracle_local_farms(name):
     passed, _ = _farms(tree_factory, name)
     assert passed > 700
@@ -74,7 +74,8 @@ def test_tree_oracle_local_farms(name):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["legacy_farm_vectors.json.gz", "farm_vectors.json.gz",
-                                  "localref_vectors.json.gz", "reconnect_vectors.json.gz"])
+                                  "localref_vectors.json.gz", "localref_stay_vectors.json.gz",
+                                  "reconnect_vectors.json.gz"])
 def test_gpu_local_farms_on_the_tree(name):
     g = _farms(device_factory, name)
     assert g == _farms(tree_factory, name)

@@ -16,6 +16,15 @@ references while editing, with lagging refSeqs, rollbacks and annotates; at
 every checkpoint every reference's position must equal the reference
 client's.  Two mutations of the slide rule (pending inserts as targets, no
 backward slide) fail 219 and 327 of the 880 checkpoints.
+
+StayOnRemove references (localReference.ts:434, 469: they stay on their
+removed segment, at its position) are pinned by 32 more farms
+(tests/golden/localref_stay_vectors.json.gz, make_farm_golden.py --stay):
+there the reference's lazy zamboni (mergeTree.ts:680-705) decides when such a
+reference reads detached -- the unlink of its tombstone -- so they hold for
+the local-client documents' tree pass (titems.c, mte_htree.h), which keeps that
+zamboni; the flat restatement's compaction at minSeq detaches them at other
+times and is not held to them.
 """
 import gzip
 import json
@@ -31,11 +40,19 @@ from fluidframework_amd.packing import BatchBuilder, DocClients, Interner
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 VECTORS = os.path.join(HERE, "golden", "localref_vectors.json.gz")
+STAY_VECTORS = os.path.join(HERE, "golden", "localref_stay_vectors.json.gz")
 
 
-def ref_sets():
-    with gzip.open(VECTORS, "rt", encoding="utf-8") as fh:
+def ref_sets(path=VECTORS):
+    with gzip.open(path, "rt", encoding="utf-8") as fh:
         return json.load(fh)["sets"]
+
+
+def tree_factory(k):
+    from oracle import OracleEngine
+    e = OracleEngine(k, tree="items")
+    e.lib.oti_set_limit(e.ctx, 1 << 20)
+    return e
 
 
 def oracle_factory(k):
@@ -66,6 +83,37 @@ def test_oracle_localref_farms():
     assert passed == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
 
 
+def test_stay_vectors_shape():
+    sets = ref_sets(STAY_VECTORS)
+    assert len(sets) == 32 and all(s["stay"] > 0 for s in sets)
+    made = [e for s in sets for ev in s["events"] for e in ev if e[0] == "F"]
+    assert len(made) > 3000 and sum(1 for e in made if e[2] == REF_STAY_ON_REMOVE) > 1400
+    vals = [p for s in sets for cp in s["checkpoints"] for st in cp["states"] for p in st["refs"]]
+    assert vals.count(-1) > 2000 and vals.count(None) > 3000
+
+
+def test_tree_oracle_stay_farms():
+    """The tree restatement equals the reference at every checkpoint of the
+    StayOnRemove farms, and the flat restatement, whose compaction at minSeq is
+    not the reference's lazy zamboni, does not (so the farms do reach the
+    unlink of a tombstone holding a StayOnRemove reference)."""
+    sets = ref_sets(STAY_VECTORS)
+    total = sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
+    passed, failures = replay_ref_farm(tree_factory, sets)
+    assert not failures, failures[:2]
+    assert passed == total
+    _, flat_failures = replay_ref_farm(oracle_factory, sets)
+    assert len(flat_failures) > 50
+
+
+@pytest.mark.gpu
+def test_gpu_stay_farms():
+    sets = ref_sets(STAY_VECTORS)
+    passed, failures = replay_ref_farm(device_factory, sets)
+    assert not failures, failures[:2]
+    assert passed == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
+
+
 def test_localref_farm_live():
     """The committed vectors are what the erased reference computes now (build
     container only: the reference does not travel)."""
@@ -73,8 +121,9 @@ def test_localref_farm_live():
     import ref_util
     if not ref_util.ref_available():
         pytest.skip("reference sources not in this container")
-    keys = ("seed", "clients", "steps", "initialText", "nCheckpoints", "maxText", "rollback", "refs", "rollbackTypes")
-    for s in ref_sets()[:4]:
+    keys = ("seed", "clients", "steps", "initialText", "nCheckpoints", "maxText", "rollback", "refs", "rollbackTypes",
+            "stay")
+    for s in ref_sets()[:4] + ref_sets(STAY_VECTORS)[:2]:
         inp = {"sets": [{k: s[k] for k in keys if k in s}]}
         p = subprocess.run(["node", os.path.join(os.path.dirname(HERE), "oracle", "ref_farm.js"), ref_util.build_ref()],
                            input=json.dumps(inp), capture_output=True, text=True, timeout=600, check=True)

@@ -78,7 +78,7 @@ def test_js_packing_matches_python_packing_on_fixtures(fresh):
 
 
 @pytest.mark.parametrize("vectors", ["farm_vectors.json.gz", "reconnect_vectors.json.gz", "localref_vectors.json.gz",
-                                     "relpos_farm_vectors.json.gz"])
+                                     "localref_stay_vectors.json.gz", "relpos_farm_vectors.json.gz"])
 def test_js_packing_matches_python_packing_on_local_farms(vectors):
     """Local ops and acks (and, on the reconnect farms, ops held offline and
     regeneratePendingOp's MTE_OP_REGEN records): the JS and Python packers emit
@@ -325,16 +325,18 @@ def test_node_farm_every_client_local_on_gpu(mode):
 
 
 @pytest.mark.gpu
-def test_node_local_references_on_gpu():
+@pytest.mark.parametrize("vectors", ["localref_vectors.json.gz", "localref_stay_vectors.json.gz"])
+def test_node_local_references_on_gpu(vectors):
     """BatchClient {localClient, refs}: every client of the 40 local-reference
-    farms the reference ran creates / removes its references through
-    createLocalReferencePosition / removeLocalReferencePosition, and at every
-    checkpoint localReferencePositionToPosition of each equals the reference's
-    (tests/node/farm_gpu.js over localref_vectors.json.gz)."""
+    farms the reference ran (and of the 32 with StayOnRemove references)
+    creates / removes its references through createLocalReferencePosition /
+    removeLocalReferencePosition, and at every checkpoint
+    localReferencePositionToPosition of each equals the reference's
+    (tests/node/farm_gpu.js)."""
     import gzip
-    j = json.loads(node("tests/node/farm_gpu.js", "batched", "all", "localref_vectors.json.gz", timeout=600))
+    j = json.loads(node("tests/node/farm_gpu.js", "batched", "all", vectors, timeout=600))
     assert j["nFailures"] == 0, j["failures"]
-    with gzip.open(os.path.join(ROOT, "tests", "golden", "localref_vectors.json.gz"), "rt") as fh:
+    with gzip.open(os.path.join(ROOT, "tests", "golden", vectors), "rt") as fh:
         sets = json.load(fh)["sets"]
     assert j["passed"] == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
 
