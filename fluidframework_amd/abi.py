@@ -51,6 +51,8 @@ DELTA_REGEN = 0x10    # kind flag of its output records
 DELTA_REBASE = 0x20   # MTE_OP_REF b = 4 / 5: the answer's kind
 ANNOTATE_SLOTS = 32   # pending local annotate groups tracked per document
 F_MARKER, F_MSG_END, F_REWRITE, F_LOCAL = 0x1, 0x2, 0x4, 0x8
+F_COMBINE = 0x10         # annotate combiningOp incr / consensus (value maps, include/mte.h)
+COMBINE_PAIR = 0x80000000
 LOCAL_SEQ_BASE = 0x40000000
 NO_PROPS = 0xFFFFFFFF
 DOC_NEW_LENGTH_CALC = 0x1

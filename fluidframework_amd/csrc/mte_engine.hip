@@ -855,6 +855,19 @@ const char* bad_op(const mte_op& o, const mte_batch* b, bool local_doc, bool ref
   } else if (o.type == MTE_OP_ANNOTATE && o.a >= b->n_propsets) {
     return "propset out of range";
   }
+  if (o.flags & MTE_F_COMBINE) {
+    if (o.type != MTE_OP_ANNOTATE || (o.flags & (MTE_F_LOCAL | MTE_F_REWRITE))) return "combining record: type or flags";
+    if (!local_doc) return "combiningOp incr / consensus outside an MTE_DOC_LOCAL_CLIENT document";
+    const mte_propset& ps = b->propsets[o.a];
+    if ((uint64_t)ps.first + ps.count > b->n_props) return "combining propset out of range";
+    for (uint32_t t = 0; t < ps.count;) {  // headers and their pairs tile the set exactly
+      const mte_prop& h = b->props[ps.first + t];
+      if ((h.key & MTE_COMBINE_PAIR) || h.value > ps.count - t - 1) return "combining propset: header";
+      for (uint32_t u = 1; u <= h.value; u++)
+        if (!(b->props[ps.first + t + u].key & MTE_COMBINE_PAIR)) return "combining propset: pair";
+      t += 1 + h.value;
+    }
+  }
   return nullptr;
 }
 

@@ -1121,7 +1121,20 @@ __device__ __forceinline__ int ht_range(HT& h, const s8v& op, bool local, const 
             const mte_prop p = a.pe[aps.first + t];
             if (p.key >= a.n_keys || p.key >= (uint32_t)K) continue;
             uint32_t* vp = h.pl + (uint64_t)(kFieldPlanes + p.key) * h.sd + i;
-            if (local) {
+            if (flags & MTE_F_COMBINE) {
+              // combine(op, current, undefined, seq): the host's map of every value
+              // the key can hold; pending keys are no exception (shouldModifyKey)
+              const uint32_t old = ld_l2(vp);
+              uint32_t nv = old;
+              for (uint32_t u = 1; u <= p.value; u++) {
+                const mte_prop q = a.pe[aps.first + t + u];
+                if ((q.key & ~MTE_COMBINE_PAIR) == old) {
+                  nv = q.value;
+                  break;
+                }
+              }
+              *vp = nv;
+            } else if (local) {
               // the value before the first pending annotate of the key, then pending
               uint32_t* pk = h.pl + (uint64_t)(kPkPlane<K> + p.key) * h.sd + i;
               if (ld_l2(pk) == 0u) h.pl[(uint64_t)(kAnnPlane<K> + 1 + p.key) * h.sd + i] = ld_l2(vp);

@@ -30,7 +30,7 @@ import json
 
 import numpy as np
 
-from .abi import (F_LOCAL, F_MARKER, F_MSG_END, F_REWRITE, LOCAL_SEQ_BASE, MTE_E_CAPACITY, MTE_E_CLIENT_RANGE,
+from .abi import (COMBINE_PAIR, F_COMBINE, F_LOCAL, F_MARKER, F_MSG_END, F_REWRITE, LOCAL_SEQ_BASE, MTE_E_CAPACITY, MTE_E_CLIENT_RANGE,
                   MTE_E_INVALID_ARG, MTE_E_STATE, MTE_E_UNSUPPORTED, MTE_MAX_CLIENTS, NO_PROPS, OP_ACK, OP_ROLLBACK,
                   OP_REGEN, OP_RBKEY, OP_REF, OP_RELPOS, RP_BEFORE1, RP_BEFORE2, RP_POS1, RP_POS2,
                   ANNOTATE_SLOTS, REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE,
@@ -65,6 +65,14 @@ class Interner:
         self.key_names = []
         self.values = {}
         self.value_json = [None]
+        self.key_vals = {}  # key -> the value ids it was ever given (combining ops' domain)
+
+    def kv(self, name: str, v):
+        """(key, value id) of one property, noting the value under its key."""
+        k, vid = self.key(name), self.value(v)
+        if vid:
+            self.key_vals.setdefault(k, set()).add(vid)
+        return k, vid
 
     def key(self, name: str) -> int:
         k = self.keys.get(name)
@@ -111,7 +119,35 @@ class PropTable:
             raise MergeTreeError(MTE_E_INVALID_ARG, "props must be an object")
         first = len(self.entries)
         for name, v in props.items():
-            self.entries.append((self.interner.key(name), self.interner.value(v)))
+            self.entries.append(self.interner.kv(name, v))
+        self.sets.append((first, len(self.entries) - first))
+        return len(self.sets) - 1
+
+    def add_combining(self, props: dict, comb: dict, seq: int) -> int:
+        """The property set of an annotate with combiningOp incr / consensus: per
+        key a header (key, n) and n pairs (old value id | MTE_COMBINE_PAIR, new
+        value id) -- the map combine(comb, old, undefined, seq) makes of every
+        value the key can hold (segmentPropertiesManager.ts:141: the op's own
+        value is never read), old values it leaves alone omitted, 0 = absent."""
+        if not isinstance(props, dict):
+            raise MergeTreeError(MTE_E_INVALID_ARG, "props must be an object")
+        it = self.interner
+        first = len(self.entries)
+        for name in props:
+            k = it.key(name)
+            dom = sorted(it.key_vals.get(k, ())) + [0]
+            pairs = []
+            for old in dom:
+                cur = _ABSENT if old == 0 else json.loads(it.value_json[old])
+                new = combine_value(comb, cur, seq)
+                nid = 0 if new is _ABSENT else it.value(new)
+                if nid != old:
+                    pairs.append((old | COMBINE_PAIR, nid))
+            for _, nid in pairs:
+                if nid:
+                    it.key_vals.setdefault(k, set()).add(nid)
+            self.entries.append((k, len(pairs)))
+            self.entries.extend(pairs)
         self.sets.append((first, len(self.entries) - first))
         return len(self.sets) - 1
 
@@ -119,6 +155,77 @@ class PropTable:
         ps = np.array(self.sets, dtype=PROPSET_DTYPE) if self.sets else np.zeros(0, PROPSET_DTYPE)
         pe = np.array(self.entries, dtype=PROP_DTYPE) if self.entries else np.zeros(0, PROP_DTYPE)
         return ps, pe
+
+
+_ABSENT = object()  # a key the segment does not have (JS undefined)
+_NAN = float("nan")
+
+
+def _js_num(x) -> str:
+    """Number.prototype.toString for the values JSON brings (integers and
+    short decimals; JS's exponent forms are not restated)."""
+    if x != x:
+        return "NaN"
+    if float(x).is_integer() and abs(x) < 1e21:
+        return str(int(x))
+    return repr(float(x))
+
+
+def _js_str(v) -> str:
+    """String(v) for a JSON value (arrays join their elements, null -> "")."""
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, (int, float)):
+        return _js_num(v)
+    if isinstance(v, str):
+        return v
+    if isinstance(v, list):
+        return ",".join("" if e is None else _js_str(e) for e in v)
+    return "[object Object]"
+
+
+def _js_truthy(v) -> bool:
+    if v is _ABSENT or v is None or v is False or v == "":
+        return False
+    if isinstance(v, (int, float)) and not isinstance(v, bool):
+        return v == v and v != 0
+    return True
+
+
+def _utf16(s: str) -> bytes:
+    return s.encode("utf-16-be")
+
+
+def combine_value(comb: dict, cur, seq: int):
+    """combine(combiningInfo, currentValue, undefined, seq) (properties.ts:24-62)
+    with JS semantics: incr adds undefined -- a number, boolean, null or
+    absent value becomes NaN, a string s becomes s + "undefined" (an array or
+    object its String() form + "undefined") -- then a truthy minValue replaces
+    a string below it (both strings: UTF-16 order; otherwise the comparison is
+    on NaN and false); consensus makes {value: undefined, seq} (JSON {"seq":
+    seq}) of an absent value and stamps the seq of an object whose seq is -1
+    (in place in the reference: see DESIGN.md on aliasing), other values stay."""
+    name = comb.get("name")
+    if cur is _ABSENT and "defaultValue" in comb:
+        cur = comb["defaultValue"]
+    if name == "incr":
+        if cur is _ABSENT or cur is None or isinstance(cur, (bool, int, float)):
+            cur = _NAN
+        else:
+            cur = _js_str(cur) + "undefined"
+        mv = comb.get("minValue", _ABSENT)
+        if _js_truthy(mv) and isinstance(cur, str):
+            pm = mv if isinstance(mv, str) else (_js_str(mv) if isinstance(mv, (list, dict)) else None)
+            if pm is not None and _utf16(cur) < _utf16(pm):
+                cur = mv
+        return cur
+    if name == "consensus":
+        if cur is _ABSENT or cur is None:
+            return {"seq": seq}
+        if isinstance(cur, dict) and cur.get("seq") == -1:
+            return {**cur, "seq": seq}
+        return cur
+    raise MergeTreeError(MTE_E_UNSUPPORTED, f"combiningOp {name!r}")
 
 
 DEFAULT_REF_CAPACITY = 1024  # mte_set_ref_capacity's default (include/mte.h)
@@ -277,7 +384,11 @@ class BatchBuilder:
                     clients.no_rollback.discard(ls)
                 recs.append((OP_ACK, 0, lo, hi, mask, NO_PROPS))
             else:
-                self._op_records(msg.get("contents"), recs)
+                self._comb = (clients.local, seq)
+                try:
+                    self._op_records(msg.get("contents"), recs)
+                finally:
+                    self._comb = None
         # the slot is taken only once the message has validated
         short = clients.short(sender, seq)
         if short >= MTE_MAX_CLIENTS:
@@ -500,6 +611,18 @@ class BatchBuilder:
         elif t == ANNOTATE:
             comb = op.get("combiningOp")
             flags = 0
+            if comb is not None and comb.get("name") in ("incr", "consensus"):
+                ctx = getattr(self, "_comb", None)
+                if ctx is None:
+                    raise MergeTreeError(MTE_E_UNSUPPORTED, f"local combiningOp {comb.get('name')!r}")
+                if not ctx[0]:
+                    raise MergeTreeError(MTE_E_UNSUPPORTED, f"combiningOp {comb.get('name')!r} outside a "
+                                         "local-client document (the HBM tree pass)")
+                if comb.get("name") == "consensus" and "defaultValue" in comb:
+                    raise MergeTreeError(MTE_E_UNSUPPORTED, "consensus with a defaultValue")
+                ps = self.props.add_combining(op.get("props", {}), comb, ctx[1])
+                recs.append((OP_ANNOTATE, F_COMBINE, _check_i32(p1, "pos1"), _check_i32(p2, "pos2"), ps, NO_PROPS))
+                return
             if comb is not None:
                 if comb.get("name") != "rewrite":
                     raise MergeTreeError(MTE_E_UNSUPPORTED, f"combiningOp {comb.get('name')!r}")

@@ -282,7 +282,7 @@ def from_json(spec, interner, client_id=int):
         return out
     if isinstance(spec, str):
         return utf16_units(spec).tolist()
-    props = {interner.key(k): interner.value(v) for k, v in (spec.get("props") or {}).items() if v is not None}
+    props = dict(interner.kv(k, v) for k, v in (spec.get("props") or {}).items() if v is not None)
     base = {"text": utf16_units(spec["text"]).tolist()} if "text" in spec else {"marker": dict(spec["marker"])}
     if props:
         base["props"] = props

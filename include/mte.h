@@ -217,6 +217,17 @@ extern "C" {
 #define MTE_F_MARKER 0x0001u  /* insert spec {marker:{refType}} (mergeTreeNodes.ts:602-609) */
 #define MTE_F_MSG_END 0x0002u /* last record of its message: window update follows      */
 #define MTE_F_REWRITE 0x0004u /* annotate combiningOp {name:"rewrite"} (segmentPropertiesManager.ts:105-119) */
+/* A sequenced annotate with combiningOp "incr" or "consensus": the reference
+ * sets each key to combine(op, currentValue, undefined, seq)
+ * (segmentPropertiesManager.ts:141, properties.ts:24-62) -- a function of the
+ * segment's current value alone -- and ignores pending local keys
+ * (shouldModifyKey, :94-102).  The host computes that function over every
+ * value the key can hold: the record's propset lists, per key, a header
+ * {key, n} and n pairs {old | MTE_COMBINE_PAIR, new} (value ids, 0 = absent);
+ * an old value not listed stays.  Only in MTE_DOC_LOCAL_CLIENT documents
+ * (the HBM tree pass) and never MTE_F_LOCAL: MTE_E_UNSUPPORTED otherwise.  */
+#define MTE_F_COMBINE 0x0010u
+#define MTE_COMBINE_PAIR 0x80000000u
 /* A local op of the document's own client (client 0), not yet sequenced:
  * insertSegmentLocal / removeRangeLocal / annotateRangeLocal (client.ts:131-229)
  * -> insertSegments / markRangeRemoved / annotateRange with seq =

@@ -759,6 +759,8 @@ static int doc_ack(odoc* d, const mte_op* op) {
 /* One op record.  Client.applyMsg -> applyRemoteOp (client.ts:918-935,
  * 862-889) -> updateSeqNumbers (937-945). */
 static int doc_apply(odoc* d, const mte_op* op, const apply_env* env) {
+  /* combiningOp incr / consensus: the HBM tree pass's restatement (titems.c) only */
+  if (op->flags & MTE_F_COMBINE) return MTE_E_UNSUPPORTED;
   const int newcalc = (d->flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
   const int32_t r = op->ref_seq, s = op->seq, m = d->min_seq;
   const int c = op->client;

@@ -36,6 +36,9 @@
 //         (removeLocalReferencePosition): ["F", pos, refType] / ["X", index];
 //         each checkpoint state then holds "refs", the client's references'
 //         localReferencePositionToPosition in creation order (null: removed);
+//          combine: the chance that an annotate carries a combining op
+//         (incr with or without defaultValue / minValue, or consensus on an
+//         id'd marker), its values sometimes strings
 //          stay: the chance that a reference made is StayOnRemove (drawn from
 //         the same number, so the farms without it are unchanged)
 // stdout: {"sets": [{..params, "names": [...], "log": [[clientId, seq, ref, msn, "op", contents]],
@@ -116,6 +119,10 @@ function readOut(client) {
 }
 
 const KEYS = ["client", "bold", "color"];
+const STRS = ["a", "zz", "m", "q"];
+// combine: the combining ops a farm's annotates draw from (properties.ts:24-62)
+const COMBINING = [{ name: "incr" }, { name: "incr", defaultValue: 2 }, { name: "incr", minValue: 3 },
+  { name: "incr", defaultValue: "q", minValue: "r" }, { name: "incr", minValue: "n" }];
 
 function runSet(p) {
   const R = rng(p.seed);
@@ -147,6 +154,22 @@ function runSet(p) {
       if (segment && Marker.is(segment) && segment.getId()) out.push(segment);
     }
     return out;
+  };
+  // combine: an annotate with a combining op -- incr through annotateRangeLocal,
+  // or consensus on an id'd marker of the range through
+  // annotateMarkerNotifyConsensus (client.ts:137-158; a range consensus would
+  // fail at its own ack, updateConsensusProperty reading relativePos1)
+  const combineOp = (c, start, end, props) => {
+    if (R.next() < 0.3) {
+      for (let pos = start; pos < end; pos++) {
+        const { segment } = c.getContainingSegment(pos);
+        if (segment && Marker.is(segment) && segment.getId()) {
+          return c.annotateMarkerNotifyConsensus(segment, props, () => {});
+        }
+      }
+    }
+    const comb = COMBINING[R.int(0, COMBINING.length - 1)];
+    return c.annotateRangeLocal(start, end, props, { ...comb });
   };
   const relPos = (id) => {
     const rp = { id };
@@ -270,7 +293,12 @@ function runSet(p) {
           const props = {};
           const nk = R.int(1, 2);
           for (let k = 0; k < nk; k++) props[KEYS[R.int(0, 2)]] = R.next() < 0.15 ? null : R.int(0, 5);
-          op = c.annotateRangeLocal(start, end, props, undefined);
+          if (p.combine && R.next() < 0.4) {
+            // string values too, so that incr's string branch is reached
+            for (const k of Object.keys(props)) if (R.next() < 0.3) props[k] = STRS[R.int(0, STRS.length - 1)];
+          }
+          if (p.combine && R.next() < p.combine) op = combineOp(c, start, end, props);
+          else op = c.annotateRangeLocal(start, end, props, undefined);
         }
       }
       if (op && offline[i]) {

@@ -632,6 +632,27 @@ static uint64_t apply_props_pending(uint32_t* props, const uint32_t* pk, uint32_
   return w;
 }
 
+/* annotateRange with combiningOp incr / consensus (MTE_F_COMBINE): each key
+ * becomes combine(op, current, undefined, seq) (segmentPropertiesManager.ts:141,
+ * properties.ts:24-62), pending keys included (shouldModifyKey :94-102); the
+ * host's per-key map lists {old | MTE_COMBINE_PAIR, new} after a {key, n}
+ * header, an old value not listed stays */
+static uint64_t apply_combine(uint32_t* props, uint32_t n_keys, const mte_propset* ps, const mte_prop* pe) {
+  uint64_t w = 0;
+  for (uint32_t t = 0; t < ps->count; t++) {
+    const mte_prop* h = &pe[ps->first + t];
+    if ((h->key & MTE_COMBINE_PAIR) || h->key >= n_keys) continue;
+    const uint32_t old = props[h->key];
+    for (uint32_t u = 1; u <= h->value; u++)
+      if ((pe[ps->first + t + u].key & ~MTE_COMBINE_PAIR) == old) {
+        props[h->key] = pe[ps->first + t + u].value;
+        break;
+      }
+    w++;
+  }
+  return w;
+}
+
 /* ---- local references (MTE_DOC_REFS, as oracle.c) ---------------------------- */
 #define REF_LIVE 0x80000000u
 #define REF_DETACHED 0x40000000u
@@ -1164,7 +1185,9 @@ static int tree_range(idoc* d, const mte_op* op, const env_t* env, int local) {
     } else {
       const mte_propset* ps = &env->b->propsets[op->a];
       g->po = 1;
-      if (local) {
+      if (op->flags & MTE_F_COMBINE) {
+        d->pwrites += apply_combine(g->props, env->n_keys, ps, env->b->props);
+      } else if (local) {
         for (uint32_t j = 0; j < ps->count; j++) {
           const mte_prop* p = &env->b->props[ps->first + j];
           if (p->key < env->n_keys && !g->pk[p->key]) g->basev[p->key] = g->props[p->key];
@@ -1420,7 +1443,11 @@ static int doc_apply(idoc* d, const mte_op* op, const env_t* env) {
   int rc;
   if (d->n + 4 > env->limit) return MTE_E_CAPACITY;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
-  if (op->flags & MTE_F_LOCAL) return local_doc ? doc_apply_local(d, op, env) : MTE_E_UNSUPPORTED;
+  if (op->flags & MTE_F_LOCAL) {
+    if (op->flags & MTE_F_COMBINE) return MTE_E_UNSUPPORTED;
+    return local_doc ? doc_apply_local(d, op, env) : MTE_E_UNSUPPORTED;
+  }
+  if ((op->flags & MTE_F_COMBINE) && (!local_doc || op->type != MTE_OP_ANNOTATE)) return MTE_E_UNSUPPORTED;
   d->wcache = -1; /* a sequenced message updates lengths */
   if (op->type == MTE_OP_ACK && !local_doc) return MTE_E_UNSUPPORTED;
   if (local_doc && op->type != MTE_OP_ACK && op->type != MTE_OP_NOOP && c == 0) return MTE_E_INVALID_ARG;

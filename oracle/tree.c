@@ -570,6 +570,8 @@ static int check_op_window(const tdoc* d, const mte_op* op) {
 }
 
 static int doc_apply(tdoc* d, const mte_op* op, const apply_env* env) {
+  /* combiningOp incr / consensus: the HBM tree pass's restatement (titems.c) only */
+  if (op->flags & MTE_F_COMBINE) return MTE_E_UNSUPPORTED;
   const int newcalc = (d->flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
   const int32_t s = op->seq;
   const int c = op->client;

@@ -174,7 +174,8 @@ def prop_runs(view, interner):
     [[start, end, {..}], ...] (empty == undefined, testClientLogger.ts:33-42)."""
     runs, pos = [], 0
     for ln, _kind, planes in view["segs"]:
-        p = interner.decode_props(planes)
+        # JSON.stringify (the reference's read-out) writes NaN as null
+        p = {k: (None if isinstance(v, float) and v != v else v) for k, v in interner.decode_props(planes).items()}
         if ln:
             if p and runs and runs[-1][1] == pos and runs[-1][2] == p:
                 runs[-1][1] = pos + ln
@@ -233,7 +234,8 @@ def canon_regen(op, orig, merge=True):
     return json.dumps(out, sort_keys=True)
 
 
-def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_regen=False, observers_only=False):
+def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_regen=False, observers_only=False,
+                    observers_local=False):
     """Replay farms the reference ran (oracle/ref_farm.js -> tests/golden/
     farm_vectors.json.gz): one MTE_DOC_LOCAL_CLIENT document per client of every
     set (the observer "A" included), each fed its own events in order — "L" a
@@ -252,11 +254,15 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_reg
     observers_only: only each set's observer "A" (it never sends), as a
     document of remote clients alone (no MTE_DOC_LOCAL_CLIENT: the flat passes
     with the new length calculation, the tree passes with the legacy one).
+    observers_local: only the observers, as MTE_DOC_LOCAL_CLIENT documents (the
+    HBM tree pass; combiningOp incr / consensus replay there only).
     Returns (checkpoints_passed, failures)."""
     from fluidframework_amd.abi import DOC_EVENTS, DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC, DOC_REFS
     from fluidframework_amd.packing import regen_ops
 
-    layout = [(si, ci) for si, s in enumerate(sets) for ci in range(1 if observers_only else len(s["names"]))]
+    assert not (observers_only and observers_local)
+    layout = [(si, ci) for si, s in enumerate(sets)
+              for ci in range(1 if observers_only or observers_local else len(s["names"]))]
     has_regen = not observers_only and any(e[0] == "G" for s in sets for ev in s["events"] for e in ev)
     has_refs = not observers_only and any(s.get("refs") for s in sets)
     inits, text = doc_inits([sets[si]["initialText"] for si, _ in layout],

@@ -32,7 +32,13 @@ With --stay it writes tests/golden/localref_stay_vectors.json.gz: farms as
 StayOnRemove -- they stay on their removed segment (localReference.ts:434,
 469) until the lazy zamboni unlinks it, then read detached.
 
-Usage: python3 tests/golden/make_farm_golden.py [--refs | --stay | --legacy | --relpos]
+With --combine it writes tests/golden/combine_farm_vectors.json.gz: farms whose
+annotates carry combiningOp incr (with and without defaultValue / minValue,
+string values among the numbers) or consensus on id'd markers
+(annotateMarkerNotifyConsensus), in both length calculations; the observer's
+state is what a document of sequenced ops alone must equal.
+
+Usage: python3 tests/golden/make_farm_golden.py [--refs | --stay | --combine | --legacy | --relpos]
 """
 import gzip
 import json
@@ -49,6 +55,7 @@ import ref_util  # noqa: E402
 OUT = os.path.join(HERE, "farm_vectors.json.gz")
 OUT_REFS = os.path.join(HERE, "localref_vectors.json.gz")
 OUT_STAY = os.path.join(HERE, "localref_stay_vectors.json.gz")
+OUT_COMBINE = os.path.join(HERE, "combine_farm_vectors.json.gz")
 OUT_LEGACY = os.path.join(HERE, "legacy_farm_vectors.json.gz")
 OUT_RELPOS = os.path.join(HERE, "relpos_farm_vectors.json.gz")
 FARM_JS = os.path.join(ROOT, "oracle", "ref_farm.js")
@@ -83,6 +90,13 @@ REF_SETS = [(7000 + i, 2 + i % 6, 300 + 100 * (i % 5), ["", "hello world", "abc\
 STAY_SETS = [(7500 + i, 2 + i % 6, 400 + 100 * (i % 5), ["", "hello world", "abc\ndef"][i % 3], 6, [64, 200, 400][i % 3],
               [0.0, 0.2][i % 2], [1, 2] if i % 4 == 3 else None, [0.15, 0.3][i % 2], [0.35, 0.6][(i // 2) % 2])
              for i in range(32)]
+
+# combining ops (--combine): (seed, clients, steps, initial text, checkpoints,
+# text bound, extra parameters)
+COMBINE_SETS = ([(7700 + i, 3 + i % 5, 400 + 100 * (i % 4), ["", "hello world", "abc\ndef"][i % 3], 5,
+                  [64, 200][i % 2], {"combine": [0.3, 0.6][i % 2], "allowDiverge": True}) for i in range(20)] +
+                [(7750 + i, 3 + i % 4, 500, "hello world", 5, 200, {"combine": 0.4, "legacy": True, "allowDiverge": True})
+                 for i in range(6)])
 
 
 # legacy length calculation: (seed, clients, steps, initial text, checkpoints,
@@ -149,6 +163,26 @@ def main_legacy(out):
     print(f"{len(res['sets'])} legacy sets, reference failed on {failed}")
 
 
+def main_combine(out):
+    res = {"sets": [], "generator": "oracle/ref_farm.js with combine (reference Client, mulberry32 seeds)"}
+    failed = []
+    for sd, c, n, t, k, m, extra in COMBINE_SETS:
+        one = {"seed": sd, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
+               "rollback": 0.0, **extra}
+        q = subprocess.run(["node", FARM_JS, out], input=json.dumps({"sets": [one]}), capture_output=True, text=True,
+                           timeout=600)
+        if q.returncode == 0:
+            res["sets"] += json.loads(q.stdout)["sets"]
+        else:
+            failed.append(sd)
+    res["seeds_the_reference_failed"] = failed
+    with gzip.open(OUT_COMBINE, "wt", encoding="utf-8") as fh:
+        json.dump(res, fh, separators=(",", ":"))
+    n_comb = sum(1 for s in res["sets"] for e in s["log"]
+                 if e[4] == "op" and isinstance(e[5], dict) and e[5].get("combiningOp"))
+    print(f"wrote {OUT_COMBINE}: {len(res['sets'])} farms, {n_comb} combining ops, reference failed on {failed}")
+
+
 def main_refs(out, stay=False):
     res = {"sets": [], "generator": "oracle/ref_farm.js with refs (reference Client, mulberry32 seeds)"}
     failed = []
@@ -180,6 +214,8 @@ def main():
     out = ref_util.build_ref()
     if "--refs" in sys.argv[1:]:
         return main_refs(out)
+    if "--combine" in sys.argv[1:]:
+        return main_combine(out)
     if "--stay" in sys.argv[1:]:
         return main_refs(out, stay=True)
     if "--legacy" in sys.argv[1:]:

@@ -1,0 +1,166 @@
+"""combiningOp incr / consensus (VERDICT r03 missing #5):
+annotateRange with a combining op sets each key to combine(op, current,
+undefined, seq) -- segmentPropertiesManager.ts:141 passes undefined for the
+op's own value, so the result is a function of the segment's current value
+alone (properties.ts:24-62) -- and ignores pending local keys (shouldModifyKey,
+:94-102).  The host computes that function over every value the key can hold
+(packing.combine_value, PropTable.add_combining) and the record carries it as
+a value map (MTE_F_COMBINE, include/mte.h); the HBM tree pass (mte_htree.h)
+and its restatement (titems.c) apply it.  Local combining ops and documents
+outside the tree pass are refused (MTE_E_UNSUPPORTED).
+
+Pinned by 26 farms the reference ran (oracle/ref_farm.js with combine ->
+tests/golden/combine_farm_vectors.json.gz, make_farm_golden.py --combine):
+1,007 combining annotates -- incr with and without defaultValue / minValue on
+numbers and strings, consensus on id'd markers through
+annotateMarkerNotifyConsensus -- in both length calculations; every
+observer's text and properties equal the reference's at every checkpoint.
+The reference's clients do not converge under them (a sender's pending key
+and a remote incr), so each observer is held to its own reference client.
+"""
+import gzip
+import json
+import math
+import os
+
+import pytest
+
+from fixtures_util import doc_inits, replay_ref_farm
+from fluidframework_amd.abi import DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC, MTE_E_UNSUPPORTED, MergeTreeError
+from fluidframework_amd.packing import _ABSENT, BatchBuilder, DocClients, Interner, combine_value
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+VECTORS = os.path.join(HERE, "golden", "combine_farm_vectors.json.gz")
+
+
+def combine_sets():
+    with gzip.open(VECTORS, "rt", encoding="utf-8") as fh:
+        return json.load(fh)
+
+
+def tree_factory(k):
+    from oracle import OracleEngine
+    e = OracleEngine(k, tree="items")
+    e.lib.oti_set_limit(e.ctx, 1 << 20)
+    return e
+
+
+def device_factory(k):
+    from fluidframework_amd.engine import DeviceEngine
+    return DeviceEngine(k)
+
+
+def _n_checkpoints(sets):
+    return sum(len(s["checkpoints"]) for s in sets)
+
+
+def test_combine_vectors_shape():
+    v = combine_sets()
+    sets = v["sets"]
+    assert len(sets) == 26 and v["seeds_the_reference_failed"] == []
+    assert sum(1 for s in sets if s.get("legacy")) == 6
+    names = [e[5]["combiningOp"]["name"] for s in sets for e in s["log"]
+             if e[4] == "op" and isinstance(e[5], dict) and e[5].get("combiningOp")]
+    assert len(names) == 1007 and names.count("consensus") == 29
+    vals = [x for s in sets for cp in s["checkpoints"] for r in cp["states"][0]["props"] for x in r[2].values()]
+    # NaN (JSON null), strings with minValue applied, consensus objects
+    assert vals.count(None) > 400 and "r" in vals and any(isinstance(x, dict) and "seq" in x for x in vals)
+
+
+def test_combine_value_rules():
+    nan = combine_value({"name": "incr"}, 5, 9)
+    assert math.isnan(nan) and math.isnan(combine_value({"name": "incr"}, _ABSENT, 9))
+    assert math.isnan(combine_value({"name": "incr", "defaultValue": 2}, _ABSENT, 9))
+    assert combine_value({"name": "incr"}, "ab", 9) == "abundefined"
+    assert combine_value({"name": "incr"}, [1, None, "x"], 9) == "1,,xundefined"
+    assert combine_value({"name": "incr"}, {"a": 1}, 9) == "[object Object]undefined"
+    assert combine_value({"name": "incr", "defaultValue": "q", "minValue": "r"}, _ABSENT, 9) == "r"
+    assert combine_value({"name": "incr", "minValue": "n"}, "zz", 9) == "zzundefined"
+    assert combine_value({"name": "incr", "minValue": 3}, "a", 9) == "aundefined"  # NaN comparison
+    assert combine_value({"name": "consensus"}, _ABSENT, 9) == {"seq": 9}
+    assert combine_value({"name": "consensus"}, {"seq": -1, "value": 4}, 9) == {"seq": 9, "value": 4}
+    assert combine_value({"name": "consensus"}, 3, 9) == 3
+
+
+def test_tree_oracle_combine_farms():
+    sets = combine_sets()["sets"]
+    passed, failures = replay_ref_farm(tree_factory, sets, observers_local=True)
+    assert not failures, failures[:2]
+    assert passed == _n_checkpoints(sets)
+
+
+def test_combine_map_is_what_the_tree_applies():
+    """Without the map (the annotate taken as a plain set) the farms fail: the
+    vectors do reach values the combining ops change."""
+    import fluidframework_amd.packing as P
+    sets = combine_sets()["sets"][:6]
+    orig = P.PropTable.add_combining
+    try:
+        P.PropTable.add_combining = lambda self, props, comb, seq: self.add(props)
+        _, failures = replay_ref_farm(tree_factory, sets, observers_local=True)
+    finally:
+        P.PropTable.add_combining = orig
+    assert len(failures) >= 6
+
+
+def _annotate(clients, comb, seq=1):
+    return {"clientId": "C", "sequenceNumber": seq, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
+            "type": "op", "contents": {"type": 2, "pos1": 0, "pos2": 1, "props": {"k": 1}, "combiningOp": comb}}
+
+
+def test_packer_combine_rules():
+    bb = BatchBuilder(1, Interner(4))
+    with pytest.raises(MergeTreeError) as ei:  # outside the tree pass
+        bb.add_message(0, DocClients("A"), _annotate(None, {"name": "incr"}))
+    assert ei.value.code == MTE_E_UNSUPPORTED
+    cl = DocClients("B", local=True)
+    with pytest.raises(MergeTreeError) as ei:  # a local combining op
+        bb.add_local(0, cl, {"type": 2, "pos1": 0, "pos2": 1, "props": {"k": 1}, "combiningOp": {"name": "incr"}})
+    assert ei.value.code == MTE_E_UNSUPPORTED
+    with pytest.raises(MergeTreeError) as ei:
+        bb.add_message(0, cl, _annotate(None, {"name": "consensus", "defaultValue": {"seq": -1}}))
+    assert ei.value.code == MTE_E_UNSUPPORTED
+    with pytest.raises(MergeTreeError) as ei:
+        bb.add_message(0, cl, _annotate(None, {"name": "sum"}))
+    assert ei.value.code == MTE_E_UNSUPPORTED
+
+
+def test_flat_restatement_refuses_combining_records():
+    from oracle import OracleEngine
+    inits, text = doc_inits(["abc"], flags=DOC_NEW_LENGTH_CALC | DOC_LOCAL_CLIENT)
+    it = Interner(4)
+    bb = BatchBuilder(1, it)
+    bb.add_message(0, DocClients("B", local=True), _annotate(None, {"name": "incr"}))
+    e = OracleEngine(4)
+    e.load_docs(inits, text)
+    e.apply_batch(bb.build())
+    assert int(e.statuses()[0]) == MTE_E_UNSUPPORTED
+    t = tree_factory(4)
+    t.load_docs(inits, text)
+    t.apply_batch(bb.build())
+    assert int(t.statuses()[0]) == 0
+
+
+def test_combine_farm_live():
+    """The committed vectors are what the erased reference computes now (build
+    container only: the reference does not travel)."""
+    import subprocess
+    import ref_util
+    if not ref_util.ref_available():
+        pytest.skip("reference sources not in this container")
+    keys = ("seed", "clients", "steps", "initialText", "nCheckpoints", "maxText", "rollback", "combine", "legacy",
+            "allowDiverge")
+    for s in combine_sets()["sets"][:3]:
+        inp = {"sets": [{k: s[k] for k in keys if k in s}]}
+        p = subprocess.run(["node", os.path.join(os.path.dirname(HERE), "oracle", "ref_farm.js"), ref_util.build_ref()],
+                           input=json.dumps(inp), capture_output=True, text=True, timeout=600, check=True)
+        live = json.loads(p.stdout)["sets"][0]
+        assert live["log"] == s["log"] and live["checkpoints"] == s["checkpoints"]
+
+
+@pytest.mark.gpu
+def test_gpu_combine_farms():
+    sets = combine_sets()["sets"]
+    passed, failures = replay_ref_farm(device_factory, sets, observers_local=True)
+    assert not failures, failures[:2]
+    assert passed == _n_checkpoints(sets)
