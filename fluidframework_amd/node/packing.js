@@ -38,6 +38,7 @@ const REF_SLIDE_ON_REMOVE = 0x40, REF_STAY_ON_REMOVE = 0x80, REF_TRANSIENT = 0x1
 const DELTA_REGEN = 0x10;    // MTE_DELTA_REGEN: kind flag of a regenerated op's records
 const ANNOTATE_SLOTS = 32;   // MTE_ANNOTATE_SLOTS: pending local annotate groups tracked per document
 const F_MARKER = 0x1, F_MSG_END = 0x2, F_REWRITE = 0x4, F_LOCAL = 0x8;
+const F_COMBINE = 0x10, COMBINE_PAIR = 0x80000000;  // incr / consensus value maps (include/mte.h)
 const LOCAL_SEQ_BASE = 0x40000000; // MTE_LOCAL_SEQ_BASE
 const NO_PROPS = 0xffffffff;
 const MAX_CLIENTS = 32;
@@ -87,6 +88,17 @@ class Interner {
     this.valueJson = [null];
     this.numIds = new Map();
     this.strIds = new Map();
+    this.keyVals = new Map();  // key -> the value ids it was ever given (combining ops' domain)
+  }
+  /** [key, value id] of one property, noting the value under its key */
+  kv(name, v) {
+    const k = this.key(name), id = this.value(v);
+    if (id) {
+      let set = this.keyVals.get(k);
+      if (set === undefined) this.keyVals.set(k, (set = new Set()));
+      set.add(id);
+    }
+    return [k, id];
   }
   key(name) {
     let k = this.keys.get(name);
@@ -109,7 +121,8 @@ class Interner {
       const id = prim.get(v);
       if (id !== undefined) return id;
     }
-    const cj = canonicalJson(v);
+    // NaN (an incr's result) is a value of its own, not JSON's null
+    const cj = typeof v === "number" && v !== v ? "NaN" : canonicalJson(v);
     let i = this.values.get(cj);
     if (i === undefined) {
       i = this.valueJson.length;
@@ -135,7 +148,8 @@ class Interner {
     for (let k = 0; k < planes.length; k++) {
       if (planes[k]) {
         if (out === undefined) out = {};
-        out[this.keyNames[k]] = JSON.parse(this.valueJson[planes[k]]);
+        const cj = this.valueJson[planes[k]];
+        out[this.keyNames[k]] = cj === "NaN" ? NaN : JSON.parse(cj);
       }
     }
     return out;
@@ -230,11 +244,68 @@ class PropTable {
     }
     const first = this.entries.length / 2;
     for (const name of Object.keys(props)) {
-      this.entries.push(this.interner.key(name), this.interner.value(props[name]));
+      const [k, id] = this.interner.kv(name, props[name]);
+      this.entries.push(k, id);
     }
     this.sets.push(first, this.entries.length / 2 - first);
     return this.sets.length / 2 - 1;
   }
+  /** An annotate with combiningOp incr / consensus (as packing.py
+   *  add_combining): per key a header [key, n] and n pairs [old | COMBINE_PAIR,
+   *  new] -- combineValue over every value the key was ever given, 0 = absent. */
+  addCombining(props, comb, seq) {
+    if (props === null || typeof props !== "object" || Array.isArray(props)) {
+      throw new MergeTreeError(E_INVALID_ARG, "props must be an object");
+    }
+    const it = this.interner;
+    const first = this.entries.length / 2;
+    for (const name of Object.keys(props)) {
+      const k = it.key(name);
+      const dom = Array.from(it.keyVals.get(k) || []).sort((x, y) => x - y);
+      dom.push(0);
+      const pairs = [];
+      for (const old of dom) {
+        const cj = it.valueJson[old];
+        const cur = old === 0 ? undefined : (cj === "NaN" ? NaN : JSON.parse(cj));
+        const nv = combineValue(comb, cur, seq);
+        const nid = nv === undefined ? 0 : it.value(nv);
+        if (nid !== old) pairs.push(old, nid);
+      }
+      for (let q = 1; q < pairs.length; q += 2) {
+        if (pairs[q]) {
+          let set = it.keyVals.get(k);
+          if (set === undefined) it.keyVals.set(k, (set = new Set()));
+          set.add(pairs[q]);
+        }
+      }
+      this.entries.push(k, pairs.length / 2);
+      for (let q = 0; q < pairs.length; q += 2) this.entries.push((pairs[q] | COMBINE_PAIR) >>> 0, pairs[q + 1]);
+    }
+    this.sets.push(first, this.entries.length / 2 - first);
+    return this.sets.length / 2 - 1;
+  }
+}
+
+/** The value an incr / consensus annotate leaves on a segment whose value is
+ *  cur (undefined: absent): the reference passes undefined for the op's own
+ *  value (segmentPropertiesManager.ts:141), so incr adds undefined to the value
+ *  (or its defaultValue) and then lets a truthy minValue replace anything
+ *  below it, and consensus makes {value: undefined, seq} of an absent value and
+ *  stamps the seq of an object whose seq is -1 (properties.ts:24-62).  Pure:
+ *  the reference mutates that object in place. */
+function combineValue(comb, cur, seq) {
+  let v = cur === undefined ? comb.defaultValue : cur;
+  if (comb.name === "incr") {
+    v += undefined;
+    if (comb.minValue && v < comb.minValue) v = comb.minValue;
+    return v;
+  }
+  if (comb.name === "consensus") {
+    if (v === undefined || v === null) return { seq };
+    if (typeof v === "object" && v.seq === -1) return Object.assign({}, v, { seq });
+    return v;
+  }
+  throw new MergeTreeError(E_UNSUPPORTED, "combiningOp " + String(comb.name));
 }
 
 function utf16(s) {
@@ -372,10 +443,13 @@ class BatchBuilder {
         this._put(doc, seq, ref, msn, OP_ACK, 0, 0, lo, hi, mask, NO_PROPS);
       } else {
         try {
+          this._combLocal = clients.local;
           this._opPut(doc, seq, ref, msn, msg.contents, this._src(doc));
         } catch (e) {
           this._truncate(k0);
           throw e;
+        } finally {
+          this._combLocal = false;
         }
       }
     }
@@ -453,6 +527,18 @@ class BatchBuilder {
     } else if (t === ANNOTATE) {
       let flags = 0;
       const comb = op.combiningOp;
+      if (comb !== undefined && comb !== null && (comb.name === "incr" || comb.name === "consensus")) {
+        if (!this._combLocal) {
+          throw new MergeTreeError(E_UNSUPPORTED, "combiningOp " + comb.name +
+            " outside a local-client document (the HBM tree pass)");
+        }
+        if (comb.name === "consensus" && "defaultValue" in comb) {
+          throw new MergeTreeError(E_UNSUPPORTED, "consensus with a defaultValue");
+        }
+        const ps = this.props.addCombining(op.props === undefined ? {} : op.props, comb, seq);
+        this._put(doc, seq, ref, msn, OP_ANNOTATE, 0, F_COMBINE, checkI32(p1, "pos1"), checkI32(p2, "pos2"), ps, NO_PROPS);
+        return;
+      }
       if (comb !== undefined && comb !== null) {
         if (comb.name !== "rewrite") throw new MergeTreeError(E_UNSUPPORTED, "combiningOp " + String(comb.name));
         flags = F_REWRITE;

@@ -52,10 +52,13 @@ function propRuns(c) {
 
 const eng = new MergeTreeEngine({ nKeys: 8 });
 const layout = [];
+// argv[5] "observers": each set's observer alone (the combining-op farms)
+const observersOnly = process.argv[5] === "observers";
 for (let si = 0; si < nSets; si++) {
   sets[si].names.forEach((name, ci) => {
+    if (observersOnly && ci !== 0) return;
     layout.push({ si, ci, refs: [], client: eng.createClient(sets[si].initialText,
-      { newLengthCalc: true, localClient: true, longClientId: name, refs: withRefs }) });
+      { newLengthCalc: !sets[si].legacy, localClient: true, longClientId: name, refs: withRefs }) });
   });
 }
 let passed = 0, opsChecked = 0;

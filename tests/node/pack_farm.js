@@ -17,7 +17,11 @@ const sets = JSON.parse(zlib.gunzipSync(fs.readFileSync(path.join(__dirname, "..
   process.argv[2] || "farm_vectors.json.gz"))).toString("utf8")).sets;
 const interner = new packing.Interner(8);
 const layout = [];
-sets.forEach((s, si) => s.names.forEach((name, ci) => layout.push([si, ci, new packing.DocClients(name, 0, true)])));
+// argv[3] "observers": each set's observer alone (the combining-op farms)
+const observers = process.argv[3] === "observers";
+sets.forEach((s, si) => s.names.forEach((name, ci) => {
+  if (!observers || ci === 0) layout.push([si, ci, new packing.DocClients(name, 0, true)]);
+}));
 const prev = layout.map(() => 0);
 const refSlots = layout.map(() => []);
 const nCp = Math.max.apply(null, sets.map((s) => s.checkpoints.length));

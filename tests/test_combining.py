@@ -158,6 +158,60 @@ def test_combine_farm_live():
         assert live["log"] == s["log"] and live["checkpoints"] == s["checkpoints"]
 
 
+def test_js_packing_of_combining_ops_matches_python():
+    """The Node packer emits the same records, property sets and value maps as
+    the Python one for every observer of the combining-op farms
+    (tests/node/pack_farm.js ... observers)."""
+    import base64
+    import subprocess
+    import numpy as np
+    from fixtures_util import as_msg
+    root = os.path.dirname(HERE)
+    p = subprocess.run(["node", os.path.join(root, "tests", "node", "pack_farm.js"), "combine_farm_vectors.json.gz",
+                        "observers"], capture_output=True, text=True, timeout=600, check=True)
+    lines = p.stdout.splitlines()
+    sets = combine_sets()["sets"]
+    interner = Interner(8)
+    layout = [(si, DocClients(s["names"][0], local=True)) for si, s in enumerate(sets)]
+    prev = [0] * len(layout)
+    assert len(lines) == max(len(s["checkpoints"]) for s in sets)
+    n_comb = 0
+    for j, line in enumerate(lines):
+        bb = BatchBuilder(len(layout), interner)
+        for d, (si, cl) in enumerate(layout):
+            s = sets[si]
+            if j >= len(s["checkpoints"]):
+                continue
+            done = s["checkpoints"][j]["done"][0]
+            for ev in s["events"][0][prev[d]:done]:
+                assert ev[0] == "A"
+                bb.add_message(d, cl, as_msg(s["log"][ev[1]]))
+            prev[d] = done
+        b = bb.build()
+        n_comb += int(((b["ops"]["flags"] & 0x10) != 0).sum()) if "flags" in b["ops"].dtype.names else 0
+        jj = json.loads(line)
+        for key, arr in (("offsets", b["op_offsets"]), ("ops", b["ops"]), ("text", b["text"]),
+                         ("propsets", b["propsets"]), ("props", b["props"])):
+            assert base64.b64decode(jj[key]) == np.ascontiguousarray(arr).tobytes(), (j, key)
+    assert n_comb > 0
+
+
+@pytest.mark.gpu
+def test_node_combine_farms_on_gpu():
+    """Node BatchClient {localClient}: every observer of the combining-op farms
+    applies the sequenced messages through applyMsg, and at every checkpoint
+    its text and getPropertiesAtPosition runs equal the reference client's
+    (tests/node/farm_gpu.js ... observers)."""
+    import subprocess
+    root = os.path.dirname(HERE)
+    p = subprocess.run(["node", os.path.join(root, "tests", "node", "farm_gpu.js"), "batched", "all",
+                        "combine_farm_vectors.json.gz", "observers"], capture_output=True, text=True, timeout=600,
+                       check=True)
+    j = json.loads(p.stdout)
+    assert j["nFailures"] == 0, j["failures"]
+    assert j["passed"] == _n_checkpoints(combine_sets()["sets"])
+
+
 @pytest.mark.gpu
 def test_gpu_combine_farms():
     sets = combine_sets()["sets"]
