@@ -39,6 +39,9 @@ function pack(upto) {
     if (end[d] > cursor[d]) count += end[d] - cursor[d];
   }
   bb = new BatchBuilder(n, interner, null, count + (count >> 4));
+  // a shard's interner sees neither the loaded documents' values nor the other
+  // shards', so it cannot close a combining op's value map: refused (loud)
+  bb.noCombining = true;
   for (let i = lo; i < hi; i++) {
     for (let d = 0; d < n; d++) {
       if (i >= cursor[d] && i < end[d]) {

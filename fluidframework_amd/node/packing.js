@@ -528,6 +528,9 @@ class BatchBuilder {
       let flags = 0;
       const comb = op.combiningOp;
       if (comb !== undefined && comb !== null && (comb.name === "incr" || comb.name === "consensus")) {
+        if (this.noCombining) {
+          throw new MergeTreeError(E_UNSUPPORTED, "combiningOp " + comb.name + " in a sharded (worker) packer");
+        }
         if (!this._combLocal) {
           throw new MergeTreeError(E_UNSUPPORTED, "combiningOp " + comb.name +
             " outside a local-client document (the HBM tree pass)");
