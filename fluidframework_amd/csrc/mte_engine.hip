@@ -345,6 +345,149 @@ __global__ __launch_bounds__(256) void digest_kernel(DigestArgs a) {
   }
 }
 
+// ---- the digest of big documents, tile-parallel ------------------------------
+// digest_kernel walks a document on one wave; a document of a million segments
+// (config 5) is 16k rows of it.  Every segment's contribution depends only on
+// its own units and its position P (c . B^(n - P - L)), so the same sums come
+// from tiles of kDgTile segments on waves of their own: the tiles' visible
+// lengths (dg_len_kernel), their prefix per document (dg_scan_kernel), each
+// tile's contributions at those positions (dg_tile_kernel), the tiles' sums
+// per document (dg_final_kernel).  Same value as digest_kernel, bit for bit.
+constexpr int kDgTile = 4 * kWave;  // segments per tile (4 per lane, row-major like digest_kernel)
+constexpr uint32_t kDgWaveMaxCap = 4096;  // contexts up to this capacity keep one wave per document
+
+struct DigestTiles {
+  uint32_t tpd;        // tiles per document (cap / kDgTile, rounded up)
+  int32_t* tsum;       // [doc][tpd] visible length, then its exclusive prefix
+  int32_t* tot;        // [doc] visible length of the document
+  uint64_t* part;      // [doc][tpd][3] h1, h2, sum of x
+};
+
+__device__ __forceinline__ int32_t dg_vis_len(const DigestArgs& a, uint64_t db, int i, int n) {
+  return (i < n && a.soa.rseq[db + i] == kNone) ? a.soa.len[db + i] : 0;
+}
+
+__global__ __launch_bounds__(256) void dg_len_kernel(DigestArgs a, DigestTiles t) {
+  const int w = threadIdx.x / kWave, l = lane_id();
+  const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
+  const int doc = (int)(wi / t.tpd), tile = (int)(wi % t.tpd);
+  if (doc >= (int)a.n_docs) return;
+  const int n = a.hdr[doc].nseg;
+  if (tile * kDgTile >= n) return;
+  const uint64_t db = (uint64_t)doc * a.cap;
+  int32_t v = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) v += dg_vis_len(a, db, tile * kDgTile + j * kWave + l, n);
+  const int32_t s = rdlane(wave_incl_scan(v), kWave - 1);
+  if (l == 0) t.tsum[(uint64_t)doc * t.tpd + tile] = s;
+}
+
+// one 256-thread workgroup per document: exclusive prefix of its tiles' lengths
+__global__ __launch_bounds__(256) void dg_scan_kernel(DigestArgs a, DigestTiles t) {
+  __shared__ int32_t wsum[4];
+  __shared__ int32_t carry_s;
+  const int doc = (int)blockIdx.x;
+  const int w = threadIdx.x / kWave, l = lane_id();
+  const int n = a.hdr[doc].nseg;
+  const int m = (n + kDgTile - 1) / kDgTile;
+  int32_t* ts = t.tsum + (uint64_t)doc * t.tpd;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  for (int b = 0; b < m; b += 256) {
+    const int i = b + (int)threadIdx.x;
+    const int32_t v = i < m ? ts[i] : 0;
+    const int32_t incl = wave_incl_scan(v);
+    if (l == kWave - 1) wsum[w] = incl;
+    __syncthreads();
+    int32_t before = carry_s;
+    for (int q = 0; q < w; q++) before += wsum[q];
+    if (i < m) ts[i] = before + incl - v;
+    __syncthreads();
+    if (threadIdx.x == 0) carry_s += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) t.tot[doc] = carry_s;
+}
+
+__global__ __launch_bounds__(256) void dg_tile_kernel(DigestArgs a, DigestTiles t) {
+  const int w = threadIdx.x / kWave, l = lane_id();
+  const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
+  const int doc = (int)(wi / t.tpd), tile = (int)(wi % t.tpd);
+  if (doc >= (int)a.n_docs) return;
+  const int n = a.hdr[doc].nseg;
+  if (tile * kDgTile >= n) return;
+  const uint64_t db = (uint64_t)doc * a.cap;
+  const int32_t tot = t.tot[doc];
+  int32_t carry = t.tsum[(uint64_t)doc * t.tpd + tile];
+  uint64_t h1 = 0, h2 = 0, xs = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int i = tile * kDgTile + j * kWave + l;
+    const int32_t L = dg_vis_len(a, db, i, n);
+    const int32_t incl = wave_incl_scan(L);
+    const int32_t P = carry + incl - L;
+    if (L > 0) {
+      uint64_t ph = 0;
+      for (uint32_t k = 0; k < a.n_keys; k++) {
+        const uint32_t v = a.soa.props[k * a.soa.plane_stride + db + i];
+        if (v) ph += mix64(((uint64_t)(k + 1) << 32) | v);
+      }
+      const uint32_t kind = a.soa.meta[db + i] >> 8;
+      const uint32_t toff = a.soa.toff[db + i];
+      uint64_t s1 = 0, s2 = 0;
+      for (int32_t u = 0; u < L; u++) {
+        const uint64_t rec = kind == 0 ? (uint64_t)a.arena[toff + (uint32_t)u] : ((1ull << 32) | (uint64_t)(kind - 1));
+        const uint64_t x = fold61(mix64(rec * 0x9E3779B97F4A7C15ull + ph));
+        s1 = addmod61(mulmod61(s1, a.pow1[0]), x);
+        s2 = addmod61(mulmod61(s2, a.pow2[0]), x);
+        xs += x;
+      }
+      const uint32_t e = (uint32_t)(tot - P - L);
+      h1 = addmod61(h1, mulmod61(s1, powmod61(a.pow1, e)));
+      h2 = addmod61(h2, mulmod61(s2, powmod61(a.pow2, e)));
+    }
+    carry += rdlane(incl, kWave - 1);
+  }
+#pragma unroll
+  for (int m = 1; m < kWave; m <<= 1) {
+    h1 = addmod61(h1, shfl_xor64(h1, m));
+    h2 = addmod61(h2, shfl_xor64(h2, m));
+    xs += shfl_xor64(xs, m);
+  }
+  if (l == 0) {
+    uint64_t* p = t.part + 3 * ((uint64_t)doc * t.tpd + tile);
+    p[0] = h1;
+    p[1] = h2;
+    p[2] = xs;
+  }
+}
+
+__global__ __launch_bounds__(256) void dg_final_kernel(DigestArgs a, DigestTiles t) {
+  const int w = threadIdx.x / kWave, l = lane_id();
+  const int doc = (int)blockIdx.x * 4 + w;
+  if (doc >= (int)a.n_docs) return;
+  const int m = (a.hdr[doc].nseg + kDgTile - 1) / kDgTile;
+  uint64_t h1 = 0, h2 = 0, xs = 0;
+  for (int i = l; i < m; i += kWave) {
+    const uint64_t* p = t.part + 3 * ((uint64_t)doc * t.tpd + (uint32_t)i);
+    h1 = addmod61(h1, p[0]);
+    h2 = addmod61(h2, p[1]);
+    xs += p[2];
+  }
+#pragma unroll
+  for (int s = 1; s < kWave; s <<= 1) {
+    h1 = addmod61(h1, shfl_xor64(h1, s));
+    h2 = addmod61(h2, shfl_xor64(h2, s));
+    xs += shfl_xor64(xs, s);
+  }
+  if (l == 0) {
+    a.out[4 * (size_t)doc + 0] = (uint64_t)t.tot[doc];
+    a.out[4 * (size_t)doc + 1] = h1;
+    a.out[4 * (size_t)doc + 2] = h2;
+    a.out[4 * (size_t)doc + 3] = xs;
+  }
+}
+
 // host helpers for the digest constants (must match oracle/oracle.c)
 uint64_t h_mulmod61(uint64_t a, uint64_t b) {
   unsigned __int128 p = (unsigned __int128)a * b;
@@ -411,6 +554,10 @@ struct mte_ctx {
   bool chunked = false;
   ChunkArgs ch{};
   uint64_t* d_digest = nullptr;
+  // tile-parallel digest of big-document contexts (dg_*_kernel), allocated at
+  // the first digest of such a context
+  void* d_dgt = nullptr;
+  DigestTiles dgt{};
 
   // text arena
   uint16_t* arena = nullptr;
@@ -598,7 +745,15 @@ int grow(mte_ctx* c, T** p, uint64_t* cap, uint64_t need, bool keep = false, uin
   HIPCHK(c, hipMalloc((void**)&q, nc * sizeof(T)));
   if (keep && *p && keep_n) HIPCHK(c, hipMemcpyAsync(q, *p, keep_n * sizeof(T), hipMemcpyDeviceToDevice, c->stream));
   if (*p) {
+    // every kernel that may still read the old buffer has to be done: the
+    // round phases' tail thread (mte_ctx::tail) enqueues onto the engine
+    // stream after this call could sync it, and the tree passes run on their
+    // own stream, which only the tail's finish() joins back (the
+    // HBM tree pass reads the text arena).  The tail's status stays in
+    // tail_rc for the next JOIN_TAIL.
+    if (c->tail.joinable()) c->tail.join();
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->tree_stream) HIPCHK(c, hipStreamSynchronize(c->tree_stream));
     HIPCHK(c, hipFree(*p));
   }
   *p = q;
@@ -628,6 +783,9 @@ void free_docs(mte_ctx* c) {
   c->chunked = false;
   if (c->d_wclock) (void)hipFree(c->d_wclock);
   c->d_wclock = nullptr;
+  if (c->d_dgt) (void)hipFree(c->d_dgt);
+  c->d_dgt = nullptr;
+  c->dgt = DigestTiles{};
   void* ps[] = {c->hdr, c->soa.len, c->stats, c->d_inits, c->d_init_props, c->d_digest, c->d_pairs,
                 c->d_tree, c->d_heap, c->d_tree_docs, c->d_rs_docs, c->d_refs, c->d_hheap, c->d_hst, c->d_hscr,
                 c->d_htree_docs};
@@ -793,7 +951,7 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   // contexts, otherwise HBM-resident and streamed per op
   if (c->chunked) {
     const size_t lds = sizeof(uint32_t) * MTE_MAX_CLIENTS * c->ch.ng_cap + sizeof(ChCtl);
-    const uint64_t col_bytes = (uint64_t)(c->ch.nch_cap + (c->ch.ng_cap + 63) / 64 * 64 + 64) * 4;
+    const uint64_t col_bytes = rnd_resolve_lds(c->ch.nch_cap);
     if (!S && c->round_phases && col_bytes <= kRoundLdsMax) {
       // round phases (mte_round.h): each phase plans every escalated
       // document's next run, replays the round-shaped runs chunk-parallel and
@@ -1657,7 +1815,26 @@ int mte_digest_device(mte_ctx* c, void* out, uint32_t n_docs) {
   a.pow1 = c->d_pow;
   a.pow2 = c->d_pow + 32;
   a.out = (uint64_t*)out;
-  hipLaunchKernelGGL(digest_kernel, dim3((n_docs + kDocsPerBlock - 1) / kDocsPerBlock), dim3(256), 0, c->stream, a);
+  if (c->cap > kDgWaveMaxCap) {
+    // documents of up to `cap` segments: tile-parallel (dg_*_kernel)
+    if (!c->d_dgt) {
+      DigestTiles& t = c->dgt;
+      t.tpd = (c->cap + kDgTile - 1) / kDgTile;
+      const uint64_t nt = (uint64_t)c->n_docs * t.tpd;
+      HIPCHK(c, hipMalloc(&c->d_dgt, nt * (4 + 24) + 4ull * c->n_docs + 64));
+      t.part = (uint64_t*)c->d_dgt;
+      t.tsum = (int32_t*)(t.part + 3 * nt);
+      t.tot = t.tsum + nt;
+    }
+    const uint64_t nt = (uint64_t)n_docs * c->dgt.tpd;
+    const uint32_t tb = (uint32_t)((nt + 3) / 4);
+    hipLaunchKernelGGL(dg_len_kernel, dim3(tb), dim3(256), 0, c->stream, a, c->dgt);
+    hipLaunchKernelGGL(dg_scan_kernel, dim3(n_docs), dim3(256), 0, c->stream, a, c->dgt);
+    hipLaunchKernelGGL(dg_tile_kernel, dim3(tb), dim3(256), 0, c->stream, a, c->dgt);
+    hipLaunchKernelGGL(dg_final_kernel, dim3((n_docs + 3) / 4), dim3(256), 0, c->stream, a, c->dgt);
+  } else {
+    hipLaunchKernelGGL(digest_kernel, dim3((n_docs + kDocsPerBlock - 1) / kDocsPerBlock), dim3(256), 0, c->stream, a);
+  }
   HIPCHK(c, hipGetLastError());
   return MTE_OK;
 }

@@ -49,6 +49,12 @@
 #ifndef MTE_STEPV_EMAX  // tiers up to this E run the per-slot-flag step (doc_step_v), larger ones doc_step
 #define MTE_STEPV_EMAX 4
 #endif
+#ifndef MTE_EARLY_PROPS  // 1: pass-1 tiers load an op's compiled propset at the op's start
+#define MTE_EARLY_PROPS 0
+#endif
+#ifndef MTE_DIAG_NOPAYLOAD  // diagnostics only (wrong results): pass-1 tiers skip the text-offset / property planes
+#define MTE_DIAG_NOPAYLOAD 0
+#endif
 #ifndef MTE_OUTLINE_E4  // 1: only the rare E = 4 tier out of line (the E <= 2 loops get the registers)
 #define MTE_OUTLINE_E4 0
 #endif

@@ -100,9 +100,9 @@ __device__ __forceinline__ void shift_v(Regs<E, K>& R, int32_t (&X)[NX > 0 ? NX 
     shift1_dpp(R.rseq, g1[0], g2[0]);
     shift1_dpp(R.rmask, g1[0], g2[0]);
     shift1_dpp(R.meta, g1[0], g2[0]);
-    shift1_dpp(R.toff, g1[0], g2[0]);
+    if constexpr (!MTE_DIAG_NOPAYLOAD) shift1_dpp(R.toff, g1[0], g2[0]);
 #pragma unroll
-    for (int k = 0; k < kRegPlanes<K>; k++) shift1_dpp(R.pr[k], g1[0], g2[0]);
+    for (int k = 0; k < (MTE_DIAG_NOPAYLOAD ? 0 : kRegPlanes<K>); k++) shift1_dpp(R.pr[k], g1[0], g2[0]);
 #pragma unroll
     for (int x = 0; x < NX; x++) shift1_dpp(X[x], g1[0], g2[0]);
   } else if constexpr (E == 1) {
@@ -112,9 +112,9 @@ __device__ __forceinline__ void shift_v(Regs<E, K>& R, int32_t (&X)[NX > 0 ? NX 
     perm_plane<E>(R.rseq, addr);
     perm_plane<E>(R.rmask, addr);
     perm_plane<E>(R.meta, addr);
-    perm_plane<E>(R.toff, addr);
+    if constexpr (!MTE_DIAG_NOPAYLOAD) perm_plane<E>(R.toff, addr);
 #pragma unroll
-    for (int k = 0; k < kRegPlanes<K>; k++) perm_plane<E>(R.pr[k], addr);
+    for (int k = 0; k < (MTE_DIAG_NOPAYLOAD ? 0 : kRegPlanes<K>); k++) perm_plane<E>(R.pr[k], addr);
 #pragma unroll
     for (int x = 0; x < NX; x++) perm_plane<E>(X[x], addr);
   } else if constexpr (E >= MTE_SHIFT_SEQ_EMIN) {
@@ -123,9 +123,9 @@ __device__ __forceinline__ void shift_v(Regs<E, K>& R, int32_t (&X)[NX > 0 ? NX 
     shift_plane<E>(R.rseq, g1, g2);
     shift_plane<E>(R.rmask, g1, g2);
     shift_plane<E>(R.meta, g1, g2);
-    shift_plane<E>(R.toff, g1, g2);
+    if constexpr (!MTE_DIAG_NOPAYLOAD) shift_plane<E>(R.toff, g1, g2);
 #pragma unroll
-    for (int k = 0; k < kRegPlanes<K>; k++) shift_plane<E>(R.pr[k], g1, g2);
+    for (int k = 0; k < (MTE_DIAG_NOPAYLOAD ? 0 : kRegPlanes<K>); k++) shift_plane<E>(R.pr[k], g1, g2);
 #pragma unroll
     for (int x = 0; x < NX; x++) shift_plane<E>(X[x], g1, g2);
   } else {
@@ -151,9 +151,9 @@ __device__ __forceinline__ void shift_v(Regs<E, K>& R, int32_t (&X)[NX > 0 ? NX 
     shift_apply<E, NF>(R.rseq, p1, p2, 2, g1, g2);
     shift_apply<E, NF>(R.rmask, p1, p2, 3, g1, g2);
     shift_apply<E, NF>(R.meta, p1, p2, 4, g1, g2);
-    shift_apply<E, NF>(R.toff, p1, p2, 5, g1, g2);
+    if constexpr (!MTE_DIAG_NOPAYLOAD) shift_apply<E, NF>(R.toff, p1, p2, 5, g1, g2);
 #pragma unroll
-    for (int k = 0; k < kRegPlanes<K>; k++) shift_apply<E, NF>(R.pr[k], p1, p2, kFieldPlanes + k, g1, g2);
+    for (int k = 0; k < (MTE_DIAG_NOPAYLOAD ? 0 : kRegPlanes<K>); k++) shift_apply<E, NF>(R.pr[k], p1, p2, kFieldPlanes + k, g1, g2);
 #pragma unroll
     for (int x = 0; x < NX; x++) shift_apply<E, NF>(X[x], p1, p2, kFieldPlanes + kRegPlanes<K> + x, g1, g2);
   }
@@ -163,19 +163,20 @@ __device__ __forceinline__ void shift_v(Regs<E, K>& R, int32_t (&X)[NX > 0 ? NX 
 // textSegment.ts:40-48, mergeTreeNodes.ts:602-609)
 template <int E, int K, bool S>
 __device__ __forceinline__ void put_new_v(Regs<E, K>& R, const bool (&at)[E], const s8v& op, uint32_t c,
-                                          uint32_t flags, const ReplayArgs& a, uint32_t (&st)[kNumStats]) {
+                                          uint32_t flags, const ReplayArgs& a, uint32_t (&st)[kNumStats],
+                                          const s8v* pq) {
   const int32_t s = op[0], pos2 = op[5];
   const bool marker = (flags & MTE_F_MARKER) != 0;
   const int32_t nlen = marker ? 1 : pos2;
   const uint32_t meta = (c + 1u) | (marker ? (1u + (uint32_t)pos2) << 8 : 0u);
   uint32_t toff = marker ? 0u : a.text_base + (uint32_t)op[6];
-  const uint32_t psi = (uint32_t)op[7];
+  const uint32_t psi = MTE_DIAG_NOPAYLOAD ? MTE_NO_PROPS : (uint32_t)op[7];
   uint32_t pr[kRP<K>][1];
   const bool one[1] = {true};
 #pragma unroll
   for (int kk = 0; kk < kRP<K>; kk++) pr[kk][0] = 0;
   if (kKeys<K> > 0 && psi != MTE_NO_PROPS) {
-    const s8v q2 = sload_props(a, psi);
+    const s8v q2 = pq ? *pq : sload_props(a, psi);
     apply_props<1, K>(pr, one, (uint32_t)q2[0], (uint32_t)q2[1], (uint32_t)q2[2], psi, a);
     MTE_STAT(st[kStPwrites] += (uint32_t)q2[3];)
     if constexpr (K == kPack4) {
@@ -222,7 +223,7 @@ template <int E, int K, bool S, bool CH>
 __device__ __forceinline__ int seg_op_v(Regs<E, K>& R, int& n, const s8v& op, uint32_t type, uint32_t c,
                                         uint32_t flags, int32_t m, bool newcalc, int32_t off, bool last,
                                         int32_t& tot, int32_t& dlen, const ReplayArgs& a,
-                                        uint32_t (&st)[kNumStats]) {
+                                        uint32_t (&st)[kNumStats], const s8v* pq = nullptr) {
   const int base = lane_id() * E;
   const int32_t s = op[0], r = op[1];
   const int32_t pos1 = op[4] - (CH ? off : 0);
@@ -302,7 +303,7 @@ __device__ __forceinline__ int seg_op_v(Regs<E, K>& R, int& n, const s8v& op, ui
       n += 1;
       MTE_STAT(st[kStWritten] += 1;)
     }
-    if (nlen > 0) put_new_v<E, K, S>(R, at, op, c, flags, a, st);
+    if (nlen > 0) put_new_v<E, K, S>(R, at, op, c, flags, a, st, pq);
     if constexpr (CH) dlen = nlen > 0 ? nlen : 0;
   } else {
     // markRangeRemoved / annotateRange: ensureIntervalBoundary at both ends
@@ -385,10 +386,10 @@ __device__ __forceinline__ int seg_op_v(Regs<E, K>& R, int& n, const s8v& op, ui
           for (int j = 0; j < E; j++) rl += in[j] ? L[j] : 0;
           dlen = -rdlane(wave_incl_scan(rl), kWave - 1);
         }
-      } else if (cnt > 0) {
+      } else if (cnt > 0 && !MTE_DIAG_NOPAYLOAD) {
         // PropertiesManager.addProperties (segmentPropertiesManager.ts:63-151)
         const uint32_t psi = (uint32_t)op[6];
-        const s8v q2 = sload_props(a, psi);
+        const s8v q2 = pq ? *pq : sload_props(a, psi);
         if (flags & MTE_F_REWRITE) {
 #pragma unroll
           for (int kk = 0; kk < kRegPlanes<K>; kk++)
@@ -439,8 +440,22 @@ __device__ __forceinline__ int doc_step_v(Regs<E, K>& R, DocRun& D, uint32_t (&s
   if (type <= MTE_OP_ANNOTATE) {
     MTE_STAT(st[kStScanned] += (uint32_t)n;)
     int32_t tot, dlen;
+#if MTE_EARLY_PROPS
+    // the op's compiled propset, loaded before the lengths and the scan so its
+    // latency hides behind them (annotates, and inserts that carry props)
+    s8v q2e;
+    const s8v* pq = nullptr;
+    if constexpr (kKeys<K> > 0) {
+      const uint32_t psi = type == MTE_OP_ANNOTATE ? (uint32_t)op[6] : (uint32_t)op[7];
+      const bool want = type == MTE_OP_ANNOTATE || (type == MTE_OP_INSERT && psi != MTE_NO_PROPS);
+      q2e = sload_props(a, want ? psi : 0u);
+      pq = &q2e;
+    }
+#else
+    const s8v* pq = nullptr;
+#endif
     const int rc = seg_op_v<E, K, S, false>(R, n, op, type, c, flags, D.min_seq, (D.flags & MTE_DOC_NEW_LENGTH_CALC) != 0,
-                                            0, true, tot, dlen, a, st);
+                                            0, true, tot, dlen, a, st, pq);
     if (rc) return rc;
   } else if (type != MTE_OP_NOOP) {
     return MTE_E_INVALID_ARG;
@@ -470,9 +485,9 @@ __device__ __forceinline__ int doc_step_v(Regs<E, K>& R, DocRun& D, uint32_t (&s
           R.rseq[0] = __builtin_amdgcn_ds_permute(addr, R.rseq[0]);
           R.rmask[0] = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int32_t)R.rmask[0]);
           R.meta[0] = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int32_t)R.meta[0]);
-          R.toff[0] = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int32_t)R.toff[0]);
+          if constexpr (!MTE_DIAG_NOPAYLOAD) R.toff[0] = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int32_t)R.toff[0]);
 #pragma unroll
-          for (int kk = 0; kk < kRegPlanes<K>; kk++)
+          for (int kk = 0; kk < (MTE_DIAG_NOPAYLOAD ? 0 : kRegPlanes<K>); kk++)
             R.pr[kk][0] = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int32_t)R.pr[kk][0]);
           const bool pad = l >= n_new;
           R.rseq[0] = pad ? kPad : R.rseq[0];
@@ -503,9 +518,9 @@ __device__ __forceinline__ int doc_step_v(Regs<E, K>& R, DocRun& D, uint32_t (&s
           compact_plane<E>(R.rseq, keep, dst, zlds);
           compact_plane<E>(R.rmask, keep, dst, zlds);
           compact_plane<E>(R.meta, keep, dst, zlds);
-          compact_plane<E>(R.toff, keep, dst, zlds);
+          if constexpr (!MTE_DIAG_NOPAYLOAD) compact_plane<E>(R.toff, keep, dst, zlds);
 #pragma unroll
-          for (int kk = 0; kk < kRegPlanes<K>; kk++) compact_plane<E>(R.pr[kk], keep, dst, zlds);
+          for (int kk = 0; kk < (MTE_DIAG_NOPAYLOAD ? 0 : kRegPlanes<K>); kk++) compact_plane<E>(R.pr[kk], keep, dst, zlds);
 #pragma unroll
           for (int jj = 0; jj < E; jj++) {
             const bool pad = base + jj >= n_new;

@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 5: round phases with the register group level + tile-parallel digest
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r05d
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_chunk.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/chunk_tests.log 2>&1 || exit 1
+P="python3 bench.py --no-cpu-baseline --no-tree-leg --no-node-leg --no-local-leg"
+timeout -k 10 300 $P --config 5 > $O/bench5.json 2> $O/bench5.err || exit 1
+timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $O/stats5 -o run --output-format csv -- $P --config 5 > $O/stats5.json 2> $O/stats5.err || exit 1
+echo done > $O/rc.txt
