@@ -951,7 +951,7 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
   // contexts, otherwise HBM-resident and streamed per op
   if (c->chunked) {
     const size_t lds = sizeof(uint32_t) * MTE_MAX_CLIENTS * c->ch.ng_cap + sizeof(ChCtl);
-    const uint64_t col_bytes = rnd_resolve_lds(c->ch.nch_cap);
+    const uint64_t col_bytes = rnd_resolve_lds(c->ch.nch_cap, c->ch.ng_cap);
     if (!S && c->round_phases && col_bytes <= kRoundLdsMax) {
       // round phases (mte_round.h): each phase plans every escalated
       // document's next run, replays the round-shaped runs chunk-parallel and

@@ -605,8 +605,10 @@ __device__ __forceinline__ int ht_scour(HT& h, int s, int e, uint32_t n_keys) {
           nl = pel > 0 && uni((uint32_t)h.arena[pet + pel - 1u]) == (uint32_t)'\n';
         }
         bool match = (tp & kTPo) == (tx & kTPo);
-        for (uint32_t k = 0; k < n_keys && k < (uint32_t)K && match; k++)
-          match = ht_pl(h, kFieldPlanes + (int)k, prev) == ht_pl(h, kFieldPlanes + (int)k, i);
+        for (uint32_t k = 0; k < n_keys && k < (uint32_t)K && match; k++) {
+          const uint32_t vx = ht_pl(h, kFieldPlanes + (int)k, i);
+          match = ht_pl(h, kFieldPlanes + (int)k, prev) == vx && !(vx & MTE_VALUE_UNEQUAL);  // NaN !== NaN
+        }
         app = (mp >> 8) == 0 && (mx >> 8) == 0 && !nl && (prev_len <= kTextGranularity || xl <= kTextGranularity) &&
               match && xl > 0;
       }

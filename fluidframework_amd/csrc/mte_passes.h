@@ -39,10 +39,12 @@ struct RoundArgs {
   unsigned long long* acct;
   uint32_t planes;
 };
-// the round phases fit a context whose per-wave column (the chunk rows:
-// nch_cap entries, mte_round.h rnd_resolve_kernel) fits this much LDS
+// the round phases fit a context whose per-wave column (nch_cap + ng_cap
+// entries, mte_round.h rnd_resolve_kernel) fits this much LDS
 constexpr uint32_t kRoundLdsMax = 150u * 1024u;
-inline uint64_t rnd_resolve_lds(uint32_t nch_cap) { return (uint64_t)nch_cap * 4u; }
+inline uint64_t rnd_resolve_lds(uint32_t nch_cap, uint32_t ng_cap) {
+  return (uint64_t)(nch_cap + (ng_cap + 63) / 64 * 64 + 64) * 4u;
+}
 
 // the tree pass over the legacy documents (mte_tree.h): `rounds` of TIER 0
 // (E <= 2) / TIER 1 (E = 4), then TIER 2 (E = 8, 16)

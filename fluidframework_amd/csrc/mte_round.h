@@ -283,102 +283,90 @@ __global__ __launch_bounds__(256) void rnd_gmove_kernel(ReplayArgs a, ChunkArgs 
 }
 
 // ---- resolve: one wave per client chain, the column as prefix sums -----------
-// The column is kept as two levels of inclusive prefix sums: CI[i] = chunk
-// i's prefix within its group of 64 chunks (in LDS, a row of 64 per group),
-// and the groups' prefixes over the whole document in registers (GR: lane l
-// of register j holds group j * 64 + l; kChMaxGroups <= 64 * kGR).  A position
-// resolves with kGR ballots over the registers, then one LDS read and one
-// ballot on the group's row; a change d to chunk i adds d to the later entries
-// of its row (one LDS write per lane, from the values the search read) and to
-// the later groups (one predicated add per register).  Round 4 held the group
-// level in LDS too, under a third (supergroup) level: three dependent LDS
-// round trips per op instead of one.
-constexpr int kGR = (int)((kChMaxGroups + kWave - 1) / kWave);  // group registers per lane
-
+// The column is kept in LDS as three levels of inclusive prefix sums over rows
+// of 64: CI[i] = chunk i's prefix within its group of 64 chunks, GS[g] = group
+// g's prefix within its supergroup of 64 groups, SS[s] = supergroup s's prefix
+// over the document.  A position resolves with one LDS read and one ballot
+// per level and no scan; a change d to chunk i adds d to the later entries of
+// the three rows it lies in (one LDS write per lane and level, from the values
+// the search just read).
 struct Col {
   int32_t* CI;  // nch_cap entries
-  int32_t GR[kGR];  // group prefixes over the document (0 past the last group)
+  int32_t* GS;  // ng_cap rounded up to 64
+  int32_t* SS;  // 64
   int nch;
-  int ng;
+  int ng, nsg;
 };
 
 struct ColHit {
-  int i, g;              // chunk, its group (i = nch: none)
-  int lc;                // lane of the chunk in its group row
+  int i, g, sg;          // chunk, its group and supergroup (i = nch: none)
+  int lc, lg;            // lane of the chunk in its group row, of the group in its supergroup row
   int32_t excl, csum;    // the chunk's exclusive prefix and length
   int32_t total;         // the column's total
-  int32_t ci;            // this lane's entry of the group's row, as read
+  int32_t ci, gs, ss;    // this lane's entries of the three rows, as read
 };
-
-// group prefix at a uniform group index g (g < ng)
-__device__ __forceinline__ int32_t col_gat(const Col& C, int g) {
-  return rdlane(pick<kGR>(C.GR, g / kWave), g % kWave);
-}
 
 // the first chunk whose inclusive prefix is > x (strict) or >= x
 __device__ __forceinline__ ColHit col_find(const Col& C, int32_t x, bool strict) {
   const int l = lane_id();
   ColHit h;
-  h.lc = 0;
-  h.ci = 0;
-  h.total = C.ng > 0 ? col_gat(C, C.ng - 1) : 0;
-  int g = -1;
-#pragma unroll
-  for (int j = 0; j < kGR; j++) {
-    const int gi = j * kWave + l;
-    const uint64_t m = __ballot(gi < C.ng && (strict ? C.GR[j] > x : C.GR[j] >= x));
-    if (g < 0 && m) g = j * kWave + (__ffsll((long long)m) - 1);
-  }
-  if (g < 0) {
+  h.g = h.sg = h.lc = h.lg = 0;
+  h.ci = h.gs = 0;
+  h.ss = l < C.nsg ? C.SS[l] : INT32_MAX / 2;
+  h.total = C.nsg > 0 ? rdlane(h.ss, C.nsg - 1) : 0;
+  const uint64_t ms = __ballot(l < C.nsg && (strict ? h.ss > x : h.ss >= x));
+  if (!ms) {
     h.i = C.nch;
-    h.g = C.ng;
     h.excl = h.total;
     h.csum = 0;
     return h;
   }
-  h.g = g;
-  const int32_t eg = g > 0 ? col_gat(C, g - 1) : 0;
-  const int ci = g * kChGroup + l;
+  h.sg = __ffsll((long long)ms) - 1;
+  const int32_t es = h.sg > 0 ? rdlane(h.ss, h.sg - 1) : 0;
+  const int gi = h.sg * kWave + l;
+  h.gs = gi < C.ng ? C.GS[gi] : INT32_MAX / 2;
+  const uint64_t mg = __ballot(gi < C.ng && (strict ? es + h.gs > x : es + h.gs >= x));
+  h.lg = mg ? __ffsll((long long)mg) - 1 : 0;
+  h.g = h.sg * kWave + h.lg;
+  const int32_t eg = es + (h.lg > 0 ? rdlane(h.gs, h.lg - 1) : 0);
+  const int ci = h.g * kChGroup + l;
   h.ci = ci < C.nch ? C.CI[ci] : INT32_MAX / 2;
   const uint64_t mc = __ballot(ci < C.nch && (strict ? eg + h.ci > x : eg + h.ci >= x));
   h.lc = mc ? __ffsll((long long)mc) - 1 : 0;
-  h.i = g * kChGroup + h.lc;
+  h.i = h.g * kChGroup + h.lc;
   const int32_t prev = h.lc > 0 ? rdlane(h.ci, h.lc - 1) : 0;
   h.excl = eg + prev;
   h.csum = rdlane(h.ci, h.lc) - prev;
   return h;
 }
 
-// the later groups (from group g on) changed by d
-__device__ __forceinline__ void col_groups_add(Col& C, int g, int32_t d) {
+// chunk h.i changed by d: the later entries of its three rows
+__device__ __forceinline__ void col_add(const Col& C, const ColHit& h, int32_t d) {
   const int l = lane_id();
-#pragma unroll
-  for (int j = 0; j < kGR; j++) C.GR[j] += (j * kWave + l >= g) ? d : 0;
-}
-
-// chunk h.i changed by d: the later entries of its row and the later groups
-__device__ __forceinline__ void col_add(Col& C, const ColHit& h, int32_t d) {
-  const int l = lane_id();
-  const int ci = h.g * kChGroup + l;
+  const int ci = h.g * kChGroup + l, gi = h.sg * kWave + l;
   if (l >= h.lc && ci < C.nch) C.CI[ci] = h.ci + d;
-  col_groups_add(C, h.g, d);
+  if (l >= h.lg && gi < C.ng) C.GS[gi] = h.gs + d;
+  if (l >= h.sg && l < C.nsg) C.SS[l] = h.ss + d;
 }
 
 // group gg's row changed by the per-lane amounts o (lane j: chunk gg * 64 + j):
-// CI of the row minus their running sum, the group's and later groups'
-// prefixes minus their total
-__device__ __forceinline__ void col_sub_row(Col& C, int gg, int32_t ci_row, int32_t o) {
+// CI of the row minus their running sum, the group's and later groups' GS /
+// SS minus their total
+__device__ __forceinline__ void col_sub_row(const Col& C, int gg, int32_t ci_row, int32_t o) {
   const int l = lane_id();
   const int32_t oi = wave_incl_scan(o);
   const int32_t og = rdlane(oi, kWave - 1);
   const int ci = gg * kChGroup + l;
   if (ci < C.nch) C.CI[ci] = ci_row - oi;
-  col_groups_add(C, gg, -og);
+  const int sg = gg / kWave, lg = gg % kWave;
+  const int gi = sg * kWave + l;
+  if (l >= lg && gi < C.ng) C.GS[gi] = C.GS[gi] - og;
+  if (l >= sg && l < C.nsg) C.SS[l] = C.SS[l] - og;
 }
 
 // WPB waves per workgroup, 8 / WPB workgroups per document; wave u = 0..7 of
 // the document takes the clients c = u, u + 8, ...; dynamic LDS: per wave a
-// CI column of nch_cap entries (rnd_resolve_lds)
+// CI column of nch_cap entries
 template <int WPB>
 __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
   extern __shared__ uint32_t rs_lds[];
@@ -394,7 +382,14 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
   Col C;
   C.nch = (int)rd.nch[doc];
   C.ng = (C.nch + kChGroup - 1) / kChGroup;
-  C.CI = reinterpret_cast<int32_t*>(rs_lds) + (uint64_t)w * ch.nch_cap;
+  C.nsg = (C.ng + kWave - 1) / kWave;
+  {
+    const uint32_t gs_cap = (ch.ng_cap + kWave - 1) / kWave * kWave;
+    int32_t* base = reinterpret_cast<int32_t*>(rs_lds) + (uint64_t)w * (ch.nch_cap + gs_cap + kWave);
+    C.CI = base;
+    C.GS = base + ch.nch_cap;
+    C.SS = base + ch.nch_cap + gs_cap;
+  }
   const int32_t* sum0 = reinterpret_cast<const int32_t*>(ch.kc + (uint64_t)doc * ch.nch_cap);
   uint4* list = rd.rlist + (uint64_t)doc * rd.rl_cap;
   // ops per client (every workgroup of the document counts them all)
@@ -412,19 +407,27 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
     const uint32_t cap_c = nc ? 2u * nc + 8u : 0u;
     if ((c % kChWaves) == u && nc) {
       // column c = the round-start column as prefix sums: the chunk rows, then
-      // the groups' prefixes over the document from the rows' totals
-      int32_t carry = 0;
-#pragma unroll
-      for (int j = 0; j < kGR; j++) C.GR[j] = 0;
+      // the group rows from the chunk rows' totals, then the supergroup row
       for (int g = 0; g < C.ng; g++) {
         const int i = g * kChGroup + l;
         const int32_t v = i < C.nch ? sum0[i] : 0;
         const int32_t incl = wave_incl_scan(v);
         if (i < C.nch) C.CI[i] = incl;
-        carry += rdlane(incl, kWave - 1);
-        // lane g % 64 of register g / 64 takes the running total
-#pragma unroll
-        for (int j = 0; j < kGR; j++) C.GR[j] = (j * kWave + l == g) ? carry : C.GR[j];
+        if (l == 0) C.GS[g] = rdlane(incl, kWave - 1);  // the group's total, for now
+      }
+      fence_wave();
+      for (int sg = 0; sg < C.nsg; sg++) {
+        const int g = sg * kWave + l;
+        const int32_t v = g < C.ng ? C.GS[g] : 0;
+        const int32_t incl = wave_incl_scan(v);
+        if (g < C.ng) C.GS[g] = incl;
+        if (l == 0) C.SS[sg] = rdlane(incl, kWave - 1);
+      }
+      fence_wave();
+      {
+        const int32_t v = l < C.nsg ? C.SS[l] : 0;
+        const int32_t incl = wave_incl_scan(v);
+        if (l < C.nsg) C.SS[l] = incl;
       }
       fence_wave();
       uint32_t m = 0;  // entries in the chain's list

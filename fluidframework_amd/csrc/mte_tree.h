@@ -443,7 +443,7 @@ __device__ __forceinline__ int scour(TReg<E, K>& X, int s, int e, int n, int32_t
       const uint32_t* rp = rc - W;
       bool match = (rp[0] & kScText) && (bits & kScText) && rp[2] == rc[2];
 #pragma unroll
-      for (int k = 0; k < K; k++) match = match && rp[3 + k] == rc[3 + k];
+      for (int k = 0; k < K; k++) match = match && rp[3 + k] == rc[3 + k] && !(rc[3 + k] & MTE_VALUE_UNEQUAL);
       bits |= match ? kScMatch : 0u;
     }
   }

@@ -40,6 +40,14 @@ class EngineBase:
 
     n_keys = 0
     n_docs = 0
+    ref_capacity = 1024  # mte_set_ref_capacity's default (include/mte.h)
+
+    def doc_clients(self, observer_id, min_seq=0, local=False):
+        """A document's client map (packing.DocClients) that knows this
+        engine's per-document reference capacity (set_ref_capacity), as the Node
+        host's BatchClient copies engine.refCapacity."""
+        from .packing import DocClients
+        return DocClients(observer_id, min_seq, local, ref_cap=self.ref_capacity)
 
     def _check(self, rc, what=""):
         if rc != 0:
@@ -239,6 +247,7 @@ class DeviceEngine(EngineBase):
 
     def set_ref_capacity(self, per_doc):
         self._check(self.lib.mte_set_ref_capacity(self.ctx, per_doc), "set_ref_capacity")
+        self.ref_capacity = int(per_doc)
 
     def _read_refs(self, doc, p, n, transient=False):
         f = self.lib.mte_read_refs_transient if transient else self.lib.mte_read_refs

@@ -1029,7 +1029,9 @@ function segJson(sg) {
   return sg.props ? { marker: { refType: sg.kind - 1 }, props: sg.props } : { marker: { refType: sg.kind - 1 } };
 }
 
-function sameProps(a, b) { // matchProperties (properties.ts:33-42): empty == undefined
+function sameProps(a, b) { // matchProperties (properties.ts:66-100) as the summary writers use it: empty == undefined
+  // NaN !== NaN: a segment holding one never coalesces (canonicalJson writes it as null)
+  for (const k in b || {}) if (typeof b[k] === "number" && b[k] !== b[k]) return false;
   return packing.canonicalJson(a || {}) === packing.canonicalJson(b || {});
 }
 

@@ -39,6 +39,8 @@ const DELTA_REGEN = 0x10;    // MTE_DELTA_REGEN: kind flag of a regenerated op's
 const ANNOTATE_SLOTS = 32;   // MTE_ANNOTATE_SLOTS: pending local annotate groups tracked per document
 const F_MARKER = 0x1, F_MSG_END = 0x2, F_REWRITE = 0x4, F_LOCAL = 0x8;
 const F_COMBINE = 0x10, COMBINE_PAIR = 0x80000000;  // incr / consensus value maps (include/mte.h)
+// a value id matching no other, itself included: NaN (matchProperties' !==, include/mte.h)
+const VALUE_UNEQUAL = 0x40000000;
 const LOCAL_SEQ_BASE = 0x40000000; // MTE_LOCAL_SEQ_BASE
 const NO_PROPS = 0xffffffff;
 const MAX_CLIENTS = 32;
@@ -93,12 +95,14 @@ class Interner {
   /** [key, value id] of one property, noting the value under its key */
   kv(name, v) {
     const k = this.key(name), id = this.value(v);
-    if (id) {
-      let set = this.keyVals.get(k);
-      if (set === undefined) this.keyVals.set(k, (set = new Set()));
-      set.add(id);
-    }
+    if (id) this.noteValue(k, id);
     return [k, id];
+  }
+  /** value id `id` was given to key `k` (the combining ops' domain) */
+  noteValue(k, id) {
+    let set = this.keyVals.get(k);
+    if (set === undefined) this.keyVals.set(k, (set = new Set()));
+    set.add(id);
   }
   key(name) {
     let k = this.keys.get(name);
@@ -121,11 +125,13 @@ class Interner {
       const id = prim.get(v);
       if (id !== undefined) return id;
     }
-    // NaN (an incr's result) is a value of its own, not JSON's null
-    const cj = typeof v === "number" && v !== v ? "NaN" : canonicalJson(v);
+    // NaN (an incr's result) is a value of its own, not JSON's null, and
+    // matches nothing (VALUE_UNEQUAL)
+    const nan = typeof v === "number" && v !== v;
+    const cj = nan ? "NaN" : canonicalJson(v);
     let i = this.values.get(cj);
     if (i === undefined) {
-      i = this.valueJson.length;
+      i = this.valueJson.length | (nan ? VALUE_UNEQUAL : 0);
       this.values.set(cj, i);
       this.valueJson.push(cj);
     }
@@ -136,11 +142,15 @@ class Interner {
   valueOfJson(cj) {
     let i = this.values.get(cj);
     if (i === undefined) {
-      i = this.valueJson.length;
+      i = this.valueJson.length | (cj === "NaN" ? VALUE_UNEQUAL : 0);
       this.values.set(cj, i);
       this.valueJson.push(cj);
     }
     return i;
+  }
+  /** canonical JSON of a value id */
+  jsonOf(id) {
+    return this.valueJson[id & ~VALUE_UNEQUAL];
   }
   /** plane values of one segment -> PropertySet (undefined when empty) */
   decode(planes) {
@@ -148,7 +158,7 @@ class Interner {
     for (let k = 0; k < planes.length; k++) {
       if (planes[k]) {
         if (out === undefined) out = {};
-        const cj = this.valueJson[planes[k]];
+        const cj = this.jsonOf(planes[k]);
         out[this.keyNames[k]] = cj === "NaN" ? NaN : JSON.parse(cj);
       }
     }
@@ -243,9 +253,12 @@ class PropTable {
       throw new MergeTreeError(E_INVALID_ARG, "props must be an object");
     }
     const first = this.entries.length / 2;
-    for (const name of Object.keys(props)) {
-      const [k, id] = this.interner.kv(name, props[name]);
-      this.entries.push(k, id);
+    const it = this.interner, E = this.entries;
+    for (const name in props) {
+      if (!Object.prototype.hasOwnProperty.call(props, name)) continue;
+      const k = it.key(name), id = it.value(props[name]);
+      if (id) it.noteValue(k, id);
+      E.push(k, id);
     }
     this.sets.push(first, this.entries.length / 2 - first);
     return this.sets.length / 2 - 1;
@@ -265,7 +278,7 @@ class PropTable {
       dom.push(0);
       const pairs = [];
       for (const old of dom) {
-        const cj = it.valueJson[old];
+        const cj = it.jsonOf(old);
         const cur = old === 0 ? undefined : (cj === "NaN" ? NaN : JSON.parse(cj));
         const nv = combineValue(comb, cur, seq);
         const nid = nv === undefined ? 0 : it.value(nv);
@@ -442,15 +455,15 @@ class BatchBuilder {
         }
         this._put(doc, seq, ref, msn, OP_ACK, 0, 0, lo, hi, mask, NO_PROPS);
       } else {
+        this._combLocal = clients.local;
         try {
-          this._combLocal = clients.local;
           this._opPut(doc, seq, ref, msn, msg.contents, this._src(doc));
         } catch (e) {
+          this._combLocal = false;
           this._truncate(k0);
           throw e;
-        } finally {
-          this._combLocal = false;
         }
+        this._combLocal = false;
       }
     }
     // the slot is taken only once the message has validated
@@ -825,6 +838,8 @@ class BatchBuilder {
    *  MTE_OP_RELPOS record the engine resolves (posFromRelativePos,
    *  mergeTree.ts:1369-1392), or null (as packing.py _relpos) */
   _relpos(op, t) {
+    // the plain-op fast path: no relative position, nothing allocated
+    if (op.relativePos1 === undefined && op.relativePos2 === undefined) return null;
     let flags = 0;
     const vids = [0, 0], offs = [0, 0];
     const spec = [["pos1", "relativePos1", RP_POS1, RP_BEFORE1], ["pos2", "relativePos2", RP_POS2, RP_BEFORE2]];

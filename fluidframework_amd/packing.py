@@ -30,7 +30,7 @@ import json
 
 import numpy as np
 
-from .abi import (COMBINE_PAIR, F_COMBINE, F_LOCAL, F_MARKER, F_MSG_END, F_REWRITE, LOCAL_SEQ_BASE, MTE_E_CAPACITY, MTE_E_CLIENT_RANGE,
+from .abi import (COMBINE_PAIR, MTE_VALUE_UNEQUAL, F_COMBINE, F_LOCAL, F_MARKER, F_MSG_END, F_REWRITE, LOCAL_SEQ_BASE, MTE_E_CAPACITY, MTE_E_CLIENT_RANGE,
                   MTE_E_INVALID_ARG, MTE_E_STATE, MTE_E_UNSUPPORTED, MTE_MAX_CLIENTS, NO_PROPS, OP_ACK, OP_ROLLBACK,
                   OP_REGEN, OP_RBKEY, OP_REF, OP_RELPOS, RP_BEFORE1, RP_BEFORE2, RP_POS1, RP_POS2,
                   ANNOTATE_SLOTS, REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE,
@@ -92,15 +92,21 @@ class Interner:
         i = self.values.get(cj)
         if i is None:
             i = len(self.value_json)
+            if cj == "NaN":  # matchProperties: NaN !== NaN (include/mte.h MTE_VALUE_UNEQUAL)
+                i |= MTE_VALUE_UNEQUAL
             self.values[cj] = i
             self.value_json.append(cj)
         return i
+
+    def json_of(self, vid: int) -> str:
+        """canonical JSON of a value id"""
+        return self.value_json[vid & ~MTE_VALUE_UNEQUAL]
 
     def decode_props(self, planes) -> dict:
         out = {}
         for k, vid in enumerate(planes):
             if vid:
-                out[self.key_names[k]] = json.loads(self.value_json[vid])
+                out[self.key_names[k]] = json.loads(self.json_of(int(vid)))
         return out
 
 
@@ -138,7 +144,7 @@ class PropTable:
             dom = sorted(it.key_vals.get(k, ())) + [0]
             pairs = []
             for old in dom:
-                cur = _ABSENT if old == 0 else json.loads(it.value_json[old])
+                cur = _ABSENT if old == 0 else json.loads(it.json_of(old))
                 new = combine_value(comb, cur, seq)
                 nid = 0 if new is _ABSENT else it.value(new)
                 if nid != old:
@@ -162,13 +168,32 @@ _NAN = float("nan")
 
 
 def _js_num(x) -> str:
-    """Number.prototype.toString for the values JSON brings (integers and
-    short decimals; JS's exponent forms are not restated)."""
+    """Number.prototype.toString (ECMA-262 Number::toString, radix 10): the
+    shortest round-trip digits (Python's repr finds the same ones), written
+    plain when the decimal exponent n is in (-6, 21], else as d.ddde+-n-1."""
+    import decimal
     if x != x:
         return "NaN"
-    if float(x).is_integer() and abs(x) < 1e21:
-        return str(int(x))
-    return repr(float(x))
+    x = float(x)
+    if x in (float("inf"), float("-inf")):
+        return "Infinity" if x > 0 else "-Infinity"
+    if x == 0:
+        return "0"
+    if x < 0:
+        return "-" + _js_num(-x)
+    t = decimal.Decimal(repr(x)).normalize().as_tuple()
+    digits = "".join(str(d) for d in t.digits)
+    k = len(digits)
+    n = k + t.exponent  # x = 0.digits x 10^n
+    if k <= n <= 21:
+        return digits + "0" * (n - k)
+    if 0 < n <= 21:
+        return digits[:n] + "." + digits[n:]
+    if -6 < n <= 0:
+        return "0." + "0" * (-n) + digits
+    e = n - 1
+    sign = "+" if e >= 0 else "-"
+    return (digits if k == 1 else digits[0] + "." + digits[1:]) + "e" + sign + str(abs(e))
 
 
 def _js_str(v) -> str:
@@ -258,7 +283,7 @@ class DocClients:
 
     NEVER = I32_MAX  # slot held for good (observer, ids registered without a seq)
 
-    def __init__(self, observer_id: str, min_seq: int = 0, local: bool = False):
+    def __init__(self, observer_id: str, min_seq: int = 0, local: bool = False, ref_cap: int = DEFAULT_REF_CAPACITY):
         self.observer = observer_id
         self.ids = {observer_id: 0}
         self.last = {0: self.NEVER}  # slot -> highest seq its client used
@@ -285,8 +310,9 @@ class DocClients:
         self.ref_free = []
         # the context's reference slots per document (mte_set_ref_capacity); a slot
         # at or past it would fail the whole batch at mte_submit, so the packer
-        # refuses the reference for this document alone
-        self.ref_cap = DEFAULT_REF_CAPACITY
+        # refuses the reference for this document alone (EngineBase.doc_clients
+        # passes the engine's capacity)
+        self.ref_cap = ref_cap
 
     def short(self, long_id, seq=None) -> int:
         i = self.ids.get(long_id)

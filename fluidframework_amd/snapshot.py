@@ -34,7 +34,7 @@ import json
 
 import numpy as np
 
-from .abi import DOC_INIT_DTYPE, NOT_REMOVED, PROP_DTYPE, PROPSET_DTYPE, SEG_DTYPE
+from .abi import DOC_INIT_DTYPE, MTE_VALUE_UNEQUAL, NOT_REMOVED, PROP_DTYPE, PROPSET_DTYPE, SEG_DTYPE
 from .packing import units_to_str, utf16_units
 
 TEXT_SEGMENT_GRANULARITY = 256  # textSegment.ts (TextSegmentGranularity)
@@ -45,6 +45,11 @@ def _can_append(prev, seg):
     # TextSegment.canAppend (textSegment.ts:72-77); markers never append
     return (prev["kind"] == 0 and seg["kind"] == 0 and (not prev["text"] or prev["text"][-1] != NEWLINE)
             and (len(prev["text"]) <= TEXT_SEGMENT_GRANULARITY or len(seg["text"]) <= TEXT_SEGMENT_GRANULARITY))
+
+
+def _match(prev, cur):
+    # matchProperties (properties.ts:66-100) on interned ids: NaN never matches
+    return prev["props"] == cur["props"] and not any(v & MTE_VALUE_UNEQUAL for v in cur["props"])
 
 
 def _json(seg):
@@ -71,7 +76,7 @@ def write_body(engine, doc, min_seq, first_remover=None):
         if int(s["seq"]) <= min_seq and not removed:
             if prev is None:
                 prev = cur
-            elif _can_append(prev, cur) and prev["props"] == cur["props"]:
+            elif _can_append(prev, cur) and _match(prev, cur):
                 prev = {"kind": 0, "props": prev["props"], "text": prev["text"] + cur["text"]}
             else:
                 out.append({"json": _json(prev)})
@@ -262,7 +267,7 @@ def to_json(spec, interner, client_name=str):
         return out
     if isinstance(spec, list):
         return units_to_str(spec)
-    props = {interner.key_names[k]: json.loads(interner.value_json[v]) for k, v in spec.get("props", {}).items()}
+    props = {interner.key_names[k]: json.loads(interner.json_of(v)) for k, v in spec.get("props", {}).items()}
     base = {"text": units_to_str(spec["text"])} if "text" in spec else {"marker": spec["marker"]}
     if props:
         base["props"] = props
@@ -319,7 +324,7 @@ def extract_legacy(engine, doc, min_seq):
         cur = {"kind": int(s["kind"]), "props": tuple(int(x) for x in props[i]),
                "text": text[int(s["text_off"]): int(s["text_off"]) + int(s["len"])].tolist()
                if int(s["kind"]) == 0 else None}
-        if prev is not None and _can_append(prev, cur) and prev["props"] == cur["props"]:
+        if prev is not None and _can_append(prev, cur) and _match(prev, cur):
             prev = {"kind": 0, "props": prev["props"], "text": prev["text"] + cur["text"]}
         else:
             if prev is not None:

@@ -228,6 +228,14 @@ extern "C" {
  * (the HBM tree pass) and never MTE_F_LOCAL: MTE_E_UNSUPPORTED otherwise.  */
 #define MTE_F_COMBINE 0x0010u
 #define MTE_COMBINE_PAIR 0x80000000u
+/* A property value id with this bit set never matches another value id, itself
+ * included: matchProperties compares values with !== (properties.ts:66-100), so
+ * two segments holding NaN (an incr's result on a number or absent value,
+ * properties.ts:24-40) never append-merge in the zamboni (mergeTree.ts:712) or
+ * coalesce in a summary (snapshotV1.ts:215, snapshotlegacy.ts:170).  Hosts
+ * intern NaN under such an id (id & ~MTE_VALUE_UNEQUAL indexes their value
+ * tables as usual). */
+#define MTE_VALUE_UNEQUAL 0x40000000u
 /* A local op of the document's own client (client 0), not yet sequenced:
  * insertSegmentLocal / removeRangeLocal / annotateRangeLocal (client.ts:131-229)
  * -> insertSegments / markRangeRemoved / annotateRange with seq =

@@ -161,7 +161,9 @@ class OracleEngine(EngineBase):
         """The restatement's event buffers grow as needed (mte_set_event_capacity's bound is the engine's)."""
 
     def set_ref_capacity(self, per_doc):
-        """The restatement's reference slots grow as needed."""
+        """The restatement's reference slots grow as needed; the capacity is
+        kept for the packers (EngineBase.doc_clients)."""
+        self.ref_capacity = int(per_doc)
 
     def _read_refs(self, doc, p, n, transient=False):
         pre = "oti" if self.tree == "items" else "orc"
@@ -293,6 +295,7 @@ class SpecOracle:
 
     def set_ref_capacity(self, per_doc):
         """The restatements' reference slots grow as needed."""
+        self.ref_capacity = int(per_doc)
 
     def stats(self):
         zero = {"ops_applied": 0, "segs_scanned": 0, "segs_written": 0, "prop_writes": 0, "units_inserted": 0,

@@ -405,7 +405,8 @@ static int scour(idoc* d, uint32_t s, uint32_t e, const uint16_t* arena, uint32_
         const item* pl = &d->it[prev_end - 1]; /* the last text of the leaf appended to */
         const int nl = pl->len > 0 && arena[pl->toff + (uint32_t)pl->len - 1] == (uint16_t)'\n';
         int match = p->po == x->po;
-        for (uint32_t k = 0; k < n_keys && match; k++) match = p->props[k] == x->props[k];
+        for (uint32_t k = 0; k < n_keys && match; k++)
+          match = p->props[k] == x->props[k] && !(x->props[k] & MTE_VALUE_UNEQUAL); /* NaN !== NaN */
         app = p->kind == 0 && x->kind == 0 && !nl && (prev_len <= TEXT_GRANULARITY || xl <= TEXT_GRANULARITY) &&
               match && xl > 0;
       }

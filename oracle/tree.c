@@ -384,7 +384,7 @@ static int nv_push(nodevec* h, tnode* x) {
 static int match_props(const tnode* a, const tnode* b, uint32_t n_keys) {
   if (a->po != b->po) return 0;
   for (uint32_t k = 0; k < n_keys; k++)
-    if (a->props[k] != b->props[k]) return 0;
+    if (a->props[k] != b->props[k] || (a->props[k] & MTE_VALUE_UNEQUAL)) return 0; /* NaN !== NaN */
   return 1;
 }
 

@@ -218,3 +218,22 @@ def test_gpu_combine_farms():
     passed, failures = replay_ref_farm(device_factory, sets, observers_local=True)
     assert not failures, failures[:2]
     assert passed == _n_checkpoints(sets)
+
+
+def test_js_number_strings_match_node():
+    """an incr on an array holding small or large numbers interns
+    String(v) + "undefined"; Python's restatement of Number::toString (the
+    exponent forms included) equals Node's own, so both packers intern the
+    same value."""
+    import shutil
+    import subprocess
+    from fluidframework_amd.packing import _js_num
+    xs = [1e-7, 1.5e-7, 1e-5, 1e-4, 1e16, 1e21, 1e22, 123.456, 5, -2.5e-10, 1.7976931348623157e308,
+          0.1 + 0.2, 100, 2 ** 53 + 2, -0.5, 3e-300]
+    assert combine_value({"name": "incr"}, [1e-7, 1e-5, 2], 9) == "1e-7,0.00001,2undefined"
+    node = shutil.which("node")
+    if node is None:
+        pytest.skip("node not installed")
+    out = subprocess.run([node, "-e", "process.stdout.write(JSON.stringify(%s.map(String)))" % json.dumps(xs)],
+                         capture_output=True, text=True, check=True).stdout
+    assert [_js_num(x) for x in xs] == json.loads(out)

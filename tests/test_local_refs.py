@@ -258,3 +258,27 @@ def test_oracle_rejects_refs_outside_refs_docs():
     bb.add_ref(0, cl, 1)
     with pytest.raises(MergeTreeError):
         e.apply_batch(bb.build())
+
+
+def test_engine_ref_capacity_reaches_the_packer():
+    """set_ref_capacity is what the document's client map checks
+    (EngineBase.doc_clients), below and above the default of 1,024."""
+    e = oracle_factory(0)
+    for cap in (5, 4096):
+        e.set_ref_capacity(cap)
+        cl = e.doc_clients("B", local=True)
+        assert cl.ref_cap == cap
+        bb = BatchBuilder(1, Interner(0))
+        for i in range(cap):
+            assert bb.add_ref(0, cl, 0) == i
+        with pytest.raises(MergeTreeError) as ei:
+            bb.add_ref(0, cl, 0)
+        assert ei.value.code == MTE_E_CAPACITY
+
+
+@pytest.mark.gpu
+def test_gpu_engine_ref_capacity_reaches_the_packer():
+    from fluidframework_amd.engine import DeviceEngine
+    e = DeviceEngine(0)
+    e.set_ref_capacity(7)
+    assert e.doc_clients("B", local=True).ref_cap == 7

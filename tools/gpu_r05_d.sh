@@ -2,7 +2,7 @@
 # round 5: round phases with the register group level + tile-parallel digest
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r05d
+O=gpurun_out/${OUT:-r05d}
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_chunk.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/chunk_tests.log 2>&1 || exit 1
 P="python3 bench.py --no-cpu-baseline --no-tree-leg --no-node-leg --no-local-leg"
