@@ -88,9 +88,20 @@ def library_build():
     from fluidframework_amd import _native
     p = _native.lib_path("libmte.so")
     st = os.stat(p)
+    # the library reports the digest of the sources it was compiled from
+    # (mte_build_info, include/mte.h); the same digest of the sources beside it
+    csrc = os.path.join(ROOT, "fluidframework_amd", "csrc")
+    names = sorted(f for f in os.listdir(csrc) if f.startswith("mte_") and f.endswith((".h", ".hip")))
+    h = hashlib.sha256()
+    for f in names + [os.path.join("..", "..", "include", "mte.h")]:
+        h.update(open(os.path.join(csrc, f), "rb").read())
+    info = _native.load_mte().mte_build_info().decode()
+    src = info.split()[0].split("=", 1)[1]
     return {"libmte_sha256": hashlib.sha256(open(p, "rb").read()).hexdigest(),
             "libmte_mtime_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(st.st_mtime)),
-            "libmte_path": os.path.relpath(p, ROOT)}
+            "libmte_path": os.path.relpath(p, ROOT),
+            "build_info": info, "sources_sha16": h.hexdigest()[:16],
+            "built_from_these_sources": src == h.hexdigest()[:16]}
 
 
 REF_BASELINE_JSON = os.path.join(ROOT, "profiles", "r02", "ref_cpu_baseline.json")

@@ -36,6 +36,7 @@ def load_mte():
     sig = {
         "mte_abi_version": ([], C.c_int),
         "mte_strerror": ([C.c_int], C.c_char_p),
+        "mte_build_info": ([], C.c_char_p),
         "mte_create": ([vp, vp], C.c_int),
         "mte_destroy": ([vp], C.c_int),
         "mte_last_error": ([vp], C.c_char_p),

@@ -122,7 +122,7 @@ class MteDocView(C.Structure):
 
 # Every symbol include/mte.h declares (tests check libmte.so exports them all).
 EXPORTED_SYMBOLS = [
-    "mte_abi_version", "mte_strerror", "mte_create", "mte_destroy", "mte_last_error",
+    "mte_abi_version", "mte_strerror", "mte_build_info", "mte_create", "mte_destroy", "mte_last_error",
     "mte_load_docs", "mte_load_segments", "mte_submit", "mte_run", "mte_sync", "mte_reset", "mte_digest",
     "mte_digest_device", "mte_read_doc", "mte_read_segments", "mte_doc_status", "mte_stats_get", "mte_set_stats",
     "mte_comm_unique_id", "mte_comm_init", "mte_comm_share", "mte_comm_barrier", "mte_comm_allreduce_f64",

@@ -1133,6 +1133,7 @@ extern "C" {
 
 int mte_abi_version(void) { return MTE_ABI_VERSION; }
 
+
 const char* mte_strerror(int code) {
   switch (code) {
     case MTE_OK: return "ok";

@@ -411,6 +411,12 @@ typedef struct mte_doc_view {
 
 int mte_abi_version(void);
 const char* mte_strerror(int code);
+/* Build provenance of this library (no reference counterpart): "src=<first 16
+ * hex digits of the sha256 of the engine sources it was compiled from
+ * (fluidframework_amd/csrc/mte_*.h, mte_*.hip, then include/mte.h, in name
+ * order)> arch=gfx950 compiler=<the HIP compiler's version string>", so a host
+ * can check that the library it loaded was built from the sources beside it. */
+const char* mte_build_info(void);
 
 int mte_create(const mte_config* cfg, mte_ctx** out);
 int mte_destroy(mte_ctx* ctx);

@@ -14,7 +14,7 @@ for spec in "$@"; do
   ( /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $flags -c \
       -o build_var/$name/flat.o fluidframework_amd/csrc/mte_pass_flat.hip &&
     /opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o build_var/$name/libmte.so \
-      $OBJ/mte_engine.o $OBJ/mte_pass_tree.o $OBJ/mte_pass_htree.o build_var/$name/flat.o $OBJ/mte_pass_chunk.o \
+      $OBJ/mte_engine.o $OBJ/mte_pass_tree.o $OBJ/mte_pass_htree.o build_var/$name/flat.o $OBJ/mte_pass_chunk.o $OBJ/mte_build.o \
       -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib ) &
 done
 wait
