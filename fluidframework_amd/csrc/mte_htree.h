@@ -1177,7 +1177,7 @@ __device__ __forceinline__ int ht_range(HT& h, const s8v& op, bool local, const 
     MTE_STAT(st[kStPwrites] += cnt_all * w;)
   }
   h.lp_n = 0;  // the marks changed lengths
-  if (rem && !local && rt && rhi) stream_slide(h.pl, h.sd, h.n, rt, rhi, s);
+  if (rem && !local && rt && rhi) stream_slide(h.pl, h.sd, h.n, rt, rhi, s, evd ? &ev : nullptr);
   return 0;
 }
 
@@ -1188,7 +1188,7 @@ __device__ __forceinline__ int ht_range(HT& h, const s8v& op, bool local, const 
 // references of the acked removals, adds each segment to the LRU set and runs
 // zamboniSegments
 template <int K>
-__device__ __forceinline__ int ht_ack(HT& h, const s8v& op, const ReplayArgs& a, uint2* rt, uint32_t rhi) {
+__device__ __forceinline__ int ht_ack(HT& h, const s8v& op, const ReplayArgs& a, uint2* rt, uint32_t rhi, EvOut* ev) {
   const int32_t lo = op[4], hi = op[5], s = op[0];
   const uint32_t mask = (uint32_t)op[6];
   const int l = lane_id();
@@ -1241,7 +1241,7 @@ __device__ __forceinline__ int ht_ack(HT& h, const s8v& op, const ReplayArgs& a,
         }
       }
     }
-    if (rt && rhi) stream_slide(h.pl, h.sd, h.n, rt, rhi, s);
+    if (rt && rhi) stream_slide(h.pl, h.sd, h.n, rt, rhi, s, ev);
     if ((rc = ht_zamboni<K>(h, a.n_keys))) return rc;
   }
   return 0;
@@ -1810,6 +1810,39 @@ __device__ __forceinline__ int ht_ref_rebase(HT& h, const s8v& op, int32_t lseq,
   return 0;
 }
 
+// The MTE_DELTA_SLIDE records of one message, [from, ev.n): the unit each
+// reference left -> that unit's order key after the message (its zambonis
+// included): the held units before it, as mte_read_ref_order counts them, -1
+// if it is gone (titems.c slide_keys).  One wave-wide search per record.
+__device__ __noinline__ void ht_slide_keys(const HT& h, EvOut& ev, uint32_t from) {
+  const uint32_t to = ev.n < ev.cap ? ev.n : (uint32_t)ev.cap;
+  if (from >= to) return;
+  vm_drain();  // this wave's record stores are visible to its loads
+  const int l = lane_id();
+  for (uint32_t q = from; q < to; q++) {
+    const uint32_t kind = uni(ld_l2(&ev.p[q].kind));
+    if ((kind & 0xc0u) != MTE_DELTA_SLIDE) continue;
+    const uint32_t u = uni(ld_l2(reinterpret_cast<const uint32_t*>(&ev.p[q].len)));
+    int32_t key = -1, carry = 0;
+    for (int tb = 0; tb < h.n; tb += kWave) {
+      const int i = tb + l;
+      const int ic = i < h.n ? i : 0;  // unconditional loads, selected after
+      const uint32_t ln = ld_l2(h.pl + ic), tf = ld_l2(h.pl + 5 * h.sd + ic);
+      const int32_t L = i < h.n ? (int32_t)ln : 0;
+      const int32_t incl = wave_incl_scan(L);
+      const uint64_t m = __ballot(i < h.n && u - tf < ln);
+      if (m) {
+        const int j = __ffsll((long long)m) - 1;
+        key = carry + rdlane(incl - L + (int32_t)(u - tf), j);
+        break;
+      }
+      carry += rdlane(incl, kWave - 1);
+    }
+    if (l == 0) ev.p[q].len = key;
+  }
+  vm_drain();
+}
+
 template <int K, bool S>
 __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStats], const ReplayArgs& a, int32_t& lseq, EvOut& ev,
                        uint32_t& rhi) {
@@ -1827,6 +1860,7 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
   const bool refd = (D.flags & MTE_DOC_REFS) != 0 && a.refs != nullptr;
   uint2* const rt = refd ? a.refs + (uint64_t)D.doc * a.ref_cap : nullptr;
   ev.op = D.k;
+  const uint32_t ev_from = ev.n;  // this record's first event
   if (h.n + 4 > h.cap) return MTE_E_CAPACITY;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
   const int32_t s = op[0], msn = op[2];
@@ -1959,7 +1993,7 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
   } else if (type == MTE_OP_ACK) {
     if (!(op[4] > 0 && op[4] <= op[5] && op[5] <= lseq)) return MTE_E_INVALID_ARG;
     HPROF_BEGIN(t0)
-    rc = ht_ack<K>(h, op, a, rt, refd ? rhi : 0u);
+    rc = ht_ack<K>(h, op, a, rt, refd ? rhi : 0u, evd ? &ev : nullptr);
     HPROF_END(h, 2, t0)
     if (rc) return rc;
   } else if (type != MTE_OP_NOOP) {
@@ -1986,6 +2020,8 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
       if ((rc = ht_zamboni<K>(h, a.n_keys))) return rc;
     }
   }
+  // the slides of this record, keyed by the units they left as they stand now
+  if (evd && rt && ev.n > ev_from) ht_slide_keys(h, ev, ev_from);
   return 0;
 }
 

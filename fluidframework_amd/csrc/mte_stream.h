@@ -156,7 +156,19 @@ __device__ __forceinline__ int find_slide_target(const uint32_t* pl, uint64_t sd
 // the last preceding one (addAfterTombstones), else come off the segment's list
 // (kRefOff); Simple references detach, or come off the list when there is no
 // segment to slide to (localReference.ts:422-485).  Slots [0, rhi) of the table rt.
-__device__ __forceinline__ void stream_slide(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t rhi, int32_t s) {
+// ev (MTE_DOC_EVENTS documents): one MTE_DELTA_SLIDE record per reference that
+// slid or came off its segment -- the reference calls its beforeSlide /
+// afterSlide callbacks there (mergeTree.ts:936-942, localReference.ts:436-447,
+// 471-480), which an interval collection turns into "changeInterval" events
+// mid-op (intervalCollection.ts:1042-1053): pos = the own-view position of the
+// removed segment it sat on, len = the unit it left (mte_htree.h
+// ht_slide_keys makes it the unit's order key), removed = its slot,
+// kind = MTE_DELTA_SLIDE | 1 if
+// it moved to a segment | its offset in the removed segment << 16 (clamped):
+// the host orders one segment's references as its LocalReferenceCollection
+// iterates them.
+__device__ __forceinline__ void stream_slide(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t rhi, int32_t s,
+                                             EvOut* ev = nullptr) {
   const int l = lane_id();
   for (int tb = 0; tb < n; tb += kWave) {
     const int i = tb + l;
@@ -177,13 +189,26 @@ __device__ __forceinline__ void stream_slide(const uint32_t* pl, uint64_t sd, in
         const uint32_t tt = uni(ld_l2(pl + 5 * sd + t)), tl = uni(ld_l2(pl + t));
         to = after ? tt + tl - 1u : tt;
       }
+      const int32_t xpos = ev ? own_prefix(pl, sd, x) : 0;
       for (uint32_t rb = 0; rb < rhi; rb += kWave) {
         const uint32_t r = rb + (uint32_t)l;
         const uint32_t rc = r < rhi ? r : 0u;  // unconditional loads, selected after
         const uint32_t anc = ld_l2(&rt[rc].x), st = ld_l2(&rt[rc].y);
-        if (r < rhi && (st & kRefLive) && !(st & (kRefDetached | MTE_REF_STAY_ON_REMOVE)) && anc - toff < len) {
-          if ((st & MTE_REF_SLIDE_ON_REMOVE) && t >= 0) rt[r].x = to;
+        const bool hit = r < rhi && (st & kRefLive) && !(st & (kRefDetached | MTE_REF_STAY_ON_REMOVE)) && anc - toff < len;
+        const bool moves = (st & MTE_REF_SLIDE_ON_REMOVE) && t >= 0;
+        if (hit) {
+          if (moves) rt[r].x = to;
           else rt[r].y = st | kRefDetached | (t < 0 ? kRefOff : 0u);
+        }
+        if (ev) {
+          const uint64_t hm = __ballot(hit);
+          if (hm) {
+            const uint32_t idx = ev->n + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+            const uint32_t off = anc - toff < 0xffffu ? anc - toff : 0xffffu;
+            if (hit && idx < ev->cap)
+              ev->p[idx] = mte_delta{ev->op, MTE_DELTA_SLIDE | (moves ? 1u : 0u) | (off << 16), xpos, (int32_t)anc, r};
+            ev->n += (uint32_t)__popcll(hm);
+          }
         }
       }
       vm_drain();

@@ -49,6 +49,7 @@ function loadAddon() {
 // MTE_E_* -> the reference assert code with the same meaning (client.ts:525-528,
 // 940-943; mergeTree.ts:1078-1084, 1666-1672)
 const ASSERT_CODES = { "-5": 0x030, "-6": 0x031, "-7": 0x039 };
+const DELTA_SLIDE = 0x40;  // MTE_DELTA_SLIDE (include/mte.h): a reference slid off a removed segment
 
 function docError(code, doc) {
   const a = loadAddon();
@@ -395,12 +396,14 @@ class MergeTreeEngine {
 
 /** A local reference (LocalReferencePosition, localReference.ts:44-118): its
  *  engine slot, ReferenceType and properties. */
+let refCreated = 0;  // creation order of references (a segment's list order at one offset)
 class LocalReferencePosition {
   constructor(client, slot, refType, properties) {
     this.client = client;
     this.slot = slot;
     this.refType = refType;
     this.properties = properties;
+    this.created = ++refCreated;
   }
   addProperties(newProps) {
     this.properties = Object.assign({}, this.properties || {}, newProps);
@@ -455,6 +458,24 @@ class BatchClient {
     }
     this.engine._batch().addMessage(this.doc, this.clients, msg);
     if (msg.minimumSequenceNumber > this.lastMinSeq) this.lastMinSeq = msg.minimumSequenceNumber;
+    // an interval collection's ends slide inside merge-tree ops (a remote
+    // remove, the ack of our own): the reference raises "changeInterval"
+    // there, mid-op (intervalCollection.ts:1042-1053), with the document as it
+    // is at that moment -- so a document whose collections hold intervals
+    // replays message by message and its slides come back as MTE_DELTA_SLIDE
+    // records (_deliver -> IntervalCollection._onSlides)
+    if (this._slideSync()) {
+      this.engine.flush();
+      this.engine.sync();
+    }
+  }
+
+  /** The document's collections hold intervals whose ends can slide, and its
+   *  slides are reported ({events: true}). */
+  _slideSync() {
+    if (!this.intervalCollections || !this.engine.docs[this.doc].events) return false;
+    for (const c of this.intervalCollections.values()) if (c.byId.size) return true;
+    return false;
   }
 
   // ---- local ops (documents created with {localClient: true}) ----
@@ -606,19 +627,41 @@ class BatchClient {
       }
       const ranges = [];
       let kind = -1;
+      let slides = null;
       while (i < n && flat[5 * i] === k) {
-        kind = flat[5 * i + 1];
+        const kd = flat[5 * i + 1];
+        if ((kd & 0xff) >= DELTA_SLIDE && (kd & 0xff) < 2 * DELTA_SLIDE) {
+          // a reference slid off a removed-and-acked segment (MTE_DELTA_SLIDE)
+          (slides || (slides = [])).push({ slot: flat[5 * i + 4], pos: flat[5 * i + 2] | 0, seg: flat[5 * i + 3],
+            moves: (kd & 1) !== 0, off: kd >>> 16 });
+          i++;
+          continue;
+        }
+        kind = kd;
         ranges.push({ position: flat[5 * i + 2] | 0, length: flat[5 * i + 3], removed: flat[5 * i + 4] === 1,
           segment: kind === 0 && src.op ? src.op.seg : undefined });
         i++;
       }
-      if (kind < 0) continue;
+      if (kind < 0) {
+        if (slides) this._slid(slides);
+        continue;
+      }
       if (cur) cur.ops.push(...opsFromDelta(kind, ranges, src.op));
       const ev = { deltaOperation: kind, operation: kinds[kind], isLocal: src.local,
         message: src.local ? undefined : src.msg, ranges, first: ranges[0], last: ranges[ranges.length - 1] };
       for (const fn of this.listeners || []) fn(ev, this);
+      // markRangeRemoved slides the newly removed segments' references after
+      // the delta callback (mergeTree.ts:1978-1993)
+      if (slides) this._slid(slides);
     }
     flushMsg();
+  }
+
+  /** The references one op slid (MTE_DELTA_SLIDE records, in the order of the
+   *  segments they left) -> the interval collections' position listeners. */
+  _slid(slides) {
+    if (!this.intervalCollections) return;
+    for (const c of this.intervalCollections.values()) c._onSlides(slides);
   }
 
   /** Client.rollback (client.ts:396-398 -> MergeTree.rollback,
@@ -783,6 +826,9 @@ class BatchClient {
    *  once it is detached or removed. */
   localReferencePositionToPosition(lref) {
     if (lref && lref.snapshot) return lref.position;  // an interval event's previousInterval end
+    // an end an interval event raised mid-op reads as it was at that moment
+    // (IntervalCollection._onSlides)
+    if (lref && lref.pinned !== undefined) return lref.pinned;
     if (!lref || lref.client !== this || lref.slot < 0) return -1;
     // transientRead: an end an interval event's previousInterval shares, read
     // as the reference reads it while emitChange holds it Transient

@@ -28,6 +28,7 @@
 // op moves without a "changeInterval" event (the reference raises one from the
 // reference's position-change listeners, :1023-1058, mid-op).
 const { MergeTreeError } = require("./packing");
+const { RedBlackTree } = require("./rbtree");
 
 // ReferenceType (merge-tree ops.ts) and IntervalType (intervalCollection.ts:48-66)
 const RefType = { Simple: 0x0, Tile: 0x1, NestBegin: 0x2, NestEnd: 0x4, RangeBegin: 0x10, RangeEnd: 0x20,
@@ -111,6 +112,7 @@ class SequenceInterval {
     return [c.localReferencePositionToPosition(this.start), c.localReferencePositionToPosition(this.end)];
   }
   _keys() {
+    if (this._pinKeys) return this._pinKeys;  // the ends as they were (an index removal before they moved)
     const c = this.collection.client;
     return [c._refOrder(this.start), c._refOrder(this.end)];
   }
@@ -215,7 +217,14 @@ class IntervalCollection {
     this.pendingEnd = new Map();
     this.nextLocalId = 0;
     this.listeners = new Map();
-    this.stamp = 0;  // index insertion order (the end tree keeps the last put, rbTree.ts:249-300)
+    this.stamp = 0;  // index insertion order
+    // the end tree (LocalIntervalCollection.endIntervalTree, :728-757): the
+    // reference's red-black tree keyed by the intervals' ends
+    // (compareSequenceIntervalEnds, :1025-1026), put / removed exactly where
+    // the reference puts / removes (addIntervalToIndex, removeIntervalFromIndex),
+    // with no conflict resolver (IntervalCollection.addConflictResolver is the
+    // application's to call): previousInterval / nextInterval read it
+    this.endTree = new RedBlackTree((a, b) => compareKeys(a._keys()[1], b._keys()[1]));
     if (serialized) this._load(serialized);
   }
 
@@ -279,6 +288,7 @@ class IntervalCollection {
   _index(ival) {
     ival.stamp = ++this.stamp;
     this.byId.set(ival.getIntervalId(), ival);
+    this.endTree.put(ival, ival);  // addIntervalToIndex (:975-987)
   }
 
   _addInterval(start, end, intervalType, props, op, fromSnapshot) {
@@ -316,6 +326,7 @@ class IntervalCollection {
    *  without an op), the others kept. */
   _changeInterval(ival, start, end, op) {
     const retype = (t) => (op ? t : ((t & ~RefType.SlideOnRemove) | RefType.StayOnRemove));
+    this.endTree.remove(ival);  // removeExistingInterval of the interval modify replaced (:999-1012)
     if (start !== undefined) {
       const old = ival.start;
       ival.start = op ? this._opRef(start, retype(old.refType), op) : this._localRef(start, retype(old.refType));
@@ -327,10 +338,12 @@ class IntervalCollection {
       this._drop(old);
     }
     ival.stamp = ++this.stamp;
+    this.endTree.put(ival, ival);  // add(newInterval)
     return ival;
   }
 
   _remove(ival) {
+    this.endTree.remove(ival);  // removeIntervalFromIndex (:960-968), while its ends still compare
     this.byId.delete(ival.getIntervalId());
     this._drop(ival.start);
     this._drop(ival.end);
@@ -389,7 +402,11 @@ class IntervalCollection {
       if (ival) this._remove(ival);  // removeExistingInterval: no event
       return undefined;
     }
-    if (ival && (r[nPos] !== -1 || r[nPos + 1] !== -1)) ival.stamp = ++this.stamp;  // re-added by changeInterval
+    if (ival && (r[nPos] !== -1 || r[nPos + 1] !== -1)) {  // re-added by changeInterval (removeExisting + add)
+      ival.stamp = ++this.stamp;
+      this.endTree.remove(ival);
+      this.endTree.put(ival, ival);
+    }
     return rebased;
   }
 
@@ -546,16 +563,96 @@ class IntervalCollection {
     const id = ival.getIntervalId();
     const watch = this._has("changeInterval");
     const prev = watch ? snapshotInterval(ival) : null;
-    const before = watch ? ival._keys() : null;
+    const before = ival._keys();
     const slide = (r) => (r.refType & ~RefType.StayOnRemove) | RefType.SlideOnRemove;
     if (!this.pendingStart.has(id) && stay(ival.start)) this.client._setRefSlide(ival.start, slide(ival.start));
     if (!this.pendingEnd.has(id) && stay(ival.end)) this.client._setRefSlide(ival.end, slide(ival.end));
-    if (watch) {
-      const after = ival._keys();
-      if (after[0] !== before[0] || after[1] !== before[1]) {
+    const after = ival._keys();
+    if (after[0] !== before[0] || after[1] !== before[1]) {
+      // removeExistingInterval (with the ends as they were) + add (:1862-1899)
+      ival._pinKeys = before;
+      this.endTree.remove(ival);
+      delete ival._pinKeys;
+      this.endTree.put(ival, ival);
+      ival.stamp = ++this.stamp;
+      if (watch) this._emitChange(ival, prev, true, op);
+    }
+  }
+
+  // ---- ends sliding inside merge-tree ops --------------------------------------
+  /** The references one merge-tree op slid off removed-and-acked segments
+   *  (MTE_DELTA_SLIDE records, BatchClient._deliver; the document replays
+   *  message by message while the collection holds intervals, so the engine's
+   *  state is the state right after this op).  The reference calls each
+   *  sliding end's beforeSlide / afterSlide (localReference.ts:436-447,
+   *  471-480, mergeTree.ts:936-942), which for an interval end are the
+   *  collection's position-change listeners (addIntervalListeners,
+   *  intervalCollection.ts:1023-1058): one "changeInterval" per end that slid,
+   *  local = true and no op (attachGraph's onPositionChange -> emitChange,
+   *  :1350-1353), in the order the segments' reference lists are walked --
+   *  segment by segment, by offset, then list order (here creation order).
+   *  previousInterval holds the ends as they were (Transient clones: a removed
+   *  segment's position), the interval the ends as they are at that moment: an
+   *  end that slides later in the same op still sits on its removed segment. */
+  _onSlides(slides) {
+    if (this.byId.size === 0) return;
+    const owner = new Map();  // slot -> [interval, 0 start | 1 end]
+    for (const x of this.byId.values()) {
+      if (x.start && x.start.slot >= 0) owner.set(x.start.slot, [x, 0]);
+      if (x.end && x.end.slot >= 0) owner.set(x.end.slot, [x, 1]);
+    }
+    const mine = slides.filter((r) => owner.has(r.slot));
+    if (mine.length === 0) return;
+    // the walk's order: the units the ends left, in document order (r.seg: the
+    // unit's order key after the op, -1 once the zamboni took it -- then the
+    // engine's report order), then list order (creation)
+    const ref = (r) => { const [x, w] = owner.get(r.slot); return w ? x.end : x.start; };
+    const at = new Map(mine.map((r, i) => [r, i]));
+    mine.sort((a, b) => ((a.seg >= 0 && b.seg >= 0) ? (a.seg - b.seg) : (at.get(a) - at.get(b))) ||
+      (ref(a).created - ref(b).created));
+    const c = this.client;
+    // every end's position now (after the op) and, for the ends that slide, at their turn
+    const now = (lref) => c.localReferencePositionToPosition(lref);
+    const after = new Map();
+    for (const r of mine) after.set(r.slot, now(ref(r)));
+    const pending = new Map(mine.map((r) => [r.slot, r.pos]));  // still on its removed segment
+    // the end tree compares the ends as they stand at each slide: an end still
+    // to slide keeps the key of the unit it sits on (pinned), one that slid its
+    // key after the op
+    const touched = new Set(mine.map((r) => owner.get(r.slot)[0]));
+    for (const x of touched) x._pinKeys = x._keys();
+    for (const r of mine) if (r.seg >= 0) owner.get(r.slot)[0]._pinKeys[owner.get(r.slot)[1]] = r.seg;
+    try {
+      for (const r of mine) {
+        const [ival, which] = owner.get(r.slot);
+        pending.delete(r.slot);
+        // the other end: on its removed segment if it slides later in this op
+        const other = which ? ival.start : ival.end;
+        const otherPos = pending.has(other.slot) ? pending.get(other.slot) : now(other);
+        const prevStart = which ? otherPos : r.pos, prevEnd = which ? r.pos : otherPos;
+        const curStart = which ? otherPos : after.get(r.slot), curEnd = which ? after.get(r.slot) : otherPos;
+        // beforeSlide removes the interval from the index (removeIntervalFromIndex, :1042-1047)
+        this.endTree.remove(ival);
+        ival._pinKeys[which] = c._refOrder(which ? ival.end : ival.start);
+        // afterSlide re-adds it (addIntervalToIndex), then onPositionChange (:1048-1053)
         ival.stamp = ++this.stamp;
-        this._emitChange(ival, prev, true, op);
+        this.endTree.put(ival, ival);
+        if (this._has("changeInterval")) {
+          const snap = (p) => ({ snapshot: true, position: p, refType: RefType.Transient });
+          const prev = new SequenceInterval(this, snap(prevStart), snap(prevEnd), ival.intervalType);
+          prev.properties = Object.assign({}, ival.properties);
+          ival.start.pinned = curStart;
+          ival.end.pinned = curEnd;
+          try {
+            this._emit("changeInterval", ival, prev, true, undefined);
+          } finally {
+            delete ival.start.pinned;
+            delete ival.end.pinned;
+          }
+        }
       }
+    } finally {
+      for (const x of touched) delete x._pinKeys;
     }
   }
 
@@ -624,28 +721,15 @@ class IntervalCollection {
     });
   }
 
-  /** previousInterval / nextInterval (:897-913): floor / ceil of a Transient
-   *  interval at pos in the end tree (ordered by end; of the intervals whose
-   *  ends sit on one unit it holds the one put last, rbTree.ts:249-300). */
-  _endTree() {
-    const byEnd = new Map();
-    for (const x of this.byId.values()) {
-      const k = x._keys()[1];
-      const cur = byEnd.get(k);
-      if (!cur || cur.stamp < x.stamp) byEnd.set(k, x);
-    }
-    return Array.from(byEnd.entries()).sort((a, b) => compareKeys(a[0], b[0]));
-  }
+  /** previousInterval / nextInterval (:897-913): the data of the end tree's
+   *  floor / ceil node of a Transient interval at pos. */
   previousInterval(pos) {
-    const k = this.client._unitKeyAt(pos);
-    let out;
-    for (const [ek, x] of this._endTree()) if (compareKeys(ek, k) <= 0) out = x;
-    return out;
+    const n = this.endTree.floor(new TransientInterval(this.client, pos, pos));
+    return n ? n.data : undefined;
   }
   nextInterval(pos) {
-    const k = this.client._unitKeyAt(pos);
-    for (const [ek, x] of this._endTree()) if (compareKeys(ek, k) >= 0) return x;
-    return undefined;
+    const n = this.endTree.ceil(new TransientInterval(this.client, pos, pos));
+    return n ? n.data : undefined;
   }
 
   // ---- summary --------------------------------------------------------------------

@@ -122,6 +122,18 @@ extern "C" {
 #define MTE_DELTA_REGEN 0x10u
 /* the answer of an MTE_OP_REF record with b = 4 / 5 (pos; len 0) */
 #define MTE_DELTA_REBASE 0x20u
+/* A local reference of an MTE_DOC_REFS | MTE_DOC_EVENTS document slid off a
+ * segment that became removed and acked (slideAckedRemovedSegmentReferences,
+ * mergeTree.ts:921-950, after a remote remove or an ack) or came off it for
+ * want of a segment to slide to: one record per reference, in the order of the
+ * segments it left; pos = the own-view position of that segment, len = its
+ * index among the document's held segments (telling apart removed neighbours
+ * at one position), removed = the reference's slot, kind = MTE_DELTA_SLIDE | 1 when it moved onto a segment |
+ * its offset in the segment it left << 16 (clamped to 0xffff).  The reference
+ * calls the reference's beforeSlide / afterSlide callbacks at each of them
+ * (localReference.ts:436-447, 471-480): an interval collection's "changeInterval"
+ * events raised mid-op (intervalCollection.ts:1042-1053). */
+#define MTE_DELTA_SLIDE 0x40u
 /* Follows an annotate's MTE_OP_ROLLBACK (a local record): for each key k the
  * rolled-back annotate set (pos1 = k), the older pending annotates that set k
  * too, latest first -- pos2 = its group slot, a = the value id it set, seq =

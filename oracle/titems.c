@@ -1002,22 +1002,38 @@ static int doc_ref(idoc* d, const mte_op* op) {
 }
 
 /* slideAckedRemovedSegmentReferences for every item whose removedSeq is now s
- * (oracle.c doc_slide_refs) */
-static void doc_slide_refs(idoc* d, int32_t s) {
-  if (!(d->flags & MTE_DOC_REFS) || !d->ref_hi) return;
+ * (oracle.c doc_slide_refs); an MTE_DOC_EVENTS document gets one
+ * MTE_DELTA_SLIDE record per reference that slid or came off (include/mte.h:
+ * the reference's beforeSlide / afterSlide callbacks, localReference.ts:436-447) */
+static int delta_push(idoc* d, uint32_t kind, int64_t pos, int32_t len, uint32_t removed);
+static int64_t own_prefix(const idoc* d, uint32_t at);
+static int doc_slide_refs(idoc* d, int32_t s) {
+  if (!(d->flags & MTE_DOC_REFS) || !d->ref_hi) return MTE_OK;
+  const int evd = (d->flags & MTE_DOC_EVENTS) != 0;
   for (uint32_t i = 0; i < d->n; i++) {
     const item* g = &d->it[i];
     if (g->rseq != s || g->empty) continue;
     uint32_t to = 0;
     const int64_t t = slide_to(d, i, &to);
+    const int64_t xpos = evd ? own_prefix(d, i) : 0;
     for (uint32_t r = 0; r < d->ref_hi; r++) {
       const uint32_t st = d->ref_state[r];
       if (!(st & REF_LIVE) || (st & REF_DETACHED) || (st & MTE_REF_STAY_ON_REMOVE)) continue;
-      if (d->ref_anchor[r] - g->toff >= (uint32_t)g->len) continue;
-      if ((st & MTE_REF_SLIDE_ON_REMOVE) && t >= 0) d->ref_anchor[r] = to;
+      const uint32_t off = d->ref_anchor[r] - g->toff;
+      if (off >= (uint32_t)g->len) continue;
+      const int moves = (st & MTE_REF_SLIDE_ON_REMOVE) && t >= 0;
+      const uint32_t left = d->ref_anchor[r];
+      if (moves) d->ref_anchor[r] = to;
       else d->ref_state[r] = st | REF_DETACHED | (t < 0 ? REF_OFF : 0u);
+      if (evd) {
+        /* len: the unit it left, made its order key once the message is done (slide_keys) */
+        const int rc = delta_push(d, MTE_DELTA_SLIDE | (moves ? 1u : 0u) | ((off < 0xffffu ? off : 0xffffu) << 16), xpos,
+                                  (int32_t)left, r);
+        if (rc) return rc;
+      }
     }
   }
+  return MTE_OK;
 }
 
 /* ---- insert, range ops (remote and local) -------------------------------------------------------- */
@@ -1431,13 +1447,44 @@ static int doc_ack(idoc* d, const mte_op* op, const env_t* env) {
       }
       if (member && !g->cont && (rc = add_lru(d, i, s))) return rc;
     }
-    doc_slide_refs(d, s);
+    if ((rc = doc_slide_refs(d, s))) return rc;
     zamboni(d, env->arena, env->n_keys);
   }
   return MTE_OK;
 }
 
+/* The MTE_DELTA_SLIDE records of the message that starts at record `from`:
+ * the unit each reference left -> that unit's order key once the message's
+ * zamboni has run (the held units before it, as mte_read_ref_order counts
+ * them; -1 if it is gone), so a host compares the ends as they were with the
+ * others as they are. */
+static void slide_keys(idoc* d, uint64_t from) {
+  for (uint64_t q = from; q < d->dl_n; q++) {
+    mte_delta* e = &d->dl[q];
+    if ((e->kind & 0xc0u) != MTE_DELTA_SLIDE) continue;
+    const uint32_t u = (uint32_t)e->len;
+    int64_t p = 0, key = -1;
+    for (uint32_t i = 0; i < d->n; i++) {
+      const item* g = &d->it[i];
+      if (!g->empty && u - g->toff < (uint32_t)g->len) {
+        key = p + (int64_t)(u - g->toff);
+        break;
+      }
+      p += g->len;
+    }
+    e->len = (int32_t)key;
+  }
+}
+
+static int doc_apply_op(idoc* d, const mte_op* op, const env_t* env);
 static int doc_apply(idoc* d, const mte_op* op, const env_t* env) {
+  const uint64_t from = d->dl_n;
+  const int rc = doc_apply_op(d, op, env);
+  if (!rc && (d->flags & MTE_DOC_EVENTS) && (d->flags & MTE_DOC_REFS) && d->dl_n > from) slide_keys(d, from);
+  return rc;
+}
+
+static int doc_apply_op(idoc* d, const mte_op* op, const env_t* env) {
   const int32_t s = op->seq;
   const int c = op->client;
   const int local_doc = (d->flags & MTE_DOC_LOCAL_CLIENT) != 0;
@@ -1468,7 +1515,7 @@ static int doc_apply(idoc* d, const mte_op* op, const env_t* env) {
     if ((rc = check_op_window(d, op))) return rc;
   } else if (op->type == MTE_OP_REMOVE || op->type == MTE_OP_ANNOTATE) {
     if ((rc = tree_range(d, op, env, 0))) return rc;
-    if (op->type == MTE_OP_REMOVE) doc_slide_refs(d, s);
+    if (op->type == MTE_OP_REMOVE && (rc = doc_slide_refs(d, s))) return rc;
     zamboni(d, env->arena, env->n_keys);
     if ((rc = check_op_window(d, op))) return rc;
   } else if (op->type == MTE_OP_ACK) {

@@ -58,13 +58,16 @@ const clone = (v) => JSON.parse(JSON.stringify(v));
 const b64 = (a) => Buffer.from(a.buffer, a.byteOffset, a.byteLength).toString("base64");
 
 // pack mode: the N-API surface the engine uses, recording the submitted batches
-let lastBatch = null;
+// (several per checkpoint: the end tree's comparisons read reference order,
+// which flushes; here every reference reads as the same unit)
+let batches = [];
 const recorder = {
   create() { return {}; }, destroy() {}, loadDocs() {}, loadSegments() {},
   submit(ctx, offsets, ops, text, propsets, props) {
-    lastBatch = { offsets: b64(offsets), ops: b64(ops), text: b64(text), propsets: b64(propsets), props: b64(props) };
+    batches.push({ offsets: b64(offsets), ops: b64(ops), text: b64(text), propsets: b64(propsets), props: b64(props) });
   },
   run() {}, sync() {}, readDeltas() { return new Uint32Array(0); },
+  readRefOrder(ctx, doc, n) { return new Int32Array(n); },
 };
 
 const eng = new MergeTreeEngine(mode === "pack" ? { nKeys: 8, addon: recorder } : { nKeys: 8 });
@@ -73,7 +76,7 @@ for (let si = 0; si < nSets; si++) {
   sets[si].names.forEach((name, ci) => {
     const L = { si, ci, sent: null };
     L.client = eng.createClient(sets[si].initialText, { newLengthCalc: true, localClient: true, refs: true,
-      longClientId: name, events: rec });
+      longClientId: name, events: ext });
     L.held = [];
     L.coll = L.client.getIntervalCollection(LABEL, { emit(opName, _p, value, meta) { L.sent = { opName, value, meta }; } });
     if (ext) {
@@ -81,8 +84,9 @@ for (let si = 0; si < nSets; si++) {
       const pos = (r) => L.client.localReferencePositionToPosition(r);
       L.coll.on("addInterval", (x, local, op) => L.ev.push(["add", x.getIntervalId(), local, !!op, false]));
       L.coll.on("deleteInterval", (x, local, op) => L.ev.push(["delete", x.getIntervalId(), local, !!op, false]));
+      // mt: raised inside a merge-tree op (an end sliding off a removed segment)
       L.coll.on("changeInterval", (x, prev, local, op) => L.ev.push(["change", x.getIntervalId(), local, !!op,
-        pos(prev.start), pos(prev.end), pos(x.start), pos(x.end), false]));
+        pos(prev.start), pos(prev.end), pos(x.start), pos(x.end), !!L.mt]));
       L.coll.on("propertyChanged", (x, deltas, local, op) => L.ev.push(["props", x.getIntervalId(), local, !!op,
         sortKeys(clone(deltas)), false]));
     }
@@ -99,6 +103,7 @@ if (ext) {
       longClientId: "loader" + si }));
   }
 }
+if (ext) eng.setEventCapacity(64);  // a remove can slide many interval ends (MTE_DELTA_SLIDE)
 eng.start();
 const prev = layout.map(() => 0);
 const failures = [];
@@ -119,7 +124,14 @@ for (let j = 0; j < nCp; j++) {
       const msg = { clientId: m[0], sequenceNumber: m[1], referenceSequenceNumber: m[2], minimumSequenceNumber: m[3],
         type: "op", contents: m[5] };
       if (kind === "A") {
-        if (m[4] === "op") L.client.applyMsg(msg);
+        if (m[4] === "op") {
+          L.mt = true;
+          try {
+            L.client.applyMsg(msg);
+          } finally {
+            L.mt = false;
+          }
+        }
         else L.coll.process(m[5].opName, m[5].value === undefined ? undefined : clone(m[5].value),
           m[0] === s.names[L.ci], msg);
         continue;
@@ -196,8 +208,8 @@ for (let j = 0; j < nCp; j++) {
       ivs.sort((a, b) => (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0));
       return { intervals: ivs, nRefs: L.client.clients.refNext };
     });
-    process.stdout.write(JSON.stringify({ batch: lastBatch, states }) + "\n");
-    lastBatch = null;
+    process.stdout.write(JSON.stringify({ batches, states }) + "\n");
+    batches = [];
     continue;
   }
   layout.forEach((L) => {
@@ -214,7 +226,7 @@ for (let j = 0; j < nCp; j++) {
     if (!ok) failures.push([L.si, L.ci, j, "state", ivs.slice(0, 3), want.intervals.slice(0, 3)]);
     if (ext && ok) {
       const ids = (xs) => xs.map((x) => x.getIntervalId());
-      const evWant = want.events.filter((e) => !e[e.length - 1]);
+      const evWant = want.events;
       const got = { events: L.ev, order: ids(Array.from(L.coll)), summary: clone(L.coll.serializeInternal()),
         queries: want.queries.map(([a, b]) => [a, b, ids(L.coll.findOverlappingIntervals(a, b)),
           ids([L.coll.previousInterval(a)].filter(Boolean)), ids([L.coll.nextInterval(a)].filter(Boolean)),

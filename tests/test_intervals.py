@@ -63,8 +63,8 @@ def replay_packed(factory, sets, lines):
     passed, failures = 0, []
     for j, line in enumerate(lines):
         rec = json.loads(line)
-        if rec["batch"] is not None:
-            eng.apply_batch(_batch(rec["batch"]))
+        for b in rec["batches"]:
+            eng.apply_batch(_batch(b))
         st = eng.statuses()
         for d, (si, ci) in enumerate(layout):
             have = rec["states"][d]
