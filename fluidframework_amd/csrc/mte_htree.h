@@ -1177,7 +1177,11 @@ __device__ __forceinline__ int ht_range(HT& h, const s8v& op, bool local, const 
     MTE_STAT(st[kStPwrites] += cnt_all * w;)
   }
   h.lp_n = 0;  // the marks changed lengths
-  if (rem && !local && rt && rhi) stream_slide(h.pl, h.sd, h.n, rt, rhi, s, evd ? &ev : nullptr);
+  if (rem && !local && rt && rhi) {
+    const uint32_t* lrp = h.pl + (uint64_t)kLrsPlane<K> * h.sd;
+    stream_slide(h.pl, h.sd, h.n, rt, rhi, s, evd ? &ev : nullptr, kSlideOverlap, lrp);
+    stream_slide(h.pl, h.sd, h.n, rt, rhi, s, evd ? &ev : nullptr, kSlideNew, lrp);
+  }
   return 0;
 }
 
@@ -1241,7 +1245,7 @@ __device__ __forceinline__ int ht_ack(HT& h, const s8v& op, const ReplayArgs& a,
         }
       }
     }
-    if (rt && rhi) stream_slide(h.pl, h.sd, h.n, rt, rhi, s, ev);
+    if (rt && rhi) stream_slide(h.pl, h.sd, h.n, rt, rhi, s, ev, lo == hi ? kSlideAck : kSlideAll);
     if ((rc = ht_zamboni<K>(h, a.n_keys))) return rc;
   }
   return 0;

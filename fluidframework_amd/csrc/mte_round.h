@@ -364,6 +364,244 @@ __device__ __forceinline__ void col_sub_row(const Col& C, int gg, int32_t ci_row
   if (l >= sg && l < C.nsg) C.SS[l] = C.SS[l] - og;
 }
 
+// one op of a chain against the column, op after op: appends its sub-ops at
+// list[m..] and changes the column; false = the run cannot take it (an insert
+// past the end: MTE_E_INSERT_FAILED op after op; the list full)
+__device__ __forceinline__ bool rnd_serial_op(const Col& C, uint32_t k, uint32_t w3, int32_t pos1, int32_t pos2,
+                                              uint4* list, uint32_t& m, uint32_t cap_c) {
+  const int l = lane_id();
+  const uint32_t type = w3 & 0xffu, flags = w3 >> 16;
+  if (type == MTE_OP_INSERT) {
+    const ColHit h = col_find(C, pos1, false);
+    if (pos1 > h.total || h.i >= C.nch || m >= cap_c) return false;
+    const int32_t nlen = (flags & MTE_F_MARKER) ? 1 : pos2;
+    if (l == 0) list[m] = make_uint4((uint32_t)h.i, k, (uint32_t)h.excl, 0u);
+    m++;
+    if (nlen > 0) col_add(C, h, nlen);
+    fence_wave();
+    return true;
+  }
+  const int32_t b1 = pos1 < pos2 ? pos1 : pos2, b2 = pos1 < pos2 ? pos2 : pos1;
+  const ColHit h = col_find(C, b1, true);
+  if (h.i < C.nch) {
+    if (b1 == b2) {
+      // ensureIntervalBoundary alone: a split strictly inside a leaf
+      if (h.excl < b1) {
+        if (m >= cap_c) return false;
+        if (l == 0) list[m] = make_uint4((uint32_t)h.i, k, (uint32_t)h.excl, 0u);
+        m++;
+      }
+    } else {
+      // group by group from the first chunk's while the chunk starts are
+      // before b2, in the op's perspective before it (eg: the group's start then)
+      int32_t eg = h.excl - (h.lc > 0 ? rdlane(h.ci, h.lc - 1) : 0);
+      for (int gg = h.g; gg < C.ng; gg++) {
+        const int i = gg * kChGroup + l;
+        const int32_t ci = i < C.nch ? C.CI[i] : 0;
+        const int32_t cprev0 = __shfl_up(ci, 1);
+        const int32_t cprev = l == 0 ? 0 : cprev0;
+        const int32_t st = eg + cprev, incl = eg + ci, v = ci - cprev;
+        const bool hit = i < C.nch && i >= h.i && v > 0 && st < b2;
+        const uint64_t hm = __ballot(hit);
+        const uint32_t at = m + lanes_below(hm);
+        m += (uint32_t)__popcll(hm);
+        if (m > cap_c) return false;
+        if (hit) list[at] = make_uint4((uint32_t)i, k, (uint32_t)st, 0u);
+        // the group's end before this op
+        const int last = C.nch - gg * kChGroup < kWave ? C.nch - gg * kChGroup - 1 : kWave - 1;
+        const int32_t gend = eg + rdlane(ci, last);
+        if (type == MTE_OP_REMOVE && hm) {
+          const int32_t lo = b1 > st ? b1 : st, hi = b2 < incl ? b2 : incl;
+          col_sub_row(C, gg, ci, hit ? hi - lo : 0);
+          fence_wave();
+        }
+        eg = gend;
+        if (gend >= b2) break;
+      }
+    }
+  }
+  fence_wave();
+  return true;
+}
+
+// ---- block-parallel chain resolve ----------------------------------------------
+// A chain's ops resolve 64 at a time, lane t = the block's t-th op.  An op
+// changes its chain's column only through the chunk boundaries B_c (inclusive
+// prefixes) it moves, a monotone map on positions -- exactly what col_add /
+// col_sub_row do to the rows:
+//   insert of n at p:  B -> B + n if p <= B (the first chunk with B >= p takes it)
+//   remove [b1, b2):   B -> B if B <= b1;  b1 if b1 < B < b2;  B - (b2 - b1) if B >= b2
+//   annotate:          identity.
+// Op t's chunk is the first c whose boundary, carried through the block's
+// earlier ops, is > x (x = b1; an insert's "first with >= pos" is "> pos - 1"),
+// and as every map is monotone that condition pulls back to the block-start
+// column: B_c > y, y = x carried back through the earlier ops, latest first:
+//   insert (p, n):  y -> y if y < p;  y - n if y >= p + n;  p - 1 otherwise (inside it: its chunk)
+//   remove (b1, r): y -> y if y < b1;  y + r otherwise.
+// So every lane finds its chunk with one search of the block-start column, the
+// chunk's start and end in its perspective are block-start boundaries carried
+// forward through the earlier ops, and the block's length changes fold into the
+// column afterwards (col_add_at, one LDS add per row and change).  A range that
+// reaches a third chunk sends the block op by op (rnd_serial_op).
+
+// first t in [0, V) with R[t] > lim over a nondecreasing row, >= V if none
+// (this lane's row: two rounds of 8 LDS reads)
+__device__ __forceinline__ int row_first_gt(const int32_t* R, int V, int32_t lim) {
+  int q = 0;
+#pragma unroll
+  for (int s = 0; s < 8; s++) {
+    const int t = 8 * s + 7;
+    q += (t < V && R[t] <= lim) ? 1 : 0;
+  }
+  if (q == 8) return kWave;
+  int u = 0;
+#pragma unroll
+  for (int s = 0; s < 8; s++) {
+    const int t = 8 * q + s;
+    u += (t < V && R[t] <= lim) ? 1 : 0;
+  }
+  return 8 * q + u;
+}
+
+struct ColPos {
+  int c;                // the first chunk with B_c > y (nch: none)
+  int32_t bm, bc, bn;   // B_{c-1} (-1 for chunk 0), B_c, B_{c+1} (B_c for the last chunk)
+};
+
+__device__ __forceinline__ ColPos col_find_lane(const Col& C, int32_t y, bool act) {
+  ColPos r;
+  r.c = C.nch;
+  r.bm = r.bc = r.bn = 0;
+  if (!act) return r;
+  const int sg = row_first_gt(C.SS, C.nsg, y);
+  if (sg >= C.nsg) return r;
+  const int32_t es = sg > 0 ? C.SS[sg - 1] : 0;
+  const int vg = C.ng - sg * kWave < kWave ? C.ng - sg * kWave : kWave;
+  const int t = row_first_gt(C.GS + sg * kWave, vg, y - es);
+  if (t >= vg) return r;  // the rows disagree: not found (the run falls back)
+  const int g = sg * kWave + t;
+  const int32_t eg = es + (t > 0 ? C.GS[g - 1] : 0);
+  const int vc = C.nch - g * kChGroup < kChGroup ? C.nch - g * kChGroup : kChGroup;
+  const int u = row_first_gt(C.CI + g * kChGroup, vc, y - eg);
+  if (u >= vc) return r;
+  r.c = g * kChGroup + u;
+  r.bm = u > 0 ? eg + C.CI[r.c - 1] : (r.c == 0 ? -1 : eg);
+  r.bc = eg + C.CI[r.c];
+  r.bn = r.bc;
+  if (r.c + 1 < C.nch) {
+    if (u + 1 < kChGroup) {
+      r.bn = eg + C.CI[r.c + 1];
+    } else {  // the next group's first chunk
+      const int g1 = g + 1, sg1 = g1 / kWave;
+      const int32_t es1 = sg1 == sg ? es : C.SS[sg1 - 1];
+      r.bn = es1 + ((g1 % kWave) ? C.GS[g1 - 1] : 0) + C.CI[r.c + 1];
+    }
+  }
+  return r;
+}
+
+// chunk i's length changed by d (wave-uniform i, d): the later entries of its rows
+__device__ __forceinline__ void col_add_at(const Col& C, int i, int32_t d) {
+  const int l = lane_id();
+  const int g = i / kChGroup, sg = g / kWave;
+  const int ci = g * kChGroup + l, gi = sg * kWave + l;
+  if (l >= i % kChGroup && ci < C.nch) atomicAdd(&C.CI[ci], d);
+  if (l >= g % kWave && gi < C.ng) atomicAdd(&C.GS[gi], d);
+  if (l >= sg && l < C.nsg) atomicAdd(&C.SS[l], d);
+}
+
+// the block of nb ops (lane t < nb: op t -- record index k, w3, pos1, pos2):
+// sub-ops appended at list[m..], the column advanced past the block.  false:
+// nothing done, the block goes op by op.  failed: an insert past the end.
+__device__ __forceinline__ bool rnd_block(const Col& C, int nb, uint32_t k, uint32_t w3, int32_t pos1, int32_t pos2,
+                                          uint4* list, uint32_t& m, uint32_t cap_c, bool& failed) {
+  if (m + 2u * (uint32_t)nb > cap_c) return false;  // at most two sub-ops an op; else op by op, checked
+  const int l = lane_id();
+  const bool v = l < nb;
+  const uint32_t type = w3 & 0xffu;
+  const bool ins = v && type == MTE_OP_INSERT, rem = v && type == MTE_OP_REMOVE;
+  const int32_t b1 = pos1 < pos2 ? pos1 : pos2, b2 = pos1 < pos2 ? pos2 : pos1;
+  const int32_t nlen = ((w3 >> 16) & MTE_F_MARKER) ? 1 : pos2;
+  // the op as a map: tn > 0 an insert of tn at tp, tn < 0 a remove of -tn at tp
+  const int32_t tp = ins ? pos1 : b1;
+  const int32_t tn = ins ? (nlen > 0 ? nlen : 0) : (rem ? b1 - b2 : 0);
+  int32_t y = ins ? pos1 - 1 : b1;
+  for (int j = nb - 2; j >= 0; j--) {
+    const int32_t nj = rdlane(tn, j);
+    if (nj == 0) continue;
+    const int32_t pj = rdlane(tp, j);
+    if (v && l > j && y >= pj) y = nj < 0 ? y - nj : (y >= pj + nj ? y - nj : pj - 1);
+  }
+  const ColPos P = col_find_lane(C, y, v);
+  const bool found = v && P.c < C.nch;
+  int32_t bm = P.bm, bc = P.bc, bn = P.bn;
+  for (int j = 0; j + 1 < nb; j++) {
+    const int32_t nj = rdlane(tn, j);
+    if (nj == 0) continue;
+    const int32_t pj = rdlane(tp, j);
+    if (found && l > j) {
+      if (nj > 0) {
+        bm += pj <= bm ? nj : 0;
+        bc += pj <= bc ? nj : 0;
+        bn += pj <= bn ? nj : 0;
+      } else {
+        const int32_t e = pj - nj;
+        bm = bm <= pj ? bm : (bm < e ? pj : bm + nj);
+        bc = bc <= pj ? bc : (bc < e ? pj : bc + nj);
+        bn = bn <= pj ? bn : (bn < e ? pj : bn + nj);
+      }
+    }
+  }
+  const int c = P.c;
+  const int32_t st = c == 0 ? 0 : bm;
+  bool s0 = false, s1 = false, more = false, bad = false;
+  int32_t d0 = 0, d1 = 0;
+  if (ins) {
+    if (!found) bad = true;
+    else {
+      s0 = true;
+      d0 = nlen > 0 ? nlen : 0;
+    }
+  } else if (found) {
+    if (b1 == b2) {
+      s0 = st < b1;  // a split strictly inside the chunk
+    } else {
+      s0 = true;
+      if (rem) d0 = (b1 > st ? b1 : st) - (b2 < bc ? b2 : bc);
+      if (bc < b2 && c + 1 < C.nch) {
+        if (bn > bc) {
+          s1 = true;
+          if (rem) d1 = bc - (b2 < bn ? b2 : bn);
+        }
+        if (bn < b2 && c + 2 < C.nch) more = true;
+      }
+    }
+  }
+  if (__ballot(more)) return false;
+  if (__ballot(bad)) {
+    failed = true;
+    return true;
+  }
+  const int32_t cnt = (s0 ? 1 : 0) + (s1 ? 1 : 0);
+  const int32_t inc = wave_incl_scan(cnt);
+  const uint32_t at = m + (uint32_t)(inc - cnt);
+  if (s0) list[at] = make_uint4((uint32_t)c, k, (uint32_t)st, 0u);
+  if (s1) list[at + (s0 ? 1u : 0u)] = make_uint4((uint32_t)c + 1u, k, (uint32_t)bc, 0u);
+  m += (uint32_t)rdlane(inc, kWave - 1);
+  for (uint64_t e = __ballot(d0 != 0); e; e &= e - 1) {
+    const int t = __ffsll((long long)e) - 1;
+    col_add_at(C, rdlane(c, t), rdlane(d0, t));
+  }
+  for (uint64_t e = __ballot(d1 != 0); e; e &= e - 1) {
+    const int t = __ffsll((long long)e) - 1;
+    col_add_at(C, rdlane(c, t) + 1, rdlane(d1, t));
+  }
+  fence_wave();
+  return true;
+}
+
+constexpr uint32_t kRing = 1024;  // a chain wave's staging ring of record indices (LDS)
+
 // WPB waves per workgroup, 8 / WPB workgroups per document; wave u = 0..7 of
 // the document takes the clients c = u, u + 8, ...; dynamic LDS: per wave a
 // CI column of nch_cap entries
@@ -385,11 +623,12 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
   C.nsg = (C.ng + kWave - 1) / kWave;
   {
     const uint32_t gs_cap = (ch.ng_cap + kWave - 1) / kWave * kWave;
-    int32_t* base = reinterpret_cast<int32_t*>(rs_lds) + (uint64_t)w * (ch.nch_cap + gs_cap + kWave);
+    int32_t* base = reinterpret_cast<int32_t*>(rs_lds) + (uint64_t)w * (ch.nch_cap + gs_cap + kWave + kRing);
     C.CI = base;
     C.GS = base + ch.nch_cap;
     C.SS = base + ch.nch_cap + gs_cap;
   }
+  uint32_t* const ring = reinterpret_cast<uint32_t*>(C.SS + kWave);
   const int32_t* sum0 = reinterpret_cast<const int32_t*>(ch.kc + (uint64_t)doc * ch.nch_cap);
   uint4* list = rd.rlist + (uint64_t)doc * rd.rl_cap;
   // ops per client (every workgroup of the document counts them all)
@@ -432,82 +671,51 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
       fence_wave();
       uint32_t m = 0;  // entries in the chain's list
       bool failed = false;
-      uint32_t b[8], nb[8];
-      ch_rec_batch(b, recp, 0);
-      for (uint32_t base = 0; base < nops && !failed; base += kWave) {
-        if (base + kWave < nops) ch_rec_batch(nb, recp, base + kWave);  // the next batch, in flight meanwhile
-        uint64_t mine = __ballot(base + (uint32_t)l < nops && ((b[3] >> 8) & 0xffu) == (uint32_t)c);
-        while (mine) {
-          const int j = __ffsll((long long)mine) - 1;
-          mine &= mine - 1;
-          const uint32_t k = base + (uint32_t)j;
-          const uint32_t w3 = rdlane(b[3], j);
-          const uint32_t type = w3 & 0xffu, flags = w3 >> 16;
-          const int32_t pos1 = (int32_t)rdlane(b[4], j), pos2 = (int32_t)rdlane(b[5], j);
-          if (type == MTE_OP_INSERT) {
-            const ColHit h = col_find(C, pos1, false);
-            if (pos1 > h.total || h.i >= C.nch || m >= cap_c) {  // MTE_E_INSERT_FAILED here: op after op
-              failed = true;
-              break;
-            }
-            const int32_t nlen = (flags & MTE_F_MARKER) ? 1 : pos2;
-            if (l == 0) list[off + m] = make_uint4((uint32_t)h.i, k, (uint32_t)h.excl, 0u);
-            m++;
-            if (nlen > 0) col_add(C, h, nlen);
-          } else {
-            const int32_t b1 = pos1 < pos2 ? pos1 : pos2, b2 = pos1 < pos2 ? pos2 : pos1;
-            const ColHit h = col_find(C, b1, true);
-            if (h.i < C.nch) {
-              if (b1 == b2) {
-                // ensureIntervalBoundary alone: a split strictly inside a leaf
-                if (h.excl < b1) {
-                  if (m >= cap_c) {
-                    failed = true;
-                    break;
-                  }
-                  if (l == 0) list[off + m] = make_uint4((uint32_t)h.i, k, (uint32_t)h.excl, 0u);
-                  m++;
-                }
-              } else {
-                // group by group from the first chunk's while the chunk starts
-                // are before b2, in the op's perspective before it (eg: the
-                // group's start then)
-                int32_t eg = h.excl - (h.lc > 0 ? rdlane(h.ci, h.lc - 1) : 0);
-                for (int gg = h.g; gg < C.ng; gg++) {
-                  const int i = gg * kChGroup + l;
-                  const int32_t ci = i < C.nch ? C.CI[i] : 0;
-                  const int32_t cprev0 = __shfl_up(ci, 1);
-                  const int32_t cprev = l == 0 ? 0 : cprev0;
-                  const int32_t st = eg + cprev, incl = eg + ci, v = ci - cprev;
-                  const bool hit = i < C.nch && i >= h.i && v > 0 && st < b2;
-                  const uint64_t hm = __ballot(hit);
-                  const uint32_t at = m + (uint32_t)__builtin_amdgcn_mbcnt_hi(
-                                              (uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
-                  m += (uint32_t)__popcll(hm);
-                  if (m > cap_c) {
-                    failed = true;
-                    break;
-                  }
-                  if (hit) list[off + at] = make_uint4((uint32_t)i, k, (uint32_t)st, 0u);
-                  // the group's end before this op
-                  const int last = C.nch - gg * kChGroup < kWave ? C.nch - gg * kChGroup - 1 : kWave - 1;
-                  const int32_t gend = eg + rdlane(ci, last);
-                  if (type == MTE_OP_REMOVE && hm) {
-                    const int32_t lo = b1 > st ? b1 : st, hi = b2 < incl ? b2 : incl;
-                    col_sub_row(C, gg, ci, hit ? hi - lo : 0);
-                    fence_wave();
-                  }
-                  eg = gend;
-                  if (gend >= b2) break;
-                }
-                if (failed) break;
-              }
-            }
-          }
-          fence_wave();
+      // the chain's ops in blocks of 64: the records' client bytes 512 at a time
+      // (the next 512 in flight meanwhile), the chain's record indices staged in
+      // an LDS ring, each block's records read back per lane
+      uint32_t head = 0, tail = 0;
+      uint32_t cw[8], nw[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const uint32_t r = (uint32_t)(q * kWave + l);
+        cw[q] = r < nops ? reinterpret_cast<const uint32_t*>(recp + 2 * r)[3] : 0xffffffffu;
+      }
+      for (uint32_t sb = 0; sb < nops && !failed; sb += 8 * kWave) {
+        const bool last = sb + 8 * kWave >= nops;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          const uint32_t r = sb + 8 * kWave + (uint32_t)(q * kWave + l);
+          nw[q] = r < nops ? reinterpret_cast<const uint32_t*>(recp + 2 * r)[3] : 0xffffffffu;
         }
 #pragma unroll
-        for (int q = 0; q < 8; q++) b[q] = nb[q];
+        for (int q = 0; q < 8; q++) {
+          const uint32_t r = sb + (uint32_t)(q * kWave + l);
+          const uint64_t mine = __ballot(r < nops && ((cw[q] >> 8) & 0xffu) == (uint32_t)c);
+          if ((mine >> l) & 1ull) ring[(tail + lanes_below(mine)) & (kRing - 1)] = r;
+          tail += (uint32_t)__popcll(mine);
+        }
+        fence_wave();
+        while (!failed && (tail - head >= (uint32_t)kWave || (last && tail > head))) {
+          const int nb = tail - head < (uint32_t)kWave ? (int)(tail - head) : kWave;
+          uint32_t k = 0, w3 = 0;
+          int32_t p1 = 0, p2 = 0;
+          if (l < nb) {
+            k = ring[(head + (uint32_t)l) & (kRing - 1)];
+            const uint32_t* rp = reinterpret_cast<const uint32_t*>(recp + 2 * k);
+            w3 = rp[3];
+            p1 = (int32_t)rp[4];
+            p2 = (int32_t)rp[5];
+          }
+          if (!rnd_block(C, nb, k, w3, p1, p2, list + off, m, cap_c, failed)) {
+            for (int t = 0; t < nb && !failed; t++)
+              failed = !rnd_serial_op(C, rdlane(k, t), rdlane(w3, t), rdlane(p1, t), rdlane(p2, t), list + off, m,
+                                      cap_c);
+          }
+          head += (uint32_t)nb;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++) cw[q] = nw[q];
       }
       if (l == 0) {
         if (failed) atomicOr(rd.rflag + doc, 2u);

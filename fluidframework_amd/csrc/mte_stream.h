@@ -124,15 +124,18 @@ constexpr uint32_t kRefLive = 0x80000000u, kRefDetached = 0x40000000u, kRefOff =
 __device__ __forceinline__ bool slide_ok(int32_t sq, int32_t rs) { return sq < kLocalBase && rs >= kLocalBase; }
 
 // the first slot a reference may slide to after x (dir > 0) or before it
-// (dir < 0), or -1; x is wave-uniform
-__device__ __forceinline__ int find_slide_target(const uint32_t* pl, uint64_t sd, int n, int x, int dir) {
+// (dir < 0), or -1; x is wave-uniform.  grp != 0: the removals of one ack
+// (removedSeq grp) are acked segment by segment, so the ones after x are still
+// pending when x's references slide (ackPendingSegment, mergeTree.ts:1285-1304)
+__device__ __forceinline__ int find_slide_target(const uint32_t* pl, uint64_t sd, int n, int x, int dir,
+                                                 int32_t grp = 0) {
   const int l = lane_id();
   if (dir > 0) {
     for (int b = x + 1; b < n; b += kWave) {
       const int i = b + l;
       const int ic = i < n ? i : 0;  // unconditional loads, selected after
       const int32_t sq = (int32_t)ld_l2(pl + sd + ic), rs = (int32_t)ld_l2(pl + 2 * sd + ic);
-      const uint64_t m = __ballot(i < n && slide_ok(sq, rs));
+      const uint64_t m = __ballot(i < n && (slide_ok(sq, rs) || (grp != 0 && rs == grp && sq < kLocalBase)));
       if (m) return b + __ffsll((long long)m) - 1;
     }
   } else {
@@ -164,21 +167,32 @@ __device__ __forceinline__ int find_slide_target(const uint32_t* pl, uint64_t sd
 // removed segment it sat on, len = the unit it left (mte_htree.h
 // ht_slide_keys makes it the unit's order key), removed = its slot,
 // kind = MTE_DELTA_SLIDE | 1 if
-// it moved to a segment | its offset in the removed segment << 16 (clamped):
+// it moved to a segment | 2 if to the end of a preceding one | its offset in
+// the removed segment << 16 (clamped):
 // the host orders one segment's references as its LocalReferenceCollection
 // iterates them.
+// mode: kSlideAll every such segment; kSlideAck the removals of one ack, in
+// order, each slid while the later ones are still pending (a reference can
+// slide again from a later one: one record per slide); kSlideOverlap /
+// kSlideNew a remote remove's segments that the local client had removed
+// already (lrp: the local-removal plane, non-zero) -- slid before the delta
+// callback -- then the newly removed ones, after it (mergeTree.ts:1970-1993).
+enum { kSlideAll = 0, kSlideAck = 1, kSlideOverlap = 2, kSlideNew = 3 };
 __device__ __forceinline__ void stream_slide(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t rhi, int32_t s,
-                                             EvOut* ev = nullptr) {
+                                             EvOut* ev = nullptr, int mode = kSlideAll,
+                                             const uint32_t* lrp = nullptr) {
   const int l = lane_id();
   for (int tb = 0; tb < n; tb += kWave) {
     const int i = tb + l;
-    const int32_t rs = (int32_t)ld_l2(pl + 2 * sd + (i < n ? i : 0));
-    uint64_t m = __ballot(i < n && rs == s);
+    const int ic = i < n ? i : 0;
+    const int32_t rs = (int32_t)ld_l2(pl + 2 * sd + ic);
+    const bool lr = mode >= kSlideOverlap && ld_l2(lrp + ic) != 0u;
+    uint64_t m = __ballot(i < n && rs == s && (mode < kSlideOverlap || lr == (mode == kSlideOverlap)));
     while (m) {
       const int x = tb + __ffsll((long long)m) - 1;
       m &= m - 1;
       const uint32_t toff = uni(ld_l2(pl + 5 * sd + x)), len = uni(ld_l2(pl + x));
-      int t = find_slide_target(pl, sd, n, x, 1);
+      int t = find_slide_target(pl, sd, n, x, 1, mode == kSlideAck ? s : 0);
       bool after = false;
       if (t < 0) {
         t = find_slide_target(pl, sd, n, x, -1);
@@ -206,7 +220,8 @@ __device__ __forceinline__ void stream_slide(const uint32_t* pl, uint64_t sd, in
             const uint32_t idx = ev->n + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
             const uint32_t off = anc - toff < 0xffffu ? anc - toff : 0xffffu;
             if (hit && idx < ev->cap)
-              ev->p[idx] = mte_delta{ev->op, MTE_DELTA_SLIDE | (moves ? 1u : 0u) | (off << 16), xpos, (int32_t)anc, r};
+              ev->p[idx] = mte_delta{ev->op, MTE_DELTA_SLIDE | (moves ? 1u : 0u) | (moves && after ? 2u : 0u) | (off << 16), xpos,
+                                     (int32_t)anc, r};
             ev->n += (uint32_t)__popcll(hm);
           }
         }

@@ -404,6 +404,15 @@ class LocalReferencePosition {
     this.refType = refType;
     this.properties = properties;
     this.created = ++refCreated;
+    // where it sits among the references at its offset (IRefsAtOffset,
+    // localReference.ts:139-215): list 0 before / 1 at / 2 after, then its
+    // place in that list -- created: pushed onto "at"
+    this.list = 1;
+    this.listOrder = this.created;
+  }
+  /** the next stamp of a list push (at / after) */
+  static pushStamp() {
+    return ++refCreated;
   }
   addProperties(newProps) {
     this.properties = Object.assign({}, this.properties || {}, newProps);
@@ -632,8 +641,8 @@ class BatchClient {
         const kd = flat[5 * i + 1];
         if ((kd & 0xff) >= DELTA_SLIDE && (kd & 0xff) < 2 * DELTA_SLIDE) {
           // a reference slid off a removed-and-acked segment (MTE_DELTA_SLIDE)
-          (slides || (slides = [])).push({ slot: flat[5 * i + 4], pos: flat[5 * i + 2] | 0, seg: flat[5 * i + 3],
-            moves: (kd & 1) !== 0, off: kd >>> 16 });
+          (slides || (slides = [])).push({ slot: flat[5 * i + 4], pos: flat[5 * i + 2] | 0, seg: flat[5 * i + 3] | 0,
+            moves: (kd & 1) !== 0, after: (kd & 2) !== 0, off: kd >>> 16, at: slides ? slides.length : 0 });
           i++;
           continue;
         }

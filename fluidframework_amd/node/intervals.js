@@ -585,15 +585,20 @@ class IntervalCollection {
    *  message by message while the collection holds intervals, so the engine's
    *  state is the state right after this op).  The reference calls each
    *  sliding end's beforeSlide / afterSlide (localReference.ts:436-447,
-   *  471-480, mergeTree.ts:936-942), which for an interval end are the
+   *  471-480, mergeTree.ts:921-950), which for an interval end are the
    *  collection's position-change listeners (addIntervalListeners,
-   *  intervalCollection.ts:1023-1058): one "changeInterval" per end that slid,
-   *  local = true and no op (attachGraph's onPositionChange -> emitChange,
-   *  :1350-1353), in the order the segments' reference lists are walked --
-   *  segment by segment, by offset, then list order (here creation order).
-   *  previousInterval holds the ends as they were (Transient clones: a removed
-   *  segment's position), the interval the ends as they are at that moment: an
-   *  end that slides later in the same op still sits on its removed segment. */
+   *  intervalCollection.ts:1023-1058): the interval leaves the index, its end
+   *  moves, it is re-added and one "changeInterval" is raised, local = true and
+   *  no op (attachGraph's onPositionChange -> emitChange, :1350-1353).
+   *  The engine reports the removed segments in the order the reference slides
+   *  them (a remote remove's overlapped segments, then its new ones; an ack's
+   *  segments one by one, a reference sliding again off a later one), each
+   *  segment's references together; within a segment the reference walks its
+   *  LocalReferenceCollection -- by offset, then the before / at / after lists
+   *  in list order (localReference.ts:181-215), which the ends' list places
+   *  track.  previousInterval holds the ends as they were (Transient clones: a
+   *  removed segment's position), the interval the ends as they are at that
+   *  moment: an end that slides later in the same op still sits where it was. */
   _onSlides(slides) {
     if (this.byId.size === 0) return;
     const owner = new Map();  // slot -> [interval, 0 start | 1 end]
@@ -603,51 +608,84 @@ class IntervalCollection {
     }
     const mine = slides.filter((r) => owner.has(r.slot));
     if (mine.length === 0) return;
-    // the walk's order: the units the ends left, in document order (r.seg: the
-    // unit's order key after the op, -1 once the zamboni took it -- then the
-    // engine's report order), then list order (creation)
     const ref = (r) => { const [x, w] = owner.get(r.slot); return w ? x.end : x.start; };
-    const at = new Map(mine.map((r, i) => [r, i]));
-    mine.sort((a, b) => ((a.seg >= 0 && b.seg >= 0) ? (a.seg - b.seg) : (at.get(a) - at.get(b))) ||
-      (ref(a).created - ref(b).created));
+    // runs of one removed segment each, in the engine's order (r.seg: the unit
+    // the end left, as an order key after the op, so r.seg - r.off keys its
+    // segment; -1 once the zamboni took it)
+    const runs = [];
+    let run = null, runId;
+    for (const r of mine) {
+      const id = r.seg >= 0 ? r.seg - r.off : -2 - r.pos;
+      if (!run || id !== runId) {
+        run = [];
+        runs.push(run);
+        runId = id;
+      }
+      run.push(r);
+    }
     const c = this.client;
-    // every end's position now (after the op) and, for the ends that slide, at their turn
     const now = (lref) => c.localReferencePositionToPosition(lref);
-    const after = new Map();
-    for (const r of mine) after.set(r.slot, now(ref(r)));
-    const pending = new Map(mine.map((r) => [r.slot, r.pos]));  // still on its removed segment
+    // each sliding end's records in order: where it sits before each one
+    const queue = new Map();
+    for (const r of mine) {
+      if (!queue.has(r.slot)) queue.set(r.slot, []);
+      queue.get(r.slot).push(r);
+    }
+    const posNow = new Map();
+    for (const [slot, q] of queue) posNow.set(slot, q[0].pos);
     // the end tree compares the ends as they stand at each slide: an end still
-    // to slide keeps the key of the unit it sits on (pinned), one that slid its
-    // key after the op
+    // to slide keeps the key of the unit it sits on (pinned)
     const touched = new Set(mine.map((r) => owner.get(r.slot)[0]));
     for (const x of touched) x._pinKeys = x._keys();
-    for (const r of mine) if (r.seg >= 0) owner.get(r.slot)[0]._pinKeys[owner.get(r.slot)[1]] = r.seg;
+    for (const [slot, q] of queue) if (q[0].seg >= 0) owner.get(slot)[0]._pinKeys[owner.get(slot)[1]] = q[0].seg;
+    const watch = this._has("changeInterval");
     try {
-      for (const r of mine) {
-        const [ival, which] = owner.get(r.slot);
-        pending.delete(r.slot);
-        // the other end: on its removed segment if it slides later in this op
-        const other = which ? ival.start : ival.end;
-        const otherPos = pending.has(other.slot) ? pending.get(other.slot) : now(other);
-        const prevStart = which ? otherPos : r.pos, prevEnd = which ? r.pos : otherPos;
-        const curStart = which ? otherPos : after.get(r.slot), curEnd = which ? after.get(r.slot) : otherPos;
-        // beforeSlide removes the interval from the index (removeIntervalFromIndex, :1042-1047)
-        this.endTree.remove(ival);
-        ival._pinKeys[which] = c._refOrder(which ? ival.end : ival.start);
-        // afterSlide re-adds it (addIntervalToIndex), then onPositionChange (:1048-1053)
-        ival.stamp = ++this.stamp;
-        this.endTree.put(ival, ival);
-        if (this._has("changeInterval")) {
-          const snap = (p) => ({ snapshot: true, position: p, refType: RefType.Transient });
-          const prev = new SequenceInterval(this, snap(prevStart), snap(prevEnd), ival.intervalType);
-          prev.properties = Object.assign({}, ival.properties);
-          ival.start.pinned = curStart;
-          ival.end.pinned = curEnd;
-          try {
-            this._emit("changeInterval", ival, prev, true, undefined);
-          } finally {
-            delete ival.start.pinned;
-            delete ival.end.pinned;
+      for (const seg of runs) {
+        seg.sort((a, b) => (a.off - b.off) || (ref(a).list - ref(b).list) || (ref(a).listOrder - ref(b).listOrder));
+        let base = null, idx = 0;
+        for (const r of seg) {
+          const [ival, which] = owner.get(r.slot);
+          const lref = ref(r);
+          const q = queue.get(r.slot);
+          q.shift();
+          const at = posNow.get(r.slot);
+          const next = q.length ? q[0].pos : now(lref);
+          const other = which ? ival.start : ival.end;
+          const otherPos = posNow.has(other.slot) ? posNow.get(other.slot) : now(other);
+          // beforeSlide: out of the index (removeIntervalFromIndex, :1042-1047)
+          this.endTree.remove(ival);
+          posNow.set(r.slot, next);
+          ival._pinKeys[which] = q.length && q[0].seg >= 0 ? q[0].seg : c._refOrder(lref);
+          // its place among the new segment's references: addBeforeTombstones
+          // puts one segment's references, in order, in front of offset 0's
+          // before list; addAfterTombstones pushes them onto the last offset's
+          // after list (localReference.ts:422-485)
+          if (r.moves) {
+            if (r.after) {
+              lref.list = 2;
+              lref.listOrder = lref.constructor.pushStamp();
+            } else {
+              if (base === null) base = -lref.constructor.pushStamp() * 65536;
+              lref.list = 0;
+              lref.listOrder = base + idx++;
+            }
+          }
+          // afterSlide: back in (addIntervalToIndex), then onPositionChange (:1048-1053)
+          ival.stamp = ++this.stamp;
+          this.endTree.put(ival, ival);
+          if (watch) {
+            const snap = (p) => ({ snapshot: true, position: p, refType: RefType.Transient });
+            const prev = new SequenceInterval(this, snap(which ? otherPos : at), snap(which ? at : otherPos),
+              ival.intervalType);
+            prev.properties = Object.assign({}, ival.properties);
+            ival.start.pinned = which ? otherPos : next;
+            ival.end.pinned = which ? next : otherPos;
+            try {
+              this._emit("changeInterval", ival, prev, true, undefined);
+            } finally {
+              delete ival.start.pinned;
+              delete ival.end.pinned;
+            }
           }
         }
       }

@@ -126,10 +126,13 @@ extern "C" {
  * segment that became removed and acked (slideAckedRemovedSegmentReferences,
  * mergeTree.ts:921-950, after a remote remove or an ack) or came off it for
  * want of a segment to slide to: one record per reference, in the order of the
- * segments it left; pos = the own-view position of that segment, len = its
- * index among the document's held segments (telling apart removed neighbours
- * at one position), removed = the reference's slot, kind = MTE_DELTA_SLIDE | 1 when it moved onto a segment |
- * its offset in the segment it left << 16 (clamped to 0xffff).  The reference
+ * segments it left; pos = the own-view position of that segment, len = the
+ * order key of the unit it left once the message is applied (the held units
+ * before it, as mte_read_ref_order counts them; -1 if the zamboni took it),
+ * removed = the reference's slot, kind = MTE_DELTA_SLIDE | 1 when it moved onto
+ * a segment | 2 when that is the end of a preceding one (addAfterTombstones;
+ * else offset 0 of a following one, addBeforeTombstones) | its offset in the
+ * segment it left << 16 (clamped to 0xffff).  The reference
  * calls the reference's beforeSlide / afterSlide callbacks at each of them
  * (localReference.ts:436-447, 471-480): an interval collection's "changeInterval"
  * events raised mid-op (intervalCollection.ts:1042-1053). */

@@ -671,9 +671,10 @@ static inline int removed_and_acked(const item* g) { return g->rseq != NONE_SEQ 
 /* where a reference on item i slides to (forwardExcursion / backwardExcursion,
  * client.ts:1117-1130): offset 0 of the first following segment, else the last
  * unit of the last preceding one; -1: nowhere */
-static int64_t slide_to(const idoc* d, uint32_t i, uint32_t* anchor) {
+static int64_t slide_to_grp(const idoc* d, uint32_t i, uint32_t* anchor, int32_t grp) {
   for (uint32_t j = i + 1; j < d->n; j++)
-    if (slide_target_ok(&d->it[j])) {
+    if (slide_target_ok(&d->it[j]) ||
+        (grp && d->it[j].rseq == grp && !d->it[j].empty && d->it[j].seq < LOCAL_BASE)) {
       *anchor = d->it[j].toff;
       return j;
     }
@@ -684,6 +685,7 @@ static int64_t slide_to(const idoc* d, uint32_t i, uint32_t* anchor) {
     }
   return -1;
 }
+static int64_t slide_to(const idoc* d, uint32_t i, uint32_t* anchor) { return slide_to_grp(d, i, anchor, 0); }
 
 static int ref_reserve(idoc* d, uint32_t slot) {
   if (slot < d->ref_cap) return MTE_OK;
@@ -1007,14 +1009,20 @@ static int doc_ref(idoc* d, const mte_op* op) {
  * the reference's beforeSlide / afterSlide callbacks, localReference.ts:436-447) */
 static int delta_push(idoc* d, uint32_t kind, int64_t pos, int32_t len, uint32_t removed);
 static int64_t own_prefix(const idoc* d, uint32_t at);
-static int doc_slide_refs(idoc* d, int32_t s) {
+/* mode (mte_stream.h stream_slide): 0 every such item; 1 the removals of one
+ * ack, in order, each slid while the later ones are still pending
+ * (ackPendingSegment, mergeTree.ts:1285-1304: a reference can slide again);
+ * 2 / 3 a remote remove's items the local client had removed already (lrs),
+ * slid before its delta callback, then the newly removed ones (:1970-1993) */
+static int doc_slide_refs(idoc* d, int32_t s, int mode) {
   if (!(d->flags & MTE_DOC_REFS) || !d->ref_hi) return MTE_OK;
   const int evd = (d->flags & MTE_DOC_EVENTS) != 0;
   for (uint32_t i = 0; i < d->n; i++) {
     const item* g = &d->it[i];
     if (g->rseq != s || g->empty) continue;
+    if (mode >= 2 && (g->lrs != 0) != (mode == 2)) continue;
     uint32_t to = 0;
-    const int64_t t = slide_to(d, i, &to);
+    const int64_t t = slide_to_grp(d, i, &to, mode == 1 ? s : 0);
     const int64_t xpos = evd ? own_prefix(d, i) : 0;
     for (uint32_t r = 0; r < d->ref_hi; r++) {
       const uint32_t st = d->ref_state[r];
@@ -1027,7 +1035,8 @@ static int doc_slide_refs(idoc* d, int32_t s) {
       else d->ref_state[r] = st | REF_DETACHED | (t < 0 ? REF_OFF : 0u);
       if (evd) {
         /* len: the unit it left, made its order key once the message is done (slide_keys) */
-        const int rc = delta_push(d, MTE_DELTA_SLIDE | (moves ? 1u : 0u) | ((off < 0xffffu ? off : 0xffffu) << 16), xpos,
+        const int rc = delta_push(d, MTE_DELTA_SLIDE | (moves ? 1u : 0u) | (moves && t < (int64_t)i ? 2u : 0u) |
+                                         ((off < 0xffffu ? off : 0xffffu) << 16), xpos,
                                   (int32_t)left, r);
         if (rc) return rc;
       }
@@ -1447,7 +1456,7 @@ static int doc_ack(idoc* d, const mte_op* op, const env_t* env) {
       }
       if (member && !g->cont && (rc = add_lru(d, i, s))) return rc;
     }
-    if ((rc = doc_slide_refs(d, s))) return rc;
+    if ((rc = doc_slide_refs(d, s, lo == hi ? 1 : 0))) return rc;
     zamboni(d, env->arena, env->n_keys);
   }
   return MTE_OK;
@@ -1515,7 +1524,7 @@ static int doc_apply_op(idoc* d, const mte_op* op, const env_t* env) {
     if ((rc = check_op_window(d, op))) return rc;
   } else if (op->type == MTE_OP_REMOVE || op->type == MTE_OP_ANNOTATE) {
     if ((rc = tree_range(d, op, env, 0))) return rc;
-    if (op->type == MTE_OP_REMOVE && (rc = doc_slide_refs(d, s))) return rc;
+    if (op->type == MTE_OP_REMOVE && ((rc = doc_slide_refs(d, s, 2)) || (rc = doc_slide_refs(d, s, 3)))) return rc;
     zamboni(d, env->arena, env->n_keys);
     if ((rc = check_op_window(d, op))) return rc;
   } else if (op->type == MTE_OP_ACK) {
