@@ -178,7 +178,7 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
   }
   if (in.flags & MTE_DOC_LOCAL_CLIENT) {  // nothing pending (mte_htree.h planes)
     const uint32_t nz = n_img ? n_img : 1u;
-    for (uint32_t k = 0; k < 2 * kt + 2; k++)
+    for (uint32_t k = 0; k < 2 * kt + 3; k++)
       for (uint32_t x = 0; x < nz; x++) soa.props[(kt + k) * soa.plane_stride + (uint64_t)d * cap + x] = 0u;
   }
   if (n_img) return;  // image_kernel writes the segments
@@ -908,7 +908,7 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
     }
     if (c->n_htree) {
       // LDS residency: (nP + 5) words per item (mte_htree.h ht_to_lds), whole wavefronts' worth
-      const uint32_t words = (uint32_t)(kFieldPlanes + 3 * K + 2 + 5);
+      const uint32_t words = (uint32_t)(kFieldPlanes + 3 * K + 3 + 5);
       uint32_t lcap = c->htree_lds >= 8 ? (c->htree_lds / 4 - 2) / words / kWave * kWave : 0u;
       if (lcap > c->cap) lcap = c->cap / kWave * kWave;
       const uint32_t* order = c->hord_ok_s[c->rslot] ? c->d_hord_s[c->rslot] : c->d_htree_docs;
@@ -1296,10 +1296,10 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     if (docs[d].flags & MTE_DOC_REFS) c->h_refs[d] = 1, any_refs = true;
   }
   if (any_refs) HIPCHK(c, hipMalloc((void**)&c->d_refs, sizeof(uint2) * (size_t)c->ref_cap * n_docs));
-  // documents with a local client hold 2 kt + 1 more planes (mte_stream.h): the
-  // pending property keys, the annotate-group mask and the keys' values before
-  // their first pending annotate
-  const uint64_t prop_planes = (c->kt ? c->kt : 1) + (any_local ? 2 * c->kt + 2 : 0);  // + localRemovedSeq
+  // documents with a local client hold 2 kt + 3 more planes (mte_htree.h): the
+  // pending property keys, the annotate-group mask, the keys' values before
+  // their first pending annotate, localRemovedSeq and the removal-group order
+  const uint64_t prop_planes = (c->kt ? c->kt : 1) + (any_local ? 2 * c->kt + 3 : 0);  // + localRemovedSeq, group order
   HIPCHK(c, hipMalloc((void**)&c->hdr, sizeof(DocHdr) * (n_docs ? n_docs : 1)));
   // one allocation, planes at stride nslots: len seq rseq rmask meta toff props[kt]
   // (kt >= n_keys planes, so the register-resident kernels never index past it)

@@ -80,6 +80,11 @@ template <int K> constexpr int kLrsPlane = kFieldPlanes + 3 * K + 1;
 // segment from its group -- it keeps the value, the group no longer holds it
 // (resetPendingDeltaToOps, client.ts:802-857; titems.c LRS_RELEASED)
 constexpr uint32_t kLrsReleased = 0x40000000u;
+// kGrpPlane: the item's place in its pending removal group (SegmentGroup.segments,
+// the order an ack walks them, mergeTree.ts:1285): its index at the local
+// remove, 0x80000000 | the tail's id for a tail split off later (splitAt's
+// segmentGroups.copyTo appends it, mergeTreeNodes.ts:505-534; titems.c gord)
+template <int K> constexpr int kGrpPlane = kFieldPlanes + 3 * K + 2;
 
 struct HT {
   uint32_t* pl;   // the document's plane base
@@ -857,6 +862,7 @@ __device__ __forceinline__ int ht_boundary(HT& h, int32_t pos, uint32_t (&st)[kN
   ht_setpl(h, 0, i, (uint32_t)off);
   ht_setpl(h, 0, i + 1, len - (uint32_t)off);
   ht_setpl(h, 5, i + 1, toff + (uint32_t)off);
+  if (h.ldoc) ht_setpl(h, kGrpPlane<K>, i + 1, 0x80000000u | h.next_id);
   ht_setT(h, i + 1, (t & (kTPo | kTNl)) | (h.next_id++ << 8));
   vm_drain();
   ht_inval(h, i);
@@ -1100,6 +1106,7 @@ __device__ __forceinline__ int ht_range(HT& h, const s8v& op, bool local, const 
           h.pl[2 * h.sd + i] = (uint32_t)(kLocalBase + s);
           h.pl[3 * h.sd + i] = 1u;
           h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = (uint32_t)s;
+          h.pl[(uint64_t)kGrpPlane<K> * h.sd + i] = (uint32_t)i;
         } else {
           const uint32_t rm = ld_l2(h.pl + 3 * h.sd + i);
           if (rs[j] == kNone) {
@@ -1245,7 +1252,9 @@ __device__ __forceinline__ int ht_ack(HT& h, const s8v& op, const ReplayArgs& a,
         }
       }
     }
-    if (rt && rhi) stream_slide(h.pl, h.sd, h.n, rt, rhi, s, ev, lo == hi ? kSlideAck : kSlideAll);
+    if (rt && rhi)
+      stream_slide(h.pl, h.sd, h.n, rt, rhi, s, ev, lo == hi ? kSlideAck : kSlideAll,
+                   h.pl + (uint64_t)kGrpPlane<K> * h.sd);
     if ((rc = ht_zamboni<K>(h, a.n_keys))) return rc;
   }
   return 0;
@@ -2052,7 +2061,7 @@ __global__ __launch_bounds__(64) void htree_kernel(ReplayArgs a, HtreeArgs t) {
   h.hp = reinterpret_cast<uint32_t*>(t.heap + (uint64_t)doc * (t.hcap + 1));
   h.hcap = t.hcap;
   h.cap = (int)a.cap;
-  h.nP = ldoc ? kFieldPlanes + 3 * K + 2 : kFieldPlanes + K;
+  h.nP = ldoc ? kFieldPlanes + 3 * K + 3 : kFieldPlanes + K;
   h.n = D.n;
   h.newcalc = (hf & MTE_DOC_NEW_LENGTH_CALC) != 0;
   h.ldoc = ldoc;

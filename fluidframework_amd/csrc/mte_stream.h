@@ -125,17 +125,19 @@ __device__ __forceinline__ bool slide_ok(int32_t sq, int32_t rs) { return sq < k
 
 // the first slot a reference may slide to after x (dir > 0) or before it
 // (dir < 0), or -1; x is wave-uniform.  grp != 0: the removals of one ack
-// (removedSeq grp) are acked segment by segment, so the ones after x are still
-// pending when x's references slide (ackPendingSegment, mergeTree.ts:1285-1304)
+// (removedSeq grp) are acked segment by segment in group order (gp: the
+// group-order plane), so the ones after `cur` in it are still pending when x's
+// references slide (ackPendingSegment, mergeTree.ts:1285-1304)
 __device__ __forceinline__ int find_slide_target(const uint32_t* pl, uint64_t sd, int n, int x, int dir,
-                                                 int32_t grp = 0) {
+                                                 int32_t grp = 0, const uint32_t* gp = nullptr, uint32_t cur = 0) {
   const int l = lane_id();
   if (dir > 0) {
     for (int b = x + 1; b < n; b += kWave) {
       const int i = b + l;
       const int ic = i < n ? i : 0;  // unconditional loads, selected after
       const int32_t sq = (int32_t)ld_l2(pl + sd + ic), rs = (int32_t)ld_l2(pl + 2 * sd + ic);
-      const uint64_t m = __ballot(i < n && (slide_ok(sq, rs) || (grp != 0 && rs == grp && sq < kLocalBase)));
+      const bool pend = grp != 0 && rs == grp && sq < kLocalBase && ld_l2(gp + ic) > cur;
+      const uint64_t m = __ballot(i < n && (slide_ok(sq, rs) || pend));
       if (m) return b + __ffsll((long long)m) - 1;
     }
   } else {
@@ -143,7 +145,8 @@ __device__ __forceinline__ int find_slide_target(const uint32_t* pl, uint64_t sd
       const int i = e - kWave + l;
       const int ic = i >= 0 ? i : 0;
       const int32_t sq = (int32_t)ld_l2(pl + sd + ic), rs = (int32_t)ld_l2(pl + 2 * sd + ic);
-      const uint64_t m = __ballot(i >= 0 && slide_ok(sq, rs));
+      const bool pend = grp != 0 && rs == grp && sq < kLocalBase && ld_l2(gp + ic) > cur;
+      const uint64_t m = __ballot(i >= 0 && (slide_ok(sq, rs) || pend));
       if (m) return e - kWave + (63 - __builtin_clzll(m));
     }
   }
@@ -171,17 +174,95 @@ __device__ __forceinline__ int find_slide_target(const uint32_t* pl, uint64_t sd
 // the removed segment << 16 (clamped):
 // the host orders one segment's references as its LocalReferenceCollection
 // iterates them.
-// mode: kSlideAll every such segment; kSlideAck the removals of one ack, in
-// order, each slid while the later ones are still pending (a reference can
-// slide again from a later one: one record per slide); kSlideOverlap /
-// kSlideNew a remote remove's segments that the local client had removed
-// already (lrp: the local-removal plane, non-zero) -- slid before the delta
-// callback -- then the newly removed ones, after it (mergeTree.ts:1970-1993).
 enum { kSlideAll = 0, kSlideAck = 1, kSlideOverlap = 2, kSlideNew = 3 };
+// one removed segment x's references (grp / gp / cur: find_slide_target)
+__device__ __forceinline__ void slide_segment(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t rhi, int x,
+                                              EvOut* ev, int32_t grp, const uint32_t* gp, uint32_t cur) {
+  const int l = lane_id();
+  const uint32_t toff = uni(ld_l2(pl + 5 * sd + x)), len = uni(ld_l2(pl + x));
+  int t = find_slide_target(pl, sd, n, x, 1, grp, gp, cur);
+  bool after = false;
+  if (t < 0) {
+    t = find_slide_target(pl, sd, n, x, -1, grp, gp, cur);
+    after = t >= 0;
+  }
+  uint32_t to = 0;
+  if (t >= 0) {
+    const uint32_t tt = uni(ld_l2(pl + 5 * sd + t)), tl = uni(ld_l2(pl + t));
+    to = after ? tt + tl - 1u : tt;
+  }
+  const int32_t xpos = ev ? own_prefix(pl, sd, x) : 0;
+  for (uint32_t rb = 0; rb < rhi; rb += kWave) {
+    const uint32_t r = rb + (uint32_t)l;
+    const uint32_t rc = r < rhi ? r : 0u;  // unconditional loads, selected after
+    const uint32_t anc = ld_l2(&rt[rc].x), st = ld_l2(&rt[rc].y);
+    const bool hit = r < rhi && (st & kRefLive) && !(st & (kRefDetached | MTE_REF_STAY_ON_REMOVE)) && anc - toff < len;
+    const bool moves = (st & MTE_REF_SLIDE_ON_REMOVE) && t >= 0;
+    if (hit) {
+      if (moves) rt[r].x = to;
+      else rt[r].y = st | kRefDetached | (t < 0 ? kRefOff : 0u);
+    }
+    if (ev) {
+      const uint64_t hm = __ballot(hit);
+      if (hm) {
+        const uint32_t idx = ev->n + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+        const uint32_t off = anc - toff < 0xffffu ? anc - toff : 0xffffu;
+        if (hit && idx < ev->cap)
+          ev->p[idx] = mte_delta{ev->op, MTE_DELTA_SLIDE | (moves ? 1u : 0u) | (moves && after ? 2u : 0u) | (off << 16), xpos,
+                                 (int32_t)anc, r};
+        ev->n += (uint32_t)__popcll(hm);
+      }
+    }
+  }
+  vm_drain();
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t w = (uint32_t)__shfl_xor((int)v, o);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+// mode: kSlideAll every such segment; kSlideAck the removals of one ack in
+// group order (gp: the group-order plane), each slid while the later ones are
+// still pending (a reference can slide again from a later one: one record per
+// slide); kSlideOverlap / kSlideNew a remote remove's segments that the local
+// client had removed already (lrp: the local-removal plane, non-zero) -- slid
+// before the delta callback -- then the newly removed ones, after it
+// (mergeTree.ts:1970-1993).  lrp: the local-removal plane (overlap modes) or
+// the group-order plane (kSlideAck).
 __device__ __forceinline__ void stream_slide(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t rhi, int32_t s,
                                              EvOut* ev = nullptr, int mode = kSlideAll,
                                              const uint32_t* lrp = nullptr) {
   const int l = lane_id();
+  if (mode == kSlideAck) {
+    const uint32_t* gp = lrp;
+    uint32_t cur = 0;
+    for (bool first = true;; first = false) {
+      // the group's next segment: the lowest order above cur among removedSeq s
+      uint32_t best = 0xffffffffu;
+      int bx = -1;
+      for (int tb = 0; tb < n; tb += kWave) {
+        const int i = tb + l;
+        const int ic = i < n ? i : 0;
+        const int32_t rs = (int32_t)ld_l2(pl + 2 * sd + ic);
+        const uint32_t g = ld_l2(gp + ic);
+        const bool c = i < n && rs == s && (first || g > cur);
+        const uint32_t mn = wave_min_u32(c ? g : 0xffffffffu);
+        const uint64_t at = __ballot(c && g == mn);
+        if (at && (bx < 0 || mn < best)) {
+          best = mn;
+          bx = tb + __ffsll((long long)at) - 1;
+        }
+      }
+      if (bx < 0) return;
+      cur = best;
+      slide_segment(pl, sd, n, rt, rhi, bx, ev, s, gp, cur);
+    }
+  }
   for (int tb = 0; tb < n; tb += kWave) {
     const int i = tb + l;
     const int ic = i < n ? i : 0;
@@ -191,42 +272,7 @@ __device__ __forceinline__ void stream_slide(const uint32_t* pl, uint64_t sd, in
     while (m) {
       const int x = tb + __ffsll((long long)m) - 1;
       m &= m - 1;
-      const uint32_t toff = uni(ld_l2(pl + 5 * sd + x)), len = uni(ld_l2(pl + x));
-      int t = find_slide_target(pl, sd, n, x, 1, mode == kSlideAck ? s : 0);
-      bool after = false;
-      if (t < 0) {
-        t = find_slide_target(pl, sd, n, x, -1);
-        after = t >= 0;
-      }
-      uint32_t to = 0;
-      if (t >= 0) {
-        const uint32_t tt = uni(ld_l2(pl + 5 * sd + t)), tl = uni(ld_l2(pl + t));
-        to = after ? tt + tl - 1u : tt;
-      }
-      const int32_t xpos = ev ? own_prefix(pl, sd, x) : 0;
-      for (uint32_t rb = 0; rb < rhi; rb += kWave) {
-        const uint32_t r = rb + (uint32_t)l;
-        const uint32_t rc = r < rhi ? r : 0u;  // unconditional loads, selected after
-        const uint32_t anc = ld_l2(&rt[rc].x), st = ld_l2(&rt[rc].y);
-        const bool hit = r < rhi && (st & kRefLive) && !(st & (kRefDetached | MTE_REF_STAY_ON_REMOVE)) && anc - toff < len;
-        const bool moves = (st & MTE_REF_SLIDE_ON_REMOVE) && t >= 0;
-        if (hit) {
-          if (moves) rt[r].x = to;
-          else rt[r].y = st | kRefDetached | (t < 0 ? kRefOff : 0u);
-        }
-        if (ev) {
-          const uint64_t hm = __ballot(hit);
-          if (hm) {
-            const uint32_t idx = ev->n + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
-            const uint32_t off = anc - toff < 0xffffu ? anc - toff : 0xffffu;
-            if (hit && idx < ev->cap)
-              ev->p[idx] = mte_delta{ev->op, MTE_DELTA_SLIDE | (moves ? 1u : 0u) | (moves && after ? 2u : 0u) | (off << 16), xpos,
-                                     (int32_t)anc, r};
-            ev->n += (uint32_t)__popcll(hm);
-          }
-        }
-      }
-      vm_drain();
+      slide_segment(pl, sd, n, rt, rhi, x, ev, 0, nullptr, 0u);
     }
   }
 }

@@ -669,6 +669,7 @@ class BatchClient {
   /** The references one op slid (MTE_DELTA_SLIDE records, in the order of the
    *  segments they left) -> the interval collections' position listeners. */
   _slid(slides) {
+    if (this.onSlideRecords) this.onSlideRecords(slides);  // a test hook (tests/node/interval_farm.js trace)
     if (!this.intervalCollections) return;
     for (const c of this.intervalCollections.values()) c._onSlides(slides);
   }

@@ -568,6 +568,14 @@ class IntervalCollection {
     if (!this.pendingStart.has(id) && stay(ival.start)) this.client._setRefSlide(ival.start, slide(ival.start));
     if (!this.pendingEnd.has(id) && stay(ival.end)) this.client._setRefSlide(ival.end, slide(ival.end));
     const after = ival._keys();
+    // an end that moved is a new reference there (createPositionReferenceFromSegoff,
+    // :1862-1890): pushed onto its offset's "at" list
+    for (const w of [0, 1]) {
+      if (after[w] === before[w]) continue;
+      const r = w ? ival.end : ival.start;
+      r.list = 1;
+      r.listOrder = r.constructor.pushStamp();
+    }
     if (after[0] !== before[0] || after[1] !== before[1]) {
       // removeExistingInterval (with the ends as they were) + add (:1862-1899)
       ival._pinKeys = before;

@@ -55,6 +55,41 @@ const { Marker } = require(path.join(refdir, "mergeTreeNodes.js"));
 const { MergeTreeTextHelper } = require(path.join(refdir, "MergeTreeTextHelper.js"));
 const iv = require(path.join(refdir, "sequence", "intervalCollection.js"));
 
+// MTE_REF_TRACE=<client name>: that client's reference slides on stderr (each
+// removed-and-acked segment whose references slide: its text, ordinal, the
+// references at each offset; each ack's pending group in order) -- a debugging
+// aid for the slide order the Node host restates
+if (process.env.MTE_REF_TRACE) {
+  const { MergeTree } = require(path.join(refdir, "mergeTree.js"));
+  const who = process.env.MTE_REF_TRACE;
+  const mine = (mt) => mt.collabWindow && mt.collabWindow.clientId === 0 && mt.__traceName === who;
+  const refName = (r) => {
+    const ivl = r.properties && r.properties.interval;
+    const id = ivl && ivl.properties ? ivl.properties.intervalId : "?";
+    return `${id}.${ivl && ivl.start === r ? "s" : ivl && ivl.end === r ? "e" : "x"}:${r.refType}`;
+  };
+  const segName = (sg) => `${sg.text !== undefined ? JSON.stringify(sg.text) : "M"}@${sg.ordinal}` +
+    `[seq ${sg.seq} rs ${sg.removedSeq} lrs ${sg.localRemovedSeq}]`;
+  const slide = MergeTree.prototype.slideAckedRemovedSegmentReferences;
+  MergeTree.prototype.slideAckedRemovedSegmentReferences = function (segment) {
+    if (this.__traceName === who && segment.localRefs && !segment.localRefs.empty) {
+      const refs = [];
+      for (const r of segment.localRefs) refs.push(`${refName(r)}@${r.getOffset()}`);
+      process.stderr.write(`  slide ${segName(segment)} refs ${refs.join(" ")}\n`);
+    }
+    return slide.call(this, segment);
+  };
+  const ack = MergeTree.prototype.ackPendingSegment;
+  MergeTree.prototype.ackPendingSegment = function (opArgs) {
+    if (this.__traceName === who && this.pendingSegments && this.pendingSegments.first) {
+      const g = this.pendingSegments.first.data;
+      process.stderr.write(`  ack seq ${opArgs.sequencedMessage.sequenceNumber} group ${g.segments.map(segName).join(" ")}\n`);
+    }
+    return ack.call(this, opArgs);
+  };
+  void mine;
+}
+
 function specToSegment(spec) {
   const t = TextSegment.fromJSONObject(spec);
   if (t) return t;
@@ -164,6 +199,7 @@ function runSet(p) {
     const c = new Client(specToSegment, logger, { mergeTreeUseNewLengthCalculations: true });
     if (p.initialText) c.insertSegmentLocal(0, new TextSegment(p.initialText));
     c.startOrUpdateCollaboration(n);
+    c._mergeTree.__traceName = n;  // MTE_REF_TRACE
     const emitter = { emit(opName, _prev, params, meta) { sent[i] = { opName, value: clone(params), meta }; } };
     const coll = factory.load(emitter, []);
     coll.attachGraph(c, LABEL);

@@ -68,6 +68,12 @@ typedef struct {
   int32_t lrs; /* localRemovedSeq; | LRS_RELEASED once a regeneration dequeued the
                  segment from its group (it keeps the value, the group no longer
                  holds it: resetPendingDeltaToOps, client.ts:802-857) */
+  /* the item's place in its pending removal group (SegmentGroup.segments, the
+   * order an ack walks them, mergeTree.ts:1285): the doc index at the local
+   * remove for the segments it marked, 0x80000000 | the new item's id for a
+   * tail split off later (splitAt's segmentGroups.copyTo appends it,
+   * mergeTreeNodes.ts:505-534) */
+  uint32_t gord;
 } item;
 
 typedef struct {
@@ -573,6 +579,7 @@ static int boundary(idoc* d, int64_t pos) {
       tl->h = 0;
       tl->cont = 0;
       tl->id = new_id(d);
+      tl->gord = 0x80000000u | tl->id;
       d->written += 2;
       hd->len = off;
       d->L[i] = off;
@@ -671,21 +678,23 @@ static inline int removed_and_acked(const item* g) { return g->rseq != NONE_SEQ 
 /* where a reference on item i slides to (forwardExcursion / backwardExcursion,
  * client.ts:1117-1130): offset 0 of the first following segment, else the last
  * unit of the last preceding one; -1: nowhere */
-static int64_t slide_to_grp(const idoc* d, uint32_t i, uint32_t* anchor, int32_t grp) {
+static inline int grp_pending(const item* g, int32_t grp, uint32_t cur) {
+  return grp && g->rseq == grp && !g->empty && g->seq < LOCAL_BASE && g->gord > cur;
+}
+static int64_t slide_to_grp(const idoc* d, uint32_t i, uint32_t* anchor, int32_t grp, uint32_t cur) {
   for (uint32_t j = i + 1; j < d->n; j++)
-    if (slide_target_ok(&d->it[j]) ||
-        (grp && d->it[j].rseq == grp && !d->it[j].empty && d->it[j].seq < LOCAL_BASE)) {
+    if (slide_target_ok(&d->it[j]) || grp_pending(&d->it[j], grp, cur)) {
       *anchor = d->it[j].toff;
       return j;
     }
   for (int64_t j = (int64_t)i - 1; j >= 0; j--)
-    if (slide_target_ok(&d->it[j])) {
+    if (slide_target_ok(&d->it[j]) || grp_pending(&d->it[j], grp, cur)) {
       *anchor = d->it[j].toff + (uint32_t)d->it[j].len - 1u;
       return j;
     }
   return -1;
 }
-static int64_t slide_to(const idoc* d, uint32_t i, uint32_t* anchor) { return slide_to_grp(d, i, anchor, 0); }
+static int64_t slide_to(const idoc* d, uint32_t i, uint32_t* anchor) { return slide_to_grp(d, i, anchor, 0, 0); }
 
 static int ref_reserve(idoc* d, uint32_t slot) {
   if (slot < d->ref_cap) return MTE_OK;
@@ -1014,33 +1023,54 @@ static int64_t own_prefix(const idoc* d, uint32_t at);
  * (ackPendingSegment, mergeTree.ts:1285-1304: a reference can slide again);
  * 2 / 3 a remote remove's items the local client had removed already (lrs),
  * slid before its delta callback, then the newly removed ones (:1970-1993) */
+static int slide_item_refs(idoc* d, uint32_t i, int32_t grp, uint32_t cur, int evd) {
+  const item* g = &d->it[i];
+  uint32_t to = 0;
+  const int64_t t = slide_to_grp(d, i, &to, grp, cur);
+  const int64_t xpos = evd ? own_prefix(d, i) : 0;
+  for (uint32_t r = 0; r < d->ref_hi; r++) {
+    const uint32_t st = d->ref_state[r];
+    if (!(st & REF_LIVE) || (st & REF_DETACHED) || (st & MTE_REF_STAY_ON_REMOVE)) continue;
+    const uint32_t off = d->ref_anchor[r] - g->toff;
+    if (off >= (uint32_t)g->len) continue;
+    const int moves = (st & MTE_REF_SLIDE_ON_REMOVE) && t >= 0;
+    const uint32_t left = d->ref_anchor[r];
+    if (moves) d->ref_anchor[r] = to;
+    else d->ref_state[r] = st | REF_DETACHED | (t < 0 ? REF_OFF : 0u);
+    if (evd) {
+      /* len: the unit it left, made its order key once the message is done (slide_keys) */
+      const int rc = delta_push(d, MTE_DELTA_SLIDE | (moves ? 1u : 0u) | (moves && t < (int64_t)i ? 2u : 0u) |
+                                         ((off < 0xffffu ? off : 0xffffu) << 16), xpos,
+                                (int32_t)left, r);
+      if (rc) return rc;
+    }
+  }
+  return MTE_OK;
+}
 static int doc_slide_refs(idoc* d, int32_t s, int mode) {
   if (!(d->flags & MTE_DOC_REFS) || !d->ref_hi) return MTE_OK;
   const int evd = (d->flags & MTE_DOC_EVENTS) != 0;
+  int rc;
+  if (mode == 1) {
+    /* the group's segments in group order, each slid while the later ones are pending */
+    uint32_t cur = 0;
+    for (int first = 1;; first = 0) {
+      int64_t bx = -1;
+      for (uint32_t i = 0; i < d->n; i++) {
+        const item* g = &d->it[i];
+        if (g->rseq != s || g->empty || (!first && g->gord <= cur)) continue;
+        if (bx < 0 || g->gord < d->it[bx].gord) bx = i;
+      }
+      if (bx < 0) return MTE_OK;
+      cur = d->it[bx].gord;
+      if ((rc = slide_item_refs(d, (uint32_t)bx, s, cur, evd))) return rc;
+    }
+  }
   for (uint32_t i = 0; i < d->n; i++) {
     const item* g = &d->it[i];
     if (g->rseq != s || g->empty) continue;
     if (mode >= 2 && (g->lrs != 0) != (mode == 2)) continue;
-    uint32_t to = 0;
-    const int64_t t = slide_to_grp(d, i, &to, mode == 1 ? s : 0);
-    const int64_t xpos = evd ? own_prefix(d, i) : 0;
-    for (uint32_t r = 0; r < d->ref_hi; r++) {
-      const uint32_t st = d->ref_state[r];
-      if (!(st & REF_LIVE) || (st & REF_DETACHED) || (st & MTE_REF_STAY_ON_REMOVE)) continue;
-      const uint32_t off = d->ref_anchor[r] - g->toff;
-      if (off >= (uint32_t)g->len) continue;
-      const int moves = (st & MTE_REF_SLIDE_ON_REMOVE) && t >= 0;
-      const uint32_t left = d->ref_anchor[r];
-      if (moves) d->ref_anchor[r] = to;
-      else d->ref_state[r] = st | REF_DETACHED | (t < 0 ? REF_OFF : 0u);
-      if (evd) {
-        /* len: the unit it left, made its order key once the message is done (slide_keys) */
-        const int rc = delta_push(d, MTE_DELTA_SLIDE | (moves ? 1u : 0u) | (moves && t < (int64_t)i ? 2u : 0u) |
-                                         ((off < 0xffffu ? off : 0xffffu) << 16), xpos,
-                                  (int32_t)left, r);
-        if (rc) return rc;
-      }
-    }
+    if ((rc = slide_item_refs(d, i, 0, 0, evd))) return rc;
   }
   return MTE_OK;
 }
@@ -1201,6 +1231,7 @@ static int tree_range(idoc* d, const mte_op* op, const env_t* env, int local) {
         g->rseq = LOCAL_BASE + s;
         g->rmask = 1u;
         g->lrs = s;
+        g->gord = i;
       } else if (g->rseq == NONE_SEQ) {
         g->rseq = s;
         g->rmask = 1u << c;

@@ -90,6 +90,12 @@ for (let si = 0; si < nSets; si++) {
       L.coll.on("propertyChanged", (x, deltas, local, op) => L.ev.push(["props", x.getIntervalId(), local, !!op,
         sortKeys(clone(deltas)), false]));
     }
+    // MTE_FARM_TRACE="set,client": that client's steps, slide records and
+    // events on stderr, with the reference's events at each checkpoint
+    if (process.env.MTE_FARM_TRACE === `${si},${ci}`) {
+      L.trace = true;
+      L.client.onSlideRecords = (sl) => process.stderr.write("  slides " + JSON.stringify(sl) + "\n");
+    }
     layout.push(L);
   });
 }
@@ -121,6 +127,10 @@ for (let j = 0; j < nCp; j++) {
     for (const [kind, li] of s.events[L.ci].slice(prev[d], done)) {
      try {
       const m = typeof li === "number" ? s.log[li] : [null, 0, 0, 0, kind === "H" ? "op" : "iv", li];
+      if (L.trace) {
+        process.stderr.write(`${kind} ${JSON.stringify(m)}\n`);
+        if (L.ev) process.stderr.write("  ev-so-far " + L.ev.length + "\n");
+      }
       const msg = { clientId: m[0], sequenceNumber: m[1], referenceSequenceNumber: m[2], minimumSequenceNumber: m[3],
         type: "op", contents: m[5] };
       if (kind === "A") {
@@ -224,6 +234,10 @@ for (let j = 0; j < nCp; j++) {
     const text = L.client.getText();
     let ok = text === want.text && JSON.stringify(ivs) === JSON.stringify(want.intervals);
     if (!ok) failures.push([L.si, L.ci, j, "state", ivs.slice(0, 3), want.intervals.slice(0, 3)]);
+    if (L.trace) {
+      process.stderr.write(`== checkpoint ${j}\n got  ${JSON.stringify(L.ev)}\n want ${JSON.stringify(want.events)}\n`);
+      process.stderr.write(` intervals ${JSON.stringify(want.intervals)}\n`);
+    }
     if (ext && ok) {
       const ids = (xs) => xs.map((x) => x.getIntervalId());
       const evWant = want.events;
