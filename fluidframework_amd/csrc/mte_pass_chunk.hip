@@ -1,4 +1,6 @@
 // The chunked pass (mte_chunk.h) in its own translation unit.
+#include <cstdio>
+
 #include "mte_passes.h"
 #include "mte_chunk.h"
 #include "mte_round.h"
@@ -24,6 +26,16 @@ hipError_t launch_round_plan(const ReplayArgs& a, const RoundArgs& rd, uint32_t 
 template <int K>
 hipError_t launch_round_run(const ReplayArgs& a, const ChunkArgs& ch, const RoundArgs& rd, uint32_t,
                             hipStream_t s) {
+#if MTE_RND_DIAG
+  {  // the counters so far (diagnostic builds)
+    unsigned long long h[16] = {};
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_rnd_diag), sizeof h) == hipSuccess)
+      fprintf(stderr,
+              "rnd_diag blocks %llu serial %llu ops %llu clk_block %llu clk_gather %llu clk_serial %llu recs %llu "
+              "back %llu find %llu fwd %llu out %llu\n",
+              h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10]);
+  }
+#endif
   const uint32_t n_docs = rd.nd;  // this launch's slice of the documents
   const uint32_t tpd = (a.cap + kT - 1) / kT;  // flat tiles per document
   const uint64_t tiles = (uint64_t)n_docs * tpd, chunks = (uint64_t)n_docs * ch.nch_cap;

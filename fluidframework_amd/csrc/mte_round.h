@@ -60,6 +60,28 @@
 
 namespace mte {
 
+// diagnostic builds (tools/variants.sh ...:"-DMTE_RND_DIAG=1"): per resolve
+// [0] blocks, [1] blocks sent op by op, [2] ops, [3] clocks in blocks,
+// [4] clocks gathering, [5] clocks in the serial fallback, in rnd_block [6]
+// to the records, [7] back pass, [8] search, [9] forward pass, [10] outputs
+// and fold; printed per launch
+#ifndef MTE_RND_DIAG
+#define MTE_RND_DIAG 0
+#endif
+#if MTE_RND_DIAG
+__device__ unsigned long long g_rnd_diag[16];
+#define RND_DIAG(i, v) \
+  do {                                                                           \
+    if (lane_id() == 0) atomicAdd(&g_rnd_diag[i], (unsigned long long)(v));     \
+  } while (0)
+#define RND_CLK(t) const long long t = clock64()
+#else
+#define RND_DIAG(i, v) \
+  do {                 \
+  } while (0)
+#define RND_CLK(t)
+#endif
+
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // one workgroup per document: its 8 waves scan the records from the cursor
@@ -516,6 +538,7 @@ __device__ __forceinline__ void col_add_at(const Col& C, int i, int32_t d) {
 __device__ __forceinline__ bool rnd_block(const Col& C, int nb, uint32_t k, uint32_t w3, int32_t pos1, int32_t pos2,
                                           uint4* list, uint32_t& m, uint32_t cap_c, bool& failed) {
   if (m + 2u * (uint32_t)nb > cap_c) return false;  // at most two sub-ops an op; else op by op, checked
+  RND_CLK(c0);
   const int l = lane_id();
   const bool v = l < nb;
   const uint32_t type = w3 & 0xffu;
@@ -526,32 +549,37 @@ __device__ __forceinline__ bool rnd_block(const Col& C, int nb, uint32_t k, uint
   const int32_t tp = ins ? pos1 : b1;
   const int32_t tn = ins ? (nlen > 0 ? nlen : 0) : (rem ? b1 - b2 : 0);
   int32_t y = ins ? pos1 - 1 : b1;
-  for (int j = nb - 2; j >= 0; j--) {
-    const int32_t nj = rdlane(tn, j);
-    if (nj == 0) continue;
-    const int32_t pj = rdlane(tp, j);
-    if (v && l > j && y >= pj) y = nj < 0 ? y - nj : (y >= pj + nj ? y - nj : pj - 1);
+#if MTE_RND_DIAG
+  y = __builtin_amdgcn_readfirstlane(0) + y;  // (the records are in)
+#endif
+  RND_CLK(c1);
+  // Straight-line passes over the earlier ops (no branch: an annotate is the
+  // identity of both forms), the lanes after j taking op j; n = the units an
+  // insert adds, r = the units a remove takes (one of them 0).
+  // back, latest first: y -> y if y < p; y + r - n if y >= p + n; p - 1 otherwise
+  // (a fixed 63 steps: the lanes past the block hold the identity, tn = 0)
+#pragma unroll 7
+  for (int j = kWave - 2; j >= 0; j--) {
+    const int32_t tj = rdlane(tn, j), pj = rdlane(tp, j);
+    const int32_t nj = tj > 0 ? tj : 0, rj = tj < 0 ? -tj : 0;
+    const int32_t y1 = y >= pj + nj ? y + rj - nj : pj - 1;
+    y = (l > j && y >= pj) ? y1 : y;
   }
+  RND_CLK(c2);
   const ColPos P = col_find_lane(C, y, v);
   const bool found = v && P.c < C.nch;
   int32_t bm = P.bm, bc = P.bc, bn = P.bn;
-  for (int j = 0; j + 1 < nb; j++) {
-    const int32_t nj = rdlane(tn, j);
-    if (nj == 0) continue;
-    const int32_t pj = rdlane(tp, j);
-    if (found && l > j) {
-      if (nj > 0) {
-        bm += pj <= bm ? nj : 0;
-        bc += pj <= bc ? nj : 0;
-        bn += pj <= bn ? nj : 0;
-      } else {
-        const int32_t e = pj - nj;
-        bm = bm <= pj ? bm : (bm < e ? pj : bm + nj);
-        bc = bc <= pj ? bc : (bc < e ? pj : bc + nj);
-        bn = bn <= pj ? bn : (bn < e ? pj : bn + nj);
-      }
-    }
+  RND_CLK(c3);
+  // forward: B -> B + n if p <= B; B - clamp(B - p, 0, r)
+#pragma unroll 7
+  for (int j = 0; j < kWave - 1; j++) {
+    const int32_t tj = rdlane(tn, j), pj = rdlane(tp, j);
+    const int32_t a = (l > j && tj > 0) ? tj : 0, r = (l > j && tj < 0) ? -tj : 0;
+    bm += (pj <= bm ? a : 0) - min(max(bm - pj, 0), r);
+    bc += (pj <= bc ? a : 0) - min(max(bc - pj, 0), r);
+    bn += (pj <= bn ? a : 0) - min(max(bn - pj, 0), r);
   }
+  RND_CLK(c4);
   const int c = P.c;
   const int32_t st = c == 0 ? 0 : bm;
   bool s0 = false, s1 = false, more = false, bad = false;
@@ -597,6 +625,11 @@ __device__ __forceinline__ bool rnd_block(const Col& C, int nb, uint32_t k, uint
     col_add_at(C, rdlane(c, t) + 1, rdlane(d1, t));
   }
   fence_wave();
+  RND_DIAG(6, c1 - c0);
+  RND_DIAG(7, c2 - c1);
+  RND_DIAG(8, c3 - c2);
+  RND_DIAG(9, c4 - c3);
+  RND_DIAG(10, clock64() - c4);
   return true;
 }
 
@@ -682,6 +715,7 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
         cw[q] = r < nops ? reinterpret_cast<const uint32_t*>(recp + 2 * r)[3] : 0xffffffffu;
       }
       for (uint32_t sb = 0; sb < nops && !failed; sb += 8 * kWave) {
+        RND_CLK(tg0);
         const bool last = sb + 8 * kWave >= nops;
 #pragma unroll
         for (int q = 0; q < 8; q++) {
@@ -696,7 +730,9 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
           tail += (uint32_t)__popcll(mine);
         }
         fence_wave();
+        RND_DIAG(4, clock64() - tg0);
         while (!failed && (tail - head >= (uint32_t)kWave || (last && tail > head))) {
+          RND_CLK(tb0);
           const int nb = tail - head < (uint32_t)kWave ? (int)(tail - head) : kWave;
           uint32_t k = 0, w3 = 0;
           int32_t p1 = 0, p2 = 0;
@@ -707,11 +743,18 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
             p1 = (int32_t)rp[4];
             p2 = (int32_t)rp[5];
           }
-          if (!rnd_block(C, nb, k, w3, p1, p2, list + off, m, cap_c, failed)) {
+          const bool par = rnd_block(C, nb, k, w3, p1, p2, list + off, m, cap_c, failed);
+          RND_CLK(tb1);
+          if (!par) {
             for (int t = 0; t < nb && !failed; t++)
               failed = !rnd_serial_op(C, rdlane(k, t), rdlane(w3, t), rdlane(p1, t), rdlane(p2, t), list + off, m,
                                       cap_c);
+            RND_DIAG(1, 1);
+            RND_DIAG(5, clock64() - tb1);
           }
+          RND_DIAG(0, 1);
+          RND_DIAG(2, nb);
+          RND_DIAG(3, tb1 - tb0);
           head += (uint32_t)nb;
         }
 #pragma unroll
