@@ -1186,8 +1186,8 @@ __device__ __forceinline__ int ht_range(HT& h, const s8v& op, bool local, const 
   h.lp_n = 0;  // the marks changed lengths
   if (rem && !local && rt && rhi) {
     const uint32_t* lrp = h.pl + (uint64_t)kLrsPlane<K> * h.sd;
-    stream_slide(h.pl, h.sd, h.n, rt, rhi, s, evd ? &ev : nullptr, kSlideOverlap, lrp);
-    stream_slide(h.pl, h.sd, h.n, rt, rhi, s, evd ? &ev : nullptr, kSlideNew, lrp);
+    stream_slide(h.pl, h.sd, h.n, rt, rhi, s, evd ? &ev : nullptr, kSlideOverlap, lrp, h.tw);
+    stream_slide(h.pl, h.sd, h.n, rt, rhi, s, evd ? &ev : nullptr, kSlideNew, lrp, h.tw);
   }
   return 0;
 }
@@ -1254,7 +1254,7 @@ __device__ __forceinline__ int ht_ack(HT& h, const s8v& op, const ReplayArgs& a,
     }
     if (rt && rhi)
       stream_slide(h.pl, h.sd, h.n, rt, rhi, s, ev, lo == hi ? kSlideAck : kSlideAll,
-                   h.pl + (uint64_t)kGrpPlane<K> * h.sd);
+                   h.pl + (uint64_t)kGrpPlane<K> * h.sd, h.tw);
     if ((rc = ht_zamboni<K>(h, a.n_keys))) return rc;
   }
   return 0;

@@ -83,6 +83,11 @@ __device__ unsigned long long g_rnd_diag[16];
 #endif
 
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// the resolve's column and ring live in the wave's own LDS, whose operations
+// complete in issue order: ordering them needs a compiler barrier and the LDS
+// counter only -- not fence_wave's vmcnt(0), which would wait out the sub-op
+// list stores and the records in flight
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // one workgroup per document: its 8 waves scan the records from the cursor
 // in interleaved batches of 64 for the first op that ends the run
@@ -400,7 +405,7 @@ __device__ __forceinline__ bool rnd_serial_op(const Col& C, uint32_t k, uint32_t
     if (l == 0) list[m] = make_uint4((uint32_t)h.i, k, (uint32_t)h.excl, 0u);
     m++;
     if (nlen > 0) col_add(C, h, nlen);
-    fence_wave();
+    lds_fence();
     return true;
   }
   const int32_t b1 = pos1 < pos2 ? pos1 : pos2, b2 = pos1 < pos2 ? pos2 : pos1;
@@ -435,14 +440,14 @@ __device__ __forceinline__ bool rnd_serial_op(const Col& C, uint32_t k, uint32_t
         if (type == MTE_OP_REMOVE && hm) {
           const int32_t lo = b1 > st ? b1 : st, hi = b2 < incl ? b2 : incl;
           col_sub_row(C, gg, ci, hit ? hi - lo : 0);
-          fence_wave();
+          lds_fence();
         }
         eg = gend;
         if (gend >= b2) break;
       }
     }
   }
-  fence_wave();
+  lds_fence();
   return true;
 }
 
@@ -624,7 +629,7 @@ __device__ __forceinline__ bool rnd_block(const Col& C, int nb, uint32_t k, uint
     const int t = __ffsll((long long)e) - 1;
     col_add_at(C, rdlane(c, t) + 1, rdlane(d1, t));
   }
-  fence_wave();
+  lds_fence();
   RND_DIAG(6, c1 - c0);
   RND_DIAG(7, c2 - c1);
   RND_DIAG(8, c3 - c2);
@@ -687,7 +692,7 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
         if (i < C.nch) C.CI[i] = incl;
         if (l == 0) C.GS[g] = rdlane(incl, kWave - 1);  // the group's total, for now
       }
-      fence_wave();
+      lds_fence();
       for (int sg = 0; sg < C.nsg; sg++) {
         const int g = sg * kWave + l;
         const int32_t v = g < C.ng ? C.GS[g] : 0;
@@ -695,13 +700,13 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
         if (g < C.ng) C.GS[g] = incl;
         if (l == 0) C.SS[sg] = rdlane(incl, kWave - 1);
       }
-      fence_wave();
+      lds_fence();
       {
         const int32_t v = l < C.nsg ? C.SS[l] : 0;
         const int32_t incl = wave_incl_scan(v);
         if (l < C.nsg) C.SS[l] = incl;
       }
-      fence_wave();
+      lds_fence();
       uint32_t m = 0;  // entries in the chain's list
       bool failed = false;
       // the chain's ops in blocks of 64: the records' client bytes 512 at a time
@@ -729,7 +734,7 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
           if ((mine >> l) & 1ull) ring[(tail + lanes_below(mine)) & (kRing - 1)] = r;
           tail += (uint32_t)__popcll(mine);
         }
-        fence_wave();
+        lds_fence();
         RND_DIAG(4, clock64() - tg0);
         while (!failed && (tail - head >= (uint32_t)kWave || (last && tail > head))) {
           RND_CLK(tb0);

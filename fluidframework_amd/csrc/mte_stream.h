@@ -22,6 +22,7 @@
 #pragma once
 
 #include "mte_replay.h"
+#include "mte_tree.h"
 
 namespace mte {
 
@@ -128,11 +129,17 @@ __device__ __forceinline__ bool slide_ok(int32_t sq, int32_t rs) { return sq < k
 // (removedSeq grp) are acked segment by segment in group order (gp: the
 // group-order plane), so the ones after `cur` in it are still pending when x's
 // references slide (ackPendingSegment, mergeTree.ts:1285-1304)
+// tw (the tree words, or nullptr): a merged leaf's items are one segment, so
+// the search starts past x's leaf (its kTCont continuations / its head)
 __device__ __forceinline__ int find_slide_target(const uint32_t* pl, uint64_t sd, int n, int x, int dir,
-                                                 int32_t grp = 0, const uint32_t* gp = nullptr, uint32_t cur = 0) {
+                                                 int32_t grp = 0, const uint32_t* gp = nullptr, uint32_t cur = 0,
+                                                 const uint32_t* tw = nullptr) {
   const int l = lane_id();
   if (dir > 0) {
-    for (int b = x + 1; b < n; b += kWave) {
+    int b0 = x + 1;
+    if (tw)
+      while (b0 < n && (uni(ld_l2(tw + b0)) & kTCont)) b0++;
+    for (int b = b0; b < n; b += kWave) {
       const int i = b + l;
       const int ic = i < n ? i : 0;  // unconditional loads, selected after
       const int32_t sq = (int32_t)ld_l2(pl + sd + ic), rs = (int32_t)ld_l2(pl + 2 * sd + ic);
@@ -141,7 +148,10 @@ __device__ __forceinline__ int find_slide_target(const uint32_t* pl, uint64_t sd
       if (m) return b + __ffsll((long long)m) - 1;
     }
   } else {
-    for (int e = x; e > 0; e -= kWave) {  // slots [e - 64, e)
+    int e0 = x;
+    if (tw)
+      while (e0 > 0 && (uni(ld_l2(tw + e0)) & kTCont)) e0--;
+    for (int e = e0; e > 0; e -= kWave) {  // slots [e - 64, e)
       const int i = e - kWave + l;
       const int ic = i >= 0 ? i : 0;
       const int32_t sq = (int32_t)ld_l2(pl + sd + ic), rs = (int32_t)ld_l2(pl + 2 * sd + ic);
@@ -177,13 +187,19 @@ __device__ __forceinline__ int find_slide_target(const uint32_t* pl, uint64_t sd
 enum { kSlideAll = 0, kSlideAck = 1, kSlideOverlap = 2, kSlideNew = 3 };
 // one removed segment x's references (grp / gp / cur: find_slide_target)
 __device__ __forceinline__ void slide_segment(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t rhi, int x,
-                                              EvOut* ev, int32_t grp, const uint32_t* gp, uint32_t cur) {
+                                              EvOut* ev, int32_t grp, const uint32_t* gp, uint32_t cur,
+                                              const uint32_t* tw) {
   const int l = lane_id();
   const uint32_t toff = uni(ld_l2(pl + 5 * sd + x)), len = uni(ld_l2(pl + x));
-  int t = find_slide_target(pl, sd, n, x, 1, grp, gp, cur);
+  // an item continuing a merged leaf is one segment with the items before it:
+  // offsets count from the leaf's first unit
+  uint32_t lead = 0;
+  if (tw)
+    for (int y = x; y > 0 && (uni(ld_l2(tw + y)) & kTCont); y--) lead += uni(ld_l2(pl + y - 1));
+  int t = find_slide_target(pl, sd, n, x, 1, grp, gp, cur, tw);
   bool after = false;
   if (t < 0) {
-    t = find_slide_target(pl, sd, n, x, -1, grp, gp, cur);
+    t = find_slide_target(pl, sd, n, x, -1, grp, gp, cur, tw);
     after = t >= 0;
   }
   uint32_t to = 0;
@@ -206,7 +222,7 @@ __device__ __forceinline__ void slide_segment(const uint32_t* pl, uint64_t sd, i
       const uint64_t hm = __ballot(hit);
       if (hm) {
         const uint32_t idx = ev->n + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
-        const uint32_t off = anc - toff < 0xffffu ? anc - toff : 0xffffu;
+        const uint32_t off = lead + (anc - toff) < 0xffffu ? lead + (anc - toff) : 0xffffu;
         if (hit && idx < ev->cap)
           ev->p[idx] = mte_delta{ev->op, MTE_DELTA_SLIDE | (moves ? 1u : 0u) | (moves && after ? 2u : 0u) | (off << 16), xpos,
                                  (int32_t)anc, r};
@@ -236,7 +252,7 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // the group-order plane (kSlideAck).
 __device__ __forceinline__ void stream_slide(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t rhi, int32_t s,
                                              EvOut* ev = nullptr, int mode = kSlideAll,
-                                             const uint32_t* lrp = nullptr) {
+                                             const uint32_t* lrp = nullptr, const uint32_t* tw = nullptr) {
   const int l = lane_id();
   if (mode == kSlideAck) {
     const uint32_t* gp = lrp;
@@ -260,7 +276,7 @@ __device__ __forceinline__ void stream_slide(const uint32_t* pl, uint64_t sd, in
       }
       if (bx < 0) return;
       cur = best;
-      slide_segment(pl, sd, n, rt, rhi, bx, ev, s, gp, cur);
+      slide_segment(pl, sd, n, rt, rhi, bx, ev, s, gp, cur, tw);
     }
   }
   for (int tb = 0; tb < n; tb += kWave) {
@@ -272,7 +288,7 @@ __device__ __forceinline__ void stream_slide(const uint32_t* pl, uint64_t sd, in
     while (m) {
       const int x = tb + __ffsll((long long)m) - 1;
       m &= m - 1;
-      slide_segment(pl, sd, n, rt, rhi, x, ev, 0, nullptr, 0u);
+      slide_segment(pl, sd, n, rt, rhi, x, ev, 0, nullptr, 0u, tw);
     }
   }
 }

@@ -620,6 +620,7 @@ class IntervalCollection {
     // runs of one removed segment each, in the engine's order (r.seg: the unit
     // the end left, as an order key after the op, so r.seg - r.off keys its
     // segment; -1 once the zamboni took it)
+    // (r.off counts from the segment's first unit, a merged leaf's items too)
     const runs = [];
     let run = null, runId;
     for (const r of mine) {

@@ -132,7 +132,8 @@ extern "C" {
  * removed = the reference's slot, kind = MTE_DELTA_SLIDE | 1 when it moved onto
  * a segment | 2 when that is the end of a preceding one (addAfterTombstones;
  * else offset 0 of a following one, addBeforeTombstones) | its offset in the
- * segment it left << 16 (clamped to 0xffff).  The reference
+ * segment it left << 16 (clamped to 0xffff; a merged leaf's items are one
+ * segment, offsets counted from its first unit).  The reference
  * calls the reference's beforeSlide / afterSlide callbacks at each of them
  * (localReference.ts:436-447, 471-480): an interval collection's "changeInterval"
  * events raised mid-op (intervalCollection.ts:1042-1053). */

@@ -682,12 +682,17 @@ static inline int grp_pending(const item* g, int32_t grp, uint32_t cur) {
   return grp && g->rseq == grp && !g->empty && g->seq < LOCAL_BASE && g->gord > cur;
 }
 static int64_t slide_to_grp(const idoc* d, uint32_t i, uint32_t* anchor, int32_t grp, uint32_t cur) {
-  for (uint32_t j = i + 1; j < d->n; j++)
+  /* a merged leaf's items are one segment: search past i's leaf */
+  uint32_t j0 = i + 1;
+  while (j0 < d->n && d->it[j0].cont) j0++;
+  for (uint32_t j = j0; j < d->n; j++)
     if (slide_target_ok(&d->it[j]) || grp_pending(&d->it[j], grp, cur)) {
       *anchor = d->it[j].toff;
       return j;
     }
-  for (int64_t j = (int64_t)i - 1; j >= 0; j--)
+  int64_t h0 = i;
+  while (h0 > 0 && d->it[h0].cont) h0--;
+  for (int64_t j = h0 - 1; j >= 0; j--)
     if (slide_target_ok(&d->it[j]) || grp_pending(&d->it[j], grp, cur)) {
       *anchor = d->it[j].toff + (uint32_t)d->it[j].len - 1u;
       return j;
@@ -1039,8 +1044,12 @@ static int slide_item_refs(idoc* d, uint32_t i, int32_t grp, uint32_t cur, int e
     else d->ref_state[r] = st | REF_DETACHED | (t < 0 ? REF_OFF : 0u);
     if (evd) {
       /* len: the unit it left, made its order key once the message is done (slide_keys) */
+      /* offsets count from the merged leaf's first unit (its items are one segment) */
+      uint32_t lead = 0;
+      for (uint32_t y = i; y > 0 && d->it[y].cont; y--) lead += (uint32_t)d->it[y - 1].len;
+      const uint32_t lo = lead + off;
       const int rc = delta_push(d, MTE_DELTA_SLIDE | (moves ? 1u : 0u) | (moves && t < (int64_t)i ? 2u : 0u) |
-                                         ((off < 0xffffu ? off : 0xffffu) << 16), xpos,
+                                         ((lo < 0xffffu ? lo : 0xffffu) << 16), xpos,
                                 (int32_t)left, r);
       if (rc) return rc;
     }
