@@ -807,48 +807,50 @@ __global__ __launch_bounds__(256) void rnd_apply_kernel(ReplayArgs a, ChunkArgs 
   if (doc >= (int)(rd.d0 + rd.nd)) return;
   const uint4 p = rd.plan[doc];
   if (p.x != kModeRound || rd.rflag[doc] != 0u || i >= (int)rd.nch[doc]) return;
+  // everything the chunk needs, issued together: its sub-op count and bucket,
+  // its segment count and planes; then each sub-op's record (bucket order)
   const uint32_t nb = rd.rcnt[(uint64_t)doc * ch.nch_cap + i];
-  if (nb == 0u) return;
-  const uint2 e = l < (int)nb ? rd.rbuf[((uint64_t)doc * ch.nch_cap + i) * kRB + l] : make_uint2(0xffffffffu, 0u);
-  // sort the bucket by op index: each entry's rank, then a push to that lane
-  uint32_t rank = 0;
-  for (uint32_t j = 0; j < nb; j++) rank += rdlane(e.x, (int)j) < e.x ? 1u : 0u;
-  const int dst = (l < (int)nb ? (int)rank : l) << 2;
-  const uint32_t ks = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)e.x);
-  const int32_t exs = __builtin_amdgcn_ds_permute(dst, (int)e.y);
-  // every sub-op's record at once: lane j loads the j-th one (in op order)
-  const uint4* recp = a.recs + 2 * (a.op_off[doc] + p.y);
-  uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0;
-  if (l < (int)nb) {
-    r0 = recp[2 * ks];
-    r1 = recp[2 * ks + 1];
-  }
+  const uint2 e0 = rd.rbuf[((uint64_t)doc * ch.nch_cap + i) * kRB + (l < kRB ? l : 0)];
   uint32_t* cntp = ch.cnt + (uint64_t)doc * ch.nch_cap;
   int ni = (int)cntp[i];
+  const int n_before = ni;
   const uint64_t x0 = ch_slot(ch, doc, i);
   Regs<kChE, K> R;
   ch_load<K>(R, ch, x0, ni);
+  if (nb == 0u) return;
+  const uint2 e = l < (int)nb ? e0 : make_uint2(0xffffffffu, 0u);
+  const uint4* recp = a.recs + 2 * (a.op_off[doc] + p.y);
+  uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0;
+  if (l < (int)nb) {
+    r0 = recp[2 * e.x];
+    r1 = recp[2 * e.x + 1];
+  }
+  // the bucket in op order: each entry's rank, and per rank the lane holding it
+  uint32_t rank = 0;
+  for (uint32_t j = 0; j < nb; j++) rank += rdlane(e.x, (int)j) < e.x ? 1u : 0u;
+  const int dst = (l < (int)nb ? (int)rank : l) << 2;
+  const int from = __builtin_amdgcn_ds_permute(dst, l);
   uint32_t st[kNumStats] = {};
   const int32_t M = (int32_t)p.w;
   int rcs = 0;
   for (uint32_t j = 0; j < nb; j++) {
-    const int32_t ex = rdlane(exs, (int)j);
+    const int q = rdlane(from, (int)j);
+    const int32_t ex = (int32_t)rdlane(e.y, q);
     s8v op;
-    op[0] = (int32_t)rdlane(r0.x, (int)j);
-    op[1] = (int32_t)rdlane(r0.y, (int)j);
-    op[2] = (int32_t)rdlane(r0.z, (int)j);
-    op[3] = (int32_t)rdlane(r0.w, (int)j);
-    op[4] = (int32_t)rdlane(r1.x, (int)j);
-    op[5] = (int32_t)rdlane(r1.y, (int)j);
-    op[6] = (int32_t)rdlane(r1.z, (int)j);
-    op[7] = (int32_t)rdlane(r1.w, (int)j);
+    op[0] = (int32_t)rdlane(r0.x, q);
+    op[1] = (int32_t)rdlane(r0.y, q);
+    op[2] = (int32_t)rdlane(r0.z, q);
+    op[3] = (int32_t)rdlane(r0.w, q);
+    op[4] = (int32_t)rdlane(r1.x, q);
+    op[5] = (int32_t)rdlane(r1.y, q);
+    op[6] = (int32_t)rdlane(r1.z, q);
+    op[7] = (int32_t)rdlane(r1.w, q);
     const uint32_t w3 = (uint32_t)op[3];
     int32_t tot = 0, dlen = 0;
     const int rc = seg_op_v<kChE, K, false, true>(R, ni, op, w3 & 0xffu, (w3 >> 8) & 0xffu, w3 >> 16, M, true, ex,
                                                   true, tot, dlen, a, st);
     rcs = rc != 0 ? rc : rcs;
   }
-  const int n_before = (int)cntp[i];
   ch_store<K>(R, ch, x0, ni);
   if (l == 0) {
     // the chunk's sub-ops (record + bucket entry), its planes in and out, its count
