@@ -90,7 +90,8 @@ class Interner {
     this.valueJson = [null];
     this.numIds = new Map();
     this.strIds = new Map();
-    this.keyVals = new Map();  // key -> the value ids it was ever given (combining ops' domain)
+    // per value index, the keys it was ever given (bit k): the combining ops' domain
+    this.keyMask = new Uint32Array(256);
   }
   /** [key, value id] of one property, noting the value under its key */
   kv(name, v) {
@@ -100,9 +101,21 @@ class Interner {
   }
   /** value id `id` was given to key `k` (the combining ops' domain) */
   noteValue(k, id) {
-    let set = this.keyVals.get(k);
-    if (set === undefined) this.keyVals.set(k, (set = new Set()));
-    set.add(id);
+    const x = id & ~VALUE_UNEQUAL;
+    if (x >= this.keyMask.length) {
+      const m = new Uint32Array(Math.max(x + 1, this.keyMask.length * 2));
+      m.set(this.keyMask);
+      this.keyMask = m;
+    }
+    this.keyMask[x] |= 1 << k;
+  }
+  /** the value ids key k was ever given, ascending */
+  domainOf(k) {
+    const out = [], b = 1 << k, M = this.keyMask;
+    for (let x = 1; x < this.valueJson.length && x < M.length; x++) {
+      if (M[x] & b) out.push((x | (this.valueJson[x] === "NaN" ? VALUE_UNEQUAL : 0)) >>> 0);
+    }
+    return out;
   }
   key(name) {
     let k = this.keys.get(name);
@@ -274,7 +287,7 @@ class PropTable {
     const first = this.entries.length / 2;
     for (const name of Object.keys(props)) {
       const k = it.key(name);
-      const dom = Array.from(it.keyVals.get(k) || []).sort((x, y) => x - y);
+      const dom = it.domainOf(k).sort((x, y) => x - y);
       dom.push(0);
       const pairs = [];
       for (const old of dom) {
@@ -284,13 +297,7 @@ class PropTable {
         const nid = nv === undefined ? 0 : it.value(nv);
         if (nid !== old) pairs.push(old, nid);
       }
-      for (let q = 1; q < pairs.length; q += 2) {
-        if (pairs[q]) {
-          let set = it.keyVals.get(k);
-          if (set === undefined) it.keyVals.set(k, (set = new Set()));
-          set.add(pairs[q]);
-        }
-      }
+      for (let q = 1; q < pairs.length; q += 2) if (pairs[q]) it.noteValue(k, pairs[q]);
       this.entries.push(k, pairs.length / 2);
       for (let q = 0; q < pairs.length; q += 2) this.entries.push((pairs[q] | COMBINE_PAIR) >>> 0, pairs[q + 1]);
     }
@@ -394,6 +401,12 @@ class BatchBuilder {
   }
 
   _text(s) {
+    const off = this._textOff(s);
+    return [off, s.length];
+  }
+
+  /** s's UTF-16 units appended to the batch text; their offset */
+  _textOff(s) {
     if (typeof s !== "string") throw new MergeTreeError(E_INVALID_ARG, "text must be a string");
     const off = this.textUnits, n = s.length;
     if (off + n > this.textBuf.length) {
@@ -406,7 +419,7 @@ class BatchBuilder {
     const T = this.textBuf;
     for (let i = 0; i < n; i++) T[off + i] = s.charCodeAt(i);  // UTF-16 code units (textSegment.ts:52-55)
     this.textUnits = off + n;
-    return [off, n];
+    return off;
   }
 
   /** Client.applyMsg(msg, local=false) for one document (client.ts:918-935). */
@@ -520,14 +533,14 @@ class BatchBuilder {
       }
       const pos = checkI32(op.pos1 === undefined ? 0 : op.pos1, "pos1");
       if (typeof seg === "string") {
-        const off = this._text(seg)[0];
+        const off = this._textOff(seg);
         this._put(doc, seq, ref, msn, OP_INSERT, 0, 0, pos, seg.length, off, NO_PROPS);
       } else if (typeof seg === "object" && "text" in seg) {
-        const tx = this._text(seg.text);
-        this._put(doc, seq, ref, msn, OP_INSERT, 0, 0, pos, tx[1], tx[0], this.props.add(seg.props));
+        const off = this._textOff(seg.text);
+        this._put(doc, seq, ref, msn, OP_INSERT, 0, 0, pos, seg.text.length, off, this.props.add(seg.props));
       } else if (typeof seg === "object" && "marker" in seg) {
         const rt = checkI32(seg.marker.refType === undefined ? 0 : seg.marker.refType, "refType");
-        const off = this._text("\ufffc")[0];  // one reserved unit names the marker in MTE_DOC_REFS documents
+        const off = this._textOff("\ufffc");  // one reserved unit names the marker in MTE_DOC_REFS documents
         this._put(doc, seq, ref, msn, OP_INSERT, 0, F_MARKER, pos, rt, off, this.props.add(seg.props));
       } else {
         throw new MergeTreeError(E_INVALID_ARG, "Unrecognized IJSONSegment type: " + JSON.stringify(seg));
