@@ -43,7 +43,7 @@ struct RoundArgs {
 // entries, mte_round.h rnd_resolve_kernel) fits this much LDS
 constexpr uint32_t kRoundLdsMax = 150u * 1024u;
 inline uint64_t rnd_resolve_lds(uint32_t nch_cap, uint32_t ng_cap) {
-  return (uint64_t)(nch_cap + (ng_cap + 63) / 64 * 64 + 64 + 1024) * 4u;  // + the staging ring (kRing)
+  return (uint64_t)(nch_cap + 2 * ((ng_cap + 63) / 64 * 64) + 64 + 1024) * 4u;  // + GD rows, the staging ring (kRing)
 }
 
 // the tree pass over the legacy documents (mte_tree.h): `rounds` of TIER 0

@@ -321,6 +321,7 @@ struct Col {
   int32_t* CI;  // nch_cap entries
   int32_t* GS;  // ng_cap rounded up to 64
   int32_t* SS;  // 64
+  int32_t* GD;  // ng_cap rounded up to 64: a block's length changes per group (zero between blocks)
   int nch;
   int ng, nsg;
 };
@@ -468,7 +469,8 @@ __device__ __forceinline__ bool rnd_serial_op(const Col& C, uint32_t k, uint32_t
 // So every lane finds its chunk with one search of the block-start column, the
 // chunk's start and end in its perspective are block-start boundaries carried
 // forward through the earlier ops, and the block's length changes fold into the
-// column afterwards (col_add_at, one LDS add per row and change).  A range that
+// column afterwards (one LDS add per chunk row and change, group rows by a
+// scan of the block's per-group changes).  A range that
 // reaches a third chunk sends the block op by op (rnd_serial_op).
 
 // first t in [0, V) with R[t] > lim over a nondecreasing row, >= V if none
@@ -525,16 +527,6 @@ __device__ __forceinline__ ColPos col_find_lane(const Col& C, int32_t y, bool ac
     }
   }
   return r;
-}
-
-// chunk i's length changed by d (wave-uniform i, d): the later entries of its rows
-__device__ __forceinline__ void col_add_at(const Col& C, int i, int32_t d) {
-  const int l = lane_id();
-  const int g = i / kChGroup, sg = g / kWave;
-  const int ci = g * kChGroup + l, gi = sg * kWave + l;
-  if (l >= i % kChGroup && ci < C.nch) atomicAdd(&C.CI[ci], d);
-  if (l >= g % kWave && gi < C.ng) atomicAdd(&C.GS[gi], d);
-  if (l >= sg && l < C.nsg) atomicAdd(&C.SS[l], d);
 }
 
 // the block of nb ops (lane t < nb: op t -- record index k, w3, pos1, pos2):
@@ -621,13 +613,38 @@ __device__ __forceinline__ bool rnd_block(const Col& C, int nb, uint32_t k, uint
   if (s0) list[at] = make_uint4((uint32_t)c, k, (uint32_t)st, 0u);
   if (s1) list[at + (s0 ? 1u : 0u)] = make_uint4((uint32_t)c + 1u, k, (uint32_t)bc, 0u);
   m += (uint32_t)rdlane(inc, kWave - 1);
+  // fold: each change into its chunk row (one add per change, no divergence),
+  // the changes per group lane-parallel into GD, then per supergroup row the
+  // groups' running sums into GS and the row totals into SS
+  const uint32_t lanes4 = (uint32_t)l;
   for (uint64_t e = __ballot(d0 != 0); e; e &= e - 1) {
     const int t = __ffsll((long long)e) - 1;
-    col_add_at(C, rdlane(c, t), rdlane(d0, t));
+    const uint32_t cc = (uint32_t)rdlane(c, t);
+    const int32_t dd = rdlane(d0, t);
+    const uint32_t g0 = cc & ~63u, ci = g0 + lanes4;
+    atomicAdd(&C.CI[ci], (lanes4 >= (cc & 63u) && ci < (uint32_t)C.nch) ? dd : 0);
   }
   for (uint64_t e = __ballot(d1 != 0); e; e &= e - 1) {
     const int t = __ffsll((long long)e) - 1;
-    col_add_at(C, rdlane(c, t) + 1, rdlane(d1, t));
+    const uint32_t cc = (uint32_t)rdlane(c, t) + 1u;
+    const int32_t dd = rdlane(d1, t);
+    const uint32_t g0 = cc & ~63u, ci = g0 + lanes4;
+    atomicAdd(&C.CI[ci], (lanes4 >= (cc & 63u) && ci < (uint32_t)C.nch) ? dd : 0);
+  }
+  if (d0 != 0) atomicAdd(&C.GD[(uint32_t)c >> 6], d0);
+  if (d1 != 0) atomicAdd(&C.GD[((uint32_t)c + 1u) >> 6], d1);
+  lds_fence();
+  for (int sg = 0; sg < C.nsg; sg++) {
+    const int gi = sg * kWave + l;
+    const bool in = gi < C.ng;
+    const int32_t dv = in ? C.GD[gi] : 0;
+    const int32_t inc = wave_incl_scan(dv);
+    if (in) {
+      C.GD[gi] = 0;
+      C.GS[gi] += inc;
+    }
+    const int32_t tot = rdlane(inc, kWave - 1);
+    if (l >= sg && l < C.nsg) C.SS[l] += tot;
   }
   lds_fence();
   RND_DIAG(6, c1 - c0);
@@ -661,20 +678,28 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
   C.nsg = (C.ng + kWave - 1) / kWave;
   {
     const uint32_t gs_cap = (ch.ng_cap + kWave - 1) / kWave * kWave;
-    int32_t* base = reinterpret_cast<int32_t*>(rs_lds) + (uint64_t)w * (ch.nch_cap + gs_cap + kWave + kRing);
+    int32_t* base = reinterpret_cast<int32_t*>(rs_lds) + (uint64_t)w * (ch.nch_cap + 2 * gs_cap + kWave + kRing);
     C.CI = base;
     C.GS = base + ch.nch_cap;
     C.SS = base + ch.nch_cap + gs_cap;
+    C.GD = C.SS + kWave;
   }
-  uint32_t* const ring = reinterpret_cast<uint32_t*>(C.SS + kWave);
+  uint32_t* const ring = reinterpret_cast<uint32_t*>(C.GD + (ch.ng_cap + kWave - 1) / kWave * kWave);
   const int32_t* sum0 = reinterpret_cast<const int32_t*>(ch.kc + (uint64_t)doc * ch.nch_cap);
   uint4* list = rd.rlist + (uint64_t)doc * rd.rl_cap;
   // ops per client (every workgroup of the document counts them all)
   for (int c = (int)threadIdx.x; c < MTE_MAX_CLIENTS; c += (int)blockDim.x) ccount[c] = 0u;
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nops; i += blockDim.x) {
-    const uint32_t w3 = reinterpret_cast<const uint32_t*>(recp + 2 * i)[3];
-    atomicAdd(&ccount[(w3 >> 8) & 31u], 1u);
+  for (uint32_t i0 = threadIdx.x; i0 < nops; i0 += 8 * blockDim.x) {  // 8 records in flight per thread
+    uint32_t w3[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const uint32_t i = i0 + (uint32_t)q * blockDim.x;
+      w3[q] = i < nops ? reinterpret_cast<const uint32_t*>(recp + 2 * i)[3] : 0xffffffffu;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++)
+      if (w3[q] != 0xffffffffu) atomicAdd(&ccount[(w3[q] >> 8) & 31u], 1u);
   }
   __syncthreads();
   // each chain's list region: twice its ops (+ 8) from the prefix over clients
@@ -700,6 +725,7 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
         if (g < C.ng) C.GS[g] = incl;
         if (l == 0) C.SS[sg] = rdlane(incl, kWave - 1);
       }
+      for (int g = l; g < C.ng; g += kWave) C.GD[g] = 0;
       lds_fence();
       {
         const int32_t v = l < C.nsg ? C.SS[l] : 0;
