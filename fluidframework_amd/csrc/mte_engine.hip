@@ -774,7 +774,7 @@ void free_image(mte_ctx* c) {
 void free_docs(mte_ctx* c) {
   free_image(c);
   void* cs[] = {c->ch.arena, c->ch.cnt, c->ch.kc, c->ch.sum, c->rd.plan, c->rd.acct, c->rd.rcnt, c->rd.rbuf, c->rd.rflag,
-                c->rd.nch, c->rd.nnew, c->rd.count, c->rd.rlist, c->rd.rchain};
+                c->rd.nch, c->rd.nnew, c->rd.count, c->rd.rlist, c->rd.rchain, c->rd.live, c->rd.gfl};
   for (void* p : cs)
     if (p) (void)hipFree(p);
   c->ch = ChunkArgs{};
@@ -860,6 +860,12 @@ int round_phase_loop(mte_ctx* c, const ReplayArgs& a, size_t lds, uint64_t max_o
   ch.rflag = rd.rflag;
   rd.planes = kFieldPlanes + (uint32_t)(K > 0 ? K : 0);
   HIPCHK(c, hipMemsetAsync(rd.acct, 0, sizeof(unsigned long long) * c->n_docs, c->stream));
+  // no document starts in the arena (rd.live: a run's chunks stay laid out for
+  // the document's next run and go back to the flat planes when it leaves)
+  HIPCHK(c, hipMemsetAsync(rd.live, 0, 4 * (uint64_t)c->n_docs, c->stream));
+  rd.d0 = 0;
+  rd.nd = c->n_docs;
+  bool carried = false;  // some document may be in the arena
   const uint64_t nch_all = (uint64_t)c->n_docs * ch.nch_cap;
   for (int ph = 0; ph < kMaxPhases; ph++) {
     rd.last = ph == kMaxPhases - 1 ? 1u : 0u;
@@ -872,12 +878,14 @@ int round_phase_loop(mte_ctx* c, const ReplayArgs& a, size_t lds, uint64_t max_o
     if (n_round) {
       HIPCHK(c, hipMemsetAsync(rd.rcnt, 0, nch_all * 4, c->stream));
       HIPCHK(c, hipMemsetAsync(rd.rflag, 0, 4 * (uint64_t)c->n_docs, c->stream));
-      rd.d0 = 0;
-      rd.nd = c->n_docs;
       HIPCHK(c, (launch_round_run<K>(a, ch, rd, c->n_docs, c->stream)));
+      carried = true;
+    } else if (carried) {  // the carried documents' runs are not rounds: back to the flat planes
+      HIPCHK(c, (launch_round_gather<K>(a, ch, rd, 0, c->stream)));
     }
     HIPCHK(c, (launch_chunk<K, false>(a, ch, c->n_docs, lds, c->stream)));
   }
+  if (carried) HIPCHK(c, (launch_round_gather<K>(a, ch, rd, 1, c->stream)));
   return MTE_OK;
 }
 
@@ -1341,6 +1349,8 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
       HIPCHK(c, hipMalloc((void**)&rd.nch, 4 * (uint64_t)n_docs));
       HIPCHK(c, hipMalloc((void**)&rd.nnew, 4 * (uint64_t)n_docs));
       HIPCHK(c, hipMalloc((void**)&rd.rchain, sizeof(uint2) * MTE_MAX_CLIENTS * (uint64_t)n_docs));
+      HIPCHK(c, hipMalloc((void**)&rd.live, 4 * (uint64_t)n_docs));
+      HIPCHK(c, hipMalloc((void**)&rd.gfl, 4 * (uint64_t)n_docs));
       HIPCHK(c, hipMalloc((void**)&rd.count, 16));
       if (!c->h_rcount) HIPCHK(c, hipHostMalloc((void**)&c->h_rcount, 16, 0));
       c->chunked = true;

@@ -24,6 +24,21 @@ hipError_t launch_round_plan(const ReplayArgs& a, const RoundArgs& rd, uint32_t 
 }
 
 template <int K>
+static void round_gather(const ReplayArgs& a, const ChunkArgs& ch, const RoundArgs& rd, hipStream_t s) {
+  const uint64_t chunks = (uint64_t)rd.nd * ch.nch_cap;
+  hipLaunchKernelGGL(rnd_gscan_kernel, dim3(rd.nd), dim3(kChWaves * kWave), 0, s, a, ch, rd);
+  hipLaunchKernelGGL((rnd_gmove_kernel<K>), dim3((uint32_t)((chunks + 3) / 4)), dim3(4 * kWave), 0, s, a, ch, rd);
+}
+
+template <int K>
+hipError_t launch_round_gather(const ReplayArgs& a, const ChunkArgs& ch, const RoundArgs& rd, int final,
+                               hipStream_t s) {
+  hipLaunchKernelGGL(rnd_live_kernel, dim3(rd.nd), dim3(256), 0, s, a, ch, rd, final);
+  round_gather<K>(a, ch, rd, s);
+  return hipGetLastError();
+}
+
+template <int K>
 hipError_t launch_round_run(const ReplayArgs& a, const ChunkArgs& ch, const RoundArgs& rd, uint32_t,
                             hipStream_t s) {
 #if MTE_RND_DIAG
@@ -40,7 +55,12 @@ hipError_t launch_round_run(const ReplayArgs& a, const ChunkArgs& ch, const Roun
   const uint32_t tpd = (a.cap + kT - 1) / kT;  // flat tiles per document
   const uint64_t tiles = (uint64_t)n_docs * tpd, chunks = (uint64_t)n_docs * ch.nch_cap;
   const dim3 w4(4 * kWave);
-  // re-layout: flat -> chunks (zamboni at M), the round-start column
+  // documents whose carried chunks go back to the flat planes first (their run
+  // is not a round, or a chunk is full: the latter are re-laid out below)
+  hipLaunchKernelGGL(rnd_live_kernel, dim3(n_docs), dim3(256), 0, s, a, ch, rd, 0);
+  round_gather<K>(a, ch, rd, s);
+  // re-layout of the documents the arena does not hold: flat -> chunks (zamboni
+  // at M); then every round document's round-start column
   hipLaunchKernelGGL((rnd_count_kernel<K>), dim3((uint32_t)((tiles + 3) / 4)), w4, 0, s, a, ch, rd, tpd);
   hipLaunchKernelGGL(rnd_scan_kernel, dim3(n_docs), dim3(kChWaves * kWave), 0, s, a, ch, rd, 0);
   hipLaunchKernelGGL((rnd_move_kernel<K>), dim3((uint32_t)((tiles + 3) / 4)), w4, 0, s, a, ch, rd, tpd);
@@ -60,14 +80,20 @@ hipError_t launch_round_run(const ReplayArgs& a, const ChunkArgs& ch, const Roun
   }
   const uint32_t bpd = (uint32_t)((rd.rl_cap + 255) / 256);
   hipLaunchKernelGGL(rnd_bucket_kernel, dim3(n_docs * bpd), dim3(256), 0, s, a, ch, rd, bpd);
+  hipLaunchKernelGGL(rnd_room_kernel, dim3((uint32_t)((chunks + 255) / 256)), dim3(256), 0, s, a, ch, rd);
   // apply: every chunk with sub-ops on its own wave
   hipLaunchKernelGGL((rnd_apply_kernel<K>), dim3((uint32_t)((chunks + 3) / 4)), w4, 0, s, a, ch, rd);
-  // gather: chunks -> flat, the header past the run
+  // the header past the run (the segments stay in the arena); the refused runs'
+  // carried documents back to the flat planes
   hipLaunchKernelGGL(rnd_scan_kernel, dim3(n_docs), dim3(kChWaves * kWave), 0, s, a, ch, rd, 1);
-  hipLaunchKernelGGL((rnd_gmove_kernel<K>), dim3((uint32_t)((chunks + 3) / 4)), w4, 0, s, a, ch, rd);
+  hipLaunchKernelGGL(rnd_post_kernel, dim3((n_docs + 63) / 64), dim3(64), 0, s, a, ch, rd);
+  round_gather<K>(a, ch, rd, s);
   return hipGetLastError();
 }
 template hipError_t launch_round_run<0>(const ReplayArgs&, const ChunkArgs&, const RoundArgs&, uint32_t, hipStream_t);
+template hipError_t launch_round_gather<0>(const ReplayArgs&, const ChunkArgs&, const RoundArgs&, int, hipStream_t);
+template hipError_t launch_round_gather<4>(const ReplayArgs&, const ChunkArgs&, const RoundArgs&, int, hipStream_t);
+template hipError_t launch_round_gather<8>(const ReplayArgs&, const ChunkArgs&, const RoundArgs&, int, hipStream_t);
 template hipError_t launch_round_run<4>(const ReplayArgs&, const ChunkArgs&, const RoundArgs&, uint32_t, hipStream_t);
 template hipError_t launch_round_run<8>(const ReplayArgs&, const ChunkArgs&, const RoundArgs&, uint32_t, hipStream_t);
 

@@ -19,6 +19,11 @@ struct ChunkArgs;
 constexpr int kRB = 62;              // sub-ops per chunk and run: 128 + 2 x 62 slots <= 254
 constexpr uint32_t kRoundMin = 256;  // the shortest run the round phases take
 constexpr int kMaxPhases = 16;       // phases per launch before the rest runs op after op
+// a document's chunks stay laid out from one run to the next (rnd_live) while
+// no chunk holds more than this many segments; a run whose sub-ops would not
+// fit a carried chunk (count + 2 per sub-op > kChSlots) is re-laid out and run
+// again in the next phase
+constexpr uint32_t kLiveFull = 192;
 struct RoundArgs {
   uint4* plan;      // [doc] x mode, y k0, z k1, w M
   uint32_t* rcnt;   // [doc][nch_cap] sub-ops per chunk
@@ -30,6 +35,11 @@ struct RoundArgs {
   uint4* rlist;     // [doc][rl_cap] the client chains' sub-ops (chunk, op index - k0, chunk start)
   uint64_t rl_cap;  // list entries per document: 2 x its ops + 8 per client
   uint2* rchain;    // [doc][MTE_MAX_CLIENTS] (list offset, entries) of each client chain
+  // [doc] where the document's segments are: 0 the flat planes; 1 the chunk
+  // arena, carried from the previous run (the flat planes are stale); 2 the
+  // arena, re-laid out for this run
+  uint32_t* live;
+  uint32_t* gfl;    // [doc] 1: this launch gathers the arena back into the flat planes
   uint32_t last;    // this phase sends every active document op after op
   uint32_t d0, nd;  // the documents [d0, d0 + nd) one launch_round_run covers
   // [doc] the bytes the round phases of the last mte_run had to read and write
@@ -42,6 +52,11 @@ struct RoundArgs {
 // the round phases fit a context whose per-wave column (nch_cap + ng_cap
 // entries, mte_round.h rnd_resolve_kernel) fits this much LDS
 constexpr uint32_t kRoundLdsMax = 150u * 1024u;
+// the documents leaving the arena (their next run is not a round, a chunk is
+// full, or final: every one) gathered back into the flat planes
+template <int K>
+hipError_t launch_round_gather(const ReplayArgs& a, const ChunkArgs& ch, const RoundArgs& rd, int final,
+                               hipStream_t s);
 inline uint64_t rnd_resolve_lds(uint32_t nch_cap, uint32_t ng_cap) {
   return (uint64_t)(nch_cap + 2 * ((ng_cap + 63) / 64 * 64) + 64 + 1024) * 4u;  // + GD rows, the staging ring (kRing)
 }

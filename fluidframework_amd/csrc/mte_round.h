@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void rnd_count_kernel(ReplayArgs a, ChunkArgs 
   if (doc >= (int)(rd.d0 + rd.nd)) return;
   const uint4 p = rd.plan[doc];
   const int n = a.hdr[doc].nseg;
-  if (p.x != kModeRound || t * kT >= n) return;
+  if (p.x != kModeRound || rd.live[doc] != 0u || t * kT >= n) return;
   const int32_t M = (int32_t)p.w;
   const uint32_t* rs = a.planes + 2 * a.stride + (uint64_t)doc * a.cap;
   int32_t k = 0;
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(512) void rnd_scan_kernel(ReplayArgs a, ChunkArgs c
   __shared__ ChCtl ctl;
   const int doc = (int)rd.d0 + (int)blockIdx.x;
   const uint4 p = rd.plan[doc];
-  if (p.x != kModeRound || (gather && rd.rflag[doc] != 0u)) return;
+  if (p.x != kModeRound || (gather && rd.rflag[doc] != 0u) || (!gather && rd.live[doc] != 0u)) return;
   uint32_t* kc = ch.kc + (uint64_t)doc * ch.nch_cap;
   int m;
   if (gather) {
@@ -198,6 +198,7 @@ __global__ __launch_bounds__(512) void rnd_scan_kernel(ReplayArgs a, ChunkArgs c
       nch = nch < 1 ? 1 : (nch > (int)ch.nch_cap ? (int)ch.nch_cap : nch);
       rd.nch[doc] = (uint32_t)nch;
       rd.nnew[doc] = (uint32_t)total;
+      rd.live[doc] = 2u;  // the arena holds it from here (rnd_move)
       // the plan's record scan, the keep counts' removedSeq reads, the kept
       // segments' planes moved into the chunks, the columns' length and
       // removedSeq reads, the chunk counts and column entries
@@ -205,8 +206,10 @@ __global__ __launch_bounds__(512) void rnd_scan_kernel(ReplayArgs a, ChunkArgs c
       atomicAdd(rd.acct + doc, 32ull * (p.z - p.y) + 4ull * n_old + 2ull * pb * (unsigned long long)total +
                                    8ull * (unsigned long long)total + 8ull * (unsigned long long)nch);
     } else {
-      // the chunks' planes back into the flat planes, the counts and their prefix
-      atomicAdd(rd.acct + doc, 2ull * pb * (unsigned long long)total + 8ull * (unsigned long long)m);
+      // the run applied: the header past it, the segments stay in the arena
+      // (rnd_live decides when they go back to the flat planes); the counts read
+      atomicAdd(rd.acct + doc, 4ull * (unsigned long long)m);
+      rd.live[doc] = 1u;
       const uint64_t kb = a.op_off[doc];
       const uint32_t ktot = (uint32_t)(a.op_off[doc + 1] - kb);
       DocHdr h = a.hdr[doc];
@@ -229,7 +232,7 @@ __global__ __launch_bounds__(256) void rnd_move_kernel(ReplayArgs a, ChunkArgs c
   if (doc >= (int)(rd.d0 + rd.nd)) return;
   const uint4 p = rd.plan[doc];
   const int n = a.hdr[doc].nseg;
-  if (p.x != kModeRound || t * kT >= n) return;
+  if (p.x != kModeRound || rd.live[doc] != 2u || t * kT >= n) return;
   const int32_t M = (int32_t)p.w;
   const uint32_t* pl = a.planes + (uint64_t)doc * a.cap;
   bool keep[kChE];
@@ -269,12 +272,14 @@ __global__ __launch_bounds__(256) void rnd_cols_kernel(ReplayArgs a, ChunkArgs c
   if (doc >= (int)(rd.d0 + rd.nd)) return;
   const uint4 p = rd.plan[doc];
   if (p.x != kModeRound || q >= (int)rd.nch[doc]) return;
+  // a re-laid-out document: kChFill per chunk; a carried one: its counts
   const int n_new = (int)rd.nnew[doc];
-  const int cn = n_new - q * kChFill < kChFill ? (n_new - q * kChFill > 0 ? n_new - q * kChFill : 0) : kChFill;
+  const int cn = rd.live[doc] == 1u ? (int)ch.cnt[(uint64_t)doc * ch.nch_cap + q]
+                 : (n_new - q * kChFill < kChFill ? (n_new - q * kChFill > 0 ? n_new - q * kChFill : 0) : kChFill);
   const uint64_t x0 = ch_slot(ch, doc, q);
   int32_t v = 0;
 #pragma unroll
-  for (int j = 0; j < kChFill / kWave; j++) {
+  for (int j = 0; j < kChSlots / kWave; j++) {
     const int s = j * kWave + l;
     if (s < cn) v += (int32_t)ch.arena[2 * ch.astride + x0 + s] == kNone ? (int32_t)ch.arena[x0 + s] : 0;
   }
@@ -293,8 +298,7 @@ __global__ __launch_bounds__(256) void rnd_gmove_kernel(ReplayArgs a, ChunkArgs 
   const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
   const int doc = (int)rd.d0 + (int)(wi / ch.nch_cap), q = (int)(wi % ch.nch_cap);
   if (doc >= (int)(rd.d0 + rd.nd)) return;
-  const uint4 p = rd.plan[doc];
-  if (p.x != kModeRound || rd.rflag[doc] != 0u || q >= (int)rd.nch[doc]) return;
+  if (rd.gfl[doc] == 0u || q >= (int)rd.nch[doc]) return;
   const int cn = (int)ch.cnt[(uint64_t)doc * ch.nch_cap + q];
   const uint32_t d0 = ch.kc[(uint64_t)doc * ch.nch_cap + q];
   const uint64_t x0 = ch_slot(ch, doc, q);
@@ -307,6 +311,81 @@ __global__ __launch_bounds__(256) void rnd_gmove_kernel(ReplayArgs a, ChunkArgs 
         pl[(uint64_t)qq * a.stride + d0 + (uint32_t)s] = ch.arena[(uint64_t)qq * ch.astride + x0 + s];
     }
   }
+}
+
+// ---- carried layouts ------------------------------------------------------------
+// per document (a workgroup): does its arena go back to the flat planes in this
+// launch?  It does when it holds the document (live 1) and the next run is not
+// a round, a chunk is past kLiveFull, or this is the launch's last gather
+__global__ __launch_bounds__(256) void rnd_live_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd, int final) {
+  __shared__ uint32_t full;
+  const int doc = (int)rd.d0 + (int)blockIdx.x;
+  const uint32_t lv = rd.live[doc];
+  if (threadIdx.x == 0) full = 0u;
+  __syncthreads();
+  const bool leave = lv == 1u && (final || rd.plan[doc].x != kModeRound);
+  if (lv == 1u && !leave) {
+    const uint32_t* cnt = ch.cnt + (uint64_t)doc * ch.nch_cap;
+    const int nch = (int)rd.nch[doc];
+    uint32_t mx = 0;
+    for (int q = (int)threadIdx.x; q < nch; q += (int)blockDim.x) mx = cnt[q] > mx ? cnt[q] : mx;
+    if (mx > kLiveFull) atomicOr(&full, 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) rd.gfl[doc] = (leave || full) ? 1u : 0u;
+}
+
+// per document after the apply: a run the round phases refused (rflag) left
+// the arena untouched -- a re-laid-out document's flat planes are still
+// current, a carried one's go back (rflag & 4: its chunks had no room, the run
+// is re-laid out and taken again next phase, not op after op)
+__global__ __launch_bounds__(64) void rnd_post_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
+  const int doc = (int)rd.d0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (doc >= (int)(rd.d0 + rd.nd)) return;
+  uint32_t g = 0;
+  const uint4 p = rd.plan[doc];
+  const uint32_t f = rd.rflag[doc];
+  if (p.x == kModeRound && f != 0u) {
+    const uint32_t lv = rd.live[doc];
+    if (lv == 2u) rd.live[doc] = 0u;
+    if (lv == 1u) {
+      g = 1u;
+      if (f & 4u) rd.plan[doc] = make_uint4(kModeIdle, 0u, 0u, 0u);
+    }
+  }
+  rd.gfl[doc] = g;
+}
+
+// the gather documents: exclusive prefix of their chunk counts (into kc); they
+// leave the arena
+__global__ __launch_bounds__(512) void rnd_gscan_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
+  __shared__ ChCtl ctl;
+  const int doc = (int)rd.d0 + (int)blockIdx.x;
+  if (rd.gfl[doc] == 0u) return;
+  uint32_t* kc = ch.kc + (uint64_t)doc * ch.nch_cap;
+  const int m = (int)rd.nch[doc];
+  const uint32_t* cnt = ch.cnt + (uint64_t)doc * ch.nch_cap;
+  for (int i = (int)threadIdx.x; i < m; i += (int)blockDim.x) kc[i] = cnt[i];
+  __syncthreads();
+  const int32_t total = ch_block_scan(kc, m, &ctl);
+  if (threadIdx.x == 0) {
+    const unsigned long long pb = 4ull * rd.planes;
+    atomicAdd(rd.acct + doc, 2ull * pb * (unsigned long long)total + 8ull * (unsigned long long)m);
+    a.hdr[doc].nseg = total;
+    rd.live[doc] = 0u;
+  }
+}
+
+// a carried document's chunks must hold the run's sub-ops: count + 2 per
+// sub-op <= kChSlots (a re-laid-out one's always do: kChFill + 2 kRB); one
+// thread per chunk
+__global__ __launch_bounds__(256) void rnd_room_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
+  const uint64_t wi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int doc = (int)rd.d0 + (int)(wi / ch.nch_cap), q = (int)(wi % ch.nch_cap);
+  if (doc >= (int)(rd.d0 + rd.nd)) return;
+  if (rd.plan[doc].x != kModeRound || rd.live[doc] != 1u || q >= (int)rd.nch[doc]) return;
+  const uint64_t i = (uint64_t)doc * ch.nch_cap + q;
+  if (ch.cnt[i] + 2u * rd.rcnt[i] > (uint32_t)kChSlots) atomicOr(rd.rflag + doc, 4u);
 }
 
 // ---- resolve: one wave per client chain, the column as prefix sums -----------
@@ -546,35 +625,45 @@ __device__ __forceinline__ bool rnd_block(const Col& C, int nb, uint32_t k, uint
   const int32_t tp = ins ? pos1 : b1;
   const int32_t tn = ins ? (nlen > 0 ? nlen : 0) : (rem ? b1 - b2 : 0);
   int32_t y = ins ? pos1 - 1 : b1;
-#if MTE_RND_DIAG
-  y = __builtin_amdgcn_readfirstlane(0) + y;  // (the records are in)
-#endif
   RND_CLK(c1);
-  // Straight-line passes over the earlier ops (no branch: an annotate is the
-  // identity of both forms), the lanes after j taking op j; n = the units an
-  // insert adds, r = the units a remove takes (one of them 0).
-  // back, latest first: y -> y if y < p; y + r - n if y >= p + n; p - 1 otherwise
-  // (a fixed 63 steps: the lanes past the block hold the identity, tn = 0)
-#pragma unroll 7
-  for (int j = kWave - 2; j >= 0; j--) {
+  // The passes visit the block's inserts and removes only (an annotate is the
+  // identity), the lanes after j taking op j; one uniform branch on the op's
+  // kind per step, selects inside.
+  const uint64_t xm = __ballot(tn != 0);
+  // back, latest first: y -> y if y < p; y - n if y >= p + n; p - 1 otherwise
+  // (insert of n at p); y + r if y >= p (remove of r at p)
+  for (uint64_t m = xm; m;) {
+    const int j = 63 - __clzll((long long)m);
+    m ^= 1ull << j;
     const int32_t tj = rdlane(tn, j), pj = rdlane(tp, j);
-    const int32_t nj = tj > 0 ? tj : 0, rj = tj < 0 ? -tj : 0;
-    const int32_t y1 = y >= pj + nj ? y + rj - nj : pj - 1;
-    y = (l > j && y >= pj) ? y1 : y;
+    const bool take = l > j && y >= pj;
+    if (tj > 0) {
+      const int32_t y1 = y >= pj + tj ? y - tj : pj - 1;
+      y = take ? y1 : y;
+    } else {
+      y = take ? y - tj : y;
+    }
   }
   RND_CLK(c2);
   const ColPos P = col_find_lane(C, y, v);
   const bool found = v && P.c < C.nch;
   int32_t bm = P.bm, bc = P.bc, bn = P.bn;
   RND_CLK(c3);
-  // forward: B -> B + n if p <= B; B - clamp(B - p, 0, r)
-#pragma unroll 7
-  for (int j = 0; j < kWave - 1; j++) {
+  // forward: B -> B + n if p <= B (insert); B - clamp(B - p, 0, r) (remove)
+  for (uint64_t m = xm; m; m &= m - 1) {
+    const int j = __ffsll((long long)m) - 1;
     const int32_t tj = rdlane(tn, j), pj = rdlane(tp, j);
-    const int32_t a = (l > j && tj > 0) ? tj : 0, r = (l > j && tj < 0) ? -tj : 0;
-    bm += (pj <= bm ? a : 0) - min(max(bm - pj, 0), r);
-    bc += (pj <= bc ? a : 0) - min(max(bc - pj, 0), r);
-    bn += (pj <= bn ? a : 0) - min(max(bn - pj, 0), r);
+    if (tj > 0) {
+      const int32_t a = l > j ? tj : 0;
+      bm += pj <= bm ? a : 0;
+      bc += pj <= bc ? a : 0;
+      bn += pj <= bn ? a : 0;
+    } else {
+      const int32_t r = l > j ? -tj : 0;
+      bm -= min(max(bm - pj, 0), r);
+      bc -= min(max(bc - pj, 0), r);
+      bn -= min(max(bn - pj, 0), r);
+    }
   }
   RND_CLK(c4);
   const int c = P.c;
