@@ -225,7 +225,31 @@ class IntervalCollection {
     // with no conflict resolver (IntervalCollection.addConflictResolver is the
     // application's to call): previousInterval / nextInterval read it
     this.endTree = new RedBlackTree((a, b) => compareKeys(a._keys()[1], b._keys()[1]));
+    this._endOrder = 0;
     if (serialized) this._load(serialized);
+  }
+
+  // ---- the end tree ----------------------------------------------------------------
+  /** The end tree follows every put / remove of the reference only when the
+   *  document reports its references' slides (createClient {events: true}):
+   *  an end that slides re-enters the tree there (_onSlides).  Without them
+   *  the tree is rebuilt at each query, the intervals put in index order --
+   *  the reference's tree where no end has slid. */
+  _tracksSlides() {
+    const e = this.client.engine;
+    return !!(e && e.docs && e.docs[this.client.doc] && e.docs[this.client.doc].events);
+  }
+  _endPut(ival) {
+    if (this._tracksSlides()) this.endTree.put(ival, ival);
+  }
+  _endRemove(ival) {
+    if (this._tracksSlides()) this.endTree.remove(ival);
+  }
+  _ends() {
+    if (this._tracksSlides()) return this.endTree;
+    const t = new RedBlackTree(this.endTree.compare);
+    for (const x of Array.from(this.byId.values()).sort((a, b) => a.stamp - b.stamp)) t.put(x, x);
+    return t;
   }
 
   // ---- events (TypedEventEmitter<IIntervalCollectionEvent>) ------------------------
@@ -288,7 +312,7 @@ class IntervalCollection {
   _index(ival) {
     ival.stamp = ++this.stamp;
     this.byId.set(ival.getIntervalId(), ival);
-    this.endTree.put(ival, ival);  // addIntervalToIndex (:975-987)
+    this._endPut(ival);  // addIntervalToIndex (:975-987)
   }
 
   _addInterval(start, end, intervalType, props, op, fromSnapshot) {
@@ -326,7 +350,7 @@ class IntervalCollection {
    *  without an op), the others kept. */
   _changeInterval(ival, start, end, op) {
     const retype = (t) => (op ? t : ((t & ~RefType.SlideOnRemove) | RefType.StayOnRemove));
-    this.endTree.remove(ival);  // removeExistingInterval of the interval modify replaced (:999-1012)
+    this._endRemove(ival);  // removeExistingInterval of the interval modify replaced (:999-1012)
     if (start !== undefined) {
       const old = ival.start;
       ival.start = op ? this._opRef(start, retype(old.refType), op) : this._localRef(start, retype(old.refType));
@@ -338,12 +362,12 @@ class IntervalCollection {
       this._drop(old);
     }
     ival.stamp = ++this.stamp;
-    this.endTree.put(ival, ival);  // add(newInterval)
+    this._endPut(ival);  // add(newInterval)
     return ival;
   }
 
   _remove(ival) {
-    this.endTree.remove(ival);  // removeIntervalFromIndex (:960-968), while its ends still compare
+    this._endRemove(ival);  // removeIntervalFromIndex (:960-968), while its ends still compare
     this.byId.delete(ival.getIntervalId());
     this._drop(ival.start);
     this._drop(ival.end);
@@ -404,8 +428,8 @@ class IntervalCollection {
     }
     if (ival && (r[nPos] !== -1 || r[nPos + 1] !== -1)) {  // re-added by changeInterval (removeExisting + add)
       ival.stamp = ++this.stamp;
-      this.endTree.remove(ival);
-      this.endTree.put(ival, ival);
+      this._endRemove(ival);
+      this._endPut(ival);
     }
     return rebased;
   }
@@ -579,9 +603,9 @@ class IntervalCollection {
     if (after[0] !== before[0] || after[1] !== before[1]) {
       // removeExistingInterval (with the ends as they were) + add (:1862-1899)
       ival._pinKeys = before;
-      this.endTree.remove(ival);
+      this._endRemove(ival);
       delete ival._pinKeys;
-      this.endTree.put(ival, ival);
+      this._endPut(ival);
       ival.stamp = ++this.stamp;
       if (watch) this._emitChange(ival, prev, true, op);
     }
@@ -662,7 +686,7 @@ class IntervalCollection {
           const other = which ? ival.start : ival.end;
           const otherPos = posNow.has(other.slot) ? posNow.get(other.slot) : now(other);
           // beforeSlide: out of the index (removeIntervalFromIndex, :1042-1047)
-          this.endTree.remove(ival);
+          this._endRemove(ival);
           posNow.set(r.slot, next);
           ival._pinKeys[which] = q.length && q[0].seg >= 0 ? q[0].seg : c._refOrder(lref);
           // its place among the new segment's references: addBeforeTombstones
@@ -681,7 +705,7 @@ class IntervalCollection {
           }
           // afterSlide: back in (addIntervalToIndex), then onPositionChange (:1048-1053)
           ival.stamp = ++this.stamp;
-          this.endTree.put(ival, ival);
+          this._endPut(ival);
           if (watch) {
             const snap = (p) => ({ snapshot: true, position: p, refType: RefType.Transient });
             const prev = new SequenceInterval(this, snap(which ? otherPos : at), snap(which ? at : otherPos),
@@ -771,11 +795,11 @@ class IntervalCollection {
   /** previousInterval / nextInterval (:897-913): the data of the end tree's
    *  floor / ceil node of a Transient interval at pos. */
   previousInterval(pos) {
-    const n = this.endTree.floor(new TransientInterval(this.client, pos, pos));
+    const n = this._ends().floor(new TransientInterval(this.client, pos, pos));
     return n ? n.data : undefined;
   }
   nextInterval(pos) {
-    const n = this.endTree.ceil(new TransientInterval(this.client, pos, pos));
+    const n = this._ends().ceil(new TransientInterval(this.client, pos, pos));
     return n ? n.data : undefined;
   }
 
