@@ -149,6 +149,14 @@ __global__ __launch_bounds__(512) void rnd_plan_kernel(ReplayArgs a, RoundArgs r
 // ---- re-layout and gather: many waves per document ---------------------------
 
 constexpr int kT = kChE * kWave;  // flat slots per tile
+// segments per chunk a re-layout aims at (fewer than the chunk pass's kChFill:
+// more chunks, and a chunk plus its run's sub-ops then fits the apply's
+// two-slot-per-lane registers); the chunk count stays within nch_cap, the
+// fill is total / chunks rounded up (rnd_fill)
+#ifndef MTE_RND_FILL
+#define MTE_RND_FILL 80
+#endif
+__device__ __forceinline__ uint32_t rnd_fill(uint32_t total, uint32_t nch) { return nch ? (total + nch - 1) / nch : 1u; }
 
 // keep counts of the flat tiles (removedSeq > M), one wave per tile
 template <int K>
@@ -194,7 +202,7 @@ __global__ __launch_bounds__(512) void rnd_scan_kernel(ReplayArgs a, ChunkArgs c
   if (threadIdx.x == 0) {
     const unsigned long long pb = 4ull * rd.planes;  // bytes of one segment's planes
     if (!gather) {
-      int nch = (total + kChFill - 1) / kChFill;
+      int nch = (total + MTE_RND_FILL - 1) / MTE_RND_FILL;
       nch = nch < 1 ? 1 : (nch > (int)ch.nch_cap ? (int)ch.nch_cap : nch);
       rd.nch[doc] = (uint32_t)nch;
       rd.nnew[doc] = (uint32_t)total;
@@ -250,13 +258,20 @@ __global__ __launch_bounds__(256) void rnd_move_kernel(ReplayArgs a, ChunkArgs c
     dst[j] = run + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
     run += __popcll(mk);
   }
-  const uint32_t lim = ch.nch_cap * kChFill;
+  const uint32_t nch = rd.nch[doc], fill = rnd_fill(rd.nnew[doc], nch);
+  const uint32_t lim = nch * fill;
+  uint64_t xs[kChE];
+#pragma unroll
+  for (int j = 0; j < kChE; j++) {
+    const uint32_t ci = (uint32_t)dst[j] / fill;
+    xs[j] = ch_slot(ch, doc, (int)ci) + ((uint32_t)dst[j] - ci * fill);
+  }
   for (int q = 0; q < kFieldPlanes + K; q++) {
 #pragma unroll
     for (int j = 0; j < kChE; j++) {
       const int i = t * kT + j * kWave + l;
       if (keep[j] && (uint32_t)dst[j] < lim) {
-        const uint64_t x = ch_slot(ch, doc, dst[j] / kChFill) + (uint32_t)(dst[j] % kChFill);
+        const uint64_t x = xs[j];
         ch.arena[(uint64_t)q * ch.astride + x] = pl[(uint64_t)q * a.stride + i];
       }
     }
@@ -273,9 +288,9 @@ __global__ __launch_bounds__(256) void rnd_cols_kernel(ReplayArgs a, ChunkArgs c
   const uint4 p = rd.plan[doc];
   if (p.x != kModeRound || q >= (int)rd.nch[doc]) return;
   // a re-laid-out document: kChFill per chunk; a carried one: its counts
-  const int n_new = (int)rd.nnew[doc];
+  const int n_new = (int)rd.nnew[doc], fill = (int)rnd_fill(rd.nnew[doc], rd.nch[doc]);
   const int cn = rd.live[doc] == 1u ? (int)ch.cnt[(uint64_t)doc * ch.nch_cap + q]
-                 : (n_new - q * kChFill < kChFill ? (n_new - q * kChFill > 0 ? n_new - q * kChFill : 0) : kChFill);
+                 : (n_new - q * fill < fill ? (n_new - q * fill > 0 ? n_new - q * fill : 0) : fill);
   const uint64_t x0 = ch_slot(ch, doc, q);
   int32_t v = 0;
 #pragma unroll
@@ -913,40 +928,66 @@ __global__ __launch_bounds__(256) void rnd_bucket_kernel(ReplayArgs a, ChunkArgs
   else atomicOr(rd.rflag + doc, 1u);
 }
 
-// one wave per chunk of a run: its sub-ops in op order through seg_op_v
-template <int K>
-__global__ __launch_bounds__(256) void rnd_apply_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
-  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
-  const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
-  const int doc = (int)rd.d0 + (int)(wi / ch.nch_cap), i = (int)(wi % ch.nch_cap);
-  if (doc >= (int)(rd.d0 + rd.nd)) return;
-  const uint4 p = rd.plan[doc];
-  if (p.x != kModeRound || rd.rflag[doc] != 0u || i >= (int)rd.nch[doc]) return;
-  // everything the chunk needs, issued together: its sub-op count and bucket,
-  // its segment count and planes; then each sub-op's record (bucket order)
-  const uint32_t nb = rd.rcnt[(uint64_t)doc * ch.nch_cap + i];
-  const uint2 e0 = rd.rbuf[((uint64_t)doc * ch.nch_cap + i) * kRB + (l < kRB ? l : 0)];
-  uint32_t* cntp = ch.cnt + (uint64_t)doc * ch.nch_cap;
-  int ni = (int)cntp[i];
-  const int n_before = ni;
-  const uint64_t x0 = ch_slot(ch, doc, i);
-  Regs<kChE, K> R;
-  ch_load<K>(R, ch, x0, ni);
-  if (nb == 0u) return;
-  const uint2 e = l < (int)nb ? e0 : make_uint2(0xffffffffu, 0u);
-  const uint4* recp = a.recs + 2 * (a.op_off[doc] + p.y);
-  uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0;
-  if (l < (int)nb) {
-    r0 = recp[2 * e.x];
-    r1 = recp[2 * e.x + 1];
+// a chunk's first E * 64 slots into registers (E = 2: one 8-byte load per
+// plane and lane; E = 4: ch_load), padding past n; and back
+template <int E, int K>
+__device__ __forceinline__ void ch_load_e(Regs<E, K>& R, const ChunkArgs& ch, uint64_t x0, int n) {
+  if constexpr (E == kChE) {
+    ch_load<K>(R, ch, x0, n);
+  } else {
+    static_assert(E == 2, "two or four slots per lane");
+    const uint32_t* pl = ch.arena + x0 + (uint32_t)lane_id() * E;
+    const uint64_t st = ch.astride;
+    uint2 q[kFieldPlanes + K];
+#pragma unroll
+    for (int p = 0; p < kFieldPlanes + K; p++) q[p] = *reinterpret_cast<const uint2*>(pl + p * st);
+    const int base = lane_id() * E;
+#pragma unroll
+    for (int j = 0; j < E; j++) {
+      const bool v = base + j < n;
+      auto el = [&](int p) -> uint32_t { return j == 0 ? q[p].x : q[p].y; };
+      R.len[j] = v ? (int32_t)el(0) : 0;
+      R.seq[j] = v ? (int32_t)el(1) : 0;
+      R.rseq[j] = v ? (int32_t)el(2) : kPad;
+      R.rmask[j] = v ? el(3) : 0u;
+      R.meta[j] = v ? el(4) : 0u;
+      R.toff[j] = v ? el(5) : 0u;
+#pragma unroll
+      for (int k = 0; k < K; k++) R.pr[k][j] = v ? el(kFieldPlanes + k) : 0u;
+    }
   }
-  // the bucket in op order: each entry's rank, and per rank the lane holding it
-  uint32_t rank = 0;
-  for (uint32_t j = 0; j < nb; j++) rank += rdlane(e.x, (int)j) < e.x ? 1u : 0u;
-  const int dst = (l < (int)nb ? (int)rank : l) << 2;
-  const int from = __builtin_amdgcn_ds_permute(dst, l);
+}
+
+template <int E, int K>
+__device__ __forceinline__ void ch_store_e(const Regs<E, K>& R, const ChunkArgs& ch, uint64_t x0, int n) {
+  uint32_t* pl = ch.arena;
+  const uint64_t st = ch.astride;
+  const int base = lane_id() * E;
+#pragma unroll
+  for (int j = 0; j < E; j++) {
+    const int i = base + j;
+    if (i < n) {
+      const uint64_t x = x0 + (uint32_t)i;
+      pl[x] = (uint32_t)R.len[j];
+      pl[st + x] = (uint32_t)R.seq[j];
+      pl[2 * st + x] = (uint32_t)R.rseq[j];
+      pl[3 * st + x] = R.rmask[j];
+      pl[4 * st + x] = R.meta[j];
+      pl[5 * st + x] = R.toff[j];
+#pragma unroll
+      for (int k = 0; k < K; k++) pl[(kFieldPlanes + k) * st + x] = R.pr[k][j];
+    }
+  }
+}
+
+// the chunk's sub-ops in op order through seg_op_v at E slots per lane
+template <int E, int K>
+__device__ __forceinline__ int rnd_apply_chunk(const ReplayArgs& a, const ChunkArgs& ch, uint64_t x0, int& ni,
+                                               uint32_t nb, int from, const uint2& e, const uint4& r0,
+                                               const uint4& r1, int32_t M) {
+  Regs<E, K> R;
+  ch_load_e<E, K>(R, ch, x0, ni);
   uint32_t st[kNumStats] = {};
-  const int32_t M = (int32_t)p.w;
   int rcs = 0;
   for (uint32_t j = 0; j < nb; j++) {
     const int q = rdlane(from, (int)j);
@@ -962,11 +1003,48 @@ __global__ __launch_bounds__(256) void rnd_apply_kernel(ReplayArgs a, ChunkArgs 
     op[7] = (int32_t)rdlane(r1.w, q);
     const uint32_t w3 = (uint32_t)op[3];
     int32_t tot = 0, dlen = 0;
-    const int rc = seg_op_v<kChE, K, false, true>(R, ni, op, w3 & 0xffu, (w3 >> 8) & 0xffu, w3 >> 16, M, true, ex,
-                                                  true, tot, dlen, a, st);
+    const int rc = seg_op_v<E, K, false, true>(R, ni, op, w3 & 0xffu, (w3 >> 8) & 0xffu, w3 >> 16, M, true, ex, true,
+                                               tot, dlen, a, st);
     rcs = rc != 0 ? rc : rcs;
   }
-  ch_store<K>(R, ch, x0, ni);
+  ch_store_e<E, K>(R, ch, x0, ni);
+  return rcs;
+}
+
+// one wave per chunk of a run: its sub-ops in op order; a chunk that stays
+// within 128 slots (its segments + 2 per sub-op) at two slots per lane
+template <int K>
+__global__ __launch_bounds__(256) void rnd_apply_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
+  const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
+  const int doc = (int)rd.d0 + (int)(wi / ch.nch_cap), i = (int)(wi % ch.nch_cap);
+  if (doc >= (int)(rd.d0 + rd.nd)) return;
+  const uint4 p = rd.plan[doc];
+  if (p.x != kModeRound || rd.rflag[doc] != 0u || i >= (int)rd.nch[doc]) return;
+  // the sub-op count and bucket and the segment count, issued together; then
+  // each sub-op's record (bucket order)
+  const uint32_t nb = rd.rcnt[(uint64_t)doc * ch.nch_cap + i];
+  const uint2 e0 = rd.rbuf[((uint64_t)doc * ch.nch_cap + i) * kRB + (l < kRB ? l : 0)];
+  uint32_t* cntp = ch.cnt + (uint64_t)doc * ch.nch_cap;
+  int ni = (int)cntp[i];
+  const int n_before = ni;
+  const uint64_t x0 = ch_slot(ch, doc, i);
+  if (nb == 0u) return;
+  const uint2 e = l < (int)nb ? e0 : make_uint2(0xffffffffu, 0u);
+  const uint4* recp = a.recs + 2 * (a.op_off[doc] + p.y);
+  uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0;
+  if (l < (int)nb) {
+    r0 = recp[2 * e.x];
+    r1 = recp[2 * e.x + 1];
+  }
+  // the bucket in op order: each entry's rank, and per rank the lane holding it
+  uint32_t rank = 0;
+  for (uint32_t j = 0; j < nb; j++) rank += rdlane(e.x, (int)j) < e.x ? 1u : 0u;
+  const int dst = (l < (int)nb ? (int)rank : l) << 2;
+  const int from = __builtin_amdgcn_ds_permute(dst, l);
+  const int32_t M = (int32_t)p.w;
+  const int rcs = ni + 2 * (int)nb <= 2 * kWave ? rnd_apply_chunk<2, K>(a, ch, x0, ni, nb, from, e, r0, r1, M)
+                                                : rnd_apply_chunk<kChE, K>(a, ch, x0, ni, nb, from, e, r0, r1, M);
   if (l == 0) {
     // the chunk's sub-ops (record + bucket entry), its planes in and out, its count
     atomicAdd(rd.acct + doc, 40ull * nb + 4ull * rd.planes * (unsigned long long)(n_before + ni) + 8ull);

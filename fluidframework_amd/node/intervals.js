@@ -243,7 +243,21 @@ class IntervalCollection {
     if (this._tracksSlides()) this.endTree.put(ival, ival);
   }
   _endRemove(ival) {
-    if (this._tracksSlides()) this.endTree.remove(ival);
+    if (!this._tracksSlides()) return;
+    try {
+      this.endTree.remove(ival);
+    } catch (e) {
+      if (!(e instanceof TypeError)) throw e;
+      // an end whose unit the zamboni took no longer compares as it did (the
+      // reference keeps comparing the removed segment's stale ordinal,
+      // referencePositions.ts:81-89): the descent left the tree -- rebuilt,
+      // the intervals put in index order, without this one
+      this.endTree = new RedBlackTree(this.endTree.compare);
+      for (const x of Array.from(this.byId.values()).sort((a, b) => a.stamp - b.stamp)) {
+        if (x !== ival) this.endTree.put(x, x);
+      }
+      this.endRebuilds = (this.endRebuilds || 0) + 1;
+    }
   }
   _ends() {
     if (this._tracksSlides()) return this.endTree;
