@@ -47,8 +47,9 @@ hipError_t launch_round_run(const ReplayArgs& a, const ChunkArgs& ch, const Roun
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_rnd_diag), sizeof h) == hipSuccess)
       fprintf(stderr,
               "rnd_diag blocks %llu serial %llu ops %llu clk_block %llu clk_gather %llu clk_serial %llu recs %llu "
-              "back %llu find %llu fwd %llu out %llu\n",
-              h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10]);
+              "back %llu find %llu fwd %llu out %llu apply_waves %llu apply_load %llu apply_ops %llu apply_subops %llu "
+              "apply_head %llu\n",
+              h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12], h[13], h[14], h[15]);
   }
 #endif
   const uint32_t n_docs = rd.nd;  // this launch's slice of the documents

@@ -154,7 +154,7 @@ constexpr int kT = kChE * kWave;  // flat slots per tile
 // two-slot-per-lane registers); the chunk count stays within nch_cap, the
 // fill is total / chunks rounded up (rnd_fill)
 #ifndef MTE_RND_FILL
-#define MTE_RND_FILL 80
+#define MTE_RND_FILL 128
 #endif
 __device__ __forceinline__ uint32_t rnd_fill(uint32_t total, uint32_t nch) { return nch ? (total + nch - 1) / nch : 1u; }
 
@@ -985,10 +985,15 @@ template <int E, int K>
 __device__ __forceinline__ int rnd_apply_chunk(const ReplayArgs& a, const ChunkArgs& ch, uint64_t x0, int& ni,
                                                uint32_t nb, int from, const uint2& e, const uint4& r0,
                                                const uint4& r1, int32_t M) {
+  RND_CLK(a0);
   Regs<E, K> R;
   ch_load_e<E, K>(R, ch, x0, ni);
   uint32_t st[kNumStats] = {};
   int rcs = 0;
+#if MTE_RND_DIAG
+  R.len[0] += __builtin_amdgcn_readfirstlane(0);  // (the planes are in)
+#endif
+  RND_CLK(a1);
   for (uint32_t j = 0; j < nb; j++) {
     const int q = rdlane(from, (int)j);
     const int32_t ex = (int32_t)rdlane(e.y, q);
@@ -1007,7 +1012,11 @@ __device__ __forceinline__ int rnd_apply_chunk(const ReplayArgs& a, const ChunkA
                                                tot, dlen, a, st);
     rcs = rc != 0 ? rc : rcs;
   }
+  RND_CLK(a2);
   ch_store_e<E, K>(R, ch, x0, ni);
+  RND_DIAG(12, a1 - a0);
+  RND_DIAG(13, a2 - a1);
+  RND_DIAG(14, nb);
   return rcs;
 }
 
@@ -1023,6 +1032,7 @@ __global__ __launch_bounds__(256) void rnd_apply_kernel(ReplayArgs a, ChunkArgs 
   if (p.x != kModeRound || rd.rflag[doc] != 0u || i >= (int)rd.nch[doc]) return;
   // the sub-op count and bucket and the segment count, issued together; then
   // each sub-op's record (bucket order)
+  RND_CLK(w0);
   const uint32_t nb = rd.rcnt[(uint64_t)doc * ch.nch_cap + i];
   const uint2 e0 = rd.rbuf[((uint64_t)doc * ch.nch_cap + i) * kRB + (l < kRB ? l : 0)];
   uint32_t* cntp = ch.cnt + (uint64_t)doc * ch.nch_cap;
@@ -1043,6 +1053,10 @@ __global__ __launch_bounds__(256) void rnd_apply_kernel(ReplayArgs a, ChunkArgs 
   const int dst = (l < (int)nb ? (int)rank : l) << 2;
   const int from = __builtin_amdgcn_ds_permute(dst, l);
   const int32_t M = (int32_t)p.w;
+#if MTE_RND_DIAG
+  RND_DIAG(11, 1);
+  RND_DIAG(15, clock64() - w0 + 0 * (r0.x + r1.w + (uint32_t)from));
+#endif
   const int rcs = ni + 2 * (int)nb <= 2 * kWave ? rnd_apply_chunk<2, K>(a, ch, x0, ni, nb, from, e, r0, r1, M)
                                                 : rnd_apply_chunk<kChE, K>(a, ch, x0, ni, nb, from, e, r0, r1, M);
   if (l == 0) {
