@@ -94,9 +94,10 @@ __device__ __forceinline__ void ch_load(Regs<kChE, K>& R, const ChunkArgs& ch, u
   const uint32_t* pl = ch.arena + x0 + (uint32_t)lane_id() * kChE;
   const uint64_t st = ch.astride;
   uint4 q[kFieldPlanes + K];
-#pragma unroll
-  for (int p = 0; p < kFieldPlanes + K; p++) q[p] = ld4(pl + p * st);
   const int base = lane_id() * kChE;
+  // the lanes past the chunk's segments read nothing (their slots are padding)
+#pragma unroll
+  for (int p = 0; p < kFieldPlanes + K; p++) q[p] = base < n ? ld4(pl + p * st) : make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
   for (int j = 0; j < kChE; j++) {
     const bool v = base + j < n;

@@ -774,7 +774,7 @@ void free_image(mte_ctx* c) {
 void free_docs(mte_ctx* c) {
   free_image(c);
   void* cs[] = {c->ch.arena, c->ch.cnt, c->ch.kc, c->ch.sum, c->rd.plan, c->rd.acct, c->rd.rcnt, c->rd.rbuf, c->rd.rflag,
-                c->rd.nch, c->rd.nnew, c->rd.count, c->rd.rlist, c->rd.rchain, c->rd.live, c->rd.gfl};
+                c->rd.nch, c->rd.nnew, c->rd.count, c->rd.rlist, c->rd.rchain, c->rd.live, c->rd.gfl, c->rd.rrec};
   for (void* p : cs)
     if (p) (void)hipFree(p);
   c->ch = ChunkArgs{};
@@ -1345,6 +1345,7 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
       HIPCHK(c, hipMemsetAsync(rd.acct, 0, sizeof(unsigned long long) * n_docs, c->stream));
       HIPCHK(c, hipMalloc((void**)&rd.rcnt, nch_all * 4));
       HIPCHK(c, hipMalloc((void**)&rd.rbuf, nch_all * kRB * sizeof(uint2)));
+      HIPCHK(c, hipMalloc((void**)&rd.rrec, nch_all * kRB * 2 * sizeof(uint4)));
       HIPCHK(c, hipMalloc((void**)&rd.rflag, 4 * (uint64_t)n_docs));
       HIPCHK(c, hipMalloc((void**)&rd.nch, 4 * (uint64_t)n_docs));
       HIPCHK(c, hipMalloc((void**)&rd.nnew, 4 * (uint64_t)n_docs));

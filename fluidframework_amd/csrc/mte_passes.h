@@ -28,6 +28,7 @@ struct RoundArgs {
   uint4* plan;      // [doc] x mode, y k0, z k1, w M
   uint32_t* rcnt;   // [doc][nch_cap] sub-ops per chunk
   uint2* rbuf;      // [doc][nch_cap][kRB] (op index - k0, chunk start in the op's perspective)
+  uint4* rrec;      // [doc][nch_cap][kRB][2] the sub-op's record, copied there by rnd_bucket
   uint32_t* rflag;  // [doc] non-zero: the run replays op after op
   uint32_t* nch;    // [doc] chunks after the re-layout
   uint32_t* nnew;   // [doc] segments after the re-layout

@@ -924,8 +924,18 @@ __global__ __launch_bounds__(256) void rnd_bucket_kernel(ReplayArgs a, ChunkArgs
   const uint4 en = rd.rlist[(uint64_t)doc * rd.rl_cap + e];
   uint32_t* rcnt = rd.rcnt + (uint64_t)doc * ch.nch_cap;
   const uint32_t pos = atomicAdd(rcnt + en.x, 1u);
-  if (pos < (uint32_t)kRB) rd.rbuf[((uint64_t)doc * ch.nch_cap + en.x) * kRB + pos] = make_uint2(en.y, en.z);
-  else atomicOr(rd.rflag + doc, 1u);
+  if (pos < (uint32_t)kRB) {
+    // the entry and the sub-op's record next to it: the apply reads its chunk's
+    // records in one contiguous load instead of one dependent random read each
+    const uint64_t slot = ((uint64_t)doc * ch.nch_cap + en.x) * kRB + pos;
+    const uint4* rec = a.recs + 2 * (a.op_off[doc] + p.y + en.y);
+    const uint4 q0 = rec[0], q1 = rec[1];
+    rd.rbuf[slot] = make_uint2(en.y, en.z);
+    rd.rrec[2 * slot] = q0;
+    rd.rrec[2 * slot + 1] = q1;
+  } else {
+    atomicOr(rd.rflag + doc, 1u);
+  }
 }
 
 // a chunk's first E * 64 slots into registers (E = 2: one 8-byte load per
@@ -939,9 +949,10 @@ __device__ __forceinline__ void ch_load_e(Regs<E, K>& R, const ChunkArgs& ch, ui
     const uint32_t* pl = ch.arena + x0 + (uint32_t)lane_id() * E;
     const uint64_t st = ch.astride;
     uint2 q[kFieldPlanes + K];
-#pragma unroll
-    for (int p = 0; p < kFieldPlanes + K; p++) q[p] = *reinterpret_cast<const uint2*>(pl + p * st);
     const int base = lane_id() * E;
+#pragma unroll
+    for (int p = 0; p < kFieldPlanes + K; p++)
+      q[p] = base < n ? *reinterpret_cast<const uint2*>(pl + p * st) : make_uint2(0u, 0u);
 #pragma unroll
     for (int j = 0; j < E; j++) {
       const bool v = base + j < n;
@@ -1034,19 +1045,16 @@ __global__ __launch_bounds__(256) void rnd_apply_kernel(ReplayArgs a, ChunkArgs 
   // each sub-op's record (bucket order)
   RND_CLK(w0);
   const uint32_t nb = rd.rcnt[(uint64_t)doc * ch.nch_cap + i];
-  const uint2 e0 = rd.rbuf[((uint64_t)doc * ch.nch_cap + i) * kRB + (l < kRB ? l : 0)];
+  const uint64_t bslot = ((uint64_t)doc * ch.nch_cap + i) * kRB + (l < kRB ? l : 0);
+  const uint2 e0 = rd.rbuf[bslot];
+  const uint4 q0 = rd.rrec[2 * bslot], q1 = rd.rrec[2 * bslot + 1];
   uint32_t* cntp = ch.cnt + (uint64_t)doc * ch.nch_cap;
   int ni = (int)cntp[i];
   const int n_before = ni;
   const uint64_t x0 = ch_slot(ch, doc, i);
   if (nb == 0u) return;
   const uint2 e = l < (int)nb ? e0 : make_uint2(0xffffffffu, 0u);
-  const uint4* recp = a.recs + 2 * (a.op_off[doc] + p.y);
-  uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0;
-  if (l < (int)nb) {
-    r0 = recp[2 * e.x];
-    r1 = recp[2 * e.x + 1];
-  }
+  const uint4 r0 = l < (int)nb ? q0 : make_uint4(0u, 0u, 0u, 0u), r1 = l < (int)nb ? q1 : make_uint4(0u, 0u, 0u, 0u);
   // the bucket in op order: each entry's rank, and per rank the lane holding it
   uint32_t rank = 0;
   for (uint32_t j = 0; j < nb; j++) rank += rdlane(e.x, (int)j) < e.x ? 1u : 0u;
