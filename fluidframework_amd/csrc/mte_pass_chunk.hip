@@ -1,4 +1,5 @@
 // The chunked pass (mte_chunk.h) in its own translation unit.
+#include <algorithm>
 #include <cstdio>
 
 #include "mte_passes.h"
@@ -83,7 +84,10 @@ hipError_t launch_round_run(const ReplayArgs& a, const ChunkArgs& ch, const Roun
   hipLaunchKernelGGL(rnd_bucket_kernel, dim3(n_docs * bpd), dim3(256), 0, s, a, ch, rd, bpd);
   hipLaunchKernelGGL(rnd_room_kernel, dim3((uint32_t)((chunks + 255) / 256)), dim3(256), 0, s, a, ch, rd);
   // apply: every chunk with sub-ops on its own wave
-  hipLaunchKernelGGL((rnd_apply_kernel<K>), dim3((uint32_t)((chunks + 3) / 4)), w4, 0, s, a, ch, rd);
+  {  // a fixed grid (rnd_apply_kernel walks the chunk slots): 2 workgroups per SIMD's worth
+    const uint32_t g = (uint32_t)std::min<uint64_t>((chunks + 3) / 4, 2048);
+    hipLaunchKernelGGL((rnd_apply_kernel<K>), dim3(g), w4, 0, s, a, ch, rd);
+  }
   // the header past the run (the segments stay in the arena); the refused runs'
   // carried documents back to the flat planes
   hipLaunchKernelGGL(rnd_scan_kernel, dim3(n_docs), dim3(kChWaves * kWave), 0, s, a, ch, rd, 1);

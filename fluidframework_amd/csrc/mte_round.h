@@ -1031,14 +1031,16 @@ __device__ __forceinline__ int rnd_apply_chunk(const ReplayArgs& a, const ChunkA
   return rcs;
 }
 
-// one wave per chunk of a run: its sub-ops in op order; a chunk that stays
-// within 128 slots (its segments + 2 per sub-op) at two slots per lane
+// one wave per chunk of a run: its sub-ops in op order (MTE_APPLY_E2: a chunk
+// that stays within 128 slots -- its segments + 2 per sub-op -- at two slots
+// per lane; off: both paths' registers cost the kernel half its occupancy)
+#ifndef MTE_APPLY_E2
+#define MTE_APPLY_E2 0
+#endif
 template <int K>
-__global__ __launch_bounds__(256) void rnd_apply_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
-  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
-  const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
-  const int doc = (int)rd.d0 + (int)(wi / ch.nch_cap), i = (int)(wi % ch.nch_cap);
-  if (doc >= (int)(rd.d0 + rd.nd)) return;
+__device__ __forceinline__ void rnd_apply_one(const ReplayArgs& a, const ChunkArgs& ch, const RoundArgs& rd, int doc,
+                                              int i) {
+  const int l = lane_id();
   const uint4 p = rd.plan[doc];
   if (p.x != kModeRound || rd.rflag[doc] != 0u || i >= (int)rd.nch[doc]) return;
   // the sub-op count and bucket and the segment count, issued together; then
@@ -1065,14 +1067,28 @@ __global__ __launch_bounds__(256) void rnd_apply_kernel(ReplayArgs a, ChunkArgs 
   RND_DIAG(11, 1);
   RND_DIAG(15, clock64() - w0 + 0 * (r0.x + r1.w + (uint32_t)from));
 #endif
+#if MTE_APPLY_E2
   const int rcs = ni + 2 * (int)nb <= 2 * kWave ? rnd_apply_chunk<2, K>(a, ch, x0, ni, nb, from, e, r0, r1, M)
                                                 : rnd_apply_chunk<kChE, K>(a, ch, x0, ni, nb, from, e, r0, r1, M);
+#else
+  const int rcs = rnd_apply_chunk<kChE, K>(a, ch, x0, ni, nb, from, e, r0, r1, M);
+#endif
   if (l == 0) {
     // the chunk's sub-ops (record + bucket entry), its planes in and out, its count
     atomicAdd(rd.acct + doc, 40ull * nb + 4ull * rd.planes * (unsigned long long)(n_before + ni) + 8ull);
     cntp[i] = (uint32_t)ni;
     if (rcs != 0) a.hdr[doc].status = MTE_E_STATE;  // resolve guarantees every sub-op fits: an engine bug
   }
+}
+
+// a fixed grid of waves walking the (document, chunk) slots with a stride: the
+// slots past a document's chunk count cost a test, not a wave launch
+template <int K>
+__global__ __launch_bounds__(256) void rnd_apply_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
+  const uint64_t n = (uint64_t)rd.nd * ch.nch_cap, stride = (uint64_t)gridDim.x * 4;
+  for (uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w; wi < n; wi += stride)
+    rnd_apply_one<K>(a, ch, rd, (int)rd.d0 + (int)(wi / ch.nch_cap), (int)(wi % ch.nch_cap));
 }
 
 }  // namespace mte
