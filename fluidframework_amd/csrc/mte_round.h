@@ -148,6 +148,17 @@ __global__ __launch_bounds__(512) void rnd_plan_kernel(ReplayArgs a, RoundArgs r
 
 // ---- re-layout and gather: many waves per document ---------------------------
 
+// a fixed grid of waves walking the (document, chunk) slots with a stride
+// (launched at most 2048 x 4 waves): a slot past a document's chunk count, or
+// of a document the kernel skips, costs a test, not a wave launch
+template <typename F>
+__device__ __forceinline__ void chunk_walk(const ChunkArgs& ch, const RoundArgs& rd, F&& f) {
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
+  const uint64_t n = (uint64_t)rd.nd * ch.nch_cap, stride = (uint64_t)gridDim.x * 4;
+  for (uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w; wi < n; wi += stride)
+    f((int)rd.d0 + (int)(wi / ch.nch_cap), (int)(wi % ch.nch_cap));
+}
+
 constexpr int kT = kChE * kWave;  // flat slots per tile
 // segments per chunk a re-layout aims at (fewer than the chunk pass's kChFill:
 // more chunks, and a chunk plus its run's sub-ops then fits the apply's
@@ -281,51 +292,49 @@ __global__ __launch_bounds__(256) void rnd_move_kernel(ReplayArgs a, ChunkArgs c
 // per chunk after the moves: its segment count and its round-start column
 // entry (the visible length: every segment is seen at refSeq R), into kc
 __global__ __launch_bounds__(256) void rnd_cols_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
-  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
-  const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
-  const int doc = (int)rd.d0 + (int)(wi / ch.nch_cap), q = (int)(wi % ch.nch_cap);
-  if (doc >= (int)(rd.d0 + rd.nd)) return;
-  const uint4 p = rd.plan[doc];
-  if (p.x != kModeRound || q >= (int)rd.nch[doc]) return;
-  // a re-laid-out document: kChFill per chunk; a carried one: its counts
-  const int n_new = (int)rd.nnew[doc], fill = (int)rnd_fill(rd.nnew[doc], rd.nch[doc]);
-  const int cn = rd.live[doc] == 1u ? (int)ch.cnt[(uint64_t)doc * ch.nch_cap + q]
-                 : (n_new - q * fill < fill ? (n_new - q * fill > 0 ? n_new - q * fill : 0) : fill);
-  const uint64_t x0 = ch_slot(ch, doc, q);
-  int32_t v = 0;
+  const int l = lane_id();
+  chunk_walk(ch, rd, [&](int doc, int q) {
+    const uint4 p = rd.plan[doc];
+    if (p.x != kModeRound || q >= (int)rd.nch[doc]) return;
+    // a re-laid-out document: kChFill per chunk; a carried one: its counts
+    const int n_new = (int)rd.nnew[doc], fill = (int)rnd_fill(rd.nnew[doc], rd.nch[doc]);
+    const int cn = rd.live[doc] == 1u ? (int)ch.cnt[(uint64_t)doc * ch.nch_cap + q]
+                   : (n_new - q * fill < fill ? (n_new - q * fill > 0 ? n_new - q * fill : 0) : fill);
+    const uint64_t x0 = ch_slot(ch, doc, q);
+    int32_t v = 0;
 #pragma unroll
-  for (int j = 0; j < kChSlots / kWave; j++) {
-    const int s = j * kWave + l;
-    if (s < cn) v += (int32_t)ch.arena[2 * ch.astride + x0 + s] == kNone ? (int32_t)ch.arena[x0 + s] : 0;
-  }
-  const int32_t tot = rdlane(wave_incl_scan(v), kWave - 1);
-  if (l == 0) {
-    ch.cnt[(uint64_t)doc * ch.nch_cap + q] = (uint32_t)cn;
-    ch.kc[(uint64_t)doc * ch.nch_cap + q] = (uint32_t)tot;
-  }
+    for (int j = 0; j < kChSlots / kWave; j++) {
+      const int s = j * kWave + l;
+      if (s < cn) v += (int32_t)ch.arena[2 * ch.astride + x0 + s] == kNone ? (int32_t)ch.arena[x0 + s] : 0;
+    }
+    const int32_t tot = rdlane(wave_incl_scan(v), kWave - 1);
+    if (l == 0) {
+      ch.cnt[(uint64_t)doc * ch.nch_cap + q] = (uint32_t)cn;
+      ch.kc[(uint64_t)doc * ch.nch_cap + q] = (uint32_t)tot;
+    }
+  });
 }
 
 // chunk -> flat planes at its prefix (nothing is dropped: the run's
 // tombstones have removedSeq > R >= M), one wave per chunk
 template <int K>
 __global__ __launch_bounds__(256) void rnd_gmove_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
-  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
-  const uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
-  const int doc = (int)rd.d0 + (int)(wi / ch.nch_cap), q = (int)(wi % ch.nch_cap);
-  if (doc >= (int)(rd.d0 + rd.nd)) return;
-  if (rd.gfl[doc] == 0u || q >= (int)rd.nch[doc]) return;
-  const int cn = (int)ch.cnt[(uint64_t)doc * ch.nch_cap + q];
-  const uint32_t d0 = ch.kc[(uint64_t)doc * ch.nch_cap + q];
-  const uint64_t x0 = ch_slot(ch, doc, q);
-  uint32_t* pl = a.planes + (uint64_t)doc * a.cap;
-  for (int qq = 0; qq < kFieldPlanes + K; qq++) {
+  const int l = lane_id();
+  chunk_walk(ch, rd, [&](int doc, int q) {
+    if (rd.gfl[doc] == 0u || q >= (int)rd.nch[doc]) return;
+    const int cn = (int)ch.cnt[(uint64_t)doc * ch.nch_cap + q];
+    const uint32_t d0 = ch.kc[(uint64_t)doc * ch.nch_cap + q];
+    const uint64_t x0 = ch_slot(ch, doc, q);
+    uint32_t* pl = a.planes + (uint64_t)doc * a.cap;
+    for (int qq = 0; qq < kFieldPlanes + K; qq++) {
 #pragma unroll
-    for (int j = 0; j < kChE; j++) {
-      const int s = j * kWave + l;
-      if (s < cn && d0 + (uint32_t)s < a.cap)
-        pl[(uint64_t)qq * a.stride + d0 + (uint32_t)s] = ch.arena[(uint64_t)qq * ch.astride + x0 + s];
+      for (int j = 0; j < kChE; j++) {
+        const int s = j * kWave + l;
+        if (s < cn && d0 + (uint32_t)s < a.cap)
+          pl[(uint64_t)qq * a.stride + d0 + (uint32_t)s] = ch.arena[(uint64_t)qq * ch.astride + x0 + s];
+      }
     }
-  }
+  });
 }
 
 // ---- carried layouts ------------------------------------------------------------
