@@ -1230,7 +1230,8 @@ __device__ __forceinline__ int ht_ack(HT& h, const s8v& op, const ReplayArgs& a,
         }
         if (rs == kLocalBase + ls) h.pl[2 * h.sd + i] = (uint32_t)s;
         if (lr == ls) {  // acked, or overtaken by a remote remove before (:1928-1938)
-          h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = 0u;
+          // (an acked removal keeps ls until its slides: it marks the group's segments)
+          if (rs != kLocalBase + ls || !(rt && rhi)) h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = 0u;
           member[j] = true;
         }
 #pragma unroll
@@ -1252,9 +1253,18 @@ __device__ __forceinline__ int ht_ack(HT& h, const s8v& op, const ReplayArgs& a,
         }
       }
     }
-    if (rt && rhi)
-      stream_slide(h.pl, h.sd, h.n, rt, rhi, s, ev, lo == hi ? kSlideAck : kSlideAll,
-                   h.pl + (uint64_t)kGrpPlane<K> * h.sd, h.tw);
+    if (rt && rhi) {
+      // this localSeq's group slides in its order, the later groups still pending
+      // (ackPendingSegment per group op, mergeTree.ts:1278-1304)
+      uint32_t* lrp = h.pl + (uint64_t)kLrsPlane<K> * h.sd;
+      stream_slide(h.pl, h.sd, h.n, rt, rhi, s, ev, kSlideAck, h.pl + (uint64_t)kGrpPlane<K> * h.sd, h.tw, lrp,
+                   (uint32_t)ls);
+      for (int tb = 0; tb < h.n; tb += kWave) {
+        const int i = tb + l;
+        if (i < h.n && (int32_t)ld_l2(lrp + i) == ls) lrp[i] = 0u;
+      }
+      vm_drain();
+    }
     if ((rc = ht_zamboni<K>(h, a.n_keys))) return rc;
   }
   return 0;

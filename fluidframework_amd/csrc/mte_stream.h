@@ -131,9 +131,11 @@ __device__ __forceinline__ bool slide_ok(int32_t sq, int32_t rs) { return sq < k
 // references slide (ackPendingSegment, mergeTree.ts:1285-1304)
 // tw (the tree words, or nullptr): a merged leaf's items are one segment, so
 // the search starts past x's leaf (its kTCont continuations / its head)
+// gm / gid: a group member's word in plane gm is gid (its localSeq)
 __device__ __forceinline__ int find_slide_target(const uint32_t* pl, uint64_t sd, int n, int x, int dir,
                                                  int32_t grp = 0, const uint32_t* gp = nullptr, uint32_t cur = 0,
-                                                 const uint32_t* tw = nullptr) {
+                                                 const uint32_t* tw = nullptr, const uint32_t* gm = nullptr,
+                                                 uint32_t gid = 0) {
   const int l = lane_id();
   if (dir > 0) {
     int b0 = x + 1;
@@ -143,7 +145,7 @@ __device__ __forceinline__ int find_slide_target(const uint32_t* pl, uint64_t sd
       const int i = b + l;
       const int ic = i < n ? i : 0;  // unconditional loads, selected after
       const int32_t sq = (int32_t)ld_l2(pl + sd + ic), rs = (int32_t)ld_l2(pl + 2 * sd + ic);
-      const bool pend = grp != 0 && rs == grp && sq < kLocalBase && ld_l2(gp + ic) > cur;
+      const bool pend = grp != 0 && rs == grp && sq < kLocalBase && ld_l2(gp + ic) > cur && ld_l2(gm + ic) == gid;
       const uint64_t m = __ballot(i < n && (slide_ok(sq, rs) || pend));
       if (m) return b + __ffsll((long long)m) - 1;
     }
@@ -155,7 +157,7 @@ __device__ __forceinline__ int find_slide_target(const uint32_t* pl, uint64_t sd
       const int i = e - kWave + l;
       const int ic = i >= 0 ? i : 0;
       const int32_t sq = (int32_t)ld_l2(pl + sd + ic), rs = (int32_t)ld_l2(pl + 2 * sd + ic);
-      const bool pend = grp != 0 && rs == grp && sq < kLocalBase && ld_l2(gp + ic) > cur;
+      const bool pend = grp != 0 && rs == grp && sq < kLocalBase && ld_l2(gp + ic) > cur && ld_l2(gm + ic) == gid;
       const uint64_t m = __ballot(i >= 0 && (slide_ok(sq, rs) || pend));
       if (m) return e - kWave + (63 - __builtin_clzll(m));
     }
@@ -188,7 +190,7 @@ enum { kSlideAll = 0, kSlideAck = 1, kSlideOverlap = 2, kSlideNew = 3 };
 // one removed segment x's references (grp / gp / cur: find_slide_target)
 __device__ __forceinline__ void slide_segment(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t rhi, int x,
                                               EvOut* ev, int32_t grp, const uint32_t* gp, uint32_t cur,
-                                              const uint32_t* tw) {
+                                              const uint32_t* tw, const uint32_t* gm = nullptr, uint32_t gid = 0) {
   const int l = lane_id();
   const uint32_t toff = uni(ld_l2(pl + 5 * sd + x)), len = uni(ld_l2(pl + x));
   // an item continuing a merged leaf is one segment with the items before it:
@@ -196,10 +198,10 @@ __device__ __forceinline__ void slide_segment(const uint32_t* pl, uint64_t sd, i
   uint32_t lead = 0;
   if (tw)
     for (int y = x; y > 0 && (uni(ld_l2(tw + y)) & kTCont); y--) lead += uni(ld_l2(pl + y - 1));
-  int t = find_slide_target(pl, sd, n, x, 1, grp, gp, cur, tw);
+  int t = find_slide_target(pl, sd, n, x, 1, grp, gp, cur, tw, gm, gid);
   bool after = false;
   if (t < 0) {
-    t = find_slide_target(pl, sd, n, x, -1, grp, gp, cur, tw);
+    t = find_slide_target(pl, sd, n, x, -1, grp, gp, cur, tw, gm, gid);
     after = t >= 0;
   }
   uint32_t to = 0;
@@ -242,9 +244,9 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   return v;
 }
 
-// mode: kSlideAll every such segment; kSlideAck the removals of one ack in
-// group order (gp: the group-order plane), each slid while the later ones are
-// still pending (a reference can slide again from a later one: one record per
+// mode: kSlideAll every such segment; kSlideAck the removals of one localSeq's
+// group (gm / gid: its members hold gid there) in group order (gp: the
+// group-order plane), each slid while the later ones are still pending (a reference can slide again from a later one: one record per
 // slide); kSlideOverlap / kSlideNew a remote remove's segments that the local
 // client had removed already (lrp: the local-removal plane, non-zero) -- slid
 // before the delta callback -- then the newly removed ones, after it
@@ -252,7 +254,8 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // the group-order plane (kSlideAck).
 __device__ __forceinline__ void stream_slide(const uint32_t* pl, uint64_t sd, int n, uint2* rt, uint32_t rhi, int32_t s,
                                              EvOut* ev = nullptr, int mode = kSlideAll,
-                                             const uint32_t* lrp = nullptr, const uint32_t* tw = nullptr) {
+                                             const uint32_t* lrp = nullptr, const uint32_t* tw = nullptr,
+                                             const uint32_t* gm = nullptr, uint32_t gid = 0) {
   const int l = lane_id();
   if (mode == kSlideAck) {
     const uint32_t* gp = lrp;
@@ -266,7 +269,7 @@ __device__ __forceinline__ void stream_slide(const uint32_t* pl, uint64_t sd, in
         const int ic = i < n ? i : 0;
         const int32_t rs = (int32_t)ld_l2(pl + 2 * sd + ic);
         const uint32_t g = ld_l2(gp + ic);
-        const bool c = i < n && rs == s && (first || g > cur);
+        const bool c = i < n && rs == s && ld_l2(gm + ic) == gid && (first || g > cur);
         const uint32_t mn = wave_min_u32(c ? g : 0xffffffffu);
         const uint64_t at = __ballot(c && g == mn);
         if (at && (bx < 0 || mn < best)) {
@@ -276,7 +279,7 @@ __device__ __forceinline__ void stream_slide(const uint32_t* pl, uint64_t sd, in
       }
       if (bx < 0) return;
       cur = best;
-      slide_segment(pl, sd, n, rt, rhi, bx, ev, s, gp, cur, tw);
+      slide_segment(pl, sd, n, rt, rhi, bx, ev, s, gp, cur, tw, gm, gid);
     }
   }
   for (int tb = 0; tb < n; tb += kWave) {

@@ -104,6 +104,7 @@ typedef struct {
   /* MTE_DOC_REFS: reference slots (as oracle.c) */
   uint32_t *ref_anchor, *ref_state;
   uint32_t ref_cap, ref_hi;
+  int32_t slide_gid; /* the localSeq whose removal group an ack is sliding (doc_ack) */
   /* MTE_DOC_EVENTS: the last batch's delta events, the record being applied */
   mte_delta* dl;
   uint64_t dl_n, dl_cap;
@@ -678,22 +679,22 @@ static inline int removed_and_acked(const item* g) { return g->rseq != NONE_SEQ 
 /* where a reference on item i slides to (forwardExcursion / backwardExcursion,
  * client.ts:1117-1130): offset 0 of the first following segment, else the last
  * unit of the last preceding one; -1: nowhere */
-static inline int grp_pending(const item* g, int32_t grp, uint32_t cur) {
-  return grp && g->rseq == grp && !g->empty && g->seq < LOCAL_BASE && g->gord > cur;
+static inline int grp_pending(const item* g, int32_t grp, uint32_t cur, int32_t gid) {
+  return grp && g->rseq == grp && !g->empty && g->seq < LOCAL_BASE && g->gord > cur && g->lrs == gid;
 }
 static int64_t slide_to_grp(const idoc* d, uint32_t i, uint32_t* anchor, int32_t grp, uint32_t cur) {
   /* a merged leaf's items are one segment: search past i's leaf */
   uint32_t j0 = i + 1;
   while (j0 < d->n && d->it[j0].cont) j0++;
   for (uint32_t j = j0; j < d->n; j++)
-    if (slide_target_ok(&d->it[j]) || grp_pending(&d->it[j], grp, cur)) {
+    if (slide_target_ok(&d->it[j]) || grp_pending(&d->it[j], grp, cur, d->slide_gid)) {
       *anchor = d->it[j].toff;
       return j;
     }
   int64_t h0 = i;
   while (h0 > 0 && d->it[h0].cont) h0--;
   for (int64_t j = h0 - 1; j >= 0; j--)
-    if (slide_target_ok(&d->it[j]) || grp_pending(&d->it[j], grp, cur)) {
+    if (slide_target_ok(&d->it[j]) || grp_pending(&d->it[j], grp, cur, d->slide_gid)) {
       *anchor = d->it[j].toff + (uint32_t)d->it[j].len - 1u;
       return j;
     }
@@ -1067,7 +1068,7 @@ static int doc_slide_refs(idoc* d, int32_t s, int mode) {
       int64_t bx = -1;
       for (uint32_t i = 0; i < d->n; i++) {
         const item* g = &d->it[i];
-        if (g->rseq != s || g->empty || (!first && g->gord <= cur)) continue;
+        if (g->rseq != s || g->empty || g->lrs != d->slide_gid || (!first && g->gord <= cur)) continue;
         if (bx < 0 || g->gord < d->it[bx].gord) bx = i;
       }
       if (bx < 0) return MTE_OK;
@@ -1483,9 +1484,10 @@ static int doc_ack(idoc* d, const mte_op* op, const env_t* env) {
         g->seq = s;
         member = 1;
       }
-      if (g->rseq == LOCAL_BASE + ls) g->rseq = s;
+      const int acked_rm = g->rseq == LOCAL_BASE + ls;
+      if (acked_rm) g->rseq = s;
       if (g->lrs == ls) { /* acked, or overtaken by a remote remove before (:1928-1938) */
-        g->lrs = 0;
+        if (!acked_rm) g->lrs = 0; /* an acked removal keeps ls until its slides: the group's mark */
         member = 1;
       }
       for (uint32_t k = 0; k < MTE_MAX_KEYS; k++)
@@ -1496,7 +1498,10 @@ static int doc_ack(idoc* d, const mte_op* op, const env_t* env) {
       }
       if (member && !g->cont && (rc = add_lru(d, i, s))) return rc;
     }
-    if ((rc = doc_slide_refs(d, s, lo == hi ? 1 : 0))) return rc;
+    d->slide_gid = ls;  /* this localSeq's group, in its order (ackPendingSegment per group op) */
+    if ((rc = doc_slide_refs(d, s, 1))) return rc;
+    for (uint32_t i = 0; i < d->n; i++)
+      if (d->it[i].lrs == ls) d->it[i].lrs = 0;
     zamboni(d, env->arena, env->n_keys);
   }
   return MTE_OK;
