@@ -1228,11 +1228,16 @@ __device__ __forceinline__ int ht_ack(HT& h, const s8v& op, const ReplayArgs& a,
           h.pl[h.sd + i] = (uint32_t)s;
           member[j] = true;
         }
-        if (rs == kLocalBase + ls) h.pl[2 * h.sd + i] = (uint32_t)s;
         if (lr == ls) {  // acked, or overtaken by a remote remove before (:1928-1938)
-          // (an acked removal keeps ls until its slides: it marks the group's segments)
-          if (rs != kLocalBase + ls || !(rt && rhi)) h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = 0u;
+          h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = 0u;
           member[j] = true;
+        }
+        if (rs == kLocalBase + ls) {
+          h.pl[2 * h.sd + i] = (uint32_t)s;
+          // the group's removals hold ls until they have slid (stream_slide's
+          // group mark; a regenerated one's localRemovedSeq is its old op's)
+          // (acked: localRemovedSeq undefined, mergeTreeNodes.ts:493)
+          h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = (rt && rhi) ? (uint32_t)ls : 0u;
         }
 #pragma unroll
         for (int k = 0; k < K; k++)

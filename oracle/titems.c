@@ -1484,11 +1484,16 @@ static int doc_ack(idoc* d, const mte_op* op, const env_t* env) {
         g->seq = s;
         member = 1;
       }
-      const int acked_rm = g->rseq == LOCAL_BASE + ls;
-      if (acked_rm) g->rseq = s;
       if (g->lrs == ls) { /* acked, or overtaken by a remote remove before (:1928-1938) */
-        if (!acked_rm) g->lrs = 0; /* an acked removal keeps ls until its slides: the group's mark */
+        g->lrs = 0;
         member = 1;
+      }
+      if (g->rseq == LOCAL_BASE + ls) {
+        g->rseq = s;
+        /* the group's removals hold ls until they have slid (doc_slide_refs'
+         * group mark; a regenerated one's localRemovedSeq is its old op's);
+         * acked: localRemovedSeq undefined (mergeTreeNodes.ts:493) */
+        g->lrs = ((d->flags & MTE_DOC_REFS) && d->ref_hi) ? ls : 0;
       }
       for (uint32_t k = 0; k < MTE_MAX_KEYS; k++)
         if (g->pk[k] && g->pk[k] <= (uint32_t)ls) g->pk[k] = 0;
