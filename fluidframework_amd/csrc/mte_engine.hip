@@ -876,6 +876,9 @@ int round_phase_loop(mte_ctx* c, const ReplayArgs& a, size_t lds, uint64_t max_o
     const uint32_t n_round = c->h_rcount[0], n_active = c->h_rcount[2];
     if (n_active == 0) break;
     if (n_round) {
+      // the resolve's columns: the largest round document's chunks (rnd_plan)
+      const uint32_t want = c->h_rcount[3] < 64u ? 64u : c->h_rcount[3];
+      rd.col_cap = (want + 63u) / 64u * 64u;
       HIPCHK(c, hipMemsetAsync(rd.rcnt, 0, nch_all * 4, c->stream));
       HIPCHK(c, hipMemsetAsync(rd.rflag, 0, 4 * (uint64_t)c->n_docs, c->stream));
       HIPCHK(c, (launch_round_run<K>(a, ch, rd, c->n_docs, c->stream)));

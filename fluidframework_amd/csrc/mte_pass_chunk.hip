@@ -69,7 +69,7 @@ hipError_t launch_round_run(const ReplayArgs& a, const ChunkArgs& ch, const Roun
   hipLaunchKernelGGL((rnd_move_kernel<K>), dim3((uint32_t)((tiles + 3) / 4)), w4, 0, s, a, ch, rd, tpd);
   hipLaunchKernelGGL(rnd_cols_kernel, dim3((uint32_t)((chunks + 3) / 4)), w4, 0, s, a, ch, rd);
   // resolve: the client chains, columns in LDS (two waves per workgroup when they fit)
-  const size_t col = (size_t)rnd_resolve_lds(ch.nch_cap, ch.ng_cap);
+  const size_t col = (size_t)rnd_resolve_lds(rd.col_cap, rd.col_cap / kChGroup);
   if (2 * col <= kRoundLdsMax) {
     hipError_t e = hipFuncSetAttribute((const void*)rnd_resolve_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)(2 * col));

@@ -42,6 +42,7 @@ struct RoundArgs {
   uint32_t* live;
   uint32_t* gfl;    // [doc] 1: this launch gathers the arena back into the flat planes
   uint32_t last;    // this phase sends every active document op after op
+  uint32_t col_cap; // chunks a resolve column holds (the phase's largest document, rounded to 64: rnd_plan's count[3])
   uint32_t d0, nd;  // the documents [d0, d0 + nd) one launch_round_run covers
   // [doc] the bytes the round phases of the last mte_run had to read and write
   // (their algorithmic bytes: records, planes re-laid out / applied /

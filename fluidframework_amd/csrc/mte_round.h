@@ -137,7 +137,14 @@ __global__ __launch_bounds__(512) void rnd_plan_kernel(ReplayArgs a, RoundArgs r
     const uint32_t k1 = k0 + len;
     // room for every op's segments (an insert or a range op adds at most 3)
     const bool room = (uint64_t)h.nseg + 3ull * len + 2ull <= (uint64_t)a.cap;
-    if (len >= kRoundMin && room) p = make_uint4(kModeRound, k0, k1, (uint32_t)M);
+    if (len >= kRoundMin && room) {
+      p = make_uint4(kModeRound, k0, k1, (uint32_t)M);
+      // the chunks this document's column may need: a carried layout's count,
+      // at most the re-layout's (its segments only drop) -- sizes the resolve's LDS
+      uint32_t nb = (uint32_t)((h.nseg + MTE_RND_FILL - 1) / MTE_RND_FILL);
+      if (rd.live[doc] == 1u && rd.nch[doc] > nb) nb = rd.nch[doc];
+      atomicMax(rd.count + 3, nb);
+    }
     else if (len >= kRoundMin) p = make_uint4(kModeSeq, k0, k1, 0u);  // this run, op after op
     else p = make_uint4(kModeSeq, k0, ktot, 0u);  // not round-shaped: the rest op after op
     atomicAdd(rd.count + (p.x == kModeRound ? 0 : 1), 1u);
@@ -790,14 +797,15 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
   C.ng = (C.nch + kChGroup - 1) / kChGroup;
   C.nsg = (C.ng + kWave - 1) / kWave;
   {
-    const uint32_t gs_cap = (ch.ng_cap + kWave - 1) / kWave * kWave;
-    int32_t* base = reinterpret_cast<int32_t*>(rs_lds) + (uint64_t)w * (ch.nch_cap + 2 * gs_cap + kWave + kRing);
+    // the column sized for this phase's largest document (rd.col_cap, a multiple of 64)
+    const uint32_t gs_cap = (rd.col_cap / kChGroup + kWave - 1) / kWave * kWave;
+    int32_t* base = reinterpret_cast<int32_t*>(rs_lds) + (uint64_t)w * (rd.col_cap + 2 * gs_cap + kWave + kRing);
     C.CI = base;
-    C.GS = base + ch.nch_cap;
-    C.SS = base + ch.nch_cap + gs_cap;
+    C.GS = base + rd.col_cap;
+    C.SS = base + rd.col_cap + gs_cap;
     C.GD = C.SS + kWave;
   }
-  uint32_t* const ring = reinterpret_cast<uint32_t*>(C.GD + (ch.ng_cap + kWave - 1) / kWave * kWave);
+  uint32_t* const ring = reinterpret_cast<uint32_t*>(C.GD + (rd.col_cap / kChGroup + kWave - 1) / kWave * kWave);
   const int32_t* sum0 = reinterpret_cast<const int32_t*>(ch.kc + (uint64_t)doc * ch.nch_cap);
   uint4* list = rd.rlist + (uint64_t)doc * rd.rl_cap;
   // ops per client (every workgroup of the document counts them all)
