@@ -60,6 +60,13 @@
 
 namespace mte {
 
+// segments per chunk a re-layout aims at (measured: 128 beats 96 / 80 / 64 --
+// more chunks cost the apply more waves than the narrower registers save); the
+// chunk count stays within nch_cap, the fill is total / chunks rounded up (rnd_fill)
+#ifndef MTE_RND_FILL
+#define MTE_RND_FILL 128
+#endif
+
 // diagnostic builds (tools/variants.sh ...:"-DMTE_RND_DIAG=1"): per resolve
 // [0] blocks, [1] blocks sent op by op, [2] ops, [3] clocks in blocks,
 // [4] clocks gathering, [5] clocks in the serial fallback, in rnd_block [6]
@@ -167,13 +174,6 @@ __device__ __forceinline__ void chunk_walk(const ChunkArgs& ch, const RoundArgs&
 }
 
 constexpr int kT = kChE * kWave;  // flat slots per tile
-// segments per chunk a re-layout aims at (fewer than the chunk pass's kChFill:
-// more chunks, and a chunk plus its run's sub-ops then fits the apply's
-// two-slot-per-lane registers); the chunk count stays within nch_cap, the
-// fill is total / chunks rounded up (rnd_fill)
-#ifndef MTE_RND_FILL
-#define MTE_RND_FILL 128
-#endif
 __device__ __forceinline__ uint32_t rnd_fill(uint32_t total, uint32_t nch) { return nch ? (total + nch - 1) / nch : 1u; }
 
 // keep counts of the flat tiles (removedSeq > M), one wave per tile
