@@ -27,7 +27,7 @@ import sys
 PATH_KERNELS = ("begin_batch_kernel", "props_kernel", "round_sync_kernel", "pair_kernel", "big_kernel", "stream_kernel",
                 "chunk_kernel", "tree_kernel", "rsmall_kernel", "rnd_plan_kernel", "rnd_count_kernel", "rnd_scan_kernel",
                 "rnd_move_kernel", "rnd_cols_kernel", "rnd_resolve_kernel", "rnd_bucket_kernel", "rnd_apply_kernel",
-                "rnd_gmove_kernel")
+                "rnd_gmove_kernel", "rnd_live_kernel", "rnd_gscan_kernel", "rnd_post_kernel", "rnd_room_kernel")
 
 
 def last_run_sum(d, counter):
