@@ -870,7 +870,7 @@ int round_phase_loop(mte_ctx* c, const ReplayArgs& a, size_t lds, uint64_t max_o
   for (int ph = 0; ph < kMaxPhases; ph++) {
     rd.last = ph == kMaxPhases - 1 ? 1u : 0u;
     HIPCHK(c, hipMemsetAsync(rd.count, 0, 16, c->stream));
-    HIPCHK(c, launch_round_plan(a, rd, c->n_docs, c->stream));
+    HIPCHK(c, launch_round_plan(a, ch, rd, c->n_docs, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->h_rcount, rd.count, 16, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const uint32_t n_round = c->h_rcount[0], n_active = c->h_rcount[2];

@@ -19,8 +19,9 @@ hipError_t launch_chunk(const ReplayArgs& a, const ChunkArgs& ch, uint32_t n_doc
 MTE_INST(0, false) MTE_INST(0, true) MTE_INST(4, false) MTE_INST(4, true) MTE_INST(8, false) MTE_INST(8, true)
 #undef MTE_INST
 
-hipError_t launch_round_plan(const ReplayArgs& a, const RoundArgs& rd, uint32_t n_docs, hipStream_t s) {
-  hipLaunchKernelGGL(rnd_plan_kernel, dim3(n_docs), dim3(kChWaves * kWave), 0, s, a, rd);
+hipError_t launch_round_plan(const ReplayArgs& a, const ChunkArgs& ch, const RoundArgs& rd, uint32_t n_docs,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(rnd_plan_kernel, dim3(n_docs), dim3(kChWaves * kWave), 0, s, a, ch, rd);
   return hipGetLastError();
 }
 

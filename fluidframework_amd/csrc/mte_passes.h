@@ -86,7 +86,8 @@ template <int K, bool S>
 hipError_t launch_chunk(const ReplayArgs& a, const ChunkArgs& ch, uint32_t n_docs, size_t lds, hipStream_t s);
 // the round phases: plan, then (scatter, resolve, apply, gather) for the
 // documents the plan gives a run
-hipError_t launch_round_plan(const ReplayArgs& a, const RoundArgs& rd, uint32_t n_docs, hipStream_t s);
+hipError_t launch_round_plan(const ReplayArgs& a, const ChunkArgs& ch, const RoundArgs& rd, uint32_t n_docs,
+                             hipStream_t s);
 template <int K>
 hipError_t launch_round_run(const ReplayArgs& a, const ChunkArgs& ch, const RoundArgs& rd, uint32_t n_docs,
                             hipStream_t s);

@@ -98,8 +98,8 @@ __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)
 
 // one workgroup per document: its 8 waves scan the records from the cursor
 // in interleaved batches of 64 for the first op that ends the run
-__global__ __launch_bounds__(512) void rnd_plan_kernel(ReplayArgs a, RoundArgs rd) {
-  __shared__ uint32_t first_bad;
+__global__ __launch_bounds__(512) void rnd_plan_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
+  __shared__ uint32_t first_bad, full;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave), l = lane_id();
   const int doc = (int)blockIdx.x;
   const DocHdr h = a.hdr[doc];
@@ -108,8 +108,15 @@ __global__ __launch_bounds__(512) void rnd_plan_kernel(ReplayArgs a, RoundArgs r
   const bool active = (h.flags & kHdrNeedsEsc) && h.status == 0 && h.resume < ktot;
   const uint32_t k0 = h.resume, nleft = active ? ktot - k0 : 0u;
   const bool newcalc = (h.flags & MTE_DOC_NEW_LENGTH_CALC) != 0;
-  if (threadIdx.x == 0) first_bad = nleft;
+  if (threadIdx.x == 0) first_bad = nleft, full = 0u;
   __syncthreads();
+  // a carried layout with a chunk past kLiveFull is re-laid out this phase (rnd_live)
+  if (rd.live[doc] == 1u) {
+    const uint32_t* cnt = ch.cnt + (uint64_t)doc * ch.nch_cap;
+    uint32_t mx = 0;
+    for (int q = (int)threadIdx.x; q < (int)rd.nch[doc]; q += (int)blockDim.x) mx = cnt[q] > mx ? cnt[q] : mx;
+    if (mx > kLiveFull) atomicOr(&full, 1u);
+  }
   const uint4* recp = a.recs + 2 * (kb + k0);
   const int32_t M = active ? (int32_t)reinterpret_cast<const uint32_t*>(recp)[2] : 0;
   if (active && !rd.last && newcalc) {
@@ -149,7 +156,7 @@ __global__ __launch_bounds__(512) void rnd_plan_kernel(ReplayArgs a, RoundArgs r
       // the chunks this document's column may need: a carried layout's count,
       // at most the re-layout's (its segments only drop) -- sizes the resolve's LDS
       uint32_t nb = (uint32_t)((h.nseg + MTE_RND_FILL - 1) / MTE_RND_FILL);
-      if (rd.live[doc] == 1u && rd.nch[doc] > nb) nb = rd.nch[doc];
+      if (rd.live[doc] == 1u) nb = full ? (rd.nch[doc] > nb ? rd.nch[doc] : nb) : rd.nch[doc];
       atomicMax(rd.count + 3, nb);
     }
     else if (len >= kRoundMin) p = make_uint4(kModeSeq, k0, k1, 0u);  // this run, op after op
