@@ -1735,6 +1735,9 @@ __device__ __forceinline__ void ht_regen(HT& h, int32_t ls, uint32_t t, uint32_t
         // (titems.c doc_regen)
         if (!hit && t == MTE_OP_REMOVE && lr == ls)
           h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = (uint32_t)ls | kLrsReleased;
+        // each re-sent segment heads a group of its own, the old group's taken
+        // by ordinal (client.ts:802, 852): the ack slides them in document order
+        if (hit && t == MTE_OP_REMOVE) h.pl[(uint64_t)kGrpPlane<K> * h.sd + i] = (uint32_t)i;
         if (!hit && t == MTE_OP_ANNOTATE && ((am >> slot) & 1u))
           h.pl[(uint64_t)kAnnPlane<K> * h.sd + i] = am & ~(1u << slot);
       }

@@ -680,6 +680,10 @@ class IntervalCollection {
     }
     const posNow = new Map();
     for (const [slot, q] of queue) posNow.set(slot, q[0].pos);
+    // an end that slid off the string keeps its removed segment (removeLocalRef
+    // relinks it there, localReference.ts:299-316): the Transient clone a later
+    // previousInterval takes of it (:1024-1039) reads that segment's position
+    const ghost = new Map();
     // the end tree compares the ends as they stand at each slide: an end still
     // to slide keeps the key of the unit it sits on (pinned)
     const touched = new Set(mine.map((r) => owner.get(r.slot)[0]));
@@ -699,9 +703,11 @@ class IntervalCollection {
           const next = q.length ? q[0].pos : now(lref);
           const other = which ? ival.start : ival.end;
           const otherPos = posNow.has(other.slot) ? posNow.get(other.slot) : now(other);
+          const otherPrev = otherPos === -1 && ghost.has(other.slot) ? ghost.get(other.slot) : otherPos;
           // beforeSlide: out of the index (removeIntervalFromIndex, :1042-1047)
           this._endRemove(ival);
           posNow.set(r.slot, next);
+          if (next === -1) ghost.set(r.slot, at);
           ival._pinKeys[which] = q.length && q[0].seg >= 0 ? q[0].seg : c._refOrder(lref);
           // its place among the new segment's references: addBeforeTombstones
           // puts one segment's references, in order, in front of offset 0's
@@ -722,7 +728,7 @@ class IntervalCollection {
           this._endPut(ival);
           if (watch) {
             const snap = (p) => ({ snapshot: true, position: p, refType: RefType.Transient });
-            const prev = new SequenceInterval(this, snap(which ? otherPos : at), snap(which ? at : otherPos),
+            const prev = new SequenceInterval(this, snap(which ? otherPrev : at), snap(which ? at : otherPrev),
               ival.intervalType);
             prev.properties = Object.assign({}, ival.properties);
             ival.start.pinned = which ? otherPos : next;

@@ -1452,6 +1452,10 @@ static int doc_regen(idoc* d, const mte_op* op) {
       if (member && !g->cont && d->wcache < 0) (void)view_prefix(d, i, d->cur_seq, ls);
     }
     if (hit) {
+      /* each re-sent segment heads a group of its own, the old group's segments
+       * taken by ordinal (client.ts:802, 852): the ack slides them in document
+       * order, split tails included */
+      if (t == MTE_OP_REMOVE) g->gord = i;
       /* findReconnectionPosition (client.ts:709-713): getPosition with the
        * localSeq, block lengths from the local partials (view_prefix) */
       if (g->cont && last == (int64_t)i - 1 && d->dl_n) d->dl[d->dl_n - 1].len += g->len;
