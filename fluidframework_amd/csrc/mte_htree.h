@@ -1845,23 +1845,25 @@ __device__ __forceinline__ int ht_ref_rebase(HT& h, const s8v& op, int32_t lseq,
 // reference left -> that unit's order key after the message (its zambonis
 // included): the held units before it, as mte_read_ref_order counts them, -1
 // if it is gone (titems.c slide_keys).  One wave-wide search per record.
-__device__ __noinline__ void ht_slide_keys(const HT& h, EvOut& ev, uint32_t from) {
-  const uint32_t to = ev.n < ev.cap ? ev.n : (uint32_t)ev.cap;
+// (Out of line, its arguments by value: a reference to the pass's state would
+// keep that state in scratch for the whole kernel.)
+__device__ __noinline__ void ht_slide_keys(const uint32_t* pl, uint64_t sd, int n, mte_delta* evp, uint32_t to,
+                                           uint32_t from) {
   if (from >= to) return;
   vm_drain();  // this wave's record stores are visible to its loads
   const int l = lane_id();
   for (uint32_t q = from; q < to; q++) {
-    const uint32_t kind = uni(ld_l2(&ev.p[q].kind));
+    const uint32_t kind = uni(ld_l2(&evp[q].kind));
     if ((kind & 0xc0u) != MTE_DELTA_SLIDE) continue;
-    const uint32_t u = uni(ld_l2(reinterpret_cast<const uint32_t*>(&ev.p[q].len)));
+    const uint32_t u = uni(ld_l2(reinterpret_cast<const uint32_t*>(&evp[q].len)));
     int32_t key = -1, carry = 0;
-    for (int tb = 0; tb < h.n; tb += kWave) {
+    for (int tb = 0; tb < n; tb += kWave) {
       const int i = tb + l;
-      const int ic = i < h.n ? i : 0;  // unconditional loads, selected after
-      const uint32_t ln = ld_l2(h.pl + ic), tf = ld_l2(h.pl + 5 * h.sd + ic);
-      const int32_t L = i < h.n ? (int32_t)ln : 0;
+      const int ic = i < n ? i : 0;  // unconditional loads, selected after
+      const uint32_t ln = ld_l2(pl + ic), tf = ld_l2(pl + 5 * sd + ic);
+      const int32_t L = i < n ? (int32_t)ln : 0;
       const int32_t incl = wave_incl_scan(L);
-      const uint64_t m = __ballot(i < h.n && u - tf < ln);
+      const uint64_t m = __ballot(i < n && u - tf < ln);
       if (m) {
         const int j = __ffsll((long long)m) - 1;
         key = carry + rdlane(incl - L + (int32_t)(u - tf), j);
@@ -1869,7 +1871,7 @@ __device__ __noinline__ void ht_slide_keys(const HT& h, EvOut& ev, uint32_t from
       }
       carry += rdlane(incl, kWave - 1);
     }
-    if (l == 0) ev.p[q].len = key;
+    if (l == 0) evp[q].len = key;
   }
   vm_drain();
 }
@@ -2052,7 +2054,8 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
     }
   }
   // the slides of this record, keyed by the units they left as they stand now
-  if (evd && rt && ev.n > ev_from) ht_slide_keys(h, ev, ev_from);
+  if (evd && rt && ev.n > ev_from)
+    ht_slide_keys(h.pl, h.sd, h.n, ev.p, ev.n < ev.cap ? ev.n : (uint32_t)ev.cap, ev_from);
   return 0;
 }
 

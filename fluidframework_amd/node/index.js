@@ -613,6 +613,8 @@ class BatchClient {
       }
       cur = null;
     };
+    // each record's events: its delta ranges and the references it slid
+    const parsed = new Array(recs.length);
     for (let k = 0; k < recs.length; k++) {
       const src = recs[k];
       if (src.rebase) {  // a reconnection query of an interval op (_rebase): its answer
@@ -629,10 +631,6 @@ class BatchClient {
           i++;
         }
         continue;
-      }
-      if (!src.local && (!cur || cur.msg !== src.msg)) {
-        flushMsg();
-        cur = { msg: src.msg, ops: [] };
       }
       const ranges = [];
       let kind = -1;
@@ -651,8 +649,56 @@ class BatchClient {
           segment: kind === 0 && src.op ? src.op.seg : undefined });
         i++;
       }
+      parsed[k] = { kind, ranges, slides };
+    }
+    // a remote group op applies its members one after another (client.ts
+    // applyRemoteOp per member), so a reference sliding at member k sees the
+    // document as member k left it: positions read after the message map back
+    // through the later members' inserts and removes, and a reference a later
+    // member slides again sat, after member k, where that member found it (its
+    // removed segment's place before the removal, mapped back the same way)
+    const undo = (p, later) => {
+      if (p < 0) return p;
+      for (let j = later.length - 1; j >= 0; j--) {
+        const { kind, ranges } = later[j];
+        if (kind !== 0 && kind !== 1) continue;
+        let d = 0;
+        for (const r of ranges) {
+          if (kind === 1 ? r.position <= p : r.position + r.length <= p) d += r.length;
+        }
+        p = kind === 1 ? p + d : p - d;
+      }
+      return p;
+    };
+    const backTo = (k) => {
+      const later = [];
+      for (let j = k + 1; j < recs.length && parsed[j] && !recs[j].local && recs[j].msg === recs[k].msg; j++) {
+        later.push(parsed[j]);
+      }
+      if (later.length === 0) return null;
+      const seen = new Map();  // slot -> its position after member k
+      later.forEach((pj, j) => {
+        for (const r of pj.slides || []) {
+          if (seen.has(r.slot)) continue;
+          // before member j removed it: the removed segment's own-view place
+          // plus the reference's offset in it (a regenerated group op removes
+          // one segment per member)
+          seen.set(r.slot, undo(r.pos + r.off, later.slice(0, j)));
+        }
+      });
+      return { at: (slot, p) => (seen.has(slot) ? seen.get(slot) : undo(p, later)) };
+    };
+    for (let k = 0; k < recs.length; k++) {
+      const src = recs[k];
+      const pr = parsed[k];
+      if (!pr) continue;
+      if (!src.local && (!cur || cur.msg !== src.msg)) {
+        flushMsg();
+        cur = { msg: src.msg, ops: [] };
+      }
+      const { kind, ranges, slides } = pr;
       if (kind < 0) {
-        if (slides) this._slid(slides);
+        if (slides) this._slid(slides, src.local ? null : backTo(k));
         continue;
       }
       if (cur) cur.ops.push(...opsFromDelta(kind, ranges, src.op));
@@ -661,17 +707,17 @@ class BatchClient {
       for (const fn of this.listeners || []) fn(ev, this);
       // markRangeRemoved slides the newly removed segments' references after
       // the delta callback (mergeTree.ts:1978-1993)
-      if (slides) this._slid(slides);
+      if (slides) this._slid(slides, src.local ? null : backTo(k));
     }
     flushMsg();
   }
 
   /** The references one op slid (MTE_DELTA_SLIDE records, in the order of the
    *  segments they left) -> the interval collections' position listeners. */
-  _slid(slides) {
+  _slid(slides, back) {
     if (this.onSlideRecords) this.onSlideRecords(slides);  // a test hook (tests/node/interval_farm.js trace)
     if (!this.intervalCollections) return;
-    for (const c of this.intervalCollections.values()) c._onSlides(slides);
+    for (const c of this.intervalCollections.values()) c._onSlides(slides, back);
   }
 
   /** Client.rollback (client.ts:396-398 -> MergeTree.rollback,

@@ -645,7 +645,7 @@ class IntervalCollection {
    *  track.  previousInterval holds the ends as they were (Transient clones: a
    *  removed segment's position), the interval the ends as they are at that
    *  moment: an end that slides later in the same op still sits where it was. */
-  _onSlides(slides) {
+  _onSlides(slides, back) {
     if (this.byId.size === 0) return;
     const owner = new Map();  // slot -> [interval, 0 start | 1 end]
     for (const x of this.byId.values()) {
@@ -671,7 +671,10 @@ class IntervalCollection {
       run.push(r);
     }
     const c = this.client;
-    const now = (lref) => c.localReferencePositionToPosition(lref);
+    // positions as the op left them; inside a remote group op, as its member
+    // that slid these left them (back: the later members undone)
+    const now = back ? (lref) => back.at(lref.slot, c.localReferencePositionToPosition(lref))
+      : (lref) => c.localReferencePositionToPosition(lref);
     // each sliding end's records in order: where it sits before each one
     const queue = new Map();
     for (const r of mine) {

@@ -210,6 +210,25 @@ function runSet(p) {
       coll.on("deleteInterval", (ival, local, op) => X.ev.push(["delete", ival.getIntervalId(), local, !!op, X.mt]));
       coll.on("changeInterval", (ival, prev, local, op) => X.ev.push(["change", ival.getIntervalId(), local, !!op,
         pos(prev.start), pos(prev.end), pos(ival.start), pos(ival.end), X.mt]));
+      if (process.env.MTE_REF_TRACE === n) {
+        // each mid-op event's positions beside the same positions summed leaf by leaf
+        const lpos = (r) => {
+          const sg = r.getSegment();
+          if (!sg || !sg.parent) return -1;
+          let q = 0;
+          const walk = (x) => {
+            if (x === sg) return true;
+            if (x.isLeaf()) { q += c._mergeTree.localNetLength(x) || 0; return false; }
+            for (let i = 0; i < x.childCount; i++) if (walk(x.children[i])) return true;
+            return false;
+          };
+          walk(c._mergeTree.root);
+          return q + (sg.removedSeq !== undefined ? 0 : r.getOffset());
+        };
+        coll.on("changeInterval", (ival, prev, local, op) => process.stderr.write(`  ev ${ival.getIntervalId()} ` +
+          `${pos(prev.start)},${pos(prev.end)} -> ${pos(ival.start)},${pos(ival.end)} leaf ${lpos(ival.start)},${lpos(ival.end)}` +
+          ` end ${(() => { const g = ival.end.getSegment(); return g ? JSON.stringify(g.text) + "@" + g.ordinal + " rs " + g.removedSeq + " off " + ival.end.getOffset() : "-"; })()}\n`));
+      }
       coll.on("propertyChanged", (ival, deltas, local, op) => X.ev.push(["props", ival.getIntervalId(), local, !!op,
         sortKeys(clone(deltas)), X.mt]));
     }

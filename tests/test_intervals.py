@@ -241,6 +241,6 @@ def test_node_interval_reconnect_on_gpu():
     # with the mid-op changeInterval events: counted, not yet exact on every
     # reconnection farm
     assert j["prevNext"]["equal"] >= 0.98 * j["prevNext"]["n"], j["prevNext"]
-    assert j["mtEvents"]["equal"] >= 0.6 * j["mtEvents"]["n"], j["mtEvents"]
+    assert j["mtEvents"]["equal"] >= 0.75 * j["mtEvents"]["n"], j["mtEvents"]
     # the order among intervals whose ends slid off the string
     assert j["orderOff"] == 0, j["orderOff"]
