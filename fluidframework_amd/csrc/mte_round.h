@@ -1108,7 +1108,16 @@ __device__ __forceinline__ void rnd_apply_one(const ReplayArgs& a, const ChunkAr
 // a fixed grid of waves walking the (document, chunk) slots with a stride: the
 // slots past a document's chunk count cost a test, not a wave launch
 template <int K>
-__global__ __launch_bounds__(256) void rnd_apply_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
+// MTE_APPLY_WPE: a waves-per-SIMD floor for the register allocator (A/B builds)
+#ifndef MTE_APPLY_WPE
+#define MTE_APPLY_WPE 0
+#endif
+#if MTE_APPLY_WPE > 0
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTE_APPLY_WPE)))
+#else
+__global__ __launch_bounds__(256)
+#endif
+void rnd_apply_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
   const uint64_t n = (uint64_t)rd.nd * ch.nch_cap, stride = (uint64_t)gridDim.x * 4;
   for (uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w; wi < n; wi += stride)

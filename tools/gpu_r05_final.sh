@@ -4,7 +4,7 @@
 # local-client leg (side legs off where a profile needs the timed launch last)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r05final
+O=gpurun_out/${OUT:-r05final}
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
 echo "tests rc=$?" > $O/rc.txt
