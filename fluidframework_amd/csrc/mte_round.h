@@ -215,15 +215,25 @@ __global__ __launch_bounds__(512) void rnd_scan_kernel(ReplayArgs a, ChunkArgs c
   if (p.x != kModeRound || (gather && rd.rflag[doc] != 0u) || (!gather && rd.live[doc] != 0u)) return;
   uint32_t* kc = ch.kc + (uint64_t)doc * ch.nch_cap;
   int m;
+  int32_t total;
   if (gather) {
+    // the chunks' segment counts summed; kc keeps the column entries the
+    // apply wrote (the next run's resolve reads them)
     m = (int)rd.nch[doc];
     const uint32_t* cnt = ch.cnt + (uint64_t)doc * ch.nch_cap;
-    for (int i = (int)threadIdx.x; i < m; i += (int)blockDim.x) kc[i] = cnt[i];
+    __shared__ int32_t tsum;
+    if (threadIdx.x == 0) tsum = 0;
     __syncthreads();
+    int32_t v = 0;
+    for (int i = (int)threadIdx.x; i < m; i += (int)blockDim.x) v += (int32_t)cnt[i];
+    v = rdlane(wave_incl_scan(v), kWave - 1);
+    if (lane_id() == 0) atomicAdd(&tsum, v);
+    __syncthreads();
+    total = tsum;
   } else {
     m = (a.hdr[doc].nseg + kT - 1) / kT;
+    total = ch_block_scan(kc, m, &ctl);
   }
-  const int32_t total = ch_block_scan(kc, m, &ctl);
   if (threadIdx.x == 0) {
     const unsigned long long pb = 4ull * rd.planes;  // bytes of one segment's planes
     if (!gather) {
@@ -309,11 +319,12 @@ __global__ __launch_bounds__(256) void rnd_cols_kernel(ReplayArgs a, ChunkArgs c
   const int l = lane_id();
   chunk_walk(ch, rd, [&](int doc, int q) {
     const uint4 p = rd.plan[doc];
-    if (p.x != kModeRound || q >= (int)rd.nch[doc]) return;
-    // a re-laid-out document: kChFill per chunk; a carried one: its counts
+    // a carried document's counts and column entries are current: the apply
+    // wrote each chunk it changed (rnd_apply_one), the rest did not change
+    if (p.x != kModeRound || q >= (int)rd.nch[doc] || rd.live[doc] == 1u) return;
+    // a re-laid-out document: kChFill per chunk
     const int n_new = (int)rd.nnew[doc], fill = (int)rnd_fill(rd.nnew[doc], rd.nch[doc]);
-    const int cn = rd.live[doc] == 1u ? (int)ch.cnt[(uint64_t)doc * ch.nch_cap + q]
-                   : (n_new - q * fill < fill ? (n_new - q * fill > 0 ? n_new - q * fill : 0) : fill);
+    const int cn = n_new - q * fill < fill ? (n_new - q * fill > 0 ? n_new - q * fill : 0) : fill;
     const uint64_t x0 = ch_slot(ch, doc, q);
     int32_t v = 0;
 #pragma unroll
@@ -994,15 +1005,18 @@ __device__ __forceinline__ void ch_load_e(Regs<E, K>& R, const ChunkArgs& ch, ui
 }
 
 template <int E, int K>
-__device__ __forceinline__ void ch_store_e(const Regs<E, K>& R, const ChunkArgs& ch, uint64_t x0, int n) {
+__device__ __forceinline__ void ch_store_e(const Regs<E, K>& R, const ChunkArgs& ch, uint64_t x0, int n,
+                                           int32_t* vis = nullptr) {
   uint32_t* pl = ch.arena;
   const uint64_t st = ch.astride;
   const int base = lane_id() * E;
+  if (vis) *vis = 0;
 #pragma unroll
   for (int j = 0; j < E; j++) {
     const int i = base + j;
     if (i < n) {
       const uint64_t x = x0 + (uint32_t)i;
+      if (vis) *vis += R.rseq[j] == kNone ? R.len[j] : 0;
       pl[x] = (uint32_t)R.len[j];
       pl[st + x] = (uint32_t)R.seq[j];
       pl[2 * st + x] = (uint32_t)R.rseq[j];
@@ -1019,7 +1033,7 @@ __device__ __forceinline__ void ch_store_e(const Regs<E, K>& R, const ChunkArgs&
 template <int E, int K>
 __device__ __forceinline__ int rnd_apply_chunk(const ReplayArgs& a, const ChunkArgs& ch, uint64_t x0, int& ni,
                                                uint32_t nb, int from, const uint2& e, const uint4& r0,
-                                               const uint4& r1, int32_t M) {
+                                               const uint4& r1, int32_t M, int32_t& vis) {
   RND_CLK(a0);
   Regs<E, K> R;
   ch_load_e<E, K>(R, ch, x0, ni);
@@ -1048,7 +1062,9 @@ __device__ __forceinline__ int rnd_apply_chunk(const ReplayArgs& a, const ChunkA
     rcs = rc != 0 ? rc : rcs;
   }
   RND_CLK(a2);
-  ch_store_e<E, K>(R, ch, x0, ni);
+  // the chunk's column entry for the next run (rnd_cols: its visible length,
+  // every segment seen at that run's refSeq): the segments not removed
+  ch_store_e<E, K>(R, ch, x0, ni, &vis);
   RND_DIAG(12, a1 - a0);
   RND_DIAG(13, a2 - a1);
   RND_DIAG(14, nb);
@@ -1092,15 +1108,19 @@ __device__ __forceinline__ void rnd_apply_one(const ReplayArgs& a, const ChunkAr
   RND_DIAG(15, clock64() - w0 + 0 * (r0.x + r1.w + (uint32_t)from));
 #endif
 #if MTE_APPLY_E2
-  const int rcs = ni + 2 * (int)nb <= 2 * kWave ? rnd_apply_chunk<2, K>(a, ch, x0, ni, nb, from, e, r0, r1, M)
-                                                : rnd_apply_chunk<kChE, K>(a, ch, x0, ni, nb, from, e, r0, r1, M);
+  int32_t vis = 0;
+  const int rcs = ni + 2 * (int)nb <= 2 * kWave ? rnd_apply_chunk<2, K>(a, ch, x0, ni, nb, from, e, r0, r1, M, vis)
+                                                : rnd_apply_chunk<kChE, K>(a, ch, x0, ni, nb, from, e, r0, r1, M, vis);
 #else
-  const int rcs = rnd_apply_chunk<kChE, K>(a, ch, x0, ni, nb, from, e, r0, r1, M);
+  int32_t vis = 0;
+  const int rcs = rnd_apply_chunk<kChE, K>(a, ch, x0, ni, nb, from, e, r0, r1, M, vis);
 #endif
+  vis = rdlane(wave_incl_scan(vis), kWave - 1);
   if (l == 0) {
     // the chunk's sub-ops (record + bucket entry), its planes in and out, its count
     atomicAdd(rd.acct + doc, 40ull * nb + 4ull * rd.planes * (unsigned long long)(n_before + ni) + 8ull);
     cntp[i] = (uint32_t)ni;
+    ch.kc[(uint64_t)doc * ch.nch_cap + i] = (uint32_t)vis;  // read by the next run's resolve
     if (rcs != 0) a.hdr[doc].status = MTE_E_STATE;  // resolve guarantees every sub-op fits: an engine bug
   }
 }
