@@ -68,7 +68,8 @@ hipError_t launch_round_run(const ReplayArgs& a, const ChunkArgs& ch, const Roun
   hipLaunchKernelGGL((rnd_count_kernel<K>), dim3((uint32_t)((tiles + 3) / 4)), w4, 0, s, a, ch, rd, tpd);
   hipLaunchKernelGGL(rnd_scan_kernel, dim3(n_docs), dim3(kChWaves * kWave), 0, s, a, ch, rd, 0);
   hipLaunchKernelGGL((rnd_move_kernel<K>), dim3((uint32_t)((tiles + 3) / 4)), w4, 0, s, a, ch, rd, tpd);
-  hipLaunchKernelGGL(rnd_cols_kernel, dim3((uint32_t)((chunks + 3) / 4)), w4, 0, s, a, ch, rd);
+  // a fixed grid walking the chunk slots (rnd_cols skips a carried document's)
+  hipLaunchKernelGGL(rnd_cols_kernel, dim3((uint32_t)std::min<uint64_t>((chunks + 3) / 4, 2048)), w4, 0, s, a, ch, rd);
   // resolve: the client chains, columns in LDS (two waves per workgroup when they fit)
   const size_t col = (size_t)rnd_resolve_lds(rd.col_cap, rd.col_cap / kChGroup);
   if (2 * col <= kRoundLdsMax) {
