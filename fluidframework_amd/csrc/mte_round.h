@@ -180,6 +180,20 @@ __device__ __forceinline__ void chunk_walk(const ChunkArgs& ch, const RoundArgs&
     f((int)rd.d0 + (int)(wi / ch.nch_cap), (int)(wi % ch.nch_cap));
 }
 
+// the same walk document by document: a document the (wave-uniform) test
+// turns down costs one test per wave, not one per chunk slot
+template <class P, class F>
+__device__ __forceinline__ void chunk_walk_docs(const ChunkArgs& ch, const RoundArgs& rd, P&& take, F&& f) {
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
+  const uint32_t wid = (uint32_t)blockIdx.x * 4u + (uint32_t)w, nw = gridDim.x * 4u;
+  for (uint32_t d = 0; d < rd.nd; d++) {
+    const int doc = (int)rd.d0 + (int)d;
+    if (!__builtin_amdgcn_readfirstlane((int)take(doc))) continue;
+    const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)rd.nch[doc]);
+    for (uint32_t q = wid; q < m; q += nw) f(doc, (int)q);
+  }
+}
+
 constexpr int kT = kChE * kWave;  // flat slots per tile
 __device__ __forceinline__ uint32_t rnd_fill(uint32_t total, uint32_t nch) { return nch ? (total + nch - 1) / nch : 1u; }
 
@@ -317,11 +331,10 @@ __global__ __launch_bounds__(256) void rnd_move_kernel(ReplayArgs a, ChunkArgs c
 // entry (the visible length: every segment is seen at refSeq R), into kc
 __global__ __launch_bounds__(256) void rnd_cols_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
   const int l = lane_id();
-  chunk_walk(ch, rd, [&](int doc, int q) {
-    const uint4 p = rd.plan[doc];
-    // a carried document's counts and column entries are current: the apply
-    // wrote each chunk it changed (rnd_apply_one), the rest did not change
-    if (p.x != kModeRound || q >= (int)rd.nch[doc] || rd.live[doc] == 1u) return;
+  // a carried document's counts and column entries are current: the apply
+  // wrote each chunk it changed (rnd_apply_one), the rest did not change
+  chunk_walk_docs(ch, rd, [&](int doc) { return rd.plan[doc].x == kModeRound && rd.live[doc] != 1u; },
+                  [&](int doc, int q) {
     // a re-laid-out document: kChFill per chunk
     const int n_new = (int)rd.nnew[doc], fill = (int)rnd_fill(rd.nnew[doc], rd.nch[doc]);
     const int cn = n_new - q * fill < fill ? (n_new - q * fill > 0 ? n_new - q * fill : 0) : fill;
@@ -345,8 +358,7 @@ __global__ __launch_bounds__(256) void rnd_cols_kernel(ReplayArgs a, ChunkArgs c
 template <int K>
 __global__ __launch_bounds__(256) void rnd_gmove_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
   const int l = lane_id();
-  chunk_walk(ch, rd, [&](int doc, int q) {
-    if (rd.gfl[doc] == 0u || q >= (int)rd.nch[doc]) return;
+  chunk_walk_docs(ch, rd, [&](int doc) { return rd.gfl[doc] != 0u; }, [&](int doc, int q) {
     const int cn = (int)ch.cnt[(uint64_t)doc * ch.nch_cap + q];
     const uint32_t d0 = ch.kc[(uint64_t)doc * ch.nch_cap + q];
     const uint64_t x0 = ch_slot(ch, doc, q);
