@@ -1150,10 +1150,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTE_APPLY_W
 __global__ __launch_bounds__(256)
 #endif
 void rnd_apply_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd) {
-  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
-  const uint64_t n = (uint64_t)rd.nd * ch.nch_cap, stride = (uint64_t)gridDim.x * 4;
-  for (uint64_t wi = (uint64_t)blockIdx.x * 4 + (uint32_t)w; wi < n; wi += stride)
-    rnd_apply_one<K>(a, ch, rd, (int)rd.d0 + (int)(wi / ch.nch_cap), (int)(wi % ch.nch_cap));
+  chunk_walk_docs(ch, rd, [&](int doc) { return rd.plan[doc].x == kModeRound && rd.rflag[doc] == 0u; },
+                  [&](int doc, int q) { rnd_apply_one<K>(a, ch, rd, doc, q); });
 }
 
 }  // namespace mte
