@@ -195,16 +195,25 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
   if (legacy) tree[i] = in.text_len > 0 ? (1u | po | (1u << 8) | ((in.flags & kInitNl) ? kTNl : 0u)) : (1u | kTEmpty);
 }
 
+// the image planes that hold one value for every segment (found at load):
+// written from the kernel argument instead of read back each reset
+struct ImgConst {
+  uint32_t mask;     // bit p: plane p is uniform
+  uint32_t val[16];  // its value
+};
+
 // the mte_load_segments image -> the flat planes (one thread per segment)
 // (the image's last plane is the tree word, for the tree pass)
 __global__ void image_kernel(SegSoA soa, uint32_t cap, uint32_t n_planes, const uint32_t* img, uint64_t img_stride,
-                             const uint32_t* img_doc, const uint64_t* img_off, uint64_t n_img, uint32_t* tree) {
+                             const uint32_t* img_doc, const uint64_t* img_off, uint64_t n_img, uint32_t* tree,
+                             ImgConst uc) {
   for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_img;
        g += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t d = img_doc[g];
     const uint64_t x = (uint64_t)d * cap + (g - img_off[d]);
     uint32_t* pl = reinterpret_cast<uint32_t*>(soa.len);
-    for (uint32_t p = 0; p < n_planes; p++) pl[p * soa.plane_stride + x] = img[p * img_stride + g];
+    for (uint32_t p = 0; p < n_planes; p++)
+      pl[p * soa.plane_stride + x] = ((uc.mask >> p) & 1u) ? uc.val[p] : img[p * img_stride + g];
     if (tree) tree[x] = img[n_planes * img_stride + g];
   }
 }
@@ -536,6 +545,7 @@ struct mte_ctx {
   uint32_t* d_img_doc = nullptr;
   uint64_t* d_img_off = nullptr;
   uint64_t n_img = 0;
+  ImgConst img_uc = {};  // the image's uniform planes (image_kernel)
 
   // pinned staging for op-record uploads (mte_submit), allocated on first use
   static constexpr int kStages = 3;
@@ -829,7 +839,7 @@ int launch_reset(mte_ctx* c) {
     const uint64_t nb = std::min<uint64_t>((c->n_img + 255) / 256, 65536);
     hipLaunchKernelGGL(image_kernel, dim3((uint32_t)nb), dim3(256), 0, c->stream, c->soa, c->cap,
                        (uint32_t)(kFieldPlanes + c->kt), c->d_img, c->n_img, c->d_img_doc,
-                       (const uint64_t*)c->d_img_off, c->n_img, c->d_tree);
+                       (const uint64_t*)c->d_img_off, c->n_img, c->d_tree, c->img_uc);
     HIPCHK(c, hipGetLastError());
   }
   c->ran = false;
@@ -1531,6 +1541,18 @@ int mte_load_segments(mte_ctx* c, const uint64_t* seg_offsets, const mte_seg* se
   }
   free_image(c);
   if (!n_segs) return launch_reset(c);
+  // planes with one value throughout (config 5's preloaded one-unit segments:
+  // all but the text offsets and tree words) are not read back at each reset
+  c->img_uc = ImgConst{};
+  for (uint32_t p = 0; p < np && p < 16; p++) {
+    const uint32_t* v = img.data() + (size_t)p * n_segs;
+    bool same = true;
+    for (uint64_t g = 1; g < n_segs && same; g++) same = v[g] == v[0];
+    if (same) {
+      c->img_uc.mask |= 1u << p;
+      c->img_uc.val[p] = v[0];
+    }
+  }
   HIPCHK(c, hipMalloc((void**)&c->d_img, img.size() * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_img_doc, doc.size() * 4));
   HIPCHK(c, hipMalloc((void**)&c->d_img_off, ((size_t)c->n_docs + 1) * 8));
