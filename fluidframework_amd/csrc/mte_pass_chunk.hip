@@ -83,8 +83,7 @@ hipError_t launch_round_run(const ReplayArgs& a, const ChunkArgs& ch, const Roun
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rnd_resolve_kernel<1>, dim3(n_docs * kChWaves), dim3(kWave), col, s, a, ch, rd);
   }
-  const uint32_t bpd = (uint32_t)((rd.rl_cap + 255) / 256);
-  hipLaunchKernelGGL(rnd_bucket_kernel, dim3(n_docs * bpd), dim3(256), 0, s, a, ch, rd, bpd);
+  // (the resolve wrote each sub-op into its chunk's bucket: rnd_emit)
   hipLaunchKernelGGL(rnd_room_kernel, dim3((uint32_t)((chunks + 255) / 256)), dim3(256), 0, s, a, ch, rd);
   // apply: every chunk with sub-ops on its own wave
   {  // a fixed grid (rnd_apply_kernel walks the chunk slots): 2 workgroups per SIMD's worth

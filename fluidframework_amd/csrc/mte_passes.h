@@ -28,12 +28,12 @@ struct RoundArgs {
   uint4* plan;      // [doc] x mode, y k0, z k1, w M
   uint32_t* rcnt;   // [doc][nch_cap] sub-ops per chunk
   uint2* rbuf;      // [doc][nch_cap][kRB] (op index - k0, chunk start in the op's perspective)
-  uint4* rrec;      // [doc][nch_cap][kRB][2] the sub-op's record, copied there by rnd_bucket
+  uint4* rrec;      // [doc][nch_cap][kRB][2] the sub-op's record, copied there by the resolve (rnd_emit)
   uint32_t* rflag;  // [doc] non-zero: the run replays op after op
   uint32_t* nch;    // [doc] chunks after the re-layout
   uint32_t* nnew;   // [doc] segments after the re-layout
   uint32_t* count;  // [0] round docs, [1] op-after-op docs, [2] active docs
-  uint4* rlist;     // [doc][rl_cap] the client chains' sub-ops (chunk, op index - k0, chunk start)
+  uint4* rlist;     // [doc][rl_cap] (unused since the resolve buckets its sub-ops itself; rl_cap sizes the chains)
   uint64_t rl_cap;  // list entries per document: 2 x its ops + 8 per client
   uint2* rchain;    // [doc][MTE_MAX_CLIENTS] (list offset, entries) of each client chain
   // [doc] where the document's segments are: 0 the flat planes; 1 the chunk

@@ -42,8 +42,8 @@
 //                per tile), then per chunk its count and round-start column
 //                entry, the visible length (rnd_cols, a wave per chunk);
 //   rnd_resolve  one wave per client chain, its column in LDS: positions ->
-//                (chunk, start), appended to the chain's sub-op list;
-//   rnd_bucket   a thread per sub-op: into its chunk's bucket;
+//                (chunk, start), each sub-op written into its chunk's bucket
+//                with its record (rnd_emit);
 //   rnd_apply    one wave per chunk with sub-ops: sort them by op index, load
 //                the chunk into registers, seg_op_v each, store;
 //   gather       chunk counts -> prefix (rnd_scan), chunks -> flat planes
@@ -444,7 +444,8 @@ __global__ __launch_bounds__(256) void rnd_room_kernel(ReplayArgs a, ChunkArgs c
   const uint64_t wi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int doc = (int)rd.d0 + (int)(wi / ch.nch_cap), q = (int)(wi % ch.nch_cap);
   if (doc >= (int)(rd.d0 + rd.nd)) return;
-  if (rd.plan[doc].x != kModeRound || rd.live[doc] != 1u || q >= (int)rd.nch[doc]) return;
+  // (a failed chain's run goes op after op anyway: its partial buckets are moot)
+  if (rd.plan[doc].x != kModeRound || rd.live[doc] != 1u || q >= (int)rd.nch[doc] || (rd.rflag[doc] & 2u)) return;
   const uint64_t i = (uint64_t)doc * ch.nch_cap + q;
   if (ch.cnt[i] + 2u * rd.rcnt[i] > (uint32_t)kChSlots) atomicOr(rd.rflag + doc, 4u);
 }
@@ -532,18 +533,43 @@ __device__ __forceinline__ void col_sub_row(const Col& C, int gg, int32_t ci_row
   if (l >= sg && l < C.nsg) C.SS[l] = C.SS[l] - og;
 }
 
-// one op of a chain against the column, op after op: appends its sub-ops at
-// list[m..] and changes the column; false = the run cannot take it (an insert
+// A resolved sub-op straight into its chunk's bucket: the entry (op index,
+// chunk start in the op's perspective) and the op's record beside it, so the
+// apply reads its chunk's records in one contiguous load; a bucket past kRB
+// refuses the run (rflag 1).  The record loads go out with the slot's atomic.
+struct Emit {
+  uint32_t* rcnt;      // the document's per-chunk counts
+  uint2* rbuf;         // its buckets
+  uint4* rrec;         // their records
+  const uint4* recp;   // the run's records
+  uint32_t* rflag;     // the document's refusal flags
+  uint64_t base;       // doc * nch_cap
+};
+__device__ __forceinline__ void rnd_emit(const Emit& E, uint32_t chunk, uint32_t k, uint32_t excl) {
+  const uint4 q0 = E.recp[2 * k], q1 = E.recp[2 * k + 1];
+  const uint32_t pos = atomicAdd(E.rcnt + chunk, 1u);
+  if (pos < (uint32_t)kRB) {
+    const uint64_t slot = (E.base + chunk) * kRB + pos;
+    E.rbuf[slot] = make_uint2(k, excl);
+    E.rrec[2 * slot] = q0;
+    E.rrec[2 * slot + 1] = q1;
+  } else {
+    atomicOr(E.rflag, 1u);
+  }
+}
+
+// one op of a chain against the column, op after op: emits its sub-ops
+// (counted in m) and changes the column; false = the run cannot take it (an insert
 // past the end: MTE_E_INSERT_FAILED op after op; the list full)
 __device__ __forceinline__ bool rnd_serial_op(const Col& C, uint32_t k, uint32_t w3, int32_t pos1, int32_t pos2,
-                                              uint4* list, uint32_t& m, uint32_t cap_c) {
+                                              const Emit& E, uint32_t& m, uint32_t cap_c) {
   const int l = lane_id();
   const uint32_t type = w3 & 0xffu, flags = w3 >> 16;
   if (type == MTE_OP_INSERT) {
     const ColHit h = col_find(C, pos1, false);
     if (pos1 > h.total || h.i >= C.nch || m >= cap_c) return false;
     const int32_t nlen = (flags & MTE_F_MARKER) ? 1 : pos2;
-    if (l == 0) list[m] = make_uint4((uint32_t)h.i, k, (uint32_t)h.excl, 0u);
+    if (l == 0) rnd_emit(E, (uint32_t)h.i, k, (uint32_t)h.excl);
     m++;
     if (nlen > 0) col_add(C, h, nlen);
     lds_fence();
@@ -556,7 +582,7 @@ __device__ __forceinline__ bool rnd_serial_op(const Col& C, uint32_t k, uint32_t
       // ensureIntervalBoundary alone: a split strictly inside a leaf
       if (h.excl < b1) {
         if (m >= cap_c) return false;
-        if (l == 0) list[m] = make_uint4((uint32_t)h.i, k, (uint32_t)h.excl, 0u);
+        if (l == 0) rnd_emit(E, (uint32_t)h.i, k, (uint32_t)h.excl);
         m++;
       }
     } else {
@@ -571,10 +597,9 @@ __device__ __forceinline__ bool rnd_serial_op(const Col& C, uint32_t k, uint32_t
         const int32_t st = eg + cprev, incl = eg + ci, v = ci - cprev;
         const bool hit = i < C.nch && i >= h.i && v > 0 && st < b2;
         const uint64_t hm = __ballot(hit);
-        const uint32_t at = m + lanes_below(hm);
         m += (uint32_t)__popcll(hm);
         if (m > cap_c) return false;
-        if (hit) list[at] = make_uint4((uint32_t)i, k, (uint32_t)st, 0u);
+        if (hit) rnd_emit(E, (uint32_t)i, k, (uint32_t)st);
         // the group's end before this op
         const int last = C.nch - gg * kChGroup < kWave ? C.nch - gg * kChGroup - 1 : kWave - 1;
         const int32_t gend = eg + rdlane(ci, last);
@@ -673,7 +698,7 @@ __device__ __forceinline__ ColPos col_find_lane(const Col& C, int32_t y, bool ac
 // sub-ops appended at list[m..], the column advanced past the block.  false:
 // nothing done, the block goes op by op.  failed: an insert past the end.
 __device__ __forceinline__ bool rnd_block(const Col& C, int nb, uint32_t k, uint32_t w3, int32_t pos1, int32_t pos2,
-                                          uint4* list, uint32_t& m, uint32_t cap_c, bool& failed) {
+                                          const Emit& E, uint32_t& m, uint32_t cap_c, bool& failed) {
   if (m + 2u * (uint32_t)nb > cap_c) return false;  // at most two sub-ops an op; else op by op, checked
   RND_CLK(c0);
   const int l = lane_id();
@@ -757,12 +782,9 @@ __device__ __forceinline__ bool rnd_block(const Col& C, int nb, uint32_t k, uint
     failed = true;
     return true;
   }
-  const int32_t cnt = (s0 ? 1 : 0) + (s1 ? 1 : 0);
-  const int32_t inc = wave_incl_scan(cnt);
-  const uint32_t at = m + (uint32_t)(inc - cnt);
-  if (s0) list[at] = make_uint4((uint32_t)c, k, (uint32_t)st, 0u);
-  if (s1) list[at + (s0 ? 1u : 0u)] = make_uint4((uint32_t)c + 1u, k, (uint32_t)bc, 0u);
-  m += (uint32_t)rdlane(inc, kWave - 1);
+  if (s0) rnd_emit(E, (uint32_t)c, k, (uint32_t)st);
+  if (s1) rnd_emit(E, (uint32_t)c + 1u, k, (uint32_t)bc);
+  m += (uint32_t)(__popcll(__ballot(s0)) + __popcll(__ballot(s1)));
   // fold: each change into its chunk row (one add per change, no divergence),
   // the changes per group lane-parallel into GD, then per supergroup row the
   // groups' running sums into GS and the row totals into SS
@@ -837,7 +859,8 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
   }
   uint32_t* const ring = reinterpret_cast<uint32_t*>(C.GD + (rd.col_cap / kChGroup + kWave - 1) / kWave * kWave);
   const int32_t* sum0 = reinterpret_cast<const int32_t*>(ch.kc + (uint64_t)doc * ch.nch_cap);
-  uint4* list = rd.rlist + (uint64_t)doc * rd.rl_cap;
+  const Emit E{rd.rcnt + (uint64_t)doc * ch.nch_cap, rd.rbuf, rd.rrec, recp, rd.rflag + doc,
+               (uint64_t)doc * ch.nch_cap};
   // ops per client (every workgroup of the document counts them all)
   for (int c = (int)threadIdx.x; c < MTE_MAX_CLIENTS; c += (int)blockDim.x) ccount[c] = 0u;
   __syncthreads();
@@ -925,11 +948,11 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
             p1 = (int32_t)rp[4];
             p2 = (int32_t)rp[5];
           }
-          const bool par = rnd_block(C, nb, k, w3, p1, p2, list + off, m, cap_c, failed);
+          const bool par = rnd_block(C, nb, k, w3, p1, p2, E, m, cap_c, failed);
           RND_CLK(tb1);
           if (!par) {
             for (int t = 0; t < nb && !failed; t++)
-              failed = !rnd_serial_op(C, rdlane(k, t), rdlane(w3, t), rdlane(p1, t), rdlane(p2, t), list + off, m,
+              failed = !rnd_serial_op(C, rdlane(k, t), rdlane(w3, t), rdlane(p1, t), rdlane(p2, t), E, m,
                                       cap_c);
             RND_DIAG(1, 1);
             RND_DIAG(5, clock64() - tb1);
@@ -945,43 +968,14 @@ __global__ __launch_bounds__(WPB * kWave) void rnd_resolve_kernel(ReplayArgs a, 
       if (l == 0) {
         if (failed) atomicOr(rd.rflag + doc, 2u);
         rd.rchain[(uint64_t)doc * MTE_MAX_CLIENTS + (uint32_t)c] = make_uint2(off, failed ? 0u : m);
-        // the chain's records and its sub-op list: written here, read and
-        // bucketed (8 B) by rnd_bucket
-        atomicAdd(rd.acct + doc, 32ull * nc + 40ull * m);
+        // the chain's records; per sub-op its record read again and copied
+        // with its bucket entry into the chunk's bucket
+        atomicAdd(rd.acct + doc, 32ull * nc + 72ull * m);
       }
     } else if ((c % kChWaves) == u && l == 0) {
       rd.rchain[(uint64_t)doc * MTE_MAX_CLIENTS + (uint32_t)c] = make_uint2(off, 0u);
     }
     off += cap_c;
-  }
-}
-
-// every chain's sub-ops into their chunks' buckets: a thread per list entry
-__global__ __launch_bounds__(256) void rnd_bucket_kernel(ReplayArgs a, ChunkArgs ch, RoundArgs rd, uint32_t bpd) {
-  __shared__ uint2 chains[MTE_MAX_CLIENTS];
-  const int doc = (int)rd.d0 + (int)(blockIdx.x / bpd);
-  const uint4 p = rd.plan[doc];
-  if (p.x != kModeRound || rd.rflag[doc] != 0u) return;
-  if (threadIdx.x < MTE_MAX_CLIENTS) chains[threadIdx.x] = rd.rchain[(uint64_t)doc * MTE_MAX_CLIENTS + threadIdx.x];
-  __syncthreads();
-  const uint32_t e = (blockIdx.x % bpd) * blockDim.x + threadIdx.x;
-  bool mine = false;
-  for (int c = 0; c < MTE_MAX_CLIENTS; c++) mine = mine || (e >= chains[c].x && e < chains[c].x + chains[c].y);
-  if (!mine) return;
-  const uint4 en = rd.rlist[(uint64_t)doc * rd.rl_cap + e];
-  uint32_t* rcnt = rd.rcnt + (uint64_t)doc * ch.nch_cap;
-  const uint32_t pos = atomicAdd(rcnt + en.x, 1u);
-  if (pos < (uint32_t)kRB) {
-    // the entry and the sub-op's record next to it: the apply reads its chunk's
-    // records in one contiguous load instead of one dependent random read each
-    const uint64_t slot = ((uint64_t)doc * ch.nch_cap + en.x) * kRB + pos;
-    const uint4* rec = a.recs + 2 * (a.op_off[doc] + p.y + en.y);
-    const uint4 q0 = rec[0], q1 = rec[1];
-    rd.rbuf[slot] = make_uint2(en.y, en.z);
-    rd.rrec[2 * slot] = q0;
-    rd.rrec[2 * slot + 1] = q1;
-  } else {
-    atomicOr(rd.rflag + doc, 1u);
   }
 }
 
