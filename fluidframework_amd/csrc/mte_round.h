@@ -315,16 +315,21 @@ __global__ __launch_bounds__(256) void rnd_move_kernel(ReplayArgs a, ChunkArgs c
     const uint32_t ci = (uint32_t)dst[j] / fill;
     xs[j] = ch_slot(ch, doc, (int)ci) + ((uint32_t)dst[j] - ci * fill);
   }
-  for (int q = 0; q < kFieldPlanes + K; q++) {
+  // every plane's loads in flight before the stores (as rnd_gmove)
+  constexpr int NP = kFieldPlanes + K;
+  uint32_t v[NP][kChE];
+#pragma unroll
+  for (int q = 0; q < NP; q++)
 #pragma unroll
     for (int j = 0; j < kChE; j++) {
       const int i = t * kT + j * kWave + l;
-      if (keep[j] && (uint32_t)dst[j] < lim) {
-        const uint64_t x = xs[j];
-        ch.arena[(uint64_t)q * ch.astride + x] = pl[(uint64_t)q * a.stride + i];
-      }
+      v[q][j] = pl[(uint64_t)q * a.stride + (i < n ? i : 0)];
     }
-  }
+#pragma unroll
+  for (int q = 0; q < NP; q++)
+#pragma unroll
+    for (int j = 0; j < kChE; j++)
+      if (keep[j] && (uint32_t)dst[j] < lim) ch.arena[(uint64_t)q * ch.astride + xs[j]] = v[q][j];
 }
 
 // per chunk after the moves: its segment count and its round-start column
@@ -363,14 +368,24 @@ __global__ __launch_bounds__(256) void rnd_gmove_kernel(ReplayArgs a, ChunkArgs 
     const uint32_t d0 = ch.kc[(uint64_t)doc * ch.nch_cap + q];
     const uint64_t x0 = ch_slot(ch, doc, q);
     uint32_t* pl = a.planes + (uint64_t)doc * a.cap;
-    for (int qq = 0; qq < kFieldPlanes + K; qq++) {
+    // every plane's loads in flight before the stores (the two may alias as
+    // far as the compiler knows: interleaved, each plane waited for the last)
+    constexpr int NP = kFieldPlanes + K;
+    uint32_t v[NP][kChE];
+#pragma unroll
+    for (int qq = 0; qq < NP; qq++)
 #pragma unroll
       for (int j = 0; j < kChE; j++) {
         const int s = j * kWave + l;
-        if (s < cn && d0 + (uint32_t)s < a.cap)
-          pl[(uint64_t)qq * a.stride + d0 + (uint32_t)s] = ch.arena[(uint64_t)qq * ch.astride + x0 + s];
+        v[qq][j] = ch.arena[(uint64_t)qq * ch.astride + x0 + (s < cn ? s : 0)];
       }
-    }
+#pragma unroll
+    for (int qq = 0; qq < NP; qq++)
+#pragma unroll
+      for (int j = 0; j < kChE; j++) {
+        const int s = j * kWave + l;
+        if (s < cn && d0 + (uint32_t)s < a.cap) pl[(uint64_t)qq * a.stride + d0 + (uint32_t)s] = v[qq][j];
+      }
   });
 }
 
