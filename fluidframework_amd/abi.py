@@ -49,6 +49,8 @@ RP_POS1, RP_BEFORE1, RP_POS2, RP_BEFORE2 = 0x100, 0x200, 0x400, 0x800
 REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE, REF_TRANSIENT = 0x40, 0x80, 0x100  # ReferenceType (ops.ts)
 DELTA_REGEN = 0x10    # kind flag of its output records
 DELTA_REBASE = 0x20   # MTE_OP_REF b = 4 / 5: the answer's kind
+DELTA_SLIDE = 0x40    # a reference slid off a removed segment (MTE_DOC_SLIDE_EVENTS)
+DELTA_REFPOS = 0x80   # every reference as the record that slid one left the document
 ANNOTATE_SLOTS = 32   # pending local annotate groups tracked per document
 F_MARKER, F_MSG_END, F_REWRITE, F_LOCAL = 0x1, 0x2, 0x4, 0x8
 F_COMBINE = 0x10         # annotate combiningOp incr / consensus (value maps, include/mte.h)
@@ -132,6 +134,7 @@ EXPORTED_SYMBOLS = [
 
 DOC_EVENTS = 0x8
 DOC_REFS = 0x10
+DOC_SLIDE_EVENTS = 0x20
 DELTA_DTYPE = np.dtype([("op", "<u4"), ("kind", "<u4"), ("pos", "<i4"), ("len", "<i4"), ("removed", "<u4")])
 
 

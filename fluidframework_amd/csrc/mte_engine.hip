@@ -152,7 +152,8 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
   h.min_seq = in.min_seq;
   h.cur_seq = in.cur_seq;
   h.status = 0;
-  h.flags = in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC | MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS | MTE_DOC_REFS);
+  h.flags = in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC | MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS | MTE_DOC_REFS |
+                        MTE_DOC_SLIDE_EVENTS);
   h.resume = 0;
   h.pad0 = h.pad1 = 0;
   if (legacy) {

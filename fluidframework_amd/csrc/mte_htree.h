@@ -1015,7 +1015,7 @@ struct EvRun {
 
 template <int K, bool S>
 __device__ __forceinline__ int ht_range(HT& h, const s8v& op, bool local, const ReplayArgs& a, uint32_t (&st)[kNumStats], EvOut& ev,
-                        bool evd, uint2* rt, uint32_t rhi) {
+                        bool evd, uint2* rt, uint32_t rhi, bool evs) {
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   const int32_t s = op[0], r = op[1], start = op[4], end = op[5];
@@ -1186,8 +1186,8 @@ __device__ __forceinline__ int ht_range(HT& h, const s8v& op, bool local, const 
   h.lp_n = 0;  // the marks changed lengths
   if (rem && !local && rt && rhi) {
     const uint32_t* lrp = h.pl + (uint64_t)kLrsPlane<K> * h.sd;
-    stream_slide(h.pl, h.sd, h.n, rt, rhi, s, evd ? &ev : nullptr, kSlideOverlap, lrp, h.tw);
-    stream_slide(h.pl, h.sd, h.n, rt, rhi, s, evd ? &ev : nullptr, kSlideNew, lrp, h.tw);
+    stream_slide(h.pl, h.sd, h.n, rt, rhi, s, evs ? &ev : nullptr, kSlideOverlap, lrp, h.tw);
+    stream_slide(h.pl, h.sd, h.n, rt, rhi, s, evs ? &ev : nullptr, kSlideNew, lrp, h.tw);
   }
   return 0;
 }
@@ -1847,14 +1847,17 @@ __device__ __forceinline__ int ht_ref_rebase(HT& h, const s8v& op, int32_t lseq,
 // if it is gone (titems.c slide_keys).  One wave-wide search per record.
 // (Out of line, its arguments by value: a reference to the pass's state would
 // keep that state in scratch for the whole kernel.)
-__device__ __noinline__ void ht_slide_keys(const uint32_t* pl, uint64_t sd, int n, mte_delta* evp, uint32_t to,
-                                           uint32_t from) {
-  if (from >= to) return;
+// Returns the number of slide records.
+__device__ __noinline__ uint32_t ht_slide_keys(const uint32_t* pl, uint64_t sd, int n, mte_delta* evp, uint32_t to,
+                                               uint32_t from) {
+  if (from >= to) return 0;
   vm_drain();  // this wave's record stores are visible to its loads
   const int l = lane_id();
+  uint32_t slid = 0;
   for (uint32_t q = from; q < to; q++) {
     const uint32_t kind = uni(ld_l2(&evp[q].kind));
     if ((kind & 0xc0u) != MTE_DELTA_SLIDE) continue;
+    slid++;
     const uint32_t u = uni(ld_l2(reinterpret_cast<const uint32_t*>(&evp[q].len)));
     int32_t key = -1, carry = 0;
     for (int tb = 0; tb < n; tb += kWave) {
@@ -1874,6 +1877,50 @@ __device__ __noinline__ void ht_slide_keys(const uint32_t* pl, uint64_t sd, int 
     if (l == 0) evp[q].len = key;
   }
   vm_drain();
+  return slid;
+}
+
+// MTE_DELTA_REFPOS (include/mte.h): every live reference of slots [0, rhi) as
+// a record that slid one left the document -- its position (as mte_read_refs;
+// -2 - its Transient position for one off the string, as
+// mte_read_refs_transient finds it) and its order key (as mte_read_ref_order):
+// what the reference's slide callbacks read mid-op (intervalCollection.ts:
+// 1042-1053; titems.c ref_snapshot).  A lane per reference walks the items
+// with wave-uniform loads: rare (records that slid something), so simple.
+// Returns the event count after the records (ev.n).
+__device__ __noinline__ uint32_t ht_ref_snapshot(const uint32_t* pl, uint64_t sd, int n, const uint2* rt, uint32_t rhi,
+                                                 mte_delta* evp, uint64_t cap, uint32_t en, uint32_t op) {
+  const int l = lane_id();
+  for (uint32_t rb = 0; rb < rhi; rb += kWave) {
+    const uint32_t r = rb + (uint32_t)l;
+    const uint32_t rc = r < rhi ? r : 0u;  // unconditional loads, selected after
+    const uint32_t anc = ld_l2(&rt[rc].x), st = ld_l2(&rt[rc].y);
+    const bool live = r < rhi && (st & kRefLive);
+    const bool det = (st & kRefDetached) != 0, off = (st & kRefOff) != 0;
+    int32_t pos = -1, tpos = -1, key = -1, own = 0, all = 0;
+    bool found = false;
+    for (int i = 0; i < n; i++) {
+      const uint32_t ln = uni(ld_l2(pl + i)), tf = uni(ld_l2(pl + 5 * sd + i));
+      const int32_t rs = (int32_t)uni(ld_l2(pl + 2 * sd + i));
+      const bool hit = !found && anc - tf < ln;
+      if (hit) {
+        const int32_t p = own + (rs != kNone ? 0 : (int32_t)(anc - tf));
+        tpos = p;
+        pos = det ? -1 : p;
+        key = (det && !off) ? -1 : all + (int32_t)(anc - tf);
+        found = true;
+      }
+      own += rs == kNone ? (int32_t)ln : 0;
+      all += (int32_t)ln;
+    }
+    if (det) pos = (off && tpos >= 0) ? -2 - tpos : -1;
+    const uint64_t lm = __ballot(live);
+    const uint32_t idx = en + lanes_below(lm);
+    if (live && idx < cap) evp[idx] = mte_delta{op, MTE_DELTA_REFPOS, pos, key, r};
+    en += (uint32_t)__popcll(lm);
+  }
+  vm_drain();
+  return en;
 }
 
 template <int K, bool S>
@@ -1891,6 +1938,7 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
   const bool ldoc = h.ldoc;
   const bool evd = (D.flags & MTE_DOC_EVENTS) != 0;
   const bool refd = (D.flags & MTE_DOC_REFS) != 0 && a.refs != nullptr;
+  const bool evs = evd && refd && (D.flags & MTE_DOC_SLIDE_EVENTS) != 0;  // slide records (and snapshots)
   uint2* const rt = refd ? a.refs + (uint64_t)D.doc * a.ref_cap : nullptr;
   ev.op = D.k;
   const uint32_t ev_from = ev.n;  // this record's first event
@@ -2020,13 +2068,13 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
     }
   } else if (type == MTE_OP_REMOVE || type == MTE_OP_ANNOTATE) {
     HPROF_BEGIN(t0)
-    rc = ht_range<K, S>(h, op, lop, a, st, ev, evd, rt, rhi);
+    rc = ht_range<K, S>(h, op, lop, a, st, ev, evd, rt, rhi, evs);
     HPROF_END(h, 1, t0)
     if (rc) return rc;
   } else if (type == MTE_OP_ACK) {
     if (!(op[4] > 0 && op[4] <= op[5] && op[5] <= lseq)) return MTE_E_INVALID_ARG;
     HPROF_BEGIN(t0)
-    rc = ht_ack<K>(h, op, a, rt, refd ? rhi : 0u, evd ? &ev : nullptr);
+    rc = ht_ack<K>(h, op, a, rt, refd ? rhi : 0u, evs ? &ev : nullptr);
     HPROF_END(h, 2, t0)
     if (rc) return rc;
   } else if (type != MTE_OP_NOOP) {
@@ -2053,9 +2101,12 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
       if ((rc = ht_zamboni<K>(h, a.n_keys))) return rc;
     }
   }
-  // the slides of this record, keyed by the units they left as they stand now
-  if (evd && rt && ev.n > ev_from)
-    ht_slide_keys(h.pl, h.sd, h.n, ev.p, ev.n < ev.cap ? ev.n : (uint32_t)ev.cap, ev_from);
+  // the slides of this record, keyed by the units they left as they stand now,
+  // then every reference as this record left them
+  if (evs && ev.n > ev_from) {
+    const uint32_t slid = ht_slide_keys(h.pl, h.sd, h.n, ev.p, ev.n < ev.cap ? ev.n : (uint32_t)ev.cap, ev_from);
+    if (slid) ev.n = ht_ref_snapshot(h.pl, h.sd, h.n, rt, rhi, ev.p, ev.cap, ev.n, ev.op);
+  }
   return 0;
 }
 

@@ -50,6 +50,7 @@ function loadAddon() {
 // 940-943; mergeTree.ts:1078-1084, 1666-1672)
 const ASSERT_CODES = { "-5": 0x030, "-6": 0x031, "-7": 0x039 };
 const DELTA_SLIDE = 0x40;  // MTE_DELTA_SLIDE (include/mte.h): a reference slid off a removed segment
+const DELTA_REFPOS = 0x80;  // MTE_DELTA_REFPOS: the references' positions after a group op's member
 
 function docError(code, doc) {
   const a = loadAddon();
@@ -129,7 +130,10 @@ class MergeTreeEngine {
     if (o.refs && !o.localClient) throw new MergeTreeError(-9, "local references need {localClient: true}");
     this.docs.push({ text: initialText || "", newLengthCalc: !!o.newLengthCalc, roundSync: !!o.roundSync, props: o.props,
       minSeq: o.minSeq || 0, currentSeq: o.currentSeq || 0, segments: o.segments, localClient: !!o.localClient,
-      events: !!o.events, refs: !!o.refs });
+      events: !!o.events, refs: !!o.refs,
+      // an interval collection's mid-op events need the references' slides
+      // (MTE_DOC_SLIDE_EVENTS): on with events and references unless asked off
+      slideEvents: !!(o.events && o.refs && o.slideEvents !== false) });
     const c = new BatchClient(this, doc, o.observerId === undefined ? (o.longClientId || "A") : o.observerId,
       !!o.localClient);
     this.clients.push(c);
@@ -468,23 +472,21 @@ class BatchClient {
     this.engine._batch().addMessage(this.doc, this.clients, msg);
     if (msg.minimumSequenceNumber > this.lastMinSeq) this.lastMinSeq = msg.minimumSequenceNumber;
     // an interval collection's ends slide inside merge-tree ops (a remote
-    // remove, the ack of our own): the reference raises "changeInterval"
-    // there, mid-op (intervalCollection.ts:1042-1053), with the document as it
-    // is at that moment -- so a document whose collections hold intervals
-    // replays message by message and its slides come back as MTE_DELTA_SLIDE
-    // records (_deliver -> IntervalCollection._onSlides)
-    if (this._slideSync()) {
-      this.engine.flush();
-      this.engine.sync();
-    }
+    // remove, the ack of our own), where the reference raises "changeInterval"
+    // (intervalCollection.ts:1042-1053): the engine reports each slide with
+    // every reference as that record left the document (MTE_DELTA_SLIDE,
+    // MTE_DELTA_REFPOS), so the message stays queued and the events come at
+    // the flush (_deliver -> IntervalCollection._onSlides)
   }
 
-  /** The document's collections hold intervals whose ends can slide, and its
-   *  slides are reported ({events: true}). */
-  _slideSync() {
-    if (!this.intervalCollections || !this.engine.docs[this.doc].events) return false;
-    for (const c of this.intervalCollections.values()) if (c.byId.size) return true;
-    return false;
+  /** Replay this document's queued messages before an interval collection
+   *  reads or changes its state (positions, the end tree): the engine-wide
+   *  flush when anything of this document is queued. */
+  _settle() {
+    const e = this.engine;
+    if (!e.started) return;
+    if (e.pending.docCount[this.doc]) e.flush();
+    e.sync();
   }
 
   // ---- local ops (documents created with {localClient: true}) ----
@@ -634,9 +636,15 @@ class BatchClient {
       }
       const ranges = [];
       let kind = -1;
-      let slides = null;
+      let slides = null, snap = null;
       while (i < n && flat[5 * i] === k) {
         const kd = flat[5 * i + 1];
+        if ((kd & 0xff) === DELTA_REFPOS) {  // slot -> [position, Transient position, order key]
+          const p = flat[5 * i + 2] | 0;
+          (snap || (snap = new Map())).set(flat[5 * i + 4], [p < -1 ? -1 : p, p < -1 ? -2 - p : p, flat[5 * i + 3] | 0]);
+          i++;
+          continue;
+        }
         if ((kd & 0xff) >= DELTA_SLIDE && (kd & 0xff) < 2 * DELTA_SLIDE) {
           // a reference slid off a removed-and-acked segment (MTE_DELTA_SLIDE)
           (slides || (slides = [])).push({ slot: flat[5 * i + 4], pos: flat[5 * i + 2] | 0, seg: flat[5 * i + 3] | 0,
@@ -649,44 +657,19 @@ class BatchClient {
           segment: kind === 0 && src.op ? src.op.seg : undefined });
         i++;
       }
-      parsed[k] = { kind, ranges, slides };
+      parsed[k] = { kind, ranges, slides, snap };
     }
-    // a remote group op applies its members one after another (client.ts
-    // applyRemoteOp per member), so a reference sliding at member k sees the
-    // document as member k left it: positions read after the message map back
-    // through the later members' inserts and removes, and a reference a later
-    // member slides again sat, after member k, where that member found it (its
-    // removed segment's place before the removal, mapped back the same way)
-    const undo = (p, later) => {
-      if (p < 0) return p;
-      for (let j = later.length - 1; j >= 0; j--) {
-        const { kind, ranges } = later[j];
-        if (kind !== 0 && kind !== 1) continue;
-        let d = 0;
-        for (const r of ranges) {
-          if (kind === 1 ? r.position <= p : r.position + r.length <= p) d += r.length;
-        }
-        p = kind === 1 ? p + d : p - d;
-      }
-      return p;
-    };
+    // the references as record k left the document (MTE_DELTA_REFPOS): a
+    // reference sliding there sees the document at that moment -- inside a
+    // remote group op, between its members (client.ts applyRemoteOp per
+    // member), and in any case before the rest of the batch
     const backTo = (k) => {
-      const later = [];
-      for (let j = k + 1; j < recs.length && parsed[j] && !recs[j].local && recs[j].msg === recs[k].msg; j++) {
-        later.push(parsed[j]);
-      }
-      if (later.length === 0) return null;
-      const seen = new Map();  // slot -> its position after member k
-      later.forEach((pj, j) => {
-        for (const r of pj.slides || []) {
-          if (seen.has(r.slot)) continue;
-          // before member j removed it: the removed segment's own-view place
-          // plus the reference's offset in it (a regenerated group op removes
-          // one segment per member)
-          seen.set(r.slot, undo(r.pos + r.off, later.slice(0, j)));
-        }
-      });
-      return { at: (slot, p) => (seen.has(slot) ? seen.get(slot) : undo(p, later)) };
+      const snap = parsed[k] && parsed[k].snap;
+      if (!snap) return null;
+      return {
+        at: (slot, transient) => (snap.has(slot) ? snap.get(slot)[transient ? 1 : 0] : -1),
+        key: (slot) => (snap.has(slot) ? snap.get(slot)[2] : -1),
+      };
     };
     for (let k = 0; k < recs.length; k++) {
       const src = recs[k];
@@ -698,7 +681,7 @@ class BatchClient {
       }
       const { kind, ranges, slides } = pr;
       if (kind < 0) {
-        if (slides) this._slid(slides, src.local ? null : backTo(k));
+        if (slides) this._slid(slides, backTo(k));
         continue;
       }
       if (cur) cur.ops.push(...opsFromDelta(kind, ranges, src.op));
@@ -707,7 +690,7 @@ class BatchClient {
       for (const fn of this.listeners || []) fn(ev, this);
       // markRangeRemoved slides the newly removed segments' references after
       // the delta callback (mergeTree.ts:1978-1993)
-      if (slides) this._slid(slides, src.local ? null : backTo(k));
+      if (slides) this._slid(slides, backTo(k));
     }
     flushMsg();
   }

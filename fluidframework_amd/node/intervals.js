@@ -25,10 +25,14 @@
 // compareReferencePositions orders them).  Events (IIntervalCollectionEvent,
 // :1257-1300) fire for the collection's own edits and the interval ops it
 // processes; an end the engine slides off a removed segment inside a merge-tree
-// op moves without a "changeInterval" event (the reference raises one from the
-// reference's position-change listeners, :1023-1058, mid-op).
+// op raises "changeInterval" as the reference's position-change listeners do
+// mid-op (:1023-1058): the engine reports the slide (MTE_DELTA_SLIDE) with
+// every reference as that record left the document (MTE_DELTA_REFPOS), and the
+// events are raised when the batch holding the op is delivered (_onSlides).
+// Each entry point first replays what its document has queued (_settle), so
+// those events come before the collection's own.
 const { MergeTreeError } = require("./packing");
-const { RedBlackTree } = require("./rbtree");
+const { RedBlackTree, KeyMovedError } = require("./rbtree");
 
 // ReferenceType (merge-tree ops.ts) and IntervalType (intervalCollection.ts:48-66)
 const RefType = { Simple: 0x0, Tile: 0x1, NestBegin: 0x2, NestEnd: 0x4, RangeBegin: 0x10, RangeEnd: 0x20,
@@ -113,6 +117,8 @@ class SequenceInterval {
   }
   _keys() {
     if (this._pinKeys) return this._pinKeys;  // the ends as they were (an index removal before they moved)
+    const v = this.collection._keyView;  // inside a group op: as one of its members left them
+    if (v) return [v(this.start), v(this.end)];
     const c = this.collection.client;
     return [c._refOrder(this.start), c._refOrder(this.end)];
   }
@@ -240,14 +246,16 @@ class IntervalCollection {
     return !!(e && e.docs && e.docs[this.client.doc] && e.docs[this.client.doc].events);
   }
   _endPut(ival) {
+    if (this.client.traceEnd) process.stderr.write(`    PUT ${ival.getIntervalId()} ${JSON.stringify(ival._keys())}\n`);
     if (this._tracksSlides()) this.endTree.put(ival, ival);
   }
   _endRemove(ival) {
+    if (this.client.traceEnd) process.stderr.write(`    DEL ${ival.getIntervalId()} ${JSON.stringify(ival._keys())}\n`);
     if (!this._tracksSlides()) return;
     try {
       this.endTree.remove(ival);
     } catch (e) {
-      if (!(e instanceof TypeError)) throw e;
+      if (!(e instanceof KeyMovedError)) throw e;
       // an end whose unit the zamboni took no longer compares as it did (the
       // reference keeps comparing the removed segment's stale ordinal,
       // referencePositions.ts:81-89): the descent left the tree -- rebuilt,
@@ -418,13 +426,17 @@ class IntervalCollection {
    *  localSeq (changeInterval with localSeq, :1782-1799).  Replays what is
    *  queued (flush + sync). */
   rebaseLocalInterval(opName, v, localSeq) {
+    this.client._settle();
     const id = v.properties && v.properties[reservedIntervalIdKey];
     const ival = id === undefined ? undefined : this.byId.get(id);
     const reqs = [];
     if (v.start !== undefined) reqs.push({ pos: v.start, seqFrom: v.sequenceNumber, localSeq });
     if (v.end !== undefined) reqs.push({ pos: v.end, seqFrom: v.sequenceNumber, localSeq });
     const nPos = reqs.length;
-    // the slides ride in the same replay (ignored if an end detaches)
+    // the slides ride in the same replay (ignored if an end detaches); the
+    // interval leaves the end tree with its ends as they were (removeExistingInterval
+    // of the unmodified interval)
+    const before = ival && this._tracksSlides() ? ival._keys() : null;
     if (ival) reqs.push({ slot: ival.start.slot, localSeq }, { slot: ival.end.slot, localSeq });
     const r = reqs.length ? this.client._rebase(reqs) : [];
     let k = 0;
@@ -441,8 +453,17 @@ class IntervalCollection {
       return undefined;
     }
     if (ival && (r[nPos] !== -1 || r[nPos + 1] !== -1)) {  // re-added by changeInterval (removeExisting + add)
+      // modify makes each moved end a new reference (createPositionReference,
+      // :573-609), pushed onto the "at" list of its offset, start first
+      for (const [k, lref] of [[nPos, ival.start], [nPos + 1, ival.end]]) {
+        if (r[k] === -1) continue;
+        lref.list = 1;
+        lref.listOrder = lref.constructor.pushStamp();
+      }
       ival.stamp = ++this.stamp;
+      ival._pinKeys = before;
       this._endRemove(ival);
+      delete ival._pinKeys;
       this._endPut(ival);
     }
     return rebased;
@@ -450,6 +471,7 @@ class IntervalCollection {
 
   /** IntervalCollection.add (:1430-1460). */
   add(start, end, intervalType, props) {
+    this.client._settle();
     const ival = this._addInterval(start, end, intervalType, props);
     this.emitter.emit("add", undefined, { end, intervalType, properties: Object.assign({}, ival.properties),
       sequenceNumber: curSeq(this.client), start }, this._meta());
@@ -459,6 +481,7 @@ class IntervalCollection {
 
   /** IntervalCollection.removeIntervalById (:1493-1502) -> deleteExistingInterval (:1462-1491). */
   removeIntervalById(id) {
+    this.client._settle();
     const ival = this.byId.get(id);
     if (ival) {
       // serialize() without the ends' positions (a replay per delete; receivers
@@ -474,6 +497,7 @@ class IntervalCollection {
 
   /** IntervalCollection.changeProperties (:1510-1537). */
   changeProperties(id, props) {
+    this.client._settle();
     if (typeof id !== "string") throw new MergeTreeError(-1, "Change API requires an ID that is a string");
     if (!props) throw new MergeTreeError(-1, "changeProperties should be called with a property set");
     const ival = this.byId.get(id);
@@ -489,6 +513,7 @@ class IntervalCollection {
   /** IntervalCollection.change (:1546-1577): the ends given move (StayOnRemove
    *  until the change is acked); a pending change per end. */
   change(id, start, end) {
+    this.client._settle();
     if (typeof id !== "string") throw new MergeTreeError(-1, "Change API requires an ID that is a string");
     const ival = this.byId.get(id);
     if (!ival) return undefined;
@@ -528,6 +553,7 @@ class IntervalCollection {
    *  intervalCollections.tryProcessMessage, sequence.ts:628-648): the merge-tree
    *  window does not move. */
   process(opName, value, local, op) {
+    this.client._settle();
     if (!value) return;  // deleted while rebasing
     if (opName === "add") this.ackAdd(value, local, op);
     else if (opName === "delete") this.ackDelete(value, local, op);
@@ -627,9 +653,9 @@ class IntervalCollection {
 
   // ---- ends sliding inside merge-tree ops --------------------------------------
   /** The references one merge-tree op slid off removed-and-acked segments
-   *  (MTE_DELTA_SLIDE records, BatchClient._deliver; the document replays
-   *  message by message while the collection holds intervals, so the engine's
-   *  state is the state right after this op).  The reference calls each
+   *  (MTE_DELTA_SLIDE records, BatchClient._deliver; back: the references
+   *  as that record left the document, MTE_DELTA_REFPOS -- positions and order
+   *  keys are read from it, not from the document after the batch).  The reference calls each
    *  sliding end's beforeSlide / afterSlide (localReference.ts:436-447,
    *  471-480, mergeTree.ts:921-950), which for an interval end are the
    *  collection's position-change listeners (addIntervalListeners,
@@ -654,6 +680,7 @@ class IntervalCollection {
     }
     const mine = slides.filter((r) => owner.has(r.slot));
     if (mine.length === 0) return;
+    if (!back) throw new MergeTreeError(-1, "slide records without the references' snapshot (MTE_DELTA_REFPOS)");
     const ref = (r) => { const [x, w] = owner.get(r.slot); return w ? x.end : x.start; };
     // runs of one removed segment each, in the engine's order (r.seg: the unit
     // the end left, as an order key after the op, so r.seg - r.off keys its
@@ -673,8 +700,8 @@ class IntervalCollection {
     const c = this.client;
     // positions as the op left them; inside a remote group op, as its member
     // that slid these left them (back: the later members undone)
-    const now = back ? (lref) => back.at(lref.slot, c.localReferencePositionToPosition(lref))
-      : (lref) => c.localReferencePositionToPosition(lref);
+    const now = (lref) => back.at(lref.slot, false);
+    const nowT = (lref) => back.at(lref.slot, true);
     // each sliding end's records in order: where it sits before each one
     const queue = new Map();
     for (const r of mine) {
@@ -689,10 +716,16 @@ class IntervalCollection {
     const ghost = new Map();
     // the end tree compares the ends as they stand at each slide: an end still
     // to slide keeps the key of the unit it sits on (pinned)
+    // every end as this record left it
+    this._keyView = (lref) => back.key(lref.slot);
+    const keyNow = (lref) => back.key(lref.slot);
     const touched = new Set(mine.map((r) => owner.get(r.slot)[0]));
     for (const x of touched) x._pinKeys = x._keys();
     for (const [slot, q] of queue) if (q[0].seg >= 0) owner.get(slot)[0]._pinKeys[owner.get(slot)[1]] = q[0].seg;
     const watch = this._has("changeInterval");
+    // the events below are the ones a merge-tree op raises (for listeners that
+    // tell them apart: the op is applied, its batch being delivered)
+    this.inMergeTreeOp = true;
     try {
       for (const seg of runs) {
         seg.sort((a, b) => (a.off - b.off) || (ref(a).list - ref(b).list) || (ref(a).listOrder - ref(b).listOrder));
@@ -706,12 +739,16 @@ class IntervalCollection {
           const next = q.length ? q[0].pos : now(lref);
           const other = which ? ival.start : ival.end;
           const otherPos = posNow.has(other.slot) ? posNow.get(other.slot) : now(other);
-          const otherPrev = otherPos === -1 && ghost.has(other.slot) ? ghost.get(other.slot) : otherPos;
+          // a previous interval's end is a Transient clone (cloneRef, :1024-1039):
+          // an end that slid off the string in an earlier op still reads its
+          // removed segment's position
+          const otherPrev = otherPos !== -1 ? otherPos
+            : (ghost.has(other.slot) ? ghost.get(other.slot) : (posNow.has(other.slot) ? -1 : nowT(other)));
           // beforeSlide: out of the index (removeIntervalFromIndex, :1042-1047)
           this._endRemove(ival);
           posNow.set(r.slot, next);
           if (next === -1) ghost.set(r.slot, at);
-          ival._pinKeys[which] = q.length && q[0].seg >= 0 ? q[0].seg : c._refOrder(lref);
+          ival._pinKeys[which] = q.length && q[0].seg >= 0 ? q[0].seg : keyNow(lref);
           // its place among the new segment's references: addBeforeTombstones
           // puts one segment's references, in order, in front of offset 0's
           // before list; addAfterTombstones pushes them onto the last offset's
@@ -747,12 +784,15 @@ class IntervalCollection {
       }
     } finally {
       for (const x of touched) delete x._pinKeys;
+      delete this._keyView;
+      this.inMergeTreeOp = false;
     }
   }
 
   // ---- queries (LocalIntervalCollection, :760-913) ------------------------------
   /** The interval tree's order (compare, :483-506). */
   _sorted() {
+    this.client._settle();
     return Array.from(this.byId.values()).sort((a, b) => a.compare(b));
   }
 
@@ -807,6 +847,7 @@ class IntervalCollection {
    *  Transient interval at [startPosition, endPosition] (ends inclusive), in
    *  tree order. */
   findOverlappingIntervals(startPosition, endPosition) {
+    this.client._settle();
     if (endPosition < startPosition || this.byId.size === 0) return [];
     const t = new TransientInterval(this.client, startPosition, endPosition);
     return this._sorted().filter((x) => {
@@ -818,10 +859,12 @@ class IntervalCollection {
   /** previousInterval / nextInterval (:897-913): the data of the end tree's
    *  floor / ceil node of a Transient interval at pos. */
   previousInterval(pos) {
+    this.client._settle();
     const n = this._ends().floor(new TransientInterval(this.client, pos, pos));
     return n ? n.data : undefined;
   }
   nextInterval(pos) {
+    this.client._settle();
     const n = this._ends().ceil(new TransientInterval(this.client, pos, pos));
     return n ? n.data : undefined;
   }

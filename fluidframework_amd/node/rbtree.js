@@ -17,6 +17,11 @@
 
 const RED = 0, BLACK = 1;
 
+/** remove(key) walked off the tree: contains(key) found a node, but a node
+ *  on the way no longer compares as it did when it was put (an end that moved
+ *  without a remove / put), so the descent toward it left the tree. */
+class KeyMovedError extends Error {}
+
 class Node {
   constructor(key, data, color) {
     this.key = key;
@@ -90,11 +95,13 @@ class RedBlackTree {
 
   _remove(node, key) {
     if (this.compare(key, node.key) < 0) {
+      if (node.left === undefined) throw new KeyMovedError("the removal left the tree");
       if (!isRed(node.left) && !isRed(node.left.left)) node = this._moveRedLeft(node);
       node.left = this._remove(node.left, key);
     } else {
       if (isRed(node.left)) node = this._rotateRight(node);
       if (this.compare(key, node.key) === 0 && node.right === undefined) return undefined;
+      if (node.right === undefined) throw new KeyMovedError("the removal left the tree");
       if (!isRed(node.right) && !isRed(node.right.left)) node = this._moveRedRight(node);
       if (this.compare(key, node.key) === 0) {
         let m = node.right;
@@ -197,4 +204,4 @@ class RedBlackTree {
   }
 }
 
-module.exports = { RedBlackTree };
+module.exports = { RedBlackTree, KeyMovedError };

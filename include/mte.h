@@ -138,6 +138,16 @@ extern "C" {
  * (localReference.ts:436-447, 471-480): an interval collection's "changeInterval"
  * events raised mid-op (intervalCollection.ts:1042-1053). */
 #define MTE_DELTA_SLIDE 0x40u
+/* MTE_DOC_SLIDE_EVENTS documents: after each record that produced
+ * MTE_DELTA_SLIDE records, one record per live reference slot, as that record
+ * left the document: pos = its position as mte_read_refs reads it (-1
+ * detached), or -2 - p for a reference off the string whose segment
+ * mte_read_refs_transient still finds at p; len = its order key (as
+ * mte_read_ref_order reads it); removed = the slot.  The reference raises the
+ * slides' events mid-op (a group op applies its members one after another,
+ * client.ts applyRemoteOp), so a host that delivers them after a batch reads
+ * positions and order from these, not from the document after the batch. */
+#define MTE_DELTA_REFPOS 0x80u
 /* Follows an annotate's MTE_OP_ROLLBACK (a local record): for each key k the
  * rolled-back annotate set (pos1 = k), the older pending annotates that set k
  * too, latest first -- pos2 = its group slot, a = the value id it set, seq =
@@ -343,6 +353,14 @@ typedef struct mte_config {
  * marker insert), which identifies the marker as a text unit's arena offset
  * identifies that unit.                                                        */
 #define MTE_DOC_REFS 0x10u
+/* With MTE_DOC_REFS | MTE_DOC_EVENTS: also record the references' slides
+ * (MTE_DELTA_SLIDE) and, after each record that slid one, every reference as
+ * that record left the document (MTE_DELTA_REFPOS) -- what an interval
+ * collection's position-change listeners read mid-op
+ * (intervalCollection.ts:1042-1053).  They take event capacity
+ * (mte_set_event_capacity) beside the delta ranges, so a host that does not
+ * read them leaves the flag clear.                                            */
+#define MTE_DOC_SLIDE_EVENTS 0x20u
 
 /* Initial document: one text segment inserted before collaboration starts, as
  * the reference replay harness does (client.replay.spec.ts:22-23): seq 0

@@ -204,6 +204,15 @@ function runSet(p) {
     const coll = factory.load(emitter, []);
     coll.attachGraph(c, LABEL);
     const X = { c, coll, lastSeq: 0, ids: [], ev: [], mt: false };
+    if (process.env.MTE_REF_TRACE === n && coll.localCollection && coll.localCollection.endIntervalTree) {
+      // the end tree's puts and removes (the host restates them, node/intervals.js)
+      const t = coll.localCollection.endIntervalTree;
+      const at = (x) => `${x.getIntervalId ? x.getIntervalId() : "?"} [${c.localReferencePositionToPosition(x.start)},` +
+        `${c.localReferencePositionToPosition(x.end)}]`;
+      const put = t.put.bind(t), remove = t.remove.bind(t);
+      t.put = (k, d, cf) => { process.stderr.write(`    PUT ${at(k)}\n`); return put(k, d, cf); };
+      t.remove = (k) => { process.stderr.write(`    DEL ${at(k)}\n`); return remove(k); };
+    }
     if (p.ext) {
       const pos = (r) => c.localReferencePositionToPosition(r);
       coll.on("addInterval", (ival, local, op) => X.ev.push(["add", ival.getIntervalId(), local, !!op, X.mt]));

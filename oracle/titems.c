@@ -1059,7 +1059,7 @@ static int slide_item_refs(idoc* d, uint32_t i, int32_t grp, uint32_t cur, int e
 }
 static int doc_slide_refs(idoc* d, int32_t s, int mode) {
   if (!(d->flags & MTE_DOC_REFS) || !d->ref_hi) return MTE_OK;
-  const int evd = (d->flags & MTE_DOC_EVENTS) != 0;
+  const int evd = (d->flags & MTE_DOC_EVENTS) && (d->flags & MTE_DOC_SLIDE_EVENTS);  /* slide records */
   int rc;
   if (mode == 1) {
     /* the group's segments in group order, each slid while the later ones are pending */
@@ -1539,11 +1539,33 @@ static void slide_keys(idoc* d, uint64_t from) {
   }
 }
 
+static int32_t ref_position(const idoc* d, uint32_t r, int transient);
+static int64_t ref_order_key(const idoc* d, uint32_t r);
+
+/* MTE_DELTA_REFPOS (include/mte.h): after a record that slid references,
+ * every live reference as it left the document -- its position (-2 - the
+ * Transient one for a reference off the string) and order key: what the
+ * reference's slide callbacks read mid-op (intervalCollection.ts:1042-1053) */
+static int ref_snapshot(idoc* d) {
+  for (uint32_t r = 0; r < d->ref_hi; r++) {
+    if (!(d->ref_state[r] & REF_LIVE)) continue;
+    const int32_t p = ref_position(d, r, 0), tp = ref_position(d, r, 1);
+    const int rc = delta_push(d, MTE_DELTA_REFPOS, p >= 0 ? p : (tp >= 0 ? -2 - tp : -1), (int32_t)ref_order_key(d, r), r);
+    if (rc) return rc;
+  }
+  return MTE_OK;
+}
+
 static int doc_apply_op(idoc* d, const mte_op* op, const env_t* env);
 static int doc_apply(idoc* d, const mte_op* op, const env_t* env) {
   const uint64_t from = d->dl_n;
-  const int rc = doc_apply_op(d, op, env);
-  if (!rc && (d->flags & MTE_DOC_EVENTS) && (d->flags & MTE_DOC_REFS) && d->dl_n > from) slide_keys(d, from);
+  int rc = doc_apply_op(d, op, env);
+  if (!rc && (d->flags & MTE_DOC_SLIDE_EVENTS) && d->dl_n > from) {
+    slide_keys(d, from);
+    int slid = 0;
+    for (uint64_t q = from; q < d->dl_n; q++) slid |= (d->dl[q].kind & 0xc0u) == MTE_DELTA_SLIDE;
+    if (slid) rc = ref_snapshot(d);
+  }
   return rc;
 }
 
@@ -2050,45 +2072,47 @@ int oti_read_deltas(oti_ctx* c, uint32_t doc, mte_delta* out, uint64_t cap, uint
  * segment unlinked by the zamboni) */
 /* mte_read_ref_order: the index, among every unit the document holds, of the
  * unit each reference sits on (-1 detached / unused) */
+/* the order key of reference slot r: the index, among every unit the document
+ * holds, of the unit it sits on (-1 detached / unused) */
+static int64_t ref_order_key(const idoc* d, uint32_t r) {
+  if (r >= d->ref_hi) return -1;
+  const uint32_t st = d->ref_state[r], u = d->ref_anchor[r];
+  if (!(st & REF_LIVE) || ((st & REF_DETACHED) && !(st & REF_OFF))) return -1; /* off the string: on its segment */
+  int64_t p = 0;
+  for (uint32_t i = 0; i < d->n; i++) {
+    const item* g = &d->it[i];
+    if (!g->empty && u - g->toff < (uint32_t)g->len) return p + (int64_t)(u - g->toff);
+    p += g->empty ? 0 : g->len;
+  }
+  return -1;
+}
+
 int oti_read_ref_order(oti_ctx* c, uint32_t doc, int64_t* key, uint32_t n) {
   if (!c || (n && !key) || doc >= c->n_docs) return MTE_E_INVALID_ARG;
   const idoc* d = &c->docs[doc];
-  for (uint32_t r = 0; r < n; r++) {
-    key[r] = -1;
-    if (r >= d->ref_hi) continue;
-    const uint32_t st = d->ref_state[r], u = d->ref_anchor[r];
-    if (!(st & REF_LIVE) || ((st & REF_DETACHED) && !(st & REF_OFF))) continue; /* off the string: on its segment */
-    int64_t p = 0;
-    for (uint32_t i = 0; i < d->n; i++) {
-      const item* g = &d->it[i];
-      if (!g->empty && u - g->toff < (uint32_t)g->len) {
-        key[r] = p + (int64_t)(u - g->toff);
-        break;
-      }
-      p += g->empty ? 0 : g->len;
-    }
-  }
+  for (uint32_t r = 0; r < n; r++) key[r] = ref_order_key(d, r);
   return MTE_OK;
+}
+
+/* the position of reference slot r (-1 detached / unused / a unit no segment
+ * holds); transient: one taken off its segment's list still finds it */
+static int32_t ref_position(const idoc* d, uint32_t r, int transient) {
+  if (r >= d->ref_hi) return -1;
+  const uint32_t st = d->ref_state[r], u = d->ref_anchor[r];
+  if (!(st & REF_LIVE) || ((st & REF_DETACHED) && !(transient && (st & REF_OFF)))) return -1;
+  int64_t p = 0;
+  for (uint32_t i = 0; i < d->n; i++) {
+    const item* g = &d->it[i];
+    if (!g->empty && u - g->toff < (uint32_t)g->len) return (int32_t)(p + (g->rseq != NONE_SEQ ? 0 : (int64_t)(u - g->toff)));
+    p += g->empty ? 0 : own_len(g);
+  }
+  return -1;
 }
 
 static int read_refs_view(oti_ctx* c, uint32_t doc, int32_t* pos, uint32_t n, int transient) {
   if (!c || (n && !pos) || doc >= c->n_docs) return MTE_E_INVALID_ARG;
   const idoc* d = &c->docs[doc];
-  for (uint32_t r = 0; r < n; r++) {
-    pos[r] = -1;
-    if (r >= d->ref_hi) continue;
-    const uint32_t st = d->ref_state[r], u = d->ref_anchor[r];
-    if (!(st & REF_LIVE) || ((st & REF_DETACHED) && !(transient && (st & REF_OFF)))) continue;
-    int64_t p = 0;
-    for (uint32_t i = 0; i < d->n; i++) {
-      const item* g = &d->it[i];
-      if (!g->empty && u - g->toff < (uint32_t)g->len) {
-        pos[r] = (int32_t)(p + (g->rseq != NONE_SEQ ? 0 : (int64_t)(u - g->toff)));
-        break;
-      }
-      p += g->empty ? 0 : own_len(g);
-    }
-  }
+  for (uint32_t r = 0; r < n; r++) pos[r] = ref_position(d, r, transient);
   return MTE_OK;
 }
 

@@ -70,7 +70,11 @@ const recorder = {
   readRefOrder(ctx, doc, n) { return new Int32Array(n); },
 };
 
-const eng = new MergeTreeEngine(mode === "pack" ? { nKeys: 8, addon: recorder } : { nKeys: 8 });
+// MTE_NODE_ADDON=oracle: the same host over the CPU restatement (oracle/mte_shim.c, tests only)
+const oracleAddon = process.env.MTE_NODE_ADDON === "oracle"
+  ? require(path.join(__dirname, "..", "..", "oracle", "_build", "mte_napi_oracle.node")) : null;
+const eng = new MergeTreeEngine(mode === "pack" ? { nKeys: 8, addon: recorder }
+  : (oracleAddon ? { nKeys: 8, addon: oracleAddon } : { nKeys: 8 }));
 const layout = [];
 for (let si = 0; si < nSets; si++) {
   sets[si].names.forEach((name, ci) => {
@@ -86,7 +90,7 @@ for (let si = 0; si < nSets; si++) {
       L.coll.on("deleteInterval", (x, local, op) => L.ev.push(["delete", x.getIntervalId(), local, !!op, false]));
       // mt: raised inside a merge-tree op (an end sliding off a removed segment)
       L.coll.on("changeInterval", (x, prev, local, op) => L.ev.push(["change", x.getIntervalId(), local, !!op,
-        pos(prev.start), pos(prev.end), pos(x.start), pos(x.end), !!L.mt]));
+        pos(prev.start), pos(prev.end), pos(x.start), pos(x.end), !!(L.mt || L.coll.inMergeTreeOp)]));
       L.coll.on("propertyChanged", (x, deltas, local, op) => L.ev.push(["props", x.getIntervalId(), local, !!op,
         sortKeys(clone(deltas)), false]));
     }
@@ -94,6 +98,7 @@ for (let si = 0; si < nSets; si++) {
     // events on stderr, with the reference's events at each checkpoint
     if (process.env.MTE_FARM_TRACE === `${si},${ci}`) {
       L.trace = true;
+      L.client.traceEnd = true;
       L.client.onSlideRecords = (sl) => process.stderr.write("  slides " + JSON.stringify(sl) + "\n");
     }
     layout.push(L);
@@ -262,8 +267,10 @@ for (let j = 0; j < nCp; j++) {
       for (const q of got.queries.keys()) {
         const gq = got.queries[q], wq = want.queries[q];
         prevNext.n += 2;
-        prevNext.equal += (JSON.stringify(gq[3]) === JSON.stringify(wq[3]) ? 1 : 0) +
+        const eq = (JSON.stringify(gq[3]) === JSON.stringify(wq[3]) ? 1 : 0) +
           (JSON.stringify(gq[4]) === JSON.stringify(wq[4]) ? 1 : 0);
+        prevNext.equal += eq;
+        if (eq < 2 && !prevNext.first) prevNext.first = [L.si, L.ci, j, q, gq.slice(0, 5), wq.slice(0, 5)];
       }
       let offOrder = false;
       for (const k of ["events", "order", "summary", "queries"]) {
@@ -346,7 +353,9 @@ if (ext) {
   }
 }
 if (mode !== "pack") {
+  const endRebuilds = layout.reduce((a, L) => a + (L.coll.endRebuilds || 0), 0);
   process.stdout.write(JSON.stringify({ passed, opsChecked, loaded, unloadable, extFail, extFirst, prevNext, mtEvents, regens, orderOff,
+    endRebuilds,
     failures: failures.slice(0, 16),
     nFailures: failures.length, docs: layout.length }) + "\n");
 } else {
