@@ -5,9 +5,10 @@ One step = replay of one batch (every doc x every op of the workload) from the
 documents' initial state: mte_reset + mte_run (device-resident inputs: ops,
 text and property tables are uploaded to HBM before the timed region).
 
-N GPUs: one process per GPU (launched by torch.distributed.run, which only
-sets RANK / WORLD_SIZE; nothing here imports torch), documents sharded with no
-data-path collective.  Default "strong": the config's documents (BASELINE: 10k
+N GPUs: one process per GPU -- launched by torch.distributed.run, which only
+sets RANK / WORLD_SIZE (nothing here imports torch), or, run directly with
+--gpus N, by bench.py itself (fluidframework_amd/launch.py) -- documents
+sharded with no data-path collective.  Default "strong": the config's documents (BASELINE: 10k
 per node) assigned to ranks by expected work, longest first onto the least
 loaded rank (fluidframework_amd/dist.py, the Node host's shardByWork rule; doc
 seeds are global doc indices); at N > 1 a "weak" side line replays the
@@ -243,9 +244,18 @@ def main():
                     help="keep the per-op counters on in the timed runs (default: off)")
     args = ap.parse_args()
 
+    # run directly with --gpus N > 1: start the N ranks here (one process per
+    # GPU, the rank variables torch.distributed.run would set), before this
+    # process touches a GPU; the children run this same main()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        from fluidframework_amd import launch
+        raise SystemExit(launch.run_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
+
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"WORLD_SIZE {world} != --gpus {args.gpus}")
 
     from fluidframework_amd import dist as fdist
     from fluidframework_amd import gen

@@ -3,101 +3,38 @@ shards from the product's work-balanced assignment (fluidframework_amd/dist.py
 shard_by_work, the Node host's shardByWork rule), generate and replay their
 documents, and gather the per-doc digests in the layout
 mte_comm_gather_digests produces (rank-major, each rank padded with zero rows
-to docs_per_rank).  The collective is a file-backed stand-in (no RCCL on CPU,
-and RCCL cannot put two ranks on one GPU); the replay is the device engine on
+to docs_per_rank).  The ranks start through the launcher bench.py --gpus N uses
+(fluidframework_amd/launch.py; tests/dist_rank.py is one rank).  The collective
+is a file-backed stand-in (no RCCL on CPU, and RCCL cannot put two ranks on one
+GPU); the replay is the device engine on
 a GPU box (the -m gpu variant) and the CPU restatement elsewhere.  The
 gathered digests, put back in global order by dist.unshard_digests, must equal
 one process replaying every document."""
-import multiprocessing as mp
 import os
-import time
+import subprocess
+import sys
 
 import numpy as np
 import pytest
 
 from fluidframework_amd import dist as fdist
 from fluidframework_amd import gen
+from fluidframework_amd import launch
 
-N_DOCS = 37  # not a multiple of the world: ragged shards, padded rows
-OPS = 300
+from dist_rank import N_DOCS, OPS, _work  # noqa: E402  (the rank's code)
 
-
-def _work():
-    # unequal expected work (ops x live segments) so LPT is not round-robin
-    return np.array([OPS * (1 + (7 * d) % 5) for d in range(N_DOCS)], np.float64)
-
-
-class FileComm:
-    """Stand-in for mte_comm_{barrier, allreduce_f64, gather_digests} over files."""
-
-    def __init__(self, root, rank, world):
-        self.root, self.rank, self.world = root, rank, world
-        self.k = 0
-
-    def _exchange(self, payload: np.ndarray):
-        self.k += 1
-        tmp = os.path.join(self.root, f"{self.k}.{self.rank}.tmp")
-        np.save(tmp, payload)
-        os.replace(tmp + ".npy", os.path.join(self.root, f"{self.k}.{self.rank}.npy"))
-        parts = []
-        for r in range(self.world):
-            path = os.path.join(self.root, f"{self.k}.{r}.npy")
-            t0 = time.time()
-            while not os.path.exists(path):
-                if time.time() - t0 > 60:
-                    raise TimeoutError(path)
-                time.sleep(0.01)
-            parts.append(np.load(path))
-        return parts
-
-    def barrier(self):
-        self._exchange(np.zeros(1))
-
-    def allreduce(self, v, op):
-        parts = self._exchange(np.array([float(v)]))
-        return float(sum(p[0] for p in parts) if op == "sum" else max(p[0] for p in parts))
-
-    def gather_digests(self, digest, docs_per_rank):
-        mine = np.zeros((docs_per_rank, 4), np.uint64)
-        mine[:len(digest)] = digest
-        return np.stack(self._exchange(mine))  # (world, docs_per_rank, 4), rank order
-
-
-def _engine(use_gpu, n_keys):
-    if use_gpu:
-        from fluidframework_amd.engine import DeviceEngine
-        return DeviceEngine(n_keys)
-    from oracle import OracleEngine
-    return OracleEngine(n_keys, threads=2)
-
-
-def _rank(rank, world, root, use_gpu):
-    comm = FileComm(root, rank, world)
-    rank_of = fdist.shard_by_work(_work(), world)
-    ids = fdist.rank_docs(rank_of, rank)
-    s = gen.generate(3, ops_per_doc=OPS, doc_ids=ids, n_threads=2, round_sync=True)
-    e = _engine(use_gpu, s["n_keys"])
-    gen.load_stream(e, s)
-    e.apply_batch(s["batch"])
-    assert (e.statuses() == 0).all()
-    comm.barrier()
-    g = comm.gather_digests(e.digest(), fdist.docs_per_rank(rank_of, world))
-    total = comm.allreduce(int(s["batch"]["op_offsets"][-1]), "sum")
-    t = comm.allreduce(rank + 1.0, "max")
-    if rank == 0:
-        np.save(os.path.join(root, "gathered.npy"), g)
-        with open(os.path.join(root, "meta"), "w") as fh:
-            fh.write(f"{total} {t}")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _run(tmp_path, use_gpu):
-    ctx = mp.get_context("spawn")
-    ps = [ctx.Process(target=_rank, args=(r, 2, str(tmp_path), use_gpu)) for r in range(2)]
-    for p in ps:
-        p.start()
-    for p in ps:
-        p.join(timeout=300)
-        assert p.exitcode == 0
+    # two ranks through the launcher bench.py --gpus N uses (RANK / WORLD_SIZE /
+    # MASTER_* as torch.distributed.run sets them); two ranks may share the one
+    # GPU here (no RCCL), so the device-count check is off
+    out = []
+    rc = launch.run_ranks(2, [sys.executable, os.path.join(ROOT, "tests", "dist_rank.py"), str(tmp_path),
+                              "1" if use_gpu else "0"], need_devices=False, timeout=300, out=out)
+    assert rc == 0
+    assert out[0].startswith("rank 0 of 2 done, rendezvous 127.0.0.1:"), out
     g = np.load(tmp_path / "gathered.npy")
     total, t = open(tmp_path / "meta").read().split()
     rank_of = fdist.shard_by_work(_work(), 2)
@@ -144,3 +81,25 @@ def test_two_ranks_shard_replay_and_gather(tmp_path):
 @pytest.mark.gpu
 def test_gpu_two_ranks_shard_replay_and_gather(tmp_path):
     _run(tmp_path, use_gpu=True)
+
+
+def test_bench_gpus_n_launches_its_ranks_or_refuses():
+    """bench.py --gpus N run directly starts N ranks itself (launch.run_ranks);
+    with fewer than N visible GPUs it exits non-zero before any GPU work -- here,
+    on a CPU container, at once -- rather than replaying on one GPU."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
+                       text=True, timeout=300, env={k: v for k, v in os.environ.items() if k != "WORLD_SIZE"})
+    if launch.visible_devices() >= 2:
+        pytest.skip("a multi-GPU host: the launch itself is the bench")
+    assert r.returncode == 2 and "2 ranks need 2 GPUs" in r.stderr, (r.returncode, r.stderr[-500:])
+    # launched with a world that is not --gpus: refused too
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
+                       text=True, timeout=300, env=dict(os.environ, WORLD_SIZE="1", RANK="0"))
+    assert r.returncode != 0 and "WORLD_SIZE 1 != --gpus 2" in r.stderr, r.stderr[-500:]
+
+
+def test_launcher_stops_the_job_when_a_rank_fails():
+    code = "import os, sys, time; r = int(os.environ['RANK']); time.sleep(0 if r == 1 else 60); sys.exit(3 if r == 1 else 0)"
+    t0 = __import__("time").time()
+    rc = launch.run_ranks(3, [sys.executable, "-c", code], need_devices=False, timeout=120, out=[])
+    assert rc == 3 and __import__("time").time() - t0 < 60
