@@ -684,7 +684,6 @@ struct mte_ctx {
   const char* hprof_path = nullptr;
   unsigned long long* d_hprof = nullptr;
   uint32_t* h_rcount = nullptr;  // pinned: the plan's counts
-  uint64_t rl_alloc = 0;         // rd.rlist entries allocated
   // The round phases' host loop (launch_replay) reads each phase's counts back
   // before launching the next, so it cannot be enqueued ahead: mte_run starts
   // it on this thread and returns (include/mte.h: mte_run does not wait); every
@@ -785,12 +784,11 @@ void free_image(mte_ctx* c) {
 void free_docs(mte_ctx* c) {
   free_image(c);
   void* cs[] = {c->ch.arena, c->ch.cnt, c->ch.kc, c->ch.sum, c->rd.plan, c->rd.acct, c->rd.rcnt, c->rd.rbuf, c->rd.rflag,
-                c->rd.nch, c->rd.nnew, c->rd.count, c->rd.rlist, c->rd.rchain, c->rd.live, c->rd.gfl, c->rd.rrec};
+                c->rd.nch, c->rd.nnew, c->rd.count, c->rd.rchain, c->rd.live, c->rd.gfl, c->rd.rrec};
   for (void* p : cs)
     if (p) (void)hipFree(p);
   c->ch = ChunkArgs{};
   c->rd = RoundArgs{};
-  c->rl_alloc = 0;
   c->chunked = false;
   if (c->d_wclock) (void)hipFree(c->d_wclock);
   c->d_wclock = nullptr;
@@ -851,20 +849,8 @@ int launch_reset(mte_ctx* c) {
 // thread (mte_ctx::tail): per phase the plan's counts come back to the host,
 // which stops when no document is left or launches the phase's runs.
 template <int K>
-int round_phase_loop(mte_ctx* c, const ReplayArgs& a, size_t lds, uint64_t max_ops) {
+int round_phase_loop(mte_ctx* c, const ReplayArgs& a, size_t lds) {
   HIPCHK(c, hipSetDevice(c->device));
-  // the client chains' sub-op lists: 2 x ops + 8 per client, per document
-  const uint64_t rl_cap = 2 * max_ops + 8 * MTE_MAX_CLIENTS;
-  if (rl_cap * c->n_docs > c->rl_alloc) {
-    if (c->rd.rlist) {
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      HIPCHK(c, hipFree(c->rd.rlist));
-    }
-    c->rd.rlist = nullptr;
-    HIPCHK(c, hipMalloc((void**)&c->rd.rlist, sizeof(uint4) * rl_cap * c->n_docs));
-    c->rl_alloc = rl_cap * c->n_docs;
-  }
-  c->rd.rl_cap = rl_cap;
   ChunkArgs ch = c->ch;
   RoundArgs rd = c->rd;
   ch.plan = rd.plan;
@@ -979,8 +965,7 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
       // document's next run, replays the round-shaped runs chunk-parallel and
       // the rest op after op; the host reads the plan's counts to stop.  The
       // loop runs on the context's tail thread (mte_run returns at once).
-      const uint64_t max_ops = c->max_doc_ops_s[c->rslot];
-      c->tail_fn = [c, a, lds, max_ops]() -> int { return round_phase_loop<K>(c, a, lds, max_ops); };
+      c->tail_fn = [c, a, lds]() -> int { return round_phase_loop<K>(c, a, lds); };
       return MTE_OK;  // the tail joins the tree stream after the loop
     } else {
       HIPCHK(c, (launch_chunk<K, S>(a, c->ch, c->n_docs, lds, c->stream)));

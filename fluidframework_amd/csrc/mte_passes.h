@@ -33,8 +33,6 @@ struct RoundArgs {
   uint32_t* nch;    // [doc] chunks after the re-layout
   uint32_t* nnew;   // [doc] segments after the re-layout
   uint32_t* count;  // [0] round docs, [1] op-after-op docs, [2] active docs
-  uint4* rlist;     // [doc][rl_cap] (unused since the resolve buckets its sub-ops itself; rl_cap sizes the chains)
-  uint64_t rl_cap;  // list entries per document: 2 x its ops + 8 per client
   uint2* rchain;    // [doc][MTE_MAX_CLIENTS] (list offset, entries) of each client chain
   // [doc] where the document's segments are: 0 the flat planes; 1 the chunk
   // arena, carried from the previous run (the flat planes are stale); 2 the

@@ -39,8 +39,9 @@ PRESETS = {
             mix=MIX_INSERT | MIX_REMOVE | MIX_ANNOTATE, marker_every=16, length_mode=0),
     4: dict(n_docs=100000, ops_per_doc=500, clients=8, min_length=8, round_ops=8,
             mix=MIX_INSERT | MIX_REMOVE | MIX_ANNOTATE, marker_every=16, length_mode=0),
-    # config 5 runs the new length calculation: its documents are far beyond
-    # the tree pass that legacy documents need (<= 1,020 items)
+    # config 5 runs the new length calculation: legacy documents take the
+    # reference's B+tree placement on the tree passes, which the
+    # chunked pass and its round phases do not restate
     5: dict(n_docs=64, ops_per_doc=262144, clients=8, min_length=16, round_ops=65536,
             mix=MIX_INSERT | MIX_REMOVE | MIX_ANNOTATE, marker_every=16, length_mode=2,
             init_segs=1 << 20, max_range=16),
@@ -123,6 +124,12 @@ def generate(config_id=2, n_docs=None, ops_per_doc=None, doc_base=0, n_threads=N
 def split_ops(stream, k, parts):
     """Batch k of `parts`: every document's ops [k/parts, (k+1)/parts) of its
     count, cut at message ends (MTE_F_MSG_END) so windows stay whole."""
+    return cut_ops(stream, k / parts, (k + 1) / parts)
+
+
+def cut_ops(stream, f0, f1):
+    """Every document's ops [f0, f1) of its count (fractions), cut at message
+    ends (MTE_F_MSG_END) so windows stay whole; the batch keeps all the text."""
     b = stream["batch"]
     o = b["op_offsets"].astype(np.int64)
     ops = b["ops"]
@@ -137,7 +144,7 @@ def split_ops(stream, k, parts):
                 return int(n)
             i = np.searchsorted(ends, x)
             return int(ends[i]) if i < len(ends) else int(n)
-        a, e = cut(n * k // parts), cut(n * (k + 1) // parts)
+        a, e = cut(int(round(n * f0))), cut(int(round(n * f1)))
         sel.append(np.arange(o[d] + a, o[d] + e))
         offs.append(offs[-1] + (e - a))
     idx = np.concatenate(sel) if sel else np.zeros(0, np.int64)

@@ -57,6 +57,7 @@ const DOC_REFS = 0x10;       // MTE_DOC_REFS
 const DOC_EVENTS = 0x8; // MTE_DOC_EVENTS
 const DOC_SLIDE_EVENTS = 0x20;  // MTE_DOC_SLIDE_EVENTS: the references' slides and their snapshots
 const E_INVALID_ARG = -1, E_CAPACITY = -4, E_UNSUPPORTED = -9, E_STATE = -10, E_CLIENT_RANGE = -12;
+const COMBINE_DOMAIN_MAX = 4096;  // distinct values of one key a combining op's value map may cover
 const DEFAULT_REF_CAPACITY = 1024;  // mte_set_ref_capacity's default (include/mte.h)
 
 class MergeTreeError extends Error {
@@ -91,8 +92,10 @@ class Interner {
     this.valueJson = [null];
     this.numIds = new Map();
     this.strIds = new Map();
-    // per value index, the keys it was ever given (bit k): the combining ops' domain
+    // per value index, the keys it was ever given (bit k), and per key how
+    // many: the combining ops' domain (packing.py Interner.note_value)
     this.keyMask = new Uint32Array(256);
+    this.keyCount = new Uint32Array(Math.max(1, nKeys));
   }
   /** [key, value id] of one property, noting the value under its key */
   kv(name, v) {
@@ -108,10 +111,18 @@ class Interner {
       m.set(this.keyMask);
       this.keyMask = m;
     }
-    this.keyMask[x] |= 1 << k;
+    if (!(this.keyMask[x] & (1 << k))) {
+      this.keyMask[x] |= 1 << k;
+      this.keyCount[k]++;
+    }
   }
-  /** the value ids key k was ever given, ascending */
+  /** the value ids key k was ever given, ascending; a key given more than
+   *  COMBINE_DOMAIN_MAX values is refused (its combining value map) */
   domainOf(k) {
+    if (this.keyCount[k] > COMBINE_DOMAIN_MAX) {
+      throw new MergeTreeError(E_UNSUPPORTED, "combiningOp over key " + this.keyNames[k] + ", given " +
+        this.keyCount[k] + " distinct values (> " + COMBINE_DOMAIN_MAX + ")");
+    }
     const out = [], b = 1 << k, M = this.keyMask;
     for (let x = 1; x < this.valueJson.length && x < M.length; x++) {
       if (M[x] & b) out.push((x | (this.valueJson[x] === "NaN" ? VALUE_UNEQUAL : 0)) >>> 0);

@@ -56,6 +56,9 @@ def units_to_str(u) -> str:
     return np.asarray(u, dtype="<u2").tobytes().decode("utf-16-le", errors="surrogatepass")
 
 
+COMBINE_DOMAIN_MAX = 4096  # distinct values of one key a combining op's value map may cover
+
+
 class Interner:
     """Key -> plane index, canonical JSON value -> id (0 is reserved for null)."""
 
@@ -65,13 +68,36 @@ class Interner:
         self.key_names = []
         self.values = {}
         self.value_json = [None]
-        self.key_vals = {}  # key -> the value ids it was ever given (combining ops' domain)
+        # per value id, the keys it was ever given (bit k), and per key how many:
+        # the combining ops' domain, one byte per value (n_keys <= 8) as the Node
+        # packer keeps it; a combining op over a key given more than
+        # COMBINE_DOMAIN_MAX values is refused (its value map would be that long)
+        self.key_mask = bytearray(256)
+        self.key_count = [0] * max(1, n_keys)
+
+    def note_value(self, k: int, vid: int):
+        """value id `vid` was given to key `k`."""
+        x = vid & ~MTE_VALUE_UNEQUAL
+        if x >= len(self.key_mask):
+            self.key_mask.extend(bytes(max(x + 1, 2 * len(self.key_mask)) - len(self.key_mask)))
+        if not self.key_mask[x] & (1 << k):
+            self.key_mask[x] |= 1 << k
+            self.key_count[k] += 1
+
+    def domain_of(self, k: int):
+        """The value ids key k was ever given, ascending (NaN's with its flag)."""
+        if self.key_count[k] > COMBINE_DOMAIN_MAX:
+            raise MergeTreeError(MTE_E_UNSUPPORTED, f"combiningOp over key {self.key_names[k]!r}, given "
+                                 f"{self.key_count[k]} distinct values (> {COMBINE_DOMAIN_MAX})")
+        b = 1 << k
+        return [x | (MTE_VALUE_UNEQUAL if self.value_json[x] == "NaN" else 0)
+                for x in range(1, min(len(self.value_json), len(self.key_mask))) if self.key_mask[x] & b]
 
     def kv(self, name: str, v):
         """(key, value id) of one property, noting the value under its key."""
         k, vid = self.key(name), self.value(v)
         if vid:
-            self.key_vals.setdefault(k, set()).add(vid)
+            self.note_value(k, vid)
         return k, vid
 
     def key(self, name: str) -> int:
@@ -141,7 +167,7 @@ class PropTable:
         first = len(self.entries)
         for name in props:
             k = it.key(name)
-            dom = sorted(it.key_vals.get(k, ())) + [0]
+            dom = sorted(it.domain_of(k)) + [0]
             pairs = []
             for old in dom:
                 cur = _ABSENT if old == 0 else json.loads(it.json_of(old))
@@ -151,7 +177,7 @@ class PropTable:
                     pairs.append((old | COMBINE_PAIR, nid))
             for _, nid in pairs:
                 if nid:
-                    it.key_vals.setdefault(k, set()).add(nid)
+                    it.note_value(k, nid)
             self.entries.append((k, len(pairs)))
             self.entries.extend(pairs)
         self.sets.append((first, len(self.entries) - first))

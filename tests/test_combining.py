@@ -237,3 +237,23 @@ def test_js_number_strings_match_node():
     out = subprocess.run([node, "-e", "process.stdout.write(JSON.stringify(%s.map(String)))" % json.dumps(xs)],
                          capture_output=True, text=True, check=True).stdout
     assert [_js_num(x) for x in xs] == json.loads(out)
+
+
+def test_combining_domain_is_bounded():
+    """The packers keep, per key, the values it was ever given (one byte per
+    value id) and refuse a combining op whose value map would cover more than
+    COMBINE_DOMAIN_MAX of them (MTE_E_UNSUPPORTED), instead of growing it."""
+    from fluidframework_amd.packing import COMBINE_DOMAIN_MAX, PropTable
+    it = Interner(4)
+    for v in range(COMBINE_DOMAIN_MAX):
+        it.kv("n", v)
+    it.kv("m", 1)
+    t = PropTable(it)
+    t.add_combining({"n": 1}, {"name": "incr"}, 5)  # at the bound: one map
+    for v in range(COMBINE_DOMAIN_MAX, COMBINE_DOMAIN_MAX + 2):
+        it.kv("n", v)
+    with pytest.raises(MergeTreeError) as e:
+        t.add_combining({"n": 1}, {"name": "incr"}, 6)
+    assert e.value.code == MTE_E_UNSUPPORTED
+    t.add_combining({"m": 1}, {"name": "incr"}, 7)  # other keys unaffected
+    assert len(it.key_mask) < 2 * (COMBINE_DOMAIN_MAX + 2 + 256)

@@ -366,3 +366,37 @@ def test_gpu_config5_full_size_equals_chunked_restatement():
     for doc in (0, 31, 63):
         assert d.read_doc(doc) == o.read_doc(doc)
     d.close()
+
+
+@pytest.mark.gpu
+def test_gpu_buffers_grow_while_the_round_phases_run():
+    """ADVICE r04 (grow / tail race): each next batch needs bigger record and
+    text buffers (mte_submit grows them) while the previous batch's round
+    phases are still running on the context's tail thread and the tree
+    stream; submitted back to back without a sync, the batches must leave the
+    documents as one batch at a time with a sync between them does, and as
+    the chunked restatement does."""
+    s = gen.generate(5, n_docs=8, ops_per_doc=8000, init_segs=20000, round_ops=2000)
+    cap = gen.seg_capacity(5, s["params"])
+    cuts = [0.0, 0.03, 0.15, 1.0]  # growing batches: every submit regrows
+    parts = [gen.cut_ops(s, cuts[i], cuts[i + 1]) for i in range(len(cuts) - 1)]
+    assert all(len(parts[i + 1]["ops"]) > 2 * len(parts[i]["ops"]) for i in range(len(parts) - 1))
+    seq = DeviceEngine(s["n_keys"], seg_capacity=cap)
+    gen.load_stream(seq, s)
+    for p in parts:
+        seq.submit(p)
+        seq.run()
+        seq.sync()
+    pipe = DeviceEngine(s["n_keys"], seg_capacity=cap)
+    gen.load_stream(pipe, s)
+    for p in parts:
+        pipe.submit(p)  # grows while the previous run's tail is in flight
+        pipe.run()
+    pipe.sync()
+    np.testing.assert_array_equal(pipe.statuses(), seq.statuses())
+    assert (pipe.statuses() == 0).all()
+    np.testing.assert_array_equal(pipe.digest(), seq.digest())
+    o = OracleEngine(s["n_keys"], threads=8, tree="chunked")
+    gen.load_stream(o, s)
+    o.apply_batch(s["batch"])
+    np.testing.assert_array_equal(pipe.digest(), o.digest())

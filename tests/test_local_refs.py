@@ -30,6 +30,7 @@ import gzip
 import json
 import os
 
+import numpy as np
 import pytest
 
 from fixtures_util import doc_inits, replay_ref_farm
@@ -282,3 +283,67 @@ def test_gpu_engine_ref_capacity_reaches_the_packer():
     e = DeviceEngine(0)
     e.set_ref_capacity(7)
     assert e.doc_clients("B", local=True).ref_cap == 7
+
+
+def _slide_events(factory, slide_events, per_op=None):
+    """A remote group op whose first member removes 'c' under 300 SlideOnRemove
+    references (they slide to 'd') and whose second removes 'e' under 2 (to
+    'f'), in an MTE_DOC_REFS | MTE_DOC_EVENTS document with or without
+    MTE_DOC_SLIDE_EVENTS (slide records are opt-in, so a host that
+    does not read them keeps the old event capacity)."""
+    from fluidframework_amd.abi import DOC_EVENTS, DOC_SLIDE_EVENTS
+    flags = DOC_NEW_LENGTH_CALC | DOC_LOCAL_CLIENT | DOC_REFS | DOC_EVENTS | (DOC_SLIDE_EVENTS if slide_events else 0)
+    inits, text = doc_inits(["abcdefgh"], flags=flags)
+    e = factory(4)
+    if per_op is not None:
+        e.set_event_capacity(per_op)
+    e.load_docs(inits, text)
+    cl = DocClients("B", local=True)
+    bb = BatchBuilder(1, Interner(4))
+    for _ in range(300):
+        bb.add_ref(0, cl, 2, REF_SLIDE_ON_REMOVE)
+    bb.add_ref(0, cl, 4, REF_SLIDE_ON_REMOVE)
+    bb.add_ref(0, cl, 4, REF_SLIDE_ON_REMOVE)
+    bb.add_message(0, cl, {"clientId": "C", "sequenceNumber": 1, "referenceSequenceNumber": 0,
+                           "minimumSequenceNumber": 0, "type": "op",
+                           "contents": {"type": 3, "ops": [{"type": 1, "pos1": 2, "pos2": 3},
+                                                           {"type": 1, "pos1": 3, "pos2": 4}]}})
+    e.apply_batch(bb.build())
+    return e
+
+
+def test_tree_oracle_slide_records_are_opt_in():
+    from fluidframework_amd.abi import DELTA_REFPOS, DELTA_SLIDE
+    e = _slide_events(tree_factory, False)
+    assert (e.statuses() == 0).all()
+    d = e.read_deltas(0)
+    assert len(d) == 2 and set(d["kind"] & 0xff) == {1}  # the two removes' ranges only
+    e = _slide_events(tree_factory, True)
+    d = e.read_deltas(0)
+    k = d["kind"] & 0xff
+    assert (k == 1).sum() == 2
+    slides, snaps = d[(k & 0xc0) == DELTA_SLIDE], d[k == DELTA_REFPOS]
+    assert len(slides) == 302 and len(snaps) == 2 * 302  # one snapshot per record that slid
+    # the snapshot after the first member: the 300 references on 'd' at 2
+    # ("abdefgh"), the 2 on 'e' at 3; after the second: on 'd' at 2, on 'f' at 3
+    first, second = snaps[snaps["op"] == snaps["op"].min()], snaps[snaps["op"] == snaps["op"].max()]
+    assert (first["pos"][:300] == 2).all() and (first["pos"][300:] == 3).all()
+    assert (second["pos"][:300] == 2).all() and (second["pos"][300:] == 3).all()
+    assert list(e.read_refs(0, 302)) == [2] * 300 + [3, 3]
+    # order keys: 'd' is held unit 3 ("abcdefgh" with 'c' still held), 'f' unit 5
+    assert (first["len"][:300] == 3).all() and (second["len"][300:] == 5).all()
+
+
+@pytest.mark.gpu
+def test_gpu_slide_records_opt_in_and_capacity():
+    from fluidframework_amd.abi import DELTA_REFPOS
+    e = _slide_events(device_factory, False, per_op=1)
+    assert (e.statuses() == 0).all() and len(e.read_deltas(0)) == 2  # fits: slides not recorded
+    e = _slide_events(device_factory, True, per_op=1)
+    with pytest.raises(MergeTreeError) as ei:  # 908 records > 1 x 304 + 256
+        e.read_deltas(0)
+    assert ei.value.code == MTE_E_CAPACITY
+    e = _slide_events(device_factory, True, per_op=8)
+    t = _slide_events(tree_factory, True)
+    np.testing.assert_array_equal(e.read_deltas(0), t.read_deltas(0))  # record for record
+    assert (e.read_deltas(0)["kind"] & 0xff == DELTA_REFPOS).sum() == 604
