@@ -51,6 +51,7 @@ DELTA_REGEN = 0x10    # kind flag of its output records
 DELTA_REBASE = 0x20   # MTE_OP_REF b = 4 / 5: the answer's kind
 DELTA_SLIDE = 0x40    # a reference slid off a removed segment (MTE_DOC_SLIDE_EVENTS)
 DELTA_REFPOS = 0x80   # every reference as the record that slid one left the document
+DELTA_MAINT = 0x100   # | MTE_MAINT_*: a maintenance callback's segment (MTE_DOC_MAINT_EVENTS)
 ANNOTATE_SLOTS = 32   # pending local annotate groups tracked per document
 F_MARKER, F_MSG_END, F_REWRITE, F_LOCAL = 0x1, 0x2, 0x4, 0x8
 F_COMBINE = 0x10         # annotate combiningOp incr / consensus (value maps, include/mte.h)
@@ -135,6 +136,7 @@ EXPORTED_SYMBOLS = [
 DOC_EVENTS = 0x8
 DOC_REFS = 0x10
 DOC_SLIDE_EVENTS = 0x20
+DOC_MAINT_EVENTS = 0x40
 DELTA_DTYPE = np.dtype([("op", "<u4"), ("kind", "<u4"), ("pos", "<i4"), ("len", "<i4"), ("removed", "<u4")])
 
 

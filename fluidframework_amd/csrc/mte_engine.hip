@@ -645,6 +645,8 @@ struct mte_ctx {
   // local references of the MTE_DOC_REFS documents (mte_stream.h): ref_cap slots
   // per document, zeroed at every reset
   std::vector<uint8_t> h_refs;      // per doc: MTE_DOC_REFS
+  std::vector<uint8_t> h_slides;    // per doc: MTE_DOC_SLIDE_EVENTS (with REFS and EVENTS)
+  std::vector<uint32_t> h_ref_hi;   // per doc: reference slots its MTE_OP_REF records used so far (+1)
   uint32_t ref_cap = 1024;
   uint2* d_refs = nullptr;
   uint32_t* d_rs_docs = nullptr;    // legacy documents declared MTE_DOC_ROUND_SYNC (flat)
@@ -834,6 +836,7 @@ int launch_reset(mte_ctx* c) {
   HIPCHK(c, hipGetLastError());
   if (c->d_refs)
     HIPCHK(c, hipMemsetAsync(c->d_refs, 0, sizeof(uint2) * (size_t)c->ref_cap * c->n_docs, c->stream));
+  std::fill(c->h_ref_hi.begin(), c->h_ref_hi.end(), 0u);  // the references are gone
   if (c->n_img) {
     const uint64_t nb = std::min<uint64_t>((c->n_img + 255) / 256, 65536);
     hipLaunchKernelGGL(image_kernel, dim3((uint32_t)nb), dim3(256), 0, c->stream, c->soa, c->cap,
@@ -1291,6 +1294,8 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
   c->h_local.assign(n_docs, 0);
   c->h_events.assign(n_docs, 0);
   c->h_refs.assign(n_docs, 0);
+  c->h_slides.assign(n_docs, 0);
+  c->h_ref_hi.assign(n_docs, 0);
   bool any_local = false, any_refs = false;
   c->h_sdocs.clear();
   for (uint32_t d = 0; d < n_docs; d++) {
@@ -1301,6 +1306,8 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     if (docs[d].flags & MTE_DOC_LOCAL_CLIENT) c->h_local[d] = 1, any_local = true;
     if (docs[d].flags & MTE_DOC_EVENTS) c->h_events[d] = 1;
     if (docs[d].flags & MTE_DOC_REFS) c->h_refs[d] = 1, any_refs = true;
+    const uint32_t sl = MTE_DOC_REFS | MTE_DOC_EVENTS | MTE_DOC_SLIDE_EVENTS;
+    if ((docs[d].flags & sl) == sl) c->h_slides[d] = 1;
   }
   if (any_refs) HIPCHK(c, hipMalloc((void**)&c->d_refs, sizeof(uint2) * (size_t)c->ref_cap * n_docs));
   // documents with a local client hold 2 kt + 3 more planes (mte_htree.h): the
@@ -1640,7 +1647,10 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
                              c->up_stream));
   }
   HIPCHK(c, hipStreamSynchronize(c->up_stream));  // host buffers may be freed after return
-  // delta event regions of the MTE_DOC_EVENTS docs (per_op x records + 256 each)
+  // delta event regions of the MTE_DOC_EVENTS docs (per_op x records + 256
+  // each); a document with slide events also gets 2 x its reference slots in
+  // use for each record that can slide references (a remote remove, an ack):
+  // its slides and the MTE_DELTA_REFPOS snapshot after them
   {
     std::vector<uint64_t>& off = c->h_dl_off_s[w];
     off.assign((size_t)b->n_docs + 1, 0);
@@ -1648,7 +1658,19 @@ int mte_submit(mte_ctx* c, const mte_batch* b) {
     for (uint32_t d = 0; d < b->n_docs; d++) {
       const bool e = d < c->h_events.size() && c->h_events[d];
       any = any || e;
-      off[d + 1] = off[d] + (e ? (uint64_t)c->ev_per_op * (b->op_offsets[d + 1] - b->op_offsets[d]) + 256 : 0);
+      uint64_t extra = 0;
+      if (e && d < c->h_slides.size() && c->h_slides[d]) {
+        uint32_t hi = c->h_ref_hi[d];
+        uint64_t sliding = 0;
+        for (uint64_t i = b->op_offsets[d]; i < b->op_offsets[d + 1]; i++) {
+          const mte_op& o = b->ops[i];
+          if (o.type == MTE_OP_REF && (uint32_t)o.pos2 + 1 > hi) hi = (uint32_t)o.pos2 + 1;
+          if ((o.type == MTE_OP_REMOVE && !(o.flags & MTE_F_LOCAL)) || o.type == MTE_OP_ACK) sliding++;
+        }
+        c->h_ref_hi[d] = hi;
+        extra = sliding * 2 * (uint64_t)hi;
+      }
+      off[d + 1] = off[d] + (e ? (uint64_t)c->ev_per_op * (b->op_offsets[d + 1] - b->op_offsets[d]) + 256 + extra : 0);
     }
     if (any) {
       if ((rc = grow(c, &c->d_dl_off_s[w], &c->dl_off_cap_s[w], (uint64_t)b->n_docs + 1))) return rc;

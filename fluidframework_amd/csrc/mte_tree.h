@@ -968,8 +968,11 @@ __device__ __forceinline__ void tree_burst(DocRun& D, TreeRun& tr, const ReplayA
 // TIER 0 launch, so a passing peak does not keep it at low occupancy for the
 // rest of the batch.  The host alternates TIER 0 / TIER 1 a few rounds (the
 // last TIER 1 keeps its documents), then runs TIER 2 (kHdrTreeBig) once.
+#ifndef MTE_TREE0_WAVES  // TIER 0's register budget in waves per SIMD (4: 128 VGPRs)
+#define MTE_TREE0_WAVES 4
+#endif
 template <int K, bool S, int TIER>
-__global__ __launch_bounds__(256) void tree_kernel(ReplayArgs a, TreeArgs t) {
+__global__ __launch_bounds__(256, TIER == 0 ? MTE_TREE0_WAVES : 1) void tree_kernel(ReplayArgs a, TreeArgs t) {
   constexpr int EMAX = TIER == 2 ? 16 : TIER == 1 ? 4 : 2;
   constexpr uint32_t kTierFlags = kHdrTreeEsc | kHdrTreeBig | kHdrTreeHbmFlag;
   __shared__ uint32_t zlds_all[kDocsPerBlock][kWave * EMAX];

@@ -148,6 +148,24 @@ extern "C" {
  * client.ts applyRemoteOp), so a host that delivers them after a batch reads
  * positions and order from these, not from the document after the batch. */
 #define MTE_DELTA_REFPOS 0x80u
+/* MTE_DOC_MAINT_EVENTS documents: one record per segment of a maintenance
+ * callback, kind = MTE_DELTA_MAINT | type (MergeTreeMaintenanceType negated,
+ * mergeTreeDeltaCallback.ts:24-50): APPEND (the merged segment, then the one
+ * appended to it), SPLIT (the two pieces), UNLINK (a tombstone the zamboni
+ * unlinks), ACKNOWLEDGED (the pending group an ack sequenced); removed = the
+ * segment's index among the callback's, in document order (the order
+ * SequenceMaintenanceEvent.ranges sorts them in, sequenceDeltaEvent.ts:
+ * 27-60), so index 0 starts a callback; len = the segment's cachedLength when
+ * the callback ran; pos = its position in the document's own view once the
+ * record is applied (Client.getPosition, client.ts:345-350), -1 when it is no
+ * longer in the tree (an appended or unlinked segment).  In record order with
+ * the delta ranges: a split before the op's range, an ack's callback after its
+ * slides, the zamboni's appends and unlinks last.                            */
+#define MTE_DELTA_MAINT 0x100u
+#define MTE_MAINT_APPEND 1u
+#define MTE_MAINT_SPLIT 2u
+#define MTE_MAINT_UNLINK 3u
+#define MTE_MAINT_ACK 4u
 /* Follows an annotate's MTE_OP_ROLLBACK (a local record): for each key k the
  * rolled-back annotate set (pos1 = k), the older pending annotates that set k
  * too, latest first -- pos2 = its group slot, a = the value id it set, seq =
@@ -357,10 +375,16 @@ typedef struct mte_config {
  * (MTE_DELTA_SLIDE) and, after each record that slid one, every reference as
  * that record left the document (MTE_DELTA_REFPOS) -- what an interval
  * collection's position-change listeners read mid-op
- * (intervalCollection.ts:1042-1053).  They take event capacity
- * (mte_set_event_capacity) beside the delta ranges, so a host that does not
- * read them leaves the flag clear.                                            */
+ * (intervalCollection.ts:1042-1053).  Such a document's event region grows by
+ * 2 x the reference slots its MTE_OP_REF records have used for every remote
+ * remove and ack record of a batch (a record's slides and snapshot); a host
+ * that does not read them leaves the flag clear.                             */
 #define MTE_DOC_SLIDE_EVENTS 0x20u
+/* With MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS: also record the merge-tree's
+ * maintenance (mergeTreeMaintenanceCallback, mergeTree.ts:695-725, 1313-1320,
+ * 1687-1694; SharedString's "maintenance" event, sequence.ts:212-216) as
+ * MTE_DELTA_MAINT records.  Opt-in: they take event capacity like the ranges. */
+#define MTE_DOC_MAINT_EVENTS 0x40u
 
 /* Initial document: one text segment inserted before collaboration starts, as
  * the reference replay harness does (client.replay.spec.ts:22-23): seq 0

@@ -55,6 +55,8 @@
 //         client sees, applied through the Client's own op path
 //         (applyRemoveRangeOp / applyInsertOp, client.ts:405-500); with relpos
 //         the marker ids are unique ("mk<n>")
+//          maint: record every client's maintenance callbacks ("maint" in
+//         the output: per client [event index, type, [[position, length]...]])
 // Client 0 ("A") never sends: the observer.
 "use strict";
 const path = require("path");
@@ -135,6 +137,32 @@ function runSet(p) {
     c.startOrUpdateCollaboration(n);
     return c;
   });
+  // maint: each client's mergeTreeMaintenanceCallback (mergeTree.ts:695-725,
+  // 1313-1320, 1687-1694), per event: [event index, MergeTreeMaintenanceType,
+  // its ranges as SequenceMaintenanceEvent.ranges sorts them (segment ordinal,
+  // sortedSegmentSet.ts) as [Client.getPosition once the event is applied (-1:
+  // out of the tree), cachedLength when the callback ran]]
+  const maint = names.map(() => []);
+  const mbuf = names.map(() => []);
+  if (p.maint) {
+    clients.forEach((c, i) => {
+      c.mergeTreeMaintenanceCallback = (args) => {
+        mbuf[i].push([args.operation, args.deltaSegments.map((d) => [d.segment, d.segment.cachedLength])]);
+      };
+    });
+  }
+  // positions once the message (or local op) that raised them is applied;
+  // the segments of an ACKNOWLEDGED callback in document order (the group's
+  // order is the segments' pending order), a SPLIT's / an APPEND's in the
+  // callback's (the pieces, the segment appended to and the one appended)
+  const settle = (i, at = events[i].length - 1) => {
+    for (const [t, segs] of mbuf[i]) {
+      const r = segs.map(([sg, len]) => [sg.ordinal, clients[i].getPosition(sg), len]);
+      if (t === -4) r.sort((a, b) => (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0));
+      maint[i].push([at, t, r.map((x) => [x[1], x[2]])]);
+    }
+    mbuf[i] = [];
+  };
   const cursor = names.map(() => 0);
   const offline = names.map(() => false);
   const held = names.map(() => []);  // [op, segment group] per held op
@@ -209,6 +237,7 @@ function runSet(p) {
       type: m[4], contents: m[5],
     });
     events[i].push(["A", cursor[i]]);
+    settle(i);
     cursor[i]++;
   };
   const reconnect = (i) => {
@@ -221,6 +250,7 @@ function runSet(p) {
       seq++;
       log.push([names[i], seq, c.getCurrentSeq(), msn, "op", JSON.parse(JSON.stringify(regen))]);
       events[i].push(["G", log.length - 1]);
+      settle(i);
     }
     held[i] = [];
     offline[i] = false;
@@ -251,11 +281,13 @@ function runSet(p) {
         const { segment, offset } = c.getContainingSegment(pos);
         refs[i].push(c.createLocalReferencePosition(segment, offset, type, undefined));
         events[i].push(["F", pos, type]);
+        settle(i);
       } else if (live.length > 0) {
         const k = live[R.int(0, live.length - 1)];
         c.removeLocalReferencePosition(refs[i][k]);
         refs[i][k] = null;
         events[i].push(["X", k]);
+        settle(i);
       }
       if ((step + 1) % every === 0 && step + 1 < p.steps) checkpoint();
       continue;
@@ -304,20 +336,24 @@ function runSet(p) {
       if (op && offline[i]) {
         // made while offline: pending, not sent
         events[i].push(["H", JSON.parse(JSON.stringify(op))]);
+        settle(i);
         held[i].push([op, c.peekPendingSegmentGroups()]);
       } else if (op && p.rollback && (p.rollbackTypes ? p.rollbackTypes.includes(op.type)
         : (p.rollbackInserts ? op.type !== 2 : op.type === 1)) && R.next() < p.rollback) {
         // Client.rollback of the op just made (client.ts:396-398 ->
         // MergeTree.rollback, mergeTree.ts:2005-2083): it is never sent
         const opJson = JSON.parse(JSON.stringify(op));
+        settle(i, events[i].length);  // the local op's, before the rollback
         c.rollback(op, c.peekPendingSegmentGroups());
         events[i].push(["R", opJson]);
+        settle(i);
       } else if (op) {
         let msn = Infinity;
         for (const x of clients) msn = Math.min(msn, x.getCurrentSeq());
         seq++;
         log.push([names[i], seq, c.getCurrentSeq(), msn, "op", JSON.parse(JSON.stringify(op))]);
         events[i].push(["L", log.length - 1]);
+        settle(i);
       }
     } else {
       // a client catches up with a few sequenced messages
@@ -340,7 +376,8 @@ function runSet(p) {
       diverged = what;
     }
   }
-  return Object.assign({}, p, { names, log, events, checkpoints }, diverged ? { diverged } : {});
+  return Object.assign({}, p, { names, log, events, checkpoints }, diverged ? { diverged } : {},
+    p.maint ? { maint } : {});
 }
 
 const input = JSON.parse(fs.readFileSync(0, "utf8"));

@@ -74,6 +74,7 @@ typedef struct {
    * tail split off later (splitAt's segmentGroups.copyTo appends it,
    * mergeTreeNodes.ts:505-534) */
   uint32_t gord;
+  uint8_t member; /* doc_ack: in the group being acked */
 } item;
 
 typedef struct {
@@ -109,6 +110,9 @@ typedef struct {
   mte_delta* dl;
   uint64_t dl_n, dl_cap;
   uint32_t cur_op;
+  int ev_rc; /* an event push that failed where no status could be returned (scour) */
+  uint64_t msg_dl; /* the first event of the message being applied (maint_positions) */
+  int msg_open;    /* a message's records are being applied (its MSG_END not yet) */
 } __attribute__((aligned(128))) idoc;
 
 struct oti_ctx {
@@ -365,6 +369,10 @@ static int add_lru(idoc* d, uint32_t i, int32_t seq) {
 /* ---- scour / pack ---------------------------------------------------------------------------- */
 
 /* end (exclusive) of the logical leaf headed at i */
+static uint32_t leaf_start(const idoc* d, uint32_t i) {
+  while (i > 0 && d->it[i].cont) i--;
+  return i;
+}
 static uint32_t leaf_end(const idoc* d, uint32_t i) {
   uint32_t j = i + 1;
   while (j < d->n && d->it[j].cont) j++;
@@ -376,6 +384,8 @@ static int64_t leaf_total(const idoc* d, uint32_t a, uint32_t b) {
   for (uint32_t j = a; j < b; j++) s += d->it[j].len;
   return s;
 }
+
+static int maint_push(idoc* d, uint32_t type, int64_t id, int64_t len, uint32_t idx);
 
 /* scourNode over the leaf block [s, e] (mergeTree.ts:681-747): marks the
  * unlinked items `drop`, turns appended leaves into continuations.  Returns
@@ -403,6 +413,9 @@ static int scour(idoc* d, uint32_t s, uint32_t e, const uint16_t* arena, uint32_
         held++;
       } else {
         for (uint32_t j = i; j < xe; j++) d->it[j].drop = 1;
+        /* UNLINK (mergeTree.ts:692-703) */
+        const int rc = maint_push(d, MTE_MAINT_UNLINK, -1, xl, 0);
+        if (rc) d->ev_rc = rc;
       }
       prev = -1;
     } else if (x->seq <= d->min_seq) {
@@ -422,6 +435,10 @@ static int scour(idoc* d, uint32_t s, uint32_t e, const uint16_t* arena, uint32_
         x->id = 0;
         prev_len += xl;
         prev_end = xe;
+        /* APPEND (mergeTree.ts:715-727): the segment appended to, then this one */
+        int rc = maint_push(d, MTE_MAINT_APPEND, d->it[prev].id, prev_len, 0);
+        if (!rc) rc = maint_push(d, MTE_MAINT_APPEND, -1, xl, 1);
+        if (rc) d->ev_rc = rc;
       } else {
         held++;
         if (xl > 0) {
@@ -554,6 +571,16 @@ static void zamboni(idoc* d, const uint16_t* arena, uint32_t n_keys) {
 
 /* ---- ensureIntervalBoundary ------------------------------------------------------------------ */
 
+/* the SPLIT callback of splitLeafSegment (mergeTree.ts:1682-1694): the leaf
+ * ending before item i and the one starting there */
+static int maint_split(idoc* d, uint32_t i) {
+  if (!(d->flags & MTE_DOC_MAINT_EVENTS)) return MTE_OK;
+  const uint32_t h = leaf_start(d, i - 1);
+  int rc = maint_push(d, MTE_MAINT_SPLIT, d->it[h].id, leaf_total(d, h, i), 0);
+  if (!rc) rc = maint_push(d, MTE_MAINT_SPLIT, d->it[i].id, leaf_total(d, i, leaf_end(d, i)), 1);
+  return rc;
+}
+
 static int boundary(idoc* d, int64_t pos) {
   for (uint32_t i = 0; i < d->n; i++) {
     const int32_t l = d->L[i];
@@ -564,7 +591,7 @@ static int boundary(idoc* d, int64_t pos) {
       d->it[i].cont = 0;
       d->it[i].id = new_id(d);
       split_cascade(d, i);
-      return MTE_OK;
+      return maint_split(d, i);
     }
     if (pos > d->P[i] && pos < d->P[i] + l) {
       const int32_t off = (int32_t)(pos - d->P[i]);
@@ -587,7 +614,7 @@ static int boundary(idoc* d, int64_t pos) {
       d->L[i + 1] = tl->len;
       d->P[i + 1] = d->P[i] + off;
       split_cascade(d, i + 1);
-      return MTE_OK;
+      return maint_split(d, i + 1);
     }
   }
   return MTE_OK;
@@ -614,6 +641,14 @@ static int delta_push(idoc* d, uint32_t kind, int64_t pos, int32_t len, uint32_t
   }
   d->dl[d->dl_n++] = (mte_delta){d->cur_op, kind, (int32_t)pos, len, removed};
   return MTE_OK;
+}
+/* MTE_DELTA_MAINT (include/mte.h): one segment of a maintenance callback,
+ * named by its leaf's id (the reference's segment object: splitAt keeps the
+ * head, append keeps the segment appended to) until the record's end, when
+ * maint_positions makes it a position; -1: out of the tree */
+static int maint_push(idoc* d, uint32_t type, int64_t id, int64_t len, uint32_t idx) {
+  if (!(d->flags & MTE_DOC_MAINT_EVENTS)) return MTE_OK;
+  return delta_push(d, MTE_DELTA_MAINT | type, id, (int32_t)len, idx);
 }
 static inline int32_t own_len(const item* g) { return g->rseq == NONE_SEQ ? g->len : 0; }
 static int64_t own_prefix(const idoc* d, uint32_t at) {
@@ -872,10 +907,6 @@ static int64_t view_prefix(idoc* d, uint32_t x, int32_t R, int32_t L) {
 
 
 /* the item a leaf starts at */
-static uint32_t leaf_start(const idoc* d, uint32_t i) {
-  while (i > 0 && d->it[i].cont) i--;
-  return i;
-}
 /* the units of its leaf before item i */
 static int32_t leaf_offset(const idoc* d, uint32_t i) {
   int32_t o = 0;
@@ -1506,11 +1537,21 @@ static int doc_ack(idoc* d, const mte_op* op, const env_t* env) {
         member = 1;
       }
       if (member && !g->cont && (rc = add_lru(d, i, s))) return rc;
+      g->member = member && !g->cont;
     }
     d->slide_gid = ls;  /* this localSeq's group, in its order (ackPendingSegment per group op) */
     if ((rc = doc_slide_refs(d, s, 1))) return rc;
-    for (uint32_t i = 0; i < d->n; i++)
+    /* ACKNOWLEDGED (mergeTree.ts:1313-1320): the group's segments, after their slides */
+    if (d->flags & MTE_DOC_MAINT_EVENTS) {
+      uint32_t idx = 0;
+      for (uint32_t i = 0; i < d->n; i++)
+        if (d->it[i].member && (rc = maint_push(d, MTE_MAINT_ACK, d->it[i].id, leaf_total(d, i, leaf_end(d, i)), idx++)))
+          return rc;
+    }
+    for (uint32_t i = 0; i < d->n; i++) {
       if (d->it[i].lrs == ls) d->it[i].lrs = 0;
+      d->it[i].member = 0;
+    }
     zamboni(d, env->arena, env->n_keys);
   }
   return MTE_OK;
@@ -1556,10 +1597,32 @@ static int ref_snapshot(idoc* d) {
   return MTE_OK;
 }
 
+/* the record's MTE_DELTA_MAINT segments, named by leaf id -> their positions
+ * in the own view now (-1: no leaf of that id is in the tree any more) */
+static void maint_positions(idoc* d, uint64_t from) {
+  for (uint64_t q = from; q < d->dl_n; q++) {
+    mte_delta* e = &d->dl[q];
+    if ((e->kind & 0xff00u) != MTE_DELTA_MAINT || e->pos < 0) continue;
+    int64_t p = -1;
+    for (uint32_t i = 0; i < d->n; i++)
+      if (d->it[i].id == (uint32_t)e->pos && !d->it[i].cont && !d->it[i].empty) {
+        p = own_prefix(d, i);
+        break;
+      }
+    e->pos = (int32_t)p;
+  }
+}
+
 static int doc_apply_op(idoc* d, const mte_op* op, const env_t* env);
 static int doc_apply(idoc* d, const mte_op* op, const env_t* env) {
   const uint64_t from = d->dl_n;
+  if (!d->msg_open) d->msg_dl = from;
   int rc = doc_apply_op(d, op, env);
+  if (!rc && d->ev_rc) rc = d->ev_rc;
+  /* maintenance positions once the message (a local record: itself) is applied */
+  d->msg_open = !(op->flags & (MTE_F_MSG_END | MTE_F_LOCAL)) && op->type != MTE_OP_RELPOS ? 1 : 0;
+  if (op->type == MTE_OP_RELPOS) d->msg_open = 1;
+  if (!rc && (d->flags & MTE_DOC_MAINT_EVENTS) && !d->msg_open && d->dl_n > d->msg_dl) maint_positions(d, d->msg_dl);
   if (!rc && (d->flags & MTE_DOC_SLIDE_EVENTS) && d->dl_n > from) {
     slide_keys(d, from);
     int slid = 0;

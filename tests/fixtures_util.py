@@ -7,6 +7,7 @@ client "A" (the original client, which never sends): initialText of round 0 is
 inserted before collaboration (seq 0, LocalClientId), every message is applied
 as a remote op, and the text must equal resultText after each round.
 """
+import bisect
 import gzip
 import json
 import os
@@ -235,7 +236,7 @@ def canon_regen(op, orig, merge=True):
 
 
 def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_regen=False, observers_only=False,
-                    observers_local=False):
+                    observers_local=False, maint=None):
     """Replay farms the reference ran (oracle/ref_farm.js -> tests/golden/
     farm_vectors.json.gz): one MTE_DOC_LOCAL_CLIENT document per client of every
     set (the observer "A" included), each fed its own events in order — "L" a
@@ -256,8 +257,13 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_reg
     with the new length calculation, the tree passes with the legacy one).
     observers_local: only the observers, as MTE_DOC_LOCAL_CLIENT documents (the
     HBM tree pass; combiningOp incr / consensus replay there only).
+    maint (a dict): the documents record their maintenance callbacks
+    (MTE_DOC_MAINT_EVENTS); maint[(set, client)] collects them as the reference
+    farm's "maint" lists: [event index, MergeTreeMaintenanceType, [[position,
+    length], ...]].
     Returns (checkpoints_passed, failures)."""
-    from fluidframework_amd.abi import DOC_EVENTS, DOC_LOCAL_CLIENT, DOC_NEW_LENGTH_CALC, DOC_REFS
+    from fluidframework_amd.abi import (DELTA_MAINT, DOC_EVENTS, DOC_LOCAL_CLIENT, DOC_MAINT_EVENTS,
+                                        DOC_NEW_LENGTH_CALC, DOC_REFS)
     from fluidframework_amd.packing import regen_ops
 
     assert not (observers_only and observers_local)
@@ -267,13 +273,14 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_reg
     has_refs = not observers_only and any(s.get("refs") for s in sets)
     inits, text = doc_inits([sets[si]["initialText"] for si, _ in layout],
                             flags=DOC_NEW_LENGTH_CALC | (0 if observers_only else DOC_LOCAL_CLIENT) |
-                            (DOC_EVENTS if has_regen else 0) | (DOC_REFS if has_refs else 0))
+                            (DOC_EVENTS if has_regen or maint is not None else 0) | (DOC_REFS if has_refs else 0) |
+                            (DOC_MAINT_EVENTS if maint is not None else 0))
     for d, (si, _) in enumerate(layout):  # sets the reference ran with the legacy length calculation
         if sets[si].get("legacy"):
             inits[d]["flags"] = int(inits[d]["flags"]) & ~DOC_NEW_LENGTH_CALC & 0xffffffff
     interner = Interner(n_keys)
     eng = engine_factory(n_keys)
-    if has_regen:
+    if has_regen or maint is not None:
         eng.set_event_capacity(64)
     eng.load_docs(inits, text)
     held = [[] for _ in layout]
@@ -285,12 +292,14 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_reg
     for j in range(n_cp):
         bb = BatchBuilder(len(layout), interner)
         regens = []  # (doc, add_regen result, original op, log index)
+        spans = [[] for _ in layout]  # maint: (event index, its first record, past its last)
         for d, (si, ci) in enumerate(layout):
             s = sets[si]
             if j >= len(s["checkpoints"]):
                 continue
             done = s["checkpoints"][j]["done"][ci]
-            for ev in s["events"][ci][prev[d]:done]:
+            for ei, ev in enumerate(s["events"][ci][prev[d]:done], prev[d]):
+                spans[d].append((ei, len(bb.ops[d])))
                 kind, li = ev[0], ev[1]
                 if kind == "F":  # a local reference at position li (ev[2]: its ReferenceType)
                     ref_slots[d].append(bb.add_ref(d, clients[d], li, ev[2]))
@@ -318,6 +327,20 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_reg
             prev[d] = done
         eng.apply_batch(bb.build())
         st = eng.statuses()
+        if maint is not None:
+            for d, (si, ci) in enumerate(layout):
+                if not spans[d] or st[d] != 0:
+                    continue
+                starts = [r for _, r in spans[d]]
+                out = maint.setdefault((si, ci), [])
+                for e in eng.read_deltas(d):
+                    if int(e["kind"]) & 0xff00 != DELTA_MAINT:
+                        continue
+                    ei = spans[d][bisect.bisect_right(starts, int(e["op"])) - 1][0]
+                    t = -(int(e["kind"]) & 0xff)
+                    if int(e["removed"]) == 0 or not out or out[-1][0] != ei or out[-1][1] != t:
+                        out.append([ei, t, []])
+                    out[-1][2].append([int(e["pos"]), int(e["len"])])
         for d, idx, orig, li in regens:
             si, ci = layout[d]
             if st[d] != 0:
