@@ -55,6 +55,7 @@ DELTA_MAINT = 0x100   # | MTE_MAINT_*: a maintenance callback's segment (MTE_DOC
 ANNOTATE_SLOTS = 32   # pending local annotate groups tracked per document
 F_MARKER, F_MSG_END, F_REWRITE, F_LOCAL = 0x1, 0x2, 0x4, 0x8
 F_COMBINE = 0x10         # annotate combiningOp incr / consensus (value maps, include/mte.h)
+F_REGENERATED = 0x20     # an ack of a regenerated message (include/mte.h)
 COMBINE_PAIR = 0x80000000
 MTE_VALUE_UNEQUAL = 0x40000000  # a value id that matches no other (NaN), include/mte.h
 LOCAL_SEQ_BASE = 0x40000000

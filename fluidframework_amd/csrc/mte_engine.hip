@@ -153,7 +153,7 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
   h.cur_seq = in.cur_seq;
   h.status = 0;
   h.flags = in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC | MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS | MTE_DOC_REFS |
-                        MTE_DOC_SLIDE_EVENTS);
+                        MTE_DOC_SLIDE_EVENTS | MTE_DOC_MAINT_EVENTS);
   h.resume = 0;
   h.pad0 = h.pad1 = 0;
   if (legacy) {
@@ -919,7 +919,7 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
     }
     if (c->n_htree) {
       // LDS residency: (nP + 5) words per item (mte_htree.h ht_to_lds), whole wavefronts' worth
-      const uint32_t words = (uint32_t)(kFieldPlanes + 3 * K + 3 + 5);
+      const uint32_t words = (uint32_t)(kLocalPlanes<K> + 5);
       uint32_t lcap = c->htree_lds >= 8 ? (c->htree_lds / 4 - 2) / words / kWave * kWave : 0u;
       if (lcap > c->cap) lcap = c->cap / kWave * kWave;
       const uint32_t* order = c->hord_ok_s[c->rslot] ? c->d_hord_s[c->rslot] : c->d_htree_docs;
@@ -1255,6 +1255,11 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
       return set_err(c, MTE_E_INVALID_ARG, "doc %u: initial text out of range", d);
     if ((in.flags & MTE_DOC_REFS) && !(in.flags & MTE_DOC_LOCAL_CLIENT))
       return set_err(c, MTE_E_UNSUPPORTED, "doc %u: local references need MTE_DOC_LOCAL_CLIENT", d);
+    // maintenance records come from the HBM tree pass, which keeps the
+    // reference's segments (a local client's document)
+    if ((in.flags & MTE_DOC_MAINT_EVENTS) && (in.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)) !=
+                                                 (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS))
+      return set_err(c, MTE_E_UNSUPPORTED, "doc %u: maintenance events need MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS", d);
     // delta events of a new length-calc document without a local client come
     // from the HBM-streamed flat pass, which big-document contexts do not run
     if ((in.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)) == MTE_DOC_EVENTS &&
@@ -1310,10 +1315,11 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     if ((docs[d].flags & sl) == sl) c->h_slides[d] = 1;
   }
   if (any_refs) HIPCHK(c, hipMalloc((void**)&c->d_refs, sizeof(uint2) * (size_t)c->ref_cap * n_docs));
-  // documents with a local client hold 2 kt + 3 more planes (mte_htree.h): the
+  // documents with a local client hold 2 kt + 5 more planes (mte_htree.h): the
   // pending property keys, the annotate-group mask, the keys' values before
-  // their first pending annotate, localRemovedSeq and the removal-group order
-  const uint64_t prop_planes = (c->kt ? c->kt : 1) + (any_local ? 2 * c->kt + 3 : 0);  // + localRemovedSeq, group order
+  // their first pending annotate, localRemovedSeq, the removal-group order, the
+  // first group an item is one of the marked segments of, the regeneration group
+  const uint64_t prop_planes = (c->kt ? c->kt : 1) + (any_local ? 2 * c->kt + 5 : 0);
   HIPCHK(c, hipMalloc((void**)&c->hdr, sizeof(DocHdr) * (n_docs ? n_docs : 1)));
   // one allocation, planes at stride nslots: len seq rseq rmask meta toff props[kt]
   // (kt >= n_keys planes, so the register-resident kernels never index past it)

@@ -85,6 +85,14 @@ constexpr uint32_t kLrsReleased = 0x40000000u;
 // remove, 0x80000000 | the tail's id for a tail split off later (splitAt's
 // segmentGroups.copyTo appends it, mergeTreeNodes.ts:505-534; titems.c gord)
 template <int K> constexpr int kGrpPlane = kFieldPlanes + 3 * K + 2;
+// kBornPlane: the first localSeq whose segment group can hold the item as one
+// of the segments its op marked -- an item split off later joins the groups
+// before it as a tail, appended (titems.c item.born); kRgPlane: a regenerated
+// segment's group, 1 + its id at its last regeneration, shared by the tails
+// split off it since (titems.c item.rg, MTE_F_REGENERATED)
+template <int K> constexpr int kBornPlane = kFieldPlanes + 3 * K + 3;
+template <int K> constexpr int kRgPlane = kFieldPlanes + 3 * K + 4;
+template <int K> constexpr int kLocalPlanes = kFieldPlanes + 3 * K + 5;  // planes of a local-client document
 
 struct HT {
   uint32_t* pl;   // the document's plane base
@@ -108,6 +116,8 @@ struct HT {
   int lp_n;
   int32_t lp_carry;
   const uint16_t* arena;
+  bool maint;     // MTE_DOC_MAINT_EVENTS: maintenance records (ht_maint)
+  uint32_t born;  // kBornPlane of an item made by the record being applied
   // MTE_OP_RELPOS: positions for the next record (rpf: MTE_RP_POS1 / POS2 given)
   uint32_t rpf;
   // the window of the reference's cached local partial lengths (ht_view_window), -1: none
@@ -554,6 +564,28 @@ __device__ __forceinline__ int32_t ht_sum_len(const HT& h, int a, int b) {
   return rdlane(wave_incl_scan(s), kWave - 1);
 }
 
+// one segment of a maintenance callback (MTE_DELTA_MAINT, include/mte.h;
+// titems.c maint_push): named by its leaf's id until the message's end
+// (ht_maint_positions), -1 out of the tree; idx its index in the callback
+__device__ __forceinline__ void ht_maint(const HT& h, EvOut& ev, uint32_t type, int32_t id, int32_t len, uint32_t idx) {
+  if (!h.maint) return;
+  if (lane_id() == 0 && ev.n < ev.cap) ev.p[ev.n] = mte_delta{ev.op, MTE_DELTA_MAINT | type, id, len, idx};
+  ev.n++;
+}
+__device__ __forceinline__ int ht_leaf_start(const HT& h, int i) {
+  const uint32_t* tw = h.tw;
+  const int s = ht_last(0, i + 1, [&](int x) { return (ld_l2(tw + x) & kTCont) == 0; });
+  return s < 0 ? 0 : s;
+}
+// the SPLIT callback (splitLeafSegment, mergeTree.ts:1682-1694): the leaf
+// ending before item i and the one starting there (titems.c maint_split)
+__device__ __forceinline__ void ht_maint_split(HT& h, EvOut& ev, int i) {
+  if (!h.maint) return;
+  const int hd = ht_leaf_start(h, i - 1);
+  ht_maint(h, ev, MTE_MAINT_SPLIT, (int32_t)t_id(ht_T(h, hd)), ht_sum_len(h, hd, i), 0u);
+  ht_maint(h, ev, MTE_MAINT_SPLIT, (int32_t)t_id(ht_T(h, i)), ht_sum_len(h, i, ht_leaf_end(h, i)), 1u);
+}
+
 // mark items [a, b) for dropping (the L scratch is the flag plane)
 __device__ __forceinline__ void ht_mark(HT& h, int a, int b, int32_t f) {
   const int l = lane_id();
@@ -569,7 +601,7 @@ __device__ __forceinline__ void ht_mark(HT& h, int a, int b, int32_t f) {
 // unlinked items, turns appended leaves into continuations; returns the
 // logical leaves held.  The caller cleared the flags of [s, e].
 template <int K>
-__device__ __forceinline__ int ht_scour(HT& h, int s, int e, uint32_t n_keys) {
+__device__ __forceinline__ int ht_scour(HT& h, int s, int e, uint32_t n_keys, EvOut& ev) {
   int held = 0;
   int prev = -1;             // head of the leaf appends go to
   int32_t prev_len = 0;
@@ -593,8 +625,12 @@ __device__ __forceinline__ int ht_scour(HT& h, int s, int e, uint32_t n_keys) {
       held++;
       prev = -1;
     } else if (rseq != kNone) {
-      if (rseq > h.min_seq) held++;
-      else ht_mark(h, i, xe, 1);
+      if (rseq > h.min_seq) {
+        held++;
+      } else {
+        ht_mark(h, i, xe, 1);
+        ht_maint(h, ev, MTE_MAINT_UNLINK, -1, xl, 0u);  // mergeTree.ts:692-703
+      }
       prev = -1;
     } else if (seq <= h.min_seq) {
       bool app = false;
@@ -621,6 +657,9 @@ __device__ __forceinline__ int ht_scour(HT& h, int s, int e, uint32_t n_keys) {
         ht_setT(h, i, (tx & ((0xffu & ~kTNs) | kTNl)) | kTCont);  // id 0: a continuation
         prev_len += xl;
         prev_end = xe;
+        // mergeTree.ts:715-727: the segment appended to, then this one
+        ht_maint(h, ev, MTE_MAINT_APPEND, (int32_t)t_id(ht_T(h, prev)), prev_len, 0u);
+        ht_maint(h, ev, MTE_MAINT_APPEND, -1, xl, 1u);
       } else {
         held++;
         if (xl > 0) {
@@ -710,20 +749,20 @@ __device__ __forceinline__ void ht_regroup(HT& h, int s, int e, int total, uint3
 }
 
 template <int K>
-__device__ __forceinline__ int ht_pack_parent(HT& h, int s, int p, uint32_t n_keys, int& status);
+__device__ __forceinline__ int ht_pack_parent(HT& h, int s, int p, uint32_t n_keys, int& status, EvOut& ev);
 
 // zamboniSegments (titems.c zamboni): at most two scours
 template <int K>
-__device__ __forceinline__ int ht_zamboni_body(HT& h, uint32_t n_keys);
+__device__ __forceinline__ int ht_zamboni_body(HT& h, uint32_t n_keys, EvOut& ev);
 template <int K>
-__device__ __forceinline__ int ht_zamboni(HT& h, uint32_t n_keys) {
+__device__ __forceinline__ int ht_zamboni(HT& h, uint32_t n_keys, EvOut& ev) {
   HPROF_BEGIN(t0)
-  const int rc = ht_zamboni_body<K>(h, n_keys);
+  const int rc = ht_zamboni_body<K>(h, n_keys, ev);
   HPROF_END(h, 3, t0)
   return rc;
 }
 template <int K>
-__device__ __forceinline__ int ht_zamboni_body(HT& h, uint32_t n_keys) {
+__device__ __forceinline__ int ht_zamboni_body(HT& h, uint32_t n_keys, EvOut& ev) {
   int status = 0;
   for (int z = 0; z < 2; z++) {
     if (h.hn == 0) break;
@@ -742,7 +781,7 @@ __device__ __forceinline__ int ht_zamboni_body(HT& h, uint32_t n_keys) {
     const int before = ht_children(h, bs, be, 1);
     ht_mark(h, bs, be + 1, 0);
     h.lp_n = 0;
-    const int held = ht_scour<K>(h, bs, be, n_keys);
+    const int held = ht_scour<K>(h, bs, be, n_keys, ev);
     {
       const uint32_t t2 = ht_T(h, bs);
       ht_setT(h, bs, (t2 & ~kTNs) | (kNsFalse << kTNsShift));
@@ -752,7 +791,7 @@ __device__ __forceinline__ int ht_zamboni_body(HT& h, uint32_t n_keys) {
       ht_drop_keep_starts(h, bs, be);
       ht_compact(h, bs, be);
       if (held < kMaxNodes / 2 && h.depth >= 2) {
-        ht_pack_parent<K>(h, ht_span_start(h, bs, 2), 2, n_keys, status);
+        ht_pack_parent<K>(h, ht_span_start(h, bs, 2), 2, n_keys, status, ev);
         if (status) return status;
       }
     }
@@ -762,7 +801,7 @@ __device__ __forceinline__ int ht_zamboni_body(HT& h, uint32_t n_keys) {
 
 // packParent (mergeTree.ts:750-798) of the level-p block starting at s
 template <int K>
-__device__ __forceinline__ int ht_pack_parent(HT& h, int s, int p, uint32_t n_keys, int& status) {
+__device__ __forceinline__ int ht_pack_parent(HT& h, int s, int p, uint32_t n_keys, int& status, EvOut& ev) {
   for (;;) {
     int e = ht_span_end(h, s, p);
     const uint32_t top = t_h(ht_T(h, s));
@@ -771,7 +810,7 @@ __device__ __forceinline__ int ht_pack_parent(HT& h, int s, int p, uint32_t n_ke
       h.lp_n = 0;
       for (int b = s; b <= e;) {
         const int be = ht_span_end(h, b, 1);
-        ht_scour<K>(h, b, be, n_keys);
+        ht_scour<K>(h, b, be, n_keys, ev);
         b = be + 1;
       }
       // the held leaves, re-packed: drop the scoured-out items and the placeholders
@@ -833,7 +872,7 @@ __device__ __forceinline__ int ht_pack_parent(HT& h, int s, int p, uint32_t n_ke
 // ---- ensureIntervalBoundary (titems.c boundary) ---------------------------------------
 
 template <int K, bool S>
-__device__ __forceinline__ int ht_boundary(HT& h, int32_t pos, uint32_t (&st)[kNumStats]) {
+__device__ __forceinline__ int ht_boundary(HT& h, int32_t pos, uint32_t (&st)[kNumStats], EvOut& ev) {
   const int32_t* Lp = h.L;
   const int32_t* Pp = h.P;
   const int i = ht_first_lp(h, 0, [&](int x) {
@@ -850,6 +889,7 @@ __device__ __forceinline__ int ht_boundary(HT& h, int32_t pos, uint32_t (&st)[kN
       ht_setT(h, i, (t & (kTPo | kTNl)) | (h.next_id++ << 8));
       vm_drain();
       ht_split_cascade(h, i);
+      ht_maint_split(h, ev, i);
     }
     return 0;
   }
@@ -862,12 +902,16 @@ __device__ __forceinline__ int ht_boundary(HT& h, int32_t pos, uint32_t (&st)[kN
   ht_setpl(h, 0, i, (uint32_t)off);
   ht_setpl(h, 0, i + 1, len - (uint32_t)off);
   ht_setpl(h, 5, i + 1, toff + (uint32_t)off);
-  if (h.ldoc) ht_setpl(h, kGrpPlane<K>, i + 1, 0x80000000u | h.next_id);
+  if (h.ldoc) {
+    ht_setpl(h, kGrpPlane<K>, i + 1, 0x80000000u | h.next_id);
+    ht_setpl(h, kBornPlane<K>, i + 1, h.born);
+  }
   ht_setT(h, i + 1, (t & (kTPo | kTNl)) | (h.next_id++ << 8));
   vm_drain();
   ht_inval(h, i);
   MTE_STAT(st[kStWritten] += 2;)
   ht_split_cascade(h, i + 1);
+  ht_maint_split(h, ev, i + 1);
   return 0;
 }
 
@@ -891,6 +935,7 @@ __device__ __forceinline__ void ht_put_new(HT& h, int g, const s8v& op, bool loc
   else if (l == 3) v = 0u;
   else if (l == 4) v = (c + 1u) | (marker ? (1u + (uint32_t)pos2) << 8 : 0u);
   else if (l == 5) v = (marker && !refd) ? 0u : a.text_base + (uint32_t)op[6];
+  else if (l == kBornPlane<K>) v = h.born;
   if (K > 0 && psi != MTE_NO_PROPS) {
     const mte_propset ps = a.ps[psi];
     for (uint32_t t = 0; t < ps.count; t++) {
@@ -908,13 +953,13 @@ __device__ __forceinline__ void ht_put_new(HT& h, int g, const s8v& op, bool loc
 // 1590-1680, 1723-1825); *at = the new item or -1
 template <int K, bool S>
 __device__ __forceinline__ int ht_insert(HT& h, const s8v& op, bool local, bool refd, const ReplayArgs& a, uint32_t (&st)[kNumStats],
-                         int& at) {
+                         int& at, EvOut& ev) {
   const uint32_t w3 = (uint32_t)op[3];
   const uint32_t c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   const int32_t s = op[0], r = op[1], pos = op[4], pos2 = op[5];
   at = -1;
   ht_persp(h, local, r, (int)c);
-  int rc = ht_boundary<K, S>(h, pos, st);
+  int rc = ht_boundary<K, S>(h, pos, st, ev);
   if (rc) return rc;
   const bool marker = (flags & MTE_F_MARKER) != 0;
   const int32_t len = marker ? 1 : pos2;
@@ -1020,9 +1065,9 @@ __device__ __forceinline__ int ht_range(HT& h, const s8v& op, bool local, const 
   const uint32_t type = w3 & 0xffu, c = (w3 >> 8) & 0xffu, flags = w3 >> 16;
   const int32_t s = op[0], r = op[1], start = op[4], end = op[5];
   ht_persp(h, local, r, (int)c);
-  int rc = ht_boundary<K, S>(h, start, st);
+  int rc = ht_boundary<K, S>(h, start, st, ev);
   if (rc) return rc;
-  if ((rc = ht_boundary<K, S>(h, end, st))) return rc;
+  if ((rc = ht_boundary<K, S>(h, end, st, ev))) return rc;
   if (end == start) return 0;
   const int32_t* Lp = h.L;
   const int32_t* Pp = h.P;
@@ -1194,83 +1239,165 @@ __device__ __forceinline__ int ht_range(HT& h, const s8v& op, bool local, const 
 
 // ---- local records (titems.c doc_ack, doc_rollback, doc_rollback_annotate, doc_regen) ----------
 
-// MTE_OP_ACK for localSeqs pos1..pos2: per localSeq, ackPendingSegment acks its
-// group (mergeTree.ts:1278-1331, mergeTreeNodes.ts:475-503), slides the
-// references of the acked removals, adds each segment to the LRU set and runs
-// zamboniSegments
+// an item the ack of ls still has to take: inserted, removed or annotated by
+// ls (am_mask: ls's annotate slot), or a removal of ls a remote one overtook
+// (titems.c ack_pending)
 template <int K>
-__device__ __forceinline__ int ht_ack(HT& h, const s8v& op, const ReplayArgs& a, uint2* rt, uint32_t rhi, EvOut* ev) {
+__device__ __forceinline__ bool ht_ack_pending(const HT& h, int i, int32_t ls, uint32_t am_mask) {
+  if (ld_l2(h.tw + i) & kTEmpty) return false;
+  return (int32_t)ld_l2(h.pl + h.sd + i) == kLocalBase + ls || (int32_t)ld_l2(h.pl + 2 * h.sd + i) == kLocalBase + ls ||
+         (int32_t)ld_l2(h.pl + (uint64_t)kLrsPlane<K> * h.sd + i) == ls ||
+         (ld_l2(h.pl + (uint64_t)kAnnPlane<K> * h.sd + i) & am_mask) != 0u;
+}
+
+// ackPendingSegment (mergeTree.ts:1278-1331, mergeTreeNodes.ts:475-503) for one
+// segment group of ls (titems.c ack_group): the items of regeneration group
+// `key` (keyed) or every item of ls get the seq, each segment is added to the
+// LRU set in the group's order -- the segments the op marked in document
+// order, then the tails split off since, as they were made -- the references
+// of the acked removals slide, the ACKNOWLEDGED record reports the group, then
+// zamboniSegments runs.  The group's segments are flagged in the L scratch.
+template <int K>
+__device__ __forceinline__ int ht_ack_group(HT& h, int32_t ls, int32_t s, uint32_t am_mask, bool keyed, uint32_t key,
+                                            const ReplayArgs& a, uint2* rt, uint32_t rhi, EvOut& ev, bool evs) {
+  const int l = lane_id();
+  int rc;
+  int bc = -1, bec = -2;
+  uint32_t tails = 0;
+  const uint32_t* rgp = h.pl + (uint64_t)kRgPlane<K> * h.sd;
+  const uint32_t* bnp = h.pl + (uint64_t)kBornPlane<K> * h.sd;
+  for (int tb = 0; tb < h.n; tb += kHT) {
+    bool member[kHE], orig[kHE];
+    uint32_t tt[kHE];
+#pragma unroll
+    for (int j = 0; j < kHE; j++) {
+      const int i = tb + j * kWave + l;
+      const bool v = i < h.n;
+      const int ic = v ? i : 0;
+      tt[j] = ld_l2(h.tw + ic);
+      const int32_t sq = (int32_t)ld_l2(h.pl + h.sd + ic), rs = (int32_t)ld_l2(h.pl + 2 * h.sd + ic);
+      const int32_t lr = (int32_t)ld_l2(h.pl + (uint64_t)kLrsPlane<K> * h.sd + ic);
+      const uint32_t am = ld_l2(h.pl + (uint64_t)kAnnPlane<K> * h.sd + ic);
+      const uint32_t rg = ld_l2(rgp + ic);
+      orig[j] = ld_l2(bnp + ic) <= (uint32_t)ls;
+      member[j] = false;
+      if (v) h.L[i] = 0;
+      if (!v || (tt[j] & kTEmpty) || (keyed && rg != key)) continue;
+      if (sq == kLocalBase + ls) {
+        h.pl[h.sd + i] = (uint32_t)s;
+        member[j] = true;
+      }
+      if (lr == ls) {  // acked, or overtaken by a remote remove before (:1928-1938)
+        h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = 0u;
+        member[j] = true;
+      }
+      if (rs == kLocalBase + ls) {
+        h.pl[2 * h.sd + i] = (uint32_t)s;
+        // the group's removals hold ls until they have slid (stream_slide's
+        // group mark; a regenerated one's localRemovedSeq is its old op's)
+        // (acked: localRemovedSeq undefined, mergeTreeNodes.ts:493)
+        h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = (rt && rhi) ? (uint32_t)ls : 0u;
+      }
+      if (am & am_mask) {
+        h.pl[(uint64_t)kAnnPlane<K> * h.sd + i] = am & ~am_mask;
+        member[j] = true;
+      }
+    }
+    vm_drain();
+#pragma unroll
+    for (int j = 0; j < kHE; j++) {
+      const bool mem = member[j] && !(tt[j] & kTCont);
+      if (mem) h.L[tb + j * kWave + l] = 1;
+      tails += (uint32_t)__popcll(__ballot(mem && !orig[j]));
+      uint64_t m = __ballot(mem && orig[j]);
+      while (m) {
+        const int i = tb + j * kWave + (__ffsll((long long)m) - 1);
+        m &= m - 1;
+        if ((rc = ht_add_lru(h, i, s, bc, bec))) return rc;
+      }
+    }
+  }
+  vm_drain();
+  const int32_t* Lf = h.L;
+  for (uint32_t last = 0; tails; tails--) {
+    // the next tail by id
+    uint32_t best = 0xffffffffu;
+    for (int tb = 0; tb < h.n; tb += kWave) {
+      const int i = tb + l;
+      if (i < h.n && ld_l2((const uint32_t*)Lf + i) == 1u && ld_l2(bnp + i) > (uint32_t)ls) {
+        const uint32_t id = t_id(ld_l2(h.tw + i));
+        if (id >= last && id < best) best = id;
+      }
+    }
+    best = uni(wave_min_u32(best));
+    const int i = ht_first(0, h.n, [&](int x) {
+      return ld_l2((const uint32_t*)Lf + x) == 1u && ld_l2(bnp + x) > (uint32_t)ls && t_id(ld_l2(h.tw + x)) == best;
+    });
+    if (i < 0) break;
+    if ((rc = ht_add_lru(h, i, s, bc, bec))) return rc;
+    last = best + 1u;
+  }
+  if (rt && rhi) {
+    // the group slides in its order, the later groups still pending
+    // (ackPendingSegment per group op, mergeTree.ts:1278-1304)
+    uint32_t* lrp = h.pl + (uint64_t)kLrsPlane<K> * h.sd;
+    stream_slide(h.pl, h.sd, h.n, rt, rhi, s, evs ? &ev : nullptr, kSlideAck, h.pl + (uint64_t)kGrpPlane<K> * h.sd,
+                 h.tw, lrp, (uint32_t)ls);
+    for (int tb = 0; tb < h.n; tb += kWave) {
+      const int i = tb + l;
+      if (i < h.n && (int32_t)ld_l2(lrp + i) == ls && (!keyed || ld_l2(rgp + i) == key)) lrp[i] = 0u;
+    }
+    vm_drain();
+  }
+  if (h.maint) {
+    // ACKNOWLEDGED (mergeTree.ts:1313-1320): the group's segments in document
+    // order, after their slides (titems.c ack_group)
+    uint32_t idx = 0;
+    for (int i = ht_first(0, h.n, [&](int x) { return ld_l2((const uint32_t*)Lf + x) == 1u; }); i >= 0;
+         i = ht_first(i + 1, h.n, [&](int x) { return ld_l2((const uint32_t*)Lf + x) == 1u; }))
+      ht_maint(h, ev, MTE_MAINT_ACK, (int32_t)t_id(ht_T(h, i)), ht_sum_len(h, i, ht_leaf_end(h, i)), idx++);
+  }
+  h.lp_n = 0;  // the L scratch held the flags
+  return ht_zamboni<K>(h, a.n_keys, ev);
+}
+
+// MTE_OP_ACK for localSeqs pos1..pos2 (titems.c doc_ack): per localSeq,
+// ackPendingSegment acks its group; a regenerated message (MTE_F_REGENERATED)
+// acks each re-sent segment of it as a group of its own, in document order
+// (resetPendingDeltaToOps, client.ts:802-857)
+template <int K>
+__device__ __forceinline__ int ht_ack(HT& h, const s8v& op, const ReplayArgs& a, uint2* rt, uint32_t rhi, EvOut& ev,
+                                      bool evs) {
   const int32_t lo = op[4], hi = op[5], s = op[0];
   const uint32_t mask = (uint32_t)op[6];
+  const bool regen = ((((uint32_t)op[3]) >> 16) & MTE_F_REGENERATED) != 0u;
   const int l = lane_id();
   int rc;
   for (int32_t ls = lo; ls <= hi; ls++) {
     const uint32_t am_mask = ls == hi ? mask : 0u;
-    int bc = -1, bec = -2;
-    for (int tb = 0; tb < h.n; tb += kHT) {
-      bool member[kHE];
-      uint32_t tt[kHE];
+    // the pending property keys of ls stop blocking remote annotates
+    for (int tb = 0; tb < h.n; tb += kWave) {
+      const int i = tb + l;
+      if (i < h.n) {
 #pragma unroll
-      for (int j = 0; j < kHE; j++) {
-        const int i = tb + j * kWave + l;
-        const bool v = i < h.n;
-        const int ic = v ? i : 0;
-        tt[j] = ld_l2(h.tw + ic);
-        const int32_t sq = (int32_t)ld_l2(h.pl + h.sd + ic), rs = (int32_t)ld_l2(h.pl + 2 * h.sd + ic);
-        const int32_t lr = (int32_t)ld_l2(h.pl + (uint64_t)kLrsPlane<K> * h.sd + ic);
-        const uint32_t am = ld_l2(h.pl + (uint64_t)kAnnPlane<K> * h.sd + ic);
-        uint32_t pk[K > 0 ? K : 1];
-#pragma unroll
-        for (int k = 0; k < K; k++) pk[k] = ld_l2(h.pl + (uint64_t)(kPkPlane<K> + k) * h.sd + ic);
-        member[j] = false;
-        if (!v || (tt[j] & kTEmpty)) continue;
-        if (sq == kLocalBase + ls) {
-          h.pl[h.sd + i] = (uint32_t)s;
-          member[j] = true;
-        }
-        if (lr == ls) {  // acked, or overtaken by a remote remove before (:1928-1938)
-          h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = 0u;
-          member[j] = true;
-        }
-        if (rs == kLocalBase + ls) {
-          h.pl[2 * h.sd + i] = (uint32_t)s;
-          // the group's removals hold ls until they have slid (stream_slide's
-          // group mark; a regenerated one's localRemovedSeq is its old op's)
-          // (acked: localRemovedSeq undefined, mergeTreeNodes.ts:493)
-          h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = (rt && rhi) ? (uint32_t)ls : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < K; k++)
-          if (pk[k] != 0u && pk[k] <= (uint32_t)ls) h.pl[(uint64_t)(kPkPlane<K> + k) * h.sd + i] = 0u;
-        if (am & am_mask) {
-          h.pl[(uint64_t)kAnnPlane<K> * h.sd + i] = am & ~am_mask;
-          member[j] = true;
-        }
-      }
-      vm_drain();
-#pragma unroll
-      for (int j = 0; j < kHE; j++) {
-        uint64_t m = __ballot(member[j] && !(tt[j] & kTCont));
-        while (m) {
-          const int i = tb + j * kWave + (__ffsll((long long)m) - 1);
-          m &= m - 1;
-          if ((rc = ht_add_lru(h, i, s, bc, bec))) return rc;
+        for (int k = 0; k < K; k++) {
+          uint32_t* pk = h.pl + (uint64_t)(kPkPlane<K> + k) * h.sd + i;
+          const uint32_t v = ld_l2(pk);
+          if (v != 0u && v <= (uint32_t)ls) *pk = 0u;
         }
       }
     }
-    if (rt && rhi) {
-      // this localSeq's group slides in its order, the later groups still pending
-      // (ackPendingSegment per group op, mergeTree.ts:1278-1304)
-      uint32_t* lrp = h.pl + (uint64_t)kLrsPlane<K> * h.sd;
-      stream_slide(h.pl, h.sd, h.n, rt, rhi, s, ev, kSlideAck, h.pl + (uint64_t)kGrpPlane<K> * h.sd, h.tw, lrp,
-                   (uint32_t)ls);
-      for (int tb = 0; tb < h.n; tb += kWave) {
-        const int i = tb + l;
-        if (i < h.n && (int32_t)ld_l2(lrp + i) == ls) lrp[i] = 0u;
-      }
-      vm_drain();
+    vm_drain();
+    if (!regen) {
+      if ((rc = ht_ack_group<K>(h, ls, s, am_mask, false, 0u, a, rt, rhi, ev, evs))) return rc;
+      continue;
     }
-    if ((rc = ht_zamboni<K>(h, a.n_keys))) return rc;
+    for (;;) {
+      const int f = ht_first(0, h.n, [&](int x) { return ht_ack_pending<K>(h, x, ls, am_mask); });
+      if (f < 0) break;
+      const uint32_t key = uld(h.pl + (uint64_t)kRgPlane<K> * h.sd + f);
+      if ((rc = ht_ack_group<K>(h, ls, s, am_mask, true, key, a, rt, rhi, ev, evs))) return rc;
+    }
   }
   return 0;
 }
@@ -1308,7 +1435,7 @@ __device__ __forceinline__ int ht_rollback(HT& h, const s8v& op, const ReplayArg
       ht_setpl(h, 3, i, 1u);
       vm_drain();
       if (evd) ev_one(ev, MTE_OP_REMOVE, lp, len);
-      if ((rc = ht_zamboni<K>(h, a.n_keys))) return rc;
+      if ((rc = ht_zamboni<K>(h, a.n_keys, ev))) return rc;
     }
     return 0;
   }
@@ -1365,7 +1492,7 @@ __device__ __forceinline__ int ht_rollback_annotate(HT& h, uint32_t b, const uin
     }
     vm_drain();
     if (evd) ev_one(ev, MTE_OP_ANNOTATE, own_prefix(h.pl, h.sd, i), tl);
-    if ((rc = ht_zamboni<K>(h, a.n_keys))) return rc;
+    if ((rc = ht_zamboni<K>(h, a.n_keys, ev))) return rc;
   }
   return 0;
 }
@@ -1661,12 +1788,7 @@ __device__ __forceinline__ int ht_view_find(HT& h, int32_t pos, int32_t R, int32
   return found;
 }
 
-// the item a leaf starts at; the units of its leaf before item i
-__device__ __forceinline__ int ht_leaf_start(const HT& h, int i) {
-  const uint32_t* tw = h.tw;
-  const int s = ht_last(0, i + 1, [&](int x) { return (ld_l2(tw + x) & kTCont) == 0; });
-  return s < 0 ? 0 : s;
-}
+// the units of its leaf before item i
 __device__ __forceinline__ int32_t ht_leaf_offset(const HT& h, int i) {
   const int s = ht_leaf_start(h, i);
   return s < i ? ht_sum_len(h, s, i) : 0;
@@ -1738,6 +1860,9 @@ __device__ __forceinline__ void ht_regen(HT& h, int32_t ls, uint32_t t, uint32_t
         // each re-sent segment heads a group of its own, the old group's taken
         // by ordinal (client.ts:802, 852): the ack slides them in document order
         if (hit && t == MTE_OP_REMOVE) h.pl[(uint64_t)kGrpPlane<K> * h.sd + i] = (uint32_t)i;
+        // and a segment group of its own (client.ts:851-854), which the
+        // tails split off it later join (a continuation: its leaf's, below)
+        if (hit && !(tt & kTCont)) h.pl[(uint64_t)kRgPlane<K> * h.sd + i] = 1u + t_id(tt);
         if (!hit && t == MTE_OP_ANNOTATE && ((am >> slot) & 1u))
           h.pl[(uint64_t)kAnnPlane<K> * h.sd + i] = am & ~(1u << slot);
       }
@@ -1753,6 +1878,17 @@ __device__ __forceinline__ void ht_regen(HT& h, int32_t ls, uint32_t t, uint32_t
         (void)ht_view_prefix<K>(h, tb + j * kWave + ln, h.cur_seq, ls);
       }
       // hit(i - 1): the lane before, or the previous row's / tile's last item
+      uint64_t cm = __ballot(hit && (tt & kTCont));
+      if (cm) {  // a merged leaf's continuations: its head's group
+        uint32_t* rgp = h.pl + (uint64_t)kRgPlane<K> * h.sd;
+        vm_drain();
+        while (cm) {
+          const int x = tb + j * kWave + (__ffsll((long long)cm) - 1);
+          cm &= cm - 1;
+          lane0_st(rgp + x, uld(rgp + x - 1));
+          vm_drain();
+        }
+      }
       const uint64_t hm = __ballot(hit);
       const bool hprev = l > 0 ? ((hm >> (l - 1)) & 1ull) != 0 : prev_hit;
       const bool ext = hit && (tt & kTCont) && hprev;
@@ -1880,6 +2016,27 @@ __device__ __noinline__ uint32_t ht_slide_keys(const uint32_t* pl, uint64_t sd, 
   return slid;
 }
 
+// The MTE_DELTA_MAINT records of one message, [from, to): each segment's leaf
+// id -> its position in the own view now, -1 when no leaf of that id is in the
+// tree (titems.c maint_positions).  Out of line, its arguments by value.
+__device__ __noinline__ void ht_maint_positions(const uint32_t* pl, uint64_t sd, const uint32_t* tw, int n, mte_delta* evp,
+                                                uint32_t to, uint32_t from) {
+  if (from >= to) return;
+  vm_drain();
+  for (uint32_t q = from; q < to; q++) {
+    const uint32_t kind = uni(ld_l2(&evp[q].kind));
+    const int32_t id = (int32_t)uni(ld_l2(reinterpret_cast<const uint32_t*>(&evp[q].pos)));
+    if ((kind & 0xff00u) != MTE_DELTA_MAINT || id < 0) continue;
+    const int i = ht_first(0, n, [&](int x) {
+      const uint32_t t = ld_l2(tw + x);
+      return t_id(t) == (uint32_t)id && (t & (kTCont | kTEmpty)) == 0;
+    });
+    const int32_t p = i < 0 ? -1 : own_prefix(pl, sd, i);
+    if (lane_id() == 0) evp[q].pos = p;
+  }
+  vm_drain();
+}
+
 // MTE_DELTA_REFPOS (include/mte.h): every live reference of slots [0, rhi) as
 // a record that slid one left the document -- its position (as mte_read_refs;
 // -2 - its Transient position for one off the string, as
@@ -1947,6 +2104,7 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
   const int32_t s = op[0], msn = op[2];
   const bool lop = (flags & MTE_F_LOCAL) != 0;
   int rc;
+  h.born = (uint32_t)lseq + 1u;  // an item split off now is a tail of the pending groups
   h.min_seq = D.min_seq;
   h.cur_seq = D.cur_seq;
   if (type == MTE_OP_RELPOS) {
@@ -2053,13 +2211,14 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
     if (type == MTE_OP_ANNOTATE && (uint32_t)op[7] != MTE_NO_PROPS && (uint32_t)op[7] >= MTE_ANNOTATE_SLOTS)
       return MTE_E_INVALID_ARG;
     lseq = s;
+    h.born = (uint32_t)s;  // an item this op makes is one of its group's own
   } else if (ldoc && type <= MTE_OP_ANNOTATE && c == 0) {
     return MTE_E_INVALID_ARG;  // a remote op from the local client's own slot
   }
   if (type == MTE_OP_INSERT) {
     int at = -1;
     HPROF_BEGIN(t0)
-    rc = ht_insert<K, S>(h, op, lop, refd, a, st, at);
+    rc = ht_insert<K, S>(h, op, lop, refd, a, st, at, ev);
     HPROF_END(h, 0, t0)
     if (rc) return rc;
     if (evd) {  // insertSegments' delta callback (mergeTree.ts:1409-1416)
@@ -2074,7 +2233,7 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
   } else if (type == MTE_OP_ACK) {
     if (!(op[4] > 0 && op[4] <= op[5] && op[5] <= lseq)) return MTE_E_INVALID_ARG;
     HPROF_BEGIN(t0)
-    rc = ht_ack<K>(h, op, a, rt, refd ? rhi : 0u, evs ? &ev : nullptr);
+    rc = ht_ack<K>(h, op, a, rt, refd ? rhi : 0u, ev, evs);
     HPROF_END(h, 2, t0)
     if (rc) return rc;
   } else if (type != MTE_OP_NOOP) {
@@ -2083,7 +2242,7 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
   D.k++;
   if (lop) return 0;  // a local op moves no window and runs no zamboni
   if (type == MTE_OP_INSERT || type == MTE_OP_REMOVE || type == MTE_OP_ANNOTATE)
-    if ((rc = ht_zamboni<K>(h, a.n_keys))) return rc;
+    if ((rc = ht_zamboni<K>(h, a.n_keys, ev))) return rc;
   if (type != MTE_OP_NOOP) {  // Client.completeAndLogOp (client.ts:525-528)
     if (!(D.cur_seq < s)) return MTE_E_SEQ_ORDER;
     if (!(D.min_seq <= msn)) return MTE_E_MSN_ORDER;
@@ -2098,7 +2257,7 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
       D.min_seq = msn;
       h.min_seq = msn;
       h.cur_seq = D.cur_seq;
-      if ((rc = ht_zamboni<K>(h, a.n_keys))) return rc;
+      if ((rc = ht_zamboni<K>(h, a.n_keys, ev))) return rc;
     }
   }
   // the slides of this record, keyed by the units they left as they stand now,
@@ -2133,7 +2292,7 @@ __global__ __launch_bounds__(64) void htree_kernel(ReplayArgs a, HtreeArgs t) {
   h.hp = reinterpret_cast<uint32_t*>(t.heap + (uint64_t)doc * (t.hcap + 1));
   h.hcap = t.hcap;
   h.cap = (int)a.cap;
-  h.nP = ldoc ? kFieldPlanes + 3 * K + 3 : kFieldPlanes + K;
+  h.nP = ldoc ? kLocalPlanes<K> : kFieldPlanes + K;
   h.n = D.n;
   h.newcalc = (hf & MTE_DOC_NEW_LENGTH_CALC) != 0;
   h.ldoc = ldoc;
@@ -2147,6 +2306,7 @@ __global__ __launch_bounds__(64) void htree_kernel(ReplayArgs a, HtreeArgs t) {
   h.pc = 0;
   h.rpf = 0;
   h.lds = false;
+  h.maint = false;
 #ifdef MTE_HTREE_PROF
   for (int q = 0; q < kHtProf; q++) h.prof[q] = 0;
 #endif
@@ -2178,7 +2338,10 @@ __global__ __launch_bounds__(64) void htree_kernel(ReplayArgs a, HtreeArgs t) {
   if ((hf & MTE_DOC_EVENTS) && a.dl_off) {
     ev.p = a.dl + a.dl_off[doc];
     ev.cap = a.dl_off[doc + 1] - a.dl_off[doc];
+    h.maint = ldoc && (hf & MTE_DOC_MAINT_EVENTS) != 0;
   }
+  uint32_t msg_ev = 0;   // MTE_DELTA_MAINT: the first event of the message being applied
+  bool msg_open = false;  // its MSG_END not applied yet
   D.running = D.status == 0 && D.k < D.k1;
   extern __shared__ uint32_t ht_lds[];
   // LDS-resident while the document fits (ht_lds_room's margins)
@@ -2187,7 +2350,18 @@ __global__ __launch_bounds__(64) void htree_kernel(ReplayArgs a, HtreeArgs t) {
   while (D.running) {
     if (h.lds && !ht_lds_room(h)) ht_spill(h);
     HPROF_BEGIN(t_rec)
+    uint32_t w3 = 0u;
+    if (h.maint) {
+      if (!msg_open) msg_ev = ev.n;
+      w3 = (uint32_t)sload8(D.recp + 2 * D.k)[3];
+    }
     const int rc = ht_step<K, S>(h, D, st, a, lseq, ev, rhi);
+    if (h.maint && rc >= 0) {
+      // maintenance positions once the message (a local record: itself) is applied
+      msg_open = (w3 & 0xffu) == MTE_OP_RELPOS || !((w3 >> 16) & (MTE_F_MSG_END | MTE_F_LOCAL));
+      if (!msg_open && ev.n > msg_ev)
+        ht_maint_positions(h.pl, h.sd, h.tw, h.n, ev.p, ev.n < ev.cap ? ev.n : (uint32_t)ev.cap, msg_ev);
+    }
     HPROF_END(h, 6, t_rec)
 #ifdef MTE_HTREE_PROF
     h.prof[7]++;

@@ -38,7 +38,8 @@ const REF_SLIDE_ON_REMOVE = 0x40, REF_STAY_ON_REMOVE = 0x80, REF_TRANSIENT = 0x1
 const DELTA_REGEN = 0x10;    // MTE_DELTA_REGEN: kind flag of a regenerated op's records
 const ANNOTATE_SLOTS = 32;   // MTE_ANNOTATE_SLOTS: pending local annotate groups tracked per document
 const F_MARKER = 0x1, F_MSG_END = 0x2, F_REWRITE = 0x4, F_LOCAL = 0x8;
-const F_COMBINE = 0x10, COMBINE_PAIR = 0x80000000;  // incr / consensus value maps (include/mte.h)
+const F_COMBINE = 0x10, COMBINE_PAIR = 0x80000000;
+const F_REGENERATED = 0x20;  // an ack of a regenerated message (include/mte.h)  // incr / consensus value maps (include/mte.h)
 // a value id matching no other, itself included: NaN (matchProperties' !==, include/mte.h)
 const VALUE_UNEQUAL = 0x40000000;
 const LOCAL_SEQ_BASE = 0x40000000; // MTE_LOCAL_SEQ_BASE
@@ -214,6 +215,9 @@ class DocClients {
     this.localSeq = 0;
     this.pending = [];
     this.pendingTypes = [];  // the record types of each pending message (rollback)
+    // the first localSeqs of the pending messages regenerated since sent (their
+    // acks carry F_REGENERATED)
+    this.regenerated = new Set();
     // segment groups of pending local annotates: localSeq -> group slot; an
     // annotate made while all are taken is not tracked (cannot be regenerated)
     this.annSlot = new Map();
@@ -478,7 +482,8 @@ class BatchBuilder {
           }
           clients.noRollback.delete(ls);
         }
-        this._put(doc, seq, ref, msn, OP_ACK, 0, 0, lo, hi, mask, NO_PROPS);
+        const regen = clients.regenerated.delete(lo);
+        this._put(doc, seq, ref, msn, OP_ACK, 0, regen ? F_REGENERATED : 0, lo, hi, mask, NO_PROPS);
       } else {
         this._combLocal = clients.local;
         try {
@@ -679,6 +684,7 @@ class BatchBuilder {
       }
       aux.set(ls, recs);
     }
+    clients.regenerated.delete(lo);
     clients.pending.pop();
     clients.pendingTypes.pop();
     const src = this._src(doc);
@@ -727,6 +733,7 @@ class BatchBuilder {
       const src = this._src(doc);
       if (src) src.push({ msg: null, op: undefined, local: true, regen: true });
     }
+    clients.regenerated.add(lo);
     clients.pending.push(clients.pending.shift());
     clients.pendingTypes.push(clients.pendingTypes.shift());
     return idx;

@@ -30,7 +30,7 @@ import json
 
 import numpy as np
 
-from .abi import (COMBINE_PAIR, MTE_VALUE_UNEQUAL, F_COMBINE, F_LOCAL, F_MARKER, F_MSG_END, F_REWRITE, LOCAL_SEQ_BASE, MTE_E_CAPACITY, MTE_E_CLIENT_RANGE,
+from .abi import (COMBINE_PAIR, MTE_VALUE_UNEQUAL, F_COMBINE, F_LOCAL, F_REGENERATED, F_MARKER, F_MSG_END, F_REWRITE, LOCAL_SEQ_BASE, MTE_E_CAPACITY, MTE_E_CLIENT_RANGE,
                   MTE_E_INVALID_ARG, MTE_E_STATE, MTE_E_UNSUPPORTED, MTE_MAX_CLIENTS, NO_PROPS, OP_ACK, OP_ROLLBACK,
                   OP_REGEN, OP_RBKEY, OP_REF, OP_RELPOS, RP_BEFORE1, RP_BEFORE2, RP_POS1, RP_POS2,
                   ANNOTATE_SLOTS, REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE,
@@ -325,6 +325,12 @@ class DocClients:
         # (MTE_ANNOTATE_SLOTS, include/mte.h); an annotate made while all are
         # taken is not tracked and cannot be regenerated
         self.ann_slot = {}
+        # acks of such untracked annotates: the engine cannot tell their
+        # segments (no ACKNOWLEDGED maintenance record, MTE_DOC_MAINT_EVENTS)
+        self.untracked_acks = 0
+        # the first localSeqs of the pending messages regenerated since sent
+        # (their acks carry F_REGENERATED)
+        self.regenerated = set()
         # the keys -> value ids each pending local annotate set (its rollback
         # puts the older values back), and the annotates whose rollback the
         # engine cannot restate exactly (see BatchBuilder.add_rollback)
@@ -420,11 +426,13 @@ class BatchBuilder:
                     raise MergeTreeError(MTE_E_UNSUPPORTED, "ack out of localSeq order past a pending annotate "
                                          "(regenerate every pending op, in order)")
                 clients.pending.pop(0)
-                clients.pending_types.pop(0)
+                types = clients.pending_types.pop(0)
                 mask = 0
                 for ls in range(lo, hi + 1):
                     if ls in clients.ann_slot:
                         mask |= 1 << clients.ann_slot.pop(ls)
+                    elif types[ls - lo] == OP_ANNOTATE:
+                        clients.untracked_acks += 1
                     # an annotate acked under a later pending one on the same key:
                     # the engine keeps the value from before the first pending
                     # annotate, not this one's, so the later one's rollback
@@ -434,7 +442,9 @@ class BatchBuilder:
                         if ls2 > hi and keys.keys() & kv.keys():
                             clients.no_rollback.add(ls2)
                     clients.no_rollback.discard(ls)
-                recs.append((OP_ACK, 0, lo, hi, mask, NO_PROPS))
+                regen = lo in clients.regenerated
+                clients.regenerated.discard(lo)
+                recs.append((OP_ACK, F_REGENERATED if regen else 0, lo, hi, mask, NO_PROPS))
             else:
                 self._comb = (clients.local, seq)
                 try:
@@ -532,6 +542,7 @@ class BatchBuilder:
                                  NO_PROPS))
                 recs.append((0, 0, 0, OP_RBKEY, 0, F_LOCAL, k, ANNOTATE_SLOTS, 0, NO_PROPS))
             aux[ls] = recs
+        clients.regenerated.discard(lo)
         clients.pending.pop()
         clients.pending_types.pop()
         out = self.ops[doc]
@@ -570,6 +581,7 @@ class BatchBuilder:
                 slot = clients.ann_slot[ls]
             idx.append((len(out), ls, t))
             out.append((ls, 0, 0, OP_REGEN, 0, F_LOCAL, t, 0, slot, NO_PROPS))
+        clients.regenerated.add(lo)
         clients.pending.append(clients.pending.pop(0))
         clients.pending_types.append(clients.pending_types.pop(0))
         return idx

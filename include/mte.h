@@ -291,6 +291,13 @@ extern "C" {
  * window does not move (no MSG_END).  Only in MTE_DOC_LOCAL_CLIENT documents;
  * a local rewrite is MTE_E_UNSUPPORTED.                                       */
 #define MTE_F_LOCAL 0x0008u
+/* On an MTE_OP_ACK record: the acked message is a regenerated one (an
+ * MTE_OP_REGEN record re-sent its localSeqs since they were last sent).
+ * resetPendingDeltaToOps gives each re-sent segment an op and a segment group
+ * of its own (client.ts:802-857), so the message acks the segments one by one,
+ * in document order -- each with the tails split off it since, its own
+ * ACKNOWLEDGED maintenance record and its own zamboni pass.                 */
+#define MTE_F_REGENERATED 0x0020u
 /* Pending (unacked) seqs are held as MTE_LOCAL_SEQ_BASE + localSeq, above any
  * sequenced seq: UnassignedSequenceNumber normalised as in breakTie / nodeLength
  * (mergeTree.ts:1009-1016, 1713-1714).  Sequenced seqs must stay below it.     */

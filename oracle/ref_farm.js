@@ -147,7 +147,8 @@ function runSet(p) {
   if (p.maint) {
     clients.forEach((c, i) => {
       c.mergeTreeMaintenanceCallback = (args) => {
-        mbuf[i].push([args.operation, args.deltaSegments.map((d) => [d.segment, d.segment.cachedLength])]);
+        mbuf[i].push([args.operation, args.deltaSegments.map((d) => [d.segment, d.segment.cachedLength,
+          d.segment.ordinal])]);
       };
     });
   }
@@ -157,7 +158,8 @@ function runSet(p) {
   // callback's (the pieces, the segment appended to and the one appended)
   const settle = (i, at = events[i].length - 1) => {
     for (const [t, segs] of mbuf[i]) {
-      const r = segs.map(([sg, len]) => [sg.ordinal, clients[i].getPosition(sg), len]);
+      // (ordinals as the callback saw them: an unlinked segment keeps a stale one)
+      const r = segs.map(([sg, len, ord]) => [ord, clients[i].getPosition(sg), len]);
       if (t === -4) r.sort((a, b) => (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0));
       maint[i].push([at, t, r.map((x) => [x[1], x[2]])]);
     }

@@ -74,6 +74,14 @@ typedef struct {
    * tail split off later (splitAt's segmentGroups.copyTo appends it,
    * mergeTreeNodes.ts:505-534) */
   uint32_t gord;
+  /* the first localSeq whose segment group can hold this item as one of the
+   * segments its op marked (an item split off later joins the groups before it
+   * as a tail, appended: mergeTreeNodes.ts:505-534) */
+  uint32_t born;
+  /* a regenerated segment's group (resetPendingDeltaToOps gives each re-sent
+   * segment one, client.ts:851-854): 1 + the segment's id at its last
+   * regeneration, shared by the tails split off it since (MTE_F_REGENERATED) */
+  uint32_t rg;
   uint8_t member; /* doc_ack: in the group being acked */
 } item;
 
@@ -106,6 +114,7 @@ typedef struct {
   uint32_t *ref_anchor, *ref_state;
   uint32_t ref_cap, ref_hi;
   int32_t slide_gid; /* the localSeq whose removal group an ack is sliding (doc_ack) */
+  uint8_t in_lop;    /* applying a local op (item.born) */
   /* MTE_DOC_EVENTS: the last batch's delta events, the record being applied */
   mte_delta* dl;
   uint64_t dl_n, dl_cap;
@@ -181,6 +190,8 @@ static void compact(idoc* d) {
 }
 
 static uint32_t new_id(idoc* d) { return d->next_id++; }
+/* item.born for an item made now: during local op ls it is one of ls's own */
+static uint32_t born_now(const idoc* d) { return (uint32_t)d->local_seq + (d->in_lop ? 0u : 1u); }
 
 static item placeholder(uint8_t h) {
   item e;
@@ -590,6 +601,7 @@ static int boundary(idoc* d, int64_t pos) {
       d->written += 1;
       d->it[i].cont = 0;
       d->it[i].id = new_id(d);
+      d->it[i].born = born_now(d);
       split_cascade(d, i);
       return maint_split(d, i);
     }
@@ -607,6 +619,7 @@ static int boundary(idoc* d, int64_t pos) {
       tl->h = 0;
       tl->cont = 0;
       tl->id = new_id(d);
+      tl->born = born_now(d);
       tl->gord = 0x80000000u | tl->id;
       d->written += 2;
       hd->len = off;
@@ -1193,6 +1206,7 @@ static int tree_insert(idoc* d, const mte_op* op, const env_t* env, int local, i
   nw.cli = c;
   nw.rseq = NONE_SEQ;
   nw.id = new_id(d);
+  nw.born = born_now(d);
   d->written += 1;
   if (is_marker) {
     nw.kind = 1u + (uint32_t)op->pos2;
@@ -1317,7 +1331,14 @@ static int doc_regen(idoc* d, const mte_op* op);
 /* A local op (MTE_F_LOCAL): insertSegmentLocal / removeRangeLocal /
  * annotateRangeLocal (client.ts:131-229) with seq Unassigned, or one of the
  * local records (rollback, regeneration, reference). */
+static int doc_apply_local_op(idoc* d, const mte_op* op, const env_t* env);
 static int doc_apply_local(idoc* d, const mte_op* op, const env_t* env) {
+  d->in_lop = 1;
+  const int rc = doc_apply_local_op(d, op, env);
+  d->in_lop = 0;
+  return rc;
+}
+static int doc_apply_local_op(idoc* d, const mte_op* op, const env_t* env) {
   const int32_t ls = op->seq;
   int rc;
   /* a length update drops the cached local partials (mergeTree.ts:2105-2110,
@@ -1487,6 +1508,7 @@ static int doc_regen(idoc* d, const mte_op* op) {
        * taken by ordinal (client.ts:802, 852): the ack slides them in document
        * order, split tails included */
       if (t == MTE_OP_REMOVE) g->gord = i;
+      g->rg = g->cont ? d->it[i - 1].rg : 1u + g->id;
       /* findReconnectionPosition (client.ts:709-713): getPosition with the
        * localSeq, block lengths from the local partials (view_prefix) */
       if (g->cont && last == (int64_t)i - 1 && d->dl_n) d->dl[d->dl_n - 1].len += g->len;
@@ -1500,11 +1522,86 @@ static int doc_regen(idoc* d, const mte_op* op) {
   return MTE_OK;
 }
 
+/* an item the ack of ls still has to take: inserted, removed or annotated by
+ * ls (am_mask: ls's annotate slot), or a removal of ls a remote one overtook */
+static inline int ack_pending(const item* g, int32_t ls, uint32_t am_mask) {
+  return !g->empty && (g->seq == LOCAL_BASE + ls || g->lrs == ls || g->rseq == LOCAL_BASE + ls || (g->am & am_mask));
+}
+
+/* ackPendingSegment (mergeTree.ts:1278-1331) for one segment group of ls: the
+ * items whose regeneration key is `key` (-1: every item of ls) get the seq,
+ * each is added to the LRU set in the group's order, the references of the
+ * acked removals slide, the ACKNOWLEDGED callback reports the group, then
+ * zamboniSegments runs. */
+static int ack_group(idoc* d, int32_t ls, int32_t s, uint32_t am_mask, int64_t key, const env_t* env) {
+  int rc;
+  for (uint32_t i = 0; i < d->n; i++) {
+    item* g = &d->it[i];
+    if (g->empty || (key >= 0 && g->rg != (uint32_t)key)) continue;
+    int member = 0;
+    if (g->seq == LOCAL_BASE + ls) {
+      g->seq = s;
+      member = 1;
+    }
+    if (g->lrs == ls) { /* acked, or overtaken by a remote remove before (:1928-1938) */
+      g->lrs = 0;
+      member = 1;
+    }
+    if (g->rseq == LOCAL_BASE + ls) {
+      g->rseq = s;
+      /* the group's removals hold ls until they have slid (doc_slide_refs'
+       * group mark; a regenerated one's localRemovedSeq is its old op's);
+       * acked: localRemovedSeq undefined (mergeTreeNodes.ts:493) */
+      g->lrs = ((d->flags & MTE_DOC_REFS) && d->ref_hi) ? ls : 0;
+    }
+    if (g->am & am_mask) {
+      g->am &= ~am_mask;
+      member = 1;
+    }
+    g->member = member && !g->cont;
+  }
+  /* addToLRUSet per segment in the group's order: the segments the op marked
+   * in document order, then the tails split off since, as they were made */
+  for (uint32_t i = 0; i < d->n; i++)
+    if (d->it[i].member && d->it[i].born <= (uint32_t)ls && (rc = add_lru(d, i, s))) return rc;
+  for (uint32_t last = 0, any = 1; any;) {
+    int64_t bx = -1;
+    for (uint32_t i = 0; i < d->n; i++) {
+      const item* g = &d->it[i];
+      if (g->member && g->born > (uint32_t)ls && g->id >= last && (bx < 0 || g->id < d->it[bx].id)) bx = i;
+    }
+    any = bx >= 0;
+    if (any) {
+      if ((rc = add_lru(d, (uint32_t)bx, s))) return rc;
+      last = d->it[bx].id + 1u;
+    }
+  }
+  d->slide_gid = ls;  /* this localSeq's group, in its order (ackPendingSegment per group op) */
+  if ((rc = doc_slide_refs(d, s, 1))) return rc;
+  /* ACKNOWLEDGED (mergeTree.ts:1313-1320): the group's segments, after their slides */
+  if (d->flags & MTE_DOC_MAINT_EVENTS) {
+    uint32_t idx = 0;
+    for (uint32_t i = 0; i < d->n; i++)
+      if (d->it[i].member && (rc = maint_push(d, MTE_MAINT_ACK, d->it[i].id, leaf_total(d, i, leaf_end(d, i)), idx++)))
+        return rc;
+  }
+  for (uint32_t i = 0; i < d->n; i++) {
+    item* g = &d->it[i];
+    if (key >= 0 && g->rg != (uint32_t)key) continue;
+    if (g->lrs == ls) g->lrs = 0;
+    g->member = 0;
+  }
+  zamboni(d, env->arena, env->n_keys);
+  return MTE_OK;
+}
+
 /* MTE_OP_ACK for localSeqs pos1..pos2 (client.ts:640-672 acks a GROUP's members
- * one by one): per localSeq, ackPendingSegment (mergeTree.ts:1278-1331) acks its
- * group's segments, slides the references of the acked removals, adds each
- * segment to the LRU set, then runs zamboniSegments.  The slot mask op->a frees
- * the annotate groups (all of them with the last localSeq of the record). */
+ * one by one): per localSeq, ackPendingSegment acks its group.  A regenerated
+ * message (MTE_F_REGENERATED) re-sent each segment of a localSeq as an op of
+ * its own with a group of its own (resetPendingDeltaToOps, client.ts:802-857):
+ * it acks them one by one, in document order, each group the segment and the
+ * tails split off it since.  The slot mask op->a frees the annotate groups (all of them
+ * with the last localSeq of the record). */
 static int doc_ack(idoc* d, const mte_op* op, const env_t* env) {
   const int32_t lo = op->pos1, hi = op->pos2, s = op->seq;
   int rc;
@@ -1513,46 +1610,20 @@ static int doc_ack(idoc* d, const mte_op* op, const env_t* env) {
     const uint32_t am_mask = ls == hi ? op->a : 0u;
     for (uint32_t i = 0; i < d->n; i++) {
       item* g = &d->it[i];
-      if (g->empty) continue;
-      int member = 0;
-      if (g->seq == LOCAL_BASE + ls) {
-        g->seq = s;
-        member = 1;
-      }
-      if (g->lrs == ls) { /* acked, or overtaken by a remote remove before (:1928-1938) */
-        g->lrs = 0;
-        member = 1;
-      }
-      if (g->rseq == LOCAL_BASE + ls) {
-        g->rseq = s;
-        /* the group's removals hold ls until they have slid (doc_slide_refs'
-         * group mark; a regenerated one's localRemovedSeq is its old op's);
-         * acked: localRemovedSeq undefined (mergeTreeNodes.ts:493) */
-        g->lrs = ((d->flags & MTE_DOC_REFS) && d->ref_hi) ? ls : 0;
-      }
       for (uint32_t k = 0; k < MTE_MAX_KEYS; k++)
         if (g->pk[k] && g->pk[k] <= (uint32_t)ls) g->pk[k] = 0;
-      if (g->am & am_mask) {
-        g->am &= ~am_mask;
-        member = 1;
-      }
-      if (member && !g->cont && (rc = add_lru(d, i, s))) return rc;
-      g->member = member && !g->cont;
     }
-    d->slide_gid = ls;  /* this localSeq's group, in its order (ackPendingSegment per group op) */
-    if ((rc = doc_slide_refs(d, s, 1))) return rc;
-    /* ACKNOWLEDGED (mergeTree.ts:1313-1320): the group's segments, after their slides */
-    if (d->flags & MTE_DOC_MAINT_EVENTS) {
-      uint32_t idx = 0;
-      for (uint32_t i = 0; i < d->n; i++)
-        if (d->it[i].member && (rc = maint_push(d, MTE_MAINT_ACK, d->it[i].id, leaf_total(d, i, leaf_end(d, i)), idx++)))
-          return rc;
+    if (!(op->flags & MTE_F_REGENERATED)) {
+      if ((rc = ack_group(d, ls, s, am_mask, -1, env))) return rc;
+      continue;
     }
-    for (uint32_t i = 0; i < d->n; i++) {
-      if (d->it[i].lrs == ls) d->it[i].lrs = 0;
-      d->it[i].member = 0;
+    for (;;) {
+      int64_t first = -1;
+      for (uint32_t i = 0; i < d->n && first < 0; i++)
+        if (ack_pending(&d->it[i], ls, am_mask)) first = i;
+      if (first < 0) break;
+      if ((rc = ack_group(d, ls, s, am_mask, d->it[first].rg, env))) return rc;
     }
-    zamboni(d, env->arena, env->n_keys);
   }
   return MTE_OK;
 }

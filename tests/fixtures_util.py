@@ -323,7 +323,10 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_reg
                 if kind == "L":
                     bb.add_local(d, clients[d], m["contents"])
                 else:
+                    u0 = clients[d].untracked_acks
                     bb.add_message(d, clients[d], m)
+                    if maint is not None and clients[d].untracked_acks != u0:
+                        maint.setdefault(("untracked", si, ci), []).append(ei)
             prev[d] = done
         eng.apply_batch(bb.build())
         st = eng.statuses()

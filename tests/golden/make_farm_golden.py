@@ -38,7 +38,12 @@ string values among the numbers) or consensus on id'd markers
 (annotateMarkerNotifyConsensus), in both length calculations; the observer's
 state is what a document of sequenced ops alone must equal.
 
-Usage: python3 tests/golden/make_farm_golden.py [--refs | --stay | --combine | --legacy | --relpos]
+With --maint it writes tests/golden/maint_farm_vectors.json.gz: farms that also
+record every client's mergeTreeMaintenanceCallback (SPLIT / APPEND / UNLINK /
+ACKNOWLEDGED): per event the callbacks it raised, each segment's position once
+the event is applied and its length at the callback.
+
+Usage: python3 tests/golden/make_farm_golden.py [--refs | --stay | --combine | --legacy | --relpos | --maint]
 """
 import gzip
 import json
@@ -58,6 +63,7 @@ OUT_STAY = os.path.join(HERE, "localref_stay_vectors.json.gz")
 OUT_COMBINE = os.path.join(HERE, "combine_farm_vectors.json.gz")
 OUT_LEGACY = os.path.join(HERE, "legacy_farm_vectors.json.gz")
 OUT_RELPOS = os.path.join(HERE, "relpos_farm_vectors.json.gz")
+OUT_MAINT = os.path.join(HERE, "maint_farm_vectors.json.gz")
 FARM_JS = os.path.join(ROOT, "oracle", "ref_farm.js")
 
 # (seed, clients incl. the observer, steps, initial text, checkpoints, text bound)
@@ -121,6 +127,45 @@ RELPOS_SETS = ([(9000 + i, 2 + i % 6, 300 + 100 * (i % 4), ["", "hello world", "
                 for i in range(8)] +
                [(9300 + i, 2 + i % 6, 300 + 100 * (i % 4), ["", "hello world"][i % 2], 4, 200,
                  {"relpos": 0.3, "legacy": True, "allowDiverge": True}) for i in range(12)])
+
+
+# maintenance callbacks (--maint): (seed, clients, steps, initial text,
+# checkpoints, text bound, extra parameters): plain farms (lagging clients:
+# splits, acks, the lazy zamboni's appends and unlinks), rollbacks, references,
+# the legacy length calculation, long farms (more zamboni work) and reconnects
+MAINT_SETS = ([(10000 + i, 2 + i % 6, 300 + 150 * (i % 4), ["", "hello world", "abc\ndef"][i % 3], 4,
+                [64, 200][i % 2], {}) for i in range(12)] +
+              [(10100 + i, 3 + i % 4, 400, "hello world", 4, 200, {"rollback": 0.15, "rollbackTypes": [1, 2]})
+               for i in range(6)] +
+              [(10200 + i, 3 + i % 4, 400, ["hello world", ""][i % 2], 4, 200, {"refs": 0.2}) for i in range(4)] +
+              [(10300 + i, 3 + i % 4, 400, "hello world", 4, 200, {"legacy": True, "allowDiverge": True})
+               for i in range(6)] +
+              [(10400 + i, 4, 1500, "the quick brown fox", 6, 120, {}) for i in range(4)] +
+              [(10500 + i, 3 + i % 4, 400, "hello world", 4, 200, {"reconnect": 0.1, "allowDiverge": True})
+               for i in range(6)])
+
+
+def main_maint(out):
+    res = {"sets": [], "generator": "oracle/ref_farm.js with maint (reference Client, mulberry32 seeds)"}
+    failed = []
+    for sd, c, n, t, k, m, extra in MAINT_SETS:
+        one = dict({"seed": sd, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
+                    "rollback": 0.0, "maint": True}, **extra)
+        q = subprocess.run(["node", FARM_JS, out], input=json.dumps({"sets": [one]}), capture_output=True, text=True,
+                           timeout=600)
+        if q.returncode == 0:
+            res["sets"] += json.loads(q.stdout)["sets"]
+        else:
+            failed.append(sd)
+    res["seeds_the_reference_failed"] = failed
+    with gzip.open(OUT_MAINT, "wt", encoding="utf-8") as fh:
+        json.dump(res, fh, separators=(",", ":"))
+    kinds = {}
+    for s in res["sets"]:
+        for cl in s["maint"]:
+            for e in cl:
+                kinds[e[1]] = kinds.get(e[1], 0) + 1
+    print(f"wrote {OUT_MAINT}: {len(res['sets'])} farms, callbacks by type {kinds}, reference failed on {failed}")
 
 
 def main_relpos(out):
@@ -222,6 +267,8 @@ def main():
         return main_legacy(out)
     if "--relpos" in sys.argv[1:]:
         return main_relpos(out)
+    if "--maint" in sys.argv[1:]:
+        return main_maint(out)
     inp = {"sets": [{"seed": s, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
                      "rollback": rb} for s, c, n, t, k, m, rb in SETS]}
     p = subprocess.run(["node", "--max-old-space-size=8192", FARM_JS, out], input=json.dumps(inp),

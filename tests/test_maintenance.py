@@ -1,0 +1,95 @@
+"""mergeTreeMaintenanceCallback records (MTE_DOC_MAINT_EVENTS, MTE_DELTA_MAINT;
+mergeTree.ts:695-725, 1313-1320, 1687-1694): SPLIT, APPEND, UNLINK and
+ACKNOWLEDGED, the structural changes SharedString reports as "maintenance"
+events (sequence.ts:212-216, SequenceMaintenanceEvent).
+
+Pinned by 38 farms the reference itself ran with every client's callback
+recorded (oracle/ref_farm.js maint -> tests/golden/maint_farm_vectors.json.gz,
+made by tests/golden/make_farm_golden.py --maint): per event of every client
+(its local ops, rollbacks and the messages it applied, its own as acks) the
+callbacks in order, each with its segments' positions once the event is
+applied and their lengths at the callback.  Plain farms with lagging clients,
+rollbacks, local references, the legacy length calculation and long farms
+(the lazy zamboni's appends) and reconnect farms (an ack of a regenerated op
+acknowledges each re-sent segment as a group of its own, one callback and one
+zamboni each: resetPendingDeltaToOps, client.ts:802-857) match exactly, on the
+tree restatement (titems.c), on the GPU (the HBM tree pass) and through the
+Node host -- except the ACKNOWLEDGED callback of an annotate made while
+MTE_ANNOTATE_SLOTS (32) others were pending, which the engine does not track
+(check() leaves those out and counts them).
+"""
+import gzip
+import json
+import os
+
+import pytest
+
+from fixtures_util import replay_ref_farm
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+VECTORS = os.path.join(HERE, "golden", "maint_farm_vectors.json.gz")
+
+
+def maint_sets():
+    with gzip.open(VECTORS, "rt", encoding="utf-8") as fh:
+        return json.load(fh)["sets"]
+
+
+def tree_factory(k):
+    from oracle import OracleEngine
+    e = OracleEngine(k, tree="items")
+    e.lib.oti_set_limit(e.ctx, 1 << 20)
+    return e
+
+
+def device_factory(k):
+    from fluidframework_amd.engine import DeviceEngine
+    return DeviceEngine(k)
+
+
+def check(factory, sets):
+    """(clients whose callback lists equal the reference's, clients, the acks
+    of untracked annotates skipped, first difference).  An annotate made while
+    MTE_ANNOTATE_SLOTS others are pending has no segment group in the engine:
+    the reference's ACKNOWLEDGED callback at its ack is left out (the host
+    counts those acks, DocClients.untracked_acks)."""
+    got = {}
+    passed, failures = replay_ref_farm(factory, sets, maint=got)
+    assert not failures, failures[:2]
+    equal, first, skipped = 0, None, 0
+    for si, s in enumerate(sets):
+        for ci in range(len(s["names"])):
+            g, w = got.get((si, ci), []), s["maint"][ci]
+            untracked = set(got.get(("untracked", si, ci), []))
+            if untracked:
+                skipped += sum(1 for x in w if x[1] == -4 and x[0] in untracked)
+                w = [x for x in w if not (x[1] == -4 and x[0] in untracked)]
+            if g == w:
+                equal += 1
+            elif first is None:
+                k = 0
+                while k < min(len(g), len(w)) and g[k] == w[k]:
+                    k += 1
+                first = (si, ci, k, g[k:k + 2], w[k:k + 2])
+    n = sum(len(s["names"]) for s in sets)
+    return equal, n, skipped, first
+
+
+def test_maint_vectors_shape():
+    sets = maint_sets()
+    assert len(sets) == 38
+    kinds = [e[1] for s in sets for cl in s["maint"] for e in cl]
+    assert {-1, -2, -3, -4} <= set(kinds) and kinds.count(-1) > 100
+
+
+def test_tree_oracle_maintenance_callbacks():
+    equal, n, skipped, first = check(tree_factory, maint_sets())
+    assert equal == n, first
+    assert skipped < 10, skipped
+
+
+@pytest.mark.gpu
+def test_gpu_maintenance_callbacks():
+    equal, n, skipped, first = check(device_factory, maint_sets())
+    assert equal == n, first
+    assert skipped < 10, skipped
