@@ -51,6 +51,9 @@ function loadAddon() {
 const ASSERT_CODES = { "-5": 0x030, "-6": 0x031, "-7": 0x039 };
 const DELTA_SLIDE = 0x40;  // MTE_DELTA_SLIDE (include/mte.h): a reference slid off a removed segment
 const DELTA_REFPOS = 0x80;  // MTE_DELTA_REFPOS: the references' positions after a group op's member
+const DELTA_MAINT = 0x100;  // MTE_DELTA_MAINT | type: a mergeTreeMaintenanceCallback segment
+// MergeTreeMaintenanceType (mergeTreeDeltaCallback.ts): MTE_MAINT_* t -> -t
+const MAINT_NAMES = { [-1]: "append", [-2]: "split", [-3]: "unlink", [-4]: "acknowledged" };
 
 function docError(code, doc) {
   const a = loadAddon();
@@ -128,12 +131,17 @@ class MergeTreeEngine {
       throw new MergeTreeError(-9, "roundSync with a local client or delta events");
     }
     if (o.refs && !o.localClient) throw new MergeTreeError(-9, "local references need {localClient: true}");
+    if (o.maintenanceEvents && !(o.localClient && o.events)) {
+      throw new MergeTreeError(-9, "maintenance events need {localClient: true, events: true}");
+    }
     this.docs.push({ text: initialText || "", newLengthCalc: !!o.newLengthCalc, roundSync: !!o.roundSync, props: o.props,
       minSeq: o.minSeq || 0, currentSeq: o.currentSeq || 0, segments: o.segments, localClient: !!o.localClient,
       events: !!o.events, refs: !!o.refs,
       // an interval collection's mid-op events need the references' slides
       // (MTE_DOC_SLIDE_EVENTS): on with events and references unless asked off
-      slideEvents: !!(o.events && o.refs && o.slideEvents !== false) });
+      slideEvents: !!(o.events && o.refs && o.slideEvents !== false),
+      // SharedString's "maintenance" events (MTE_DOC_MAINT_EVENTS)
+      maintenanceEvents: !!o.maintenanceEvents });
     const c = new BatchClient(this, doc, o.observerId === undefined ? (o.longClientId || "A") : o.observerId,
       !!o.localClient);
     this.clients.push(c);
@@ -571,12 +579,37 @@ class BatchClient {
   // inserted spec for an insert, else undefined: the engine keeps no segment
   // objects.  They arrive at the flush, not synchronously with applyMsg.
 
-  /** on("sequenceDelta", listener(event, client)) */
+  /** on("sequenceDelta", listener(event, client)); on("maintenance",
+   *  listener(event, client)) in a document created with {maintenanceEvents:
+   *  true}: SharedString's "maintenance" events (sequence.ts:212-216,
+   *  SequenceMaintenanceEvent), one per mergeTreeMaintenanceCallback --
+   *  deltaOperation the MergeTreeMaintenanceType (APPEND -1, SPLIT -2, UNLINK
+   *  -3, ACKNOWLEDGED -4), opArgs {op, sequencedMessage} of the op that caused
+   *  it (undefined for a local op's), ranges {operation, position, length,
+   *  propertyDeltas, segment} in document order: the segments' positions once
+   *  the op's message is applied (-1: unlinked) and their lengths at the
+   *  callback; segment undefined (the engine keeps no segment objects). */
   on(name, listener) {
-    if (name !== "sequenceDelta") throw new MergeTreeError(-9, "only sequenceDelta events are delivered");
+    if (name === "maintenance") {
+      if (!this.engine.docs[this.doc].maintenanceEvents) {
+        throw new MergeTreeError(-9, "createClient(..., {maintenanceEvents: true}) first");
+      }
+      (this.maintListeners || (this.maintListeners = [])).push(listener);
+      return this;
+    }
+    if (name !== "sequenceDelta") throw new MergeTreeError(-9, "only sequenceDelta and maintenance events are delivered");
     if (!this.engine.docs[this.doc].events) throw new MergeTreeError(-9, "createClient(..., {events: true}) first");
     (this.listeners || (this.listeners = [])).push(listener);
     return this;
+  }
+
+  _maint(list, src) {
+    for (const m of list) {
+      const ev = { deltaOperation: m.t, operation: MAINT_NAMES[m.t], ranges: m.ranges, first: m.ranges[0],
+        last: m.ranges[m.ranges.length - 1], clientId: this.longClientId,
+        opArgs: src ? { op: src.op, sequencedMessage: src.local ? undefined : src.msg } : undefined };
+      for (const fn of this.maintListeners || []) fn(ev, this);
+    }
   }
 
   /** Messages since the last minSeq change, catch-up ops rewritten as
@@ -636,9 +669,21 @@ class BatchClient {
       }
       const ranges = [];
       let kind = -1;
-      let slides = null, snap = null;
+      let slides = null, snap = null, mBefore = null, mAfter = null;
       while (i < n && flat[5 * i] === k) {
         const kd = flat[5 * i + 1];
+        if ((kd & 0xff00) === DELTA_MAINT) {
+          // a maintenance callback's segment (MTE_DELTA_MAINT): the callbacks
+          // before the op's delta ranges (its splits) and after them
+          const t = -(kd & 0xff);
+          const list = ranges.length ? (mAfter || (mAfter = [])) : (mBefore || (mBefore = []));
+          const r = { operation: t, position: flat[5 * i + 2] | 0, length: flat[5 * i + 3], propertyDeltas: {},
+            segment: undefined };
+          if (flat[5 * i + 4] === 0 || !list.length || list[list.length - 1].t !== t) list.push({ t, ranges: [r] });
+          else list[list.length - 1].ranges.push(r);
+          i++;
+          continue;
+        }
         if ((kd & 0xff) === DELTA_REFPOS) {  // slot -> [position, Transient position, order key]
           const p = flat[5 * i + 2] | 0;
           (snap || (snap = new Map())).set(flat[5 * i + 4], [p < -1 ? -1 : p, p < -1 ? -2 - p : p, flat[5 * i + 3] | 0]);
@@ -657,7 +702,7 @@ class BatchClient {
           segment: kind === 0 && src.op ? src.op.seg : undefined });
         i++;
       }
-      parsed[k] = { kind, ranges, slides, snap };
+      parsed[k] = { kind, ranges, slides, snap, mBefore, mAfter };
     }
     // the references as record k left the document (MTE_DELTA_REFPOS): a
     // reference sliding there sees the document at that moment -- inside a
@@ -679,11 +724,13 @@ class BatchClient {
         flushMsg();
         cur = { msg: src.msg, ops: [] };
       }
-      const { kind, ranges, slides } = pr;
-      if (kind < 0) {
+      const { kind, ranges, slides, mBefore, mAfter } = pr;
+      if (kind < 0) {  // an ack: its slides come before its ACKNOWLEDGED callback
         if (slides) this._slid(slides, backTo(k));
+        if (mBefore) this._maint(mBefore, src);
         continue;
       }
+      if (mBefore) this._maint(mBefore, src);
       if (cur) cur.ops.push(...opsFromDelta(kind, ranges, src.op));
       const ev = { deltaOperation: kind, operation: kinds[kind], isLocal: src.local,
         message: src.local ? undefined : src.msg, ranges, first: ranges[0], last: ranges[ranges.length - 1] };
@@ -691,6 +738,7 @@ class BatchClient {
       // markRangeRemoved slides the newly removed segments' references after
       // the delta callback (mergeTree.ts:1978-1993)
       if (slides) this._slid(slides, backTo(k));
+      if (mAfter) this._maint(mAfter, src);
     }
     flushMsg();
   }

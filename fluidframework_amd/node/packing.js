@@ -57,6 +57,7 @@ const DOC_LOCAL_CLIENT = 0x4; // MTE_DOC_LOCAL_CLIENT
 const DOC_REFS = 0x10;       // MTE_DOC_REFS
 const DOC_EVENTS = 0x8; // MTE_DOC_EVENTS
 const DOC_SLIDE_EVENTS = 0x20;  // MTE_DOC_SLIDE_EVENTS: the references' slides and their snapshots
+const DOC_MAINT_EVENTS = 0x40;  // MTE_DOC_MAINT_EVENTS: mergeTreeMaintenanceCallback records
 const E_INVALID_ARG = -1, E_CAPACITY = -4, E_UNSUPPORTED = -9, E_STATE = -10, E_CLIENT_RANGE = -12;
 const COMBINE_DOMAIN_MAX = 4096;  // distinct values of one key a combining op's value map may cover
 const DEFAULT_REF_CAPACITY = 1024;  // mte_set_ref_capacity's default (include/mte.h)
@@ -218,6 +219,9 @@ class DocClients {
     // the first localSeqs of the pending messages regenerated since sent (their
     // acks carry F_REGENERATED)
     this.regenerated = new Set();
+    // acks of annotates made while every slot was taken: the engine cannot
+    // tell their segments (no ACKNOWLEDGED maintenance record)
+    this.untrackedAcks = 0;
     // segment groups of pending local annotates: localSeq -> group slot; an
     // annotate made while all are taken is not tracked (cannot be regenerated)
     this.annSlot = new Map();
@@ -465,12 +469,14 @@ class BatchBuilder {
           }
         }
         clients.pending.shift();
-        clients.pendingTypes.shift();
+        clients.pendingAckTypes = clients.pendingTypes.shift();
         let mask = 0;
         for (let ls = lo; ls <= hi; ls++) {
           if (clients.annSlot.has(ls)) {
             mask |= 1 << clients.annSlot.get(ls);
             clients.annSlot.delete(ls);
+          } else if (clients.pendingAckTypes && clients.pendingAckTypes[ls - lo] === OP_ANNOTATE) {
+            clients.untrackedAcks++;
           }
           // an annotate acked under a later pending one on the same key (packing.py)
           const keys = clients.annProps.get(ls);
@@ -1040,7 +1046,7 @@ function packDocInits(docs, interner) {
     buf.writeUInt32LE(d.text.length, o + 4);
     buf.writeUInt32LE((d.newLengthCalc ? DOC_NEW_LENGTH_CALC : 0) | (d.roundSync ? DOC_ROUND_SYNC : 0) |
       (d.localClient ? DOC_LOCAL_CLIENT : 0) | (d.events ? DOC_EVENTS : 0) | (d.refs ? DOC_REFS : 0) |
-      (d.slideEvents ? DOC_SLIDE_EVENTS : 0), o + 8);
+      (d.slideEvents ? DOC_SLIDE_EVENTS : 0) | (d.maintenanceEvents ? DOC_MAINT_EVENTS : 0), o + 8);
     buf.writeUInt32LE(props.add(d.props) >>> 0, o + 12);
     buf.writeInt32LE(d.minSeq || 0, o + 16);
     buf.writeInt32LE(d.currentSeq || 0, o + 20);

@@ -93,3 +93,29 @@ def test_gpu_maintenance_callbacks():
     equal, n, skipped, first = check(device_factory, maint_sets())
     assert equal == n, first
     assert skipped < 10, skipped
+
+
+def _node_farm(mode):
+    import subprocess
+    root = os.path.dirname(HERE)
+    r = subprocess.run(["node", "tests/node/maint_farm.js", mode], cwd=root, capture_output=True, text=True,
+                       timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_node_maintenance_events_on_restatement():
+    """SharedString "maintenance" events through the Node host
+    (BatchClient.on("maintenance"), tests/node/maint_farm.js) over the CPU
+    restatement's addon: every client of the 38 farms gets the reference's
+    callback list, event by event."""
+    j = _node_farm("oracle")
+    assert j["equal"] == j["clients"] == sum(len(s["names"]) for s in maint_sets()), j["first"]
+    assert j["callbacks"] > 30000 and j["skipped"] < 10, j
+
+
+@pytest.mark.gpu
+def test_gpu_node_maintenance_events():
+    j = _node_farm("gpu")
+    assert j["equal"] == j["clients"], j["first"]
+    assert j["skipped"] < 10, j
