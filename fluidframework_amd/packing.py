@@ -143,6 +143,7 @@ class PropTable:
         self.interner = interner
         self.sets = []
         self.entries = []
+        self.comb_of = {}  # a combining set's index -> (props, combiningOp)
 
     def add(self, props: dict) -> int:
         if props is None:
@@ -181,6 +182,7 @@ class PropTable:
             self.entries.append((k, len(pairs)))
             self.entries.extend(pairs)
         self.sets.append((first, len(self.entries) - first))
+        self.comb_of[len(self.sets) - 1] = (props, comb)
         return len(self.sets) - 1
 
     def arrays(self):
@@ -335,6 +337,8 @@ class DocClients:
         # puts the older values back), and the annotates whose rollback the
         # engine cannot restate exactly (see BatchBuilder.add_rollback)
         self.ann_props = {}
+        # the pending local incr / consensus annotates: localSeq -> (props, combiningOp)
+        self.ann_comb = {}
         self.no_rollback = set()
         # local reference slots (MTE_DOC_REFS documents): the next unused one and
         # the removed ones, reused first
@@ -444,7 +448,15 @@ class BatchBuilder:
                     clients.no_rollback.discard(ls)
                 regen = lo in clients.regenerated
                 clients.regenerated.discard(lo)
-                recs.append((OP_ACK, F_REGENERATED if regen else 0, lo, hi, mask, NO_PROPS))
+                flags, stamp = F_REGENERATED if regen else 0, NO_PROPS
+                comb = clients.ann_comb.pop(hi, None)
+                if comb is not None and comb[1].get("name") == "consensus":
+                    # updateConsensusProperty: the marker's consensus value takes the seq
+                    stamp = self.props.add_combining(comb[0], comb[1], seq)
+                    flags |= F_COMBINE
+                for ls in range(lo, hi):
+                    clients.ann_comb.pop(ls, None)
+                recs.append((OP_ACK, flags, lo, hi, mask, stamp))
             else:
                 self._comb = (clients.local, seq)
                 try:
@@ -478,11 +490,31 @@ class BatchBuilder:
         if not clients.local:
             raise MergeTreeError(MTE_E_UNSUPPORTED, "local op in an observer document")
         recs = []
-        self._op_records(op, recs)
+        # a local incr / consensus: its value map at seq UnassignedSequenceNumber
+        # (-1), what annotateRange makes of every value (segmentPropertiesManager.ts:141)
+        self._comb = (True, -1)
+        try:
+            self._op_records(op, recs)
+        finally:
+            self._comb = None
         if not recs:
             recs.append((OP_NOOP, 0, 0, 0, 0, NO_PROPS))
         if any(t != OP_RELPOS and f & F_REWRITE for t, f, *_ in recs):
             raise MergeTreeError(MTE_E_UNSUPPORTED, "local combiningOp rewrite")
+        # a local consensus is annotateMarkerNotifyConsensus's (client.ts:137-158):
+        # its ack stamps the marker's consensus value with the seq
+        # (updateConsensusProperty, :646-650, 1083-1090), which needs the op's own
+        # group slot and a message of that op alone; a consensus over a range
+        # fails at its ack in the reference (relativePos1 undefined)
+        cons = [i for i, r in enumerate(recs) if r[0] == OP_ANNOTATE and r[1] & F_COMBINE and
+                self.props.comb_of[r[4]][1].get("name") == "consensus"]
+        if cons:
+            if len([r for r in recs if r[0] != OP_RELPOS]) != 1 or recs[0][0] != OP_RELPOS:
+                raise MergeTreeError(MTE_E_UNSUPPORTED, "a local consensus annotate is a marker's "
+                                     "(annotateMarkerNotifyConsensus), alone in its message")
+            if len(clients.ann_slot) >= ANNOTATE_SLOTS:
+                raise MergeTreeError(MTE_E_UNSUPPORTED, f"a local consensus annotate with {ANNOTATE_SLOTS} "
+                                     "annotates pending")
         first = clients.local_seq + 1
         n_ops = sum(1 for r in recs if r[0] != OP_RELPOS)
         if first + n_ops >= LOCAL_SEQ_BASE:
@@ -500,7 +532,16 @@ class BatchBuilder:
                     clients.ann_slot[first + i] = free
                     b = free
                 f0, cnt = self.props.sets[a]
-                clients.ann_props[first + i] = dict(self.props.entries[f0:f0 + cnt])
+                if flags & F_COMBINE:
+                    # its keys (the map's headers); what it sets depends on each
+                    # segment, so no rollback restates it (nor one past it)
+                    comb = self.props.comb_of[a]
+                    clients.ann_props[first + i] = {k: None for k, n in self.props.entries[f0:f0 + cnt]
+                                                    if not k & COMBINE_PAIR}
+                    clients.ann_comb[first + i] = comb
+                    clients.no_rollback.add(first + i)
+                else:
+                    clients.ann_props[first + i] = dict(self.props.entries[f0:f0 + cnt])
             out.append((first + i, 0, 0, t, 0, flags | F_LOCAL, p1, p2, a, b))
             i += 1
         clients.local_seq += n_ops
@@ -537,6 +578,8 @@ class BatchBuilder:
                 older = sorted((x for x, kv in clients.ann_props.items() if x < ls and k in kv), reverse=True)
                 if any(x not in clients.ann_slot for x in older):
                     raise MergeTreeError(MTE_E_UNSUPPORTED, "rollback past an untracked pending annotate")
+                if any(x in clients.ann_comb for x in older):
+                    raise MergeTreeError(MTE_E_UNSUPPORTED, "rollback past a pending local incr / consensus")
                 for x in older:
                     recs.append((x, 0, 0, OP_RBKEY, 0, F_LOCAL, k, clients.ann_slot[x], clients.ann_props[x][k],
                                  NO_PROPS))
@@ -552,6 +595,7 @@ class BatchBuilder:
                 out.append((ls, 0, 0, OP_ROLLBACK, 0, F_LOCAL, t, len(aux[ls]), clients.ann_slot.pop(ls), NO_PROPS))
                 out.extend(aux[ls])
                 del clients.ann_props[ls]
+                clients.ann_comb.pop(ls, None)
             elif t != OP_NOOP:
                 out.append((ls, 0, 0, OP_ROLLBACK, 0, F_LOCAL, t, 0, 0, NO_PROPS))
 

@@ -1297,7 +1297,20 @@ static int tree_range(idoc* d, const mte_op* op, const env_t* env, int local) {
     } else {
       const mte_propset* ps = &env->b->propsets[op->a];
       g->po = 1;
-      if (op->flags & MTE_F_COMBINE) {
+      if ((op->flags & MTE_F_COMBINE) && local) {
+        /* a local incr / consensus: pending keys and group as any local
+         * annotate, each key's value mapped (segmentPropertiesManager.ts:117-147) */
+        for (uint32_t t = 0; t < ps->count; t++) {
+          const mte_prop* h = &env->b->props[ps->first + t];
+          if (!(h->key & MTE_COMBINE_PAIR) && h->key < env->n_keys && !g->pk[h->key]) g->basev[h->key] = g->props[h->key];
+        }
+        d->pwrites += apply_combine(g->props, env->n_keys, ps, env->b->props);
+        for (uint32_t t = 0; t < ps->count; t++) {
+          const mte_prop* h = &env->b->props[ps->first + t];
+          if (!(h->key & MTE_COMBINE_PAIR) && h->key < env->n_keys) g->pk[h->key] = (uint32_t)s;
+        }
+        if (op->b != MTE_NO_PROPS) g->am |= 1u << op->b;
+      } else if (op->flags & MTE_F_COMBINE) {
         d->pwrites += apply_combine(g->props, env->n_keys, ps, env->b->props);
       } else if (local) {
         for (uint32_t j = 0; j < ps->count; j++) {
@@ -1533,7 +1546,8 @@ static inline int ack_pending(const item* g, int32_t ls, uint32_t am_mask) {
  * each is added to the LRU set in the group's order, the references of the
  * acked removals slide, the ACKNOWLEDGED callback reports the group, then
  * zamboniSegments runs. */
-static int ack_group(idoc* d, int32_t ls, int32_t s, uint32_t am_mask, int64_t key, const env_t* env) {
+static int ack_group(idoc* d, int32_t ls, int32_t s, uint32_t am_mask, int64_t key, const mte_propset* stamp,
+                     const env_t* env) {
   int rc;
   for (uint32_t i = 0; i < d->n; i++) {
     item* g = &d->it[i];
@@ -1555,6 +1569,10 @@ static int ack_group(idoc* d, int32_t ls, int32_t s, uint32_t am_mask, int64_t k
       g->lrs = ((d->flags & MTE_DOC_REFS) && d->ref_hi) ? ls : 0;
     }
     if (g->am & am_mask) {
+      /* updateConsensusProperty (client.ts:646-650, 1083-1090): the ack of a
+       * local consensus stamps its marker's value with the seq, outside the
+       * pending-key rules (addProperties without a collab window) */
+      if (stamp) (void)apply_combine(g->props, env->n_keys, stamp, env->b->props);
       g->am &= ~am_mask;
       member = 1;
     }
@@ -1608,13 +1626,14 @@ static int doc_ack(idoc* d, const mte_op* op, const env_t* env) {
   if (!(lo > 0 && lo <= hi && hi <= d->local_seq)) return MTE_E_INVALID_ARG;
   for (int32_t ls = lo; ls <= hi; ls++) {
     const uint32_t am_mask = ls == hi ? op->a : 0u;
+    const mte_propset* stamp = (ls == hi && (op->flags & MTE_F_COMBINE)) ? &env->b->propsets[op->b] : NULL;
     for (uint32_t i = 0; i < d->n; i++) {
       item* g = &d->it[i];
       for (uint32_t k = 0; k < MTE_MAX_KEYS; k++)
         if (g->pk[k] && g->pk[k] <= (uint32_t)ls) g->pk[k] = 0;
     }
     if (!(op->flags & MTE_F_REGENERATED)) {
-      if ((rc = ack_group(d, ls, s, am_mask, -1, env))) return rc;
+      if ((rc = ack_group(d, ls, s, am_mask, -1, stamp, env))) return rc;
       continue;
     }
     for (;;) {
@@ -1622,7 +1641,7 @@ static int doc_ack(idoc* d, const mte_op* op, const env_t* env) {
       for (uint32_t i = 0; i < d->n && first < 0; i++)
         if (ack_pending(&d->it[i], ls, am_mask)) first = i;
       if (first < 0) break;
-      if ((rc = ack_group(d, ls, s, am_mask, d->it[first].rg, env))) return rc;
+      if ((rc = ack_group(d, ls, s, am_mask, d->it[first].rg, stamp, env))) return rc;
     }
   }
   return MTE_OK;
@@ -1711,10 +1730,12 @@ static int doc_apply_op(idoc* d, const mte_op* op, const env_t* env) {
   if (d->n + 4 > env->limit) return MTE_E_CAPACITY;
   if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
   if (op->flags & MTE_F_LOCAL) {
-    if (op->flags & MTE_F_COMBINE) return MTE_E_UNSUPPORTED;
+    if ((op->flags & MTE_F_COMBINE) && op->type != MTE_OP_ANNOTATE) return MTE_E_UNSUPPORTED;
     return local_doc ? doc_apply_local(d, op, env) : MTE_E_UNSUPPORTED;
   }
-  if ((op->flags & MTE_F_COMBINE) && (!local_doc || op->type != MTE_OP_ANNOTATE)) return MTE_E_UNSUPPORTED;
+  /* a combining annotate, or the ack of a local consensus (its stamp) */
+  if ((op->flags & MTE_F_COMBINE) && (!local_doc || (op->type != MTE_OP_ANNOTATE && op->type != MTE_OP_ACK)))
+    return MTE_E_UNSUPPORTED;
   d->wcache = -1; /* a sequenced message updates lengths */
   if (op->type == MTE_OP_ACK && !local_doc) return MTE_E_UNSUPPORTED;
   if (local_doc && op->type != MTE_OP_ACK && op->type != MTE_OP_NOOP && c == 0) return MTE_E_INVALID_ARG;
