@@ -1024,9 +1024,15 @@ const char* bad_op(const mte_op& o, const mte_batch* b, bool local_doc, bool ref
     return "propset out of range";
   }
   if (o.flags & MTE_F_COMBINE) {
-    if (o.type != MTE_OP_ANNOTATE || (o.flags & (MTE_F_LOCAL | MTE_F_REWRITE))) return "combining record: type or flags";
+    // a sequenced or local incr / consensus annotate, or the ack of a local
+    // consensus (b = the stamp's value map)
+    const bool ack = o.type == MTE_OP_ACK;
+    if ((o.type != MTE_OP_ANNOTATE && !ack) || (o.flags & MTE_F_REWRITE) || (ack && (o.flags & MTE_F_LOCAL)))
+      return "combining record: type or flags";
     if (!local_doc) return "combiningOp incr / consensus outside an MTE_DOC_LOCAL_CLIENT document";
-    const mte_propset& ps = b->propsets[o.a];
+    const uint32_t psi = ack ? o.b : o.a;
+    if (psi >= b->n_propsets) return "combining propset out of range";
+    const mte_propset& ps = b->propsets[psi];
     if ((uint64_t)ps.first + ps.count > b->n_props) return "combining propset out of range";
     for (uint32_t t = 0; t < ps.count;) {  // headers and their pairs tile the set exactly
       const mte_prop& h = b->props[ps.first + t];

@@ -1187,6 +1187,11 @@ __device__ __forceinline__ int ht_range(HT& h, const s8v& op, bool local, const 
                   break;
                 }
               }
+              if (local) {  // a local incr / consensus: the key pending as for any local annotate
+                uint32_t* pk = h.pl + (uint64_t)(kPkPlane<K> + p.key) * h.sd + i;
+                if (ld_l2(pk) == 0u) h.pl[(uint64_t)(kAnnPlane<K> + 1 + p.key) * h.sd + i] = old;
+                *pk = (uint32_t)s;
+              }
               *vp = nv;
             } else if (local) {
               // the value before the first pending annotate of the key, then pending
@@ -1258,8 +1263,9 @@ __device__ __forceinline__ bool ht_ack_pending(const HT& h, int i, int32_t ls, u
 // of the acked removals slide, the ACKNOWLEDGED record reports the group, then
 // zamboniSegments runs.  The group's segments are flagged in the L scratch.
 template <int K>
-__device__ __forceinline__ int ht_ack_group(HT& h, int32_t ls, int32_t s, uint32_t am_mask, bool keyed, uint32_t key,
-                                            const ReplayArgs& a, uint2* rt, uint32_t rhi, EvOut& ev, bool evs) {
+__device__ __forceinline__ int ht_ack_group(HT& h, int32_t ls, int32_t s, uint32_t am_mask, uint32_t stamp, bool keyed,
+                                            uint32_t key, const ReplayArgs& a, uint2* rt, uint32_t rhi, EvOut& ev,
+                                            bool evs) {
   const int l = lane_id();
   int rc;
   int bc = -1, bec = -2;
@@ -1301,6 +1307,25 @@ __device__ __forceinline__ int ht_ack_group(HT& h, int32_t ls, int32_t s, uint32
       if (am & am_mask) {
         h.pl[(uint64_t)kAnnPlane<K> * h.sd + i] = am & ~am_mask;
         member[j] = true;
+        // updateConsensusProperty (client.ts:646-650, 1083-1090): a local
+        // consensus's ack stamps its marker's value with the seq, outside the
+        // pending-key rules (titems.c ack_group)
+        if (K > 0 && stamp != MTE_NO_PROPS) {
+          const mte_propset sp = a.ps[stamp];
+          for (uint32_t t = 0; t < sp.count; t++) {
+            const mte_prop hd = a.pe[sp.first + t];
+            if ((hd.key & MTE_COMBINE_PAIR) || hd.key >= a.n_keys || hd.key >= (uint32_t)K) continue;
+            uint32_t* vp = h.pl + (uint64_t)(kFieldPlanes + hd.key) * h.sd + i;
+            const uint32_t old = ld_l2(vp);
+            for (uint32_t u = 1; u <= hd.value; u++) {
+              const mte_prop q = a.pe[sp.first + t + u];
+              if ((q.key & ~MTE_COMBINE_PAIR) == old) {
+                *vp = q.value;
+                break;
+              }
+            }
+          }
+        }
       }
     }
     vm_drain();
@@ -1370,11 +1395,14 @@ __device__ __forceinline__ int ht_ack(HT& h, const s8v& op, const ReplayArgs& a,
                                       bool evs) {
   const int32_t lo = op[4], hi = op[5], s = op[0];
   const uint32_t mask = (uint32_t)op[6];
-  const bool regen = ((((uint32_t)op[3]) >> 16) & MTE_F_REGENERATED) != 0u;
+  const uint32_t oflags = ((uint32_t)op[3]) >> 16;
+  const bool regen = (oflags & MTE_F_REGENERATED) != 0u;
   const int l = lane_id();
   int rc;
   for (int32_t ls = lo; ls <= hi; ls++) {
     const uint32_t am_mask = ls == hi ? mask : 0u;
+    // the stamp of a local consensus (MTE_F_COMBINE: b = its propset), with the last localSeq's group
+    const uint32_t stamp = (ls == hi && (oflags & MTE_F_COMBINE)) ? (uint32_t)op[7] : MTE_NO_PROPS;
     // the pending property keys of ls stop blocking remote annotates
     for (int tb = 0; tb < h.n; tb += kWave) {
       const int i = tb + l;
@@ -1389,14 +1417,14 @@ __device__ __forceinline__ int ht_ack(HT& h, const s8v& op, const ReplayArgs& a,
     }
     vm_drain();
     if (!regen) {
-      if ((rc = ht_ack_group<K>(h, ls, s, am_mask, false, 0u, a, rt, rhi, ev, evs))) return rc;
+      if ((rc = ht_ack_group<K>(h, ls, s, am_mask, stamp, false, 0u, a, rt, rhi, ev, evs))) return rc;
       continue;
     }
     for (;;) {
       const int f = ht_first(0, h.n, [&](int x) { return ht_ack_pending<K>(h, x, ls, am_mask); });
       if (f < 0) break;
       const uint32_t key = uld(h.pl + (uint64_t)kRgPlane<K> * h.sd + f);
-      if ((rc = ht_ack_group<K>(h, ls, s, am_mask, true, key, a, rt, rhi, ev, evs))) return rc;
+      if ((rc = ht_ack_group<K>(h, ls, s, am_mask, stamp, true, key, a, rt, rhi, ev, evs))) return rc;
     }
   }
   return 0;

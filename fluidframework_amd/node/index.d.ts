@@ -65,6 +65,8 @@ export interface ClientOptions {
   events?: boolean;
   /** Hold local references (MTE_DOC_REFS; needs localClient): createLocalReferencePosition. */
   refs?: boolean;
+  /** mergeTreeMaintenanceCallback records -> BatchClient.on("maintenance") (needs localClient, events). */
+  maintenanceEvents?: boolean;
   newLengthCalc?: boolean;
   props?: PropertySet;
   minSeq?: number;
@@ -195,6 +197,18 @@ export interface SequenceDeltaEvent {
   last: SequenceDeltaRange;
 }
 
+/** SequenceMaintenanceEvent (sequenceDeltaEvent.ts:128-136): one mergeTreeMaintenanceCallback. */
+export interface SequenceMaintenanceEvent {
+  deltaOperation: number;  // MergeTreeMaintenanceType: APPEND -1, SPLIT -2, UNLINK -3, ACKNOWLEDGED -4
+  operation: "append" | "split" | "unlink" | "acknowledged";
+  opArgs: { op: any; sequencedMessage?: ISequencedDocumentMessage } | undefined;
+  clientId: string;
+  /** position in the client's view once the message is applied (-1: unlinked), length at the callback */
+  ranges: { operation: number; position: number; length: number; propertyDeltas: PropertySet; segment: undefined }[];
+  first: { operation: number; position: number; length: number };
+  last: { operation: number; position: number; length: number };
+}
+
 /** ReferenceType flags (ops.ts): Simple 0, SlideOnRemove 0x40, StayOnRemove 0x80 (Transient unsupported). */
 export class LocalReferencePosition {
   readonly refType: number;
@@ -279,7 +293,17 @@ export class BatchClient {
   insertMarkerLocal(pos: number, refType: number, props?: PropertySet): IMergeTreeOp;
   insertSegmentLocal(pos: number, segment: unknown): IMergeTreeOp;
   removeRangeLocal(start: number, end: number): IMergeTreeOp;
+  /** combiningOp rewrite, incr (and consensus, though the reference's ack then needs a marker's relative position). */
   annotateRangeLocal(start: number, end: number, props: PropertySet, combiningOp?: { name: string }): IMergeTreeOp;
+  /** Client.annotateMarker: the marker by id (or an object with getId()); its position resolved by the engine. */
+  annotateMarker(marker: string | { getId(): string }, props: PropertySet, combiningOp?: { name: string }):
+    IMergeTreeOp | undefined;
+  /** Client.annotateMarkerNotifyConsensus: a consensus annotate whose ack stamps the marker's value with the
+   *  seq; consensusCallback(marker) once minSeq reaches that seq. */
+  annotateMarkerNotifyConsensus(marker: string | { getId(): string }, props: PropertySet,
+    consensusCallback: (marker: any) => void): IMergeTreeOp | undefined;
+  /** A local op as its IMergeTreeDeltaOp JSON (relative positions included). */
+  applyLocalOp(op: IMergeTreeOp): IMergeTreeOp;
   makeOpMessage(op: IMergeTreeOp, seq?: number, refSeq?: number, minSeq?: number): ISequencedDocumentMessage;
   getPendingCount(): number;
   /** Client.regeneratePendingOp for reconnection: the op re-sending the oldest
@@ -289,6 +313,9 @@ export class BatchClient {
   rollback(op?: IMergeTreeOp): void;
   /** SharedString "sequenceDelta" events ({events: true} documents), delivered at each flush in op order. */
   on(name: "sequenceDelta", listener: (event: SequenceDeltaEvent, client: BatchClient) => void): this;
+  /** SharedString "maintenance" events ({maintenanceEvents: true} documents): SPLIT / APPEND / UNLINK /
+   *  ACKNOWLEDGED callbacks (deltaOperation -2 / -1 / -3 / -4), ranges at the message's end. */
+  on(name: "maintenance", listener: (event: SequenceMaintenanceEvent, client: BatchClient) => void): this;
   /** The catch-up stash of a legacy summary, ops rewritten to refSeq = seq - 1 (sequence.ts:688-725). */
   getMessagesSinceMSNChange(): ISequencedDocumentMessage[];
   getOrAddShortClientId(longId: string): number;

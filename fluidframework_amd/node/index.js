@@ -479,6 +479,7 @@ class BatchClient {
     }
     this.engine._batch().addMessage(this.doc, this.clients, msg);
     if (msg.minimumSequenceNumber > this.lastMinSeq) this.lastMinSeq = msg.minimumSequenceNumber;
+    if (this.pendingConsensus) this._consensus(msg);
     // an interval collection's ends slide inside merge-tree ops (a remote
     // remove, the ack of our own), where the reference raises "changeInterval"
     // (intervalCollection.ts:1042-1053): the engine reports each slide with
@@ -550,6 +551,31 @@ class BatchClient {
     const op = { props, relativePos1: { id, before: true }, relativePos2: { id }, type: 2 };
     if (combiningOp) op.combiningOp = combiningOp;
     return this._local(op);
+  }
+
+  /** Client.annotateMarkerNotifyConsensus (client.ts:137-158): annotateMarker
+   *  with combiningOp consensus; the ack stamps the marker's consensus value
+   *  with its seq (updateConsensusProperty, :1083-1090: MTE_F_COMBINE on the
+   *  ack record) and consensusCallback(marker) runs once the window's minSeq
+   *  reaches that seq (addMinSeqListener, mergeTree.ts:1059-1075). */
+  annotateMarkerNotifyConsensus(marker, props, consensusCallback) {
+    const op = this.annotateMarker(marker, props, { name: "consensus" });
+    if (op) (this.pendingConsensus || (this.pendingConsensus = [])).push({ op, marker, callback: consensusCallback });
+    return op;
+  }
+
+  // the consensus ops sequenced, then their callbacks as minSeq passes them
+  _consensus(msg) {
+    const pc = this.pendingConsensus;
+    if (!pc || !pc.length) return;
+    if (msg.clientId === this.longClientId) {
+      const e = pc.find((x) => x.seq === undefined);
+      if (e && (msg.contents === e.op || JSON.stringify(msg.contents) === JSON.stringify(e.op))) e.seq = msg.sequenceNumber;
+    }
+    const due = pc.filter((x) => x.seq !== undefined && x.seq <= msg.minimumSequenceNumber).sort((x, y) => x.seq - y.seq);
+    if (!due.length) return;
+    this.pendingConsensus = pc.filter((x) => !due.includes(x));
+    for (const x of due) if (typeof x.callback === "function") x.callback(x.marker);
   }
 
   /** A local op given as its IMergeTreeDeltaOp JSON -- the Client's own op

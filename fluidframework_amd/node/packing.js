@@ -229,6 +229,8 @@ class DocClients {
     // older values back), and the annotates whose rollback the engine cannot
     // restate exactly (as packing.py)
     this.annProps = new Map();
+    // the pending local incr / consensus annotates: localSeq -> [props, combiningOp]
+    this.annComb = new Map();
     this.noRollback = new Set();
     // local reference slots (MTE_DOC_REFS documents): the next unused one and the
     // removed ones, reused first (as packing.py)
@@ -279,6 +281,7 @@ class PropTable {
     this.interner = interner;
     this.sets = [];
     this.entries = [];
+    this.combOf = new Map();  // a local combining set's index -> [props, combiningOp]
   }
   add(props) {
     if (props === undefined || props === null) return NO_PROPS;
@@ -489,7 +492,15 @@ class BatchBuilder {
           clients.noRollback.delete(ls);
         }
         const regen = clients.regenerated.delete(lo);
-        this._put(doc, seq, ref, msn, OP_ACK, 0, regen ? F_REGENERATED : 0, lo, hi, mask, NO_PROPS);
+        let flags = regen ? F_REGENERATED : 0, stamp = NO_PROPS;
+        const comb = clients.annComb.get(hi);
+        if (comb && comb[1].name === "consensus") {
+          // updateConsensusProperty: the marker's consensus value takes the seq
+          stamp = this.props.addCombining(comb[0], comb[1], seq);
+          flags |= F_COMBINE;
+        }
+        for (let ls = lo; ls <= hi; ls++) clients.annComb.delete(ls);
+        this._put(doc, seq, ref, msn, OP_ACK, 0, flags, lo, hi, mask, stamp);
       } else {
         this._combLocal = clients.local;
         try {
@@ -615,6 +626,17 @@ class BatchBuilder {
     if (recs.some((r) => r[0] !== OP_RELPOS && (r[1] & F_REWRITE))) {
       throw new MergeTreeError(E_UNSUPPORTED, "local combiningOp rewrite");
     }
+    // a local consensus is annotateMarkerNotifyConsensus's: alone in its message,
+    // with a group slot (its ack's stamp, packing.py add_local)
+    if (recs.some((r) => r[0] === OP_ANNOTATE && (r[1] & F_COMBINE) && this.props.combOf.get(r[4])[1].name === "consensus")) {
+      if (recs.filter((r) => r[0] !== OP_RELPOS).length !== 1 || recs[0][0] !== OP_RELPOS) {
+        throw new MergeTreeError(E_UNSUPPORTED,
+          "a local consensus annotate is a marker's (annotateMarkerNotifyConsensus), alone in its message");
+      }
+      if (clients.annSlot.size >= ANNOTATE_SLOTS) {
+        throw new MergeTreeError(E_UNSUPPORTED, "a local consensus annotate with " + ANNOTATE_SLOTS + " annotates pending");
+      }
+    }
     const first = clients.localSeq + 1;
     const nOps = recs.filter((r) => r[0] !== OP_RELPOS).length;  // a RELPOS record takes no localSeq
     if (first + nOps >= LOCAL_SEQ_BASE) throw new MergeTreeError(E_INVALID_ARG, "localSeq overflow");
@@ -642,7 +664,16 @@ class BatchBuilder {
         }
         const kv = new Map();
         const f0 = this.props.sets[2 * r[4]], cnt = this.props.sets[2 * r[4] + 1];
-        for (let t = f0; t < f0 + cnt; t++) kv.set(this.props.entries[2 * t], this.props.entries[2 * t + 1]);
+        if (r[1] & F_COMBINE) {
+          // its keys (the map's headers); no rollback restates it, nor one past it
+          for (let t = f0; t < f0 + cnt; t++) {
+            if (!(this.props.entries[2 * t] & COMBINE_PAIR)) kv.set(this.props.entries[2 * t], null);
+          }
+          clients.annComb.set(first + i, this.props.combOf.get(r[4]));
+          clients.noRollback.add(first + i);
+        } else {
+          for (let t = f0; t < f0 + cnt; t++) kv.set(this.props.entries[2 * t], this.props.entries[2 * t + 1]);
+        }
         clients.annProps.set(first + i, kv);
       }
       this._put(doc, first + i, 0, 0, r[0], 0, r[1] | F_LOCAL, r[2], r[3], r[4], b);
@@ -682,6 +713,9 @@ class BatchBuilder {
           .sort((p, q) => q - p);
         if (older.some((x) => !clients.annSlot.has(x))) {
           throw new MergeTreeError(E_UNSUPPORTED, "rollback past an untracked pending annotate");
+        }
+        if (older.some((x) => clients.annComb.has(x))) {
+          throw new MergeTreeError(E_UNSUPPORTED, "rollback past a pending local incr / consensus");
         }
         for (const x of older) {
           recs.push([x, 0, 0, OP_RBKEY, 0, F_LOCAL, k, clients.annSlot.get(x), clients.annProps.get(x).get(k), NO_PROPS]);
@@ -948,6 +982,22 @@ class BatchBuilder {
     } else if (t === ANNOTATE) {
       let flags = 0;
       const comb = op.combiningOp;
+      if (comb !== undefined && comb !== null && (comb.name === "incr" || comb.name === "consensus")) {
+        // a local incr / consensus: its value map at seq UnassignedSequenceNumber
+        // (segmentPropertiesManager.ts:141), as packing.py add_local
+        if (this.noCombining) {
+          throw new MergeTreeError(E_UNSUPPORTED, "combiningOp " + comb.name + " in a sharded (worker) packer");
+        }
+        if (comb.name === "consensus" && "defaultValue" in comb) {
+          throw new MergeTreeError(E_UNSUPPORTED, "consensus with a defaultValue");
+        }
+        const props = op.props === undefined ? {} : op.props;
+        const ps = this.props.addCombining(props, comb, -1);
+        this.props.combOf.set(ps, [props, comb]);
+        recs.push([OP_ANNOTATE, F_COMBINE, checkI32(op.pos1 === undefined ? 0 : op.pos1, "pos1"),
+          checkI32(op.pos2 === undefined ? 0 : op.pos2, "pos2"), ps, NO_PROPS]);
+        return;
+      }
       if (comb !== undefined && comb !== null) {
         if (comb.name !== "rewrite") throw new MergeTreeError(E_UNSUPPORTED, "combiningOp " + String(comb.name));
         flags = F_REWRITE;

@@ -269,7 +269,12 @@ extern "C" {
  * value the key can hold: the record's propset lists, per key, a header
  * {key, n} and n pairs {old | MTE_COMBINE_PAIR, new} (value ids, 0 = absent);
  * an old value not listed stays.  Only in MTE_DOC_LOCAL_CLIENT documents
- * (the HBM tree pass) and never MTE_F_LOCAL: MTE_E_UNSUPPORTED otherwise.  */
+ * (the HBM tree pass): MTE_E_UNSUPPORTED otherwise.  A local one (MTE_F_LOCAL,
+ * the map made at seq UnassignedSequenceNumber) marks its keys pending and
+ * joins its group slot as any local annotate.  On an MTE_OP_ACK record: b is
+ * the stamp of a local consensus (updateConsensusProperty, client.ts:646-650,
+ * 1083-1090) -- the map made at the ack's seq, applied to the segments of
+ * pos2's annotate group (slot in a) whatever their pending keys.             */
 #define MTE_F_COMBINE 0x0010u
 #define MTE_COMBINE_PAIR 0x80000000u
 /* A property value id with this bit set never matches another value id, itself

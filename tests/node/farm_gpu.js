@@ -19,6 +19,9 @@ const zlib = require("zlib");
 const { MergeTreeEngine } = require("../../fluidframework_amd/node");
 const { asMsg } = require("./fixtures");
 
+// MTE_NODE_ADDON=oracle: the same host over the CPU restatement (oracle/mte_shim.c, tests only)
+const oracleAddon = process.env.MTE_NODE_ADDON === "oracle"
+  ? require(path.join(__dirname, "..", "..", "oracle", "_build", "mte_napi_oracle.node")) : null;
 const sets = JSON.parse(zlib.gunzipSync(fs.readFileSync(path.join(__dirname, "..", "golden",
   process.argv[4] || "farm_vectors.json.gz"))).toString("utf8")).sets;
 const nSets = process.argv[3] && process.argv[3] !== "all" ? Number(process.argv[3]) : sets.length;
@@ -50,21 +53,26 @@ function propRuns(c) {
   return runs;
 }
 
-const eng = new MergeTreeEngine({ nKeys: 8 });
-const layout = [];
-// argv[5] "observers": each set's observer alone (the combining-op farms)
+// argv[5] "observers": each set's observer alone (the combining-op farms);
+// "perset": every client, each set in an engine of its own (a context's
+// combining value maps cover the values its documents gave a key)
 const observersOnly = process.argv[5] === "observers";
-for (let si = 0; si < nSets; si++) {
+const perSet = process.argv[5] === "perset";
+let passed = 0, opsChecked = 0, pending = 0, nDocs = 0;
+const failures = [];
+const groups = perSet ? Array.from({ length: nSets }, (_, i) => [i]) : [Array.from({ length: nSets }, (_, i) => i)];
+for (const group of groups) {
+const eng = new MergeTreeEngine(oracleAddon ? { nKeys: 8, addon: oracleAddon } : { nKeys: 8 });
+const layout = [];
+for (const si of group) {
   sets[si].names.forEach((name, ci) => {
     if (observersOnly && ci !== 0) return;
     layout.push({ si, ci, refs: [], client: eng.createClient(sets[si].initialText,
       { newLengthCalc: !sets[si].legacy, localClient: true, longClientId: name, refs: withRefs }) });
   });
 }
-let passed = 0, opsChecked = 0;
-const failures = [];
 const prev = layout.map(() => 0);
-const nCp = Math.max.apply(null, sets.slice(0, nSets).map((s) => s.checkpoints.length));
+const nCp = Math.max.apply(null, group.map((si) => sets[si].checkpoints.length));
 for (let j = 0; j < nCp; j++) {
   layout.forEach((L, d) => {
     const s = sets[L.si];
@@ -100,7 +108,10 @@ for (let j = 0; j < nCp; j++) {
       let op;
       if (o.type === 0) op = L.client.insertSegmentLocal(o.pos1, o.seg);
       else if (o.type === 1) op = L.client.removeRangeLocal(o.pos1, o.pos2);
-      else op = L.client.annotateRangeLocal(o.pos1, o.pos2, o.props);
+      else if (o.relativePos1 && o.combiningOp && o.combiningOp.name === "consensus") {
+        op = L.client.annotateMarkerNotifyConsensus(o.relativePos1.id, o.props, () => {});
+      } else if (o.relativePos1 || o.relativePos2) op = L.client.applyLocalOp(o);
+      else op = L.client.annotateRangeLocal(o.pos1, o.pos2, o.props, o.combiningOp);
       if (JSON.stringify(sortKeys(op)) !== JSON.stringify(sortKeys(o))) failures.push([L.si, L.ci, j, "op", op, o]);
       opsChecked++;
     }
@@ -118,7 +129,9 @@ for (let j = 0; j < nCp; j++) {
     else failures.push([L.si, L.ci, j, "state"]);
   });
 }
-const pending = layout.reduce((a, L) => a + L.client.getPendingCount(), 0);
-process.stdout.write(JSON.stringify({ passed, opsChecked, pending, failures: failures.slice(0, 5),
-  nFailures: failures.length, docs: layout.length }) + "\n");
+pending += layout.reduce((a, L) => a + L.client.getPendingCount(), 0);
+nDocs += layout.length;
 eng.close();
+}
+process.stdout.write(JSON.stringify({ passed, opsChecked, pending, failures: failures.slice(0, 5),
+  nFailures: failures.length, docs: nDocs }) + "\n");

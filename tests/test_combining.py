@@ -6,17 +6,23 @@ alone (properties.ts:24-62) -- and ignores pending local keys (shouldModifyKey,
 :94-102).  The host computes that function over every value the key can hold
 (packing.combine_value, PropTable.add_combining) and the record carries it as
 a value map (MTE_F_COMBINE, include/mte.h); the HBM tree pass (mte_htree.h)
-and its restatement (titems.c) apply it.  Local combining ops and documents
-outside the tree pass are refused (MTE_E_UNSUPPORTED).
+and its restatement (titems.c) apply it.  A local one is the map made at seq
+UnassignedSequenceNumber, its keys pending as for any local annotate; the ack
+of a local consensus (annotateMarkerNotifyConsensus) stamps the marker's value
+with its seq (updateConsensusProperty, client.ts:646-650, 1083-1090: the ack
+record's MTE_F_COMBINE map).  Documents outside the tree pass are refused
+(MTE_E_UNSUPPORTED).
 
 Pinned by 26 farms the reference ran (oracle/ref_farm.js with combine ->
 tests/golden/combine_farm_vectors.json.gz, make_farm_golden.py --combine):
 1,007 combining annotates -- incr with and without defaultValue / minValue on
 numbers and strings, consensus on id'd markers through
 annotateMarkerNotifyConsensus -- in both length calculations; every
-observer's text and properties equal the reference's at every checkpoint.
-The reference's clients do not converge under them (a sender's pending key
-and a remote incr), so each observer is held to its own reference client.
+observer's text and properties equal the reference's at every checkpoint,
+and so do every client's -- its own 978 local incr and 29 local consensus
+annotates among them, each op it emits the reference's.  The reference's
+clients do not converge under them (a sender's pending key and a remote
+incr), so each client is held to its own reference client.
 """
 import gzip
 import json
@@ -89,6 +95,43 @@ def test_tree_oracle_combine_farms():
     assert passed == _n_checkpoints(sets)
 
 
+def _every_client(factory):
+    """Every client of every farm, each set in a context of its own (a
+    context's value maps cover the values its documents gave a key)."""
+    sets = combine_sets()["sets"]
+    passed, failures = 0, []
+    for s in sets:
+        p, f = replay_ref_farm(factory, [s])
+        passed += p
+        failures += f
+    return passed, failures, sum(len(s["checkpoints"]) * len(s["names"]) for s in sets)
+
+
+def test_tree_oracle_combine_farms_every_client():
+    passed, failures, n = _every_client(tree_factory)
+    assert not failures, failures[:2]
+    assert passed == n == 625
+
+
+def _node_every_client(env=None):
+    import subprocess
+    root = os.path.dirname(HERE)
+    p = subprocess.run(["node", os.path.join(root, "tests", "node", "farm_gpu.js"), "batched", "all",
+                        "combine_farm_vectors.json.gz", "perset"], capture_output=True, text=True, timeout=900,
+                       env=dict(os.environ, **(env or {})))
+    assert p.returncode == 0, p.stderr[-3000:]
+    return json.loads(p.stdout)
+
+
+def test_node_combine_farms_every_client_on_restatement():
+    """Node BatchClient over the restatement's addon: every client's local
+    incr (annotateRangeLocal) and consensus (annotateMarkerNotifyConsensus)
+    ops equal the reference's, and so does every checkpoint."""
+    j = _node_every_client({"MTE_NODE_ADDON": "oracle"})
+    assert j["nFailures"] == 0, j["failures"]
+    assert j["passed"] == 625 and j["opsChecked"] == 7612
+
+
 def test_combine_map_is_what_the_tree_applies():
     """Without the map (the annotate taken as a plain set) the farms fail: the
     vectors do reach values the combining ops change."""
@@ -114,8 +157,14 @@ def test_packer_combine_rules():
         bb.add_message(0, DocClients("A"), _annotate(None, {"name": "incr"}))
     assert ei.value.code == MTE_E_UNSUPPORTED
     cl = DocClients("B", local=True)
-    with pytest.raises(MergeTreeError) as ei:  # a local combining op
-        bb.add_local(0, cl, {"type": 2, "pos1": 0, "pos2": 1, "props": {"k": 1}, "combiningOp": {"name": "incr"}})
+    # a local incr is a value map; a local consensus over a range is refused
+    # (the reference's ack of one fails: updateConsensusProperty reads relativePos1)
+    bb.add_local(0, cl, {"type": 2, "pos1": 0, "pos2": 1, "props": {"k": 1}, "combiningOp": {"name": "incr"}})
+    with pytest.raises(MergeTreeError) as ei:
+        bb.add_local(0, cl, {"type": 2, "pos1": 0, "pos2": 1, "props": {"k": 1}, "combiningOp": {"name": "consensus"}})
+    assert ei.value.code == MTE_E_UNSUPPORTED
+    with pytest.raises(MergeTreeError) as ei:  # no rollback restates a local incr
+        bb.add_rollback(0, cl)
     assert ei.value.code == MTE_E_UNSUPPORTED
     with pytest.raises(MergeTreeError) as ei:
         bb.add_message(0, cl, _annotate(None, {"name": "consensus", "defaultValue": {"seq": -1}}))
@@ -210,6 +259,20 @@ def test_node_combine_farms_on_gpu():
     j = json.loads(p.stdout)
     assert j["nFailures"] == 0, j["failures"]
     assert j["passed"] == _n_checkpoints(combine_sets()["sets"])
+
+
+@pytest.mark.gpu
+def test_gpu_combine_farms_every_client():
+    passed, failures, n = _every_client(device_factory)
+    assert not failures, failures[:2]
+    assert passed == n == 625
+
+
+@pytest.mark.gpu
+def test_node_combine_farms_every_client_on_gpu():
+    j = _node_every_client()
+    assert j["nFailures"] == 0, j["failures"]
+    assert j["passed"] == 625 and j["opsChecked"] == 7612
 
 
 @pytest.mark.gpu
