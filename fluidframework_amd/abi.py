@@ -138,6 +138,7 @@ DOC_EVENTS = 0x8
 DOC_REFS = 0x10
 DOC_SLIDE_EVENTS = 0x20
 DOC_MAINT_EVENTS = 0x40
+DOC_TREE = 0x80  # a new-calc document without a local client on the HBM tree pass (segment-exact events)
 DELTA_DTYPE = np.dtype([("op", "<u4"), ("kind", "<u4"), ("pos", "<i4"), ("len", "<i4"), ("removed", "<u4")])
 
 

@@ -115,7 +115,7 @@ __global__ void rel_route_kernel(DocHdr* hdr, const uint32_t* docs, uint32_t n, 
   DocHdr* h = hdr + docs[i];
   if (h->status != 0) return;
   const uint32_t f = h->flags;
-  if (f & MTE_DOC_LOCAL_CLIENT) return;
+  if (f & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_TREE)) return;
   if (!(f & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC))) {
     if (!(f & MTE_DOC_EVENTS)) h->flags = f | kHdrTreeHbmFlag;
     return;
@@ -146,14 +146,14 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
   // HBM tree pass) and the HBM tree pass's own (a local client, or legacy with
   // delta events)
   const bool legacy = tree != nullptr && (!(in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC)) ||
-                                          (in.flags & MTE_DOC_LOCAL_CLIENT));
+                                          (in.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_TREE)));
   DocHdr h;
   h.nseg = n_img ? (int32_t)n_img : (in.text_len > 0 || legacy ? 1 : 0);
   h.min_seq = in.min_seq;
   h.cur_seq = in.cur_seq;
   h.status = 0;
   h.flags = in.flags & (MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_ROUND_SYNC | MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS | MTE_DOC_REFS |
-                        MTE_DOC_SLIDE_EVENTS | MTE_DOC_MAINT_EVENTS);
+                        MTE_DOC_SLIDE_EVENTS | MTE_DOC_MAINT_EVENTS | MTE_DOC_TREE);
   h.resume = 0;
   h.pad0 = h.pad1 = 0;
   if (legacy) {
@@ -174,12 +174,12 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
     st[kHsHeapN] = 0u;
     st[kHsLseq] = 0u;
     st[kHsRhi] = 0u;
-    st[kHsEntered] = (in.flags & MTE_DOC_LOCAL_CLIENT) ? 1u : 0u;
+    st[kHsEntered] = (in.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_TREE)) ? 1u : 0u;
     st[kHsWin] = 0u;  // no cached local partials
   }
   if (in.flags & MTE_DOC_LOCAL_CLIENT) {  // nothing pending (mte_htree.h planes)
     const uint32_t nz = n_img ? n_img : 1u;
-    for (uint32_t k = 0; k < 2 * kt + 3; k++)
+    for (uint32_t k = 0; k < 2 * kt + 5; k++)  // the local planes (mte_htree.h kLocalPlanes)
       for (uint32_t x = 0; x < nz; x++) soa.props[(kt + k) * soa.plane_stride + (uint64_t)d * cap + x] = 0u;
   }
   if (n_img) return;  // image_kernel writes the segments
@@ -1262,13 +1262,17 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     if ((in.flags & MTE_DOC_REFS) && !(in.flags & MTE_DOC_LOCAL_CLIENT))
       return set_err(c, MTE_E_UNSUPPORTED, "doc %u: local references need MTE_DOC_LOCAL_CLIENT", d);
     // maintenance records come from the HBM tree pass, which keeps the
-    // reference's segments (a local client's document)
-    if ((in.flags & MTE_DOC_MAINT_EVENTS) && (in.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)) !=
-                                                 (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS))
-      return set_err(c, MTE_E_UNSUPPORTED, "doc %u: maintenance events need MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS", d);
+    // reference's segments (a local client's, MTE_DOC_TREE or a legacy document)
+    if ((in.flags & MTE_DOC_MAINT_EVENTS) &&
+        (!(in.flags & MTE_DOC_EVENTS) ||
+         !((in.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_TREE)) || !(in.flags & MTE_DOC_NEW_LENGTH_CALC))))
+      return set_err(c, MTE_E_UNSUPPORTED, "doc %u: maintenance events need MTE_DOC_EVENTS on the HBM tree pass "
+                     "(MTE_DOC_LOCAL_CLIENT, MTE_DOC_TREE or the legacy length calculation)", d);
+    if ((in.flags & MTE_DOC_TREE) && (in.flags & MTE_DOC_ROUND_SYNC))
+      return set_err(c, MTE_E_UNSUPPORTED, "doc %u: MTE_DOC_TREE with MTE_DOC_ROUND_SYNC", d);
     // delta events of a new length-calc document without a local client come
     // from the HBM-streamed flat pass, which big-document contexts do not run
-    if ((in.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS)) == MTE_DOC_EVENTS &&
+    if ((in.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS | MTE_DOC_TREE)) == MTE_DOC_EVENTS &&
         (in.flags & MTE_DOC_NEW_LENGTH_CALC) && c->cap >= kChunkMinCap)
       return set_err(c, MTE_E_UNSUPPORTED, "doc %u: delta events of a document without a local client need a "
                      "context below %u segments", d, kChunkMinCap);
@@ -1311,7 +1315,7 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
   c->h_sdocs.clear();
   for (uint32_t d = 0; d < n_docs; d++) {
     // the flat HBM-streamed pass's own: new length-calc documents with delta events and no local client
-    if ((docs[d].flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS | MTE_DOC_NEW_LENGTH_CALC)) ==
+    if ((docs[d].flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS | MTE_DOC_NEW_LENGTH_CALC | MTE_DOC_TREE)) ==
         (MTE_DOC_EVENTS | MTE_DOC_NEW_LENGTH_CALC))
       c->h_sdocs.push_back(d);
     if (docs[d].flags & MTE_DOC_LOCAL_CLIENT) c->h_local[d] = 1, any_local = true;
@@ -1393,7 +1397,7 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
     c->h_legacy.assign(n_docs, 0);  // the document carries tree words (read-outs join merged leaves)
     for (uint32_t d = 0; d < n_docs; d++) {
       const uint32_t f = docs[d].flags;
-      if ((f & MTE_DOC_LOCAL_CLIENT) || ((f & MTE_DOC_EVENTS) && !(f & MTE_DOC_NEW_LENGTH_CALC))) {
+      if ((f & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_TREE)) || ((f & MTE_DOC_EVENTS) && !(f & MTE_DOC_NEW_LENGTH_CALC))) {
         htree_docs.push_back(d);  // the HBM tree pass's own (mte_htree.h)
         c->h_legacy[d] = 1;
       } else if (f & MTE_DOC_EVENTS) {

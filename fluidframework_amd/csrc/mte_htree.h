@@ -2307,7 +2307,10 @@ __global__ __launch_bounds__(64) void htree_kernel(ReplayArgs a, HtreeArgs t) {
   const int doc = uni((int)t.docs[idx]);
   const uint32_t hf = uni(a.hdr[doc].flags);
   const bool ldoc = (hf & MTE_DOC_LOCAL_CLIENT) != 0;
-  if (!ldoc && !(hf & kHdrTreeHbm)) return;
+  // its own documents from the start (a local client's, MTE_DOC_TREE, legacy
+  // ones with delta events), the other legacy ones once TIER 2 hands them over
+  const bool own = ldoc || (hf & MTE_DOC_TREE) || ((hf & MTE_DOC_EVENTS) && !(hf & MTE_DOC_NEW_LENGTH_CALC));
+  if (!own && !(hf & kHdrTreeHbm)) return;
   DocRun D;
   run_init(D, a, doc, false);
   uint32_t* stp = t.st + (uint64_t)doc * kHtState;
@@ -2366,7 +2369,7 @@ __global__ __launch_bounds__(64) void htree_kernel(ReplayArgs a, HtreeArgs t) {
   if ((hf & MTE_DOC_EVENTS) && a.dl_off) {
     ev.p = a.dl + a.dl_off[doc];
     ev.cap = a.dl_off[doc + 1] - a.dl_off[doc];
-    h.maint = ldoc && (hf & MTE_DOC_MAINT_EVENTS) != 0;
+    h.maint = (hf & MTE_DOC_MAINT_EVENTS) != 0;
   }
   uint32_t msg_ev = 0;   // MTE_DELTA_MAINT: the first event of the message being applied
   bool msg_open = false;  // its MSG_END not applied yet

@@ -855,7 +855,7 @@ __global__ __launch_bounds__(256) void stream_kernel(ReplayArgs a) {
   // documents pass 2 escalated, and the new length-calc documents with delta
   // events and no local client (a local client's go to the HBM tree pass)
   const uint32_t hf = a.hdr[doc].flags;
-  if (hf & MTE_DOC_LOCAL_CLIENT) return;
+  if (hf & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_TREE)) return;  // the HBM tree pass's
   const bool own = (hf & (MTE_DOC_EVENTS | MTE_DOC_NEW_LENGTH_CALC)) == (MTE_DOC_EVENTS | MTE_DOC_NEW_LENGTH_CALC);
   if (!(hf & kHdrNeedsEsc) && !own) return;  // untouched doc: leave the header alone
   DocRun D;

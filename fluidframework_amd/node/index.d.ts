@@ -67,6 +67,8 @@ export interface ClientOptions {
   refs?: boolean;
   /** mergeTreeMaintenanceCallback records -> BatchClient.on("maintenance") (needs localClient, events). */
   maintenanceEvents?: boolean;
+  /** MTE_DOC_TREE: replay on the tree pass (the reference's segmentation; segment-exact sequenceDelta ranges). */
+  tree?: boolean;
   newLengthCalc?: boolean;
   props?: PropertySet;
   minSeq?: number;

@@ -131,9 +131,10 @@ class MergeTreeEngine {
       throw new MergeTreeError(-9, "roundSync with a local client or delta events");
     }
     if (o.refs && !o.localClient) throw new MergeTreeError(-9, "local references need {localClient: true}");
-    if (o.maintenanceEvents && !(o.localClient && o.events)) {
-      throw new MergeTreeError(-9, "maintenance events need {localClient: true, events: true}");
+    if (o.maintenanceEvents && !(o.events && (o.localClient || o.tree || !o.newLengthCalc))) {
+      throw new MergeTreeError(-9, "maintenance events need {events: true} on the tree pass (localClient, tree or the legacy length calculation)");
     }
+    if (o.tree && o.roundSync) throw new MergeTreeError(-9, "tree with roundSync");
     this.docs.push({ text: initialText || "", newLengthCalc: !!o.newLengthCalc, roundSync: !!o.roundSync, props: o.props,
       minSeq: o.minSeq || 0, currentSeq: o.currentSeq || 0, segments: o.segments, localClient: !!o.localClient,
       events: !!o.events, refs: !!o.refs,
@@ -141,7 +142,10 @@ class MergeTreeEngine {
       // (MTE_DOC_SLIDE_EVENTS): on with events and references unless asked off
       slideEvents: !!(o.events && o.refs && o.slideEvents !== false),
       // SharedString's "maintenance" events (MTE_DOC_MAINT_EVENTS)
-      maintenanceEvents: !!o.maintenanceEvents });
+      maintenanceEvents: !!o.maintenanceEvents,
+      // the HBM tree pass for a document without a local client (MTE_DOC_TREE):
+      // the reference's own segments, so sequenceDelta ranges are segment-exact
+      tree: !!o.tree });
     const c = new BatchClient(this, doc, o.observerId === undefined ? (o.longClientId || "A") : o.observerId,
       !!o.localClient);
     this.clients.push(c);

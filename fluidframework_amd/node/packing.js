@@ -58,6 +58,7 @@ const DOC_REFS = 0x10;       // MTE_DOC_REFS
 const DOC_EVENTS = 0x8; // MTE_DOC_EVENTS
 const DOC_SLIDE_EVENTS = 0x20;  // MTE_DOC_SLIDE_EVENTS: the references' slides and their snapshots
 const DOC_MAINT_EVENTS = 0x40;  // MTE_DOC_MAINT_EVENTS: mergeTreeMaintenanceCallback records
+const DOC_TREE = 0x80;  // MTE_DOC_TREE: the HBM tree pass (the reference's segmentation)
 const E_INVALID_ARG = -1, E_CAPACITY = -4, E_UNSUPPORTED = -9, E_STATE = -10, E_CLIENT_RANGE = -12;
 const COMBINE_DOMAIN_MAX = 4096;  // distinct values of one key a combining op's value map may cover
 const DEFAULT_REF_CAPACITY = 1024;  // mte_set_ref_capacity's default (include/mte.h)
@@ -1096,7 +1097,8 @@ function packDocInits(docs, interner) {
     buf.writeUInt32LE(d.text.length, o + 4);
     buf.writeUInt32LE((d.newLengthCalc ? DOC_NEW_LENGTH_CALC : 0) | (d.roundSync ? DOC_ROUND_SYNC : 0) |
       (d.localClient ? DOC_LOCAL_CLIENT : 0) | (d.events ? DOC_EVENTS : 0) | (d.refs ? DOC_REFS : 0) |
-      (d.slideEvents ? DOC_SLIDE_EVENTS : 0) | (d.maintenanceEvents ? DOC_MAINT_EVENTS : 0), o + 8);
+      (d.slideEvents ? DOC_SLIDE_EVENTS : 0) | (d.maintenanceEvents ? DOC_MAINT_EVENTS : 0) |
+      (d.tree ? DOC_TREE : 0), o + 8);
     buf.writeUInt32LE(props.add(d.props) >>> 0, o + 12);
     buf.writeInt32LE(d.minSeq || 0, o + 16);
     buf.writeInt32LE(d.currentSeq || 0, o + 20);

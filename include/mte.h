@@ -392,11 +392,22 @@ typedef struct mte_config {
  * remove and ack record of a batch (a record's slides and snapshot); a host
  * that does not read them leaves the flag clear.                             */
 #define MTE_DOC_SLIDE_EVENTS 0x20u
-/* With MTE_DOC_LOCAL_CLIENT | MTE_DOC_EVENTS: also record the merge-tree's
- * maintenance (mergeTreeMaintenanceCallback, mergeTree.ts:695-725, 1313-1320,
- * 1687-1694; SharedString's "maintenance" event, sequence.ts:212-216) as
- * MTE_DELTA_MAINT records.  Opt-in: they take event capacity like the ranges. */
+/* With MTE_DOC_EVENTS, on a document of the HBM tree pass (MTE_DOC_LOCAL_CLIENT,
+ * MTE_DOC_TREE or the legacy length calculation): also record the
+ * merge-tree's maintenance (mergeTreeMaintenanceCallback, mergeTree.ts:695-725,
+ * 1313-1320, 1687-1694; SharedString's "maintenance" event,
+ * sequence.ts:212-216) as MTE_DELTA_MAINT records.  Opt-in: they take event
+ * capacity like the ranges. */
 #define MTE_DOC_MAINT_EVENTS 0x40u
+/* Replay a new length-calc document without a local client on the HBM tree
+ * pass too: the reference's own segmentation (its B+tree, the lazy zamboni's
+ * appends), so its delta records are segment-exact -- one range per segment
+ * as mergeTreeDeltaCallback reports it, an annotate over a segment removed in
+ * the own view with that segment's cachedLength -- where the flat passes'
+ * canonical segments can split or join them.  Slower than the flat passes
+ * (one wavefront per document); local-client and legacy documents with
+ * events replay there anyway. */
+#define MTE_DOC_TREE 0x80u
 
 /* Initial document: one text segment inserted before collaboration starts, as
  * the reference replay harness does (client.replay.spec.ts:22-23): seq 0

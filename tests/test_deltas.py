@@ -11,7 +11,10 @@ the position (Client.getPosition) and length of every delta segment.  Segment
 boundaries are not the reference's (the flat passes split on op boundaries and
 never append-merge), so the comparison is on what does not depend
 on them: inserts and removes as createOpsFromDelta merges them (the rewritten
-catch-up ops), annotates as the set of own-view units they changed.
+catch-up ops), annotates as the set of own-view units they changed.  A
+document flagged MTE_DOC_TREE replays on the HBM tree pass, with the
+reference's own segments: its records equal the reference's callbacks range
+for range (tree restatement and GPU).
 """
 import gzip
 import json
@@ -21,7 +24,7 @@ import numpy as np
 import pytest
 
 from fluidframework_amd import gen
-from fluidframework_amd.abi import DOC_EVENTS
+from fluidframework_amd.abi import DOC_EVENTS, DOC_TREE
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = os.path.join(HERE, "golden", "delta_vectors.json.gz")
@@ -100,6 +103,47 @@ def device_factory(k):
 def test_oracle_deltas_match_reference(i):
     S = golden()[i]
     bad = run_set(oracle_factory, S)
+    assert not bad, bad[:3]
+
+
+def run_set_exact(factory, S):
+    """Every record equal to the reference's callback ranges (MTE_DOC_TREE)."""
+    st = gen.generate(S["config"], n_docs=S["n_docs"], ops_per_doc=S["ops_per_doc"], **S["params"])
+    inits = st["inits"].copy()
+    inits["flags"] |= DOC_EVENTS | DOC_TREE
+    e = factory(st["n_keys"])
+    e.load_docs(inits, st["init_text"])
+    e.apply_batch(st["batch"])
+    assert (e.statuses() == 0).all()
+    bad = []
+    for d, doc in enumerate(S["docs"]):
+        got = [[int(x["op"]), int(x["kind"]), int(x["pos"]), int(x["len"]), int(x["removed"])]
+               for x in e.read_deltas(d)]
+        if got != doc["events"]:
+            k = 0
+            while k < min(len(got), len(doc["events"])) and got[k] == doc["events"][k]:
+                k += 1
+            bad.append((S["name"], d, k, got[k:k + 2], doc["events"][k:k + 2]))
+    return bad
+
+
+def tree_factory(k):
+    from oracle import OracleEngine
+    e = OracleEngine(k, tree="items")
+    e.lib.oti_set_limit(e.ctx, 1 << 20)
+    return e
+
+
+@pytest.mark.parametrize("i", range(3))
+def test_tree_oracle_deltas_segment_exact(i):
+    bad = run_set_exact(tree_factory, golden()[i])
+    assert not bad, bad[:3]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i", range(3))
+def test_gpu_tree_deltas_segment_exact(i):
+    bad = run_set_exact(device_factory, golden()[i])
     assert not bad, bad[:3]
 
 

@@ -456,3 +456,32 @@ slots.push(bb.addRef(0, a, 0));
 console.log(JSON.stringify({slots, code}));
 """)
     assert json.loads(out) == {"slots": [0, 1, 0, 0], "code": -4}
+
+
+def _node_tree_deltas(i, env=None):
+    import test_deltas as T
+    from fluidframework_amd import gen
+    from fluidframework_amd.messages import stream_docs
+    S = T.golden()[i]
+    st = gen.generate(S["config"], n_docs=12, ops_per_doc=S["ops_per_doc"], **S["params"])
+    docs = stream_docs(st, 0, 12)
+    r = subprocess.run([NODE, "tests/node/deltas_gpu.js"], cwd=ROOT, input=json.dumps({"docs": docs, "tree": True}),
+                       capture_output=True, text=True, timeout=600, env=dict(os.environ, **(env or {})))
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = json.loads(r.stdout.strip().splitlines()[-1])["docs"]
+    for d in range(12):
+        assert got[d]["events"] == S["docs"][d]["events"], (d,)
+
+
+@pytest.mark.parametrize("i", range(3))
+def test_node_tree_delta_events_on_restatement(i):
+    """createClient {events: true, tree: true} (MTE_DOC_TREE): the sequenceDelta
+    ranges equal the reference's callbacks range for range -- its segments,
+    not the flat passes' canonical ones (CPU restatement's addon)."""
+    _node_tree_deltas(i, {"MTE_NODE_ADDON": "oracle"})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i", range(3))
+def test_node_tree_delta_events_on_gpu(i):
+    _node_tree_deltas(i)
