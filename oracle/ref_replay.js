@@ -66,6 +66,21 @@ function replayDoc(d) {
           ds.segment.removedSeq !== undefined ? 1 : 0])]);
     };
   }
+  // d.maint: every mergeTreeMaintenanceCallback (mergeTree.ts:695-725,
+  // 1687-1694) as [message index, MergeTreeMaintenanceType, [[Client.getPosition
+  // once the message is applied (-1: unlinked), cachedLength at the callback],
+  // ...]] -- the ranges SharedString's "maintenance" event reads (sequence.ts:212-216)
+  const maint = [];
+  let mbuf = [];
+  if (d.maint) {
+    client.mergeTreeMaintenanceCallback = (args) => {
+      mbuf.push([applied, args.operation, args.deltaSegments.map((ds) => [ds.segment, ds.segment.cachedLength])]);
+    };
+  }
+  const settle = () => {
+    for (const [mi, t, segs] of mbuf) maint.push([mi, t, segs.map(([sg, len]) => [client.getPosition(sg), len])]);
+    mbuf = [];
+  };
   for (const m of d.msgs) {
     const msg = {
       clientId: m[0],
@@ -81,6 +96,7 @@ function replayDoc(d) {
       error = String(e && e.message ? e.message : e);
       break;
     }
+    if (d.maint) settle();
     applied++;
   }
   const ms = Number(process.hrtime.bigint() - t0) / 1e6;
@@ -115,7 +131,8 @@ function replayDoc(d) {
       return true;
     });
   }
-  return { text, length, props, segs, error, applied, ms, deltas: d.deltas ? deltas : undefined };
+  return { text, length, props, segs, error, applied, ms, deltas: d.deltas ? deltas : undefined,
+    maint: d.maint ? maint : undefined };
 }
 
 const input = JSON.parse(fs.readFileSync(0, "utf8"));

@@ -12,7 +12,7 @@ is deterministic), so the file holds only parameters and the expected events
 (flattened [message index, kind, position, length, removed] per range): data, no
 reference source.  Run in the build container.
 
-Usage: python3 tests/golden/make_delta_golden.py
+Usage: python3 tests/golden/make_delta_golden.py [--maint]
 """
 import gzip
 import json
@@ -32,6 +32,34 @@ SETS = [
     ("newcalc_lag64_c2", 2, 60, 800, dict(length_mode=2, max_lag=64)),
     ("newcalc_rounds_c3", 3, 40, 1200, dict(length_mode=2)),
 ]
+
+
+# --maint: the maintenance callbacks of remote-only documents (SPLIT / APPEND /
+# UNLINK: an observer acks nothing), new and legacy length calculation ->
+# tests/golden/maint_observer_vectors.json.gz
+OUT_MAINT = os.path.join(HERE, "maint_observer_vectors.json.gz")
+MAINT_SETS = SETS + [("legacy_lag16_c3", 3, 60, 800, dict(length_mode=1, max_lag=16)),
+                     ("legacy_rounds_c2", 2, 40, 1200, dict(length_mode=1))]
+
+
+def main_maint():
+    if not ref_util.ref_available():
+        sys.exit("the reference sources are not in this container")
+    out = {"generator": "fluidframework_amd/gen.py (mte_gen.cpp), seeded MT19937; oracle/ref_replay.js maint",
+           "sets": []}
+    for name, cfg, nd, nops, kw in MAINT_SETS:
+        st = gen.generate(cfg, n_docs=nd, ops_per_doc=nops, **kw)
+        docs = ref_util.stream_docs(st, 0, nd)
+        for d in docs:
+            d["maint"] = True
+            d["props"] = False
+        res = ref_util.ref_replay(docs)
+        out["sets"].append({"name": name, "config": cfg, "n_docs": nd, "ops_per_doc": nops, "params": kw,
+                            "docs": [{"error": r["error"], "maint": r["maint"]} for r in res]})
+        print(name, sum(len(r["maint"]) for r in res), "callbacks", flush=True)
+    with gzip.open(OUT_MAINT, "wt", encoding="utf-8") as fh:
+        json.dump(out, fh, separators=(",", ":"))
+    print("wrote", OUT_MAINT, os.path.getsize(OUT_MAINT))
 
 
 def main():
@@ -58,4 +86,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--maint" in sys.argv[1:]:
+        main_maint()
+    else:
+        main()

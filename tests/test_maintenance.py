@@ -3,6 +3,11 @@ mergeTree.ts:695-725, 1313-1320, 1687-1694): SPLIT, APPEND, UNLINK and
 ACKNOWLEDGED, the structural changes SharedString reports as "maintenance"
 events (sequence.ts:212-216, SequenceMaintenanceEvent).
 
+Remote-only documents (MTE_DOC_TREE, or the legacy length calculation) get the
+same records from the tree pass: pinned by 260 generated lagging documents the
+reference replayed as an observer (oracle/ref_replay.js maint,
+tests/golden/maint_observer_vectors.json.gz: SPLIT, APPEND and UNLINK).
+
 Pinned by 38 farms the reference itself ran with every client's callback
 recorded (oracle/ref_farm.js maint -> tests/golden/maint_farm_vectors.json.gz,
 made by tests/golden/make_farm_golden.py --maint): per event of every client
@@ -119,3 +124,62 @@ def test_gpu_node_maintenance_events():
     j = _node_farm("gpu")
     assert j["equal"] == j["clients"], j["first"]
     assert j["skipped"] < 10, j
+
+
+OBSERVER_VECTORS = os.path.join(HERE, "golden", "maint_observer_vectors.json.gz")
+
+
+def _group(ev):
+    from fluidframework_amd.abi import DELTA_MAINT
+    out = []
+    for x in ev:
+        k = int(x["kind"])
+        if k & 0xff00 != DELTA_MAINT:
+            continue
+        t, mi = -(k & 0xff), int(x["op"])
+        if int(x["removed"]) == 0 or not out or out[-1][0] != mi or out[-1][1] != t:
+            out.append([mi, t, []])
+        out[-1][2].append([int(x["pos"]), int(x["len"])])
+    return out
+
+
+def check_observers(factory):
+    """Remote-only documents (the reference client as an observer, through
+    oracle/ref_replay.js maint; tests/golden/make_delta_golden.py --maint): new
+    length-calc ones flagged MTE_DOC_TREE, legacy ones on the tree pass anyway.
+    Returns (documents, equal, first difference)."""
+    from fluidframework_amd import gen
+    from fluidframework_amd.abi import DOC_EVENTS, DOC_MAINT_EVENTS, DOC_TREE
+    with gzip.open(OBSERVER_VECTORS, "rt", encoding="utf-8") as fh:
+        sets = json.load(fh)["sets"]
+    n = equal = 0
+    first = None
+    for S in sets:
+        st = gen.generate(S["config"], n_docs=S["n_docs"], ops_per_doc=S["ops_per_doc"], **S["params"])
+        inits = st["inits"].copy()
+        inits["flags"] |= DOC_EVENTS | DOC_MAINT_EVENTS | DOC_TREE
+        e = factory(st["n_keys"])
+        e.set_event_capacity(64)
+        e.load_docs(inits, st["init_text"])
+        e.apply_batch(st["batch"])
+        status = e.statuses()
+        for d, doc in enumerate(S["docs"]):
+            n += 1
+            got, want = _group(e.read_deltas(d)), doc["maint"]
+            # a document the reference failed on ("MergeTree insert failed") fails here too
+            if got == want and (doc["error"] is None) == (int(status[d]) == 0):
+                equal += 1
+            elif first is None:
+                first = (S["name"], d, doc["error"], int(status[d]), got[:2], want[:2])
+    return n, equal, first
+
+
+def test_tree_oracle_maintenance_of_remote_only_documents():
+    n, equal, first = check_observers(tree_factory)
+    assert equal == n == 260, first
+
+
+@pytest.mark.gpu
+def test_gpu_maintenance_of_remote_only_documents():
+    n, equal, first = check_observers(device_factory)
+    assert equal == n == 260, first
