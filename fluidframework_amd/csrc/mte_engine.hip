@@ -619,7 +619,7 @@ struct mte_ctx {
   uint32_t* d_htree_docs = nullptr; // the candidates
   uint32_t n_htree = 0;
   std::vector<uint8_t> h_legacy;    // per doc
-  std::vector<uint8_t> h_local;     // per doc: MTE_DOC_LOCAL_CLIENT
+  std::vector<uint8_t> h_local;     // per doc: 1 MTE_DOC_LOCAL_CLIENT, 2 MTE_DOC_TREE (the HBM tree pass's)
   std::vector<uint8_t> h_events;    // per doc: MTE_DOC_EVENTS
   // delta events per batch slot: region offsets (n_docs + 1, host and device),
   // the events, their counts; ev_slot = the slot of the last mte_run
@@ -981,7 +981,7 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
 
 // Validation of one op record (the kernels index with these fields, so a bad
 // record must never reach them).  Returns nullptr or the reason.
-const char* bad_op(const mte_op& o, const mte_batch* b, bool local_doc, bool refs_doc, uint32_t ref_cap) {
+const char* bad_op(const mte_op& o, const mte_batch* b, bool local_doc, bool tree_doc, bool refs_doc, uint32_t ref_cap) {
   if (o.type > MTE_OP_RELPOS) return "type";
   if (o.type == MTE_OP_RELPOS) {  // the record after it is checked by the caller
     const uint32_t rp = MTE_RP_POS1 | MTE_RP_BEFORE1 | MTE_RP_POS2 | MTE_RP_BEFORE2;
@@ -1029,7 +1029,8 @@ const char* bad_op(const mte_op& o, const mte_batch* b, bool local_doc, bool ref
     const bool ack = o.type == MTE_OP_ACK;
     if ((o.type != MTE_OP_ANNOTATE && !ack) || (o.flags & MTE_F_REWRITE) || (ack && (o.flags & MTE_F_LOCAL)))
       return "combining record: type or flags";
-    if (!local_doc) return "combiningOp incr / consensus outside an MTE_DOC_LOCAL_CLIENT document";
+    if (!local_doc && (ack || !tree_doc))
+      return "combiningOp incr / consensus outside an MTE_DOC_LOCAL_CLIENT or MTE_DOC_TREE document";
     const uint32_t psi = ack ? o.b : o.a;
     if (psi >= b->n_propsets) return "combining propset out of range";
     const mte_propset& ps = b->propsets[psi];
@@ -1082,8 +1083,8 @@ int upload_ops(mte_ctx* c, const mte_batch* b, int w, uint64_t* bad, const char*
         for (uint64_t k = a; k < e; k++) {
           while (d + 1 < b->n_docs && b->op_offsets[d + 1] <= k0 + k) d++;
           const mte_op& o = b->ops[k0 + k];
-          const char* r = bad_op(o, b, !c->h_local.empty() && c->h_local[d], !c->h_refs.empty() && c->h_refs[d],
-                                 c->ref_cap);
+          const uint8_t hl = c->h_local.empty() ? 0 : c->h_local[d];
+          const char* r = bad_op(o, b, (hl & 1) != 0, (hl & 2) != 0, !c->h_refs.empty() && c->h_refs[d], c->ref_cap);
           if (!r && o.type == MTE_OP_RELPOS) {
             const mte_op* nx = k0 + k + 1 < b->op_offsets[d + 1] ? &b->ops[k0 + k + 1] : nullptr;
             if (!nx || nx->type > MTE_OP_ANNOTATE) r = "relative position record not followed by an insert, remove "
@@ -1319,6 +1320,7 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
         (MTE_DOC_EVENTS | MTE_DOC_NEW_LENGTH_CALC))
       c->h_sdocs.push_back(d);
     if (docs[d].flags & MTE_DOC_LOCAL_CLIENT) c->h_local[d] = 1, any_local = true;
+    else if (docs[d].flags & MTE_DOC_TREE) c->h_local[d] = 2;
     if (docs[d].flags & MTE_DOC_EVENTS) c->h_events[d] = 1;
     if (docs[d].flags & MTE_DOC_REFS) c->h_refs[d] = 1, any_refs = true;
     const uint32_t sl = MTE_DOC_REFS | MTE_DOC_EVENTS | MTE_DOC_SLIDE_EVENTS;

@@ -444,7 +444,7 @@ class BatchClient {
     this.engine = engine;
     this.doc = doc;
     this.longClientId = observerId;
-    this.clients = new DocClients(observerId, engine.docs[doc].minSeq, local);
+    this.clients = new DocClients(observerId, engine.docs[doc].minSeq, local, engine.docs[doc].tree);
     this.clients.refCap = engine.refCapacity;
     this.lastMinSeq = 0;
     const self = this;

@@ -203,8 +203,11 @@ class Interner {
  *  visibility rule any more (same rule as fluidframework_amd/packing.py). */
 const NEVER = 0x7fffffff;
 class DocClients {
-  constructor(observerId, minSeq, local) {
+  constructor(observerId, minSeq, local, tree) {
     this.observer = observerId;
+    // an MTE_DOC_TREE document (the HBM tree pass without a local client): it
+    // takes sequenced combining ops too
+    this.tree = !!tree;
     this.ids = new Map([[observerId, 0]]);
     this.last = new Int32Array(MAX_CLIENTS).fill(NEVER); // slot -> highest seq its client used
     this.lastId = observerId;  // the last sender and its slot (messages come in runs per sender)
@@ -503,7 +506,7 @@ class BatchBuilder {
         for (let ls = lo; ls <= hi; ls++) clients.annComb.delete(ls);
         this._put(doc, seq, ref, msn, OP_ACK, 0, flags, lo, hi, mask, stamp);
       } else {
-        this._combLocal = clients.local;
+        this._combLocal = clients.local || clients.tree;
         try {
           this._opPut(doc, seq, ref, msn, msg.contents, this._src(doc));
         } catch (e) {
@@ -594,7 +597,7 @@ class BatchBuilder {
         }
         if (!this._combLocal) {
           throw new MergeTreeError(E_UNSUPPORTED, "combiningOp " + comb.name +
-            " outside a local-client document (the HBM tree pass)");
+            " outside a local-client or tree document (the HBM tree pass)");
         }
         if (comb.name === "consensus" && "defaultValue" in comb) {
           throw new MergeTreeError(E_UNSUPPORTED, "consensus with a defaultValue");

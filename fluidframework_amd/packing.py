@@ -311,8 +311,12 @@ class DocClients:
 
     NEVER = I32_MAX  # slot held for good (observer, ids registered without a seq)
 
-    def __init__(self, observer_id: str, min_seq: int = 0, local: bool = False, ref_cap: int = DEFAULT_REF_CAPACITY):
+    def __init__(self, observer_id: str, min_seq: int = 0, local: bool = False, ref_cap: int = DEFAULT_REF_CAPACITY,
+                 tree: bool = False):
         self.observer = observer_id
+        # an MTE_DOC_TREE document (the HBM tree pass without a local client):
+        # it takes sequenced combining ops too
+        self.tree = tree
         self.ids = {observer_id: 0}
         self.last = {0: self.NEVER}  # slot -> highest seq its client used
         self.min_seq = min_seq       # the window's minSeq before the next message
@@ -458,7 +462,7 @@ class BatchBuilder:
                     clients.ann_comb.pop(ls, None)
                 recs.append((OP_ACK, flags, lo, hi, mask, stamp))
             else:
-                self._comb = (clients.local, seq)
+                self._comb = (clients.local or clients.tree, seq)
                 try:
                     self._op_records(msg.get("contents"), recs)
                 finally:
@@ -725,7 +729,7 @@ class BatchBuilder:
                     raise MergeTreeError(MTE_E_UNSUPPORTED, f"local combiningOp {comb.get('name')!r}")
                 if not ctx[0]:
                     raise MergeTreeError(MTE_E_UNSUPPORTED, f"combiningOp {comb.get('name')!r} outside a "
-                                         "local-client document (the HBM tree pass)")
+                                         "local-client or tree document (the HBM tree pass)")
                 if comb.get("name") == "consensus" and "defaultValue" in comb:
                     raise MergeTreeError(MTE_E_UNSUPPORTED, "consensus with a defaultValue")
                 ps = self.props.add_combining(op.get("props", {}), comb, ctx[1])

@@ -268,8 +268,8 @@ extern "C" {
  * (shouldModifyKey, :94-102).  The host computes that function over every
  * value the key can hold: the record's propset lists, per key, a header
  * {key, n} and n pairs {old | MTE_COMBINE_PAIR, new} (value ids, 0 = absent);
- * an old value not listed stays.  Only in MTE_DOC_LOCAL_CLIENT documents
- * (the HBM tree pass): MTE_E_UNSUPPORTED otherwise.  A local one (MTE_F_LOCAL,
+ * an old value not listed stays.  Only in MTE_DOC_LOCAL_CLIENT and
+ * MTE_DOC_TREE documents (the HBM tree pass): MTE_E_UNSUPPORTED otherwise.  A local one (MTE_F_LOCAL,
  * the map made at seq UnassignedSequenceNumber) marks its keys pending and
  * joins its group slot as any local annotate.  On an MTE_OP_ACK record: b is
  * the stamp of a local consensus (updateConsensusProperty, client.ts:646-650,

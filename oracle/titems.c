@@ -1734,7 +1734,8 @@ static int doc_apply_op(idoc* d, const mte_op* op, const env_t* env) {
     return local_doc ? doc_apply_local(d, op, env) : MTE_E_UNSUPPORTED;
   }
   /* a combining annotate, or the ack of a local consensus (its stamp) */
-  if ((op->flags & MTE_F_COMBINE) && (!local_doc || (op->type != MTE_OP_ANNOTATE && op->type != MTE_OP_ACK)))
+  if ((op->flags & MTE_F_COMBINE) && (!(local_doc || (d->flags & MTE_DOC_TREE)) ||
+                                       (op->type != MTE_OP_ANNOTATE && op->type != MTE_OP_ACK)))
     return MTE_E_UNSUPPORTED;
   d->wcache = -1; /* a sequenced message updates lengths */
   if (op->type == MTE_OP_ACK && !local_doc) return MTE_E_UNSUPPORTED;

@@ -236,7 +236,7 @@ def canon_regen(op, orig, merge=True):
 
 
 def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_regen=False, observers_only=False,
-                    observers_local=False, maint=None):
+                    observers_local=False, maint=None, extra_flags=0):
     """Replay farms the reference ran (oracle/ref_farm.js -> tests/golden/
     farm_vectors.json.gz): one MTE_DOC_LOCAL_CLIENT document per client of every
     set (the observer "A" included), each fed its own events in order — "L" a
@@ -257,6 +257,7 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_reg
     with the new length calculation, the tree passes with the legacy one).
     observers_local: only the observers, as MTE_DOC_LOCAL_CLIENT documents (the
     HBM tree pass; combiningOp incr / consensus replay there only).
+    extra_flags: more MTE_DOC_* flags for every document (MTE_DOC_TREE).
     maint (a dict): the documents record their maintenance callbacks
     (MTE_DOC_MAINT_EVENTS); maint[(set, client)] collects them as the reference
     farm's "maint" lists: [event index, MergeTreeMaintenanceType, [[position,
@@ -274,7 +275,7 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_reg
     inits, text = doc_inits([sets[si]["initialText"] for si, _ in layout],
                             flags=DOC_NEW_LENGTH_CALC | (0 if observers_only else DOC_LOCAL_CLIENT) |
                             (DOC_EVENTS if has_regen or maint is not None else 0) | (DOC_REFS if has_refs else 0) |
-                            (DOC_MAINT_EVENTS if maint is not None else 0))
+                            (DOC_MAINT_EVENTS if maint is not None else 0) | extra_flags)
     for d, (si, _) in enumerate(layout):  # sets the reference ran with the legacy length calculation
         if sets[si].get("legacy"):
             inits[d]["flags"] = int(inits[d]["flags"]) & ~DOC_NEW_LENGTH_CALC & 0xffffffff
@@ -285,7 +286,8 @@ def replay_ref_farm(engine_factory, sets, n_keys=8, regen_checks=None, exact_reg
     eng.load_docs(inits, text)
     held = [[] for _ in layout]
     ref_slots = [[] for _ in layout]  # the farm's reference index -> engine slot
-    clients = [DocClients(sets[si]["names"][ci], local=not observers_only) for si, ci in layout]
+    clients = [DocClients(sets[si]["names"][ci], local=not observers_only, tree=bool(extra_flags & 0x80))
+               for si, ci in layout]
     n_cp = max(len(s["checkpoints"]) for s in sets)
     prev = [0] * len(layout)
     passed, failures = 0, []

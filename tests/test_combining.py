@@ -10,7 +10,8 @@ and its restatement (titems.c) apply it.  A local one is the map made at seq
 UnassignedSequenceNumber, its keys pending as for any local annotate; the ack
 of a local consensus (annotateMarkerNotifyConsensus) stamps the marker's value
 with its seq (updateConsensusProperty, client.ts:646-650, 1083-1090: the ack
-record's MTE_F_COMBINE map).  Documents outside the tree pass are refused
+record's MTE_F_COMBINE map).  Remote-only documents flagged MTE_DOC_TREE
+replay them on the same pass; documents outside it are refused
 (MTE_E_UNSUPPORTED).
 
 Pinned by 26 farms the reference ran (oracle/ref_farm.js with combine ->
@@ -130,6 +131,26 @@ def test_node_combine_farms_every_client_on_restatement():
     j = _node_every_client({"MTE_NODE_ADDON": "oracle"})
     assert j["nFailures"] == 0, j["failures"]
     assert j["passed"] == 625 and j["opsChecked"] == 7612
+
+
+def test_tree_oracle_combine_farms_remote_only_tree_documents():
+    """Each set's observer as a document of remote clients alone flagged
+    MTE_DOC_TREE (the HBM tree pass without a local client) takes the
+    sequenced combining ops too."""
+    from fluidframework_amd.abi import DOC_TREE
+    sets = combine_sets()["sets"]
+    passed, failures = replay_ref_farm(tree_factory, sets, observers_only=True, extra_flags=DOC_TREE)
+    assert not failures, failures[:2]
+    assert passed == _n_checkpoints(sets)
+
+
+@pytest.mark.gpu
+def test_gpu_combine_farms_remote_only_tree_documents():
+    from fluidframework_amd.abi import DOC_TREE
+    sets = combine_sets()["sets"]
+    passed, failures = replay_ref_farm(device_factory, sets, observers_only=True, extra_flags=DOC_TREE)
+    assert not failures, failures[:2]
+    assert passed == _n_checkpoints(sets)
 
 
 def test_combine_map_is_what_the_tree_applies():

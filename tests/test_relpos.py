@@ -26,7 +26,7 @@ import pytest
 
 from fixtures_util import replay_ref_farm
 from fluidframework_amd import gen
-from fluidframework_amd.abi import (DOC_NEW_LENGTH_CALC, MTE_E_UNSUPPORTED, OP_ANNOTATE, OP_INSERT, OP_RELPOS,
+from fluidframework_amd.abi import (DOC_NEW_LENGTH_CALC, DOC_TREE, MTE_E_UNSUPPORTED, OP_ANNOTATE, OP_INSERT, OP_RELPOS,
                                     RP_BEFORE1, RP_POS1, RP_POS2)
 from fluidframework_amd.packing import BatchBuilder, DocClients, Interner
 
@@ -66,9 +66,9 @@ def _all_clients(factory):
     return passed, len(checks)
 
 
-def _observers(factory):
+def _observers(factory, extra_flags=0):
     sets = vector_sets()["sets"]
-    passed, failures = replay_ref_farm(factory, sets, observers_only=True)
+    passed, failures = replay_ref_farm(factory, sets, observers_only=True, extra_flags=extra_flags)
     assert not failures, failures[:2]
     assert passed == sum(len(s["checkpoints"]) for s in sets)
     return passed
@@ -207,6 +207,22 @@ def test_gpu_relpos_chunked_context():
     d2.load_docs(inits2, np.zeros(0, np.uint16))
     d2.apply_batch(sub)
     assert d2.statuses()[0] == 0 and d2.read_doc(0)["text"] == "helo"
+    # the same new length-calc document flagged MTE_DOC_TREE replays on the HBM tree pass
+    inits3 = inits.copy()
+    inits3["flags"] = int(inits["flags"][0]) | DOC_TREE
+    d3 = DeviceEngine(4, seg_capacity=8192)
+    d3.load_docs(inits3, np.zeros(0, np.uint16))
+    d3.apply_batch(sub)
+    assert d3.statuses()[0] == 0 and d3.read_doc(0)["text"] == "helo"
+
+
+@pytest.mark.gpu
+def test_gpu_relpos_observers_tree_documents_in_chunked_context():
+    """Relative positions in new length-calc documents of a big-document
+    context (>= 8,192 segments): flagged MTE_DOC_TREE they replay on the HBM
+    tree pass, every observer of the 42 reference farms at every checkpoint."""
+    from fluidframework_amd.engine import DeviceEngine
+    assert _observers(lambda k: DeviceEngine(k, seg_capacity=8192), extra_flags=DOC_TREE) == 176
 
 
 @pytest.mark.gpu
