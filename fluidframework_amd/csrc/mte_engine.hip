@@ -646,6 +646,7 @@ struct mte_ctx {
   // per document, zeroed at every reset
   std::vector<uint8_t> h_refs;      // per doc: MTE_DOC_REFS
   std::vector<uint8_t> h_slides;    // per doc: MTE_DOC_SLIDE_EVENTS (with REFS and EVENTS)
+  bool any_maint = false;           // a document records maintenance (the HBM tree pass's M build)
   std::vector<uint32_t> h_ref_hi;   // per doc: reference slots its MTE_OP_REF records used so far (+1)
   uint32_t ref_cap = 1024;
   uint2* d_refs = nullptr;
@@ -928,7 +929,7 @@ int launch_replay(mte_ctx* c, const ReplayArgs& a) {
         HIPCHK(c, hipMemsetAsync(c->d_hprof, 0, kHtProf * 8, c->tree_stream));
       }
       HtreeArgs ht{c->d_tree, c->d_heap, c->d_hheap, c->hcap, lcap, c->d_hst, c->d_hscr, order, c->n_htree,
-                   c->arena, c->d_hprof};
+                   c->arena, c->d_hprof, c->any_maint ? 1u : 0u};
       HIPCHK(c, (launch_htree<K, S>(a, ht, c->tree_stream)));
     }
     HIPCHK(c, hipEventRecord(c->ev_join, c->tree_stream));
@@ -1311,6 +1312,9 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
   c->h_events.assign(n_docs, 0);
   c->h_refs.assign(n_docs, 0);
   c->h_slides.assign(n_docs, 0);
+  c->any_maint = false;
+  for (uint32_t d = 0; d < n_docs; d++)
+    if (docs[d].flags & MTE_DOC_MAINT_EVENTS) c->any_maint = true;
   c->h_ref_hi.assign(n_docs, 0);
   bool any_local = false, any_refs = false;
   c->h_sdocs.clear();

@@ -71,6 +71,7 @@ struct HtreeArgs {
   uint32_t n_docs;
   const uint16_t* arena;
   unsigned long long* prof;  // kHtProf phase clocks (MTE_HTREE_PROF builds), or nullptr
+  uint32_t maint;        // some document records maintenance (the htree_kernel<K, S, true> build)
 };
 
 // plane indices of a local-client document (after the K property planes)
@@ -1255,6 +1256,25 @@ __device__ __forceinline__ bool ht_ack_pending(const HT& h, int i, int32_t ls, u
          (ld_l2(h.pl + (uint64_t)kAnnPlane<K> * h.sd + i) & am_mask) != 0u;
 }
 
+// the group's next tail split off after ls (a member flagged in L whose born >
+// ls), by id from `last` on: (its index or -1, its id)
+__device__ __forceinline__ uint2 ht_next_tail(const uint32_t* Lf, const uint32_t* bnp, const uint32_t* tw,
+                                                        int n, uint32_t ls, uint32_t last) {
+  const int l = lane_id();
+  uint32_t best = 0xffffffffu;
+  for (int tb = 0; tb < n; tb += kWave) {
+    const int i = tb + l;
+    if (i < n && ld_l2(Lf + i) == 1u && ld_l2(bnp + i) > ls) {
+      const uint32_t id = t_id(ld_l2(tw + i));
+      if (id >= last && id < best) best = id;
+    }
+  }
+  best = uni(wave_min_u32(best));
+  if (best == 0xffffffffu) return make_uint2(0xffffffffu, 0u);
+  const int i = ht_first(0, n, [&](int x) { return ld_l2(Lf + x) == 1u && ld_l2(bnp + x) > ls && t_id(ld_l2(tw + x)) == best; });
+  return make_uint2((uint32_t)i, best);
+}
+
 // ackPendingSegment (mergeTree.ts:1278-1331, mergeTreeNodes.ts:475-503) for one
 // segment group of ls (titems.c ack_group): the items of regeneration group
 // `key` (keyed) or every item of ls get the seq, each segment is added to the
@@ -1345,22 +1365,10 @@ __device__ __forceinline__ int ht_ack_group(HT& h, int32_t ls, int32_t s, uint32
   vm_drain();
   const int32_t* Lf = h.L;
   for (uint32_t last = 0; tails; tails--) {
-    // the next tail by id
-    uint32_t best = 0xffffffffu;
-    for (int tb = 0; tb < h.n; tb += kWave) {
-      const int i = tb + l;
-      if (i < h.n && ld_l2((const uint32_t*)Lf + i) == 1u && ld_l2(bnp + i) > (uint32_t)ls) {
-        const uint32_t id = t_id(ld_l2(h.tw + i));
-        if (id >= last && id < best) best = id;
-      }
-    }
-    best = uni(wave_min_u32(best));
-    const int i = ht_first(0, h.n, [&](int x) {
-      return ld_l2((const uint32_t*)Lf + x) == 1u && ld_l2(bnp + x) > (uint32_t)ls && t_id(ld_l2(h.tw + x)) == best;
-    });
-    if (i < 0) break;
-    if ((rc = ht_add_lru(h, i, s, bc, bec))) return rc;
-    last = best + 1u;
+    const uint2 nx = ht_next_tail((const uint32_t*)Lf, bnp, h.tw, h.n, (uint32_t)ls, last);
+    if ((int)nx.x < 0) break;
+    if ((rc = ht_add_lru(h, (int)nx.x, s, bc, bec))) return rc;
+    last = nx.y + 1u;
   }
   if (rt && rhi) {
     // the group slides in its order, the later groups still pending
@@ -1416,15 +1424,17 @@ __device__ __forceinline__ int ht_ack(HT& h, const s8v& op, const ReplayArgs& a,
       }
     }
     vm_drain();
-    if (!regen) {
-      if ((rc = ht_ack_group<K>(h, ls, s, am_mask, stamp, false, 0u, a, rt, rhi, ev, evs))) return rc;
-      continue;
-    }
+    // one group, or (regenerated) one per re-sent segment; one call site keeps
+    // the inlined group body single
     for (;;) {
-      const int f = ht_first(0, h.n, [&](int x) { return ht_ack_pending<K>(h, x, ls, am_mask); });
-      if (f < 0) break;
-      const uint32_t key = uld(h.pl + (uint64_t)kRgPlane<K> * h.sd + f);
-      if ((rc = ht_ack_group<K>(h, ls, s, am_mask, stamp, true, key, a, rt, rhi, ev, evs))) return rc;
+      uint32_t key = 0u;
+      if (regen) {
+        const int f = ht_first(0, h.n, [&](int x) { return ht_ack_pending<K>(h, x, ls, am_mask); });
+        if (f < 0) break;
+        key = uld(h.pl + (uint64_t)kRgPlane<K> * h.sd + f);
+      }
+      if ((rc = ht_ack_group<K>(h, ls, s, am_mask, stamp, regen, key, a, rt, rhi, ev, evs))) return rc;
+      if (!regen) break;
     }
   }
   return 0;
@@ -2300,8 +2310,19 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
 // The HBM tree pass: one wavefront (workgroup) per candidate document — every
 // local-client document, and the legacy documents the register tiers handed
 // over (kHdrTreeHbm; their heap and tree state move over on first entry).
-template <int K, bool S>
-__global__ __launch_bounds__(64) void htree_kernel(ReplayArgs a, HtreeArgs t) {
+// M: the build with the maintenance records (MTE_DOC_MAINT_EVENTS), launched
+// only for a batch that asks for them -- their code costs the kernel registers
+// (189 VGPRs against 80 without, two waves per SIMD instead of six)
+#ifndef MTE_HTREE_WPE  // a waves-per-SIMD floor for the register allocator (A/B builds)
+#define MTE_HTREE_WPE 0
+#endif
+#if MTE_HTREE_WPE > 0
+#define MTE_HTREE_ATTR __attribute__((amdgpu_waves_per_eu(MTE_HTREE_WPE)))
+#else
+#define MTE_HTREE_ATTR
+#endif
+template <int K, bool S, bool M>
+__global__ __launch_bounds__(64) MTE_HTREE_ATTR void htree_kernel(ReplayArgs a, HtreeArgs t) {
   const int idx = (int)blockIdx.x;
   if (idx >= (int)t.n_docs) return;
   const int doc = uni((int)t.docs[idx]);
@@ -2369,7 +2390,7 @@ __global__ __launch_bounds__(64) void htree_kernel(ReplayArgs a, HtreeArgs t) {
   if ((hf & MTE_DOC_EVENTS) && a.dl_off) {
     ev.p = a.dl + a.dl_off[doc];
     ev.cap = a.dl_off[doc + 1] - a.dl_off[doc];
-    h.maint = (hf & MTE_DOC_MAINT_EVENTS) != 0;
+    h.maint = M && (hf & MTE_DOC_MAINT_EVENTS) != 0;
   }
   uint32_t msg_ev = 0;   // MTE_DELTA_MAINT: the first event of the message being applied
   bool msg_open = false;  // its MSG_END not applied yet

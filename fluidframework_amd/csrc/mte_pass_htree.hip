@@ -9,7 +9,8 @@ hipError_t launch_htree(const ReplayArgs& a, const HtreeArgs& t, hipStream_t s) 
   if (!t.n_docs) return hipSuccess;
   // dynamic LDS: (nP + 5) words per item of lcap (ht_to_lds), nP of a local-client document
   const size_t lds = t.lcap ? ((size_t)(kLocalPlanes<K> + 5) * t.lcap + 2) * 4 : 0;
-  hipLaunchKernelGGL((htree_kernel<K, S>), dim3(t.n_docs), dim3(kWave), lds, s, a, t);
+  if (t.maint) hipLaunchKernelGGL((htree_kernel<K, S, true>), dim3(t.n_docs), dim3(kWave), lds, s, a, t);
+  else hipLaunchKernelGGL((htree_kernel<K, S, false>), dim3(t.n_docs), dim3(kWave), lds, s, a, t);
   return hipGetLastError();
 }
 

@@ -39,6 +39,9 @@
 //          combine: the chance that an annotate carries a combining op
 //         (incr with or without defaultValue / minValue, or consensus on an
 //         id'd marker), its values sometimes strings
+//          transient: the chance that a reference made is Transient (a
+//         segment and offset the tree does not track: localReference.ts:263,
+//         mergeTree.ts:1095-1112), drawn before stay;
 //          stay: the chance that a reference made is StayOnRemove (drawn from
 //         the same number, so the farms without it are unchanged)
 // stdout: {"sets": [{..params, "names": [...], "log": [[clientId, seq, ref, msn, "op", contents]],
@@ -278,8 +281,9 @@ function runSet(p) {
       if (len > 0 && (live.length === 0 || R.next() < 0.75)) {
         const pos = R.int(0, len - 1);
         const u = R.next();
-        const type = p.stay && u < p.stay ? ReferenceType.StayOnRemove
-          : u < 0.8 ? ReferenceType.SlideOnRemove : ReferenceType.Simple;
+        const type = p.transient && u < p.transient ? ReferenceType.Transient
+          : p.stay && u < p.stay ? ReferenceType.StayOnRemove
+            : u < 0.8 ? ReferenceType.SlideOnRemove : ReferenceType.Simple;
         const { segment, offset } = c.getContainingSegment(pos);
         refs[i].push(c.createLocalReferencePosition(segment, offset, type, undefined));
         events[i].push(["F", pos, type]);

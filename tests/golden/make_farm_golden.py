@@ -43,7 +43,7 @@ record every client's mergeTreeMaintenanceCallback (SPLIT / APPEND / UNLINK /
 ACKNOWLEDGED): per event the callbacks it raised, each segment's position once
 the event is applied and its length at the callback.
 
-Usage: python3 tests/golden/make_farm_golden.py [--refs | --stay | --combine | --legacy | --relpos | --maint]
+Usage: python3 tests/golden/make_farm_golden.py [--refs | --stay | --transient | --combine | --legacy | --relpos | --maint]
 """
 import gzip
 import json
@@ -96,6 +96,13 @@ REF_SETS = [(7000 + i, 2 + i % 6, 300 + 100 * (i % 5), ["", "hello world", "abc\
 STAY_SETS = [(7500 + i, 2 + i % 6, 400 + 100 * (i % 5), ["", "hello world", "abc\ndef"][i % 3], 6, [64, 200, 400][i % 3],
               [0.0, 0.2][i % 2], [1, 2] if i % 4 == 3 else None, [0.15, 0.3][i % 2], [0.35, 0.6][(i // 2) % 2])
              for i in range(32)]
+
+# Transient references among them (--transient): as STAY_SETS, the last field
+# the chance that a reference made is Transient
+OUT_TRANSIENT = os.path.join(HERE, "localref_transient_vectors.json.gz")
+TRANSIENT_SETS = [(7800 + i, 2 + i % 6, 400 + 100 * (i % 5), ["", "hello world", "abc\ndef"][i % 3], 6,
+                   [64, 200, 400][i % 3], [0.0, 0.2][i % 2], [1, 2] if i % 4 == 3 else None, [0.15, 0.3][i % 2],
+                   [0.35, 0.6][(i // 2) % 2]) for i in range(24)]
 
 # combining ops (--combine): (seed, clients, steps, initial text, checkpoints,
 # text bound, extra parameters)
@@ -228,15 +235,17 @@ def main_combine(out):
     print(f"wrote {OUT_COMBINE}: {len(res['sets'])} farms, {n_comb} combining ops, reference failed on {failed}")
 
 
-def main_refs(out, stay=False):
+def main_refs(out, stay=False, transient=False):
     res = {"sets": [], "generator": "oracle/ref_farm.js with refs (reference Client, mulberry32 seeds)"}
     failed = []
-    for row in (STAY_SETS if stay else REF_SETS):
+    for row in (TRANSIENT_SETS if transient else STAY_SETS if stay else REF_SETS):
         sd, c, n, t, k, m, rb, types, refs = row[:9]
         one = {"seed": sd, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
                "rollback": rb, "refs": refs}
         if stay:
             one["stay"] = row[9]
+        if transient:
+            one["transient"] = row[9]
         if types:
             one["rollbackTypes"] = types
         q = subprocess.run(["node", FARM_JS, out], input=json.dumps({"sets": [one]}), capture_output=True, text=True,
@@ -246,7 +255,7 @@ def main_refs(out, stay=False):
         else:
             failed.append(sd)
     res["seeds_the_reference_failed"] = failed
-    dst = OUT_STAY if stay else OUT_REFS
+    dst = OUT_TRANSIENT if transient else OUT_STAY if stay else OUT_REFS
     with gzip.open(dst, "wt", encoding="utf-8") as fh:
         json.dump(res, fh, separators=(",", ":"))
     n_refs = sum(1 for s in res["sets"] for ev in s["events"] for e in ev if e[0] == "F")
@@ -263,6 +272,8 @@ def main():
         return main_combine(out)
     if "--stay" in sys.argv[1:]:
         return main_refs(out, stay=True)
+    if "--transient" in sys.argv[1:]:
+        return main_refs(out, transient=True)
     if "--legacy" in sys.argv[1:]:
         return main_legacy(out)
     if "--relpos" in sys.argv[1:]:
