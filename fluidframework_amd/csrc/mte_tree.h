@@ -971,8 +971,12 @@ __device__ __forceinline__ void tree_burst(DocRun& D, TreeRun& tr, const ReplayA
 #ifndef MTE_TREE0_WAVES  // TIER 0's register budget in waves per SIMD (4: 128 VGPRs)
 #define MTE_TREE0_WAVES 4
 #endif
+#ifndef MTE_TREE1_WAVES  // TIER 1's (1: no bound, 224 VGPRs = 2 waves per SIMD)
+#define MTE_TREE1_WAVES 1
+#endif
 template <int K, bool S, int TIER>
-__global__ __launch_bounds__(256, TIER == 0 ? MTE_TREE0_WAVES : 1) void tree_kernel(ReplayArgs a, TreeArgs t) {
+__global__ __launch_bounds__(256, TIER == 0 ? MTE_TREE0_WAVES : TIER == 1 ? MTE_TREE1_WAVES : 1) void tree_kernel(
+    ReplayArgs a, TreeArgs t) {
   constexpr int EMAX = TIER == 2 ? 16 : TIER == 1 ? 4 : 2;
   constexpr uint32_t kTierFlags = kHdrTreeEsc | kHdrTreeBig | kHdrTreeHbmFlag;
   __shared__ uint32_t zlds_all[kDocsPerBlock][kWave * EMAX];
