@@ -961,15 +961,20 @@ __device__ __forceinline__ void tree_burst(DocRun& D, TreeRun& tr, const ReplayA
 
 // The tree pass.  A kernel's register allocation is that of its largest tier,
 // so the tiers are separate kernels: TIER 0 runs E = 1, 2 (documents up to 124
-// items, ~137 VGPRs: 3 waves per SIMD), TIER 1 E = 4 (up to 252 items, ~225
-// VGPRs: 2 waves), TIER 2 E = 8, 16 (up to 1,020 items).  A document that
+// items, bounded to MTE_TREE0_WAVES waves per SIMD), TIER 1 E = 4 (up to 252
+// items, ~225 VGPRs: 2 waves), TIER 2 E = 8, 16 (up to 1,020 items).  A document that
 // outgrows TIER 0 is flagged kHdrTreeEsc and continues in the TIER 1 launch
 // that follows; one that shrinks back (20 items of slack) returns to the next
 // TIER 0 launch, so a passing peak does not keep it at low occupancy for the
 // rest of the batch.  The host alternates TIER 0 / TIER 1 a few rounds (the
 // last TIER 1 keeps its documents), then runs TIER 2 (kHdrTreeBig) once.
-#ifndef MTE_TREE0_WAVES  // TIER 0's register budget in waves per SIMD (4: 128 VGPRs)
-#define MTE_TREE0_WAVES 4
+// TIER 0's register budget in waves per SIMD (5: 96 VGPRs, 40 spilled).  It
+// decides how many of a batch's documents are resident at once: config 3's
+// 5,000 legacy documents (one wave each) fit the chip's 1,024 SIMDs at five
+// waves, but not at four, where the last 904 start only as the first finish --
+// 82.5 -> 68.6 ms per step, digests unchanged (round 6)
+#ifndef MTE_TREE0_WAVES
+#define MTE_TREE0_WAVES 5
 #endif
 #ifndef MTE_TREE1_WAVES  // TIER 1's (1: no bound, 224 VGPRs = 2 waves per SIMD)
 #define MTE_TREE1_WAVES 1
