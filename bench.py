@@ -42,7 +42,7 @@ METRIC = "sequenced ops merged/sec (node) at 10k docs×10k ops; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md "Chip-level parameters"
 # PMC-measured HBM bytes of one replay launch (tools/pmc_traffic.py over two
 # rocprofv3 --pmc passes); reported only for the libmte.so it was measured on
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r05", "final", "pmc_traffic_config{cfg}.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r06", "final", "pmc_traffic_config{cfg}.json")
 
 WORKLOADS = {
     3: "config3: 10k docs x 10k ops/doc, insert/remove/annotate 1:1:1, 1/16 markers, 8 clients, R=64, "
