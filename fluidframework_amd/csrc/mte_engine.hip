@@ -2018,10 +2018,15 @@ static int read_refs_view(mte_ctx* c, uint32_t doc, int32_t* pos, uint32_t n, bo
   std::vector<int32_t> len(ns + 1), rseq(ns + 1);
   std::vector<uint32_t> toff(ns + 1);
   std::vector<uint2> rt(n + 1);
+  std::vector<uint32_t> tw;  // tree words, for Transient references (their leaf ids)
   if (ns) {
     HIPCHK(c, hipMemcpyAsync(len.data(), c->soa.len + db, ns * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(rseq.data(), c->soa.rseq + db, ns * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(toff.data(), c->soa.toff + db, ns * 4, hipMemcpyDeviceToHost, c->stream));
+    if (c->d_tree) {
+      tw.resize(ns);
+      HIPCHK(c, hipMemcpyAsync(tw.data(), c->d_tree + db, ns * 4, hipMemcpyDeviceToHost, c->stream));
+    }
   }
   if (n)
     HIPCHK(c, hipMemcpyAsync(rt.data(), c->d_refs + (uint64_t)doc * c->ref_cap, n * sizeof(uint2),
@@ -2029,6 +2034,20 @@ static int read_refs_view(mte_ctx* c, uint32_t doc, int32_t* pos, uint32_t n, bo
   HIPCHK(c, hipStreamSynchronize(c->stream));
   for (uint32_t r = 0; r < n; r++) {
     pos[r] = -1;
+    if ((rt[r].y & kRefLive) && (rt[r].y & kRefTrans)) {
+      // a Transient reference: its segment (leaf id) + its offset, the offset
+      // dropped once removed; -1 once the segment is gone (mergeTree.ts:1095-1112)
+      int64_t p = 0;
+      for (uint32_t i = 0; i < ns && i < (uint32_t)tw.size(); i++) {
+        const bool head = !(tw[i] & (kTCont | kTEmpty));
+        if (head && ((tw[i] >> 8) & (kIdLimit - 1u)) == rt[r].x) {
+          pos[r] = (int32_t)(p + (rseq[i] != kNone ? 0 : (int64_t)(rt[r].y & kRefTransOff)));
+          break;
+        }
+        p += rseq[i] == kNone ? len[i] : 0;
+      }
+      continue;
+    }
     if (!(rt[r].y & kRefLive) || ((rt[r].y & kRefDetached) && !(transient && (rt[r].y & kRefOff)))) continue;
     int64_t p = 0;
     for (uint32_t i = 0; i < ns; i++) {

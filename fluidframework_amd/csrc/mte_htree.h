@@ -1245,6 +1245,33 @@ __device__ __forceinline__ int ht_range(HT& h, const s8v& op, bool local, const 
 
 // ---- local records (titems.c doc_ack, doc_rollback, doc_rollback_annotate, doc_regen) ----------
 
+// createLocalReferencePosition of a Transient reference (titems.c doc_ref):
+// getContainingSegment(pos) in the local view -- the leaf holding pos and the
+// offset in it -- kept as (leaf id, offset), never moved (kRefTrans)
+template <int K>
+__device__ __forceinline__ int ht_ref_transient(HT& h, uint2* rt, uint32_t& rhi, const s8v& op) {
+  const uint32_t slot = (uint32_t)op[5], typ = (uint32_t)op[6];
+  const int32_t pos = op[4];
+  if (typ & (MTE_REF_SLIDE_ON_REMOVE | MTE_REF_STAY_ON_REMOVE)) return MTE_E_INVALID_ARG;
+  ht_persp(h, true, 0, 0);  // the local view
+  const int32_t* Lp = h.L;
+  const int32_t* Pp = h.P;
+  const int x = ht_first_lp(h, 0, [&](int i) {
+    const int32_t l = (int32_t)ld_l2((const uint32_t*)Lp + i);
+    const int32_t p = (int32_t)ld_l2((const uint32_t*)Pp + i);
+    return l > 0 && pos >= p && pos < p + l;
+  });
+  if (x < 0) return MTE_E_INVALID_ARG;  // no segment holds pos in the local view
+  const int hd = ht_leaf_start(h, x);
+  const int32_t off = pos - own_prefix(h.pl, h.sd, hd);
+  if (off < 0 || (uint32_t)off > kRefTransOff) return MTE_E_UNSUPPORTED;
+  lane0_st(&rt[slot].x, t_id(ht_T(h, hd)));
+  lane0_st(&rt[slot].y, kRefLive | kRefDetached | kRefTrans | (uint32_t)off);
+  vm_drain();
+  if (slot + 1 > rhi) rhi = slot + 1;
+  return 0;
+}
+
 // an item the ack of ls still has to take: inserted, removed or annotated by
 // ls (am_mask: ls's annotate slot), or a removal of ls a remote one overtook
 // (titems.c ack_pending)
@@ -2090,7 +2117,7 @@ __device__ __noinline__ uint32_t ht_ref_snapshot(const uint32_t* pl, uint64_t sd
     const uint32_t r = rb + (uint32_t)l;
     const uint32_t rc = r < rhi ? r : 0u;  // unconditional loads, selected after
     const uint32_t anc = ld_l2(&rt[rc].x), st = ld_l2(&rt[rc].y);
-    const bool live = r < rhi && (st & kRefLive);
+    const bool live = r < rhi && (st & kRefLive) && !(st & kRefTrans);  // a Transient one slides no interval
     const bool det = (st & kRefDetached) != 0, off = (st & kRefOff) != 0;
     int32_t pos = -1, tpos = -1, key = -1, own = 0, all = 0;
     bool found = false;
@@ -2193,7 +2220,8 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
       // reference made on a segment (b = 0 / 2), or one ackInterval re-makes (b = 3)
       const uint32_t slot = (uint32_t)op[5];
       const uint2 before = make_uint2(uni(ld_l2(&rt[slot].x)), uni(ld_l2(&rt[slot].y)));
-      rc = stream_ref<K>(h.pl, h.sd, h.n, rt, rhi, op, D.min_seq, h.newcalc);
+      if ((uint32_t)op[7] == 0u && ((uint32_t)op[6] & MTE_REF_TRANSIENT)) rc = ht_ref_transient<K>(h, rt, rhi, op);
+      else rc = stream_ref<K>(h.pl, h.sd, h.n, rt, rhi, op, D.min_seq, h.newcalc);
       const uint2 after = make_uint2(uni(ld_l2(&rt[slot].x)), uni(ld_l2(&rt[slot].y)));
       const uint32_t b = (uint32_t)op[7];
       if ((b == 0u || b == 2u) ? !(after.y & kRefDetached)

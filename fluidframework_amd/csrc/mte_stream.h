@@ -119,6 +119,12 @@ __device__ __forceinline__ int32_t own_prefix(const uint32_t* pl, uint64_t sd, i
 // (mergeTree.ts:935-942, removeLocalRef keeps the segment): detached for
 // every read but mte_read_refs_transient, which still finds its segment.
 constexpr uint32_t kRefLive = 0x80000000u, kRefDetached = 0x40000000u, kRefOff = 0x20000000u;
+// a Transient reference (localReference.ts:263: never on its segment's list, so
+// nothing moves or slides it): kRefLive | kRefDetached | kRefTrans | its offset
+// in its segment, x = that segment's leaf id (mte_htree.h ht_ref_transient;
+// titems.c REF_TRANS): read as its segment's position + the offset, the offset
+// dropped once the segment is removed, -1 once the segment is gone
+constexpr uint32_t kRefTrans = 0x10000000u, kRefTransOff = 0x0fffffffu;
 
 // a segment references may slide to (_getSlideToSegment, mergeTree.ts:893-913):
 // not a pending insert and not removed-and-acked (a pending removal is fine)

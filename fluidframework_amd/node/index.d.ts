@@ -211,7 +211,7 @@ export interface SequenceMaintenanceEvent {
   last: { operation: number; position: number; length: number };
 }
 
-/** ReferenceType flags (ops.ts): Simple 0, SlideOnRemove 0x40, StayOnRemove 0x80 (Transient unsupported). */
+/** ReferenceType flags (ops.ts): Simple 0, SlideOnRemove 0x40, StayOnRemove 0x80, Transient 0x100. */
 export class LocalReferencePosition {
   readonly refType: number;
   properties?: PropertySet;

@@ -854,8 +854,9 @@ class BatchClient {
   /** Client.createLocalReferencePosition (client.ts:360-364): a reference at
    *  offset of segment (from getContainingSegment; a number is taken as a
    *  position of this client's view).  refType: ReferenceType flags --
-   *  SlideOnRemove (0x40), StayOnRemove (0x80) or Simple (0), with any label
-   *  bits; Transient throws.  Queued with the document's next replay. */
+   *  SlideOnRemove (0x40), StayOnRemove (0x80), Simple (0) or Transient
+   *  (0x100: kept on its segment, never slid -- localReference.ts:263), with
+   *  any label bits.  Queued with the document's next replay. */
   createLocalReferencePosition(segment, offset, refType, properties) {
     if (!this.engine.docs[this.doc].refs) throw new MergeTreeError(-9, "createClient(..., {refs: true}) first");
     const base = typeof segment === "number" ? segment : (segment && typeof segment.start === "number" ? segment.start : NaN);

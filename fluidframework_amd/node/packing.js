@@ -789,8 +789,8 @@ class BatchBuilder {
   addRef(doc, clients, pos, refType) {
     if (!clients.local) throw new MergeTreeError(E_UNSUPPORTED, "local reference in an observer document");
     const rt = checkI32(refType === undefined ? REF_SLIDE_ON_REMOVE : refType, "refType");
-    if (rt < 0 || (rt & REF_TRANSIENT)) {
-      throw new MergeTreeError(E_UNSUPPORTED, "Transient local references (positions are not tracked)");
+    if (rt < 0 || ((rt & REF_TRANSIENT) && (rt & (REF_SLIDE_ON_REMOVE | REF_STAY_ON_REMOVE)))) {
+      throw new MergeTreeError(E_INVALID_ARG, "Transient with SlideOnRemove or StayOnRemove (localReference.ts:27-38)");
     }
     if ((rt & REF_SLIDE_ON_REMOVE) && (rt & REF_STAY_ON_REMOVE)) {
       throw new MergeTreeError(E_INVALID_ARG, "SlideOnRemove and StayOnRemove together");

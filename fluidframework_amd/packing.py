@@ -638,12 +638,15 @@ class BatchBuilder:
         """Client.createLocalReferencePosition on the segment and offset that
         getContainingSegment(pos) finds in the local view (client.ts:360-364,
         1107-1110; mergeTree.ts:872-885, 2124-2143): an MTE_OP_REF record in an
-        MTE_DOC_REFS document.  Returns the reference's slot (mte_read_refs)."""
+        MTE_DOC_REFS document.  A Transient one is its segment and offset, never
+        moved or slid (localReference.ts:263).  Returns the reference's slot
+        (mte_read_refs)."""
         if not clients.local:
             raise MergeTreeError(MTE_E_UNSUPPORTED, "local reference in an observer document")
         ref_type = _check_i32(ref_type, "refType")
-        if ref_type & REF_TRANSIENT or ref_type < 0:
-            raise MergeTreeError(MTE_E_UNSUPPORTED, "Transient local references (positions are not tracked)")
+        if ref_type < 0 or (ref_type & REF_TRANSIENT and ref_type & (REF_SLIDE_ON_REMOVE | REF_STAY_ON_REMOVE)):
+            raise MergeTreeError(MTE_E_INVALID_ARG, "Transient with SlideOnRemove or StayOnRemove "
+                                 "(localReference.ts:27-38)")
         if ref_type & REF_SLIDE_ON_REMOVE and ref_type & REF_STAY_ON_REMOVE:
             raise MergeTreeError(MTE_E_INVALID_ARG, "SlideOnRemove and StayOnRemove together")
         slot = _ref_slot(clients)

@@ -181,9 +181,15 @@ extern "C" {
  *     (client.ts:360-364, mergeTree.ts:2124-2143) on the segment and offset
  *     that getContainingSegment(pos1) finds in the local view
  *     (mergeTree.ts:872-885); a = the ReferenceType flags (ops.ts): Simple (0),
- *     SlideOnRemove (0x40) or StayOnRemove (0x80), plus any of the label bits;
- *     SlideOnRemove with StayOnRemove is MTE_E_INVALID_ARG, Transient
- *     MTE_E_UNSUPPORTED; pos1 outside the local view MTE_E_INVALID_ARG.
+ *     SlideOnRemove (0x40), StayOnRemove (0x80) or Transient (0x100), plus
+ *     any of the label bits; SlideOnRemove with StayOnRemove (or either with
+ *     Transient) is MTE_E_INVALID_ARG; pos1 outside the local view
+ *     MTE_E_INVALID_ARG.  A Transient reference (localReference.ts:263) stays
+ *     on that segment and offset -- never moved, slid or detached -- and
+ *     reads as the segment's position, plus the offset unless the segment is
+ *     removed, -1 once it is unlinked; local-client documents only (the HBM
+ *     tree pass; elsewhere MTE_E_UNSUPPORTED).  b = 2 / 3 with Transient:
+ *     MTE_E_UNSUPPORTED.
  *   1 remove: removeLocalReferencePosition (mergeTree.ts:2113-2123).
  *   2 create in a sequenced op's perspective (the interval collection's
  *     remote add / change, intervalCollection.ts:639-658): ref_seq and client
@@ -250,7 +256,7 @@ extern "C" {
 #define MTE_RP_BEFORE2 0x0800u
 #define MTE_REF_SLIDE_ON_REMOVE 0x40u /* ReferenceType.SlideOnRemove             */
 #define MTE_REF_STAY_ON_REMOVE 0x80u  /* ReferenceType.StayOnRemove              */
-#define MTE_REF_TRANSIENT 0x100u      /* ReferenceType.Transient (unsupported)    */
+#define MTE_REF_TRANSIENT 0x100u      /* ReferenceType.Transient (b = 0 only)     */
 /* Segment groups of pending local annotates (mergeTree.ts:1874-1880): a local
  * annotate record with b = a slot 0..31 marks every segment it visits with
  * that slot (MTE_NO_PROPS: not tracked); an MTE_OP_ACK record's a is the mask

@@ -716,6 +716,14 @@ static uint64_t apply_combine(uint32_t* props, uint32_t n_keys, const mte_propse
 /* with REF_DETACHED: taken off its segment's list for want of a segment to
  * slide to (mergeTree.ts:935-942; removeLocalRef keeps the segment) */
 #define REF_OFF 0x20000000u
+/* a Transient reference (localReference.ts:263: never on its segment's list,
+ * so nothing moves or slides it): REF_LIVE | REF_DETACHED | REF_TRANS | the
+ * offset in its segment; the anchor is that segment's leaf id -- the segment
+ * keeps it across splits (splitAt keeps the head), loses it for good when the
+ * zamboni appends it to the one before (a later split there makes a new
+ * segment, a new id) or unlinks it (position -1, mergeTree.ts:1095-1112) */
+#define REF_TRANS 0x10000000u
+#define REF_TRANS_OFF 0x0fffffffu
 #define REF_LIMIT (1u << 24)
 
 /* a segment references may slide to (_getSlideToSegment, mergeTree.ts:893-913):
@@ -1015,8 +1023,27 @@ static int doc_ref(idoc* d, const mte_op* op) {
     d->ref_state[slot] = 0;
     return MTE_OK;
   }
-  if (op->a & MTE_REF_TRANSIENT) return MTE_E_UNSUPPORTED;
+  if ((op->a & MTE_REF_TRANSIENT) && op->b != 0) return MTE_E_UNSUPPORTED;
   if ((op->a & MTE_REF_SLIDE_ON_REMOVE) && (op->a & MTE_REF_STAY_ON_REMOVE)) return MTE_E_INVALID_ARG;
+  if (op->a & MTE_REF_TRANSIENT) {
+    /* createLocalReferencePosition(getContainingSegment(pos)) in the local view */
+    d->scanned += d->n;
+    int64_t p = 0;
+    for (uint32_t i = 0; i < d->n; i++) {
+      const int32_t l = d->it[i].empty ? 0 : own_len(&d->it[i]);
+      if (l > 0 && op->pos1 >= p && op->pos1 < p + l) {
+        const uint32_t h = leaf_start(d, i);
+        const int64_t off = op->pos1 - own_prefix(d, h);
+        if (off < 0 || off > (int64_t)REF_TRANS_OFF) return MTE_E_UNSUPPORTED;
+        if (slot + 1 > d->ref_hi) d->ref_hi = slot + 1;
+        d->ref_anchor[slot] = d->it[h].id;
+        d->ref_state[slot] = REF_LIVE | REF_DETACHED | REF_TRANS | (uint32_t)off;
+        return MTE_OK;
+      }
+      if (l > 0) p += l;
+    }
+    return MTE_E_INVALID_ARG;
+  }
   d->scanned += d->n;
   if (op->b == 3) {
     uint32_t st = d->ref_state[slot];
@@ -1679,7 +1706,7 @@ static int64_t ref_order_key(const idoc* d, uint32_t r);
  * reference's slide callbacks read mid-op (intervalCollection.ts:1042-1053) */
 static int ref_snapshot(idoc* d) {
   for (uint32_t r = 0; r < d->ref_hi; r++) {
-    if (!(d->ref_state[r] & REF_LIVE)) continue;
+    if (!(d->ref_state[r] & REF_LIVE) || (d->ref_state[r] & REF_TRANS)) continue;  /* no interval end */
     const int32_t p = ref_position(d, r, 0), tp = ref_position(d, r, 1);
     const int rc = delta_push(d, MTE_DELTA_REFPOS, p >= 0 ? p : (tp >= 0 ? -2 - tp : -1), (int32_t)ref_order_key(d, r), r);
     if (rc) return rc;
@@ -2255,6 +2282,16 @@ int oti_read_ref_order(oti_ctx* c, uint32_t doc, int64_t* key, uint32_t n) {
 static int32_t ref_position(const idoc* d, uint32_t r, int transient) {
   if (r >= d->ref_hi) return -1;
   const uint32_t st = d->ref_state[r], u = d->ref_anchor[r];
+  if ((st & REF_LIVE) && (st & REF_TRANS)) {
+    /* referencePositionToLocalPosition of a Transient one: its segment's
+     * position, plus the offset unless the segment is removed; -1 unlinked */
+    for (uint32_t i = 0; i < d->n; i++) {
+      const item* g = &d->it[i];
+      if (!g->empty && !g->cont && g->id == u)
+        return (int32_t)(own_prefix(d, i) + (g->rseq != NONE_SEQ ? 0 : (int64_t)(st & REF_TRANS_OFF)));
+    }
+    return -1;
+  }
   if (!(st & REF_LIVE) || ((st & REF_DETACHED) && !(transient && (st & REF_OFF)))) return -1;
   int64_t p = 0;
   for (uint32_t i = 0; i < d->n; i++) {

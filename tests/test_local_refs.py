@@ -25,6 +25,15 @@ reference reads detached -- the unlink of its tombstone -- so they hold for
 the local-client documents' tree pass (titems.c, mte_htree.h), which keeps that
 zamboni; the flat restatement's compaction at minSeq detaches them at other
 times and is not held to them.
+
+Transient references (localReference.ts:263: createLocalReferencePosition
+keeps the segment and offset but never adds the reference to the segment's
+list, so nothing slides or detaches it; localReferencePositionToPosition
+reads its segment's position, plus the offset while the segment is not
+removed, -1 once the segment is unlinked) are pinned by 24 more farms
+(tests/golden/localref_transient_vectors.json.gz, make_farm_golden.py
+--transient), again for the tree pass: anchored by the leaf id of their
+segment, which splits never move (a split leaves the id on the head).
 """
 import gzip
 import json
@@ -42,6 +51,7 @@ from fluidframework_amd.packing import BatchBuilder, DocClients, Interner
 HERE = os.path.dirname(os.path.abspath(__file__))
 VECTORS = os.path.join(HERE, "golden", "localref_vectors.json.gz")
 STAY_VECTORS = os.path.join(HERE, "golden", "localref_stay_vectors.json.gz")
+TRANSIENT_VECTORS = os.path.join(HERE, "golden", "localref_transient_vectors.json.gz")
 
 
 def ref_sets(path=VECTORS):
@@ -115,6 +125,75 @@ def test_gpu_stay_farms():
     assert passed == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
 
 
+def test_transient_vectors_shape():
+    sets = ref_sets(TRANSIENT_VECTORS)
+    assert len(sets) == 24 and all(s["transient"] > 0 for s in sets)
+    made = [e for s in sets for ev in s["events"] for e in ev if e[0] == "F"]
+    assert len(made) > 2000 and sum(1 for e in made if e[2] & REF_TRANSIENT) > 500
+    vals = [p for s in sets for cp in s["checkpoints"] for st in cp["states"] for p in st["refs"]]
+    assert vals.count(-1) > 1000 and vals.count(None) > 1000
+
+
+def test_tree_oracle_transient_farms():
+    """The tree restatement equals the reference at every checkpoint of the
+    Transient farms; the flat restatement refuses Transient references."""
+    sets = ref_sets(TRANSIENT_VECTORS)
+    passed, failures = replay_ref_farm(tree_factory, sets)
+    assert not failures, failures[:2]
+    assert passed == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
+
+
+@pytest.mark.gpu
+def test_gpu_transient_farms():
+    sets = ref_sets(TRANSIENT_VECTORS)
+    passed, failures = replay_ref_farm(device_factory, sets)
+    assert not failures, failures[:2]
+    assert passed == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
+
+
+def _transient_scenario(factory):
+    """"abcdef" as "abc" + "def" (two segments); a Transient reference on 'e'
+    (segment "def", offset 1) and one on 'b'; a remote insert of "XY" at 4
+    splits "def" -- the reference stays on the head "d", offset 1, so it reads
+    4 ('X', not 'e': nothing moves a Transient reference); a remote remove of
+    [0, 3) makes 'b''s read its removed segment's position, offset dropped,
+    and 'd''s 0 + 1.  The flat restatement refuses Transient references."""
+    inits, text = doc_inits(["abc"], flags=DOC_NEW_LENGTH_CALC | DOC_LOCAL_CLIENT | DOC_REFS)
+    e = factory(4)
+    e.load_docs(inits, text)
+    cl = DocClients("B", local=True)
+    bb = BatchBuilder(1, Interner(4))
+    bb.add_message(0, cl, {"clientId": "C", "sequenceNumber": 1, "referenceSequenceNumber": 0,
+                           "minimumSequenceNumber": 0, "type": "op", "contents": {"type": 0, "pos1": 3, "seg": "def"}})
+    e.apply_batch(bb.build())
+    bb = BatchBuilder(1, Interner(4))
+    bb.add_ref(0, cl, 4, REF_TRANSIENT)
+    bb.add_ref(0, cl, 1, REF_TRANSIENT)
+    bb.add_message(0, cl, {"clientId": "C", "sequenceNumber": 2, "referenceSequenceNumber": 1,
+                           "minimumSequenceNumber": 0, "type": "op", "contents": {"type": 0, "pos1": 4, "seg": "XY"}})
+    e.apply_batch(bb.build())
+    mid = list(e.read_refs(0, 2))
+    bb = BatchBuilder(1, Interner(4))
+    bb.add_message(0, cl, {"clientId": "C", "sequenceNumber": 3, "referenceSequenceNumber": 2,
+                           "minimumSequenceNumber": 0, "type": "op", "contents": {"type": 1, "pos1": 0, "pos2": 3}})
+    e.apply_batch(bb.build())
+    return e, mid, list(e.read_refs(0, 2)), list(e.read_refs(0, 2, transient=True))
+
+
+def test_tree_oracle_transient_scenario():
+    e, mid, end, end_t = _transient_scenario(tree_factory)
+    assert (e.statuses() == 0).all()
+    assert mid == [4, 1] and end == [1, 0] and end_t == end
+    assert list(_transient_scenario(oracle_factory)[0].statuses()) == [MTE_E_UNSUPPORTED]
+
+
+@pytest.mark.gpu
+def test_gpu_transient_scenario():
+    e, mid, end, end_t = _transient_scenario(device_factory)
+    assert (e.statuses() == 0).all()
+    assert mid == [4, 1] and end == [1, 0] and end_t == end
+
+
 def test_localref_farm_live():
     """The committed vectors are what the erased reference computes now (build
     container only: the reference does not travel)."""
@@ -123,8 +202,8 @@ def test_localref_farm_live():
     if not ref_util.ref_available():
         pytest.skip("reference sources not in this container")
     keys = ("seed", "clients", "steps", "initialText", "nCheckpoints", "maxText", "rollback", "refs", "rollbackTypes",
-            "stay")
-    for s in ref_sets()[:4] + ref_sets(STAY_VECTORS)[:2]:
+            "stay", "transient")
+    for s in ref_sets()[:4] + ref_sets(STAY_VECTORS)[:2] + ref_sets(TRANSIENT_VECTORS)[:2]:
         inp = {"sets": [{k: s[k] for k in keys if k in s}]}
         p = subprocess.run(["node", os.path.join(os.path.dirname(HERE), "oracle", "ref_farm.js"), ref_util.build_ref()],
                            input=json.dumps(inp), capture_output=True, text=True, timeout=600, check=True)
@@ -219,13 +298,11 @@ def test_gpu_localref_farms():
 def test_packer_ref_rules():
     cl = DocClients("B", local=True)
     bb = BatchBuilder(1, Interner(4))
-    with pytest.raises(MergeTreeError) as ei:
-        bb.add_ref(0, cl, 0, REF_TRANSIENT)
-    assert ei.value.code == MTE_E_UNSUPPORTED
-    with pytest.raises(MergeTreeError) as ei:
-        bb.add_ref(0, cl, 0, REF_STAY_ON_REMOVE | REF_SLIDE_ON_REMOVE)
-    assert ei.value.code == MTE_E_INVALID_ARG
-    assert bb.add_ref(0, cl, 0) == 0 and bb.add_ref(0, cl, 1) == 1
+    for bad in (REF_STAY_ON_REMOVE | REF_SLIDE_ON_REMOVE, REF_TRANSIENT | REF_SLIDE_ON_REMOVE):
+        with pytest.raises(MergeTreeError) as ei:
+            bb.add_ref(0, cl, 0, bad)
+        assert ei.value.code == MTE_E_INVALID_ARG
+    assert bb.add_ref(0, cl, 0) == 0 and bb.add_ref(0, cl, 1) == 1 and bb.add_ref(0, cl, 1, REF_TRANSIENT) == 2
     bb.remove_ref(0, cl, 0)
     assert bb.add_ref(0, cl, 2) == 0  # a removed slot is reused
     with pytest.raises(MergeTreeError) as ei:

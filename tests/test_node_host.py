@@ -29,8 +29,9 @@ EXPORTS = ["abiVersion", "strerror", "create", "destroy", "lastError", "loadDocs
            "setRefCapacity", "readRefs", "readRefOrder"]
 
 
-def node(*args, timeout=300):
-    r = subprocess.run([NODE, *args], cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+def node(*args, timeout=300, env=None):
+    r = subprocess.run([NODE, *args], cwd=ROOT, capture_output=True, text=True, timeout=timeout,
+                       env=dict(os.environ, **env) if env else None)
     assert r.returncode == 0, r.stderr[-3000:]
     return r.stdout
 
@@ -78,7 +79,8 @@ def test_js_packing_matches_python_packing_on_fixtures(fresh):
 
 
 @pytest.mark.parametrize("vectors", ["farm_vectors.json.gz", "reconnect_vectors.json.gz", "localref_vectors.json.gz",
-                                     "localref_stay_vectors.json.gz", "relpos_farm_vectors.json.gz"])
+                                     "localref_stay_vectors.json.gz", "localref_transient_vectors.json.gz",
+                                     "relpos_farm_vectors.json.gz"])
 def test_js_packing_matches_python_packing_on_local_farms(vectors):
     """Local ops and acks (and, on the reconnect farms, ops held offline and
     regeneratePendingOp's MTE_OP_REGEN records): the JS and Python packers emit
@@ -324,11 +326,22 @@ def test_node_farm_every_client_local_on_gpu(mode):
         assert j["passed"] == sum(len(s["names"]) * len(s["checkpoints"]) for s in sets)
 
 
+def test_node_transient_references_on_restatement():
+    """BatchClient {localClient, refs} over the restatement's addon: the 24
+    Transient-reference farms, every checkpoint (tests/node/farm_gpu.js)."""
+    j = json.loads(node("tests/node/farm_gpu.js", "batched", "all", "localref_transient_vectors.json.gz", timeout=600,
+                        env={"MTE_NODE_ADDON": "oracle"}))
+    assert j["nFailures"] == 0, j["failures"]
+    assert j["passed"] == 734
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("vectors", ["localref_vectors.json.gz", "localref_stay_vectors.json.gz"])
+@pytest.mark.parametrize("vectors", ["localref_vectors.json.gz", "localref_stay_vectors.json.gz",
+                                     "localref_transient_vectors.json.gz"])
 def test_node_local_references_on_gpu(vectors):
     """BatchClient {localClient, refs}: every client of the 40 local-reference
-    farms the reference ran (and of the 32 with StayOnRemove references)
+    farms the reference ran (and of the 32 with StayOnRemove references, and
+    of the 24 with Transient ones)
     creates / removes its references through createLocalReferencePosition /
     removeLocalReferencePosition, and at every checkpoint
     localReferencePositionToPosition of each equals the reference's
