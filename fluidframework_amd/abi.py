@@ -10,6 +10,7 @@ import numpy as np
 MTE_ABI_VERSION = 1
 MTE_MAX_KEYS = 8
 MTE_MAX_CLIENTS = 32
+MTE_MAX_CLIENTS_TREE = 64  # local-client and MTE_DOC_TREE documents (include/mte.h)
 
 MTE_OK = 0
 MTE_E_INVALID_ARG = -1

@@ -177,9 +177,9 @@ __global__ void reset_kernel(DocHdr* hdr, SegSoA soa, uint32_t cap, const mte_do
     st[kHsEntered] = (in.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_TREE)) ? 1u : 0u;
     st[kHsWin] = 0u;  // no cached local partials
   }
-  if (in.flags & MTE_DOC_LOCAL_CLIENT) {  // nothing pending (mte_htree.h planes)
+  if (in.flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_TREE)) {  // nothing pending, no removers >= 32 (mte_htree.h planes)
     const uint32_t nz = n_img ? n_img : 1u;
-    for (uint32_t k = 0; k < 2 * kt + 5; k++)  // the local planes (mte_htree.h kLocalPlanes)
+    for (uint32_t k = 0; k < 2 * kt + 6; k++)  // the local planes (mte_htree.h kLocalPlanes)
       for (uint32_t x = 0; x < nz; x++) soa.props[(kt + k) * soa.plane_stride + (uint64_t)d * cap + x] = 0u;
   }
   if (n_img) return;  // image_kernel writes the segments
@@ -1324,18 +1324,20 @@ int mte_load_docs(mte_ctx* c, uint32_t n_docs, const mte_doc_init* docs, const u
         (MTE_DOC_EVENTS | MTE_DOC_NEW_LENGTH_CALC))
       c->h_sdocs.push_back(d);
     if (docs[d].flags & MTE_DOC_LOCAL_CLIENT) c->h_local[d] = 1, any_local = true;
-    else if (docs[d].flags & MTE_DOC_TREE) c->h_local[d] = 2;
+    else if (docs[d].flags & MTE_DOC_TREE) c->h_local[d] = 2, any_local = true;
     if (docs[d].flags & MTE_DOC_EVENTS) c->h_events[d] = 1;
     if (docs[d].flags & MTE_DOC_REFS) c->h_refs[d] = 1, any_refs = true;
     const uint32_t sl = MTE_DOC_REFS | MTE_DOC_EVENTS | MTE_DOC_SLIDE_EVENTS;
     if ((docs[d].flags & sl) == sl) c->h_slides[d] = 1;
   }
   if (any_refs) HIPCHK(c, hipMalloc((void**)&c->d_refs, sizeof(uint2) * (size_t)c->ref_cap * n_docs));
-  // documents with a local client hold 2 kt + 5 more planes (mte_htree.h): the
+  // documents with a local client hold 2 kt + 6 more planes (mte_htree.h): the
   // pending property keys, the annotate-group mask, the keys' values before
   // their first pending annotate, localRemovedSeq, the removal-group order, the
-  // first group an item is one of the marked segments of, the regeneration group
-  const uint64_t prop_planes = (c->kt ? c->kt : 1) + (any_local ? 2 * c->kt + 5 : 0);
+  // first group an item is one of the marked segments of, the regeneration
+  // group, the removers of short ids 32 .. 63 (the last one MTE_DOC_TREE
+  // documents use too)
+  const uint64_t prop_planes = (c->kt ? c->kt : 1) + (any_local ? 2 * c->kt + 6 : 0);
   HIPCHK(c, hipMalloc((void**)&c->hdr, sizeof(DocHdr) * (n_docs ? n_docs : 1)));
   // one allocation, planes at stride nslots: len seq rseq rmask meta toff props[kt]
   // (kt >= n_keys planes, so the register-resident kernels never index past it)
@@ -2144,7 +2146,18 @@ int mte_read_segments(mte_ctx* c, uint32_t doc, mte_seg_list* v) {
     HIPCHK(c, hipMemcpyAsync(pl.data() + (size_t)p * n, reinterpret_cast<const uint32_t*>(c->soa.len) +
                                                              p * c->soa.plane_stride + db,
                              n * 4, hipMemcpyDeviceToHost, c->stream));
+  // the removers of short ids >= 32 (mte_htree.h kRmHiPlane): mte_seg.removers has 32 bits
+  std::vector<uint32_t> rmh;
+  if (n && !c->h_local.empty() && c->h_local[doc]) {
+    rmh.resize(n);
+    HIPCHK(c, hipMemcpyAsync(rmh.data(), reinterpret_cast<const uint32_t*>(c->soa.len) +
+                                             (uint64_t)(kFieldPlanes + 3 * c->kt + 5) * c->soa.plane_stride + db,
+                             n * 4, hipMemcpyDeviceToHost, c->stream));
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (uint32_t i = 0; i < (uint32_t)rmh.size(); i++)
+    if (rmh[i] && !(tw[i] & kTEmpty) && (int32_t)pl[2 * (size_t)n + i] != kNone)
+      return set_err(c, MTE_E_UNSUPPORTED, "doc %u: a segment removed by a short id >= 32 (mte_seg.removers)", doc);
   uint64_t nt = 0;
   uint64_t m = 0;  // segments out (a tree pass placeholder is none, a merged leaf one)
   for (uint32_t i = 0; i < n; i++) {

@@ -93,7 +93,11 @@ template <int K> constexpr int kGrpPlane = kFieldPlanes + 3 * K + 2;
 // split off it since (titems.c item.rg, MTE_F_REGENERATED)
 template <int K> constexpr int kBornPlane = kFieldPlanes + 3 * K + 3;
 template <int K> constexpr int kRgPlane = kFieldPlanes + 3 * K + 4;
-template <int K> constexpr int kLocalPlanes = kFieldPlanes + 3 * K + 5;  // planes of a local-client document
+// kRmHiPlane: removedClientIds of short ids 32 .. 63 (MTE_MAX_CLIENTS_TREE;
+// plane 3 holds 0 .. 31), zero while the item is not removed; the last plane
+// of every document with nP = kLocalPlanes (local-client and MTE_DOC_TREE ones)
+template <int K> constexpr int kRmHiPlane = kFieldPlanes + 3 * K + 5;
+template <int K> constexpr int kLocalPlanes = kFieldPlanes + 3 * K + 6;  // planes of a local-client / MTE_DOC_TREE document
 
 struct HT {
   uint32_t* pl;   // the document's plane base
@@ -165,7 +169,7 @@ __device__ __forceinline__ int32_t ht_item_len(const HT& h, int32_t len, int32_t
   }
   const int c = h.pc;
   const int32_t r = h.pr;
-  const bool by_c = ((rmask >> c) & 1u) != 0;
+  const bool by_c = ((rmask >> (c & 31)) & 1u) != 0;  // rmask: the half of the mask that holds c (ht_ensure)
   const int cli = (int)(meta & 0xffu) - 1;
   if (h.newcalc) {  // mergeTree.ts:1003-1026
     if (removed) {
@@ -200,6 +204,8 @@ __device__ __forceinline__ void ht_inval(HT& h, int from) {
 __device__ __forceinline__ void ht_ensure(HT& h, int upto) {
   const int l = lane_id();
   bool wrote = false;
+  // the removers plane holding the perspective's client (ht_item_len)
+  const uint32_t* rmp = h.pl + (uint64_t)(h.pc < 32 ? 3 : h.nP - 1) * h.sd;
   while (h.lp_n <= upto && h.lp_n < h.n) {
     const int tb = h.lp_n;
     int32_t len[kHE], seq[kHE], rseq[kHE];
@@ -211,7 +217,7 @@ __device__ __forceinline__ void ht_ensure(HT& h, int upto) {
       len[j] = (int32_t)ld_l2(h.pl + ic);
       seq[j] = (int32_t)ld_l2(h.pl + h.sd + ic);
       rseq[j] = (int32_t)ld_l2(h.pl + 2 * h.sd + ic);
-      rmask[j] = ld_l2(h.pl + 3 * h.sd + ic);
+      rmask[j] = ld_l2(rmp + ic);
       meta[j] = ld_l2(h.pl + 4 * h.sd + ic);
       t[j] = ld_l2(h.tw + ic);
     }
@@ -1154,13 +1160,15 @@ __device__ __forceinline__ int ht_range(HT& h, const s8v& op, bool local, const 
           h.pl[(uint64_t)kLrsPlane<K> * h.sd + i] = (uint32_t)s;
           h.pl[(uint64_t)kGrpPlane<K> * h.sd + i] = (uint32_t)i;
         } else {
-          const uint32_t rm = ld_l2(h.pl + 3 * h.sd + i);
+          // removers: plane 3 for short ids < 32, the last plane (kRmHiPlane) for the rest
+          uint32_t* rmp = h.pl + (uint64_t)(c < 32 ? 3 : h.nP - 1) * h.sd + i;
+          const uint32_t rm = ld_l2(rmp);
           if (rs[j] == kNone) {
             h.pl[2 * h.sd + i] = (uint32_t)s;
-            h.pl[3 * h.sd + i] = 1u << c;
+            *rmp = 1u << (c & 31);  // the other half is zero while the item is not removed
           } else {
             if (rs[j] >= kLocalBase) h.pl[2 * h.sd + i] = (uint32_t)s;  // overtaking our pending removal (:1928-1938)
-            h.pl[3 * h.sd + i] = rm | (1u << c);
+            *rmp = rm | (1u << (c & 31));
           }
         }
       } else {
@@ -1498,6 +1506,7 @@ __device__ __forceinline__ int ht_rollback(HT& h, const s8v& op, const ReplayArg
       ht_setpl(h, 1, i, 0u);
       ht_setpl(h, 2, i, 0u);
       ht_setpl(h, 3, i, 1u);
+      ht_setpl(h, kRmHiPlane<K>, i, 0u);
       vm_drain();
       if (evd) ev_one(ev, MTE_OP_REMOVE, lp, len);
       if ((rc = ht_zamboni<K>(h, a.n_keys, ev))) return rc;
@@ -1507,6 +1516,7 @@ __device__ __forceinline__ int ht_rollback(HT& h, const s8v& op, const ReplayArg
   for (int i = ht_member<K>(h, 0, t, ls, 0); i >= 0; i = ht_member<K>(h, i + 1, t, ls, 0)) {
     ht_setpl(h, 2, i, (uint32_t)kNone);
     ht_setpl(h, 3, i, 0u);
+    ht_setpl(h, kRmHiPlane<K>, i, 0u);
     ht_setpl(h, kLrsPlane<K>, i, 0u);
     vm_drain();
     if (evd) ev_one(ev, MTE_OP_INSERT, own_prefix(h.pl, h.sd, i), (int32_t)ht_pl(h, 0, i));
@@ -1705,7 +1715,7 @@ __device__ __forceinline__ void ht_item_partial(const HT& h, int i, int32_t R, i
   const uint32_t tt = ld_l2(h.tw + i);
   const int32_t c = (int32_t)ld_l2(h.pl + i), sq = (int32_t)ld_l2(h.pl + h.sd + i);
   const int32_t rs = (int32_t)ld_l2(h.pl + 2 * h.sd + i);
-  const uint32_t rm = ld_l2(h.pl + 3 * h.sd + i);
+  const uint32_t rm = ld_l2(h.pl + 3 * h.sd + i), rmh = ld_l2(h.pl + (uint64_t)kRmHiPlane<K> * h.sd + i);
   const int32_t lr = (int32_t)(ld_l2(h.pl + (uint64_t)kLrsPlane<K> * h.sd + i) & ~kLrsReleased);
   if (tt & kTEmpty) return;
   if (sq < kLocalBase) {
@@ -1727,7 +1737,7 @@ __device__ __forceinline__ void ht_item_partial(const HT& h, int i, int32_t R, i
     return;
   }
   if (rs <= R) a -= c;
-  if (__popc(rm) > 1 && lr != 0 && lr <= L) {
+  if (__popc(rm) + __popc(rmh) > 1 && lr != 0 && lr <= L) {
     b -= c;
     fl = true;
     if (rs <= R) o -= c;
@@ -2165,7 +2175,9 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
   ev.op = D.k;
   const uint32_t ev_from = ev.n;  // this record's first event
   if (h.n + 4 > h.cap) return MTE_E_CAPACITY;
-  if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
+  // short ids: 64 where the removers' upper half has its plane (kRmHiPlane)
+  const uint32_t max_c = h.nP == kLocalPlanes<K> ? MTE_MAX_CLIENTS_TREE : MTE_MAX_CLIENTS;
+  if (c >= max_c) return MTE_E_CLIENT_RANGE;
   const int32_t s = op[0], msn = op[2];
   const bool lop = (flags & MTE_F_LOCAL) != 0;
   int rc;
@@ -2181,7 +2193,7 @@ __device__ __forceinline__ int ht_step(HT& h, DocRun& D, uint32_t (&st)[kNumStat
     const uint32_t nw3 = (uint32_t)nx[3];
     const uint32_t nt = nw3 & 0xffu, nc = (nw3 >> 8) & 0xffu;
     const bool nloc = ((nw3 >> 16) & MTE_F_LOCAL) != 0;
-    if (nt > MTE_OP_ANNOTATE || nc >= MTE_MAX_CLIENTS) return MTE_E_INVALID_ARG;
+    if (nt > MTE_OP_ANNOTATE || nc >= max_c) return MTE_E_INVALID_ARG;
     const uint32_t key = (uint32_t)op[6];
     h.rpf = 0;
     if (flags & MTE_RP_POS1) {
@@ -2372,7 +2384,7 @@ __global__ __launch_bounds__(64) MTE_HTREE_ATTR void htree_kernel(ReplayArgs a, 
   h.hp = reinterpret_cast<uint32_t*>(t.heap + (uint64_t)doc * (t.hcap + 1));
   h.hcap = t.hcap;
   h.cap = (int)a.cap;
-  h.nP = ldoc ? kLocalPlanes<K> : kFieldPlanes + K;
+  h.nP = (ldoc || (hf & MTE_DOC_TREE)) ? kLocalPlanes<K> : kFieldPlanes + K;
   h.n = D.n;
   h.newcalc = (hf & MTE_DOC_NEW_LENGTH_CALC) != 0;
   h.ldoc = ldoc;

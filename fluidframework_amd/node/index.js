@@ -963,7 +963,7 @@ class BatchClient {
    *  message senders are recycled behind the window (DocClients). */
   getOrAddShortClientId(longId) {
     const i = this.clients.short(longId);
-    if (i >= packing.MAX_CLIENTS) throw new MergeTreeError(-12, "client " + String(longId) + ": no free client slot");
+    if (i >= this.clients.maxClients) throw new MergeTreeError(-12, "client " + String(longId) + ": no free client slot");
     return i;
   }
 

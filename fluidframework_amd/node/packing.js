@@ -45,6 +45,8 @@ const VALUE_UNEQUAL = 0x40000000;
 const LOCAL_SEQ_BASE = 0x40000000; // MTE_LOCAL_SEQ_BASE
 const NO_PROPS = 0xffffffff;
 const MAX_CLIENTS = 32;
+// local-client and MTE_DOC_TREE documents (the HBM tree pass: a second removers plane)
+const MAX_CLIENTS_TREE = 64;
 const OP_BYTES = 32;
 const DOC_INIT_BYTES = 24;
 const DOC_NEW_LENGTH_CALC = 0x1;
@@ -194,9 +196,9 @@ class Interner {
   }
 }
 
-/** Per-document long -> short client id map (client.ts:683-698). */
 /** Per-document long -> short client id map (client.ts:683-698) over the
- *  engine's MAX_CLIENTS slots.  A slot is recycled for a new client once the
+ *  engine's MAX_CLIENTS slots (MAX_CLIENTS_TREE in local-client and tree
+ *  documents).  A slot is recycled for a new client once the
  *  window's minSeq has passed every seq its client used: its segments are then
  *  visible to every perspective and its tombstones compacted
  *  (mergeTree.ts:1003-1054, 1077-1093), so the slot number decides no
@@ -208,8 +210,9 @@ class DocClients {
     // an MTE_DOC_TREE document (the HBM tree pass without a local client): it
     // takes sequenced combining ops too
     this.tree = !!tree;
+    this.maxClients = local || tree ? MAX_CLIENTS_TREE : MAX_CLIENTS;
     this.ids = new Map([[observerId, 0]]);
-    this.last = new Int32Array(MAX_CLIENTS).fill(NEVER); // slot -> highest seq its client used
+    this.last = new Int32Array(MAX_CLIENTS_TREE).fill(NEVER); // slot -> highest seq its client used
     this.lastId = observerId;  // the last sender and its slot (messages come in runs per sender)
     this.lastSlot = 0;
     this.minSeq = minSeq || 0;          // the window's minSeq before the next message
@@ -249,7 +252,7 @@ class DocClients {
     let i = longId === this.lastId ? this.lastSlot : this.ids.get(longId);
     if (i === undefined) {
       i = this._freeSlot();
-      if (i >= MAX_CLIENTS) return i; // the caller throws E_CLIENT_RANGE
+      if (i >= this.maxClients) return i; // the caller throws E_CLIENT_RANGE
       this.ids.set(longId, i);
       this.last[i] = seq === undefined ? NEVER : seq;
     } else if (seq !== undefined && this.last[i] !== NEVER) {
@@ -261,7 +264,7 @@ class DocClients {
   }
   _freeSlot() {
     const used = new Set(this.ids.values());
-    for (let s = 1; s < MAX_CLIENTS; s++) if (!used.has(s)) return s;
+    for (let s = 1; s < this.maxClients; s++) if (!used.has(s)) return s;
     let best = -1, bestSeq = NEVER;
     for (const v of used) {
       if (v !== 0 && (best < 0 || this.last[v] < bestSeq || (this.last[v] === bestSeq && v < best))) {
@@ -269,7 +272,7 @@ class DocClients {
         bestSeq = this.last[v];
       }
     }
-    if (best < 0 || bestSeq > this.minSeq) return MAX_CLIENTS;
+    if (best < 0 || bestSeq > this.minSeq) return this.maxClients;
     for (const [k, v] of this.ids) if (v === best) { this.ids.delete(k); break; }
     if (this.lastSlot === best) this.lastId = undefined;  // its client leaves the cache with its slot
     return best;
@@ -830,6 +833,7 @@ class BatchBuilder {
     }
     if (msg.clientId === clients.observer) throw new MergeTreeError(E_INVALID_ARG, "a remote op of the local client");
     const short = slotOf(clients, msg.clientId, seq);
+    if (short >= MAX_CLIENTS) throw new MergeTreeError(E_CLIENT_RANGE, "an op's reference: short id " + short + " >= 32");
     const slot = this._refSlot(clients);
     this._put(doc, 0, ref, 0, OP_REF, short, F_LOCAL, checkI32(pos, "pos"), slot, rt, 2);
     const src = this._src(doc);
@@ -1126,10 +1130,10 @@ function packDocInits(docs, interner) {
  * does (snapshotLoader.ts:90-118); a missing client / seq means NonCollabClient
  * / UniversalSequenceNumber.
  */
-function slotOf(clients, longId, seq) {
+function slotOf(clients, longId, seq, max) {
   const s = clients.short(longId, seq);
-  if (s >= MAX_CLIENTS) {
-    throw new MergeTreeError(E_CLIENT_RANGE, "client " + String(longId) + ": more than " + MAX_CLIENTS +
+  if (s >= (max || clients.maxClients)) {
+    throw new MergeTreeError(E_CLIENT_RANGE, "client " + String(longId) + ": more than " + (max || clients.maxClients) +
       " clients inside the collab window");
   }
   return s;
@@ -1166,9 +1170,10 @@ function packSegments(docs, clientsOf, inits) {
       // slots recycle once minSeq passes it like those of live senders
       let mask = 0;
       const rc = sp.removedClientIds || (sp.removedClient !== undefined ? [sp.removedClient] : []);
-      for (const id of rc) mask |= 1 << slotOf(clientsOf(i), id, removed ? sp.removedSeq : undefined);
+      // a loaded segment's ids fit mte_seg (removers: 32 bits)
+      for (const id of rc) mask |= 1 << slotOf(clientsOf(i), id, removed ? sp.removedSeq : undefined, MAX_CLIENTS);
       buf.writeUInt32LE(mask >>> 0, o + 16);
-      buf.writeInt32LE(sp.client === undefined ? -1 : slotOf(clientsOf(i), sp.client, sp.seq), o + 20);
+      buf.writeInt32LE(sp.client === undefined ? -1 : slotOf(clientsOf(i), sp.client, sp.seq, MAX_CLIENTS), o + 20);
       buf.writeUInt32LE(kind, o + 24);
       buf.writeUInt32LE(props.add(segProps) >>> 0, o + 28);
       if (text !== null) { extra.push(text); textOff += text.length; }
@@ -1231,7 +1236,7 @@ function regenOps(op, idx, recs) {
 
 module.exports = {
   OP_INSERT, OP_REMOVE, OP_ANNOTATE, OP_NOOP, OP_ACK, OP_REGEN, DELTA_REGEN, ANNOTATE_SLOTS, F_MARKER, F_MSG_END, F_REWRITE,
-  F_LOCAL, NO_PROPS, MAX_CLIENTS, OP_REF, REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE, REF_TRANSIENT,
+  F_LOCAL, NO_PROPS, MAX_CLIENTS, MAX_CLIENTS_TREE, OP_REF, REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE, REF_TRANSIENT,
   INSERT, REMOVE, ANNOTATE, GROUP,
   MergeTreeError, Interner, DocClients, PropTable, BatchBuilder, canonicalJson, packDocInits, packSegments, utf16,
   regenOps,

@@ -31,7 +31,7 @@ import json
 import numpy as np
 
 from .abi import (COMBINE_PAIR, MTE_VALUE_UNEQUAL, F_COMBINE, F_LOCAL, F_REGENERATED, F_MARKER, F_MSG_END, F_REWRITE, LOCAL_SEQ_BASE, MTE_E_CAPACITY, MTE_E_CLIENT_RANGE,
-                  MTE_E_INVALID_ARG, MTE_E_STATE, MTE_E_UNSUPPORTED, MTE_MAX_CLIENTS, NO_PROPS, OP_ACK, OP_ROLLBACK,
+                  MTE_E_INVALID_ARG, MTE_E_STATE, MTE_E_UNSUPPORTED, MTE_MAX_CLIENTS, MTE_MAX_CLIENTS_TREE, NO_PROPS, OP_ACK, OP_ROLLBACK,
                   OP_REGEN, OP_RBKEY, OP_REF, OP_RELPOS, RP_BEFORE1, RP_BEFORE2, RP_POS1, RP_POS2,
                   ANNOTATE_SLOTS, REF_SLIDE_ON_REMOVE, REF_STAY_ON_REMOVE,
                   REF_TRANSIENT,
@@ -300,7 +300,8 @@ class DocClients:
     """Per-document long -> short client id map (client.ts:683-698).
 
     The reference numbers clients forever; the engine's short ids are MTE_MAX_CLIENTS
-    slots (the removers bitmask is 32 bits).  A slot is recycled for a new client once the
+    slots (the removers bitmask is 32 bits), MTE_MAX_CLIENTS_TREE in the documents the
+    HBM tree pass replays (local-client and MTE_DOC_TREE ones: 64 bits).  A slot is recycled for a new client once the
     collab window's minSeq has passed every seq its client used: from then on each of its
     segments has seq <= minSeq <= refSeq (visible to every perspective whoever inserted
     it, mergeTree.ts:1003-1054) and each segment it removed has removedSeq <= minSeq and
@@ -317,6 +318,7 @@ class DocClients:
         # an MTE_DOC_TREE document (the HBM tree pass without a local client):
         # it takes sequenced combining ops too
         self.tree = tree
+        self.max_clients = MTE_MAX_CLIENTS_TREE if (local or tree) else MTE_MAX_CLIENTS
         self.ids = {observer_id: 0}
         self.last = {0: self.NEVER}  # slot -> highest seq its client used
         self.min_seq = min_seq       # the window's minSeq before the next message
@@ -358,7 +360,7 @@ class DocClients:
         i = self.ids.get(long_id)
         if i is None:
             i = self._free_slot()
-            if i >= MTE_MAX_CLIENTS:
+            if i >= self.max_clients:
                 return i  # the caller raises MTE_E_CLIENT_RANGE
             self.ids[long_id] = i
             self.last[i] = self.NEVER if seq is None else seq
@@ -368,12 +370,12 @@ class DocClients:
 
     def _free_slot(self) -> int:
         used = set(self.ids.values())
-        for slot in range(1, MTE_MAX_CLIENTS):
+        for slot in range(1, self.max_clients):
             if slot not in used:
                 return slot
         seq, slot = min((self.last[v], v) for v in used if v != 0)
         if seq > self.min_seq:
-            return MTE_MAX_CLIENTS
+            return self.max_clients
         del self.ids[next(k for k, v in self.ids.items() if v == slot)]
         return slot
 
@@ -469,8 +471,8 @@ class BatchBuilder:
                     self._comb = None
         # the slot is taken only once the message has validated
         short = clients.short(sender, seq)
-        if short >= MTE_MAX_CLIENTS:
-            raise MergeTreeError(MTE_E_CLIENT_RANGE, f"client {sender!r}: more than {MTE_MAX_CLIENTS} "
+        if short >= clients.max_clients:
+            raise MergeTreeError(MTE_E_CLIENT_RANGE, f"client {sender!r}: more than {clients.max_clients} "
                                  "clients inside the collab window")
         if not recs:
             recs.append((OP_NOOP, 0, 0, 0, 0, NO_PROPS))

@@ -42,8 +42,15 @@ extern "C" {
 
 /* Property key planes held per segment (host interns key strings to 0..n_keys-1). */
 #define MTE_MAX_KEYS 8
-/* Distinct short client ids per document (removedClientIds is a bitmask). */
+/* Distinct short client ids per document (removedClientIds is a bitmask):
+ * MTE_MAX_CLIENTS on the flat passes, MTE_MAX_CLIENTS_TREE in documents the
+ * HBM tree pass replays (MTE_DOC_LOCAL_CLIENT, MTE_DOC_TREE), which hold the
+ * mask's upper half in a plane of their own.  A host recycles a short id once
+ * the collab window's minSeq passed every seq its client used, so these bound
+ * the clients sending inside one window, not a document's clients.  MTE_OP_REF
+ * records (b = 2) and mte_seg.removers take ids < MTE_MAX_CLIENTS. */
 #define MTE_MAX_CLIENTS 32
+#define MTE_MAX_CLIENTS_TREE 64
 
 /* ---- status codes ---------------------------------------------------------
  * Where the reference raises an assert with a hex code, the equivalent code is

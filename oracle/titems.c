@@ -49,7 +49,7 @@
 
 typedef struct {
   int32_t len, seq, rseq;
-  uint32_t rmask;
+  uint64_t rmask; /* removedClientIds: short ids < MTE_MAX_CLIENTS_TREE */
   int32_t cli;
   uint32_t kind, toff;
   uint32_t props[MTE_MAX_KEYS];
@@ -206,7 +206,7 @@ static item placeholder(uint8_t h) {
 
 static inline int32_t leaf_len(const item* s, int32_t r, int c, int32_t m, int newcalc) {
   const int removed = s->rseq != NONE_SEQ;
-  const int by_c = (int)((s->rmask >> c) & 1u);
+  const int by_c = (int)((s->rmask >> c) & 1u); /* c < 64 */
   if (newcalc) {
     if (removed) {
       if (s->rseq <= m) return -1;
@@ -829,7 +829,7 @@ static void item_partial(const item* g, int32_t R, int32_t L, int64_t W, pl_acc*
   }
   if (g->rseq <= R) x->a -= c;
   const int32_t lrs = g->lrs & ~LRS_RELEASED;
-  if (__builtin_popcount(g->rmask) > 1 && lrs != 0 && lrs <= L) { /* an overlapping remove */
+  if (__builtin_popcountll(g->rmask) > 1 && lrs != 0 && lrs <= L) { /* an overlapping remove */
     x->b -= c;
     x->flag = 1;
     if (g->rseq <= R) x->o -= c;
@@ -1316,10 +1316,10 @@ static int tree_range(idoc* d, const mte_op* op, const env_t* env, int local) {
         g->gord = i;
       } else if (g->rseq == NONE_SEQ) {
         g->rseq = s;
-        g->rmask = 1u << c;
+        g->rmask = 1ull << c;
       } else {
         if (is_pending(g->rseq)) g->rseq = s; /* overtaking our pending removal (:1928-1938) */
-        g->rmask |= 1u << c;
+        g->rmask |= 1ull << c;
       }
     } else {
       const mte_propset* ps = &env->b->propsets[op->a];
@@ -1755,7 +1755,10 @@ static int doc_apply_op(idoc* d, const mte_op* op, const env_t* env) {
   const int local_doc = (d->flags & MTE_DOC_LOCAL_CLIENT) != 0;
   int rc;
   if (d->n + 4 > env->limit) return MTE_E_CAPACITY;
-  if (c >= MTE_MAX_CLIENTS) return MTE_E_CLIENT_RANGE;
+  /* short ids: 32 on the flat passes (a 32-bit removers plane), 64 on the HBM
+   * tree pass (local-client and MTE_DOC_TREE documents: a second plane) */
+  if (c >= ((d->flags & (MTE_DOC_LOCAL_CLIENT | MTE_DOC_TREE)) ? MTE_MAX_CLIENTS_TREE : MTE_MAX_CLIENTS))
+    return MTE_E_CLIENT_RANGE;
   if (op->flags & MTE_F_LOCAL) {
     if ((op->flags & MTE_F_COMBINE) && op->type != MTE_OP_ANNOTATE) return MTE_E_UNSUPPORTED;
     return local_doc ? doc_apply_local(d, op, env) : MTE_E_UNSUPPORTED;
@@ -2219,7 +2222,9 @@ int oti_read_segments(oti_ctx* c, uint32_t doc, mte_seg_list* v) {
         s->len = (uint32_t)g->len;
         s->seq = g->seq;
         s->removed_seq = g->rseq == NONE_SEQ ? MTE_NOT_REMOVED : g->rseq;
-        s->removers = g->rseq == NONE_SEQ ? 0u : g->rmask;
+        /* mte_seg.removers holds short ids < 32 */
+        if (g->rseq != NONE_SEQ && (g->rmask >> 32)) return MTE_E_UNSUPPORTED;
+        s->removers = g->rseq == NONE_SEQ ? 0u : (uint32_t)g->rmask;
         s->client = g->cli;
         s->kind = g->kind;
         s->propset = MTE_NO_PROPS;

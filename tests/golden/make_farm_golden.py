@@ -43,7 +43,13 @@ record every client's mergeTreeMaintenanceCallback (SPLIT / APPEND / UNLINK /
 ACKNOWLEDGED): per event the callbacks it raised, each segment's position once
 the event is applied and its length at the callback.
 
-Usage: python3 tests/golden/make_farm_golden.py [--refs | --stay | --transient | --combine | --legacy | --relpos | --maint]
+With --many it writes tests/golden/many_clients_vectors.json.gz: farms of 34
+to 64 clients, so that more than 31 of them send inside one collab window
+(short ids past the 32-bit removers mask of the flat passes), in both length
+calculations, with rollbacks and references among them.
+
+Usage: python3 tests/golden/make_farm_golden.py [--refs | --stay | --transient | --combine | --legacy | --relpos | --maint
+                                                 | --many]
 """
 import gzip
 import json
@@ -150,6 +156,49 @@ MAINT_SETS = ([(10000 + i, 2 + i % 6, 300 + 150 * (i % 4), ["", "hello world", "
               [(10400 + i, 4, 1500, "the quick brown fox", 6, 120, {}) for i in range(4)] +
               [(10500 + i, 3 + i % 4, 400, "hello world", 4, 200, {"reconnect": 0.1, "allowDiverge": True})
                for i in range(6)])
+
+
+# many clients (--many): (seed, clients, steps, initial text, checkpoints, text
+# bound, extra parameters)
+OUT_MANY = os.path.join(HERE, "many_clients_vectors.json.gz")
+MANY_SETS = ([(11000 + i, [34, 40, 48, 56][i % 4], 700 + 100 * (i % 3), ["", "hello world", "abc\ndef"][i % 3], 4,
+               [64, 200][i % 2], {}) for i in range(8)] +
+             [(11100 + i, [40, 56][i % 2], 800, "hello world", 4, 200, {"rollback": 0.15, "rollbackTypes": [1, 2]})
+              for i in range(4)] +
+             [(11200 + i, [36, 50][i % 2], 700, "hello world", 4, 200, {"refs": 0.2}) for i in range(4)] +
+             [(11300 + i, [34, 48][i % 2], 700, "hello world", 4, 200, {"legacy": True, "allowDiverge": True})
+              for i in range(4)])
+
+
+def window_senders(log):
+    """The most short ids a document needs at once: the senders whose last op is
+    past the collab window's minSeq, plus the document's own client (slot 0) --
+    DocClients recycles a slot only once minSeq passed every seq its client used."""
+    last, msn, most = {}, 0, 0
+    for cid, seq, _ref, m, _t, _c in log:
+        last[cid] = seq
+        most = max(most, sum(1 for v in last.values() if v > msn) + 1)
+        msn = max(msn, m)
+    return most
+
+
+def main_many(out):
+    res = {"sets": [], "generator": "oracle/ref_farm.js, 34-64 clients (reference Client, mulberry32 seeds)"}
+    failed = []
+    for sd, c, n, t, k, m, extra in MANY_SETS:
+        one = dict({"seed": sd, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
+                    "rollback": 0.0}, **extra)
+        q = subprocess.run(["node", "--max-old-space-size=8192", FARM_JS, out], input=json.dumps({"sets": [one]}),
+                           capture_output=True, text=True, timeout=1200)
+        if q.returncode == 0:
+            res["sets"] += json.loads(q.stdout)["sets"]
+        else:
+            failed.append(sd)
+    res["seeds_the_reference_failed"] = failed
+    with gzip.open(OUT_MANY, "wt", encoding="utf-8") as fh:
+        json.dump(res, fh, separators=(",", ":"))
+    most = [window_senders(s["log"]) for s in res["sets"]]
+    print(f"wrote {OUT_MANY}: {len(res['sets'])} farms, short ids needed at once {most}, reference failed on {failed}")
 
 
 def main_maint(out):
@@ -280,6 +329,8 @@ def main():
         return main_relpos(out)
     if "--maint" in sys.argv[1:]:
         return main_maint(out)
+    if "--many" in sys.argv[1:]:
+        return main_many(out)
     inp = {"sets": [{"seed": s, "clients": c, "steps": n, "initialText": t, "nCheckpoints": k, "maxText": m,
                      "rollback": rb} for s, c, n, t, k, m, rb in SETS]}
     p = subprocess.run(["node", "--max-old-space-size=8192", FARM_JS, out], input=json.dumps(inp),

@@ -80,7 +80,7 @@ def test_js_packing_matches_python_packing_on_fixtures(fresh):
 
 @pytest.mark.parametrize("vectors", ["farm_vectors.json.gz", "reconnect_vectors.json.gz", "localref_vectors.json.gz",
                                      "localref_stay_vectors.json.gz", "localref_transient_vectors.json.gz",
-                                     "relpos_farm_vectors.json.gz"])
+                                     "relpos_farm_vectors.json.gz", "many_clients_vectors.json.gz"])
 def test_js_packing_matches_python_packing_on_local_farms(vectors):
     """Local ops and acks (and, on the reconnect farms, ops held offline and
     regeneratePendingOp's MTE_OP_REGEN records): the JS and Python packers emit
