@@ -67,7 +67,8 @@ export interface ClientOptions {
   refs?: boolean;
   /** mergeTreeMaintenanceCallback records -> BatchClient.on("maintenance") (needs localClient, events). */
   maintenanceEvents?: boolean;
-  /** MTE_DOC_TREE: replay on the tree pass (the reference's segmentation; segment-exact sequenceDelta ranges). */
+  /** MTE_DOC_TREE: replay on the tree pass (the reference's segmentation; segment-exact sequenceDelta ranges;
+   *  up to 63 senders inside one collab window, 31 on the flat passes). */
   tree?: boolean;
   newLengthCalc?: boolean;
   props?: PropertySet;
