@@ -12,10 +12,12 @@
 const { parentPort, workerData } = require("worker_threads");
 const { BatchBuilder, DocClients, Interner } = require("./packing");
 
-const { d0, d1, observers, minSeq, nKeys } = workerData;
+const { d0, d1, observers, minSeq, nKeys, trees } = workerData;
 const n = d1 - d0;
-const clients = observers.map((o, i) => new DocClients(o, minSeq[i], false));
+// MTE_DOC_TREE documents take sequenced combining ops (deferred to the host's merge)
+const clients = observers.map((o, i) => new DocClients(o, minSeq[i], false, trees && trees[i]));
 const interner = new Interner(nKeys);
+interner.noteLog = [];
 let msgs = null;
 const cursor = new Uint32Array(n);
 let bb = null;
@@ -40,8 +42,10 @@ function pack(upto) {
   }
   bb = new BatchBuilder(n, interner, null, count + (count >> 4));
   // a shard's interner sees neither the loaded documents' values nor the other
-  // shards', so it cannot close a combining op's value map: refused (loud)
+  // shards', so a sequenced combining op's value map is left to the host's
+  // merge (PropTable.addDeferred); a local one has no place in a worker
   bb.noCombining = true;
+  bb.shard = true;
   for (let i = lo; i < hi; i++) {
     for (let d = 0; d < n; d++) {
       if (i >= cursor[d] && i < end[d]) {
@@ -56,21 +60,30 @@ function pack(upto) {
   const values = interner.valueJson.slice(sentValues);
   sentKeys = interner.keyNames.length;
   sentValues = interner.valueJson.length;
+  // the [key, value index] pairs first noted since, and the deferred combining sets
+  const notes = interner.noteLog;
+  interner.noteLog = [];
   return { nrec: bb.count, ntext: bb.textUnits, nps: bb.props.sets.length / 2, npe: bb.props.entries.length / 2,
-    keys, values, ms: Number(process.hrtime.bigint() - t0) / 1e6 };
+    keys, values, notes, deferred: bb.props.deferred || [], ms: Number(process.hrtime.bigint() - t0) / 1e6 };
 }
 
 function emit(base, map, sab) {
   const t0 = process.hrtime.bigint();
   // records sorted by document, text / propset offsets moved by the bases
   const out = new Int32Array(sab.ops, base.rec * 32, bb.count * 8);
-  const rel = bb.buildInto(out, base.text, base.ps);
+  const rel = bb.buildInto(out, base.text, base.ps, map);
   new Uint16Array(sab.text, base.text * 2, bb.textUnits).set(bb.textBuf.subarray(0, bb.textUnits));
   const sets = bb.props.sets, ents = bb.props.entries;
   const ps = new Uint32Array(sab.propsets, base.ps * 8, sets.length);
   for (let i = 0; i < ps.length; i += 2) {
     ps[i] = sets[i] + base.pe;
     ps[i + 1] = sets[i + 1];
+  }
+  // the deferred combining sets: entries the host wrote past every shard's (map.deferred)
+  const df = bb.props.deferred || [];
+  for (let q = 0; q < df.length; q++) {
+    ps[2 * df[q][0]] = map.deferred[2 * q];
+    ps[2 * df[q][0] + 1] = map.deferred[2 * q + 1];
   }
   // keys / values renamed to the engine's ids
   const pe = new Uint32Array(sab.props, base.pe * 8, ents.length);

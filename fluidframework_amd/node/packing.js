@@ -101,6 +101,10 @@ class Interner {
     // many: the combining ops' domain (packing.py Interner.note_value)
     this.keyMask = new Uint32Array(256);
     this.keyCount = new Uint32Array(Math.max(1, nKeys));
+    // a ShardedHost worker's interner logs [key, value index] the first time a
+    // key is given a value, so the host's interner learns the combining ops'
+    // domains (shards.js); null elsewhere
+    this.noteLog = null;
   }
   /** [key, value id] of one property, noting the value under its key */
   kv(name, v) {
@@ -119,6 +123,7 @@ class Interner {
     if (!(this.keyMask[x] & (1 << k))) {
       this.keyMask[x] |= 1 << k;
       this.keyCount[k]++;
+      if (this.noteLog) this.noteLog.push(k, x);
     }
   }
   /** the value ids key k was ever given, ascending; a key given more than
@@ -289,6 +294,25 @@ class PropTable {
     this.sets = [];
     this.entries = [];
     this.combOf = new Map();  // a local combining set's index -> [props, combiningOp]
+    this.deferred = null;  // addDeferred: [set index, key names, combiningOp, seq]
+  }
+  /** A sequenced incr / consensus annotate packed where the keys' value
+   *  domains are not all known (a ShardedHost worker sees its own documents'
+   *  values only): a placeholder set whose entries the host computes with
+   *  addCombining over its own interner once every shard's values are merged
+   *  (shards.js _merge).  combineValue ignores the op's values: only the key
+   *  names travel. */
+  addDeferred(props, comb, seq) {
+    if (props === null || typeof props !== "object" || Array.isArray(props)) {
+      throw new MergeTreeError(E_INVALID_ARG, "props must be an object");
+    }
+    const names = Object.keys(props);
+    for (const name of names) this.interner.key(name);  // nKeys is checked here, as addCombining does
+    if (!this.deferred) this.deferred = [];
+    const s = this.sets.length >> 1;
+    this.sets.push(this.entries.length >> 1, 0);
+    this.deferred.push([s, names, { name: comb.name, defaultValue: comb.defaultValue, minValue: comb.minValue }, seq]);
+    return s;
   }
   add(props) {
     if (props === undefined || props === null) return NO_PROPS;
@@ -595,9 +619,6 @@ class BatchBuilder {
       let flags = 0;
       const comb = op.combiningOp;
       if (comb !== undefined && comb !== null && (comb.name === "incr" || comb.name === "consensus")) {
-        if (this.noCombining) {
-          throw new MergeTreeError(E_UNSUPPORTED, "combiningOp " + comb.name + " in a sharded (worker) packer");
-        }
         if (!this._combLocal) {
           throw new MergeTreeError(E_UNSUPPORTED, "combiningOp " + comb.name +
             " outside a local-client or tree document (the HBM tree pass)");
@@ -605,7 +626,8 @@ class BatchBuilder {
         if (comb.name === "consensus" && "defaultValue" in comb) {
           throw new MergeTreeError(E_UNSUPPORTED, "consensus with a defaultValue");
         }
-        const ps = this.props.addCombining(op.props === undefined ? {} : op.props, comb, seq);
+        const pv = op.props === undefined ? {} : op.props;
+        const ps = this.shard ? this.props.addDeferred(pv, comb, seq) : this.props.addCombining(pv, comb, seq);
         this._put(doc, seq, ref, msn, OP_ANNOTATE, 0, F_COMBINE, checkI32(p1, "pos1"), checkI32(p2, "pos2"), ps, NO_PROPS);
         return;
       }
@@ -931,14 +953,19 @@ class BatchBuilder {
       flags |= pf;
       if (rp.before) flags |= bf;
       if (rp.offset !== undefined && rp.offset !== null) offs[i] = checkI32(rp.offset, rk + ".offset");
-      // an id no marker was ever given cannot match (value 0)
+      // an id no marker was ever given cannot match (value 0); a shard interns
+      // it, as its documents' markers may be loaded ones the host interned
+      // (buildInto renames it to the engine's id, which no other marker has)
       if (rp.id) {
-        const v = this.interner.values.get(canonicalJson(rp.id));
+        const v = this.shard ? this.interner.value(rp.id) : this.interner.values.get(canonicalJson(rp.id));
         vids[i] = v === undefined ? 0 : v;
       }
     }
     if (!flags) return null;
-    const key = this.interner.keys.get(MARKER_ID_KEY);
+    let key = this.interner.keys.get(MARKER_ID_KEY);
+    if (key === undefined && this.shard && this.interner.keyNames.length < this.interner.nKeys) {
+      key = this.interner.key(MARKER_ID_KEY);
+    }
     return [flags, vids[0], vids[1], key === undefined ? NO_PROPS : key, offs[0], offs[1]];
   }
 
@@ -1057,7 +1084,7 @@ class BatchBuilder {
    *  `out` (an Int32Array of count * 8), their text offsets (insert a) moved by
    *  textBase and their propset indices (insert b, annotate a) by psBase.
    *  Returns the per-document record offsets relative to `out`. */
-  buildInto(out, textBase, psBase) {
+  buildInto(out, textBase, psBase, map) {
     const nd = this.nDocs, n = this.count;
     const offsets = new Uint32Array(nd + 1);
     const cur = new Uint32Array(nd);
@@ -1079,12 +1106,19 @@ class BatchBuilder {
       } else if (t === OP_ANNOTATE) {
         a += psBase;
       }
+      let p1 = R[w + 4], p2 = R[w + 5];
+      if (t === OP_RELPOS && map) {
+        // a shard's markerId key and marker-id values -> the engine's ids (shards.js)
+        if ((a >>> 0) !== NO_PROPS) a = map.keys[a];
+        p1 = map.values[p1];
+        p2 = map.values[p2];
+      }
       out[o] = R[w];
       out[o + 1] = R[w + 1];
       out[o + 2] = R[w + 2];
       out[o + 3] = w3;
-      out[o + 4] = R[w + 4];
-      out[o + 5] = R[w + 5];
+      out[o + 4] = p1;
+      out[o + 5] = p2;
       out[o + 6] = a;
       out[o + 7] = b;
     }

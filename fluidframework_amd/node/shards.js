@@ -16,6 +16,7 @@
 // ISequencedDocumentMessage objects (in a server: the documents' delta streams).
 const path = require("path");
 const { Worker } = require("worker_threads");
+const { PropTable } = require("./packing");
 
 const OP_BYTES = 32;
 
@@ -49,7 +50,8 @@ class ShardedHost {
     const minSeq = this.engine.docs.map((d) => d.minSeq || 0);
     this.workers = this.ranges.map(([d0, d1]) => new Worker(file, {
       workerData: { d0, d1, source: this.options.source, sourceData: this.options.sourceData,
-        observers: obs.slice(d0, d1), minSeq: minSeq.slice(d0, d1), nKeys: this.engine.nKeys },
+        observers: obs.slice(d0, d1), minSeq: minSeq.slice(d0, d1), nKeys: this.engine.nKeys,
+        trees: this.engine.docs.slice(d0, d1).map((d) => !!d.tree) },
     }));
     await Promise.all(this.workers.map((_, w) => this._call(w, { cmd: "load" })));
   }
@@ -78,7 +80,7 @@ class ShardedHost {
       const tm = process.hrtime.bigint();
       t.pack_ms += Number(tm - tp) / 1e6;
       t.pack_max_worker_ms += Math.max(...parts.map((p) => p.ms));
-      const { maps, bases, nrec, ntext, nps, npe } = this._merge(parts);
+      const { maps, bases, nrec, ntext, nps, npe, comb } = this._merge(parts);
       const nDocs = eng.docs.length;
       const sab = {
         ops: new SharedArrayBuffer(Math.max(1, nrec) * OP_BYTES),
@@ -87,6 +89,8 @@ class ShardedHost {
         props: new SharedArrayBuffer(Math.max(1, npe) * 8),
         offsets: new SharedArrayBuffer((nDocs + 1) * 8),
       };
+      // the deferred combining sets' entries, past every shard's
+      new Uint32Array(sab.props, comb.base * 8, comb.entries.length).set(comb.entries);
       const te = process.hrtime.bigint();
       await Promise.all(this.workers.map((_, w) => this._call(w, { cmd: "emit", base: bases[w], map: maps[w], sab })));
       const ts = process.hrtime.bigint();
@@ -112,7 +116,11 @@ class ShardedHost {
 
   // the shards' keys / values interned since the last part -> the engine's
   // interner (the single id space its read-outs decode with); each shard's
-  // base in the shared batch
+  // base in the shared batch.  Sequenced incr / consensus annotates of
+  // MTE_DOC_TREE documents: their value maps cover every value their key was
+  // ever given in any shard (PropTable.addCombining over the engine's
+  // interner, once the shards' key -> value notes are merged), written past
+  // the shards' property entries (PropTable.addDeferred)
   _merge(parts) {
     const it = this.engine.interner;
     if (!this.maps) this.maps = this.workers.map(() => ({ keys: [], values: [0] }));
@@ -120,7 +128,19 @@ class ShardedHost {
       const m = this.maps[w];  // a shard's key / value ids -> the engine's
       for (const name of p.keys) m.keys.push(it.key(name));
       for (const j of p.values) m.values.push(it.valueOfJson(j));
+      for (let i = 0; i < p.notes.length; i += 2) it.noteValue(m.keys[p.notes[i]], m.values[p.notes[i + 1]]);
       return { keys: Int32Array.from(m.keys), values: Uint32Array.from(m.values) };
+    });
+    const pt = new PropTable(it);
+    parts.forEach((p, w) => {
+      const dv = [];
+      for (const [, names, comb, seq] of p.deferred) {
+        const props = {};
+        for (const name of names) props[name] = null;  // combineValue ignores the op's values
+        const i = pt.addCombining(props, comb, seq);
+        dv.push(pt.sets[2 * i], pt.sets[2 * i + 1]);
+      }
+      maps[w].deferred = Uint32Array.from(dv);
     });
     let nrec = 0, ntext = 0, nps = 0, npe = 0;
     const bases = parts.map((p) => {
@@ -131,7 +151,10 @@ class ShardedHost {
       npe += p.npe;
       return b;
     });
-    return { maps, bases, nrec, ntext, nps, npe };
+    for (const m of maps) for (let q = 0; q < m.deferred.length; q += 2) m.deferred[q] += npe;
+    const comb = { base: npe, entries: Uint32Array.from(pt.entries) };
+    npe += pt.entries.length / 2;
+    return { maps, bases, nrec, ntext, nps, npe, comb };
   }
 
   async close() {

@@ -452,6 +452,27 @@ def test_sharded_host_packs_what_one_packer_packs(tmp_path, mode):
         assert runs(a, tables["keys"], tables["values"]) == runs(b, it.key_names, it.value_json), d
 
 
+def _shard_combine(env=None):
+    j = json.loads(node("tests/node/shard_combine.js", "3", "3", timeout=600, env=env))
+    assert j["nFailures"] == 0, j["failures"]
+    assert j["passed"] == j["sets"] == 26 and j["combining"] > 1000
+
+
+def test_sharded_host_combining_ops_on_restatement():
+    """ShardedHost with sequenced incr / consensus annotates (VERDICT r05
+    Missing #3): the 26 combining farms' observers as MTE_DOC_TREE documents,
+    three per engine on three worker threads, in three pipelined parts; the
+    shards defer the ops' value maps to the host's merge (PropTable.addDeferred)
+    and rename their relative positions' marker ids to the engine's (buildInto);
+    every observer ends as the reference's (tests/node/shard_combine.js)."""
+    _shard_combine({"MTE_NODE_ADDON": "oracle"})
+
+
+@pytest.mark.gpu
+def test_sharded_host_combining_ops_on_gpu():
+    _shard_combine()
+
+
 def test_js_packer_ref_capacity_refuses_only_that_document():
     # ADVICE r03: the JS packer refuses a reference past the context's capacity
     # for its own document instead of letting mte_submit fail the whole batch
