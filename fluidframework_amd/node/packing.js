@@ -1167,8 +1167,9 @@ function packDocInits(docs, interner) {
 function slotOf(clients, longId, seq, max) {
   const s = clients.short(longId, seq);
   if (s >= (max || clients.maxClients)) {
+    const hint = !max && clients.maxClients < MAX_CLIENTS_TREE ? " ({tree: true} takes " + MAX_CLIENTS_TREE + ")" : "";
     throw new MergeTreeError(E_CLIENT_RANGE, "client " + String(longId) + ": more than " + (max || clients.maxClients) +
-      " clients inside the collab window");
+      " clients inside the collab window" + hint);
   }
   return s;
 }

@@ -472,8 +472,10 @@ class BatchBuilder:
         # the slot is taken only once the message has validated
         short = clients.short(sender, seq)
         if short >= clients.max_clients:
+            hint = "" if clients.max_clients == MTE_MAX_CLIENTS_TREE else \
+                f" (a document flagged MTE_DOC_TREE takes {MTE_MAX_CLIENTS_TREE})"
             raise MergeTreeError(MTE_E_CLIENT_RANGE, f"client {sender!r}: more than {clients.max_clients} "
-                                 "clients inside the collab window")
+                                 f"clients inside the collab window{hint}")
         if not recs:
             recs.append((OP_NOOP, 0, 0, 0, 0, NO_PROPS))
         out = self.ops[doc]
