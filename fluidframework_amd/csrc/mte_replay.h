@@ -38,7 +38,9 @@
 #define MTE_FAIR_PRIO 4
 #endif
 #ifndef MTE_VREC  // 1: pass-1 op records fetched with vector loads (vmcnt), 0: scalar loads (lgkmcnt)
-#define MTE_VREC 0
+// 1 since round 6 (profiles/r06/ab/vrec/): config 3 at 10k documents 22.3 -> 21.6 ms (an LDS wait
+// no longer waits for the next record's scalar load too); 1,250 documents 8.01 -> 8.07 ms
+#define MTE_VREC 1
 #endif
 #ifndef MTE_E1_DPP  // 1: the E = 1 shift moves slots with DPP instead of ds_bpermute
 #define MTE_E1_DPP 0
